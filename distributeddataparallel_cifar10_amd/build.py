@@ -1,0 +1,72 @@
+"""Build the native HIP/C++ code of the framework for gfx950 (MI355X), in-tree.
+
+``python -m distributeddataparallel_cifar10_amd.build`` compiles ``csrc/engine.hip`` (which includes the kernel
+translation unit) with ``hipcc --offload-arch=gfx950`` into ``_lib/libdca_engine.so``.  hipcc cross-compiles without
+a GPU, so this runs on the CPU-only build host too.  The library links the HIP runtime and RCCL by SONAME
+(``libamdhip64.so.7``, ``librccl.so.1``); loaded after ``import torch`` it binds to the copies torch already
+loaded, so there is exactly one HIP runtime in the process.
+"""
+from __future__ import annotations
+
+import hashlib
+import os
+import shutil
+import subprocess
+import sys
+
+PKG_DIR = os.path.dirname(os.path.abspath(__file__))
+CSRC = os.path.join(PKG_DIR, "csrc")
+LIB_DIR = os.path.join(PKG_DIR, "_lib")
+ENGINE_LIB = os.path.join(LIB_DIR, "libdca_engine.so")
+ARCH = os.environ.get("DCA_OFFLOAD_ARCH", "gfx950")
+
+
+def _hipcc() -> str:
+    for cand in (os.environ.get("HIPCC"), "/opt/rocm/bin/hipcc", shutil.which("hipcc")):
+        if cand and os.path.exists(cand):
+            return cand
+    raise RuntimeError("hipcc not found (ROCm toolchain required to build the native engine)")
+
+
+def _sources():
+    return sorted(os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith((".hip", ".h", ".cpp")))
+
+
+def _digest() -> str:
+    h = hashlib.sha256(ARCH.encode())
+    for p in _sources():
+        with open(p, "rb") as f:
+            h.update(os.path.basename(p).encode())
+            h.update(f.read())
+    return h.hexdigest()
+
+
+def build(force: bool = False, verbose: bool = False) -> str:
+    """Compile the engine library if sources changed; returns the .so path."""
+    os.makedirs(LIB_DIR, exist_ok=True)
+    stamp = ENGINE_LIB + ".sha256"
+    digest = _digest()
+    if not force and os.path.exists(ENGINE_LIB) and os.path.exists(stamp):
+        with open(stamp) as f:
+            if f.read().strip() == digest:
+                return ENGINE_LIB
+    tmp = ENGINE_LIB + f".tmp{os.getpid()}"
+    cmd = [
+        _hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
+        "-Wall", "-Wno-unused-function", "-Wno-unused-variable",
+        os.path.join(CSRC, "engine.hip"), "-o", tmp, "-lrccl",
+    ]
+    if verbose:
+        print(" ".join(cmd), flush=True)
+    res = subprocess.run(cmd, capture_output=True, text=True)
+    if res.returncode != 0:
+        raise RuntimeError(f"hipcc failed ({res.returncode}):\n{res.stderr[-6000:]}")
+    os.replace(tmp, ENGINE_LIB)
+    with open(stamp, "w") as f:
+        f.write(digest)
+    return ENGINE_LIB
+
+
+if __name__ == "__main__":
+    path = build(force="--force" in sys.argv, verbose=True)
+    print(path)

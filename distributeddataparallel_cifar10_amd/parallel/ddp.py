@@ -1,0 +1,53 @@
+"""Data-parallel training wrappers.
+
+``FusedDDPTrainer`` is the MI355X fast path for NetResDeep: DDP semantics of reference ``main.py:63``
+(``DistributedDataParallel(model, device_ids=[rank])``) implemented inside the native engine:
+
+  * CC3 (construction): rank 0's parameters and BN buffers are broadcast to every rank;
+  * CC5 (every backward): gradients averaged over ranks through two flat RCCL buckets; bucket A (fc1/fc2) is
+    all-reduced on a comm stream while the trunk backward runs;
+  * CC4 (every forward): rank 0's BN running statistics reach every rank through a 64-float tail segment of
+    bucket B (no separate broadcast collective).
+
+The generic ``FlatBucketDDP`` (any nn.Module, autograd hooks) lives in ``parallel/flat_ddp.py``.
+"""
+from __future__ import annotations
+
+from typing import Optional
+
+import torch
+import torch.distributed as dist
+import torch.nn as nn
+
+from ..runtime.engine import EngineConfig, NetResDeepEngine, nccl_unique_id
+
+
+def broadcast_module_state(model: nn.Module, src: int = 0) -> None:
+    """CC3: make every rank's parameters and buffers equal to rank `src`'s (reference DDP constructor)."""
+    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
+        return
+    with torch.no_grad():
+        for t in list(model.parameters()) + list(model.buffers()):
+            dist.broadcast(t.data, src)
+
+
+class FusedDDPTrainer:
+    """NetResDeep + DDP + SGD as one native, graph-captured training step per batch."""
+
+    def __init__(self, model: nn.Module, data_u8: torch.Tensor, labels: torch.Tensor, batch_max: int = 32,
+                 lr: float = 1e-2, dtype: str = "bf16", rows: int = 4, max_indices: Optional[int] = None):
+        world = dist.get_world_size() if dist.is_available() and dist.is_initialized() else 1
+        rank = dist.get_rank() if world > 1 else 0
+        self.world_size, self.rank = world, rank
+        nccl_id = None
+        if world > 1:
+            broadcast_module_state(model, 0)
+            obj = [nccl_unique_id() if rank == 0 else None]
+            dist.broadcast_object_list(obj, src=0)
+            nccl_id = obj[0]
+        cfg = EngineConfig(batch_max=batch_max, lr=lr, dtype=dtype, rows=rows, world_size=world, rank=rank)
+        self.engine = NetResDeepEngine(model, data_u8, labels, cfg, nccl_id=nccl_id, max_indices=max_indices)
+        self.module = model
+
+    def close(self):
+        self.engine.close()

@@ -1,0 +1,242 @@
+"""Python face of the native NetResDeep training engine (``csrc/engine.hip``).
+
+``NetResDeepEngine`` takes an ``nn.Module`` NetResDeep, re-homes its 9 unique parameters into ONE flat device
+buffer (the module's ``nn.Parameter``s become views of it, so ``state_dict()`` / checkpoints always show what the
+kernels train), and drives whole training steps that run as one hipGraph replay each.
+
+Reference parity: the step is ``main.py:33-41`` (forward, CrossEntropyLoss, zero_grad, backward, SGD step,
+``loss.item()`` accumulated) with DDP gradient averaging (``main.py:63``) when world_size > 1.  The loss is
+accumulated on the device and read only at log points.
+"""
+from __future__ import annotations
+
+import ctypes
+from dataclasses import dataclass
+from typing import Optional
+
+import numpy as np
+import torch
+import torch.nn as nn
+
+from . import native
+
+# ---- flat parameter layout (mirrors csrc/common.h) --------------------------------------------------------
+FLAT_N = 76140
+FLAT_ALLOC = 76160
+OFF_RS = 76076
+BUCKET_A_END = 65900
+LAYOUT = {
+    "fc1.weight": (0, (32, 2048)),
+    "fc2.weight": (65536, (10, 32)),
+    "fc1.bias": (65856, (32,)),
+    "fc2.bias": (65888, (10,)),
+    "resblocks.0.conv.weight": (65900, (32, 32, 3, 3)),
+    "resblocks.0.batch_norm.weight": (75116, (32,)),
+    "resblocks.0.batch_norm.bias": (75148, (32,)),
+    "conv1.weight": (75180, (32, 3, 3, 3)),
+    "conv1.bias": (76044, (32,)),
+}
+# gradient buckets (contiguous slices of the flat gradient buffer, ordered by gradient-ready time)
+BUCKETS = (("fc", 0, BUCKET_A_END), ("trunk+stem+bn_stats", BUCKET_A_END, FLAT_N))
+
+
+class _DcaInit(ctypes.Structure):
+    _fields_ = [
+        ("params", ctypes.c_void_p),
+        ("grads", ctypes.c_void_p),
+        ("rm", ctypes.c_void_p),
+        ("rv", ctypes.c_void_p),
+        ("nbt", ctypes.c_void_p),
+        ("data", ctypes.c_void_p),
+        ("labels", ctypes.c_void_p),
+        ("n_data", ctypes.c_int),
+        ("bmax", ctypes.c_int),
+        ("bf16", ctypes.c_int),
+        ("rows", ctypes.c_int),
+        ("lr", ctypes.c_float),
+        ("bn_mom", ctypes.c_float),
+        ("bn_eps", ctypes.c_float),
+        ("world_size", ctypes.c_int),
+        ("rank", ctypes.c_int),
+        ("nccl_id", ctypes.c_char_p),
+    ]
+
+
+def bind_flat_parameters(model: nn.Module, device) -> tuple[torch.Tensor, torch.Tensor]:
+    """Move NetResDeep's unique parameters into one flat buffer; params and grads become views of it."""
+    flat = torch.zeros(FLAT_ALLOC, dtype=torch.float32, device=device)
+    grads = torch.zeros(FLAT_ALLOC, dtype=torch.float32, device=device)
+    names = dict(model.named_parameters())
+    if set(names) != set(LAYOUT):
+        raise ValueError(f"engine supports NetResDeep(32, 10) only; got parameters {sorted(names)}")
+    for name, p in names.items():
+        off, shape = LAYOUT[name]
+        if tuple(p.shape) != shape:
+            raise ValueError(f"{name}: expected shape {shape}, got {tuple(p.shape)}")
+        n = p.numel()
+        with torch.no_grad():
+            flat[off:off + n].copy_(p.detach().reshape(-1))
+        p.data = flat[off:off + n].view(shape)
+        p.grad = grads[off:off + n].view(shape)
+    return flat, grads
+
+
+def nccl_unique_id() -> bytes:
+    lib = native.require_native()
+    buf = ctypes.create_string_buffer(128)
+    native.check(lib.dca_nccl_unique_id(buf), "ncclGetUniqueId")
+    return buf.raw
+
+
+@dataclass
+class EngineConfig:
+    batch_max: int = 32
+    lr: float = 1e-2
+    dtype: str = "bf16"          # "bf16": bf16 MFMA (fp32 accumulate/storage); "fp32": exact fp32 MFMA
+    rows: int = 4                # trunk rows per workgroup tile (2 or 4)
+    world_size: int = 1
+    rank: int = 0
+    bn_momentum: float = 0.1
+    bn_eps: float = 1e-5
+
+
+class NetResDeepEngine:
+    """Fused, graph-captured training step for NetResDeep on one MI355X (one rank of DDP)."""
+
+    def __init__(self, model: nn.Module, data_u8: torch.Tensor, labels: torch.Tensor, cfg: EngineConfig,
+                 nccl_id: Optional[bytes] = None, max_indices: Optional[int] = None):
+        if cfg.dtype not in ("bf16", "fp32"):
+            raise ValueError("dtype must be 'bf16' or 'fp32'")
+        if getattr(model, "n_chans1", 32) != 32 or getattr(model, "n_blocks", 10) != 10:
+            raise ValueError("the fused engine is specialised for NetResDeep(n_chans1=32, n_blocks=10)")
+        self.lib = native.require_native()
+        dev = data_u8.device
+        if dev.type != "cuda":
+            raise ValueError("engine tensors must live on the GPU")
+        self.cfg = cfg
+        self.model = model
+        self.device = dev
+        assert data_u8.dtype == torch.uint8 and data_u8.dim() == 4 and tuple(data_u8.shape[1:]) == (3, 32, 32)
+        self.data = data_u8.contiguous()
+        self.labels = labels.to(device=dev, dtype=torch.int32).contiguous()
+        self.flat, self.grads = bind_flat_parameters(model, dev)
+        bn = model.resblocks[0].batch_norm
+        self.bn = bn
+        for name in ("running_mean", "running_var"):
+            t = getattr(bn, name)
+            if t.device != dev or not t.is_contiguous() or t.dtype != torch.float32:
+                setattr(bn, name, t.to(dev, torch.float32).contiguous())
+        if bn.num_batches_tracked.device != dev:
+            bn.num_batches_tracked = bn.num_batches_tracked.to(dev)
+        torch.cuda.synchronize(dev)
+        self._nccl_id = ctypes.create_string_buffer(nccl_id or b"\0" * 128, 128)
+        init = _DcaInit(
+            params=self.flat.data_ptr(), grads=self.grads.data_ptr(),
+            rm=bn.running_mean.data_ptr(), rv=bn.running_var.data_ptr(), nbt=bn.num_batches_tracked.data_ptr(),
+            data=self.data.data_ptr(), labels=self.labels.data_ptr(), n_data=int(self.data.shape[0]),
+            bmax=int(cfg.batch_max), bf16=1 if cfg.dtype == "bf16" else 0, rows=int(cfg.rows), lr=float(cfg.lr),
+            bn_mom=float(cfg.bn_momentum), bn_eps=float(cfg.bn_eps), world_size=int(cfg.world_size),
+            rank=int(cfg.rank), nccl_id=ctypes.cast(self._nccl_id, ctypes.c_char_p),
+        )
+        self._init = init
+        self.max_indices = int(max_indices or self.data.shape[0])
+        h = ctypes.c_void_p()
+        with torch.cuda.device(dev):
+            native.check(self.lib.dca_engine_create(ctypes.byref(init), self.max_indices, ctypes.byref(h)),
+                         "dca_engine_create")
+        self.h = h
+        self.derive()
+        self._n_indices = 0
+
+    # ---- state sync ---------------------------------------------------------------------------------------
+    def derive(self):
+        """Re-derive the kernel-layout weight copies after the fp32 params changed outside the engine."""
+        torch.cuda.synchronize(self.device)
+        native.check(self.lib.dca_engine_derive(self.h), "dca_engine_derive")
+
+    def sync(self):
+        native.check(self.lib.dca_engine_sync(self.h), "dca_engine_sync")
+
+    # ---- data order -----------------------------------------------------------------------------------------
+    def set_indices(self, indices) -> None:
+        idx = np.ascontiguousarray(np.asarray(indices, dtype=np.int32))
+        if idx.size and (idx.min() < 0 or idx.max() >= self.data.shape[0]):
+            raise IndexError("sample index out of range")
+        native.check(self.lib.dca_engine_set_indices(self.h, idx.ctypes.data, int(idx.size)), "set_indices")
+        self._n_indices = int(idx.size)
+
+    def set_cursor(self, pos: int = 0) -> None:
+        native.check(self.lib.dca_engine_set_cursor(self.h, int(pos)), "set_cursor")
+
+    # ---- stepping -------------------------------------------------------------------------------------------
+    def run(self, batch: int, steps: int = 1, graph: bool = True) -> None:
+        """Enqueue `steps` training steps of `batch` images each (asynchronous)."""
+        native.check(self.lib.dca_engine_run(self.h, int(batch), int(steps), 1 if graph else 0), "dca_engine_run")
+
+    def read_loss(self, reset: bool = False) -> tuple[float, int]:
+        """(sum of per-step mean losses, steps) since the last reset.  Synchronises."""
+        loss = ctypes.c_double()
+        steps = ctypes.c_int()
+        native.check(self.lib.dca_engine_read_loss(self.h, ctypes.byref(loss), ctypes.byref(steps), int(reset)),
+                     "read_loss")
+        return loss.value, steps.value
+
+    def run_epoch(self, indices, batch: int, graph: bool = True) -> tuple[float, int]:
+        """One pass over `indices` in batches of `batch` (ragged last batch kept, drop_last=False)."""
+        n = len(indices)
+        self.set_indices(indices)
+        self.set_cursor(0)
+        self.read_loss(reset=True)
+        full, rem = divmod(n, batch)
+        if full:
+            self.run(batch, full, graph)
+        if rem:
+            self.run(rem, 1, graph)
+        return self.read_loss(reset=True)
+
+    # ---- introspection (tests) --------------------------------------------------------------------------
+    def region(self, name: str, numel: int, dtype=torch.float32) -> torch.Tensor:
+        """Copy of a workspace region (synchronises)."""
+        self.sync()
+        ptr = self.lib.dca_engine_region(self.h, name.encode())
+        if not ptr:
+            raise KeyError(name)
+        out = torch.empty(numel, dtype=dtype, device=self.device)
+        torch.cuda.synchronize(self.device)
+        _copy_from_ptr(out, ptr)
+        return out
+
+    def workspace_bytes(self) -> int:
+        return int(self.lib.dca_engine_workspace_bytes(self.h))
+
+    def close(self):
+        if getattr(self, "h", None):
+            self.lib.dca_engine_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def _copy_from_ptr(out: torch.Tensor, ptr: int) -> None:
+    """Copy out.numel() elements from raw device pointer `ptr` into `out` (same device)."""
+    hip = _hip_runtime()
+    nbytes = out.numel() * out.element_size()
+    rc = hip.hipMemcpy(ctypes.c_void_p(out.data_ptr()), ctypes.c_void_p(ptr), ctypes.c_size_t(nbytes), 3)
+    if rc != 0:
+        raise RuntimeError(f"hipMemcpy failed: {rc}")
+
+
+_HIP = None
+
+
+def _hip_runtime():
+    global _HIP
+    if _HIP is None:
+        _HIP = ctypes.CDLL("libamdhip64.so.7")
+        _HIP.hipMemcpy.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int]
+        _HIP.hipMemcpy.restype = ctypes.c_int
+    return _HIP
