@@ -1,0 +1,91 @@
+"""Where does a training step spend its time?  (diagnostic; needs the stamps build)
+
+Runs the engine built with -DDCA_STAMPS (in-kernel s_memtime/s_memrealtime at phase boundaries) and prints, per
+kernel of one step: dispatch skew across workgroups, per-phase medians (shader cycles), kernel span, and the
+gap to the previous kernel (last workgroup end -> first workgroup start, 100 MHz realtime clock).
+Also calibrates the launch floor with graphs of empty / load-only kernels (dca_microbench).
+
+    DCA_ENGINE_VARIANT=stamps python bench/stamps.py
+"""
+from __future__ import annotations
+
+import ctypes
+import json
+import os
+import sys
+
+os.environ.setdefault("DCA_ENGINE_VARIANT", "stamps")
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from model.resnet import NetResDeep  # noqa: E402
+from distributeddataparallel_cifar10_amd.runtime import native  # noqa: E402
+from distributeddataparallel_cifar10_amd.runtime.engine import EngineConfig, NetResDeepEngine  # noqa: E402
+
+SLOTS = ["stem+conv0"] + [f"fwd{i}" for i in range(1, 10)] + ["head1", "head2"] + \
+        [f"bwd{i}" for i in range(9, -1, -1)] + ["reduce"]
+
+
+def microbench(lib):
+    out = {}
+    kinds = ((0, "empty"), (1, "shared32K_serialreduce"), (2, "1float_private"), (3, "private32K"),
+             (4, "fresh32K_sameWG"), (5, "fresh32K_nextWG"), (6, "fresh32K_broadcast"))
+    for kind, name in kinds:
+        for grid in (128, 256):
+            us = ctypes.c_float()
+            native.check(lib.dca_microbench(kind, 23, grid, 200, ctypes.byref(us)), "microbench")
+            out[f"{name}/grid{grid}"] = round(us.value, 3)
+    return out
+
+
+def main():
+    dtype = sys.argv[1] if len(sys.argv) > 1 else "bf16"
+    dev = torch.device("cuda", 0)
+    torch.manual_seed(0)
+    data = torch.randint(0, 256, (4096, 3, 32, 32), dtype=torch.uint8, device=dev)
+    labels = torch.randint(0, 10, (4096,), device=dev)
+    model = NetResDeep().to(dev)
+    eng = NetResDeepEngine(model, data, labels, EngineConfig(batch_max=32, dtype=dtype))
+    eng.set_indices(np.arange(4096, dtype=np.int32))
+    eng.set_cursor(0)
+    eng.run(32, 50)   # warm up, then one more step whose stamps we keep
+    eng.sync()
+    eng.run(32, 1)
+    eng.sync()
+    raw = eng.region("STAMPS", 32 * 256 * 8 * 2, dtype=torch.int64).cpu().numpy().astype(np.int64)
+    st = raw.reshape(32, 256, 8, 2)
+    res = {"dtype": dtype, "kernels": []}
+    prev_end = None
+    for k, name in enumerate(SLOTS):
+        s = st[k]
+        valid = s[:, 0, 1] != 0
+        if not valid.any():
+            continue
+        s = s[valid]
+        rt0 = s[:, 0, 1]
+        rt5 = s[:, 5, 1]
+        ok5 = rt5 != 0
+        entry = {"kernel": name, "wgs": int(valid.sum()),
+                 "skew_us": round((rt0.max() - rt0.min()) / 100.0, 2)}
+        if ok5.any():
+            entry["span_us"] = round((rt5[ok5].max() - rt0.min()) / 100.0, 2)
+            entry["wg_med_us"] = round(float(np.median(rt5[ok5] - rt0[ok5])) / 100.0, 2)
+            if prev_end is not None:
+                entry["gap_us"] = round((rt0.min() - prev_end) / 100.0, 2)
+            prev_end = rt5[ok5].max()
+        phases = {}
+        for a, b in ((0, 1), (1, 2), (2, 3), (3, 4), (4, 5)):
+            m = (s[:, a, 0] != 0) & (s[:, b, 0] != 0)
+            if m.any():
+                phases[f"p{a}{b}_cyc"] = int(np.median(s[m, b, 0] - s[m, a, 0]))
+        entry.update(phases)
+        res["kernels"].append(entry)
+        print(json.dumps(entry), flush=True)
+    res["microbench_us_per_kernel"] = microbench(native.load())
+    print(json.dumps({"microbench_us_per_kernel": res["microbench_us_per_kernel"]}), flush=True)
+    eng.close()
+
+
+if __name__ == "__main__":
+    main()

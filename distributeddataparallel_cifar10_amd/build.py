@@ -19,6 +19,12 @@ CSRC = os.path.join(PKG_DIR, "csrc")
 LIB_DIR = os.path.join(PKG_DIR, "_lib")
 ENGINE_LIB = os.path.join(LIB_DIR, "libdca_engine.so")
 ARCH = os.environ.get("DCA_OFFLOAD_ARCH", "gfx950")
+# Variants: "" = production; "stamps" = diagnostic build with in-kernel phase stamps (-DDCA_STAMPS).
+VARIANTS = {"": [], "stamps": ["-DDCA_STAMPS"]}
+
+
+def lib_path(variant: str = "") -> str:
+    return ENGINE_LIB if not variant else os.path.join(LIB_DIR, f"libdca_engine_{variant}.so")
 
 
 def _hipcc() -> str:
@@ -32,8 +38,8 @@ def _sources():
     return sorted(os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith((".hip", ".h", ".cpp")))
 
 
-def _digest() -> str:
-    h = hashlib.sha256(ARCH.encode())
+def _digest(variant: str = "") -> str:
+    h = hashlib.sha256((ARCH + "|" + variant).encode())
     for p in _sources():
         with open(p, "rb") as f:
             h.update(os.path.basename(p).encode())
@@ -41,19 +47,20 @@ def _digest() -> str:
     return h.hexdigest()
 
 
-def build(force: bool = False, verbose: bool = False) -> str:
+def build(force: bool = False, verbose: bool = False, variant: str = "") -> str:
     """Compile the engine library if sources changed; returns the .so path."""
     os.makedirs(LIB_DIR, exist_ok=True)
-    stamp = ENGINE_LIB + ".sha256"
-    digest = _digest()
-    if not force and os.path.exists(ENGINE_LIB) and os.path.exists(stamp):
+    out = lib_path(variant)
+    stamp = out + ".sha256"
+    digest = _digest(variant)
+    if not force and os.path.exists(out) and os.path.exists(stamp):
         with open(stamp) as f:
             if f.read().strip() == digest:
-                return ENGINE_LIB
-    tmp = ENGINE_LIB + f".tmp{os.getpid()}"
+                return out
+    tmp = out + f".tmp{os.getpid()}"
     cmd = [
         _hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
-        "-Wall", "-Wno-unused-function", "-Wno-unused-variable",
+        "-Wall", "-Wno-unused-function", "-Wno-unused-variable", *VARIANTS[variant],
         os.path.join(CSRC, "engine.hip"), "-o", tmp, "-lrccl",
     ]
     if verbose:
@@ -61,12 +68,12 @@ def build(force: bool = False, verbose: bool = False) -> str:
     res = subprocess.run(cmd, capture_output=True, text=True)
     if res.returncode != 0:
         raise RuntimeError(f"hipcc failed ({res.returncode}):\n{res.stderr[-6000:]}")
-    os.replace(tmp, ENGINE_LIB)
+    os.replace(tmp, out)
     with open(stamp, "w") as f:
         f.write(digest)
-    return ENGINE_LIB
+    return out
 
 
 if __name__ == "__main__":
-    path = build(force="--force" in sys.argv, verbose=True)
-    print(path)
+    for v in (["", "stamps"] if "--all" in sys.argv else [""]):
+        print(build(force="--force" in sys.argv, verbose=True, variant=v))

@@ -34,8 +34,9 @@ constexpr int FLAT_ALLOC = 76160;  // padded allocation
 constexpr int WSLAB_N = 9216;      // trunk-conv wgrad partial (MFMA fragment order)
 constexpr int SSLAB_N = 1088;      // stem wgrad partial: 1024 fragment (32co x 32k) + 32 bias + pad
 constexpr int N_FC_WG = 32;        // workgroups computing the fc1/fc2 weight gradients (inside bwd block 9)
-constexpr int N_TRUNK_RED_WG = 144;  // 9216 / 64
-constexpr int N_STEM_RED_WG = 17;    // 1088 / 64
+constexpr int RED_CHUNK = 32;        // floats reduced per k_reduce workgroup (8 float4 slots x 32 slab groups)
+constexpr int N_TRUNK_RED_WG = WSLAB_N / RED_CHUNK;  // 288
+constexpr int N_STEM_RED_WG = SSLAB_N / RED_CHUNK;   // 34
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
@@ -79,8 +80,32 @@ struct Ctx {
   float* HDH;      // [B][32]   d fc1-preactivation
   float* HDL;      // [B][10]   d logits
   float* HLOSS;    // [B]       per-image CE loss
+  float* HPART;    // [nparts][32] per-tile partial fc1 pre-activations
+  uint8_t* HCODE;  // [B][64][32] head max-pool argmax
   int pstride;     // FPART/BPART stride per block (>= max nparts)
+  unsigned long long* stamps;  // [32 kernel slots][256 wg][8 stamps][2] (diagnostic DCA_STAMPS builds only)
 };
+
+// In-kernel phase stamps (diagnostic build, -DDCA_STAMPS): thread 0 of each workgroup records
+// (s_memtime, s_memrealtime) at phase boundaries.  Never compiled into the production library.
+#ifdef DCA_STAMPS
+#define DCA_STAMP(cx, slot, wg, k)                                                                        \
+  do {                                                                                                     \
+    if (threadIdx.x == 0 && (wg) < 256) {                                                                  \
+      unsigned long long t0_, t1_;                                                                         \
+      __builtin_amdgcn_sched_barrier(0);                                                                   \
+      asm volatile("s_memtime %0\n\ts_memrealtime %1\n\ts_waitcnt lgkmcnt(0)" : "=s"(t0_), "=s"(t1_)::"memory"); \
+      __builtin_amdgcn_sched_barrier(0);                                                                   \
+      unsigned long long* p_ = (cx).stamps + ((((size_t)(slot) * 256 + (wg)) * 8 + (k)) << 1);           \
+      p_[0] = t0_;                                                                                         \
+      p_[1] = t1_;                                                                                         \
+    }                                                                                                      \
+  } while (0)
+#else
+#define DCA_STAMP(cx, slot, wg, k) \
+  do {                             \
+  } while (0)
+#endif
 
 // sample id of image n of the current batch, clamped into range
 __device__ __forceinline__ int sample_id(const Ctx& cx, int n) {
@@ -99,4 +124,27 @@ __device__ __forceinline__ unsigned pack2bf(float a, float b) {
   return (unsigned)f2bf(a) | ((unsigned)f2bf(b) << 16);
 }
 
+}  // namespace dca
+
+namespace dca {
+constexpr int RED_F = 1600;  // floats of per-workgroup reduction scratch in LDS
+// Dynamic-LDS plan of every kernel, shared by the device carve-up and the host launch sizes (bytes; every
+// region a multiple of 16 so carve offsets stay 16-byte aligned -- cdna guide Guideline 17).
+template <bool BF, int R, int RW>
+struct LdsPlan {
+  static constexpr size_t RB = BF ? 64 : 128, ESZ = BF ? 2 : 4, PADE = 16 / ESZ, RR = R + 2;
+  static constexpr size_t RED = RED_F * 4;  // reduction scratch
+  static constexpr size_t IR = 2 * RR + 2, IW = 34;
+  static constexpr size_t stem = 288 * RB + RR * 18 * RB + 3 * IR * IW * 4 + 32 * 32 * ESZ + 32 * 4 + RED + 32 * 4;
+  static constexpr size_t fwd = 288 * RB + RR * 18 * RB + RED + 4 * 32 * 4;
+  static constexpr size_t head1 = R * 512 * 4 + 128 * R * 4 + RED + 5 * 32 * 4;
+  static constexpr size_t head2 = 256 * 4 + 320 * 4 + 96 * 4 + 128 * R + 128 * R * 4 + RED + 4 * 32 * 4;
+  static constexpr size_t dgrad = 288 * RB + RR * 18 * RB + 2 * R * 512 * 4 + RED + 11 * 32 * 4;
+  static constexpr size_t DS0 = R * 16 + PADE, XS0 = RR * 16 + PADE, IRb = 2 * R + 2, DSP = 2 * R * 32 + PADE;
+  static constexpr size_t dgrad0 = dgrad + 32 * DS0 * ESZ + 3 * 32 * XS0 * ESZ + 3 * IRb * IW * 4 + 32 * DSP * ESZ;
+  static constexpr size_t DS = RW * 16 + PADE, XS = (RW + 2) * 16 + PADE;
+  static constexpr size_t wgrad = 32 * DS * ESZ + 3 * 32 * XS * ESZ;
+  static constexpr size_t fc = (64 * 32 + 64 * 64 + 64 * 32 + 64 * 16) * 4;  // batch <= 64
+};
+constexpr int BMAX_LIMIT = 64;  // per-rank batch supported by the unrolled staging paths
 }  // namespace dca

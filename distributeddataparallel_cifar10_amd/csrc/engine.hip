@@ -82,11 +82,12 @@ struct Engine {
   std::map<int, hipGraphExec_t> graphs;
   std::map<std::string, void*> regions;
   // dynamic LDS sizes
-  size_t s_stem = 0, s_fwd = 0, s_head = 0, s_dgrad = 0, s_dgrad0 = 0, s_wgrad = 0;
+  size_t s_stem = 0, s_fwd = 0, s_head1 = 0, s_head2 = 0, s_dgrad = 0, s_dgrad0 = 0, s_wgrad = 0, s_fc = 0;
   // kernel entry points for the selected (BF, R, RW) instantiation
   void (*kstem)(Ctx) = nullptr;
   void (*kfwd)(Ctx, int) = nullptr;
-  void (*khead)(Ctx) = nullptr;
+  void (*khead1)(Ctx) = nullptr;
+  void (*khead2)(Ctx) = nullptr;
   void (*kbwd)(Ctx, int) = nullptr;
   void (*kred)(Ctx, int, int) = nullptr;
   void (*kapply)(Ctx, int) = nullptr;
@@ -98,24 +99,20 @@ template <bool BF, int R, int RW>
 static void bind_kernels(Engine* e) {
   e->kstem = k_stem_block0<BF, R>;
   e->kfwd = k_fwd_block<BF, R>;
-  e->khead = k_head<R>;
+  e->khead1 = k_head1<R>;
+  e->khead2 = k_head2<R>;
+  using L = LdsPlan<BF, R, RW>;
+  e->s_stem = L::stem;
+  e->s_fwd = L::fwd;
+  e->s_head1 = L::head1;
+  e->s_head2 = L::head2;
+  e->s_dgrad = L::dgrad;
+  e->s_dgrad0 = L::dgrad0;
+  e->s_wgrad = L::wgrad;
+  e->s_fc = L::fc;
   e->kbwd = k_bwd_block<BF, R, RW>;
   e->kred = k_reduce<BF>;
   e->kapply = k_apply_sgd<BF>;
-}
-
-static void compute_lds(Engine* e) {
-  const int R = e->R, RR = R + 2, RW = e->RW;
-  const size_t RB = e->bf ? 64 : 128, ESZ = e->bf ? 2 : 4, PADE = 16 / ESZ;
-  const size_t IR = 2 * RR + 2, IW = 34;
-  e->s_stem = 288 * RB + RR * 18 * RB + 3 * IR * IW * 4 + 32 * 32 * ESZ + 32 * 4 + 512 * 4 + 32 * 4;
-  e->s_fwd = 288 * RB + RR * 18 * RB + (512 + 4 * 32) * 4;
-  e->s_head = (8192 * 2 + 2048 * 2) * 4 + 2048 + (512 + 5 * 32 + 32 + 32 + 16 + 16) * 4;
-  e->s_dgrad = 288 * RB + RR * 18 * RB + 2 * R * 512 * 4 + (512 + 11 * 32) * 4;
-  const size_t DS0 = R * 16 + PADE, XS0 = RR * 16 + PADE, IRb = 2 * R + 2, DSP = 2 * R * 32 + PADE;
-  e->s_dgrad0 = e->s_dgrad + 32 * DS0 * ESZ + 3 * 32 * XS0 * ESZ + 3 * IRb * IW * 4 + 32 * DSP * ESZ;
-  const size_t DS = RW * 16 + PADE, XS = (RW + 2) * 16 + PADE;
-  e->s_wgrad = 32 * DS * ESZ + 3 * 32 * XS * ESZ;
 }
 
 static int alloc_workspace(Engine* e) {
@@ -132,9 +129,10 @@ static int alloc_workspace(Engine* e) {
       {"STATS", 10 * 32 * 8},        {"BPART", 2 * pstride * 32 * 8}, {"WSLAB", nslab * WSLAB_N * 4},
       {"SSLAB", pstride * SSLAB_N * 4}, {"HP", bmax * 2048 * 4},      {"HH", bmax * 32 * 4},
       {"HDH", bmax * 32 * 4},        {"HDL", bmax * 16 * 4},          {"HLOSS", bmax * 4},
+      {"HPART", pstride * 32 * 4},   {"HCODE", bmax * 2048},
       {"WT_F", 9216 * esz},          {"WT_D", 9216 * esz},            {"SW", 1024 * esz},
       {"RS_BASE", 64 * 4},           {"CURSOR", 16},                  {"STEPS", 16},
-      {"LOSS", 16},
+      {"LOSS", 16},                  {"STAMPS", 32 * 256 * 8 * 2 * 8},
   };
   size_t total = 0;
   for (auto& r : regs) total += align_up(r.bytes, 256);
@@ -162,6 +160,8 @@ static int alloc_workspace(Engine* e) {
   c.HDH = (float*)e->regions["HDH"];
   c.HDL = (float*)e->regions["HDL"];
   c.HLOSS = (float*)e->regions["HLOSS"];
+  c.HPART = (float*)e->regions["HPART"];
+  c.HCODE = (uint8_t*)e->regions["HCODE"];
   c.wt_f = e->regions["WT_F"];
   c.wt_d = e->regions["WT_D"];
   c.sw = e->regions["SW"];
@@ -170,14 +170,16 @@ static int alloc_workspace(Engine* e) {
   c.step_count = (int*)e->regions["STEPS"];
   c.loss_acc = (double*)e->regions["LOSS"];
   c.pstride = (int)pstride;
+  c.stamps = (unsigned long long*)e->regions["STAMPS"];
   return 0;
 }
 
 static int set_lds_limits(Engine* e) {
-  const size_t dg = std::max(std::max(e->s_dgrad, e->s_dgrad0), e->s_wgrad);
+  const size_t dg = std::max(std::max(e->s_dgrad, e->s_dgrad0), std::max(e->s_wgrad, e->s_fc));
   HIPCK(hipFuncSetAttribute((const void*)e->kstem, hipFuncAttributeMaxDynamicSharedMemorySize, (int)e->s_stem));
   HIPCK(hipFuncSetAttribute((const void*)e->kfwd, hipFuncAttributeMaxDynamicSharedMemorySize, (int)e->s_fwd));
-  HIPCK(hipFuncSetAttribute((const void*)e->khead, hipFuncAttributeMaxDynamicSharedMemorySize, (int)e->s_head));
+  HIPCK(hipFuncSetAttribute((const void*)e->khead1, hipFuncAttributeMaxDynamicSharedMemorySize, (int)e->s_head1));
+  HIPCK(hipFuncSetAttribute((const void*)e->khead2, hipFuncAttributeMaxDynamicSharedMemorySize, (int)e->s_head2));
   HIPCK(hipFuncSetAttribute((const void*)e->kbwd, hipFuncAttributeMaxDynamicSharedMemorySize, (int)dg));
   return 0;
 }
@@ -191,11 +193,12 @@ static int enqueue_step(Engine* e, int B) {
   const dim3 blk(NT);
   hipLaunchKernelGGL(e->kstem, dim3(nparts), blk, e->s_stem, e->st, cx);
   for (int i = 1; i < NBLK; ++i) hipLaunchKernelGGL(e->kfwd, dim3(nparts), blk, e->s_fwd, e->st, cx, i);
-  hipLaunchKernelGGL(e->khead, dim3(B), blk, e->s_head, e->st, cx);
+  hipLaunchKernelGGL(e->khead1, dim3(nparts), blk, e->s_head1, e->st, cx);
+  hipLaunchKernelGGL(e->khead2, dim3(nparts), blk, e->s_head2, e->st, cx);
   for (int i = NBLK - 1; i >= 0; --i) {
     const int extra = (i == NBLK - 1) ? N_FC_WG : nw;
     size_t lds = (i == 0) ? e->s_dgrad0 : e->s_dgrad;
-    if (i < NBLK - 1) lds = std::max(lds, e->s_wgrad);
+    lds = std::max(lds, (i < NBLK - 1) ? e->s_wgrad : e->s_fc);
     hipLaunchKernelGGL(e->kbwd, dim3(nparts + extra), blk, lds, e->st, cx, i);
     if (i == NBLK - 1 && e->in.world_size > 1) {  // bucket A ready: overlap its all-reduce with the trunk bwd
       HIPCK(hipEventRecord(e->evA, e->st));
@@ -220,6 +223,153 @@ static int enqueue_step(Engine* e, int B) {
 
 }  // namespace dca
 
+namespace dca {
+__global__ void k_mb_empty(int) {}
+// Memory round-trip calibration kernels (8 float4 = 32 KiB per workgroup unless noted):
+//   1: all WGs read the same 32 KiB (never written) + serial LDS reduce by thread 0
+//   2: one float per thread, WG-private, then store
+//   3: WG-private 32 KiB (never written), per-thread sums stored
+//   4: WG-private 32 KiB written by the PREVIOUS kernel at the same WG index (ping-pong)
+//   5: like 4 but reading the region written by WG (w+1) % grid (another XCD under round-robin dispatch)
+//   6: every WG reads the same 32 KiB that WG 0 of the previous kernel wrote (BN-partials pattern)
+__global__ void __launch_bounds__(NT) k_mb_load(const f32x4* src, f32x4* dst, int kind) {
+  const int t = threadIdx.x, w = blockIdx.x, g = gridDim.x;
+  if (kind == 2) {
+    const float v = ((const float*)src)[w * NT + t];
+    ((float*)dst)[w * NT + t] = v + 1.f;
+    return;
+  }
+  const int base = kind == 1 || kind == 6 ? 0 : (kind == 5 ? ((w + 1) % g) : w) * 2048;
+  f32x4 v[8];
+#pragma unroll
+  for (int m = 0; m < 8; ++m) v[m] = src[base + t + NT * m];
+  if (kind == 1) {
+    float s = 0.f;
+#pragma unroll
+    for (int m = 0; m < 8; ++m) s += v[m].x + v[m].y + v[m].z + v[m].w;
+    __shared__ float r[NT];
+    r[t] = s;
+    __syncthreads();
+    if (t == 0) {
+      float a = 0.f;
+      for (int k = 0; k < NT; ++k) a += r[k];
+      ((float*)dst)[w] = a;
+    }
+    return;
+  }
+  if (kind == 3) {
+    f32x4 s = v[0];
+#pragma unroll
+    for (int m = 1; m < 8; ++m) s += v[m];
+    dst[w * NT + t] = s;
+    return;
+  }
+  if (kind == 6 && w != 0) {
+    f32x4 s = v[0];
+#pragma unroll
+    for (int m = 1; m < 8; ++m) s += v[m];
+    dst[4096 + w * NT + t] = s;  // scratch, away from the region the next kernel reads
+    return;
+  }
+#pragma unroll
+  for (int m = 0; m < 8; ++m) dst[(kind == 6 ? 0 : w * 2048) + t + NT * m] = v[m] + 1.f;
+}
+// In-kernel all-gather of 64 floats per workgroup among G co-resident workgroups, `rounds` times
+// (the BN-statistics exchange of a persistent design).  Data-as-flag granules {tag, value} (8-byte relaxed
+// agent-scope atomic stores/loads, i.e. sc1 write-through / L2-bypassing): no fences needed.  Parity
+// double-buffered by round.  Every spin is bounded; a timeout sets *err and the kernel still completes.
+template <int NTH>
+__global__ void __launch_bounds__(NTH) k_mb_xchg(unsigned long long* gran, unsigned* err, int rounds, int sleep) {
+  const int t = threadIdx.x, w = blockIdx.x, G = gridDim.x;
+  __shared__ float red[64];
+  float keep = 0.f;
+  for (int r = 0; r < rounds; ++r) {
+    const unsigned long long tag = (unsigned long long)(r + 1) << 32;
+    unsigned long long* buf = gran + (size_t)(r & 1) * G * 64;
+    if (t < 64) {
+      const float v = (float)(w + t) + keep;
+      __hip_atomic_store(buf + w * 64 + t, tag | __float_as_uint(v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      float acc = 0.f;
+      for (unsigned spins = 0;; ++spins) {
+        bool ok = true;
+        acc = 0.f;
+        for (int k = 0; k < G; ++k) {
+          const unsigned long long x = __hip_atomic_load(buf + k * 64 + t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          ok &= (x & 0xffffffff00000000ull) == tag;
+          acc += __uint_as_float((unsigned)x);
+        }
+        if (__all(ok)) break;
+        if (spins > (1u << 20)) {
+          atomicOr(err, 1u);
+          break;
+        }
+        if (sleep) __builtin_amdgcn_s_sleep(1);
+      }
+      red[t] = acc;
+    }
+    __syncthreads();
+    keep = red[t & 63] * 1e-9f;
+    __syncthreads();
+  }
+  if (t == 0 && keep == 12345.f) err[1] = 1;  // keep the chain live
+}
+// Same exchange, but the sweep is spread over all waves of the workgroup and uses plain (non-volatile)
+// sc1 buffer loads, so every wave has all of its granule loads in flight at once.
+template <int NTH>
+__global__ void __launch_bounds__(NTH) k_mb_xchg2(unsigned long long* gran, unsigned* err, int rounds) {
+  constexpr int NW = NTH / 64, KMAX = 8;
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6, w = blockIdx.x, G = gridDim.x;
+  __shared__ float red[NW][64];
+  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(gran, (short)0, 2 * G * 64 * 8, 0x00020000);
+  float keep = 0.f;
+  for (int r = 0; r < rounds; ++r) {
+    const unsigned tag = (unsigned)(r + 1);
+    const int boff = (r & 1) * G * 64;
+    if (wave == 0) {
+      const float v = (float)(w + lane) + keep;
+      __hip_atomic_store(gran + boff + w * 64 + lane, ((unsigned long long)tag << 32) | __float_as_uint(v),
+                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    float acc = 0.f;
+    for (unsigned spins = 0;; ++spins) {
+      bool ok = true;
+      acc = 0.f;
+      unsigned lo[KMAX], hi[KMAX];
+#pragma unroll
+      for (int kk = 0; kk < KMAX; ++kk) {
+        const int k = wave + NW * kk;
+        if (k < G) {
+          const auto x = __builtin_amdgcn_raw_buffer_load_b64(rs, (boff + k * 64 + lane) * 8, 0, 16);
+          lo[kk] = x[0];
+          hi[kk] = x[1];
+        } else {
+          lo[kk] = 0u;
+          hi[kk] = tag;
+        }
+      }
+#pragma unroll
+      for (int kk = 0; kk < KMAX; ++kk) {
+        ok &= hi[kk] == tag;
+        acc += __uint_as_float(lo[kk]);
+      }
+      if (__all(ok)) break;
+      if (spins > (1u << 20)) {
+        atomicOr(err, 1u);
+        break;
+      }
+    }
+    red[wave][lane] = acc;
+    __syncthreads();
+    float s = 0.f;
+#pragma unroll
+    for (int k = 0; k < NW; ++k) s += red[k][lane];
+    keep = s * 1e-9f;
+    __syncthreads();
+  }
+  if (t == 0 && keep == 12345.f) err[1] = 1;
+}
+}  // namespace dca
+
 using dca::Engine;
 
 extern "C" {
@@ -242,6 +392,11 @@ int dca_engine_create(const DcaInit* in, int n_indices, void** out) {
   e->bf = in->bf16 != 0;
   e->R = in->rows;
   e->RW = e->bf ? 16 : 8;
+  if (in->bmax < 1 || in->bmax > dca::BMAX_LIMIT) {
+    g_err = "batch_max must be in [1, 64]";
+    delete e;
+    return -1;
+  }
   if (e->R != 2 && e->R != 4) {
     g_err = "rows must be 2 or 4";
     delete e;
@@ -252,7 +407,6 @@ int dca_engine_create(const DcaInit* in, int n_indices, void** out) {
   else if (e->bf) dca::bind_kernels<true, 2, 16>(e);
   else if (e->R == 4) dca::bind_kernels<false, 4, 8>(e);
   else dca::bind_kernels<false, 2, 8>(e);
-  dca::compute_lds(e);
   if (dca::set_lds_limits(e)) { delete e; return -1; }
   HIPCK(hipStreamCreateWithFlags(&e->st, hipStreamNonBlocking));
   HIPCK(hipStreamCreateWithFlags(&e->cst, hipStreamNonBlocking));
@@ -399,5 +553,85 @@ void* dca_engine_region(void* h, const char* name) {
 }
 
 size_t dca_engine_workspace_bytes(void* h) { return ((Engine*)h)->ws_bytes; }
+
+// Persistent-exchange calibration: G workgroups of `nth` threads, `rounds` all-gather rounds.
+// Writes the kernel time (us, median of `iters`) and the timeout flag.
+int dca_microbench_xchg(int G, int nth, int rounds, int iters, int sleep, float* us, int* err_out) {
+  hipStream_t s;
+  HIPCK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+  unsigned long long* gran;
+  unsigned* err;
+  HIPCK(hipMalloc(&gran, (size_t)2 * G * 64 * 8));
+  HIPCK(hipMalloc(&err, 16));
+  HIPCK(hipMemset(err, 0, 16));
+  hipEvent_t a, b;
+  HIPCK(hipEventCreate(&a));
+  HIPCK(hipEventCreate(&b));
+  float best = 1e30f;
+  for (int it = 0; it < iters; ++it) {
+    HIPCK(hipMemsetAsync(gran, 0, (size_t)2 * G * 64 * 8, s));
+    HIPCK(hipEventRecord(a, s));
+    if (sleep == 2 && nth == 1024) hipLaunchKernelGGL(dca::k_mb_xchg2<1024>, dim3(G), dim3(1024), 0, s, gran, err, rounds);
+    else if (sleep == 2) hipLaunchKernelGGL(dca::k_mb_xchg2<256>, dim3(G), dim3(256), 0, s, gran, err, rounds);
+    else if (nth == 1024) hipLaunchKernelGGL(dca::k_mb_xchg<1024>, dim3(G), dim3(1024), 0, s, gran, err, rounds, sleep);
+    else hipLaunchKernelGGL(dca::k_mb_xchg<256>, dim3(G), dim3(256), 0, s, gran, err, rounds, sleep);
+    HIPCK(hipEventRecord(b, s));
+    HIPCK(hipEventSynchronize(b));
+    float ms = 0.f;
+    HIPCK(hipEventElapsedTime(&ms, a, b));
+    best = std::min(best, ms);
+  }
+  unsigned herr[2];
+  HIPCK(hipMemcpy(herr, err, 8, hipMemcpyDeviceToHost));
+  *us = best * 1e3f;
+  *err_out = (int)herr[0];
+  (void)hipFree(gran);
+  (void)hipFree(err);
+  (void)hipEventDestroy(a);
+  (void)hipEventDestroy(b);
+  (void)hipStreamDestroy(s);
+  return 0;
+}
+
+// Launch-floor calibration: a hipGraph of `nk` dependent kernels of `kind` (0 empty; 1..6 see k_mb_load)
+// with `grid` workgroups, replayed `iters` times.  Writes microseconds per kernel to *us.
+int dca_microbench(int kind, int nk, int grid, int iters, float* us) {
+  hipStream_t s;
+  HIPCK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+  char* buf;
+  const size_t half = (size_t)(grid + 1) * 2048 * 16 + (1 << 16);
+  HIPCK(hipMalloc(&buf, 2 * half));
+  HIPCK(hipMemset(buf, 0, 2 * half));
+  hipGraph_t g;
+  HIPCK(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
+  for (int k = 0; k < nk; ++k) {
+    const bool odd = (k & 1) && kind >= 4;
+    const dca::f32x4* src = (const dca::f32x4*)(buf + (odd ? half : 0));
+    dca::f32x4* dst = (dca::f32x4*)(buf + (odd ? 0 : half));
+    if (kind == 0) hipLaunchKernelGGL(dca::k_mb_empty, dim3(grid), dim3(dca::NT), 0, s, k);
+    else hipLaunchKernelGGL(dca::k_mb_load, dim3(grid), dim3(dca::NT), 0, s, src, dst, kind);
+  }
+  HIPCK(hipStreamEndCapture(s, &g));
+  hipGraphExec_t ex;
+  HIPCK(hipGraphInstantiate(&ex, g, nullptr, nullptr, 0));
+  hipEvent_t a, b;
+  HIPCK(hipEventCreate(&a));
+  HIPCK(hipEventCreate(&b));
+  for (int w = 0; w < 3; ++w) HIPCK(hipGraphLaunch(ex, s));
+  HIPCK(hipEventRecord(a, s));
+  for (int it = 0; it < iters; ++it) HIPCK(hipGraphLaunch(ex, s));
+  HIPCK(hipEventRecord(b, s));
+  HIPCK(hipEventSynchronize(b));
+  float ms = 0.f;
+  HIPCK(hipEventElapsedTime(&ms, a, b));
+  *us = 1e3f * ms / (float)(iters * nk);
+  (void)hipGraphExecDestroy(ex);
+  (void)hipGraphDestroy(g);
+  (void)hipEventDestroy(a);
+  (void)hipEventDestroy(b);
+  (void)hipFree(buf);
+  (void)hipStreamDestroy(s);
+  return 0;
+}
 
 }  // extern "C"

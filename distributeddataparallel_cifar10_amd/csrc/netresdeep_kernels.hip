@@ -1,11 +1,12 @@
 // Fused NetResDeep training step for CDNA4 (gfx950 / MI355X).
 //
-// One training step = 22 dependent kernels (world_size 1), all captured in one hipGraph by engine.cpp:
+// One training step = 23 dependent kernels (world_size 1), all captured in one hipGraph by engine.cpp:
 //   k_stem_block0           : uint8 gather + normalise + conv1+bias+ReLU+maxpool (MFMA) -> x0, then trunk conv 0
 //   k_fwd_block  (i=1..9)   : finalise BN(i-1) batch stats, apply BN+ReLU+residual while staging the LDS tile,
 //                             trunk conv i on MFMA, per-tile BN partials (mean, M2) in the epilogue
-//   k_head                  : BN(9)+ReLU+residual, maxpool, fc1+ReLU, fc2, cross-entropy fwd+bwd, fc bwd to the
-//                             pooled features, maxpool bwd -> g10, first BN-backward partial sums
+//   k_head1                 : BN(9)+ReLU+residual, maxpool, per-tile partial fc1 (each tile owns a K-slice of W1)
+//   k_head2                 : fc1 finish+ReLU, fc2, cross-entropy fwd+bwd, fc bwd to the tile's pooled features,
+//                             maxpool bwd -> g10, first BN-backward partial sums
 //   k_bwd_block  (i=9..0)   : BN-backward (grid-wide sums finalised in the prologue) -> dgrad conv on MFMA
 //                             (+ residual), next block's BN-backward partials in the epilogue; horizontally fused
 //                             extra workgroups compute the wgrad of block i+1 (or the fc1/fc2 grads for i=9);
@@ -14,6 +15,9 @@
 //                             rebuild of the MFMA-layout weight copies, loss/cursor bookkeeping
 // With world_size > 1, k_reduce only writes gradients; engine.cpp all-reduces them over RCCL (bucket A overlaps
 // the trunk backward) and k_apply_sgd updates.
+//
+// Latency discipline: every kernel issues ALL of its global loads (tiles, BN partials, weights) before its first
+// use of any of them, so a kernel pays ~one memory round trip, not one per loop iteration.
 //
 // Reference semantics mirrored: model/resnet.py:5-37 (weight-shared ResBlock, skip after ReLU), main.py:27-39
 // (SGD lr, CrossEntropy mean), BatchNorm2d train-mode statistics and running-stat EMA applied 10x per forward.
@@ -78,12 +82,28 @@ template <bool BF> __device__ __forceinline__ void zero_recs(char* base, int rec
     *(uint4*)(base + ((r * Rec<BF>::NCH + idx % Rec<BF>::NCH) << 4)) = uint4{0u, 0u, 0u, 0u};
   }
 }
-// derived weight [9][32 out][32 in] (plain, compute type) -> swizzled LDS records (key = out)
-template <bool BF> __device__ __forceinline__ void stage_weights(char* ws, const void* src) {
+// derived weight [9][32 out][32 in] (plain, compute type) -> swizzled LDS records (key = out).
+// Split in two so the global loads can be issued together with a kernel's other prologue loads.
+template <bool BF> struct WStage {
+  static constexpr int N = 288 * Rec<BF>::NCH, M = (N + NT - 1) / NT;
+  uint4 v[M];
+};
+template <bool BF> __device__ __forceinline__ void wstage_load(WStage<BF>& w, const void* src) {
   const uint4* s = (const uint4*)src;
-  for (int idx = threadIdx.x; idx < 288 * Rec<BF>::NCH; idx += NT) {
-    const int rec = idx / Rec<BF>::NCH, ch = idx % Rec<BF>::NCH;
-    *(uint4*)(ws + rec_off<BF>(rec, rec & 31, ch)) = s[idx];
+#pragma unroll
+  for (int m = 0; m < WStage<BF>::M; ++m) {
+    const int idx = threadIdx.x + NT * m;
+    if (idx < WStage<BF>::N) w.v[m] = s[idx];
+  }
+}
+template <bool BF> __device__ __forceinline__ void wstage_store(const WStage<BF>& w, char* ws) {
+#pragma unroll
+  for (int m = 0; m < WStage<BF>::M; ++m) {
+    const int idx = threadIdx.x + NT * m;
+    if (idx < WStage<BF>::N) {
+      const int rec = idx / Rec<BF>::NCH, ch = idx % Rec<BF>::NCH;
+      *(uint4*)(ws + rec_off<BF>(rec, rec & 31, ch)) = w.v[m];
+    }
   }
 }
 
@@ -176,57 +196,115 @@ __device__ __forceinline__ void wgrad_core(const char* dyT, int DS, const char* 
 }
 
 // ------------------------------------------------------------------------------------------------------------
-// BatchNorm statistic reductions (deterministic, fixed order).
+// BatchNorm statistics (deterministic, fixed order).  A block's per-tile partials are float2 per channel; thread t
+// owns float4 #(t + 256 m) = channels 2(t&15), 2(t&15)+1 of tile (t>>4) + 16 m.  parts_load issues the loads
+// (in flight together with the kernel's other prologue loads), *_finish consumes them.
 // ------------------------------------------------------------------------------------------------------------
-// forward: per-tile (mean, M2) with equal counts -> batch mean and biased variance (Chan's combination)
-__device__ void reduce_fstats(const float2* part, int nparts, float cnt, float* red, float* s_mean, float* s_var) {
-  const int t = threadIdx.x, c = t & 31, g = t >> 5;
-  float sm = 0.f;
-  for (int w = g; w < nparts; w += 8) sm += part[w * 32 + c].x;
-  red[t] = sm;
-  __syncthreads();
-  if (t < 32) {
-    float s = 0.f;
+struct Parts {
+  f32x4 v[8];
+};
+__device__ __forceinline__ void parts_load(Parts& P, const float2* part, int nparts) {
+  const f32x4* p4 = (const f32x4*)part;
+  const int n4 = nparts * 16;
 #pragma unroll
-    for (int k = 0; k < 8; ++k) s += red[k * 32 + t];
-    s_mean[t] = s / (float)nparts;
+  for (int m = 0; m < 8; ++m) {
+    const int idx = threadIdx.x + NT * m;
+    P.v[m] = idx < n4 ? p4[idx] : z4();
+  }
+}
+// forward: per-tile (mean m_w, M2_w) over `cnt` pixels each -> batch mean and biased variance.
+// Division-free single pass with a per-channel shift K = m_0 (tile 0's mean, loaded by every thread):
+//   S1 = sum (m_w - K), S2 = sum (m_w - K)^2, Q = sum M2_w
+//   mean = K + S1/n,  M2 = Q + cnt * (S2 - S1^2/n)          (n = nparts; exact algebra, no cancellation
+// beyond the spread of the tile means around K).  red: RED_F floats.
+__device__ void fstats_finish(const Parts& P, const float2* part, int nparts, float cnt, float* red, float* s_mean,
+                              float* s_var) {
+  const int t = threadIdx.x, grp = t >> 4, cp = t & 15;
+  const int n4 = nparts * 16;
+  const f32x4* p4 = (const f32x4*)part;
+  const f32x4 k4 = p4[cp];  // tile 0, channels 2cp, 2cp+1 (same lines as thread cp's first load)
+  float s10 = 0.f, s20 = 0.f, q0 = 0.f, s11 = 0.f, s21 = 0.f, q1 = 0.f;
+#pragma unroll
+  for (int m = 0; m < 8; ++m) {
+    if (t + NT * m < n4) {
+      const float d0 = P.v[m].x - k4.x, d1 = P.v[m].z - k4.z;
+      s10 += d0;
+      s20 += d0 * d0;
+      q0 += P.v[m].y;
+      s11 += d1;
+      s21 += d1 * d1;
+      q1 += P.v[m].w;
+    }
+  }
+  for (int idx = 8 * NT + t; idx < n4; idx += NT) {  // more than 128 tiles (batch > 32): rare slow path
+    const f32x4 v = p4[idx];
+    const float d0 = v.x - k4.x, d1 = v.z - k4.z;
+    s10 += d0;
+    s20 += d0 * d0;
+    q0 += v.y;
+    s11 += d1;
+    s21 += d1 * d1;
+    q1 += v.w;
+  }
+  red[grp * 32 + 2 * cp] = s10;
+  red[grp * 32 + 2 * cp + 1] = s11;
+  red[512 + grp * 32 + 2 * cp] = s20;
+  red[512 + grp * 32 + 2 * cp + 1] = s21;
+  red[1024 + grp * 32 + 2 * cp] = q0;
+  red[1024 + grp * 32 + 2 * cp + 1] = q1;
+  if (t < 16) {
+    red[1536 + 2 * t] = k4.x;  // shifts for the finishing threads
+    red[1536 + 2 * t + 1] = k4.z;
   }
   __syncthreads();
-  const float mean = s_mean[c];
-  float m2 = 0.f;
-  for (int w = g; w < nparts; w += 8) {
-    const float2 p = part[w * 32 + c];
-    const float d = p.x - mean;
-    m2 += p.y + cnt * d * d;
-  }
-  red[t] = m2;
-  __syncthreads();
   if (t < 32) {
-    float s = 0.f;
+    float s1 = 0.f, s2 = 0.f, q = 0.f;
 #pragma unroll
-    for (int k = 0; k < 8; ++k) s += red[k * 32 + t];
-    s_var[t] = s / ((float)nparts * cnt);
+    for (int g = 0; g < 16; ++g) {
+      s1 += red[g * 32 + t];
+      s2 += red[512 + g * 32 + t];
+      q += red[1024 + g * 32 + t];
+    }
+    const float inv_n = 1.f / (float)nparts;
+    const float m2 = q + cnt * (s2 - s1 * s1 * inv_n);
+    s_mean[t] = red[1536 + t] + s1 * inv_n;
+    s_var[t] = fmaxf(m2, 0.f) * inv_n / cnt;
   }
   __syncthreads();
 }
-// backward: per-tile (sum dz, sum dz*xhat) -> totals
-__device__ void reduce_bsums(const float2* part, int nparts, float* red, float* s_a, float* s_b) {
-  const int t = threadIdx.x, c = t & 31, g = t >> 5;
-  float sa = 0.f, sb = 0.f;
-  for (int w = g; w < nparts; w += 8) {
-    const float2 p = part[w * 32 + c];
-    sa += p.x;
-    sb += p.y;
+// backward: per-tile (sum dz, sum dz*xhat) -> totals.  red: 1024 floats.
+__device__ void bsums_finish(const Parts& P, const float2* part, int nparts, float* red, float* s_a, float* s_b) {
+  const int t = threadIdx.x, grp = t >> 4, cp = t & 15;
+  const int n4 = nparts * 16;
+  float a0 = 0.f, b0 = 0.f, a1 = 0.f, b1 = 0.f;
+#pragma unroll
+  for (int m = 0; m < 8; ++m) {
+    if (t + NT * m < n4) {
+      a0 += P.v[m].x;
+      b0 += P.v[m].y;
+      a1 += P.v[m].z;
+      b1 += P.v[m].w;
+    }
   }
-  red[t] = sa;
-  red[256 + t] = sb;
+  const f32x4* p4 = (const f32x4*)part;
+  for (int idx = 8 * NT + t; idx < n4; idx += NT) {
+    const f32x4 v = p4[idx];
+    a0 += v.x;
+    b0 += v.y;
+    a1 += v.z;
+    b1 += v.w;
+  }
+  red[grp * 32 + 2 * cp] = a0;
+  red[grp * 32 + 2 * cp + 1] = a1;
+  red[512 + grp * 32 + 2 * cp] = b0;
+  red[512 + grp * 32 + 2 * cp + 1] = b1;
   __syncthreads();
   if (t < 32) {
     float a = 0.f, b = 0.f;
 #pragma unroll
-    for (int k = 0; k < 8; ++k) {
-      a += red[k * 32 + t];
-      b += red[256 + k * 32 + t];
+    for (int g = 0; g < 16; ++g) {
+      a += red[g * 32 + t];
+      b += red[512 + g * 32 + t];
     }
     s_a[t] = a;
     s_b[t] = b;
@@ -293,6 +371,45 @@ __device__ __forceinline__ void fwd_epilogue(const f32x4 (&acc)[R / 2], float* y
 
 __device__ __forceinline__ size_t act_off(int blk, int B) { return (size_t)blk * B * 8192; }
 
+// normalise one CIFAR byte (ToTensor + Normalize, reference main.py:55-57)
+__device__ __forceinline__ float norm_px(unsigned byte, int ch) {
+  const float mean = ch == 0 ? 0.4915f : (ch == 1 ? 0.4823f : 0.4468f);
+  const float stdv = ch == 0 ? 0.2470f : (ch == 1 ? 0.2435f : 0.2616f);
+  return ((float)byte / 255.f - mean) / stdv;
+}
+// Stage NROWS input rows (image rows y0 .. y0+NROWS-1, zero outside [0,32)) of the 3 channels into an LDS
+// float tile [3][NROWS][34] with zero pad columns 0 and 33.  Loads are 4-byte words, all issued up front.
+template <int NROWS>
+struct InRows {
+  static constexpr int NW = 3 * NROWS * 8, M = (NW + NT - 1) / NT;
+  unsigned w[M];
+};
+template <int NROWS>
+__device__ __forceinline__ void inrows_load(InRows<NROWS>& I, const uint8_t* img, int y0) {
+  const unsigned* s = (const unsigned*)img;
+#pragma unroll
+  for (int m = 0; m < InRows<NROWS>::M; ++m) {
+    const int idx = threadIdx.x + NT * m;
+    const int ch = idx / (NROWS * 8), ir = (idx >> 3) % NROWS, wd = idx & 7, y = y0 + ir;
+    I.w[m] = (idx < InRows<NROWS>::NW && y >= 0 && y < 32) ? s[(ch * 1024 + y * 32) / 4 + wd] : 0u;
+  }
+}
+template <int NROWS>
+__device__ __forceinline__ void inrows_store(const InRows<NROWS>& I, float* xin, int y0) {
+  constexpr int IW = 34;
+  for (int idx = threadIdx.x; idx < 3 * NROWS * 2; idx += NT) xin[(idx >> 1) * IW + (idx & 1) * 33] = 0.f;
+#pragma unroll
+  for (int m = 0; m < InRows<NROWS>::M; ++m) {
+    const int idx = threadIdx.x + NT * m;
+    if (idx >= InRows<NROWS>::NW) continue;
+    const int ch = idx / (NROWS * 8), ir = (idx >> 3) % NROWS, wd = idx & 7, y = y0 + ir;
+    const bool v = y >= 0 && y < 32;
+    float* dst = xin + (ch * NROWS + ir) * IW + 1 + 4 * wd;
+#pragma unroll
+    for (int b = 0; b < 4; ++b) dst[b] = v ? norm_px((I.w[m] >> (8 * b)) & 255u, ch) : 0.f;
+  }
+}
+
 // ============================================================================================================
 // Forward, block 0: stem (gather+normalise+conv1+bias+ReLU+maxpool) fused with the first trunk conv.
 // ============================================================================================================
@@ -309,27 +426,27 @@ __global__ void __launch_bounds__(NT) k_stem_block0(Ctx cx) {
   TA* swl = (TA*)(xin + 3 * IR * IW);         // [32][32]
   float* s_bias = (float*)(swl + 32 * 32);
   float* red = s_bias + 32;
-  float* s_tmp = red + 512;
+  float* s_tmp = red + RED_F;
+  DCA_STAMP(cx, 0, wg, 0);
 
-  const uint8_t* src = cx.data + (size_t)sample_id(cx, n) * 3072;
-  const float nmean[3] = {0.4915f, 0.4823f, 0.4468f};  // reference main.py:56-57
-  const float nstd[3] = {0.2470f, 0.2435f, 0.2616f};
-  for (int idx = t; idx < 3 * IR * IW; idx += NT) {
-    const int ch = idx / (IR * IW), rem = idx % (IR * IW), ir = rem / IW, ic = rem % IW;
-    const int y = 2 * r0 - 3 + ir, x = ic - 1;
-    float v = 0.f;
-    if (y >= 0 && y < 32 && x >= 0 && x < 32) v = ((float)src[ch * 1024 + y * 32 + x] / 255.f - nmean[ch]) / nstd[ch];
-    xin[idx] = v;
-  }
-  stage_weights<BF>(ws, cx.wt_f);
-  {
-    const uint4* s = (const uint4*)cx.sw;
-    for (int idx = t; idx < 32 * 32 * (int)sizeof(TA) / 16; idx += NT) ((uint4*)swl)[idx] = s[idx];
-  }
-  if (t < 32) s_bias[t] = cx.params[OFF_C1B + t];
+  // ---- issue every global load ----
+  InRows<IR> I;
+  inrows_load<IR>(I, cx.data + (size_t)sample_id(cx, n) * 3072, 2 * r0 - 3);
+  WStage<BF> W;
+  wstage_load<BF>(W, cx.wt_f);
+  constexpr int NSW = 32 * 32 * (int)sizeof(TA) / 16;
+  uint4 swv = uint4{0u, 0u, 0u, 0u};
+  if (t < NSW) swv = ((const uint4*)cx.sw)[t];
+  const float bias_v = t < 32 ? cx.params[OFF_C1B + t] : 0.f;
+  // ---- LDS fills ----
+  inrows_store<IR>(I, xin, 2 * r0 - 3);
+  wstage_store<BF>(W, ws);
+  if (t < NSW) ((uint4*)swl)[t] = swv;
+  if (t < 32) s_bias[t] = bias_v;
   zero_recs<BF>(xs, 0, RR, 18);
   zero_recs<BF>(xs, 17, RR, 18);
   __syncthreads();
+  DCA_STAMP(cx, 0, wg, 1);
 
   // per-lane im2col offsets (k = ci*9 + kh*3 + kw)
   constexpr int NK = BF ? 8 : 7;
@@ -391,9 +508,12 @@ __global__ void __launch_bounds__(NT) k_stem_block0(Ctx cx) {
     }
   }
   __syncthreads();
+  DCA_STAMP(cx, 0, wg, 3);
   f32x4 acc[R / 2];
   conv_core<BF, R>(xs, ws, acc, wave, lane);
+  DCA_STAMP(cx, 0, wg, 4);
   fwd_epilogue<R>(acc, cx.Y + (size_t)n * 8192 + r0 * 512, cx.FPART + (size_t)wg * 32, red, s_tmp, wave, lane);
+  DCA_STAMP(cx, 0, wg, 5);
 }
 
 // ============================================================================================================
@@ -409,11 +529,13 @@ __global__ void __launch_bounds__(NT) k_fwd_block(Ctx cx, int i) {
   char* ws = smem;
   char* xs = ws + 288 * RB;
   float* red = (float*)(xs + RR * 18 * RB);
-  float* s_mean = red + 512;
+  float* s_mean = red + RED_F;
   float* s_var = s_mean + 32;
   float* s_scale = s_var + 32;
   float* s_shift = s_scale + 32;
+  DCA_STAMP(cx, i, wg, 0);
 
+  // ---- issue every global load ----
   const float* Yp = cx.Y + act_off(i - 1, cx.B) + (size_t)n * 8192;
   const float* Xp = cx.X + act_off(i - 1, cx.B) + (size_t)n * 8192;
   f32x4 yv[NF], xv[NF];
@@ -429,13 +551,21 @@ __global__ void __launch_bounds__(NT) k_fwd_block(Ctx cx, int i) {
       xv[m] = z4();
     }
   }
-  stage_weights<BF>(ws, cx.wt_f);
+  const float2* fpart = cx.FPART + (size_t)(i - 1) * cx.pstride * 32;
+  Parts P;
+  parts_load(P, fpart, nparts);
+  WStage<BF> W;
+  wstage_load<BF>(W, cx.wt_f);
+  const float gam = t < 32 ? cx.params[OFF_BNW + t] : 0.f, bet = t < 32 ? cx.params[OFF_BNB + t] : 0.f;
+  // ---- use ----
+  wstage_store<BF>(W, ws);
+  DCA_STAMP(cx, i, wg, 1);
   zero_recs<BF>(xs, 0, RR, 18);
   zero_recs<BF>(xs, 17, RR, 18);
-  reduce_fstats(cx.FPART + (size_t)(i - 1) * cx.pstride * 32, nparts, (float)(R * 16), red, s_mean, s_var);
+  fstats_finish(P, fpart, nparts, (float)(R * 16), red, s_mean, s_var);
+  DCA_STAMP(cx, i, wg, 2);
   if (t < 32) {
     const float mean = s_mean[t], var = s_var[t], invstd = rsqrtf(var + cx.bn_eps);
-    const float gam = cx.params[OFF_BNW + t], bet = cx.params[OFF_BNB + t];
     s_scale[t] = gam * invstd;
     s_shift[t] = bet - mean * gam * invstd;
     if (wg == 0) {
@@ -461,51 +591,61 @@ __global__ void __launch_bounds__(NT) k_fwd_block(Ctx cx, int i) {
     st4_rec<BF>(xs, tr * 18 + col + 1, col + 1, c4, xn);
   }
   __syncthreads();
+  DCA_STAMP(cx, i, wg, 3);
   f32x4 acc[R / 2];
   conv_core<BF, R>(xs, ws, acc, wave, lane);
+  DCA_STAMP(cx, i, wg, 4);
   fwd_epilogue<R>(acc, cx.Y + act_off(i, cx.B) + (size_t)n * 8192 + r0 * 512,
                   cx.FPART + ((size_t)i * cx.pstride + wg) * 32, red, s_mean, wave, lane);
+  DCA_STAMP(cx, i, wg, 5);
 }
 
 // ============================================================================================================
-// Head: BN(9)+ReLU+residual -> maxpool -> fc1+ReLU -> fc2 -> cross-entropy (fwd + bwd) -> back to g10,
-// plus the first BN-backward partial sums.  One workgroup per image.
+// Head, part 1 (one workgroup per trunk tile = R/2 pooled rows of one image):
+//   x10 = relu(BN9(y9)) + x9 -> 2x2 max-pool -> partial fc1 over this tile's 128R pooled features.
+// Each tile reads only its K-slice of W1 (16R KB), so W1 is streamed by B*TPI CUs instead of re-read by B.
 // ============================================================================================================
 template <int R>
-__global__ void __launch_bounds__(NT) k_head(Ctx cx) {
+__global__ void __launch_bounds__(NT) k_head1(Ctx cx) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  constexpr int TPI = 16 / R;
-  const int t = threadIdx.x, wave = t >> 6, lane = t & 63;
-  const int n = blockIdx.x, nparts = cx.B * TPI;
-  float* x10 = (float*)smem;        // [256][32]  (reused as dz)
-  float* dzx = x10 + 8192;          // [256][32]
-  float* P = dzx + 8192;            // [2048] NCHW-flatten order (c*64 + ph*8 + pw)
-  float* dpl = P + 2048;            // [2048]
-  uint8_t* code = (uint8_t*)(dpl + 2048);  // [64 pooled px][32]
-  float* red = (float*)(code + 2048);
-  float* s_mean = red + 512;
+  constexpr int TPI = 16 / R, NO = R / 2, F4 = 4 * R;  // F4: pooled features per channel in this tile
+  const int t = threadIdx.x;
+  const int wg = blockIdx.x, n = wg / TPI, r0 = (wg % TPI) * R;
+  const int nparts = cx.B * TPI;
+  float* x10 = (float*)smem;       // [16R px][32]
+  float* Ps = x10 + R * 512;       // [32 ch][4R]
+  float* red = Ps + 128 * R;
+  float* s_mean = red + RED_F;
   float* s_var = s_mean + 32;
   float* s_scale = s_var + 32;
   float* s_shift = s_scale + 32;
-  float* s_invstd = s_shift + 32;
-  float* hv = s_invstd + 32;   // fc1 pre-activation [32]
-  float* sdh = hv + 32;        // [32]
-  float* logit = sdh + 32;     // [16]
-  float* sdl = logit + 16;     // [16]
+  DCA_STAMP(cx, 10, wg, 0);
 
-  const float* Yp = cx.Y + act_off(9, cx.B) + (size_t)n * 8192;
-  const float* Xp = cx.X + act_off(9, cx.B) + (size_t)n * 8192;
-  f32x4 yv[8];
+  const size_t toff = act_off(9, cx.B) + (size_t)n * 8192 + r0 * 512;
+  f32x4 yv[NO], xv[NO];
 #pragma unroll
-  for (int m = 0; m < 8; ++m) yv[m] = ld4(Yp + 4 * (t + NT * m));
-  reduce_fstats(cx.FPART + (size_t)9 * cx.pstride * 32, nparts, (float)(R * 16), red, s_mean, s_var);
+  for (int m = 0; m < NO; ++m) {
+    yv[m] = ld4(cx.Y + toff + 4 * (t + NT * m));
+    xv[m] = ld4(cx.X + toff + 4 * (t + NT * m));
+  }
+  const float2* fpart = cx.FPART + (size_t)9 * cx.pstride * 32;
+  Parts P;
+  parts_load(P, fpart, nparts);
+  const int j = t >> 3, s8 = t & 7;
+  f32x4 w1v[4 * R];
+#pragma unroll
+  for (int cc = 0; cc < 4; ++cc)
+#pragma unroll
+    for (int r = 0; r < R; ++r)
+      w1v[cc * R + r] = ld4(cx.params + OFF_FC1W + j * 2048 + (4 * s8 + cc) * 64 + 4 * r0 + 4 * r);
+  const float gam = t < 32 ? cx.params[OFF_BNW + t] : 0.f, bet = t < 32 ? cx.params[OFF_BNB + t] : 0.f;
+
+  fstats_finish(P, fpart, nparts, (float)(R * 16), red, s_mean, s_var);
   if (t < 32) {
     const float mean = s_mean[t], var = s_var[t], invstd = rsqrtf(var + cx.bn_eps);
-    const float gam = cx.params[OFF_BNW + t], bet = cx.params[OFF_BNB + t];
     s_scale[t] = gam * invstd;
     s_shift[t] = bet - mean * gam * invstd;
-    s_invstd[t] = invstd;
-    if (n == 0) {
+    if (wg == 0) {
       cx.STATS[9 * 32 + t] = make_float2(mean, invstd);
       bn_running_update(cx, t, mean, var, false);
       if (t == 0) *cx.nbt += 1;
@@ -513,151 +653,268 @@ __global__ void __launch_bounds__(NT) k_head(Ctx cx) {
   }
   __syncthreads();
 #pragma unroll
-  for (int m = 0; m < 8; ++m) {
+  for (int m = 0; m < NO; ++m) {
     const int f = t + NT * m, c4 = f & 7;
-    const f32x4 xv = ld4(Xp + 4 * f);
     f32x4 o;
 #pragma unroll
-    for (int e = 0; e < 4; ++e) o[e] = fmaxf(yv[m][e] * s_scale[4 * c4 + e] + s_shift[4 * c4 + e], 0.f) + xv[e];
+    for (int e = 0; e < 4; ++e) o[e] = fmaxf(yv[m][e] * s_scale[4 * c4 + e] + s_shift[4 * c4 + e], 0.f) + xv[m][e];
     st4(x10 + 4 * f, o);
   }
   __syncthreads();
-  // 2x2 max-pool with first-max tie break (PyTorch scan order)
+  // 2x2 max-pool, first-max tie break (PyTorch scan order); NCHW-flatten index c*64 + ph*8 + pw
 #pragma unroll
-  for (int m = 0; m < 8; ++m) {
-    const int o = t + NT * m, ch = o & 31, pp = o >> 5, ph = pp >> 3, pw = pp & 7;
-    const int p00 = ((2 * ph) * 16 + 2 * pw) * 32 + ch;
+  for (int m = 0; m < NO; ++m) {
+    const int o = t + NT * m, ch = o & 31, pp = o >> 5, pr = pp >> 3, pw = pp & 7;
+    const int p00 = ((2 * pr) * 16 + 2 * pw) * 32 + ch;
     const float v00 = x10[p00], v01 = x10[p00 + 32], v10 = x10[p00 + 512], v11 = x10[p00 + 544];
     float best = v00;
     int id = 0;
     if (v01 > best) { best = v01; id = 1; }
     if (v10 > best) { best = v10; id = 2; }
     if (v11 > best) { best = v11; id = 3; }
-    P[ch * 64 + pp] = best;
-    code[pp * 32 + ch] = (uint8_t)id;
+    Ps[ch * F4 + pp] = best;
+    cx.HCODE[(size_t)n * 2048 + ((r0 / 2) * 8 + pp) * 32 + ch] = (uint8_t)id;
+    cx.HP[(size_t)n * 2048 + ch * 64 + (r0 / 2) * 8 + pp] = best;
   }
   __syncthreads();
-  // fc1: wave w computes outputs j = 8w .. 8w+7 (coalesced 1 KiB rows of W1)
-  const float* W1 = cx.params + OFF_FC1W;
-#pragma unroll 2
-  for (int jj = 0; jj < 8; ++jj) {
-    const int j = 8 * wave + jj;
-    float s = 0.f;
+  float acc = 0.f;
 #pragma unroll
-    for (int m = 0; m < 8; ++m) {
-      const f32x4 w4 = ld4(W1 + j * 2048 + 4 * lane + 256 * m);
-      const f32x4 p4 = ld4(P + 4 * lane + 256 * m);
-      s += w4.x * p4.x + w4.y * p4.y + w4.z * p4.z + w4.w * p4.w;
+  for (int cc = 0; cc < 4; ++cc)
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      const f32x4 p4 = ld4(Ps + (4 * s8 + cc) * F4 + 4 * r);
+      const f32x4 w4 = w1v[cc * R + r];
+      acc += w4.x * p4.x + w4.y * p4.y + w4.z * p4.z + w4.w * p4.w;
     }
+  acc += __shfl_xor(acc, 1);
+  acc += __shfl_xor(acc, 2);
+  acc += __shfl_xor(acc, 4);
+  if (s8 == 0) cx.HPART[(size_t)wg * 32 + j] = acc;
+  DCA_STAMP(cx, 10, wg, 5);
+}
+
+// ============================================================================================================
+// Head, part 2 (same tiling): fc1 finish + ReLU, fc2, cross-entropy fwd/bwd, dh, dp = W1_slice^T dh,
+// max-pool backward -> g10 (own rows), dz9 = g10*[z9>0] and the tile's BN-backward partial sums.
+// ============================================================================================================
+template <int R>
+__global__ void __launch_bounds__(NT) k_head2(Ctx cx) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  constexpr int TPI = 16 / R, NO = R / 2, F4 = 4 * R, U = R / 2;  // U: pooled features per thread
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int wg = blockIdx.x, n = wg / TPI, r0 = (wg % TPI) * R;
+  float* s_hp = (float*)smem;      // [TPI][32]
+  float* s_w2 = s_hp + 256;        // [10][32]
+  float* s_h = s_w2 + 320;         // [32]
+  float* s_dh = s_h + 32;          // [32]
+  float* s_lg = s_dh + 32;         // [16]
+  float* s_dl = s_lg + 16;         // [16]
+  uint8_t* s_code = (uint8_t*)(s_dl + 16);  // [4R pooled px][32]
+  float* s_dp = (float*)(s_code + 128 * R); // [32 ch][4R]
+  float* red = s_dp + 128 * R;
+  float* s_mean = red + RED_F;
+  float* s_inv = s_mean + 32;
+  float* s_scale = s_inv + 32;
+  float* s_shift = s_scale + 32;
+  DCA_STAMP(cx, 11, wg, 0);
+
+  // ---- issue every global load ----
+  const float hp = t < TPI * 32 ? cx.HPART[(size_t)n * TPI * 32 + t] : 0.f;
+  const f32x4 w2v = t < 80 ? ld4(cx.params + OFF_FC2W + 4 * t) : z4();
+  const float b1 = t < 32 ? cx.params[OFF_FC1B + t] : 0.f;
+  const float b2 = t < 10 ? cx.params[OFF_FC2B + t] : 0.f;
+  const int label = t == 0 ? cx.labels[sample_id(cx, n)] : 0;
+  const unsigned codew = t < 32 * R ? ((const unsigned*)(cx.HCODE + (size_t)n * 2048 + (r0 / 2) * 256))[t] : 0u;
+  const size_t toff = act_off(9, cx.B) + (size_t)n * 8192 + r0 * 512;
+  f32x4 yv[NO];
 #pragma unroll
-    for (int o = 32; o >= 1; o >>= 1) s += __shfl_xor(s, o);
-    if (lane == 0) hv[j] = s + cx.params[OFF_FC1B + j];
+  for (int m = 0; m < NO; ++m) yv[m] = ld4(cx.Y + toff + 4 * (t + NT * m));
+  const float2 st = t < 32 ? cx.STATS[9 * 32 + t] : make_float2(0.f, 0.f);
+  const float gam = t < 32 ? cx.params[OFF_BNW + t] : 0.f, bet = t < 32 ? cx.params[OFF_BNB + t] : 0.f;
+  const int u0 = t * U, cu = u0 / F4, vu = u0 % F4;
+  const float* w1p = cx.params + OFF_FC1W + cu * 64 + 4 * r0 + vu;
+  float w1v[32][U];
+#pragma unroll
+  for (int jj = 0; jj < 32; ++jj)
+#pragma unroll
+    for (int uu = 0; uu < U; ++uu) w1v[jj][uu] = w1p[jj * 2048 + uu];
+  // ---- use ----
+  s_hp[t] = hp;
+  if (t < 80) st4(s_w2 + 4 * t, w2v);
+  if (t < 32 * R) ((unsigned*)s_code)[t] = codew;
+  if (t < 32) {
+    s_mean[t] = st.x;
+    s_inv[t] = st.y;
+    s_scale[t] = gam * st.y;
+    s_shift[t] = bet - st.x * gam * st.y;
+  }
+  __syncthreads();
+  if (t < 32) {
+    float h = b1;
+#pragma unroll
+    for (int k = 0; k < TPI; ++k) h += s_hp[k * 32 + t];
+    s_h[t] = h;
   }
   __syncthreads();
   if (t < 10) {
-    float s = cx.params[OFF_FC2B + t];
-    for (int j = 0; j < 32; ++j) s += cx.params[OFF_FC2W + t * 32 + j] * fmaxf(hv[j], 0.f);
-    logit[t] = s;
+    float s = b2;
+#pragma unroll 8
+    for (int jj = 0; jj < 32; ++jj) s += s_w2[t * 32 + jj] * fmaxf(s_h[jj], 0.f);
+    s_lg[t] = s;
   }
   __syncthreads();
+  const bool lead = (wg % TPI) == 0;
   if (t == 0) {
-    const int label = cx.labels[sample_id(cx, n)];
-    float mx = logit[0];
-    for (int o = 1; o < 10; ++o) mx = fmaxf(mx, logit[o]);
+    float mx = s_lg[0];
+    for (int o = 1; o < 10; ++o) mx = fmaxf(mx, s_lg[o]);
     float se = 0.f;
-    for (int o = 0; o < 10; ++o) se += expf(logit[o] - mx);
+    for (int o = 0; o < 10; ++o) se += expf(s_lg[o] - mx);
     const float lse = mx + logf(se);
-    cx.HLOSS[n] = lse - logit[label];
+    if (lead) cx.HLOSS[n] = lse - s_lg[label];
     const float invB = 1.f / (float)cx.B;
-    for (int o = 0; o < 10; ++o) sdl[o] = (expf(logit[o] - lse) - (o == label ? 1.f : 0.f)) * invB;
+    for (int o = 0; o < 10; ++o) s_dl[o] = (expf(s_lg[o] - lse) - (o == label ? 1.f : 0.f)) * invB;
   }
   __syncthreads();
   if (t < 32) {
     float s = 0.f;
-    for (int o = 0; o < 10; ++o) s += cx.params[OFF_FC2W + o * 32 + t] * sdl[o];
-    const float dh = hv[t] > 0.f ? s : 0.f;
-    sdh[t] = dh;
-    cx.HDH[n * 32 + t] = dh;
-    cx.HH[n * 32 + t] = fmaxf(hv[t], 0.f);
-    if (t < 10) cx.HDL[n * 10 + t] = sdl[t];
+#pragma unroll
+    for (int o = 0; o < 10; ++o) s += s_w2[o * 32 + t] * s_dl[o];
+    const float h = s_h[t];
+    const float dh = h > 0.f ? s : 0.f;
+    s_dh[t] = dh;
+    if (lead) {
+      cx.HDH[n * 32 + t] = dh;
+      cx.HH[n * 32 + t] = fmaxf(h, 0.f);
+      if (t < 10) cx.HDL[n * 10 + t] = s_dl[t];
+    }
   }
-#pragma unroll
-  for (int m = 0; m < 2; ++m) st4(cx.HP + (size_t)n * 2048 + 4 * (t + NT * m), ld4(P + 4 * (t + NT * m)));
   __syncthreads();
-  // dp = W1^T dh  (coalesced over k)
 #pragma unroll
-  for (int m = 0; m < 8; ++m) {
-    const int k = t + NT * m;
+  for (int uu = 0; uu < U; ++uu) {
     float s = 0.f;
-#pragma unroll 8
-    for (int j = 0; j < 32; ++j) s += W1[j * 2048 + k] * sdh[j];
-    dpl[k] = s;
+#pragma unroll
+    for (int jj = 0; jj < 32; ++jj) s += w1v[jj][uu] * s_dh[jj];
+    s_dp[u0 + uu] = s;
   }
   __syncthreads();
-  // g10 = maxpool-backward(dp); dz9 = g10 * [z9 > 0]; per-tile sums of dz and dz*xhat
-  float* G0 = cx.G + (size_t)n * 8192;  // ping-pong slot 0 holds g10
-  float* dzl = x10;
+  float* G0 = cx.G + (size_t)n * 8192 + r0 * 512;  // ping-pong slot 0 holds g10
+  f32x4 sa = z4(), sb = z4();
 #pragma unroll
-  for (int m = 0; m < 8; ++m) {
-    const int f = t + NT * m, pix = f >> 3, c4 = f & 7, row = pix >> 4, col = pix & 15;
-    const int pp = (row >> 1) * 8 + (col >> 1), pos = (row & 1) * 2 + (col & 1);
-    f32x4 g, dz, dzxv;
+  for (int m = 0; m < NO; ++m) {
+    const int f = t + NT * m, p = f >> 3, c4 = f & 7, lr = p >> 4, col = p & 15;
+    const int pp = (lr >> 1) * 8 + (col >> 1), pos = (lr & 1) * 2 + (col & 1);
+    f32x4 g;
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
       const int ch = 4 * c4 + e;
-      g[e] = (code[pp * 32 + ch] == pos) ? dpl[ch * 64 + pp] : 0.f;
+      g[e] = (s_code[pp * 32 + ch] == pos) ? s_dp[ch * F4 + pp] : 0.f;
       const float y = yv[m][e];
       const float z = y * s_scale[ch] + s_shift[ch];
-      const float xh = (y - s_mean[ch]) * s_invstd[ch];
-      dz[e] = z > 0.f ? g[e] : 0.f;
-      dzxv[e] = dz[e] * xh;
+      const float dz = z > 0.f ? g[e] : 0.f;
+      sa[e] += dz;
+      sb[e] += dz * (y - s_mean[ch]) * s_inv[ch];
     }
     st4(G0 + 4 * f, g);
-    st4(dzl + 4 * f, dz);
-    st4(dzx + 4 * f, dzxv);
   }
-  __syncthreads();
-  {
-    const int ch = t & 31, k = t >> 5;
-    if (k < TPI) {
-      float sa = 0.f, sb = 0.f;
-      for (int p = k * R * 16; p < (k + 1) * R * 16; ++p) {
-        sa += dzl[p * 32 + ch];
-        sb += dzx[p * 32 + ch];
-      }
-      cx.BPART[(size_t)(n * TPI + k) * 32 + ch] = make_float2(sa, sb);
+  // reduce over the threads sharing channel group c4 = t & 7
+#pragma unroll
+  for (int o = 8; o <= 32; o <<= 1) {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      sa[e] += __shfl_xor(sa[e], o);
+      sb[e] += __shfl_xor(sb[e], o);
     }
   }
+  if (lane < 8) {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      red[wave * 32 + 4 * lane + e] = sa[e];
+      red[128 + wave * 32 + 4 * lane + e] = sb[e];
+    }
+  }
+  __syncthreads();
+  if (t < 32) {
+    float a = 0.f, b = 0.f;
+#pragma unroll
+    for (int w = 0; w < 4; ++w) {
+      a += red[w * 32 + t];
+      b += red[128 + w * 32 + t];
+    }
+    cx.BPART[(size_t)wg * 32 + t] = make_float2(a, b);
+  }
+  DCA_STAMP(cx, 11, wg, 5);
 }
 
 // ============================================================================================================
 // Backward workgroup roles
 // ============================================================================================================
-// fc1/fc2 weight gradients from the head's saved per-image vectors (sum over the batch, fixed order)
-__device__ void fc_grads_role(const Ctx& cx, int f) {
-  const int t = threadIdx.x, j = t >> 3, k = 64 * f + 8 * (t & 7);
-  f32x4 a0 = z4(), a1 = z4();
-  for (int b = 0; b < cx.B; ++b) {
-    const float dh = cx.HDH[b * 32 + j];
-    const f32x4 p0 = ld4(cx.HP + (size_t)b * 2048 + k), p1 = ld4(cx.HP + (size_t)b * 2048 + k + 4);
-    a0 += dh * p0;
-    a1 += dh * p1;
+// fc1/fc2 weight gradients from the head's saved per-image vectors (sum over the batch, fixed order).
+// Workgroup f owns fc1 columns 64f .. 64f+63; the batch vectors are staged in LDS with one load round trip.
+__device__ void fc_grads_role(const Ctx& cx, int f, char* smem) {
+  const int t = threadIdx.x, B = cx.B;
+  float* dh_s = (float*)smem;   // [B][32]
+  float* p_s = dh_s + 64 * 32;  // [B][64]
+  float* hh_s = p_s + 64 * 64;  // [B][32]
+  float* dl_s = hh_s + 64 * 32; // [B][16]
+  f32x4 dh4[2], p4[4], hh4[2];
+  float dlv[3];
+#pragma unroll
+  for (int m = 0; m < 2; ++m) {
+    const int idx = t + NT * m;
+    dh4[m] = idx < B * 8 ? ld4(cx.HDH + 4 * idx) : z4();
+    hh4[m] = (f == 0 && idx < B * 8) ? ld4(cx.HH + 4 * idx) : z4();
   }
-  st4(cx.grads + OFF_FC1W + j * 2048 + k, a0);
-  st4(cx.grads + OFF_FC1W + j * 2048 + k + 4, a1);
+#pragma unroll
+  for (int m = 0; m < 4; ++m) {
+    const int idx = t + NT * m, b = idx >> 4, k4 = idx & 15;
+    p4[m] = idx < B * 16 ? ld4(cx.HP + (size_t)b * 2048 + 64 * f + 4 * k4) : z4();
+  }
+#pragma unroll
+  for (int m = 0; m < 3; ++m) {
+    const int idx = t + NT * m;
+    dlv[m] = (f == 0 && idx < B * 10) ? cx.HDL[idx] : 0.f;
+  }
+#pragma unroll
+  for (int m = 0; m < 2; ++m) {
+    const int idx = t + NT * m;
+    if (idx < B * 8) {
+      st4(dh_s + 4 * idx, dh4[m]);
+      st4(hh_s + 4 * idx, hh4[m]);
+    }
+  }
+#pragma unroll
+  for (int m = 0; m < 4; ++m) {
+    const int idx = t + NT * m;
+    if (idx < B * 16) st4(p_s + 4 * idx, p4[m]);
+  }
+#pragma unroll
+  for (int m = 0; m < 3; ++m) {
+    const int idx = t + NT * m;
+    if (idx < B * 10) dl_s[(idx / 10) * 16 + idx % 10] = dlv[m];
+  }
+  __syncthreads();
+  const int j = t >> 3, kk = 8 * (t & 7);
+  f32x4 a0 = z4(), a1 = z4();
+  for (int b = 0; b < B; ++b) {
+    const float dh = dh_s[b * 32 + j];
+    a0 += dh * ld4(p_s + b * 64 + kk);
+    a1 += dh * ld4(p_s + b * 64 + kk + 4);
+  }
+  st4(cx.grads + OFF_FC1W + j * 2048 + 64 * f + kk, a0);
+  st4(cx.grads + OFF_FC1W + j * 2048 + 64 * f + kk + 4, a1);
   if (f == 0) {
     for (int idx = t; idx < 32 + 320 + 10; idx += NT) {
       float s = 0.f;
       if (idx < 32) {
-        for (int b = 0; b < cx.B; ++b) s += cx.HDH[b * 32 + idx];
+        for (int b = 0; b < B; ++b) s += dh_s[b * 32 + idx];
         cx.grads[OFF_FC1B + idx] = s;
       } else if (idx < 352) {
         const int o = (idx - 32) >> 5, jj = (idx - 32) & 31;
-        for (int b = 0; b < cx.B; ++b) s += cx.HDL[b * 10 + o] * cx.HH[b * 32 + jj];
+        for (int b = 0; b < B; ++b) s += dl_s[b * 16 + o] * hh_s[b * 32 + jj];
         cx.grads[OFF_FC2W + o * 32 + jj] = s;
       } else {
         const int o = idx - 352;
-        for (int b = 0; b < cx.B; ++b) s += cx.HDL[b * 10 + o];
+        for (int b = 0; b < B; ++b) s += dl_s[b * 16 + o];
         cx.grads[OFF_FC2B + o] = s;
       }
     }
@@ -669,34 +926,41 @@ template <bool BF, int RW>
 __device__ void wgrad_role(const Ctx& cx, int blk, int wv, char* smem) {
   constexpr int ESZ = Rec<BF>::ESZ, PADE = 16 / ESZ;
   constexpr int DS = RW * 16 + PADE, XS = (RW + 2) * 16 + PADE;
+  constexpr int ND = RW / 2, NX = (RW + 2) / 2;  // float4 loads per thread
   using TA = typename std::conditional<BF, unsigned short, float>::type;
   const int t = threadIdx.x, wave = t >> 6, lane = t & 63;
   const int n = wv / (16 / RW), r0 = (wv % (16 / RW)) * RW;
   TA* dyT = (TA*)smem;
   TA* xT = dyT + 32 * DS;
-  for (int idx = t; idx < 3 * 32 * XS * ESZ / 16; idx += NT) ((uint4*)xT)[idx] = uint4{0u, 0u, 0u, 0u};
   const float* dyp = cx.DY + act_off(blk, cx.B) + (size_t)n * 8192 + r0 * 512;
   const float* xp = cx.X + act_off(blk, cx.B) + (size_t)n * 8192;
-  __syncthreads();
-  for (int f = t; f < RW * 128; f += NT) {
-    const int pix = f >> 3, c4 = f & 7;
-    const f32x4 v = ld4(dyp + 4 * f);
+  f32x4 dv[ND], xv[NX];
 #pragma unroll
-    for (int e = 0; e < 4; ++e) dyT[(4 * c4 + e) * DS + pix] = BF ? (TA)bfbits(v[e]) : (TA)v[e];
+  for (int m = 0; m < ND; ++m) dv[m] = ld4(dyp + 4 * (t + NT * m));
+#pragma unroll
+  for (int m = 0; m < NX; ++m) {
+    const int f = t + NT * m, tr = f >> 7, row = r0 - 1 + tr;
+    xv[m] = (row >= 0 && row < 16) ? ld4(xp + (row * 16 + ((f >> 3) & 15)) * 32 + 4 * (f & 7)) : z4();
   }
-  for (int f = t; f < (RW + 2) * 128; f += NT) {
-    const int tr = f >> 7, col = (f >> 3) & 15, c4 = f & 7, row = r0 - 1 + tr;
+  for (int idx = t; idx < 3 * 32 * XS * ESZ / 16; idx += NT) ((uint4*)xT)[idx] = uint4{0u, 0u, 0u, 0u};
+  __syncthreads();
+#pragma unroll
+  for (int m = 0; m < ND; ++m) {
+    const int f = t + NT * m, pix = f >> 3, c4 = f & 7;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) dyT[(4 * c4 + e) * DS + pix] = BF ? (TA)bfbits(dv[m][e]) : (TA)dv[m][e];
+  }
+#pragma unroll
+  for (int m = 0; m < NX; ++m) {
+    const int f = t + NT * m, tr = f >> 7, col = (f >> 3) & 15, c4 = f & 7, row = r0 - 1 + tr;
     if (row < 0 || row >= 16) continue;
-    const f32x4 v = ld4(xp + (row * 16 + col) * 32 + 4 * c4);
 #pragma unroll
     for (int kw = 0; kw < 3; ++kw) {
       const int cc = col + 1 - kw;
       if (cc < 0 || cc >= 16) continue;
 #pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        TA* dst = xT + (kw * 32 + 4 * c4 + e) * XS + tr * 16 + cc;
-        *dst = BF ? (TA)bfbits(v[e]) : (TA)v[e];
-      }
+      for (int e = 0; e < 4; ++e)
+        xT[(kw * 32 + 4 * c4 + e) * XS + tr * 16 + cc] = BF ? (TA)bfbits(xv[m][e]) : (TA)xv[m][e];
     }
   }
   __syncthreads();
@@ -708,7 +972,7 @@ __device__ void wgrad_role(const Ctx& cx, int blk, int wv, char* smem) {
 // dgrad role: BN-backward of block i -> dgrad conv -> g_i; epilogue prepares block i-1 (or the stem, i == 0)
 template <bool BF, int R, int RW>
 __device__ void dgrad_role(const Ctx& cx, int i, int wg, char* smem) {
-  constexpr int RR = R + 2, TPI = 16 / R, NF = RR * 128 / NT, RB = Rec<BF>::BYTES;
+  constexpr int RR = R + 2, TPI = 16 / R, NF = RR * 128 / NT, RB = Rec<BF>::BYTES, NO = R / 2;
   constexpr int ESZ = Rec<BF>::ESZ, PADE = 16 / ESZ;
   constexpr int DS0 = R * 16 + PADE, XS0 = RR * 16 + PADE;          // block-0 in-tile wgrad
   constexpr int IRb = 2 * R + 2, IW = 34, DSP = 2 * R * 32 + PADE;   // stem backward
@@ -722,8 +986,8 @@ __device__ void dgrad_role(const Ctx& cx, int i, int wg, char* smem) {
   char* dys = ws + 288 * RB;
   float* gown = (float*)(dys + RR * 18 * RB);  // [R*16][32]
   float* yprev = gown + R * 512;               // [R*16][32]
-  float* red = yprev + R * 512;                // [512]
-  float* s_a = red + 512;
+  float* red = yprev + R * 512;                // [RED_F]
+  float* s_a = red + RED_F;
   float* s_b = s_a + 32;
   float* s_mean = s_b + 32;
   float* s_inv = s_mean + 32;
@@ -740,49 +1004,72 @@ __device__ void dgrad_role(const Ctx& cx, int i, int wg, char* smem) {
   float* xin = (float*)(xT + 3 * 32 * XS0);     // [3][IRb][IW]
   TA* dsT = (TA*)(xin + 3 * IRb * IW);          // [32][DSP]
 
+  // ---- issue every global load ----
   const size_t img = (size_t)n * 8192;
   const float* gin = cx.G + (size_t)rd * cx.B * 8192 + img;
   const float* yi = cx.Y + act_off(i, cx.B) + img;
-  f32x4 gv[NF], yv[NF];
+  const float* x0p = cx.X + img;  // block 0 input (in-tile wgrad, i == 0)
+  f32x4 gv[NF], yv[NF], xv[NF];
 #pragma unroll
   for (int m = 0; m < NF; ++m) {
     const int f = t + NT * m, tr = f >> 7, col = (f >> 3) & 15, c4 = f & 7, row = r0 - 1 + tr;
-    if (row >= 0 && row < 16) {
-      const int off = (row * 16 + col) * 32 + 4 * c4;
-      gv[m] = ld4(gin + off);
-      yv[m] = ld4(yi + off);
-    } else {
-      gv[m] = z4();
-      yv[m] = z4();
+    const bool ok = row >= 0 && row < 16;
+    const int off = (row * 16 + col) * 32 + 4 * c4;
+    gv[m] = ok ? ld4(gin + off) : z4();
+    yv[m] = ok ? ld4(yi + off) : z4();
+    xv[m] = (ok && i == 0) ? ld4(x0p + off) : z4();
+  }
+  f32x4 ypv[NO];
+  {
+    const float* yp = cx.Y + act_off(i > 0 ? i - 1 : 0, cx.B) + img + r0 * 512;
+#pragma unroll
+    for (int m = 0; m < NO; ++m) ypv[m] = i >= 1 ? ld4(yp + 4 * (t + NT * m)) : z4();
+  }
+  const float2* bpart = cx.BPART + (size_t)rd * cx.pstride * 32;
+  Parts P;
+  parts_load(P, bpart, nparts);
+  WStage<BF> W;
+  wstage_load<BF>(W, cx.wt_d);
+  float2 st = make_float2(0.f, 0.f), stp = make_float2(0.f, 0.f);
+  float gam = 0.f, bet = 0.f, pgw = 0.f, pgb = 0.f;
+  if (t < 32) {
+    st = cx.STATS[i * 32 + t];
+    if (i >= 1) stp = cx.STATS[(i - 1) * 32 + t];
+    gam = cx.params[OFF_BNW + t];
+    bet = cx.params[OFF_BNB + t];
+    if (wg == 0 && i != 9) {
+      pgw = cx.grads[OFF_BNW + t];
+      pgb = cx.grads[OFF_BNB + t];
     }
   }
-  if (i >= 1) {
-    const float* yp = cx.Y + act_off(i - 1, cx.B) + img + r0 * 512;
-    for (int f = t; f < R * 128; f += NT) st4(yprev + 4 * f, ld4(yp + 4 * f));
+  InRows<IRb> I;
+  if (i == 0) inrows_load<IRb>(I, cx.data + (size_t)sample_id(cx, n) * 3072, 2 * r0 - 1);
+  uint8_t codes[NO][4];
+  if (i == 0) {
+    const uint8_t* codep = cx.SCODE + img + r0 * 512;
+#pragma unroll
+    for (int j = 0; j < NO; ++j)
+#pragma unroll
+      for (int ii = 0; ii < 4; ++ii) {
+        const int tt = wave + 4 * j, rr = tt >> 1, ch = 16 * (tt & 1) + c;
+        codes[j][ii] = codep[(rr * 16 + 4 * q + ii) * 32 + ch];
+      }
   }
-  stage_weights<BF>(ws, cx.wt_d);
+  // ---- LDS fills ----
+  wstage_store<BF>(W, ws);
   zero_recs<BF>(dys, 0, RR, 18);
   zero_recs<BF>(dys, 17, RR, 18);
+#pragma unroll
+  for (int m = 0; m < NO; ++m) st4(yprev + 4 * (t + NT * m), ypv[m]);
   if (i == 0) {
     for (int idx = t; idx < 3 * 32 * XS0 * ESZ / 16; idx += NT) ((uint4*)xT)[idx] = uint4{0u, 0u, 0u, 0u};
     for (int idx = t; idx < 32 * DSP * ESZ / 16; idx += NT) ((uint4*)dsT)[idx] = uint4{0u, 0u, 0u, 0u};
-    // stem input rows 2r0-1 .. 2r0+2R (normalised, zero padded)
-    const uint8_t* src = cx.data + (size_t)sample_id(cx, n) * 3072;
-    const float nmean[3] = {0.4915f, 0.4823f, 0.4468f};
-    const float nstd[3] = {0.2470f, 0.2435f, 0.2616f};
-    for (int idx = t; idx < 3 * IRb * IW; idx += NT) {
-      const int ch = idx / (IRb * IW), rem = idx % (IRb * IW), ir = rem / IW, ic = rem % IW;
-      const int y = 2 * r0 - 1 + ir, x = ic - 1;
-      float v = 0.f;
-      if (y >= 0 && y < 32 && x >= 0 && x < 32)
-        v = ((float)src[ch * 1024 + y * 32 + x] / 255.f - nmean[ch]) / nstd[ch];
-      xin[idx] = v;
-    }
+    inrows_store<IRb>(I, xin, 2 * r0 - 1);
   }
-  reduce_bsums(cx.BPART + (size_t)rd * cx.pstride * 32, nparts, red, s_a, s_b);
+  DCA_STAMP(cx, 21 - i, wg, 1);
+  bsums_finish(P, bpart, nparts, red, s_a, s_b);
+  DCA_STAMP(cx, 21 - i, wg, 2);
   if (t < 32) {
-    const float2 st = cx.STATS[i * 32 + t];
-    const float gam = cx.params[OFF_BNW + t], bet = cx.params[OFF_BNB + t];
     const float N = (float)cx.B * 256.f;
     s_mean[t] = st.x;
     s_inv[t] = st.y;
@@ -791,23 +1078,17 @@ __device__ void dgrad_role(const Ctx& cx, int i, int wg, char* smem) {
     s_k1[t] = gam * st.y / N;
     s_gam[t] = gam;
     s_bet[t] = bet;
-    if (i >= 1) {
-      const float2 sp = cx.STATS[(i - 1) * 32 + t];
-      s_pm[t] = sp.x;
-      s_pi[t] = sp.y;
-    }
+    s_pm[t] = stp.x;
+    s_pi[t] = stp.y;
     if (wg == 0) {  // shared BN affine grads accumulate over the 10 applications
-      const float pw = (i == 9) ? 0.f : cx.grads[OFF_BNW + t];
-      const float pb = (i == 9) ? 0.f : cx.grads[OFF_BNB + t];
-      cx.grads[OFF_BNW + t] = pw + s_b[t];
-      cx.grads[OFF_BNB + t] = pb + s_a[t];
+      cx.grads[OFF_BNW + t] = pgw + s_b[t];
+      cx.grads[OFF_BNB + t] = pgb + s_a[t];
     }
   }
   __syncthreads();
   {
     const float N = (float)cx.B * 256.f;
     float* dyo = cx.DY + act_off(i, cx.B) + img;
-    const float* x0p = cx.X + img;  // block 0 input (for the in-tile wgrad, i == 0)
 #pragma unroll
     for (int m = 0; m < NF; ++m) {
       const int f = t + NT * m, tr = f >> 7, col = (f >> 3) & 15, c4 = f & 7, row = r0 - 1 + tr;
@@ -833,14 +1114,13 @@ __device__ void dgrad_role(const Ctx& cx, int i, int wg, char* smem) {
           }
         }
         if (i == 0) {
-          const f32x4 xv = ld4(x0p + (row * 16 + col) * 32 + 4 * c4);
 #pragma unroll
           for (int kw = 0; kw < 3; ++kw) {
             const int cc = col + 1 - kw;
             if (cc < 0 || cc >= 16) continue;
 #pragma unroll
             for (int e = 0; e < 4; ++e)
-              xT[(kw * 32 + 4 * c4 + e) * XS0 + tr * 16 + cc] = BF ? (TA)bfbits(xv[e]) : (TA)xv[e];
+              xT[(kw * 32 + 4 * c4 + e) * XS0 + tr * 16 + cc] = BF ? (TA)bfbits(xv[m][e]) : (TA)xv[m][e];
           }
         }
       }
@@ -848,8 +1128,10 @@ __device__ void dgrad_role(const Ctx& cx, int i, int wg, char* smem) {
     }
   }
   __syncthreads();
+  DCA_STAMP(cx, 21 - i, wg, 3);
   f32x4 acc[R / 2];
   conv_core<BF, R>(dys, ws, acc, wave, lane);
+  DCA_STAMP(cx, 21 - i, wg, 4);
 
   if (i >= 1) {
     float* gout = cx.G + (size_t)wr * cx.B * 8192 + img + r0 * 512;
@@ -893,7 +1175,6 @@ __device__ void dgrad_role(const Ctx& cx, int i, int wg, char* smem) {
   }
 
   // ---- i == 0: stem backward (maxpool-bwd routed by the saved argmax, ReLU mask) + stem & block-0 wgrads ----
-  const uint8_t* codep = cx.SCODE + img + r0 * 512;
 #pragma unroll
   for (int j = 0; j < R / 2; ++j) {
     const int tt = wave + 4 * j, rr = tt >> 1, ch = 16 * (tt & 1) + c;
@@ -902,7 +1183,7 @@ __device__ void dgrad_role(const Ctx& cx, int i, int wg, char* smem) {
     for (int ii = 0; ii < 4; ++ii) {
       const int col = 4 * q + ii, po = (rr * 16 + col) * 32 + ch;
       const float g = gown[po] + acc[j][ii];
-      const int code = codep[po];
+      const int code = codes[j][ii];
       if (code & 4) {
         const int pos = code & 3;
         const int sr = 2 * rr + (pos >> 1), sc = 2 * col + (pos & 1);
@@ -942,9 +1223,9 @@ __device__ void dgrad_role(const Ctx& cx, int i, int wg, char* smem) {
         for (int b2 = 0; b2 < 2; ++b2) {
           const f32x4 a = *(const f32x4*)(dsT + co * DSP + s * 32 + 16 * b2 + 4 * q);
 #pragma unroll
-          for (int st = 0; st < 4; ++st) {
-            const float bv = kv ? xb[s * IW + 16 * b2 + 4 * q + st] : 0.f;
-            acc2 = mfma4(a[st], bv, acc2);
+          for (int st2 = 0; st2 < 4; ++st2) {
+            const float bv = kv ? xb[s * IW + 16 * b2 + 4 * q + st2] : 0.f;
+            acc2 = mfma4(a[st2], bv, acc2);
           }
         }
       }
@@ -962,16 +1243,15 @@ __global__ void __launch_bounds__(NT) k_bwd_block(Ctx cx, int i) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int nparts = cx.B * (16 / R);
   int bid = blockIdx.x;
+  DCA_STAMP(cx, 21 - i, blockIdx.x, 0);
   if (bid < nparts) {
     dgrad_role<BF, R, RW>(cx, i, bid, smem);
-    return;
+  } else {
+    bid -= nparts;
+    if (i == 9) fc_grads_role(cx, bid, smem);
+    else wgrad_role<BF, RW>(cx, i + 1, bid, smem);
   }
-  bid -= nparts;
-  if (i == 9) {
-    fc_grads_role(cx, bid);
-    return;
-  }
-  wgrad_role<BF, RW>(cx, i + 1, bid, smem);
+  DCA_STAMP(cx, 21 - i, blockIdx.x, 5);
 }
 
 // ============================================================================================================
@@ -987,23 +1267,33 @@ template <bool BF>
 __global__ void __launch_bounds__(NT) k_reduce(Ctx cx, int nslab, int nsslab) {
   __shared__ f32x4 red[NT];
   const int t = threadIdx.x, bid = blockIdx.x;
+  DCA_STAMP(cx, 22, bid, 0);
   if (bid < N_TRUNK_RED_WG + N_STEM_RED_WG) {
     const bool stem = bid >= N_TRUNK_RED_WG;
     const int chunk = stem ? bid - N_TRUNK_RED_WG : bid;
-    const int slot = t & 15, grp = t >> 4, e0 = chunk * 64 + slot * 4;
+    const int slot = t & 7, grp = t >> 3, e0 = chunk * RED_CHUNK + slot * 4;
     const float* src = stem ? cx.SSLAB : cx.WSLAB;
     const int stride = stem ? SSLAB_N : WSLAB_N, cnt = stem ? nsslab : nslab;
     f32x4 s = z4();
-    for (int k = grp; k < cnt; k += 16) s += ld4(src + (size_t)k * stride + e0);
+    for (int k0 = grp; k0 < cnt; k0 += 32 * 8) {  // 8 slab loads in flight per thread
+      f32x4 v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int k = k0 + 32 * u;
+        v[u] = k < cnt ? ld4(src + (size_t)k * stride + e0) : z4();
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u) s += v[u];
+    }
     red[t] = s;
     __syncthreads();
-    if (t < 16) {
+    if (t < 8) {
       f32x4 tot = z4();
 #pragma unroll
-      for (int g = 0; g < 16; ++g) tot += red[g * 16 + t];
+      for (int g = 0; g < 32; ++g) tot += red[g * 8 + t];
 #pragma unroll
       for (int ii = 0; ii < 4; ++ii) {
-        const int e = chunk * 64 + t * 4 + ii;
+        const int e = chunk * RED_CHUNK + t * 4 + ii;
         int pidx = -1, kind = 0, d0 = 0, d1 = 0;
         if (!stem) {
           const int tt = e >> 8, ln = (e >> 2) & 63, mt = tt & 1, nt = tt >> 1, tap = nt >> 1, cih = nt & 1;
@@ -1051,13 +1341,20 @@ __global__ void __launch_bounds__(NT) k_reduce(Ctx cx, int nslab, int nsslab) {
     }
     return;
   }
-  // bookkeeping workgroup
-  if (t == 0) {
-    float s = 0.f;
-    for (int b = 0; b < cx.B; ++b) s += cx.HLOSS[b];
-    *cx.loss_acc += (double)(s / (float)cx.B);
-    *cx.cursor += cx.B;
-    *cx.step_count += 1;
+  // bookkeeping workgroup: batch-mean loss (fixed-order reduction), cursor, step counter, CC4 segment
+  {
+    float* rl = (float*)red;
+    float v = 0.f;
+    for (int b = t; b < cx.B; b += NT) v += cx.HLOSS[b];
+    rl[t] = v;
+    __syncthreads();
+    if (t == 0) {
+      float s = 0.f;
+      for (int k = 0; k < NT && k < cx.B; ++k) s += rl[k];
+      *cx.loss_acc += (double)(s / (float)cx.B);
+      *cx.cursor += cx.B;
+      *cx.step_count += 1;
+    }
   }
   if (!cx.fuse_sgd && t < 64) {  // CC4: rank 0's running stats ride the bucket-B all-reduce (others add 0)
     const float v = t < 32 ? cx.rm[t] : cx.rv[t - 32];
@@ -1090,23 +1387,5 @@ __global__ void __launch_bounds__(NT) k_apply_sgd(Ctx cx, int mode) {
   }
   if (!mode && gid < 32 * 5) put_w<BF>(cx.sw, (gid / 5) * 32 + 27 + gid % 5, 0.f);
 }
-
-// ------------------------------------------------------------------------------------------------------------
-// explicit instantiations used by engine.cpp
-// ------------------------------------------------------------------------------------------------------------
-#define DCA_INST(BF, R, RW)                                                   \
-  template __global__ void k_stem_block0<BF, R>(Ctx);                         \
-  template __global__ void k_fwd_block<BF, R>(Ctx, int);                      \
-  template __global__ void k_bwd_block<BF, R, RW>(Ctx, int);
-DCA_INST(false, 4, 8)
-DCA_INST(true, 4, 16)
-DCA_INST(false, 2, 8)
-DCA_INST(true, 2, 16)
-template __global__ void k_head<4>(Ctx);
-template __global__ void k_head<2>(Ctx);
-template __global__ void k_reduce<false>(Ctx, int, int);
-template __global__ void k_reduce<true>(Ctx, int, int);
-template __global__ void k_apply_sgd<false>(Ctx, int);
-template __global__ void k_apply_sgd<true>(Ctx, int);
 
 }  // namespace dca

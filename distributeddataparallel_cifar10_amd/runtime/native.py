@@ -43,11 +43,19 @@ def _declare(lib):
     lib.dca_engine_region.restype = c_void_p
     lib.dca_engine_workspace_bytes.argtypes = [c_void_p]
     lib.dca_engine_workspace_bytes.restype = ctypes.c_size_t
+    lib.dca_microbench.argtypes = [c_int, c_int, c_int, c_int, ctypes.POINTER(ctypes.c_float)]
+    lib.dca_microbench_xchg.argtypes = [c_int, c_int, c_int, c_int, c_int, ctypes.POINTER(ctypes.c_float),
+                                        ctypes.POINTER(c_int)]
     return lib
 
 
+def variant() -> str:
+    """Library variant selected by DCA_ENGINE_VARIANT ("" production, "stamps" diagnostic)."""
+    return os.environ.get("DCA_ENGINE_VARIANT", "")
+
+
 def library_path() -> str:
-    return _build.ENGINE_LIB
+    return _build.lib_path(variant())
 
 
 def load(build_if_missing: bool = True):
@@ -56,10 +64,10 @@ def load(build_if_missing: bool = True):
     with _lock:
         if _lib is not None:
             return _lib
-        path = _build.ENGINE_LIB
+        path = library_path()
         if build_if_missing:
             try:
-                path = _build.build()
+                path = _build.build(variant=variant())
             except Exception as exc:  # toolchain missing: only acceptable if the .so already exists
                 if not os.path.exists(path):
                     raise NativeUnavailable(f"cannot build native engine: {exc}") from exc
