@@ -39,6 +39,7 @@ def main() -> int:
     ap.add_argument("--batch", type=int, default=32, help="per-rank batch (reference main.py:61)")
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
     ap.add_argument("--rows", type=int, default=4)
+    ap.add_argument("--engine", default="auto", choices=["auto", "persistent", "multikernel"])
     a = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -61,8 +62,9 @@ def main() -> int:
     data, labels = synthetic_cifar(50000, seed=0)
     torch.manual_seed(1234 + rank)  # ranks init differently; the DDP wrap broadcasts rank 0's weights (CC3)
     model = NetResDeep().to(dev)
+    persistent = None if a.engine == "auto" else a.engine == "persistent"
     trainer = FusedDDPTrainer(model, data.to(dev), labels.to(dev), batch_max=a.batch, lr=1e-2, dtype=a.dtype,
-                              rows=a.rows, max_indices=(a.warmup + a.steps) * a.batch)
+                              rows=a.rows, max_indices=(a.warmup + a.steps) * a.batch, persistent=persistent)
     sampler = torch.utils.data.distributed.DistributedSampler(range(50000), num_replicas=world, rank=rank)
     order = np.resize(np.fromiter(iter(sampler), dtype=np.int32), (a.warmup + a.steps) * a.batch)
     trainer.engine.set_indices(order)
@@ -98,6 +100,7 @@ def main() -> int:
             "scaling": "weak",
             "vs_baseline": round(value / (REF_EAGER_IPS_PER_GPU * world), 3),
             "dtype": a.dtype,
+            "engine": "persistent" if trainer.engine.cfg.persistent else "multikernel",
             "data": "synthetic (CIFAR-10-shaped uint8 3x32x32, 50000 samples, random labels; random-init weights)",
             "config": {"model": "NetResDeep(n_chans1=32, n_blocks=10)", "global_batch": a.batch * world,
                        "per_rank_batch": a.batch, "seq_len": None, "image": "3x32x32",

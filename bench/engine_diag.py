@@ -36,7 +36,13 @@ def rel_l2(a: torch.Tensor, b: torch.Tensor) -> float:
     return (a - b).norm().item() / (den if den > 0 else 1.0)
 
 
-def compare_one_step(dtype: str, rows: int, B: int, graph: bool, seed: int = 0, verbose: bool = True) -> dict:
+def _cfg(dtype, rows, B, persistent):
+    return EngineConfig(batch_max=max(B, 32), lr=1e-2, dtype=dtype, rows=rows, persistent=persistent,
+                        debug=bool(persistent))
+
+
+def compare_one_step(dtype: str, rows: int, B: int, graph: bool, seed: int = 0, verbose: bool = True,
+                     persistent: bool = False) -> dict:
     torch.manual_seed(seed)
     dev = torch.device("cuda", 0)
     ndata = 2 * B + 8
@@ -46,8 +52,7 @@ def compare_one_step(dtype: str, rows: int, B: int, graph: bool, seed: int = 0, 
     model = NetResDeep()
     ref = copy.deepcopy(model)
     model = model.to(dev)
-    eng = NetResDeepEngine(model, data.to(dev), labels.to(dev),
-                           EngineConfig(batch_max=max(B, 32), lr=1e-2, dtype=dtype, rows=rows))
+    eng = NetResDeepEngine(model, data.to(dev), labels.to(dev), _cfg(dtype, rows, B, persistent))
     eng.set_indices(idx.numpy())
     eng.set_cursor(0)
     eng.read_loss(reset=True)
@@ -73,7 +78,7 @@ def compare_one_step(dtype: str, rows: int, B: int, graph: bool, seed: int = 0, 
         rep(f"x{i}", X[i], nchw_to_nhwc(r["x"][i]))
     for i in range(10):
         rep(f"y{i}", Y[i], nchw_to_nhwc(r["y"][i]))
-    for i in range(1, 10):
+    for i in range(0 if persistent else 1, 10):
         rep(f"dy{i}", DY[i], nchw_to_nhwc(r["dy"][i]))
     rep("g2", G[0], nchw_to_nhwc(r["dx"][2]))
     rep("g1", G[1], nchw_to_nhwc(r["dx"][1]))
@@ -98,7 +103,7 @@ def compare_one_step(dtype: str, rows: int, B: int, graph: bool, seed: int = 0, 
     return out
 
 
-def trajectory(dtype: str, rows: int, B: int, steps: int, seed: int = 1) -> dict:
+def trajectory(dtype: str, rows: int, B: int, steps: int, seed: int = 1, persistent: bool = False) -> dict:
     """Multi-step loss trajectory + final params vs the oracle (graph mode)."""
     torch.manual_seed(seed)
     dev = torch.device("cuda", 0)
@@ -108,8 +113,8 @@ def trajectory(dtype: str, rows: int, B: int, steps: int, seed: int = 1) -> dict
     model = NetResDeep()
     ref = copy.deepcopy(model)
     model = model.to(dev)
-    eng = NetResDeepEngine(model, data.to(dev), labels.to(dev),
-                           EngineConfig(batch_max=B, lr=1e-2, dtype=dtype, rows=rows))
+    eng = NetResDeepEngine(model, data.to(dev), labels.to(dev), EngineConfig(
+        batch_max=B, lr=1e-2, dtype=dtype, rows=rows, persistent=persistent))
     idx = torch.arange(ndata)
     eng.set_indices(idx.numpy())
     eng.set_cursor(0)
@@ -133,8 +138,30 @@ def main():
     ap.add_argument("--rows", default="4,2")
     ap.add_argument("--batches", default="32,16")
     ap.add_argument("--traj-steps", type=int, default=5)
+    ap.add_argument("--persistent", type=int, default=-1, help="1: persistent engine only, 0: multi-kernel only")
     a = ap.parse_args()
     summary = {}
+    if a.persistent != 0:
+        for B in [int(x) for x in a.batches.split(",")]:
+            for graph in (False, True):
+                key = f"bf16/persistent/B{B}/{'graph' if graph else 'eager'}"
+                print(f"== {key}", flush=True)
+                try:
+                    res = compare_one_step("bf16", 4, B, graph, persistent=True)
+                    summary[key] = max(res.values())
+                except Exception as exc:
+                    print(f"  FAILED: {exc!r}", flush=True)
+                    summary[key] = f"error: {exc}"
+        print("== trajectory bf16/persistent", flush=True)
+        try:
+            tr = trajectory("bf16", 4, 32, a.traj_steps, persistent=True)
+            print("  " + json.dumps(tr), flush=True)
+            summary["traj/bf16/persistent"] = tr["max_param_rel_err"]
+        except Exception as exc:
+            print(f"  FAILED: {exc!r}", flush=True)
+    if a.persistent == 1:
+        print(json.dumps({"summary": summary}), flush=True)
+        return
     for dtype in a.dtypes.split(","):
         for rows in [int(x) for x in a.rows.split(",")]:
             for B in [int(x) for x in a.batches.split(",")]:

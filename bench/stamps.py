@@ -39,8 +39,51 @@ def microbench(lib):
     return out
 
 
+PK_NAMES = (["start", "stem"] + [f"fwd{i}" for i in range(10)] + ["bn9+head_start", "head"] +
+            [f"bwd{i}" for i in range(9, -1, -1)] + ["stem_bwd", "fwd5_pre_xchg", "fwd5_post_xchg",
+                                                     "bwd5_pre_xchg", "bwd5_post_xchg"])
+
+
+def persistent_report(st):
+    """Per-phase durations of the persistent kernel (median over workgroups, shader cycles and us)."""
+    flat = st[24:28].transpose(1, 0, 2, 3).reshape(256, 32, 2)  # [wg][stamp][memtime|realtime]
+    valid = flat[:, 0, 1] != 0
+    f = flat[valid]
+    out = []
+    for s in range(1, 29):
+        prev = s - 1 if s not in (25, 27) else {25: 6, 27: 18}[s]
+        if s in (26, 28):
+            prev = s - 1
+        if s == 25:
+            prev = 6   # fwd4 end -> fwd5 pre-xchg
+        cyc = np.median(f[:, s, 0] - f[:, prev, 0])
+        us = np.median(f[:, s, 1] - f[:, prev, 1]) / 100.0
+        out.append({"phase": PK_NAMES[s], "cyc": int(cyc), "us": round(float(us), 2)})
+    tot = np.median(f[:, 24, 1] - f[:, 0, 1]) / 100.0
+    return out, round(float(tot), 2)
+
+
 def main():
     dtype = sys.argv[1] if len(sys.argv) > 1 else "bf16"
+    if len(sys.argv) > 2 and sys.argv[2] == "persistent":
+        dev = torch.device("cuda", 0)
+        data = torch.randint(0, 256, (4096, 3, 32, 32), dtype=torch.uint8, device=dev)
+        labels = torch.randint(0, 10, (4096,), device=dev)
+        model = NetResDeep().to(dev)
+        eng = NetResDeepEngine(model, data, labels, EngineConfig(batch_max=32, dtype="bf16", persistent=True))
+        eng.set_indices(np.arange(4096, dtype=np.int32))
+        eng.set_cursor(0)
+        eng.run(32, 50)
+        eng.sync()
+        eng.run(32, 1)
+        eng.sync()
+        raw = eng.region("STAMPS", 32 * 256 * 8 * 2, dtype=torch.int64).cpu().numpy().astype(np.int64)
+        phases, tot = persistent_report(raw.reshape(32, 256, 8, 2))
+        for p in phases:
+            print(json.dumps(p), flush=True)
+        print(json.dumps({"persistent_kernel_us": tot}), flush=True)
+        eng.close()
+        return
     dev = torch.device("cuda", 0)
     torch.manual_seed(0)
     data = torch.randint(0, 256, (4096, 3, 32, 32), dtype=torch.uint8, device=dev)

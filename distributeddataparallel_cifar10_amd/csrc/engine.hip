@@ -16,6 +16,7 @@
 #include <string>
 
 #include "netresdeep_kernels.hip"
+#include "netresdeep_persistent.hip"
 
 namespace {
 
@@ -61,6 +62,9 @@ struct DcaInit {
   int world_size;
   int rank;
   const char* nccl_id;  // 128 bytes (world_size > 1)
+  int persistent;       // 1: one-launch persistent trunk kernel (bf16 only)
+  int debug;            // persistent engine: also store DY / G for diagnostics
+  int pk_waves;         // persistent engine: waves per workgroup (8 or 4; 0 = default 8)
 };
 
 }  // extern "C"
@@ -80,6 +84,9 @@ struct Engine {
   int n_indices = 0;
   ncclComm_t comm = nullptr;
   std::map<int, hipGraphExec_t> graphs;
+  bool persistent = false;
+  int pk_waves = 8;
+  pk::PkArgs pa{};
   std::map<std::string, void*> regions;
   // dynamic LDS sizes
   size_t s_stem = 0, s_fwd = 0, s_head1 = 0, s_head2 = 0, s_dgrad = 0, s_dgrad0 = 0, s_wgrad = 0, s_fc = 0;
@@ -133,6 +140,8 @@ static int alloc_workspace(Engine* e) {
       {"WT_F", 9216 * esz},          {"WT_D", 9216 * esz},            {"SW", 1024 * esz},
       {"RS_BASE", 64 * 4},           {"CURSOR", 16},                  {"STEPS", 16},
       {"LOSS", 16},                  {"STAMPS", 32 * 256 * 8 * 2 * 8},
+      {"GRAN", 2 * 64 * 64 * 8},     {"EPOCH", 16},                   {"ERR", 16},
+      {"TSLAB", bmax * WSLAB_N * 4}, {"BNG", 64 * 4},
   };
   size_t total = 0;
   for (auto& r : regs) total += align_up(r.bytes, 256);
@@ -171,6 +180,12 @@ static int alloc_workspace(Engine* e) {
   c.loss_acc = (double*)e->regions["LOSS"];
   c.pstride = (int)pstride;
   c.stamps = (unsigned long long*)e->regions["STAMPS"];
+  e->pa.gran = (unsigned long long*)e->regions["GRAN"];
+  e->pa.epoch = (int*)e->regions["EPOCH"];
+  e->pa.err = (unsigned*)e->regions["ERR"];
+  e->pa.tslab = (float*)e->regions["TSLAB"];
+  e->pa.bng = (float*)e->regions["BNG"];
+  e->pa.debug = e->in.debug;
   return 0;
 }
 
@@ -181,11 +196,33 @@ static int set_lds_limits(Engine* e) {
   HIPCK(hipFuncSetAttribute((const void*)e->khead1, hipFuncAttributeMaxDynamicSharedMemorySize, (int)e->s_head1));
   HIPCK(hipFuncSetAttribute((const void*)e->khead2, hipFuncAttributeMaxDynamicSharedMemorySize, (int)e->s_head2));
   HIPCK(hipFuncSetAttribute((const void*)e->kbwd, hipFuncAttributeMaxDynamicSharedMemorySize, (int)dg));
+  HIPCK(hipFuncSetAttribute((const void*)pk::k_pk_step<8>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            pk::Plan::TOTAL));
+  HIPCK(hipFuncSetAttribute((const void*)pk::k_pk_step<4>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            pk::Plan::TOTAL));
+  return 0;
+}
+
+// Persistent path: one launch for the whole trunk, one for reduction + SGD.
+static int enqueue_step_persistent(Engine* e, int B) {
+  Ctx cx = e->base;
+  cx.B = B;
+  if (e->pk_waves == 4)
+    hipLaunchKernelGGL(pk::k_pk_step<4>, dim3(B), dim3(64 * 4), pk::Plan::TOTAL, e->st, cx, e->pa);
+  else
+    hipLaunchKernelGGL(pk::k_pk_step<8>, dim3(B), dim3(64 * 8), pk::Plan::TOTAL, e->st, cx, e->pa);
+  hipLaunchKernelGGL(pk::k_pk_reduce, dim3(pk::R_GRID), dim3(256), 0, e->st, cx, e->pa);
+  if (e->in.world_size > 1) {
+    NCCK(ncclAllReduce(cx.grads, cx.grads, FLAT_N, ncclFloat32, ncclSum, e->comm, e->st));
+    hipLaunchKernelGGL(e->kapply, dim3(64), dim3(NT), 0, e->st, cx, 1);
+  }
+  HIPCK(hipGetLastError());
   return 0;
 }
 
 // Enqueue one full training step for batch B on e->st (and e->cst for the collectives).
 static int enqueue_step(Engine* e, int B) {
+  if (e->persistent) return enqueue_step_persistent(e, B);
   Ctx cx = e->base;
   cx.B = B;
   const int nparts = B * e->TPI, nw = B * (16 / e->RW);
@@ -403,6 +440,13 @@ int dca_engine_create(const DcaInit* in, int n_indices, void** out) {
     return -1;
   }
   e->TPI = 16 / e->R;
+  e->persistent = in->persistent != 0;
+  e->pk_waves = in->pk_waves == 4 ? 4 : 8;
+  if (e->persistent && !e->bf) {
+    g_err = "the persistent engine is bf16-only (fp32 MFMA needs all CUs: use the multi-kernel engine)";
+    delete e;
+    return -1;
+  }
   if (e->bf && e->R == 4) dca::bind_kernels<true, 4, 16>(e);
   else if (e->bf) dca::bind_kernels<true, 2, 16>(e);
   else if (e->R == 4) dca::bind_kernels<false, 4, 8>(e);
@@ -487,6 +531,16 @@ int dca_engine_set_cursor(void* h, int v) {
   Engine* e = (Engine*)h;
   HIPCK(hipMemcpyAsync(e->base.cursor, &v, sizeof(int), hipMemcpyHostToDevice, e->st));
   HIPCK(hipStreamSynchronize(e->st));
+  return 0;
+}
+
+// Device-side error flags of the persistent engine (bit r: BN exchange round r timed out).  Synchronises;
+// reset clears them.
+int dca_engine_errors(void* h, unsigned* flags, int reset) {
+  Engine* e = (Engine*)h;
+  HIPCK(hipStreamSynchronize(e->st));
+  HIPCK(hipMemcpy(flags, e->pa.err, sizeof(unsigned), hipMemcpyDeviceToHost));
+  if (reset) HIPCK(hipMemset(e->pa.err, 0, sizeof(unsigned)));
   return 0;
 }
 

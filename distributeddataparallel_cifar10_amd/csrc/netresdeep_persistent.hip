@@ -1,0 +1,1001 @@
+// Persistent NetResDeep training step for CDNA4 (gfx950 / MI355X), bf16 MFMA, one workgroup per image.
+//
+// Why: the multi-kernel engine (netresdeep_kernels.hip) pays a dependent-kernel boundary (~1.5-1.9 us, measured)
+// plus a cold reload of activations / weights / BN partials written by other XCDs (~3-5 us, measured) at each of
+// its 23 seams.  Here ONE launch runs the whole trunk of a step:
+//   stem -> 10 forward blocks -> head (fc1/fc2/cross-entropy fwd+bwd) -> 10 backward blocks -> stem backward
+// Each workgroup (1024 threads = 16 waves, one wave per image row) owns one image: its activations stay in
+// registers in the MFMA C-fragment layout, the conv weights stay in LDS, and the only cross-workgroup traffic is
+// the batch-norm statistics (64 floats per image per block), exchanged in-kernel with an all-gather of tagged
+// 8-byte granules (data-as-flag: relaxed agent-scope stores, L1-bypassing sc1 buffer loads, parity
+// double-buffered, every spin bounded) -- ~1.4 us per exchange measured (profiles/xchg_calibration.log).
+// The trunk weight gradient is accumulated in registers across all 10 applications of the shared conv and
+// written once per image; k_pk_reduce then reduces slabs, computes fc grads, and applies SGD.
+//
+// Element ownership (C layout of v_mfma_f32_16x16x32_bf16): thread (wave w, lane l = 16q + c) owns
+//   pixel (row w, col 4q+i), channel 16h + c   for h in {0,1}, i in {0..3}   (8 values)
+//
+// Reference semantics: model/resnet.py:5-37 (shared ResBlock, skip after ReLU), main.py:27-39 (SGD, CE mean),
+// BatchNorm2d training statistics and 10 sequential running-stat updates per forward.
+
+namespace dca {
+namespace pk {
+
+constexpr int NTP = 1024;
+constexpr int NWV = 16;
+constexpr int KSW = 4;                    // granule loads per lane per sweep pass  (batch <= 64)
+constexpr unsigned SPIN_LIMIT = 1u << 18; // bounded spin: a missing peer sets an error flag, never hangs
+constexpr int ROUNDS = 20;                // exchanges per step (10 forward + 10 backward)
+
+struct PkArgs {
+  unsigned long long* gran;  // [2][64][64] granules
+  int* epoch;                // device scalar, advanced by k_pk_reduce after every step
+  unsigned* err;             // bit r: exchange round r timed out
+  float* tslab;              // [B][9216] trunk wgrad (fragment order)
+  float* bng;                // [64] dgamma | dbeta  (written by workgroup 0)
+  int debug;                 // also store DY / G for the numerical diagnostics
+};
+
+constexpr int cmax(int a, int b) { return a > b ? a : b; }
+
+// diagnostic stamps (DCA_STAMPS builds): global stamp index s -> slot 24 + s/8, entry s%8
+#define PK_STAMP(cx, s) DCA_STAMP(cx, 24 + (s) / 8, blockIdx.x, (s) % 8)
+
+struct Plan {
+  static constexpr int RB = 80;                        // bf16 record = 32 channels (64 B) + 16 B pad
+  static constexpr int O_CRED = 0;                     // [2][16][64] f32 combine scratch
+  static constexpr int O_STAT = 8192;                  // [10][64] f32: mean[32] | invstd[32]
+  static constexpr int O_MISC = O_STAT + 2560;         // [1024] f32 (layout: see k_pk_step)
+  static constexpr int O_U = O_MISC + 4096;            // phase union
+  // forward
+  static constexpr int U_WT = 0;                       // 288 weight records
+  static constexpr int U_XR = 288 * RB;                // 18 x 18 conv-input records (zero halo)
+  static constexpr int U_XR_END = U_XR + 324 * RB;
+  // stem (start of the step)
+  static constexpr int U_XIN = U_XR_END;               // [3][34][34] f32 normalised input
+  static constexpr int U_SW = U_XIN + 13872;           // [32][32] bf16 stem weight
+  static constexpr int U_SB = U_SW + 2048;             // [32] f32 stem bias
+  static constexpr int U_X0 = U_SB + 128;              // [256][32] f32 pooled stem output
+  static constexpr int STEM_END = U_X0 + 32768;
+  // head
+  static constexpr int U_X10 = 0;                      // [256][32] f32
+  static constexpr int U_P = 32768;                    // [2048] f32  (NCHW flatten c*64 + ph*8 + pw)
+  static constexpr int U_CODE = U_P + 8192;            // [64][32] u8 pool argmax
+  static constexpr int U_DP = U_CODE + 2048;           // [2048] f32
+  static constexpr int U_HP = U_DP + 8192;             // [16][32] f32 per-wave fc1 partials
+  static constexpr int U_HV = U_HP + 2048;             // h[32] dh[32] logits[16] dl[16]
+  static constexpr int U_DPP = U_HV + 384;             // [8 waves max][2048] f32 per-wave dp partials
+  static constexpr int HEAD_END = U_DPP + 8 * 2048 * 4;
+  // backward
+  static constexpr int DYT_S = 256 + 8;
+  static constexpr int U_DYT = U_XR_END;               // [32][DYT_S] bf16  dy, pixel-contiguous
+  static constexpr int XT_S = 18 * 16 + 8;
+  static constexpr int U_XT = U_DYT + 32 * DYT_S * 2;  // [3 kw][32][XT_S] bf16 shifted x copies
+  static constexpr int BWD_END = U_XT + 3 * 32 * XT_S * 2;
+  // stem backward
+  static constexpr int DSP = 1024 + 8;
+  static constexpr int U_DST = 0;                      // [32][DSP] bf16 d(stem conv output), pixel-contiguous
+  static constexpr int U_XIN2 = 32 * DSP * 2;          // [3][34][34] f32
+  static constexpr int U_SRED = U_XIN2 + 13872;        // [16 waves][64 lanes][4] f32 stem-wgrad partials
+  static constexpr int SBWD_END = U_SRED + 16384;
+  static constexpr int UNION = cmax(cmax(STEM_END, HEAD_END), cmax(BWD_END, SBWD_END));
+  static constexpr int TOTAL = O_U + UNION;
+};
+static_assert(Plan::TOTAL <= 160 * 1024, "LDS budget");
+static_assert(Plan::U_XIN % 16 == 0 && Plan::U_SW % 16 == 0 && Plan::U_X0 % 16 == 0 && Plan::U_XT % 16 == 0 &&
+                  Plan::U_XIN2 % 16 == 0 && Plan::O_U % 16 == 0 && Plan::U_SRED % 16 == 0,
+              "16-byte aligned carve");
+
+// Workgroup barrier for LDS-only hand-offs.  __syncthreads() also waits for every outstanding global load and
+// store of the wave (vmcnt(0)); here waves share data only through LDS, so global prefetches and write-backs
+// stay in flight across the barrier.  Cross-thread hand-offs through GLOBAL memory use __syncthreads().
+__device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
+// Workgroup geometry: NW waves, each owning RPW consecutive image rows.
+template <int NW>
+struct Geo {
+  static constexpr int NT = 64 * NW;              // threads per workgroup
+  static constexpr int RPW = 16 / NW;             // image rows per wave
+  static constexpr int KSW = (64 + NW - 1) / NW;  // granule loads per lane per sweep pass (batch <= 64)
+  static constexpr int WTL = (36 + NW - 1) / NW;  // wgrad output tiles per wave
+  static constexpr int KPT = 2048 / NT;           // fc1 input features per thread
+  static constexpr int SBC = 16 / NW;             // stem-wgrad (tile, row-quarter) combos per wave
+};
+
+// offset of the C-layout element (row, h, i) of lane (q, c) inside an NHWC [16][16][32] image
+__device__ __forceinline__ int el(int row, int q, int c, int h, int i) {
+  return ((row * 16 + 4 * q + i) << 5) + 16 * h + c;
+}
+
+// per-image channel sums of two per-thread C-layout partials (a0: channel c, a1: channel 16+c; same for b);
+// results oa[32], ob[32] in LDS, valid after the call.  Two LDS barriers.
+template <int NW>
+__device__ __forceinline__ void img_csum2(float a0, float a1, float b0, float b1, float* cred, float* oa, float* ob) {
+  const int t = threadIdx.x, w = t >> 6, lane = t & 63, c = lane & 15;
+  a0 += __shfl_xor(a0, 16);
+  a0 += __shfl_xor(a0, 32);
+  a1 += __shfl_xor(a1, 16);
+  a1 += __shfl_xor(a1, 32);
+  b0 += __shfl_xor(b0, 16);
+  b0 += __shfl_xor(b0, 32);
+  b1 += __shfl_xor(b1, 16);
+  b1 += __shfl_xor(b1, 32);
+  if (lane < 16) {
+    cred[w * 32 + c] = a0;
+    cred[w * 32 + 16 + c] = a1;
+    cred[512 + w * 32 + c] = b0;
+    cred[512 + w * 32 + 16 + c] = b1;
+  }
+  lds_barrier();
+  if (t < 64) {
+    const int ch = t & 31, off = t < 32 ? 0 : 512;
+    float s = 0.f;
+#pragma unroll
+    for (int k = 0; k < NW; ++k) s += cred[off + k * 32 + ch];
+    (t < 32 ? oa : ob)[ch] = s;
+  }
+  lds_barrier();
+}
+
+// In-kernel all-gather: every workgroup contributes misc[0..64); on return misc[64..128) holds the sum over
+// workgroups of each value and misc[128..192) the sum of squares.  Ends with a barrier.
+template <int NW>
+__device__ void xchg(const PkArgs& pa, int epoch, int round, float* cred, float* misc) {
+  constexpr int KSW = Geo<NW>::KSW;
+  const int t = threadIdx.x, lane = t & 63, n = blockIdx.x, G = gridDim.x;
+  const int w = __builtin_amdgcn_readfirstlane(t >> 6);  // wave-uniform -> scalar branches in the sweep
+  const unsigned tag = (unsigned)(epoch * 64 + round + 1);
+  unsigned long long* buf = pa.gran + (size_t)(round & 1) * 64 * 64;
+  if (t < 64)
+    __hip_atomic_store(buf + n * 64 + t, ((unsigned long long)tag << 32) | __float_as_uint(misc[t]),
+                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(buf, (short)0, 64 * 64 * 8, 0x00020000);
+  float s1 = 0.f, s2 = 0.f;
+  for (unsigned spins = 0;; ++spins) {
+    unsigned lo[KSW], hi[KSW];
+#pragma unroll
+    for (int kk = 0; kk < KSW; ++kk) {
+      const int k = w + NW * kk;
+      if (k < G) {
+        const auto x = __builtin_amdgcn_raw_buffer_load_b64(rs, (k * 64 + lane) * 8, 0, 16);  // sc1
+        lo[kk] = x[0];
+        hi[kk] = x[1];
+      } else {
+        lo[kk] = 0u;
+        hi[kk] = tag;
+      }
+    }
+    bool ok = true;
+    s1 = 0.f;
+    s2 = 0.f;
+#pragma unroll
+    for (int kk = 0; kk < KSW; ++kk) {
+      ok &= hi[kk] == tag;
+      const float v = __uint_as_float(lo[kk]);
+      s1 += v;
+      s2 += v * v;
+    }
+    if (__all(ok)) break;
+    if (spins >= SPIN_LIMIT) {
+      if (lane == 0) atomicOr(pa.err, 1u << (round & 31));
+      break;
+    }
+  }
+  cred[w * 64 + lane] = s1;
+  cred[1024 + w * 64 + lane] = s2;
+  lds_barrier();
+  if (t < 64) {
+    float a = 0.f, b = 0.f;
+#pragma unroll
+    for (int k = 0; k < NW; ++k) {
+      a += cred[k * 64 + t];
+      b += cred[1024 + k * 64 + t];
+    }
+    misc[64 + t] = a;
+    misc[128 + t] = b;
+  }
+  lds_barrier();
+}
+
+// Records are 80 bytes (32 bf16 channels + 16 B pad, which also staggers the banks of neighbouring
+// records), so every tap is the per-lane base address plus a compile-time immediate offset.
+__device__ __forceinline__ void st1r(char* xr, int rec, int ch, float v) {
+  *(unsigned short*)(xr + rec * Plan::RB + ch * 2) = bfbits(v);
+}
+// whole-image 3x3 conv on MFMA: rows r0 .. r0+RPW-1, both channel halves.  xr: 18x18 records, wt: 288 records.
+template <int RPW>
+__device__ __forceinline__ void conv_img(const char* xr, const char* wt, f32x4 (&acc)[RPW][2], int r0, int lane) {
+  const int c = lane & 15, q = lane >> 4;
+  const char* abase = xr + (r0 * 18 + c) * Plan::RB + q * 16;
+  const char* bbase = wt + c * Plan::RB + q * 16;
+#pragma unroll
+  for (int rr = 0; rr < RPW; ++rr) {
+    acc[rr][0] = z4();
+    acc[rr][1] = z4();
+  }
+#pragma unroll
+  for (int tap = 0; tap < 9; ++tap) {
+    const int kh = tap / 3, kw = tap % 3;
+    const bf16x8 b0 = *(const bf16x8*)(bbase + (tap * 32) * Plan::RB);
+    const bf16x8 b1 = *(const bf16x8*)(bbase + (tap * 32 + 16) * Plan::RB);
+#pragma unroll
+    for (int rr = 0; rr < RPW; ++rr) {
+      const bf16x8 a = *(const bf16x8*)(abase + ((rr + kh) * 18 + kw) * Plan::RB);
+      acc[rr][0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b0, acc[rr][0], 0, 0, 0);
+      acc[rr][1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b1, acc[rr][1], 0, 0, 0);
+    }
+  }
+}
+
+// forward BN statistics of y (C layout) for block `blk`: exchange, finalise, scale/shift -> misc[192..256),
+// (mean, invstd) -> stat[blk]; workgroup 0 updates the running stats.  Ends with a barrier.
+template <int NW>
+__device__ void bn_fwd_stats(const Ctx& cx, const PkArgs& pa, int epoch, int blk,
+                             const float (&y)[Geo<NW>::RPW][2][4], float* cred, float* misc, float* stat) {
+  constexpr int RPW = Geo<NW>::RPW;
+  const int t = threadIdx.x, lane = t & 63, c = lane & 15;
+  float a0 = 0.f, a1 = 0.f;
+#pragma unroll
+  for (int rr = 0; rr < RPW; ++rr)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      a0 += y[rr][0][i];
+      a1 += y[rr][1][i];
+    }
+  img_csum2<NW>(a0, a1, 0.f, 0.f, cred, misc + 256, misc + 288);  // image sums -> misc[256..288)
+  const float m0 = misc[256 + c] * (1.f / 256.f), m1 = misc[256 + 16 + c] * (1.f / 256.f);
+  float d0 = 0.f, d1 = 0.f;
+#pragma unroll
+  for (int rr = 0; rr < RPW; ++rr)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      d0 += (y[rr][0][i] - m0) * (y[rr][0][i] - m0);
+      d1 += (y[rr][1][i] - m1) * (y[rr][1][i] - m1);
+    }
+  if (t < 32) misc[t] = misc[256 + t] * (1.f / 256.f);           // image mean -> misc[0..32)
+  img_csum2<NW>(d0, d1, 0.f, 0.f, cred, misc + 32, misc + 288);  // image M2 -> misc[32..64)
+  if (blk == 5) PK_STAMP(cx, 25);
+  xchg<NW>(pa, epoch, blk, cred, misc);
+  if (blk == 5) PK_STAMP(cx, 26);
+  if (t < 32) {
+    const float G = (float)gridDim.x;
+    const float s1 = misc[64 + t], s2 = misc[128 + t], qm = misc[96 + t];
+    const float mean = s1 / G;
+    const float m2 = fmaxf(qm + 256.f * (s2 - s1 * mean), 0.f);
+    const float var = m2 / (G * 256.f);
+    const float invstd = rsqrtf(var + cx.bn_eps);
+    const float gam = misc[320 + t], bet = misc[352 + t];
+    misc[192 + t] = gam * invstd;
+    misc[224 + t] = bet - mean * gam * invstd;
+    stat[blk * 64 + t] = mean;
+    stat[blk * 64 + 32 + t] = invstd;
+    if (blockIdx.x == 0) {  // running stats live in LDS (misc[448..512)) for the whole forward
+      cx.STATS[blk * 32 + t] = make_float2(mean, invstd);
+      const float ntot = G * 256.f, unb = var * ntot / (ntot - 1.f), mo = cx.bn_mom;
+      misc[448 + t] = misc[448 + t] * (1.f - mo) + mean * mo;
+      misc[480 + t] = misc[480 + t] * (1.f - mo) + unb * mo;
+    }
+  }
+  lds_barrier();
+}
+
+template <int NW>
+__device__ __forceinline__ void zero_xr_halo(char* xr) {
+  // rows 0 and 17 (18 records each) + columns 0 and 17 of rows 1..16 -> 68 records x 4 chunks
+  for (int idx = threadIdx.x; idx < 68 * 4; idx += 64 * NW) {
+    const int r = idx >> 2, ch = idx & 3;
+    const int rec = r < 18 ? r : (r < 36 ? 17 * 18 + (r - 18) : ((r - 36) / 2 + 1) * 18 + ((r - 36) & 1) * 17);
+    *(uint4*)(xr + rec * Plan::RB + ch * 16) = uint4{0u, 0u, 0u, 0u};
+  }
+}
+template <int NW>
+__device__ __forceinline__ void stage_wt(char* wt, const void* src) {
+  constexpr int M = (1152 + 64 * NW - 1) / (64 * NW);
+  const uint4* s = (const uint4*)src;
+  uint4 v[M];
+#pragma unroll
+  for (int m = 0; m < M; ++m) {
+    const int idx = threadIdx.x + 64 * NW * m;
+    if (idx < 1152) v[m] = s[idx];
+  }
+#pragma unroll
+  for (int m = 0; m < M; ++m) {
+    const int idx = threadIdx.x + 64 * NW * m;
+    if (idx < 1152) *(uint4*)(wt + (idx >> 2) * Plan::RB + (idx & 3) * 16) = v[m];
+  }
+}
+// normalised input image [3][34][34] f32 (zero border) from the uint8 CHW image
+template <int NW>
+__device__ __forceinline__ void stage_input(float* xin, const uint8_t* img) {
+  constexpr int NTH = 64 * NW, M = (768 + NTH - 1) / NTH;
+  const int t = threadIdx.x;
+  unsigned wd[M];
+#pragma unroll
+  for (int m = 0; m < M; ++m) {
+    const int idx = t + NTH * m;
+    wd[m] = idx < 768 ? ((const unsigned*)img)[idx] : 0u;
+  }
+  for (int idx = t; idx < 3 * 34 * 34; idx += NTH) {
+    const int rem = idx % (34 * 34), r = rem / 34, cc = rem % 34;
+    if (r == 0 || r == 33 || cc == 0 || cc == 33) xin[idx] = 0.f;
+  }
+#pragma unroll
+  for (int m = 0; m < M; ++m) {
+    const int idx = t + NTH * m;
+    if (idx < 768) {
+      const int ch = idx >> 8, y = (idx >> 3) & 31, x0 = 4 * (idx & 7);
+      float* dst = xin + ch * 34 * 34 + (y + 1) * 34 + 1 + x0;
+#pragma unroll
+      for (int b = 0; b < 4; ++b) dst[b] = norm_px((wd[m] >> (8 * b)) & 255u, ch);
+    }
+  }
+}
+
+// ============================================================================================================
+template <int NW>
+__global__ void __launch_bounds__(64 * NW) k_pk_step(Ctx cx, PkArgs pa) {
+  static_assert(NW == 4 || NW == 8, "4 or 8 waves per workgroup (LDS dp scratch is sized for 8)");
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  using P = Plan;
+  using Gm = Geo<NW>;
+  constexpr int RPW = Gm::RPW, NTH = Gm::NT;
+  const int t = threadIdx.x, w = t >> 6, lane = t & 63, c = lane & 15, q = lane >> 4;
+  const int r0 = w * RPW;  // first image row owned by this wave
+  const int n = blockIdx.x;
+  float* cred = (float*)(smem + P::O_CRED);
+  float* stat = (float*)(smem + P::O_STAT);
+  float* misc = (float*)(smem + P::O_MISC);  // [0,64) publish | [64,192) sums | [192,256) scale/shift | ...
+  char* U = smem + P::O_U;
+  char* WT = U + P::U_WT;
+  char* XR = U + P::U_XR;
+  const int epoch = *pa.epoch;
+  const size_t img = (size_t)n * 8192;
+  const int B = cx.B;
+  PK_STAMP(cx, 0);
+
+  // ======================= stem: gather + normalise + conv1 + bias + ReLU + 2x2 max-pool =================
+  {
+    float* xin = (float*)(U + P::U_XIN);
+    unsigned short* swl = (unsigned short*)(U + P::U_SW);
+    float* sb = (float*)(U + P::U_SB);
+    float* x0i = (float*)(U + P::U_X0);
+    stage_input<NW>(xin, cx.data + (size_t)sample_id(cx, n) * 3072);
+    if (t < 128) ((uint4*)swl)[t] = ((const uint4*)cx.sw)[t];
+    if (t < 32) {
+      sb[t] = cx.params[OFF_C1B + t];
+      misc[320 + t] = cx.params[OFF_BNW + t];  // BN gamma / beta, constant for the step
+      misc[352 + t] = cx.params[OFF_BNB + t];
+      misc[512 + t] = cx.params[OFF_FC1B + t];  // fc constants for the head
+      if (n == 0) {  // running stats (rank 0's base under DDP, reference CC4 semantics)
+        misc[448 + t] = cx.ws > 1 ? cx.rs_base[t] : cx.rm[t];
+        misc[480 + t] = cx.ws > 1 ? cx.rs_base[32 + t] : cx.rv[t];
+      }
+    }
+    for (int idx = t; idx < 330; idx += NTH) misc[544 + idx] = cx.params[OFF_FC2W + idx];  // W2 [10][32] + b2
+    stage_wt<NW>(WT, cx.wt_f);
+    zero_xr_halo<NW>(XR);
+    lds_barrier();
+    int koff[8];
+    bool kval[8];
+#pragma unroll
+    for (int s = 0; s < 8; ++s) {
+      const int k = 8 * q + s;
+      kval[s] = k < 27;
+      koff[s] = kval[s] ? (k / 9) * 34 * 34 + ((k % 9) / 3) * 34 + (k % 3) : 0;
+    }
+    uint8_t* code_out = cx.SCODE + img;
+    float* X0 = cx.X + img;
+#pragma unroll 1
+    for (int j = 0; j < 64 / NW; ++j) {
+      const int u = w + NW * j, pr = u >> 2, chalf = (u >> 1) & 1, h = u & 1, co = 16 * h + c;
+      const int base0 = (2 * pr) * 34 + 16 * chalf + c;
+      const bf16x8 b = *(const bf16x8*)(swl + co * 32 + 8 * q);
+      bf16x8 v0, v1;
+#pragma unroll
+      for (int s = 0; s < 8; ++s) {
+        v0[s] = (__bf16)(kval[s] ? xin[koff[s] + base0] : 0.f);
+        v1[s] = (__bf16)(kval[s] ? xin[koff[s] + base0 + 34] : 0.f);
+      }
+      const f32x4 a0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(v0, b, z4(), 0, 0, 0);
+      const f32x4 a1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(v1, b, z4(), 0, 0, 0);
+      const float bias = sb[co];
+#pragma unroll
+      for (int pp = 0; pp < 2; ++pp) {
+        const float v00 = fmaxf(a0[2 * pp] + bias, 0.f), v01 = fmaxf(a0[2 * pp + 1] + bias, 0.f);
+        const float v10 = fmaxf(a1[2 * pp] + bias, 0.f), v11 = fmaxf(a1[2 * pp + 1] + bias, 0.f);
+        float best = v00;
+        int code = 0;
+        if (v01 > best) { best = v01; code = 1; }
+        if (v10 > best) { best = v10; code = 2; }
+        if (v11 > best) { best = v11; code = 3; }
+        if (best > 0.f) code |= 4;
+        const int pc = 8 * chalf + 2 * q + pp, po = (pr * 16 + pc) * 32 + co;
+        x0i[po] = best;
+        X0[po] = best;
+        code_out[po] = (uint8_t)code;
+        st1r(XR, (pr + 1) * 18 + pc + 1, co, best);
+      }
+    }
+    lds_barrier();
+  }
+  PK_STAMP(cx, 1);
+  float x[RPW][2][4], y[RPW][2][4];
+  {
+    const float* x0i = (const float*)(U + P::U_X0);
+#pragma unroll
+    for (int rr = 0; rr < RPW; ++rr)
+#pragma unroll
+      for (int h = 0; h < 2; ++h)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) x[rr][h][i] = x0i[el(r0 + rr, q, c, h, i)];
+  }
+
+  // ======================= forward: 10 applications of the shared ResBlock =================================
+#pragma unroll 1
+  for (int i = 0; i < NBLK; ++i) {
+    if (i > 0) {
+      bn_fwd_stats<NW>(cx, pa, epoch, i - 1, y, cred, misc, stat);
+      float* Xo = cx.X + (size_t)i * B * 8192 + img;
+      float* Yo = cx.Y + (size_t)(i - 1) * B * 8192 + img;  // y_{i-1}, written now that its exchange is done
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int ch = 16 * h + c;
+        const float sc = misc[192 + ch], sh = misc[224 + ch];
+#pragma unroll
+        for (int rr = 0; rr < RPW; ++rr)
+#pragma unroll
+          for (int i2 = 0; i2 < 4; ++i2) {
+            const int e = el(r0 + rr, q, c, h, i2), col = 4 * q + i2;
+            const float v = fmaxf(y[rr][h][i2] * sc + sh, 0.f) + x[rr][h][i2];
+            Yo[e] = y[rr][h][i2];
+            x[rr][h][i2] = v;
+            Xo[e] = v;
+            st1r(XR, (r0 + rr + 1) * 18 + col + 1, ch, v);
+          }
+      }
+      lds_barrier();
+    }
+    f32x4 acc[RPW][2];
+    conv_img<RPW>(XR, WT, acc, r0, lane);
+#pragma unroll
+    for (int rr = 0; rr < RPW; ++rr)
+#pragma unroll
+      for (int h = 0; h < 2; ++h)
+#pragma unroll
+        for (int i2 = 0; i2 < 4; ++i2) y[rr][h][i2] = acc[rr][h][i2];
+    PK_STAMP(cx, 2 + i);
+  }
+  bn_fwd_stats<NW>(cx, pa, epoch, NBLK - 1, y, cred, misc, stat);
+  if (n == 0 && t == 0) *cx.nbt += NBLK;
+  if (n == 0 && t < 32) {
+    cx.rm[t] = misc[448 + t];
+    cx.rv[t] = misc[480 + t];
+  }
+  {
+    float* Yo = cx.Y + (size_t)(NBLK - 1) * B * 8192 + img;
+#pragma unroll
+    for (int rr = 0; rr < RPW; ++rr)
+#pragma unroll
+      for (int h = 0; h < 2; ++h)
+#pragma unroll
+        for (int i2 = 0; i2 < 4; ++i2) Yo[el(r0 + rr, q, c, h, i2)] = y[rr][h][i2];
+  }
+  PK_STAMP(cx, 12);
+
+  // ======================= head =============================================================================
+  float g[RPW][2][4];
+  {
+    float* x10 = (float*)(U + P::U_X10);
+    float* Pv = (float*)(U + P::U_P);
+    uint8_t* code = (uint8_t*)(U + P::U_CODE);
+    float* dp = (float*)(U + P::U_DP);
+    float* hp = (float*)(U + P::U_HP);
+    float* hv = (float*)(U + P::U_HV);  // h[0..32) dh[32..64) logits[64..80) dl[80..96)
+    float* dpp = (float*)(U + P::U_DPP);
+    constexpr int NWR = 32 / NW;  // fc1 rows owned by each wave
+    const float* W1 = cx.params + OFF_FC1W;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int ch = 16 * h + c;
+      const float sc = misc[192 + ch], sh = misc[224 + ch];
+#pragma unroll
+      for (int rr = 0; rr < RPW; ++rr)
+#pragma unroll
+        for (int i2 = 0; i2 < 4; ++i2)
+          x10[el(r0 + rr, q, c, h, i2)] = fmaxf(y[rr][h][i2] * sc + sh, 0.f) + x[rr][h][i2];
+    }
+    lds_barrier();
+#pragma unroll
+    for (int m = 0; m < 2048 / NTH; ++m) {
+      const int o = t + NTH * m, ch = o & 31, pp = o >> 5, pr = pp >> 3, pw = pp & 7;
+      const int p00 = ((2 * pr) * 16 + 2 * pw) * 32 + ch;
+      const float v00 = x10[p00], v01 = x10[p00 + 32], v10 = x10[p00 + 512], v11 = x10[p00 + 544];
+      float best = v00;
+      int id = 0;
+      if (v01 > best) { best = v01; id = 1; }
+      if (v10 > best) { best = v10; id = 2; }
+      if (v11 > best) { best = v11; id = 3; }
+      Pv[ch * 64 + pp] = best;
+      code[pp * 32 + ch] = (uint8_t)id;
+      cx.HP[(size_t)n * 2048 + ch * 64 + pp] = best;
+    }
+    lds_barrier();
+    // fc1: wave w computes rows j = w*NWR .. +NWR-1 (8 KiB of W1 each, streamed, next row prefetched);
+    // lane l covers features 4l + 256m (m < 8).
+    {
+      f32x4 p4[8];
+#pragma unroll
+      for (int m = 0; m < 8; ++m) p4[m] = ld4(Pv + 4 * lane + 256 * m);
+      f32x4 wa[8], wb[8];
+#pragma unroll
+      for (int m = 0; m < 8; ++m) wa[m] = ld4(W1 + (w * NWR) * 2048 + 4 * lane + 256 * m);
+#pragma unroll
+      for (int jr = 0; jr < NWR; ++jr) {
+        const int j = w * NWR + jr;
+        if (jr + 1 < NWR) {
+#pragma unroll
+          for (int m = 0; m < 8; ++m) wb[m] = ld4(W1 + (j + 1) * 2048 + 4 * lane + 256 * m);
+        }
+        float s = 0.f;
+#pragma unroll
+        for (int m = 0; m < 8; ++m) s += wa[m].x * p4[m].x + wa[m].y * p4[m].y + wa[m].z * p4[m].z + wa[m].w * p4[m].w;
+#pragma unroll
+        for (int o = 32; o >= 1; o >>= 1) s += __shfl_xor(s, o);
+        if (lane == 0) hp[j] = s;
+#pragma unroll
+        for (int m = 0; m < 8; ++m) wa[m] = wb[m];
+      }
+    }
+    lds_barrier();
+    if (t < 32) hv[t] = misc[512 + t] + hp[t];
+    lds_barrier();
+    if (t < 10) {
+      float s = misc[544 + 320 + t];
+#pragma unroll
+      for (int j = 0; j < 32; ++j) s += misc[544 + t * 32 + j] * fmaxf(hv[j], 0.f);
+      hv[64 + t] = s;
+    }
+    lds_barrier();
+    if (t == 0) {
+      const int label = cx.labels[sample_id(cx, n)];
+      float mx = hv[64];
+      for (int o = 1; o < 10; ++o) mx = fmaxf(mx, hv[64 + o]);
+      float se = 0.f;
+      for (int o = 0; o < 10; ++o) se += expf(hv[64 + o] - mx);
+      const float lse = mx + logf(se);
+      cx.HLOSS[n] = lse - hv[64 + label];
+      const float invB = 1.f / (float)B;
+      for (int o = 0; o < 10; ++o) hv[80 + o] = (expf(hv[64 + o] - lse) - (o == label ? 1.f : 0.f)) * invB;
+    }
+    lds_barrier();
+    if (t < 32) {
+      float s = 0.f;
+#pragma unroll
+      for (int o = 0; o < 10; ++o) s += misc[544 + o * 32 + t] * hv[80 + o];
+      const float hh = hv[t];
+      const float dh = hh > 0.f ? s : 0.f;
+      hv[32 + t] = dh;
+      cx.HDH[n * 32 + t] = dh;
+      cx.HH[n * 32 + t] = fmaxf(hh, 0.f);
+      if (t < 10) cx.HDL[n * 10 + t] = hv[80 + t];
+    }
+    lds_barrier();
+    // dp = W1^T dh: per-wave partials over the wave's rows (rows streamed again), summed in fixed order
+    {
+      f32x4 d4[8];
+#pragma unroll
+      for (int m = 0; m < 8; ++m) d4[m] = z4();
+#pragma unroll
+      for (int jr = 0; jr < NWR; ++jr) {
+        const int j = w * NWR + jr;
+        const float dh = hv[32 + j];
+#pragma unroll
+        for (int m = 0; m < 8; ++m) d4[m] += dh * ld4(W1 + j * 2048 + 4 * lane + 256 * m);
+      }
+#pragma unroll
+      for (int m = 0; m < 8; ++m) st4(dpp + w * 2048 + 4 * lane + 256 * m, d4[m]);
+    }
+    lds_barrier();
+    for (int k = t; k < 2048; k += NTH) {
+      float s = 0.f;
+#pragma unroll
+      for (int k2 = 0; k2 < NW; ++k2) s += dpp[k2 * 2048 + k];
+      dp[k] = s;
+    }
+    lds_barrier();
+#pragma unroll
+    for (int rr = 0; rr < RPW; ++rr)
+#pragma unroll
+      for (int h = 0; h < 2; ++h)
+#pragma unroll
+        for (int i2 = 0; i2 < 4; ++i2) {
+          const int row = r0 + rr, ch = 16 * h + c, col = 4 * q + i2;
+          const int pp = (row >> 1) * 8 + (col >> 1), pos = (row & 1) * 2 + (col & 1);
+          g[rr][h][i2] = code[pp * 32 + ch] == pos ? dp[ch * 64 + pp] : 0.f;
+        }
+    if (pa.debug) {
+#pragma unroll
+      for (int rr = 0; rr < RPW; ++rr)
+#pragma unroll
+        for (int h = 0; h < 2; ++h)
+#pragma unroll
+          for (int i2 = 0; i2 < 4; ++i2) cx.G[img + el(r0 + rr, q, c, h, i2)] = g[rr][h][i2];
+    }
+    lds_barrier();
+  }
+  PK_STAMP(cx, 13);
+  __syncthreads();  // X[0] / SCODE (stem) and Y[9] are re-read from global by other threads from here on
+
+  // ======================= backward: 10 applications, newest first ========================================
+  unsigned short* dyT = (unsigned short*)(U + P::U_DYT);
+  unsigned short* xT = (unsigned short*)(U + P::U_XT);
+  stage_wt<NW>(WT, cx.wt_d);
+  zero_xr_halo<NW>(XR);
+  for (int idx = t; idx < 3 * 32 * P::XT_S * 2 / 16; idx += NTH) ((uint4*)xT)[idx] = uint4{0u, 0u, 0u, 0u};
+  float yb[RPW][2][4], xb[RPW][2][4];
+  {
+    const float* yp = cx.Y + (size_t)(NBLK - 1) * B * 8192 + img;
+    const float* xp = cx.X + (size_t)(NBLK - 1) * B * 8192 + img;
+#pragma unroll
+    for (int rr = 0; rr < RPW; ++rr)
+#pragma unroll
+      for (int h = 0; h < 2; ++h)
+#pragma unroll
+        for (int i2 = 0; i2 < 4; ++i2) {
+          yb[rr][h][i2] = yp[el(r0 + rr, q, c, h, i2)];
+          xb[rr][h][i2] = xp[el(r0 + rr, q, c, h, i2)];
+        }
+  }
+  f32x4 wacc[Gm::WTL];
+#pragma unroll
+  for (int j = 0; j < Gm::WTL; ++j) wacc[j] = z4();
+  float dgam = 0.f, dbet = 0.f;
+  lds_barrier();
+  const float Ntot = (float)B * 256.f;
+#pragma unroll 1
+  for (int i = NBLK - 1; i >= 0; --i) {
+    // yb / xb hold y_i / x_i (loaded during the previous block)
+    float sa[2] = {0.f, 0.f}, sbv[2] = {0.f, 0.f}, dz[RPW][2][4], xh[RPW][2][4];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int ch = 16 * h + c;
+      const float mean = stat[i * 64 + ch], inv = stat[i * 64 + 32 + ch];
+      const float gam = misc[320 + ch], bet = misc[352 + ch];
+      const float sc = gam * inv, sh = bet - mean * sc;
+#pragma unroll
+      for (int rr = 0; rr < RPW; ++rr)
+#pragma unroll
+        for (int i2 = 0; i2 < 4; ++i2) {
+          xh[rr][h][i2] = (yb[rr][h][i2] - mean) * inv;
+          dz[rr][h][i2] = (yb[rr][h][i2] * sc + sh) > 0.f ? g[rr][h][i2] : 0.f;
+          sa[h] += dz[rr][h][i2];
+          sbv[h] += dz[rr][h][i2] * xh[rr][h][i2];
+        }
+    }
+    img_csum2<NW>(sa[0], sa[1], sbv[0], sbv[1], cred, misc, misc + 32);  // image sums -> publish slots
+    // (the barriers above also retire every wave's reads of dyT / xT / XR from the previous block)
+#pragma unroll
+    for (int rr = 0; rr < RPW; ++rr)
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int ch = 16 * h + c, rowoff = (r0 + rr + 1) * 16 + 4 * q;
+        const unsigned b0 = bfbits(xb[rr][h][0]), b1 = bfbits(xb[rr][h][1]);
+        const unsigned b2 = bfbits(xb[rr][h][2]), b3 = bfbits(xb[rr][h][3]);
+        unsigned short* p1 = xT + (32 + ch) * P::XT_S + rowoff;  // kw = 1: x at the same column
+        *(uint2*)p1 = uint2{b0 | (b1 << 16), b2 | (b3 << 16)};
+        unsigned short* p0 = xT + ch * P::XT_S + rowoff;  // kw = 0: column + 1
+        p0[1] = (unsigned short)b0;
+        *(unsigned*)(p0 + 2) = b1 | (b2 << 16);
+        if (q < 3) p0[4] = (unsigned short)b3;
+        unsigned short* p2 = xT + (64 + ch) * P::XT_S + rowoff;  // kw = 2: column - 1
+        if (q > 0) p2[-1] = (unsigned short)b0;
+        *(unsigned*)p2 = b1 | (b2 << 16);
+        p2[2] = (unsigned short)b3;
+      }
+    if (i == 5) PK_STAMP(cx, 27);
+    xchg<NW>(pa, epoch, NBLK + (NBLK - 1 - i), cred, misc);
+    if (i == 5) PK_STAMP(cx, 28);
+    if (i > 0) {  // prefetch y_{i-1} / x_{i-1}; the loads land while this block's convolutions run
+      const float* yp = cx.Y + (size_t)(i - 1) * B * 8192 + img;
+      const float* xp = cx.X + (size_t)(i - 1) * B * 8192 + img;
+#pragma unroll
+      for (int rr = 0; rr < RPW; ++rr)
+#pragma unroll
+        for (int h = 0; h < 2; ++h)
+#pragma unroll
+          for (int i2 = 0; i2 < 4; ++i2) {
+            yb[rr][h][i2] = yp[el(r0 + rr, q, c, h, i2)];
+            xb[rr][h][i2] = xp[el(r0 + rr, q, c, h, i2)];
+          }
+    }
+    if (n == 0 && t < 32) {
+      dbet += misc[64 + t];
+      dgam += misc[96 + t];
+    }
+    float* dyo = cx.DY + (size_t)i * B * 8192 + img;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int ch = 16 * h + c;
+      const float Sa = misc[64 + ch], Sb = misc[96 + ch];
+      const float k1 = misc[320 + ch] * stat[i * 64 + 32 + ch] / Ntot;
+#pragma unroll
+      for (int rr = 0; rr < RPW; ++rr) {
+        const int row = r0 + rr;
+        unsigned bits[4];
+#pragma unroll
+        for (int i2 = 0; i2 < 4; ++i2) {
+          const float dyv = k1 * (Ntot * dz[rr][h][i2] - Sa - xh[rr][h][i2] * Sb);
+          const int col = 4 * q + i2;
+          st1r(XR, (row + 1) * 18 + col + 1, ch, dyv);
+          bits[i2] = bfbits(dyv);
+          if (pa.debug) dyo[el(row, q, c, h, i2)] = dyv;
+        }
+        *(uint2*)(dyT + ch * P::DYT_S + row * 16 + 4 * q) = uint2{bits[0] | (bits[1] << 16), bits[2] | (bits[3] << 16)};
+      }
+    }
+    lds_barrier();
+    // dgrad: g_i = g_{i+1} + conv(dy, W^T flipped)
+    {
+      f32x4 acc[RPW][2];
+      conv_img<RPW>(XR, WT, acc, r0, lane);
+#pragma unroll
+      for (int rr = 0; rr < RPW; ++rr)
+#pragma unroll
+        for (int h = 0; h < 2; ++h)
+#pragma unroll
+          for (int i2 = 0; i2 < 4; ++i2) g[rr][h][i2] += acc[rr][h][i2];
+    }
+    // wgrad of the shared conv, accumulated in registers over all 10 applications
+#pragma unroll
+    for (int j = 0; j < Gm::WTL; ++j) {
+      const int tt = w + NW * j;
+      if (tt < 36) {
+        const int mt = tt & 1, nt = tt >> 1, tap = nt >> 1, cih = nt & 1, kh = tap / 3, kw = tap % 3;
+#pragma unroll
+        for (int s = 0; s < 8; ++s) {
+          const int row = 2 * s + (q >> 1), c0 = 8 * (q & 1);
+          const bf16x8 a = *(const bf16x8*)(dyT + (16 * mt + c) * P::DYT_S + row * 16 + c0);
+          const bf16x8 b = *(const bf16x8*)(xT + (kw * 32 + 16 * cih + c) * P::XT_S + (row + kh) * 16 + c0);
+          wacc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, wacc[j], 0, 0, 0);
+        }
+      }
+    }
+    PK_STAMP(cx, 14 + (NBLK - 1 - i));
+    if (pa.debug && i >= 1) {
+      float* gout = cx.G + (size_t)((10 - i) & 1) * B * 8192 + img;
+#pragma unroll
+      for (int rr = 0; rr < RPW; ++rr)
+#pragma unroll
+        for (int h = 0; h < 2; ++h)
+#pragma unroll
+          for (int i2 = 0; i2 < 4; ++i2) gout[el(r0 + rr, q, c, h, i2)] = g[rr][h][i2];
+    }
+  }
+  // trunk wgrad slab + BN affine grads
+#pragma unroll
+  for (int j = 0; j < Gm::WTL; ++j) {
+    const int tt = w + NW * j;
+    if (tt < 36) st4(pa.tslab + (size_t)n * WSLAB_N + ((tt * 64 + lane) << 2), wacc[j]);
+  }
+  if (n == 0 && t < 32) {
+    pa.bng[t] = dgam;
+    pa.bng[32 + t] = dbet;
+  }
+
+  // ======================= stem backward: max-pool bwd (saved argmax) -> ReLU mask -> conv1 wgrad ==========
+  __syncthreads();
+  {
+    unsigned short* dsT = (unsigned short*)(U + P::U_DST);
+    float* xin = (float*)(U + P::U_XIN2);
+    uint8_t codes[RPW][2][4];
+#pragma unroll
+    for (int rr = 0; rr < RPW; ++rr)
+#pragma unroll
+      for (int h = 0; h < 2; ++h)
+#pragma unroll
+        for (int i2 = 0; i2 < 4; ++i2) codes[rr][h][i2] = cx.SCODE[img + el(r0 + rr, q, c, h, i2)];
+    for (int idx = t; idx < 32 * P::DSP * 2 / 16; idx += NTH) ((uint4*)dsT)[idx] = uint4{0u, 0u, 0u, 0u};
+    stage_input<NW>(xin, cx.data + (size_t)sample_id(cx, n) * 3072);
+    lds_barrier();
+    float db0 = 0.f, db1 = 0.f;
+#pragma unroll
+    for (int rr = 0; rr < RPW; ++rr)
+#pragma unroll
+      for (int h = 0; h < 2; ++h)
+#pragma unroll
+        for (int i2 = 0; i2 < 4; ++i2) {
+          const int code = codes[rr][h][i2];
+          if (code & 4) {
+            const int pos = code & 3, col = 4 * q + i2, ch = 16 * h + c;
+            const int sr = 2 * (r0 + rr) + (pos >> 1), sc = 2 * col + (pos & 1);
+            dsT[ch * P::DSP + sr * 32 + sc] = bfbits(g[rr][h][i2]);
+            if (h == 0) db0 += g[rr][h][i2];
+            else db1 += g[rr][h][i2];
+          }
+        }
+    img_csum2<NW>(db0, db1, 0.f, 0.f, cred, misc + 384, misc + 416);  // also the barrier before the MFMAs
+    float* ss = cx.SSLAB + (size_t)n * SSLAB_N;
+    if (t < 32) ss[1024 + t] = misc[384 + t];
+    // D[co][k] = sum over 1024 stem pixels of ds[p][co] * im2col[p][k];
+    // combo = (tile, row quarter): tile = combo & 3 (mt = tile & 1, nt = tile >> 1), rows 8*(combo>>2) .. +8
+    float* sred = (float*)(U + P::U_SRED);
+#pragma unroll
+    for (int cb = 0; cb < Gm::SBC; ++cb) {
+      const int combo = w + NW * cb, tile = combo & 3, part = combo >> 2, mt = tile & 1, nt = tile >> 1;
+      const int kidx = 16 * nt + c, co = 16 * mt + c;
+      const bool kv = kidx < 27;
+      const float* xb2 = xin + (kv ? (kidx / 9) * 34 * 34 + ((kidx % 9) / 3) * 34 + (kidx % 3) : 0);
+      f32x4 acc2 = z4();
+#pragma unroll 2
+      for (int s = 8 * part; s < 8 * part + 8; ++s) {
+        const bf16x8 a = *(const bf16x8*)(dsT + co * P::DSP + s * 32 + 8 * q);
+        bf16x8 b;
+#pragma unroll
+        for (int jj = 0; jj < 8; ++jj) b[jj] = (__bf16)(kv ? xb2[s * 34 + 8 * q + jj] : 0.f);
+        acc2 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, acc2, 0, 0, 0);
+      }
+      st4(sred + ((combo * 64 + lane) << 2), acc2);  // [16 combos][64 lanes][4]
+    }
+    lds_barrier();
+    if (t < 256) {
+      const int tile = t >> 6, ln = t & 63;
+      f32x4 s4 = z4();
+#pragma unroll
+      for (int pt = 0; pt < 4; ++pt) s4 += ld4(sred + (((pt * 4 + tile) * 64 + ln) << 2));
+      st4(ss + ((tile * 64 + ln) << 2), s4);
+    }
+  }
+  PK_STAMP(cx, 24);
+}
+
+// ============================================================================================================
+// Reduction + SGD after the persistent step.  Grid: 36 trunk chunks | 5 stem chunks | 32 fc1 column blocks |
+// 1 bookkeeping workgroup (fc2, biases, BN, loss, cursor, epoch).  256 threads.
+// ============================================================================================================
+constexpr int R_TRUNK = 36, R_STEM = 5, R_FC = 32, R_GRID = R_TRUNK + R_STEM + R_FC + 1;
+
+__device__ __forceinline__ void sgd_put(const Ctx& cx, int pidx, float gval) {
+  cx.grads[pidx] = gval;
+  if (cx.fuse_sgd) cx.params[pidx] -= cx.lr * gval;
+}
+
+__global__ void __launch_bounds__(256) k_pk_reduce(Ctx cx, PkArgs pa) {
+  __shared__ f32x4 red[256];
+  __shared__ float stage[64 * 32 + 64 * 64];
+  const int t = threadIdx.x, bid = blockIdx.x, B = cx.B;
+  if (bid < R_TRUNK + R_STEM) {
+    const bool stem = bid >= R_TRUNK;
+    const int chunk = stem ? bid - R_TRUNK : bid;
+    const int slot = t & 63, grp = t >> 6, e0 = chunk * 256 + slot * 4;
+    const float* src = stem ? cx.SSLAB : pa.tslab;
+    const int stride = stem ? SSLAB_N : WSLAB_N, lim = stem ? SSLAB_N : WSLAB_N;
+    f32x4 s = z4();
+    if (e0 < lim) {
+      f32x4 v[16];
+#pragma unroll
+      for (int u = 0; u < 16; ++u) {
+        const int k = grp + 4 * u;
+        v[u] = k < B ? ld4(src + (size_t)k * stride + e0) : z4();
+      }
+#pragma unroll
+      for (int u = 0; u < 16; ++u) s += v[u];
+    }
+    red[t] = s;
+    __syncthreads();
+    if (t < 64 && e0 < lim) {
+      const f32x4 tot = red[t] + red[64 + t] + red[128 + t] + red[192 + t];
+#pragma unroll
+      for (int ii = 0; ii < 4; ++ii) {
+        const int e = e0 + ii;
+        if (!stem) {
+          const int tt = e >> 8, ln = (e >> 2) & 63, mt = tt & 1, nt = tt >> 1, tap = nt >> 1, cih = nt & 1;
+          const int co = 16 * mt + 4 * (ln >> 4) + ii, ci = 16 * cih + (ln & 15);
+          const int pidx = OFF_CONVW + co * 288 + ci * 9 + tap;
+          sgd_put(cx, pidx, tot[ii]);
+          if (cx.fuse_sgd) {
+            const float wv = cx.params[pidx];
+            ((unsigned short*)cx.wt_f)[(tap * 32 + co) * 32 + ci] = bfbits(wv);
+            ((unsigned short*)cx.wt_d)[((8 - tap) * 32 + ci) * 32 + co] = bfbits(wv);
+          }
+        } else if (e < 1024) {
+          const int tt = e >> 8, ln = (e >> 2) & 63, mt = tt & 1, nt = tt >> 1;
+          const int co = 16 * mt + 4 * (ln >> 4) + ii, k = 16 * nt + (ln & 15);
+          if (k < 27) {
+            const int pidx = OFF_C1W + co * 27 + k;
+            sgd_put(cx, pidx, tot[ii]);
+            if (cx.fuse_sgd) ((unsigned short*)cx.sw)[co * 32 + k] = bfbits(cx.params[pidx]);
+          }
+        } else if (e < 1056) {
+          sgd_put(cx, OFF_C1B + (e - 1024), tot[ii]);
+        }
+      }
+    }
+    return;
+  }
+  if (bid < R_TRUNK + R_STEM + R_FC) {  // dW1[j][64f .. 64f+63] = sum_b dh[b][j] * p[b][k]
+    const int f = bid - R_TRUNK - R_STEM;
+    float* dh_s = stage;          // [B][32]
+    float* p_s = stage + 64 * 32; // [B][64]
+    f32x4 dh4[2], p4[4];
+#pragma unroll
+    for (int m = 0; m < 2; ++m) {
+      const int idx = t + 256 * m;
+      dh4[m] = idx < B * 8 ? ld4(cx.HDH + 4 * idx) : z4();
+    }
+#pragma unroll
+    for (int m = 0; m < 4; ++m) {
+      const int idx = t + 256 * m, b = idx >> 4, k4 = idx & 15;
+      p4[m] = idx < B * 16 ? ld4(cx.HP + (size_t)b * 2048 + 64 * f + 4 * k4) : z4();
+    }
+#pragma unroll
+    for (int m = 0; m < 2; ++m)
+      if (t + 256 * m < B * 8) st4(dh_s + 4 * (t + 256 * m), dh4[m]);
+#pragma unroll
+    for (int m = 0; m < 4; ++m)
+      if (t + 256 * m < B * 16) st4(p_s + 4 * (t + 256 * m), p4[m]);
+    __syncthreads();
+    const int j = t >> 3, kk = 8 * (t & 7);
+    f32x4 a0 = z4(), a1 = z4();
+    for (int b = 0; b < B; ++b) {
+      const float dh = dh_s[b * 32 + j];
+      a0 += dh * ld4(p_s + b * 64 + kk);
+      a1 += dh * ld4(p_s + b * 64 + kk + 4);
+    }
+    const int base = OFF_FC1W + j * 2048 + 64 * f + kk;
+    st4(cx.grads + base, a0);
+    st4(cx.grads + base + 4, a1);
+    if (cx.fuse_sgd) {
+      st4(cx.params + base, ld4(cx.params + base) - cx.lr * a0);
+      st4(cx.params + base + 4, ld4(cx.params + base + 4) - cx.lr * a1);
+    }
+    return;
+  }
+  // bookkeeping workgroup: fc1 bias, fc2, BN affine grads, loss, cursor, epoch, CC4 segment
+  {
+    float* hh_s = stage;             // [B][32]
+    float* dl_s = stage + 64 * 32;   // [B][16]
+    float* dh_s = dl_s + 64 * 16;    // [B][32]
+    for (int idx = t; idx < B * 32; idx += 256) {
+      hh_s[idx] = cx.HH[idx];
+      dh_s[idx] = cx.HDH[idx];
+    }
+    for (int idx = t; idx < B * 10; idx += 256) dl_s[(idx / 10) * 16 + idx % 10] = cx.HDL[idx];
+    float lsum = 0.f;
+    for (int b = t; b < B; b += 256) lsum += cx.HLOSS[b];
+    ((float*)red)[t] = lsum;
+    __syncthreads();
+    for (int idx = t; idx < 32 + 320 + 10 + 64; idx += 256) {
+      float s = 0.f;
+      if (idx < 32) {
+        for (int b = 0; b < B; ++b) s += dh_s[b * 32 + idx];
+        sgd_put(cx, OFF_FC1B + idx, s);
+      } else if (idx < 352) {
+        const int o = (idx - 32) >> 5, jj = (idx - 32) & 31;
+        for (int b = 0; b < B; ++b) s += dl_s[b * 16 + o] * hh_s[b * 32 + jj];
+        sgd_put(cx, OFF_FC2W + o * 32 + jj, s);
+      } else if (idx < 362) {
+        const int o = idx - 352;
+        for (int b = 0; b < B; ++b) s += dl_s[b * 16 + o];
+        sgd_put(cx, OFF_FC2B + o, s);
+      } else {
+        const int k = idx - 362;  // 0..31 dgamma, 32..63 dbeta
+        sgd_put(cx, (k < 32 ? OFF_BNW : OFF_BNB) + (k & 31), pa.bng[k]);
+      }
+    }
+    if (t == 0) {
+      float s = 0.f;
+      for (int k = 0; k < 256 && k < B; ++k) s += ((float*)red)[k];
+      *cx.loss_acc += (double)(s / (float)B);
+      *cx.cursor += B;
+      *cx.step_count += 1;
+      *pa.epoch += 1;
+    }
+    if (!cx.fuse_sgd && t < 64) {
+      const float v = t < 32 ? cx.rm[t] : cx.rv[t - 32];
+      cx.grads[OFF_RS + t] = cx.rank == 0 ? v : 0.f;
+    }
+  }
+}
+
+}  // namespace pk
+}  // namespace dca

@@ -35,7 +35,8 @@ class FusedDDPTrainer:
     """NetResDeep + DDP + SGD as one native, graph-captured training step per batch."""
 
     def __init__(self, model: nn.Module, data_u8: torch.Tensor, labels: torch.Tensor, batch_max: int = 32,
-                 lr: float = 1e-2, dtype: str = "bf16", rows: int = 4, max_indices: Optional[int] = None):
+                 lr: float = 1e-2, dtype: str = "bf16", rows: int = 4, max_indices: Optional[int] = None,
+                 persistent: Optional[bool] = None):
         world = dist.get_world_size() if dist.is_available() and dist.is_initialized() else 1
         rank = dist.get_rank() if world > 1 else 0
         self.world_size, self.rank = world, rank
@@ -45,7 +46,8 @@ class FusedDDPTrainer:
             obj = [nccl_unique_id() if rank == 0 else None]
             dist.broadcast_object_list(obj, src=0)
             nccl_id = obj[0]
-        cfg = EngineConfig(batch_max=batch_max, lr=lr, dtype=dtype, rows=rows, world_size=world, rank=rank)
+        cfg = EngineConfig(batch_max=batch_max, lr=lr, dtype=dtype, rows=rows, world_size=world, rank=rank,
+                           persistent=persistent)
         self.engine = NetResDeepEngine(model, data_u8, labels, cfg, nccl_id=nccl_id, max_indices=max_indices)
         self.module = model
 

@@ -59,6 +59,9 @@ class _DcaInit(ctypes.Structure):
         ("world_size", ctypes.c_int),
         ("rank", ctypes.c_int),
         ("nccl_id", ctypes.c_char_p),
+        ("persistent", ctypes.c_int),
+        ("debug", ctypes.c_int),
+        ("pk_waves", ctypes.c_int),
     ]
 
 
@@ -93,7 +96,10 @@ class EngineConfig:
     batch_max: int = 32
     lr: float = 1e-2
     dtype: str = "bf16"          # "bf16": bf16 MFMA (fp32 accumulate/storage); "fp32": exact fp32 MFMA
-    rows: int = 4                # trunk rows per workgroup tile (2 or 4)
+    rows: int = 4                # multi-kernel engine: trunk rows per workgroup tile (2 or 4)
+    persistent: Optional[bool] = None  # one-launch persistent trunk kernel (default: on for bf16)
+    debug: bool = False          # persistent engine: also store per-block dy / residual grads (diagnostics)
+    pk_waves: int = 8            # persistent engine: waves per workgroup (8: 2 image rows per wave; or 4)
     world_size: int = 1
     rank: int = 0
     bn_momentum: float = 0.1
@@ -107,6 +113,10 @@ class NetResDeepEngine:
                  nccl_id: Optional[bytes] = None, max_indices: Optional[int] = None):
         if cfg.dtype not in ("bf16", "fp32"):
             raise ValueError("dtype must be 'bf16' or 'fp32'")
+        if cfg.persistent is None:
+            cfg.persistent = cfg.dtype == "bf16"
+        if cfg.persistent and cfg.dtype != "bf16":
+            raise ValueError("the persistent engine is bf16-only; use persistent=False for fp32")
         if getattr(model, "n_chans1", 32) != 32 or getattr(model, "n_blocks", 10) != 10:
             raise ValueError("the fused engine is specialised for NetResDeep(n_chans1=32, n_blocks=10)")
         self.lib = native.require_native()
@@ -137,6 +147,7 @@ class NetResDeepEngine:
             bmax=int(cfg.batch_max), bf16=1 if cfg.dtype == "bf16" else 0, rows=int(cfg.rows), lr=float(cfg.lr),
             bn_mom=float(cfg.bn_momentum), bn_eps=float(cfg.bn_eps), world_size=int(cfg.world_size),
             rank=int(cfg.rank), nccl_id=ctypes.cast(self._nccl_id, ctypes.c_char_p),
+            persistent=1 if cfg.persistent else 0, debug=1 if cfg.debug else 0, pk_waves=int(cfg.pk_waves),
         )
         self._init = init
         self.max_indices = int(max_indices or self.data.shape[0])
@@ -173,8 +184,17 @@ class NetResDeepEngine:
         """Enqueue `steps` training steps of `batch` images each (asynchronous)."""
         native.check(self.lib.dca_engine_run(self.h, int(batch), int(steps), 1 if graph else 0), "dca_engine_run")
 
+    def check_errors(self, reset: bool = True) -> None:
+        """Raise if a persistent-kernel BN exchange timed out (a workgroup was not co-resident)."""
+        flags = ctypes.c_uint()
+        native.check(self.lib.dca_engine_errors(self.h, ctypes.byref(flags), int(reset)), "dca_engine_errors")
+        if flags.value:
+            raise RuntimeError(f"persistent engine: BN-statistics exchange timed out (round mask {flags.value:#x}); "
+                               "results of the affected steps are invalid")
+
     def read_loss(self, reset: bool = False) -> tuple[float, int]:
         """(sum of per-step mean losses, steps) since the last reset.  Synchronises."""
+        self.check_errors()
         loss = ctypes.c_double()
         steps = ctypes.c_int()
         native.check(self.lib.dca_engine_read_loss(self.h, ctypes.byref(loss), ctypes.byref(steps), int(reset)),

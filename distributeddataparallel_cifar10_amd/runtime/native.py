@@ -43,6 +43,7 @@ def _declare(lib):
     lib.dca_engine_region.restype = c_void_p
     lib.dca_engine_workspace_bytes.argtypes = [c_void_p]
     lib.dca_engine_workspace_bytes.restype = ctypes.c_size_t
+    lib.dca_engine_errors.argtypes = [c_void_p, ctypes.POINTER(ctypes.c_uint), c_int]
     lib.dca_microbench.argtypes = [c_int, c_int, c_int, c_int, ctypes.POINTER(ctypes.c_float)]
     lib.dca_microbench_xchg.argtypes = [c_int, c_int, c_int, c_int, c_int, ctypes.POINTER(ctypes.c_float),
                                         ctypes.POINTER(c_int)]
