@@ -70,10 +70,10 @@ def compare_one_step(dtype: str, rows: int, B: int, graph: bool, seed: int = 0, 
     loss, steps = eng.read_loss()
     rep("loss", torch.tensor([loss]), torch.tensor([r["loss"]]))
     n = B * 8192
-    X = eng.region("X", 10 * n).view(10, B, 16, 16, 32)
-    Y = eng.region("Y", 10 * n).view(10, B, 16, 16, 32)
-    DY = eng.region("DY", 10 * n).view(10, B, 16, 16, 32)
-    G = eng.region("G", 2 * n).view(2, B, 16, 16, 32)
+    X = eng.activations("X", 10, B)
+    Y = eng.activations("Y", 10, B)
+    DY = eng.activations("DY", 10, B)
+    G = eng.activations("G", 2, B)
     for i in range(10):
         rep(f"x{i}", X[i], nchw_to_nhwc(r["x"][i]))
     for i in range(10):

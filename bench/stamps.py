@@ -39,26 +39,29 @@ def microbench(lib):
     return out
 
 
-PK_NAMES = (["start", "stem"] + [f"fwd{i}" for i in range(10)] + ["bn9+head_start", "head"] +
-            [f"bwd{i}" for i in range(9, -1, -1)] + ["stem_bwd", "fwd5_pre_xchg", "fwd5_post_xchg",
-                                                     "bwd5_pre_xchg", "bwd5_post_xchg"])
+# persistent-kernel stamp ids (netresdeep_persistent.hip PK_STAMP): 0 start, 1 stem end, 2+i fwd block i conv end,
+# 12 bn9 stats, 13 head end, 14+k bwd block 9-k end, 24 kernel end, 25/26 and 27/28 around the block-5 exchanges,
+# 29 stem staged, 30 stem MFMA done, 31 head pooled, 32 fc1 done, 33 CE done, 34 stem-bwd staged, 35 stem-bwd MFMA
+PK_INTERVALS = ([("stem", 0, 1), ("stem.stage", 0, 29), ("stem.mfma", 29, 30), ("stem.tail", 30, 1)] +
+                [(f"fwd{i}", 1 + i, 2 + i) for i in range(10)] +
+                [("bn9+head_start", 11, 12), ("head", 12, 13), ("head.pool", 12, 31), ("head.fc1", 31, 32),
+                 ("head.ce", 32, 33), ("head.dp", 33, 13)] +
+                [(f"bwd{9 - k}", 13 + k, 14 + k) for k in range(10)] +
+                [("stem_bwd", 23, 24), ("stem_bwd.stage", 23, 34), ("stem_bwd.mfma", 34, 35),
+                 ("stem_bwd.tail", 35, 24),
+                 ("fwd5_pre_xchg", 6, 25), ("fwd5_xchg", 25, 26), ("bwd5_pre_xchg", 18, 27), ("bwd5_xchg", 27, 28)])
 
 
 def persistent_report(st):
     """Per-phase durations of the persistent kernel (median over workgroups, shader cycles and us)."""
-    flat = st[24:28].transpose(1, 0, 2, 3).reshape(256, 32, 2)  # [wg][stamp][memtime|realtime]
+    flat = st[24:32].transpose(1, 0, 2, 3).reshape(256, 64, 2)  # [wg][stamp][memtime|realtime]
     valid = flat[:, 0, 1] != 0
-    f = flat[valid]
+    f = flat[valid].astype(np.int64)
     out = []
-    for s in range(1, 29):
-        prev = s - 1 if s not in (25, 27) else {25: 6, 27: 18}[s]
-        if s in (26, 28):
-            prev = s - 1
-        if s == 25:
-            prev = 6   # fwd4 end -> fwd5 pre-xchg
-        cyc = np.median(f[:, s, 0] - f[:, prev, 0])
-        us = np.median(f[:, s, 1] - f[:, prev, 1]) / 100.0
-        out.append({"phase": PK_NAMES[s], "cyc": int(cyc), "us": round(float(us), 2)})
+    for name, a, b in PK_INTERVALS:
+        cyc = np.median(f[:, b, 0] - f[:, a, 0])
+        us = np.median(f[:, b, 1] - f[:, a, 1]) / 100.0
+        out.append({"phase": name, "cyc": int(cyc), "us": round(float(us), 2)})
     tot = np.median(f[:, 24, 1] - f[:, 0, 1]) / 100.0
     return out, round(float(tot), 2)
 

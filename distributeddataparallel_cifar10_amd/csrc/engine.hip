@@ -141,7 +141,7 @@ static int alloc_workspace(Engine* e) {
       {"RS_BASE", 64 * 4},           {"CURSOR", 16},                  {"STEPS", 16},
       {"LOSS", 16},                  {"STAMPS", 32 * 256 * 8 * 2 * 8},
       {"GRAN", 2 * 64 * 64 * 8},     {"EPOCH", 16},                   {"ERR", 16},
-      {"TSLAB", bmax * WSLAB_N * 4}, {"BNG", 64 * 4},
+      {"TSLAB", bmax * WSLAB_N * 4}, {"BNG", 64 * 4}, {"IDS", 64 * 4},
   };
   size_t total = 0;
   for (auto& r : regs) total += align_up(r.bytes, 256);
@@ -185,6 +185,7 @@ static int alloc_workspace(Engine* e) {
   e->pa.err = (unsigned*)e->regions["ERR"];
   e->pa.tslab = (float*)e->regions["TSLAB"];
   e->pa.bng = (float*)e->regions["BNG"];
+  e->pa.ids = (int*)e->regions["IDS"];
   e->pa.debug = e->in.debug;
   return 0;
 }
@@ -423,6 +424,8 @@ int dca_nccl_unique_id(char* out128) {
   return 0;
 }
 
+static int prime_ids(Engine* e);
+
 int dca_engine_create(const DcaInit* in, int n_indices, void** out) {
   Engine* e = new Engine();
   e->in = *in;
@@ -484,6 +487,8 @@ int dca_engine_create(const DcaInit* in, int n_indices, void** out) {
     memcpy(&id, in->nccl_id, 128);
     NCCK(ncclCommInitRank(&e->comm, in->world_size, id, in->rank));
   }
+  if (prime_ids(e)) return -1;
+  HIPCK(hipStreamSynchronize(e->st));
   *out = e;
   return 0;
 }
@@ -516,6 +521,14 @@ int dca_engine_derive(void* h) {
   return 0;
 }
 
+// persistent engine: the batch ids of the next step are produced by the previous step; re-derive them whenever
+// the host moves the cursor or replaces the index list
+static int prime_ids(Engine* e) {
+  hipLaunchKernelGGL(dca::pk::k_pk_prime_ids, dim3(1), dim3(64), 0, e->st, e->base, e->pa);
+  HIPCK(hipGetLastError());
+  return 0;
+}
+
 int dca_engine_set_indices(void* h, const int* host_idx, int n) {
   Engine* e = (Engine*)h;
   if (n > e->n_indices) {
@@ -523,6 +536,7 @@ int dca_engine_set_indices(void* h, const int* host_idx, int n) {
     return -1;
   }
   HIPCK(hipMemcpyAsync(e->indices, host_idx, sizeof(int) * (size_t)n, hipMemcpyHostToDevice, e->st));
+  if (prime_ids(e)) return -1;
   HIPCK(hipStreamSynchronize(e->st));
   return 0;
 }
@@ -530,6 +544,7 @@ int dca_engine_set_indices(void* h, const int* host_idx, int n) {
 int dca_engine_set_cursor(void* h, int v) {
   Engine* e = (Engine*)h;
   HIPCK(hipMemcpyAsync(e->base.cursor, &v, sizeof(int), hipMemcpyHostToDevice, e->st));
+  if (prime_ids(e)) return -1;
   HIPCK(hipStreamSynchronize(e->st));
   return 0;
 }

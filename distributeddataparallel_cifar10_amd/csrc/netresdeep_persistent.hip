@@ -33,6 +33,7 @@ struct PkArgs {
   unsigned* err;             // bit r: exchange round r timed out
   float* tslab;              // [B][9216] trunk wgrad (fragment order)
   float* bng;                // [64] dgamma | dbeta  (written by workgroup 0)
+  int* ids;                  // [64] dataset ids of the current batch (written by the previous step's reduce)
   int debug;                 // also store DY / G for the numerical diagnostics
 };
 
@@ -91,6 +92,14 @@ static_assert(Plan::U_XIN % 16 == 0 && Plan::U_SW % 16 == 0 && Plan::U_X0 % 16 =
 // stay in flight across the barrier.  Cross-thread hand-offs through GLOBAL memory use __syncthreads().
 __device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
+// Force a loaded value to be materialised here.  hipcc otherwise sinks a load whose only use is a guarded
+// LDS store into the guarded branch, where it is waited for on its own: N guarded loads become N serial
+// memory round trips.  Pinning after all loads of a phase keeps them in flight together.
+__device__ __forceinline__ void pin(float& x) { asm volatile("" : "+v"(x)); }
+__device__ __forceinline__ void pin(unsigned& x) { asm volatile("" : "+v"(x)); }
+__device__ __forceinline__ void pin(int& x) { asm volatile("" : "+v"(x)); }
+__device__ __forceinline__ void pin(uint4& x) { asm volatile("" : "+v"(x.x), "+v"(x.y), "+v"(x.z), "+v"(x.w)); }
+
 // Workgroup geometry: NW waves, each owning RPW consecutive image rows.
 template <int NW>
 struct Geo {
@@ -100,11 +109,22 @@ struct Geo {
   static constexpr int WTL = (36 + NW - 1) / NW;  // wgrad output tiles per wave
   static constexpr int KPT = 2048 / NT;           // fc1 input features per thread
   static constexpr int SBC = 16 / NW;             // stem-wgrad (tile, row-quarter) combos per wave
+  static constexpr int IMW = (768 + NT - 1) / NT; // uint8 image words per thread
 };
 
-// offset of the C-layout element (row, h, i) of lane (q, c) inside an NHWC [16][16][32] image
+// offset of the C-layout element (row, h, i) of lane (q, c) inside an NHWC [16][16][32] image (LDS staging)
 __device__ __forceinline__ int el(int row, int q, int c, int h, int i) {
   return ((row * 16 + 4 * q + i) << 5) + 16 * h + c;
+}
+// Global activations (X, Y, DY, G, SCODE) use the fragment-tiled layout [row][h][lane][i]: a thread's four
+// values of (row, h) are 16 contiguous bytes, so every global access is one dwordx4 per (row, h) and one wave
+// instruction covers a whole 1 KiB line run.  Element (row, col = 4q + i, ch = 16h + c) lives at
+// tl(row, h, 16q + c) + i.  (runtime/engine.py: NetResDeepEngine.activations() converts to NHWC.)
+__device__ __forceinline__ int tl(int row, int h, int lane) { return row * 512 + h * 256 + lane * 4; }
+__device__ __forceinline__ void st4v(float* p, const float (&v)[4]) { *(f32x4*)p = f32x4{v[0], v[1], v[2], v[3]}; }
+__device__ __forceinline__ void ld4v(const float* p, float (&v)[4]) {
+  const f32x4 u = *(const f32x4*)p;
+  v[0] = u[0]; v[1] = u[1]; v[2] = u[2]; v[3] = u[3];
 }
 
 // per-image channel sums of two per-thread C-layout partials (a0: channel c, a1: channel 16+c; same for b);
@@ -139,9 +159,39 @@ __device__ __forceinline__ void img_csum2(float a0, float a1, float b0, float b1
 
 // In-kernel all-gather: every workgroup contributes misc[0..64); on return misc[64..128) holds the sum over
 // workgroups of each value and misc[128..192) the sum of squares.  Ends with a barrier.
+// one sweep pass over the granules of round `tag`: KS loads per lane, all issued before any is waited for
+// (a guarded load per slot would be compiled into KS serial round trips).  Slots past the grid read a valid
+// granule (clamped index) and are then replaced by a neutral (0, tag) pair.
+template <int NW, int KS>
+__device__ __forceinline__ bool sweep(const __amdgpu_buffer_rsrc_t rs, int w, int lane, int G, unsigned tag,
+                                      float& s1, float& s2) {
+  unsigned lo[KS], hi[KS];
+#pragma unroll
+  for (int kk = 0; kk < KS; ++kk) {
+    const int k = w + NW * kk, kc = k < G ? k : G - 1;
+    const auto x = __builtin_amdgcn_raw_buffer_load_b64(rs, (kc * 64 + lane) * 8, 0, 16);  // sc1
+    lo[kk] = x[0];
+    hi[kk] = x[1];
+  }
+  bool ok = true;
+  s1 = 0.f;
+  s2 = 0.f;
+#pragma unroll
+  for (int kk = 0; kk < KS; ++kk) {
+    const bool valid = w + NW * kk < G;
+    ok &= !valid || hi[kk] == tag;
+    const float v = valid ? __uint_as_float(lo[kk]) : 0.f;
+    s1 += v;
+    s2 += v * v;
+  }
+  return ok;
+}
+
+// In-kernel all-gather: every workgroup contributes misc[0..64); on return misc[64..128) holds the sum over
+// workgroups of each value and misc[128..192) the sum of squares.  Ends with a barrier.
 template <int NW>
 __device__ void xchg(const PkArgs& pa, int epoch, int round, float* cred, float* misc) {
-  constexpr int KSW = Geo<NW>::KSW;
+  constexpr int KSW = Geo<NW>::KSW, KSH = (32 + NW - 1) / NW;
   const int t = threadIdx.x, lane = t & 63, n = blockIdx.x, G = gridDim.x;
   const int w = __builtin_amdgcn_readfirstlane(t >> 6);  // wave-uniform -> scalar branches in the sweep
   const unsigned tag = (unsigned)(epoch * 64 + round + 1);
@@ -152,29 +202,8 @@ __device__ void xchg(const PkArgs& pa, int epoch, int round, float* cred, float*
   const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(buf, (short)0, 64 * 64 * 8, 0x00020000);
   float s1 = 0.f, s2 = 0.f;
   for (unsigned spins = 0;; ++spins) {
-    unsigned lo[KSW], hi[KSW];
-#pragma unroll
-    for (int kk = 0; kk < KSW; ++kk) {
-      const int k = w + NW * kk;
-      if (k < G) {
-        const auto x = __builtin_amdgcn_raw_buffer_load_b64(rs, (k * 64 + lane) * 8, 0, 16);  // sc1
-        lo[kk] = x[0];
-        hi[kk] = x[1];
-      } else {
-        lo[kk] = 0u;
-        hi[kk] = tag;
-      }
-    }
-    bool ok = true;
-    s1 = 0.f;
-    s2 = 0.f;
-#pragma unroll
-    for (int kk = 0; kk < KSW; ++kk) {
-      ok &= hi[kk] == tag;
-      const float v = __uint_as_float(lo[kk]);
-      s1 += v;
-      s2 += v * v;
-    }
+    asm volatile("" ::: "memory");  // the granule loads are re-issued every pass (no hoisting out of the spin)
+    const bool ok = G <= 32 ? sweep<NW, KSH>(rs, w, lane, G, tag, s1, s2) : sweep<NW, KSW>(rs, w, lane, G, tag, s1, s2);
     if (__all(ok)) break;
     if (spins >= SPIN_LIMIT) {
       if (lane == 0) atomicOr(pa.err, 1u << (round & 31));
@@ -294,14 +323,45 @@ __device__ __forceinline__ void stage_wt(char* wt, const void* src) {
   const uint4* s = (const uint4*)src;
   uint4 v[M];
 #pragma unroll
-  for (int m = 0; m < M; ++m) {
+  for (int m = 0; m < M; ++m) {  // unconditional (clamped) loads: all in flight together, no scratch
     const int idx = threadIdx.x + 64 * NW * m;
-    if (idx < 1152) v[m] = s[idx];
+    v[m] = s[idx < 1152 ? idx : 1151];
   }
+#pragma unroll
+  for (int m = 0; m < M; ++m) pin(v[m]);
 #pragma unroll
   for (int m = 0; m < M; ++m) {
     const int idx = threadIdx.x + 64 * NW * m;
     if (idx < 1152) *(uint4*)(wt + (idx >> 2) * Plan::RB + (idx & 3) * 16) = v[m];
+  }
+}
+// stage_input in two halves, so the global loads can be issued long before the LDS region is free
+template <int NW>
+__device__ __forceinline__ void stage_input_load(unsigned (&wd)[Geo<NW>::IMW], const uint8_t* img) {
+  constexpr int NTH = 64 * NW;
+#pragma unroll
+  for (int m = 0; m < Geo<NW>::IMW; ++m) {
+    const int idx = threadIdx.x + NTH * m;
+    wd[m] = ((const unsigned*)img)[idx < 768 ? idx : 767];
+  }
+}
+template <int NW>
+__device__ __forceinline__ void stage_input_store(float* xin, const unsigned (&wd)[Geo<NW>::IMW]) {
+  constexpr int NTH = 64 * NW;
+  const int t = threadIdx.x;
+  for (int idx = t; idx < 3 * 34 * 34; idx += NTH) {
+    const int rem = idx % (34 * 34), r = rem / 34, cc = rem % 34;
+    if (r == 0 || r == 33 || cc == 0 || cc == 33) xin[idx] = 0.f;
+  }
+#pragma unroll
+  for (int m = 0; m < Geo<NW>::IMW; ++m) {
+    const int idx = t + NTH * m;
+    if (idx < 768) {
+      const int ch = idx >> 8, y = (idx >> 3) & 31, x0 = 4 * (idx & 7);
+      float* dst = xin + ch * 34 * 34 + (y + 1) * 34 + 1 + x0;
+#pragma unroll
+      for (int b = 0; b < 4; ++b) dst[b] = norm_px((wd[m] >> (8 * b)) & 255u, ch);
+    }
   }
 }
 // normalised input image [3][34][34] f32 (zero border) from the uint8 CHW image
@@ -313,8 +373,10 @@ __device__ __forceinline__ void stage_input(float* xin, const uint8_t* img) {
 #pragma unroll
   for (int m = 0; m < M; ++m) {
     const int idx = t + NTH * m;
-    wd[m] = idx < 768 ? ((const unsigned*)img)[idx] : 0u;
+    wd[m] = ((const unsigned*)img)[idx < 768 ? idx : 767];
   }
+#pragma unroll
+  for (int m = 0; m < M; ++m) pin(wd[m]);
   for (int idx = t; idx < 3 * 34 * 34; idx += NTH) {
     const int rem = idx % (34 * 34), r = rem / 34, cc = rem % 34;
     if (r == 0 || r == 33 || cc == 0 || cc == 33) xin[idx] = 0.f;
@@ -351,30 +413,52 @@ __global__ void __launch_bounds__(64 * NW) k_pk_step(Ctx cx, PkArgs pa) {
   const int epoch = *pa.epoch;
   const size_t img = (size_t)n * 8192;
   const int B = cx.B;
+  const int sid = pa.ids[n];  // (clamped by the writer)
   PK_STAMP(cx, 0);
 
   // ======================= stem: gather + normalise + conv1 + bias + ReLU + 2x2 max-pool =================
   {
     float* xin = (float*)(U + P::U_XIN);
     unsigned short* swl = (unsigned short*)(U + P::U_SW);
-    float* sb = (float*)(U + P::U_SB);
+    const float* sb = misc + 874;
     float* x0i = (float*)(U + P::U_X0);
-    stage_input<NW>(xin, cx.data + (size_t)sample_id(cx, n) * 3072);
-    if (t < 128) ((uint4*)swl)[t] = ((const uint4*)cx.sw)[t];
-    if (t < 32) {
-      sb[t] = cx.params[OFF_C1B + t];
-      misc[320 + t] = cx.params[OFF_BNW + t];  // BN gamma / beta, constant for the step
-      misc[352 + t] = cx.params[OFF_BNB + t];
-      misc[512 + t] = cx.params[OFF_FC1B + t];  // fc constants for the head
-      if (n == 0) {  // running stats (rank 0's base under DDP, reference CC4 semantics)
-        misc[448 + t] = cx.ws > 1 ? cx.rs_base[t] : cx.rm[t];
-        misc[480 + t] = cx.ws > 1 ? cx.rs_base[32 + t] : cx.rv[t];
-      }
+    // step constants -> misc: k < 64: BN gamma|beta -> misc[320 + k]; k >= 64 -> misc[384 + k]: running
+    // mean|var (rank 0's base under DDP, reference CC4) [448,512), fc1 bias [512,544), W2 [544,864),
+    // b2 [864,874), conv1 bias [874,906).  Every load is issued before any is waited for.
+    constexpr int NKC = 522, KCM = (NKC + NTH - 1) / NTH;
+    float kc[KCM];
+#pragma unroll
+    for (int m = 0; m < KCM; ++m) {
+      const int k = min(t + NTH * m, NKC - 1);
+      const float* rsm = cx.ws > 1 ? cx.rs_base : cx.rm;
+      const float* rsv = cx.ws > 1 ? cx.rs_base + 32 : cx.rv;
+      const float* src = k < 64 ? cx.params + OFF_BNW + k
+                       : k < 96 ? rsm + (k - 64)
+                       : k < 128 ? rsv + (k - 96)
+                       : k < 160 ? cx.params + OFF_FC1B + (k - 128)
+                       : k < 480 ? cx.params + OFF_FC2W + (k - 160)
+                       : k < 490 ? cx.params + OFF_FC2B + (k - 480)
+                                 : cx.params + OFF_C1B + (k - 490);
+      kc[m] = *src;
     }
-    for (int idx = t; idx < 330; idx += NTH) misc[544 + idx] = cx.params[OFF_FC2W + idx];  // W2 [10][32] + b2
+    uint4 swv = ((const uint4*)cx.sw)[t & 127];
+    int lab = cx.labels[sid];
+#pragma unroll
+    for (int m = 0; m < KCM; ++m) pin(kc[m]);
+    pin(swv);
+    pin(lab);
+    stage_input<NW>(xin, cx.data + (size_t)sid * 3072);
+#pragma unroll
+    for (int m = 0; m < KCM; ++m) {
+      const int k = t + NTH * m;
+      if (k < NKC) misc[(k < 64 ? 320 : 384) + k] = kc[m];
+    }
+    if (t < 128) ((uint4*)swl)[t] = swv;
+    if (t == 0) misc[1000] = __int_as_float(lab);  // label for the head's cross-entropy
     stage_wt<NW>(WT, cx.wt_f);
     zero_xr_halo<NW>(XR);
     lds_barrier();
+    PK_STAMP(cx, 29);
     int koff[8];
     bool kval[8];
 #pragma unroll
@@ -384,7 +468,6 @@ __global__ void __launch_bounds__(64 * NW) k_pk_step(Ctx cx, PkArgs pa) {
       koff[s] = kval[s] ? (k / 9) * 34 * 34 + ((k % 9) / 3) * 34 + (k % 3) : 0;
     }
     uint8_t* code_out = cx.SCODE + img;
-    float* X0 = cx.X + img;
 #pragma unroll 1
     for (int j = 0; j < 64 / NW; ++j) {
       const int u = w + NW * j, pr = u >> 2, chalf = (u >> 1) & 1, h = u & 1, co = 16 * h + c;
@@ -392,9 +475,10 @@ __global__ void __launch_bounds__(64 * NW) k_pk_step(Ctx cx, PkArgs pa) {
       const bf16x8 b = *(const bf16x8*)(swl + co * 32 + 8 * q);
       bf16x8 v0, v1;
 #pragma unroll
-      for (int s = 0; s < 8; ++s) {
-        v0[s] = (__bf16)(kval[s] ? xin[koff[s] + base0] : 0.f);
-        v1[s] = (__bf16)(kval[s] ? xin[koff[s] + base0 + 34] : 0.f);
+      for (int s = 0; s < 8; ++s) {  // loads are unconditional (koff = 0 for padded k), the select is not
+        const float e0 = xin[koff[s] + base0], e1 = xin[koff[s] + base0 + 34];
+        v0[s] = (__bf16)(kval[s] ? e0 : 0.f);
+        v1[s] = (__bf16)(kval[s] ? e1 : 0.f);
       }
       const f32x4 a0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(v0, b, z4(), 0, 0, 0);
       const f32x4 a1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(v1, b, z4(), 0, 0, 0);
@@ -411,11 +495,11 @@ __global__ void __launch_bounds__(64 * NW) k_pk_step(Ctx cx, PkArgs pa) {
         if (best > 0.f) code |= 4;
         const int pc = 8 * chalf + 2 * q + pp, po = (pr * 16 + pc) * 32 + co;
         x0i[po] = best;
-        X0[po] = best;
-        code_out[po] = (uint8_t)code;
+        code_out[tl(pr, h, 16 * (pc >> 2) + c) + (pc & 3)] = (uint8_t)code;
         st1r(XR, (pr + 1) * 18 + pc + 1, co, best);
       }
     }
+    PK_STAMP(cx, 30);
     lds_barrier();
   }
   PK_STAMP(cx, 1);
@@ -428,6 +512,10 @@ __global__ void __launch_bounds__(64 * NW) k_pk_step(Ctx cx, PkArgs pa) {
       for (int h = 0; h < 2; ++h)
 #pragma unroll
         for (int i = 0; i < 4; ++i) x[rr][h][i] = x0i[el(r0 + rr, q, c, h, i)];
+#pragma unroll
+    for (int rr = 0; rr < RPW; ++rr)
+#pragma unroll
+      for (int h = 0; h < 2; ++h) st4v(cx.X + img + tl(r0 + rr, h, lane), x[rr][h]);
   }
 
   // ======================= forward: 10 applications of the shared ResBlock =================================
@@ -442,16 +530,16 @@ __global__ void __launch_bounds__(64 * NW) k_pk_step(Ctx cx, PkArgs pa) {
         const int ch = 16 * h + c;
         const float sc = misc[192 + ch], sh = misc[224 + ch];
 #pragma unroll
-        for (int rr = 0; rr < RPW; ++rr)
+        for (int rr = 0; rr < RPW; ++rr) {
 #pragma unroll
           for (int i2 = 0; i2 < 4; ++i2) {
-            const int e = el(r0 + rr, q, c, h, i2), col = 4 * q + i2;
             const float v = fmaxf(y[rr][h][i2] * sc + sh, 0.f) + x[rr][h][i2];
-            Yo[e] = y[rr][h][i2];
             x[rr][h][i2] = v;
-            Xo[e] = v;
-            st1r(XR, (r0 + rr + 1) * 18 + col + 1, ch, v);
+            st1r(XR, (r0 + rr + 1) * 18 + 4 * q + i2 + 1, ch, v);
           }
+          st4v(Yo + tl(r0 + rr, h, lane), y[rr][h]);
+          st4v(Xo + tl(r0 + rr, h, lane), x[rr][h]);
+        }
       }
       lds_barrier();
     }
@@ -466,7 +554,6 @@ __global__ void __launch_bounds__(64 * NW) k_pk_step(Ctx cx, PkArgs pa) {
     PK_STAMP(cx, 2 + i);
   }
   bn_fwd_stats<NW>(cx, pa, epoch, NBLK - 1, y, cred, misc, stat);
-  if (n == 0 && t == 0) *cx.nbt += NBLK;
   if (n == 0 && t < 32) {
     cx.rm[t] = misc[448 + t];
     cx.rv[t] = misc[480 + t];
@@ -476,9 +563,7 @@ __global__ void __launch_bounds__(64 * NW) k_pk_step(Ctx cx, PkArgs pa) {
 #pragma unroll
     for (int rr = 0; rr < RPW; ++rr)
 #pragma unroll
-      for (int h = 0; h < 2; ++h)
-#pragma unroll
-        for (int i2 = 0; i2 < 4; ++i2) Yo[el(r0 + rr, q, c, h, i2)] = y[rr][h][i2];
+      for (int h = 0; h < 2; ++h) st4v(Yo + tl(r0 + rr, h, lane), y[rr][h]);
   }
   PK_STAMP(cx, 12);
 
@@ -520,6 +605,7 @@ __global__ void __launch_bounds__(64 * NW) k_pk_step(Ctx cx, PkArgs pa) {
       cx.HP[(size_t)n * 2048 + ch * 64 + pp] = best;
     }
     lds_barrier();
+    PK_STAMP(cx, 31);
     // fc1: wave w computes rows j = w*NWR .. +NWR-1 (8 KiB of W1 each, streamed, next row prefetched);
     // lane l covers features 4l + 256m (m < 8).
     {
@@ -547,6 +633,7 @@ __global__ void __launch_bounds__(64 * NW) k_pk_step(Ctx cx, PkArgs pa) {
       }
     }
     lds_barrier();
+    PK_STAMP(cx, 32);
     if (t < 32) hv[t] = misc[512 + t] + hp[t];
     lds_barrier();
     if (t < 10) {
@@ -557,7 +644,7 @@ __global__ void __launch_bounds__(64 * NW) k_pk_step(Ctx cx, PkArgs pa) {
     }
     lds_barrier();
     if (t == 0) {
-      const int label = cx.labels[sample_id(cx, n)];
+      const int label = __float_as_int(misc[1000]);
       float mx = hv[64];
       for (int o = 1; o < 10; ++o) mx = fmaxf(mx, hv[64 + o]);
       float se = 0.f;
@@ -580,6 +667,7 @@ __global__ void __launch_bounds__(64 * NW) k_pk_step(Ctx cx, PkArgs pa) {
       if (t < 10) cx.HDL[n * 10 + t] = hv[80 + t];
     }
     lds_barrier();
+    PK_STAMP(cx, 33);
     // dp = W1^T dh: per-wave partials over the wave's rows (rows streamed again), summed in fixed order
     {
       f32x4 d4[8];
@@ -617,9 +705,7 @@ __global__ void __launch_bounds__(64 * NW) k_pk_step(Ctx cx, PkArgs pa) {
 #pragma unroll
       for (int rr = 0; rr < RPW; ++rr)
 #pragma unroll
-        for (int h = 0; h < 2; ++h)
-#pragma unroll
-          for (int i2 = 0; i2 < 4; ++i2) cx.G[img + el(r0 + rr, q, c, h, i2)] = g[rr][h][i2];
+        for (int h = 0; h < 2; ++h) st4v(cx.G + img + tl(r0 + rr, h, lane), g[rr][h]);
     }
     lds_barrier();
   }
@@ -639,17 +725,17 @@ __global__ void __launch_bounds__(64 * NW) k_pk_step(Ctx cx, PkArgs pa) {
 #pragma unroll
     for (int rr = 0; rr < RPW; ++rr)
 #pragma unroll
-      for (int h = 0; h < 2; ++h)
-#pragma unroll
-        for (int i2 = 0; i2 < 4; ++i2) {
-          yb[rr][h][i2] = yp[el(r0 + rr, q, c, h, i2)];
-          xb[rr][h][i2] = xp[el(r0 + rr, q, c, h, i2)];
-        }
+      for (int h = 0; h < 2; ++h) {
+        ld4v(yp + tl(r0 + rr, h, lane), yb[rr][h]);
+        ld4v(xp + tl(r0 + rr, h, lane), xb[rr][h]);
+      }
   }
   f32x4 wacc[Gm::WTL];
 #pragma unroll
   for (int j = 0; j < Gm::WTL; ++j) wacc[j] = z4();
   float dgam = 0.f, dbet = 0.f;
+  unsigned codew[RPW][2];                         // stem-backward prefetch (filled during block 0)
+  unsigned imgw[Gm::IMW];
   lds_barrier();
   const float Ntot = (float)B * 256.f;
 #pragma unroll 1
@@ -701,12 +787,16 @@ __global__ void __launch_bounds__(64 * NW) k_pk_step(Ctx cx, PkArgs pa) {
 #pragma unroll
       for (int rr = 0; rr < RPW; ++rr)
 #pragma unroll
-        for (int h = 0; h < 2; ++h)
+        for (int h = 0; h < 2; ++h) {
+          ld4v(yp + tl(r0 + rr, h, lane), yb[rr][h]);
+          ld4v(xp + tl(r0 + rr, h, lane), xb[rr][h]);
+        }
+    } else {  // last block: prefetch what the stem backward needs (pool codes, raw image words)
 #pragma unroll
-          for (int i2 = 0; i2 < 4; ++i2) {
-            yb[rr][h][i2] = yp[el(r0 + rr, q, c, h, i2)];
-            xb[rr][h][i2] = xp[el(r0 + rr, q, c, h, i2)];
-          }
+      for (int rr = 0; rr < RPW; ++rr)
+#pragma unroll
+        for (int h = 0; h < 2; ++h) codew[rr][h] = *(const unsigned*)(cx.SCODE + img + tl(r0 + rr, h, lane));
+      stage_input_load<NW>(imgw, cx.data + (size_t)sid * 3072);
     }
     if (n == 0 && t < 32) {
       dbet += misc[64 + t];
@@ -722,14 +812,16 @@ __global__ void __launch_bounds__(64 * NW) k_pk_step(Ctx cx, PkArgs pa) {
       for (int rr = 0; rr < RPW; ++rr) {
         const int row = r0 + rr;
         unsigned bits[4];
+        float dyv4[4];
 #pragma unroll
         for (int i2 = 0; i2 < 4; ++i2) {
           const float dyv = k1 * (Ntot * dz[rr][h][i2] - Sa - xh[rr][h][i2] * Sb);
+          dyv4[i2] = dyv;
           const int col = 4 * q + i2;
           st1r(XR, (row + 1) * 18 + col + 1, ch, dyv);
           bits[i2] = bfbits(dyv);
-          if (pa.debug) dyo[el(row, q, c, h, i2)] = dyv;
         }
+        if (pa.debug) st4v(dyo + tl(row, h, lane), dyv4);
         *(uint2*)(dyT + ch * P::DYT_S + row * 16 + 4 * q) = uint2{bits[0] | (bits[1] << 16), bits[2] | (bits[3] << 16)};
       }
     }
@@ -766,16 +858,8 @@ __global__ void __launch_bounds__(64 * NW) k_pk_step(Ctx cx, PkArgs pa) {
 #pragma unroll
       for (int rr = 0; rr < RPW; ++rr)
 #pragma unroll
-        for (int h = 0; h < 2; ++h)
-#pragma unroll
-          for (int i2 = 0; i2 < 4; ++i2) gout[el(r0 + rr, q, c, h, i2)] = g[rr][h][i2];
+        for (int h = 0; h < 2; ++h) st4v(gout + tl(r0 + rr, h, lane), g[rr][h]);
     }
-  }
-  // trunk wgrad slab + BN affine grads
-#pragma unroll
-  for (int j = 0; j < Gm::WTL; ++j) {
-    const int tt = w + NW * j;
-    if (tt < 36) st4(pa.tslab + (size_t)n * WSLAB_N + ((tt * 64 + lane) << 2), wacc[j]);
   }
   if (n == 0 && t < 32) {
     pa.bng[t] = dgam;
@@ -783,20 +867,14 @@ __global__ void __launch_bounds__(64 * NW) k_pk_step(Ctx cx, PkArgs pa) {
   }
 
   // ======================= stem backward: max-pool bwd (saved argmax) -> ReLU mask -> conv1 wgrad ==========
-  __syncthreads();
+  lds_barrier();  // every wave is done with the backward's LDS regions
   {
     unsigned short* dsT = (unsigned short*)(U + P::U_DST);
     float* xin = (float*)(U + P::U_XIN2);
-    uint8_t codes[RPW][2][4];
-#pragma unroll
-    for (int rr = 0; rr < RPW; ++rr)
-#pragma unroll
-      for (int h = 0; h < 2; ++h)
-#pragma unroll
-        for (int i2 = 0; i2 < 4; ++i2) codes[rr][h][i2] = cx.SCODE[img + el(r0 + rr, q, c, h, i2)];
     for (int idx = t; idx < 32 * P::DSP * 2 / 16; idx += NTH) ((uint4*)dsT)[idx] = uint4{0u, 0u, 0u, 0u};
-    stage_input<NW>(xin, cx.data + (size_t)sample_id(cx, n) * 3072);
+    stage_input_store<NW>(xin, imgw);
     lds_barrier();
+    PK_STAMP(cx, 34);
     float db0 = 0.f, db1 = 0.f;
 #pragma unroll
     for (int rr = 0; rr < RPW; ++rr)
@@ -804,7 +882,7 @@ __global__ void __launch_bounds__(64 * NW) k_pk_step(Ctx cx, PkArgs pa) {
       for (int h = 0; h < 2; ++h)
 #pragma unroll
         for (int i2 = 0; i2 < 4; ++i2) {
-          const int code = codes[rr][h][i2];
+          const int code = (codew[rr][h] >> (8 * i2)) & 255u;
           if (code & 4) {
             const int pos = code & 3, col = 4 * q + i2, ch = 16 * h + c;
             const int sr = 2 * (r0 + rr) + (pos >> 1), sc = 2 * col + (pos & 1);
@@ -831,11 +909,15 @@ __global__ void __launch_bounds__(64 * NW) k_pk_step(Ctx cx, PkArgs pa) {
         const bf16x8 a = *(const bf16x8*)(dsT + co * P::DSP + s * 32 + 8 * q);
         bf16x8 b;
 #pragma unroll
-        for (int jj = 0; jj < 8; ++jj) b[jj] = (__bf16)(kv ? xb2[s * 34 + 8 * q + jj] : 0.f);
+        for (int jj = 0; jj < 8; ++jj) {
+          const float e = xb2[s * 34 + 8 * q + jj];  // unconditional load, select after
+          b[jj] = (__bf16)(kv ? e : 0.f);
+        }
         acc2 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, acc2, 0, 0, 0);
       }
       st4(sred + ((combo * 64 + lane) << 2), acc2);  // [16 combos][64 lanes][4]
     }
+    PK_STAMP(cx, 35);
     lds_barrier();
     if (t < 256) {
       const int tile = t >> 6, ln = t & 63;
@@ -845,6 +927,12 @@ __global__ void __launch_bounds__(64 * NW) k_pk_step(Ctx cx, PkArgs pa) {
       st4(ss + ((tile * 64 + ln) << 2), s4);
     }
   }
+  // trunk wgrad slab (accumulated over the 10 applications)
+#pragma unroll
+  for (int j = 0; j < Gm::WTL; ++j) {
+    const int tt = w + NW * j;
+    if (tt < 36) st4(pa.tslab + (size_t)n * WSLAB_N + ((tt * 64 + lane) << 2), wacc[j]);
+  }
   PK_STAMP(cx, 24);
 }
 
@@ -852,6 +940,11 @@ __global__ void __launch_bounds__(64 * NW) k_pk_step(Ctx cx, PkArgs pa) {
 // Reduction + SGD after the persistent step.  Grid: 36 trunk chunks | 5 stem chunks | 32 fc1 column blocks |
 // 1 bookkeeping workgroup (fc2, biases, BN, loss, cursor, epoch).  256 threads.
 // ============================================================================================================
+// Batch ids for the first step after the host moved the cursor or replaced the index list.
+__global__ void __launch_bounds__(64) k_pk_prime_ids(Ctx cx, PkArgs pa) {
+  pa.ids[threadIdx.x] = sample_id(cx, threadIdx.x);
+}
+
 constexpr int R_TRUNK = 36, R_STEM = 5, R_FC = 32, R_GRID = R_TRUNK + R_STEM + R_FC + 1;
 
 __device__ __forceinline__ void sgd_put(const Ctx& cx, int pidx, float gval) {
@@ -950,8 +1043,9 @@ __global__ void __launch_bounds__(256) k_pk_reduce(Ctx cx, PkArgs pa) {
     }
     return;
   }
-  // bookkeeping workgroup: fc1 bias, fc2, BN affine grads, loss, cursor, epoch, CC4 segment
+  // bookkeeping workgroup: fc1 bias, fc2, BN affine grads, loss, cursor, epoch, next batch ids, CC4 segment
   {
+    if (t < 64) pa.ids[t] = sample_id(cx, B + t);  // the next step's batch (cursor advances by B below)
     float* hh_s = stage;             // [B][32]
     float* dl_s = stage + 64 * 32;   // [B][16]
     float* dh_s = dl_s + 64 * 16;    // [B][32]
@@ -988,6 +1082,7 @@ __global__ void __launch_bounds__(256) k_pk_reduce(Ctx cx, PkArgs pa) {
       *cx.loss_acc += (double)(s / (float)B);
       *cx.cursor += B;
       *cx.step_count += 1;
+      *cx.nbt += NBLK;  // BatchNorm num_batches_tracked: +1 per application
       *pa.epoch += 1;
     }
     if (!cx.fuse_sgd && t < 64) {

@@ -226,6 +226,18 @@ class NetResDeepEngine:
         _copy_from_ptr(out, ptr)
         return out
 
+    def activations(self, name: str, count: int, batch: int) -> torch.Tensor:
+        """Per-block activation region (X, Y, DY, G) as NHWC [count, batch, 16, 16, 32].
+
+        The multi-kernel engine stores NHWC directly.  The persistent engine stores the MFMA fragment-tiled layout
+        [row][h][lane = 16q + c][i] holding element (row, col = 4q + i, ch = 16h + c) (netresdeep_persistent.hip: tl).
+        """
+        raw = self.region(name, count * batch * 8192)
+        if not self.cfg.persistent:
+            return raw.view(count, batch, 16, 16, 32)
+        t = raw.view(count, batch, 16, 2, 4, 16, 4)           # [.., row, h, q, c, i]
+        return t.permute(0, 1, 2, 4, 6, 3, 5).reshape(count, batch, 16, 16, 32)  # [.., row, q, i, h, c]
+
     def workspace_bytes(self) -> int:
         return int(self.lib.dca_engine_workspace_bytes(self.h))
 
