@@ -74,6 +74,11 @@ def build(force: bool = False, verbose: bool = False, variant: str = "") -> str:
     return out
 
 
+def build_all(force: bool = False, verbose: bool = False, variants=("",)) -> list:
+    """Build the listed library variants (default: production only); returns their paths."""
+    return [build(force=force, verbose=verbose, variant=v) for v in variants]
+
+
 if __name__ == "__main__":
     for v in (["", "stamps"] if "--all" in sys.argv else [""]):
         print(build(force="--force" in sys.argv, verbose=True, variant=v))

@@ -1,0 +1,188 @@
+"""Generic flat-bucket data parallelism for any ``nn.Module`` (the stock-op path of the framework).
+
+Reference: ``DDP(model, device_ids=[rank], output_device=rank)`` (``main.py:63``), whose implicit behaviour is
+pinned down in SURVEY.md section 2.4:
+  * CC3 -- at construction rank 0's parameters and buffers are broadcast to every rank;
+  * CC4 -- at every forward rank 0's buffers (BN running stats, num_batches_tracked) are broadcast
+    (``broadcast_buffers=True``);
+  * CC5 -- during backward, gradients are averaged over ranks bucket by bucket.
+
+Design (not a copy of the c10d Reducer):
+  * all unique parameters live in ONE flat buffer and all gradients in ONE flat gradient buffer; ``p.data`` /
+    ``p.grad`` are views, so there is no bucket copy-in/copy-out and the SGD update is one fused op over the flat
+    buffer (``FlatSGD``);
+  * the flat layout is REVERSE registration order (approximately gradient-ready order), so every bucket is a
+    contiguous slice that becomes ready as a unit;
+  * a bucket's all-reduce is launched asynchronously from the gradient hook of its last parameter, so it
+    overlaps the rest of the backward (RCCL runs on its own HIP stream); the backward's final callback waits
+    for all buckets;
+  * bucket sizes default to a cap sized for xGMI (``bucket_cap_mb``): big enough that a ring step moves well over
+    64 KB per link, small enough that the first bucket fires early.  With ``first_bucket_mb`` the first (earliest
+    ready) bucket can be made smaller, like DDP's 1 MiB first bucket.
+
+The fused NetResDeep engine (``parallel/ddp.py``) implements the same semantics inside its graph-captured step;
+this wrapper is the path for arbitrary models and for CPU/gloo testing.
+"""
+from __future__ import annotations
+
+from typing import List, Optional
+
+import torch
+import torch.distributed as dist
+import torch.nn as nn
+
+
+def _dist_on(group=None) -> bool:
+    return dist.is_available() and dist.is_initialized() and dist.get_world_size(group) > 1
+
+
+class FlatBucketDDP(nn.Module):
+    def __init__(self, module: nn.Module, bucket_cap_mb: float = 4.0, first_bucket_mb: Optional[float] = 1.0,
+                 broadcast_buffers: bool = True, process_group=None, device_ids=None, output_device=None):
+        super().__init__()
+        self.module = module
+        self.process_group = process_group
+        self.world_size = dist.get_world_size(process_group) if _dist_on(process_group) else 1
+        self.broadcast_buffers = broadcast_buffers
+        params = [p for _, p in module.named_parameters() if p.requires_grad]
+        if not params:
+            raise ValueError("module has no trainable parameters")
+        dev, dtype = params[0].device, params[0].dtype
+        if any(p.device != dev or p.dtype != dtype for p in params):
+            raise ValueError("FlatBucketDDP needs all parameters on one device with one dtype")
+        order = list(reversed(params))  # approximately gradient-ready order
+        total = sum(p.numel() for p in order)
+        self.flat = torch.zeros(total, dtype=dtype, device=dev)
+        self.flat_grad = torch.zeros(total, dtype=dtype, device=dev)
+        self._views = {}
+        off = 0
+        with torch.no_grad():
+            for p in order:
+                n = p.numel()
+                self.flat[off:off + n].copy_(p.detach().reshape(-1))
+                p.data = self.flat[off:off + n].view_as(p)
+                g = self.flat_grad[off:off + n].view_as(p)
+                p.grad = g
+                self._views[p] = (off, n, g)
+                off += n
+        # bucket plan: contiguous slices of the flat buffer
+        esz = self.flat.element_size()
+        cap = max(1, int(bucket_cap_mb * 2 ** 20 / esz))
+        first_cap = max(1, int(first_bucket_mb * 2 ** 20 / esz)) if first_bucket_mb else cap
+        self.buckets: List[tuple] = []  # (start, end, n_params)
+        start, count, limit = 0, 0, first_cap
+        cursor = 0
+        for p in order:
+            n = p.numel()
+            if count and cursor + n - start > limit:
+                self.buckets.append((start, cursor, count))
+                start, count, limit = cursor, 0, cap
+            cursor += n
+            count += 1
+        self.buckets.append((start, cursor, count))
+        self._bucket_of = {}
+        for bi, (s, e, _) in enumerate(self.buckets):
+            for p in order:
+                o = self._views[p][0]
+                if s <= o < e:
+                    self._bucket_of[p] = bi
+        self._pending = [0] * len(self.buckets)
+        self._works: list = []
+        self._callback_queued = False
+        self.bucket_fire_order: List[int] = []  # for tests: order in which buckets were launched
+        self._sync_module_states()  # CC3
+        for p in order:
+            p.register_post_accumulate_grad_hook(self._make_hook(p))
+
+    # ---- collectives ------------------------------------------------------------------------------------------
+    def _sync_module_states(self) -> None:
+        if self.world_size == 1:
+            return
+        with torch.no_grad():
+            dist.broadcast(self.flat, 0, group=self.process_group)
+        self._broadcast_buffers_now()
+
+    def _broadcast_buffers_now(self) -> None:
+        bufs = [b for b in self.module.buffers()]
+        if not bufs or self.world_size == 1:
+            return
+        by_dtype = {}
+        for b in bufs:
+            by_dtype.setdefault(b.dtype, []).append(b)
+        with torch.no_grad():
+            for group in by_dtype.values():  # one coalesced broadcast per dtype
+                flat = torch.cat([b.reshape(-1) for b in group])
+                dist.broadcast(flat, 0, group=self.process_group)
+                o = 0
+                for b in group:
+                    b.copy_(flat[o:o + b.numel()].view_as(b))
+                    o += b.numel()
+
+    def _make_hook(self, p):
+        def hook(param):
+            off, n, view = self._views[p]
+            if param.grad is None or param.grad.data_ptr() != view.data_ptr():
+                # optimizer.zero_grad(set_to_none=True) dropped the view; fold the fresh grad back in
+                if param.grad is not None:
+                    view.copy_(param.grad)
+                param.grad = view
+            if self.world_size == 1:
+                return
+            if not self._callback_queued:
+                torch.autograd.Variable._execution_engine.queue_callback(self._finish_backward)
+                self._callback_queued = True
+            bi = self._bucket_of[p]
+            self._pending[bi] -= 1
+            if self._pending[bi] == 0:
+                s, e, _ = self.buckets[bi]
+                seg = self.flat_grad[s:e]
+                seg.div_(self.world_size)  # average: pre-divide, then sum
+                self._works.append(dist.all_reduce(seg, group=self.process_group, async_op=True))
+                self.bucket_fire_order.append(bi)
+        return hook
+
+    def _finish_backward(self) -> None:
+        for w in self._works:
+            w.wait()
+        if any(self._pending):
+            # parameters that received no gradient this step: reduce their (zero) slices too, in order
+            for bi, left in enumerate(self._pending):
+                if left:
+                    s, e, _ = self.buckets[bi]
+                    seg = self.flat_grad[s:e]
+                    seg.div_(self.world_size)
+                    dist.all_reduce(seg, group=self.process_group)
+        self._works = []
+        self._callback_queued = False
+        self._reset_pending()
+
+    def _reset_pending(self) -> None:
+        self._pending = [b[2] for b in self.buckets]
+
+    # ---- module API -------------------------------------------------------------------------------------------
+    def forward(self, *args, **kwargs):
+        if self.world_size > 1 and self.broadcast_buffers:
+            self._broadcast_buffers_now()  # CC4
+        self._reset_pending()
+        self.bucket_fire_order = []
+        return self.module(*args, **kwargs)
+
+    def zero_grad(self, set_to_none: bool = False) -> None:  # grads stay views of the flat buffer
+        self.flat_grad.zero_()
+
+
+class FlatSGD(torch.optim.Optimizer):
+    """``optim.SGD(lr)`` without momentum/weight decay (reference ``main.py:27``) as ONE op over a flat buffer."""
+
+    def __init__(self, ddp: FlatBucketDDP, lr: float = 1e-2):
+        super().__init__(list(ddp.module.parameters()), dict(lr=lr))
+        self.ddp = ddp
+
+    @torch.no_grad()
+    def step(self, closure=None):
+        loss = closure() if closure is not None else None
+        self.ddp.flat.add_(self.ddp.flat_grad, alpha=-self.param_groups[0]["lr"])
+        return loss
+
+    def zero_grad(self, set_to_none: bool = True) -> None:
+        self.ddp.flat_grad.zero_()

@@ -84,6 +84,15 @@ def bind_flat_parameters(model: nn.Module, device) -> tuple[torch.Tensor, torch.
     return flat, grads
 
 
+def tile_to_nhwc(raw: torch.Tensor, count: int, batch: int) -> torch.Tensor:
+    """Fragment-tiled activations of the persistent engine -> NHWC [count, batch, 16, 16, 32].
+
+    Tiled index of element (row, col = 4q + i, ch = 16h + c): row*512 + h*256 + (16q + c)*4 + i
+    (csrc/netresdeep_persistent.hip: tl)."""
+    t = raw.reshape(count, batch, 16, 2, 4, 16, 4)  # [.., row, h, q, c, i]
+    return t.permute(0, 1, 2, 4, 6, 3, 5).reshape(count, batch, 16, 16, 32)  # [.., row, q, i, h, c]
+
+
 def nccl_unique_id() -> bytes:
     lib = native.require_native()
     buf = ctypes.create_string_buffer(128)
@@ -235,8 +244,7 @@ class NetResDeepEngine:
         raw = self.region(name, count * batch * 8192)
         if not self.cfg.persistent:
             return raw.view(count, batch, 16, 16, 32)
-        t = raw.view(count, batch, 16, 2, 4, 16, 4)           # [.., row, h, q, c, i]
-        return t.permute(0, 1, 2, 4, 6, 3, 5).reshape(count, batch, 16, 16, 32)  # [.., row, q, i, h, c]
+        return tile_to_nhwc(raw, count, batch)
 
     def workspace_bytes(self) -> int:
         return int(self.lib.dca_engine_workspace_bytes(self.h))

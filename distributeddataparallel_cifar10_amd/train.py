@@ -1,0 +1,187 @@
+"""Training application shared by ``main.py`` (DDP) and ``main_no_ddp.py`` (single device).
+
+Reference: ``main.py:26-65`` (``train_loop``, ``main``) and ``main_no_ddp.py:22-63`` (``prepare``,
+``training_loop``).  Defaults reproduce the reference exactly -- SGD(lr=1e-2), CrossEntropyLoss, epochs 1..99,
+per-rank batch 32 with DistributedSampler order (no set_epoch), log + checkpoint at epoch 1 and every 10th epoch,
+the same stdout lines -- while the step itself runs on the MI355X-native path:
+
+* ``engine="fused"`` (default on a GPU, NetResDeep): the whole step (forward, loss, backward, gradient
+  all-reduce over RCCL, SGD, BN running stats) is ONE hipGraph replay of the native engine; the dataset is
+  device-resident; the loss is accumulated on the device and read once per epoch (reference ``loss.item()``
+  every step, SURVEY.md Q9: same printed value, no per-step host sync).
+* ``engine="torch"``: stock PyTorch ops + ``FlatBucketDDP`` (generic path; CPU / gloo; any model).
+
+Options beyond the reference (all off by default): max_steps (per epoch), synthetic data, resume, metrics JSON,
+fault injection (``fail_at_step``), process-group timeout, set_epoch reshuffling, bf16/fp32 engine precision.
+"""
+from __future__ import annotations
+
+import argparse
+import os
+import time
+from dataclasses import dataclass, field
+from typing import Optional
+
+import torch
+import torch.nn as nn
+
+from .data.cifar import load_cifar10
+from .data.loader import DeviceLoader
+from .data.synthetic import synthetic_cifar
+from .utils.checkpoint import CHECKPOINT_NAME, load_checkpoint, save_checkpoint, unwrap
+from .utils.metrics import MetricsLog, epoch_line, should_log, time_line
+
+
+@dataclass
+class TrainConfig:
+    epochs: int = 99                 # range(1, 100) (reference main.py:30)
+    lr: float = 1e-2                 # reference main.py:27
+    batch_size: int = 32             # reference main.py:61 (main_no_ddp.py:31 hard-codes 64)
+    data_path: str = "data/CIFAR-10/"
+    synthetic: int = 0               # >0: use N synthetic CIFAR-shaped samples instead of the dataset
+    engine: str = "auto"             # auto | fused | torch
+    dtype: str = "bf16"              # fused engine compute precision (bf16 MFMA or exact fp32 MFMA)
+    max_steps: Optional[int] = None  # per-epoch step cap (smoke tests / benchmarking)
+    checkpoint: bool = True
+    checkpoint_path: Optional[str] = None
+    resume: Optional[str] = None
+    metrics_json: Optional[str] = None
+    seed: int = 0
+    set_epoch: bool = False
+    fail_at_step: Optional[int] = None
+    backend: str = "nccl"
+    port: Optional[int] = None
+    timeout_s: Optional[float] = None
+    extra: dict = field(default_factory=dict)
+
+
+def add_cli_args(ap: argparse.ArgumentParser, batch_default: int = 32) -> argparse.ArgumentParser:
+    ap.add_argument("--epochs", type=int, default=99)
+    ap.add_argument("--max-steps", type=int, default=None, help="cap on steps per epoch")
+    ap.add_argument("--batch-size", type=int, default=batch_default)
+    ap.add_argument("--lr", type=float, default=1e-2)
+    ap.add_argument("--data-root", default=None)
+    ap.add_argument("--synthetic", type=int, nargs="?", const=50000, default=0,
+                    help="train on N synthetic CIFAR-shaped samples (default 50000)")
+    ap.add_argument("--engine", default="auto", choices=["auto", "fused", "torch"])
+    ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
+    ap.add_argument("--no-checkpoint", action="store_true")
+    ap.add_argument("--checkpoint-path", default=None)
+    ap.add_argument("--resume", default=None)
+    ap.add_argument("--metrics-json", default=None)
+    ap.add_argument("--seed", type=int, default=0)
+    ap.add_argument("--set-epoch", action="store_true", help="reshuffle every epoch (reference never does)")
+    ap.add_argument("--fail-at-step", type=int, default=None, help="fault injection: raise on this global step")
+    ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"])
+    ap.add_argument("--world-size", type=int, default=None, help="number of ranks (default: GPU count)")
+    ap.add_argument("--port", type=int, default=None)
+    ap.add_argument("--timeout", type=float, default=None, help="process-group timeout in seconds")
+    return ap
+
+
+def config_from_args(a: argparse.Namespace, data_path_default: str) -> TrainConfig:
+    return TrainConfig(epochs=a.epochs, lr=a.lr, batch_size=a.batch_size, data_path=a.data_root or data_path_default,
+                       synthetic=a.synthetic or 0, engine=a.engine, dtype=a.dtype, max_steps=a.max_steps,
+                       checkpoint=not a.no_checkpoint, checkpoint_path=a.checkpoint_path, resume=a.resume,
+                       metrics_json=a.metrics_json, seed=a.seed, set_epoch=a.set_epoch, fail_at_step=a.fail_at_step,
+                       backend=a.backend, port=a.port, timeout_s=a.timeout)
+
+
+def load_dataset(cfg: TrainConfig):
+    if cfg.synthetic:
+        return synthetic_cifar(cfg.synthetic, seed=cfg.seed)
+    return load_cifar10(cfg.data_path, train=True)
+
+
+def resolve_engine(cfg: TrainConfig, device: torch.device, model: nn.Module) -> str:
+    if cfg.engine != "auto":
+        return cfg.engine
+    is_netresdeep = getattr(model, "n_chans1", None) == 32 and getattr(model, "n_blocks", None) == 10
+    return "fused" if device.type == "cuda" and is_netresdeep else "torch"
+
+
+class _Fault(RuntimeError):
+    pass
+
+
+def train_loop(model, train_loader: DeviceLoader, rank: int, cfg: Optional[TrainConfig] = None,
+               optimizer=None) -> dict:
+    """Reference ``main.py:26-49`` / ``main_no_ddp.py:36-59``.  `model` is a ``FusedDDPTrainer`` (engine path),
+    a ``FlatBucketDDP`` or a plain module (torch path).  Returns a summary dict."""
+    from .parallel.ddp import FusedDDPTrainer
+    cfg = cfg or TrainConfig()
+    mlog = MetricsLog(cfg.metrics_json, rank)
+    ckpt = cfg.checkpoint_path or os.path.join(cfg.data_path, CHECKPOINT_NAME)
+    fused = isinstance(model, FusedDDPTrainer)
+    n_batches = len(train_loader)
+    steps_per_epoch = min(n_batches, cfg.max_steps) if cfg.max_steps else n_batches
+    start_epoch = int(cfg.extra.get("start_epoch", 1))
+    global_step = int(cfg.extra.get("start_step", 0))
+    history = []
+    if not fused:
+        loss_fn = nn.CrossEntropyLoss()
+        if optimizer is None:
+            from .parallel.flat_ddp import FlatBucketDDP, FlatSGD
+            optimizer = FlatSGD(model, cfg.lr) if isinstance(model, FlatBucketDDP) else \
+                torch.optim.SGD(model.parameters(), lr=cfg.lr)
+    start_time = time.time()
+    for epoch in range(start_epoch, cfg.epochs + 1):
+        train_loader.set_epoch(epoch)
+        t0 = time.perf_counter()
+        if fused:
+            idx = train_loader.indices()[:steps_per_epoch * train_loader.batch_size]
+            if cfg.fail_at_step is not None and global_step < cfg.fail_at_step <= global_step + steps_per_epoch:
+                raise _Fault(f"injected failure at step {cfg.fail_at_step} (rank {rank})")
+            loss_sum, nsteps = model.engine.run_epoch(idx, train_loader.batch_size)
+        else:
+            loss_sum, nsteps = 0.0, 0
+            for imgs, labels in train_loader:
+                if nsteps >= steps_per_epoch:
+                    break
+                if cfg.fail_at_step is not None and global_step + nsteps + 1 == cfg.fail_at_step:
+                    raise _Fault(f"injected failure at step {cfg.fail_at_step} (rank {rank})")
+                outputs = model(imgs)
+                loss = loss_fn(outputs, labels)
+                optimizer.zero_grad()
+                loss.backward()
+                optimizer.step()
+                loss_sum += loss.item()
+                nsteps += 1
+        global_step += nsteps
+        dt = time.perf_counter() - t0
+        mean = loss_sum / n_batches  # reference divides by len(train_loader) (main.py:44)
+        history.append(mean)
+        mlog.write(epoch=epoch, loss=mean, steps=nsteps, seconds=dt,
+                   images_per_sec=nsteps * train_loader.batch_size / max(dt, 1e-9))
+        if should_log(epoch):
+            print(epoch_line(epoch, mean), flush=True)
+            if cfg.checkpoint:
+                save_checkpoint(model, ckpt, rank, meta={"epoch": epoch, "step": global_step})
+    total = time.time() - start_time
+    print(time_line(total), flush=True)
+    return {"losses": history, "seconds": total, "steps": global_step}
+
+
+def build_model_for_rank(cfg: TrainConfig, rank: int, world_size: int, device: torch.device, data, labels,
+                         loader: DeviceLoader):
+    """NetResDeep wrapped for data parallelism on `device` (fused engine or FlatBucketDDP)."""
+    from .models.netresdeep import NetResDeep
+    from .parallel.ddp import FusedDDPTrainer
+    from .parallel.flat_ddp import FlatBucketDDP
+    model = NetResDeep().to(device)
+    meta = None
+    if cfg.resume:
+        meta = load_checkpoint(model, cfg.resume, strict=True, map_location=device)
+        if meta:
+            cfg.extra["start_epoch"] = int(meta.get("epoch", 0)) + 1
+            cfg.extra["start_step"] = int(meta.get("step", 0))
+    kind = resolve_engine(cfg, device, model)
+    if kind == "fused":
+        n_idx = len(loader) * loader.batch_size
+        return FusedDDPTrainer(model, loader.data, loader.labels, batch_max=loader.batch_size, lr=cfg.lr,
+                               dtype=cfg.dtype, max_indices=max(n_idx, loader.batch_size))
+    return FlatBucketDDP(model)
+
+
+def unwrap_model(model) -> nn.Module:
+    return unwrap(model)

@@ -1,0 +1,139 @@
+"""FlatBucketDDP semantics on CPU with gloo, world_size 2 (SURVEY.md section 4 layer 3).
+
+Checks CC3 (init broadcast), CC4 (rank-0 buffers at every forward), CC5 (averaged gradients, bucket-wise,
+first bucket launched before the backward ends) and end-to-end equivalence with torch's own DDP.
+"""
+import copy
+import os
+import traceback
+
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+import torch.nn.functional as F
+
+from distributeddataparallel_cifar10_amd.models.netresdeep import NetResDeep
+from distributeddataparallel_cifar10_amd.parallel.flat_ddp import FlatBucketDDP, FlatSGD
+
+WS = 2
+
+
+def _worker(rank, ws, port, fn, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    torch.set_num_threads(2)
+    dist.init_process_group("gloo", rank=rank, world_size=ws)
+    try:
+        fn(rank, ws)
+        q.put((rank, None))
+    except Exception:
+        q.put((rank, traceback.format_exc()))
+    finally:
+        dist.destroy_process_group()
+
+
+def _spawn(fn, port, ws=WS):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_worker, args=(r, ws, port, fn, q)) for r in range(ws)]
+    for p in procs:
+        p.start()
+    errs = [q.get(timeout=300) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+    bad = [e for e in errs if e[1]]
+    assert not bad, "\n".join(f"rank {r}:\n{e}" for r, e in bad)
+
+
+def _batch(rank, step, n=8):
+    g = torch.Generator().manual_seed(1000 * step + rank)
+    return torch.randn(n, 3, 32, 32, generator=g), torch.randint(0, 10, (n,), generator=g)
+
+
+def _case_init_broadcast_and_grad_average(rank, ws):
+    torch.manual_seed(100 + rank)  # different init per rank; CC3 must make them equal
+    m = NetResDeep()
+    ddp = FlatBucketDDP(m, bucket_cap_mb=0.1, first_bucket_mb=0.05)
+    assert len(ddp.buckets) >= 2
+    # CC3: everyone now holds rank 0's parameters
+    ref = [p.detach().clone() for p in m.parameters()]
+    for t in ref:
+        ts = [torch.empty_like(t) for _ in range(ws)]
+        dist.all_gather(ts, t)
+        assert all(torch.equal(ts[0], x) for x in ts)
+    # CC5: averaged gradients equal the mean of per-rank local gradients
+    local = copy.deepcopy(m)
+    x, y = _batch(rank, 0)
+    F.cross_entropy(local(x), y).backward()
+    F.cross_entropy(ddp(x), y).backward()
+    for (n, p), lp in zip(m.named_parameters(), local.parameters()):
+        g = lp.grad.clone()
+        dist.all_reduce(g)
+        g /= ws
+        assert torch.allclose(p.grad, g, atol=1e-6, rtol=1e-5), n
+    # buckets fire in gradient-ready order, the fc bucket first (before conv1's grad exists)
+    assert ddp.bucket_fire_order[0] == 0 and sorted(ddp.bucket_fire_order) == list(range(len(ddp.buckets)))
+
+
+def _case_buffer_broadcast_every_forward(rank, ws):
+    torch.manual_seed(7)
+    m = NetResDeep()
+    ddp = FlatBucketDDP(m)
+    bn = m.resblocks[0].batch_norm
+    with torch.no_grad():
+        bn.running_mean.fill_(float(rank + 1))  # ranks diverge between forwards
+    expected = copy.deepcopy(m)
+    with torch.no_grad():
+        expected.resblocks[0].batch_norm.running_mean.fill_(1.0)  # rank 0's buffer wins (CC4)
+    x, _ = _batch(rank, 1)
+    with torch.no_grad():
+        ddp(x)
+        expected(x)  # then 10 local EMA updates on this rank's batch
+    assert torch.allclose(bn.running_mean, expected.resblocks[0].batch_norm.running_mean, atol=1e-6)
+    assert int(bn.num_batches_tracked) == 10
+
+
+def _case_matches_torch_ddp(rank, ws):
+    torch.manual_seed(3)
+    base = NetResDeep()
+    a = copy.deepcopy(base)
+    b = copy.deepcopy(base)
+    ours = FlatBucketDDP(a, bucket_cap_mb=0.1)
+    opt_a = FlatSGD(ours, lr=1e-2)
+    theirs = torch.nn.parallel.DistributedDataParallel(b)
+    opt_b = torch.optim.SGD(b.parameters(), lr=1e-2)
+    for step in range(3):
+        x, y = _batch(rank, step)
+        for model, opt in ((ours, opt_a), (theirs, opt_b)):
+            loss = F.cross_entropy(model(x), y)
+            opt.zero_grad()
+            loss.backward()
+            opt.step()
+    for (n, pa), pb in zip(a.named_parameters(), b.parameters()):
+        assert torch.allclose(pa, pb, atol=1e-5, rtol=1e-4), n
+    sa, sb = a.state_dict(), b.state_dict()
+    for k in sa:
+        if sa[k].dtype.is_floating_point:
+            assert torch.allclose(sa[k], sb[k], atol=1e-5, rtol=1e-4), k
+        else:
+            assert torch.equal(sa[k], sb[k]), k
+
+
+@pytest.mark.parametrize("case", [_case_init_broadcast_and_grad_average, _case_buffer_broadcast_every_forward,
+                                  _case_matches_torch_ddp])
+def test_flat_ddp_gloo(case, port):
+    _spawn(case, port)
+
+
+def test_flat_ddp_single_process_zero_grad_none():
+    m = NetResDeep()
+    ddp = FlatBucketDDP(m)
+    opt = torch.optim.SGD(m.parameters(), lr=0.1)
+    x, y = _batch(0, 0)
+    F.cross_entropy(ddp(x), y).backward()
+    g1 = ddp.flat_grad.clone()
+    opt.zero_grad(set_to_none=True)  # drops the views; the hook must fold grads back in
+    F.cross_entropy(ddp(x), y).backward()
+    assert all(p.grad.data_ptr() >= ddp.flat_grad.data_ptr() for p in m.parameters())
+    assert torch.allclose(ddp.flat_grad, g1, atol=1e-6)
