@@ -65,6 +65,8 @@ struct DcaInit {
   int persistent;       // 1: one-launch persistent trunk kernel (bf16 only)
   int debug;            // persistent engine: also store DY / G for diagnostics
   int pk_waves;         // persistent engine: waves per workgroup (8 or 4; 0 = default 8)
+  int comm_mode;        // world_size > 1: 0 = RCCL inside the step; 1 = external (host drives the all-reduce
+                        // between dca_engine_run_part(.., 1) and (.., 2); test/debug path, no RCCL communicator)
 };
 
 }  // extern "C"
@@ -205,27 +207,36 @@ static int set_lds_limits(Engine* e) {
 }
 
 // Persistent path: one launch for the whole trunk, one for reduction + SGD.
-static int enqueue_step_persistent(Engine* e, int B) {
+// `part`: 0 = the whole step; 1 = compute up to (not including) the gradient all-reduce; 2 = what follows it
+// (averaging SGD + CC4 base).  Parts 1/2 exist for comm_mode 1, where the host runs the all-reduce in between.
+static int enqueue_step_persistent(Engine* e, int B, int part) {
   Ctx cx = e->base;
   cx.B = B;
-  if (e->pk_waves == 4)
-    hipLaunchKernelGGL(pk::k_pk_step<4>, dim3(B), dim3(64 * 4), pk::Plan::TOTAL, e->st, cx, e->pa);
-  else
-    hipLaunchKernelGGL(pk::k_pk_step<8>, dim3(B), dim3(64 * 8), pk::Plan::TOTAL, e->st, cx, e->pa);
-  hipLaunchKernelGGL(pk::k_pk_reduce, dim3(pk::R_GRID), dim3(256), 0, e->st, cx, e->pa);
+  if (part != 2) {
+    if (e->pk_waves == 4)
+      hipLaunchKernelGGL(pk::k_pk_step<4>, dim3(B), dim3(64 * 4), pk::Plan::TOTAL, e->st, cx, e->pa);
+    else
+      hipLaunchKernelGGL(pk::k_pk_step<8>, dim3(B), dim3(64 * 8), pk::Plan::TOTAL, e->st, cx, e->pa);
+    hipLaunchKernelGGL(pk::k_pk_reduce, dim3(pk::R_GRID), dim3(256), 0, e->st, cx, e->pa);
+  }
   if (e->in.world_size > 1) {
-    NCCK(ncclAllReduce(cx.grads, cx.grads, FLAT_N, ncclFloat32, ncclSum, e->comm, e->st));
-    hipLaunchKernelGGL(e->kapply, dim3(64), dim3(NT), 0, e->st, cx, 1);
+    if (part == 0) NCCK(ncclAllReduce(cx.grads, cx.grads, FLAT_N, ncclFloat32, ncclSum, e->comm, e->st));
+    if (part != 1) hipLaunchKernelGGL(e->kapply, dim3(64), dim3(NT), 0, e->st, cx, 1);
   }
   HIPCK(hipGetLastError());
   return 0;
 }
 
 // Enqueue one full training step for batch B on e->st (and e->cst for the collectives).
-static int enqueue_step(Engine* e, int B) {
-  if (e->persistent) return enqueue_step_persistent(e, B);
+static int enqueue_step(Engine* e, int B, int part = 0) {
+  if (e->persistent) return enqueue_step_persistent(e, B, part);
   Ctx cx = e->base;
   cx.B = B;
+  if (part == 2) {  // external all-reduce done: averaging SGD + CC4 base
+    hipLaunchKernelGGL(e->kapply, dim3(64), dim3(NT), 0, e->st, cx, 1);
+    HIPCK(hipGetLastError());
+    return 0;
+  }
   const int nparts = B * e->TPI, nw = B * (16 / e->RW);
   const int nslab = 9 * nw + nparts;
   const dim3 blk(NT);
@@ -238,7 +249,7 @@ static int enqueue_step(Engine* e, int B) {
     size_t lds = (i == 0) ? e->s_dgrad0 : e->s_dgrad;
     lds = std::max(lds, (i < NBLK - 1) ? e->s_wgrad : e->s_fc);
     hipLaunchKernelGGL(e->kbwd, dim3(nparts + extra), blk, lds, e->st, cx, i);
-    if (i == NBLK - 1 && e->in.world_size > 1) {  // bucket A ready: overlap its all-reduce with the trunk bwd
+    if (i == NBLK - 1 && e->in.world_size > 1 && part == 0) {  // bucket A ready: overlap its all-reduce with the trunk bwd
       HIPCK(hipEventRecord(e->evA, e->st));
       HIPCK(hipStreamWaitEvent(e->cst, e->evA, 0));
       NCCK(ncclAllReduce(cx.grads, cx.grads, BUCKET_A_END, ncclFloat32, ncclSum, e->comm, e->cst));
@@ -246,7 +257,7 @@ static int enqueue_step(Engine* e, int B) {
   }
   const int nother = cx.fuse_sgd ? 64 : 0;
   hipLaunchKernelGGL(e->kred, dim3(N_TRUNK_RED_WG + N_STEM_RED_WG + nother + 1), blk, 0, e->st, cx, nslab, nparts);
-  if (e->in.world_size > 1) {
+  if (e->in.world_size > 1 && part == 0) {
     HIPCK(hipEventRecord(e->evB, e->st));
     HIPCK(hipStreamWaitEvent(e->cst, e->evB, 0));
     NCCK(ncclAllReduce(cx.grads + OFF_CONVW, cx.grads + OFF_CONVW, FLAT_N - OFF_CONVW, ncclFloat32, ncclSum, e->comm,
@@ -414,7 +425,7 @@ extern "C" {
 
 const char* dca_last_error() { return g_err.c_str(); }
 
-int dca_abi_version() { return 1; }
+int dca_abi_version() { return 2; }  // bump with every DcaInit / signature change
 
 int dca_nccl_unique_id(char* out128) {
   ncclUniqueId id;
@@ -482,7 +493,7 @@ int dca_engine_create(const DcaInit* in, int n_indices, void** out) {
   c.indices = e->indices;
   c.n_data = in->n_data;
   c.n_idx = std::max(n_indices, 1);
-  if (in->world_size > 1) {
+  if (in->world_size > 1 && in->comm_mode == 0) {
     ncclUniqueId id;
     memcpy(&id, in->nccl_id, 128);
     NCCK(ncclCommInitRank(&e->comm, in->world_size, id, in->rank));
@@ -579,6 +590,10 @@ int dca_engine_run(void* h, int B, int nsteps, int use_graph) {
     g_err = "batch out of range";
     return -1;
   }
+  if (e->in.world_size > 1 && e->in.comm_mode != 0) {
+    g_err = "comm_mode 1 (external all-reduce): drive steps with dca_engine_run_part";
+    return -1;
+  }
   if (!use_graph) {
     for (int s = 0; s < nsteps; ++s)
       if (dca::enqueue_step(e, B)) return -1;
@@ -602,6 +617,16 @@ int dca_engine_run(void* h, int B, int nsteps, int use_graph) {
   }
   for (int s = 0; s < nsteps; ++s) HIPCK(hipGraphLaunch(it->second, e->st));
   return 0;
+}
+
+// comm_mode 1: one part of a step, eager (see enqueue_step_persistent)
+int dca_engine_run_part(void* h, int B, int part) {
+  Engine* e = (Engine*)h;
+  if (B < 1 || B > e->in.bmax || part < 1 || part > 2 || e->in.world_size < 2 || e->in.comm_mode != 1) {
+    g_err = "run_part: needs world_size > 1, comm_mode 1, part 1 or 2, batch in range";
+    return -1;
+  }
+  return dca::enqueue_step(e, B, part);
 }
 
 int dca_engine_sync(void* h) {

@@ -62,6 +62,7 @@ class _DcaInit(ctypes.Structure):
         ("persistent", ctypes.c_int),
         ("debug", ctypes.c_int),
         ("pk_waves", ctypes.c_int),
+        ("comm_mode", ctypes.c_int),
     ]
 
 
@@ -111,6 +112,8 @@ class EngineConfig:
     pk_waves: int = 8            # persistent engine: waves per workgroup (8: 2 image rows per wave; or 4)
     world_size: int = 1
     rank: int = 0
+    comm: str = "rccl"           # world_size > 1: "rccl" (all-reduce inside the graph-captured step) or
+                                 # "external" (host all-reduce between step parts; tests / any torch backend)
     bn_momentum: float = 0.1
     bn_eps: float = 1e-5
 
@@ -157,6 +160,7 @@ class NetResDeepEngine:
             bn_mom=float(cfg.bn_momentum), bn_eps=float(cfg.bn_eps), world_size=int(cfg.world_size),
             rank=int(cfg.rank), nccl_id=ctypes.cast(self._nccl_id, ctypes.c_char_p),
             persistent=1 if cfg.persistent else 0, debug=1 if cfg.debug else 0, pk_waves=int(cfg.pk_waves),
+            comm_mode=1 if cfg.comm == "external" else 0,
         )
         self._init = init
         self.max_indices = int(max_indices or self.data.shape[0])
@@ -192,6 +196,21 @@ class NetResDeepEngine:
     def run(self, batch: int, steps: int = 1, graph: bool = True) -> None:
         """Enqueue `steps` training steps of `batch` images each (asynchronous)."""
         native.check(self.lib.dca_engine_run(self.h, int(batch), int(steps), 1 if graph else 0), "dca_engine_run")
+
+    def run_external(self, batch: int, steps: int, allreduce) -> None:
+        """comm="external": `steps` steps whose gradient all-reduce is done by the host.  `allreduce(t)` must sum
+        the fp32 device tensor `t` (the flat gradient buffer incl. the CC4 running-stat segment) over ranks in
+        place, e.g. ``torch.distributed.all_reduce`` on any backend.  Synchronous, eager (no graph)."""
+        if self.cfg.comm != "external" or self.cfg.world_size < 2:
+            raise RuntimeError("run_external needs EngineConfig(comm='external', world_size > 1)")
+        seg = self.grads[:FLAT_N]
+        for _ in range(steps):
+            native.check(self.lib.dca_engine_run_part(self.h, int(batch), 1), "run_part(1)")
+            self.sync()
+            allreduce(seg)
+            torch.cuda.synchronize(self.device)
+            native.check(self.lib.dca_engine_run_part(self.h, int(batch), 2), "run_part(2)")
+        self.sync()
 
     def check_errors(self, reset: bool = True) -> None:
         """Raise if a persistent-kernel BN exchange timed out (a workgroup was not co-resident)."""

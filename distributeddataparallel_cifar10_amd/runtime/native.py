@@ -16,6 +16,7 @@ import torch  # noqa: F401  (must be imported before the native library, see mod
 
 from .. import build as _build
 
+ABI_VERSION = 2  # csrc/engine.hip dca_abi_version(): DcaInit layout / C signatures
 _lock = threading.Lock()
 _lib = None
 
@@ -36,6 +37,7 @@ def _declare(lib):
     lib.dca_engine_set_cursor.argtypes = [c_void_p, c_int]
     lib.dca_engine_read_loss.argtypes = [c_void_p, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(c_int), c_int]
     lib.dca_engine_run.argtypes = [c_void_p, c_int, c_int, c_int]
+    lib.dca_engine_run_part.argtypes = [c_void_p, c_int, c_int]
     lib.dca_engine_sync.argtypes = [c_void_p]
     lib.dca_engine_stream.argtypes = [c_void_p]
     lib.dca_engine_stream.restype = c_void_p
@@ -79,6 +81,9 @@ def load(build_if_missing: bool = True):
         except OSError as exc:
             raise NativeUnavailable(f"cannot load {path}: {exc}") from exc
         _lib = _declare(lib)
+        if _lib.dca_abi_version() != ABI_VERSION:
+            _lib = None
+            raise NativeUnavailable(f"{path}: ABI {lib.dca_abi_version()} != expected {ABI_VERSION} (stale build?)")
         return _lib
 
 

@@ -1,0 +1,109 @@
+"""Data-parallel semantics of the native engine with 2 ranks sharing one MI355X (gloo carries the all-reduce:
+RCCL refuses two ranks on one device, so the engine's comm="external" mode lets the host all-reduce the flat
+gradient buffer between the two halves of each step).
+
+Checks against a single-process simulation of reference DDP: CC3 init broadcast, CC5 averaged
+gradients + SGD, CC4 rank-0 BN buffers at each forward followed by 10 local EMA updates.  Everything except the
+RCCL call itself (one ncclAllReduce over the same buffer) is exercised.
+"""
+import copy
+import os
+import traceback
+
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+pytestmark = pytest.mark.gpu
+WS, B, STEPS, NDATA = 2, 16, 3, 256
+
+
+def _simulate(model0, data, labels, order, lr, bf16):
+    from distributeddataparallel_cifar10_amd.utils.oracle import reference_step
+    models = [copy.deepcopy(model0) for _ in range(WS)]
+    for s in range(STEPS):
+        snap = {k: v.clone() for k, v in models[0].named_buffers()}
+        grads = []
+        for r in range(WS):
+            with torch.no_grad():
+                for k, v in models[r].named_buffers():
+                    v.copy_(snap[k])
+            sel = order[r][s * B:(s + 1) * B]
+            out = reference_step(models[r], data[sel], labels[sel], lr=lr, apply_sgd=False, bf16_operands=bf16)
+            grads.append(out["grads"])
+        with torch.no_grad():
+            for r in range(WS):
+                for n, p in models[r].named_parameters():
+                    p -= lr * sum(g[n] for g in grads) / WS
+    return models
+
+
+def _worker(rank, port, dtype, persistent, q):
+    try:
+        os.environ["MASTER_ADDR"] = "127.0.0.1"
+        os.environ["MASTER_PORT"] = str(port)
+        dist.init_process_group("gloo", rank=rank, world_size=WS)
+        from distributeddataparallel_cifar10_amd.data.sampler import distributed_indices
+        from distributeddataparallel_cifar10_amd.data.synthetic import synthetic_cifar
+        from distributeddataparallel_cifar10_amd.models.netresdeep import NetResDeep
+        from distributeddataparallel_cifar10_amd.parallel.ddp import broadcast_module_state
+        from distributeddataparallel_cifar10_amd.runtime.engine import EngineConfig, NetResDeepEngine
+        dev = torch.device("cuda", 0)
+        data, labels = synthetic_cifar(NDATA, seed=5)
+        order = [distributed_indices(NDATA, WS, r) for r in range(WS)]
+        torch.manual_seed(100 + rank)  # different init per rank; CC3 fixes it
+        model = NetResDeep()
+        broadcast_module_state(model, 0)  # CC3 (gloo, CPU tensors)
+        ref0 = copy.deepcopy(model)
+        model = model.to(dev)
+        eng = NetResDeepEngine(model, data.to(dev), labels.to(dev),
+                               EngineConfig(batch_max=32, dtype=dtype, persistent=persistent, world_size=WS,
+                                            rank=rank, comm="external"))
+        eng.set_indices(order[rank])
+        eng.set_cursor(0)
+        eng.read_loss(reset=True)
+
+        def allreduce(t):
+            h = t.cpu()
+            dist.all_reduce(h)
+            t.copy_(h.to(t.device))
+
+        eng.run_external(B, STEPS, allreduce)
+        loss, steps = eng.read_loss()
+        assert steps == STEPS
+        sim = _simulate(ref0, data, labels, order, 1e-2, dtype == "bf16")[rank]
+        tol = 1e-3 if dtype == "fp32" else 3e-2
+        sd, rsd = model.state_dict(), sim.state_dict()
+        for k in ("fc1.weight", "fc2.bias", "resblocks.0.conv.weight", "resblocks.0.batch_norm.weight",
+                  "conv1.weight", "resblocks.0.batch_norm.running_mean", "resblocks.0.batch_norm.running_var"):
+            a, b = sd[k].detach().double().cpu(), rsd[k].detach().double()
+            err = ((a - b).norm() / b.norm()).item()
+            assert err < tol, (k, err)
+        assert int(sd["resblocks.0.batch_norm.num_batches_tracked"]) == 10 * STEPS
+        # every rank ends with identical parameters
+        flat = torch.cat([p.detach().reshape(-1).cpu() for p in model.parameters()])
+        other = flat.clone()
+        dist.broadcast(other, 0)
+        assert torch.equal(flat, other)
+        eng.close()
+        q.put((rank, None))
+    except Exception:
+        q.put((rank, traceback.format_exc()))
+    finally:
+        if dist.is_initialized():
+            dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("dtype,persistent", [("bf16", True), ("fp32", False), ("bf16", False)])
+def test_engine_ddp_two_ranks_one_gpu(gpu, port, dtype, persistent):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_worker, args=(r, port, dtype, persistent, q)) for r in range(WS)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=600) for _ in procs]
+    for p in procs:
+        p.join(timeout=120)
+    bad = [r for r in res if r[1]]
+    assert not bad, "\n".join(f"rank {r}:\n{e}" for r, e in bad)
