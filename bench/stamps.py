@@ -41,7 +41,8 @@ def microbench(lib):
 
 # persistent-kernel stamp ids (netresdeep_persistent.hip PK_STAMP): 0 start, 1 stem end, 2+i fwd block i conv end,
 # 12 bn9 stats, 13 head end, 14+k bwd block 9-k end, 24 kernel end, 25/26 and 27/28 around the block-5 exchanges,
-# 29 stem staged, 30 stem MFMA done, 31 head pooled, 32 fc1 done, 33 CE done, 34 stem-bwd staged, 35 stem-bwd MFMA
+# 29 stem staged, 30 stem MFMA done, 31 head pooled, 32 fc1 done, 33 CE done, 34 stem-bwd staged, 35 stem-bwd MFMA,
+# block detail: 36 bwd5 published, 38 bwd5 wgrad(6) done, 37 bwd5 dy staged, 39 fwd6 apply done
 PK_INTERVALS = ([("stem", 0, 1), ("stem.stage", 0, 29), ("stem.mfma", 29, 30), ("stem.tail", 30, 1)] +
                 [(f"fwd{i}", 1 + i, 2 + i) for i in range(10)] +
                 [("bn9+head_start", 11, 12), ("head", 12, 13), ("head.pool", 12, 31), ("head.fc1", 31, 32),
@@ -49,7 +50,9 @@ PK_INTERVALS = ([("stem", 0, 1), ("stem.stage", 0, 29), ("stem.mfma", 29, 30), (
                 [(f"bwd{9 - k}", 13 + k, 14 + k) for k in range(10)] +
                 [("stem_bwd", 23, 24), ("stem_bwd.stage", 23, 34), ("stem_bwd.mfma", 34, 35),
                  ("stem_bwd.tail", 35, 24),
-                 ("fwd5_pre_xchg", 6, 25), ("fwd5_xchg", 25, 26), ("bwd5_pre_xchg", 18, 27), ("bwd5_xchg", 27, 28)])
+                 ("fwd5_pre_xchg", 7, 25), ("fwd5_xchg", 25, 26), ("fwd6_apply", 26, 39), ("fwd6_conv", 39, 8),
+                 ("bwd5.dz+csum+pub", 17, 36), ("bwd5.wgrad6", 36, 38), ("bwd5.xT", 38, 27), ("bwd5_wait", 27, 28),
+                 ("bwd5.dy", 28, 37), ("bwd5.dgrad", 37, 18)])
 
 
 def persistent_report(st):

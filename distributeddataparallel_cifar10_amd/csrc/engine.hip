@@ -584,6 +584,8 @@ int dca_engine_read_loss(void* h, double* loss, int* steps, int reset) {
 }
 
 // Enqueue `nsteps` training steps of batch B.  use_graph: replay a captured hipGraph (captured on first use).
+constexpr int GRAPH_CHUNK = 16;  // steps per graph replay
+
 int dca_engine_run(void* h, int B, int nsteps, int use_graph) {
   Engine* e = (Engine*)h;
   if (B < 1 || B > e->in.bmax) {
@@ -599,23 +601,35 @@ int dca_engine_run(void* h, int B, int nsteps, int use_graph) {
       if (dca::enqueue_step(e, B)) return -1;
     return 0;
   }
-  auto it = e->graphs.find(B);
-  if (it == e->graphs.end()) {
-    hipGraph_t g;
-    HIPCK(hipStreamBeginCapture(e->st, hipStreamCaptureModeThreadLocal));
-    const int rc = dca::enqueue_step(e, B);
-    const hipError_t ec = hipStreamEndCapture(e->st, &g);
-    if (rc) return -1;
-    if (ec != hipSuccess) {
-      g_err = std::string("hipStreamEndCapture: ") + hipGetErrorString(ec);
-      return -1;
+  // Steps are replayed from graphs holding GRAPH_CHUNK consecutive steps (the data cursor / batch ids advance
+  // on the device, so consecutive steps need no host input): launching one graph per step leaves a ~5-8 us
+  // gap between graph launches on the GPU (rocprofv3, profiles/), inside a graph consecutive kernels are
+  // back to back.
+  int done = 0;
+  for (const int chunk : {GRAPH_CHUNK, 1}) {
+    const int reps = (nsteps - done) / chunk;
+    if (reps == 0) continue;
+    const int key = B * 1024 + chunk;
+    auto it = e->graphs.find(key);
+    if (it == e->graphs.end()) {
+      hipGraph_t g;
+      HIPCK(hipStreamBeginCapture(e->st, hipStreamCaptureModeThreadLocal));
+      int rc = 0;
+      for (int s = 0; s < chunk && !rc; ++s) rc = dca::enqueue_step(e, B);
+      const hipError_t ec = hipStreamEndCapture(e->st, &g);
+      if (rc) return -1;
+      if (ec != hipSuccess) {
+        g_err = std::string("hipStreamEndCapture: ") + hipGetErrorString(ec);
+        return -1;
+      }
+      hipGraphExec_t ex;
+      HIPCK(hipGraphInstantiate(&ex, g, nullptr, nullptr, 0));
+      HIPCK(hipGraphDestroy(g));
+      it = e->graphs.emplace(key, ex).first;
     }
-    hipGraphExec_t ex;
-    HIPCK(hipGraphInstantiate(&ex, g, nullptr, nullptr, 0));
-    HIPCK(hipGraphDestroy(g));
-    it = e->graphs.emplace(B, ex).first;
+    for (int r = 0; r < reps; ++r) HIPCK(hipGraphLaunch(it->second, e->st));
+    done += reps * chunk;
   }
-  for (int s = 0; s < nsteps; ++s) HIPCK(hipGraphLaunch(it->second, e->st));
   return 0;
 }
 

@@ -42,12 +42,15 @@ constexpr int cmax(int a, int b) { return a > b ? a : b; }
 // diagnostic stamps (DCA_STAMPS builds): global stamp index s -> slot 24 + s/8, entry s%8
 #define PK_STAMP(cx, s) DCA_STAMP(cx, 24 + (s) / 8, blockIdx.x, (s) % 8)
 
+constexpr int P_KSHIFT = 906;  // misc offset of the [10][32] BN shift table (last step's batch means)
+constexpr int P_LABEL = 1240; // misc offset of this image's label
+
 struct Plan {
   static constexpr int RB = 80;                        // bf16 record = 32 channels (64 B) + 16 B pad
   static constexpr int O_CRED = 0;                     // [2][16][64] f32 combine scratch
   static constexpr int O_STAT = 8192;                  // [10][64] f32: mean[32] | invstd[32]
-  static constexpr int O_MISC = O_STAT + 2560;         // [1024] f32 (layout: see k_pk_step)
-  static constexpr int O_U = O_MISC + 4096;            // phase union
+  static constexpr int O_MISC = O_STAT + 2560;         // [1280] f32 (layout: see k_pk_step)
+  static constexpr int O_U = O_MISC + 5120;            // phase union
   // forward
   static constexpr int U_WT = 0;                       // 288 weight records
   static constexpr int U_XR = 288 * RB;                // 18 x 18 conv-input records (zero halo)
@@ -106,7 +109,7 @@ struct Geo {
   static constexpr int NT = 64 * NW;              // threads per workgroup
   static constexpr int RPW = 16 / NW;             // image rows per wave
   static constexpr int KSW = (64 + NW - 1) / NW;  // granule loads per lane per sweep pass (batch <= 64)
-  static constexpr int WTL = (36 + NW - 1) / NW;  // wgrad output tiles per wave
+  static constexpr int NNT = (18 + NW - 1) / NW;  // wgrad tile columns (ci half x tap) per wave; both co halves
   static constexpr int KPT = 2048 / NT;           // fc1 input features per thread
   static constexpr int SBC = 16 / NW;             // stem-wgrad (tile, row-quarter) combos per wave
   static constexpr int IMW = (768 + NT - 1) / NT; // uint8 image words per thread
@@ -157,14 +160,12 @@ __device__ __forceinline__ void img_csum2(float a0, float a1, float b0, float b1
   lds_barrier();
 }
 
-// In-kernel all-gather: every workgroup contributes misc[0..64); on return misc[64..128) holds the sum over
-// workgroups of each value and misc[128..192) the sum of squares.  Ends with a barrier.
 // one sweep pass over the granules of round `tag`: KS loads per lane, all issued before any is waited for
 // (a guarded load per slot would be compiled into KS serial round trips).  Slots past the grid read a valid
 // granule (clamped index) and are then replaced by a neutral (0, tag) pair.
 template <int NW, int KS>
 __device__ __forceinline__ bool sweep(const __amdgpu_buffer_rsrc_t rs, int w, int lane, int G, unsigned tag,
-                                      float& s1, float& s2) {
+                                      float& s1) {
   unsigned lo[KS], hi[KS];
 #pragma unroll
   for (int kk = 0; kk < KS; ++kk) {
@@ -175,35 +176,70 @@ __device__ __forceinline__ bool sweep(const __amdgpu_buffer_rsrc_t rs, int w, in
   }
   bool ok = true;
   s1 = 0.f;
-  s2 = 0.f;
 #pragma unroll
   for (int kk = 0; kk < KS; ++kk) {
     const bool valid = w + NW * kk < G;
     ok &= !valid || hi[kk] == tag;
-    const float v = valid ? __uint_as_float(lo[kk]) : 0.f;
-    s1 += v;
-    s2 += v * v;
+    s1 += valid ? __uint_as_float(lo[kk]) : 0.f;
   }
   return ok;
 }
 
-// In-kernel all-gather: every workgroup contributes misc[0..64); on return misc[64..128) holds the sum over
-// workgroups of each value and misc[128..192) the sum of squares.  Ends with a barrier.
+// Per-image channel sums of per-thread C-layout partials, delivered straight to the publishing threads: on
+// return thread t < 64 holds  t < 32: sum of a (channel t),  t >= 32: sum of b (channel t - 32)
+// (a0/b0: channel c, a1/b1: channel 16 + c).  One LDS barrier.
 template <int NW>
-__device__ void xchg(const PkArgs& pa, int epoch, int round, float* cred, float* misc) {
-  constexpr int KSW = Geo<NW>::KSW, KSH = (32 + NW - 1) / NW;
-  const int t = threadIdx.x, lane = t & 63, n = blockIdx.x, G = gridDim.x;
-  const int w = __builtin_amdgcn_readfirstlane(t >> 6);  // wave-uniform -> scalar branches in the sweep
+__device__ __forceinline__ float img_csum_pub(float a0, float a1, float b0, float b1, float* cred) {
+  const int t = threadIdx.x, w = t >> 6, lane = t & 63, c = lane & 15;
+  a0 += __shfl_xor(a0, 16);
+  a0 += __shfl_xor(a0, 32);
+  a1 += __shfl_xor(a1, 16);
+  a1 += __shfl_xor(a1, 32);
+  b0 += __shfl_xor(b0, 16);
+  b0 += __shfl_xor(b0, 32);
+  b1 += __shfl_xor(b1, 16);
+  b1 += __shfl_xor(b1, 32);
+  float* r = cred + 1024;  // [NW][64], disjoint from the sweep's cred[0 .. NW*64)
+  if (lane < 16) {
+    r[w * 64 + c] = a0;
+    r[w * 64 + 16 + c] = a1;
+    r[w * 64 + 32 + c] = b0;
+    r[w * 64 + 48 + c] = b1;
+  }
+  lds_barrier();
+  float v = 0.f;
+  if (t < 64) {
+#pragma unroll
+    for (int k = 0; k < NW; ++k) v += r[k * 64 + t];
+  }
+  return v;
+}
+
+// In-kernel all-gather + sum, in two halves so that independent work can run between them:
+//   xchg_publish: thread t < 64 of every workgroup contributes `v` to round `round`;
+//   xchg_wait:    on return thread t < 64 of every workgroup holds the sum of slot t over all workgroups.
+// One LDS barrier (the cross-wave combine).  The sweep is split over the waves (wave w reads workgroups
+// w, w + NW, ...).
+__device__ __forceinline__ void xchg_publish(const PkArgs& pa, int epoch, int round, float v) {
+  const int t = threadIdx.x;
   const unsigned tag = (unsigned)(epoch * 64 + round + 1);
   unsigned long long* buf = pa.gran + (size_t)(round & 1) * 64 * 64;
   if (t < 64)
-    __hip_atomic_store(buf + n * 64 + t, ((unsigned long long)tag << 32) | __float_as_uint(misc[t]),
+    __hip_atomic_store(buf + blockIdx.x * 64 + t, ((unsigned long long)tag << 32) | __float_as_uint(v),
                        __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+template <int NW>
+__device__ float xchg_wait(const PkArgs& pa, int epoch, int round, float* cred) {
+  constexpr int KSW = Geo<NW>::KSW, KSH = (32 + NW - 1) / NW;
+  const int t = threadIdx.x, lane = t & 63, G = gridDim.x;
+  const int w = __builtin_amdgcn_readfirstlane(t >> 6);  // wave-uniform -> scalar branches in the sweep
+  const unsigned tag = (unsigned)(epoch * 64 + round + 1);
+  unsigned long long* buf = pa.gran + (size_t)(round & 1) * 64 * 64;
   const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(buf, (short)0, 64 * 64 * 8, 0x00020000);
-  float s1 = 0.f, s2 = 0.f;
+  float s1 = 0.f;
   for (unsigned spins = 0;; ++spins) {
     asm volatile("" ::: "memory");  // the granule loads are re-issued every pass (no hoisting out of the spin)
-    const bool ok = G <= 32 ? sweep<NW, KSH>(rs, w, lane, G, tag, s1, s2) : sweep<NW, KSW>(rs, w, lane, G, tag, s1, s2);
+    const bool ok = G <= 32 ? sweep<NW, KSH>(rs, w, lane, G, tag, s1) : sweep<NW, KSW>(rs, w, lane, G, tag, s1);
     if (__all(ok)) break;
     if (spins >= SPIN_LIMIT) {
       if (lane == 0) atomicOr(pa.err, 1u << (round & 31));
@@ -211,19 +247,18 @@ __device__ void xchg(const PkArgs& pa, int epoch, int round, float* cred, float*
     }
   }
   cred[w * 64 + lane] = s1;
-  cred[1024 + w * 64 + lane] = s2;
   lds_barrier();
+  float a = 0.f;
   if (t < 64) {
-    float a = 0.f, b = 0.f;
 #pragma unroll
-    for (int k = 0; k < NW; ++k) {
-      a += cred[k * 64 + t];
-      b += cred[1024 + k * 64 + t];
-    }
-    misc[64 + t] = a;
-    misc[128 + t] = b;
+    for (int k = 0; k < NW; ++k) a += cred[k * 64 + t];
   }
-  lds_barrier();
+  return a;
+}
+template <int NW>
+__device__ __forceinline__ float xchg(const PkArgs& pa, int epoch, int round, float v, float* cred) {
+  xchg_publish(pa, epoch, round, v);
+  return xchg_wait<NW>(pa, epoch, round, cred);
 }
 
 // Records are 80 bytes (32 bf16 channels + 16 B pad, which also staggers the banks of neighbouring
@@ -256,42 +291,39 @@ __device__ __forceinline__ void conv_img(const char* xr, const char* wt, f32x4 (
   }
 }
 
-// forward BN statistics of y (C layout) for block `blk`: exchange, finalise, scale/shift -> misc[192..256),
-// (mean, invstd) -> stat[blk]; workgroup 0 updates the running stats.  Ends with a barrier.
+// forward BN statistics of y (C layout) for block `blk`: one pass of shifted sums S1 = sum(y - K),
+// S2 = sum((y - K)^2) per image, all-gathered; K (kshift) is this block's batch mean from the previous step (0 at
+// the first), identical in every workgroup, so the shifted sums combine exactly and the E[d^2] - E[d]^2
+// cancellation is negligible.  Finalise: scale/shift -> misc[192..256), (mean, invstd) -> stat[blk]; workgroup 0
+// updates the running stats and STATS.  Ends with a barrier.
 template <int NW>
 __device__ void bn_fwd_stats(const Ctx& cx, const PkArgs& pa, int epoch, int blk,
                              const float (&y)[Geo<NW>::RPW][2][4], float* cred, float* misc, float* stat) {
   constexpr int RPW = Geo<NW>::RPW;
   const int t = threadIdx.x, lane = t & 63, c = lane & 15;
-  float a0 = 0.f, a1 = 0.f;
+  const float* kshift = misc + P_KSHIFT;
+  const float K0 = kshift[blk * 32 + c], K1 = kshift[blk * 32 + 16 + c];
+  float a0 = 0.f, a1 = 0.f, b0 = 0.f, b1 = 0.f;
 #pragma unroll
   for (int rr = 0; rr < RPW; ++rr)
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      a0 += y[rr][0][i];
-      a1 += y[rr][1][i];
+      const float d0 = y[rr][0][i] - K0, d1 = y[rr][1][i] - K1;
+      a0 += d0;
+      a1 += d1;
+      b0 += d0 * d0;
+      b1 += d1 * d1;
     }
-  img_csum2<NW>(a0, a1, 0.f, 0.f, cred, misc + 256, misc + 288);  // image sums -> misc[256..288)
-  const float m0 = misc[256 + c] * (1.f / 256.f), m1 = misc[256 + 16 + c] * (1.f / 256.f);
-  float d0 = 0.f, d1 = 0.f;
-#pragma unroll
-  for (int rr = 0; rr < RPW; ++rr)
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      d0 += (y[rr][0][i] - m0) * (y[rr][0][i] - m0);
-      d1 += (y[rr][1][i] - m1) * (y[rr][1][i] - m1);
-    }
-  if (t < 32) misc[t] = misc[256 + t] * (1.f / 256.f);           // image mean -> misc[0..32)
-  img_csum2<NW>(d0, d1, 0.f, 0.f, cred, misc + 32, misc + 288);  // image M2 -> misc[32..64)
+  const float v = img_csum_pub<NW>(a0, a1, b0, b1, cred);
   if (blk == 5) PK_STAMP(cx, 25);
-  xchg<NW>(pa, epoch, blk, cred, misc);
+  const float tot = xchg<NW>(pa, epoch, blk, v, cred);
   if (blk == 5) PK_STAMP(cx, 26);
+  const float sq = __shfl(tot, (lane & 31) + 32);  // wave 0: lane t < 32 also gets slot 32 + t
   if (t < 32) {
-    const float G = (float)gridDim.x;
-    const float s1 = misc[64 + t], s2 = misc[128 + t], qm = misc[96 + t];
-    const float mean = s1 / G;
-    const float m2 = fmaxf(qm + 256.f * (s2 - s1 * mean), 0.f);
-    const float var = m2 / (G * 256.f);
+    const float N = (float)gridDim.x * 256.f;
+    const float dm = tot / N;
+    const float mean = kshift[blk * 32 + t] + dm;
+    const float var = fmaxf(sq / N - dm * dm, 0.f);
     const float invstd = rsqrtf(var + cx.bn_eps);
     const float gam = misc[320 + t], bet = misc[352 + t];
     misc[192 + t] = gam * invstd;
@@ -300,12 +332,37 @@ __device__ void bn_fwd_stats(const Ctx& cx, const PkArgs& pa, int epoch, int blk
     stat[blk * 64 + 32 + t] = invstd;
     if (blockIdx.x == 0) {  // running stats live in LDS (misc[448..512)) for the whole forward
       cx.STATS[blk * 32 + t] = make_float2(mean, invstd);
-      const float ntot = G * 256.f, unb = var * ntot / (ntot - 1.f), mo = cx.bn_mom;
+      const float unb = var * N / (N - 1.f), mo = cx.bn_mom;
       misc[448 + t] = misc[448 + t] * (1.f - mo) + mean * mo;
       misc[480 + t] = misc[480 + t] * (1.f - mo) + unb * mo;
     }
   }
   lds_barrier();
+}
+
+// wgrad of the shared conv for one application (dyT / xT staged in LDS), accumulated in registers.  Wave w
+// owns tile columns nt = w, w + NW, ... (ci half x tap) for BOTH co halves: per K step the two dy fragments are
+// read once and each x fragment feeds two MFMAs.
+template <int NW>
+__device__ __forceinline__ void wgrad_acc(const unsigned short* dyT, const unsigned short* xT,
+                                          f32x4 (&wacc)[Geo<NW>::NNT][2], int w, int lane) {
+  const int c = lane & 15, q = lane >> 4;
+#pragma unroll
+  for (int s = 0; s < 8; ++s) {
+    const int row = 2 * s + (q >> 1), c0 = 8 * (q & 1);
+    const bf16x8 a0 = *(const bf16x8*)(dyT + c * Plan::DYT_S + row * 16 + c0);
+    const bf16x8 a1 = *(const bf16x8*)(dyT + (16 + c) * Plan::DYT_S + row * 16 + c0);
+#pragma unroll
+    for (int j = 0; j < Geo<NW>::NNT; ++j) {
+      const int nt = w + NW * j;
+      if (nt < 18) {
+        const int tap = nt >> 1, cih = nt & 1, kh = tap / 3, kw = tap % 3;
+        const bf16x8 b = *(const bf16x8*)(xT + (kw * 32 + 16 * cih + c) * Plan::XT_S + (row + kh) * 16 + c0);
+        wacc[j][0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0, b, wacc[j][0], 0, 0, 0);
+        wacc[j][1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1, b, wacc[j][1], 0, 0, 0);
+      }
+    }
+  }
 }
 
 template <int NW>
@@ -424,8 +481,9 @@ __global__ void __launch_bounds__(64 * NW) k_pk_step(Ctx cx, PkArgs pa) {
     float* x0i = (float*)(U + P::U_X0);
     // step constants -> misc: k < 64: BN gamma|beta -> misc[320 + k]; k >= 64 -> misc[384 + k]: running
     // mean|var (rank 0's base under DDP, reference CC4) [448,512), fc1 bias [512,544), W2 [544,864),
-    // b2 [864,874), conv1 bias [874,906).  Every load is issued before any is waited for.
-    constexpr int NKC = 522, KCM = (NKC + NTH - 1) / NTH;
+    // b2 [864,874), conv1 bias [874,906), BN shifts [906,1226) (= P_KSHIFT).  Every load is issued before any
+    // is waited for.
+    constexpr int NKC = 842, KCM = (NKC + NTH - 1) / NTH;
     float kc[KCM];
 #pragma unroll
     for (int m = 0; m < KCM; ++m) {
@@ -438,7 +496,8 @@ __global__ void __launch_bounds__(64 * NW) k_pk_step(Ctx cx, PkArgs pa) {
                        : k < 160 ? cx.params + OFF_FC1B + (k - 128)
                        : k < 480 ? cx.params + OFF_FC2W + (k - 160)
                        : k < 490 ? cx.params + OFF_FC2B + (k - 480)
-                                 : cx.params + OFF_C1B + (k - 490);
+                       : k < 522 ? cx.params + OFF_C1B + (k - 490)
+                                 : (const float*)cx.STATS + 2 * (k - 522);  // BN shifts (.x = mean)
       kc[m] = *src;
     }
     uint4 swv = ((const uint4*)cx.sw)[t & 127];
@@ -451,10 +510,10 @@ __global__ void __launch_bounds__(64 * NW) k_pk_step(Ctx cx, PkArgs pa) {
 #pragma unroll
     for (int m = 0; m < KCM; ++m) {
       const int k = t + NTH * m;
-      if (k < NKC) misc[(k < 64 ? 320 : 384) + k] = kc[m];
+      if (k < NKC) misc[(k < 64 ? 320 : 384) + k] = k >= 522 && !(fabsf(kc[m]) < 1e30f) ? 0.f : kc[m];
     }
     if (t < 128) ((uint4*)swl)[t] = swv;
-    if (t == 0) misc[1000] = __int_as_float(lab);  // label for the head's cross-entropy
+    if (t == 0) misc[P_LABEL] = __int_as_float(lab);  // label for the head's cross-entropy
     stage_wt<NW>(WT, cx.wt_f);
     zero_xr_halo<NW>(XR);
     lds_barrier();
@@ -543,6 +602,7 @@ __global__ void __launch_bounds__(64 * NW) k_pk_step(Ctx cx, PkArgs pa) {
       }
       lds_barrier();
     }
+    if (i == 6) PK_STAMP(cx, 39);
     f32x4 acc[RPW][2];
     conv_img<RPW>(XR, WT, acc, r0, lane);
 #pragma unroll
@@ -644,7 +704,7 @@ __global__ void __launch_bounds__(64 * NW) k_pk_step(Ctx cx, PkArgs pa) {
     }
     lds_barrier();
     if (t == 0) {
-      const int label = __float_as_int(misc[1000]);
+      const int label = __float_as_int(misc[P_LABEL]);
       float mx = hv[64];
       for (int o = 1; o < 10; ++o) mx = fmaxf(mx, hv[64 + o]);
       float se = 0.f;
@@ -730,9 +790,9 @@ __global__ void __launch_bounds__(64 * NW) k_pk_step(Ctx cx, PkArgs pa) {
         ld4v(xp + tl(r0 + rr, h, lane), xb[rr][h]);
       }
   }
-  f32x4 wacc[Gm::WTL];
+  f32x4 wacc[Gm::NNT][2];
 #pragma unroll
-  for (int j = 0; j < Gm::WTL; ++j) wacc[j] = z4();
+  for (int j = 0; j < Gm::NNT; ++j) wacc[j][0] = wacc[j][1] = z4();
   float dgam = 0.f, dbet = 0.f;
   unsigned codew[RPW][2];                         // stem-backward prefetch (filled during block 0)
   unsigned imgw[Gm::IMW];
@@ -758,8 +818,15 @@ __global__ void __launch_bounds__(64 * NW) k_pk_step(Ctx cx, PkArgs pa) {
           sbv[h] += dz[rr][h][i2] * xh[rr][h][i2];
         }
     }
-    img_csum2<NW>(sa[0], sa[1], sbv[0], sbv[1], cred, misc, misc + 32);  // image sums -> publish slots
-    // (the barriers above also retire every wave's reads of dyT / xT / XR from the previous block)
+    const float pv = img_csum_pub<NW>(sa[0], sa[1], sbv[0], sbv[1], cred);  // image sums -> publish value
+    xchg_publish(pa, epoch, NBLK + (NBLK - 1 - i), pv);
+    if (i == 5) PK_STAMP(cx, 36);
+    // While the exchange is in flight: the weight gradient of the PREVIOUS application (block i + 1), whose
+    // dy / x tiles are still staged in dyT / xT.  Then the barrier retires every wave's reads of them (and of
+    // XR by block i + 1's dgrad) before x_i replaces them.
+    if (i < NBLK - 1) wgrad_acc<NW>(dyT, xT, wacc, w, lane);
+    if (i == 5) PK_STAMP(cx, 38);
+    lds_barrier();
 #pragma unroll
     for (int rr = 0; rr < RPW; ++rr)
 #pragma unroll
@@ -779,7 +846,11 @@ __global__ void __launch_bounds__(64 * NW) k_pk_step(Ctx cx, PkArgs pa) {
         p2[2] = (unsigned short)b3;
       }
     if (i == 5) PK_STAMP(cx, 27);
-    xchg<NW>(pa, epoch, NBLK + (NBLK - 1 - i), cred, misc);
+    {
+      const float tot = xchg_wait<NW>(pa, epoch, NBLK + (NBLK - 1 - i), cred);
+      if (t < 64) misc[64 + t] = tot;  // batch sums: [64, 96) sum dz, [96, 128) sum dz * xhat
+      lds_barrier();
+    }
     if (i == 5) PK_STAMP(cx, 28);
     if (i > 0) {  // prefetch y_{i-1} / x_{i-1}; the loads land while this block's convolutions run
       const float* yp = cx.Y + (size_t)(i - 1) * B * 8192 + img;
@@ -826,6 +897,7 @@ __global__ void __launch_bounds__(64 * NW) k_pk_step(Ctx cx, PkArgs pa) {
       }
     }
     lds_barrier();
+    if (i == 5) PK_STAMP(cx, 37);
     // dgrad: g_i = g_{i+1} + conv(dy, W^T flipped)
     {
       f32x4 acc[RPW][2];
@@ -837,21 +909,6 @@ __global__ void __launch_bounds__(64 * NW) k_pk_step(Ctx cx, PkArgs pa) {
 #pragma unroll
           for (int i2 = 0; i2 < 4; ++i2) g[rr][h][i2] += acc[rr][h][i2];
     }
-    // wgrad of the shared conv, accumulated in registers over all 10 applications
-#pragma unroll
-    for (int j = 0; j < Gm::WTL; ++j) {
-      const int tt = w + NW * j;
-      if (tt < 36) {
-        const int mt = tt & 1, nt = tt >> 1, tap = nt >> 1, cih = nt & 1, kh = tap / 3, kw = tap % 3;
-#pragma unroll
-        for (int s = 0; s < 8; ++s) {
-          const int row = 2 * s + (q >> 1), c0 = 8 * (q & 1);
-          const bf16x8 a = *(const bf16x8*)(dyT + (16 * mt + c) * P::DYT_S + row * 16 + c0);
-          const bf16x8 b = *(const bf16x8*)(xT + (kw * 32 + 16 * cih + c) * P::XT_S + (row + kh) * 16 + c0);
-          wacc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, wacc[j], 0, 0, 0);
-        }
-      }
-    }
     PK_STAMP(cx, 14 + (NBLK - 1 - i));
     if (pa.debug && i >= 1) {
       float* gout = cx.G + (size_t)((10 - i) & 1) * B * 8192 + img;
@@ -861,6 +918,7 @@ __global__ void __launch_bounds__(64 * NW) k_pk_step(Ctx cx, PkArgs pa) {
         for (int h = 0; h < 2; ++h) st4v(gout + tl(r0 + rr, h, lane), g[rr][h]);
     }
   }
+  wgrad_acc<NW>(dyT, xT, wacc, w, lane);  // application 0 (its dyT / xT are staged by the last iteration)
   if (n == 0 && t < 32) {
     pa.bng[t] = dgam;
     pa.bng[32 + t] = dbet;
@@ -929,9 +987,12 @@ __global__ void __launch_bounds__(64 * NW) k_pk_step(Ctx cx, PkArgs pa) {
   }
   // trunk wgrad slab (accumulated over the 10 applications)
 #pragma unroll
-  for (int j = 0; j < Gm::WTL; ++j) {
-    const int tt = w + NW * j;
-    if (tt < 36) st4(pa.tslab + (size_t)n * WSLAB_N + ((tt * 64 + lane) << 2), wacc[j]);
+  for (int j = 0; j < Gm::NNT; ++j) {
+    const int nt = w + NW * j;
+    if (nt < 18) {  // slab tile tt = 2 nt + mt (layout read by k_pk_reduce)
+      st4(pa.tslab + (size_t)n * WSLAB_N + (((2 * nt) * 64 + lane) << 2), wacc[j][0]);
+      st4(pa.tslab + (size_t)n * WSLAB_N + (((2 * nt + 1) * 64 + lane) << 2), wacc[j][1]);
+    }
   }
   PK_STAMP(cx, 24);
 }
