@@ -58,7 +58,8 @@ def compare_one_step(dtype: str, rows: int, B: int, graph: bool, seed: int = 0, 
     eng.read_loss(reset=True)
     eng.run(B, 1, graph=graph)
     eng.sync()
-    r = reference_step(ref, data[idx], labels[idx], lr=1e-2, bf16_operands=(dtype == "bf16"))
+    r = reference_step(ref, data[idx], labels[idx], lr=1e-2, bf16_operands=(dtype == "bf16"),
+                       fc1_bf16=bool(persistent))
     out = {}
 
     def rep(name, a, b):
@@ -125,7 +126,8 @@ def trajectory(dtype: str, rows: int, B: int, steps: int, seed: int = 1, persist
         lsum, _ = eng.read_loss(reset=True)
         losses_e.append(lsum)
         sel = idx[s * B:(s + 1) * B]
-        losses_r.append(reference_step(ref, data[sel], labels[sel], bf16_operands=(dtype == "bf16"))["loss"])
+        losses_r.append(reference_step(ref, data[sel], labels[sel], bf16_operands=(dtype == "bf16"),
+                                       fc1_bf16=bool(persistent))["loss"])
     sd, rsd = model.state_dict(), ref.state_dict()
     perr = max(rel(sd[k], rsd[k]) for k in rsd if rsd[k].dtype != torch.int64)
     eng.close()

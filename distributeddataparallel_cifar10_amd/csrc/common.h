@@ -83,6 +83,7 @@ struct Ctx {
   float* HPART;    // [nparts][32] per-tile partial fc1 pre-activations
   uint8_t* HCODE;  // [B][64][32] head max-pool argmax
   int pstride;     // FPART/BPART stride per block (>= max nparts)
+  void* w1b;                   // [32][2048] bf16 copy of fc1.weight (persistent engine's head; kept by every SGD)
   unsigned long long* stamps;  // [32 kernel slots][256 wg][8 stamps][2] (diagnostic DCA_STAMPS builds only)
 };
 

@@ -64,7 +64,7 @@ struct DcaInit {
   const char* nccl_id;  // 128 bytes (world_size > 1)
   int persistent;       // 1: one-launch persistent trunk kernel (bf16 only)
   int debug;            // persistent engine: also store DY / G for diagnostics
-  int pk_waves;         // persistent engine: waves per workgroup (8 or 4; 0 = default 8)
+  int pk_waves;         // persistent engine: waves per workgroup (8; 0 = default)
   int comm_mode;        // world_size > 1: 0 = RCCL inside the step; 1 = external (host drives the all-reduce
                         // between dca_engine_run_part(.., 1) and (.., 2); test/debug path, no RCCL communicator)
 };
@@ -143,7 +143,7 @@ static int alloc_workspace(Engine* e) {
       {"RS_BASE", 64 * 4},           {"CURSOR", 16},                  {"STEPS", 16},
       {"LOSS", 16},                  {"STAMPS", 32 * 256 * 8 * 2 * 8},
       {"GRAN", 2 * 64 * 64 * 8},     {"EPOCH", 16},                   {"ERR", 16},
-      {"TSLAB", bmax * WSLAB_N * 4}, {"BNG", 64 * 4}, {"IDS", 64 * 4},
+      {"TSLAB", bmax * WSLAB_N * 4}, {"BNG", 64 * 4}, {"IDS", 64 * 4}, {"W1B", 65536 * 2},
   };
   size_t total = 0;
   for (auto& r : regs) total += align_up(r.bytes, 256);
@@ -182,6 +182,7 @@ static int alloc_workspace(Engine* e) {
   c.loss_acc = (double*)e->regions["LOSS"];
   c.pstride = (int)pstride;
   c.stamps = (unsigned long long*)e->regions["STAMPS"];
+  c.w1b = e->regions["W1B"];
   e->pa.gran = (unsigned long long*)e->regions["GRAN"];
   e->pa.epoch = (int*)e->regions["EPOCH"];
   e->pa.err = (unsigned*)e->regions["ERR"];
@@ -201,8 +202,7 @@ static int set_lds_limits(Engine* e) {
   HIPCK(hipFuncSetAttribute((const void*)e->kbwd, hipFuncAttributeMaxDynamicSharedMemorySize, (int)dg));
   HIPCK(hipFuncSetAttribute((const void*)pk::k_pk_step<8>, hipFuncAttributeMaxDynamicSharedMemorySize,
                             pk::Plan::TOTAL));
-  HIPCK(hipFuncSetAttribute((const void*)pk::k_pk_step<4>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                            pk::Plan::TOTAL));
+
   return 0;
 }
 
@@ -213,10 +213,7 @@ static int enqueue_step_persistent(Engine* e, int B, int part) {
   Ctx cx = e->base;
   cx.B = B;
   if (part != 2) {
-    if (e->pk_waves == 4)
-      hipLaunchKernelGGL(pk::k_pk_step<4>, dim3(B), dim3(64 * 4), pk::Plan::TOTAL, e->st, cx, e->pa);
-    else
-      hipLaunchKernelGGL(pk::k_pk_step<8>, dim3(B), dim3(64 * 8), pk::Plan::TOTAL, e->st, cx, e->pa);
+    hipLaunchKernelGGL(pk::k_pk_step<8>, dim3(B), dim3(64 * 8), pk::Plan::TOTAL, e->st, cx, e->pa);
     hipLaunchKernelGGL(pk::k_pk_reduce, dim3(pk::R_GRID), dim3(256), 0, e->st, cx, e->pa);
   }
   if (e->in.world_size > 1) {
@@ -455,7 +452,11 @@ int dca_engine_create(const DcaInit* in, int n_indices, void** out) {
   }
   e->TPI = 16 / e->R;
   e->persistent = in->persistent != 0;
-  e->pk_waves = in->pk_waves == 4 ? 4 : 8;
+  if (in->pk_waves != 0 && in->pk_waves != 8) {
+    g_err = "persistent engine: pk_waves must be 8";
+    return -1;
+  }
+  e->pk_waves = 8;
   if (e->persistent && !e->bf) {
     g_err = "the persistent engine is bf16-only (fp32 MFMA needs all CUs: use the multi-kernel engine)";
     delete e;

@@ -1372,7 +1372,9 @@ __global__ void __launch_bounds__(NT) k_apply_sgd(Ctx cx, int mode) {
       w -= cx.lr * cx.grads[e] * cx.inv_ws;
       cx.params[e] = w;
     }
-    if (e >= OFF_CONVW && e < OFF_CONVW + 9216) {
+    if (e < OFF_FC1W + 65536) {
+      ((unsigned short*)cx.w1b)[e - OFF_FC1W] = bfbits(w);  // bf16 fc1 copy (persistent engine's head)
+    } else if (e >= OFF_CONVW && e < OFF_CONVW + 9216) {
       const int r = e - OFF_CONVW, co = r / 288, ci = (r / 9) % 32, tap = r % 9;
       put_w<BF>(cx.wt_f, (tap * 32 + co) * 32 + ci, w);
       put_w<BF>(cx.wt_d, ((8 - tap) * 32 + ci) * 32 + co, w);

@@ -60,7 +60,8 @@ struct Plan {
   static constexpr int U_SW = U_XIN + 13872;           // [32][32] bf16 stem weight
   static constexpr int U_SB = U_SW + 2048;             // [32] f32 stem bias
   static constexpr int U_X0 = U_SB + 128;              // [256][32] f32 pooled stem output
-  static constexpr int STEM_END = U_X0 + 32768;
+  static constexpr int U_SCODE = U_X0 + 32768;         // [256][32] u8 stem pool argmax (re-laid out for global)
+  static constexpr int STEM_END = U_SCODE + 8192;
   // head
   static constexpr int U_X10 = 0;                      // [256][32] f32
   static constexpr int U_P = 32768;                    // [2048] f32  (NCHW flatten c*64 + ph*8 + pw)
@@ -374,6 +375,21 @@ __device__ __forceinline__ void zero_xr_halo(char* xr) {
     *(uint4*)(xr + rec * Plan::RB + ch * 16) = uint4{0u, 0u, 0u, 0u};
   }
 }
+// stage_wt split in a load half and a store half (three named registers, not an array: a uint4 array that
+// lives across a loop is demoted to scratch by the compiler).  512 threads x 3 chunks >= 1152.
+__device__ __forceinline__ void stage_wt_load3(uint4& v0, uint4& v1, uint4& v2, const void* src) {
+  const uint4* s = (const uint4*)src;
+  const int i0 = threadIdx.x, i2 = i0 + 1024;
+  v0 = s[i0];
+  v1 = s[i0 + 512];
+  v2 = s[i2 < 1152 ? i2 : 1151];
+}
+__device__ __forceinline__ void stage_wt_store3(char* wt, const uint4& v0, const uint4& v1, const uint4& v2) {
+  const int i0 = threadIdx.x, i1 = i0 + 512, i2 = i0 + 1024;
+  *(uint4*)(wt + (i0 >> 2) * Plan::RB + (i0 & 3) * 16) = v0;
+  *(uint4*)(wt + (i1 >> 2) * Plan::RB + (i1 & 3) * 16) = v1;
+  if (i2 < 1152) *(uint4*)(wt + (i2 >> 2) * Plan::RB + (i2 & 3) * 16) = v2;
+}
 template <int NW>
 __device__ __forceinline__ void stage_wt(char* wt, const void* src) {
   constexpr int M = (1152 + 64 * NW - 1) / (64 * NW);
@@ -453,7 +469,7 @@ __device__ __forceinline__ void stage_input(float* xin, const uint8_t* img) {
 // ============================================================================================================
 template <int NW>
 __global__ void __launch_bounds__(64 * NW) k_pk_step(Ctx cx, PkArgs pa) {
-  static_assert(NW == 4 || NW == 8, "4 or 8 waves per workgroup (LDS dp scratch is sized for 8)");
+  static_assert(NW == 8, "8 waves per workgroup: 2 image rows (one pool row) per wave, 4 fc1 rows per wave");
   extern __shared__ __attribute__((aligned(16))) char smem[];
   using P = Plan;
   using Gm = Geo<NW>;
@@ -526,7 +542,7 @@ __global__ void __launch_bounds__(64 * NW) k_pk_step(Ctx cx, PkArgs pa) {
       kval[s] = k < 27;
       koff[s] = kval[s] ? (k / 9) * 34 * 34 + ((k % 9) / 3) * 34 + (k % 3) : 0;
     }
-    uint8_t* code_out = cx.SCODE + img;
+    uint8_t* scl = (uint8_t*)(U + P::U_SCODE);
 #pragma unroll 1
     for (int j = 0; j < 64 / NW; ++j) {
       const int u = w + NW * j, pr = u >> 2, chalf = (u >> 1) & 1, h = u & 1, co = 16 * h + c;
@@ -554,7 +570,7 @@ __global__ void __launch_bounds__(64 * NW) k_pk_step(Ctx cx, PkArgs pa) {
         if (best > 0.f) code |= 4;
         const int pc = 8 * chalf + 2 * q + pp, po = (pr * 16 + pc) * 32 + co;
         x0i[po] = best;
-        code_out[tl(pr, h, 16 * (pc >> 2) + c) + (pc & 3)] = (uint8_t)code;
+        scl[po] = (uint8_t)code;
         st1r(XR, (pr + 1) * 18 + pc + 1, co, best);
       }
     }
@@ -571,10 +587,19 @@ __global__ void __launch_bounds__(64 * NW) k_pk_step(Ctx cx, PkArgs pa) {
       for (int h = 0; h < 2; ++h)
 #pragma unroll
         for (int i = 0; i < 4; ++i) x[rr][h][i] = x0i[el(r0 + rr, q, c, h, i)];
+    // x0 and the stem pool codes go to global in the tiled layout, written by the very threads that read them
+    // back in the backward (so no workgroup-wide memory barrier is ever needed for them)
+    const uint8_t* scl = (const uint8_t*)(U + P::U_SCODE);
 #pragma unroll
     for (int rr = 0; rr < RPW; ++rr)
 #pragma unroll
-      for (int h = 0; h < 2; ++h) st4v(cx.X + img + tl(r0 + rr, h, lane), x[rr][h]);
+      for (int h = 0; h < 2; ++h) {
+        st4v(cx.X + img + tl(r0 + rr, h, lane), x[rr][h]);
+        unsigned cw = 0;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) cw |= (unsigned)scl[el(r0 + rr, q, c, h, i)] << (8 * i);
+        *(unsigned*)(cx.SCODE + img + tl(r0 + rr, h, lane)) = cw;
+      }
   }
 
   // ======================= forward: 10 applications of the shared ResBlock =================================
@@ -613,6 +638,16 @@ __global__ void __launch_bounds__(64 * NW) k_pk_step(Ctx cx, PkArgs pa) {
         for (int i2 = 0; i2 < 4; ++i2) y[rr][h][i2] = acc[rr][h][i2];
     PK_STAMP(cx, 2 + i);
   }
+  // fc1 weight slice of this wave (bf16 copy): all 32 rows x features 256w + 4l .. +3 (lane l) = 64 VGPRs,
+  // loaded once (issued before the last BN exchange, whose wait hides the latency), used by fc1 AND its
+  // transpose (dp), so W1 is read once per step
+  uint2 wv[32];
+  {
+    const uint2* W1b = (const uint2*)cx.w1b;
+#pragma unroll
+    for (int j = 0; j < 32; ++j) wv[j] = W1b[j * 512 + w * 64 + lane];
+  }
+
   bn_fwd_stats<NW>(cx, pa, epoch, NBLK - 1, y, cred, misc, stat);
   if (n == 0 && t < 32) {
     cx.rm[t] = misc[448 + t];
@@ -627,169 +662,192 @@ __global__ void __launch_bounds__(64 * NW) k_pk_step(Ctx cx, PkArgs pa) {
   }
   PK_STAMP(cx, 12);
 
+  float yb[RPW][2][4], xb[RPW][2][4];  // the backward's y_i / x_i tiles (y_9 / x_9 reloaded during the head)
   // ======================= head =============================================================================
+  // x10 = relu(bn(y9)) + x9, 2x2 max-pool, fc1 + ReLU, fc2, cross-entropy (mean over the batch) and their
+  // backward down to g = dL/dx10, all inside the workgroup.
   float g[RPW][2][4];
   {
-    float* x10 = (float*)(U + P::U_X10);
-    float* Pv = (float*)(U + P::U_P);
-    uint8_t* code = (uint8_t*)(U + P::U_CODE);
-    float* dp = (float*)(U + P::U_DP);
-    float* hp = (float*)(U + P::U_HP);
-    float* hv = (float*)(U + P::U_HV);  // h[0..32) dh[32..64) logits[64..80) dl[80..96)
-    float* dpp = (float*)(U + P::U_DPP);
-    constexpr int NWR = 32 / NW;  // fc1 rows owned by each wave
-    const float* W1 = cx.params + OFF_FC1W;
+    float* Pv = (float*)(U + P::U_P);      // [2048] pooled features, NCHW flatten order c*64 + ph*8 + pw
+    float* dp = (float*)(U + P::U_DP);     // [2048] dL/dpooled
+    float* hp = (float*)(U + P::U_HP);     // [8 waves][32] fc1 partial sums; [256, 288) dh
+    // pool straight from registers: the wave's two rows are one pool row; cols 4q..4q+3 are two windows
+    unsigned codes = 0;  // 2-bit argmax per (h, window)
+    float pooled[4];     // this thread's pooled outputs (stored for the reduce kernel after the loss)
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
       const int ch = 16 * h + c;
       const float sc = misc[192 + ch], sh = misc[224 + ch];
 #pragma unroll
-      for (int rr = 0; rr < RPW; ++rr)
+      for (int k = 0; k < 2; ++k) {
+        float v[4];
 #pragma unroll
-        for (int i2 = 0; i2 < 4; ++i2)
-          x10[el(r0 + rr, q, c, h, i2)] = fmaxf(y[rr][h][i2] * sc + sh, 0.f) + x[rr][h][i2];
-    }
-    lds_barrier();
-#pragma unroll
-    for (int m = 0; m < 2048 / NTH; ++m) {
-      const int o = t + NTH * m, ch = o & 31, pp = o >> 5, pr = pp >> 3, pw = pp & 7;
-      const int p00 = ((2 * pr) * 16 + 2 * pw) * 32 + ch;
-      const float v00 = x10[p00], v01 = x10[p00 + 32], v10 = x10[p00 + 512], v11 = x10[p00 + 544];
-      float best = v00;
-      int id = 0;
-      if (v01 > best) { best = v01; id = 1; }
-      if (v10 > best) { best = v10; id = 2; }
-      if (v11 > best) { best = v11; id = 3; }
-      Pv[ch * 64 + pp] = best;
-      code[pp * 32 + ch] = (uint8_t)id;
-      cx.HP[(size_t)n * 2048 + ch * 64 + pp] = best;
+        for (int e = 0; e < 4; ++e) {  // window order (0,0) (0,1) (1,0) (1,1): first maximum wins
+          const int rr = e >> 1, i2 = 2 * k + (e & 1);
+          v[e] = fmaxf(y[rr][h][i2] * sc + sh, 0.f) + x[rr][h][i2];
+        }
+        float best = v[0];
+        unsigned id = 0;
+        if (v[1] > best) { best = v[1]; id = 1; }
+        if (v[2] > best) { best = v[2]; id = 2; }
+        if (v[3] > best) { best = v[3]; id = 3; }
+        codes |= id << (2 * (2 * h + k));
+        Pv[ch * 64 + w * 8 + 2 * q + k] = best;  // pool row = w, pool col = 2q + k
+        pooled[2 * h + k] = best;
+      }
     }
     lds_barrier();
     PK_STAMP(cx, 31);
-    // fc1: wave w computes rows j = w*NWR .. +NWR-1 (8 KiB of W1 each, streamed, next row prefetched);
-    // lane l covers features 4l + 256m (m < 8).
+    // fc1 partial sums over this wave's 256 features for all 32 rows, then a butterfly reduce-scatter across the
+    // lanes (31 shuffles): lane l ends with the wave's sum for row (l >> 1) & 31
     {
-      f32x4 p4[8];
+      const f32x4 pv = ld4(Pv + 256 * w + 4 * lane);
+      float v[32];
 #pragma unroll
-      for (int m = 0; m < 8; ++m) p4[m] = ld4(Pv + 4 * lane + 256 * m);
-      f32x4 wa[8], wb[8];
-#pragma unroll
-      for (int m = 0; m < 8; ++m) wa[m] = ld4(W1 + (w * NWR) * 2048 + 4 * lane + 256 * m);
-#pragma unroll
-      for (int jr = 0; jr < NWR; ++jr) {
-        const int j = w * NWR + jr;
-        if (jr + 1 < NWR) {
-#pragma unroll
-          for (int m = 0; m < 8; ++m) wb[m] = ld4(W1 + (j + 1) * 2048 + 4 * lane + 256 * m);
-        }
-        float s = 0.f;
-#pragma unroll
-        for (int m = 0; m < 8; ++m) s += wa[m].x * p4[m].x + wa[m].y * p4[m].y + wa[m].z * p4[m].z + wa[m].w * p4[m].w;
-#pragma unroll
-        for (int o = 32; o >= 1; o >>= 1) s += __shfl_xor(s, o);
-        if (lane == 0) hp[j] = s;
-#pragma unroll
-        for (int m = 0; m < 8; ++m) wa[m] = wb[m];
+      for (int j = 0; j < 32; ++j) {
+        const uint2 u = wv[j];
+        v[j] = __uint_as_float(u.x << 16) * pv[0] + __uint_as_float(u.x & 0xffff0000u) * pv[1] +
+               __uint_as_float(u.y << 16) * pv[2] + __uint_as_float(u.y & 0xffff0000u) * pv[3];
       }
+#pragma unroll
+      for (int step = 0; step < 5; ++step) {
+        const int half = 16 >> step, off = 32 >> step;
+        const bool upper = (lane & off) != 0;
+#pragma unroll
+        for (int r = 0; r < half; ++r) {
+          const float keep = upper ? v[half + r] : v[r], give = upper ? v[r] : v[half + r];
+          v[r] = keep + __shfl_xor(give, off);
+        }
+      }
+      const float tot = v[0] + __shfl_xor(v[0], 1);
+      if ((lane & 1) == 0) hp[w * 32 + (lane >> 1)] = tot;
     }
     lds_barrier();
     PK_STAMP(cx, 32);
-    if (t < 32) hv[t] = misc[512 + t] + hp[t];
-    lds_barrier();
-    if (t < 10) {
-      float s = misc[544 + 320 + t];
+    if (w == 0) {
+      // wave 0: fc1 bias + ReLU, fc2, softmax cross-entropy and dh, lane-parallel with shuffles (no barriers)
+      float hh = 0.f;
+      if (lane < 32) {
+        hh = misc[512 + lane];
 #pragma unroll
-      for (int j = 0; j < 32; ++j) s += misc[544 + t * 32 + j] * fmaxf(hv[j], 0.f);
-      hv[64 + t] = s;
-    }
-    lds_barrier();
-    if (t == 0) {
-      const int label = __float_as_int(misc[P_LABEL]);
-      float mx = hv[64];
-      for (int o = 1; o < 10; ++o) mx = fmaxf(mx, hv[64 + o]);
+        for (int k2 = 0; k2 < NW; ++k2) hh += hp[k2 * 32 + lane];
+      }
+      const float hr = fmaxf(hh, 0.f);
+      const int o = lane < 10 ? lane : 0;
+      float logit = misc[864 + o];
+#pragma unroll
+      for (int j = 0; j < 32; ++j)
+        logit += misc[544 + o * 32 + j] * __int_as_float(__builtin_amdgcn_readlane(__float_as_int(hr), j));
+      float lg[10];  // the 10 logits, broadcast to every lane (scalar reads, no LDS shuffles)
+#pragma unroll
+      for (int oo = 0; oo < 10; ++oo) lg[oo] = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(logit), oo));
+      float mx = lg[0];
+#pragma unroll
+      for (int oo = 1; oo < 10; ++oo) mx = fmaxf(mx, lg[oo]);
       float se = 0.f;
-      for (int o = 0; o < 10; ++o) se += expf(hv[64 + o] - mx);
-      const float lse = mx + logf(se);
-      cx.HLOSS[n] = lse - hv[64 + label];
-      const float invB = 1.f / (float)B;
-      for (int o = 0; o < 10; ++o) hv[80 + o] = (expf(hv[64 + o] - lse) - (o == label ? 1.f : 0.f)) * invB;
-    }
-    lds_barrier();
-    if (t < 32) {
-      float s = 0.f;
 #pragma unroll
-      for (int o = 0; o < 10; ++o) s += misc[544 + o * 32 + t] * hv[80 + o];
-      const float hh = hv[t];
-      const float dh = hh > 0.f ? s : 0.f;
-      hv[32 + t] = dh;
-      cx.HDH[n * 32 + t] = dh;
-      cx.HH[n * 32 + t] = fmaxf(hh, 0.f);
-      if (t < 10) cx.HDL[n * 10 + t] = hv[80 + t];
+      for (int oo = 0; oo < 10; ++oo) se += expf(lg[oo] - mx);
+      const float lse = mx + logf(se);
+      const int label = __float_as_int(misc[P_LABEL]);
+      float lt = lg[0];
+#pragma unroll
+      for (int oo = 1; oo < 10; ++oo) lt = label == oo ? lg[oo] : lt;
+      if (lane == 0) cx.HLOSS[n] = lse - lt;
+      const float invB = 1.f / (float)B;
+      float sd = 0.f, dl = 0.f;
+#pragma unroll
+      for (int oo = 0; oo < 10; ++oo) {
+        const float dlo = (expf(lg[oo] - lse) - (oo == label ? 1.f : 0.f)) * invB;
+        sd += misc[544 + oo * 32 + (lane & 31)] * dlo;
+        dl = lane == oo ? dlo : dl;
+      }
+      const float dh = hh > 0.f ? sd : 0.f;
+      if (lane < 32) {
+        hp[256 + lane] = dh;
+        cx.HDH[n * 32 + lane] = dh;
+        cx.HH[n * 32 + lane] = hr;
+      }
+      if (lane < 10) cx.HDL[n * 10 + lane] = dl;
+    } else {
+      // waves 1..7 meanwhile: the backward conv weights (taps flipped, ci <-> co transposed) re-laid out from
+      // the forward copy still in WT -- no global reload.  Chunk o: record R = (8 - tap) * 32 + ci, co 8(o&3)..+7
+      unsigned wtr[3][4];
+#pragma unroll
+      for (int m = 0; m < 3; ++m) {
+        const int o0 = t - 64 + (NTH - 64) * m, o = o0 < 1152 ? o0 : 1151, R = o >> 2, co0 = 8 * (o & 3);
+        const int tap = 8 - (R >> 5), ci = R & 31;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const unsigned lo = *(const unsigned short*)(WT + (tap * 32 + co0 + 2 * e) * P::RB + 2 * ci);
+          const unsigned hi = *(const unsigned short*)(WT + (tap * 32 + co0 + 2 * e + 1) * P::RB + 2 * ci);
+          wtr[m][e] = lo | (hi << 16);
+        }
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");  // waves 1..7: all WT reads done
+#pragma unroll
+      for (int m = 0; m < 3; ++m) {
+        const int o = t - 64 + (NTH - 64) * m;
+        if (o < 1152) *(uint4*)(WT + (o >> 2) * P::RB + (o & 3) * 16) = uint4{wtr[m][0], wtr[m][1], wtr[m][2], wtr[m][3]};
+      }
     }
+    if (w == 0) asm volatile("s_barrier" ::: "memory");  // wave 0's side of the waves-1..7 barrier above
     lds_barrier();
     PK_STAMP(cx, 33);
-    // dp = W1^T dh: per-wave partials over the wave's rows (rows streamed again), summed in fixed order
+#pragma unroll
+    for (int hk = 0; hk < 4; ++hk)  // fc1 input for the weight gradient (k_pk_reduce)
+      cx.HP[(size_t)n * 2048 + (16 * (hk >> 1) + c) * 64 + w * 8 + 2 * q + (hk & 1)] = pooled[hk];
+    // dp = W1^T dh for this wave's features (complete per lane: all 32 rows are in its registers)
     {
-      f32x4 d4[8];
+      f32x4 d = z4();
 #pragma unroll
-      for (int m = 0; m < 8; ++m) d4[m] = z4();
-#pragma unroll
-      for (int jr = 0; jr < NWR; ++jr) {
-        const int j = w * NWR + jr;
-        const float dh = hv[32 + j];
-#pragma unroll
-        for (int m = 0; m < 8; ++m) d4[m] += dh * ld4(W1 + j * 2048 + 4 * lane + 256 * m);
+      for (int j = 0; j < 32; ++j) {
+        const float dhj = hp[256 + j];
+        const uint2 u = wv[j];
+        d[0] += dhj * __uint_as_float(u.x << 16);
+        d[1] += dhj * __uint_as_float(u.x & 0xffff0000u);
+        d[2] += dhj * __uint_as_float(u.y << 16);
+        d[3] += dhj * __uint_as_float(u.y & 0xffff0000u);
       }
-#pragma unroll
-      for (int m = 0; m < 8; ++m) st4(dpp + w * 2048 + 4 * lane + 256 * m, d4[m]);
+      st4(dp + 256 * w + 4 * lane, d);
     }
-    lds_barrier();
-    for (int k = t; k < 2048; k += NTH) {
-      float s = 0.f;
+    {  // y_9 / x_9 for the first backward block (this thread's own stores: no cross-thread hand-off)
+      const float* yp = cx.Y + (size_t)(NBLK - 1) * B * 8192 + img;
+      const float* xp = cx.X + (size_t)(NBLK - 1) * B * 8192 + img;
 #pragma unroll
-      for (int k2 = 0; k2 < NW; ++k2) s += dpp[k2 * 2048 + k];
-      dp[k] = s;
-    }
-    lds_barrier();
+      for (int rr = 0; rr < RPW; ++rr)
 #pragma unroll
-    for (int rr = 0; rr < RPW; ++rr)
-#pragma unroll
-      for (int h = 0; h < 2; ++h)
-#pragma unroll
-        for (int i2 = 0; i2 < 4; ++i2) {
-          const int row = r0 + rr, ch = 16 * h + c, col = 4 * q + i2;
-          const int pp = (row >> 1) * 8 + (col >> 1), pos = (row & 1) * 2 + (col & 1);
-          g[rr][h][i2] = code[pp * 32 + ch] == pos ? dp[ch * 64 + pp] : 0.f;
+        for (int h = 0; h < 2; ++h) {
+          ld4v(yp + tl(r0 + rr, h, lane), yb[rr][h]);
+          ld4v(xp + tl(r0 + rr, h, lane), xb[rr][h]);
         }
+    }
+    lds_barrier();
+    // g = max-pool backward of dp, routed by the saved argmax
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+      for (int k = 0; k < 2; ++k) {
+        const float dpv = dp[(16 * h + c) * 64 + w * 8 + 2 * q + k];
+        const unsigned id = (codes >> (2 * (2 * h + k))) & 3u;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) g[e >> 1][h][2 * k + (e & 1)] = id == (unsigned)e ? dpv : 0.f;
+      }
     if (pa.debug) {
 #pragma unroll
       for (int rr = 0; rr < RPW; ++rr)
 #pragma unroll
         for (int h = 0; h < 2; ++h) st4v(cx.G + img + tl(r0 + rr, h, lane), g[rr][h]);
     }
-    lds_barrier();
   }
   PK_STAMP(cx, 13);
-  __syncthreads();  // X[0] / SCODE (stem) and Y[9] are re-read from global by other threads from here on
+  lds_barrier();  // every wave is done with the head's LDS before the backward's tiles overwrite it
 
   // ======================= backward: 10 applications, newest first ========================================
   unsigned short* dyT = (unsigned short*)(U + P::U_DYT);
   unsigned short* xT = (unsigned short*)(U + P::U_XT);
-  stage_wt<NW>(WT, cx.wt_d);
   zero_xr_halo<NW>(XR);
   for (int idx = t; idx < 3 * 32 * P::XT_S * 2 / 16; idx += NTH) ((uint4*)xT)[idx] = uint4{0u, 0u, 0u, 0u};
-  float yb[RPW][2][4], xb[RPW][2][4];
-  {
-    const float* yp = cx.Y + (size_t)(NBLK - 1) * B * 8192 + img;
-    const float* xp = cx.X + (size_t)(NBLK - 1) * B * 8192 + img;
-#pragma unroll
-    for (int rr = 0; rr < RPW; ++rr)
-#pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        ld4v(yp + tl(r0 + rr, h, lane), yb[rr][h]);
-        ld4v(xp + tl(r0 + rr, h, lane), xb[rr][h]);
-      }
-  }
+
   f32x4 wacc[Gm::NNT][2];
 #pragma unroll
   for (int j = 0; j < Gm::NNT; ++j) wacc[j][0] = wacc[j][1] = z4();
@@ -1099,8 +1157,11 @@ __global__ void __launch_bounds__(256) k_pk_reduce(Ctx cx, PkArgs pa) {
     st4(cx.grads + base, a0);
     st4(cx.grads + base + 4, a1);
     if (cx.fuse_sgd) {
-      st4(cx.params + base, ld4(cx.params + base) - cx.lr * a0);
-      st4(cx.params + base + 4, ld4(cx.params + base + 4) - cx.lr * a1);
+      const f32x4 n0 = ld4(cx.params + base) - cx.lr * a0, n1 = ld4(cx.params + base + 4) - cx.lr * a1;
+      st4(cx.params + base, n0);
+      st4(cx.params + base + 4, n1);
+      *(uint4*)((unsigned short*)cx.w1b + base - OFF_FC1W) =
+          uint4{pk2(n0[0], n0[1]), pk2(n0[2], n0[3]), pk2(n1[0], n1[1]), pk2(n1[2], n1[3])};
     }
     return;
   }

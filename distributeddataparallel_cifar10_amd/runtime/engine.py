@@ -109,7 +109,7 @@ class EngineConfig:
     rows: int = 4                # multi-kernel engine: trunk rows per workgroup tile (2 or 4)
     persistent: Optional[bool] = None  # one-launch persistent trunk kernel (default: on for bf16)
     debug: bool = False          # persistent engine: also store per-block dy / residual grads (diagnostics)
-    pk_waves: int = 8            # persistent engine: waves per workgroup (8: 2 image rows per wave; or 4)
+    pk_waves: int = 8            # persistent engine: waves per workgroup (8: 2 image rows per wave)
     world_size: int = 1
     rank: int = 0
     comm: str = "rccl"           # world_size > 1: "rccl" (all-reduce inside the graph-captured step) or

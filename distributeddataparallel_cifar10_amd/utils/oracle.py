@@ -53,11 +53,12 @@ def _conv(mod, x, bf16_operands: bool):
 
 
 def reference_step(model, imgs_u8: torch.Tensor, labels: torch.Tensor, lr: float = 1e-2, apply_sgd: bool = True,
-                   bf16_operands: bool = False):
+                   bf16_operands: bool = False, fc1_bf16: bool = False):
     """One SGD step of `model` (mutated in place).  Returns a dict of intermediates and gradients.
 
     bf16_operands=True emulates the engine's bf16 mode (bf16 MFMA operands, fp32 everything else), so the
-    comparison isolates kernel bugs from bf16 rounding."""
+    comparison isolates kernel bugs from bf16 rounding; fc1_bf16=True additionally rounds the fc1 weight the
+    persistent engine reads (its head keeps a bf16 copy of fc1.weight)."""
     x = normalize_u8(imgs_u8)
     blk = model.resblocks[0]
     out0 = F.max_pool2d(torch.relu(_conv(model.conv1, x, bf16_operands)), 2)
@@ -73,7 +74,13 @@ def reference_step(model, imgs_u8: torch.Tensor, labels: torch.Tensor, lr: float
         xs.append(nxt)
         cur = nxt
     pooled = F.max_pool2d(cur, 2).view(-1, 8 * 8 * model.n_chans1)
-    logits = model.fc2(torch.relu(model.fc1(pooled)))
+    if fc1_bf16:  # persistent engine: fc1 forward and its input-gradient use a bf16 copy of the weight
+        w1 = model.fc1.weight
+        w1r = w1 + (_bf(w1) - w1).detach()  # straight-through: dW is taken w.r.t. the fp32 master weight
+        h = F.linear(pooled, w1r, model.fc1.bias)
+    else:
+        h = model.fc1(pooled)
+    logits = model.fc2(torch.relu(h))
     loss = F.cross_entropy(logits, labels.long())
     for p in model.parameters():
         p.grad = None

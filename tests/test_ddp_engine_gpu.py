@@ -19,7 +19,7 @@ pytestmark = pytest.mark.gpu
 WS, B, STEPS, NDATA = 2, 16, 3, 256
 
 
-def _simulate(model0, data, labels, order, lr, bf16):
+def _simulate(model0, data, labels, order, lr, bf16, fc1_bf16):
     from distributeddataparallel_cifar10_amd.utils.oracle import reference_step
     models = [copy.deepcopy(model0) for _ in range(WS)]
     for s in range(STEPS):
@@ -30,7 +30,8 @@ def _simulate(model0, data, labels, order, lr, bf16):
                 for k, v in models[r].named_buffers():
                     v.copy_(snap[k])
             sel = order[r][s * B:(s + 1) * B]
-            out = reference_step(models[r], data[sel], labels[sel], lr=lr, apply_sgd=False, bf16_operands=bf16)
+            out = reference_step(models[r], data[sel], labels[sel], lr=lr, apply_sgd=False, bf16_operands=bf16,
+                                 fc1_bf16=fc1_bf16)
             grads.append(out["grads"])
         with torch.no_grad():
             for r in range(WS):
@@ -72,7 +73,7 @@ def _worker(rank, port, dtype, persistent, q):
         eng.run_external(B, STEPS, allreduce)
         loss, steps = eng.read_loss()
         assert steps == STEPS
-        sim = _simulate(ref0, data, labels, order, 1e-2, dtype == "bf16")[rank]
+        sim = _simulate(ref0, data, labels, order, 1e-2, dtype == "bf16", persistent)[rank]
         tol = 1e-3 if dtype == "fp32" else 3e-2
         sd, rsd = model.state_dict(), sim.state_dict()
         for k in ("fc1.weight", "fc2.bias", "resblocks.0.conv.weight", "resblocks.0.batch_norm.weight",
