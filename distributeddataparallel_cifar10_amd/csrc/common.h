@@ -40,6 +40,7 @@ constexpr int N_STEM_RED_WG = SSLAB_N / RED_CHUNK;   // 34
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef short s4v __attribute__((ext_vector_type(4)));  // 4 bf16 bit patterns (16x16x16 MFMA operand)
 
 // Everything a kernel needs, passed by value (kernarg segment).
 struct Ctx {

@@ -80,15 +80,16 @@ struct Plan {
   // stem backward
   static constexpr int DSP = 1024 + 8;
   static constexpr int U_DST = 0;                      // [32][DSP] bf16 d(stem conv output), pixel-contiguous
-  static constexpr int U_XIN2 = 32 * DSP * 2;          // [3][34][34] f32
-  static constexpr int U_SRED = U_XIN2 + 13872;        // [16 waves][64 lanes][4] f32 stem-wgrad partials
-  static constexpr int SBWD_END = U_SRED + 16384;
+  static constexpr int XS_S = 40;                      // row stride (bf16) of the shifted input copies
+  static constexpr int U_XS = 32 * DSP * 2;            // [3 kw][3 ci][34 rows][XS_S] bf16: col c holds x[c + kw - 1]
+  static constexpr int U_SRED = U_XS + 9 * 34 * XS_S * 2;  // [8 waves][64 lanes][4] f32 stem-wgrad partials
+  static constexpr int SBWD_END = U_SRED + 8192;
   static constexpr int UNION = cmax(cmax(STEM_END, HEAD_END), cmax(BWD_END, SBWD_END));
   static constexpr int TOTAL = O_U + UNION;
 };
 static_assert(Plan::TOTAL <= 160 * 1024, "LDS budget");
 static_assert(Plan::U_XIN % 16 == 0 && Plan::U_SW % 16 == 0 && Plan::U_X0 % 16 == 0 && Plan::U_XT % 16 == 0 &&
-                  Plan::U_XIN2 % 16 == 0 && Plan::O_U % 16 == 0 && Plan::U_SRED % 16 == 0,
+                  Plan::U_XS % 16 == 0 && Plan::O_U % 16 == 0 && Plan::U_SRED % 16 == 0,
               "16-byte aligned carve");
 
 // Workgroup barrier for LDS-only hand-offs.  __syncthreads() also waits for every outstanding global load and
@@ -490,15 +491,17 @@ __global__ void __launch_bounds__(64 * NW) k_pk_step(Ctx cx, PkArgs pa) {
   PK_STAMP(cx, 0);
 
   // ======================= stem: gather + normalise + conv1 + bias + ReLU + 2x2 max-pool =================
+  // Input staged as bf16 NHWC4 pixels (3 channels + a zero), so an MFMA K-group of 4 is one tap of one pixel:
+  // v_mfma_f32_16x16x16_bf16 with K = (tap, channel), 3 MFMAs cover the 9 taps (taps 9..11 have zero weights).
   {
-    float* xin = (float*)(U + P::U_XIN);
+    uint2* xin4 = (uint2*)(U + P::U_XIN);  // [34][34] pixels, zero halo
     unsigned short* swl = (unsigned short*)(U + P::U_SW);
     const float* sb = misc + 874;
     float* x0i = (float*)(U + P::U_X0);
     // step constants -> misc: k < 64: BN gamma|beta -> misc[320 + k]; k >= 64 -> misc[384 + k]: running
     // mean|var (rank 0's base under DDP, reference CC4) [448,512), fc1 bias [512,544), W2 [544,864),
-    // b2 [864,874), conv1 bias [874,906), BN shifts [906,1226) (= P_KSHIFT).  Every load is issued before any
-    // is waited for.
+    // b2 [864,874), conv1 bias [874,906), BN shifts [906,1226) (= P_KSHIFT).  Every global load of the
+    // prologue is issued before any is waited for.
     constexpr int NKC = 842, KCM = (NKC + NTH - 1) / NTH;
     float kc[KCM];
 #pragma unroll
@@ -518,11 +521,21 @@ __global__ void __launch_bounds__(64 * NW) k_pk_step(Ctx cx, PkArgs pa) {
     }
     uint4 swv = ((const uint4*)cx.sw)[t & 127];
     int lab = cx.labels[sid];
+    const int tq = t & 255;  // threads < 256: pixels (y = tq >> 3, x = 4 (tq & 7) .. +3), all 3 channels
+    const unsigned* imw = (const unsigned*)(cx.data + (size_t)sid * 3072);
+    unsigned iw0 = imw[tq], iw1 = imw[256 + tq], iw2 = imw[512 + tq];
+    uint4 wt0, wt1, wt2;
+    stage_wt_load3(wt0, wt1, wt2, cx.wt_f);
 #pragma unroll
     for (int m = 0; m < KCM; ++m) pin(kc[m]);
     pin(swv);
     pin(lab);
-    stage_input<NW>(xin, cx.data + (size_t)sid * 3072);
+    pin(iw0);
+    pin(iw1);
+    pin(iw2);
+    pin(wt0);
+    pin(wt1);
+    pin(wt2);
 #pragma unroll
     for (int m = 0; m < KCM; ++m) {
       const int k = t + NTH * m;
@@ -530,48 +543,73 @@ __global__ void __launch_bounds__(64 * NW) k_pk_step(Ctx cx, PkArgs pa) {
     }
     if (t < 128) ((uint4*)swl)[t] = swv;
     if (t == 0) misc[P_LABEL] = __int_as_float(lab);  // label for the head's cross-entropy
-    stage_wt<NW>(WT, cx.wt_f);
+    if (t < 256) {
+      const int y = tq >> 3, x0 = 4 * (tq & 7);
+#pragma unroll
+      for (int b2 = 0; b2 < 4; ++b2) {
+        const unsigned c0 = bfbits(norm_px((iw0 >> (8 * b2)) & 255u, 0));
+        const unsigned c1 = bfbits(norm_px((iw1 >> (8 * b2)) & 255u, 1));
+        const unsigned c2 = bfbits(norm_px((iw2 >> (8 * b2)) & 255u, 2));
+        xin4[(y + 1) * 34 + x0 + 1 + b2] = uint2{c0 | (c1 << 16), c2};
+      }
+    } else if (tq < 132) {  // the 132 halo pixels: rows 0 / 33 (34 each), cols 0 / 33 of rows 1..32
+      const int px = tq < 34 ? tq : tq < 68 ? 33 * 34 + (tq - 34) : ((tq - 68) / 2 + 1) * 34 + ((tq - 68) & 1) * 33;
+      xin4[px] = uint2{0u, 0u};
+    }
+    stage_wt_store3(WT, wt0, wt1, wt2);
     zero_xr_halo<NW>(XR);
     lds_barrier();
     PK_STAMP(cx, 29);
-    int koff[8];
-    bool kval[8];
+    // B fragments (weights), fixed for the whole stem: lane (co = 16h + c, k-group q) of MFMA m holds
+    // W[co][ci = 0..2][tap = 4m + q] and a zero for the 4th channel
+    s4v bw[2][3];
 #pragma unroll
-    for (int s = 0; s < 8; ++s) {
-      const int k = 8 * q + s;
-      kval[s] = k < 27;
-      koff[s] = kval[s] ? (k / 9) * 34 * 34 + ((k % 9) / 3) * 34 + (k % 3) : 0;
-    }
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+      for (int m = 0; m < 3; ++m) {
+        const int tap = 4 * m + q, co = 16 * h + c;
+        const bool tv = tap < 9;
+        const int tc = tv ? tap : 0;
+        const unsigned short e0 = swl[co * 32 + tc], e1 = swl[co * 32 + 9 + tc], e2 = swl[co * 32 + 18 + tc];
+        bw[h][m] = s4v{(short)(tv ? e0 : 0), (short)(tv ? e1 : 0), (short)(tv ? e2 : 0), 0};
+      }
     uint8_t* scl = (uint8_t*)(U + P::U_SCODE);
 #pragma unroll 1
-    for (int j = 0; j < 64 / NW; ++j) {
-      const int u = w + NW * j, pr = u >> 2, chalf = (u >> 1) & 1, h = u & 1, co = 16 * h + c;
-      const int base0 = (2 * pr) * 34 + 16 * chalf + c;
-      const bf16x8 b = *(const bf16x8*)(swl + co * 32 + 8 * q);
-      bf16x8 v0, v1;
+    for (int j = 0; j < 32 / NW; ++j) {
+      const int u = w + NW * j, pr = u >> 1, chalf = u & 1;  // pool row pr, image cols 16 chalf .. +15
+      f32x4 acc[2][2];
 #pragma unroll
-      for (int s = 0; s < 8; ++s) {  // loads are unconditional (koff = 0 for padded k), the select is not
-        const float e0 = xin[koff[s] + base0], e1 = xin[koff[s] + base0 + 34];
-        v0[s] = (__bf16)(kval[s] ? e0 : 0.f);
-        v1[s] = (__bf16)(kval[s] ? e1 : 0.f);
+      for (int rw = 0; rw < 2; ++rw) {
+        acc[rw][0] = z4();
+        acc[rw][1] = z4();
+#pragma unroll
+        for (int m = 0; m < 3; ++m) {
+          const int tap = 4 * m + q, tc = tap < 9 ? tap : 0, kh = tc / 3, kw = tc % 3;
+          const uint2 av = xin4[(2 * pr + rw + kh) * 34 + 16 * chalf + c + kw];
+          const s4v a = __builtin_bit_cast(s4v, av);
+          acc[rw][0] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(a, bw[0][m], acc[rw][0], 0, 0, 0);
+          acc[rw][1] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(a, bw[1][m], acc[rw][1], 0, 0, 0);
+        }
       }
-      const f32x4 a0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(v0, b, z4(), 0, 0, 0);
-      const f32x4 a1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(v1, b, z4(), 0, 0, 0);
-      const float bias = sb[co];
 #pragma unroll
-      for (int pp = 0; pp < 2; ++pp) {
-        const float v00 = fmaxf(a0[2 * pp] + bias, 0.f), v01 = fmaxf(a0[2 * pp + 1] + bias, 0.f);
-        const float v10 = fmaxf(a1[2 * pp] + bias, 0.f), v11 = fmaxf(a1[2 * pp + 1] + bias, 0.f);
-        float best = v00;
-        int code = 0;
-        if (v01 > best) { best = v01; code = 1; }
-        if (v10 > best) { best = v10; code = 2; }
-        if (v11 > best) { best = v11; code = 3; }
-        if (best > 0.f) code |= 4;
-        const int pc = 8 * chalf + 2 * q + pp, po = (pr * 16 + pc) * 32 + co;
-        x0i[po] = best;
-        scl[po] = (uint8_t)code;
-        st1r(XR, (pr + 1) * 18 + pc + 1, co, best);
+      for (int h = 0; h < 2; ++h) {
+        const int co = 16 * h + c;
+        const float bias = sb[co];
+#pragma unroll
+        for (int pp = 0; pp < 2; ++pp) {
+          const float v00 = fmaxf(acc[0][h][2 * pp] + bias, 0.f), v01 = fmaxf(acc[0][h][2 * pp + 1] + bias, 0.f);
+          const float v10 = fmaxf(acc[1][h][2 * pp] + bias, 0.f), v11 = fmaxf(acc[1][h][2 * pp + 1] + bias, 0.f);
+          float best = v00;
+          int code = 0;
+          if (v01 > best) { best = v01; code = 1; }
+          if (v10 > best) { best = v10; code = 2; }
+          if (v11 > best) { best = v11; code = 3; }
+          if (best > 0.f) code |= 4;
+          const int pc = 8 * chalf + 2 * q + pp, po = (pr * 16 + pc) * 32 + co;
+          x0i[po] = best;
+          scl[po] = (uint8_t)code;
+          st1r(XR, (pr + 1) * 18 + pc + 1, co, best);
+        }
       }
     }
     PK_STAMP(cx, 30);
@@ -985,12 +1023,10 @@ __global__ void __launch_bounds__(64 * NW) k_pk_step(Ctx cx, PkArgs pa) {
   // ======================= stem backward: max-pool bwd (saved argmax) -> ReLU mask -> conv1 wgrad ==========
   lds_barrier();  // every wave is done with the backward's LDS regions
   {
-    unsigned short* dsT = (unsigned short*)(U + P::U_DST);
-    float* xin = (float*)(U + P::U_XIN2);
-    for (int idx = t; idx < 32 * P::DSP * 2 / 16; idx += NTH) ((uint4*)dsT)[idx] = uint4{0u, 0u, 0u, 0u};
-    stage_input_store<NW>(xin, imgw);
-    lds_barrier();
-    PK_STAMP(cx, 34);
+    unsigned short* dsT = (unsigned short*)(U + P::U_DST);  // [32 co][DSP] bf16 d(stem conv output)
+    unsigned short* xs = (unsigned short*)(U + P::U_XS);
+    // d(conv1 output): every 2x2 pool window written whole (value at the argmax if the ReLU was active, zeros
+    // elsewhere), so dsT needs no clearing pass
     float db0 = 0.f, db1 = 0.f;
 #pragma unroll
     for (int rr = 0; rr < RPW; ++rr)
@@ -998,49 +1034,72 @@ __global__ void __launch_bounds__(64 * NW) k_pk_step(Ctx cx, PkArgs pa) {
       for (int h = 0; h < 2; ++h)
 #pragma unroll
         for (int i2 = 0; i2 < 4; ++i2) {
-          const int code = (codew[rr][h] >> (8 * i2)) & 255u;
-          if (code & 4) {
-            const int pos = code & 3, col = 4 * q + i2, ch = 16 * h + c;
-            const int sr = 2 * (r0 + rr) + (pos >> 1), sc = 2 * col + (pos & 1);
-            dsT[ch * P::DSP + sr * 32 + sc] = bfbits(g[rr][h][i2]);
-            if (h == 0) db0 += g[rr][h][i2];
-            else db1 += g[rr][h][i2];
-          }
+          const unsigned code = (codew[rr][h] >> (8 * i2)) & 255u, pos = code & 3u;
+          const float val = (code & 4u) ? g[rr][h][i2] : 0.f;
+          const unsigned vb = bfbits(val);
+          const int ch = 16 * h + c, sr = 2 * (r0 + rr), sc = 2 * (4 * q + i2);
+          unsigned short* d0 = dsT + ch * P::DSP + sr * 32 + sc;
+          *(unsigned*)d0 = (pos == 0 ? vb : 0u) | ((pos == 1 ? vb : 0u) << 16);
+          *(unsigned*)(d0 + 32) = (pos == 2 ? vb : 0u) | ((pos == 3 ? vb : 0u) << 16);
+          if (h == 0) db0 += val;
+          else db1 += val;
         }
+    // three column-shifted bf16 copies of the normalised input (copy kw, col c holds x[c + kw - 1]); row r + 1
+    // holds image row r, rows 0 / 33 are the zero halo
+#pragma unroll
+    for (int m = 0; m < Gm::IMW; ++m) {
+      const int idx = t + NTH * m;
+      if (idx < 768) {
+        const int ch = idx >> 8, row = ((idx >> 3) & 31) + 1, x0 = 4 * (idx & 7);
+        unsigned bb[4];
+#pragma unroll
+        for (int b2 = 0; b2 < 4; ++b2) bb[b2] = bfbits(norm_px((imgw[m] >> (8 * b2)) & 255u, ch));
+        unsigned short* p1 = xs + ((3 + ch) * 34 + row) * P::XS_S + x0;  // kw = 1
+        *(uint2*)p1 = uint2{bb[0] | (bb[1] << 16), bb[2] | (bb[3] << 16)};
+        unsigned short* p0 = xs + ((0 + ch) * 34 + row) * P::XS_S + x0;  // kw = 0: col c holds x[c - 1]
+        p0[1] = (unsigned short)bb[0];
+        *(unsigned*)(p0 + 2) = bb[1] | (bb[2] << 16);
+        if (x0 + 4 < 32) p0[4] = (unsigned short)bb[3];
+        unsigned short* p2 = xs + ((6 + ch) * 34 + row) * P::XS_S + x0;  // kw = 2: col c holds x[c + 1]
+        if (x0 > 0) p2[-1] = (unsigned short)bb[0];
+        *(unsigned*)p2 = bb[1] | (bb[2] << 16);
+        p2[2] = (unsigned short)bb[3];
+      }
+    }
+    if (t < 72) {  // halo rows 0 and 33 of the 9 planes (32 cols = 4 x 16 B each)
+      const int plane = t >> 3, row = (t >> 2) & 1 ? 33 : 0, part = t & 3;
+      *(uint4*)(xs + (plane * 34 + row) * P::XS_S + 8 * part) = uint4{0u, 0u, 0u, 0u};
+    } else if (t < 72 + 192) {  // kw = 0: col 0 (x[-1]); kw = 2: col 31 (x[32]) of rows 1..32
+      const int e = t - 72, kwe = e < 96 ? 0 : 2, ci = (e % 96) >> 5, row = (e & 31) + 1;
+      xs[((kwe * 3 + ci) * 34 + row) * P::XS_S + (kwe ? 31 : 0)] = 0;
+    }
     img_csum2<NW>(db0, db1, 0.f, 0.f, cred, misc + 384, misc + 416);  // also the barrier before the MFMAs
+    PK_STAMP(cx, 34);
     float* ss = cx.SSLAB + (size_t)n * SSLAB_N;
     if (t < 32) ss[1024 + t] = misc[384 + t];
-    // D[co][k] = sum over 1024 stem pixels of ds[p][co] * im2col[p][k];
-    // combo = (tile, row quarter): tile = combo & 3 (mt = tile & 1, nt = tile >> 1), rows 8*(combo>>2) .. +8
-    float* sred = (float*)(U + P::U_SRED);
-#pragma unroll
-    for (int cb = 0; cb < Gm::SBC; ++cb) {
-      const int combo = w + NW * cb, tile = combo & 3, part = combo >> 2, mt = tile & 1, nt = tile >> 1;
-      const int kidx = 16 * nt + c, co = 16 * mt + c;
-      const bool kv = kidx < 27;
-      const float* xb2 = xin + (kv ? (kidx / 9) * 34 * 34 + ((kidx % 9) / 3) * 34 + (kidx % 3) : 0);
+    // D[co][k] = sum over the 1024 stem pixels of ds[p][co] * im2col[p][k], K step = one image row.
+    // Wave w: tile w & 3 (mt = co half, nt = k tile), rows 16 (w >> 2) .. +15; k >= 27 columns are discarded.
+    {
+      const int tile = w & 3, mt = tile & 1, nt = tile >> 1, r0s = 16 * (w >> 2);
+      const int kidx = 16 * nt + c, kk = kidx < 27 ? kidx : 0, ci = kk / 9, kh = (kk % 9) / 3, kw = kk % 3;
+      const unsigned short* abase = dsT + (16 * mt + c) * P::DSP + 8 * q;
+      const unsigned short* bbase = xs + ((kw * 3 + ci) * 34 + kh) * P::XS_S + 8 * q;
       f32x4 acc2 = z4();
-#pragma unroll 2
-      for (int s = 8 * part; s < 8 * part + 8; ++s) {
-        const bf16x8 a = *(const bf16x8*)(dsT + co * P::DSP + s * 32 + 8 * q);
-        bf16x8 b;
-#pragma unroll
-        for (int jj = 0; jj < 8; ++jj) {
-          const float e = xb2[s * 34 + 8 * q + jj];  // unconditional load, select after
-          b[jj] = (__bf16)(kv ? e : 0.f);
-        }
+#pragma unroll 4
+      for (int sr = r0s; sr < r0s + 16; ++sr) {
+        const bf16x8 a = *(const bf16x8*)(abase + sr * 32);
+        const bf16x8 b = *(const bf16x8*)(bbase + sr * P::XS_S);
         acc2 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, acc2, 0, 0, 0);
       }
-      st4(sred + ((combo * 64 + lane) << 2), acc2);  // [16 combos][64 lanes][4]
+      float* sred = (float*)(U + P::U_SRED);
+      st4(sred + ((w * 64 + lane) << 2), acc2);  // [8 waves][64 lanes][4]
     }
     PK_STAMP(cx, 35);
     lds_barrier();
     if (t < 256) {
+      const float* sred = (const float*)(U + P::U_SRED);
       const int tile = t >> 6, ln = t & 63;
-      f32x4 s4 = z4();
-#pragma unroll
-      for (int pt = 0; pt < 4; ++pt) s4 += ld4(sred + (((pt * 4 + tile) * 64 + ln) << 2));
-      st4(ss + ((tile * 64 + ln) << 2), s4);
+      st4(ss + ((tile * 64 + ln) << 2), ld4(sred + ((tile * 64 + ln) << 2)) + ld4(sred + (((tile + 4) * 64 + ln) << 2)));
     }
   }
   // trunk wgrad slab (accumulated over the 10 applications)
