@@ -162,13 +162,13 @@ __device__ __forceinline__ void img_csum2(float a0, float a1, float b0, float b1
   lds_barrier();
 }
 
-// one sweep pass over the granules of round `tag`: KS loads per lane, all issued before any is waited for
-// (a guarded load per slot would be compiled into KS serial round trips).  Slots past the grid read a valid
-// granule (clamped index) and are then replaced by a neutral (0, tag) pair.
+// one sweep pass over the granules of a round: KS loads per lane, all issued before any is waited for (a
+// guarded load per slot would be compiled into KS serial round trips).  Slots past the grid read a valid granule
+// (clamped index) and are then replaced by a neutral (0, tag) pair.  Split in issue / evaluate halves so a pass
+// can be issued early and evaluated after independent work.
 template <int NW, int KS>
-__device__ __forceinline__ bool sweep(const __amdgpu_buffer_rsrc_t rs, int w, int lane, int G, unsigned tag,
-                                      float& s1) {
-  unsigned lo[KS], hi[KS];
+__device__ __forceinline__ void sweep_load(const __amdgpu_buffer_rsrc_t rs, int w, int lane, int G, unsigned (&lo)[KS],
+                                           unsigned (&hi)[KS]) {
 #pragma unroll
   for (int kk = 0; kk < KS; ++kk) {
     const int k = w + NW * kk, kc = k < G ? k : G - 1;
@@ -176,6 +176,10 @@ __device__ __forceinline__ bool sweep(const __amdgpu_buffer_rsrc_t rs, int w, in
     lo[kk] = x[0];
     hi[kk] = x[1];
   }
+}
+template <int NW, int KS>
+__device__ __forceinline__ bool sweep_eval(int w, int G, unsigned tag, const unsigned (&lo)[KS], const unsigned (&hi)[KS],
+                                           float& s1) {
   bool ok = true;
   s1 = 0.f;
 #pragma unroll
@@ -185,6 +189,16 @@ __device__ __forceinline__ bool sweep(const __amdgpu_buffer_rsrc_t rs, int w, in
     s1 += valid ? __uint_as_float(lo[kk]) : 0.f;
   }
   return ok;
+}
+template <int NW, int KS>
+__device__ __forceinline__ bool sweep(const __amdgpu_buffer_rsrc_t rs, int w, int lane, int G, unsigned tag,
+                                      float& s1) {
+  unsigned lo[KS], hi[KS];
+  sweep_load<NW, KS>(rs, w, lane, G, lo, hi);
+  return sweep_eval<NW, KS>(w, G, tag, lo, hi, s1);
+}
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t gran_rsrc(const PkArgs& pa, int round) {
+  return __builtin_amdgcn_make_buffer_rsrc(pa.gran + (size_t)(round & 1) * 64 * 64, (short)0, 64 * 64 * 8, 0x00020000);
 }
 
 // Per-image channel sums of per-thread C-layout partials, delivered straight to the publishing threads: on
@@ -230,16 +244,28 @@ __device__ __forceinline__ void xchg_publish(const PkArgs& pa, int epoch, int ro
     __hip_atomic_store(buf + blockIdx.x * 64 + t, ((unsigned long long)tag << 32) | __float_as_uint(v),
                        __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
+// Early pass for xchg_wait (batch <= 32): issue it, do independent work, then hand it to xchg_wait.
 template <int NW>
-__device__ float xchg_wait(const PkArgs& pa, int epoch, int round, float* cred) {
+struct EarlyPass {
+  static constexpr int KS = (32 + NW - 1) / NW;
+  unsigned lo[KS], hi[KS];
+};
+template <int NW>
+__device__ __forceinline__ void xchg_early(const PkArgs& pa, int round, EarlyPass<NW>& ep) {
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  if (gridDim.x <= 32) sweep_load<NW, EarlyPass<NW>::KS>(gran_rsrc(pa, round), w, threadIdx.x & 63, gridDim.x, ep.lo, ep.hi);
+}
+template <int NW>
+__device__ float xchg_wait(const PkArgs& pa, int epoch, int round, float* cred, const EarlyPass<NW>* ep = nullptr) {
   constexpr int KSW = Geo<NW>::KSW, KSH = (32 + NW - 1) / NW;
   const int t = threadIdx.x, lane = t & 63, G = gridDim.x;
   const int w = __builtin_amdgcn_readfirstlane(t >> 6);  // wave-uniform -> scalar branches in the sweep
   const unsigned tag = (unsigned)(epoch * 64 + round + 1);
-  unsigned long long* buf = pa.gran + (size_t)(round & 1) * 64 * 64;
-  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(buf, (short)0, 64 * 64 * 8, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rs = gran_rsrc(pa, round);
   float s1 = 0.f;
-  for (unsigned spins = 0;; ++spins) {
+  bool done = false;
+  if (ep != nullptr && G <= 32) done = __all(sweep_eval<NW, KSH>(w, G, tag, ep->lo, ep->hi, s1));
+  for (unsigned spins = 0; !done; ++spins) {
     asm volatile("" ::: "memory");  // the granule loads are re-issued every pass (no hoisting out of the spin)
     const bool ok = G <= 32 ? sweep<NW, KSH>(rs, w, lane, G, tag, s1) : sweep<NW, KSW>(rs, w, lane, G, tag, s1);
     if (__all(ok)) break;
@@ -922,6 +948,8 @@ __global__ void __launch_bounds__(64 * NW) k_pk_step(Ctx cx, PkArgs pa) {
     // XR by block i + 1's dgrad) before x_i replaces them.
     if (i < NBLK - 1) wgrad_acc<NW>(dyT, xT, wacc, w, lane);
     if (i == 5) PK_STAMP(cx, 38);
+    EarlyPass<NW> ep;  // first sweep pass issued now, evaluated after the x tile writes
+    xchg_early<NW>(pa, NBLK + (NBLK - 1 - i), ep);
     lds_barrier();
 #pragma unroll
     for (int rr = 0; rr < RPW; ++rr)
@@ -943,7 +971,7 @@ __global__ void __launch_bounds__(64 * NW) k_pk_step(Ctx cx, PkArgs pa) {
       }
     if (i == 5) PK_STAMP(cx, 27);
     {
-      const float tot = xchg_wait<NW>(pa, epoch, NBLK + (NBLK - 1 - i), cred);
+      const float tot = xchg_wait<NW>(pa, epoch, NBLK + (NBLK - 1 - i), cred, &ep);
       if (t < 64) misc[64 + t] = tot;  // batch sums: [64, 96) sum dz, [96, 128) sum dz * xhat
       lds_barrier();
     }
