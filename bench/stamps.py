@@ -51,6 +51,8 @@ PK_INTERVALS = ([("stem", 0, 1), ("stem.stage", 0, 29), ("stem.mfma", 29, 30), (
                 [("stem_bwd", 23, 24), ("stem_bwd.stage", 23, 34), ("stem_bwd.mfma", 34, 35),
                  ("stem_bwd.tail", 35, 24),
                  ("fwd5_pre_xchg", 7, 25), ("fwd5_xchg", 25, 26), ("fwd6_apply", 26, 39), ("fwd6_conv", 39, 8),
+                 ("head.ce.hh", 32, 40), ("head.ce.logits", 40, 41), ("head.ce.softmax_dh", 41, 42),
+                 ("head.ce.rest", 42, 33), ("stem.bfrag", 29, 43), ("stem.iter0", 43, 44), ("stem.iter1-3", 44, 30),
                  ("bwd5.dz+csum+pub", 17, 36), ("bwd5.wgrad6", 36, 38), ("bwd5.xT", 38, 27), ("bwd5_wait", 27, 28),
                  ("bwd5.dy", 28, 37), ("bwd5.dgrad", 37, 18)])
 

@@ -85,6 +85,7 @@ struct Ctx {
   uint8_t* HCODE;  // [B][64][32] head max-pool argmax
   int pstride;     // FPART/BPART stride per block (>= max nparts)
   void* w1b;                   // [32][2048] bf16 copy of fc1.weight (persistent engine's head; kept by every SGD)
+  void* swf;                   // [2 co half][3 k group][64 lanes][4] bf16 conv1 weights as 16x16x16 MFMA B fragments
   unsigned long long* stamps;  // [32 kernel slots][256 wg][8 stamps][2] (diagnostic DCA_STAMPS builds only)
 };
 
@@ -115,6 +116,12 @@ __device__ __forceinline__ int sample_id(const Ctx& cx, int n) {
   pos = pos < 0 ? 0 : (pos >= cx.n_idx ? cx.n_idx - 1 : pos);
   int id = cx.indices[pos];
   return id < 0 ? 0 : (id >= cx.n_data ? cx.n_data - 1 : id);
+}
+
+// conv1 weight element (co, k = ci * 9 + tap) -> its slot in the persistent stem's MFMA B fragments
+__device__ __forceinline__ int swf_slot(int co, int k) {
+  const int ci = k / 9, tap = k % 9;
+  return (((co >> 4) * 3 + (tap >> 2)) * 64 + 16 * (tap & 3) + (co & 15)) * 4 + ci;
 }
 
 __device__ __forceinline__ unsigned short f2bf(float f) {

@@ -143,7 +143,7 @@ static int alloc_workspace(Engine* e) {
       {"RS_BASE", 64 * 4},           {"CURSOR", 16},                  {"STEPS", 16},
       {"LOSS", 16},                  {"STAMPS", 32 * 256 * 8 * 2 * 8},
       {"GRAN", 2 * 64 * 64 * 8},     {"EPOCH", 16},                   {"ERR", 16},
-      {"TSLAB", bmax * WSLAB_N * 4}, {"BNG", 64 * 4}, {"IDS", 64 * 4}, {"W1B", 65536 * 2},
+      {"TSLAB", bmax * WSLAB_N * 4}, {"BNG", 64 * 4}, {"IDS", 64 * 4}, {"W1B", 65536 * 2}, {"SWF", 2 * 3 * 64 * 4 * 2},
   };
   size_t total = 0;
   for (auto& r : regs) total += align_up(r.bytes, 256);
@@ -183,6 +183,7 @@ static int alloc_workspace(Engine* e) {
   c.pstride = (int)pstride;
   c.stamps = (unsigned long long*)e->regions["STAMPS"];
   c.w1b = e->regions["W1B"];
+  c.swf = e->regions["SWF"];
   e->pa.gran = (unsigned long long*)e->regions["GRAN"];
   e->pa.epoch = (int*)e->regions["EPOCH"];
   e->pa.err = (unsigned*)e->regions["ERR"];

@@ -1381,6 +1381,7 @@ __global__ void __launch_bounds__(NT) k_apply_sgd(Ctx cx, int mode) {
     } else if (e >= OFF_C1W && e < OFF_C1W + 864) {
       const int r = e - OFF_C1W, co = r / 27, k = r % 27;
       put_w<BF>(cx.sw, co * 32 + k, w);
+      ((unsigned short*)cx.swf)[swf_slot(co, k)] = bfbits(w);
     }
   }
   if (gid < 64) {
@@ -1388,6 +1389,10 @@ __global__ void __launch_bounds__(NT) k_apply_sgd(Ctx cx, int mode) {
     else cx.rs_base[gid] = gid < 32 ? cx.rm[gid] : cx.rv[gid - 32];
   }
   if (!mode && gid < 32 * 5) put_w<BF>(cx.sw, (gid / 5) * 32 + 27 + gid % 5, 0.f);
+  if (!mode && gid < 2 * 3 * 64 * 4) {  // the never-written zero slots of the stem fragments (4th channel, taps 9..11)
+    const int ci = gid & 3, lane = (gid >> 2) & 63, m = (gid >> 8) % 3, tap = 4 * m + (lane >> 4);
+    if (ci == 3 || tap >= 9) ((unsigned short*)cx.swf)[gid] = 0;
+  }
 }
 
 }  // namespace dca

@@ -59,8 +59,9 @@ struct Plan {
   static constexpr int U_XIN = U_XR_END;               // [3][34][34] f32 normalised input
   static constexpr int U_SW = U_XIN + 13872;           // [32][32] bf16 stem weight
   static constexpr int U_SB = U_SW + 2048;             // [32] f32 stem bias
-  static constexpr int U_X0 = U_SB + 128;              // [256][32] f32 pooled stem output
-  static constexpr int U_SCODE = U_X0 + 32768;         // [256][32] u8 stem pool argmax (re-laid out for global)
+  static constexpr int X0S = 36;                       // pixel stride (f32) of the pooled stem output
+  static constexpr int U_X0 = U_SB + 128;              // [256][X0S] f32 pooled stem output
+  static constexpr int U_SCODE = U_X0 + 256 * X0S * 4; // [256][32] u8 stem pool argmax (re-laid out for global)
   static constexpr int STEM_END = U_SCODE + 8192;
   // head
   static constexpr int U_X10 = 0;                      // [256][32] f32
@@ -521,7 +522,6 @@ __global__ void __launch_bounds__(64 * NW) k_pk_step(Ctx cx, PkArgs pa) {
   // v_mfma_f32_16x16x16_bf16 with K = (tap, channel), 3 MFMAs cover the 9 taps (taps 9..11 have zero weights).
   {
     uint2* xin4 = (uint2*)(U + P::U_XIN);  // [34][34] pixels, zero halo
-    unsigned short* swl = (unsigned short*)(U + P::U_SW);
     const float* sb = misc + 874;
     float* x0i = (float*)(U + P::U_X0);
     // step constants -> misc: k < 64: BN gamma|beta -> misc[320 + k]; k >= 64 -> misc[384 + k]: running
@@ -545,16 +545,21 @@ __global__ void __launch_bounds__(64 * NW) k_pk_step(Ctx cx, PkArgs pa) {
                                  : (const float*)cx.STATS + 2 * (k - 522);  // BN shifts (.x = mean)
       kc[m] = *src;
     }
-    uint4 swv = ((const uint4*)cx.sw)[t & 127];
     int lab = cx.labels[sid];
     const int tq = t & 255;  // threads < 256: pixels (y = tq >> 3, x = 4 (tq & 7) .. +3), all 3 channels
     const unsigned* imw = (const unsigned*)(cx.data + (size_t)sid * 3072);
     unsigned iw0 = imw[tq], iw1 = imw[256 + tq], iw2 = imw[512 + tq];
     uint4 wt0, wt1, wt2;
     stage_wt_load3(wt0, wt1, wt2, cx.wt_f);
+    // B fragments (conv1 weights) for the whole stem, prepared by the SGD kernels: lane (co = 16h + c,
+    // k-group q) of MFMA m holds W[co][ci = 0..2][tap = 4m + q] and a zero (4th channel / taps 9..11)
+    uint2 bwr[2][3];
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+      for (int m = 0; m < 3; ++m) bwr[h][m] = ((const uint2*)cx.swf)[(h * 3 + m) * 64 + lane];
 #pragma unroll
     for (int m = 0; m < KCM; ++m) pin(kc[m]);
-    pin(swv);
     pin(lab);
     pin(iw0);
     pin(iw1);
@@ -563,11 +568,17 @@ __global__ void __launch_bounds__(64 * NW) k_pk_step(Ctx cx, PkArgs pa) {
     pin(wt1);
     pin(wt2);
 #pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+      for (int m = 0; m < 3; ++m) {
+        pin(bwr[h][m].x);
+        pin(bwr[h][m].y);
+      }
+#pragma unroll
     for (int m = 0; m < KCM; ++m) {
       const int k = t + NTH * m;
       if (k < NKC) misc[(k < 64 ? 320 : 384) + k] = k >= 522 && !(fabsf(kc[m]) < 1e30f) ? 0.f : kc[m];
     }
-    if (t < 128) ((uint4*)swl)[t] = swv;
     if (t == 0) misc[P_LABEL] = __int_as_float(lab);  // label for the head's cross-entropy
     if (t < 256) {
       const int y = tq >> 3, x0 = 4 * (tq & 7);
@@ -586,22 +597,16 @@ __global__ void __launch_bounds__(64 * NW) k_pk_step(Ctx cx, PkArgs pa) {
     zero_xr_halo<NW>(XR);
     lds_barrier();
     PK_STAMP(cx, 29);
-    // B fragments (weights), fixed for the whole stem: lane (co = 16h + c, k-group q) of MFMA m holds
-    // W[co][ci = 0..2][tap = 4m + q] and a zero for the 4th channel
     s4v bw[2][3];
 #pragma unroll
     for (int h = 0; h < 2; ++h)
 #pragma unroll
-      for (int m = 0; m < 3; ++m) {
-        const int tap = 4 * m + q, co = 16 * h + c;
-        const bool tv = tap < 9;
-        const int tc = tv ? tap : 0;
-        const unsigned short e0 = swl[co * 32 + tc], e1 = swl[co * 32 + 9 + tc], e2 = swl[co * 32 + 18 + tc];
-        bw[h][m] = s4v{(short)(tv ? e0 : 0), (short)(tv ? e1 : 0), (short)(tv ? e2 : 0), 0};
-      }
+      for (int m = 0; m < 3; ++m) bw[h][m] = __builtin_bit_cast(s4v, bwr[h][m]);
     uint8_t* scl = (uint8_t*)(U + P::U_SCODE);
+    PK_STAMP(cx, 43);
 #pragma unroll 1
     for (int j = 0; j < 32 / NW; ++j) {
+      if (j == 1) PK_STAMP(cx, 44);
       const int u = w + NW * j, pr = u >> 1, chalf = u & 1;  // pool row pr, image cols 16 chalf .. +15
       f32x4 acc[2][2];
 #pragma unroll
@@ -632,7 +637,7 @@ __global__ void __launch_bounds__(64 * NW) k_pk_step(Ctx cx, PkArgs pa) {
           if (v11 > best) { best = v11; code = 3; }
           if (best > 0.f) code |= 4;
           const int pc = 8 * chalf + 2 * q + pp, po = (pr * 16 + pc) * 32 + co;
-          x0i[po] = best;
+          x0i[(pr * 16 + pc) * P::X0S + co] = best;
           scl[po] = (uint8_t)code;
           st1r(XR, (pr + 1) * 18 + pc + 1, co, best);
         }
@@ -650,7 +655,7 @@ __global__ void __launch_bounds__(64 * NW) k_pk_step(Ctx cx, PkArgs pa) {
 #pragma unroll
       for (int h = 0; h < 2; ++h)
 #pragma unroll
-        for (int i = 0; i < 4; ++i) x[rr][h][i] = x0i[el(r0 + rr, q, c, h, i)];
+        for (int i = 0; i < 4; ++i) x[rr][h][i] = x0i[((r0 + rr) * 16 + 4 * q + i) * P::X0S + 16 * h + c];
     // x0 and the stem pool codes go to global in the tiled layout, written by the very threads that read them
     // back in the backward (so no workgroup-wide memory barrier is ever needed for them)
     const uint8_t* scl = (const uint8_t*)(U + P::U_SCODE);
@@ -796,22 +801,27 @@ __global__ void __launch_bounds__(64 * NW) k_pk_step(Ctx cx, PkArgs pa) {
 #pragma unroll
         for (int k2 = 0; k2 < NW; ++k2) hh += hp[k2 * 32 + lane];
       }
+      PK_STAMP(cx, 40);
       const float hr = fmaxf(hh, 0.f);
       const int o = lane < 10 ? lane : 0;
       float logit = misc[864 + o];
 #pragma unroll
       for (int j = 0; j < 32; ++j)
         logit += misc[544 + o * 32 + j] * __int_as_float(__builtin_amdgcn_readlane(__float_as_int(hr), j));
+      PK_STAMP(cx, 41);
       float lg[10];  // the 10 logits, broadcast to every lane (scalar reads, no LDS shuffles)
 #pragma unroll
       for (int oo = 0; oo < 10; ++oo) lg[oo] = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(logit), oo));
       float mx = lg[0];
 #pragma unroll
       for (int oo = 1; oo < 10; ++oo) mx = fmaxf(mx, lg[oo]);
-      float se = 0.f;
+      float ex[10], se = 0.f;
 #pragma unroll
-      for (int oo = 0; oo < 10; ++oo) se += expf(lg[oo] - mx);
-      const float lse = mx + logf(se);
+      for (int oo = 0; oo < 10; ++oo) {
+        ex[oo] = __expf(lg[oo] - mx);
+        se += ex[oo];
+      }
+      const float lse = mx + __logf(se), rse = 1.f / se;
       const int label = __float_as_int(misc[P_LABEL]);
       float lt = lg[0];
 #pragma unroll
@@ -821,11 +831,12 @@ __global__ void __launch_bounds__(64 * NW) k_pk_step(Ctx cx, PkArgs pa) {
       float sd = 0.f, dl = 0.f;
 #pragma unroll
       for (int oo = 0; oo < 10; ++oo) {
-        const float dlo = (expf(lg[oo] - lse) - (oo == label ? 1.f : 0.f)) * invB;
+        const float dlo = (ex[oo] * rse - (oo == label ? 1.f : 0.f)) * invB;
         sd += misc[544 + oo * 32 + (lane & 31)] * dlo;
         dl = lane == oo ? dlo : dl;
       }
       const float dh = hh > 0.f ? sd : 0.f;
+      PK_STAMP(cx, 42);
       if (lane < 32) {
         hp[256 + lane] = dh;
         cx.HDH[n * 32 + lane] = dh;
@@ -1202,7 +1213,11 @@ __global__ void __launch_bounds__(256) k_pk_reduce(Ctx cx, PkArgs pa) {
           if (k < 27) {
             const int pidx = OFF_C1W + co * 27 + k;
             sgd_put(cx, pidx, tot[ii]);
-            if (cx.fuse_sgd) ((unsigned short*)cx.sw)[co * 32 + k] = bfbits(cx.params[pidx]);
+            if (cx.fuse_sgd) {
+              const unsigned short wb = bfbits(cx.params[pidx]);
+              ((unsigned short*)cx.sw)[co * 32 + k] = wb;
+              ((unsigned short*)cx.swf)[swf_slot(co, k)] = wb;
+            }
           }
         } else if (e < 1056) {
           sgd_put(cx, OFF_C1B + (e - 1024), tot[ii]);
