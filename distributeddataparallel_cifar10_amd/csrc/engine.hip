@@ -11,6 +11,7 @@
 #include <rccl/rccl.h>
 
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <map>
 #include <string>
@@ -88,6 +89,7 @@ struct Engine {
   std::map<int, hipGraphExec_t> graphs;
   bool persistent = false;
   int pk_waves = 8;
+  int xpack = 0;  // experimental one-XCD placement of the persistent kernel (env DCA_PK_XPACK=1)
   pk::PkArgs pa{};
   std::map<std::string, void*> regions;
   // dynamic LDS sizes
@@ -143,7 +145,7 @@ static int alloc_workspace(Engine* e) {
       {"RS_BASE", 64 * 4},           {"CURSOR", 16},                  {"STEPS", 16},
       {"LOSS", 16},                  {"STAMPS", 32 * 256 * 8 * 2 * 8},
       {"GRAN", 2 * 64 * 64 * 8},     {"EPOCH", 16},                   {"ERR", 16},
-      {"TSLAB", bmax * WSLAB_N * 4}, {"BNG", 64 * 4}, {"IDS", 64 * 4}, {"W1B", 65536 * 2}, {"SWF", 2 * 3 * 64 * 4 * 2},
+      {"TSLAB", bmax * WSLAB_N * 4}, {"BNG", 64 * 4}, {"IDS", 64 * 4}, {"W1B", 65536 * 2}, {"XCC", 64 * 8}, {"SWF", 2 * 3 * 64 * 4 * 2},
   };
   size_t total = 0;
   for (auto& r : regs) total += align_up(r.bytes, 256);
@@ -190,6 +192,7 @@ static int alloc_workspace(Engine* e) {
   e->pa.tslab = (float*)e->regions["TSLAB"];
   e->pa.bng = (float*)e->regions["BNG"];
   e->pa.ids = (int*)e->regions["IDS"];
+  e->pa.xcc = (unsigned long long*)e->regions["XCC"];
   e->pa.debug = e->in.debug;
   return 0;
 }
@@ -214,7 +217,12 @@ static int enqueue_step_persistent(Engine* e, int B, int part) {
   Ctx cx = e->base;
   cx.B = B;
   if (part != 2) {
-    hipLaunchKernelGGL(pk::k_pk_step<8>, dim3(B), dim3(64 * 8), pk::Plan::TOTAL, e->st, cx, e->pa);
+    pk::PkArgs pa = e->pa;
+    // Packing the image workgroups onto one XCD (grid 8 x B, see pk_img) keeps the BN exchange inside one L2,
+    // but measured slower end to end (119 vs 105 us/step: every workgroup then shares one L2 and its
+    // bandwidth); opt-in for experiments only (DCA_PK_XPACK=1).
+    pa.xpack = (B <= 32 && e->xpack) ? 1 : 0;
+    hipLaunchKernelGGL(pk::k_pk_step<8>, dim3(pa.xpack ? 8 * B : B), dim3(64 * 8), pk::Plan::TOTAL, e->st, cx, pa);
     hipLaunchKernelGGL(pk::k_pk_reduce, dim3(pk::R_GRID), dim3(256), 0, e->st, cx, e->pa);
   }
   if (e->in.world_size > 1) {
@@ -458,6 +466,10 @@ int dca_engine_create(const DcaInit* in, int n_indices, void** out) {
     return -1;
   }
   e->pk_waves = 8;
+  {
+    const char* xp = getenv("DCA_PK_XPACK");
+    e->xpack = xp && xp[0] == '1';
+  }
   if (e->persistent && !e->bf) {
     g_err = "the persistent engine is bf16-only (fp32 MFMA needs all CUs: use the multi-kernel engine)";
     delete e;

@@ -34,16 +34,30 @@ struct PkArgs {
   float* tslab;              // [B][9216] trunk wgrad (fragment order)
   float* bng;                // [64] dgamma | dbeta  (written by workgroup 0)
   int* ids;                  // [64] dataset ids of the current batch (written by the previous step's reduce)
+  unsigned long long* xcc;   // [64] granules: XCD id of each image workgroup (published with round 0)
+  int xpack;                 // 1: grid = 8 x batch, only blocks b % 8 == 0 work (one XCD under round-robin dispatch)
   int debug;                 // also store DY / G for the numerical diagnostics
 };
 
 constexpr int cmax(int a, int b) { return a > b ? a : b; }
 
+// Image / grid size of the persistent launch.  With xpack the grid is 8 x batch and only blocks b % 8 == 0 run:
+// blocks b and b + 8 share an XCD under the (observed, never relied on for correctness) round-robin dispatch,
+// so all image workgroups sit behind one L2 and the BN exchange can use L2-resident stores (see xchg_publish).
+__device__ __forceinline__ int pk_img(int xpack) { return xpack ? (int)(blockIdx.x >> 3) : (int)blockIdx.x; }
+__device__ __forceinline__ int pk_grid(int xpack) { return xpack ? (int)(gridDim.x >> 3) : (int)gridDim.x; }
+__device__ __forceinline__ unsigned xcc_id() {
+  unsigned v;
+  asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID, 0, 4)" : "=s"(v));
+  return v;
+}
+
 // diagnostic stamps (DCA_STAMPS builds): global stamp index s -> slot 24 + s/8, entry s%8
-#define PK_STAMP(cx, s) DCA_STAMP(cx, 24 + (s) / 8, blockIdx.x, (s) % 8)
+#define PK_STAMP(cx, s) DCA_STAMP(cx, 24 + (s) / 8, pk_img(pa.xpack), (s) % 8)
 
 constexpr int P_KSHIFT = 906;  // misc offset of the [10][32] BN shift table (last step's batch means)
 constexpr int P_LABEL = 1240; // misc offset of this image's label
+constexpr int P_FAST = 1241;  // misc offset of the exchange-protocol flag (1: one XCD, L2-resident publishes)
 
 struct Plan {
   static constexpr int RB = 80;                        // bf16 record = 32 channels (64 B) + 16 B pad
@@ -237,13 +251,41 @@ __device__ __forceinline__ float img_csum_pub(float a0, float a1, float b0, floa
 //   xchg_wait:    on return thread t < 64 of every workgroup holds the sum of slot t over all workgroups.
 // One LDS barrier (the cross-wave combine).  The sweep is split over the waves (wave w reads workgroups
 // w, w + NW, ...).
-__device__ __forceinline__ void xchg_publish(const PkArgs& pa, int epoch, int round, float v) {
+// fast: every image workgroup was found on ONE XCD (checked with round 0), so a plain store -- which stays in
+// that XCD's L2, where the sc1 polls of the other workgroups read -- is enough; otherwise a write-through (sc1)
+// agent-scope store.
+__device__ __forceinline__ void xchg_publish(const PkArgs& pa, int epoch, int round, float v, bool fast) {
   const int t = threadIdx.x;
   const unsigned tag = (unsigned)(epoch * 64 + round + 1);
-  unsigned long long* buf = pa.gran + (size_t)(round & 1) * 64 * 64;
-  if (t < 64)
-    __hip_atomic_store(buf + blockIdx.x * 64 + t, ((unsigned long long)tag << 32) | __float_as_uint(v),
-                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  unsigned long long* dst = pa.gran + (size_t)(round & 1) * 64 * 64 + pk_img(pa.xpack) * 64 + t;
+  const unsigned long long g = ((unsigned long long)tag << 32) | __float_as_uint(v);
+  if (t < 64) {
+    if (fast) *(volatile unsigned long long*)dst = g;
+    else __hip_atomic_store(dst, g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  if (round == 0 && t == 64)  // this workgroup's XCD, for the fast-path decision
+    __hip_atomic_store(pa.xcc + pk_img(pa.xpack), ((unsigned long long)tag << 32) | xcc_id(), __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+}
+// After round 0: 1 if every image workgroup reported the same XCD (identical answer in every workgroup).
+// Wave 0 only; bounded spin like the exchange.
+__device__ __forceinline__ int xcc_all_same(const PkArgs& pa, int epoch) {
+  const int lane = threadIdx.x & 63, G = pk_grid(pa.xpack);
+  const unsigned tag = (unsigned)(epoch * 64 + 1);
+  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(pa.xcc, (short)0, 64 * 8, 0x00020000);
+  unsigned id = 0;
+  for (unsigned spins = 0;; ++spins) {
+    asm volatile("" ::: "memory");
+    const auto x = __builtin_amdgcn_raw_buffer_load_b64(rs, (lane < G ? lane : 0) * 8, 0, 16);  // sc1
+    id = x[0];
+    if (__all(lane >= G || x[1] == tag)) break;
+    if (spins >= SPIN_LIMIT) {
+      if (lane == 0) atomicOr(pa.err, 1u << 31);
+      return 0;
+    }
+  }
+  const unsigned id0 = __builtin_amdgcn_readfirstlane(id);
+  return __all(lane >= G || id == id0) ? 1 : 0;
 }
 // Early pass for xchg_wait (batch <= 32): issue it, do independent work, then hand it to xchg_wait.
 template <int NW>
@@ -254,12 +296,13 @@ struct EarlyPass {
 template <int NW>
 __device__ __forceinline__ void xchg_early(const PkArgs& pa, int round, EarlyPass<NW>& ep) {
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  if (gridDim.x <= 32) sweep_load<NW, EarlyPass<NW>::KS>(gran_rsrc(pa, round), w, threadIdx.x & 63, gridDim.x, ep.lo, ep.hi);
+  const int G = pk_grid(pa.xpack);
+  if (G <= 32) sweep_load<NW, EarlyPass<NW>::KS>(gran_rsrc(pa, round), w, threadIdx.x & 63, G, ep.lo, ep.hi);
 }
 template <int NW>
 __device__ float xchg_wait(const PkArgs& pa, int epoch, int round, float* cred, const EarlyPass<NW>* ep = nullptr) {
   constexpr int KSW = Geo<NW>::KSW, KSH = (32 + NW - 1) / NW;
-  const int t = threadIdx.x, lane = t & 63, G = gridDim.x;
+  const int t = threadIdx.x, lane = t & 63, G = pk_grid(pa.xpack);
   const int w = __builtin_amdgcn_readfirstlane(t >> 6);  // wave-uniform -> scalar branches in the sweep
   const unsigned tag = (unsigned)(epoch * 64 + round + 1);
   const __amdgpu_buffer_rsrc_t rs = gran_rsrc(pa, round);
@@ -285,8 +328,8 @@ __device__ float xchg_wait(const PkArgs& pa, int epoch, int round, float* cred, 
   return a;
 }
 template <int NW>
-__device__ __forceinline__ float xchg(const PkArgs& pa, int epoch, int round, float v, float* cred) {
-  xchg_publish(pa, epoch, round, v);
+__device__ __forceinline__ float xchg(const PkArgs& pa, int epoch, int round, float v, float* cred, bool fast) {
+  xchg_publish(pa, epoch, round, v, fast);
   return xchg_wait<NW>(pa, epoch, round, cred);
 }
 
@@ -345,11 +388,15 @@ __device__ void bn_fwd_stats(const Ctx& cx, const PkArgs& pa, int epoch, int blk
     }
   const float v = img_csum_pub<NW>(a0, a1, b0, b1, cred);
   if (blk == 5) PK_STAMP(cx, 25);
-  const float tot = xchg<NW>(pa, epoch, blk, v, cred);
+  const float tot = xchg<NW>(pa, epoch, blk, v, cred, blk > 0 && misc[P_FAST] != 0.f);
   if (blk == 5) PK_STAMP(cx, 26);
+  if (blk == 0 && threadIdx.x < 64) {  // decide the exchange protocol of rounds 1.. (same answer everywhere)
+    const int same = xcc_all_same(pa, epoch);
+    if (threadIdx.x == 0) misc[P_FAST] = same ? 1.f : 0.f;  // read after the barrier at the end of this function
+  }
   const float sq = __shfl(tot, (lane & 31) + 32);  // wave 0: lane t < 32 also gets slot 32 + t
   if (t < 32) {
-    const float N = (float)gridDim.x * 256.f;
+    const float N = (float)pk_grid(pa.xpack) * 256.f;
     const float dm = tot / N;
     const float mean = kshift[blk * 32 + t] + dm;
     const float var = fmaxf(sq / N - dm * dm, 0.f);
@@ -359,7 +406,7 @@ __device__ void bn_fwd_stats(const Ctx& cx, const PkArgs& pa, int epoch, int blk
     misc[224 + t] = bet - mean * gam * invstd;
     stat[blk * 64 + t] = mean;
     stat[blk * 64 + 32 + t] = invstd;
-    if (blockIdx.x == 0) {  // running stats live in LDS (misc[448..512)) for the whole forward
+    if (pk_img(pa.xpack) == 0) {  // running stats live in LDS (misc[448..512)) for the whole forward
       cx.STATS[blk * 32 + t] = make_float2(mean, invstd);
       const float unb = var * N / (N - 1.f), mo = cx.bn_mom;
       misc[448 + t] = misc[448 + t] * (1.f - mo) + mean * mo;
@@ -504,7 +551,8 @@ __global__ void __launch_bounds__(64 * NW) k_pk_step(Ctx cx, PkArgs pa) {
   constexpr int RPW = Gm::RPW, NTH = Gm::NT;
   const int t = threadIdx.x, w = t >> 6, lane = t & 63, c = lane & 15, q = lane >> 4;
   const int r0 = w * RPW;  // first image row owned by this wave
-  const int n = blockIdx.x;
+  if (pa.xpack && (blockIdx.x & 7)) return;  // placement filler (see pk_img)
+  const int n = pk_img(pa.xpack);
   float* cred = (float*)(smem + P::O_CRED);
   float* stat = (float*)(smem + P::O_STAT);
   float* misc = (float*)(smem + P::O_MISC);  // [0,64) publish | [64,192) sums | [192,256) scale/shift | ...
@@ -952,7 +1000,7 @@ __global__ void __launch_bounds__(64 * NW) k_pk_step(Ctx cx, PkArgs pa) {
         }
     }
     const float pv = img_csum_pub<NW>(sa[0], sa[1], sbv[0], sbv[1], cred);  // image sums -> publish value
-    xchg_publish(pa, epoch, NBLK + (NBLK - 1 - i), pv);
+    xchg_publish(pa, epoch, NBLK + (NBLK - 1 - i), pv, misc[P_FAST] != 0.f);
     if (i == 5) PK_STAMP(cx, 36);
     // While the exchange is in flight: the weight gradient of the PREVIOUS application (block i + 1), whose
     // dy / x tiles are still staged in dyT / xT.  Then the barrier retires every wave's reads of them (and of
