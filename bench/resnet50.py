@@ -1,0 +1,88 @@
+"""ResNet-50 data-parallel training throughput (BASELINE.json extension config: synthetic 3x224x224, DDP).
+
+Generic path of the framework: FlatBucketDDP (flat parameter/gradient buffers, bucketed asynchronous RCCL
+all-reduce launched from gradient hooks so it overlaps the backward) + FlatSGD (momentum 0.9, one fused update),
+bf16 autocast.  Prints one JSON line (whole-job images/sec, slowest rank).
+
+    python bench/resnet50.py [--batch 64] [--steps 30] [--warmup 5]
+    python -m torch.distributed.run --nproc-per-node 8 --master-addr 127.0.0.1 bench/resnet50.py --gpus 8
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+import torch.distributed as dist
+import torch.nn.functional as F
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def main() -> int:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--batch", type=int, default=64, help="per-rank batch")
+    ap.add_argument("--steps", type=int, default=30)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--image", type=int, default=224)
+    ap.add_argument("--bucket-mb", type=float, default=8.0)
+    ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
+    a = ap.parse_args()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    os.environ.setdefault("MASTER_PORT", "29531")
+    dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
+    from distributeddataparallel_cifar10_amd.models.resnet50 import resnet50
+    from distributeddataparallel_cifar10_amd.parallel.flat_ddp import FlatBucketDDP, FlatSGD
+    torch.manual_seed(rank)
+    model = resnet50().to(dev)
+    ddp = FlatBucketDDP(model, bucket_cap_mb=a.bucket_mb, first_bucket_mb=1.0)
+    opt = FlatSGD(ddp, lr=0.1, momentum=0.9)
+    g = torch.Generator(device=dev).manual_seed(1234 + rank)
+    x = torch.randn(a.batch, 3, a.image, a.image, device=dev, generator=g)
+    y = torch.randint(0, 1000, (a.batch,), device=dev, generator=g)
+    amp = torch.autocast("cuda", dtype=torch.bfloat16, enabled=a.dtype == "bf16")
+
+    def step():
+        with amp:
+            loss = F.cross_entropy(ddp(x), y)
+        opt.zero_grad()
+        loss.backward()
+        opt.step()
+        return loss
+
+    for _ in range(a.warmup):
+        step()
+    torch.cuda.synchronize()
+    dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        loss = step()
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    t = torch.tensor([dt], device=dev, dtype=torch.float64)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    dt = float(t.item())
+    if rank == 0:
+        v = world * a.batch * a.steps / dt
+        print(json.dumps({"metric": "images/sec (whole node) ResNet-50 synthetic 3x224x224 DDP", "value": round(v, 1),
+                          "unit": "images/sec", "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
+                          "ms_per_step": round(1e3 * dt / a.steps, 3), "higher_is_better": True, "scaling": "weak",
+                          "dtype": a.dtype, "data": "synthetic", "loss": float(loss),
+                          "config": {"model": "ResNet-50", "per_rank_batch": a.batch, "image": a.image,
+                                     "parallelism": f"dp{world}", "optimizer": "SGD(0.1, momentum 0.9)",
+                                     "path": "FlatBucketDDP + stock conv (MIOpen), bf16 autocast"}}), flush=True)
+    dist.destroy_process_group()
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

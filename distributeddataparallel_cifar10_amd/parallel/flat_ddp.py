@@ -172,16 +172,30 @@ class FlatBucketDDP(nn.Module):
 
 
 class FlatSGD(torch.optim.Optimizer):
-    """``optim.SGD(lr)`` without momentum/weight decay (reference ``main.py:27``) as ONE op over a flat buffer."""
+    """``optim.SGD`` over the flat buffer in one or two fused ops.
 
-    def __init__(self, ddp: FlatBucketDDP, lr: float = 1e-2):
-        super().__init__(list(ddp.module.parameters()), dict(lr=lr))
+    Default = reference ``main.py:27`` (lr only).  ``momentum`` / ``weight_decay`` follow torch.optim.SGD's
+    formulas (buf = m * buf + (g + wd * p); p -= lr * buf), e.g. the ppe_main_ddp.py setting SGD(1e-3, 0.9)."""
+
+    def __init__(self, ddp: FlatBucketDDP, lr: float = 1e-2, momentum: float = 0.0, weight_decay: float = 0.0):
+        super().__init__(list(ddp.module.parameters()), dict(lr=lr, momentum=momentum, weight_decay=weight_decay))
         self.ddp = ddp
+        self._buf = None
 
     @torch.no_grad()
     def step(self, closure=None):
         loss = closure() if closure is not None else None
-        self.ddp.flat.add_(self.ddp.flat_grad, alpha=-self.param_groups[0]["lr"])
+        g = self.param_groups[0]
+        grad = self.ddp.flat_grad
+        if g["weight_decay"]:
+            grad = grad.add(self.ddp.flat, alpha=g["weight_decay"])
+        if g["momentum"]:
+            if self._buf is None:
+                self._buf = grad.clone()
+            else:
+                self._buf.mul_(g["momentum"]).add_(grad)
+            grad = self._buf
+        self.ddp.flat.add_(grad, alpha=-g["lr"])
         return loss
 
     def zero_grad(self, set_to_none: bool = True) -> None:
