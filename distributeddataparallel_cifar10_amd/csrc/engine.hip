@@ -145,7 +145,7 @@ static int alloc_workspace(Engine* e) {
       {"RS_BASE", 64 * 4},           {"CURSOR", 16},                  {"STEPS", 16},
       {"LOSS", 16},                  {"STAMPS", 32 * 256 * 8 * 2 * 8},
       {"GRAN", 2 * 64 * 64 * 8},     {"EPOCH", 16},                   {"ERR", 16},
-      {"TSLAB", bmax * WSLAB_N * 4}, {"BNG", 64 * 4}, {"IDS", 64 * 4}, {"W1B", 65536 * 2}, {"XCC", 64 * 8}, {"SWF", 2 * 3 * 64 * 4 * 2},
+      {"TSLAB", bmax * WSLAB_N * 4}, {"BNG", 64 * 4}, {"IDS", 64 * 4}, {"W1B", 65536 * 2}, {"XCC", 64 * 8}, {"SIMG", 64 * 3072}, {"SLAB", 64 * 4}, {"SWF", 2 * 3 * 64 * 4 * 2},
   };
   size_t total = 0;
   for (auto& r : regs) total += align_up(r.bytes, 256);
@@ -193,6 +193,8 @@ static int alloc_workspace(Engine* e) {
   e->pa.bng = (float*)e->regions["BNG"];
   e->pa.ids = (int*)e->regions["IDS"];
   e->pa.xcc = (unsigned long long*)e->regions["XCC"];
+  e->pa.simg = (uint8_t*)e->regions["SIMG"];
+  e->pa.slab = (int*)e->regions["SLAB"];
   e->pa.debug = e->in.debug;
   return 0;
 }
@@ -549,7 +551,7 @@ int dca_engine_derive(void* h) {
 // persistent engine: the batch ids of the next step are produced by the previous step; re-derive them whenever
 // the host moves the cursor or replaces the index list
 static int prime_ids(Engine* e) {
-  hipLaunchKernelGGL(dca::pk::k_pk_prime_ids, dim3(1), dim3(64), 0, e->st, e->base, e->pa);
+  hipLaunchKernelGGL(dca::pk::k_pk_prime_ids, dim3(64), dim3(256), 0, e->st, e->base, e->pa);
   HIPCK(hipGetLastError());
   return 0;
 }

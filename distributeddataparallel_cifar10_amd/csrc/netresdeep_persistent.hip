@@ -34,6 +34,8 @@ struct PkArgs {
   float* tslab;              // [B][9216] trunk wgrad (fragment order)
   float* bng;                // [64] dgamma | dbeta  (written by workgroup 0)
   int* ids;                  // [64] dataset ids of the current batch (written by the previous step's reduce)
+  uint8_t* simg;             // [64][3072] the current batch's images, staged contiguously by the previous reduce
+  int* slab;                 // [64] their labels
   unsigned long long* xcc;   // [64] granules: XCD id of each image workgroup (published with round 0)
   int xpack;                 // 1: grid = 8 x batch, only blocks b % 8 == 0 work (one XCD under round-robin dispatch)
   int debug;                 // also store DY / G for the numerical diagnostics
@@ -562,7 +564,8 @@ __global__ void __launch_bounds__(64 * NW) k_pk_step(Ctx cx, PkArgs pa) {
   const int epoch = *pa.epoch;
   const size_t img = (size_t)n * 8192;
   const int B = cx.B;
-  const int sid = pa.ids[n];  // (clamped by the writer)
+  const uint8_t* my_img = pa.simg + (size_t)n * 3072;  // staged by the previous step (no id indirection)
+  if (n == 0 && t == 0) *cx.cursor += B;  // the next batch starts here (k_pk_reduce stages it from the cursor)
   PK_STAMP(cx, 0);
 
   // ======================= stem: gather + normalise + conv1 + bias + ReLU + 2x2 max-pool =================
@@ -593,9 +596,9 @@ __global__ void __launch_bounds__(64 * NW) k_pk_step(Ctx cx, PkArgs pa) {
                                  : (const float*)cx.STATS + 2 * (k - 522);  // BN shifts (.x = mean)
       kc[m] = *src;
     }
-    int lab = cx.labels[sid];
+    int lab = pa.slab[n];
     const int tq = t & 255;  // threads < 256: pixels (y = tq >> 3, x = 4 (tq & 7) .. +3), all 3 channels
-    const unsigned* imw = (const unsigned*)(cx.data + (size_t)sid * 3072);
+    const unsigned* imw = (const unsigned*)my_img;
     unsigned iw0 = imw[tq], iw1 = imw[256 + tq], iw2 = imw[512 + tq];
     uint4 wt0, wt1, wt2;
     stage_wt_load3(wt0, wt1, wt2, cx.wt_f);
@@ -1050,7 +1053,7 @@ __global__ void __launch_bounds__(64 * NW) k_pk_step(Ctx cx, PkArgs pa) {
       for (int rr = 0; rr < RPW; ++rr)
 #pragma unroll
         for (int h = 0; h < 2; ++h) codew[rr][h] = *(const unsigned*)(cx.SCODE + img + tl(r0 + rr, h, lane));
-      stage_input_load<NW>(imgw, cx.data + (size_t)sid * 3072);
+      stage_input_load<NW>(imgw, my_img);
     }
     if (n == 0 && t < 32) {
       dbet += misc[64 + t];
@@ -1206,9 +1209,17 @@ __global__ void __launch_bounds__(64 * NW) k_pk_step(Ctx cx, PkArgs pa) {
 // 1 bookkeeping workgroup (fc2, biases, BN, loss, cursor, epoch).  256 threads.
 // ============================================================================================================
 // Batch ids for the first step after the host moved the cursor or replaced the index list.
-__global__ void __launch_bounds__(64) k_pk_prime_ids(Ctx cx, PkArgs pa) {
-  pa.ids[threadIdx.x] = sample_id(cx, threadIdx.x);
+// Stage images / labels / ids of batch position `b` (= cursor + b) into the contiguous per-step buffers.
+__device__ __forceinline__ void stage_sample(const Ctx& cx, const PkArgs& pa, int b) {
+  const int t = threadIdx.x, id = sample_id(cx, b);
+  if (t < 192) ((uint4*)(pa.simg + (size_t)b * 3072))[t] = ((const uint4*)(cx.data + (size_t)id * 3072))[t];
+  if (t == 192) {
+    pa.slab[b] = cx.labels[id];
+    pa.ids[b] = id;
+  }
 }
+// The first batch after the host moved the cursor or replaced the index list (grid 64 x 256).
+__global__ void __launch_bounds__(256) k_pk_prime_ids(Ctx cx, PkArgs pa) { stage_sample(cx, pa, blockIdx.x); }
 
 constexpr int R_TRUNK = 36, R_STEM = 5, R_FC = 32, R_GRID = R_TRUNK + R_STEM + R_FC + 1;
 
@@ -1221,6 +1232,9 @@ __global__ void __launch_bounds__(256) k_pk_reduce(Ctx cx, PkArgs pa) {
   __shared__ f32x4 red[256];
   __shared__ float stage[64 * 32 + 64 * 64];
   const int t = threadIdx.x, bid = blockIdx.x, B = cx.B;
+  // Stage the NEXT step's batch (images, labels) contiguously: the step kernel then reads its image without
+  // the id -> image dependent load.  k_pk_step already advanced the cursor to the next batch.
+  if (bid < BMAX_LIMIT) stage_sample(cx, pa, bid);  // all 64 slots: the next run may use a larger batch
   if (bid < R_TRUNK + R_STEM) {
     const bool stem = bid >= R_TRUNK;
     const int chunk = stem ? bid - R_TRUNK : bid;
@@ -1317,7 +1331,6 @@ __global__ void __launch_bounds__(256) k_pk_reduce(Ctx cx, PkArgs pa) {
   }
   // bookkeeping workgroup: fc1 bias, fc2, BN affine grads, loss, cursor, epoch, next batch ids, CC4 segment
   {
-    if (t < 64) pa.ids[t] = sample_id(cx, B + t);  // the next step's batch (cursor advances by B below)
     float* hh_s = stage;             // [B][32]
     float* dl_s = stage + 64 * 32;   // [B][16]
     float* dh_s = dl_s + 64 * 16;    // [B][32]
@@ -1352,7 +1365,6 @@ __global__ void __launch_bounds__(256) k_pk_reduce(Ctx cx, PkArgs pa) {
       float s = 0.f;
       for (int k = 0; k < 256 && k < B; ++k) s += ((float*)red)[k];
       *cx.loss_acc += (double)(s / (float)B);
-      *cx.cursor += B;
       *cx.step_count += 1;
       *cx.nbt += NBLK;  // BatchNorm num_batches_tracked: +1 per application
       *pa.epoch += 1;
