@@ -90,6 +90,7 @@ struct Engine {
   bool persistent = false;
   int pk_waves = 8;
   int xpack = 0;  // experimental one-XCD placement of the persistent kernel (env DCA_PK_XPACK=1)
+  int staged_b = 0;  // persistent engine: batch slots of the current staging parity that hold the next batch
   pk::PkArgs pa{};
   std::map<std::string, void*> regions;
   // dynamic LDS sizes
@@ -145,7 +146,7 @@ static int alloc_workspace(Engine* e) {
       {"RS_BASE", 64 * 4},           {"CURSOR", 16},                  {"STEPS", 16},
       {"LOSS", 16},                  {"STAMPS", 32 * 256 * 8 * 2 * 8},
       {"GRAN", 2 * 64 * 64 * 8},     {"EPOCH", 16},                   {"ERR", 16},
-      {"TSLAB", bmax * WSLAB_N * 4}, {"BNG", 64 * 4}, {"IDS", 64 * 4}, {"W1B", 65536 * 2}, {"XCC", 64 * 8}, {"SIMG", 64 * 3072}, {"SLAB", 64 * 4}, {"SWF", 2 * 3 * 64 * 4 * 2},
+      {"TSLAB", bmax * WSLAB_N * 4}, {"BNG", 64 * 4}, {"IDS", 64 * 4}, {"W1B", 65536 * 2}, {"XCC", 64 * 8}, {"SIMG", 2 * 64 * 3072}, {"SLAB", 2 * 64 * 4}, {"SWF", 2 * 3 * 64 * 4 * 2},
   };
   size_t total = 0;
   for (auto& r : regs) total += align_up(r.bytes, 256);
@@ -553,6 +554,13 @@ int dca_engine_derive(void* h) {
 static int prime_ids(Engine* e) {
   hipLaunchKernelGGL(dca::pk::k_pk_prime_ids, dim3(64), dim3(256), 0, e->st, e->base, e->pa);
   HIPCK(hipGetLastError());
+  e->staged_b = 64;
+  return 0;
+}
+// A persistent step of batch B stages only B slots of the next batch; a following larger batch re-primes.
+static int ensure_staged(Engine* e, int B) {
+  if (e->persistent && B > e->staged_b && prime_ids(e)) return -1;
+  if (e->persistent) e->staged_b = B;
   return 0;
 }
 
@@ -612,6 +620,7 @@ int dca_engine_run(void* h, int B, int nsteps, int use_graph) {
     g_err = "comm_mode 1 (external all-reduce): drive steps with dca_engine_run_part";
     return -1;
   }
+  if (nsteps > 0 && ensure_staged(e, B)) return -1;
   if (!use_graph) {
     for (int s = 0; s < nsteps; ++s)
       if (dca::enqueue_step(e, B)) return -1;
@@ -656,6 +665,7 @@ int dca_engine_run_part(void* h, int B, int part) {
     g_err = "run_part: needs world_size > 1, comm_mode 1, part 1 or 2, batch in range";
     return -1;
   }
+  if (part == 1 && ensure_staged(e, B)) return -1;
   return dca::enqueue_step(e, B, part);
 }
 

@@ -34,8 +34,8 @@ struct PkArgs {
   float* tslab;              // [B][9216] trunk wgrad (fragment order)
   float* bng;                // [64] dgamma | dbeta  (written by workgroup 0)
   int* ids;                  // [64] dataset ids of the current batch (written by the previous step's reduce)
-  uint8_t* simg;             // [64][3072] the current batch's images, staged contiguously by the previous reduce
-  int* slab;                 // [64] their labels
+  uint8_t* simg;             // [2][64][3072] batch images staged contiguously (parity = epoch & 1); each step
+  int* slab;                 // [2][64]       stages the NEXT batch into the other parity, see k_pk_step
   unsigned long long* xcc;   // [64] granules: XCD id of each image workgroup (published with round 0)
   int xpack;                 // 1: grid = 8 x batch, only blocks b % 8 == 0 work (one XCD under round-robin dispatch)
   int debug;                 // also store DY / G for the numerical diagnostics
@@ -564,8 +564,9 @@ __global__ void __launch_bounds__(64 * NW) k_pk_step(Ctx cx, PkArgs pa) {
   const int epoch = *pa.epoch;
   const size_t img = (size_t)n * 8192;
   const int B = cx.B;
-  const uint8_t* my_img = pa.simg + (size_t)n * 3072;  // staged by the previous step (no id indirection)
-  if (n == 0 && t == 0) *cx.cursor += B;  // the next batch starts here (k_pk_reduce stages it from the cursor)
+  const int par = epoch & 1;
+  const uint8_t* my_img = pa.simg + (size_t)(par * 64 + n) * 3072;  // staged by the previous step
+  const int next_id = sample_id(cx, B + n);  // image n of the NEXT batch (staged at the end of this step)
   PK_STAMP(cx, 0);
 
   // ======================= stem: gather + normalise + conv1 + bias + ReLU + 2x2 max-pool =================
@@ -596,7 +597,7 @@ __global__ void __launch_bounds__(64 * NW) k_pk_step(Ctx cx, PkArgs pa) {
                                  : (const float*)cx.STATS + 2 * (k - 522);  // BN shifts (.x = mean)
       kc[m] = *src;
     }
-    int lab = pa.slab[n];
+    int lab = pa.slab[par * 64 + n];
     const int tq = t & 255;  // threads < 256: pixels (y = tq >> 3, x = 4 (tq & 7) .. +3), all 3 channels
     const unsigned* imw = (const unsigned*)my_img;
     unsigned iw0 = imw[tq], iw1 = imw[256 + tq], iw2 = imw[512 + tq];
@@ -977,6 +978,8 @@ __global__ void __launch_bounds__(64 * NW) k_pk_step(Ctx cx, PkArgs pa) {
   f32x4 wacc[Gm::NNT][2];
 #pragma unroll
   for (int j = 0; j < Gm::NNT; ++j) wacc[j][0] = wacc[j][1] = z4();
+  uint4 nxt = uint4{0u, 0u, 0u, 0u};  // next batch's image n (+ label): loaded during the last backward block,
+  int nxt_lab = 0;                    // stored into the other staging parity at the end of the step
   float dgam = 0.f, dbet = 0.f;
   unsigned codew[RPW][2];                         // stem-backward prefetch (filled during block 0)
   unsigned imgw[Gm::IMW];
@@ -1054,6 +1057,8 @@ __global__ void __launch_bounds__(64 * NW) k_pk_step(Ctx cx, PkArgs pa) {
 #pragma unroll
         for (int h = 0; h < 2; ++h) codew[rr][h] = *(const unsigned*)(cx.SCODE + img + tl(r0 + rr, h, lane));
       stage_input_load<NW>(imgw, my_img);
+      nxt = ((const uint4*)(cx.data + (size_t)next_id * 3072))[t < 192 ? t : 0];
+      nxt_lab = cx.labels[next_id];
     }
     if (n == 0 && t < 32) {
       dbet += misc[64 + t];
@@ -1192,6 +1197,8 @@ __global__ void __launch_bounds__(64 * NW) k_pk_step(Ctx cx, PkArgs pa) {
       st4(ss + ((tile * 64 + ln) << 2), ld4(sred + ((tile * 64 + ln) << 2)) + ld4(sred + (((tile + 4) * 64 + ln) << 2)));
     }
   }
+  if (t < 192) ((uint4*)(pa.simg + (size_t)((par ^ 1) * 64 + n) * 3072))[t] = nxt;
+  if (t == 192) pa.slab[(par ^ 1) * 64 + n] = nxt_lab;
   // trunk wgrad slab (accumulated over the 10 applications)
 #pragma unroll
   for (int j = 0; j < Gm::NNT; ++j) {
@@ -1209,48 +1216,83 @@ __global__ void __launch_bounds__(64 * NW) k_pk_step(Ctx cx, PkArgs pa) {
 // 1 bookkeeping workgroup (fc2, biases, BN, loss, cursor, epoch).  256 threads.
 // ============================================================================================================
 // Batch ids for the first step after the host moved the cursor or replaced the index list.
-// Stage images / labels / ids of batch position `b` (= cursor + b) into the contiguous per-step buffers.
-__device__ __forceinline__ void stage_sample(const Ctx& cx, const PkArgs& pa, int b) {
+// Stage image / label / id of batch position `b` (= cursor + b) into staging parity `par`.
+__device__ __forceinline__ void stage_sample(const Ctx& cx, const PkArgs& pa, int b, int par) {
   const int t = threadIdx.x, id = sample_id(cx, b);
-  if (t < 192) ((uint4*)(pa.simg + (size_t)b * 3072))[t] = ((const uint4*)(cx.data + (size_t)id * 3072))[t];
+  if (t < 192)
+    ((uint4*)(pa.simg + (size_t)(par * 64 + b) * 3072))[t] = ((const uint4*)(cx.data + (size_t)id * 3072))[t];
   if (t == 192) {
-    pa.slab[b] = cx.labels[id];
+    pa.slab[par * 64 + b] = cx.labels[id];
     pa.ids[b] = id;
   }
 }
 // The first batch after the host moved the cursor or replaced the index list (grid 64 x 256).
-__global__ void __launch_bounds__(256) k_pk_prime_ids(Ctx cx, PkArgs pa) { stage_sample(cx, pa, blockIdx.x); }
+__global__ void __launch_bounds__(256) k_pk_prime_ids(Ctx cx, PkArgs pa) {
+  stage_sample(cx, pa, blockIdx.x, *pa.epoch & 1);
+}
 
-constexpr int R_TRUNK = 36, R_STEM = 5, R_FC = 32, R_GRID = R_TRUNK + R_STEM + R_FC + 1;
+constexpr int R_TRUNK = 36, R_STEM = 5, R_FC = 32, R_WORK = R_TRUNK + R_STEM + R_FC + 1;
+constexpr int R_GRID = R_WORK;
 
 __device__ __forceinline__ void sgd_put(const Ctx& cx, int pidx, float gval) {
   cx.grads[pidx] = gval;
   if (cx.fuse_sgd) cx.params[pidx] -= cx.lr * gval;
+}
+// same with the old parameter value loaded up front (no load -> store round trip after the reduction);
+// returns the value the parameter now has
+__device__ __forceinline__ float sgd_put_pre(const Ctx& cx, int pidx, float gval, float oldp) {
+  cx.grads[pidx] = gval;
+  if (cx.fuse_sgd) {
+    const float np = oldp - cx.lr * gval;
+    cx.params[pidx] = np;
+    return np;
+  }
+  return oldp;
 }
 
 __global__ void __launch_bounds__(256) k_pk_reduce(Ctx cx, PkArgs pa) {
   __shared__ f32x4 red[256];
   __shared__ float stage[64 * 32 + 64 * 64];
   const int t = threadIdx.x, bid = blockIdx.x, B = cx.B;
-  // Stage the NEXT step's batch (images, labels) contiguously: the step kernel then reads its image without
-  // the id -> image dependent load.  k_pk_step already advanced the cursor to the next batch.
-  if (bid < BMAX_LIMIT) stage_sample(cx, pa, bid);  // all 64 slots: the next run may use a larger batch
   if (bid < R_TRUNK + R_STEM) {
     const bool stem = bid >= R_TRUNK;
     const int chunk = stem ? bid - R_TRUNK : bid;
     const int slot = t & 63, grp = t >> 6, e0 = chunk * 256 + slot * 4;
     const float* src = stem ? cx.SSLAB : pa.tslab;
     const int stride = stem ? SSLAB_N : WSLAB_N, lim = stem ? SSLAB_N : WSLAB_N;
+    // parameter index of each of this thread's 4 outputs (slab fragment order -> flat layout), -1 if none
+    int pix[4];
+    float pold[4];
+#pragma unroll
+    for (int ii = 0; ii < 4; ++ii) {
+      const int e = e0 + ii;
+      int pidx = -1;
+      if (e < lim) {
+        if (!stem) {
+          const int tt = e >> 8, ln = (e >> 2) & 63, mt = tt & 1, nt = tt >> 1, tap = nt >> 1, cih = nt & 1;
+          pidx = OFF_CONVW + (16 * mt + 4 * (ln >> 4) + ii) * 288 + (16 * cih + (ln & 15)) * 9 + tap;
+        } else if (e < 1024) {
+          const int tt = e >> 8, ln = (e >> 2) & 63, mt = tt & 1, nt = tt >> 1, k = 16 * nt + (ln & 15);
+          if (k < 27) pidx = OFF_C1W + (16 * mt + 4 * (ln >> 4) + ii) * 27 + k;
+        } else if (e < 1056) {
+          pidx = OFF_C1B + (e - 1024);
+        }
+      }
+      pix[ii] = pidx;
+      pold[ii] = cx.params[pidx >= 0 ? pidx : 0];  // issued with the slab loads
+    }
     f32x4 s = z4();
-    if (e0 < lim) {
+    {  // every load unconditional (clamped index), all in flight together; out-of-range ones are dropped after
+      const int ec = e0 < lim ? e0 : lim - 4;
       f32x4 v[16];
 #pragma unroll
       for (int u = 0; u < 16; ++u) {
         const int k = grp + 4 * u;
-        v[u] = k < B ? ld4(src + (size_t)k * stride + e0) : z4();
+        v[u] = ld4(src + (size_t)(k < B ? k : B - 1) * stride + ec);
       }
 #pragma unroll
-      for (int u = 0; u < 16; ++u) s += v[u];
+      for (int u = 0; u < 16; ++u)
+        if (grp + 4 * u < B) s += v[u];
     }
     red[t] = s;
     __syncthreads();
@@ -1258,31 +1300,19 @@ __global__ void __launch_bounds__(256) k_pk_reduce(Ctx cx, PkArgs pa) {
       const f32x4 tot = red[t] + red[64 + t] + red[128 + t] + red[192 + t];
 #pragma unroll
       for (int ii = 0; ii < 4; ++ii) {
-        const int e = e0 + ii;
-        if (!stem) {
-          const int tt = e >> 8, ln = (e >> 2) & 63, mt = tt & 1, nt = tt >> 1, tap = nt >> 1, cih = nt & 1;
-          const int co = 16 * mt + 4 * (ln >> 4) + ii, ci = 16 * cih + (ln & 15);
-          const int pidx = OFF_CONVW + co * 288 + ci * 9 + tap;
-          sgd_put(cx, pidx, tot[ii]);
-          if (cx.fuse_sgd) {
-            const float wv = cx.params[pidx];
-            ((unsigned short*)cx.wt_f)[(tap * 32 + co) * 32 + ci] = bfbits(wv);
-            ((unsigned short*)cx.wt_d)[((8 - tap) * 32 + ci) * 32 + co] = bfbits(wv);
-          }
-        } else if (e < 1024) {
-          const int tt = e >> 8, ln = (e >> 2) & 63, mt = tt & 1, nt = tt >> 1;
-          const int co = 16 * mt + 4 * (ln >> 4) + ii, k = 16 * nt + (ln & 15);
-          if (k < 27) {
-            const int pidx = OFF_C1W + co * 27 + k;
-            sgd_put(cx, pidx, tot[ii]);
-            if (cx.fuse_sgd) {
-              const unsigned short wb = bfbits(cx.params[pidx]);
-              ((unsigned short*)cx.sw)[co * 32 + k] = wb;
-              ((unsigned short*)cx.swf)[swf_slot(co, k)] = wb;
-            }
-          }
-        } else if (e < 1056) {
-          sgd_put(cx, OFF_C1B + (e - 1024), tot[ii]);
+        const int pidx = pix[ii];
+        if (pidx < 0) continue;
+        const float wv = sgd_put_pre(cx, pidx, tot[ii], pold[ii]);
+        if (!cx.fuse_sgd) continue;
+        if (pidx >= OFF_CONVW && pidx < OFF_CONVW + 9216) {
+          const int r = pidx - OFF_CONVW, co = r / 288, ci = (r / 9) % 32, tap = r % 9;
+          ((unsigned short*)cx.wt_f)[(tap * 32 + co) * 32 + ci] = bfbits(wv);
+          ((unsigned short*)cx.wt_d)[((8 - tap) * 32 + ci) * 32 + co] = bfbits(wv);
+        } else if (pidx >= OFF_C1W && pidx < OFF_C1W + 864) {
+          const int r = pidx - OFF_C1W, co = r / 27, k = r % 27;
+          const unsigned short wb = bfbits(wv);
+          ((unsigned short*)cx.sw)[co * 32 + k] = wb;
+          ((unsigned short*)cx.swf)[swf_slot(co, k)] = wb;
         }
       }
     }
@@ -1293,15 +1323,18 @@ __global__ void __launch_bounds__(256) k_pk_reduce(Ctx cx, PkArgs pa) {
     float* dh_s = stage;          // [B][32]
     float* p_s = stage + 64 * 32; // [B][64]
     f32x4 dh4[2], p4[4];
+    const int j = t >> 3, kk = 8 * (t & 7);
+    const int base = OFF_FC1W + j * 2048 + 64 * f + kk;
+    const f32x4 o0 = ld4(cx.params + base), o1 = ld4(cx.params + base + 4);  // old weights, fetched early
 #pragma unroll
     for (int m = 0; m < 2; ++m) {
       const int idx = t + 256 * m;
-      dh4[m] = idx < B * 8 ? ld4(cx.HDH + 4 * idx) : z4();
+      dh4[m] = ld4(cx.HDH + 4 * (idx < B * 8 ? idx : 0));
     }
 #pragma unroll
     for (int m = 0; m < 4; ++m) {
-      const int idx = t + 256 * m, b = idx >> 4, k4 = idx & 15;
-      p4[m] = idx < B * 16 ? ld4(cx.HP + (size_t)b * 2048 + 64 * f + 4 * k4) : z4();
+      const int idx = t + 256 * m, ic = idx < B * 16 ? idx : 0, b = ic >> 4, k4 = ic & 15;
+      p4[m] = ld4(cx.HP + (size_t)b * 2048 + 64 * f + 4 * k4);
     }
 #pragma unroll
     for (int m = 0; m < 2; ++m)
@@ -1310,18 +1343,17 @@ __global__ void __launch_bounds__(256) k_pk_reduce(Ctx cx, PkArgs pa) {
     for (int m = 0; m < 4; ++m)
       if (t + 256 * m < B * 16) st4(p_s + 4 * (t + 256 * m), p4[m]);
     __syncthreads();
-    const int j = t >> 3, kk = 8 * (t & 7);
     f32x4 a0 = z4(), a1 = z4();
+#pragma unroll 8
     for (int b = 0; b < B; ++b) {
       const float dh = dh_s[b * 32 + j];
       a0 += dh * ld4(p_s + b * 64 + kk);
       a1 += dh * ld4(p_s + b * 64 + kk + 4);
     }
-    const int base = OFF_FC1W + j * 2048 + 64 * f + kk;
     st4(cx.grads + base, a0);
     st4(cx.grads + base + 4, a1);
     if (cx.fuse_sgd) {
-      const f32x4 n0 = ld4(cx.params + base) - cx.lr * a0, n1 = ld4(cx.params + base + 4) - cx.lr * a1;
+      const f32x4 n0 = o0 - cx.lr * a0, n1 = o1 - cx.lr * a1;
       st4(cx.params + base, n0);
       st4(cx.params + base + 4, n1);
       *(uint4*)((unsigned short*)cx.w1b + base - OFF_FC1W) =
@@ -1334,26 +1366,50 @@ __global__ void __launch_bounds__(256) k_pk_reduce(Ctx cx, PkArgs pa) {
     float* hh_s = stage;             // [B][32]
     float* dl_s = stage + 64 * 32;   // [B][16]
     float* dh_s = dl_s + 64 * 16;    // [B][32]
-    for (int idx = t; idx < B * 32; idx += 256) {
-      hh_s[idx] = cx.HH[idx];
-      dh_s[idx] = cx.HDH[idx];
+    {  // all loads first (clamped, unconditional), then the LDS stores
+      float hv[8], dv[8], lv[3];
+#pragma unroll
+      for (int m = 0; m < 8; ++m) {
+        const int idx = t + 256 * m, ic = idx < B * 32 ? idx : 0;
+        hv[m] = cx.HH[ic];
+        dv[m] = cx.HDH[ic];
+      }
+#pragma unroll
+      for (int m = 0; m < 3; ++m) {
+        const int idx = t + 256 * m;
+        lv[m] = cx.HDL[idx < B * 10 ? idx : 0];
+      }
+      const float lo = cx.HLOSS[t < B ? t : 0];
+#pragma unroll
+      for (int m = 0; m < 8; ++m) {
+        const int idx = t + 256 * m;
+        if (idx < B * 32) {
+          hh_s[idx] = hv[m];
+          dh_s[idx] = dv[m];
+        }
+      }
+#pragma unroll
+      for (int m = 0; m < 3; ++m) {
+        const int idx = t + 256 * m;
+        if (idx < B * 10) dl_s[(idx / 10) * 16 + idx % 10] = lv[m];
+      }
+      ((float*)red)[t] = t < B ? lo : 0.f;
     }
-    for (int idx = t; idx < B * 10; idx += 256) dl_s[(idx / 10) * 16 + idx % 10] = cx.HDL[idx];
-    float lsum = 0.f;
-    for (int b = t; b < B; b += 256) lsum += cx.HLOSS[b];
-    ((float*)red)[t] = lsum;
     __syncthreads();
     for (int idx = t; idx < 32 + 320 + 10 + 64; idx += 256) {
       float s = 0.f;
       if (idx < 32) {
+#pragma unroll 8
         for (int b = 0; b < B; ++b) s += dh_s[b * 32 + idx];
         sgd_put(cx, OFF_FC1B + idx, s);
       } else if (idx < 352) {
         const int o = (idx - 32) >> 5, jj = (idx - 32) & 31;
+#pragma unroll 8
         for (int b = 0; b < B; ++b) s += dl_s[b * 16 + o] * hh_s[b * 32 + jj];
         sgd_put(cx, OFF_FC2W + o * 32 + jj, s);
       } else if (idx < 362) {
         const int o = idx - 352;
+#pragma unroll 8
         for (int b = 0; b < B; ++b) s += dl_s[b * 16 + o];
         sgd_put(cx, OFF_FC2B + o, s);
       } else {
@@ -1363,8 +1419,9 @@ __global__ void __launch_bounds__(256) k_pk_reduce(Ctx cx, PkArgs pa) {
     }
     if (t == 0) {
       float s = 0.f;
-      for (int k = 0; k < 256 && k < B; ++k) s += ((float*)red)[k];
+      for (int k = 0; k < B; ++k) s += ((float*)red)[k];
       *cx.loss_acc += (double)(s / (float)B);
+      *cx.cursor += B;
       *cx.step_count += 1;
       *cx.nbt += NBLK;  // BatchNorm num_batches_tracked: +1 per application
       *pa.epoch += 1;
