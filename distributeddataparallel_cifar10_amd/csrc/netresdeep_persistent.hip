@@ -144,6 +144,14 @@ __device__ __forceinline__ int el(int row, int q, int c, int h, int i) {
 // tl(row, h, 16q + c) + i.  (runtime/engine.py: NetResDeepEngine.activations() converts to NHWC.)
 __device__ __forceinline__ int tl(int row, int h, int lane) { return row * 512 + h * 256 + lane * 4; }
 __device__ __forceinline__ void st4v(float* p, const float (&v)[4]) { *(f32x4*)p = f32x4{v[0], v[1], v[2], v[3]}; }
+// X (block inputs) is stored as bf16 in the same tiled order: the backward only uses it as a bf16 MFMA operand
+__device__ __forceinline__ void stx(float* xbase, int row, int h, int lane, const float (&v)[4]) {
+  *(uint2*)((unsigned short*)xbase + tl(row, h, lane)) =
+      uint2{(unsigned)bfbits(v[0]) | ((unsigned)bfbits(v[1]) << 16), (unsigned)bfbits(v[2]) | ((unsigned)bfbits(v[3]) << 16)};
+}
+__device__ __forceinline__ uint2 ldx(const float* xbase, int row, int h, int lane) {
+  return *(const uint2*)((const unsigned short*)xbase + tl(row, h, lane));
+}
 __device__ __forceinline__ void ld4v(const float* p, float (&v)[4]) {
   const f32x4 u = *(const f32x4*)p;
   v[0] = u[0]; v[1] = u[1]; v[2] = u[2]; v[3] = u[3];
@@ -715,7 +723,7 @@ __global__ void __launch_bounds__(64 * NW) k_pk_step(Ctx cx, PkArgs pa) {
     for (int rr = 0; rr < RPW; ++rr)
 #pragma unroll
       for (int h = 0; h < 2; ++h) {
-        st4v(cx.X + img + tl(r0 + rr, h, lane), x[rr][h]);
+        stx(cx.X + img / 2, r0 + rr, h, lane, x[rr][h]);
         unsigned cw = 0;
 #pragma unroll
         for (int i = 0; i < 4; ++i) cw |= (unsigned)scl[el(r0 + rr, q, c, h, i)] << (8 * i);
@@ -728,7 +736,7 @@ __global__ void __launch_bounds__(64 * NW) k_pk_step(Ctx cx, PkArgs pa) {
   for (int i = 0; i < NBLK; ++i) {
     if (i > 0) {
       bn_fwd_stats<NW>(cx, pa, epoch, i - 1, y, cred, misc, stat);
-      float* Xo = cx.X + (size_t)i * B * 8192 + img;
+      float* Xo = cx.X + ((size_t)i * B * 8192 + img) / 2;  // bf16 tiles
       float* Yo = cx.Y + (size_t)(i - 1) * B * 8192 + img;  // y_{i-1}, written now that its exchange is done
 #pragma unroll
       for (int h = 0; h < 2; ++h) {
@@ -743,7 +751,7 @@ __global__ void __launch_bounds__(64 * NW) k_pk_step(Ctx cx, PkArgs pa) {
             st1r(XR, (r0 + rr + 1) * 18 + 4 * q + i2 + 1, ch, v);
           }
           st4v(Yo + tl(r0 + rr, h, lane), y[rr][h]);
-          st4v(Xo + tl(r0 + rr, h, lane), x[rr][h]);
+          stx(Xo, r0 + rr, h, lane, x[rr][h]);
         }
       }
       lds_barrier();
@@ -783,7 +791,8 @@ __global__ void __launch_bounds__(64 * NW) k_pk_step(Ctx cx, PkArgs pa) {
   }
   PK_STAMP(cx, 12);
 
-  float yb[RPW][2][4], xb[RPW][2][4];  // the backward's y_i / x_i tiles (y_9 / x_9 reloaded during the head)
+  float yb[RPW][2][4];  // the backward's y_i tile and its x_i tile (packed bf16), y_9 / x_9 reloaded in the head
+  uint2 xb[RPW][2];
   // ======================= head =============================================================================
   // x10 = relu(bn(y9)) + x9, 2x2 max-pool, fc1 + ReLU, fc2, cross-entropy (mean over the batch) and their
   // backward down to g = dL/dx10, all inside the workgroup.
@@ -939,13 +948,13 @@ __global__ void __launch_bounds__(64 * NW) k_pk_step(Ctx cx, PkArgs pa) {
     }
     {  // y_9 / x_9 for the first backward block (this thread's own stores: no cross-thread hand-off)
       const float* yp = cx.Y + (size_t)(NBLK - 1) * B * 8192 + img;
-      const float* xp = cx.X + (size_t)(NBLK - 1) * B * 8192 + img;
+      const float* xp = cx.X + ((size_t)(NBLK - 1) * B * 8192 + img) / 2;
 #pragma unroll
       for (int rr = 0; rr < RPW; ++rr)
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
           ld4v(yp + tl(r0 + rr, h, lane), yb[rr][h]);
-          ld4v(xp + tl(r0 + rr, h, lane), xb[rr][h]);
+          xb[rr][h] = ldx(xp, r0 + rr, h, lane);
         }
     }
     lds_barrier();
@@ -1021,8 +1030,8 @@ __global__ void __launch_bounds__(64 * NW) k_pk_step(Ctx cx, PkArgs pa) {
 #pragma unroll
       for (int h = 0; h < 2; ++h) {
         const int ch = 16 * h + c, rowoff = (r0 + rr + 1) * 16 + 4 * q;
-        const unsigned b0 = bfbits(xb[rr][h][0]), b1 = bfbits(xb[rr][h][1]);
-        const unsigned b2 = bfbits(xb[rr][h][2]), b3 = bfbits(xb[rr][h][3]);
+        const unsigned b0 = xb[rr][h].x & 0xffffu, b1 = xb[rr][h].x >> 16;
+        const unsigned b2 = xb[rr][h].y & 0xffffu, b3 = xb[rr][h].y >> 16;
         unsigned short* p1 = xT + (32 + ch) * P::XT_S + rowoff;  // kw = 1: x at the same column
         *(uint2*)p1 = uint2{b0 | (b1 << 16), b2 | (b3 << 16)};
         unsigned short* p0 = xT + ch * P::XT_S + rowoff;  // kw = 0: column + 1
@@ -1043,13 +1052,13 @@ __global__ void __launch_bounds__(64 * NW) k_pk_step(Ctx cx, PkArgs pa) {
     if (i == 5) PK_STAMP(cx, 28);
     if (i > 0) {  // prefetch y_{i-1} / x_{i-1}; the loads land while this block's convolutions run
       const float* yp = cx.Y + (size_t)(i - 1) * B * 8192 + img;
-      const float* xp = cx.X + (size_t)(i - 1) * B * 8192 + img;
+      const float* xp = cx.X + ((size_t)(i - 1) * B * 8192 + img) / 2;
 #pragma unroll
       for (int rr = 0; rr < RPW; ++rr)
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
           ld4v(yp + tl(r0 + rr, h, lane), yb[rr][h]);
-          ld4v(xp + tl(r0 + rr, h, lane), xb[rr][h]);
+          xb[rr][h] = ldx(xp, r0 + rr, h, lane);
         }
     } else {  // last block: prefetch what the stem backward needs (pool codes, raw image words)
 #pragma unroll

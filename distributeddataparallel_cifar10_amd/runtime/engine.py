@@ -258,8 +258,12 @@ class NetResDeepEngine:
         """Per-block activation region (X, Y, DY, G) as NHWC [count, batch, 16, 16, 32].
 
         The multi-kernel engine stores NHWC directly.  The persistent engine stores the MFMA fragment-tiled layout
-        [row][h][lane = 16q + c][i] holding element (row, col = 4q + i, ch = 16h + c) (netresdeep_persistent.hip: tl).
+        [row][h][lane = 16q + c][i] holding element (row, col = 4q + i, ch = 16h + c) (netresdeep_persistent.hip: tl),
+        with X in bf16.
         """
+        if self.cfg.persistent and name == "X":  # block inputs are kept as bf16 (only used as a bf16 operand)
+            raw = self.region(name, count * batch * 4096).view(torch.bfloat16).float()
+            return tile_to_nhwc(raw, count, batch)
         raw = self.region(name, count * batch * 8192)
         if not self.cfg.persistent:
             return raw.view(count, batch, 16, 16, 32)
