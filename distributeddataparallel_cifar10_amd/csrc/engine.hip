@@ -91,6 +91,7 @@ struct Engine {
   int pk_waves = 8;
   int xpack = 0;  // experimental one-XCD placement of the persistent kernel (env DCA_PK_XPACK=1)
   int staged_b = 0;  // persistent engine: batch slots of the current staging parity that hold the next batch
+  int split = 0;     // persistent engine: two-phase step (fc all-reduce overlapped); default on when world_size > 1
   pk::PkArgs pa{};
   std::map<std::string, void*> regions;
   // dynamic LDS sizes
@@ -146,7 +147,7 @@ static int alloc_workspace(Engine* e) {
       {"RS_BASE", 64 * 4},           {"CURSOR", 16},                  {"STEPS", 16},
       {"LOSS", 16},                  {"STAMPS", 32 * 256 * 8 * 2 * 8},
       {"GRAN", 2 * 64 * 64 * 8},     {"EPOCH", 16},                   {"ERR", 16},
-      {"TSLAB", bmax * WSLAB_N * 4}, {"BNG", 64 * 4}, {"IDS", 64 * 4}, {"W1B", 65536 * 2}, {"XCC", 64 * 8}, {"SIMG", 2 * 64 * 3072}, {"SLAB", 2 * 64 * 4}, {"SWF", 2 * 3 * 64 * 4 * 2},
+      {"TSLAB", bmax * WSLAB_N * 4}, {"BNG", 64 * 4}, {"IDS", 64 * 4}, {"W1B", 65536 * 2}, {"XCC", 64 * 8}, {"SIMG", 2 * 64 * 3072}, {"SLAB", 2 * 64 * 4}, {"GH", bmax * 8192 * 4}, {"SWF", 2 * 3 * 64 * 4 * 2},
   };
   size_t total = 0;
   for (auto& r : regs) total += align_up(r.bytes, 256);
@@ -195,6 +196,7 @@ static int alloc_workspace(Engine* e) {
   e->pa.ids = (int*)e->regions["IDS"];
   e->pa.xcc = (unsigned long long*)e->regions["XCC"];
   e->pa.simg = (uint8_t*)e->regions["SIMG"];
+  e->pa.gh = (float*)e->regions["GH"];
   e->pa.slab = (int*)e->regions["SLAB"];
   e->pa.debug = e->in.debug;
   return 0;
@@ -219,17 +221,48 @@ static int set_lds_limits(Engine* e) {
 static int enqueue_step_persistent(Engine* e, int B, int part) {
   Ctx cx = e->base;
   cx.B = B;
+  const bool multi = e->in.world_size > 1;
+  const bool rccl_overlap = e->split && multi && part == 0;  // fc all-reduce overlapped with the trunk backward
   if (part != 2) {
     pk::PkArgs pa = e->pa;
     // Packing the image workgroups onto one XCD (grid 8 x B, see pk_img) keeps the BN exchange inside one L2,
     // but measured slower end to end (119 vs 105 us/step: every workgroup then shares one L2 and its
     // bandwidth); opt-in for experiments only (DCA_PK_XPACK=1).
     pa.xpack = (B <= 32 && e->xpack) ? 1 : 0;
-    hipLaunchKernelGGL(pk::k_pk_step<8>, dim3(pa.xpack ? 8 * B : B), dim3(64 * 8), pk::Plan::TOTAL, e->st, cx, pa);
-    hipLaunchKernelGGL(pk::k_pk_reduce, dim3(pk::R_GRID), dim3(256), 0, e->st, cx, e->pa);
+    const dim3 grid(pa.xpack ? 8 * B : B), blk(64 * 8);
+    if (!e->split) {
+      pa.phase = 0;
+      hipLaunchKernelGGL(pk::k_pk_step<8>, grid, blk, pk::Plan::TOTAL, e->st, cx, pa);
+      hipLaunchKernelGGL(pk::k_pk_reduce, dim3(pk::R_GRID), dim3(256), 0, e->st, cx, e->pa, 1);
+    } else {
+      // Split mode: phase 1 (stem, forward, head) | phase 2 (backward).  The fc gradients -- bucket A, 86 % of
+      // the gradient bytes -- are final after phase 1, so with RCCL they are reduced and all-reduced on the
+      // comm stream while phase 2 runs; bucket B (trunk, BN, stem, CC4 segment) follows the slab reduction.
+      pa.phase = 1;
+      hipLaunchKernelGGL(pk::k_pk_step<8>, grid, blk, pk::Plan::TOTAL, e->st, cx, pa);
+      if (rccl_overlap) {
+        HIPCK(hipEventRecord(e->evA, e->st));
+        HIPCK(hipStreamWaitEvent(e->cst, e->evA, 0));
+        hipLaunchKernelGGL(pk::k_pk_fc, dim3(pk::R_FC + 1), dim3(256), 0, e->cst, cx);
+        NCCK(ncclAllReduce(cx.grads, cx.grads, BUCKET_A_END, ncclFloat32, ncclSum, e->comm, e->cst));
+      }
+      pa.phase = 2;
+      hipLaunchKernelGGL(pk::k_pk_step<8>, grid, blk, pk::Plan::TOTAL, e->st, cx, pa);
+      hipLaunchKernelGGL(pk::k_pk_reduce, dim3(pk::R_TRUNK + pk::R_STEM + 1), dim3(256), 0, e->st, cx, e->pa, 0);
+      if (!rccl_overlap) hipLaunchKernelGGL(pk::k_pk_fc, dim3(pk::R_FC + 1), dim3(256), 0, e->st, cx);
+    }
   }
-  if (e->in.world_size > 1) {
-    if (part == 0) NCCK(ncclAllReduce(cx.grads, cx.grads, FLAT_N, ncclFloat32, ncclSum, e->comm, e->st));
+  if (multi) {
+    if (rccl_overlap) {  // bucket B on the comm stream, after bucket A (one communicator, one stream: ordered)
+      HIPCK(hipEventRecord(e->evB, e->st));
+      HIPCK(hipStreamWaitEvent(e->cst, e->evB, 0));
+      NCCK(ncclAllReduce(cx.grads + OFF_CONVW, cx.grads + OFF_CONVW, FLAT_N - OFF_CONVW, ncclFloat32, ncclSum,
+                         e->comm, e->cst));
+      HIPCK(hipEventRecord(e->evC, e->cst));
+      HIPCK(hipStreamWaitEvent(e->st, e->evC, 0));
+    } else if (part == 0) {
+      NCCK(ncclAllReduce(cx.grads, cx.grads, FLAT_N, ncclFloat32, ncclSum, e->comm, e->st));
+    }
     if (part != 1) hipLaunchKernelGGL(e->kapply, dim3(64), dim3(NT), 0, e->st, cx, 1);
   }
   HIPCK(hipGetLastError());
@@ -472,6 +505,11 @@ int dca_engine_create(const DcaInit* in, int n_indices, void** out) {
   {
     const char* xp = getenv("DCA_PK_XPACK");
     e->xpack = xp && xp[0] == '1';
+    // Split mode (phase 1 | phase 2, fc all-reduce overlapped with the trunk backward): +7.7 us/step at
+    // world_size 1 (kernel boundary + state restore, profiles/bench_split_ws1.log), which the overlap repays
+    // only if RCCL needs more than that for the 264 KB fc bucket.  Opt-in: DCA_PK_SPLIT=1.
+    const char* sp = getenv("DCA_PK_SPLIT");
+    e->split = sp && sp[0] == '1';
   }
   if (e->persistent && !e->bf) {
     g_err = "the persistent engine is bf16-only (fp32 MFMA needs all CUs: use the multi-kernel engine)";

@@ -38,6 +38,8 @@ struct PkArgs {
   int* slab;                 // [2][64]       stages the NEXT batch into the other parity, see k_pk_step
   unsigned long long* xcc;   // [64] granules: XCD id of each image workgroup (published with round 0)
   int xpack;                 // 1: grid = 8 x batch, only blocks b % 8 == 0 work (one XCD under round-robin dispatch)
+  int phase;                 // 0: whole step; split mode: 1 = stem + forward + head, 2 = backward + stem backward
+  float* gh;                 // [64][8192] split mode: dL/dx10 of each image (tiled), handed from phase 1 to 2
   int debug;                 // also store DY / G for the numerical diagnostics
 };
 
@@ -577,6 +579,10 @@ __global__ void __launch_bounds__(64 * NW) k_pk_step(Ctx cx, PkArgs pa) {
   const int next_id = sample_id(cx, B + n);  // image n of the NEXT batch (staged at the end of this step)
   PK_STAMP(cx, 0);
 
+  float g[RPW][2][4];   // dL/dx of the current block input (backward), starting with dL/dx10 from the head
+  float yb[RPW][2][4];  // the backward's y_i tile and its x_i tile (packed bf16), y_9 / x_9 loaded by the head
+  uint2 xb[RPW][2];
+  if (pa.phase != 2) {  // ---------------- stem, forward, head (whole step, or split-mode phase 1) ----------------
   // ======================= stem: gather + normalise + conv1 + bias + ReLU + 2x2 max-pool =================
   // Input staged as bf16 NHWC4 pixels (3 channels + a zero), so an MFMA K-group of 4 is one tap of one pixel:
   // v_mfma_f32_16x16x16_bf16 with K = (tap, channel), 3 MFMAs cover the 9 taps (taps 9..11 have zero weights).
@@ -791,12 +797,9 @@ __global__ void __launch_bounds__(64 * NW) k_pk_step(Ctx cx, PkArgs pa) {
   }
   PK_STAMP(cx, 12);
 
-  float yb[RPW][2][4];  // the backward's y_i tile and its x_i tile (packed bf16), y_9 / x_9 reloaded in the head
-  uint2 xb[RPW][2];
   // ======================= head =============================================================================
   // x10 = relu(bn(y9)) + x9, 2x2 max-pool, fc1 + ReLU, fc2, cross-entropy (mean over the batch) and their
   // backward down to g = dL/dx10, all inside the workgroup.
-  float g[RPW][2][4];
   {
     float* Pv = (float*)(U + P::U_P);      // [2048] pooled features, NCHW flatten order c*64 + ph*8 + pw
     float* dp = (float*)(U + P::U_DP);     // [2048] dL/dpooled
@@ -974,6 +977,31 @@ __global__ void __launch_bounds__(64 * NW) k_pk_step(Ctx cx, PkArgs pa) {
 #pragma unroll
         for (int h = 0; h < 2; ++h) st4v(cx.G + img + tl(r0 + rr, h, lane), g[rr][h]);
     }
+  }
+  if (pa.phase == 1) {  // split mode: hand dL/dx10 to phase 2 (own-thread layout) and end here
+#pragma unroll
+    for (int rr = 0; rr < RPW; ++rr)
+#pragma unroll
+      for (int h = 0; h < 2; ++h) st4v(pa.gh + img + tl(r0 + rr, h, lane), g[rr][h]);
+    return;
+  }
+  } else {  // ---------------- split-mode phase 2: restore what phase 1 left in LDS / registers ----------------
+#pragma unroll
+    for (int rr = 0; rr < RPW; ++rr)
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        ld4v(pa.gh + img + tl(r0 + rr, h, lane), g[rr][h]);
+        ld4v(cx.Y + (size_t)(NBLK - 1) * B * 8192 + img + tl(r0 + rr, h, lane), yb[rr][h]);
+        xb[rr][h] = ldx(cx.X + ((size_t)(NBLK - 1) * B * 8192 + img) / 2, r0 + rr, h, lane);
+      }
+    if (t < NBLK * 32) {  // batch (mean, invstd) of every block, written by workgroup 0 of phase 1
+      const float2 st = cx.STATS[t];
+      stat[(t >> 5) * 64 + (t & 31)] = st.x;
+      stat[(t >> 5) * 64 + 32 + (t & 31)] = st.y;
+    }
+    if (t < 64) misc[320 + t] = cx.params[OFF_BNW + t];  // gamma | beta
+    if (t == 0) misc[P_FAST] = 0.f;
+    stage_wt<NW>(WT, cx.wt_d);
   }
   PK_STAMP(cx, 13);
   lds_barrier();  // every wave is done with the head's LDS before the backward's tiles overwrite it
@@ -1259,187 +1287,217 @@ __device__ __forceinline__ float sgd_put_pre(const Ctx& cx, int pidx, float gval
   return oldp;
 }
 
-__global__ void __launch_bounds__(256) k_pk_reduce(Ctx cx, PkArgs pa) {
-  __shared__ f32x4 red[256];
-  __shared__ float stage[64 * 32 + 64 * 64];
-  const int t = threadIdx.x, bid = blockIdx.x, B = cx.B;
-  if (bid < R_TRUNK + R_STEM) {
-    const bool stem = bid >= R_TRUNK;
-    const int chunk = stem ? bid - R_TRUNK : bid;
-    const int slot = t & 63, grp = t >> 6, e0 = chunk * 256 + slot * 4;
-    const float* src = stem ? cx.SSLAB : pa.tslab;
-    const int stride = stem ? SSLAB_N : WSLAB_N, lim = stem ? SSLAB_N : WSLAB_N;
-    // parameter index of each of this thread's 4 outputs (slab fragment order -> flat layout), -1 if none
-    int pix[4];
-    float pold[4];
+// slab reduction + SGD of the shared trunk conv (36 chunks of 256 outputs) and of conv1 (5 chunks)
+__device__ __forceinline__ void pk_red_trunk_stem(const Ctx& cx, const PkArgs& pa, int bid, f32x4* red) {
+  const int t = threadIdx.x, B = cx.B;
+  const bool stem = bid >= R_TRUNK;
+  const int chunk = stem ? bid - R_TRUNK : bid;
+  const int slot = t & 63, grp = t >> 6, e0 = chunk * 256 + slot * 4;
+  const float* src = stem ? cx.SSLAB : pa.tslab;
+  const int stride = stem ? SSLAB_N : WSLAB_N, lim = stem ? SSLAB_N : WSLAB_N;
+  // parameter index of each of this thread's 4 outputs (slab fragment order -> flat layout), -1 if none
+  int pix[4];
+  float pold[4];
+#pragma unroll
+  for (int ii = 0; ii < 4; ++ii) {
+    const int e = e0 + ii;
+    int pidx = -1;
+    if (e < lim) {
+      if (!stem) {
+        const int tt = e >> 8, ln = (e >> 2) & 63, mt = tt & 1, nt = tt >> 1, tap = nt >> 1, cih = nt & 1;
+        pidx = OFF_CONVW + (16 * mt + 4 * (ln >> 4) + ii) * 288 + (16 * cih + (ln & 15)) * 9 + tap;
+      } else if (e < 1024) {
+        const int tt = e >> 8, ln = (e >> 2) & 63, mt = tt & 1, nt = tt >> 1, k = 16 * nt + (ln & 15);
+        if (k < 27) pidx = OFF_C1W + (16 * mt + 4 * (ln >> 4) + ii) * 27 + k;
+      } else if (e < 1056) {
+        pidx = OFF_C1B + (e - 1024);
+      }
+    }
+    pix[ii] = pidx;
+    pold[ii] = cx.params[pidx >= 0 ? pidx : 0];  // issued with the slab loads
+  }
+  f32x4 s = z4();
+  {  // every load unconditional (clamped index), all in flight together; out-of-range ones are dropped after
+    const int ec = e0 < lim ? e0 : lim - 4;
+    f32x4 v[16];
+#pragma unroll
+    for (int u = 0; u < 16; ++u) {
+      const int k = grp + 4 * u;
+      v[u] = ld4(src + (size_t)(k < B ? k : B - 1) * stride + ec);
+    }
+#pragma unroll
+    for (int u = 0; u < 16; ++u)
+      if (grp + 4 * u < B) s += v[u];
+  }
+  red[t] = s;
+  __syncthreads();
+  if (t < 64 && e0 < lim) {
+    const f32x4 tot = red[t] + red[64 + t] + red[128 + t] + red[192 + t];
 #pragma unroll
     for (int ii = 0; ii < 4; ++ii) {
-      const int e = e0 + ii;
-      int pidx = -1;
-      if (e < lim) {
-        if (!stem) {
-          const int tt = e >> 8, ln = (e >> 2) & 63, mt = tt & 1, nt = tt >> 1, tap = nt >> 1, cih = nt & 1;
-          pidx = OFF_CONVW + (16 * mt + 4 * (ln >> 4) + ii) * 288 + (16 * cih + (ln & 15)) * 9 + tap;
-        } else if (e < 1024) {
-          const int tt = e >> 8, ln = (e >> 2) & 63, mt = tt & 1, nt = tt >> 1, k = 16 * nt + (ln & 15);
-          if (k < 27) pidx = OFF_C1W + (16 * mt + 4 * (ln >> 4) + ii) * 27 + k;
-        } else if (e < 1056) {
-          pidx = OFF_C1B + (e - 1024);
-        }
+      const int pidx = pix[ii];
+      if (pidx < 0) continue;
+      const float wv = sgd_put_pre(cx, pidx, tot[ii], pold[ii]);
+      if (!cx.fuse_sgd) continue;
+      if (pidx >= OFF_CONVW && pidx < OFF_CONVW + 9216) {
+        const int r = pidx - OFF_CONVW, co = r / 288, ci = (r / 9) % 32, tap = r % 9;
+        ((unsigned short*)cx.wt_f)[(tap * 32 + co) * 32 + ci] = bfbits(wv);
+        ((unsigned short*)cx.wt_d)[((8 - tap) * 32 + ci) * 32 + co] = bfbits(wv);
+      } else if (pidx >= OFF_C1W && pidx < OFF_C1W + 864) {
+        const int r = pidx - OFF_C1W, co = r / 27, k = r % 27;
+        const unsigned short wb = bfbits(wv);
+        ((unsigned short*)cx.sw)[co * 32 + k] = wb;
+        ((unsigned short*)cx.swf)[swf_slot(co, k)] = wb;
       }
-      pix[ii] = pidx;
-      pold[ii] = cx.params[pidx >= 0 ? pidx : 0];  // issued with the slab loads
-    }
-    f32x4 s = z4();
-    {  // every load unconditional (clamped index), all in flight together; out-of-range ones are dropped after
-      const int ec = e0 < lim ? e0 : lim - 4;
-      f32x4 v[16];
-#pragma unroll
-      for (int u = 0; u < 16; ++u) {
-        const int k = grp + 4 * u;
-        v[u] = ld4(src + (size_t)(k < B ? k : B - 1) * stride + ec);
-      }
-#pragma unroll
-      for (int u = 0; u < 16; ++u)
-        if (grp + 4 * u < B) s += v[u];
-    }
-    red[t] = s;
-    __syncthreads();
-    if (t < 64 && e0 < lim) {
-      const f32x4 tot = red[t] + red[64 + t] + red[128 + t] + red[192 + t];
-#pragma unroll
-      for (int ii = 0; ii < 4; ++ii) {
-        const int pidx = pix[ii];
-        if (pidx < 0) continue;
-        const float wv = sgd_put_pre(cx, pidx, tot[ii], pold[ii]);
-        if (!cx.fuse_sgd) continue;
-        if (pidx >= OFF_CONVW && pidx < OFF_CONVW + 9216) {
-          const int r = pidx - OFF_CONVW, co = r / 288, ci = (r / 9) % 32, tap = r % 9;
-          ((unsigned short*)cx.wt_f)[(tap * 32 + co) * 32 + ci] = bfbits(wv);
-          ((unsigned short*)cx.wt_d)[((8 - tap) * 32 + ci) * 32 + co] = bfbits(wv);
-        } else if (pidx >= OFF_C1W && pidx < OFF_C1W + 864) {
-          const int r = pidx - OFF_C1W, co = r / 27, k = r % 27;
-          const unsigned short wb = bfbits(wv);
-          ((unsigned short*)cx.sw)[co * 32 + k] = wb;
-          ((unsigned short*)cx.swf)[swf_slot(co, k)] = wb;
-        }
-      }
-    }
-    return;
-  }
-  if (bid < R_TRUNK + R_STEM + R_FC) {  // dW1[j][64f .. 64f+63] = sum_b dh[b][j] * p[b][k]
-    const int f = bid - R_TRUNK - R_STEM;
-    float* dh_s = stage;          // [B][32]
-    float* p_s = stage + 64 * 32; // [B][64]
-    f32x4 dh4[2], p4[4];
-    const int j = t >> 3, kk = 8 * (t & 7);
-    const int base = OFF_FC1W + j * 2048 + 64 * f + kk;
-    const f32x4 o0 = ld4(cx.params + base), o1 = ld4(cx.params + base + 4);  // old weights, fetched early
-#pragma unroll
-    for (int m = 0; m < 2; ++m) {
-      const int idx = t + 256 * m;
-      dh4[m] = ld4(cx.HDH + 4 * (idx < B * 8 ? idx : 0));
-    }
-#pragma unroll
-    for (int m = 0; m < 4; ++m) {
-      const int idx = t + 256 * m, ic = idx < B * 16 ? idx : 0, b = ic >> 4, k4 = ic & 15;
-      p4[m] = ld4(cx.HP + (size_t)b * 2048 + 64 * f + 4 * k4);
-    }
-#pragma unroll
-    for (int m = 0; m < 2; ++m)
-      if (t + 256 * m < B * 8) st4(dh_s + 4 * (t + 256 * m), dh4[m]);
-#pragma unroll
-    for (int m = 0; m < 4; ++m)
-      if (t + 256 * m < B * 16) st4(p_s + 4 * (t + 256 * m), p4[m]);
-    __syncthreads();
-    f32x4 a0 = z4(), a1 = z4();
-#pragma unroll 8
-    for (int b = 0; b < B; ++b) {
-      const float dh = dh_s[b * 32 + j];
-      a0 += dh * ld4(p_s + b * 64 + kk);
-      a1 += dh * ld4(p_s + b * 64 + kk + 4);
-    }
-    st4(cx.grads + base, a0);
-    st4(cx.grads + base + 4, a1);
-    if (cx.fuse_sgd) {
-      const f32x4 n0 = o0 - cx.lr * a0, n1 = o1 - cx.lr * a1;
-      st4(cx.params + base, n0);
-      st4(cx.params + base + 4, n1);
-      *(uint4*)((unsigned short*)cx.w1b + base - OFF_FC1W) =
-          uint4{pk2(n0[0], n0[1]), pk2(n0[2], n0[3]), pk2(n1[0], n1[1]), pk2(n1[2], n1[3])};
-    }
-    return;
-  }
-  // bookkeeping workgroup: fc1 bias, fc2, BN affine grads, loss, cursor, epoch, next batch ids, CC4 segment
-  {
-    float* hh_s = stage;             // [B][32]
-    float* dl_s = stage + 64 * 32;   // [B][16]
-    float* dh_s = dl_s + 64 * 16;    // [B][32]
-    {  // all loads first (clamped, unconditional), then the LDS stores
-      float hv[8], dv[8], lv[3];
-#pragma unroll
-      for (int m = 0; m < 8; ++m) {
-        const int idx = t + 256 * m, ic = idx < B * 32 ? idx : 0;
-        hv[m] = cx.HH[ic];
-        dv[m] = cx.HDH[ic];
-      }
-#pragma unroll
-      for (int m = 0; m < 3; ++m) {
-        const int idx = t + 256 * m;
-        lv[m] = cx.HDL[idx < B * 10 ? idx : 0];
-      }
-      const float lo = cx.HLOSS[t < B ? t : 0];
-#pragma unroll
-      for (int m = 0; m < 8; ++m) {
-        const int idx = t + 256 * m;
-        if (idx < B * 32) {
-          hh_s[idx] = hv[m];
-          dh_s[idx] = dv[m];
-        }
-      }
-#pragma unroll
-      for (int m = 0; m < 3; ++m) {
-        const int idx = t + 256 * m;
-        if (idx < B * 10) dl_s[(idx / 10) * 16 + idx % 10] = lv[m];
-      }
-      ((float*)red)[t] = t < B ? lo : 0.f;
-    }
-    __syncthreads();
-    for (int idx = t; idx < 32 + 320 + 10 + 64; idx += 256) {
-      float s = 0.f;
-      if (idx < 32) {
-#pragma unroll 8
-        for (int b = 0; b < B; ++b) s += dh_s[b * 32 + idx];
-        sgd_put(cx, OFF_FC1B + idx, s);
-      } else if (idx < 352) {
-        const int o = (idx - 32) >> 5, jj = (idx - 32) & 31;
-#pragma unroll 8
-        for (int b = 0; b < B; ++b) s += dl_s[b * 16 + o] * hh_s[b * 32 + jj];
-        sgd_put(cx, OFF_FC2W + o * 32 + jj, s);
-      } else if (idx < 362) {
-        const int o = idx - 352;
-#pragma unroll 8
-        for (int b = 0; b < B; ++b) s += dl_s[b * 16 + o];
-        sgd_put(cx, OFF_FC2B + o, s);
-      } else {
-        const int k = idx - 362;  // 0..31 dgamma, 32..63 dbeta
-        sgd_put(cx, (k < 32 ? OFF_BNW : OFF_BNB) + (k & 31), pa.bng[k]);
-      }
-    }
-    if (t == 0) {
-      float s = 0.f;
-      for (int k = 0; k < B; ++k) s += ((float*)red)[k];
-      *cx.loss_acc += (double)(s / (float)B);
-      *cx.cursor += B;
-      *cx.step_count += 1;
-      *cx.nbt += NBLK;  // BatchNorm num_batches_tracked: +1 per application
-      *pa.epoch += 1;
-    }
-    if (!cx.fuse_sgd && t < 64) {
-      const float v = t < 32 ? cx.rm[t] : cx.rv[t - 32];
-      cx.grads[OFF_RS + t] = cx.rank == 0 ? v : 0.f;
     }
   }
+  }
+
+// dW1[j][64f .. 64f+63] = sum_b dh[b][j] * p[b][k] (+ SGD and the head's bf16 copy)
+__device__ __forceinline__ void pk_red_fc1(const Ctx& cx, int f, float* stage) {
+  const int t = threadIdx.x, B = cx.B;
+  float* dh_s = stage;          // [B][32]
+  float* p_s = stage + 64 * 32; // [B][64]
+  f32x4 dh4[2], p4[4];
+  const int j = t >> 3, kk = 8 * (t & 7);
+  const int base = OFF_FC1W + j * 2048 + 64 * f + kk;
+  const f32x4 o0 = ld4(cx.params + base), o1 = ld4(cx.params + base + 4);  // old weights, fetched early
+#pragma unroll
+  for (int m = 0; m < 2; ++m) {
+    const int idx = t + 256 * m;
+    dh4[m] = ld4(cx.HDH + 4 * (idx < B * 8 ? idx : 0));
+  }
+#pragma unroll
+  for (int m = 0; m < 4; ++m) {
+    const int idx = t + 256 * m, ic = idx < B * 16 ? idx : 0, b = ic >> 4, k4 = ic & 15;
+    p4[m] = ld4(cx.HP + (size_t)b * 2048 + 64 * f + 4 * k4);
+  }
+#pragma unroll
+  for (int m = 0; m < 2; ++m)
+    if (t + 256 * m < B * 8) st4(dh_s + 4 * (t + 256 * m), dh4[m]);
+#pragma unroll
+  for (int m = 0; m < 4; ++m)
+    if (t + 256 * m < B * 16) st4(p_s + 4 * (t + 256 * m), p4[m]);
+  __syncthreads();
+  f32x4 a0 = z4(), a1 = z4();
+#pragma unroll 8
+  for (int b = 0; b < B; ++b) {
+    const float dh = dh_s[b * 32 + j];
+    a0 += dh * ld4(p_s + b * 64 + kk);
+    a1 += dh * ld4(p_s + b * 64 + kk + 4);
+  }
+  st4(cx.grads + base, a0);
+  st4(cx.grads + base + 4, a1);
+  if (cx.fuse_sgd) {
+    const f32x4 n0 = o0 - cx.lr * a0, n1 = o1 - cx.lr * a1;
+    st4(cx.params + base, n0);
+    st4(cx.params + base + 4, n1);
+    *(uint4*)((unsigned short*)cx.w1b + base - OFF_FC1W) =
+        uint4{pk2(n0[0], n0[1]), pk2(n0[2], n0[3]), pk2(n1[0], n1[1]), pk2(n1[2], n1[3])};
+  }
+  }
+
+// fc1 bias, fc2 weight / bias gradients (+ SGD) from the head's per-image vectors
+__device__ __forceinline__ void pk_red_fc_small(const Ctx& cx, float* stage) {
+  const int t = threadIdx.x, B = cx.B;
+  float* hh_s = stage;             // [B][32]
+  float* dl_s = stage + 64 * 32;   // [B][16]
+  float* dh_s = dl_s + 64 * 16;    // [B][32]
+  {  // all loads first (clamped, unconditional), then the LDS stores
+  float hv[8], dv[8], lv[3];
+#pragma unroll
+  for (int m = 0; m < 8; ++m) {
+    const int idx = t + 256 * m, ic = idx < B * 32 ? idx : 0;
+    hv[m] = cx.HH[ic];
+    dv[m] = cx.HDH[ic];
+  }
+#pragma unroll
+  for (int m = 0; m < 3; ++m) {
+    const int idx = t + 256 * m;
+    lv[m] = cx.HDL[idx < B * 10 ? idx : 0];
+  }
+#pragma unroll
+  for (int m = 0; m < 8; ++m) {
+    const int idx = t + 256 * m;
+    if (idx < B * 32) {
+      hh_s[idx] = hv[m];
+      dh_s[idx] = dv[m];
+    }
+  }
+#pragma unroll
+  for (int m = 0; m < 3; ++m) {
+    const int idx = t + 256 * m;
+    if (idx < B * 10) dl_s[(idx / 10) * 16 + idx % 10] = lv[m];
+  }
+  }
+  __syncthreads();
+  for (int idx = t; idx < 32 + 320 + 10; idx += 256) {
+  float s = 0.f;
+  if (idx < 32) {
+#pragma unroll 8
+    for (int b = 0; b < B; ++b) s += dh_s[b * 32 + idx];
+    sgd_put(cx, OFF_FC1B + idx, s);
+  } else if (idx < 352) {
+    const int o = (idx - 32) >> 5, jj = (idx - 32) & 31;
+#pragma unroll 8
+    for (int b = 0; b < B; ++b) s += dl_s[b * 16 + o] * hh_s[b * 32 + jj];
+    sgd_put(cx, OFF_FC2W + o * 32 + jj, s);
+  } else {
+    const int o = idx - 352;
+#pragma unroll 8
+    for (int b = 0; b < B; ++b) s += dl_s[b * 16 + o];
+    sgd_put(cx, OFF_FC2B + o, s);
+  }
+  }
+}
+
+// BN affine grads (+ SGD), loss, cursor, step count, num_batches_tracked, epoch, CC4 running-stat segment
+__device__ __forceinline__ void pk_bookkeeping(const Ctx& cx, const PkArgs& pa, float* red) {
+  const int t = threadIdx.x, B = cx.B;
+  const float lo = cx.HLOSS[t < B ? t : 0];
+  const float bg = pa.bng[t & 63];
+  red[t] = t < B ? lo : 0.f;
+  if (t < 64) sgd_put(cx, (t < 32 ? OFF_BNW : OFF_BNB) + (t & 31), bg);  // 0..31 dgamma, 32..63 dbeta
+  __syncthreads();
+  if (t == 0) {
+    float s = 0.f;
+    for (int k = 0; k < B; ++k) s += red[k];
+    *cx.loss_acc += (double)(s / (float)B);
+    *cx.cursor += B;
+    *cx.step_count += 1;
+    *cx.nbt += NBLK;  // BatchNorm num_batches_tracked: +1 per application
+    *pa.epoch += 1;
+  }
+  if (!cx.fuse_sgd && t < 64) {
+    const float v = t < 32 ? cx.rm[t] : cx.rv[t - 32];
+    cx.grads[OFF_RS + t] = cx.rank == 0 ? v : 0.f;
+  }
+}
+
+// Reduction + SGD after the persistent step.  with_fc = 1: grid R_GRID (trunk | stem | fc1 | bookkeeping incl.
+// the small fc grads); with_fc = 0 (split mode, the fc part runs as k_pk_fc on the comm stream): grid
+// R_TRUNK + R_STEM + 1.
+__global__ void __launch_bounds__(256) k_pk_reduce(Ctx cx, PkArgs pa, int with_fc) {
+  __shared__ f32x4 red[256];
+  __shared__ float stage[64 * 32 + 64 * 64];
+  const int bid = blockIdx.x;
+  if (bid < R_TRUNK + R_STEM) {
+    pk_red_trunk_stem(cx, pa, bid, red);
+  } else if (with_fc && bid < R_TRUNK + R_STEM + R_FC) {
+    pk_red_fc1(cx, bid - R_TRUNK - R_STEM, stage);
+  } else {
+    if (with_fc) pk_red_fc_small(cx, stage);
+    __syncthreads();
+    pk_bookkeeping(cx, pa, (float*)red);
+  }
+}
+
+// Split mode: the fc gradients (bucket A, 86 % of the gradient bytes) as soon as the head has run, so their
+// all-reduce overlaps the trunk backward.  Grid R_FC + 1.
+__global__ void __launch_bounds__(256) k_pk_fc(Ctx cx) {
+  __shared__ float stage[64 * 32 + 64 * 64];
+  if (blockIdx.x < R_FC) pk_red_fc1(cx, blockIdx.x, stage);
+  else pk_red_fc_small(cx, stage);
 }
 
 }  // namespace pk

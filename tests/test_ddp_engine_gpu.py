@@ -96,8 +96,10 @@ def _worker(rank, port, dtype, persistent, q):
             dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("dtype,persistent", [("bf16", True), ("fp32", False), ("bf16", False)])
-def test_engine_ddp_two_ranks_one_gpu(gpu, port, dtype, persistent):
+@pytest.mark.parametrize("dtype,persistent,split", [("bf16", True, "0"), ("bf16", True, "1"), ("fp32", False, "0"),
+                                                    ("bf16", False, "0")])
+def test_engine_ddp_two_ranks_one_gpu(gpu, port, dtype, persistent, split, monkeypatch):
+    monkeypatch.setenv("DCA_PK_SPLIT", split)  # inherited by the spawned ranks
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     procs = [ctx.Process(target=_worker, args=(r, port, dtype, persistent, q)) for r in range(WS)]

@@ -113,3 +113,13 @@ def test_bench_contract(gpu):
               "vs_baseline", "dtype", "data", "config"):
         assert k in rec, k
     assert rec["n_gpus"] == 1 and rec["value"] > 0 and rec["loss_finite"]
+
+
+def test_split_mode_matches_oracle(gpu, monkeypatch):
+    """Two-phase persistent step (phase 1: stem/forward/head, phase 2: backward; fc gradients in their own
+    kernel) gives the same step as the fused kernel."""
+    from engine_diag import compare_one_step
+    monkeypatch.setenv("DCA_PK_SPLIT", "1")
+    res = compare_one_step("bf16", 4, 32, True, seed=7, verbose=False, persistent=True)
+    bad = {k: v for k, v in res.items() if v > 5e-2}
+    assert not bad, bad
