@@ -7,7 +7,8 @@ The reference sets ``MASTER_ADDR=localhost``, ``MASTER_PORT=12355`` and calls
     created eagerly on the right GPU;
   * MASTER_ADDR / MASTER_PORT already in the environment win (the reference's fixed port collides between
     concurrent jobs); the default address is 127.0.0.1 because the container hostname may not resolve;
-  * ``gloo`` is accepted for CPU runs/tests; ``timeout_s`` sets the process-group timeout (failure detection).
+  * ``gloo`` is accepted for CPU runs/tests; ``timeout_s`` sets the process-group timeout and
+    ``TORCH_NCCL_ASYNC_ERROR_HANDLING=1`` makes a stuck collective raise (failure detection).
 """
 from __future__ import annotations
 
@@ -24,6 +25,8 @@ DEFAULT_PORT = 12355  # reference main.py:23
 def setup(rank: int, world_size: int, backend: str = "nccl", port: Optional[int] = None,
           timeout_s: Optional[float] = None, local_rank: Optional[int] = None) -> None:
     os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    # a failed/timed-out RCCL collective aborts the communicator and raises instead of hanging (failure detection)
+    os.environ.setdefault("TORCH_NCCL_ASYNC_ERROR_HANDLING", "1")
     if port is not None:
         os.environ["MASTER_PORT"] = str(port)
     else:

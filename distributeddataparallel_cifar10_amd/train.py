@@ -52,6 +52,10 @@ class TrainConfig:
     backend: str = "nccl"
     port: Optional[int] = None
     timeout_s: Optional[float] = None
+    model: str = "netresdeep"        # netresdeep | resnet50 (generic path)
+    bucket_mb: float = 4.0           # FlatBucketDDP bucket cap (generic path)
+    profile: Optional[str] = None    # directory for torch.profiler traces / kernel summary
+    check_sync: int = 0              # >0: assert cross-rank parameter equality every N epochs (and at start)
     extra: dict = field(default_factory=dict)
 
 
@@ -76,6 +80,11 @@ def add_cli_args(ap: argparse.ArgumentParser, batch_default: int = 32) -> argpar
     ap.add_argument("--world-size", type=int, default=None, help="number of ranks (default: GPU count)")
     ap.add_argument("--port", type=int, default=None)
     ap.add_argument("--timeout", type=float, default=None, help="process-group timeout in seconds")
+    ap.add_argument("--model", default="netresdeep", choices=["netresdeep", "resnet50"])
+    ap.add_argument("--bucket-mb", type=float, default=4.0, help="gradient bucket cap (generic DDP path)")
+    ap.add_argument("--profile", default=None, metavar="DIR", help="write torch.profiler traces to DIR")
+    ap.add_argument("--check-sync", type=int, default=0, metavar="N",
+                    help="assert parameters are identical on all ranks at start and every N epochs")
     return ap
 
 
@@ -84,7 +93,8 @@ def config_from_args(a: argparse.Namespace, data_path_default: str) -> TrainConf
                        synthetic=a.synthetic or 0, engine=a.engine, dtype=a.dtype, max_steps=a.max_steps,
                        checkpoint=not a.no_checkpoint, checkpoint_path=a.checkpoint_path, resume=a.resume,
                        metrics_json=a.metrics_json, seed=a.seed, set_epoch=a.set_epoch, fail_at_step=a.fail_at_step,
-                       backend=a.backend, port=a.port, timeout_s=a.timeout)
+                       backend=a.backend, port=a.port, timeout_s=a.timeout, model=a.model, bucket_mb=a.bucket_mb,
+                       profile=a.profile, check_sync=a.check_sync)
 
 
 def load_dataset(cfg: TrainConfig):
@@ -96,8 +106,11 @@ def load_dataset(cfg: TrainConfig):
 def resolve_engine(cfg: TrainConfig, device: torch.device, model: nn.Module) -> str:
     if cfg.engine != "auto":
         return cfg.engine
-    is_netresdeep = getattr(model, "n_chans1", None) == 32 and getattr(model, "n_blocks", None) == 10
-    return "fused" if device.type == "cuda" and is_netresdeep else "torch"
+    return "fused" if device.type == "cuda" and _is_netresdeep(model) else "torch"
+
+
+def _is_netresdeep(model: nn.Module) -> bool:
+    return getattr(model, "n_chans1", None) == 32 and getattr(model, "n_blocks", None) == 10
 
 
 class _Fault(RuntimeError):
@@ -124,6 +137,15 @@ def train_loop(model, train_loader: DeviceLoader, rank: int, cfg: Optional[Train
             from .parallel.flat_ddp import FlatBucketDDP, FlatSGD
             optimizer = FlatSGD(model, cfg.lr) if isinstance(model, FlatBucketDDP) else \
                 torch.optim.SGD(model.parameters(), lr=cfg.lr)
+    from contextlib import ExitStack
+    from torch.profiler import record_function
+    from .parallel.dist import assert_params_in_sync
+    autocast = (not fused and cfg.dtype == "bf16" and train_loader.device.type == "cuda"
+                and not _is_netresdeep(unwrap(model)))  # generic models train in bf16; NetResDeep torch path = fp32
+    if cfg.check_sync:
+        assert_params_in_sync(unwrap(model))
+    stack = ExitStack()
+    prof = stack.enter_context(_profiler(cfg.profile, train_loader.device)) if cfg.profile else None
     start_time = time.time()
     for epoch in range(start_epoch, cfg.epochs + 1):
         train_loader.set_epoch(epoch)
@@ -132,7 +154,8 @@ def train_loop(model, train_loader: DeviceLoader, rank: int, cfg: Optional[Train
             idx = train_loader.indices()[:steps_per_epoch * train_loader.batch_size]
             if cfg.fail_at_step is not None and global_step < cfg.fail_at_step <= global_step + steps_per_epoch:
                 raise _Fault(f"injected failure at step {cfg.fail_at_step} (rank {rank})")
-            loss_sum, nsteps = model.engine.run_epoch(idx, train_loader.batch_size)
+            with record_function(f"epoch{epoch}:engine"):
+                loss_sum, nsteps = model.engine.run_epoch(idx, train_loader.batch_size)
         else:
             loss_sum, nsteps = 0.0, 0
             for imgs, labels in train_loader:
@@ -140,11 +163,14 @@ def train_loop(model, train_loader: DeviceLoader, rank: int, cfg: Optional[Train
                     break
                 if cfg.fail_at_step is not None and global_step + nsteps + 1 == cfg.fail_at_step:
                     raise _Fault(f"injected failure at step {cfg.fail_at_step} (rank {rank})")
-                outputs = model(imgs)
-                loss = loss_fn(outputs, labels)
+                with record_function("forward"), torch.autocast("cuda", torch.bfloat16, enabled=autocast):
+                    outputs = model(imgs)
+                    loss = loss_fn(outputs.float(), labels)
                 optimizer.zero_grad()
-                loss.backward()
-                optimizer.step()
+                with record_function("backward+allreduce"):
+                    loss.backward()
+                with record_function("optimizer"):
+                    optimizer.step()
                 loss_sum += loss.item()
                 nsteps += 1
         global_step += nsteps
@@ -157,18 +183,48 @@ def train_loop(model, train_loader: DeviceLoader, rank: int, cfg: Optional[Train
             print(epoch_line(epoch, mean), flush=True)
             if cfg.checkpoint:
                 save_checkpoint(model, ckpt, rank, meta={"epoch": epoch, "step": global_step})
+        if cfg.check_sync and epoch % cfg.check_sync == 0:
+            assert_params_in_sync(unwrap(model))
     total = time.time() - start_time
+    stack.close()
+    if prof is not None:
+        _export_profile(prof, cfg.profile, rank, train_loader.device)
     print(time_line(total), flush=True)
     return {"losses": history, "seconds": total, "steps": global_step}
 
 
+def _profiler(out_dir: str, device: torch.device):
+    """torch.profiler over the training loop (CPU ops + HIP kernels through roctracer on ROCm)."""
+    from torch.profiler import ProfilerActivity, profile
+    acts = [ProfilerActivity.CPU] + ([ProfilerActivity.CUDA] if device.type == "cuda" else [])
+    os.makedirs(out_dir, exist_ok=True)
+    return profile(activities=acts, record_shapes=False)
+
+
+def _export_profile(prof, out_dir: str, rank: int, device: torch.device) -> None:
+    prof.export_chrome_trace(os.path.join(out_dir, f"trace_rank{rank}.json"))
+    key = "self_cuda_time_total" if device.type == "cuda" else "self_cpu_time_total"
+    with open(os.path.join(out_dir, f"summary_rank{rank}.txt"), "w") as f:
+        f.write(prof.key_averages().table(sort_by=key, row_limit=40))
+
+
 def build_model_for_rank(cfg: TrainConfig, rank: int, world_size: int, device: torch.device, data, labels,
                          loader: DeviceLoader):
-    """NetResDeep wrapped for data parallelism on `device` (fused engine or FlatBucketDDP)."""
+    """The model wrapped for data parallelism on `device`: NetResDeep on the fused engine, or any model on
+    FlatBucketDDP (``--model resnet50`` trains a 10-class ResNet-50 on the CIFAR tensors, channels-last, bf16)."""
     from .models.netresdeep import NetResDeep
     from .parallel.ddp import FusedDDPTrainer
     from .parallel.flat_ddp import FlatBucketDDP
-    model = NetResDeep().to(device)
+    if cfg.model == "resnet50":
+        from .models.resnet50 import resnet50
+        torch.manual_seed(cfg.seed)
+        model = resnet50(num_classes=10).to(device)
+        if device.type == "cuda":
+            model = model.to(memory_format=torch.channels_last)
+        if cfg.engine == "fused":
+            raise ValueError("the fused engine implements NetResDeep only; use --engine torch/auto for resnet50")
+    else:
+        model = NetResDeep().to(device)
     meta = None
     if cfg.resume:
         meta = load_checkpoint(model, cfg.resume, strict=True, map_location=device)
@@ -180,7 +236,7 @@ def build_model_for_rank(cfg: TrainConfig, rank: int, world_size: int, device: t
         n_idx = len(loader) * loader.batch_size
         return FusedDDPTrainer(model, loader.data, loader.labels, batch_max=loader.batch_size, lr=cfg.lr,
                                dtype=cfg.dtype, max_indices=max(n_idx, loader.batch_size))
-    return FlatBucketDDP(model)
+    return FlatBucketDDP(model, bucket_cap_mb=cfg.bucket_mb)
 
 
 def unwrap_model(model) -> nn.Module:

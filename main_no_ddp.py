@@ -60,6 +60,11 @@ if __name__ == "__main__":
     _cfg = config_from_args(args, data_path)
     _cfg.checkpoint = False
     print(f"Training on device {device}.")
-    model = NetResDeep().to(device)
+    if _cfg.model == "resnet50":
+        from distributeddataparallel_cifar10_amd.models.resnet50 import resnet50
+        torch.manual_seed(_cfg.seed)
+        model = resnet50(num_classes=10).to(device)
+    else:
+        model = NetResDeep().to(device)
     train_loader = prepare()
     training_loop(model, train_loader)

@@ -43,3 +43,42 @@ def test_fault_injection_tears_down(tmp_path, port):
               "--timeout", "60"])
     assert r.returncode != 0
     assert "injected failure at step 2" in r.stderr
+
+
+def test_debug_flags_profile_check_sync_bucket(tmp_path, port):
+    """--profile writes per-rank traces + kernel summaries; --check-sync asserts cross-rank parameter equality;
+    --bucket-mb sets the generic path's bucket cap."""
+    prof = tmp_path / "prof"
+    r = _run(["main.py", "--backend", "gloo", "--world-size", "2", "--synthetic", "256", "--epochs", "1",
+              "--max-steps", "2", "--engine", "torch", "--no-checkpoint", "--port", str(port), "--profile",
+              str(prof), "--check-sync", "1", "--bucket-mb", "0.05"])
+    assert r.returncode == 0, r.stderr[-3000:]
+    for rk in (0, 1):
+        assert (prof / f"trace_rank{rk}.json").stat().st_size > 0
+        text = (prof / f"summary_rank{rk}.txt").read_text()
+        assert "convolution" in text
+
+
+def test_model_resnet50_flag(tmp_path):
+    r = _run(["main_no_ddp.py", "--synthetic", "128", "--epochs", "1", "--max-steps", "1", "--model", "resnet50"])
+    assert r.returncode == 0, r.stderr[-3000:]
+    assert "Epoch 1, Training loss" in r.stdout
+
+
+def _case_sync_check(rank, ws):
+    import pytest as _pt
+    import torch.nn as nn
+    from distributeddataparallel_cifar10_amd.parallel import dist as pdist
+    torch.manual_seed(0)
+    m = nn.Linear(4, 4)
+    pdist.assert_params_in_sync(m)  # identical on both ranks
+    if rank == 1:
+        with torch.no_grad():
+            m.bias[0] += 1e-3
+    with _pt.raises(RuntimeError, match="diverged"):
+        pdist.assert_params_in_sync(m)
+
+
+def test_check_sync_detects_divergence(port):
+    from test_flat_ddp import _spawn
+    _spawn(_case_sync_check, port, ws=2)
