@@ -2,10 +2,10 @@
 
 Metric/config from BASELINE.json: "images/sec (whole node) CIFAR-10 ResNet at 1/2/4/8 MI355X; scaling efficiency",
 NetResDeep(n_chans1=32, n_blocks=10), per-rank batch 32 (reference main.py:61), SGD lr 1e-2, one process per GPU,
-gradient all-reduce over RCCL.  Synthetic CIFAR-shaped uint8 data (no datasets offline), random-init weights.
+gradient all-reduce = one-shot xGMI peer reads fused with SGD (RCCL fallback).  Synthetic CIFAR-shaped uint8 data (no datasets offline), random-init weights.
 
 Each step is the FULL training step (stem+10 blocks forward, loss, backward, gradient all-reduce, SGD update,
-BN running stats) replayed as one hipGraph by the native engine.  W warm-up steps, then K timed steps bracketed by
+BN running stats) replayed as hipGraphs (16 steps per launch) by the native engine.  W warm-up steps, then K timed steps bracketed by
 barrier + device sync on both sides; the slowest rank's time is reported.
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--dtype bf16|fp32]
@@ -40,6 +40,8 @@ def main() -> int:
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
     ap.add_argument("--rows", type=int, default=4)
     ap.add_argument("--engine", default="auto", choices=["auto", "persistent", "multikernel"])
+    ap.add_argument("--allreduce", default="auto", choices=["auto", "xgmi", "rccl"],
+                    help="gradient all-reduce for N>1: one-shot xGMI peer reads (default inside a node) or RCCL")
     a = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -64,7 +66,8 @@ def main() -> int:
     model = NetResDeep().to(dev)
     persistent = None if a.engine == "auto" else a.engine == "persistent"
     trainer = FusedDDPTrainer(model, data.to(dev), labels.to(dev), batch_max=a.batch, lr=1e-2, dtype=a.dtype,
-                              rows=a.rows, max_indices=(a.warmup + a.steps) * a.batch, persistent=persistent)
+                              rows=a.rows, max_indices=(a.warmup + a.steps) * a.batch, persistent=persistent,
+                              comm=a.allreduce)
     sampler = torch.utils.data.distributed.DistributedSampler(range(50000), num_replicas=world, rank=rank)
     order = np.resize(np.fromiter(iter(sampler), dtype=np.int32), (a.warmup + a.steps) * a.batch)
     trainer.engine.set_indices(order)
@@ -101,6 +104,7 @@ def main() -> int:
             "vs_baseline": round(value / (REF_EAGER_IPS_PER_GPU * world), 3),
             "dtype": a.dtype,
             "engine": "persistent" if trainer.engine.cfg.persistent else "multikernel",
+            "allreduce": trainer.comm,
             "data": "synthetic (CIFAR-10-shaped uint8 3x32x32, 50000 samples, random labels; random-init weights)",
             "config": {"model": "NetResDeep(n_chans1=32, n_blocks=10)", "global_batch": a.batch * world,
                        "per_rank_batch": a.batch, "seq_len": None, "image": "3x32x32",

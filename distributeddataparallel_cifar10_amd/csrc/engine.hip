@@ -18,6 +18,7 @@
 
 #include "netresdeep_kernels.hip"
 #include "netresdeep_persistent.hip"
+#include "xgmi_allreduce.hip"
 
 namespace {
 
@@ -67,7 +68,8 @@ struct DcaInit {
   int debug;            // persistent engine: also store DY / G for diagnostics
   int pk_waves;         // persistent engine: waves per workgroup (8; 0 = default)
   int comm_mode;        // world_size > 1: 0 = RCCL inside the step; 1 = external (host drives the all-reduce
-                        // between dca_engine_run_part(.., 1) and (.., 2); test/debug path, no RCCL communicator)
+                        // between dca_engine_run_part(.., 1) and (.., 2); test/debug path, no RCCL communicator);
+                        // 2 = xGMI one-shot (peer-to-peer reads of IPC-mapped gradient slabs, fused with SGD)
 };
 
 }  // extern "C"
@@ -86,6 +88,11 @@ struct Engine {
   int* indices = nullptr;
   int n_indices = 0;
   ncclComm_t comm = nullptr;
+  // comm_mode 2 (xGMI one-shot): this rank's shared region and every rank's mapping of it
+  char* xregion = nullptr;
+  xg::Peers peers{};
+  bool peers_open = false;
+  unsigned long long ar_deadline = 3000ull * 100000000ull;  // 3000 s in 100 MHz ticks (a peer may be in host code)
   std::map<int, hipGraphExec_t> graphs;
   bool persistent = false;
   int pk_waves = 8;
@@ -215,6 +222,22 @@ static int set_lds_limits(Engine* e) {
   return 0;
 }
 
+// comm_mode 2: the one-shot xGMI all-reduce fused with the averaging SGD (replaces all-reduce + k_apply_sgd)
+static int enqueue_xgmi_sgd(Engine* e, const Ctx& cx) {
+  if (!e->peers_open) {
+    g_err = "xGMI all-reduce: peers not mapped (call dca_engine_ipc_open first)";
+    return -1;
+  }
+  if (e->bf)
+    hipLaunchKernelGGL(xg::k_xgmi_ar_sgd<true>, dim3(xg::AR_NB), dim3(xg::AR_T), 0, e->st, cx, e->peers,
+                       (const float*)cx.grads, (float*)nullptr, e->pa.err + 1, 1, e->ar_deadline);
+  else
+    hipLaunchKernelGGL(xg::k_xgmi_ar_sgd<false>, dim3(xg::AR_NB), dim3(xg::AR_T), 0, e->st, cx, e->peers,
+                       (const float*)cx.grads, (float*)nullptr, e->pa.err + 1, 1, e->ar_deadline);
+  HIPCK(hipGetLastError());
+  return 0;
+}
+
 // Persistent path: one launch for the whole trunk, one for reduction + SGD.
 // `part`: 0 = the whole step; 1 = compute up to (not including) the gradient all-reduce; 2 = what follows it
 // (averaging SGD + CC4 base).  Parts 1/2 exist for comm_mode 1, where the host runs the all-reduce in between.
@@ -222,7 +245,7 @@ static int enqueue_step_persistent(Engine* e, int B, int part) {
   Ctx cx = e->base;
   cx.B = B;
   const bool multi = e->in.world_size > 1;
-  const bool rccl_overlap = e->split && multi && part == 0;  // fc all-reduce overlapped with the trunk backward
+  const bool rccl_overlap = e->split && multi && part == 0 && e->in.comm_mode == 0;  // fc all-reduce overlapped with the trunk backward
   if (part != 2) {
     pk::PkArgs pa = e->pa;
     // Packing the image workgroups onto one XCD (grid 8 x B, see pk_img) keeps the BN exchange inside one L2,
@@ -260,6 +283,8 @@ static int enqueue_step_persistent(Engine* e, int B, int part) {
                          e->comm, e->cst));
       HIPCK(hipEventRecord(e->evC, e->cst));
       HIPCK(hipStreamWaitEvent(e->st, e->evC, 0));
+    } else if (part == 0 && e->in.comm_mode == 2) {
+      return enqueue_xgmi_sgd(e, cx);
     } else if (part == 0) {
       NCCK(ncclAllReduce(cx.grads, cx.grads, FLAT_N, ncclFloat32, ncclSum, e->comm, e->st));
     }
@@ -291,7 +316,7 @@ static int enqueue_step(Engine* e, int B, int part = 0) {
     size_t lds = (i == 0) ? e->s_dgrad0 : e->s_dgrad;
     lds = std::max(lds, (i < NBLK - 1) ? e->s_wgrad : e->s_fc);
     hipLaunchKernelGGL(e->kbwd, dim3(nparts + extra), blk, lds, e->st, cx, i);
-    if (i == NBLK - 1 && e->in.world_size > 1 && part == 0) {  // bucket A ready: overlap its all-reduce with the trunk bwd
+    if (i == NBLK - 1 && e->in.world_size > 1 && part == 0 && e->in.comm_mode == 0) {  // bucket A ready: overlap its all-reduce with the trunk bwd
       HIPCK(hipEventRecord(e->evA, e->st));
       HIPCK(hipStreamWaitEvent(e->cst, e->evA, 0));
       NCCK(ncclAllReduce(cx.grads, cx.grads, BUCKET_A_END, ncclFloat32, ncclSum, e->comm, e->cst));
@@ -299,6 +324,7 @@ static int enqueue_step(Engine* e, int B, int part = 0) {
   }
   const int nother = cx.fuse_sgd ? 64 : 0;
   hipLaunchKernelGGL(e->kred, dim3(N_TRUNK_RED_WG + N_STEM_RED_WG + nother + 1), blk, 0, e->st, cx, nslab, nparts);
+  if (e->in.world_size > 1 && part == 0 && e->in.comm_mode == 2) return enqueue_xgmi_sgd(e, cx);
   if (e->in.world_size > 1 && part == 0) {
     HIPCK(hipEventRecord(e->evB, e->st));
     HIPCK(hipStreamWaitEvent(e->cst, e->evB, 0));
@@ -467,7 +493,7 @@ extern "C" {
 
 const char* dca_last_error() { return g_err.c_str(); }
 
-int dca_abi_version() { return 2; }  // bump with every DcaInit / signature change
+int dca_abi_version() { return 3; }  // bump with every DcaInit / signature change
 
 int dca_nccl_unique_id(char* out128) {
   ncclUniqueId id;
@@ -548,6 +574,21 @@ int dca_engine_create(const DcaInit* in, int n_indices, void** out) {
   c.indices = e->indices;
   c.n_data = in->n_data;
   c.n_idx = std::max(n_indices, 1);
+  if (in->world_size > 1 && in->comm_mode == 2) {
+    if (in->world_size > dca::xg::MAXR) {
+      g_err = "xGMI all-reduce: world_size > 8 (one node) -- use RCCL";
+      return -1;
+    }
+    // uncached device memory: peers read it over xGMI and no L2 may hold a stale line of it
+    if (hipExtMallocWithFlags((void**)&e->xregion, dca::xg::REGION_BYTES, hipDeviceMallocUncached) != hipSuccess) {
+      (void)hipGetLastError();
+      HIPCK(hipMalloc(&e->xregion, dca::xg::REGION_BYTES));
+    }
+    HIPCK(hipMemset(e->xregion, 0, dca::xg::REGION_BYTES));
+    HIPCK(hipDeviceSynchronize());
+    const char* dl = getenv("DCA_XGMI_TIMEOUT_S");
+    if (dl) e->ar_deadline = (unsigned long long)(atof(dl) * 1e8);
+  }
   if (in->world_size > 1 && in->comm_mode == 0) {
     ncclUniqueId id;
     memcpy(&id, in->nccl_id, 128);
@@ -566,6 +607,10 @@ int dca_engine_destroy(void* h) {
   (void)hipStreamSynchronize(e->cst);
   for (auto& kv : e->graphs) (void)hipGraphExecDestroy(kv.second);
   if (e->comm) (void)ncclCommDestroy(e->comm);
+  for (int q = 0; q < dca::xg::MAXR; ++q)
+    if (e->peers_open && q != e->in.rank && q < e->in.world_size && e->peers.base[q])
+      (void)hipIpcCloseMemHandle(e->peers.base[q]);
+  if (e->xregion) (void)hipFree(e->xregion);
   (void)hipFree(e->wsp);
   (void)hipFree(e->indices);
   (void)hipEventDestroy(e->evA);
@@ -622,13 +667,13 @@ int dca_engine_set_cursor(void* h, int v) {
   return 0;
 }
 
-// Device-side error flags of the persistent engine (bit r: BN exchange round r timed out).  Synchronises;
-// reset clears them.
+// Device-side error flags: flags[0] of the persistent engine (bit r: BN exchange round r timed out),
+// flags[1] of the xGMI all-reduce (bit 31: a peer-flag wait timed out).  Synchronises; reset clears them.
 int dca_engine_errors(void* h, unsigned* flags, int reset) {
   Engine* e = (Engine*)h;
   HIPCK(hipStreamSynchronize(e->st));
-  HIPCK(hipMemcpy(flags, e->pa.err, sizeof(unsigned), hipMemcpyDeviceToHost));
-  if (reset) HIPCK(hipMemset(e->pa.err, 0, sizeof(unsigned)));
+  HIPCK(hipMemcpy(flags, e->pa.err, 2 * sizeof(unsigned), hipMemcpyDeviceToHost));
+  if (reset) HIPCK(hipMemset(e->pa.err, 0, 2 * sizeof(unsigned)));
   return 0;
 }
 
@@ -693,6 +738,68 @@ int dca_engine_run(void* h, int B, int nsteps, int use_graph) {
     for (int r = 0; r < reps; ++r) HIPCK(hipGraphLaunch(it->second, e->st));
     done += reps * chunk;
   }
+  return 0;
+}
+
+// comm_mode 2: the IPC handle (64 bytes) of this rank's shared region, to be all-gathered by the host.
+int dca_engine_ipc_handle(void* h, char* out64) {
+  Engine* e = (Engine*)h;
+  if (!e->xregion) {
+    g_err = "ipc_handle: engine not created with comm_mode 2";
+    return -1;
+  }
+  static_assert(sizeof(hipIpcMemHandle_t) == 64, "unexpected hipIpcMemHandle_t size");
+  hipIpcMemHandle_t hd;
+  HIPCK(hipIpcGetMemHandle(&hd, e->xregion));
+  memcpy(out64, &hd, 64);
+  return 0;
+}
+
+// comm_mode 2: map every peer's region (`all` = world_size handles of 64 bytes, in rank order).
+int dca_engine_ipc_open(void* h, const char* all, int world) {
+  Engine* e = (Engine*)h;
+  if (!e->xregion || world != e->in.world_size) {
+    g_err = "ipc_open: engine not created with comm_mode 2, or world size mismatch";
+    return -1;
+  }
+  for (int q = 0; q < world; ++q) {
+    if (q == e->in.rank) {
+      e->peers.base[q] = e->xregion;
+      continue;
+    }
+    hipIpcMemHandle_t hd;
+    memcpy(&hd, all + 64 * q, 64);
+    void* p = nullptr;
+    HIPCK(hipIpcOpenMemHandle(&p, hd, hipIpcMemLazyEnablePeerAccess));
+    e->peers.base[q] = (char*)p;
+  }
+  e->peers_open = true;
+  return 0;
+}
+
+// comm_mode 2 self-test: one all-reduce (no SGD) of `n = FLAT_N` floats from device `src` into device `dst`
+// through the same protocol, epochs and slabs as a training step.  Collective: every rank must call it.
+// timeout_s bounds the flag waits; returns 1 in *timed_out when a wait expired.  Synchronous.
+int dca_engine_ipc_selftest(void* h, const float* src, float* dst, float timeout_s, int* timed_out) {
+  Engine* e = (Engine*)h;
+  if (!e->peers_open) {
+    g_err = "ipc_selftest: peers not mapped";
+    return -1;
+  }
+  HIPCK(hipMemsetAsync(e->pa.err + 1, 0, sizeof(unsigned), e->st));
+  const unsigned long long dl = (unsigned long long)((double)timeout_s * 1e8);
+  if (e->bf)
+    hipLaunchKernelGGL(dca::xg::k_xgmi_ar_sgd<true>, dim3(dca::xg::AR_NB), dim3(dca::xg::AR_T), 0, e->st,
+                       e->base, e->peers, src, dst, e->pa.err + 1, 0, dl);
+  else
+    hipLaunchKernelGGL(dca::xg::k_xgmi_ar_sgd<false>, dim3(dca::xg::AR_NB), dim3(dca::xg::AR_T), 0, e->st,
+                       e->base, e->peers, src, dst, e->pa.err + 1, 0, dl);
+  HIPCK(hipGetLastError());
+  HIPCK(hipStreamSynchronize(e->st));
+  unsigned f = 0;
+  HIPCK(hipMemcpy(&f, e->pa.err + 1, sizeof(unsigned), hipMemcpyDeviceToHost));
+  HIPCK(hipMemset(e->pa.err + 1, 0, sizeof(unsigned)));
+  *timed_out = (f & 0x80000000u) ? 1 : 0;
   return 0;
 }
 

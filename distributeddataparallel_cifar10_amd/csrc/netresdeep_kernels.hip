@@ -1362,6 +1362,23 @@ __global__ void __launch_bounds__(NT) k_reduce(Ctx cx, int nslab, int nsslab) {
   }
 }
 
+// Kernel-layout copies of flat parameter e (value w): bf16 fc1 for the persistent head, the forward / dgrad
+// conv weight tiles, the stem weight (plain and as MFMA B fragments).  Other parameters have no copy.
+template <bool BF>
+__device__ __forceinline__ void derive_param(const Ctx& cx, int e, float w) {
+  if (e < OFF_FC1W + 65536) {
+    ((unsigned short*)cx.w1b)[e - OFF_FC1W] = bfbits(w);  // bf16 fc1 copy (persistent engine's head)
+  } else if (e >= OFF_CONVW && e < OFF_CONVW + 9216) {
+    const int r = e - OFF_CONVW, co = r / 288, ci = (r / 9) % 32, tap = r % 9;
+    put_w<BF>(cx.wt_f, (tap * 32 + co) * 32 + ci, w);
+    put_w<BF>(cx.wt_d, ((8 - tap) * 32 + ci) * 32 + co, w);
+  } else if (e >= OFF_C1W && e < OFF_C1W + 864) {
+    const int r = e - OFF_C1W, co = r / 27, k = r % 27;
+    put_w<BF>(cx.sw, co * 32 + k, w);
+    ((unsigned short*)cx.swf)[swf_slot(co, k)] = bfbits(w);
+  }
+}
+
 // SGD after the gradient all-reduce (world_size > 1), or mode 0 = derive weight layouts / init state only.
 template <bool BF>
 __global__ void __launch_bounds__(NT) k_apply_sgd(Ctx cx, int mode) {
@@ -1372,17 +1389,7 @@ __global__ void __launch_bounds__(NT) k_apply_sgd(Ctx cx, int mode) {
       w -= cx.lr * cx.grads[e] * cx.inv_ws;
       cx.params[e] = w;
     }
-    if (e < OFF_FC1W + 65536) {
-      ((unsigned short*)cx.w1b)[e - OFF_FC1W] = bfbits(w);  // bf16 fc1 copy (persistent engine's head)
-    } else if (e >= OFF_CONVW && e < OFF_CONVW + 9216) {
-      const int r = e - OFF_CONVW, co = r / 288, ci = (r / 9) % 32, tap = r % 9;
-      put_w<BF>(cx.wt_f, (tap * 32 + co) * 32 + ci, w);
-      put_w<BF>(cx.wt_d, ((8 - tap) * 32 + ci) * 32 + co, w);
-    } else if (e >= OFF_C1W && e < OFF_C1W + 864) {
-      const int r = e - OFF_C1W, co = r / 27, k = r % 27;
-      put_w<BF>(cx.sw, co * 32 + k, w);
-      ((unsigned short*)cx.swf)[swf_slot(co, k)] = bfbits(w);
-    }
+    derive_param<BF>(cx, e, w);
   }
   if (gid < 64) {
     if (mode) cx.rs_base[gid] = cx.grads[OFF_RS + gid];

@@ -1,0 +1,113 @@
+// One-shot gradient all-reduce over xGMI peer-to-peer reads, fused with the averaging SGD step.
+//
+// Replaces the reference's DDP Reducer all-reduce (reference main.py:63, SURVEY.md 2.4 CC5 + CC4) for ranks of
+// ONE node.  The whole NetResDeep gradient is 304 KB (fp32): a ring all-reduce over 8 GPUs is 14 dependent
+// latency-bound steps, while the 8 MI355X of a node are fully connected by xGMI (7 point-to-point links per GPU),
+// so every rank simply reads all 7 peers' gradients at once -- one link per peer, ~38 KB per link per 1/8 of the
+// buffer -- and sums them in registers (SURVEY.md 5.8 cost model: one-shot wins for buckets this small).
+//
+// Shared region (one per rank, exported with hipIpcGetMemHandle and mapped by every peer):
+//   [flags: MAXR ranks x AR_NB workgroups ints, padded to 4 KiB][slab parity 0][slab parity 1]
+// allocated uncached (hipDeviceMallocUncached) so no L2 line of it is ever stale on any GPU.
+//
+// Protocol of workgroup b (it owns float4 chunk b of the flat buffer [0, FLAT_N), on every rank):
+//   1. ep = my_flags[me][b] + 1 (the epoch this workgroup last published, plus one); slab parity = ep & 1
+//   2. copy my chunk b of cx.grads into my slab[parity]; system-scope release fence
+//   3. store ep into flags[me][b] of EVERY rank (itself included)
+//   4. wait until my flags[q][b] >= ep for all ranks q (bounded by a real-time deadline -> error bit, no hang)
+//   5. system-scope acquire; read chunk b of all W slabs[parity]; sum in rank order 0..W-1 (bitwise identical
+//      on every rank); write the sum to cx.grads; SGD with 1/W averaging + derived weight copies; the
+//      running-stat segment [OFF_RS, FLAT_N) is rank 0's BN buffers (others contribute 0): CC4.
+// Reuse safety: a rank writes slab[parity] again at epoch ep+2 only after its workgroup b passed step 4 of
+// epoch ep+1, i.e. after every peer started epoch ep+1, i.e. (stream order) after every peer finished reading
+// epoch ep.  Parities alternate, so epoch ep+1's writes never touch what epoch ep's readers read.
+#pragma once
+#include "common.h"
+
+namespace dca {
+namespace xg {
+
+constexpr int MAXR = 8;                                  // ranks of one xGMI node
+constexpr int AR_T = 256;                                // threads per workgroup: one float4 each
+constexpr int AR_V4 = FLAT_N / 4;                        // 19035 float4 (FLAT_N is a multiple of 4)
+constexpr int AR_NB = (AR_V4 + AR_T - 1) / AR_T;         // 75 workgroups
+constexpr size_t FLAG_BYTES = 4096;                      // >= MAXR * AR_NB * 4
+constexpr size_t SLAB_FLOATS = (size_t)AR_NB * AR_T * 4;  // 76800 >= FLAT_N
+constexpr size_t REGION_BYTES = FLAG_BYTES + 2 * SLAB_FLOATS * 4;
+static_assert(MAXR * AR_NB * 4 <= (int)FLAG_BYTES, "flag area too small");
+static_assert(FLAT_N % 4 == 0, "flat buffer must be float4 granular");
+
+struct Peers {
+  char* base[MAXR];  // every rank's shared region, mapped into this process (own one at base[rank])
+};
+
+__device__ __forceinline__ int flag_load(const int* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__device__ __forceinline__ void flag_store(int* p, int v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__device__ __forceinline__ float* slab(const Peers& P, int q, int parity) {
+  return (float*)(P.base[q] + FLAG_BYTES) + (size_t)parity * SLAB_FLOATS;
+}
+
+// src: this rank's gradient (cx.grads); `sgd` 0 = sum into `sum_out` only (self-test), 1 = training step.
+// `deadline_ticks`: wait limit in s_memrealtime ticks (100 MHz); on expiry err bit 31 is set and the
+// workgroup goes on with whatever it read (the host raises on the flag at its next check).
+template <bool BF>
+__global__ void __launch_bounds__(AR_T) k_xgmi_ar_sgd(Ctx cx, Peers P, const float* src, float* sum_out,
+                                                      unsigned* err, int sgd, unsigned long long deadline_ticks) {
+  const int b = blockIdx.x, t = threadIdx.x, W = cx.ws, me = cx.rank;
+  const int v = b * AR_T + t;
+  const bool live = v < AR_V4;
+  int* myflags = (int*)P.base[me];
+  __shared__ int s_ep;
+  if (t == 0) s_ep = flag_load(myflags + me * AR_NB + b) + 1;
+  const f32x4 g = live ? *(const f32x4*)(src + 4 * v) : f32x4{0.f, 0.f, 0.f, 0.f};
+  __syncthreads();
+  const int ep = s_ep, par = ep & 1;
+  *(f32x4*)(slab(P, me, par) + 4 * v) = g;
+  __threadfence_system();  // release: my slab chunk is visible at system scope before any flag says so
+  __syncthreads();
+  if (t < W) flag_store((int*)P.base[t] + me * AR_NB + b, ep);
+  if (t < W) {
+    const int* f = myflags + t * AR_NB + b;
+    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+    while (flag_load(f) < ep) {
+      __builtin_amdgcn_s_sleep(2);
+      if (__builtin_amdgcn_s_memrealtime() - t0 > deadline_ticks) {
+        atomicOr(err, 0x80000000u);
+        break;
+      }
+    }
+  }
+  __syncthreads();
+  __threadfence_system();  // acquire: peers' slab chunks as of their flag stores
+  if (!live) return;
+  // All W loads in flight at once (one per peer link): unconditional loads (ranks >= W re-read rank 0, which
+  // is never summed) so the compiler issues them back to back instead of branching around each one.
+  f32x4 part[MAXR];
+#pragma unroll
+  for (int q = 0; q < MAXR; ++q) part[q] = *(const f32x4*)(slab(P, q < W ? q : 0, par) + 4 * v);
+  f32x4 s = part[0];
+#pragma unroll
+  for (int q = 1; q < MAXR; ++q) s += q < W ? part[q] : f32x4{0.f, 0.f, 0.f, 0.f};
+  if (!sgd) {
+    *(f32x4*)(sum_out + 4 * v) = s;
+    return;
+  }
+  *(f32x4*)(cx.grads + 4 * v) = s;  // the all-reduced (summed) gradient, as after an RCCL all-reduce
+  const int e0 = 4 * v;
+  if (e0 >= OFF_RS) {  // CC4 segment (OFF_RS is float4 aligned): rank 0's running stats become the base
+    *(f32x4*)(cx.rs_base + (e0 - OFF_RS)) = s;
+    return;
+  }
+  f32x4 w = *(const f32x4*)(cx.params + e0);
+  w -= cx.lr * s * cx.inv_ws;  // same rounding as k_apply_sgd (the RCCL path)
+  *(f32x4*)(cx.params + e0) = w;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) derive_param<BF>(cx, e0 + k, w[k]);
+}
+
+}  // namespace xg
+}  // namespace dca

@@ -112,7 +112,9 @@ class EngineConfig:
     pk_waves: int = 8            # persistent engine: waves per workgroup (8: 2 image rows per wave)
     world_size: int = 1
     rank: int = 0
-    comm: str = "rccl"           # world_size > 1: "rccl" (all-reduce inside the graph-captured step) or
+    comm: str = "rccl"           # world_size > 1: "rccl" (all-reduce inside the graph-captured step),
+                                 # "xgmi" (one-shot peer-to-peer all-reduce over IPC-mapped slabs, fused with
+                                 # SGD; ranks of one node; call connect_peers() before stepping) or
                                  # "external" (host all-reduce between step parts; tests / any torch backend)
     bn_momentum: float = 0.1
     bn_eps: float = 1e-5
@@ -123,6 +125,8 @@ class NetResDeepEngine:
 
     def __init__(self, model: nn.Module, data_u8: torch.Tensor, labels: torch.Tensor, cfg: EngineConfig,
                  nccl_id: Optional[bytes] = None, max_indices: Optional[int] = None):
+        if cfg.comm not in ("rccl", "external", "xgmi"):
+            raise ValueError("comm must be 'rccl', 'external' or 'xgmi'")
         if cfg.dtype not in ("bf16", "fp32"):
             raise ValueError("dtype must be 'bf16' or 'fp32'")
         if cfg.persistent is None:
@@ -160,7 +164,7 @@ class NetResDeepEngine:
             bn_mom=float(cfg.bn_momentum), bn_eps=float(cfg.bn_eps), world_size=int(cfg.world_size),
             rank=int(cfg.rank), nccl_id=ctypes.cast(self._nccl_id, ctypes.c_char_p),
             persistent=1 if cfg.persistent else 0, debug=1 if cfg.debug else 0, pk_waves=int(cfg.pk_waves),
-            comm_mode=1 if cfg.comm == "external" else 0,
+            comm_mode={"rccl": 0, "external": 1, "xgmi": 2}[cfg.comm],
         )
         self._init = init
         self.max_indices = int(max_indices or self.data.shape[0])
@@ -180,6 +184,34 @@ class NetResDeepEngine:
 
     def sync(self):
         native.check(self.lib.dca_engine_sync(self.h), "dca_engine_sync")
+
+    # ---- xGMI peer mapping (comm="xgmi") --------------------------------------------------------------------
+    def ipc_handle(self) -> bytes:
+        """64-byte IPC handle of this rank's shared gradient region (to be all-gathered over the ranks)."""
+        buf = ctypes.create_string_buffer(64)
+        native.check(self.lib.dca_engine_ipc_handle(self.h, buf), "dca_engine_ipc_handle")
+        return buf.raw
+
+    def connect_peers(self, handles) -> None:
+        """Map every rank's region (`handles`: world_size 64-byte handles in rank order)."""
+        blob = b"".join(handles)
+        if len(blob) != 64 * self.cfg.world_size:
+            raise ValueError("need one 64-byte handle per rank")
+        native.check(self.lib.dca_engine_ipc_open(self.h, blob, int(self.cfg.world_size)), "dca_engine_ipc_open")
+
+    def xgmi_selftest(self, timeout_s: float = 20.0) -> bool:
+        """Collective: all-reduce a rank-dependent pattern through the xGMI protocol and check the sum exactly.
+        Every rank must call it (it advances the shared epochs like a training step does)."""
+        n, w, r = FLAT_N, self.cfg.world_size, self.cfg.rank
+        base = torch.arange(n, device=self.device, dtype=torch.float32).remainder_(997.0)
+        src = base * float(r + 1)
+        dst = torch.empty_like(src)
+        torch.cuda.synchronize(self.device)
+        timed_out = ctypes.c_int()
+        native.check(self.lib.dca_engine_ipc_selftest(self.h, src.data_ptr(), dst.data_ptr(), float(timeout_s),
+                                                       ctypes.byref(timed_out)), "dca_engine_ipc_selftest")
+        expect = base * float(w * (w + 1) // 2)
+        return not timed_out.value and bool(torch.equal(dst, expect))
 
     # ---- data order -----------------------------------------------------------------------------------------
     def set_indices(self, indices) -> None:
@@ -214,8 +246,12 @@ class NetResDeepEngine:
 
     def check_errors(self, reset: bool = True) -> None:
         """Raise if a persistent-kernel BN exchange timed out (a workgroup was not co-resident)."""
-        flags = ctypes.c_uint()
-        native.check(self.lib.dca_engine_errors(self.h, ctypes.byref(flags), int(reset)), "dca_engine_errors")
+        both = (ctypes.c_uint * 2)()
+        native.check(self.lib.dca_engine_errors(self.h, both, int(reset)), "dca_engine_errors")
+        flags = ctypes.c_uint(both[0])
+        if both[1]:
+            raise RuntimeError("xGMI gradient all-reduce: a peer's flag wait timed out (a rank stopped stepping?); "
+                               "results of the affected steps are invalid")
         if flags.value:
             raise RuntimeError(f"persistent engine: BN-statistics exchange timed out (round mask {flags.value:#x}); "
                                "results of the affected steps are invalid")

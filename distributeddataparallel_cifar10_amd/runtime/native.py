@@ -16,7 +16,7 @@ import torch  # noqa: F401  (must be imported before the native library, see mod
 
 from .. import build as _build
 
-ABI_VERSION = 2  # csrc/engine.hip dca_abi_version(): DcaInit layout / C signatures
+ABI_VERSION = 3  # csrc/engine.hip dca_abi_version(): DcaInit layout / C signatures
 _lock = threading.Lock()
 _lib = None
 
@@ -45,7 +45,10 @@ def _declare(lib):
     lib.dca_engine_region.restype = c_void_p
     lib.dca_engine_workspace_bytes.argtypes = [c_void_p]
     lib.dca_engine_workspace_bytes.restype = ctypes.c_size_t
-    lib.dca_engine_errors.argtypes = [c_void_p, ctypes.POINTER(ctypes.c_uint), c_int]
+    lib.dca_engine_ipc_handle.argtypes = [c_void_p, ctypes.c_char_p]
+    lib.dca_engine_ipc_open.argtypes = [c_void_p, ctypes.c_char_p, c_int]
+    lib.dca_engine_ipc_selftest.argtypes = [c_void_p, c_void_p, c_void_p, ctypes.c_float, ctypes.POINTER(c_int)]
+    lib.dca_engine_errors.argtypes = [c_void_p, ctypes.POINTER(ctypes.c_uint), c_int]  # flags[2]
     lib.dca_microbench.argtypes = [c_int, c_int, c_int, c_int, ctypes.POINTER(ctypes.c_float)]
     lib.dca_microbench_xchg.argtypes = [c_int, c_int, c_int, c_int, c_int, ctypes.POINTER(ctypes.c_float),
                                         ctypes.POINTER(c_int)]

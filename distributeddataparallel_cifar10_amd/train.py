@@ -6,7 +6,7 @@ per-rank batch 32 with DistributedSampler order (no set_epoch), log + checkpoint
 the same stdout lines -- while the step itself runs on the MI355X-native path:
 
 * ``engine="fused"`` (default on a GPU, NetResDeep): the whole step (forward, loss, backward, gradient
-  all-reduce over RCCL, SGD, BN running stats) is ONE hipGraph replay of the native engine; the dataset is
+  all-reduce -- one-shot xGMI peer reads or RCCL --, SGD, BN running stats) is ONE hipGraph replay of the native engine; the dataset is
   device-resident; the loss is accumulated on the device and read once per epoch (reference ``loss.item()``
   every step, SURVEY.md Q9: same printed value, no per-step host sync).
 * ``engine="torch"``: stock PyTorch ops + ``FlatBucketDDP`` (generic path; CPU / gloo; any model).
@@ -56,6 +56,7 @@ class TrainConfig:
     bucket_mb: float = 4.0           # FlatBucketDDP bucket cap (generic path)
     profile: Optional[str] = None    # directory for torch.profiler traces / kernel summary
     check_sync: int = 0              # >0: assert cross-rank parameter equality every N epochs (and at start)
+    allreduce: str = "auto"          # fused engine gradient all-reduce: auto | xgmi (one-shot P2P) | rccl
     extra: dict = field(default_factory=dict)
 
 
@@ -85,6 +86,8 @@ def add_cli_args(ap: argparse.ArgumentParser, batch_default: int = 32) -> argpar
     ap.add_argument("--profile", default=None, metavar="DIR", help="write torch.profiler traces to DIR")
     ap.add_argument("--check-sync", type=int, default=0, metavar="N",
                     help="assert parameters are identical on all ranks at start and every N epochs")
+    ap.add_argument("--allreduce", default="auto", choices=["auto", "xgmi", "rccl"],
+                    help="fused engine gradient all-reduce: one-shot xGMI peer reads (auto inside a node) or RCCL")
     return ap
 
 
@@ -94,7 +97,7 @@ def config_from_args(a: argparse.Namespace, data_path_default: str) -> TrainConf
                        checkpoint=not a.no_checkpoint, checkpoint_path=a.checkpoint_path, resume=a.resume,
                        metrics_json=a.metrics_json, seed=a.seed, set_epoch=a.set_epoch, fail_at_step=a.fail_at_step,
                        backend=a.backend, port=a.port, timeout_s=a.timeout, model=a.model, bucket_mb=a.bucket_mb,
-                       profile=a.profile, check_sync=a.check_sync)
+                       profile=a.profile, check_sync=a.check_sync, allreduce=a.allreduce)
 
 
 def load_dataset(cfg: TrainConfig):
@@ -235,7 +238,7 @@ def build_model_for_rank(cfg: TrainConfig, rank: int, world_size: int, device: t
     if kind == "fused":
         n_idx = len(loader) * loader.batch_size
         return FusedDDPTrainer(model, loader.data, loader.labels, batch_max=loader.batch_size, lr=cfg.lr,
-                               dtype=cfg.dtype, max_indices=max(n_idx, loader.batch_size))
+                               dtype=cfg.dtype, max_indices=max(n_idx, loader.batch_size), comm=cfg.allreduce)
     return FlatBucketDDP(model, bucket_cap_mb=cfg.bucket_mb)
 
 

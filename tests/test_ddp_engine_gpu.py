@@ -110,3 +110,89 @@ def test_engine_ddp_two_ranks_one_gpu(gpu, port, dtype, persistent, split, monke
         p.join(timeout=120)
     bad = [r for r in res if r[1]]
     assert not bad, "\n".join(f"rank {r}:\n{e}" for r, e in bad)
+
+
+def _xgmi_worker(rank, ws, port, dtype, persistent, q):
+    """One rank of the fused trainer with the one-shot xGMI all-reduce (all ranks share GPU 0: the IPC-mapped
+    slabs are then peers on the same device, which exercises the whole protocol -- epochs, parities, flags)."""
+    try:
+        os.environ["MASTER_ADDR"] = "127.0.0.1"
+        os.environ["MASTER_PORT"] = str(port)
+        os.environ["DCA_XGMI_TIMEOUT_S"] = "60"  # a protocol bug ends as an error flag, not a hang
+        dist.init_process_group("gloo", rank=rank, world_size=ws)
+        from distributeddataparallel_cifar10_amd.data.sampler import distributed_indices
+        from distributeddataparallel_cifar10_amd.data.synthetic import synthetic_cifar
+        from distributeddataparallel_cifar10_amd.models.netresdeep import NetResDeep
+        from distributeddataparallel_cifar10_amd.parallel.ddp import FusedDDPTrainer
+        from distributeddataparallel_cifar10_amd.utils.oracle import reference_step
+        torch.cuda.set_device(0)
+        dev = torch.device("cuda", 0)
+        data, labels = synthetic_cifar(NDATA, seed=5)
+        order = [distributed_indices(NDATA, ws, r) for r in range(ws)]
+        torch.manual_seed(100 + rank)
+        model = NetResDeep()
+        from distributeddataparallel_cifar10_amd.parallel.ddp import broadcast_module_state
+        broadcast_module_state(model, 0)
+        ref0 = copy.deepcopy(model)
+        model = model.to(dev)
+        tr = FusedDDPTrainer(model, data.to(dev), labels.to(dev), batch_max=32, dtype=dtype, persistent=persistent,
+                             comm="xgmi", max_indices=len(order[rank]))
+        assert tr.comm == "xgmi", "fell back to RCCL: the xGMI path did not come up"
+        eng = tr.engine
+        eng.set_indices(order[rank])
+        eng.set_cursor(0)
+        eng.read_loss(reset=True)
+        eng.run(B, STEPS)  # graph-captured steps, the all-reduce inside the graph
+        loss, steps = eng.read_loss()
+        assert steps == STEPS
+        # single-process simulation of reference DDP over `ws` ranks
+        models = [copy.deepcopy(ref0) for _ in range(ws)]
+        for s in range(STEPS):
+            snap = {k: v.clone() for k, v in models[0].named_buffers()}
+            grads = []
+            for r in range(ws):
+                with torch.no_grad():
+                    for k, v in models[r].named_buffers():
+                        v.copy_(snap[k])
+                sel = order[r][s * B:(s + 1) * B]
+                out = reference_step(models[r], data[sel], labels[sel], lr=1e-2, apply_sgd=False,
+                                     bf16_operands=dtype == "bf16", fc1_bf16=persistent)
+                grads.append(out["grads"])
+            with torch.no_grad():
+                for r in range(ws):
+                    for n, p in models[r].named_parameters():
+                        p -= 1e-2 * sum(g[n] for g in grads) / ws
+        sim = models[rank]
+        tol = 1e-3 if dtype == "fp32" else 3e-2
+        sd, rsd = model.state_dict(), sim.state_dict()
+        for k in ("fc1.weight", "fc2.bias", "resblocks.0.conv.weight", "resblocks.0.batch_norm.weight",
+                  "conv1.weight", "resblocks.0.batch_norm.running_mean", "resblocks.0.batch_norm.running_var"):
+            a, b = sd[k].detach().double().cpu(), rsd[k].detach().double()
+            err = ((a - b).norm() / b.norm()).item()
+            assert err < tol, (k, err)
+        # bitwise-identical parameters on every rank (fixed rank-order summation)
+        flat = torch.cat([p.detach().reshape(-1).cpu() for p in model.parameters()])
+        other = flat.clone()
+        dist.broadcast(other, 0)
+        assert torch.equal(flat, other)
+        tr.close()
+        q.put((rank, None))
+    except Exception:
+        q.put((rank, traceback.format_exc()))
+    finally:
+        if dist.is_initialized():
+            dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("ws,dtype,persistent", [(2, "bf16", True), (4, "bf16", True), (2, "fp32", False)])
+def test_xgmi_allreduce_ranks_one_gpu(gpu, port, ws, dtype, persistent):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_xgmi_worker, args=(r, ws, port, dtype, persistent, q)) for r in range(ws)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=600) for _ in procs]
+    for p in procs:
+        p.join(timeout=120)
+    bad = [r for r in res if r[1]]
+    assert not bad, "\n".join(f"rank {r}:\n{e}" for r, e in bad)
