@@ -699,7 +699,7 @@ int dca_engine_run(void* h, int B, int nsteps, int use_graph) {
     g_err = "batch out of range";
     return -1;
   }
-  if (e->in.world_size > 1 && e->in.comm_mode != 0) {
+  if (e->in.world_size > 1 && e->in.comm_mode == 1) {
     g_err = "comm_mode 1 (external all-reduce): drive steps with dca_engine_run_part";
     return -1;
   }

@@ -142,7 +142,10 @@ def _xgmi_worker(rank, ws, port, dtype, persistent, q):
         eng.set_indices(order[rank])
         eng.set_cursor(0)
         eng.read_loss(reset=True)
-        eng.run(B, STEPS)  # graph-captured steps, the all-reduce inside the graph
+        import time
+        for s in range(STEPS):  # uneven producer timing: ranks reach each step's all-reduce at different times
+            time.sleep(0.03 * ((rank + s) % ws))
+            eng.run(B, 1)  # graph-captured step, the all-reduce inside the graph
         loss, steps = eng.read_loss()
         assert steps == STEPS
         # single-process simulation of reference DDP over `ws` ranks
