@@ -31,6 +31,10 @@ def main() -> int:
     ap.add_argument("--image", type=int, default=224)
     ap.add_argument("--bucket-mb", type=float, default=8.0)
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
+    ap.add_argument("--path", default="torch", choices=["torch", "ops"],
+                    help="torch: stock conv/BN (MIOpen) under bf16 autocast; ops: the framework's HIP kernels "
+                         "(MFMA GEMM convs, fused BN+ReLU+residual, fused CE, HIP SGD)")
+    ap.add_argument("--fp8", action="store_true", help="ops path: fp8 e4m3 forward GEMMs for 1x1 convs and fc")
     a = ap.parse_args()
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -44,16 +48,20 @@ def main() -> int:
     from distributeddataparallel_cifar10_amd.parallel.flat_ddp import FlatBucketDDP, FlatSGD
     torch.manual_seed(rank)
     model = resnet50().to(dev)
+    if a.path == "ops":
+        from distributeddataparallel_cifar10_amd.ops import OpsModel, cross_entropy
+        model = OpsModel(model, fp8=a.fp8)
     ddp = FlatBucketDDP(model, bucket_cap_mb=a.bucket_mb, first_bucket_mb=1.0)
     opt = FlatSGD(ddp, lr=0.1, momentum=0.9)
     g = torch.Generator(device=dev).manual_seed(1234 + rank)
     x = torch.randn(a.batch, 3, a.image, a.image, device=dev, generator=g)
     y = torch.randint(0, 1000, (a.batch,), device=dev, generator=g)
-    amp = torch.autocast("cuda", dtype=torch.bfloat16, enabled=a.dtype == "bf16")
+    amp = torch.autocast("cuda", dtype=torch.bfloat16, enabled=a.dtype == "bf16" and a.path == "torch")
+    ce = cross_entropy if a.path == "ops" else F.cross_entropy
 
     def step():
         with amp:
-            loss = F.cross_entropy(ddp(x), y)
+            loss = ce(ddp(x), y)
         opt.zero_grad()
         loss.backward()
         opt.step()
@@ -79,7 +87,9 @@ def main() -> int:
                           "dtype": a.dtype, "data": "synthetic", "loss": float(loss),
                           "config": {"model": "ResNet-50", "per_rank_batch": a.batch, "image": a.image,
                                      "parallelism": f"dp{world}", "optimizer": "SGD(0.1, momentum 0.9)",
-                                     "path": "FlatBucketDDP + stock conv (MIOpen), bf16 autocast"}}), flush=True)
+                                     "path": ("FlatBucketDDP + ops HIP kernels" + (" (fp8 fwd GEMMs)" if a.fp8 else " (bf16)"))
+                                     if a.path == "ops" else "FlatBucketDDP + stock conv (MIOpen), bf16 autocast"}}),
+              flush=True)
     dist.destroy_process_group()
     return 0
 

@@ -1,7 +1,9 @@
 """Build the native HIP/C++ code of the framework for gfx950 (MI355X), in-tree.
 
-``python -m distributeddataparallel_cifar10_amd.build`` compiles ``csrc/engine.hip`` (which includes the kernel
-translation unit) with ``hipcc --offload-arch=gfx950`` into ``_lib/libdca_engine.so``.  hipcc cross-compiles without
+``python -m distributeddataparallel_cifar10_amd.build`` compiles, with ``hipcc --offload-arch=gfx950``:
+  * ``csrc/engine.hip`` (the NetResDeep training engine + xGMI all-reduce) -> ``_lib/libdca_engine.so``
+  * ``csrc/ops_api.hip`` (the general layer kernels of ``ops/``: MFMA GEMM bf16/fp8, im2col, BN, pooling, CE,
+    SGD, fp8 quantisation) -> ``_lib/libdca_ops.so``  hipcc cross-compiles without
 a GPU, so this runs on the CPU-only build host too.  The library links the HIP runtime and RCCL by SONAME
 (``libamdhip64.so.7``, ``librccl.so.1``); loaded after ``import torch`` it binds to the copies torch already
 loaded, so there is exactly one HIP runtime in the process.
@@ -18,12 +20,15 @@ PKG_DIR = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(PKG_DIR, "csrc")
 LIB_DIR = os.path.join(PKG_DIR, "_lib")
 ENGINE_LIB = os.path.join(LIB_DIR, "libdca_engine.so")
+OPS_LIB = os.path.join(LIB_DIR, "libdca_ops.so")
 ARCH = os.environ.get("DCA_OFFLOAD_ARCH", "gfx950")
 # Variants: "" = production; "stamps" = diagnostic build with in-kernel phase stamps (-DDCA_STAMPS).
-VARIANTS = {"": [], "stamps": ["-DDCA_STAMPS"]}
+VARIANTS = {"": [], "stamps": ["-DDCA_STAMPS"], "ops": []}
 
 
 def lib_path(variant: str = "") -> str:
+    if variant == "ops":
+        return OPS_LIB
     return ENGINE_LIB if not variant else os.path.join(LIB_DIR, f"libdca_engine_{variant}.so")
 
 
@@ -61,7 +66,8 @@ def build(force: bool = False, verbose: bool = False, variant: str = "") -> str:
     cmd = [
         _hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
         "-Wall", "-Wno-unused-function", "-Wno-unused-variable", *VARIANTS[variant],
-        os.path.join(CSRC, "engine.hip"), "-o", tmp, "-lrccl",
+        os.path.join(CSRC, "ops_api.hip" if variant == "ops" else "engine.hip"), "-o", tmp,
+        *([] if variant == "ops" else ["-lrccl"]),
     ]
     if verbose:
         print(" ".join(cmd), flush=True)
@@ -74,11 +80,14 @@ def build(force: bool = False, verbose: bool = False, variant: str = "") -> str:
     return out
 
 
-def build_all(force: bool = False, verbose: bool = False, variants=("",)) -> list:
-    """Build the listed library variants (default: production only); returns their paths."""
-    return [build(force=force, verbose=verbose, variant=v) for v in variants]
+def build_all(force: bool = False, verbose: bool = False, variants=("", "ops")) -> list:
+    """Build the listed library variants (default: the engine and the ops library, compiled concurrently);
+    returns their paths."""
+    from concurrent.futures import ThreadPoolExecutor
+    with ThreadPoolExecutor(max_workers=len(variants)) as ex:
+        return list(ex.map(lambda v: build(force=force, verbose=verbose, variant=v), variants))
 
 
 if __name__ == "__main__":
-    for v in (["", "stamps"] if "--all" in sys.argv else [""]):
+    for v in (["", "ops", "stamps"] if "--all" in sys.argv else ["", "ops"]):
         print(build(force="--force" in sys.argv, verbose=True, variant=v))

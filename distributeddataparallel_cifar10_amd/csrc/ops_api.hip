@@ -1,0 +1,212 @@
+// C ABI of the ops layer (libdca_ops.so), driven from ops/_native.py with torch-allocated tensors and the
+// caller's HIP stream.  Every entry point validates what the kernels assume about shapes before launching
+// (a bad shape is an error string, never an out-of-bounds access on the GPU).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstring>
+#include <string>
+
+#include "ops_nn.hip"
+
+namespace {
+thread_local std::string g_err;
+#define OPCK(x)                                              \
+  do {                                                       \
+    hipError_t e_ = (x);                                     \
+    if (e_ != hipSuccess) {                                  \
+      g_err = std::string(#x) + ": " + hipGetErrorString(e_); \
+      return -1;                                             \
+    }                                                        \
+  } while (0)
+#define REQUIRE(c, msg)  \
+  do {                   \
+    if (!(c)) {          \
+      g_err = msg;       \
+      return -1;         \
+    }                    \
+  } while (0)
+
+inline int grid_for(long work, int per_block = 256, int cap = 8192) {
+  long b = (work + per_block - 1) / per_block;
+  return (int)std::max(1L, std::min(b, (long)cap));
+}
+bool g_lds_set = false;
+}  // namespace
+
+using namespace dca::ops;
+
+extern "C" {
+
+const char* dca_ops_last_error() { return g_err.c_str(); }
+int dca_ops_abi_version() { return 1; }
+
+// Must match ops/_native.py::GemmArgs.
+int dca_ops_gemm(const GemmArgs* a, void* stream) {
+  GemmArgs g = *a;
+  hipStream_t st = (hipStream_t)stream;
+  REQUIRE(g.M > 0 && g.N > 0 && g.K > 0, "gemm: empty problem");
+  REQUIRE(!g.fp8 || (!g.ta && !g.tb), "gemm: fp8 operands must be K-contiguous (ta = tb = 0)");
+  REQUIRE(!g.fp8 || (g.K % 16 == 0 && g.lda % 16 == 0 && g.ldb % 16 == 0), "gemm: fp8 needs K, lda, ldb % 16 == 0");
+  REQUIRE(g.ta || g.lda >= g.K, "gemm: lda < K");
+  REQUIRE(g.tb || g.ldb >= g.K, "gemm: ldb < K");
+  REQUIRE(!g.ta || g.lda >= g.M, "gemm: lda < M (transposed A)");
+  REQUIRE(!g.tb || g.ldb >= g.N, "gemm: ldb < N (transposed B)");
+  REQUIRE(g.ldc >= g.N, "gemm: ldc < N");
+  if (!g_lds_set) {
+    OPCK(hipFuncSetAttribute((const void*)k_gemm<false>, hipFuncAttributeMaxDynamicSharedMemorySize, G_LDS));
+    OPCK(hipFuncSetAttribute((const void*)k_gemm<true>, hipFuncAttributeMaxDynamicSharedMemorySize, G_LDS));
+    g_lds_set = true;
+  }
+  const int kt = GBK_BYTES / (g.fp8 ? 1 : 2);
+  if (g.splits < 1) g.splits = 1;
+  if (g.splits > 1) {
+    REQUIRE(g.ws != nullptr, "gemm: split-K needs a workspace");
+    int kps = (g.K + g.splits - 1) / g.splits;
+    kps = (kps + kt - 1) / kt * kt;
+    g.k_per_split = kps;
+    g.splits = (g.K + kps - 1) / kps;
+  } else {
+    g.k_per_split = g.K;
+  }
+  const int tiles = ((g.M + GBM - 1) / GBM) * ((g.N + GBN - 1) / GBN);
+  const dim3 grid(tiles, g.splits);
+  if (g.fp8) hipLaunchKernelGGL(k_gemm<true>, grid, dim3(GT), G_LDS, st, g);
+  else hipLaunchKernelGGL(k_gemm<false>, grid, dim3(GT), G_LDS, st, g);
+  if (g.splits > 1) hipLaunchKernelGGL(k_gemm_splitk_reduce, dim3(grid_for((long)g.M * g.N)), dim3(256), 0, st, g);
+  OPCK(hipGetLastError());
+  return 0;
+}
+
+int dca_ops_im2col(const void* x, void* cols, const ConvGeom* geom, void* stream) {
+  const ConvGeom g = *geom;
+  REQUIRE(g.Kp % 8 == 0 && g.Kp >= g.K && g.K == g.KH * g.KW * g.C, "im2col: bad column geometry");
+  const long work = (long)g.N * g.Ho * g.Wo * (g.Kp / 8);
+  hipLaunchKernelGGL(k_im2col, dim3(grid_for(work)), dim3(256), 0, (hipStream_t)stream, (const bf16_t*)x,
+                     (bf16_t*)cols, g);
+  OPCK(hipGetLastError());
+  return 0;
+}
+
+int dca_ops_col2im(const void* dcols, void* dx, const ConvGeom* geom, void* stream) {
+  const ConvGeom g = *geom;
+  REQUIRE(g.Kp % 8 == 0 && g.Kp >= g.K, "col2im: bad column geometry");
+  hipLaunchKernelGGL(k_col2im, dim3(grid_for((long)g.N * g.H * g.W * g.C)), dim3(256), 0, (hipStream_t)stream,
+                     (const bf16_t*)dcols, (bf16_t*)dx, g);
+  OPCK(hipGetLastError());
+  return 0;
+}
+
+// BatchNorm train forward fused with ReLU / residual.  part: [ceil(M/256)][C] float2 scratch; stats: [C] float2
+// (mean, invstd) kept for the backward.  momentum 0: running stats untouched (but still the shift).
+int dca_ops_bn_fwd(const void* x, const void* r, void* out, float* part, float* stats, const float* gamma,
+                   const float* beta, float* rm, float* rv, long M, int C, float eps, float momentum, int relu,
+                   int res_mode, void* stream) {
+  REQUIRE(C % 8 == 0, "bn: C must be a multiple of 8");
+  REQUIRE(res_mode == 0 || r != nullptr, "bn: residual missing");
+  hipStream_t st = (hipStream_t)stream;
+  const int nparts = (int)((M + BN_ROWS - 1) / BN_ROWS);
+  hipLaunchKernelGGL(k_bn_stats, dim3((C + 63) / 64, nparts), dim3(256), 0, st, (const bf16_t*)x, rm, (float2*)part,
+                     (int)M, C);
+  hipLaunchKernelGGL(k_bn_finalize, dim3((C + 255) / 256), dim3(256), 0, st, (const float2*)part, nparts, (int)M, C,
+                     rm, rv, (float2*)stats, eps, momentum);
+  hipLaunchKernelGGL(k_bn_apply, dim3(grid_for(M * C / 8)), dim3(256), 0, st, (const bf16_t*)x, (const bf16_t*)r,
+                     (bf16_t*)out, (const float2*)stats, gamma, beta, M, C, relu, res_mode);
+  OPCK(hipGetLastError());
+  return 0;
+}
+
+int dca_ops_bn_bwd(const void* dy, const void* x, const void* r, const float* stats, const float* gamma,
+                   const float* beta, float* part, float* sums, float* dgamma, float* dbeta, void* dx, void* dr,
+                   long M, int C, int relu, int res_mode, int accumulate, void* stream) {
+  REQUIRE(C % 8 == 0, "bn: C must be a multiple of 8");
+  REQUIRE(res_mode != 2 || (r != nullptr && dr != nullptr), "bn bwd: residual tensors missing");
+  hipStream_t st = (hipStream_t)stream;
+  const int nparts = (int)((M + BN_ROWS - 1) / BN_ROWS);
+  hipLaunchKernelGGL(k_bn_bwd_stats, dim3((C + 63) / 64, nparts), dim3(256), 0, st, (const bf16_t*)dy,
+                     (const bf16_t*)x, (const bf16_t*)r, (const float2*)stats, gamma, beta, (float2*)part, (int)M, C,
+                     relu, res_mode);
+  hipLaunchKernelGGL(k_bn_bwd_finalize, dim3((C + 255) / 256), dim3(256), 0, st, (const float2*)part, nparts, C,
+                     dgamma, dbeta, (float2*)sums, accumulate);
+  hipLaunchKernelGGL(k_bn_bwd_apply, dim3(grid_for(M * C / 8)), dim3(256), 0, st, (const bf16_t*)dy, (const bf16_t*)x,
+                     (const bf16_t*)r, (const float2*)stats, gamma, beta, (const float2*)sums, (bf16_t*)dx,
+                     (bf16_t*)dr, M, C, relu, res_mode);
+  OPCK(hipGetLastError());
+  return 0;
+}
+
+int dca_ops_maxpool_fwd(const void* x, void* y, void* arg, const PoolGeom* geom, void* stream) {
+  const PoolGeom g = *geom;
+  REQUIRE(g.K * g.K <= 255 && g.K > 0 && g.S > 0, "maxpool: bad window");
+  hipLaunchKernelGGL(k_maxpool_fwd, dim3(grid_for((long)g.N * g.Ho * g.Wo * g.C)), dim3(256), 0, (hipStream_t)stream,
+                     (const bf16_t*)x, (bf16_t*)y, (uint8_t*)arg, g);
+  OPCK(hipGetLastError());
+  return 0;
+}
+
+int dca_ops_maxpool_bwd(const void* dy, const void* arg, void* dx, const PoolGeom* geom, void* stream) {
+  const PoolGeom g = *geom;
+  hipLaunchKernelGGL(k_maxpool_bwd, dim3(grid_for((long)g.N * g.H * g.W * g.C)), dim3(256), 0, (hipStream_t)stream,
+                     (const bf16_t*)dy, (const uint8_t*)arg, (bf16_t*)dx, g);
+  OPCK(hipGetLastError());
+  return 0;
+}
+
+int dca_ops_avgpool_fwd(const void* x, float* y, int N, int HW, int C, void* stream) {
+  hipLaunchKernelGGL(k_avgpool_fwd, dim3((C + 255) / 256, N), dim3(256), 0, (hipStream_t)stream, (const bf16_t*)x, y,
+                     N, HW, C);
+  OPCK(hipGetLastError());
+  return 0;
+}
+
+int dca_ops_avgpool_bwd(const float* dy, void* dx, int N, int HW, int C, void* stream) {
+  hipLaunchKernelGGL(k_avgpool_bwd, dim3(grid_for((long)N * HW * C)), dim3(256), 0, (hipStream_t)stream, dy,
+                     (bf16_t*)dx, N, HW, C);
+  OPCK(hipGetLastError());
+  return 0;
+}
+
+int dca_ops_cross_entropy(const float* logits, const long* labels, float* loss, float* dlogits, int B, int K,
+                          float grad_scale, void* stream) {
+  REQUIRE(B > 0 && K > 0, "cross_entropy: empty input");
+  hipLaunchKernelGGL(k_cross_entropy, dim3(B), dim3(64), 0, (hipStream_t)stream, logits, labels, loss, dlogits, B, K,
+                     grad_scale);
+  OPCK(hipGetLastError());
+  return 0;
+}
+
+// first: device int (1 on the first momentum step); cleared after the update.
+int dca_ops_sgd(float* p, const float* g, float* buf, long n, float lr, float mu, float wd, int* first, void* stream) {
+  REQUIRE(mu == 0.f || buf != nullptr, "sgd: momentum buffer missing");
+  hipStream_t st = (hipStream_t)stream;
+  hipLaunchKernelGGL(k_sgd, dim3(grid_for(n, 256, 2048)), dim3(256), 0, st, p, g, buf, n, lr, mu, wd, first);
+  if (first) hipLaunchKernelGGL(k_clear_flag, dim3(1), dim3(1), 0, st, first);
+  OPCK(hipGetLastError());
+  return 0;
+}
+
+// x (fp32 if is_f32 else bf16, n elements) -> q fp8 e4m3; amax_bits: device uint, zeroed here first.
+int dca_ops_quant_fp8(const void* x, int is_f32, long n, void* q, unsigned* amax_bits, void* stream) {
+  hipStream_t st = (hipStream_t)stream;
+  OPCK(hipMemsetAsync(amax_bits, 0, sizeof(unsigned), st));
+  const int grid = grid_for(n, 256, 1024);
+  if (is_f32) {
+    hipLaunchKernelGGL(k_amax<float>, dim3(grid), dim3(256), 0, st, (const float*)x, n, amax_bits);
+    hipLaunchKernelGGL(k_quant_fp8<float>, dim3(grid_for(n / 4 + 1)), dim3(256), 0, st, (const float*)x,
+                       (uint8_t*)q, n, amax_bits);
+  } else {
+    hipLaunchKernelGGL(k_amax<bf16_t>, dim3(grid), dim3(256), 0, st, (const bf16_t*)x, n, amax_bits);
+    hipLaunchKernelGGL(k_quant_fp8<bf16_t>, dim3(grid_for(n / 4 + 1)), dim3(256), 0, st, (const bf16_t*)x,
+                       (uint8_t*)q, n, amax_bits);
+  }
+  OPCK(hipGetLastError());
+  return 0;
+}
+
+int dca_ops_fp8_alpha(const unsigned* amax_a, const unsigned* amax_b, float extra, float* alpha, void* stream) {
+  hipLaunchKernelGGL(k_fp8_alpha, dim3(1), dim3(1), 0, (hipStream_t)stream, amax_a, amax_b, extra, alpha);
+  OPCK(hipGetLastError());
+  return 0;
+}
+
+}  // extern "C"

@@ -1,0 +1,279 @@
+// General MFMA GEMM for the ops layer (ops/): C[M,N] = alpha * sum_k A(m,k) * B(n,k)  (+ bias[n]) (+ beta*C) (ReLU)
+//
+// Operands are bf16 (v_mfma_f32_16x16x32_bf16) or OCP fp8 e4m3 (v_mfma_scale_f32_16x16x128_f8f6f4 with unit
+// E8M0 block scales: the MX-scaled form is the one that runs at the fp8 rate on CDNA4; the per-tensor fp8
+// scales are folded into alpha).  Accumulation is fp32; the output is fp32 or bf16.
+//
+// Operand access: A(m,k) = A[m*lda + k] (ta = 0, K contiguous -- the MFMA-natural "NT" form) or A[k*lda + m]
+// (ta = 1, bf16 only: the loader transposes while writing LDS); B(n,k) likewise with tb.  This covers, for a
+// channels-last 1x1 convolution / linear layer with X[M,Cin], W[Cout,Cin], dY[M,Cout]:
+//   forward  Y  = X  . W^T   (ta 0, tb 0)      dgrad dX = dY . W   (ta 0, tb 1)
+//   wgrad    dW = dY^T . X   (ta 1, tb 1, split-K over the pixel dimension into an fp32 slab + reduce kernel)
+//
+// Tiling (CDNA4, 64-wide waves): 128x128 output tile per 256-thread workgroup (4 waves as 2x2, each 64x64 =
+// 4x4 MFMA 16x16 tiles, 64 fp32 accumulator VGPRs), K-tile = 128 bytes per row (64 bf16 / 128 fp8), LDS
+// double-buffered (64 KiB -> 2 workgroups per CU), register-staged prefetch of tile k+1 during the MFMAs of
+// tile k, one barrier per K-tile.  LDS rows are 128 B with 16-B chunks XOR-swizzled by (row >> 1) & 7, so a
+// ds_read_b128 of 16 lanes (16 rows, one chunk) covers all 64 banks once.  Workgroup ids are remapped so that
+// consecutive output tiles (which share their A rows) run on the same XCD and share its L2.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace dca {
+namespace ops {
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef short s16x8 __attribute__((ext_vector_type(8)));
+typedef int i32x8 __attribute__((ext_vector_type(8)));
+
+constexpr int GT = 256;          // threads per GEMM workgroup
+constexpr int GBM = 128, GBN = 128;
+constexpr int GBK_BYTES = 128;   // bytes of K per row per K-tile
+constexpr int G_TILE_BYTES = GBM * GBK_BYTES;  // 16 KiB per operand per buffer
+constexpr int G_LDS = 2 * 2 * G_TILE_BYTES;     // 64 KiB
+
+struct GemmArgs {
+  const void* A;
+  const void* B;
+  void* C;             // output (fp32 or bf16), row stride ldc
+  const float* bias;   // [N] or null
+  float* ws;           // split-K slab [splits][M][N] fp32 (splits > 1)
+  int M, N, K;         // K in elements
+  int lda, ldb, ldc;   // strides in elements
+  float alpha, beta;   // beta: C += beta * C_old (fp32/bf16 read of the output)
+  int ta, tb;          // transposed operand access (bf16 only)
+  int fp8;             // 1: operands are fp8 e4m3 (ta = tb = 0)
+  int relu, out_bf16;
+  int splits, k_per_split;  // split-K (k_per_split a multiple of the K-tile)
+  const float* alpha_dev;   // optional device-side factor (fp8 per-tensor scales: no host sync)
+};
+
+__device__ __forceinline__ int lds_off(int row, int chunk) { return row * 128 + ((chunk ^ ((row >> 1) & 7)) << 4); }
+
+__device__ __forceinline__ unsigned short f2bf_rne(float f) {
+  return __builtin_bit_cast(unsigned short, (__bf16)f);
+}
+__device__ __forceinline__ float bf2f(unsigned short h) { return __uint_as_float((unsigned)h << 16); }
+
+// Stage of one operand tile held in registers between its global load and its LDS write.
+struct Stage {
+  uint4 v[4];
+};
+
+// Non-transposed operand: rows r0.., K bytes kb0.. (row-major, K contiguous).  Thread t owns chunks
+// idx = t + 256 i: row idx >> 3, chunk idx & 7.  Rows past R are clamped (their results are never stored);
+// bytes past the K range are zero.  A chunk that straddles the K end, or a row stride that is not 16-B
+// aligned, takes the element-wise path (esz-byte loads).
+template <int ESZ>
+__device__ __forceinline__ void load_nt(Stage& s, const char* base, int r0, int R, size_t ld_bytes, int kb0,
+                                        int kb_end) {
+  const bool vec_ok = (ld_bytes & 15) == 0;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int idx = threadIdx.x + GT * i, row = idx >> 3, ch = idx & 7;
+    int rg = r0 + row;
+    rg = rg < R ? rg : R - 1;
+    const int kb = kb0 + ch * 16;
+    const char* rowp = base + (size_t)rg * ld_bytes;
+    if (vec_ok && kb + 16 <= kb_end) {
+      s.v[i] = *(const uint4*)(rowp + kb);
+    } else {
+      unsigned w[4] = {0u, 0u, 0u, 0u};
+#pragma unroll
+      for (int e = 0; e < 16 / ESZ; ++e) {
+        const int b = kb + e * ESZ;
+        unsigned x = 0u;
+        if (b < kb_end) x = ESZ == 2 ? (unsigned)*(const unsigned short*)(rowp + b) : (unsigned)*(const uint8_t*)(rowp + b);
+        w[(e * ESZ) >> 2] |= x << (((e * ESZ) & 3) * 8);
+      }
+      s.v[i] = uint4{w[0], w[1], w[2], w[3]};
+    }
+  }
+}
+__device__ __forceinline__ void store_nt(const Stage& s, char* lds) {
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int idx = threadIdx.x + GT * i;
+    *(uint4*)(lds + lds_off(idx >> 3, idx & 7)) = s.v[i];
+  }
+}
+// Transposed bf16 operand: element (r, k) at base[k*ld + r].  Thread t owns 8 consecutive r at one k:
+// idx = t + 256 i: k = idx >> 4 (64 per tile), r group (idx & 15) * 8.  Vector loads where the 8 rows are in
+// range and 16-B aligned, element-wise loads otherwise (rows past R clamped, never stored).
+__device__ __forceinline__ void load_t(Stage& s, const unsigned short* base, int r0, int R, size_t ld, int k0,
+                                       int k_end) {
+  const bool vec_ok = (ld & 7) == 0;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int idx = threadIdx.x + GT * i, k = k0 + (idx >> 4);
+    const int rg = r0 + (idx & 15) * 8;
+    if (k >= k_end) {
+      s.v[i] = uint4{0u, 0u, 0u, 0u};
+    } else if (vec_ok && rg + 8 <= R) {
+      s.v[i] = *(const uint4*)(base + (size_t)k * ld + rg);
+    } else {
+      unsigned w[4] = {0u, 0u, 0u, 0u};
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const int r = rg + e < R ? rg + e : R - 1;
+        w[e >> 1] |= (unsigned)base[(size_t)k * ld + r] << ((e & 1) * 16);
+      }
+      s.v[i] = uint4{w[0], w[1], w[2], w[3]};
+    }
+  }
+}
+__device__ __forceinline__ void store_t(const Stage& s, char* lds) {
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int idx = threadIdx.x + GT * i, k = idx >> 4, rb = (idx & 15) * 8;
+    const unsigned w[4] = {s.v[i].x, s.v[i].y, s.v[i].z, s.v[i].w};
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const unsigned short h = (unsigned short)(w[j >> 1] >> ((j & 1) * 16));
+      *(unsigned short*)(lds + lds_off(rb + j, k >> 3) + (k & 7) * 2) = h;
+    }
+  }
+}
+
+__device__ __forceinline__ int xcd_remap(int orig, int nwg) {
+  const int xcd = orig & 7, q = nwg >> 3, r = nwg & 7;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (orig >> 3);
+}
+
+template <bool FP8>
+__global__ void __launch_bounds__(GT) k_gemm(GemmArgs g) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int ntm = (g.M + GBM - 1) / GBM, ntn = (g.N + GBN - 1) / GBN;
+  const int tile = xcd_remap(blockIdx.x, ntm * ntn);
+  const int tm = tile / ntn, tn = tile % ntn;
+  const int m0 = tm * GBM, n0 = tn * GBN;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, wr = wave >> 1, wc = wave & 1;
+  constexpr int ESZ = FP8 ? 1 : 2;
+  const int ksplit = blockIdx.y;
+  const int k_begin = ksplit * g.k_per_split;
+  const int k_end = min(g.K, k_begin + g.k_per_split);
+  constexpr int KT = GBK_BYTES / ESZ;  // elements per K-tile
+  const int nk = (k_end - k_begin + KT - 1) / KT;
+
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int m = 0; m < 4; ++m)
+#pragma unroll
+    for (int n = 0; n < 4; ++n) acc[m][n] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  auto load = [&](Stage& sa, Stage& sb, int kt) {
+    const int k0 = k_begin + kt * KT;
+    if (g.ta) load_t(sa, (const unsigned short*)g.A, m0, g.M, g.lda, k0, k_end);
+    else load_nt<ESZ>(sa, (const char*)g.A, m0, g.M, (size_t)g.lda * ESZ, k0 * ESZ, k_end * ESZ);
+    if (g.tb) load_t(sb, (const unsigned short*)g.B, n0, g.N, g.ldb, k0, k_end);
+    else load_nt<ESZ>(sb, (const char*)g.B, n0, g.N, (size_t)g.ldb * ESZ, k0 * ESZ, k_end * ESZ);
+  };
+  auto store = [&](const Stage& sa, const Stage& sb, int buf) {
+    char* la = smem + buf * 2 * G_TILE_BYTES;
+    char* lb = la + G_TILE_BYTES;
+    if (g.ta) store_t(sa, la);
+    else store_nt(sa, la);
+    if (g.tb) store_t(sb, lb);
+    else store_nt(sb, lb);
+  };
+
+  Stage sa, sb;
+  if (nk > 0) {
+    load(sa, sb, 0);
+    store(sa, sb, 0);
+  }
+  __syncthreads();
+  for (int kt = 0; kt < nk; ++kt) {
+    const int buf = kt & 1;
+    if (kt + 1 < nk) load(sa, sb, kt + 1);  // global loads in flight during the MFMAs below
+    const char* la = smem + buf * 2 * G_TILE_BYTES;
+    const char* lb = la + G_TILE_BYTES;
+    if constexpr (!FP8) {
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        s16x8 af[4], bfr[4];
+#pragma unroll
+        for (int m = 0; m < 4; ++m)
+          af[m] = *(const s16x8*)(la + lds_off(wr * 64 + m * 16 + (lane & 15), s * 4 + (lane >> 4)));
+#pragma unroll
+        for (int n = 0; n < 4; ++n)
+          bfr[n] = *(const s16x8*)(lb + lds_off(wc * 64 + n * 16 + (lane & 15), s * 4 + (lane >> 4)));
+#pragma unroll
+        for (int m = 0; m < 4; ++m)
+#pragma unroll
+          for (int n = 0; n < 4; ++n)
+            acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[m], bfr[n], acc[m][n], 0, 0, 0);
+      }
+    } else {
+      i32x8 af[4], bfr[4];
+#pragma unroll
+      for (int m = 0; m < 4; ++m) {
+        const int row = wr * 64 + m * 16 + (lane & 15), c = 2 * (lane >> 4);
+        const uint4 lo = *(const uint4*)(la + lds_off(row, c)), hi = *(const uint4*)(la + lds_off(row, c + 1));
+        af[m] = i32x8{(int)lo.x, (int)lo.y, (int)lo.z, (int)lo.w, (int)hi.x, (int)hi.y, (int)hi.z, (int)hi.w};
+      }
+#pragma unroll
+      for (int n = 0; n < 4; ++n) {
+        const int row = wc * 64 + n * 16 + (lane & 15), c = 2 * (lane >> 4);
+        const uint4 lo = *(const uint4*)(lb + lds_off(row, c)), hi = *(const uint4*)(lb + lds_off(row, c + 1));
+        bfr[n] = i32x8{(int)lo.x, (int)lo.y, (int)lo.z, (int)lo.w, (int)hi.x, (int)hi.y, (int)hi.z, (int)hi.w};
+      }
+#pragma unroll
+      for (int m = 0; m < 4; ++m)
+#pragma unroll
+        for (int n = 0; n < 4; ++n)  // fp8 e4m3 x fp8 e4m3, unit E8M0 scales (127)
+          acc[m][n] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(af[m], bfr[n], acc[m][n], 0, 0, 0, 127, 0, 127);
+    }
+    if (kt + 1 < nk) store(sa, sb, buf ^ 1);
+    __syncthreads();
+  }
+
+  // epilogue: C/D fragment (16x16): col = lane & 15, row = (lane >> 4) * 4 + j
+  const float alpha = g.alpha * (g.alpha_dev ? *g.alpha_dev : 1.f);
+#pragma unroll
+  for (int m = 0; m < 4; ++m) {
+#pragma unroll
+    for (int n = 0; n < 4; ++n) {
+      const int col = n0 + wc * 64 + n * 16 + (lane & 15);
+      if (col >= g.N) continue;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int row = m0 + wr * 64 + m * 16 + (lane >> 4) * 4 + j;
+        if (row >= g.M) continue;
+        float v = acc[m][n][j];
+        if (g.splits > 1) {
+          g.ws[((size_t)ksplit * g.M + row) * g.N + col] = v;
+          continue;
+        }
+        v *= alpha;
+        if (g.bias) v += g.bias[col];
+        const size_t o = (size_t)row * g.ldc + col;
+        if (g.beta != 0.f) v += g.beta * (g.out_bf16 ? bf2f(((const unsigned short*)g.C)[o]) : ((const float*)g.C)[o]);
+        if (g.relu) v = v > 0.f ? v : 0.f;
+        if (g.out_bf16) ((unsigned short*)g.C)[o] = f2bf_rne(v);
+        else ((float*)g.C)[o] = v;
+      }
+    }
+  }
+}
+
+// Split-K combine: C = alpha * sum_s ws[s] (+bias) (+beta*C) (ReLU), fixed summation order (deterministic).
+__global__ void __launch_bounds__(256) k_gemm_splitk_reduce(GemmArgs g) {
+  const size_t total = (size_t)g.M * g.N;
+  for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < total; i += (size_t)gridDim.x * 256) {
+    float v = 0.f;
+    for (int s = 0; s < g.splits; ++s) v += g.ws[(size_t)s * total + i];
+    const int row = (int)(i / g.N), col = (int)(i % g.N);
+    v *= g.alpha * (g.alpha_dev ? *g.alpha_dev : 1.f);
+    if (g.bias) v += g.bias[col];
+    const size_t o = (size_t)row * g.ldc + col;
+    if (g.beta != 0.f) v += g.beta * (g.out_bf16 ? bf2f(((const unsigned short*)g.C)[o]) : ((const float*)g.C)[o]);
+    if (g.relu) v = v > 0.f ? v : 0.f;
+    if (g.out_bf16) ((unsigned short*)g.C)[o] = f2bf_rne(v);
+    else ((float*)g.C)[o] = v;
+  }
+}
+
+}  // namespace ops
+}  // namespace dca

@@ -1,0 +1,448 @@
+// Layer kernels of the ops layer (ops/): channels-last (NHWC) bf16 activations, fp32 statistics / parameters.
+//
+// Reference ops they implement: conv2d via im2col + MFMA GEMM (K1/K4/K19/K22: the GEMM is
+// ops_gemm.hip), BatchNorm2d train forward/backward with the ReLU and residual add fused (K5-K7, K17, K18, K20),
+// max_pool2d forward/backward (K3, K16), global average pool (ResNet family), cross-entropy forward+backward
+// (K11, K12), SGD with momentum / weight decay over a flat buffer (K24), and the fp8 e4m3 quantisation used by
+// the fp8 GEMM path (amax + scale computed on the device: no host sync).
+//
+// Every reduction has a fixed order (per-block partials, then one finalize): results are deterministic.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "ops_gemm.hip"
+
+namespace dca {
+namespace ops {
+
+typedef unsigned short bf16_t;
+
+__device__ __forceinline__ float ld_bf(const bf16_t* p) { return bf2f(*p); }
+
+// ---------------------------------------------------------------------------------------------------------
+// im2col / col2im (NHWC).  Column index k = (kh * KW + kw) * C + c, rows = output pixels (n, oh, ow); columns
+// k >= KH*KW*C up to the padded width Kp are zero.
+// ---------------------------------------------------------------------------------------------------------
+struct ConvGeom {
+  int N, H, W, C;        // input
+  int KH, KW, stride, pad;
+  int Ho, Wo;            // output
+  int K, Kp;             // K = KH*KW*C, Kp = padded column count (multiple of 8)
+};
+
+__global__ void __launch_bounds__(256) k_im2col(const bf16_t* __restrict__ x, bf16_t* __restrict__ cols, ConvGeom g) {
+  const int groups = g.Kp >> 3;  // 8 columns per thread
+  const long total = (long)g.N * g.Ho * g.Wo * groups;
+  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < total; i += (long)gridDim.x * 256) {
+    const int kg = (int)(i % groups);
+    const long row = i / groups;
+    const int ow = (int)(row % g.Wo), oh = (int)((row / g.Wo) % g.Ho), n = (int)(row / ((long)g.Wo * g.Ho));
+    const int k0 = kg * 8;
+    uint4 out;
+    if ((g.C & 7) == 0) {  // 8 consecutive k share (kh, kw): one 16-B load
+      const int tap = k0 / g.C, c = k0 % g.C, kh = tap / g.KW, kw = tap % g.KW;
+      const int h = oh * g.stride - g.pad + kh, w = ow * g.stride - g.pad + kw;
+      const bool in = k0 < g.K && h >= 0 && h < g.H && w >= 0 && w < g.W;
+      out = in ? *(const uint4*)(x + (((long)n * g.H + h) * g.W + w) * g.C + c) : uint4{0u, 0u, 0u, 0u};
+    } else {
+      unsigned wd[4] = {0u, 0u, 0u, 0u};
+      for (int e = 0; e < 8; ++e) {
+        const int k = k0 + e;
+        if (k >= g.K) break;
+        const int tap = k / g.C, c = k % g.C, kh = tap / g.KW, kw = tap % g.KW;
+        const int h = oh * g.stride - g.pad + kh, w = ow * g.stride - g.pad + kw;
+        if (h >= 0 && h < g.H && w >= 0 && w < g.W)
+          wd[e >> 1] |= (unsigned)x[(((long)n * g.H + h) * g.W + w) * g.C + c] << ((e & 1) * 16);
+      }
+      out = uint4{wd[0], wd[1], wd[2], wd[3]};
+    }
+    *(uint4*)(cols + row * g.Kp + k0) = out;
+  }
+}
+
+// dX[n,h,w,c] = sum over the (kh, kw) taps whose output pixel read (h, w): gather form, no atomics.
+__global__ void __launch_bounds__(256) k_col2im(const bf16_t* __restrict__ dcols, bf16_t* __restrict__ dx, ConvGeom g) {
+  const long total = (long)g.N * g.H * g.W * g.C;
+  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < total; i += (long)gridDim.x * 256) {
+    const int c = (int)(i % g.C);
+    const long pix = i / g.C;
+    const int w = (int)(pix % g.W), h = (int)((pix / g.W) % g.H), n = (int)(pix / ((long)g.W * g.H));
+    float s = 0.f;
+    for (int kh = 0; kh < g.KH; ++kh) {
+      const int th = h + g.pad - kh;
+      if (th < 0 || th % g.stride) continue;
+      const int oh = th / g.stride;
+      if (oh >= g.Ho) continue;
+      for (int kw = 0; kw < g.KW; ++kw) {
+        const int tw = w + g.pad - kw;
+        if (tw < 0 || tw % g.stride) continue;
+        const int ow = tw / g.stride;
+        if (ow >= g.Wo) continue;
+        s += ld_bf(dcols + (((long)n * g.Ho + oh) * g.Wo + ow) * g.Kp + (kh * g.KW + kw) * g.C + c);
+      }
+    }
+    dx[i] = f2bf_rne(s);
+  }
+}
+
+// ---------------------------------------------------------------------------------------------------------
+// BatchNorm (training) over x[M][C] (M = N*H*W), fused with ReLU and a residual add.
+//   res_mode 0: out = act(z)            1: out = act(z) + r  (NetResDeep: skip after the ReLU)
+//   res_mode 2: out = act(z + r)        (ResNet bottleneck)            z = (x - mean) * invstd * gamma + beta
+// Statistics: per-block partial sums of (x - shift) and (x - shift)^2 in fp32 (shift = running_mean, close to
+// the batch mean: a single pass without cancellation trouble), then one finalize.
+// ---------------------------------------------------------------------------------------------------------
+constexpr int BN_ROWS = 256;  // rows per partial block (threads: 64 channel lanes x 4 row lanes)
+
+// grid (ceil(C/64), ceil(M/BN_ROWS)); part[blockIdx.y][C] = (sum, sumsq)
+__global__ void __launch_bounds__(256) k_bn_stats(const bf16_t* __restrict__ x, const float* __restrict__ shift,
+                                                  float2* __restrict__ part, int M, int C) {
+  __shared__ float2 red[4][64];
+  const int cl = threadIdx.x & 63, rl = threadIdx.x >> 6, c = blockIdx.x * 64 + cl;
+  const int r0 = blockIdx.y * BN_ROWS;
+  float s = 0.f, q = 0.f;
+  if (c < C) {
+    const float k = shift[c];
+    for (int r = r0 + rl; r < min(M, r0 + BN_ROWS); r += 4) {
+      const float v = ld_bf(x + (long)r * C + c) - k;
+      s += v;
+      q += v * v;
+    }
+  }
+  red[rl][cl] = float2{s, q};
+  __syncthreads();
+  if (rl == 0 && c < C) {
+    float2 a = red[0][cl];
+    for (int j = 1; j < 4; ++j) {
+      a.x += red[j][cl].x;
+      a.y += red[j][cl].y;
+    }
+    part[(long)blockIdx.y * C + c] = a;
+  }
+}
+
+// mean/invstd per channel; running stats EMA (unbiased variance), as torch BatchNorm2d in train mode.
+__global__ void __launch_bounds__(256) k_bn_finalize(const float2* __restrict__ part, int nparts, int M, int C,
+                                                     float* __restrict__ running_mean, float* __restrict__ running_var,
+                                                     float2* __restrict__ stats, float eps, float momentum) {
+  const int c = blockIdx.x * 256 + threadIdx.x;
+  if (c >= C) return;
+  float s = 0.f, q = 0.f;
+  for (int p = 0; p < nparts; ++p) {
+    const float2 a = part[(long)p * C + c];
+    s += a.x;
+    q += a.y;
+  }
+  const float k = running_mean[c];
+  const float dm = s / M;
+  const float var = fmaxf(q / M - dm * dm, 0.f);
+  const float mean = k + dm;
+  stats[c] = float2{mean, rsqrtf(var + eps)};
+  if (momentum > 0.f) {
+    const float unb = M > 1 ? var * M / (M - 1) : var;
+    running_mean[c] = (1.f - momentum) * k + momentum * mean;
+    running_var[c] = (1.f - momentum) * running_var[c] + momentum * unb;
+  }
+}
+
+__device__ __forceinline__ void unpack8(uint4 u, float* f) {
+  const unsigned w[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+  for (int j = 0; j < 8; ++j) f[j] = __uint_as_float((w[j >> 1] >> ((j & 1) * 16)) << 16);
+}
+__device__ __forceinline__ uint4 pack8(const float* f) {
+  unsigned w[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) w[j] = (unsigned)f2bf_rne(f[2 * j]) | ((unsigned)f2bf_rne(f[2 * j + 1]) << 16);
+  return uint4{w[0], w[1], w[2], w[3]};
+}
+
+// out = fused(x); vectorised by 8 channels (C % 8 == 0)
+__global__ void __launch_bounds__(256) k_bn_apply(const bf16_t* __restrict__ x, const bf16_t* __restrict__ r,
+                                                  bf16_t* __restrict__ out, const float2* __restrict__ stats,
+                                                  const float* __restrict__ gamma, const float* __restrict__ beta,
+                                                  long M, int C, int relu, int res_mode) {
+  const int cg = C >> 3;
+  const long total = M * cg;
+  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < total; i += (long)gridDim.x * 256) {
+    const int c0 = (int)(i % cg) * 8;
+    float v[8], rv[8];
+    unpack8(*(const uint4*)(x + i * 8), v);
+    if (res_mode) unpack8(*(const uint4*)(r + i * 8), rv);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float2 st = stats[c0 + j];
+      float z = (v[j] - st.x) * st.y * gamma[c0 + j] + beta[c0 + j];
+      if (res_mode == 2) z += rv[j];
+      if (relu) z = z > 0.f ? z : 0.f;
+      if (res_mode == 1) z += rv[j];
+      v[j] = z;
+    }
+    *(uint4*)(out + i * 8) = pack8(v);
+  }
+}
+
+// dz = dy * act'(.) recomputed from x (and r); partial sums of dz and dz * xhat per channel.
+__global__ void __launch_bounds__(256) k_bn_bwd_stats(const bf16_t* __restrict__ dy, const bf16_t* __restrict__ x,
+                                                      const bf16_t* __restrict__ r, const float2* __restrict__ stats,
+                                                      const float* __restrict__ gamma, const float* __restrict__ beta,
+                                                      float2* __restrict__ part, int M, int C, int relu, int res_mode) {
+  __shared__ float2 red[4][64];
+  const int cl = threadIdx.x & 63, rl = threadIdx.x >> 6, c = blockIdx.x * 64 + cl;
+  const int r0 = blockIdx.y * BN_ROWS;
+  float s = 0.f, q = 0.f;
+  if (c < C) {
+    const float2 st = stats[c];
+    const float ga = gamma[c], be = beta[c];
+    for (int row = r0 + rl; row < min(M, r0 + BN_ROWS); row += 4) {
+      const long o = (long)row * C + c;
+      const float xh = (ld_bf(x + o) - st.x) * st.y;
+      float d = ld_bf(dy + o);
+      if (relu) {
+        float z = xh * ga + be;
+        if (res_mode == 2) z += ld_bf(r + o);
+        d = z > 0.f ? d : 0.f;
+      }
+      s += d;
+      q += d * xh;
+    }
+  }
+  red[rl][cl] = float2{s, q};
+  __syncthreads();
+  if (rl == 0 && c < C) {
+    float2 a = red[0][cl];
+    for (int j = 1; j < 4; ++j) {
+      a.x += red[j][cl].x;
+      a.y += red[j][cl].y;
+    }
+    part[(long)blockIdx.y * C + c] = a;
+  }
+}
+
+// dgamma = sum(dz * xhat), dbeta = sum(dz) (written, or added when accumulate: shared modules); sums for dx
+__global__ void __launch_bounds__(256) k_bn_bwd_finalize(const float2* __restrict__ part, int nparts, int C,
+                                                         float* __restrict__ dgamma, float* __restrict__ dbeta,
+                                                         float2* __restrict__ sums, int accumulate) {
+  const int c = blockIdx.x * 256 + threadIdx.x;
+  if (c >= C) return;
+  float s = 0.f, q = 0.f;
+  for (int p = 0; p < nparts; ++p) {
+    const float2 a = part[(long)p * C + c];
+    s += a.x;
+    q += a.y;
+  }
+  sums[c] = float2{s, q};
+  dgamma[c] = accumulate ? dgamma[c] + q : q;
+  dbeta[c] = accumulate ? dbeta[c] + s : s;
+}
+
+// dx = gamma * invstd * (dz - mean(dz) - xhat * mean(dz * xhat)); res_mode 2 also writes dr = dz
+__global__ void __launch_bounds__(256) k_bn_bwd_apply(const bf16_t* __restrict__ dy, const bf16_t* __restrict__ x,
+                                                      const bf16_t* __restrict__ r, const float2* __restrict__ stats,
+                                                      const float* __restrict__ gamma, const float* __restrict__ beta,
+                                                      const float2* __restrict__ sums, bf16_t* __restrict__ dx,
+                                                      bf16_t* __restrict__ dr, long M, int C, int relu, int res_mode) {
+  const int cg = C >> 3;
+  const long total = M * cg;
+  const float inv_m = 1.f / (float)M;
+  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < total; i += (long)gridDim.x * 256) {
+    const int c0 = (int)(i % cg) * 8;
+    float xv[8], d[8], rv[8];
+    unpack8(*(const uint4*)(x + i * 8), xv);
+    unpack8(*(const uint4*)(dy + i * 8), d);
+    if (res_mode == 2) unpack8(*(const uint4*)(r + i * 8), rv);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int c = c0 + j;
+      const float2 st = stats[c], sm = sums[c];
+      const float xh = (xv[j] - st.x) * st.y;
+      float dz = d[j];
+      if (relu) {
+        float z = xh * gamma[c] + beta[c];
+        if (res_mode == 2) z += rv[j];
+        dz = z > 0.f ? dz : 0.f;
+      }
+      rv[j] = dz;
+      d[j] = gamma[c] * st.y * (dz - sm.x * inv_m - xh * sm.y * inv_m);
+    }
+    *(uint4*)(dx + i * 8) = pack8(d);
+    if (res_mode == 2) *(uint4*)(dr + i * 8) = pack8(rv);
+  }
+}
+
+// ---------------------------------------------------------------------------------------------------------
+// Max pooling (NHWC, window KxK, stride S, padding P) with the argmax tap kept as a byte; backward gathers.
+// ---------------------------------------------------------------------------------------------------------
+struct PoolGeom {
+  int N, H, W, C, K, S, P, Ho, Wo;
+};
+
+__global__ void __launch_bounds__(256) k_maxpool_fwd(const bf16_t* __restrict__ x, bf16_t* __restrict__ y,
+                                                     uint8_t* __restrict__ arg, PoolGeom g) {
+  const long total = (long)g.N * g.Ho * g.Wo * g.C;
+  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < total; i += (long)gridDim.x * 256) {
+    const int c = (int)(i % g.C);
+    const long p = i / g.C;
+    const int ow = (int)(p % g.Wo), oh = (int)((p / g.Wo) % g.Ho), n = (int)(p / ((long)g.Wo * g.Ho));
+    float best = -INFINITY;
+    int bi = 0;
+    for (int kh = 0; kh < g.K; ++kh) {
+      const int h = oh * g.S - g.P + kh;
+      if (h < 0 || h >= g.H) continue;
+      for (int kw = 0; kw < g.K; ++kw) {
+        const int w = ow * g.S - g.P + kw;
+        if (w < 0 || w >= g.W) continue;
+        const float v = ld_bf(x + (((long)n * g.H + h) * g.W + w) * g.C + c);
+        if (v > best || (v != v && best == best)) {  // first max wins; NaN propagates like torch
+          best = v;
+          bi = kh * g.K + kw;
+        }
+      }
+    }
+    y[i] = f2bf_rne(best);
+    arg[i] = (uint8_t)bi;
+  }
+}
+
+__global__ void __launch_bounds__(256) k_maxpool_bwd(const bf16_t* __restrict__ dy, const uint8_t* __restrict__ arg,
+                                                     bf16_t* __restrict__ dx, PoolGeom g) {
+  const long total = (long)g.N * g.H * g.W * g.C;
+  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < total; i += (long)gridDim.x * 256) {
+    const int c = (int)(i % g.C);
+    const long p = i / g.C;
+    const int w = (int)(p % g.W), h = (int)((p / g.W) % g.H), n = (int)(p / ((long)g.W * g.H));
+    float s = 0.f;
+    for (int kh = 0; kh < g.K; ++kh) {
+      const int th = h + g.P - kh;
+      if (th < 0 || th % g.S) continue;
+      const int oh = th / g.S;
+      if (oh >= g.Ho) continue;
+      for (int kw = 0; kw < g.K; ++kw) {
+        const int tw = w + g.P - kw;
+        if (tw < 0 || tw % g.S) continue;
+        const int ow = tw / g.S;
+        if (ow >= g.Wo) continue;
+        const long o = (((long)n * g.Ho + oh) * g.Wo + ow) * g.C + c;
+        if (arg[o] == kh * g.K + kw) s += ld_bf(dy + o);
+      }
+    }
+    dx[i] = f2bf_rne(s);
+  }
+}
+
+// global average pool [N][HW][C] -> [N][C] (fp32 out) and its backward (broadcast / HW, bf16 out)
+__global__ void __launch_bounds__(256) k_avgpool_fwd(const bf16_t* __restrict__ x, float* __restrict__ y, int N,
+                                                     int HW, int C) {
+  const int c = blockIdx.x * 256 + threadIdx.x, n = blockIdx.y;
+  if (c >= C) return;
+  float s = 0.f;
+  for (int p = 0; p < HW; ++p) s += ld_bf(x + ((long)n * HW + p) * C + c);
+  y[(long)n * C + c] = s / HW;
+}
+__global__ void __launch_bounds__(256) k_avgpool_bwd(const float* __restrict__ dy, bf16_t* __restrict__ dx, int N,
+                                                     int HW, int C) {
+  const long total = (long)N * HW * C;
+  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < total; i += (long)gridDim.x * 256) {
+    const int c = (int)(i % C);
+    const long n = i / ((long)HW * C);
+    dx[i] = f2bf_rne(dy[n * C + c] / HW);
+  }
+}
+
+// ---------------------------------------------------------------------------------------------------------
+// Cross-entropy (mean over the batch): per-row loss and dlogits = (softmax - onehot) / B.  One wave per row.
+// ---------------------------------------------------------------------------------------------------------
+__global__ void __launch_bounds__(64) k_cross_entropy(const float* __restrict__ logits, const long* __restrict__ labels,
+                                                      float* __restrict__ loss, float* __restrict__ dlogits, int B,
+                                                      int K, float grad_scale) {
+  const int b = blockIdx.x, l = threadIdx.x;
+  const float* row = logits + (long)b * K;
+  float m = -INFINITY;
+  for (int k = l; k < K; k += 64) m = fmaxf(m, row[k]);
+  for (int o = 32; o; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
+  float s = 0.f;
+  for (int k = l; k < K; k += 64) s += __expf(row[k] - m);
+  for (int o = 32; o; o >>= 1) s += __shfl_xor(s, o);
+  long y = labels[b];
+  y = y < 0 ? 0 : (y >= K ? K - 1 : y);
+  const float lse = m + __logf(s);
+  if (l == 0) loss[b] = lse - row[y];
+  if (dlogits) {
+    const float inv = 1.f / s;
+    for (int k = l; k < K; k += 64)
+      dlogits[(long)b * K + k] = (__expf(row[k] - m) * inv - (k == y ? 1.f : 0.f)) * grad_scale;
+  }
+}
+
+// ---------------------------------------------------------------------------------------------------------
+// SGD over a flat fp32 buffer, torch.optim.SGD semantics: d = g + wd*p; buf = first ? d : mu*buf + d; p -= lr*buf
+// (mu == 0: no buffer).  `first` is a device flag (the step counter lives on the device: no host sync).
+// ---------------------------------------------------------------------------------------------------------
+__global__ void __launch_bounds__(256) k_sgd(float* __restrict__ p, const float* __restrict__ g, float* __restrict__ buf,
+                                             long n, float lr, float mu, float wd, int* __restrict__ first) {
+  const bool init = first ? *first != 0 : false;
+  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long)gridDim.x * 256) {
+    float d = g[i];
+    if (wd != 0.f) d += wd * p[i];
+    if (mu != 0.f) {
+      d = init ? d : mu * buf[i] + d;
+      buf[i] = d;
+    }
+    p[i] -= lr * d;
+  }
+}
+__global__ void k_clear_flag(int* f) { *f = 0; }
+
+// ---------------------------------------------------------------------------------------------------------
+// fp8 e4m3 (OCP) quantisation with a per-tensor scale computed on the device:
+//   amax = max |x|  (k_amax: per-block max, then atomicMax on the float bits -- non-negative floats order as
+//   unsigned ints);  q = sat(x * 448 / amax);  the GEMM multiplies by amax / 448 (inv scale) in its epilogue.
+// ---------------------------------------------------------------------------------------------------------
+template <typename T>
+__device__ __forceinline__ float ld_any(const T* p, long i);
+template <> __device__ __forceinline__ float ld_any<float>(const float* p, long i) { return p[i]; }
+template <> __device__ __forceinline__ float ld_any<bf16_t>(const bf16_t* p, long i) { return bf2f(p[i]); }
+
+template <typename T>
+__global__ void __launch_bounds__(256) k_amax(const T* __restrict__ x, long n, unsigned* __restrict__ amax_bits) {
+  __shared__ float red[256];
+  float m = 0.f;
+  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long)gridDim.x * 256) m = fmaxf(m, fabsf(ld_any(x, i)));
+  red[threadIdx.x] = m;
+  __syncthreads();
+  for (int o = 128; o; o >>= 1) {
+    if (threadIdx.x < o) red[threadIdx.x] = fmaxf(red[threadIdx.x], red[threadIdx.x + o]);
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) atomicMax(amax_bits, __float_as_uint(red[0]));
+}
+
+template <typename T>
+__global__ void __launch_bounds__(256) k_quant_fp8(const T* __restrict__ x, uint8_t* __restrict__ q, long n,
+                                                   const unsigned* __restrict__ amax_bits) {
+  const float amax = __uint_as_float(*amax_bits);
+  const float sc = amax > 0.f ? 448.f / amax : 1.f;
+  const long n4 = n >> 2;
+  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < n4; i += (long)gridDim.x * 256) {
+    float v[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) v[j] = fminf(fmaxf(ld_any(x, 4 * i + j) * sc, -448.f), 448.f);
+    int w = __builtin_amdgcn_cvt_pk_fp8_f32(v[0], v[1], 0, false);
+    w = __builtin_amdgcn_cvt_pk_fp8_f32(v[2], v[3], w, true);
+    ((int*)q)[i] = w;
+  }
+  for (long i = 4 * n4 + (long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long)gridDim.x * 256) {
+    const float v = fminf(fmaxf(ld_any(x, i) * sc, -448.f), 448.f);
+    q[i] = (uint8_t)(__builtin_amdgcn_cvt_pk_fp8_f32(v, 0.f, 0, false) & 0xff);
+  }
+}
+
+// alpha for an fp8 GEMM: (amax_a / 448) * (amax_b / 448) * extra  -> one float on the device
+__global__ void k_fp8_alpha(const unsigned* amax_a, const unsigned* amax_b, float extra, float* alpha) {
+  const float a = __uint_as_float(*amax_a), b = __uint_as_float(*amax_b);
+  *alpha = (a > 0.f ? a / 448.f : 1.f) * (b > 0.f ? b / 448.f : 1.f) * extra;
+}
+
+}  // namespace ops
+}  // namespace dca

@@ -1,0 +1,362 @@
+"""Autograd functions over the ops-layer HIP kernels (csrc/ops_*.hip).
+
+Activations are channels-last bf16 tensors ``[N, H, W, C]`` (contiguous); parameters stay fp32 in the module
+layout of torch (``Conv2d.weight [Cout, Cin, KH, KW]``, ``Linear.weight [out, in]``) so ``state_dict`` is the
+reference's.  GEMMs run on MFMA (bf16, or fp8 e4m3 for the forward when ``fp8=True``) with fp32 accumulation;
+BatchNorm statistics are fp32.
+
+Reference ops: conv2d K1/K4/K19/K22, BatchNorm2d + ReLU + residual K5-K7/K17/K18/K20,
+max_pool2d K3/K16, linear K9/K10/K13/K15, cross-entropy K11/K12, SGD K24.
+"""
+from __future__ import annotations
+
+import math
+from typing import Optional
+
+import torch
+
+from . import _native as N
+
+
+def _dev_check(*ts):
+    for t in ts:
+        if t is not None and not t.is_cuda:
+            raise ValueError("ops kernels need GPU tensors")
+
+
+# ------------------------------------------------------------------------------------------------------------
+# GEMM
+# ------------------------------------------------------------------------------------------------------------
+def gemm(a: torch.Tensor, b: torch.Tensor, *, ta: bool = False, tb: bool = False, bias: Optional[torch.Tensor] = None,
+         relu: bool = False, out_dtype=torch.float32, alpha: float = 1.0, out: Optional[torch.Tensor] = None,
+         beta: float = 0.0, splits: int = 0, alpha_dev: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """C[M,N] = alpha * A(m,k) B(n,k) (+bias) (+beta*out) (ReLU).
+
+    A is [M,K] (ta=False) or [K,M] (ta=True); B is [N,K] (tb=False) or [K,N] (tb=True).  bf16 operands, or
+    fp8 e4m3 stored as uint8 (both, K-contiguous).  splits=0 chooses split-K automatically."""
+    _dev_check(a, b, bias, out)
+    fp8 = a.dtype == torch.uint8
+    if fp8 != (b.dtype == torch.uint8) or (not fp8 and (a.dtype != torch.bfloat16 or b.dtype != torch.bfloat16)):
+        raise TypeError("gemm operands: both bf16 or both fp8 (uint8)")
+    if a.dim() != 2 or b.dim() != 2 or a.stride(1) != 1 or b.stride(1) != 1:
+        raise ValueError("gemm operands must be 2-D with unit inner stride")
+    M, K = (a.shape[1], a.shape[0]) if ta else (a.shape[0], a.shape[1])
+    Nn, Kb = (b.shape[1], b.shape[0]) if tb else (b.shape[0], b.shape[1])
+    if K != Kb:
+        raise ValueError(f"gemm: K mismatch {K} vs {Kb}")
+    if out is None:
+        out = torch.empty(M, Nn, dtype=out_dtype, device=a.device)
+    if out.dtype not in (torch.float32, torch.bfloat16) or out.shape != (M, Nn) or out.stride(1) != 1:
+        raise ValueError("gemm: bad output tensor")
+    if bias is not None and (bias.dtype != torch.float32 or bias.numel() != Nn):
+        raise ValueError("gemm: bias must be fp32 [N]")
+    tiles = math.ceil(M / 128) * math.ceil(Nn / 128)
+    if splits <= 0:
+        splits = 1
+        kt = 128 if fp8 else 64
+        if tiles < 256 and K >= 4 * kt:
+            splits = max(1, min(K // (2 * kt), 512 // tiles, 64))
+    ws = torch.empty(splits * M * Nn, dtype=torch.float32, device=a.device) if splits > 1 else None
+    args = N.GemmArgs(A=a.data_ptr(), B=b.data_ptr(), C=out.data_ptr(), bias=bias.data_ptr() if bias is not None else None,
+                      ws=ws.data_ptr() if ws is not None else None, M=M, N=Nn, K=K, lda=a.stride(0),
+                      ldb=b.stride(0), ldc=out.stride(0), alpha=float(alpha), beta=float(beta), ta=int(ta),
+                      tb=int(tb), fp8=int(fp8), relu=int(relu), out_bf16=int(out.dtype == torch.bfloat16),
+                      splits=splits, k_per_split=0,
+                      alpha_dev=alpha_dev.data_ptr() if alpha_dev is not None else None)
+    N.check(N.lib().dca_ops_gemm(args, N.stream(a.device)), "gemm")
+    return out
+
+
+def quantize_fp8(x: torch.Tensor):
+    """Per-tensor fp8 e4m3 quantisation on the device: (q uint8 same shape, amax bits int32 [1]).
+    q = sat(x * 448 / amax); dequantise with amax / 448."""
+    _dev_check(x)
+    x = x.contiguous()
+    q = torch.empty(x.shape, dtype=torch.uint8, device=x.device)
+    amax = torch.empty(1, dtype=torch.int32, device=x.device)
+    if x.dtype not in (torch.float32, torch.bfloat16):
+        raise TypeError("quantize_fp8: fp32 or bf16 input")
+    N.check(N.lib().dca_ops_quant_fp8(N.ptr(x), int(x.dtype == torch.float32), x.numel(), N.ptr(q), N.ptr(amax),
+                                      N.stream(x.device)), "quant_fp8")
+    return q, amax
+
+
+def fp8_alpha(amax_a: torch.Tensor, amax_b: torch.Tensor, extra: float = 1.0) -> torch.Tensor:
+    out = torch.empty(1, dtype=torch.float32, device=amax_a.device)
+    N.check(N.lib().dca_ops_fp8_alpha(N.ptr(amax_a), N.ptr(amax_b), float(extra), N.ptr(out), N.stream(amax_a.device)),
+            "fp8_alpha")
+    return out
+
+
+def amax_value(amax_bits: torch.Tensor) -> torch.Tensor:
+    return amax_bits.view(torch.float32)
+
+
+def _wgrad_splits(M: int, Nn: int, K: int) -> int:
+    """Split-K factor for a weight-gradient GEMM (K = pixels: long): ~512 workgroups, fp32 slab <= 64 MiB."""
+    tiles = math.ceil(M / 128) * math.ceil(Nn / 128)
+    return max(1, min(K // 256, max(1, 512 // tiles), 128, max(1, (16 << 20) // (M * Nn))))
+
+
+# ------------------------------------------------------------------------------------------------------------
+# Linear (x [B, in] bf16, w [out, in] fp32 master) -> fp32 or bf16
+# ------------------------------------------------------------------------------------------------------------
+class _Linear(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, w, b, relu, out_dtype, fp8):
+        xb = x.contiguous()
+        wb = w.to(torch.bfloat16).contiguous()
+        if fp8:
+            qx, ax = quantize_fp8(xb)
+            qw, aw = quantize_fp8(wb)
+            y = gemm(qx, qw, bias=b, relu=relu, out_dtype=out_dtype, alpha_dev=fp8_alpha(ax, aw))
+        else:
+            y = gemm(xb, wb, bias=b, relu=relu, out_dtype=out_dtype)
+        ctx.save_for_backward(xb, wb, y if relu else None)
+        ctx.relu, ctx.has_b = relu, b is not None
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        xb, wb, y = ctx.saved_tensors
+        if ctx.relu:
+            dy = dy * (y > 0)
+        dyb = dy.to(torch.bfloat16).contiguous()
+        dx = dw = db = None
+        if ctx.needs_input_grad[0]:
+            dx = gemm(dyb, wb, tb=True, out_dtype=torch.bfloat16)  # dX = dY . W
+        if ctx.needs_input_grad[1]:
+            M, Nn, K = wb.shape[0], wb.shape[1], xb.shape[0]
+            dw = gemm(dyb, xb, ta=True, tb=True, splits=_wgrad_splits(M, Nn, K))  # dW = dY^T . X (fp32)
+        if ctx.has_b and ctx.needs_input_grad[2]:
+            db = dy.float().sum(0)
+        return dx, dw, db, None, None, None
+
+
+def linear(x, w, b=None, relu=False, out_dtype=torch.float32, fp8=False):
+    return _Linear.apply(x, w, b, relu, out_dtype, fp8)
+
+
+# ------------------------------------------------------------------------------------------------------------
+# Conv2d, NHWC: im2col (or the input itself for 1x1/stride 1) + MFMA GEMM; bias and ReLU fused in the epilogue
+# ------------------------------------------------------------------------------------------------------------
+def _geom(x, w, stride, pad):
+    n, h, wd, c = x.shape
+    co, ci, kh, kw = w.shape
+    if ci != c:
+        raise ValueError(f"conv: input has {c} channels, weight expects {ci}")
+    ho, wo = (h + 2 * pad - kh) // stride + 1, (wd + 2 * pad - kw) // stride + 1
+    k = kh * kw * c
+    kp = (k + 7) // 8 * 8
+    return N.ConvGeom(N=n, H=h, W=wd, C=c, KH=kh, KW=kw, stride=stride, pad=pad, Ho=ho, Wo=wo, K=k, Kp=kp)
+
+
+def _weight_matrix(w: torch.Tensor, kp: int) -> torch.Tensor:
+    """[Cout, Cin, KH, KW] fp32 -> [Cout, Kp] bf16 with column k = (kh*KW + kw)*Cin + ci (zero padded)."""
+    co = w.shape[0]
+    m = w.permute(0, 2, 3, 1).reshape(co, -1)
+    if m.shape[1] != kp:
+        m = torch.nn.functional.pad(m, (0, kp - m.shape[1]))
+    return m.to(torch.bfloat16).contiguous()
+
+
+class _Conv2d(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, w, b, stride, pad, relu, fp8):
+        x = x.contiguous()
+        g = _geom(x, w, stride, pad)
+        direct = w.shape[2] == 1 and w.shape[3] == 1 and stride == 1 and pad == 0 and g.Kp == g.K
+        M = g.N * g.Ho * g.Wo
+        if direct:
+            cols = x.view(M, g.K)
+        else:
+            cols = torch.empty(M, g.Kp, dtype=torch.bfloat16, device=x.device)
+            N.check(N.lib().dca_ops_im2col(N.ptr(x), N.ptr(cols), g, N.stream(x.device)), "im2col")
+        wm = _weight_matrix(w, g.Kp)
+        if fp8 and g.Kp % 16 == 0:
+            qc, ac = quantize_fp8(cols)
+            qw, aw = quantize_fp8(wm)
+            y = gemm(qc, qw, bias=b, relu=relu, out_dtype=torch.bfloat16, alpha_dev=fp8_alpha(ac, aw))
+        else:
+            y = gemm(cols, wm, bias=b, relu=relu, out_dtype=torch.bfloat16)
+        y = y.view(g.N, g.Ho, g.Wo, w.shape[0])
+        ctx.save_for_backward(cols, wm, y if relu else None)
+        ctx.geom, ctx.direct, ctx.relu, ctx.has_b, ctx.wshape = g, direct, relu, b is not None, tuple(w.shape)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        cols, wm, y = ctx.saved_tensors
+        g = ctx.geom
+        co = ctx.wshape[0]
+        M = g.N * g.Ho * g.Wo
+        if ctx.relu:
+            dy = dy * (y > 0)
+        dyb = dy.to(torch.bfloat16).contiguous().view(M, co)
+        dx = dw = db = None
+        if ctx.needs_input_grad[0]:
+            dcols = gemm(dyb, wm, tb=True, out_dtype=torch.bfloat16)  # [M, Kp] = dY . Wm
+            if ctx.direct:
+                dx = dcols.view(g.N, g.H, g.W, g.C)
+            else:
+                dx = torch.empty(g.N, g.H, g.W, g.C, dtype=torch.bfloat16, device=dy.device)
+                N.check(N.lib().dca_ops_col2im(N.ptr(dcols), N.ptr(dx), g, N.stream(dy.device)), "col2im")
+        if ctx.needs_input_grad[1]:
+            dwm = gemm(dyb, cols, ta=True, tb=True, splits=_wgrad_splits(co, g.Kp, M))  # [Cout, Kp] fp32
+            kh, kw, ci = ctx.wshape[2], ctx.wshape[3], ctx.wshape[1]
+            dw = dwm[:, :g.K].reshape(co, kh, kw, ci).permute(0, 3, 1, 2).contiguous()
+        if ctx.has_b and ctx.needs_input_grad[2]:
+            db = dyb.float().sum(0)
+        return dx, dw, db, None, None, None, None
+
+
+def conv2d(x, w, b=None, stride=1, pad=0, relu=False, fp8=False):
+    """x: [N, H, W, Cin] bf16 (NHWC); w: [Cout, Cin, KH, KW] fp32 -> [N, Ho, Wo, Cout] bf16."""
+    return _Conv2d.apply(x, w, b, stride, pad, relu, fp8)
+
+
+# ------------------------------------------------------------------------------------------------------------
+# BatchNorm (train) + ReLU + residual, NHWC bf16.  res_mode 0: act(bn(x)); 1: act(bn(x)) + r; 2: act(bn(x) + r)
+# ------------------------------------------------------------------------------------------------------------
+class _BatchNormAct(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, r, gamma, beta, running_mean, running_var, eps, momentum, relu, res_mode):
+        x = x.contiguous()
+        C = x.shape[-1]
+        M = x.numel() // C
+        r = r.contiguous() if r is not None else None
+        out = torch.empty_like(x)
+        part = torch.empty((M + 255) // 256, C, 2, dtype=torch.float32, device=x.device)
+        stats = torch.empty(C, 2, dtype=torch.float32, device=x.device)
+        N.check(N.lib().dca_ops_bn_fwd(N.ptr(x), N.ptr(r), N.ptr(out), N.ptr(part), N.ptr(stats), N.ptr(gamma),
+                                       N.ptr(beta), N.ptr(running_mean), N.ptr(running_var), M, C, float(eps),
+                                       float(momentum), int(relu), int(res_mode), N.stream(x.device)), "bn_fwd")
+        ctx.save_for_backward(x, r, gamma, beta, stats)
+        ctx.relu, ctx.res_mode = relu, res_mode
+        return out
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, r, gamma, beta, stats = ctx.saved_tensors
+        dy = dy.to(torch.bfloat16).contiguous()
+        C = x.shape[-1]
+        M = x.numel() // C
+        part = torch.empty((M + 255) // 256, C, 2, dtype=torch.float32, device=x.device)
+        sums = torch.empty(C, 2, dtype=torch.float32, device=x.device)
+        dgamma = torch.empty(C, dtype=torch.float32, device=x.device)
+        dbeta = torch.empty_like(dgamma)
+        dx = torch.empty_like(x)
+        dr = torch.empty_like(x) if ctx.res_mode == 2 else None
+        N.check(N.lib().dca_ops_bn_bwd(N.ptr(dy), N.ptr(x), N.ptr(r), N.ptr(stats), N.ptr(gamma), N.ptr(beta),
+                                       N.ptr(part), N.ptr(sums), N.ptr(dgamma), N.ptr(dbeta), N.ptr(dx), N.ptr(dr),
+                                       M, C, int(ctx.relu), int(ctx.res_mode), 0, N.stream(x.device)), "bn_bwd")
+        if ctx.res_mode == 1:
+            dr = dy
+        return dx, dr, dgamma, dbeta, None, None, None, None, None, None
+
+
+def batch_norm_act(x, bn: torch.nn.BatchNorm2d, r=None, relu=True, res_mode=0):
+    """Training-mode BatchNorm2d `bn` over NHWC x (running stats updated in place; num_batches_tracked += 1)."""
+    if res_mode and r is None:
+        raise ValueError("batch_norm_act: residual mode needs r")
+    momentum = bn.momentum if bn.training and bn.track_running_stats else 0.0
+    if bn.training and bn.track_running_stats:
+        bn.num_batches_tracked.add_(1)
+    if not bn.training:
+        raise NotImplementedError("batch_norm_act implements training mode (eval uses torch)")
+    return _BatchNormAct.apply(x, r if res_mode else None, bn.weight, bn.bias, bn.running_mean, bn.running_var,
+                               bn.eps, momentum, relu, res_mode)
+
+
+# ------------------------------------------------------------------------------------------------------------
+# Pooling
+# ------------------------------------------------------------------------------------------------------------
+class _MaxPool(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, k, s, p):
+        x = x.contiguous()
+        n, h, w, c = x.shape
+        ho, wo = (h + 2 * p - k) // s + 1, (w + 2 * p - k) // s + 1
+        g = N.PoolGeom(N=n, H=h, W=w, C=c, K=k, S=s, P=p, Ho=ho, Wo=wo)
+        y = torch.empty(n, ho, wo, c, dtype=torch.bfloat16, device=x.device)
+        arg = torch.empty(n, ho, wo, c, dtype=torch.uint8, device=x.device)
+        N.check(N.lib().dca_ops_maxpool_fwd(N.ptr(x), N.ptr(y), N.ptr(arg), g, N.stream(x.device)), "maxpool_fwd")
+        ctx.save_for_backward(arg)
+        ctx.geom = g
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        (arg,) = ctx.saved_tensors
+        g = ctx.geom
+        dy = dy.to(torch.bfloat16).contiguous()
+        dx = torch.empty(g.N, g.H, g.W, g.C, dtype=torch.bfloat16, device=dy.device)
+        N.check(N.lib().dca_ops_maxpool_bwd(N.ptr(dy), N.ptr(arg), N.ptr(dx), g, N.stream(dy.device)), "maxpool_bwd")
+        return dx, None, None, None
+
+
+def max_pool2d(x, k=2, s=None, p=0):
+    return _MaxPool.apply(x, k, s or k, p)
+
+
+class _AvgPool(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x):
+        x = x.contiguous()
+        n, h, w, c = x.shape
+        y = torch.empty(n, c, dtype=torch.float32, device=x.device)
+        N.check(N.lib().dca_ops_avgpool_fwd(N.ptr(x), N.ptr(y), n, h * w, c, N.stream(x.device)), "avgpool_fwd")
+        ctx.shape = (n, h, w, c)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        n, h, w, c = ctx.shape
+        dy = dy.float().contiguous()
+        dx = torch.empty(n, h, w, c, dtype=torch.bfloat16, device=dy.device)
+        N.check(N.lib().dca_ops_avgpool_bwd(N.ptr(dy), N.ptr(dx), n, h * w, c, N.stream(dy.device)), "avgpool_bwd")
+        return dx
+
+
+def global_avg_pool(x):
+    """[N, H, W, C] bf16 -> [N, C] fp32 mean over H, W."""
+    return _AvgPool.apply(x)
+
+
+# ------------------------------------------------------------------------------------------------------------
+# Cross-entropy (mean) with the softmax gradient computed in the same kernel
+# ------------------------------------------------------------------------------------------------------------
+class _CrossEntropy(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, logits, labels):
+        logits = logits.float().contiguous()
+        B, K = logits.shape
+        loss = torch.empty(B, dtype=torch.float32, device=logits.device)
+        dl = torch.empty_like(logits) if logits.requires_grad else None
+        N.check(N.lib().dca_ops_cross_entropy(N.ptr(logits), N.ptr(labels.long().contiguous()), N.ptr(loss),
+                                              N.ptr(dl), B, K, 1.0 / B, N.stream(logits.device)), "cross_entropy")
+        ctx.save_for_backward(dl)
+        return loss.mean()
+
+    @staticmethod
+    def backward(ctx, g):
+        (dl,) = ctx.saved_tensors
+        return dl * g, None
+
+
+def cross_entropy(logits, labels):
+    return _CrossEntropy.apply(logits, labels)
+
+
+# ------------------------------------------------------------------------------------------------------------
+# SGD over flat fp32 buffers (torch.optim.SGD semantics incl. momentum's first-step buffer init)
+# ------------------------------------------------------------------------------------------------------------
+def sgd_step_(p: torch.Tensor, g: torch.Tensor, lr: float, momentum: float = 0.0, weight_decay: float = 0.0,
+              buf: Optional[torch.Tensor] = None, first: Optional[torch.Tensor] = None) -> None:
+    _dev_check(p, g, buf)
+    if p.dtype != torch.float32 or g.dtype != torch.float32 or not p.is_contiguous() or not g.is_contiguous():
+        raise TypeError("sgd_step_: contiguous fp32 buffers")
+    if momentum and buf is None:
+        raise ValueError("sgd_step_: momentum needs a buffer")
+    N.check(N.lib().dca_ops_sgd(N.ptr(p), N.ptr(g), N.ptr(buf), p.numel(), float(lr), float(momentum),
+                                float(weight_decay), N.ptr(first), N.stream(p.device)), "sgd")

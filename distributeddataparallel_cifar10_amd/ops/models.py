@@ -1,0 +1,70 @@
+"""Model forwards on the ops layer (HIP kernels for every layer), sharing the parameters of the torch modules.
+
+``OpsModel(model)`` wraps a ``NetResDeep`` (reference ``model/resnet.py``) or a ResNet (``models/resnet50.py``)
+without copying anything: the wrapped module's ``nn.Parameter``s and BN buffers are the ones the kernels read
+and the optimizer updates, so ``state_dict()`` is unchanged.  The forward takes the usual NCHW fp32 batch,
+switches to channels-last bf16 once, and runs:
+
+* NetResDeep (reference ``model/resnet.py:15-37``): conv1 + bias + ReLU fused in the GEMM epilogue -> 2x2 max
+  pool -> 10 x [3x3 conv (im2col + MFMA GEMM) -> BN + ReLU + skip fused (res_mode 1)] -> max pool -> fc1 + ReLU
+  -> fc2 (fp32 logits).  fc1's columns are permuted from the reference's NCHW flatten order to NHWC.
+* ResNet-50/101: stem 7x7/2 conv -> BN + ReLU -> 3x3/2 max pool -> bottlenecks (1x1, 3x3, 1x1 convs, each BN
+  fused with its ReLU; the last one with the residual add before the ReLU, res_mode 2) -> global average pool
+  -> fc.  With ``fp8=True`` the 1x1 convolutions and fc run their forward GEMM in fp8 e4m3 (per-tensor scales
+  from a device-side amax; the MX-scaled MFMA at the fp8 rate); gradients stay bf16 (BASELINE config 5).
+"""
+from __future__ import annotations
+
+import torch
+import torch.nn as nn
+
+from . import functional as F
+
+
+def _is_netresdeep(m: nn.Module) -> bool:
+    return hasattr(m, "resblocks") and hasattr(m, "fc1") and hasattr(m, "fc2")
+
+
+class OpsModel(nn.Module):
+    def __init__(self, model: nn.Module, fp8: bool = False):
+        super().__init__()
+        self.module = model
+        self.fp8 = fp8
+        self.kind = "netresdeep" if _is_netresdeep(model) else "resnet"
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        h = x.permute(0, 2, 3, 1).to(torch.bfloat16).contiguous()  # NCHW fp32 -> NHWC bf16
+        return self._netresdeep(h) if self.kind == "netresdeep" else self._resnet(h)
+
+    # reference model/resnet.py:15-22, 33-37
+    def _netresdeep(self, h):
+        m = self.module
+        h = F.conv2d(h, m.conv1.weight, m.conv1.bias, stride=1, pad=1, relu=True)
+        h = F.max_pool2d(h, 2)
+        for blk in m.resblocks:
+            y = F.conv2d(h, blk.conv.weight, None, stride=1, pad=1)
+            h = F.batch_norm_act(y, blk.batch_norm, r=h, relu=True, res_mode=1)  # relu(bn(conv(x))) + x
+        h = F.max_pool2d(h, 2)
+        n, hh, ww, c = h.shape
+        flat = h.reshape(n, hh * ww * c)
+        w1 = m.fc1.weight.view(-1, c, hh, ww).permute(0, 2, 3, 1).reshape(m.fc1.weight.shape[0], -1)
+        z = F.linear(flat, w1, m.fc1.bias, relu=True, out_dtype=torch.bfloat16)
+        return F.linear(z, m.fc2.weight, m.fc2.bias, out_dtype=torch.float32)
+
+    def _conv_bn(self, h, conv, bn, relu=True, r=None):
+        one = conv.kernel_size == (1, 1)
+        y = F.conv2d(h, conv.weight, conv.bias, stride=conv.stride[0], pad=conv.padding[0], fp8=self.fp8 and one)
+        return F.batch_norm_act(y, bn, r=r, relu=relu, res_mode=2 if r is not None else 0)
+
+    def _resnet(self, h):
+        m = self.module
+        h = self._conv_bn(h, m.conv1, m.bn1)
+        h = F.max_pool2d(h, 3, 2, 1)
+        for stage in (m.layer1, m.layer2, m.layer3, m.layer4):
+            for b in stage:
+                idt = h if b.downsample is None else self._conv_bn(h, b.downsample[0], b.downsample[1], relu=False)
+                out = self._conv_bn(h, b.conv1, b.bn1)
+                out = self._conv_bn(out, b.conv2, b.bn2)
+                h = self._conv_bn(out, b.conv3, b.bn3, relu=True, r=idt)  # relu(bn3(conv3) + identity)
+        feat = F.global_avg_pool(h)
+        return F.linear(feat.to(torch.bfloat16), m.fc.weight, m.fc.bias, out_dtype=torch.float32, fp8=self.fp8)

@@ -186,6 +186,14 @@ class FlatSGD(torch.optim.Optimizer):
     def step(self, closure=None):
         loss = closure() if closure is not None else None
         g = self.param_groups[0]
+        if self.ddp.flat.is_cuda:  # one HIP kernel over the flat buffer (ops/functional.py sgd_step_)
+            from ..ops.functional import sgd_step_
+            if g["momentum"] and self._buf is None:
+                self._buf = torch.empty_like(self.ddp.flat)
+                self._first = torch.ones(1, dtype=torch.int32, device=self.ddp.flat.device)
+            sgd_step_(self.ddp.flat, self.ddp.flat_grad, g["lr"], g["momentum"], g["weight_decay"], buf=self._buf,
+                      first=getattr(self, "_first", None))
+            return loss
         grad = self.ddp.flat_grad
         if g["weight_decay"]:
             grad = grad.add(self.ddp.flat, alpha=g["weight_decay"])

@@ -9,6 +9,8 @@ the same stdout lines -- while the step itself runs on the MI355X-native path:
   all-reduce -- one-shot xGMI peer reads or RCCL --, SGD, BN running stats) is ONE hipGraph replay of the native engine; the dataset is
   device-resident; the loss is accumulated on the device and read once per epoch (reference ``loss.item()``
   every step, SURVEY.md Q9: same printed value, no per-step host sync).
+* ``engine="ops"``: the framework's general HIP layer kernels (``ops/``: MFMA GEMM convolutions, fused
+  BN + ReLU + residual, fused cross-entropy, HIP SGD; fp8 forward GEMMs with ``fp8``) + ``FlatBucketDDP``.
 * ``engine="torch"``: stock PyTorch ops + ``FlatBucketDDP`` (generic path; CPU / gloo; any model).
 
 Options beyond the reference (all off by default): max_steps (per epoch), synthetic data, resume, metrics JSON,
@@ -57,6 +59,7 @@ class TrainConfig:
     profile: Optional[str] = None    # directory for torch.profiler traces / kernel summary
     check_sync: int = 0              # >0: assert cross-rank parameter equality every N epochs (and at start)
     allreduce: str = "auto"          # fused engine gradient all-reduce: auto | xgmi (one-shot P2P) | rccl
+    fp8: bool = False                # ops engine: fp8 e4m3 forward GEMMs for 1x1 convs / fc (ResNet family)
     extra: dict = field(default_factory=dict)
 
 
@@ -68,7 +71,10 @@ def add_cli_args(ap: argparse.ArgumentParser, batch_default: int = 32) -> argpar
     ap.add_argument("--data-root", default=None)
     ap.add_argument("--synthetic", type=int, nargs="?", const=50000, default=0,
                     help="train on N synthetic CIFAR-shaped samples (default 50000)")
-    ap.add_argument("--engine", default="auto", choices=["auto", "fused", "torch"])
+    ap.add_argument("--engine", default="auto", choices=["auto", "fused", "ops", "torch"],
+                    help="fused: NetResDeep native engine; ops: the framework's HIP layer kernels (any supported "
+                         "model) + FlatBucketDDP; torch: stock PyTorch ops + FlatBucketDDP")
+    ap.add_argument("--fp8", action="store_true", help="ops engine: fp8 e4m3 forward GEMMs (1x1 convs, fc)")
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
     ap.add_argument("--no-checkpoint", action="store_true")
     ap.add_argument("--checkpoint-path", default=None)
@@ -97,7 +103,7 @@ def config_from_args(a: argparse.Namespace, data_path_default: str) -> TrainConf
                        checkpoint=not a.no_checkpoint, checkpoint_path=a.checkpoint_path, resume=a.resume,
                        metrics_json=a.metrics_json, seed=a.seed, set_epoch=a.set_epoch, fail_at_step=a.fail_at_step,
                        backend=a.backend, port=a.port, timeout_s=a.timeout, model=a.model, bucket_mb=a.bucket_mb,
-                       profile=a.profile, check_sync=a.check_sync, allreduce=a.allreduce)
+                       profile=a.profile, check_sync=a.check_sync, allreduce=a.allreduce, fp8=a.fp8)
 
 
 def load_dataset(cfg: TrainConfig):
@@ -134,8 +140,12 @@ def train_loop(model, train_loader: DeviceLoader, rank: int, cfg: Optional[Train
     start_epoch = int(cfg.extra.get("start_epoch", 1))
     global_step = int(cfg.extra.get("start_step", 0))
     history = []
+    from .ops.models import OpsModel
+    on_ops = isinstance(getattr(model, "module", None), OpsModel)
     if not fused:
         loss_fn = nn.CrossEntropyLoss()
+        if on_ops:
+            from .ops.functional import cross_entropy as loss_fn
         if optimizer is None:
             from .parallel.flat_ddp import FlatBucketDDP, FlatSGD
             optimizer = FlatSGD(model, cfg.lr) if isinstance(model, FlatBucketDDP) else \
@@ -143,7 +153,7 @@ def train_loop(model, train_loader: DeviceLoader, rank: int, cfg: Optional[Train
     from contextlib import ExitStack
     from torch.profiler import record_function
     from .parallel.dist import assert_params_in_sync
-    autocast = (not fused and cfg.dtype == "bf16" and train_loader.device.type == "cuda"
+    autocast = (not fused and not on_ops and cfg.dtype == "bf16" and train_loader.device.type == "cuda"
                 and not _is_netresdeep(unwrap(model)))  # generic models train in bf16; NetResDeep torch path = fp32
     if cfg.check_sync:
         assert_params_in_sync(unwrap(model))
@@ -235,6 +245,11 @@ def build_model_for_rank(cfg: TrainConfig, rank: int, world_size: int, device: t
             cfg.extra["start_epoch"] = int(meta.get("epoch", 0)) + 1
             cfg.extra["start_step"] = int(meta.get("step", 0))
     kind = resolve_engine(cfg, device, model)
+    if kind == "ops":
+        from .ops.models import OpsModel
+        if device.type != "cuda":
+            raise ValueError("--engine ops runs the HIP kernels: it needs a GPU")
+        return FlatBucketDDP(OpsModel(model, fp8=cfg.fp8), bucket_cap_mb=cfg.bucket_mb)
     if kind == "fused":
         n_idx = len(loader) * loader.batch_size
         return FusedDDPTrainer(model, loader.data, loader.labels, batch_max=loader.batch_size, lr=cfg.lr,

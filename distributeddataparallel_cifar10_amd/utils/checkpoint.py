@@ -25,8 +25,11 @@ CHECKPOINT_NAME = "birds_vs_airplanes.pt"
 
 
 def unwrap(model: nn.Module) -> nn.Module:
-    """``model.module`` for DDP-style wrappers (reference main.py:45 strips the prefix the same way)."""
-    return getattr(model, "module", model)
+    """The innermost ``.module`` of DDP-style wrappers (FlatBucketDDP, ops.OpsModel, FusedDDPTrainer; reference
+    main.py:45 strips the ``module.`` prefix the same way)."""
+    while hasattr(model, "module") and isinstance(getattr(model, "module"), nn.Module):
+        model = model.module
+    return model
 
 
 def export_state_dict(model: nn.Module) -> dict:

@@ -79,3 +79,37 @@ def test_code_object_targets_gfx950():
     # the fat binary embeds the offload bundle id "hipv4-amdgcn-amd-amdhsa--gfx950"
     blob = open(nbuild.lib_path(), "rb").read()
     assert b"amdgcn-amd-amdhsa--gfx950" in blob
+
+
+def test_ops_library_builds_and_exports():
+    """The ops layer's library (csrc/ops_api.hip) cross-compiles for gfx950 and exports its C ABI."""
+    path = nbuild.build(variant="ops")
+    lib = ctypes.CDLL(path, mode=ctypes.RTLD_GLOBAL)
+    lib.dca_ops_abi_version.restype = ctypes.c_int
+    from distributeddataparallel_cifar10_amd.ops import _native
+    assert lib.dca_ops_abi_version() == _native.ABI_VERSION
+    for sym in ("dca_ops_gemm", "dca_ops_im2col", "dca_ops_col2im", "dca_ops_bn_fwd", "dca_ops_bn_bwd",
+                "dca_ops_maxpool_fwd", "dca_ops_maxpool_bwd", "dca_ops_avgpool_fwd", "dca_ops_avgpool_bwd",
+                "dca_ops_cross_entropy", "dca_ops_sgd", "dca_ops_quant_fp8", "dca_ops_fp8_alpha"):
+        assert hasattr(lib, sym), sym
+    assert b"amdgcn-amd-amdhsa--gfx950" in open(path, "rb").read()
+
+
+def test_ops_gemm_args_mirror_matches_header():
+    """ops/_native.py GemmArgs lists the fields of csrc/ops_gemm.hip GemmArgs in the same order."""
+    src = open(os.path.join(nbuild.CSRC, "ops_gemm.hip")).read()
+    body = src[src.index("struct GemmArgs {"):src.index("};", src.index("struct GemmArgs {"))]
+    names = []
+    for line in body.splitlines()[1:]:
+        decl = line.split("//")[0].strip().rstrip(";")
+        if decl:
+            names += [n.strip() for n in re.sub(r"^(const\s+)?\w+\s*\**\s*", "", decl).split(",")]
+    from distributeddataparallel_cifar10_amd.ops._native import GemmArgs
+    assert [f[0] for f in GemmArgs._fields_] == [n.strip() for n in names]
+
+
+def test_ops_reject_cpu_tensors():
+    import pytest
+    from distributeddataparallel_cifar10_amd import ops
+    with pytest.raises(ValueError):
+        ops.gemm(torch.zeros(4, 8, dtype=torch.bfloat16), torch.zeros(4, 8, dtype=torch.bfloat16))

@@ -1,0 +1,282 @@
+"""Unit tests of the ops-layer HIP kernels (csrc/ops_*.hip) against plain PyTorch fp32 references of the same op
+(layer 1: one test family per kernel family, random + ragged shapes, asymmetric operands)."""
+import pytest
+import torch
+import torch.nn.functional as TF
+
+pytestmark = pytest.mark.gpu
+
+
+def _rel(a, b):
+    a, b = a.double(), b.double()
+    return ((a - b).norm() / b.norm().clamp_min(1e-30)).item()
+
+
+def _bf(x):
+    return x.to(torch.bfloat16)
+
+
+@pytest.mark.parametrize("M,N,K,ta,tb", [(256, 128, 64, 0, 0), (300, 200, 136, 0, 0), (77, 10, 32, 0, 0),
+                                         (130, 96, 200, 0, 1), (64, 48, 1000, 1, 1), (10, 32, 37, 1, 1),
+                                         (512, 256, 4096, 0, 0)])
+def test_gemm_bf16(gpu, M, N, K, ta, tb):
+    from distributeddataparallel_cifar10_amd.ops import gemm
+    g = torch.Generator(device=gpu).manual_seed(M * 7 + N)
+    a = torch.randn(M, K, device=gpu, generator=g)
+    b = torch.randn(N, K, device=gpu, generator=g) * torch.linspace(0.5, 2.0, K, device=gpu)  # asymmetric B
+    bias = torch.randn(N, device=gpu, generator=g)
+    A = _bf(a.t().contiguous() if ta else a)
+    B = _bf(b.t().contiguous() if tb else b)
+    ref = _bf(a).float() @ _bf(b).float().t() + bias
+    out = gemm(A, B, ta=bool(ta), tb=bool(tb), bias=bias)
+    assert _rel(out, ref) < 1e-5, _rel(out, ref)
+    out2 = gemm(A, B, ta=bool(ta), tb=bool(tb), bias=bias, relu=True, out_dtype=torch.bfloat16, splits=3)
+    assert _rel(out2.float(), ref.clamp_min(0)) < 1e-2
+
+
+def test_gemm_identity_layout(gpu):
+    """A = I with an asymmetric B must return B^T exactly (catches row/col swaps in the C write)."""
+    from distributeddataparallel_cifar10_amd.ops import gemm
+    n = 64
+    a = torch.eye(n, device=gpu, dtype=torch.bfloat16)
+    b = torch.arange(n * n, device=gpu, dtype=torch.float32).remainder(97).view(n, n).to(torch.bfloat16)
+    out = gemm(a, b)  # C[m, n] = sum_k I[m,k] B[n,k] = B[n, m]
+    assert torch.equal(out, b.float().t())
+
+
+def test_gemm_fp8_exact_integers(gpu):
+    """fp8 e4m3 operands holding small integers (exactly representable) give exact products."""
+    from distributeddataparallel_cifar10_amd.ops import gemm
+    M, N, K = 160, 144, 256
+    g = torch.Generator(device=gpu).manual_seed(3)
+    a = torch.randint(-4, 5, (M, K), device=gpu, generator=g).float()
+    b = torch.randint(-4, 5, (N, K), device=gpu, generator=g).float()
+    qa = a.to(torch.float8_e4m3fn).view(torch.uint8)
+    qb = b.to(torch.float8_e4m3fn).view(torch.uint8)
+    out = gemm(qa, qb)
+    assert torch.equal(out, a @ b.t())
+
+
+def test_quantize_fp8_and_scaled_gemm(gpu):
+    from distributeddataparallel_cifar10_amd.ops import fp8_alpha, gemm, quantize_fp8
+    g = torch.Generator(device=gpu).manual_seed(4)
+    x = torch.randn(512, 256, device=gpu, generator=g)
+    w = torch.randn(384, 256, device=gpu, generator=g) * 0.05
+    qx, ax = quantize_fp8(_bf(x))
+    qw, aw = quantize_fp8(w)
+    amax = ax.view(torch.float32).item()
+    assert abs(amax - _bf(x).float().abs().max().item()) < 1e-6
+    deq = qx.view(torch.float8_e4m3fn).float() * amax / 448.0
+    assert _rel(deq, _bf(x).float()) < 0.05
+    out = gemm(qx, qw, alpha_dev=fp8_alpha(ax, aw))
+    assert _rel(out, x @ w.t()) < 0.06
+
+
+@pytest.mark.parametrize("n,h,c,co,k,s,p,bias", [(2, 16, 32, 32, 3, 1, 1, False), (3, 32, 3, 32, 3, 1, 1, True),
+                                                  (2, 14, 16, 24, 7, 2, 3, False), (2, 9, 64, 48, 1, 2, 0, False),
+                                                  (4, 8, 64, 128, 1, 1, 0, False)])
+def test_conv2d_fwd_bwd(gpu, n, h, c, co, k, s, p, bias):
+    from distributeddataparallel_cifar10_amd.ops import conv2d
+    g = torch.Generator(device=gpu).manual_seed(n * h + c)
+    x = _bf(torch.randn(n, h, h, c, device=gpu, generator=g)).requires_grad_()
+    w = (torch.randn(co, c, k, k, device=gpu, generator=g) * 0.2).requires_grad_()
+    b = torch.randn(co, device=gpu, generator=g).requires_grad_() if bias else None
+    y = conv2d(x, w, b, stride=s, pad=p)
+    dy = torch.randn(y.shape, device=gpu, generator=g)
+    y.backward(_bf(dy))
+    xr = x.detach().float().permute(0, 3, 1, 2).requires_grad_()
+    wr = _bf(w.detach()).float().requires_grad_()
+    br = b.detach().clone().requires_grad_() if bias else None
+    yr = TF.conv2d(xr, wr, br, stride=s, padding=p)
+    yr.backward(_bf(dy).float().permute(0, 3, 1, 2))
+    assert _rel(y.float().permute(0, 3, 1, 2), yr) < 1e-2
+    assert _rel(x.grad.float().permute(0, 3, 1, 2), xr.grad) < 2e-2
+    assert _rel(w.grad, wr.grad) < 1e-2
+    if bias:
+        assert _rel(b.grad, br.grad) < 1e-2
+
+
+@pytest.mark.parametrize("res_mode,relu", [(0, True), (1, True), (2, True), (0, False)])
+def test_batch_norm_act(gpu, res_mode, relu):
+    from distributeddataparallel_cifar10_amd.ops import batch_norm_act
+    g = torch.Generator(device=gpu).manual_seed(res_mode * 2 + relu)
+    n, h, c = 4, 12, 48
+    x = _bf(torch.randn(n, h, h, c, device=gpu, generator=g) * 2 + 0.5).requires_grad_()
+    r = _bf(torch.randn(n, h, h, c, device=gpu, generator=g)).requires_grad_() if res_mode else None
+    bn = torch.nn.BatchNorm2d(c).to(gpu)
+    with torch.no_grad():
+        bn.weight.uniform_(0.5, 1.5)
+        bn.bias.uniform_(-0.2, 0.2)
+    ref_bn = torch.nn.BatchNorm2d(c).to(gpu)
+    ref_bn.load_state_dict(bn.state_dict())
+    y = batch_norm_act(x, bn, r=r, relu=relu, res_mode=res_mode)
+    dy = torch.randn(y.shape, device=gpu, generator=g)
+    y.backward(_bf(dy))
+    xr = x.detach().float().permute(0, 3, 1, 2).requires_grad_()
+    rr = r.detach().float().permute(0, 3, 1, 2).requires_grad_() if res_mode else None
+    z = ref_bn(xr)
+    if res_mode == 2:
+        z = z + rr
+    if relu:
+        z = torch.relu(z)
+    if res_mode == 1:
+        z = z + rr
+    z.backward(_bf(dy).float().permute(0, 3, 1, 2))
+    assert _rel(y.float().permute(0, 3, 1, 2), z) < 1e-2
+    assert _rel(x.grad.float().permute(0, 3, 1, 2), xr.grad) < 2e-2
+    assert _rel(bn.weight.grad, ref_bn.weight.grad) < 1e-3
+    assert _rel(bn.bias.grad, ref_bn.bias.grad) < 1e-3
+    if res_mode:
+        assert _rel(r.grad.float().permute(0, 3, 1, 2), rr.grad) < 1e-2
+    assert _rel(bn.running_mean, ref_bn.running_mean) < 1e-5
+    assert _rel(bn.running_var, ref_bn.running_var) < 1e-5
+    assert int(bn.num_batches_tracked) == int(ref_bn.num_batches_tracked) == 1
+
+
+@pytest.mark.parametrize("k,s,p,h", [(2, 2, 0, 16), (3, 2, 1, 15), (2, 2, 0, 7)])
+def test_max_pool(gpu, k, s, p, h):
+    from distributeddataparallel_cifar10_amd.ops import max_pool2d
+    g = torch.Generator(device=gpu).manual_seed(k + h)
+    x = _bf(torch.randn(2, h, h, 24, device=gpu, generator=g)).requires_grad_()
+    y = max_pool2d(x, k, s, p)
+    dy = _bf(torch.randn(y.shape, device=gpu, generator=g))
+    y.backward(dy)
+    xr = x.detach().float().permute(0, 3, 1, 2).requires_grad_()
+    yr = TF.max_pool2d(xr, k, s, p)
+    yr.backward(dy.float().permute(0, 3, 1, 2))
+    assert torch.equal(y.float().permute(0, 3, 1, 2), yr)
+    assert _rel(x.grad.float().permute(0, 3, 1, 2), xr.grad) < 1e-2
+
+
+def test_avg_pool_and_cross_entropy(gpu):
+    from distributeddataparallel_cifar10_amd.ops import cross_entropy, global_avg_pool
+    g = torch.Generator(device=gpu).manual_seed(9)
+    x = _bf(torch.randn(5, 7, 7, 40, device=gpu, generator=g)).requires_grad_()
+    y = global_avg_pool(x)
+    y.backward(torch.ones_like(y))
+    assert _rel(y, x.detach().float().mean((1, 2))) < 1e-5
+    assert _rel(x.grad.float(), torch.full_like(x.grad.float(), 1 / 49)) < 1e-2
+    logits = (torch.randn(33, 1000, device=gpu, generator=g) * 3).requires_grad_()
+    labels = torch.randint(0, 1000, (33,), device=gpu, generator=g)
+    loss = cross_entropy(logits, labels)
+    loss.backward()
+    lr_ = logits.detach().clone().requires_grad_()
+    ref = TF.cross_entropy(lr_, labels)
+    ref.backward()
+    assert abs(loss.item() - ref.item()) < 1e-4
+    assert _rel(logits.grad, lr_.grad) < 1e-4
+
+
+@pytest.mark.parametrize("mu,wd", [(0.0, 0.0), (0.9, 1e-4)])
+def test_sgd(gpu, mu, wd):
+    from distributeddataparallel_cifar10_amd.ops import sgd_step_
+    g = torch.Generator(device=gpu).manual_seed(11)
+    p0 = torch.randn(10001, device=gpu, generator=g)
+    ref = p0.clone().requires_grad_()
+    opt = torch.optim.SGD([ref], lr=0.05, momentum=mu, weight_decay=wd)
+    p = p0.clone()
+    buf = torch.zeros_like(p) if mu else None
+    first = torch.ones(1, dtype=torch.int32, device=gpu)
+    for _ in range(3):
+        grad = torch.randn(10001, device=gpu, generator=g)
+        ref.grad = grad.clone()
+        opt.step()
+        sgd_step_(p, grad, 0.05, mu, wd, buf=buf, first=first)
+    assert _rel(p, ref.detach()) < 1e-6
+
+
+@pytest.mark.parametrize("fp8", [False, True])
+def test_ops_resnet_step(gpu, fp8):
+    """A ResNet-50-structured net (reduced depth for test time) trains one step on the ops path.  Loss and every
+    parameter gradient are compared with stock PyTorch fp32; the tolerance is set by stock PyTorch's own bf16
+    autocast error on the same step (the ops path must be within 2x of it, +0.02; fp8 forward: 3x, +0.05)."""
+    import copy
+    from distributeddataparallel_cifar10_amd.models.resnet50 import ResNet
+    from distributeddataparallel_cifar10_amd.ops import OpsModel, cross_entropy
+    torch.manual_seed(0)
+    net = ResNet([1, 1, 1, 1], num_classes=10, zero_init_residual=False).to(gpu)
+    ref = copy.deepcopy(net)
+    amp = copy.deepcopy(net)
+    x = torch.randn(8, 3, 128, 128, device=gpu)
+    y = torch.randint(0, 10, (8,), device=gpu)
+    loss = cross_entropy(OpsModel(net, fp8=fp8)(x), y)
+    loss.backward()
+    lref = TF.cross_entropy(ref(x), y)
+    lref.backward()
+    with torch.autocast("cuda", dtype=torch.bfloat16):
+        lamp = TF.cross_entropy(amp(x), y)
+    lamp.backward()
+    k, c = (3.0, 0.12) if fp8 else (2.0, 0.02)
+    assert abs(loss.item() - lref.item()) <= k * abs(lamp.item() - lref.item()) + c * max(1.0, lref.item())
+    rows = []
+    for (n, p), (_, q), (_, r) in zip(net.named_parameters(), ref.named_parameters(), amp.named_parameters()):
+        assert p.grad is not None, n
+        rows.append((n, _rel(p.grad, q.grad), _rel(r.grad, q.grad)))
+    print("\n".join(f"{n:40s} ops {e:.4f}  autocast {a:.4f}" for n, e, a in rows))
+    # fp8 forward noise is amplified through the (chaotic, random-init) backward: compare fp8 only near the head,
+    # where the gradient is still a function of the forward it perturbs; bf16 is compared everywhere.
+    checked = rows if not fp8 else [r for r in rows if r[0].startswith(("fc.", "layer4.0.bn3", "layer4.0.downsample.1"))]
+    bad = [(n, e, a) for n, e, a in checked if e > k * a + c]
+    assert not bad, bad
+
+
+@pytest.mark.parametrize("fp8", [False, True])
+def test_ops_resnet_trains(gpu, fp8):
+    """20 SGD steps on one fixed batch through the ops path (FlatBucketDDP + HIP SGD with momentum) fit it."""
+    from distributeddataparallel_cifar10_amd.models.resnet50 import ResNet
+    from distributeddataparallel_cifar10_amd.ops import OpsModel, cross_entropy
+    from distributeddataparallel_cifar10_amd.parallel.flat_ddp import FlatBucketDDP, FlatSGD
+    torch.manual_seed(1)
+    net = OpsModel(ResNet([1, 1, 1, 1], num_classes=10).to(gpu), fp8=fp8)
+    ddp = FlatBucketDDP(net)
+    opt = FlatSGD(ddp, lr=0.05, momentum=0.9)
+    x = torch.randn(16, 3, 64, 64, device=gpu)
+    y = torch.randint(0, 10, (16,), device=gpu)
+    losses = []
+    for _ in range(20):
+        loss = cross_entropy(ddp(x), y)
+        opt.zero_grad()
+        loss.backward()
+        opt.step()
+        losses.append(loss.item())
+    assert all(torch.isfinite(torch.tensor(losses)))
+    assert losses[-1] < 0.5 * losses[0], losses
+
+
+def test_ops_netresdeep_step(gpu):
+    """NetResDeep (reference model/resnet.py) on the ops path: loss and all 9 gradients vs stock fp32 PyTorch,
+    within 2x stock bf16 autocast's own error (+0.02); BN running stats updated 10x per forward."""
+    import copy
+    from distributeddataparallel_cifar10_amd.models.netresdeep import NetResDeep
+    from distributeddataparallel_cifar10_amd.ops import OpsModel, cross_entropy
+    torch.manual_seed(0)
+    net = NetResDeep().to(gpu)
+    ref, amp = copy.deepcopy(net), copy.deepcopy(net)
+    x = torch.randn(32, 3, 32, 32, device=gpu)
+    y = torch.randint(0, 10, (32,), device=gpu)
+    loss = cross_entropy(OpsModel(net)(x), y)
+    loss.backward()
+    lref = TF.cross_entropy(ref(x), y)
+    lref.backward()
+    with torch.autocast("cuda", dtype=torch.bfloat16):
+        lamp = TF.cross_entropy(amp(x), y)
+    lamp.backward()
+    assert abs(loss.item() - lref.item()) <= 2 * abs(lamp.item() - lref.item()) + 0.02
+    for (n, p), (_, q), (_, r) in zip(net.named_parameters(), ref.named_parameters(), amp.named_parameters()):
+        e, a = _rel(p.grad, q.grad), _rel(r.grad, q.grad)
+        assert e <= 2 * a + 0.02, (n, e, a)
+    bn, rbn = net.resblocks[0].batch_norm, ref.resblocks[0].batch_norm
+    assert int(bn.num_batches_tracked) == int(rbn.num_batches_tracked) == 10
+    assert _rel(bn.running_mean, rbn.running_mean) < 2e-2 and _rel(bn.running_var, rbn.running_var) < 2e-2
+
+
+def test_main_no_ddp_ops_engine(gpu, tmp_path):
+    """main_no_ddp.py --engine ops trains NetResDeep on the HIP layer kernels (reference output lines)."""
+    import subprocess
+    import sys
+    import os
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([sys.executable, "main_no_ddp.py", "--synthetic", "512", "--epochs", "1", "--engine", "ops"],
+                       cwd=root, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    assert "Epoch 1, Training loss" in r.stdout and "training time:" in r.stdout
