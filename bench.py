@@ -51,11 +51,18 @@ def main() -> int:
         if world == 1 and a.gpus > 1:
             print(f"bench.py: --gpus {a.gpus} needs torch.distributed.run with {a.gpus} processes", file=sys.stderr)
             return 2
-    torch.cuda.set_device(local_rank)
-    dev = torch.device("cuda", local_rank)
+    # Rehearsal hook (tests / 1-GPU boxes): DCA_BENCH_SHARE_GPU=1 puts every rank on GPU 0 with a gloo process
+    # group (RCCL refuses two ranks per device); the gradient all-reduce is still the engine's xGMI path.
+    share = os.environ.get("DCA_BENCH_SHARE_GPU") == "1"
+    dev_index = 0 if share else local_rank
+    torch.cuda.set_device(dev_index)
+    dev = torch.device("cuda", dev_index)
     os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
     os.environ.setdefault("MASTER_PORT", "29511")
-    dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
+    if share:
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+    else:
+        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
 
     from model.resnet import NetResDeep
     from distributeddataparallel_cifar10_amd.data.synthetic import synthetic_cifar
@@ -84,7 +91,7 @@ def main() -> int:
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
     dist.barrier()
-    t = torch.tensor([dt], device=dev, dtype=torch.float64)
+    t = torch.tensor([dt], device="cpu" if share else dev, dtype=torch.float64)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     dt = float(t.item())
     loss_sum, nsteps = trainer.engine.read_loss()

@@ -20,12 +20,13 @@ def main(path: str) -> None:
     for n, s, e, gx, wx, lds, vg, sg, scr in rows:
         by[n].append((e - s) / 1e3)
         meta[n] = (gx, wx, lds, vg, sg, scr)
-    print(f"{'kernel':60s} {'calls':>6s} {'median_us':>10s} {'p10_us':>8s} {'p90_us':>8s} "
+    grand = sum(sum(v) for v in by.values()) or 1.0
+    print(f"{'kernel':60s} {'calls':>6s} {'total_ms':>9s} {'pct':>5s} {'median_us':>10s} {'p10_us':>8s} {'p90_us':>8s} "
           f"{'grid':>6s} {'wg':>5s} {'lds':>7s} {'vgpr':>5s} {'sgpr':>5s} {'scratch':>7s}")
     for n, v in sorted(by.items(), key=lambda kv: -sum(kv[1])):
         v.sort()
         gx, wx, lds, vg, sg, scr = meta[n]
-        print(f"{n[:60]:60s} {len(v):6d} {v[len(v) // 2]:10.2f} {v[len(v) // 10]:8.2f} {v[9 * len(v) // 10]:8.2f} "
+        print(f"{n[:60]:60s} {len(v):6d} {sum(v) / 1e3:9.2f} {100 * sum(v) / grand:5.1f} {v[len(v) // 2]:10.2f} {v[len(v) // 10]:8.2f} {v[9 * len(v) // 10]:8.2f} "
               f"{gx:6d} {wx:5d} {lds:7d} {vg:5d} {sg:5d} {scr:7d}")
     seq = [(n, s, e) for n, s, e, *_ in rows if "k_pk_step" in n or "k_pk_reduce" in n]
     if len(seq) > 20:

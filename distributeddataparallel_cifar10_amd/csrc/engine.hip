@@ -92,7 +92,7 @@ struct Engine {
   char* xregion = nullptr;
   xg::Peers peers{};
   bool peers_open = false;
-  unsigned long long ar_deadline = 3000ull * 100000000ull;  // 3000 s in 100 MHz ticks (a peer may be in host code)
+  unsigned long long ar_deadline = 300ull * 100000000ull;  // 300 s in 100 MHz ticks (a peer may be in host code)
   std::map<int, hipGraphExec_t> graphs;
   bool persistent = false;
   int pk_waves = 8;

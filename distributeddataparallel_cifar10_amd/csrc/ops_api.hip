@@ -39,7 +39,7 @@ using namespace dca::ops;
 extern "C" {
 
 const char* dca_ops_last_error() { return g_err.c_str(); }
-int dca_ops_abi_version() { return 1; }
+int dca_ops_abi_version() { return 2; }
 
 // Must match ops/_native.py::GemmArgs.
 int dca_ops_gemm(const GemmArgs* a, void* stream) {
@@ -48,11 +48,21 @@ int dca_ops_gemm(const GemmArgs* a, void* stream) {
   REQUIRE(g.M > 0 && g.N > 0 && g.K > 0, "gemm: empty problem");
   REQUIRE(!g.fp8 || (!g.ta && !g.tb), "gemm: fp8 operands must be K-contiguous (ta = tb = 0)");
   REQUIRE(!g.fp8 || (g.K % 16 == 0 && g.lda % 16 == 0 && g.ldb % 16 == 0), "gemm: fp8 needs K, lda, ldb % 16 == 0");
-  REQUIRE(g.ta || g.lda >= g.K, "gemm: lda < K");
-  REQUIRE(g.tb || g.ldb >= g.K, "gemm: ldb < K");
-  REQUIRE(!g.ta || g.lda >= g.M, "gemm: lda < M (transposed A)");
-  REQUIRE(!g.tb || g.ldb >= g.N, "gemm: ldb < N (transposed B)");
+  REQUIRE(g.conv == 1 || g.ta || g.lda >= g.K, "gemm: lda < K");
+  REQUIRE(g.conv == 2 || !g.tb || g.ldb >= g.N, "gemm: ldb < N (transposed B)");
+  REQUIRE(g.conv == 2 || g.tb || g.ldb >= g.K, "gemm: ldb < K");
+  REQUIRE(g.conv == 1 || !g.ta || g.lda >= g.M, "gemm: lda < M (transposed A)");
   REQUIRE(g.ldc >= g.N, "gemm: ldc < N");
+  REQUIRE(g.conv >= 0 && g.conv <= 2, "gemm: bad conv mode");
+  if (g.conv) {
+    REQUIRE(!g.fp8 && g.cC % 8 == 0 && g.cC > 0, "gemm: implicit conv needs bf16 and C % 8 == 0");
+    REQUIRE(g.cHo == (g.cH + 2 * g.cP - g.cKH) / g.cS + 1 && g.cWo == (g.cW + 2 * g.cP - g.cKW) / g.cS + 1,
+            "gemm: inconsistent conv geometry");
+    const long pix = (long)g.cN * g.cHo * g.cWo, kc = (long)g.cKH * g.cKW * g.cC;
+    REQUIRE(g.conv != 1 || (g.M == pix && g.K == kc && !g.ta), "gemm: conv A shape mismatch");
+    REQUIRE(g.conv != 2 || (g.K == pix && g.N == kc && !g.tb), "gemm: conv B shape mismatch");
+  }
+  REQUIRE(!g.col_stats || (g.stats_shift && g.splits <= 1), "gemm: column stats need a shift and no split-K");
   if (!g_lds_set) {
     OPCK(hipFuncSetAttribute((const void*)k_gemm<false>, hipFuncAttributeMaxDynamicSharedMemorySize, G_LDS));
     OPCK(hipFuncSetAttribute((const void*)k_gemm<true>, hipFuncAttributeMaxDynamicSharedMemorySize, G_LDS));
@@ -108,7 +118,23 @@ int dca_ops_bn_fwd(const void* x, const void* r, void* out, float* part, float* 
   const int nparts = (int)((M + BN_ROWS - 1) / BN_ROWS);
   hipLaunchKernelGGL(k_bn_stats, dim3((C + 63) / 64, nparts), dim3(256), 0, st, (const bf16_t*)x, rm, (float2*)part,
                      (int)M, C);
-  hipLaunchKernelGGL(k_bn_finalize, dim3((C + 255) / 256), dim3(256), 0, st, (const float2*)part, nparts, (int)M, C,
+  hipLaunchKernelGGL(k_bn_finalize, dim3((C + 15) / 16), dim3(256), 0, st, (const float2*)part, nparts, (int)M, C,
+                     rm, rv, (float2*)stats, eps, momentum);
+  hipLaunchKernelGGL(k_bn_apply, dim3(grid_for(M * C / 8)), dim3(256), 0, st, (const bf16_t*)x, (const bf16_t*)r,
+                     (bf16_t*)out, (const float2*)stats, gamma, beta, M, C, relu, res_mode);
+  OPCK(hipGetLastError());
+  return 0;
+}
+
+// BatchNorm forward when the per-tile column partials were produced by the GEMM epilogue (col_stats): finalize
+// over `nparts` partial rows + apply.
+int dca_ops_bn_fwd_parts(const void* x, const void* r, void* out, const float* part, int nparts, float* stats,
+                         const float* gamma, const float* beta, float* rm, float* rv, long M, int C, float eps,
+                         float momentum, int relu, int res_mode, void* stream) {
+  REQUIRE(C % 8 == 0, "bn: C must be a multiple of 8");
+  REQUIRE(res_mode == 0 || r != nullptr, "bn: residual missing");
+  hipStream_t st = (hipStream_t)stream;
+  hipLaunchKernelGGL(k_bn_finalize, dim3((C + 15) / 16), dim3(256), 0, st, (const float2*)part, nparts, (int)M, C,
                      rm, rv, (float2*)stats, eps, momentum);
   hipLaunchKernelGGL(k_bn_apply, dim3(grid_for(M * C / 8)), dim3(256), 0, st, (const bf16_t*)x, (const bf16_t*)r,
                      (bf16_t*)out, (const float2*)stats, gamma, beta, M, C, relu, res_mode);
@@ -126,7 +152,7 @@ int dca_ops_bn_bwd(const void* dy, const void* x, const void* r, const float* st
   hipLaunchKernelGGL(k_bn_bwd_stats, dim3((C + 63) / 64, nparts), dim3(256), 0, st, (const bf16_t*)dy,
                      (const bf16_t*)x, (const bf16_t*)r, (const float2*)stats, gamma, beta, (float2*)part, (int)M, C,
                      relu, res_mode);
-  hipLaunchKernelGGL(k_bn_bwd_finalize, dim3((C + 255) / 256), dim3(256), 0, st, (const float2*)part, nparts, C,
+  hipLaunchKernelGGL(k_bn_bwd_finalize, dim3((C + 15) / 16), dim3(256), 0, st, (const float2*)part, nparts, C,
                      dgamma, dbeta, (float2*)sums, accumulate);
   hipLaunchKernelGGL(k_bn_bwd_apply, dim3(grid_for(M * C / 8)), dim3(256), 0, st, (const bf16_t*)dy, (const bf16_t*)x,
                      (const bf16_t*)r, (const float2*)stats, gamma, beta, (const float2*)sums, (bf16_t*)dx,

@@ -47,6 +47,15 @@ struct GemmArgs {
   int relu, out_bf16;
   int splits, k_per_split;  // split-K (k_per_split a multiple of the K-tile)
   const float* alpha_dev;   // optional device-side factor (fp8 per-tensor scales: no host sync)
+  // implicit-GEMM convolution (bf16, NHWC input with C % 8 == 0; no im2col buffer):
+  //   conv = 1: A(m = output pixel, k = (kh*KW + kw)*C + c) gathered from A = x        (forward / dgrad)
+  //   conv = 2: B(n = (kh*KW + kw)*C + c, k = output pixel) gathered from B = x        (weight gradient)
+  int conv;
+  int cN, cH, cW, cC, cKH, cKW, cS, cP, cHo, cWo;
+  // fused BatchNorm statistics of the output (splits == 1): col_stats[tile_m][N] = (sum, sumsq) over the tile's
+  // rows of (out - stats_shift[col]), the layout k_bn_finalize reduces
+  float2* col_stats;
+  const float* stats_shift;
 };
 
 __device__ __forceinline__ int lds_off(int row, int chunk) { return row * 128 + ((chunk ^ ((row >> 1) & 7)) << 4); }
@@ -136,6 +145,66 @@ __device__ __forceinline__ void store_t(const Stage& s, char* lds) {
   }
 }
 
+// Implicit-GEMM gathers.  Per-thread row decompositions are computed once per tile (the rows a thread loads
+// are fixed across the K loop); every load is unconditional from a clamped address, then selected to zero.
+struct ConvRows {  // conv = 1: the 4 output pixels (A rows) this thread loads
+  int nh[4], ih[4], iw[4];
+};
+__device__ __forceinline__ void conv_rows(ConvRows& cr, const GemmArgs& g, int m0) {
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    int m = m0 + ((threadIdx.x + GT * i) >> 3);
+    m = m < g.M ? m : g.M - 1;
+    const int ow = m % g.cWo, t = m / g.cWo, oh = t % g.cHo, n = t / g.cHo;
+    cr.nh[i] = n * g.cH;
+    cr.ih[i] = oh * g.cS - g.cP;
+    cr.iw[i] = ow * g.cS - g.cP;
+  }
+}
+__device__ __forceinline__ void load_conv_a(Stage& s, const unsigned short* x, const ConvRows& cr, const GemmArgs& g,
+                                            int k0, int k_end) {
+  const int k = k0 + (threadIdx.x & 7) * 8;  // 8 channels of one tap (C % 8 == 0)
+  const int tap = k / g.cC, c = k - tap * g.cC, kh = tap / g.cKW, kw = tap - kh * g.cKW;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int h = cr.ih[i] + kh, w = cr.iw[i] + kw;
+    const bool ok = k < k_end && h >= 0 && h < g.cH && w >= 0 && w < g.cW;
+    const long off = ok ? ((long)(cr.nh[i] + h) * g.cW + w) * g.cC + c : 0;
+    const uint4 v = *(const uint4*)(x + off);
+    s.v[i] = ok ? v : uint4{0u, 0u, 0u, 0u};
+  }
+}
+struct ConvCols {  // conv = 2: the 4 column groups (8 consecutive n = 8 channels of one tap) this thread loads
+  int kh[4], kw[4], c[4];
+  bool in[4];
+};
+__device__ __forceinline__ void conv_cols(ConvCols& cc, const GemmArgs& g, int n0) {
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int n = n0 + ((threadIdx.x + GT * i) & 15) * 8;
+    const int tap = n / g.cC;
+    cc.c[i] = n - tap * g.cC;
+    cc.kh[i] = tap / g.cKW;
+    cc.kw[i] = tap - cc.kh[i] * g.cKW;
+    cc.in[i] = n < g.N;
+  }
+}
+__device__ __forceinline__ void load_conv_b(Stage& s, const unsigned short* x, const ConvCols& cc, const GemmArgs& g,
+                                            int k0, int k_end) {
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    int p = k0 + ((threadIdx.x + GT * i) >> 4);  // output pixel = GEMM k
+    const bool pin = p < k_end;
+    p = pin ? p : k0;
+    const int ow = p % g.cWo, t = p / g.cWo, oh = t % g.cHo, n = t / g.cHo;
+    const int h = oh * g.cS - g.cP + cc.kh[i], w = ow * g.cS - g.cP + cc.kw[i];
+    const bool ok = pin && cc.in[i] && h >= 0 && h < g.cH && w >= 0 && w < g.cW;
+    const long off = ok ? ((long)(n * g.cH + h) * g.cW + w) * g.cC + cc.c[i] : 0;
+    const uint4 v = *(const uint4*)(x + off);
+    s.v[i] = ok ? v : uint4{0u, 0u, 0u, 0u};
+  }
+}
+
 __device__ __forceinline__ int xcd_remap(int orig, int nwg) {
   const int xcd = orig & 7, q = nwg >> 3, r = nwg & 7;
   return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (orig >> 3);
@@ -162,19 +231,25 @@ __global__ void __launch_bounds__(GT) k_gemm(GemmArgs g) {
 #pragma unroll
     for (int n = 0; n < 4; ++n) acc[m][n] = f32x4{0.f, 0.f, 0.f, 0.f};
 
+  ConvRows cr;
+  ConvCols cc;
+  if (g.conv == 1) conv_rows(cr, g, m0);
+  if (g.conv == 2) conv_cols(cc, g, n0);
   auto load = [&](Stage& sa, Stage& sb, int kt) {
     const int k0 = k_begin + kt * KT;
-    if (g.ta) load_t(sa, (const unsigned short*)g.A, m0, g.M, g.lda, k0, k_end);
+    if (g.conv == 1) load_conv_a(sa, (const unsigned short*)g.A, cr, g, k0, k_end);
+    else if (g.ta) load_t(sa, (const unsigned short*)g.A, m0, g.M, g.lda, k0, k_end);
     else load_nt<ESZ>(sa, (const char*)g.A, m0, g.M, (size_t)g.lda * ESZ, k0 * ESZ, k_end * ESZ);
-    if (g.tb) load_t(sb, (const unsigned short*)g.B, n0, g.N, g.ldb, k0, k_end);
+    if (g.conv == 2) load_conv_b(sb, (const unsigned short*)g.B, cc, g, k0, k_end);
+    else if (g.tb) load_t(sb, (const unsigned short*)g.B, n0, g.N, g.ldb, k0, k_end);
     else load_nt<ESZ>(sb, (const char*)g.B, n0, g.N, (size_t)g.ldb * ESZ, k0 * ESZ, k_end * ESZ);
   };
   auto store = [&](const Stage& sa, const Stage& sb, int buf) {
     char* la = smem + buf * 2 * G_TILE_BYTES;
     char* lb = la + G_TILE_BYTES;
-    if (g.ta) store_t(sa, la);
+    if (g.ta && g.conv != 1) store_t(sa, la);
     else store_nt(sa, la);
-    if (g.tb) store_t(sb, lb);
+    if (g.tb || g.conv == 2) store_t(sb, lb);
     else store_nt(sb, lb);
   };
 
@@ -229,31 +304,106 @@ __global__ void __launch_bounds__(GT) k_gemm(GemmArgs g) {
     __syncthreads();
   }
 
-  // epilogue: C/D fragment (16x16): col = lane & 15, row = (lane >> 4) * 4 + j
-  const float alpha = g.alpha * (g.alpha_dev ? *g.alpha_dev : 1.f);
+  // Epilogue.  Split-K partials go straight to the fp32 slab.  Otherwise the 128x128 fp32 tile is staged in
+  // LDS (the K-loop buffers are free: 64 KiB exactly; 16-column groups XOR-swizzled by (row >> 2) & 3 so the
+  // fragment writes of one instruction hit distinct banks), then written back row-contiguously, 16 B per lane,
+  // with alpha / bias / beta / ReLU applied -- and, when asked, the per-column BN partial sums of the tile.
+  if (g.splits > 1) {
 #pragma unroll
-  for (int m = 0; m < 4; ++m) {
+    for (int m = 0; m < 4; ++m)
 #pragma unroll
-    for (int n = 0; n < 4; ++n) {
-      const int col = n0 + wc * 64 + n * 16 + (lane & 15);
-      if (col >= g.N) continue;
+      for (int n = 0; n < 4; ++n) {
+        const int col = n0 + wc * 64 + n * 16 + (lane & 15);
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int row = m0 + wr * 64 + m * 16 + (lane >> 4) * 4 + j;
-        if (row >= g.M) continue;
-        float v = acc[m][n][j];
-        if (g.splits > 1) {
-          g.ws[((size_t)ksplit * g.M + row) * g.N + col] = v;
-          continue;
+        for (int j = 0; j < 4; ++j) {
+          const int row = m0 + wr * 64 + m * 16 + (lane >> 4) * 4 + j;
+          if (row < g.M && col < g.N) g.ws[((size_t)ksplit * g.M + row) * g.N + col] = acc[m][n][j];
         }
-        v *= alpha;
-        if (g.bias) v += g.bias[col];
-        const size_t o = (size_t)row * g.ldc + col;
-        if (g.beta != 0.f) v += g.beta * (g.out_bf16 ? bf2f(((const unsigned short*)g.C)[o]) : ((const float*)g.C)[o]);
-        if (g.relu) v = v > 0.f ? v : 0.f;
-        if (g.out_bf16) ((unsigned short*)g.C)[o] = f2bf_rne(v);
-        else ((float*)g.C)[o] = v;
       }
+    return;
+  }
+  float* ct = (float*)smem;
+  auto cidx = [](int r, int c) { return r * GBN + (c ^ (((r >> 2) & 3) << 4)); };
+#pragma unroll
+  for (int m = 0; m < 4; ++m)
+#pragma unroll
+    for (int n = 0; n < 4; ++n)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        ct[cidx(wr * 64 + m * 16 + (lane >> 4) * 4 + j, wc * 64 + n * 16 + (lane & 15))] = acc[m][n][j];
+  __syncthreads();
+  const float alpha = g.alpha * (g.alpha_dev ? *g.alpha_dev : 1.f);
+  // thread t: column group cg = t & 31 (4 columns), rows (t >> 5) + 8 r, r = 0..15
+  const int cg = threadIdx.x & 31, col0 = n0 + cg * 4;
+  float bias4[4], shift4[4], s1[4] = {0.f, 0.f, 0.f, 0.f}, s2[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    const int col = min(col0 + e, g.N - 1);
+    bias4[e] = g.bias ? g.bias[col] : 0.f;
+    shift4[e] = g.col_stats ? g.stats_shift[col] : 0.f;
+  }
+  const bool full4 = col0 + 4 <= g.N && (g.ldc & 3) == 0;
+  for (int r = 0; r < 16; ++r) {
+    const int lr = (threadIdx.x >> 5) + 8 * r, row = m0 + lr;
+    if (row >= g.M || col0 >= g.N) continue;
+    const f32x4 a = *(const f32x4*)(ct + cidx(lr, cg * 4));
+    float v[4];
+    const size_t o = (size_t)row * g.ldc + col0;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      float x = a[e] * alpha + bias4[e];
+      if (g.beta != 0.f && col0 + e < g.N)
+        x += g.beta * (g.out_bf16 ? bf2f(((const unsigned short*)g.C)[o + e]) : ((const float*)g.C)[o + e]);
+      if (g.relu) x = x > 0.f ? x : 0.f;
+      v[e] = x;
+    }
+    if (g.out_bf16) {
+      unsigned short h[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) h[e] = f2bf_rne(v[e]);
+      if (g.col_stats) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {  // statistics of the values as stored (bf16)
+          const float d = bf2f(h[e]) - shift4[e];
+          s1[e] += d;
+          s2[e] += d * d;
+        }
+      }
+      if (full4) {
+        *(uint2*)((unsigned short*)g.C + o) = uint2{h[0] | ((unsigned)h[1] << 16), h[2] | ((unsigned)h[3] << 16)};
+      } else {
+        for (int e = 0; e < 4 && col0 + e < g.N; ++e) ((unsigned short*)g.C)[o + e] = h[e];
+      }
+    } else {
+      if (g.col_stats) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const float d = v[e] - shift4[e];
+          s1[e] += d;
+          s2[e] += d * d;
+        }
+      }
+      if (full4) {
+        *(f32x4*)((float*)g.C + o) = f32x4{v[0], v[1], v[2], v[3]};
+      } else {
+        for (int e = 0; e < 4 && col0 + e < g.N; ++e) ((float*)g.C)[o + e] = v[e];
+      }
+    }
+  }
+  if (g.col_stats) {  // combine the 8 row-lanes of each column group (fixed order), one float2 per column
+    __syncthreads();
+    float2* red = (float2*)smem;  // [8 row lanes][128 cols]
+#pragma unroll
+    for (int e = 0; e < 4; ++e) red[(threadIdx.x >> 5) * GBN + cg * 4 + e] = float2{s1[e], s2[e]};
+    __syncthreads();
+    if (threadIdx.x < GBN) {
+      const int col = n0 + threadIdx.x;
+      float2 t = red[threadIdx.x];
+      for (int k = 1; k < 8; ++k) {
+        t.x += red[k * GBN + threadIdx.x].x;
+        t.y += red[k * GBN + threadIdx.x].y;
+      }
+      if (col < g.N) g.col_stats[(size_t)tm * g.N + col] = t;
     }
   }
 }

@@ -122,21 +122,51 @@ __global__ void __launch_bounds__(256) k_bn_stats(const bf16_t* __restrict__ x, 
   }
 }
 
+// Reduce the per-block partials of 16 channels per workgroup: 16 part-lanes x 16 channels, 8 loads in flight
+// per thread, then a fixed-order LDS combine (deterministic).  Returns the (sum, sumsq) of channel c in lane 0..15.
+__device__ __forceinline__ float2 reduce_parts(const float2* __restrict__ part, int nparts, int C, int c, float2* red) {
+  const int pl = threadIdx.x >> 4, cl = threadIdx.x & 15;
+  float sx = 0.f, sy = 0.f;
+  if (c < C) {
+    for (int p0 = pl; p0 < nparts; p0 += 16 * 8) {
+      float2 v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int p = p0 + 16 * u;
+        v[u] = part[(long)min(p, nparts - 1) * C + c];  // clamped, unconditional: all 8 loads in flight
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const bool in = p0 + 16 * u < nparts;
+        sx += in ? v[u].x : 0.f;
+        sy += in ? v[u].y : 0.f;
+      }
+    }
+  }
+  red[pl * 16 + cl] = float2{sx, sy};
+  __syncthreads();
+  float2 a{0.f, 0.f};
+  if (pl == 0) {
+    for (int j = 0; j < 16; ++j) {
+      a.x += red[j * 16 + cl].x;
+      a.y += red[j * 16 + cl].y;
+    }
+  }
+  return a;
+}
+
 // mean/invstd per channel; running stats EMA (unbiased variance), as torch BatchNorm2d in train mode.
+// grid ceil(C/16), 256 threads.
 __global__ void __launch_bounds__(256) k_bn_finalize(const float2* __restrict__ part, int nparts, int M, int C,
                                                      float* __restrict__ running_mean, float* __restrict__ running_var,
                                                      float2* __restrict__ stats, float eps, float momentum) {
-  const int c = blockIdx.x * 256 + threadIdx.x;
-  if (c >= C) return;
-  float s = 0.f, q = 0.f;
-  for (int p = 0; p < nparts; ++p) {
-    const float2 a = part[(long)p * C + c];
-    s += a.x;
-    q += a.y;
-  }
+  __shared__ float2 red[256];
+  const int c = blockIdx.x * 16 + (threadIdx.x & 15);
+  const float2 a = reduce_parts(part, nparts, C, c, red);
+  if (threadIdx.x >= 16 || c >= C) return;
   const float k = running_mean[c];
-  const float dm = s / M;
-  const float var = fmaxf(q / M - dm * dm, 0.f);
+  const float dm = a.x / M;
+  const float var = fmaxf(a.y / M - dm * dm, 0.f);
   const float mean = k + dm;
   stats[c] = float2{mean, rsqrtf(var + eps)};
   if (momentum > 0.f) {
@@ -220,21 +250,18 @@ __global__ void __launch_bounds__(256) k_bn_bwd_stats(const bf16_t* __restrict__
   }
 }
 
-// dgamma = sum(dz * xhat), dbeta = sum(dz) (written, or added when accumulate: shared modules); sums for dx
+// dgamma = sum(dz * xhat), dbeta = sum(dz) (written, or added when accumulate: shared modules); sums for dx.
+// grid ceil(C/16), 256 threads.
 __global__ void __launch_bounds__(256) k_bn_bwd_finalize(const float2* __restrict__ part, int nparts, int C,
                                                          float* __restrict__ dgamma, float* __restrict__ dbeta,
                                                          float2* __restrict__ sums, int accumulate) {
-  const int c = blockIdx.x * 256 + threadIdx.x;
-  if (c >= C) return;
-  float s = 0.f, q = 0.f;
-  for (int p = 0; p < nparts; ++p) {
-    const float2 a = part[(long)p * C + c];
-    s += a.x;
-    q += a.y;
-  }
-  sums[c] = float2{s, q};
-  dgamma[c] = accumulate ? dgamma[c] + q : q;
-  dbeta[c] = accumulate ? dbeta[c] + s : s;
+  __shared__ float2 red[256];
+  const int c = blockIdx.x * 16 + (threadIdx.x & 15);
+  const float2 a = reduce_parts(part, nparts, C, c, red);
+  if (threadIdx.x >= 16 || c >= C) return;
+  sums[c] = a;
+  dgamma[c] = accumulate ? dgamma[c] + a.y : a.y;
+  dbeta[c] = accumulate ? dbeta[c] + a.x : a.x;
 }
 
 // dx = gamma * invstd * (dz - mean(dz) - xhat * mean(dz * xhat)); res_mode 2 also writes dr = dz

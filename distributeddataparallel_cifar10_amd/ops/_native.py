@@ -13,7 +13,7 @@ import torch
 
 from .. import build as _build
 
-ABI_VERSION = 1
+ABI_VERSION = 2
 _lock = threading.Lock()
 _lib = None
 
@@ -27,6 +27,9 @@ class GemmArgs(ctypes.Structure):
         ("M", c_int), ("N", c_int), ("K", c_int), ("lda", c_int), ("ldb", c_int), ("ldc", c_int),
         ("alpha", c_float), ("beta", c_float), ("ta", c_int), ("tb", c_int), ("fp8", c_int),
         ("relu", c_int), ("out_bf16", c_int), ("splits", c_int), ("k_per_split", c_int), ("alpha_dev", c_void_p),
+        ("conv", c_int), ("cN", c_int), ("cH", c_int), ("cW", c_int), ("cC", c_int), ("cKH", c_int), ("cKW", c_int),
+        ("cS", c_int), ("cP", c_int), ("cHo", c_int), ("cWo", c_int), ("col_stats", c_void_p),
+        ("stats_shift", c_void_p),
     ]
 
 
@@ -47,6 +50,8 @@ def _declare(lib):
     lib.dca_ops_col2im.argtypes = [c_void_p, c_void_p, P(ConvGeom), c_void_p]
     lib.dca_ops_bn_fwd.argtypes = [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                                    c_void_p, c_long, c_int, c_float, c_float, c_int, c_int, c_void_p]
+    lib.dca_ops_bn_fwd_parts.argtypes = [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_void_p,
+                                         c_void_p, c_void_p, c_long, c_int, c_float, c_float, c_int, c_int, c_void_p]
     lib.dca_ops_bn_bwd.argtypes = [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                                    c_void_p, c_void_p, c_void_p, c_void_p, c_long, c_int, c_int, c_int, c_int,
                                    c_void_p]

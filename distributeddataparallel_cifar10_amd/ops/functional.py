@@ -29,21 +29,28 @@ def _dev_check(*ts):
 # ------------------------------------------------------------------------------------------------------------
 def gemm(a: torch.Tensor, b: torch.Tensor, *, ta: bool = False, tb: bool = False, bias: Optional[torch.Tensor] = None,
          relu: bool = False, out_dtype=torch.float32, alpha: float = 1.0, out: Optional[torch.Tensor] = None,
-         beta: float = 0.0, splits: int = 0, alpha_dev: Optional[torch.Tensor] = None) -> torch.Tensor:
+         beta: float = 0.0, splits: int = 0, alpha_dev: Optional[torch.Tensor] = None, conv: int = 0,
+         geom=None, col_stats: Optional[torch.Tensor] = None, stats_shift: Optional[torch.Tensor] = None,
+         mnk=None) -> torch.Tensor:
     """C[M,N] = alpha * A(m,k) B(n,k) (+bias) (+beta*out) (ReLU).
 
     A is [M,K] (ta=False) or [K,M] (ta=True); B is [N,K] (tb=False) or [K,N] (tb=True).  bf16 operands, or
-    fp8 e4m3 stored as uint8 (both, K-contiguous).  splits=0 chooses split-K automatically."""
+    fp8 e4m3 stored as uint8 (both, K-contiguous).  splits=0 chooses split-K automatically.
+    conv=1 / conv=2: A / B is an NHWC input gathered as im2col on the fly (``geom`` = conv geometry, ``mnk`` =
+    the GEMM shape).  col_stats [ceil(M/128), N, 2] fp32 receives per-tile BN partial sums of the output."""
     _dev_check(a, b, bias, out)
     fp8 = a.dtype == torch.uint8
     if fp8 != (b.dtype == torch.uint8) or (not fp8 and (a.dtype != torch.bfloat16 or b.dtype != torch.bfloat16)):
         raise TypeError("gemm operands: both bf16 or both fp8 (uint8)")
-    if a.dim() != 2 or b.dim() != 2 or a.stride(1) != 1 or b.stride(1) != 1:
-        raise ValueError("gemm operands must be 2-D with unit inner stride")
-    M, K = (a.shape[1], a.shape[0]) if ta else (a.shape[0], a.shape[1])
-    Nn, Kb = (b.shape[1], b.shape[0]) if tb else (b.shape[0], b.shape[1])
-    if K != Kb:
-        raise ValueError(f"gemm: K mismatch {K} vs {Kb}")
+    if conv:
+        M, Nn, K = mnk
+    else:
+        if a.dim() != 2 or b.dim() != 2 or a.stride(1) != 1 or b.stride(1) != 1:
+            raise ValueError("gemm operands must be 2-D with unit inner stride")
+        M, K = (a.shape[1], a.shape[0]) if ta else (a.shape[0], a.shape[1])
+        Nn, Kb = (b.shape[1], b.shape[0]) if tb else (b.shape[0], b.shape[1])
+        if K != Kb:
+            raise ValueError(f"gemm: K mismatch {K} vs {Kb}")
     if out is None:
         out = torch.empty(M, Nn, dtype=out_dtype, device=a.device)
     if out.dtype not in (torch.float32, torch.bfloat16) or out.shape != (M, Nn) or out.stride(1) != 1:
@@ -51,6 +58,8 @@ def gemm(a: torch.Tensor, b: torch.Tensor, *, ta: bool = False, tb: bool = False
     if bias is not None and (bias.dtype != torch.float32 or bias.numel() != Nn):
         raise ValueError("gemm: bias must be fp32 [N]")
     tiles = math.ceil(M / 128) * math.ceil(Nn / 128)
+    if col_stats is not None:
+        splits = 1
     if splits <= 0:
         splits = 1
         kt = 128 if fp8 else 64
@@ -58,11 +67,18 @@ def gemm(a: torch.Tensor, b: torch.Tensor, *, ta: bool = False, tb: bool = False
             splits = max(1, min(K // (2 * kt), 512 // tiles, 64))
     ws = torch.empty(splits * M * Nn, dtype=torch.float32, device=a.device) if splits > 1 else None
     args = N.GemmArgs(A=a.data_ptr(), B=b.data_ptr(), C=out.data_ptr(), bias=bias.data_ptr() if bias is not None else None,
-                      ws=ws.data_ptr() if ws is not None else None, M=M, N=Nn, K=K, lda=a.stride(0),
-                      ldb=b.stride(0), ldc=out.stride(0), alpha=float(alpha), beta=float(beta), ta=int(ta),
+                      ws=ws.data_ptr() if ws is not None else None, M=M, N=Nn, K=K,
+                      lda=a.stride(0) if a.dim() == 2 else 0, ldb=b.stride(0) if b.dim() == 2 else 0,
+                      ldc=out.stride(0), alpha=float(alpha), beta=float(beta), ta=int(ta),
                       tb=int(tb), fp8=int(fp8), relu=int(relu), out_bf16=int(out.dtype == torch.bfloat16),
                       splits=splits, k_per_split=0,
-                      alpha_dev=alpha_dev.data_ptr() if alpha_dev is not None else None)
+                      alpha_dev=alpha_dev.data_ptr() if alpha_dev is not None else None, conv=int(conv),
+                      col_stats=col_stats.data_ptr() if col_stats is not None else None,
+                      stats_shift=stats_shift.data_ptr() if stats_shift is not None else None)
+    if conv:
+        for f in ("N", "H", "W", "C", "KH", "KW", "Ho", "Wo"):
+            setattr(args, "c" + f, getattr(geom, f))
+        args.cS, args.cP = geom.stride, geom.pad
     N.check(N.lib().dca_ops_gemm(args, N.stream(a.device)), "gemm")
     return out
 
@@ -160,54 +176,144 @@ def _weight_matrix(w: torch.Tensor, kp: int) -> torch.Tensor:
     return m.to(torch.bfloat16).contiguous()
 
 
-class _Conv2d(torch.autograd.Function):
-    @staticmethod
-    def forward(ctx, x, w, b, stride, pad, relu, fp8):
-        x = x.contiguous()
-        g = _geom(x, w, stride, pad)
-        direct = w.shape[2] == 1 and w.shape[3] == 1 and stride == 1 and pad == 0 and g.Kp == g.K
-        M = g.N * g.Ho * g.Wo
+def _implicit_ok(g) -> bool:
+    return g.C % 8 == 0
+
+
+def _conv_fwd(x, w, b, stride, pad, relu, fp8, col_stats=None, shift=None):
+    """Forward GEMM of a conv; returns (y [N,Ho,Wo,Cout] bf16, state for _conv_bwd)."""
+    x = x.contiguous()
+    g = _geom(x, w, stride, pad)
+    co = w.shape[0]
+    M = g.N * g.Ho * g.Wo
+    direct = w.shape[2] == 1 and w.shape[3] == 1 and stride == 1 and pad == 0
+    st = dict(geom=g, wshape=tuple(w.shape), x=x, cols=None)
+    use_fp8 = fp8 and g.Kp % 16 == 0
+    if direct or use_fp8 or not _implicit_ok(g):
         if direct:
             cols = x.view(M, g.K)
         else:
             cols = torch.empty(M, g.Kp, dtype=torch.bfloat16, device=x.device)
             N.check(N.lib().dca_ops_im2col(N.ptr(x), N.ptr(cols), g, N.stream(x.device)), "im2col")
+        st["cols"] = cols
         wm = _weight_matrix(w, g.Kp)
-        if fp8 and g.Kp % 16 == 0:
+        if use_fp8:
             qc, ac = quantize_fp8(cols)
             qw, aw = quantize_fp8(wm)
-            y = gemm(qc, qw, bias=b, relu=relu, out_dtype=torch.bfloat16, alpha_dev=fp8_alpha(ac, aw))
+            y = gemm(qc, qw, bias=b, relu=relu, out_dtype=torch.bfloat16, alpha_dev=fp8_alpha(ac, aw),
+                     col_stats=col_stats, stats_shift=shift)
         else:
-            y = gemm(cols, wm, bias=b, relu=relu, out_dtype=torch.bfloat16)
-        y = y.view(g.N, g.Ho, g.Wo, w.shape[0])
-        ctx.save_for_backward(cols, wm, y if relu else None)
-        ctx.geom, ctx.direct, ctx.relu, ctx.has_b, ctx.wshape = g, direct, relu, b is not None, tuple(w.shape)
+            y = gemm(cols, wm, bias=b, relu=relu, out_dtype=torch.bfloat16, col_stats=col_stats, stats_shift=shift)
+    else:  # implicit GEMM: the im2col matrix is never materialised
+        wm = _weight_matrix(w, g.K)
+        y = gemm(x, wm, conv=1, geom=g, mnk=(M, co, g.K), bias=b, relu=relu, out_dtype=torch.bfloat16,
+                 col_stats=col_stats, stats_shift=shift)
+    st["wm"] = wm
+    return y.view(g.N, g.Ho, g.Wo, co), st
+
+
+def _conv_bwd(dy, st, need_x: bool, need_w: bool):
+    """(dx, dw) of a conv from dY [N,Ho,Wo,Cout] (any dtype) and the forward state."""
+    g, (co, ci, kh, kw) = st["geom"], st["wshape"]
+    M = g.N * g.Ho * g.Wo
+    dyb = dy.to(torch.bfloat16).contiguous().view(M, co)
+    dx = dw = None
+    cols = st["cols"]
+    if need_x:
+        if cols is not None and cols.data_ptr() == st["x"].data_ptr():  # 1x1 / stride 1: dX = dY . W
+            dx = gemm(dyb, st["wm"], tb=True, out_dtype=torch.bfloat16).view(g.N, g.H, g.W, g.C)
+        elif g.stride == 1 and co % 8 == 0 and kh == kw and g.pad <= kh - 1:
+            # stride 1: dX = conv(dY, W flipped, ci<->co, pad KH-1-pad), implicit GEMM (no col2im)
+            gd = N.ConvGeom(N=g.N, H=g.Ho, W=g.Wo, C=co, KH=kh, KW=kw, stride=1, pad=kh - 1 - g.pad, Ho=g.H, Wo=g.W,
+                            K=kh * kw * co, Kp=kh * kw * co)
+            wd = st.get("w_master").flip(2, 3).permute(1, 2, 3, 0).reshape(ci, -1).to(torch.bfloat16).contiguous()
+            dx = gemm(dyb.view(g.N, g.Ho, g.Wo, co), wd, conv=1, geom=gd, mnk=(g.N * g.H * g.W, ci, gd.K),
+                      out_dtype=torch.bfloat16).view(g.N, g.H, g.W, g.C)
+        else:
+            wm = st["wm"]
+            dcols = gemm(dyb, wm, tb=True, out_dtype=torch.bfloat16)  # [M, Kp] = dY . Wm
+            kp = wm.shape[1]
+            gc = N.ConvGeom(N=g.N, H=g.H, W=g.W, C=g.C, KH=g.KH, KW=g.KW, stride=g.stride, pad=g.pad, Ho=g.Ho,
+                            Wo=g.Wo, K=g.K, Kp=kp)
+            dx = torch.empty(g.N, g.H, g.W, g.C, dtype=torch.bfloat16, device=dy.device)
+            N.check(N.lib().dca_ops_col2im(N.ptr(dcols), N.ptr(dx), gc, N.stream(dy.device)), "col2im")
+    if need_w:
+        if cols is not None:
+            kp = cols.shape[1]
+            dwm = gemm(dyb, cols, ta=True, tb=True, splits=_wgrad_splits(co, kp, M))  # [Cout, Kp] fp32
+        else:  # implicit: B(n = tap*C + c, k = pixel) gathered from x
+            dwm = gemm(dyb, st["x"], ta=True, conv=2, geom=g, mnk=(co, g.K, M), splits=_wgrad_splits(co, g.K, M))
+        dw = dwm[:, :g.K].reshape(co, kh, kw, ci).permute(0, 3, 1, 2).contiguous()
+    return dx, dw
+
+
+class _Conv2d(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, w, b, stride, pad, relu, fp8):
+        y, st = _conv_fwd(x, w, b, stride, pad, relu, fp8)
+        st["w_master"] = w.detach()
+        ctx.st = st
+        ctx.save_for_backward(y if relu else None)
+        ctx.relu, ctx.has_b = relu, b is not None
         return y
 
     @staticmethod
     def backward(ctx, dy):
-        cols, wm, y = ctx.saved_tensors
-        g = ctx.geom
-        co = ctx.wshape[0]
-        M = g.N * g.Ho * g.Wo
+        (y,) = ctx.saved_tensors
         if ctx.relu:
             dy = dy * (y > 0)
-        dyb = dy.to(torch.bfloat16).contiguous().view(M, co)
-        dx = dw = db = None
-        if ctx.needs_input_grad[0]:
-            dcols = gemm(dyb, wm, tb=True, out_dtype=torch.bfloat16)  # [M, Kp] = dY . Wm
-            if ctx.direct:
-                dx = dcols.view(g.N, g.H, g.W, g.C)
-            else:
-                dx = torch.empty(g.N, g.H, g.W, g.C, dtype=torch.bfloat16, device=dy.device)
-                N.check(N.lib().dca_ops_col2im(N.ptr(dcols), N.ptr(dx), g, N.stream(dy.device)), "col2im")
-        if ctx.needs_input_grad[1]:
-            dwm = gemm(dyb, cols, ta=True, tb=True, splits=_wgrad_splits(co, g.Kp, M))  # [Cout, Kp] fp32
-            kh, kw, ci = ctx.wshape[2], ctx.wshape[3], ctx.wshape[1]
-            dw = dwm[:, :g.K].reshape(co, kh, kw, ci).permute(0, 3, 1, 2).contiguous()
-        if ctx.has_b and ctx.needs_input_grad[2]:
-            db = dyb.float().sum(0)
+        dx, dw = _conv_bwd(dy, ctx.st, ctx.needs_input_grad[0], ctx.needs_input_grad[1])
+        db = dy.float().sum((0, 1, 2)) if ctx.has_b and ctx.needs_input_grad[2] else None
+        ctx.st = None
         return dx, dw, db, None, None, None, None
+
+
+class _ConvBNAct(torch.autograd.Function):
+    """conv (no bias) -> BatchNorm (train) -> ReLU / residual, with the BN statistics computed in the conv
+    GEMM's epilogue (no separate statistics pass over the conv output)."""
+
+    @staticmethod
+    def forward(ctx, x, w, r, gamma, beta, running_mean, running_var, stride, pad, eps, momentum, relu, res_mode, fp8):
+        co = w.shape[0]
+        g = _geom(x, w, stride, pad)
+        M = g.N * g.Ho * g.Wo
+        nparts = (M + 127) // 128
+        part = torch.empty(nparts, co, 2, dtype=torch.float32, device=x.device)
+        y, st = _conv_fwd(x, w, None, stride, pad, False, fp8, col_stats=part, shift=running_mean)
+        st["w_master"] = w.detach()
+        r = r.contiguous() if r is not None else None
+        out = torch.empty_like(y)
+        stats = torch.empty(co, 2, dtype=torch.float32, device=x.device)
+        N.check(N.lib().dca_ops_bn_fwd_parts(N.ptr(y), N.ptr(r), N.ptr(out), N.ptr(part), nparts, N.ptr(stats),
+                                             N.ptr(gamma), N.ptr(beta), N.ptr(running_mean), N.ptr(running_var), M, co,
+                                             float(eps), float(momentum), int(relu), int(res_mode),
+                                             N.stream(x.device)), "bn_fwd_parts")
+        ctx.st = st
+        ctx.save_for_backward(y, r, gamma, beta, stats)
+        ctx.relu, ctx.res_mode = relu, res_mode
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        y, r, gamma, beta, stats = ctx.saved_tensors
+        dy_conv, dr, dgamma, dbeta = _bn_backward(dout, y, r, gamma, beta, stats, ctx.relu, ctx.res_mode)
+        dx, dw = _conv_bwd(dy_conv, ctx.st, ctx.needs_input_grad[0], ctx.needs_input_grad[1])
+        ctx.st = None
+        return dx, dw, dr, dgamma, dbeta, None, None, None, None, None, None, None, None, None
+
+
+def conv_bn_act(x, conv: torch.nn.Conv2d, bn: torch.nn.BatchNorm2d, r=None, relu=True, fp8=False, res_mode=None):
+    """Training-mode act(bn(conv(x))) for NHWC bf16 x, conv without bias; with a residual r: res_mode 2 (default,
+    ResNet: act(bn + r)) or 1 (NetResDeep: act(bn) + r)."""
+    if res_mode is None:
+        res_mode = 2 if r is not None else 0
+    if conv.bias is not None or not bn.training:
+        raise ValueError("conv_bn_act: conv without bias, BN in training mode")
+    momentum = bn.momentum if bn.track_running_stats else 0.0
+    if bn.track_running_stats:
+        bn.num_batches_tracked.add_(1)
+    return _ConvBNAct.apply(x, conv.weight, r, bn.weight, bn.bias, bn.running_mean, bn.running_var, conv.stride[0],
+                            conv.padding[0], bn.eps, momentum, relu, res_mode, fp8)
 
 
 def conv2d(x, w, b=None, stride=1, pad=0, relu=False, fp8=False):
@@ -238,21 +344,27 @@ class _BatchNormAct(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dy):
         x, r, gamma, beta, stats = ctx.saved_tensors
-        dy = dy.to(torch.bfloat16).contiguous()
-        C = x.shape[-1]
-        M = x.numel() // C
-        part = torch.empty((M + 255) // 256, C, 2, dtype=torch.float32, device=x.device)
-        sums = torch.empty(C, 2, dtype=torch.float32, device=x.device)
-        dgamma = torch.empty(C, dtype=torch.float32, device=x.device)
-        dbeta = torch.empty_like(dgamma)
-        dx = torch.empty_like(x)
-        dr = torch.empty_like(x) if ctx.res_mode == 2 else None
-        N.check(N.lib().dca_ops_bn_bwd(N.ptr(dy), N.ptr(x), N.ptr(r), N.ptr(stats), N.ptr(gamma), N.ptr(beta),
-                                       N.ptr(part), N.ptr(sums), N.ptr(dgamma), N.ptr(dbeta), N.ptr(dx), N.ptr(dr),
-                                       M, C, int(ctx.relu), int(ctx.res_mode), 0, N.stream(x.device)), "bn_bwd")
-        if ctx.res_mode == 1:
-            dr = dy
+        dx, dr, dgamma, dbeta = _bn_backward(dy, x, r, gamma, beta, stats, ctx.relu, ctx.res_mode)
         return dx, dr, dgamma, dbeta, None, None, None, None, None, None
+
+
+def _bn_backward(dy, x, r, gamma, beta, stats, relu, res_mode):
+    """(dx, dr, dgamma, dbeta) of the fused BN + ReLU + residual."""
+    dy = dy.to(torch.bfloat16).contiguous()
+    C = x.shape[-1]
+    M = x.numel() // C
+    part = torch.empty((M + 255) // 256, C, 2, dtype=torch.float32, device=x.device)
+    sums = torch.empty(C, 2, dtype=torch.float32, device=x.device)
+    dgamma = torch.empty(C, dtype=torch.float32, device=x.device)
+    dbeta = torch.empty_like(dgamma)
+    dx = torch.empty_like(x)
+    dr = torch.empty_like(x) if res_mode == 2 else None
+    N.check(N.lib().dca_ops_bn_bwd(N.ptr(dy), N.ptr(x), N.ptr(r), N.ptr(stats), N.ptr(gamma), N.ptr(beta),
+                                   N.ptr(part), N.ptr(sums), N.ptr(dgamma), N.ptr(dbeta), N.ptr(dx), N.ptr(dr),
+                                   M, C, int(relu), int(res_mode), 0, N.stream(x.device)), "bn_bwd")
+    if res_mode == 1:
+        dr = dy
+    return dx, dr, dgamma, dbeta
 
 
 def batch_norm_act(x, bn: torch.nn.BatchNorm2d, r=None, relu=True, res_mode=0):

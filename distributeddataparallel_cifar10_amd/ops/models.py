@@ -41,9 +41,8 @@ class OpsModel(nn.Module):
         m = self.module
         h = F.conv2d(h, m.conv1.weight, m.conv1.bias, stride=1, pad=1, relu=True)
         h = F.max_pool2d(h, 2)
-        for blk in m.resblocks:
-            y = F.conv2d(h, blk.conv.weight, None, stride=1, pad=1)
-            h = F.batch_norm_act(y, blk.batch_norm, r=h, relu=True, res_mode=1)  # relu(bn(conv(x))) + x
+        for blk in m.resblocks:  # relu(bn(conv(x))) + x, BN statistics from the conv GEMM's epilogue
+            h = F.conv_bn_act(h, blk.conv, blk.batch_norm, r=h, relu=True, res_mode=1)
         h = F.max_pool2d(h, 2)
         n, hh, ww, c = h.shape
         flat = h.reshape(n, hh * ww * c)
@@ -53,8 +52,7 @@ class OpsModel(nn.Module):
 
     def _conv_bn(self, h, conv, bn, relu=True, r=None):
         one = conv.kernel_size == (1, 1)
-        y = F.conv2d(h, conv.weight, conv.bias, stride=conv.stride[0], pad=conv.padding[0], fp8=self.fp8 and one)
-        return F.batch_norm_act(y, bn, r=r, relu=relu, res_mode=2 if r is not None else 0)
+        return F.conv_bn_act(h, conv, bn, r=r, relu=relu, fp8=self.fp8 and one)
 
     def _resnet(self, h):
         m = self.module

@@ -199,3 +199,23 @@ def test_xgmi_allreduce_ranks_one_gpu(gpu, port, ws, dtype, persistent):
         p.join(timeout=120)
     bad = [r for r in res if r[1]]
     assert not bad, "\n".join(f"rank {r}:\n{e}" for r, e in bad)
+
+
+def test_bench_two_ranks_shared_gpu(gpu, port):
+    """The driver's multi-GPU bench command (torch.distributed.run, one rank per GPU) rehearsed with 2 ranks on
+    this box's one GPU: JSON contract, whole-job value, the xGMI all-reduce actually in use."""
+    import json
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, DCA_BENCH_SHARE_GPU="1", DCA_XGMI_TIMEOUT_S="60")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2", "--master-addr",
+           "127.0.0.1", "--master-port", str(port), "bench.py", "--gpus", "2", "--steps", "48", "--warmup", "16"]
+    r = subprocess.run(cmd, cwd=root, env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-4000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    out = json.loads(lines[0])
+    assert out["n_gpus"] == 2 and out["steps"] == 48 and out["allreduce"] == "xgmi" and out["loss_finite"]
+    assert out["config"]["global_batch"] == 64 and out["config"]["parallelism"] == "dp2"
+    assert out["value"] > 0
