@@ -64,8 +64,14 @@ int dca_ops_gemm(const GemmArgs* a, void* stream) {
   }
   REQUIRE(!g.col_stats || (g.stats_shift && g.splits <= 1), "gemm: column stats need a shift and no split-K");
   if (!g_lds_set) {
-    OPCK(hipFuncSetAttribute((const void*)k_gemm<false>, hipFuncAttributeMaxDynamicSharedMemorySize, G_LDS));
-    OPCK(hipFuncSetAttribute((const void*)k_gemm<true>, hipFuncAttributeMaxDynamicSharedMemorySize, G_LDS));
+    OPCK(hipFuncSetAttribute((const void*)k_gemm<false, 128>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                             GemmTile<128>::LDS));
+    OPCK(hipFuncSetAttribute((const void*)k_gemm<true, 128>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                             GemmTile<128>::LDS));
+    OPCK(hipFuncSetAttribute((const void*)k_gemm<false, 64>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                             GemmTile<64>::LDS));
+    OPCK(hipFuncSetAttribute((const void*)k_gemm<true, 64>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                             GemmTile<64>::LDS));
     g_lds_set = true;
   }
   const int kt = GBK_BYTES / (g.fp8 ? 1 : 2);
@@ -79,10 +85,18 @@ int dca_ops_gemm(const GemmArgs* a, void* stream) {
   } else {
     g.k_per_split = g.K;
   }
-  const int tiles = ((g.M + GBM - 1) / GBM) * ((g.N + GBN - 1) / GBN);
+  // narrow N (<= 64) with a K-contiguous B operand: the 128x64 tile
+  const bool narrow = g.N <= 64 && !g.tb && g.conv != 2;
+  const int bn = narrow ? 64 : 128;
+  const int tiles = ((g.M + GBM - 1) / GBM) * ((g.N + bn - 1) / bn);
   const dim3 grid(tiles, g.splits);
-  if (g.fp8) hipLaunchKernelGGL(k_gemm<true>, grid, dim3(GT), G_LDS, st, g);
-  else hipLaunchKernelGGL(k_gemm<false>, grid, dim3(GT), G_LDS, st, g);
+  if (narrow) {
+    if (g.fp8) hipLaunchKernelGGL((k_gemm<true, 64>), grid, dim3(GT), GemmTile<64>::LDS, st, g);
+    else hipLaunchKernelGGL((k_gemm<false, 64>), grid, dim3(GT), GemmTile<64>::LDS, st, g);
+  } else {
+    if (g.fp8) hipLaunchKernelGGL((k_gemm<true, 128>), grid, dim3(GT), GemmTile<128>::LDS, st, g);
+    else hipLaunchKernelGGL((k_gemm<false, 128>), grid, dim3(GT), GemmTile<128>::LDS, st, g);
+  }
   if (g.splits > 1) hipLaunchKernelGGL(k_gemm_splitk_reduce, dim3(grid_for((long)g.M * g.N)), dim3(256), 0, st, g);
   OPCK(hipGetLastError());
   return 0;

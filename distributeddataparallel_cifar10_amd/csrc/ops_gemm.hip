@@ -28,10 +28,10 @@ typedef short s16x8 __attribute__((ext_vector_type(8)));
 typedef int i32x8 __attribute__((ext_vector_type(8)));
 
 constexpr int GT = 256;          // threads per GEMM workgroup
-constexpr int GBM = 128, GBN = 128;
+constexpr int GBM = 128;
 constexpr int GBK_BYTES = 128;   // bytes of K per row per K-tile
 constexpr int G_TILE_BYTES = GBM * GBK_BYTES;  // 16 KiB per operand per buffer
-constexpr int G_LDS = 2 * 2 * G_TILE_BYTES;     // 64 KiB
+
 
 struct GemmArgs {
   const void* A;
@@ -65,21 +65,24 @@ __device__ __forceinline__ unsigned short f2bf_rne(float f) {
 }
 __device__ __forceinline__ float bf2f(unsigned short h) { return __uint_as_float((unsigned)h << 16); }
 
-// Stage of one operand tile held in registers between its global load and its LDS write.
-struct Stage {
-  uint4 v[4];
+// Stage of one operand tile held in registers between its global load and its LDS write (NI x 16 B per thread:
+// 4 for a 128-row tile, 2 for a 64-row tile).
+template <int NI>
+struct StageT {
+  uint4 v[NI];
 };
+using Stage = StageT<4>;
 
 // Non-transposed operand: rows r0.., K bytes kb0.. (row-major, K contiguous).  Thread t owns chunks
 // idx = t + 256 i: row idx >> 3, chunk idx & 7.  Rows past R are clamped (their results are never stored);
 // bytes past the K range are zero.  A chunk that straddles the K end, or a row stride that is not 16-B
 // aligned, takes the element-wise path (esz-byte loads).
-template <int ESZ>
-__device__ __forceinline__ void load_nt(Stage& s, const char* base, int r0, int R, size_t ld_bytes, int kb0,
+template <int ESZ, int NI = 4>
+__device__ __forceinline__ void load_nt(StageT<NI>& s, const char* base, int r0, int R, size_t ld_bytes, int kb0,
                                         int kb_end) {
   const bool vec_ok = (ld_bytes & 15) == 0;
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
+  for (int i = 0; i < NI; ++i) {
     const int idx = threadIdx.x + GT * i, row = idx >> 3, ch = idx & 7;
     int rg = r0 + row;
     rg = rg < R ? rg : R - 1;
@@ -100,23 +103,25 @@ __device__ __forceinline__ void load_nt(Stage& s, const char* base, int r0, int 
     }
   }
 }
-__device__ __forceinline__ void store_nt(const Stage& s, char* lds) {
+template <int NI = 4>
+__device__ __forceinline__ void store_nt(const StageT<NI>& s, char* lds) {
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
+  for (int i = 0; i < NI; ++i) {
     const int idx = threadIdx.x + GT * i;
     *(uint4*)(lds + lds_off(idx >> 3, idx & 7)) = s.v[i];
   }
 }
-// Transposed bf16 operand: element (r, k) at base[k*ld + r].  Thread t owns 8 consecutive r at one k:
-// idx = t + 256 i: k = idx >> 4 (64 per tile), r group (idx & 15) * 8.  Vector loads where the 8 rows are in
-// range and 16-B aligned, element-wise loads otherwise (rows past R clamped, never stored).
+// Transposed bf16 operand: element (r, k) at base[k*ld + r].  Thread t owns 8 consecutive r (group t & 15) at 4
+// consecutive k (4 (t >> 4) .. +3): 4 row loads of 16 B, transposed in registers into 8 LDS writes of 8 B (the
+// 4 k values of one r).  Vector loads where the 8 rows are in range and 16-B aligned, element-wise otherwise
+// (rows past R clamped, never stored).  s.v[i] = the 8 r values at k = k0 + 4 (t >> 4) + i.
 __device__ __forceinline__ void load_t(Stage& s, const unsigned short* base, int r0, int R, size_t ld, int k0,
                                        int k_end) {
   const bool vec_ok = (ld & 7) == 0;
+  const int rg = r0 + (threadIdx.x & 15) * 8;
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
-    const int idx = threadIdx.x + GT * i, k = k0 + (idx >> 4);
-    const int rg = r0 + (idx & 15) * 8;
+    const int k = k0 + 4 * (threadIdx.x >> 4) + i;
     if (k >= k_end) {
       s.v[i] = uint4{0u, 0u, 0u, 0u};
     } else if (vec_ok && rg + 8 <= R) {
@@ -133,15 +138,15 @@ __device__ __forceinline__ void load_t(Stage& s, const unsigned short* base, int
   }
 }
 __device__ __forceinline__ void store_t(const Stage& s, char* lds) {
+  const int kq = 4 * (threadIdx.x >> 4), rb = (threadIdx.x & 15) * 8;
+  const unsigned w[4][4] = {{s.v[0].x, s.v[0].y, s.v[0].z, s.v[0].w}, {s.v[1].x, s.v[1].y, s.v[1].z, s.v[1].w},
+                            {s.v[2].x, s.v[2].y, s.v[2].z, s.v[2].w}, {s.v[3].x, s.v[3].y, s.v[3].z, s.v[3].w}};
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int idx = threadIdx.x + GT * i, k = idx >> 4, rb = (idx & 15) * 8;
-    const unsigned w[4] = {s.v[i].x, s.v[i].y, s.v[i].z, s.v[i].w};
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const unsigned short h = (unsigned short)(w[j >> 1] >> ((j & 1) * 16));
-      *(unsigned short*)(lds + lds_off(rb + j, k >> 3) + (k & 7) * 2) = h;
-    }
+  for (int j = 0; j < 8; ++j) {
+    const int sh = (j & 1) * 16;
+    const unsigned e0 = (w[0][j >> 1] >> sh) & 0xffffu, e1 = (w[1][j >> 1] >> sh) & 0xffffu;
+    const unsigned e2 = (w[2][j >> 1] >> sh) & 0xffffu, e3 = (w[3][j >> 1] >> sh) & 0xffffu;
+    *(uint2*)(lds + lds_off(rb + j, kq >> 3) + (kq & 7) * 2) = uint2{e0 | (e1 << 16), e2 | (e3 << 16)};
   }
 }
 
@@ -193,7 +198,7 @@ __device__ __forceinline__ void load_conv_b(Stage& s, const unsigned short* x, c
                                             int k0, int k_end) {
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
-    int p = k0 + ((threadIdx.x + GT * i) >> 4);  // output pixel = GEMM k
+    int p = k0 + 4 * (threadIdx.x >> 4) + i;  // output pixel = GEMM k (load_t's thread layout)
     const bool pin = p < k_end;
     p = pin ? p : k0;
     const int ow = p % g.cWo, t = p / g.cWo, oh = t % g.cHo, n = t / g.cHo;
@@ -210,13 +215,28 @@ __device__ __forceinline__ int xcd_remap(int orig, int nwg) {
   return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (orig >> 3);
 }
 
-template <bool FP8>
+template <int BN_>
+struct GemmTile {
+  static constexpr int B_BYTES = BN_ * GBK_BYTES;              // B tile per buffer
+  static constexpr int BUF = G_TILE_BYTES + B_BYTES;           // A + B per buffer
+  static constexpr int LDS = 2 * BUF;                          // double buffered (>= the fp32 epilogue tile)
+  static constexpr int NF = BN_ / 32;                          // 16-wide MFMA column fragments per wave
+  static constexpr int WCW = BN_ / 2;                          // columns per wave (2 x 2 waves)
+  static_assert(LDS >= GBM * BN_ * 4, "epilogue tile must fit in the K-loop LDS");
+};
+
+// BN_ = 128: the general tile.  BN_ = 64: narrow-N GEMMs (e.g. 64-channel convolutions) -- half the B tile, no
+// wasted MFMA columns, 48 KiB LDS (3 workgroups per CU); its B operand must be K-contiguous (no tb / conv 2).
+// K loop: register prefetch of tile k+1 during the MFMAs of tile k, written to the other LDS buffer after them.
+// (A two-tile-deep prefetch measured neutral to 20 % slower: 196 VGPRs = 1 wave per SIMD, bench/gemm_bench.py.)
+template <bool FP8, int BN_>
 __global__ void __launch_bounds__(GT) k_gemm(GemmArgs g) {
+  using T = GemmTile<BN_>;
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int ntm = (g.M + GBM - 1) / GBM, ntn = (g.N + GBN - 1) / GBN;
+  const int ntm = (g.M + GBM - 1) / GBM, ntn = (g.N + BN_ - 1) / BN_;
   const int tile = xcd_remap(blockIdx.x, ntm * ntn);
   const int tm = tile / ntn, tn = tile % ntn;
-  const int m0 = tm * GBM, n0 = tn * GBN;
+  const int m0 = tm * GBM, n0 = tn * BN_;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, wr = wave >> 1, wc = wave & 1;
   constexpr int ESZ = FP8 ? 1 : 2;
   const int ksplit = blockIdx.y;
@@ -225,63 +245,75 @@ __global__ void __launch_bounds__(GT) k_gemm(GemmArgs g) {
   constexpr int KT = GBK_BYTES / ESZ;  // elements per K-tile
   const int nk = (k_end - k_begin + KT - 1) / KT;
 
-  f32x4 acc[4][4];
+  f32x4 acc[4][T::NF];
 #pragma unroll
   for (int m = 0; m < 4; ++m)
 #pragma unroll
-    for (int n = 0; n < 4; ++n) acc[m][n] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int n = 0; n < T::NF; ++n) acc[m][n] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   ConvRows cr;
   ConvCols cc;
   if (g.conv == 1) conv_rows(cr, g, m0);
-  if (g.conv == 2) conv_cols(cc, g, n0);
-  auto load = [&](Stage& sa, Stage& sb, int kt) {
+  if constexpr (BN_ == 128) {
+    if (g.conv == 2) conv_cols(cc, g, n0);
+  }
+  using SB = StageT<BN_ / 32>;
+  auto load = [&](Stage& sa, SB& sb, int kt) {
     const int k0 = k_begin + kt * KT;
     if (g.conv == 1) load_conv_a(sa, (const unsigned short*)g.A, cr, g, k0, k_end);
     else if (g.ta) load_t(sa, (const unsigned short*)g.A, m0, g.M, g.lda, k0, k_end);
     else load_nt<ESZ>(sa, (const char*)g.A, m0, g.M, (size_t)g.lda * ESZ, k0 * ESZ, k_end * ESZ);
-    if (g.conv == 2) load_conv_b(sb, (const unsigned short*)g.B, cc, g, k0, k_end);
-    else if (g.tb) load_t(sb, (const unsigned short*)g.B, n0, g.N, g.ldb, k0, k_end);
-    else load_nt<ESZ>(sb, (const char*)g.B, n0, g.N, (size_t)g.ldb * ESZ, k0 * ESZ, k_end * ESZ);
+    if constexpr (BN_ == 128) {
+      if (g.conv == 2) load_conv_b(sb, (const unsigned short*)g.B, cc, g, k0, k_end);
+      else if (g.tb) load_t(sb, (const unsigned short*)g.B, n0, g.N, g.ldb, k0, k_end);
+      else load_nt<ESZ>(sb, (const char*)g.B, n0, g.N, (size_t)g.ldb * ESZ, k0 * ESZ, k_end * ESZ);
+    } else {
+      load_nt<ESZ, BN_ / 32>(sb, (const char*)g.B, n0, g.N, (size_t)g.ldb * ESZ, k0 * ESZ, k_end * ESZ);
+    }
   };
-  auto store = [&](const Stage& sa, const Stage& sb, int buf) {
-    char* la = smem + buf * 2 * G_TILE_BYTES;
+  auto store = [&](const Stage& sa, const SB& sb, int buf) {
+    char* la = smem + buf * T::BUF;
     char* lb = la + G_TILE_BYTES;
     if (g.ta && g.conv != 1) store_t(sa, la);
     else store_nt(sa, la);
-    if (g.tb || g.conv == 2) store_t(sb, lb);
-    else store_nt(sb, lb);
+    if constexpr (BN_ == 128) {
+      if (g.tb || g.conv == 2) store_t(sb, lb);
+      else store_nt(sb, lb);
+    } else {
+      store_nt<BN_ / 32>(sb, lb);
+    }
   };
 
-  Stage sa, sb;
+  Stage sa1;
+  SB sb1;
   if (nk > 0) {
-    load(sa, sb, 0);
-    store(sa, sb, 0);
+    load(sa1, sb1, 0);
+    store(sa1, sb1, 0);
   }
   __syncthreads();
   for (int kt = 0; kt < nk; ++kt) {
     const int buf = kt & 1;
-    if (kt + 1 < nk) load(sa, sb, kt + 1);  // global loads in flight during the MFMAs below
-    const char* la = smem + buf * 2 * G_TILE_BYTES;
+    if (kt + 1 < nk) load(sa1, sb1, kt + 1);  // global loads in flight during the MFMAs below
+    const char* la = smem + buf * T::BUF;
     const char* lb = la + G_TILE_BYTES;
     if constexpr (!FP8) {
 #pragma unroll
       for (int s = 0; s < 2; ++s) {
-        s16x8 af[4], bfr[4];
+        s16x8 af[4], bfr[T::NF];
 #pragma unroll
         for (int m = 0; m < 4; ++m)
           af[m] = *(const s16x8*)(la + lds_off(wr * 64 + m * 16 + (lane & 15), s * 4 + (lane >> 4)));
 #pragma unroll
-        for (int n = 0; n < 4; ++n)
-          bfr[n] = *(const s16x8*)(lb + lds_off(wc * 64 + n * 16 + (lane & 15), s * 4 + (lane >> 4)));
+        for (int n = 0; n < T::NF; ++n)
+          bfr[n] = *(const s16x8*)(lb + lds_off(wc * T::WCW + n * 16 + (lane & 15), s * 4 + (lane >> 4)));
 #pragma unroll
         for (int m = 0; m < 4; ++m)
 #pragma unroll
-          for (int n = 0; n < 4; ++n)
+          for (int n = 0; n < T::NF; ++n)
             acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[m], bfr[n], acc[m][n], 0, 0, 0);
       }
     } else {
-      i32x8 af[4], bfr[4];
+      i32x8 af[4], bfr[T::NF];
 #pragma unroll
       for (int m = 0; m < 4; ++m) {
         const int row = wr * 64 + m * 16 + (lane & 15), c = 2 * (lane >> 4);
@@ -289,18 +321,18 @@ __global__ void __launch_bounds__(GT) k_gemm(GemmArgs g) {
         af[m] = i32x8{(int)lo.x, (int)lo.y, (int)lo.z, (int)lo.w, (int)hi.x, (int)hi.y, (int)hi.z, (int)hi.w};
       }
 #pragma unroll
-      for (int n = 0; n < 4; ++n) {
-        const int row = wc * 64 + n * 16 + (lane & 15), c = 2 * (lane >> 4);
+      for (int n = 0; n < T::NF; ++n) {
+        const int row = wc * T::WCW + n * 16 + (lane & 15), c = 2 * (lane >> 4);
         const uint4 lo = *(const uint4*)(lb + lds_off(row, c)), hi = *(const uint4*)(lb + lds_off(row, c + 1));
         bfr[n] = i32x8{(int)lo.x, (int)lo.y, (int)lo.z, (int)lo.w, (int)hi.x, (int)hi.y, (int)hi.z, (int)hi.w};
       }
 #pragma unroll
       for (int m = 0; m < 4; ++m)
 #pragma unroll
-        for (int n = 0; n < 4; ++n)  // fp8 e4m3 x fp8 e4m3, unit E8M0 scales (127)
+        for (int n = 0; n < T::NF; ++n)  // fp8 e4m3 x fp8 e4m3, unit E8M0 scales (127)
           acc[m][n] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(af[m], bfr[n], acc[m][n], 0, 0, 0, 127, 0, 127);
     }
-    if (kt + 1 < nk) store(sa, sb, buf ^ 1);
+    if (kt + 1 < nk) store(sa1, sb1, buf ^ 1);
     __syncthreads();
   }
 
@@ -312,8 +344,8 @@ __global__ void __launch_bounds__(GT) k_gemm(GemmArgs g) {
 #pragma unroll
     for (int m = 0; m < 4; ++m)
 #pragma unroll
-      for (int n = 0; n < 4; ++n) {
-        const int col = n0 + wc * 64 + n * 16 + (lane & 15);
+      for (int n = 0; n < T::NF; ++n) {
+        const int col = n0 + wc * T::WCW + n * 16 + (lane & 15);
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
           const int row = m0 + wr * 64 + m * 16 + (lane >> 4) * 4 + j;
@@ -323,18 +355,19 @@ __global__ void __launch_bounds__(GT) k_gemm(GemmArgs g) {
     return;
   }
   float* ct = (float*)smem;
-  auto cidx = [](int r, int c) { return r * GBN + (c ^ (((r >> 2) & 3) << 4)); };
+  auto cidx = [](int r, int c) { return r * BN_ + (c ^ (((r >> 2) & 3) << 4)); };
 #pragma unroll
   for (int m = 0; m < 4; ++m)
 #pragma unroll
-    for (int n = 0; n < 4; ++n)
+    for (int n = 0; n < T::NF; ++n)
 #pragma unroll
       for (int j = 0; j < 4; ++j)
-        ct[cidx(wr * 64 + m * 16 + (lane >> 4) * 4 + j, wc * 64 + n * 16 + (lane & 15))] = acc[m][n][j];
+        ct[cidx(wr * 64 + m * 16 + (lane >> 4) * 4 + j, wc * T::WCW + n * 16 + (lane & 15))] = acc[m][n][j];
   __syncthreads();
   const float alpha = g.alpha * (g.alpha_dev ? *g.alpha_dev : 1.f);
-  // thread t: column group cg = t & 31 (4 columns), rows (t >> 5) + 8 r, r = 0..15
-  const int cg = threadIdx.x & 31, col0 = n0 + cg * 4;
+  // thread t: column group cg = t % CG (4 columns each), rows t / CG + RL * r
+  constexpr int CG = BN_ / 4, RL = GT / CG;
+  const int cg = threadIdx.x % CG, col0 = n0 + cg * 4;
   float bias4[4], shift4[4], s1[4] = {0.f, 0.f, 0.f, 0.f}, s2[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
   for (int e = 0; e < 4; ++e) {
@@ -343,8 +376,8 @@ __global__ void __launch_bounds__(GT) k_gemm(GemmArgs g) {
     shift4[e] = g.col_stats ? g.stats_shift[col] : 0.f;
   }
   const bool full4 = col0 + 4 <= g.N && (g.ldc & 3) == 0;
-  for (int r = 0; r < 16; ++r) {
-    const int lr = (threadIdx.x >> 5) + 8 * r, row = m0 + lr;
+  for (int r = 0; r < GBM / RL; ++r) {
+    const int lr = threadIdx.x / CG + RL * r, row = m0 + lr;
     if (row >= g.M || col0 >= g.N) continue;
     const f32x4 a = *(const f32x4*)(ct + cidx(lr, cg * 4));
     float v[4];
@@ -392,16 +425,16 @@ __global__ void __launch_bounds__(GT) k_gemm(GemmArgs g) {
   }
   if (g.col_stats) {  // combine the 8 row-lanes of each column group (fixed order), one float2 per column
     __syncthreads();
-    float2* red = (float2*)smem;  // [8 row lanes][128 cols]
+    float2* red = (float2*)smem;  // [RL row lanes][BN_ cols]
 #pragma unroll
-    for (int e = 0; e < 4; ++e) red[(threadIdx.x >> 5) * GBN + cg * 4 + e] = float2{s1[e], s2[e]};
+    for (int e = 0; e < 4; ++e) red[(threadIdx.x / CG) * BN_ + cg * 4 + e] = float2{s1[e], s2[e]};
     __syncthreads();
-    if (threadIdx.x < GBN) {
+    if (threadIdx.x < BN_) {
       const int col = n0 + threadIdx.x;
       float2 t = red[threadIdx.x];
-      for (int k = 1; k < 8; ++k) {
-        t.x += red[k * GBN + threadIdx.x].x;
-        t.y += red[k * GBN + threadIdx.x].y;
+      for (int k = 1; k < RL; ++k) {
+        t.x += red[k * BN_ + threadIdx.x].x;
+        t.y += red[k * BN_ + threadIdx.x].y;
       }
       if (col < g.N) g.col_stats[(size_t)tm * g.N + col] = t;
     }
