@@ -32,6 +32,7 @@ inline int grid_for(long work, int per_block = 256, int cap = 8192) {
   return (int)std::max(1L, std::min(b, (long)cap));
 }
 bool g_lds_set = false;
+inline int nparts_rows(long M) { return (int)((M + dca::ops::BN_ROWS - 1) / dca::ops::BN_ROWS); }
 }  // namespace
 
 using namespace dca::ops;
@@ -39,7 +40,7 @@ using namespace dca::ops;
 extern "C" {
 
 const char* dca_ops_last_error() { return g_err.c_str(); }
-int dca_ops_abi_version() { return 2; }
+int dca_ops_abi_version() { return 3; }
 
 // Must match ops/_native.py::GemmArgs.
 int dca_ops_gemm(const GemmArgs* a, void* stream) {
@@ -134,24 +135,31 @@ int dca_ops_bn_fwd(const void* x, const void* r, void* out, float* part, float* 
                      (int)M, C);
   hipLaunchKernelGGL(k_bn_finalize, dim3((C + 15) / 16), dim3(256), 0, st, (const float2*)part, nparts, (int)M, C,
                      rm, rv, (float2*)stats, eps, momentum);
-  hipLaunchKernelGGL(k_bn_apply, dim3(grid_for(M * C / 8)), dim3(256), 0, st, (const bf16_t*)x, (const bf16_t*)r,
-                     (bf16_t*)out, (const float2*)stats, gamma, beta, M, C, relu, res_mode);
+  hipLaunchKernelGGL(k_bn_apply, dim3((C + 63) / 64, nparts_rows(M)), dim3(256), 0, st, (const bf16_t*)x, (const bf16_t*)r,
+                     (bf16_t*)out, (const float2*)stats, gamma, beta, M, C, relu, res_mode, (uint8_t*)nullptr,
+                     (const float*)nullptr, (unsigned*)nullptr);
   OPCK(hipGetLastError());
   return 0;
 }
 
 // BatchNorm forward when the per-tile column partials were produced by the GEMM epilogue (col_stats): finalize
 // over `nparts` partial rows + apply.
+// q / amax_prev / amax_out (optional): also write an fp8 copy of the output with delayed scaling (k_bn_apply);
+// amax_out is zeroed here first.
 int dca_ops_bn_fwd_parts(const void* x, const void* r, void* out, const float* part, int nparts, float* stats,
                          const float* gamma, const float* beta, float* rm, float* rv, long M, int C, float eps,
-                         float momentum, int relu, int res_mode, void* stream) {
+                         float momentum, int relu, int res_mode, void* q, const float* amax_prev, unsigned* amax_out,
+                         void* stream) {
   REQUIRE(C % 8 == 0, "bn: C must be a multiple of 8");
   REQUIRE(res_mode == 0 || r != nullptr, "bn: residual missing");
+  REQUIRE(!q || (amax_prev && amax_out), "bn: fp8 output needs amax_prev and amax_out");
   hipStream_t st = (hipStream_t)stream;
+  if (q) OPCK(hipMemsetAsync(amax_out, 0, sizeof(unsigned), st));
   hipLaunchKernelGGL(k_bn_finalize, dim3((C + 15) / 16), dim3(256), 0, st, (const float2*)part, nparts, (int)M, C,
                      rm, rv, (float2*)stats, eps, momentum);
-  hipLaunchKernelGGL(k_bn_apply, dim3(grid_for(M * C / 8)), dim3(256), 0, st, (const bf16_t*)x, (const bf16_t*)r,
-                     (bf16_t*)out, (const float2*)stats, gamma, beta, M, C, relu, res_mode);
+  hipLaunchKernelGGL(k_bn_apply, dim3((C + 63) / 64, nparts_rows(M)), dim3(256), 0, st, (const bf16_t*)x, (const bf16_t*)r,
+                     (bf16_t*)out, (const float2*)stats, gamma, beta, M, C, relu, res_mode, (uint8_t*)q, amax_prev,
+                     amax_out);
   OPCK(hipGetLastError());
   return 0;
 }
@@ -168,7 +176,7 @@ int dca_ops_bn_bwd(const void* dy, const void* x, const void* r, const float* st
                      relu, res_mode);
   hipLaunchKernelGGL(k_bn_bwd_finalize, dim3((C + 15) / 16), dim3(256), 0, st, (const float2*)part, nparts, C,
                      dgamma, dbeta, (float2*)sums, accumulate);
-  hipLaunchKernelGGL(k_bn_bwd_apply, dim3(grid_for(M * C / 8)), dim3(256), 0, st, (const bf16_t*)dy, (const bf16_t*)x,
+  hipLaunchKernelGGL(k_bn_bwd_apply, dim3((C + 63) / 64, nparts_rows(M)), dim3(256), 0, st, (const bf16_t*)dy, (const bf16_t*)x,
                      (const bf16_t*)r, (const float2*)stats, gamma, beta, (const float2*)sums, (bf16_t*)dx,
                      (bf16_t*)dr, M, C, relu, res_mode);
   OPCK(hipGetLastError());
@@ -186,7 +194,7 @@ int dca_ops_maxpool_fwd(const void* x, void* y, void* arg, const PoolGeom* geom,
 
 int dca_ops_maxpool_bwd(const void* dy, const void* arg, void* dx, const PoolGeom* geom, void* stream) {
   const PoolGeom g = *geom;
-  hipLaunchKernelGGL(k_maxpool_bwd, dim3(grid_for((long)g.N * g.H * g.W * g.C)), dim3(256), 0, (hipStream_t)stream,
+  hipLaunchKernelGGL(k_maxpool_bwd, dim3(grid_for((long)g.N * g.H * g.W * g.C / ((g.C & 7) == 0 ? 8 : 1))), dim3(256), 0, (hipStream_t)stream,
                      (const bf16_t*)dy, (const uint8_t*)arg, (bf16_t*)dx, g);
   OPCK(hipGetLastError());
   return 0;

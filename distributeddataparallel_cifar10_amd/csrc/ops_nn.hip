@@ -189,62 +189,124 @@ __device__ __forceinline__ uint4 pack8(const float* f) {
 }
 
 // out = fused(x); vectorised by 8 channels (C % 8 == 0)
+// Optionally also emits an fp8 e4m3 copy of the output for an fp8 consumer GEMM, with DELAYED scaling: the scale
+// 448 / amax comes from the previous step's amax of this tensor (amax_prev), and this step's amax is recorded in
+// amax_out for the next step -- no extra pass over the activation, no host sync.
 __global__ void __launch_bounds__(256) k_bn_apply(const bf16_t* __restrict__ x, const bf16_t* __restrict__ r,
                                                   bf16_t* __restrict__ out, const float2* __restrict__ stats,
                                                   const float* __restrict__ gamma, const float* __restrict__ beta,
-                                                  long M, int C, int relu, int res_mode) {
-  const int cg = C >> 3;
-  const long total = M * cg;
-  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < total; i += (long)gridDim.x * 256) {
-    const int c0 = (int)(i % cg) * 8;
-    float v[8], rv[8];
-    unpack8(*(const uint4*)(x + i * 8), v);
-    if (res_mode) unpack8(*(const uint4*)(r + i * 8), rv);
+                                                  long M, int C, int relu, int res_mode, uint8_t* __restrict__ q,
+                                                  const float* __restrict__ amax_prev, unsigned* __restrict__ amax_out) {
+  // grid (ceil(C/64), ceil(M/BN_ROWS)): 8 channel groups x 32 row lanes, z = x * sc + sh per channel
+  __shared__ float red[256];
+  const int cgl = threadIdx.x & 7, rl = threadIdx.x >> 3, c0 = blockIdx.x * 64 + cgl * 8;
+  const long r0 = (long)blockIdx.y * BN_ROWS;
+  float qs = 1.f, amax = 0.f;
+  if (q) qs = *amax_prev > 0.f ? 448.f / *amax_prev : 1.f;
+  if (c0 < C) {
+    float sc[8], sh[8];
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       const float2 st = stats[c0 + j];
-      float z = (v[j] - st.x) * st.y * gamma[c0 + j] + beta[c0 + j];
-      if (res_mode == 2) z += rv[j];
-      if (relu) z = z > 0.f ? z : 0.f;
-      if (res_mode == 1) z += rv[j];
-      v[j] = z;
+      sc[j] = st.y * gamma[c0 + j];
+      sh[j] = beta[c0 + j] - st.x * sc[j];
     }
-    *(uint4*)(out + i * 8) = pack8(v);
+    const long rend = M < r0 + BN_ROWS ? M : r0 + BN_ROWS;
+    for (long row = r0 + rl; row < rend; row += 32) {
+      const long o = row * C + c0;
+      float v[8], rv[8];
+      unpack8(*(const uint4*)(x + o), v);
+      if (res_mode) unpack8(*(const uint4*)(r + o), rv);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        float z = v[j] * sc[j] + sh[j];
+        if (res_mode == 2) z += rv[j];
+        if (relu) z = z > 0.f ? z : 0.f;
+        if (res_mode == 1) z += rv[j];
+        v[j] = z;
+      }
+      const uint4 ov = pack8(v);
+      *(uint4*)(out + o) = ov;
+      if (q) {
+        float f[8];
+        unpack8(ov, f);  // quantise the value as stored (bf16)
+        int w[2];
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          float c[4];
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            amax = fmaxf(amax, fabsf(f[4 * h + j]));
+            c[j] = fminf(fmaxf(f[4 * h + j] * qs, -448.f), 448.f);
+          }
+          w[h] = __builtin_amdgcn_cvt_pk_fp8_f32(c[0], c[1], 0, false);
+          w[h] = __builtin_amdgcn_cvt_pk_fp8_f32(c[2], c[3], w[h], true);
+        }
+        *(uint2*)(q + o) = uint2{(unsigned)w[0], (unsigned)w[1]};
+      }
+    }
+  }
+  if (q) {
+    red[threadIdx.x] = amax;
+    __syncthreads();
+    for (int o = 128; o; o >>= 1) {
+      if (threadIdx.x < o) red[threadIdx.x] = fmaxf(red[threadIdx.x], red[threadIdx.x + o]);
+      __syncthreads();
+    }
+    if (threadIdx.x == 0) atomicMax(amax_out, __float_as_uint(red[0]));
   }
 }
 
 // dz = dy * act'(.) recomputed from x (and r); partial sums of dz and dz * xhat per channel.
+// grid (ceil(C/64), ceil(M/BN_ROWS)); 256 threads = 8 channel groups (8 channels, one 16-B load per tensor per
+// row) x 32 row lanes; all rows' loads of a thread are independent (issued back to back).
 __global__ void __launch_bounds__(256) k_bn_bwd_stats(const bf16_t* __restrict__ dy, const bf16_t* __restrict__ x,
                                                       const bf16_t* __restrict__ r, const float2* __restrict__ stats,
                                                       const float* __restrict__ gamma, const float* __restrict__ beta,
                                                       float2* __restrict__ part, int M, int C, int relu, int res_mode) {
-  __shared__ float2 red[4][64];
-  const int cl = threadIdx.x & 63, rl = threadIdx.x >> 6, c = blockIdx.x * 64 + cl;
+  __shared__ float2 red[32][64];
+  const int cgl = threadIdx.x & 7, rl = threadIdx.x >> 3, c0 = blockIdx.x * 64 + cgl * 8;
   const int r0 = blockIdx.y * BN_ROWS;
-  float s = 0.f, q = 0.f;
-  if (c < C) {
-    const float2 st = stats[c];
-    const float ga = gamma[c], be = beta[c];
-    for (int row = r0 + rl; row < min(M, r0 + BN_ROWS); row += 4) {
-      const long o = (long)row * C + c;
-      const float xh = (ld_bf(x + o) - st.x) * st.y;
-      float d = ld_bf(dy + o);
-      if (relu) {
-        float z = xh * ga + be;
-        if (res_mode == 2) z += ld_bf(r + o);
-        d = z > 0.f ? d : 0.f;
+  float s[8], q[8], mu[8], is[8], ga[8], be[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int c = min(c0 + j, C - 1);
+    s[j] = q[j] = 0.f;
+    mu[j] = stats[c].x;
+    is[j] = stats[c].y;
+    ga[j] = gamma[c];
+    be[j] = beta[c];
+  }
+  if (c0 < C) {
+    for (int row = r0 + rl; row < min(M, r0 + BN_ROWS); row += 32) {
+      const long o = (long)row * C + c0;
+      float xv[8], dv[8], rv[8];
+      unpack8(*(const uint4*)(x + o), xv);
+      unpack8(*(const uint4*)(dy + o), dv);
+      if (res_mode == 2) unpack8(*(const uint4*)(r + o), rv);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float xh = (xv[j] - mu[j]) * is[j];
+        float d = dv[j];
+        if (relu) {
+          float z = xh * ga[j] + be[j];
+          if (res_mode == 2) z += rv[j];
+          d = z > 0.f ? d : 0.f;
+        }
+        s[j] += d;
+        q[j] += d * xh;
       }
-      s += d;
-      q += d * xh;
     }
   }
-  red[rl][cl] = float2{s, q};
+#pragma unroll
+  for (int j = 0; j < 8; ++j) red[rl][cgl * 8 + j] = float2{s[j], q[j]};
   __syncthreads();
-  if (rl == 0 && c < C) {
-    float2 a = red[0][cl];
-    for (int j = 1; j < 4; ++j) {
-      a.x += red[j][cl].x;
-      a.y += red[j][cl].y;
+  const int c = blockIdx.x * 64 + threadIdx.x;
+  if (threadIdx.x < 64 && c < C) {
+    float2 a = red[0][threadIdx.x];
+    for (int k = 1; k < 32; ++k) {
+      a.x += red[k][threadIdx.x].x;
+      a.y += red[k][threadIdx.x].y;
     }
     part[(long)blockIdx.y * C + c] = a;
   }
@@ -264,37 +326,51 @@ __global__ void __launch_bounds__(256) k_bn_bwd_finalize(const float2* __restric
   dbeta[c] = accumulate ? dbeta[c] + a.x : a.x;
 }
 
-// dx = gamma * invstd * (dz - mean(dz) - xhat * mean(dz * xhat)); res_mode 2 also writes dr = dz
+// dx = gamma * invstd * (dz - mean(dz) - xhat * mean(dz * xhat)); res_mode 2 also writes dr = dz.
+// grid (ceil(C/64), ceil(M/BN_ROWS)): 8 channel groups x 32 row lanes, per-channel coefficients folded once per
+// thread (dx = A*dz + B*x + D), one 16-B load / store per tensor per row.
 __global__ void __launch_bounds__(256) k_bn_bwd_apply(const bf16_t* __restrict__ dy, const bf16_t* __restrict__ x,
                                                       const bf16_t* __restrict__ r, const float2* __restrict__ stats,
                                                       const float* __restrict__ gamma, const float* __restrict__ beta,
                                                       const float2* __restrict__ sums, bf16_t* __restrict__ dx,
                                                       bf16_t* __restrict__ dr, long M, int C, int relu, int res_mode) {
-  const int cg = C >> 3;
-  const long total = M * cg;
+  const int cgl = threadIdx.x & 7, rl = threadIdx.x >> 3, c0 = blockIdx.x * 64 + cgl * 8;
+  if (c0 >= C) return;
+  const long r0 = (long)blockIdx.y * BN_ROWS;
   const float inv_m = 1.f / (float)M;
-  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < total; i += (long)gridDim.x * 256) {
-    const int c0 = (int)(i % cg) * 8;
+  float mu[8], is[8], ga[8], be[8], ca[8], cb[8], cd[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const float2 st = stats[c0 + j], sm = sums[c0 + j];
+    mu[j] = st.x;
+    is[j] = st.y;
+    ga[j] = gamma[c0 + j];
+    be[j] = beta[c0 + j];
+    // dx = g*is*(dz - sx/M - (x - mu)*is * sy/M) = ca*dz + cb*x + cd
+    ca[j] = ga[j] * is[j];
+    cb[j] = -ca[j] * is[j] * sm.y * inv_m;
+    cd[j] = -ca[j] * sm.x * inv_m - cb[j] * mu[j];
+  }
+  const long rend = M < r0 + BN_ROWS ? M : r0 + BN_ROWS;
+  for (long row = r0 + rl; row < rend; row += 32) {
+    const long o = row * C + c0;
     float xv[8], d[8], rv[8];
-    unpack8(*(const uint4*)(x + i * 8), xv);
-    unpack8(*(const uint4*)(dy + i * 8), d);
-    if (res_mode == 2) unpack8(*(const uint4*)(r + i * 8), rv);
+    unpack8(*(const uint4*)(x + o), xv);
+    unpack8(*(const uint4*)(dy + o), d);
+    if (res_mode == 2) unpack8(*(const uint4*)(r + o), rv);
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-      const int c = c0 + j;
-      const float2 st = stats[c], sm = sums[c];
-      const float xh = (xv[j] - st.x) * st.y;
       float dz = d[j];
       if (relu) {
-        float z = xh * gamma[c] + beta[c];
+        float z = (xv[j] - mu[j]) * is[j] * ga[j] + be[j];
         if (res_mode == 2) z += rv[j];
         dz = z > 0.f ? dz : 0.f;
       }
       rv[j] = dz;
-      d[j] = gamma[c] * st.y * (dz - sm.x * inv_m - xh * sm.y * inv_m);
+      d[j] = ca[j] * dz + cb[j] * xv[j] + cd[j];
     }
-    *(uint4*)(dx + i * 8) = pack8(d);
-    if (res_mode == 2) *(uint4*)(dr + i * 8) = pack8(rv);
+    *(uint4*)(dx + o) = pack8(d);
+    if (res_mode == 2) *(uint4*)(dr + o) = pack8(rv);
   }
 }
 
@@ -332,14 +408,17 @@ __global__ void __launch_bounds__(256) k_maxpool_fwd(const bf16_t* __restrict__ 
   }
 }
 
+// one thread per input pixel and 8 channels (C % 8 == 0: 16-B dy loads, 8-B argmax loads), else per element
 __global__ void __launch_bounds__(256) k_maxpool_bwd(const bf16_t* __restrict__ dy, const uint8_t* __restrict__ arg,
                                                      bf16_t* __restrict__ dx, PoolGeom g) {
-  const long total = (long)g.N * g.H * g.W * g.C;
+  const int vec = (g.C & 7) == 0 ? 8 : 1;
+  const int cgs = g.C / vec;
+  const long total = (long)g.N * g.H * g.W * cgs;
   for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < total; i += (long)gridDim.x * 256) {
-    const int c = (int)(i % g.C);
-    const long p = i / g.C;
+    const int c = (int)(i % cgs) * vec;
+    const long p = i / cgs;
     const int w = (int)(p % g.W), h = (int)((p / g.W) % g.H), n = (int)(p / ((long)g.W * g.H));
-    float s = 0.f;
+    float s[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
     for (int kh = 0; kh < g.K; ++kh) {
       const int th = h + g.P - kh;
       if (th < 0 || th % g.S) continue;
@@ -351,10 +430,24 @@ __global__ void __launch_bounds__(256) k_maxpool_bwd(const bf16_t* __restrict__ 
         const int ow = tw / g.S;
         if (ow >= g.Wo) continue;
         const long o = (((long)n * g.Ho + oh) * g.Wo + ow) * g.C + c;
-        if (arg[o] == kh * g.K + kw) s += ld_bf(dy + o);
+        const int tap = kh * g.K + kw;
+        if (vec == 8) {
+          float d[8];
+          unpack8(*(const uint4*)(dy + o), d);
+          const uint2 a = *(const uint2*)(arg + o);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            const unsigned aj = ((j < 4 ? a.x : a.y) >> ((j & 3) * 8)) & 0xffu;
+            s[j] += aj == (unsigned)tap ? d[j] : 0.f;
+          }
+        } else if (arg[o] == tap) {
+          s[0] += ld_bf(dy + o);
+        }
       }
     }
-    dx[i] = f2bf_rne(s);
+    const long xo = p * g.C + c;
+    if (vec == 8) *(uint4*)(dx + xo) = pack8(s);
+    else dx[xo] = f2bf_rne(s[0]);
   }
 }
 

@@ -13,7 +13,7 @@ import torch
 
 from .. import build as _build
 
-ABI_VERSION = 2
+ABI_VERSION = 3
 _lock = threading.Lock()
 _lib = None
 
@@ -51,7 +51,8 @@ def _declare(lib):
     lib.dca_ops_bn_fwd.argtypes = [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                                    c_void_p, c_long, c_int, c_float, c_float, c_int, c_int, c_void_p]
     lib.dca_ops_bn_fwd_parts.argtypes = [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_void_p,
-                                         c_void_p, c_void_p, c_long, c_int, c_float, c_float, c_int, c_int, c_void_p]
+                                         c_void_p, c_void_p, c_long, c_int, c_float, c_float, c_int, c_int, c_void_p,
+                                         c_void_p, c_void_p, c_void_p]
     lib.dca_ops_bn_bwd.argtypes = [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                                    c_void_p, c_void_p, c_void_p, c_void_p, c_long, c_int, c_int, c_int, c_int,
                                    c_void_p]

@@ -180,7 +180,40 @@ def _implicit_ok(g) -> bool:
     return g.C % 8 == 0
 
 
-def _conv_fwd(x, w, b, stride, pad, relu, fp8, col_stats=None, shift=None):
+class Fp8Delayed:
+    """Delayed-scaling fp8 state of ONE activation tensor feeding ONE fp8 GEMM (Transformer-Engine style).
+
+    The producer (a fused BN apply) writes the fp8 copy with scale 448 / amax_prev -- the previous step's amax --
+    and records this step's amax; the consumer GEMM dequantises with amax_prev, then promotes the new amax for the
+    next step.  All on the device: no host sync, no extra pass over the activation.  Before the first amax is
+    known the consumer quantises the tensor itself (``quantize_fp8``) and seeds the state."""
+
+    def __init__(self):
+        self.amax_prev = None   # fp32 [1]
+        self.amax_out = None    # int32 [1] (float bits) written by the producer
+        self.q = None           # fp8 copy emitted for the current step
+        self.src_ptr = 0        # data_ptr of the bf16 tensor it is a copy of
+
+    @property
+    def ready(self) -> bool:
+        return self.amax_prev is not None
+
+
+def _fp8_operand(cols, state: Optional["Fp8Delayed"]):
+    """(q, amax bits) of the activation operand: the producer's delayed-scaled copy when there is one."""
+    if state is not None and state.q is not None and state.src_ptr == cols.data_ptr() \
+            and state.q.numel() == cols.numel():
+        q, bits = state.q.view(cols.shape), state.amax_prev.view(torch.int32)
+        state.q = None
+        return q, bits, True
+    q, bits = quantize_fp8(cols)
+    if state is not None and not state.ready:
+        state.amax_prev = bits.view(torch.float32).clone()
+        state.amax_out = torch.zeros(1, dtype=torch.int32, device=cols.device)
+    return q, bits, False
+
+
+def _conv_fwd(x, w, b, stride, pad, relu, fp8, col_stats=None, shift=None, fp8_state=None):
     """Forward GEMM of a conv; returns (y [N,Ho,Wo,Cout] bf16, state for _conv_bwd)."""
     x = x.contiguous()
     g = _geom(x, w, stride, pad)
@@ -198,10 +231,12 @@ def _conv_fwd(x, w, b, stride, pad, relu, fp8, col_stats=None, shift=None):
         st["cols"] = cols
         wm = _weight_matrix(w, g.Kp)
         if use_fp8:
-            qc, ac = quantize_fp8(cols)
+            qc, ac, delayed = _fp8_operand(cols, fp8_state)
             qw, aw = quantize_fp8(wm)
             y = gemm(qc, qw, bias=b, relu=relu, out_dtype=torch.bfloat16, alpha_dev=fp8_alpha(ac, aw),
                      col_stats=col_stats, stats_shift=shift)
+            if delayed:  # this step's amax (recorded by the producer) scales the next step
+                fp8_state.amax_prev.copy_(fp8_state.amax_out.view(torch.float32))
         else:
             y = gemm(cols, wm, bias=b, relu=relu, out_dtype=torch.bfloat16, col_stats=col_stats, stats_shift=shift)
     else:  # implicit GEMM: the im2col matrix is never materialised
@@ -273,21 +308,30 @@ class _ConvBNAct(torch.autograd.Function):
     GEMM's epilogue (no separate statistics pass over the conv output)."""
 
     @staticmethod
-    def forward(ctx, x, w, r, gamma, beta, running_mean, running_var, stride, pad, eps, momentum, relu, res_mode, fp8):
+    def forward(ctx, x, w, r, gamma, beta, running_mean, running_var, stride, pad, eps, momentum, relu, res_mode, fp8,
+                fp8_state, emit):
         co = w.shape[0]
         g = _geom(x, w, stride, pad)
         M = g.N * g.Ho * g.Wo
         nparts = (M + 127) // 128
         part = torch.empty(nparts, co, 2, dtype=torch.float32, device=x.device)
-        y, st = _conv_fwd(x, w, None, stride, pad, False, fp8, col_stats=part, shift=running_mean)
+        y, st = _conv_fwd(x, w, None, stride, pad, False, fp8, col_stats=part, shift=running_mean,
+                          fp8_state=fp8_state)
         st["w_master"] = w.detach()
         r = r.contiguous() if r is not None else None
         out = torch.empty_like(y)
         stats = torch.empty(co, 2, dtype=torch.float32, device=x.device)
+        q = None
+        if emit is not None and emit.ready:  # fp8 copy of the output for the next (fp8) GEMM, delayed scaling
+            q = torch.empty(out.shape, dtype=torch.uint8, device=x.device)
         N.check(N.lib().dca_ops_bn_fwd_parts(N.ptr(y), N.ptr(r), N.ptr(out), N.ptr(part), nparts, N.ptr(stats),
                                              N.ptr(gamma), N.ptr(beta), N.ptr(running_mean), N.ptr(running_var), M, co,
-                                             float(eps), float(momentum), int(relu), int(res_mode),
+                                             float(eps), float(momentum), int(relu), int(res_mode), N.ptr(q),
+                                             N.ptr(emit.amax_prev) if q is not None else None,
+                                             N.ptr(emit.amax_out) if q is not None else None,
                                              N.stream(x.device)), "bn_fwd_parts")
+        if q is not None:
+            emit.q, emit.src_ptr = q, out.data_ptr()
         ctx.st = st
         ctx.save_for_backward(y, r, gamma, beta, stats)
         ctx.relu, ctx.res_mode = relu, res_mode
@@ -299,12 +343,14 @@ class _ConvBNAct(torch.autograd.Function):
         dy_conv, dr, dgamma, dbeta = _bn_backward(dout, y, r, gamma, beta, stats, ctx.relu, ctx.res_mode)
         dx, dw = _conv_bwd(dy_conv, ctx.st, ctx.needs_input_grad[0], ctx.needs_input_grad[1])
         ctx.st = None
-        return dx, dw, dr, dgamma, dbeta, None, None, None, None, None, None, None, None, None
+        return dx, dw, dr, dgamma, dbeta, None, None, None, None, None, None, None, None, None, None, None
 
 
-def conv_bn_act(x, conv: torch.nn.Conv2d, bn: torch.nn.BatchNorm2d, r=None, relu=True, fp8=False, res_mode=None):
+def conv_bn_act(x, conv: torch.nn.Conv2d, bn: torch.nn.BatchNorm2d, r=None, relu=True, fp8=False, res_mode=None,
+                fp8_state: Optional[Fp8Delayed] = None, emit: Optional[Fp8Delayed] = None):
     """Training-mode act(bn(conv(x))) for NHWC bf16 x, conv without bias; with a residual r: res_mode 2 (default,
-    ResNet: act(bn + r)) or 1 (NetResDeep: act(bn) + r)."""
+    ResNet: act(bn + r)) or 1 (NetResDeep: act(bn) + r).  fp8: forward GEMM in fp8 e4m3 (fp8_state: this conv's
+    delayed-scaling input state); emit: also produce the fp8 copy of the output that the consumer of ``emit`` reads."""
     if res_mode is None:
         res_mode = 2 if r is not None else 0
     if conv.bias is not None or not bn.training:
@@ -313,7 +359,7 @@ def conv_bn_act(x, conv: torch.nn.Conv2d, bn: torch.nn.BatchNorm2d, r=None, relu
     if bn.track_running_stats:
         bn.num_batches_tracked.add_(1)
     return _ConvBNAct.apply(x, conv.weight, r, bn.weight, bn.bias, bn.running_mean, bn.running_var, conv.stride[0],
-                            conv.padding[0], bn.eps, momentum, relu, res_mode, fp8)
+                            conv.padding[0], bn.eps, momentum, relu, res_mode, fp8, fp8_state, emit)
 
 
 def conv2d(x, w, b=None, stride=1, pad=0, relu=False, fp8=False):

@@ -151,7 +151,7 @@ def train_loop(model, train_loader: DeviceLoader, rank: int, cfg: Optional[Train
             optimizer = FlatSGD(model, cfg.lr) if isinstance(model, FlatBucketDDP) else \
                 torch.optim.SGD(model.parameters(), lr=cfg.lr)
     from contextlib import ExitStack
-    from torch.profiler import record_function
+    from .utils.trace import trace_range as record_function  # torch.profiler + roctx ranges
     from .parallel.dist import assert_params_in_sync
     autocast = (not fused and not on_ops and cfg.dtype == "bf16" and train_loader.device.type == "cuda"
                 and not _is_netresdeep(unwrap(model)))  # generic models train in bf16; NetResDeep torch path = fp32

@@ -52,3 +52,11 @@ def test_export_is_cpu_and_detached():
     m = NetResDeep()
     sd = export_state_dict(m)
     assert all(t.device.type == "cpu" and not t.requires_grad for t in sd.values())
+
+
+def test_trace_range_nests_and_never_fails():
+    from distributeddataparallel_cifar10_amd.utils.trace import trace_range
+    with trace_range("outer"):
+        with trace_range("inner"):
+            x = 1 + 1
+    assert x == 2
