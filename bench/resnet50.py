@@ -31,7 +31,7 @@ def main() -> int:
     ap.add_argument("--image", type=int, default=224)
     ap.add_argument("--bucket-mb", type=float, default=8.0)
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
-    ap.add_argument("--path", default="torch", choices=["torch", "ops"],
+    ap.add_argument("--path", default="ops", choices=["torch", "ops"],
                     help="torch: stock conv/BN (MIOpen) under bf16 autocast; ops: the framework's HIP kernels "
                          "(MFMA GEMM convs, fused BN+ReLU+residual, fused CE, HIP SGD)")
     ap.add_argument("--fp8", action="store_true", help="ops path: fp8 e4m3 forward GEMMs for 1x1 convs and fc")

@@ -803,6 +803,36 @@ int dca_engine_ipc_selftest(void* h, const float* src, float* dst, float timeout
   return 0;
 }
 
+// comm_mode 2 protocol latency: `iters` back-to-back all-reduces (no SGD) of FLAT_N floats; writes the mean
+// microseconds per all-reduce (HIP events around the loop).  Collective: every rank must call it.
+int dca_engine_ipc_bench(void* h, const float* src, float* dst, int iters, float* us) {
+  Engine* e = (Engine*)h;
+  if (!e->peers_open || iters < 1) {
+    g_err = "ipc_bench: peers not mapped or iters < 1";
+    return -1;
+  }
+  hipEvent_t a, b;
+  HIPCK(hipEventCreate(&a));
+  HIPCK(hipEventCreate(&b));
+  HIPCK(hipEventRecord(a, e->st));
+  for (int i = 0; i < iters; ++i) {
+    if (e->bf)
+      hipLaunchKernelGGL(dca::xg::k_xgmi_ar_sgd<true>, dim3(dca::xg::AR_NB), dim3(dca::xg::AR_T), 0, e->st,
+                         e->base, e->peers, src, dst, e->pa.err + 1, 0, e->ar_deadline);
+    else
+      hipLaunchKernelGGL(dca::xg::k_xgmi_ar_sgd<false>, dim3(dca::xg::AR_NB), dim3(dca::xg::AR_T), 0, e->st,
+                         e->base, e->peers, src, dst, e->pa.err + 1, 0, e->ar_deadline);
+  }
+  HIPCK(hipEventRecord(b, e->st));
+  HIPCK(hipEventSynchronize(b));
+  float ms = 0.f;
+  HIPCK(hipEventElapsedTime(&ms, a, b));
+  *us = 1e3f * ms / (float)iters;
+  (void)hipEventDestroy(a);
+  (void)hipEventDestroy(b);
+  return 0;
+}
+
 // comm_mode 1: one part of a step, eager (see enqueue_step_persistent)
 int dca_engine_run_part(void* h, int B, int part) {
   Engine* e = (Engine*)h;

@@ -213,6 +213,17 @@ class NetResDeepEngine:
         expect = base * float(w * (w + 1) // 2)
         return not timed_out.value and bool(torch.equal(dst, expect))
 
+    def xgmi_bench(self, iters: int = 200) -> float:
+        """Collective: mean microseconds per xGMI all-reduce of the flat gradient (protocol + data, no SGD)."""
+        src = torch.ones(FLAT_N, device=self.device)
+        dst = torch.empty_like(src)
+        torch.cuda.synchronize(self.device)
+        us = ctypes.c_float()
+        native.check(self.lib.dca_engine_ipc_bench(self.h, src.data_ptr(), dst.data_ptr(), int(iters),
+                                                   ctypes.byref(us)), "dca_engine_ipc_bench")
+        self.check_errors()
+        return float(us.value)
+
     # ---- data order -----------------------------------------------------------------------------------------
     def set_indices(self, indices) -> None:
         idx = np.ascontiguousarray(np.asarray(indices, dtype=np.int32))
