@@ -39,5 +39,24 @@ def main():
     dist.destroy_process_group()
 
 
+
+
+def single_process(ws_list=(1, 2, 3), iters=500):
+    """Protocol cost with W ranks simulated in ONE process (co-resident kernels on W streams): the lower bound of
+    what the all-reduce adds per step, free of the cross-process scheduling of a shared GPU."""
+    import ctypes
+    from distributeddataparallel_cifar10_amd.runtime import native
+    lib = native.require_native()
+    torch.cuda.init()
+    for w in ws_list:
+        us, err = ctypes.c_float(), ctypes.c_int()
+        native.check(lib.dca_microbench_xgmi(w, iters, ctypes.byref(us), ctypes.byref(err)), "microbench_xgmi")
+        print(json.dumps({"ranks_in_process": w, "us_per_allreduce": round(us.value, 2), "timeout": bool(err.value),
+                          "bytes": 76140 * 4}), flush=True)
+
+
 if __name__ == "__main__":
-    main()
+    if "--single-process" in sys.argv:
+        single_process()
+    else:
+        main()

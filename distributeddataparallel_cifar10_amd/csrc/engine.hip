@@ -902,6 +902,79 @@ int dca_microbench_xchg(int G, int nth, int rounds, int iters, int sleep, float*
   return 0;
 }
 
+// xGMI all-reduce protocol cost without peers in other processes: W ranks simulated in THIS process, one
+// stream and one uncached region each (so all ranks' kernels are co-resident, as on W separate GPUs), `iters`
+// all-reduces of FLAT_N floats per rank.  Writes mean microseconds per all-reduce; *err_out = timeout flag.
+int dca_microbench_xgmi(int W, int iters, float* us, int* err_out) {
+  // W <= 3: with GPU_MAX_HW_QUEUES=4 a 4th user stream can share a hardware queue with another, which serialises
+  // two ranks' kernels and deadlocks the flag wait until its deadline (measured: the W=4 run never finished).
+  if (W < 1 || W > dca::xg::MAXR || W > 3 || iters < 1) {
+    g_err = "microbench_xgmi: 1 <= W <= 3 (co-resident streams per process), iters >= 1";
+    return -1;
+  }
+  hipStream_t st[3];
+  char* reg[3];
+  float *src, *dst;
+  unsigned* err;
+  dca::xg::Peers P{};
+  for (int q = 0; q < W; ++q) {
+    HIPCK(hipStreamCreateWithFlags(&st[q], hipStreamNonBlocking));
+    HIPCK(hipExtMallocWithFlags((void**)&reg[q], dca::xg::REGION_BYTES, hipDeviceMallocUncached));
+    HIPCK(hipMemset(reg[q], 0, dca::xg::REGION_BYTES));
+    P.base[q] = reg[q];
+  }
+  HIPCK(hipMalloc(&src, sizeof(float) * dca::FLAT_ALLOC * W));
+  HIPCK(hipMalloc(&dst, sizeof(float) * dca::FLAT_ALLOC * W));
+  HIPCK(hipMemset(src, 0, sizeof(float) * dca::FLAT_ALLOC * W));
+  HIPCK(hipMalloc(&err, 16));
+  HIPCK(hipMemset(err, 0, 16));
+  HIPCK(hipDeviceSynchronize());
+  hipEvent_t a, b;
+  HIPCK(hipEventCreate(&a));
+  HIPCK(hipEventCreate(&b));
+  float best = 1e30f;
+  for (int rep = 0; rep < 3; ++rep) {
+    HIPCK(hipDeviceSynchronize());
+    HIPCK(hipEventRecord(a, st[0]));
+    for (int q = 1; q < W; ++q) HIPCK(hipStreamWaitEvent(st[q], a, 0));
+    for (int i = 0; i < iters; ++i)
+      for (int q = 0; q < W; ++q) {
+        dca::Ctx cx{};
+        cx.ws = W;
+        cx.rank = q;
+        hipLaunchKernelGGL(dca::xg::k_xgmi_ar_sgd<true>, dim3(dca::xg::AR_NB), dim3(dca::xg::AR_T), 0, st[q], cx, P,
+                           (const float*)(src + (size_t)q * dca::FLAT_ALLOC), dst + (size_t)q * dca::FLAT_ALLOC, err,
+                           0, 2ull * 100000000ull);
+      }
+    for (int q = 1; q < W; ++q) {
+      hipEvent_t e;
+      HIPCK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+      HIPCK(hipEventRecord(e, st[q]));
+      HIPCK(hipStreamWaitEvent(st[0], e, 0));
+      (void)hipEventDestroy(e);
+    }
+    HIPCK(hipEventRecord(b, st[0]));
+    HIPCK(hipEventSynchronize(b));
+    float ms = 0.f;
+    HIPCK(hipEventElapsedTime(&ms, a, b));
+    best = std::min(best, 1e3f * ms / (float)iters);
+  }
+  unsigned h = 0;
+  HIPCK(hipMemcpy(&h, err, sizeof(unsigned), hipMemcpyDeviceToHost));
+  *us = best;
+  *err_out = h ? 1 : 0;
+  for (int q = 0; q < W; ++q) {
+    (void)hipStreamDestroy(st[q]);
+    (void)hipFree(reg[q]);
+  }
+  (void)hipFree(src);
+  (void)hipFree(dst);
+  (void)hipFree(err);
+  (void)hipEventDestroy(a);
+  (void)hipEventDestroy(b);
+  return 0;
+}
+
 // Launch-floor calibration: a hipGraph of `nk` dependent kernels of `kind` (0 empty; 1..6 see k_mb_load)
 // with `grid` workgroups, replayed `iters` times.  Writes microseconds per kernel to *us.
 int dca_microbench(int kind, int nk, int grid, int iters, float* us) {

@@ -12,12 +12,16 @@
 //
 // Protocol of workgroup b (it owns float4 chunk b of the flat buffer [0, FLAT_N), on every rank):
 //   1. ep = my_flags[me][b] + 1 (the epoch this workgroup last published, plus one); slab parity = ep & 1
-//   2. copy my chunk b of cx.grads into my slab[parity]; system-scope release fence
+//   2. copy my chunk b of cx.grads into my slab[parity] (write-through store); wait for it (vmcnt) + barrier
 //   3. store ep into flags[me][b] of EVERY rank (itself included)
 //   4. wait until my flags[q][b] >= ep for all ranks q (bounded by a real-time deadline -> error bit, no hang)
-//   5. system-scope acquire; read chunk b of all W slabs[parity]; sum in rank order 0..W-1 (bitwise identical
+//   5. read chunk b of all W slabs[parity] (cache-bypassing loads); sum in rank order 0..W-1 (bitwise identical
 //      on every rank); write the sum to cx.grads; SGD with 1/W averaging + derived weight copies; the
 //      running-stat segment [OFF_RS, FLAT_N) is rank 0's BN buffers (others contribute 0): CC4.
+// Memory ordering without L2 write-backs: the slab and flag stores are system-coherent write-through stores
+// (cache policy sc0 sc1) to uncached memory, a `s_waitcnt vmcnt(0)` + workgroup barrier orders them before the
+// flag store, and the slab loads are sc0 sc1 loads that bypass every cache.  (A __threadfence_system() per wave
+// -- buffer_wbl2 of the whole XCD L2 + buffer_inv -- measured ~48 us per all-reduce with 2 ranks on one GPU.)
 // Reuse safety: a rank writes slab[parity] again at epoch ep+2 only after its workgroup b passed step 4 of
 // epoch ep+1, i.e. after every peer started epoch ep+1, i.e. (stream order) after every peer finished reading
 // epoch ep.  Parities alternate, so epoch ep+1's writes never touch what epoch ep's readers read.
@@ -40,6 +44,8 @@ static_assert(FLAT_N % 4 == 0, "flat buffer must be float4 granular");
 struct Peers {
   char* base[MAXR];  // every rank's shared region, mapped into this process (own one at base[rank])
 };
+
+typedef unsigned v4u __attribute__((ext_vector_type(4)));
 
 __device__ __forceinline__ int flag_load(const int* p) {
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -66,15 +72,18 @@ __global__ void __launch_bounds__(AR_T) k_xgmi_ar_sgd(Ctx cx, Peers P, const flo
   const f32x4 g = live ? *(const f32x4*)(src + 4 * v) : f32x4{0.f, 0.f, 0.f, 0.f};
   __syncthreads();
   const int ep = s_ep, par = ep & 1;
-  *(f32x4*)(slab(P, me, par) + 4 * v) = g;
-  __threadfence_system();  // release: my slab chunk is visible at system scope before any flag says so
-  __syncthreads();
+  constexpr int SYS = 17;  // cache policy sc0 | sc1: system-coherent (write-through store / cache-bypassing load)
+  const __amdgpu_buffer_rsrc_t mine =
+      __builtin_amdgcn_make_buffer_rsrc(slab(P, me, par), (short)0, (int)(SLAB_FLOATS * 4), 0x00020000);
+  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u, g), mine, 16 * v, 0, SYS);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this thread's slab store is performed
+  __syncthreads();                                    // ... and every thread's of this workgroup
   if (t < W) flag_store((int*)P.base[t] + me * AR_NB + b, ep);
   if (t < W) {
     const int* f = myflags + t * AR_NB + b;
     const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
     while (flag_load(f) < ep) {
-      __builtin_amdgcn_s_sleep(2);
+      __builtin_amdgcn_s_sleep(1);
       if (__builtin_amdgcn_s_memrealtime() - t0 > deadline_ticks) {
         atomicOr(err, 0x80000000u);
         break;
@@ -82,13 +91,16 @@ __global__ void __launch_bounds__(AR_T) k_xgmi_ar_sgd(Ctx cx, Peers P, const flo
     }
   }
   __syncthreads();
-  __threadfence_system();  // acquire: peers' slab chunks as of their flag stores
   if (!live) return;
-  // All W loads in flight at once (one per peer link): unconditional loads (ranks >= W re-read rank 0, which
-  // is never summed) so the compiler issues them back to back instead of branching around each one.
+  // All W loads in flight at once (one per peer link), cache-bypassing: unconditional loads (ranks >= W re-read
+  // rank 0, which is never summed) so the compiler issues them back to back instead of branching around each one.
   f32x4 part[MAXR];
 #pragma unroll
-  for (int q = 0; q < MAXR; ++q) part[q] = *(const f32x4*)(slab(P, q < W ? q : 0, par) + 4 * v);
+  for (int q = 0; q < MAXR; ++q) {
+    const __amdgpu_buffer_rsrc_t rs =
+        __builtin_amdgcn_make_buffer_rsrc(slab(P, q < W ? q : 0, par), (short)0, (int)(SLAB_FLOATS * 4), 0x00020000);
+    part[q] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, 16 * v, 0, SYS));
+  }
   f32x4 s = part[0];
 #pragma unroll
   for (int q = 1; q < MAXR; ++q) s += q < W ? part[q] : f32x4{0.f, 0.f, 0.f, 0.f};

@@ -48,6 +48,7 @@ def _declare(lib):
     lib.dca_engine_ipc_handle.argtypes = [c_void_p, ctypes.c_char_p]
     lib.dca_engine_ipc_open.argtypes = [c_void_p, ctypes.c_char_p, c_int]
     lib.dca_engine_ipc_selftest.argtypes = [c_void_p, c_void_p, c_void_p, ctypes.c_float, ctypes.POINTER(c_int)]
+    lib.dca_microbench_xgmi.argtypes = [c_int, c_int, ctypes.POINTER(ctypes.c_float), ctypes.POINTER(c_int)]
     lib.dca_engine_ipc_bench.argtypes = [c_void_p, c_void_p, c_void_p, c_int, ctypes.POINTER(ctypes.c_float)]
     lib.dca_engine_errors.argtypes = [c_void_p, ctypes.POINTER(ctypes.c_uint), c_int]  # flags[2]
     lib.dca_microbench.argtypes = [c_int, c_int, c_int, c_int, ctypes.POINTER(ctypes.c_float)]
