@@ -3,7 +3,10 @@
 ``python -m distributeddataparallel_cifar10_amd.build`` compiles, with ``hipcc --offload-arch=gfx950``:
   * ``csrc/engine.hip`` (the NetResDeep training engine + xGMI all-reduce) -> ``_lib/libdca_engine.so``
   * ``csrc/ops_api.hip`` (the general layer kernels of ``ops/``: MFMA GEMM bf16/fp8, im2col, BN, pooling, CE,
-    SGD, fp8 quantisation) -> ``_lib/libdca_ops.so``  hipcc cross-compiles without
+    SGD, fp8 quantisation) -> ``_lib/libdca_ops.so``
+  * ``csrc/comm_api.hip`` (generic xGMI one-shot / two-shot all-reduce for any model's flat buckets)
+    -> ``_lib/libdca_comm.so``
+hipcc cross-compiles without
 a GPU, so this runs on the CPU-only build host too.  The library links the HIP runtime and RCCL by SONAME
 (``libamdhip64.so.7``, ``librccl.so.1``); loaded after ``import torch`` it binds to the copies torch already
 loaded, so there is exactly one HIP runtime in the process.
@@ -21,14 +24,16 @@ CSRC = os.path.join(PKG_DIR, "csrc")
 LIB_DIR = os.path.join(PKG_DIR, "_lib")
 ENGINE_LIB = os.path.join(LIB_DIR, "libdca_engine.so")
 OPS_LIB = os.path.join(LIB_DIR, "libdca_ops.so")
+COMM_LIB = os.path.join(LIB_DIR, "libdca_comm.so")
+_ENTRY = {"ops": ("ops_api.hip", OPS_LIB), "comm": ("comm_api.hip", COMM_LIB)}
 ARCH = os.environ.get("DCA_OFFLOAD_ARCH", "gfx950")
 # Variants: "" = production; "stamps" = diagnostic build with in-kernel phase stamps (-DDCA_STAMPS).
-VARIANTS = {"": [], "stamps": ["-DDCA_STAMPS"], "ops": []}
+VARIANTS = {"": [], "stamps": ["-DDCA_STAMPS"], "ops": [], "comm": []}
 
 
 def lib_path(variant: str = "") -> str:
-    if variant == "ops":
-        return OPS_LIB
+    if variant in _ENTRY:
+        return _ENTRY[variant][1]
     return ENGINE_LIB if not variant else os.path.join(LIB_DIR, f"libdca_engine_{variant}.so")
 
 
@@ -66,8 +71,8 @@ def build(force: bool = False, verbose: bool = False, variant: str = "") -> str:
     cmd = [
         _hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
         "-Wall", "-Wno-unused-function", "-Wno-unused-variable", *VARIANTS[variant],
-        os.path.join(CSRC, "ops_api.hip" if variant == "ops" else "engine.hip"), "-o", tmp,
-        *([] if variant == "ops" else ["-lrccl"]),
+        os.path.join(CSRC, _ENTRY[variant][0] if variant in _ENTRY else "engine.hip"), "-o", tmp,
+        *([] if variant in _ENTRY else ["-lrccl"]),
     ]
     if verbose:
         print(" ".join(cmd), flush=True)
@@ -80,8 +85,8 @@ def build(force: bool = False, verbose: bool = False, variant: str = "") -> str:
     return out
 
 
-def build_all(force: bool = False, verbose: bool = False, variants=("", "ops")) -> list:
-    """Build the listed library variants (default: the engine and the ops library, compiled concurrently);
+def build_all(force: bool = False, verbose: bool = False, variants=("", "ops", "comm")) -> list:
+    """Build the listed library variants (default: the engine, ops and comm libraries, compiled concurrently);
     returns their paths."""
     from concurrent.futures import ThreadPoolExecutor
     with ThreadPoolExecutor(max_workers=len(variants)) as ex:
@@ -89,5 +94,5 @@ def build_all(force: bool = False, verbose: bool = False, variants=("", "ops")) 
 
 
 if __name__ == "__main__":
-    for v in (["", "ops", "stamps"] if "--all" in sys.argv else ["", "ops"]):
+    for v in (["", "ops", "comm", "stamps"] if "--all" in sys.argv else ["", "ops", "comm"]):
         print(build(force="--force" in sys.argv, verbose=True, variant=v))

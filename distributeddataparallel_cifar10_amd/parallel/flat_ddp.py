@@ -20,11 +20,18 @@ Design (not a copy of the c10d Reducer):
     64 KB per link, small enough that the first bucket fires early.  With ``first_bucket_mb`` the first (earliest
     ready) bucket can be made smaller, like DDP's 1 MiB first bucket.
 
+  * the bucket all-reduce is either the process group's (RCCL over xGMI on GPUs, gloo on CPU) or, for CUDA
+    models inside one node, the framework's own xGMI peer-read all-reduce (``parallel/xgmi.py``: one-shot for
+    small buckets, two-shot reduce-scatter/all-gather for large ones, fp32 or bf16 on the wire), launched on a
+    dedicated comm stream with the 1/W average fused into the kernel.  Every bucket starts on a 16-byte
+    boundary (parameters are padded to 4 elements) so buckets can be handed to the kernel as they are.
+
 The fused NetResDeep engine (``parallel/ddp.py``) implements the same semantics inside its graph-captured step;
 this wrapper is the path for arbitrary models and for CPU/gloo testing.
 """
 from __future__ import annotations
 
+import os
 from typing import List, Optional
 
 import torch
@@ -38,8 +45,14 @@ def _dist_on(group=None) -> bool:
 
 class FlatBucketDDP(nn.Module):
     def __init__(self, module: nn.Module, bucket_cap_mb: float = 4.0, first_bucket_mb: Optional[float] = 1.0,
-                 broadcast_buffers: bool = True, process_group=None, device_ids=None, output_device=None):
+                 broadcast_buffers: bool = True, process_group=None, device_ids=None, output_device=None,
+                 comm: str = "auto", wire: str = "fp32", algo: str = "auto"):
+        """``comm``: "auto" (xGMI for CUDA models when every rank is on this node, else the process group),
+        "xgmi", or "process_group".  ``wire`` ("fp32" | "bf16") and ``algo`` ("auto" | "oneshot" | "twoshot")
+        apply to the xGMI path."""
         super().__init__()
+        if comm not in ("auto", "xgmi", "process_group"):
+            raise ValueError("comm must be 'auto', 'xgmi' or 'process_group'")
         self.module = module
         self.process_group = process_group
         self.world_size = dist.get_world_size(process_group) if _dist_on(process_group) else 1
@@ -51,7 +64,7 @@ class FlatBucketDDP(nn.Module):
         if any(p.device != dev or p.dtype != dtype for p in params):
             raise ValueError("FlatBucketDDP needs all parameters on one device with one dtype")
         order = list(reversed(params))  # approximately gradient-ready order
-        total = sum(p.numel() for p in order)
+        total = sum((p.numel() + 3) // 4 * 4 for p in order)  # every parameter starts 16-byte aligned
         self.flat = torch.zeros(total, dtype=dtype, device=dev)
         self.flat_grad = torch.zeros(total, dtype=dtype, device=dev)
         self._views = {}
@@ -64,7 +77,7 @@ class FlatBucketDDP(nn.Module):
                 g = self.flat_grad[off:off + n].view_as(p)
                 p.grad = g
                 self._views[p] = (off, n, g)
-                off += n
+                off += (n + 3) // 4 * 4
         # bucket plan: contiguous slices of the flat buffer
         esz = self.flat.element_size()
         cap = max(1, int(bucket_cap_mb * 2 ** 20 / esz))
@@ -73,7 +86,7 @@ class FlatBucketDDP(nn.Module):
         start, count, limit = 0, 0, first_cap
         cursor = 0
         for p in order:
-            n = p.numel()
+            n = (p.numel() + 3) // 4 * 4
             if count and cursor + n - start > limit:
                 self.buckets.append((start, cursor, count))
                 start, count, limit = cursor, 0, cap
@@ -91,6 +104,17 @@ class FlatBucketDDP(nn.Module):
         self._callback_queued = False
         self.bucket_fire_order: List[int] = []  # for tests: order in which buckets were launched
         self._sync_module_states()  # CC3
+        self.comm, self.xgmi, self._comm_stream = "process_group" if self.world_size > 1 else "none", None, None
+        self._wire, self._algo = wire, algo
+        if self.world_size > 1 and dev.type == "cuda" and dtype == torch.float32 and comm != "process_group":
+            local = int(os.environ.get("LOCAL_WORLD_SIZE", str(self.world_size)))
+            if comm == "xgmi" or (local == self.world_size and self.world_size <= 8):
+                from .xgmi import XgmiComm
+                self.xgmi = XgmiComm.create(max(e - s for s, e, _ in self.buckets), group=process_group,
+                                            device=dev, wire=wire)
+                if self.xgmi is not None:
+                    self.comm = "xgmi"
+                    self._comm_stream = torch.cuda.Stream(dev)
         for p in order:
             p.register_post_accumulate_grad_hook(self._make_hook(p))
 
@@ -134,24 +158,30 @@ class FlatBucketDDP(nn.Module):
             bi = self._bucket_of[p]
             self._pending[bi] -= 1
             if self._pending[bi] == 0:
-                s, e, _ = self.buckets[bi]
-                seg = self.flat_grad[s:e]
-                seg.div_(self.world_size)  # average: pre-divide, then sum
-                self._works.append(dist.all_reduce(seg, group=self.process_group, async_op=True))
-                self.bucket_fire_order.append(bi)
+                self._launch(bi)
         return hook
 
+    def _launch(self, bi: int) -> None:
+        s, e, _ = self.buckets[bi]
+        seg = self.flat_grad[s:e]
+        if self.xgmi is not None:  # own xGMI all-reduce on the comm stream, average fused, no host sync
+            cs = self._comm_stream
+            cs.wait_stream(torch.cuda.current_stream(seg.device))
+            self.xgmi.all_reduce_(seg, average=True, algo=self._algo, wire=self._wire, stream=cs)
+        else:
+            seg.div_(self.world_size)  # average: pre-divide, then sum
+            self._works.append(dist.all_reduce(seg, group=self.process_group, async_op=True))
+        self.bucket_fire_order.append(bi)
+
     def _finish_backward(self) -> None:
+        # parameters that received no gradient this step: reduce their (zero) slices too, in bucket order
+        for bi, left in enumerate(self._pending):
+            if left:
+                self._launch(bi)
         for w in self._works:
             w.wait()
-        if any(self._pending):
-            # parameters that received no gradient this step: reduce their (zero) slices too, in order
-            for bi, left in enumerate(self._pending):
-                if left:
-                    s, e, _ = self.buckets[bi]
-                    seg = self.flat_grad[s:e]
-                    seg.div_(self.world_size)
-                    dist.all_reduce(seg, group=self.process_group)
+        if self._comm_stream is not None:
+            torch.cuda.current_stream(self.flat_grad.device).wait_stream(self._comm_stream)
         self._works = []
         self._callback_queued = False
         self._reset_pending()
@@ -169,6 +199,17 @@ class FlatBucketDDP(nn.Module):
 
     def zero_grad(self, set_to_none: bool = False) -> None:  # grads stay views of the flat buffer
         self.flat_grad.zero_()
+
+    def check_comm(self) -> None:
+        """Raise if the xGMI all-reduce recorded a peer timeout (synchronous; call at log points)."""
+        if self.xgmi is not None:
+            self.xgmi.check()
+
+    def close(self) -> None:
+        """Release the xGMI communicator (collective: every rank must call it)."""
+        if self.xgmi is not None:
+            self.xgmi.close()
+            self.xgmi = None
 
 
 class FlatSGD(torch.optim.Optimizer):

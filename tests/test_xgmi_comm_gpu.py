@@ -1,0 +1,144 @@
+"""Generic xGMI all-reduce communicator (parallel/xgmi.py, csrc/xgmi_comm.hip) with 2 and 4 ranks sharing one
+MI355X: the IPC-mapped regions are then peers on the same device, which exercises the whole protocol (epochs,
+slab parities, in/out flags, one-shot and two-shot partitions, partial last float4, bf16 wire).
+
+Every result is compared for EXACT equality with a rank-order fp32 sum computed on the host (the kernel sums
+rank 0..W-1 in order, then scales; the bf16 wire rounds each input and the final value once, RNE).  Ranks arrive
+at each call at different times (sleeps), the stress the reference's DDP never sees.  FlatBucketDDP on the xGMI
+path must give the same averaged gradients as the process-group path.
+"""
+import os
+import time
+import traceback
+
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+pytestmark = pytest.mark.gpu
+SIZES = [1, 5, 4099, 262147, 1 << 20]
+
+
+def _inputs(ws, n, seed):
+    g = torch.Generator().manual_seed(seed)
+    return [torch.randn(n, generator=g) * (r + 1) for r in range(ws)]
+
+
+def _expect(xs, wire, scale):
+    if wire == "bf16":
+        xs = [x.bfloat16().float() for x in xs]
+    s = xs[0].clone()
+    for x in xs[1:]:
+        s += x
+    s *= scale
+    return s.bfloat16().float() if wire == "bf16" else s
+
+
+def _spawn(target, ws, *args):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=target, args=(r, ws, *args, q)) for r in range(ws)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=600) for _ in procs]
+    for p in procs:
+        p.join(timeout=120)
+    bad = [r for r in res if r[1]]
+    assert not bad, "\n".join(f"rank {r}:\n{e}" for r, e in bad)
+
+
+def _init(rank, ws, port):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=ws)
+    torch.cuda.set_device(0)
+    return torch.device("cuda", 0)
+
+
+def _collective_worker(rank, ws, port, q):
+    try:
+        dev = _init(rank, ws, port)
+        from distributeddataparallel_cifar10_amd.parallel.xgmi import XgmiComm
+        comm = XgmiComm.create(max(SIZES), device=dev, timeout_s=60.0)
+        assert comm is not None, "xGMI communicator did not come up (self-test failed)"
+        it = 0
+        for rep in range(2):  # every (size, algo, wire) twice: both slab parities, advancing epochs
+            for n in SIZES:
+                for algo in ("oneshot", "twoshot", "auto"):
+                    for wire in ("fp32", "bf16"):
+                        xs = _inputs(ws, n, seed=1000 * it + n)
+                        t = xs[rank].to(dev)
+                        time.sleep(0.002 * ((rank + it) % ws))  # uneven arrival
+                        comm.all_reduce_(t, average=(it % 2 == 0), algo=algo, wire=wire)
+                        want = _expect(xs, wire, 1.0 / ws if it % 2 == 0 else 1.0)
+                        got = t.cpu()
+                        if not torch.equal(got, want):
+                            bad = (got != want).nonzero()[:5].flatten().tolist()
+                            raise AssertionError(f"n={n} algo={algo} wire={wire} rep={rep}: mismatch at {bad}: "
+                                                 f"{got[bad].tolist()} vs {want[bad].tolist()}")
+                        it += 1
+        # a large odd tail through the two-shot path on a side stream, then the error word is clean
+        s = torch.cuda.Stream()
+        xs = _inputs(ws, (1 << 20) - 3, seed=7)
+        t = xs[rank].to(dev)
+        s.wait_stream(torch.cuda.current_stream())
+        comm.all_reduce_(t, average=True, algo="twoshot", stream=s)
+        s.synchronize()
+        assert torch.equal(t.cpu(), _expect(xs, "fp32", 1.0 / ws))
+        assert comm.errors() == 0
+        comm.close()
+        q.put((rank, None))
+    except Exception:
+        q.put((rank, traceback.format_exc()))
+    finally:
+        if dist.is_initialized():
+            dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("ws", [2, 4])
+def test_xgmi_comm_exact_sums(gpu, port, ws):
+    _spawn(_collective_worker, ws, port)
+
+
+def _ddp_worker(rank, ws, port, algo, wire, q):
+    try:
+        dev = _init(rank, ws, port)
+        import torch.nn as nn
+        from distributeddataparallel_cifar10_amd.parallel.flat_ddp import FlatBucketDDP
+        torch.manual_seed(0)  # identical init everywhere (CC3 is checked elsewhere)
+        net = nn.Sequential(nn.Conv2d(3, 16, 3, padding=1), nn.BatchNorm2d(16), nn.ReLU(), nn.Flatten(),
+                            nn.Linear(16 * 8 * 8, 10)).to(dev)
+        ref = nn.Sequential(nn.Conv2d(3, 16, 3, padding=1), nn.BatchNorm2d(16), nn.ReLU(), nn.Flatten(),
+                            nn.Linear(16 * 8 * 8, 10)).to(dev)
+        ref.load_state_dict(net.state_dict())
+        ddp = FlatBucketDDP(net, bucket_cap_mb=0.02, first_bucket_mb=0.01, comm="xgmi", wire=wire, algo=algo)
+        assert ddp.comm == "xgmi" and len(ddp.buckets) >= 2, (ddp.comm, ddp.buckets)
+        for step in range(3):
+            g = torch.Generator().manual_seed(100 * step + rank)
+            x, y = torch.randn(8, 3, 8, 8, generator=g).to(dev), torch.randint(0, 10, (8,), generator=g).to(dev)
+            ddp.zero_grad()
+            nn.functional.cross_entropy(ddp(x), y).backward()
+            ref.zero_grad()
+            nn.functional.cross_entropy(ref(x), y).backward()
+            ddp.check_comm()
+            for (name, p), rp in zip(net.named_parameters(), ref.parameters()):
+                parts = [torch.zeros_like(rp.grad, device="cpu") for _ in range(ws)]
+                dist.all_gather(parts, rp.grad.detach().cpu())
+                want = _expect([t.reshape(-1) for t in parts], wire, 1.0 / ws).view_as(rp.grad)
+                # the two replicas' local grads may differ in the last bit (library conv algorithm choice), so
+                # compare with a tolerance here; exactness of the collective itself is test_xgmi_comm_exact_sums
+                tol = dict(rtol=1e-5, atol=1e-7) if wire == "fp32" else dict(rtol=1e-2, atol=1e-5)
+                torch.testing.assert_close(p.grad.cpu(), want, **tol, msg=f"step {step} {name}")
+        ddp.close()
+        q.put((rank, None))
+    except Exception:
+        q.put((rank, traceback.format_exc()))
+    finally:
+        if dist.is_initialized():
+            dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("ws,algo,wire", [(2, "auto", "fp32"), (4, "twoshot", "fp32"), (2, "oneshot", "bf16")])
+def test_flat_ddp_xgmi_matches_averaged_grads(gpu, port, ws, algo, wire):
+    _spawn(_ddp_worker, ws, port, algo, wire)
