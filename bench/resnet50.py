@@ -4,7 +4,7 @@ Generic path of the framework: FlatBucketDDP (flat parameter/gradient buffers, b
 all-reduce launched from gradient hooks so it overlaps the backward) + FlatSGD (momentum 0.9, one fused update),
 bf16 autocast.  Prints one JSON line (whole-job images/sec, slowest rank).
 
-    python bench/resnet50.py [--batch 64] [--steps 30] [--warmup 5]
+    python bench/resnet50.py [--batch 256] [--steps 30] [--warmup 5]
     python -m torch.distributed.run --nproc-per-node 8 --master-addr 127.0.0.1 bench/resnet50.py --gpus 8
 """
 from __future__ import annotations
@@ -25,7 +25,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 def main() -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--batch", type=int, default=64, help="per-rank batch")
+    ap.add_argument("--batch", type=int, default=256, help="per-rank batch (288 GB HBM per GPU: large per-GPU batches)")
     ap.add_argument("--steps", type=int, default=30)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--image", type=int, default=224)

@@ -40,7 +40,7 @@ using namespace dca::ops;
 extern "C" {
 
 const char* dca_ops_last_error() { return g_err.c_str(); }
-int dca_ops_abi_version() { return 3; }
+int dca_ops_abi_version() { return 4; }
 
 // Must match ops/_native.py::GemmArgs.
 int dca_ops_gemm(const GemmArgs* a, void* stream) {
@@ -77,6 +77,8 @@ int dca_ops_gemm(const GemmArgs* a, void* stream) {
   }
   const int kt = GBK_BYTES / (g.fp8 ? 1 : 2);
   if (g.splits < 1) g.splits = 1;
+  REQUIRE(g.wperm_T <= 0 || (g.ws && !g.col_stats && g.wperm_C > 0 && g.wperm_Cpad >= g.wperm_C),
+          "gemm: weight-layout remap needs a workspace and no column stats");
   if (g.splits > 1) {
     REQUIRE(g.ws != nullptr, "gemm: split-K needs a workspace");
     int kps = (g.K + g.splits - 1) / g.splits;
@@ -98,7 +100,7 @@ int dca_ops_gemm(const GemmArgs* a, void* stream) {
     if (g.fp8) hipLaunchKernelGGL((k_gemm<true, 128>), grid, dim3(GT), GemmTile<128>::LDS, st, g);
     else hipLaunchKernelGGL((k_gemm<false, 128>), grid, dim3(GT), GemmTile<128>::LDS, st, g);
   }
-  if (g.splits > 1) hipLaunchKernelGGL(k_gemm_splitk_reduce, dim3(grid_for((long)g.M * g.N)), dim3(256), 0, st, g);
+  if (g.splits > 1 || g.wperm_T > 0) hipLaunchKernelGGL(k_gemm_splitk_reduce, dim3(grid_for((long)g.M * g.N)), dim3(256), 0, st, g);
   OPCK(hipGetLastError());
   return 0;
 }
@@ -256,5 +258,19 @@ int dca_ops_fp8_alpha(const unsigned* amax_a, const unsigned* amax_b, float extr
   OPCK(hipGetLastError());
   return 0;
 }
+
+// descs: device array of nd PackDesc (ops/functional.py WeightPack); amax: n_amax device words zeroed first.
+int dca_ops_pack_weights(const void* descs, int nd, int blocks_per_layer, unsigned* amax, int n_amax, void* stream) {
+  REQUIRE(nd > 0 && blocks_per_layer > 0, "pack_weights: empty");
+  hipStream_t st = (hipStream_t)stream;
+  if (n_amax > 0) OPCK(hipMemsetAsync(amax, 0, sizeof(unsigned) * n_amax, st));
+  const dim3 grid(blocks_per_layer, nd);
+  hipLaunchKernelGGL(k_pack_weights, grid, dim3(256), 0, st, (const PackDesc*)descs);
+  if (n_amax > 0) hipLaunchKernelGGL(k_pack_fp8, grid, dim3(256), 0, st, (const PackDesc*)descs);
+  OPCK(hipGetLastError());
+  return 0;
+}
+
+int dca_ops_pack_desc_size() { return (int)sizeof(PackDesc); }
 
 }  // extern "C"

@@ -56,7 +56,23 @@ struct GemmArgs {
   // rows of (out - stats_shift[col]), the layout k_bn_finalize reduces
   float2* col_stats;
   const float* stats_shift;
+  // fp8 per-tensor scales as device amax bits (q = x * 448 / amax): alpha *= (amax_a / 448) * (amax_b / 448)
+  const unsigned* amax_a;
+  const unsigned* amax_b;
+  // weight-gradient layout remap (wperm_T > 0): output column n = tap * wperm_Cpad + c of the GEMM is stored at
+  // row * (wperm_C * wperm_T) + c * wperm_T + tap -- torch's [Cout][Cin][KH][KW] -- and dropped for padded
+  // channels (c >= wperm_C); always through the fp32 slab + reduce kernel.
+  int wperm_C, wperm_Cpad, wperm_T;
 };
+
+__device__ __forceinline__ float amax_scale(const unsigned* a) {
+  if (!a) return 1.f;
+  const float v = __uint_as_float(*a);
+  return v > 0.f ? v * (1.f / 448.f) : 1.f;
+}
+__device__ __forceinline__ float gemm_alpha(const GemmArgs& g) {
+  return g.alpha * (g.alpha_dev ? *g.alpha_dev : 1.f) * amax_scale(g.amax_a) * amax_scale(g.amax_b);
+}
 
 __device__ __forceinline__ int lds_off(int row, int chunk) { return row * 128 + ((chunk ^ ((row >> 1) & 7)) << 4); }
 
@@ -340,7 +356,7 @@ __global__ void __launch_bounds__(GT) k_gemm(GemmArgs g) {
   // LDS (the K-loop buffers are free: 64 KiB exactly; 16-column groups XOR-swizzled by (row >> 2) & 3 so the
   // fragment writes of one instruction hit distinct banks), then written back row-contiguously, 16 B per lane,
   // with alpha / bias / beta / ReLU applied -- and, when asked, the per-column BN partial sums of the tile.
-  if (g.splits > 1) {
+  if (g.splits > 1 || g.wperm_T > 0) {
 #pragma unroll
     for (int m = 0; m < 4; ++m)
 #pragma unroll
@@ -364,7 +380,7 @@ __global__ void __launch_bounds__(GT) k_gemm(GemmArgs g) {
       for (int j = 0; j < 4; ++j)
         ct[cidx(wr * 64 + m * 16 + (lane >> 4) * 4 + j, wc * T::WCW + n * 16 + (lane & 15))] = acc[m][n][j];
   __syncthreads();
-  const float alpha = g.alpha * (g.alpha_dev ? *g.alpha_dev : 1.f);
+  const float alpha = gemm_alpha(g);
   // thread t: column group cg = t % CG (4 columns each), rows t / CG + RL * r
   constexpr int CG = BN_ / 4, RL = GT / CG;
   const int cg = threadIdx.x % CG, col0 = n0 + cg * 4;
@@ -442,15 +458,22 @@ __global__ void __launch_bounds__(GT) k_gemm(GemmArgs g) {
 }
 
 // Split-K combine: C = alpha * sum_s ws[s] (+bias) (+beta*C) (ReLU), fixed summation order (deterministic).
+// With wperm_T > 0 the column is remapped to torch's weight layout (see GemmArgs) and padded channels dropped.
 __global__ void __launch_bounds__(256) k_gemm_splitk_reduce(GemmArgs g) {
   const size_t total = (size_t)g.M * g.N;
+  const float alpha = gemm_alpha(g);
   for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < total; i += (size_t)gridDim.x * 256) {
+    const int row = (int)(i / g.N), col = (int)(i % g.N);
+    size_t o = (size_t)row * g.ldc + col;
+    if (g.wperm_T > 0) {
+      const int tap = col / g.wperm_Cpad, c = col - tap * g.wperm_Cpad;
+      if (c >= g.wperm_C || tap >= g.wperm_T) continue;
+      o = ((size_t)row * g.wperm_C + c) * g.wperm_T + tap;
+    }
     float v = 0.f;
     for (int s = 0; s < g.splits; ++s) v += g.ws[(size_t)s * total + i];
-    const int row = (int)(i / g.N), col = (int)(i % g.N);
-    v *= g.alpha * (g.alpha_dev ? *g.alpha_dev : 1.f);
+    v *= alpha;
     if (g.bias) v += g.bias[col];
-    const size_t o = (size_t)row * g.ldc + col;
     if (g.beta != 0.f) v += g.beta * (g.out_bf16 ? bf2f(((const unsigned short*)g.C)[o]) : ((const float*)g.C)[o]);
     if (g.relu) v = v > 0.f ? v : 0.f;
     if (g.out_bf16) ((unsigned short*)g.C)[o] = f2bf_rne(v);

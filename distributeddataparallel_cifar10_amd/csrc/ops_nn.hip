@@ -564,5 +564,78 @@ __global__ void k_fp8_alpha(const unsigned* amax_a, const unsigned* amax_b, floa
   *alpha = (a > 0.f ? a / 448.f : 1.f) * (b > 0.f ? b / 448.f : 1.f) * extra;
 }
 
+// ---------------------------------------------------------------------------------------------------------
+// Per-step weight packing: every layer's fp32 master weight [Cout][Cin][KH][KW] (torch layout -- the parameter
+// itself) becomes its bf16 GEMM operands in ONE launch for the whole model, instead of a chain of
+// permute / pad / cast ops per layer:
+//   fwd   [Cout][Kp]            column (kh*KW + kw)*Cin_pad + c, zero for padded channels (Cin_pad = 8 for a
+//                               3-channel stem) -> forward and strided-dgrad operand
+//   dgrad [Cin][KH*KW*Cout]     taps flipped, ci/co swapped -> the stride-1 input gradient as an implicit conv
+// and, for fp8 layers, the per-layer amax (k_pack_weights) then the e4m3 copy q = sat(w * 448 / amax)
+// (k_pack_fp8).  grid (blocks per layer, layers); every block grid-strides over its layer's fwd elements.
+// ---------------------------------------------------------------------------------------------------------
+struct PackDesc {
+  const float* w;
+  bf16_t* fwd;
+  bf16_t* dgrad;    // or null
+  uint8_t* q8;      // or null
+  unsigned* amax;   // float bits, zeroed before k_pack_weights (q8 layers only)
+  int co, ci, ci_pad, kh, kw, kp;
+};
+
+__device__ __forceinline__ bool pack_src(const PackDesc& d, long i, long& src, int& n, int& c, int& a, int& b) {
+  n = (int)(i / d.kp);
+  const int k = (int)(i - (long)n * d.kp);
+  const int tap = k / d.ci_pad;
+  c = k - tap * d.ci_pad;
+  a = tap / d.kw;
+  b = tap - a * d.kw;
+  if (c >= d.ci || tap >= d.kh * d.kw) return false;
+  src = (((long)n * d.ci + c) * d.kh + a) * d.kw + b;
+  return true;
+}
+
+__global__ void __launch_bounds__(256) k_pack_weights(const PackDesc* __restrict__ descs) {
+  const PackDesc d = descs[blockIdx.y];
+  const long total = (long)d.co * d.kp;
+  float m = 0.f;
+  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < total; i += (long)gridDim.x * 256) {
+    long src;
+    int n, c, a, b;
+    float v = 0.f;
+    if (pack_src(d, i, src, n, c, a, b)) {
+      v = d.w[src];
+      if (d.dgrad)
+        d.dgrad[(long)c * (d.kh * d.kw * d.co) + ((d.kh - 1 - a) * d.kw + (d.kw - 1 - b)) * d.co + n] = f2bf_rne(v);
+    }
+    d.fwd[i] = f2bf_rne(v);
+    m = fmaxf(m, fabsf(v));
+  }
+  if (d.q8) {
+    __shared__ float red[256];
+    red[threadIdx.x] = m;
+    __syncthreads();
+    for (int o = 128; o; o >>= 1) {
+      if (threadIdx.x < o) red[threadIdx.x] = fmaxf(red[threadIdx.x], red[threadIdx.x + o]);
+      __syncthreads();
+    }
+    if (threadIdx.x == 0) atomicMax(d.amax, __float_as_uint(red[0]));
+  }
+}
+
+__global__ void __launch_bounds__(256) k_pack_fp8(const PackDesc* __restrict__ descs) {
+  const PackDesc d = descs[blockIdx.y];
+  if (!d.q8) return;
+  const float amax = __uint_as_float(*d.amax);
+  const float sc = amax > 0.f ? 448.f / amax : 1.f;
+  const long total = (long)d.co * d.kp;
+  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < total; i += (long)gridDim.x * 256) {
+    long src;
+    int n, c, a, b;
+    const float v = pack_src(d, i, src, n, c, a, b) ? fminf(fmaxf(d.w[src] * sc, -448.f), 448.f) : 0.f;
+    d.q8[i] = (uint8_t)(__builtin_amdgcn_cvt_pk_fp8_f32(v, 0.f, 0, false) & 0xff);
+  }
+}
+
 }  // namespace ops
 }  // namespace dca

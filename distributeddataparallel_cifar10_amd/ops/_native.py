@@ -13,7 +13,7 @@ import torch
 
 from .. import build as _build
 
-ABI_VERSION = 3
+ABI_VERSION = 4
 _lock = threading.Lock()
 _lib = None
 
@@ -29,12 +29,19 @@ class GemmArgs(ctypes.Structure):
         ("relu", c_int), ("out_bf16", c_int), ("splits", c_int), ("k_per_split", c_int), ("alpha_dev", c_void_p),
         ("conv", c_int), ("cN", c_int), ("cH", c_int), ("cW", c_int), ("cC", c_int), ("cKH", c_int), ("cKW", c_int),
         ("cS", c_int), ("cP", c_int), ("cHo", c_int), ("cWo", c_int), ("col_stats", c_void_p),
-        ("stats_shift", c_void_p),
+        ("stats_shift", c_void_p), ("amax_a", c_void_p), ("amax_b", c_void_p),
+        ("wperm_C", c_int), ("wperm_Cpad", c_int), ("wperm_T", c_int),
     ]
 
 
 class ConvGeom(ctypes.Structure):
     _fields_ = [(n, c_int) for n in ("N", "H", "W", "C", "KH", "KW", "stride", "pad", "Ho", "Wo", "K", "Kp")]
+
+
+class PackDesc(ctypes.Structure):
+    """Mirror of csrc/ops_nn.hip::PackDesc (one layer of the per-step weight pack)."""
+    _fields_ = [("w", c_void_p), ("fwd", c_void_p), ("dgrad", c_void_p), ("q8", c_void_p), ("amax", c_void_p),
+                ("co", c_int), ("ci", c_int), ("ci_pad", c_int), ("kh", c_int), ("kw", c_int), ("kp", c_int)]
 
 
 class PoolGeom(ctypes.Structure):
@@ -64,6 +71,8 @@ def _declare(lib):
     lib.dca_ops_sgd.argtypes = [c_void_p, c_void_p, c_void_p, c_long, c_float, c_float, c_float, c_void_p, c_void_p]
     lib.dca_ops_quant_fp8.argtypes = [c_void_p, c_int, c_long, c_void_p, c_void_p, c_void_p]
     lib.dca_ops_fp8_alpha.argtypes = [c_void_p, c_void_p, c_float, c_void_p, c_void_p]
+    lib.dca_ops_pack_weights.argtypes = [c_void_p, c_int, c_int, c_void_p, c_int, c_void_p]
+    lib.dca_ops_pack_desc_size.restype = c_int
     return lib
 
 
@@ -86,6 +95,8 @@ def lib():
         handle = _declare(ctypes.CDLL(path, mode=ctypes.RTLD_GLOBAL))
         if handle.dca_ops_abi_version() != ABI_VERSION:
             raise RuntimeError(f"{path}: ABI {handle.dca_ops_abi_version()} != {ABI_VERSION} (stale build?)")
+        if handle.dca_ops_pack_desc_size() != ctypes.sizeof(PackDesc):
+            raise RuntimeError(f"{path}: PackDesc layout mismatch")
         _lib = handle
         return _lib
 

@@ -31,13 +31,17 @@ def gemm(a: torch.Tensor, b: torch.Tensor, *, ta: bool = False, tb: bool = False
          relu: bool = False, out_dtype=torch.float32, alpha: float = 1.0, out: Optional[torch.Tensor] = None,
          beta: float = 0.0, splits: int = 0, alpha_dev: Optional[torch.Tensor] = None, conv: int = 0,
          geom=None, col_stats: Optional[torch.Tensor] = None, stats_shift: Optional[torch.Tensor] = None,
-         mnk=None) -> torch.Tensor:
+         mnk=None, amax_a: Optional[torch.Tensor] = None, amax_b: Optional[torch.Tensor] = None,
+         wperm=None) -> torch.Tensor:
     """C[M,N] = alpha * A(m,k) B(n,k) (+bias) (+beta*out) (ReLU).
 
     A is [M,K] (ta=False) or [K,M] (ta=True); B is [N,K] (tb=False) or [K,N] (tb=True).  bf16 operands, or
     fp8 e4m3 stored as uint8 (both, K-contiguous).  splits=0 chooses split-K automatically.
     conv=1 / conv=2: A / B is an NHWC input gathered as im2col on the fly (``geom`` = conv geometry, ``mnk`` =
-    the GEMM shape).  col_stats [ceil(M/128), N, 2] fp32 receives per-tile BN partial sums of the output."""
+    the GEMM shape).  col_stats [ceil(M/128), N, 2] fp32 receives per-tile BN partial sums of the output.
+    amax_a / amax_b: fp8 per-tensor amax bits (int32 [1]) of the operands, folded into alpha on the device.
+    wperm = (C, Cpad, T): weight-gradient output written straight into torch's [M, C, KH, KW] fp32 layout
+    (``out``), GEMM column n = tap * Cpad + c; padded channels dropped."""
     _dev_check(a, b, bias, out)
     fp8 = a.dtype == torch.uint8
     if fp8 != (b.dtype == torch.uint8) or (not fp8 and (a.dtype != torch.bfloat16 or b.dtype != torch.bfloat16)):
@@ -51,10 +55,15 @@ def gemm(a: torch.Tensor, b: torch.Tensor, *, ta: bool = False, tb: bool = False
         Nn, Kb = (b.shape[1], b.shape[0]) if tb else (b.shape[0], b.shape[1])
         if K != Kb:
             raise ValueError(f"gemm: K mismatch {K} vs {Kb}")
-    if out is None:
-        out = torch.empty(M, Nn, dtype=out_dtype, device=a.device)
-    if out.dtype not in (torch.float32, torch.bfloat16) or out.shape != (M, Nn) or out.stride(1) != 1:
-        raise ValueError("gemm: bad output tensor")
+    if wperm is not None:
+        if out is None or out.dtype != torch.float32 or not out.is_contiguous() \
+                or out.numel() != M * wperm[0] * wperm[2]:
+            raise ValueError("gemm: weight-layout output must be contiguous fp32 [M, C, KH, KW]")
+    else:
+        if out is None:
+            out = torch.empty(M, Nn, dtype=out_dtype, device=a.device)
+        if out.dtype not in (torch.float32, torch.bfloat16) or out.shape != (M, Nn) or out.stride(1) != 1:
+            raise ValueError("gemm: bad output tensor")
     if bias is not None and (bias.dtype != torch.float32 or bias.numel() != Nn):
         raise ValueError("gemm: bias must be fp32 [N]")
     tiles = math.ceil(M / 128) * math.ceil(Nn / 128)
@@ -65,16 +74,21 @@ def gemm(a: torch.Tensor, b: torch.Tensor, *, ta: bool = False, tb: bool = False
         kt = 128 if fp8 else 64
         if tiles < 256 and K >= 4 * kt:
             splits = max(1, min(K // (2 * kt), 512 // tiles, 64))
-    ws = torch.empty(splits * M * Nn, dtype=torch.float32, device=a.device) if splits > 1 else None
+    ws = torch.empty(splits * M * Nn, dtype=torch.float32, device=a.device) \
+        if splits > 1 or wperm is not None else None
     args = N.GemmArgs(A=a.data_ptr(), B=b.data_ptr(), C=out.data_ptr(), bias=bias.data_ptr() if bias is not None else None,
                       ws=ws.data_ptr() if ws is not None else None, M=M, N=Nn, K=K,
                       lda=a.stride(0) if a.dim() == 2 else 0, ldb=b.stride(0) if b.dim() == 2 else 0,
-                      ldc=out.stride(0), alpha=float(alpha), beta=float(beta), ta=int(ta),
+                      ldc=Nn if wperm is not None else out.stride(0), alpha=float(alpha), beta=float(beta), ta=int(ta),
                       tb=int(tb), fp8=int(fp8), relu=int(relu), out_bf16=int(out.dtype == torch.bfloat16),
                       splits=splits, k_per_split=0,
                       alpha_dev=alpha_dev.data_ptr() if alpha_dev is not None else None, conv=int(conv),
                       col_stats=col_stats.data_ptr() if col_stats is not None else None,
-                      stats_shift=stats_shift.data_ptr() if stats_shift is not None else None)
+                      stats_shift=stats_shift.data_ptr() if stats_shift is not None else None,
+                      amax_a=amax_a.data_ptr() if amax_a is not None else None,
+                      amax_b=amax_b.data_ptr() if amax_b is not None else None)
+    if wperm is not None:
+        args.wperm_C, args.wperm_Cpad, args.wperm_T = (int(v) for v in wperm)
     if conv:
         for f in ("N", "H", "W", "C", "KH", "KW", "Ho", "Wo"):
             setattr(args, "c" + f, getattr(geom, f))
@@ -125,7 +139,7 @@ class _Linear(torch.autograd.Function):
         if fp8:
             qx, ax = quantize_fp8(xb)
             qw, aw = quantize_fp8(wb)
-            y = gemm(qx, qw, bias=b, relu=relu, out_dtype=out_dtype, alpha_dev=fp8_alpha(ax, aw))
+            y = gemm(qx, qw, bias=b, relu=relu, out_dtype=out_dtype, amax_a=ax, amax_b=aw)
         else:
             y = gemm(xb, wb, bias=b, relu=relu, out_dtype=out_dtype)
         ctx.save_for_backward(xb, wb, y if relu else None)
@@ -159,7 +173,7 @@ def linear(x, w, b=None, relu=False, out_dtype=torch.float32, fp8=False):
 def _geom(x, w, stride, pad):
     n, h, wd, c = x.shape
     co, ci, kh, kw = w.shape
-    if ci != c:
+    if ci != c and not (ci < c and c % 8 == 0 and ci <= 8):  # a 3-channel stem may arrive zero-padded to 8
         raise ValueError(f"conv: input has {c} channels, weight expects {ci}")
     ho, wo = (h + 2 * pad - kh) // stride + 1, (wd + 2 * pad - kw) // stride + 1
     k = kh * kw * c
@@ -178,6 +192,75 @@ def _weight_matrix(w: torch.Tensor, kp: int) -> torch.Tensor:
 
 def _implicit_ok(g) -> bool:
     return g.C % 8 == 0
+
+
+class WeightPack:
+    """The bf16 (and fp8) GEMM operands of every convolution of a model, rebuilt from the fp32 master weights
+    by ONE kernel launch per step (``pack()``; csrc/ops_nn.hip k_pack_weights / k_pack_fp8) instead of a
+    permute / pad / cast chain per layer and per use.
+
+    Per conv: ``fwd`` [Cout, KH*KW*Cin_pad] (forward, strided input gradient), ``dgrad`` [Cin, KH*KW*Cout]
+    (flipped; stride-1 KxK input gradient as an implicit conv) and, for ``fp8`` layers, ``q8`` + ``amax``.
+    Cin_pad = 8 for a stem with fewer than 8 channels (its input is zero-padded to 8 channels, so the stem runs
+    as an implicit GEMM instead of through an im2col buffer)."""
+
+    BLOCKS_PER_LAYER = 32
+
+    def __init__(self, convs, fp8_convs=()):
+        self.convs = list(convs)
+        fp8_ids = {id(c) for c in fp8_convs}
+        self.entries = {}
+        n_fp8 = sum(1 for c in self.convs if id(c) in fp8_ids)
+        dev = self.convs[0].weight.device
+        self.amax = torch.zeros(max(1, n_fp8), dtype=torch.int32, device=dev)
+        j = 0
+        for c in self.convs:
+            co, ci, kh, kw = c.weight.shape
+            ci_pad = ci if ci % 8 == 0 else (ci + 7) // 8 * 8
+            kp = kh * kw * ci_pad
+            e = dict(ci_pad=ci_pad, kp=kp, fwd=torch.empty(co, kp, dtype=torch.bfloat16, device=dev), dgrad=None,
+                     q8=None, amax=None)
+            if kh > 1 and c.stride[0] == 1 and ci_pad == ci and co % 8 == 0:
+                e["dgrad"] = torch.empty(ci, kh * kw * co, dtype=torch.bfloat16, device=dev)
+            if id(c) in fp8_ids:
+                e["q8"] = torch.empty(co, kp, dtype=torch.uint8, device=dev)
+                e["amax"] = self.amax[j:j + 1]
+                j += 1
+            self.entries[id(c)] = e
+        self.n_fp8 = n_fp8
+        self._key = None
+        self._descs = None
+
+    def get(self, conv):
+        return self.entries.get(id(conv))
+
+    def pack(self) -> None:
+        key = tuple(c.weight.data_ptr() for c in self.convs)
+        if key != self._key:  # parameters re-pointed (e.g. into a flat DDP buffer): rebuild the descriptors
+            arr = (N.PackDesc * len(self.convs))()
+            for i, c in enumerate(self.convs):
+                e = self.entries[id(c)]
+                co, ci, kh, kw = c.weight.shape
+                if not c.weight.is_contiguous():
+                    raise ValueError("WeightPack: conv weights must be contiguous")
+                arr[i] = N.PackDesc(w=c.weight.data_ptr(), fwd=e["fwd"].data_ptr(),
+                                    dgrad=e["dgrad"].data_ptr() if e["dgrad"] is not None else None,
+                                    q8=e["q8"].data_ptr() if e["q8"] is not None else None,
+                                    amax=e["amax"].data_ptr() if e["amax"] is not None else None,
+                                    co=co, ci=ci, ci_pad=e["ci_pad"], kh=kh, kw=kw, kp=e["kp"])
+            host = torch.frombuffer(bytearray(bytes(arr)), dtype=torch.uint8)
+            self._descs = host.to(self.amax.device)
+            self._key = key
+        N.check(N.lib().dca_ops_pack_weights(N.ptr(self._descs), len(self.convs), self.BLOCKS_PER_LAYER,
+                                             N.ptr(self.amax), self.n_fp8, N.stream(self.amax.device)),
+                "pack_weights")
+
+
+def grad_sink(p: torch.Tensor):
+    """(flat gradient view, ready callback) that FlatBucketDDP attaches to its parameters, or None.  A kernel
+    that owns a parameter's whole gradient for the step writes (accumulates) it straight into the view and
+    signals readiness, so no gradient tensor is materialised and no accumulate kernel runs."""
+    return getattr(p, "_dca_grad_sink", None)
 
 
 class Fp8Delayed:
@@ -213,15 +296,18 @@ def _fp8_operand(cols, state: Optional["Fp8Delayed"]):
     return q, bits, False
 
 
-def _conv_fwd(x, w, b, stride, pad, relu, fp8, col_stats=None, shift=None, fp8_state=None):
-    """Forward GEMM of a conv; returns (y [N,Ho,Wo,Cout] bf16, state for _conv_bwd)."""
+def _conv_fwd(x, w, b, stride, pad, relu, fp8, col_stats=None, shift=None, fp8_state=None, packed=None):
+    """Forward GEMM of a conv; returns (y [N,Ho,Wo,Cout] bf16, state for _conv_bwd).  ``packed``: this conv's
+    WeightPack entry (pre-built bf16 / fp8 operands) or None (operands built here from the fp32 weight)."""
     x = x.contiguous()
     g = _geom(x, w, stride, pad)
     co = w.shape[0]
     M = g.N * g.Ho * g.Wo
     direct = w.shape[2] == 1 and w.shape[3] == 1 and stride == 1 and pad == 0
-    st = dict(geom=g, wshape=tuple(w.shape), x=x, cols=None)
-    use_fp8 = fp8 and g.Kp % 16 == 0
+    st = dict(geom=g, wshape=tuple(w.shape), x=x, cols=None, packed=packed)
+    if packed is not None and packed["kp"] != g.K:
+        raise ValueError("conv: packed weight does not match the input channels")
+    use_fp8 = fp8 and g.Kp % 16 == 0 and (packed is None or packed["q8"] is not None)
     if direct or use_fp8 or not _implicit_ok(g):
         if direct:
             cols = x.view(M, g.K)
@@ -229,27 +315,33 @@ def _conv_fwd(x, w, b, stride, pad, relu, fp8, col_stats=None, shift=None, fp8_s
             cols = torch.empty(M, g.Kp, dtype=torch.bfloat16, device=x.device)
             N.check(N.lib().dca_ops_im2col(N.ptr(x), N.ptr(cols), g, N.stream(x.device)), "im2col")
         st["cols"] = cols
-        wm = _weight_matrix(w, g.Kp)
+        wm = packed["fwd"] if packed is not None and g.Kp == g.K else _weight_matrix(w, g.Kp)
         if use_fp8:
             qc, ac, delayed = _fp8_operand(cols, fp8_state)
-            qw, aw = quantize_fp8(wm)
-            y = gemm(qc, qw, bias=b, relu=relu, out_dtype=torch.bfloat16, alpha_dev=fp8_alpha(ac, aw),
+            if packed is not None:
+                qw, aw = packed["q8"], packed["amax"]
+            else:
+                qw, aw = quantize_fp8(wm)
+            y = gemm(qc, qw, bias=b, relu=relu, out_dtype=torch.bfloat16, amax_a=ac, amax_b=aw,
                      col_stats=col_stats, stats_shift=shift)
             if delayed:  # this step's amax (recorded by the producer) scales the next step
                 fp8_state.amax_prev.copy_(fp8_state.amax_out.view(torch.float32))
         else:
             y = gemm(cols, wm, bias=b, relu=relu, out_dtype=torch.bfloat16, col_stats=col_stats, stats_shift=shift)
     else:  # implicit GEMM: the im2col matrix is never materialised
-        wm = _weight_matrix(w, g.K)
+        wm = packed["fwd"] if packed is not None else _weight_matrix(w, g.K)
         y = gemm(x, wm, conv=1, geom=g, mnk=(M, co, g.K), bias=b, relu=relu, out_dtype=torch.bfloat16,
                  col_stats=col_stats, stats_shift=shift)
     st["wm"] = wm
     return y.view(g.N, g.Ho, g.Wo, co), st
 
 
-def _conv_bwd(dy, st, need_x: bool, need_w: bool):
-    """(dx, dw) of a conv from dY [N,Ho,Wo,Cout] (any dtype) and the forward state."""
+def _conv_bwd(dy, st, need_x: bool, need_w: bool, sink=None):
+    """(dx, dw) of a conv from dY [N,Ho,Wo,Cout] (any dtype) and the forward state.  The weight gradient is
+    written by the GEMM's reduce pass directly in torch's [Cout, Cin, KH, KW] layout -- into ``sink`` (a flat
+    gradient view, accumulated; dw returned as None) when given."""
     g, (co, ci, kh, kw) = st["geom"], st["wshape"]
+    packed = st.get("packed")
     M = g.N * g.Ho * g.Wo
     dyb = dy.to(torch.bfloat16).contiguous().view(M, co)
     dx = dw = None
@@ -257,11 +349,14 @@ def _conv_bwd(dy, st, need_x: bool, need_w: bool):
     if need_x:
         if cols is not None and cols.data_ptr() == st["x"].data_ptr():  # 1x1 / stride 1: dX = dY . W
             dx = gemm(dyb, st["wm"], tb=True, out_dtype=torch.bfloat16).view(g.N, g.H, g.W, g.C)
-        elif g.stride == 1 and co % 8 == 0 and kh == kw and g.pad <= kh - 1:
+        elif g.stride == 1 and co % 8 == 0 and kh == kw and g.pad <= kh - 1 and g.C == ci:
             # stride 1: dX = conv(dY, W flipped, ci<->co, pad KH-1-pad), implicit GEMM (no col2im)
             gd = N.ConvGeom(N=g.N, H=g.Ho, W=g.Wo, C=co, KH=kh, KW=kw, stride=1, pad=kh - 1 - g.pad, Ho=g.H, Wo=g.W,
                             K=kh * kw * co, Kp=kh * kw * co)
-            wd = st.get("w_master").flip(2, 3).permute(1, 2, 3, 0).reshape(ci, -1).to(torch.bfloat16).contiguous()
+            if packed is not None and packed["dgrad"] is not None:
+                wd = packed["dgrad"]
+            else:
+                wd = st.get("w_master").flip(2, 3).permute(1, 2, 3, 0).reshape(ci, -1).to(torch.bfloat16).contiguous()
             dx = gemm(dyb.view(g.N, g.Ho, g.Wo, co), wd, conv=1, geom=gd, mnk=(g.N * g.H * g.W, ci, gd.K),
                       out_dtype=torch.bfloat16).view(g.N, g.H, g.W, g.C)
         else:
@@ -273,12 +368,16 @@ def _conv_bwd(dy, st, need_x: bool, need_w: bool):
             dx = torch.empty(g.N, g.H, g.W, g.C, dtype=torch.bfloat16, device=dy.device)
             N.check(N.lib().dca_ops_col2im(N.ptr(dcols), N.ptr(dx), gc, N.stream(dy.device)), "col2im")
     if need_w:
+        dst = sink if sink is not None else torch.empty(co, ci, kh, kw, dtype=torch.float32, device=dy.device)
+        beta = 1.0 if sink is not None else 0.0
+        perm = (ci, g.C, kh * kw)
         if cols is not None:
             kp = cols.shape[1]
-            dwm = gemm(dyb, cols, ta=True, tb=True, splits=_wgrad_splits(co, kp, M))  # [Cout, Kp] fp32
+            gemm(dyb, cols, ta=True, tb=True, splits=_wgrad_splits(co, kp, M), out=dst, beta=beta, wperm=perm)
         else:  # implicit: B(n = tap*C + c, k = pixel) gathered from x
-            dwm = gemm(dyb, st["x"], ta=True, conv=2, geom=g, mnk=(co, g.K, M), splits=_wgrad_splits(co, g.K, M))
-        dw = dwm[:, :g.K].reshape(co, kh, kw, ci).permute(0, 3, 1, 2).contiguous()
+            gemm(dyb, st["x"], ta=True, conv=2, geom=g, mnk=(co, g.K, M), splits=_wgrad_splits(co, g.K, M),
+                 out=dst, beta=beta, wperm=perm)
+        dw = None if sink is not None else dst
     return dx, dw
 
 
@@ -309,14 +408,14 @@ class _ConvBNAct(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, w, r, gamma, beta, running_mean, running_var, stride, pad, eps, momentum, relu, res_mode, fp8,
-                fp8_state, emit):
+                fp8_state, emit, packed, sinks):
         co = w.shape[0]
         g = _geom(x, w, stride, pad)
         M = g.N * g.Ho * g.Wo
         nparts = (M + 127) // 128
         part = torch.empty(nparts, co, 2, dtype=torch.float32, device=x.device)
         y, st = _conv_fwd(x, w, None, stride, pad, False, fp8, col_stats=part, shift=running_mean,
-                          fp8_state=fp8_state)
+                          fp8_state=fp8_state, packed=packed)
         st["w_master"] = w.detach()
         r = r.contiguous() if r is not None else None
         out = torch.empty_like(y)
@@ -333,6 +432,7 @@ class _ConvBNAct(torch.autograd.Function):
         if q is not None:
             emit.q, emit.src_ptr = q, out.data_ptr()
         ctx.st = st
+        ctx.sinks = sinks
         ctx.save_for_backward(y, r, gamma, beta, stats)
         ctx.relu, ctx.res_mode = relu, res_mode
         return out
@@ -340,17 +440,28 @@ class _ConvBNAct(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dout):
         y, r, gamma, beta, stats = ctx.saved_tensors
-        dy_conv, dr, dgamma, dbeta = _bn_backward(dout, y, r, gamma, beta, stats, ctx.relu, ctx.res_mode)
-        dx, dw = _conv_bwd(dy_conv, ctx.st, ctx.needs_input_grad[0], ctx.needs_input_grad[1])
-        ctx.st = None
-        return dx, dw, dr, dgamma, dbeta, None, None, None, None, None, None, None, None, None, None, None
+        sw, sg, sb = ctx.sinks if ctx.sinks is not None else (None, None, None)
+        dy_conv, dr, dgamma, dbeta = _bn_backward(dout, y, r, gamma, beta, stats, ctx.relu, ctx.res_mode,
+                                                  dgamma_out=sg[0] if sg else None, dbeta_out=sb[0] if sb else None)
+        if sg:
+            sg[1]()
+            sb[1]()
+        dx, dw = _conv_bwd(dy_conv, ctx.st, ctx.needs_input_grad[0], ctx.needs_input_grad[1] or sw is not None,
+                           sink=sw[0] if sw else None)
+        if sw:
+            sw[1]()
+        ctx.st = ctx.sinks = None
+        return dx, dw, dr, dgamma, dbeta, None, None, None, None, None, None, None, None, None, None, None, None, None
 
 
 def conv_bn_act(x, conv: torch.nn.Conv2d, bn: torch.nn.BatchNorm2d, r=None, relu=True, fp8=False, res_mode=None,
-                fp8_state: Optional[Fp8Delayed] = None, emit: Optional[Fp8Delayed] = None):
+                fp8_state: Optional[Fp8Delayed] = None, emit: Optional[Fp8Delayed] = None, packed=None,
+                direct_grads: bool = False):
     """Training-mode act(bn(conv(x))) for NHWC bf16 x, conv without bias; with a residual r: res_mode 2 (default,
     ResNet: act(bn + r)) or 1 (NetResDeep: act(bn) + r).  fp8: forward GEMM in fp8 e4m3 (fp8_state: this conv's
-    delayed-scaling input state); emit: also produce the fp8 copy of the output that the consumer of ``emit`` reads."""
+    delayed-scaling input state); emit: also produce the fp8 copy of the output that the consumer of ``emit`` reads.
+    packed: the conv's WeightPack entry.  direct_grads: the conv weight and BN affine parameters are used once
+    per step, so their gradients may be written straight into FlatBucketDDP's flat buffer (``grad_sink``)."""
     if res_mode is None:
         res_mode = 2 if r is not None else 0
     if conv.bias is not None or not bn.training:
@@ -358,8 +469,13 @@ def conv_bn_act(x, conv: torch.nn.Conv2d, bn: torch.nn.BatchNorm2d, r=None, relu
     momentum = bn.momentum if bn.track_running_stats else 0.0
     if bn.track_running_stats:
         bn.num_batches_tracked.add_(1)
+    sinks = None
+    if direct_grads and torch.is_grad_enabled():
+        sw, sg, sb = grad_sink(conv.weight), grad_sink(bn.weight), grad_sink(bn.bias)
+        if sw is not None and sg is not None and sb is not None:
+            sinks = (sw, sg, sb)
     return _ConvBNAct.apply(x, conv.weight, r, bn.weight, bn.bias, bn.running_mean, bn.running_var, conv.stride[0],
-                            conv.padding[0], bn.eps, momentum, relu, res_mode, fp8, fp8_state, emit)
+                            conv.padding[0], bn.eps, momentum, relu, res_mode, fp8, fp8_state, emit, packed, sinks)
 
 
 def conv2d(x, w, b=None, stride=1, pad=0, relu=False, fp8=False):
@@ -394,22 +510,26 @@ class _BatchNormAct(torch.autograd.Function):
         return dx, dr, dgamma, dbeta, None, None, None, None, None, None
 
 
-def _bn_backward(dy, x, r, gamma, beta, stats, relu, res_mode):
-    """(dx, dr, dgamma, dbeta) of the fused BN + ReLU + residual."""
+def _bn_backward(dy, x, r, gamma, beta, stats, relu, res_mode, dgamma_out=None, dbeta_out=None):
+    """(dx, dr, dgamma, dbeta) of the fused BN + ReLU + residual.  dgamma_out / dbeta_out: flat gradient views
+    to accumulate into (then dgamma / dbeta are returned as None)."""
     dy = dy.to(torch.bfloat16).contiguous()
     C = x.shape[-1]
     M = x.numel() // C
     part = torch.empty((M + 255) // 256, C, 2, dtype=torch.float32, device=x.device)
     sums = torch.empty(C, 2, dtype=torch.float32, device=x.device)
-    dgamma = torch.empty(C, dtype=torch.float32, device=x.device)
-    dbeta = torch.empty_like(dgamma)
+    direct = dgamma_out is not None and dbeta_out is not None
+    dgamma = dgamma_out if direct else torch.empty(C, dtype=torch.float32, device=x.device)
+    dbeta = dbeta_out if direct else torch.empty_like(dgamma)
     dx = torch.empty_like(x)
     dr = torch.empty_like(x) if res_mode == 2 else None
     N.check(N.lib().dca_ops_bn_bwd(N.ptr(dy), N.ptr(x), N.ptr(r), N.ptr(stats), N.ptr(gamma), N.ptr(beta),
                                    N.ptr(part), N.ptr(sums), N.ptr(dgamma), N.ptr(dbeta), N.ptr(dx), N.ptr(dr),
-                                   M, C, int(relu), int(res_mode), 0, N.stream(x.device)), "bn_bwd")
+                                   M, C, int(relu), int(res_mode), int(direct), N.stream(x.device)), "bn_bwd")
     if res_mode == 1:
         dr = dy
+    if direct:
+        return dx, dr, None, None
     return dx, dr, dgamma, dbeta
 
 

@@ -10,7 +10,10 @@ switches to channels-last bf16 once, and runs:
   -> fc2 (fp32 logits).  fc1's columns are permuted from the reference's NCHW flatten order to NHWC.
 * ResNet-50/101: stem 7x7/2 conv -> BN + ReLU -> 3x3/2 max pool -> bottlenecks (1x1, 3x3, 1x1 convs, each BN
   fused with its ReLU; the last one with the residual add before the ReLU, res_mode 2) -> global average pool
-  -> fc.  With ``fp8=True`` the 1x1 convolutions (Cin >= 128) and fc run their forward GEMM in fp8 e4m3 on the
+  -> fc.  The bf16 (and fp8) GEMM operands of all convolutions are rebuilt from the fp32 weights by one
+  ``WeightPack`` launch per step, and the conv / BN parameter gradients are written straight into the flat
+  gradient buffer of ``FlatBucketDDP`` when the model is wrapped in it (``functional.grad_sink``).
+  With ``fp8=True`` the 1x1 convolutions (Cin >= 128) and fc run their forward GEMM in fp8 e4m3 on the
   MX-scaled MFMA (fp8 rate): weights are quantised per step with a device-side amax; activations are emitted in
   fp8 directly by the producing BN kernel with delayed scaling (previous step's amax, ``functional.Fp8Delayed``);
   gradients and the backward stay bf16 (BASELINE config 5).
@@ -33,10 +36,22 @@ class OpsModel(nn.Module):
         self.module = model
         self.fp8 = fp8
         self.kind = "netresdeep" if _is_netresdeep(model) else "resnet"
+        self._pack = None
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
-        h = x.permute(0, 2, 3, 1).to(torch.bfloat16).contiguous()  # NCHW fp32 -> NHWC bf16
-        return self._netresdeep(h) if self.kind == "netresdeep" else self._resnet(h)
+        if self.kind == "netresdeep":
+            h = x.permute(0, 2, 3, 1).to(torch.bfloat16).contiguous()  # NCHW fp32 -> NHWC bf16
+            return self._netresdeep(h)
+        # ResNet: the 3-channel input is zero-padded to 8 channels so the 7x7 stem is an implicit GEMM
+        h = x.permute(0, 2, 3, 1)
+        if h.shape[-1] % 8:
+            h = torch.nn.functional.pad(h, (0, 8 - h.shape[-1] % 8))
+        h = h.to(torch.bfloat16).contiguous()
+        if self._pack is None:
+            convs = [m for m in self.module.modules() if isinstance(m, nn.Conv2d)]
+            self._pack = F.WeightPack(convs, [c for c in convs if self._fp8_ok(c)])
+        self._pack.pack()  # every conv's bf16 / fp8 GEMM operands from this step's fp32 weights: one launch
+        return self._resnet(h)
 
     # reference model/resnet.py:15-22, 33-37
     def _netresdeep(self, h):
@@ -65,8 +80,10 @@ class OpsModel(nn.Module):
         return self._fp8.setdefault(id(conv), F.Fp8Delayed())
 
     def _conv_bn(self, h, conv, bn, relu=True, r=None, consumer=None):
+        # every ResNet conv / BN is applied once per step: gradients may go straight into the flat DDP buffer
         return F.conv_bn_act(h, conv, bn, r=r, relu=relu, fp8=self._fp8_ok(conv), fp8_state=self._state(conv),
-                             emit=self._state(consumer) if consumer is not None else None)
+                             emit=self._state(consumer) if consumer is not None else None,
+                             packed=self._pack.get(conv), direct_grads=True)
 
     def _resnet(self, h):
         m = self.module

@@ -117,6 +117,9 @@ class FlatBucketDDP(nn.Module):
                     self._comm_stream = torch.cuda.Stream(dev)
         for p in order:
             p.register_post_accumulate_grad_hook(self._make_hook(p))
+            # direct-write protocol (ops/functional.py grad_sink): a kernel that produces a parameter's whole
+            # gradient for the step accumulates it into the flat view and reports readiness itself
+            p._dca_grad_sink = (self._views[p][2], self._make_ready(p))
 
     # ---- collectives ------------------------------------------------------------------------------------------
     def _sync_module_states(self) -> None:
@@ -143,6 +146,8 @@ class FlatBucketDDP(nn.Module):
                     o += b.numel()
 
     def _make_hook(self, p):
+        ready = self._make_ready(p)
+
         def hook(param):
             off, n, view = self._views[p]
             if param.grad is None or param.grad.data_ptr() != view.data_ptr():
@@ -150,6 +155,11 @@ class FlatBucketDDP(nn.Module):
                 if param.grad is not None:
                     view.copy_(param.grad)
                 param.grad = view
+            ready()
+        return hook
+
+    def _make_ready(self, p):
+        def ready():
             if self.world_size == 1:
                 return
             if not self._callback_queued:
@@ -159,7 +169,7 @@ class FlatBucketDDP(nn.Module):
             self._pending[bi] -= 1
             if self._pending[bi] == 0:
                 self._launch(bi)
-        return hook
+        return ready
 
     def _launch(self, bi: int) -> None:
         s, e, _ = self.buckets[bi]

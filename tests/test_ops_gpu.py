@@ -322,3 +322,75 @@ def test_conv_bn_act(gpu, k, s, p, res_mode, fp8):
     assert _rel(bn.running_mean, rbn.running_mean) < 1e-2 and _rel(bn.running_var, rbn.running_var) < 1e-2
     if res_mode:
         assert _rel(r.grad.float().permute(0, 3, 1, 2), rr.grad) < gtol
+
+
+def test_weight_pack(gpu):
+    """WeightPack (one launch for all layers) == the per-layer torch formulation of every GEMM operand: bf16
+    forward matrix (3-channel stem zero-padded to 8 channels), flipped dgrad matrix, fp8 copy + amax."""
+    from distributeddataparallel_cifar10_amd.ops import functional as F
+    torch.manual_seed(3)
+    convs = [torch.nn.Conv2d(3, 16, 7, stride=2, padding=3, bias=False), torch.nn.Conv2d(32, 64, 3, padding=1),
+             torch.nn.Conv2d(128, 64, 1, bias=False)]
+    convs = [c.to(gpu) for c in convs]
+    pack = F.WeightPack(convs, [convs[2]])
+    pack.pack()
+    w0 = convs[0].weight.detach()
+    ref0 = TF.pad(w0.permute(0, 2, 3, 1), (0, 5)).reshape(16, -1).to(torch.bfloat16)
+    assert torch.equal(pack.get(convs[0])["fwd"], ref0)
+    assert pack.get(convs[0])["dgrad"] is None
+    w1 = convs[1].weight.detach()
+    e1 = pack.get(convs[1])
+    assert torch.equal(e1["fwd"], F._weight_matrix(w1, 288))
+    assert torch.equal(e1["dgrad"], w1.flip(2, 3).permute(1, 2, 3, 0).reshape(32, -1).to(torch.bfloat16))
+    e2 = pack.get(convs[2])
+    q, amax = F.quantize_fp8(convs[2].weight.detach().reshape(64, 128).contiguous())
+    assert torch.equal(e2["amax"], amax) and torch.equal(e2["q8"], q)
+    with torch.no_grad():  # weights change -> the next pack() reflects them (same descriptors)
+        convs[1].weight.mul_(-2.0)
+    pack.pack()
+    assert torch.equal(e1["fwd"], F._weight_matrix(convs[1].weight.detach(), 288))
+
+
+def test_weight_grad_layout_remap(gpu):
+    """Weight gradients written by the GEMM reduce pass straight into [Cout, Cin, KH, KW] (accumulating with
+    beta = 1), for the implicit and the explicit (im2col) form."""
+    from distributeddataparallel_cifar10_amd.ops import functional as F
+    g = torch.Generator(device=gpu).manual_seed(5)
+    x = _bf(torch.randn(2, 9, 9, 16, device=gpu, generator=g))
+    w = torch.randn(24, 16, 3, 3, device=gpu, generator=g)
+    geo = F._geom(x, w, 1, 1)
+    M = 2 * 9 * 9
+    dy = _bf(torch.randn(M, 24, device=gpu, generator=g))
+    ref = torch.nn.grad.conv2d_weight(x.float().permute(0, 3, 1, 2), w.shape,
+                                      dy.float().view(2, 9, 9, 24).permute(0, 3, 1, 2), padding=1)
+    out = torch.ones_like(w)
+    F.gemm(dy, x, ta=True, conv=2, geom=geo, mnk=(24, geo.K, M), splits=2, out=out, beta=1.0, wperm=(16, 16, 9))
+    assert _rel(out - 1.0, ref) < 1e-5
+    cols = torch.empty(M, geo.Kp, dtype=torch.bfloat16, device=gpu)
+    from distributeddataparallel_cifar10_amd.ops import _native as N
+    N.check(N.lib().dca_ops_im2col(N.ptr(x), N.ptr(cols), geo, N.stream(gpu)), "im2col")
+    out2 = torch.empty_like(w)
+    F.gemm(dy, cols, ta=True, tb=True, splits=1, out=out2, wperm=(16, 16, 9))
+    assert _rel(out2, ref) < 1e-5
+
+
+@pytest.mark.parametrize("fp8", [False, True])
+def test_direct_grads_match_autograd(gpu, fp8):
+    """With FlatBucketDDP the ResNet conv / BN gradients are written straight into the flat buffer (grad
+    sinks); they must equal the autograd-accumulated gradients of the same step without the wrapper."""
+    import copy
+    from distributeddataparallel_cifar10_amd.models.resnet50 import ResNet
+    from distributeddataparallel_cifar10_amd.ops import OpsModel, cross_entropy
+    from distributeddataparallel_cifar10_amd.parallel.flat_ddp import FlatBucketDDP
+    torch.manual_seed(2)
+    a = ResNet([1, 1, 1, 1], num_classes=10).to(gpu)
+    b = copy.deepcopy(a)
+    x = torch.randn(4, 3, 64, 64, device=gpu)
+    y = torch.randint(0, 10, (4,), device=gpu)
+    ddp = FlatBucketDDP(OpsModel(a, fp8=fp8))
+    ddp.zero_grad()
+    cross_entropy(ddp(x), y).backward()
+    cross_entropy(OpsModel(b, fp8=fp8)(x), y).backward()
+    for (n, p), (_, q) in zip(a.named_parameters(), b.named_parameters()):
+        assert p.grad is not None and q.grad is not None, n
+        assert _rel(p.grad, q.grad) < 1e-6, (n, _rel(p.grad, q.grad))
