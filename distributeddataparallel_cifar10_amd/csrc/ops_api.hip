@@ -100,7 +100,8 @@ int dca_ops_gemm(const GemmArgs* a, void* stream) {
     if (g.fp8) hipLaunchKernelGGL((k_gemm<true, 128>), grid, dim3(GT), GemmTile<128>::LDS, st, g);
     else hipLaunchKernelGGL((k_gemm<false, 128>), grid, dim3(GT), GemmTile<128>::LDS, st, g);
   }
-  if (g.splits > 1 || g.wperm_T > 0) hipLaunchKernelGGL(k_gemm_splitk_reduce, dim3(grid_for((long)g.M * g.N)), dim3(256), 0, st, g);
+  if (g.splits > 1 || g.wperm_T > 0)
+    hipLaunchKernelGGL(k_gemm_splitk_reduce, dim3(grid_for((long)g.M * g.N, RED_EL, 4096)), dim3(256), 0, st, g);
   OPCK(hipGetLastError());
   return 0;
 }

@@ -457,27 +457,47 @@ __global__ void __launch_bounds__(GT) k_gemm(GemmArgs g) {
   }
 }
 
-// Split-K combine: C = alpha * sum_s ws[s] (+bias) (+beta*C) (ReLU), fixed summation order (deterministic).
+// Split-K combine: C = alpha * sum_s ws[s] (+bias) (+beta*C) (ReLU).  256 threads = 64 consecutive elements x 4
+// split lanes (lane l sums slabs l, l+4, ...; the 4 partials are added in lane order: deterministic), so
+// thousands of slabs of a small weight gradient are read by many threads with 256-B row segments.
 // With wperm_T > 0 the column is remapped to torch's weight layout (see GemmArgs) and padded channels dropped.
+constexpr int RED_EL = 64, RED_LANES = 4;
 __global__ void __launch_bounds__(256) k_gemm_splitk_reduce(GemmArgs g) {
+  __shared__ float red[RED_LANES][RED_EL];
   const size_t total = (size_t)g.M * g.N;
   const float alpha = gemm_alpha(g);
-  for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < total; i += (size_t)gridDim.x * 256) {
-    const int row = (int)(i / g.N), col = (int)(i % g.N);
-    size_t o = (size_t)row * g.ldc + col;
-    if (g.wperm_T > 0) {
-      const int tap = col / g.wperm_Cpad, c = col - tap * g.wperm_Cpad;
-      if (c >= g.wperm_C || tap >= g.wperm_T) continue;
-      o = ((size_t)row * g.wperm_C + c) * g.wperm_T + tap;
-    }
+  const int el = threadIdx.x % RED_EL, sl = threadIdx.x / RED_EL;
+  for (size_t base = (size_t)blockIdx.x * RED_EL; base < total; base += (size_t)gridDim.x * RED_EL) {
+    const size_t i = base + el;
     float v = 0.f;
-    for (int s = 0; s < g.splits; ++s) v += g.ws[(size_t)s * total + i];
-    v *= alpha;
-    if (g.bias) v += g.bias[col];
-    if (g.beta != 0.f) v += g.beta * (g.out_bf16 ? bf2f(((const unsigned short*)g.C)[o]) : ((const float*)g.C)[o]);
-    if (g.relu) v = v > 0.f ? v : 0.f;
-    if (g.out_bf16) ((unsigned short*)g.C)[o] = f2bf_rne(v);
-    else ((float*)g.C)[o] = v;
+    if (i < total) {
+      const float* p = g.ws + i;
+      int s = sl;
+#pragma unroll 4
+      for (; s < g.splits; s += RED_LANES) v += p[(size_t)s * total];
+    }
+    red[sl][el] = v;
+    __syncthreads();
+    if (sl == 0 && i < total) {
+      v = (red[0][el] + red[1][el]) + (red[2][el] + red[3][el]);
+      const int row = (int)(i / g.N), col = (int)(i % g.N);
+      size_t o = (size_t)row * g.ldc + col;
+      bool keep = true;
+      if (g.wperm_T > 0) {
+        const int tap = col / g.wperm_Cpad, c = col - tap * g.wperm_Cpad;
+        keep = c < g.wperm_C && tap < g.wperm_T;
+        o = ((size_t)row * g.wperm_C + c) * g.wperm_T + tap;
+      }
+      if (keep) {
+        v *= alpha;
+        if (g.bias) v += g.bias[col];
+        if (g.beta != 0.f) v += g.beta * (g.out_bf16 ? bf2f(((const unsigned short*)g.C)[o]) : ((const float*)g.C)[o]);
+        if (g.relu) v = v > 0.f ? v : 0.f;
+        if (g.out_bf16) ((unsigned short*)g.C)[o] = f2bf_rne(v);
+        else ((float*)g.C)[o] = v;
+      }
+    }
+    __syncthreads();
   }
 }
 

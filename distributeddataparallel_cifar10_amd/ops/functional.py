@@ -123,9 +123,12 @@ def amax_value(amax_bits: torch.Tensor) -> torch.Tensor:
 
 
 def _wgrad_splits(M: int, Nn: int, K: int) -> int:
-    """Split-K factor for a weight-gradient GEMM (K = pixels: long): ~512 workgroups, fp32 slab <= 64 MiB."""
+    """Split-K factor for a weight-gradient GEMM (K = pixels: long, M x N small): enough workgroups to fill the
+    chip twice over (2 resident per CU x 256 CUs), >= 4 K-tiles per split, fp32 slab <= 64 MiB."""
     tiles = math.ceil(M / 128) * math.ceil(Nn / 128)
-    return max(1, min(K // 256, max(1, 512 // tiles), 128, max(1, (16 << 20) // (M * Nn))))
+    s = math.ceil(1024 / tiles)
+    s = min(s, K // 256, max(1, (64 << 20) // (4 * M * Nn)))
+    return max(1, s)
 
 
 # ------------------------------------------------------------------------------------------------------------
@@ -200,7 +203,7 @@ class WeightPack:
     permute / pad / cast chain per layer and per use.
 
     Per conv: ``fwd`` [Cout, KH*KW*Cin_pad] (forward, strided input gradient), ``dgrad`` [Cin, KH*KW*Cout]
-    (flipped; stride-1 KxK input gradient as an implicit conv) and, for ``fp8`` layers, ``q8`` + ``amax``.
+    (flipped; stride-1 input gradient: an implicit conv for KxK, a plain NT GEMM with W^T for 1x1) and, for ``fp8`` layers, ``q8`` + ``amax``.
     Cin_pad = 8 for a stem with fewer than 8 channels (its input is zero-padded to 8 channels, so the stem runs
     as an implicit GEMM instead of through an im2col buffer)."""
 
@@ -220,7 +223,7 @@ class WeightPack:
             kp = kh * kw * ci_pad
             e = dict(ci_pad=ci_pad, kp=kp, fwd=torch.empty(co, kp, dtype=torch.bfloat16, device=dev), dgrad=None,
                      q8=None, amax=None)
-            if kh > 1 and c.stride[0] == 1 and ci_pad == ci and co % 8 == 0:
+            if c.stride[0] == 1 and ci_pad == ci and co % 8 == 0 and (kh > 1 or c.padding[0] == 0):
                 e["dgrad"] = torch.empty(ci, kh * kw * co, dtype=torch.bfloat16, device=dev)
             if id(c) in fp8_ids:
                 e["q8"] = torch.empty(co, kp, dtype=torch.uint8, device=dev)
@@ -348,7 +351,10 @@ def _conv_bwd(dy, st, need_x: bool, need_w: bool, sink=None):
     cols = st["cols"]
     if need_x:
         if cols is not None and cols.data_ptr() == st["x"].data_ptr():  # 1x1 / stride 1: dX = dY . W
-            dx = gemm(dyb, st["wm"], tb=True, out_dtype=torch.bfloat16).view(g.N, g.H, g.W, g.C)
+            if packed is not None and packed["dgrad"] is not None:  # W^T [Cin, Cout] from the pack: plain NT
+                dx = gemm(dyb, packed["dgrad"], out_dtype=torch.bfloat16).view(g.N, g.H, g.W, g.C)
+            else:
+                dx = gemm(dyb, st["wm"], tb=True, out_dtype=torch.bfloat16).view(g.N, g.H, g.W, g.C)
         elif g.stride == 1 and co % 8 == 0 and kh == kw and g.pad <= kh - 1 and g.C == ci:
             # stride 1: dX = conv(dY, W flipped, ci<->co, pad KH-1-pad), implicit GEMM (no col2im)
             gd = N.ConvGeom(N=g.N, H=g.Ho, W=g.Wo, C=co, KH=kh, KW=kw, stride=1, pad=kh - 1 - g.pad, Ho=g.H, Wo=g.W,

@@ -345,6 +345,7 @@ def test_weight_pack(gpu):
     e2 = pack.get(convs[2])
     q, amax = F.quantize_fp8(convs[2].weight.detach().reshape(64, 128).contiguous())
     assert torch.equal(e2["amax"], amax) and torch.equal(e2["q8"], q)
+    assert torch.equal(e2["dgrad"], convs[2].weight.detach().reshape(64, 128).t().to(torch.bfloat16))
     with torch.no_grad():  # weights change -> the next pack() reflects them (same descriptors)
         convs[1].weight.mul_(-2.0)
     pack.pack()
