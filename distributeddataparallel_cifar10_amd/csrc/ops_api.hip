@@ -6,8 +6,10 @@
 #include <algorithm>
 #include <cstring>
 #include <string>
+#include <cstdlib>
 
 #include "ops_nn.hip"
+#include "ops_wgrad.hip"
 
 namespace {
 thread_local std::string g_err;
@@ -32,6 +34,14 @@ inline int grid_for(long work, int per_block = 256, int cap = 8192) {
   return (int)std::max(1L, std::min(b, (long)cap));
 }
 bool g_lds_set = false;
+// DCA_OPS_WGRAD=0 routes weight gradients through the general k_gemm (A/B comparisons)
+inline bool getenv_wgrad_ok() {
+  static const int v = [] {
+    const char* e = getenv("DCA_OPS_WGRAD");
+    return (e && e[0] == '0') ? 0 : 1;
+  }();
+  return v != 0;
+}
 inline int nparts_rows(long M) { return (int)((M + dca::ops::BN_ROWS - 1) / dca::ops::BN_ROWS); }
 }  // namespace
 
@@ -73,6 +83,14 @@ int dca_ops_gemm(const GemmArgs* a, void* stream) {
                              GemmTile<64>::LDS));
     OPCK(hipFuncSetAttribute((const void*)k_gemm<true, 64>, hipFuncAttributeMaxDynamicSharedMemorySize,
                              GemmTile<64>::LDS));
+    {
+      constexpr int l00 = WgradTile<64, 64, 2>::LDS, l01 = WgradTile<64, 128, 1>::LDS;
+      constexpr int l10 = WgradTile<128, 64, 4>::LDS, l11 = WgradTile<128, 128, 2>::LDS;
+      OPCK(hipFuncSetAttribute((const void*)k_wgrad<64, 64, 2>, hipFuncAttributeMaxDynamicSharedMemorySize, l00));
+      OPCK(hipFuncSetAttribute((const void*)k_wgrad<64, 128, 1>, hipFuncAttributeMaxDynamicSharedMemorySize, l01));
+      OPCK(hipFuncSetAttribute((const void*)k_wgrad<128, 64, 4>, hipFuncAttributeMaxDynamicSharedMemorySize, l10));
+      OPCK(hipFuncSetAttribute((const void*)k_wgrad<128, 128, 2>, hipFuncAttributeMaxDynamicSharedMemorySize, l11));
+    }
     g_lds_set = true;
   }
   const int kt = GBK_BYTES / (g.fp8 ? 1 : 2);
@@ -87,6 +105,25 @@ int dca_ops_gemm(const GemmArgs* a, void* stream) {
     g.splits = (g.K + kps - 1) / kps;
   } else {
     g.k_per_split = g.K;
+  }
+  // weight gradients (both operands pixel-major, bf16, 16-B aligned channel rows): the transposed-read kernel,
+  // always through the slab + reduce pass
+  const bool wgrad = !g.fp8 && g.ta && (g.tb || g.conv == 2) && g.M % 8 == 0 && g.N % 8 == 0 && g.lda % 8 == 0 &&
+                     (g.conv == 2 || g.ldb % 8 == 0) && g.ws != nullptr && getenv_wgrad_ok();
+  if (wgrad) {
+    const int bm = g.M <= 64 ? 64 : 128, bn = g.N <= 64 ? 64 : 128;
+    const long items = (long)((g.M + bm - 1) / bm) * ((g.N + bn - 1) / bn) * g.splits;
+    REQUIRE(items < (1L << 31), "gemm: too many work items");
+    const dim3 grid((unsigned)items);
+    constexpr int l00 = WgradTile<64, 64, 2>::LDS, l01 = WgradTile<64, 128, 1>::LDS;
+    constexpr int l10 = WgradTile<128, 64, 4>::LDS, l11 = WgradTile<128, 128, 2>::LDS;
+    if (bm == 64 && bn == 64) hipLaunchKernelGGL((k_wgrad<64, 64, 2>), grid, dim3(256), l00, st, g);
+    else if (bm == 64) hipLaunchKernelGGL((k_wgrad<64, 128, 1>), grid, dim3(256), l01, st, g);
+    else if (bn == 64) hipLaunchKernelGGL((k_wgrad<128, 64, 4>), grid, dim3(256), l10, st, g);
+    else hipLaunchKernelGGL((k_wgrad<128, 128, 2>), grid, dim3(256), l11, st, g);
+    hipLaunchKernelGGL(k_gemm_splitk_reduce, dim3(grid_for((long)g.M * g.N, RED_EL, 4096)), dim3(256), 0, st, g);
+    OPCK(hipGetLastError());
+    return 0;
   }
   // narrow N (<= 64) with a K-contiguous B operand: the 128x64 tile
   const bool narrow = g.N <= 64 && !g.tb && g.conv != 2;

@@ -395,3 +395,17 @@ def test_direct_grads_match_autograd(gpu, fp8):
     for (n, p), (_, q) in zip(a.named_parameters(), b.named_parameters()):
         assert p.grad is not None and q.grad is not None, n
         assert _rel(p.grad, q.grad) < 1e-6, (n, _rel(p.grad, q.grad))
+
+
+@pytest.mark.parametrize("M,N,K,splits", [(64, 64, 5000, 7), (64, 200, 3000, 3), (200, 64, 777, 1), (256, 392, 4096, 16),
+                                          (136, 1000, 130, 2), (8, 8, 64, 1)])
+def test_wgrad_transposed_read_kernel(gpu, M, N, K, splits):
+    """Weight-gradient GEMM C = A^T B with both operands pixel-major (k_wgrad: LDS tiles as loaded, MFMA fragments
+    by ds_read_b64_tr_b16) for every tile shape (64/128 x 64/128), ragged M, N, K and split-K, vs fp32 torch."""
+    from distributeddataparallel_cifar10_amd.ops import gemm
+    g = torch.Generator(device=gpu).manual_seed(M + N + K)
+    a = _bf(torch.randn(K, M, device=gpu, generator=g))
+    b = _bf(torch.randn(K, N, device=gpu, generator=g) * torch.linspace(0.5, 2.0, N, device=gpu))
+    ref = a.float().t() @ b.float()
+    out = gemm(a, b, ta=True, tb=True, splits=splits)
+    assert _rel(out, ref) < 1e-5, _rel(out, ref)
