@@ -130,12 +130,15 @@ int dca_ops_gemm(const GemmArgs* a, void* stream) {
   const int bn = narrow ? 64 : 128;
   const int tiles = ((g.M + GBM - 1) / GBM) * ((g.N + bn - 1) / bn);
   const dim3 grid(tiles, g.splits);
+  g.single = g.k_per_split <= 4 * kt ? 1 : 0;  // short K: one operand buffer, twice the workgroups per CU
   if (narrow) {
-    if (g.fp8) hipLaunchKernelGGL((k_gemm<true, 64>), grid, dim3(GT), GemmTile<64>::LDS, st, g);
-    else hipLaunchKernelGGL((k_gemm<false, 64>), grid, dim3(GT), GemmTile<64>::LDS, st, g);
+    const int lds = g.single ? GemmTile<64>::LDS_SINGLE : GemmTile<64>::LDS;
+    if (g.fp8) hipLaunchKernelGGL((k_gemm<true, 64>), grid, dim3(GT), lds, st, g);
+    else hipLaunchKernelGGL((k_gemm<false, 64>), grid, dim3(GT), lds, st, g);
   } else {
-    if (g.fp8) hipLaunchKernelGGL((k_gemm<true, 128>), grid, dim3(GT), GemmTile<128>::LDS, st, g);
-    else hipLaunchKernelGGL((k_gemm<false, 128>), grid, dim3(GT), GemmTile<128>::LDS, st, g);
+    const int lds = g.single ? GemmTile<128>::LDS_SINGLE : GemmTile<128>::LDS;
+    if (g.fp8) hipLaunchKernelGGL((k_gemm<true, 128>), grid, dim3(GT), lds, st, g);
+    else hipLaunchKernelGGL((k_gemm<false, 128>), grid, dim3(GT), lds, st, g);
   }
   if (g.splits > 1 || g.wperm_T > 0)
     hipLaunchKernelGGL(k_gemm_splitk_reduce, dim3(grid_for((long)g.M * g.N, RED_EL, 4096)), dim3(256), 0, st, g);
@@ -156,7 +159,8 @@ int dca_ops_im2col(const void* x, void* cols, const ConvGeom* geom, void* stream
 int dca_ops_col2im(const void* dcols, void* dx, const ConvGeom* geom, void* stream) {
   const ConvGeom g = *geom;
   REQUIRE(g.Kp % 8 == 0 && g.Kp >= g.K, "col2im: bad column geometry");
-  hipLaunchKernelGGL(k_col2im, dim3(grid_for((long)g.N * g.H * g.W * g.C)), dim3(256), 0, (hipStream_t)stream,
+  hipLaunchKernelGGL(k_col2im, dim3(grid_for((long)g.N * g.H * g.W * g.C / ((g.C & 7) == 0 ? 8 : 1))), dim3(256), 0,
+                     (hipStream_t)stream,
                      (const bf16_t*)dcols, (bf16_t*)dx, g);
   OPCK(hipGetLastError());
   return 0;
@@ -226,7 +230,8 @@ int dca_ops_bn_bwd(const void* dy, const void* x, const void* r, const float* st
 int dca_ops_maxpool_fwd(const void* x, void* y, void* arg, const PoolGeom* geom, void* stream) {
   const PoolGeom g = *geom;
   REQUIRE(g.K * g.K <= 255 && g.K > 0 && g.S > 0, "maxpool: bad window");
-  hipLaunchKernelGGL(k_maxpool_fwd, dim3(grid_for((long)g.N * g.Ho * g.Wo * g.C)), dim3(256), 0, (hipStream_t)stream,
+  hipLaunchKernelGGL(k_maxpool_fwd, dim3(grid_for((long)g.N * g.Ho * g.Wo * g.C / ((g.C & 7) == 0 ? 8 : 1))), dim3(256), 0,
+                     (hipStream_t)stream,
                      (const bf16_t*)x, (bf16_t*)y, (uint8_t*)arg, g);
   OPCK(hipGetLastError());
   return 0;

@@ -63,6 +63,9 @@ struct GemmArgs {
   // row * (wperm_C * wperm_T) + c * wperm_T + tap -- torch's [Cout][Cin][KH][KW] -- and dropped for padded
   // channels (c >= wperm_C); always through the fp32 slab + reduce kernel.
   int wperm_C, wperm_Cpad, wperm_T;
+  // single = 1: one LDS operand buffer (2 barriers per K-tile) so short-K GEMMs run with half the LDS and
+  // twice the workgroups per CU (set by the launcher when a split has <= 4 K-tiles)
+  int single;
 };
 
 __device__ __forceinline__ float amax_scale(const unsigned* a) {
@@ -235,10 +238,12 @@ template <int BN_>
 struct GemmTile {
   static constexpr int B_BYTES = BN_ * GBK_BYTES;              // B tile per buffer
   static constexpr int BUF = G_TILE_BYTES + B_BYTES;           // A + B per buffer
-  static constexpr int LDS = 2 * BUF;                          // double buffered (>= the fp32 epilogue tile)
+  static constexpr int LDS = 2 * BUF;                          // double buffered
+  static constexpr int EPI = GBM / 2 * BN_ * 4;                // fp32 epilogue staging: one 64-row half
+  static constexpr int LDS_SINGLE = BUF > EPI ? BUF : EPI;     // single-buffer launch
   static constexpr int NF = BN_ / 32;                          // 16-wide MFMA column fragments per wave
   static constexpr int WCW = BN_ / 2;                          // columns per wave (2 x 2 waves)
-  static_assert(LDS >= GBM * BN_ * 4, "epilogue tile must fit in the K-loop LDS");
+  static_assert(LDS >= EPI, "epilogue half tile must fit in the K-loop LDS");
 };
 
 // BN_ = 128: the general tile.  BN_ = 64: narrow-N GEMMs (e.g. 64-channel convolutions) -- half the B tile, no
@@ -307,8 +312,9 @@ __global__ void __launch_bounds__(GT) k_gemm(GemmArgs g) {
     store(sa1, sb1, 0);
   }
   __syncthreads();
+  const bool single = g.single != 0;
   for (int kt = 0; kt < nk; ++kt) {
-    const int buf = kt & 1;
+    const int buf = single ? 0 : (kt & 1);
     if (kt + 1 < nk) load(sa1, sb1, kt + 1);  // global loads in flight during the MFMAs below
     const char* la = smem + buf * T::BUF;
     const char* lb = la + G_TILE_BYTES;
@@ -348,7 +354,10 @@ __global__ void __launch_bounds__(GT) k_gemm(GemmArgs g) {
         for (int n = 0; n < T::NF; ++n)  // fp8 e4m3 x fp8 e4m3, unit E8M0 scales (127)
           acc[m][n] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(af[m], bfr[n], acc[m][n], 0, 0, 0, 127, 0, 127);
     }
-    if (kt + 1 < nk) store(sa1, sb1, buf ^ 1);
+    if (kt + 1 < nk) {
+      if (single) __syncthreads();  // every wave is done reading the buffer it is about to overwrite
+      store(sa1, sb1, single ? 0 : buf ^ 1);
+    }
     __syncthreads();
   }
 
@@ -370,80 +379,91 @@ __global__ void __launch_bounds__(GT) k_gemm(GemmArgs g) {
       }
     return;
   }
+  // Two 64-row halves (32 KiB of fp32 staging for a 128-column tile): the waves owning rows half*64.. stage
+  // their fragments, then all 256 threads write 8 columns (one 16-B bf16 / two 16-B fp32 stores) per row.
   float* ct = (float*)smem;
   auto cidx = [](int r, int c) { return r * BN_ + (c ^ (((r >> 2) & 3) << 4)); };
-#pragma unroll
-  for (int m = 0; m < 4; ++m)
-#pragma unroll
-    for (int n = 0; n < T::NF; ++n)
-#pragma unroll
-      for (int j = 0; j < 4; ++j)
-        ct[cidx(wr * 64 + m * 16 + (lane >> 4) * 4 + j, wc * T::WCW + n * 16 + (lane & 15))] = acc[m][n][j];
-  __syncthreads();
   const float alpha = gemm_alpha(g);
-  // thread t: column group cg = t % CG (4 columns each), rows t / CG + RL * r
-  constexpr int CG = BN_ / 4, RL = GT / CG;
-  const int cg = threadIdx.x % CG, col0 = n0 + cg * 4;
-  float bias4[4], shift4[4], s1[4] = {0.f, 0.f, 0.f, 0.f}, s2[4] = {0.f, 0.f, 0.f, 0.f};
+  constexpr int CG = BN_ / 8, RL = GT / CG;  // column groups of 8, row lanes
+  const int cg = threadIdx.x % CG, col0 = n0 + cg * 8;
+  float bias8[8], shift8[8], s1[8], s2[8];
 #pragma unroll
-  for (int e = 0; e < 4; ++e) {
+  for (int e = 0; e < 8; ++e) {
     const int col = min(col0 + e, g.N - 1);
-    bias4[e] = g.bias ? g.bias[col] : 0.f;
-    shift4[e] = g.col_stats ? g.stats_shift[col] : 0.f;
+    bias8[e] = g.bias ? g.bias[col] : 0.f;
+    shift8[e] = g.col_stats ? g.stats_shift[col] : 0.f;
+    s1[e] = s2[e] = 0.f;
   }
-  const bool full4 = col0 + 4 <= g.N && (g.ldc & 3) == 0;
-  for (int r = 0; r < GBM / RL; ++r) {
-    const int lr = threadIdx.x / CG + RL * r, row = m0 + lr;
-    if (row >= g.M || col0 >= g.N) continue;
-    const f32x4 a = *(const f32x4*)(ct + cidx(lr, cg * 4));
-    float v[4];
-    const size_t o = (size_t)row * g.ldc + col0;
+  const bool full8 = col0 + 8 <= g.N && (g.ldc & 7) == 0;
+#pragma unroll 1
+  for (int half = 0; half < 2; ++half) {
+    if (wr == half) {
 #pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      float x = a[e] * alpha + bias4[e];
-      if (g.beta != 0.f && col0 + e < g.N)
-        x += g.beta * (g.out_bf16 ? bf2f(((const unsigned short*)g.C)[o + e]) : ((const float*)g.C)[o + e]);
-      if (g.relu) x = x > 0.f ? x : 0.f;
-      v[e] = x;
+      for (int m = 0; m < 4; ++m)
+#pragma unroll
+        for (int n = 0; n < T::NF; ++n)
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+            ct[cidx(m * 16 + (lane >> 4) * 4 + j, wc * T::WCW + n * 16 + (lane & 15))] = acc[m][n][j];
     }
-    if (g.out_bf16) {
-      unsigned short h[4];
-#pragma unroll
-      for (int e = 0; e < 4; ++e) h[e] = f2bf_rne(v[e]);
-      if (g.col_stats) {
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {  // statistics of the values as stored (bf16)
-          const float d = bf2f(h[e]) - shift4[e];
-          s1[e] += d;
-          s2[e] += d * d;
-        }
-      }
-      if (full4) {
-        *(uint2*)((unsigned short*)g.C + o) = uint2{h[0] | ((unsigned)h[1] << 16), h[2] | ((unsigned)h[3] << 16)};
-      } else {
-        for (int e = 0; e < 4 && col0 + e < g.N; ++e) ((unsigned short*)g.C)[o + e] = h[e];
-      }
-    } else {
-      if (g.col_stats) {
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const float d = v[e] - shift4[e];
-          s1[e] += d;
-          s2[e] += d * d;
-        }
-      }
-      if (full4) {
-        *(f32x4*)((float*)g.C + o) = f32x4{v[0], v[1], v[2], v[3]};
-      } else {
-        for (int e = 0; e < 4 && col0 + e < g.N; ++e) ((float*)g.C)[o + e] = v[e];
-      }
-    }
-  }
-  if (g.col_stats) {  // combine the 8 row-lanes of each column group (fixed order), one float2 per column
     __syncthreads();
+    for (int r = 0; r < GBM / 2 / RL; ++r) {
+      const int lr = threadIdx.x / CG + RL * r, row = m0 + half * 64 + lr;
+      if (row >= g.M || col0 >= g.N) continue;
+      const f32x4 a0 = *(const f32x4*)(ct + cidx(lr, cg * 8)), a1 = *(const f32x4*)(ct + cidx(lr, cg * 8 + 4));
+      const float av[8] = {a0[0], a0[1], a0[2], a0[3], a1[0], a1[1], a1[2], a1[3]};
+      float v[8];
+      const size_t o = (size_t)row * g.ldc + col0;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        float x = av[e] * alpha + bias8[e];
+        if (g.beta != 0.f && col0 + e < g.N)
+          x += g.beta * (g.out_bf16 ? bf2f(((const unsigned short*)g.C)[o + e]) : ((const float*)g.C)[o + e]);
+        if (g.relu) x = x > 0.f ? x : 0.f;
+        v[e] = x;
+      }
+      if (g.out_bf16) {
+        unsigned short h[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) h[e] = f2bf_rne(v[e]);
+        if (g.col_stats) {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {  // statistics of the values as stored (bf16)
+            const float d = bf2f(h[e]) - shift8[e];
+            s1[e] += d;
+            s2[e] += d * d;
+          }
+        }
+        if (full8) {
+          *(uint4*)((unsigned short*)g.C + o) =
+              uint4{h[0] | ((unsigned)h[1] << 16), h[2] | ((unsigned)h[3] << 16), h[4] | ((unsigned)h[5] << 16),
+                    h[6] | ((unsigned)h[7] << 16)};
+        } else {
+          for (int e = 0; e < 8 && col0 + e < g.N; ++e) ((unsigned short*)g.C)[o + e] = h[e];
+        }
+      } else {
+        if (g.col_stats) {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            const float d = v[e] - shift8[e];
+            s1[e] += d;
+            s2[e] += d * d;
+          }
+        }
+        if (full8) {
+          *(f32x4*)((float*)g.C + o) = f32x4{v[0], v[1], v[2], v[3]};
+          *(f32x4*)((float*)g.C + o + 4) = f32x4{v[4], v[5], v[6], v[7]};
+        } else {
+          for (int e = 0; e < 8 && col0 + e < g.N; ++e) ((float*)g.C)[o + e] = v[e];
+        }
+      }
+    }
+    __syncthreads();
+  }
+  if (g.col_stats) {  // combine the row lanes of each column group (fixed order), one float2 per column
     float2* red = (float2*)smem;  // [RL row lanes][BN_ cols]
 #pragma unroll
-    for (int e = 0; e < 4; ++e) red[(threadIdx.x / CG) * BN_ + cg * 4 + e] = float2{s1[e], s2[e]};
+    for (int e = 0; e < 8; ++e) red[(threadIdx.x / CG) * BN_ + cg * 8 + e] = float2{s1[e], s2[e]};
     __syncthreads();
     if (threadIdx.x < BN_) {
       const int col = n0 + threadIdx.x;

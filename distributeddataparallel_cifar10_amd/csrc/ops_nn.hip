@@ -31,6 +31,18 @@ struct ConvGeom {
   int K, Kp;             // K = KH*KW*C, Kp = padded column count (multiple of 8)
 };
 
+__device__ __forceinline__ void unpack8(uint4 u, float* f) {
+  const unsigned w[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+  for (int j = 0; j < 8; ++j) f[j] = __uint_as_float((w[j >> 1] >> ((j & 1) * 16)) << 16);
+}
+__device__ __forceinline__ uint4 pack8(const float* f) {
+  unsigned w[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) w[j] = (unsigned)f2bf_rne(f[2 * j]) | ((unsigned)f2bf_rne(f[2 * j + 1]) << 16);
+  return uint4{w[0], w[1], w[2], w[3]};
+}
+
 __global__ void __launch_bounds__(256) k_im2col(const bf16_t* __restrict__ x, bf16_t* __restrict__ cols, ConvGeom g) {
   const int groups = g.Kp >> 3;  // 8 columns per thread
   const long total = (long)g.N * g.Ho * g.Wo * groups;
@@ -62,13 +74,16 @@ __global__ void __launch_bounds__(256) k_im2col(const bf16_t* __restrict__ x, bf
 }
 
 // dX[n,h,w,c] = sum over the (kh, kw) taps whose output pixel read (h, w): gather form, no atomics.
+// C % 8 == 0: one thread per pixel and 8 channels (16-B loads / stores, fp32 sums); else one per element.
 __global__ void __launch_bounds__(256) k_col2im(const bf16_t* __restrict__ dcols, bf16_t* __restrict__ dx, ConvGeom g) {
-  const long total = (long)g.N * g.H * g.W * g.C;
+  const int vec = (g.C & 7) == 0 ? 8 : 1;
+  const int cgs = g.C / vec;
+  const long total = (long)g.N * g.H * g.W * cgs;
   for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < total; i += (long)gridDim.x * 256) {
-    const int c = (int)(i % g.C);
-    const long pix = i / g.C;
+    const int c = (int)(i % cgs) * vec;
+    const long pix = i / cgs;
     const int w = (int)(pix % g.W), h = (int)((pix / g.W) % g.H), n = (int)(pix / ((long)g.W * g.H));
-    float s = 0.f;
+    float s[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
     for (int kh = 0; kh < g.KH; ++kh) {
       const int th = h + g.pad - kh;
       if (th < 0 || th % g.stride) continue;
@@ -79,10 +94,20 @@ __global__ void __launch_bounds__(256) k_col2im(const bf16_t* __restrict__ dcols
         if (tw < 0 || tw % g.stride) continue;
         const int ow = tw / g.stride;
         if (ow >= g.Wo) continue;
-        s += ld_bf(dcols + (((long)n * g.Ho + oh) * g.Wo + ow) * g.Kp + (kh * g.KW + kw) * g.C + c);
+        const long o = (((long)n * g.Ho + oh) * g.Wo + ow) * g.Kp + (kh * g.KW + kw) * g.C + c;
+        if (vec == 8) {
+          float d[8];
+          unpack8(*(const uint4*)(dcols + o), d);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) s[j] += d[j];
+        } else {
+          s[0] += ld_bf(dcols + o);
+        }
       }
     }
-    dx[i] = f2bf_rne(s);
+    const long xo = pix * g.C + c;
+    if (vec == 8) *(uint4*)(dx + xo) = pack8(s);
+    else dx[xo] = f2bf_rne(s[0]);
   }
 }
 
@@ -176,17 +201,6 @@ __global__ void __launch_bounds__(256) k_bn_finalize(const float2* __restrict__ 
   }
 }
 
-__device__ __forceinline__ void unpack8(uint4 u, float* f) {
-  const unsigned w[4] = {u.x, u.y, u.z, u.w};
-#pragma unroll
-  for (int j = 0; j < 8; ++j) f[j] = __uint_as_float((w[j >> 1] >> ((j & 1) * 16)) << 16);
-}
-__device__ __forceinline__ uint4 pack8(const float* f) {
-  unsigned w[4];
-#pragma unroll
-  for (int j = 0; j < 4; ++j) w[j] = (unsigned)f2bf_rne(f[2 * j]) | ((unsigned)f2bf_rne(f[2 * j + 1]) << 16);
-  return uint4{w[0], w[1], w[2], w[3]};
-}
 
 // out = fused(x); vectorised by 8 channels (C % 8 == 0)
 // Optionally also emits an fp8 e4m3 copy of the output for an fp8 consumer GEMM, with DELAYED scaling: the scale
@@ -381,30 +395,51 @@ struct PoolGeom {
   int N, H, W, C, K, S, P, Ho, Wo;
 };
 
+// C % 8 == 0: one thread per output pixel and 8 channels (16-B loads, 8-B argmax stores); else per element
 __global__ void __launch_bounds__(256) k_maxpool_fwd(const bf16_t* __restrict__ x, bf16_t* __restrict__ y,
                                                      uint8_t* __restrict__ arg, PoolGeom g) {
-  const long total = (long)g.N * g.Ho * g.Wo * g.C;
+  const int vec = (g.C & 7) == 0 ? 8 : 1;
+  const int cgs = g.C / vec;
+  const long total = (long)g.N * g.Ho * g.Wo * cgs;
   for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < total; i += (long)gridDim.x * 256) {
-    const int c = (int)(i % g.C);
-    const long p = i / g.C;
+    const int c = (int)(i % cgs) * vec;
+    const long p = i / cgs;
     const int ow = (int)(p % g.Wo), oh = (int)((p / g.Wo) % g.Ho), n = (int)(p / ((long)g.Wo * g.Ho));
-    float best = -INFINITY;
-    int bi = 0;
+    float best[8];
+    int bi[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      best[j] = -INFINITY;
+      bi[j] = 0;
+    }
     for (int kh = 0; kh < g.K; ++kh) {
       const int h = oh * g.S - g.P + kh;
       if (h < 0 || h >= g.H) continue;
       for (int kw = 0; kw < g.K; ++kw) {
         const int w = ow * g.S - g.P + kw;
         if (w < 0 || w >= g.W) continue;
-        const float v = ld_bf(x + (((long)n * g.H + h) * g.W + w) * g.C + c);
-        if (v > best || (v != v && best == best)) {  // first max wins; NaN propagates like torch
-          best = v;
-          bi = kh * g.K + kw;
+        const long xo = (((long)n * g.H + h) * g.W + w) * g.C + c;
+        float v[8];
+        if (vec == 8) unpack8(*(const uint4*)(x + xo), v);
+        else v[0] = ld_bf(x + xo);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          if (j < vec && (v[j] > best[j] || (v[j] != v[j] && best[j] == best[j]))) {  // first max wins; NaN propagates
+            best[j] = v[j];
+            bi[j] = kh * g.K + kw;
+          }
         }
       }
     }
-    y[i] = f2bf_rne(best);
-    arg[i] = (uint8_t)bi;
+    const long o = p * g.C + c;
+    if (vec == 8) {
+      *(uint4*)(y + o) = pack8(best);
+      *(uint2*)(arg + o) = uint2{(unsigned)bi[0] | ((unsigned)bi[1] << 8) | ((unsigned)bi[2] << 16) | ((unsigned)bi[3] << 24),
+                                 (unsigned)bi[4] | ((unsigned)bi[5] << 8) | ((unsigned)bi[6] << 16) | ((unsigned)bi[7] << 24)};
+    } else {
+      y[o] = f2bf_rne(best[0]);
+      arg[o] = (uint8_t)bi[0];
+    }
   }
 }
 

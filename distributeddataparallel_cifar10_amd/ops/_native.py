@@ -30,7 +30,7 @@ class GemmArgs(ctypes.Structure):
         ("conv", c_int), ("cN", c_int), ("cH", c_int), ("cW", c_int), ("cC", c_int), ("cKH", c_int), ("cKW", c_int),
         ("cS", c_int), ("cP", c_int), ("cHo", c_int), ("cWo", c_int), ("col_stats", c_void_p),
         ("stats_shift", c_void_p), ("amax_a", c_void_p), ("amax_b", c_void_p),
-        ("wperm_C", c_int), ("wperm_Cpad", c_int), ("wperm_T", c_int),
+        ("wperm_C", c_int), ("wperm_Cpad", c_int), ("wperm_T", c_int), ("single", c_int),
     ]
 
 

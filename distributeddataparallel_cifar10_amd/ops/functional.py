@@ -207,7 +207,7 @@ class WeightPack:
     Cin_pad = 8 for a stem with fewer than 8 channels (its input is zero-padded to 8 channels, so the stem runs
     as an implicit GEMM instead of through an im2col buffer)."""
 
-    BLOCKS_PER_LAYER = 32
+    BLOCKS_PER_LAYER = 256
 
     def __init__(self, convs, fp8_convs=()):
         self.convs = list(convs)

@@ -74,7 +74,7 @@ def test_quantize_fp8_and_scaled_gemm(gpu):
 
 @pytest.mark.parametrize("n,h,c,co,k,s,p,bias", [(2, 16, 32, 32, 3, 1, 1, False), (3, 32, 3, 32, 3, 1, 1, True),
                                                   (2, 14, 16, 24, 7, 2, 3, False), (2, 9, 64, 48, 1, 2, 0, False),
-                                                  (4, 8, 64, 128, 1, 1, 0, False)])
+                                                  (4, 8, 64, 128, 1, 1, 0, False), (2, 10, 3, 16, 3, 2, 1, False)])
 def test_conv2d_fwd_bwd(gpu, n, h, c, co, k, s, p, bias):
     from distributeddataparallel_cifar10_amd.ops import conv2d
     g = torch.Generator(device=gpu).manual_seed(n * h + c)
@@ -134,10 +134,11 @@ def test_batch_norm_act(gpu, res_mode, relu):
 
 
 @pytest.mark.parametrize("k,s,p,h", [(2, 2, 0, 16), (3, 2, 1, 15), (2, 2, 0, 7)])
-def test_max_pool(gpu, k, s, p, h):
+@pytest.mark.parametrize("c", [24, 5])
+def test_max_pool(gpu, k, s, p, h, c):
     from distributeddataparallel_cifar10_amd.ops import max_pool2d
     g = torch.Generator(device=gpu).manual_seed(k + h)
-    x = _bf(torch.randn(2, h, h, 24, device=gpu, generator=g)).requires_grad_()
+    x = _bf(torch.randn(2, h, h, c, device=gpu, generator=g)).requires_grad_()
     y = max_pool2d(x, k, s, p)
     dy = _bf(torch.randn(y.shape, device=gpu, generator=g))
     y.backward(dy)
