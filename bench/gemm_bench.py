@@ -37,7 +37,8 @@ def main():
                      "gbps": round(bytes_ / us / 1e3, 1)})
         print(json.dumps(rows[-1]), flush=True)
 
-    for M, Nn, K in [(4096, 4096, 4096), (200704, 64, 64), (200704, 256, 64), (50176, 128, 512),
+    for M, Nn, K in [(4096, 4096, 4096), (200704, 64, 64), (200704, 256, 64), (50176, 128, 512), (200704, 128, 512),
+                     (802816, 256, 64), (200704, 512, 128), (50176, 256, 1024),
                      (12544, 1024, 256), (3136, 2048, 512)]:
         a = torch.randn(M, K, device=dev).to(bf)
         b = torch.randn(Nn, K, device=dev).to(bf)

@@ -7,6 +7,7 @@
 #include <cstring>
 #include <string>
 #include <cstdlib>
+#include <cstdint>
 
 #include "ops_nn.hip"
 #include "ops_wgrad.hip"
@@ -35,6 +36,14 @@ inline int grid_for(long work, int per_block = 256, int cap = 8192) {
 }
 bool g_lds_set = false;
 // DCA_OPS_WGRAD=0 routes weight gradients through the general k_gemm (A/B comparisons)
+inline bool getenv_flag(const char* name) {
+  const char* e = getenv(name);
+  return !(e && e[0] == '0');
+}
+inline bool getenv_glds_ok() {
+  static const bool v = getenv_flag("DCA_OPS_GLDS");
+  return v;
+}
 inline bool getenv_wgrad_ok() {
   static const int v = [] {
     const char* e = getenv("DCA_OPS_WGRAD");
@@ -90,6 +99,14 @@ int dca_ops_gemm(const GemmArgs* a, void* stream) {
       OPCK(hipFuncSetAttribute((const void*)k_wgrad<64, 128, 1>, hipFuncAttributeMaxDynamicSharedMemorySize, l01));
       OPCK(hipFuncSetAttribute((const void*)k_wgrad<128, 64, 4>, hipFuncAttributeMaxDynamicSharedMemorySize, l10));
       OPCK(hipFuncSetAttribute((const void*)k_wgrad<128, 128, 2>, hipFuncAttributeMaxDynamicSharedMemorySize, l11));
+      OPCK(hipFuncSetAttribute((const void*)k_gemm_glds<false, 128>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                               GemmTile<128>::LDS));
+      OPCK(hipFuncSetAttribute((const void*)k_gemm_glds<true, 128>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                               GemmTile<128>::LDS));
+      OPCK(hipFuncSetAttribute((const void*)k_gemm_glds<false, 64>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                               GemmTile<64>::LDS));
+      OPCK(hipFuncSetAttribute((const void*)k_gemm_glds<true, 64>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                               GemmTile<64>::LDS));
     }
     g_lds_set = true;
   }
@@ -131,7 +148,22 @@ int dca_ops_gemm(const GemmArgs* a, void* stream) {
   const int tiles = ((g.M + GBM - 1) / GBM) * ((g.N + bn - 1) / bn);
   const dim3 grid(tiles, g.splits);
   g.single = g.k_per_split <= 4 * kt ? 1 : 0;  // short K: one operand buffer, twice the workgroups per CU
-  if (narrow) {
+  // K-contiguous operands with 16-B aligned rows: direct global -> LDS staging (k_gemm_glds)
+  const int esz = g.fp8 ? 1 : 2;
+  // (measured, bench/gemm_bench.py: +18..100 % on plain NT GEMMs; the implicit-conv gather and short-K narrow
+  // tiles stay on the register-staged kernel, whose per-thread tap decode and single-buffer mode win there)
+  const bool glds = getenv_glds_ok() && !g.ta && !g.tb && g.conv == 0 && !(narrow && g.single) &&
+                    (long)g.lda * esz % 16 == 0 && (long)g.K * esz % 16 == 0 &&
+                    (long)g.ldb * esz % 16 == 0 && ((uintptr_t)g.A & 15) == 0 && ((uintptr_t)g.B & 15) == 0;
+  if (glds) {
+    if (narrow) {
+      if (g.fp8) hipLaunchKernelGGL((k_gemm_glds<true, 64>), grid, dim3(GT), GemmTile<64>::LDS, st, g);
+      else hipLaunchKernelGGL((k_gemm_glds<false, 64>), grid, dim3(GT), GemmTile<64>::LDS, st, g);
+    } else {
+      if (g.fp8) hipLaunchKernelGGL((k_gemm_glds<true, 128>), grid, dim3(GT), GemmTile<128>::LDS, st, g);
+      else hipLaunchKernelGGL((k_gemm_glds<false, 128>), grid, dim3(GT), GemmTile<128>::LDS, st, g);
+    }
+  } else if (narrow) {
     const int lds = g.single ? GemmTile<64>::LDS_SINGLE : GemmTile<64>::LDS;
     if (g.fp8) hipLaunchKernelGGL((k_gemm<true, 64>), grid, dim3(GT), lds, st, g);
     else hipLaunchKernelGGL((k_gemm<false, 64>), grid, dim3(GT), lds, st, g);

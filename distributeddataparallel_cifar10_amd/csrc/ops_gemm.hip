@@ -250,117 +250,12 @@ struct GemmTile {
 // wasted MFMA columns, 48 KiB LDS (3 workgroups per CU); its B operand must be K-contiguous (no tb / conv 2).
 // K loop: register prefetch of tile k+1 during the MFMAs of tile k, written to the other LDS buffer after them.
 // (A two-tile-deep prefetch measured neutral to 20 % slower: 196 VGPRs = 1 wave per SIMD, bench/gemm_bench.py.)
-template <bool FP8, int BN_>
-__global__ void __launch_bounds__(GT) k_gemm(GemmArgs g) {
+// Shared epilogue of the GEMM kernels (acc = this wave's 64 x BN_/2 fp32 fragments of the 128 x BN_ tile).
+template <int BN_>
+__device__ __forceinline__ void gemm_epilogue(const GemmArgs& g, f32x4 (&acc)[4][BN_ / 32], char* smem, int m0,
+                                              int n0, int tm, int ksplit) {
   using T = GemmTile<BN_>;
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int ntm = (g.M + GBM - 1) / GBM, ntn = (g.N + BN_ - 1) / BN_;
-  const int tile = xcd_remap(blockIdx.x, ntm * ntn);
-  const int tm = tile / ntn, tn = tile % ntn;
-  const int m0 = tm * GBM, n0 = tn * BN_;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, wr = wave >> 1, wc = wave & 1;
-  constexpr int ESZ = FP8 ? 1 : 2;
-  const int ksplit = blockIdx.y;
-  const int k_begin = ksplit * g.k_per_split;
-  const int k_end = min(g.K, k_begin + g.k_per_split);
-  constexpr int KT = GBK_BYTES / ESZ;  // elements per K-tile
-  const int nk = (k_end - k_begin + KT - 1) / KT;
-
-  f32x4 acc[4][T::NF];
-#pragma unroll
-  for (int m = 0; m < 4; ++m)
-#pragma unroll
-    for (int n = 0; n < T::NF; ++n) acc[m][n] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  ConvRows cr;
-  ConvCols cc;
-  if (g.conv == 1) conv_rows(cr, g, m0);
-  if constexpr (BN_ == 128) {
-    if (g.conv == 2) conv_cols(cc, g, n0);
-  }
-  using SB = StageT<BN_ / 32>;
-  auto load = [&](Stage& sa, SB& sb, int kt) {
-    const int k0 = k_begin + kt * KT;
-    if (g.conv == 1) load_conv_a(sa, (const unsigned short*)g.A, cr, g, k0, k_end);
-    else if (g.ta) load_t(sa, (const unsigned short*)g.A, m0, g.M, g.lda, k0, k_end);
-    else load_nt<ESZ>(sa, (const char*)g.A, m0, g.M, (size_t)g.lda * ESZ, k0 * ESZ, k_end * ESZ);
-    if constexpr (BN_ == 128) {
-      if (g.conv == 2) load_conv_b(sb, (const unsigned short*)g.B, cc, g, k0, k_end);
-      else if (g.tb) load_t(sb, (const unsigned short*)g.B, n0, g.N, g.ldb, k0, k_end);
-      else load_nt<ESZ>(sb, (const char*)g.B, n0, g.N, (size_t)g.ldb * ESZ, k0 * ESZ, k_end * ESZ);
-    } else {
-      load_nt<ESZ, BN_ / 32>(sb, (const char*)g.B, n0, g.N, (size_t)g.ldb * ESZ, k0 * ESZ, k_end * ESZ);
-    }
-  };
-  auto store = [&](const Stage& sa, const SB& sb, int buf) {
-    char* la = smem + buf * T::BUF;
-    char* lb = la + G_TILE_BYTES;
-    if (g.ta && g.conv != 1) store_t(sa, la);
-    else store_nt(sa, la);
-    if constexpr (BN_ == 128) {
-      if (g.tb || g.conv == 2) store_t(sb, lb);
-      else store_nt(sb, lb);
-    } else {
-      store_nt<BN_ / 32>(sb, lb);
-    }
-  };
-
-  Stage sa1;
-  SB sb1;
-  if (nk > 0) {
-    load(sa1, sb1, 0);
-    store(sa1, sb1, 0);
-  }
-  __syncthreads();
-  const bool single = g.single != 0;
-  for (int kt = 0; kt < nk; ++kt) {
-    const int buf = single ? 0 : (kt & 1);
-    if (kt + 1 < nk) load(sa1, sb1, kt + 1);  // global loads in flight during the MFMAs below
-    const char* la = smem + buf * T::BUF;
-    const char* lb = la + G_TILE_BYTES;
-    if constexpr (!FP8) {
-#pragma unroll
-      for (int s = 0; s < 2; ++s) {
-        s16x8 af[4], bfr[T::NF];
-#pragma unroll
-        for (int m = 0; m < 4; ++m)
-          af[m] = *(const s16x8*)(la + lds_off(wr * 64 + m * 16 + (lane & 15), s * 4 + (lane >> 4)));
-#pragma unroll
-        for (int n = 0; n < T::NF; ++n)
-          bfr[n] = *(const s16x8*)(lb + lds_off(wc * T::WCW + n * 16 + (lane & 15), s * 4 + (lane >> 4)));
-#pragma unroll
-        for (int m = 0; m < 4; ++m)
-#pragma unroll
-          for (int n = 0; n < T::NF; ++n)
-            acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[m], bfr[n], acc[m][n], 0, 0, 0);
-      }
-    } else {
-      i32x8 af[4], bfr[T::NF];
-#pragma unroll
-      for (int m = 0; m < 4; ++m) {
-        const int row = wr * 64 + m * 16 + (lane & 15), c = 2 * (lane >> 4);
-        const uint4 lo = *(const uint4*)(la + lds_off(row, c)), hi = *(const uint4*)(la + lds_off(row, c + 1));
-        af[m] = i32x8{(int)lo.x, (int)lo.y, (int)lo.z, (int)lo.w, (int)hi.x, (int)hi.y, (int)hi.z, (int)hi.w};
-      }
-#pragma unroll
-      for (int n = 0; n < T::NF; ++n) {
-        const int row = wc * T::WCW + n * 16 + (lane & 15), c = 2 * (lane >> 4);
-        const uint4 lo = *(const uint4*)(lb + lds_off(row, c)), hi = *(const uint4*)(lb + lds_off(row, c + 1));
-        bfr[n] = i32x8{(int)lo.x, (int)lo.y, (int)lo.z, (int)lo.w, (int)hi.x, (int)hi.y, (int)hi.z, (int)hi.w};
-      }
-#pragma unroll
-      for (int m = 0; m < 4; ++m)
-#pragma unroll
-        for (int n = 0; n < T::NF; ++n)  // fp8 e4m3 x fp8 e4m3, unit E8M0 scales (127)
-          acc[m][n] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(af[m], bfr[n], acc[m][n], 0, 0, 0, 127, 0, 127);
-    }
-    if (kt + 1 < nk) {
-      if (single) __syncthreads();  // every wave is done reading the buffer it is about to overwrite
-      store(sa1, sb1, single ? 0 : buf ^ 1);
-    }
-    __syncthreads();
-  }
-
   // Epilogue.  Split-K partials go straight to the fp32 slab.  Otherwise the 128x128 fp32 tile is staged in
   // LDS (the K-loop buffers are free: 64 KiB exactly; 16-column groups XOR-swizzled by (row >> 2) & 3 so the
   // fragment writes of one instruction hit distinct banks), then written back row-contiguously, 16 B per lane,
@@ -475,6 +370,274 @@ __global__ void __launch_bounds__(GT) k_gemm(GemmArgs g) {
       if (col < g.N) g.col_stats[(size_t)tm * g.N + col] = t;
     }
   }
+}
+
+template <bool FP8, int BN_>
+__global__ void __launch_bounds__(GT) k_gemm(GemmArgs g) {
+  using T = GemmTile<BN_>;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int ntm = (g.M + GBM - 1) / GBM, ntn = (g.N + BN_ - 1) / BN_;
+  const int tile = xcd_remap(blockIdx.x, ntm * ntn);
+  const int tm = tile / ntn, tn = tile % ntn;
+  const int m0 = tm * GBM, n0 = tn * BN_;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, wr = wave >> 1, wc = wave & 1;
+  constexpr int ESZ = FP8 ? 1 : 2;
+  const int ksplit = blockIdx.y;
+  const int k_begin = ksplit * g.k_per_split;
+  const int k_end = min(g.K, k_begin + g.k_per_split);
+  constexpr int KT = GBK_BYTES / ESZ;  // elements per K-tile
+  const int nk = (k_end - k_begin + KT - 1) / KT;
+
+  f32x4 acc[4][T::NF];
+#pragma unroll
+  for (int m = 0; m < 4; ++m)
+#pragma unroll
+    for (int n = 0; n < T::NF; ++n) acc[m][n] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  ConvRows cr;
+  ConvCols cc;
+  if (g.conv == 1) conv_rows(cr, g, m0);
+  if constexpr (BN_ == 128) {
+    if (g.conv == 2) conv_cols(cc, g, n0);
+  }
+  using SB = StageT<BN_ / 32>;
+  auto load = [&](Stage& sa, SB& sb, int kt) {
+    const int k0 = k_begin + kt * KT;
+    if (g.conv == 1) load_conv_a(sa, (const unsigned short*)g.A, cr, g, k0, k_end);
+    else if (g.ta) load_t(sa, (const unsigned short*)g.A, m0, g.M, g.lda, k0, k_end);
+    else load_nt<ESZ>(sa, (const char*)g.A, m0, g.M, (size_t)g.lda * ESZ, k0 * ESZ, k_end * ESZ);
+    if constexpr (BN_ == 128) {
+      if (g.conv == 2) load_conv_b(sb, (const unsigned short*)g.B, cc, g, k0, k_end);
+      else if (g.tb) load_t(sb, (const unsigned short*)g.B, n0, g.N, g.ldb, k0, k_end);
+      else load_nt<ESZ>(sb, (const char*)g.B, n0, g.N, (size_t)g.ldb * ESZ, k0 * ESZ, k_end * ESZ);
+    } else {
+      load_nt<ESZ, BN_ / 32>(sb, (const char*)g.B, n0, g.N, (size_t)g.ldb * ESZ, k0 * ESZ, k_end * ESZ);
+    }
+  };
+  auto store = [&](const Stage& sa, const SB& sb, int buf) {
+    char* la = smem + buf * T::BUF;
+    char* lb = la + G_TILE_BYTES;
+    if (g.ta && g.conv != 1) store_t(sa, la);
+    else store_nt(sa, la);
+    if constexpr (BN_ == 128) {
+      if (g.tb || g.conv == 2) store_t(sb, lb);
+      else store_nt(sb, lb);
+    } else {
+      store_nt<BN_ / 32>(sb, lb);
+    }
+  };
+
+  Stage sa1;
+  SB sb1;
+  if (nk > 0) {
+    load(sa1, sb1, 0);
+    store(sa1, sb1, 0);
+  }
+  __syncthreads();
+  const bool single = g.single != 0;
+  for (int kt = 0; kt < nk; ++kt) {
+    const int buf = single ? 0 : (kt & 1);
+    if (kt + 1 < nk) load(sa1, sb1, kt + 1);  // global loads in flight during the MFMAs below
+    const char* la = smem + buf * T::BUF;
+    const char* lb = la + G_TILE_BYTES;
+    if constexpr (!FP8) {
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        s16x8 af[4], bfr[T::NF];
+#pragma unroll
+        for (int m = 0; m < 4; ++m)
+          af[m] = *(const s16x8*)(la + lds_off(wr * 64 + m * 16 + (lane & 15), s * 4 + (lane >> 4)));
+#pragma unroll
+        for (int n = 0; n < T::NF; ++n)
+          bfr[n] = *(const s16x8*)(lb + lds_off(wc * T::WCW + n * 16 + (lane & 15), s * 4 + (lane >> 4)));
+#pragma unroll
+        for (int m = 0; m < 4; ++m)
+#pragma unroll
+          for (int n = 0; n < T::NF; ++n)
+            acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[m], bfr[n], acc[m][n], 0, 0, 0);
+      }
+    } else {
+      i32x8 af[4], bfr[T::NF];
+#pragma unroll
+      for (int m = 0; m < 4; ++m) {
+        const int row = wr * 64 + m * 16 + (lane & 15), c = 2 * (lane >> 4);
+        const uint4 lo = *(const uint4*)(la + lds_off(row, c)), hi = *(const uint4*)(la + lds_off(row, c + 1));
+        af[m] = i32x8{(int)lo.x, (int)lo.y, (int)lo.z, (int)lo.w, (int)hi.x, (int)hi.y, (int)hi.z, (int)hi.w};
+      }
+#pragma unroll
+      for (int n = 0; n < T::NF; ++n) {
+        const int row = wc * T::WCW + n * 16 + (lane & 15), c = 2 * (lane >> 4);
+        const uint4 lo = *(const uint4*)(lb + lds_off(row, c)), hi = *(const uint4*)(lb + lds_off(row, c + 1));
+        bfr[n] = i32x8{(int)lo.x, (int)lo.y, (int)lo.z, (int)lo.w, (int)hi.x, (int)hi.y, (int)hi.z, (int)hi.w};
+      }
+#pragma unroll
+      for (int m = 0; m < 4; ++m)
+#pragma unroll
+        for (int n = 0; n < T::NF; ++n)  // fp8 e4m3 x fp8 e4m3, unit E8M0 scales (127)
+          acc[m][n] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(af[m], bfr[n], acc[m][n], 0, 0, 0, 127, 0, 127);
+    }
+    if (kt + 1 < nk) {
+      if (single) __syncthreads();  // every wave is done reading the buffer it is about to overwrite
+      store(sa1, sb1, single ? 0 : buf ^ 1);
+    }
+    __syncthreads();
+  }
+
+  gemm_epilogue<BN_>(g, acc, smem, m0, n0, tm, ksplit);
+}
+
+
+// ---------------------------------------------------------------------------------------------------------
+// k_gemm_glds: the same tile / fragments / epilogue as k_gemm for K-contiguous operands (ta = tb = 0, or the
+// implicit conv gather of A), but staged global -> LDS with global_load_lds_dwordx4 (no VGPR staging, no
+// ds_write pass): tile k+1's loads stay in flight during tile k's MFMAs, retired by a counted vmcnt and a raw
+// s_barrier (a __syncthreads() would drain them: CDNA4 guide, "Pipelining across barriers").
+// The LDS image must be lane-linear per wave instruction (8 rows x 128 B), so the XOR swizzle of lds_off is
+// applied to the SOURCE chunk each lane loads (an involution: the fragment reads use lds_off unchanged).
+// Out-of-range chunks (K tail, conv padding) load from a zeroed global word.
+// ---------------------------------------------------------------------------------------------------------
+__device__ __attribute__((aligned(16))) unsigned char g_gemm_zero16[16];
+
+__device__ __forceinline__ void glds16(const void* src, char* lds_wave_base) {
+  __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
+                                   (__attribute__((address_space(3))) void*)lds_wave_base, 16, 0, 0);
+}
+template <int N>
+__device__ __forceinline__ void wait_vmcnt() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+template <bool FP8, int BN_>
+__global__ void __launch_bounds__(GT) k_gemm_glds(GemmArgs g) {
+  using T = GemmTile<BN_>;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int ntm = (g.M + GBM - 1) / GBM, ntn = (g.N + BN_ - 1) / BN_;
+  const int tile = xcd_remap(blockIdx.x, ntm * ntn);
+  const int tm = tile / ntn, tn = tile % ntn;
+  const int m0 = tm * GBM, n0 = tn * BN_;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, wr = wave >> 1, wc = wave & 1;
+  constexpr int ESZ = FP8 ? 1 : 2;
+  constexpr int KT = GBK_BYTES / ESZ;
+  constexpr int NBI = BN_ / 32;      // B wave instructions (8 rows each) per tile
+  constexpr int NI = 4 + NBI;        // glds per thread per tile
+  const int ksplit = blockIdx.y;
+  const int k_begin = ksplit * g.k_per_split;
+  const int k_end = min(g.K, k_begin + g.k_per_split);
+  const int nk = (k_end - k_begin + KT - 1) / KT;
+  const int lr = lane >> 3, lj = lane & 7;
+
+  // per-lane rows: A row wave*32 + i*8 + lr, B row wave*(BN_/4) + i*8 + lr
+  const char* arow[4];
+  int nh[4], ih[4], iw[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    int m = m0 + wave * 32 + i * 8 + lr;
+    m = m < g.M ? m : g.M - 1;
+    arow[i] = (const char*)g.A + (size_t)m * g.lda * ESZ;
+    if (g.conv == 1) {
+      const int ow = m % g.cWo, t = m / g.cWo, oh = t % g.cHo, n = t / g.cHo;
+      nh[i] = n * g.cH;
+      ih[i] = oh * g.cS - g.cP;
+      iw[i] = ow * g.cS - g.cP;
+    }
+  }
+  const char* brow[NBI];
+#pragma unroll
+  for (int i = 0; i < NBI; ++i) {
+    int n = n0 + wave * (BN_ / 4) + i * 8 + lr;
+    n = n < g.N ? n : g.N - 1;
+    brow[i] = (const char*)g.B + (size_t)n * g.ldb * ESZ;
+  }
+  const int kb_end = k_end * ESZ;
+
+  auto issue = [&](int kt, int buf) {
+    const int kb0 = (k_begin + kt * KT) * ESZ;
+    char* la = smem + buf * T::BUF;
+    char* lb = la + G_TILE_BYTES;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int r = wave * 32 + i * 8 + lr;
+      const int kb = kb0 + ((lj ^ ((r >> 1) & 7)) << 4);
+      const void* src = g_gemm_zero16;
+      if (g.conv == 1) {
+        const int k = kb >> 1, tap = k / g.cC, c = k - tap * g.cC, kh = tap / g.cKW, kw = tap - kh * g.cKW;
+        const int h = ih[i] + kh, w = iw[i] + kw;
+        if (kb < kb_end && h >= 0 && h < g.cH && w >= 0 && w < g.cW)
+          src = (const unsigned short*)g.A + ((size_t)(nh[i] + h) * g.cW + w) * g.cC + c;
+      } else if (kb < kb_end) {
+        src = arow[i] + kb;
+      }
+      glds16(src, la + (wave * 32 + i * 8) * 128);
+    }
+#pragma unroll
+    for (int i = 0; i < NBI; ++i) {
+      const int r = wave * (BN_ / 4) + i * 8 + lr;
+      const int kb = kb0 + ((lj ^ ((r >> 1) & 7)) << 4);
+      glds16(kb < kb_end ? (const void*)(brow[i] + kb) : (const void*)g_gemm_zero16,
+             lb + (wave * (BN_ / 4) + i * 8) * 128);
+    }
+  };
+
+  f32x4 acc[4][T::NF];
+#pragma unroll
+  for (int m = 0; m < 4; ++m)
+#pragma unroll
+    for (int n = 0; n < T::NF; ++n) acc[m][n] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  if (nk > 0) issue(0, 0);
+  for (int kt = 0; kt < nk; ++kt) {
+    const int buf = kt & 1;
+    if (kt + 1 < nk) {
+      issue(kt + 1, buf ^ 1);  // the buffer every wave finished reading before the previous closing barrier
+      wait_vmcnt<NI>();         // this thread's loads of tile kt have landed (tile kt+1's still in flight)
+    } else {
+      wait_vmcnt<0>();
+    }
+    __builtin_amdgcn_s_barrier();  // ... and every thread's
+    asm volatile("" ::: "memory");
+    const char* la = smem + buf * T::BUF;
+    const char* lb = la + G_TILE_BYTES;
+    if constexpr (!FP8) {
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        s16x8 af[4], bfr[T::NF];
+#pragma unroll
+        for (int m = 0; m < 4; ++m)
+          af[m] = *(const s16x8*)(la + lds_off(wr * 64 + m * 16 + (lane & 15), s * 4 + (lane >> 4)));
+#pragma unroll
+        for (int n = 0; n < T::NF; ++n)
+          bfr[n] = *(const s16x8*)(lb + lds_off(wc * T::WCW + n * 16 + (lane & 15), s * 4 + (lane >> 4)));
+#pragma unroll
+        for (int m = 0; m < 4; ++m)
+#pragma unroll
+          for (int n = 0; n < T::NF; ++n)
+            acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[m], bfr[n], acc[m][n], 0, 0, 0);
+      }
+    } else {
+      i32x8 af[4], bfr[T::NF];
+#pragma unroll
+      for (int m = 0; m < 4; ++m) {
+        const int row = wr * 64 + m * 16 + (lane & 15), c = 2 * (lane >> 4);
+        const uint4 lo = *(const uint4*)(la + lds_off(row, c)), hi = *(const uint4*)(la + lds_off(row, c + 1));
+        af[m] = i32x8{(int)lo.x, (int)lo.y, (int)lo.z, (int)lo.w, (int)hi.x, (int)hi.y, (int)hi.z, (int)hi.w};
+      }
+#pragma unroll
+      for (int n = 0; n < T::NF; ++n) {
+        const int row = wc * T::WCW + n * 16 + (lane & 15), c = 2 * (lane >> 4);
+        const uint4 lo = *(const uint4*)(lb + lds_off(row, c)), hi = *(const uint4*)(lb + lds_off(row, c + 1));
+        bfr[n] = i32x8{(int)lo.x, (int)lo.y, (int)lo.z, (int)lo.w, (int)hi.x, (int)hi.y, (int)hi.z, (int)hi.w};
+      }
+#pragma unroll
+      for (int m = 0; m < 4; ++m)
+#pragma unroll
+        for (int n = 0; n < T::NF; ++n)
+          acc[m][n] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(af[m], bfr[n], acc[m][n], 0, 0, 0, 127, 0, 127);
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();  // every wave is done reading buf before it is refilled
+    asm volatile("" ::: "memory");
+  }
+  gemm_epilogue<BN_>(g, acc, smem, m0, n0, tm, ksplit);
 }
 
 // Split-K combine: C = alpha * sum_s ws[s] (+bias) (+beta*C) (ReLU).  256 threads = 64 consecutive elements x 4
