@@ -44,6 +44,14 @@ inline bool getenv_glds_ok() {
   static const bool v = getenv_flag("DCA_OPS_GLDS");
   return v;
 }
+// implicit-conv glds measured neutral vs the register-staged gather (profiles/gemm_bench_*_r1c.log): opt-in
+inline bool getenv_glds_conv() {
+  static const bool v = [] {
+    const char* e = getenv("DCA_OPS_GLDS_CONV");
+    return e && e[0] == '1';
+  }();
+  return v;
+}
 inline bool getenv_wgrad_ok() {
   static const int v = [] {
     const char* e = getenv("DCA_OPS_WGRAD");
@@ -150,10 +158,11 @@ int dca_ops_gemm(const GemmArgs* a, void* stream) {
   g.single = g.k_per_split <= 4 * kt ? 1 : 0;  // short K: one operand buffer, twice the workgroups per CU
   // K-contiguous operands with 16-B aligned rows: direct global -> LDS staging (k_gemm_glds)
   const int esz = g.fp8 ? 1 : 2;
-  // (measured, bench/gemm_bench.py: +18..100 % on plain NT GEMMs; the implicit-conv gather and short-K narrow
-  // tiles stay on the register-staged kernel, whose per-thread tap decode and single-buffer mode win there)
-  const bool glds = getenv_glds_ok() && !g.ta && !g.tb && g.conv == 0 && !(narrow && g.single) &&
-                    (long)g.lda * esz % 16 == 0 && (long)g.K * esz % 16 == 0 &&
+  // (measured, bench/gemm_bench.py: +18..100 % on plain NT GEMMs; implicit convs only when C % 64 == 0 (one
+  // tap per K-tile: a wave-uniform decode); short-K narrow tiles stay on the single-buffer register kernel)
+  const bool glds = getenv_glds_ok() && !g.ta && !g.tb && !(narrow && g.single) &&
+                    (g.conv == 1 ? (g.cC % 64 == 0 && getenv_glds_conv())
+                                 : (g.conv == 0 && (long)g.lda * esz % 16 == 0 && (long)g.K * esz % 16 == 0)) &&
                     (long)g.ldb * esz % 16 == 0 && ((uintptr_t)g.A & 15) == 0 && ((uintptr_t)g.B & 15) == 0;
   if (glds) {
     if (narrow) {

@@ -550,17 +550,35 @@ __global__ void __launch_bounds__(GT) k_gemm_glds(GemmArgs g) {
   }
   const int kb_end = k_end * ESZ;
 
+  const bool c64 = g.conv == 1 && g.cC % KT == 0;
   auto issue = [&](int kt, int buf) {
     const int kb0 = (k_begin + kt * KT) * ESZ;
     char* la = smem + buf * T::BUF;
     char* lb = la + G_TILE_BYTES;
+    int tc0 = 0, tkh = 0, tkw = 0;
+    if (c64) {
+      const int k0 = kb0 / ESZ, tap = k0 / g.cC;
+      tc0 = k0 - tap * g.cC;
+      tkh = tap / g.cKW;
+      tkw = tap - tkh * g.cKW;
+    }
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int r = wave * 32 + i * 8 + lr;
       const int kb = kb0 + ((lj ^ ((r >> 1) & 7)) << 4);
       const void* src = g_gemm_zero16;
       if (g.conv == 1) {
-        const int k = kb >> 1, tap = k / g.cC, c = k - tap * g.cC, kh = tap / g.cKW, kw = tap - kh * g.cKW;
+        int c, kh, kw;
+        if (c64) {  // the whole K-tile is one tap: wave-uniform decode, per-lane channel offset only
+          c = tc0 + ((kb - kb0) >> 1);
+          kh = tkh;
+          kw = tkw;
+        } else {
+          const int k = kb >> 1, tap = k / g.cC;
+          c = k - tap * g.cC;
+          kh = tap / g.cKW;
+          kw = tap - kh * g.cKW;
+        }
         const int h = ih[i] + kh, w = iw[i] + kw;
         if (kb < kb_end && h >= 0 && h < g.cH && w >= 0 && w < g.cW)
           src = (const unsigned short*)g.A + ((size_t)(nh[i] + h) * g.cW + w) * g.cC + c;
