@@ -67,7 +67,7 @@ using namespace dca::ops;
 extern "C" {
 
 const char* dca_ops_last_error() { return g_err.c_str(); }
-int dca_ops_abi_version() { return 4; }
+int dca_ops_abi_version() { return 5; }
 
 // Must match ops/_native.py::GemmArgs.
 int dca_ops_gemm(const GemmArgs* a, void* stream) {
@@ -197,12 +197,12 @@ int dca_ops_im2col(const void* x, void* cols, const ConvGeom* geom, void* stream
   return 0;
 }
 
-int dca_ops_col2im(const void* dcols, void* dx, const ConvGeom* geom, void* stream) {
+int dca_ops_col2im(const void* dcols, void* dx, const ConvGeom* geom, int accumulate, void* stream) {
   const ConvGeom g = *geom;
   REQUIRE(g.Kp % 8 == 0 && g.Kp >= g.K, "col2im: bad column geometry");
   hipLaunchKernelGGL(k_col2im, dim3(grid_for((long)g.N * g.H * g.W * g.C / ((g.C & 7) == 0 ? 8 : 1))), dim3(256), 0,
                      (hipStream_t)stream,
-                     (const bf16_t*)dcols, (bf16_t*)dx, g);
+                     (const bf16_t*)dcols, (bf16_t*)dx, g, accumulate);
   OPCK(hipGetLastError());
   return 0;
 }

@@ -309,11 +309,28 @@ __device__ __forceinline__ void gemm_epilogue(const GemmArgs& g, f32x4 (&acc)[4]
       const float av[8] = {a0[0], a0[1], a0[2], a0[3], a1[0], a1[1], a1[2], a1[3]};
       float v[8];
       const size_t o = (size_t)row * g.ldc + col0;
+      float old[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+      if (g.beta != 0.f) {  // accumulate into the existing output: one 16-B (two for fp32) load per row chunk
+        if (full8 && g.out_bf16) {
+          const uint4 u = *(const uint4*)((const unsigned short*)g.C + o);
+          const unsigned w4[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+          for (int e = 0; e < 8; ++e) old[e] = __uint_as_float((w4[e >> 1] >> ((e & 1) * 16)) << 16);
+        } else if (full8) {
+          const f32x4 a = *(const f32x4*)((const float*)g.C + o), b = *(const f32x4*)((const float*)g.C + o + 4);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            old[e] = a[e];
+            old[e + 4] = b[e];
+          }
+        } else {
+          for (int e = 0; e < 8 && col0 + e < g.N; ++e)
+            old[e] = g.out_bf16 ? bf2f(((const unsigned short*)g.C)[o + e]) : ((const float*)g.C)[o + e];
+        }
+      }
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
-        float x = av[e] * alpha + bias8[e];
-        if (g.beta != 0.f && col0 + e < g.N)
-          x += g.beta * (g.out_bf16 ? bf2f(((const unsigned short*)g.C)[o + e]) : ((const float*)g.C)[o + e]);
+        float x = av[e] * alpha + bias8[e] + g.beta * old[e];
         if (g.relu) x = x > 0.f ? x : 0.f;
         v[e] = x;
       }

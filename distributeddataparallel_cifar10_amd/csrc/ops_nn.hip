@@ -75,7 +75,9 @@ __global__ void __launch_bounds__(256) k_im2col(const bf16_t* __restrict__ x, bf
 
 // dX[n,h,w,c] = sum over the (kh, kw) taps whose output pixel read (h, w): gather form, no atomics.
 // C % 8 == 0: one thread per pixel and 8 channels (16-B loads / stores, fp32 sums); else one per element.
-__global__ void __launch_bounds__(256) k_col2im(const bf16_t* __restrict__ dcols, bf16_t* __restrict__ dx, ConvGeom g) {
+// accumulate: dx += (the other consumer's input gradient already in dx, fused instead of a separate add)
+__global__ void __launch_bounds__(256) k_col2im(const bf16_t* __restrict__ dcols, bf16_t* __restrict__ dx, ConvGeom g,
+                                                int accumulate) {
   const int vec = (g.C & 7) == 0 ? 8 : 1;
   const int cgs = g.C / vec;
   const long total = (long)g.N * g.H * g.W * cgs;
@@ -106,6 +108,13 @@ __global__ void __launch_bounds__(256) k_col2im(const bf16_t* __restrict__ dcols
       }
     }
     const long xo = pix * g.C + c;
+    if (accumulate) {
+      float o[8];
+      if (vec == 8) unpack8(*(const uint4*)(dx + xo), o);
+      else o[0] = ld_bf(dx + xo);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) s[j] += o[j];
+    }
     if (vec == 8) *(uint4*)(dx + xo) = pack8(s);
     else dx[xo] = f2bf_rne(s[0]);
   }
@@ -637,14 +646,19 @@ __global__ void __launch_bounds__(256) k_pack_weights(const PackDesc* __restrict
   for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < total; i += (long)gridDim.x * 256) {
     long src;
     int n, c, a, b;
-    float v = 0.f;
-    if (pack_src(d, i, src, n, c, a, b)) {
-      v = d.w[src];
-      if (d.dgrad)
-        d.dgrad[(long)c * (d.kh * d.kw * d.co) + ((d.kh - 1 - a) * d.kw + (d.kw - 1 - b)) * d.co + n] = f2bf_rne(v);
-    }
+    const float v = pack_src(d, i, src, n, c, a, b) ? d.w[src] : 0.f;
     d.fwd[i] = f2bf_rne(v);
     m = fmaxf(m, fabsf(v));
+  }
+  if (d.dgrad) {  // second pass in the dgrad matrix's own order: coalesced writes, gathered (L2-resident) reads
+    const int taps = d.kh * d.kw;
+    const long dtot = (long)d.ci * taps * d.co;
+    for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < dtot; i += (long)gridDim.x * 256) {
+      const int n = (int)(i % d.co);
+      const long r = i / d.co;
+      const int tflip = (int)(r % taps), c = (int)(r / taps);
+      d.dgrad[i] = f2bf_rne(d.w[((long)n * d.ci + c) * taps + (taps - 1 - tflip)]);
+    }
   }
   if (d.q8) {
     __shared__ float red[256];

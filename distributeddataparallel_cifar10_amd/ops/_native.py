@@ -13,7 +13,7 @@ import torch
 
 from .. import build as _build
 
-ABI_VERSION = 4
+ABI_VERSION = 5
 _lock = threading.Lock()
 _lib = None
 
@@ -54,7 +54,7 @@ def _declare(lib):
     P = ctypes.POINTER
     lib.dca_ops_gemm.argtypes = [P(GemmArgs), c_void_p]
     lib.dca_ops_im2col.argtypes = [c_void_p, c_void_p, P(ConvGeom), c_void_p]
-    lib.dca_ops_col2im.argtypes = [c_void_p, c_void_p, P(ConvGeom), c_void_p]
+    lib.dca_ops_col2im.argtypes = [c_void_p, c_void_p, P(ConvGeom), c_int, c_void_p]
     lib.dca_ops_bn_fwd.argtypes = [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                                    c_void_p, c_long, c_int, c_float, c_float, c_int, c_int, c_void_p]
     lib.dca_ops_bn_fwd_parts.argtypes = [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_void_p,

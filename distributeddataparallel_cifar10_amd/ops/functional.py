@@ -266,6 +266,29 @@ def grad_sink(p: torch.Tensor):
     return getattr(p, "_dca_grad_sink", None)
 
 
+class GradJoin:
+    """A tensor consumed by ``n`` ops-layer functions (a ResNet block input: conv1 and the identity path / the
+    downsample conv) whose input gradients must be summed.  Instead of autograd's separate add kernel, the
+    first producer writes the gradient buffer and returns None; later producers accumulate into it inside their
+    own kernel (GEMM beta = 1, col2im accumulate); the last one returns the sum."""
+
+    def __init__(self, n: int = 2):
+        self.buf = None
+        self.left = n
+
+    def contribute(self, t):
+        """Register a producer's result (the buffer itself when it accumulated); returns what that producer
+        hands to autograd."""
+        if self.buf is None:
+            self.buf = t
+        elif t is not self.buf:
+            raise RuntimeError("GradJoin: a later producer must accumulate into the shared buffer")
+        self.left -= 1
+        if self.left < 0:
+            raise RuntimeError("GradJoin: more producers than declared")
+        return self.buf if self.left == 0 else None
+
+
 class Fp8Delayed:
     """Delayed-scaling fp8 state of ONE activation tensor feeding ONE fp8 GEMM (Transformer-Engine style).
 
@@ -339,10 +362,11 @@ def _conv_fwd(x, w, b, stride, pad, relu, fp8, col_stats=None, shift=None, fp8_s
     return y.view(g.N, g.Ho, g.Wo, co), st
 
 
-def _conv_bwd(dy, st, need_x: bool, need_w: bool, sink=None):
+def _conv_bwd(dy, st, need_x: bool, need_w: bool, sink=None, x_join: Optional[GradJoin] = None):
     """(dx, dw) of a conv from dY [N,Ho,Wo,Cout] (any dtype) and the forward state.  The weight gradient is
     written by the GEMM's reduce pass directly in torch's [Cout, Cin, KH, KW] layout -- into ``sink`` (a flat
-    gradient view, accumulated; dw returned as None) when given."""
+    gradient view, accumulated; dw returned as None) when given.  ``x_join``: the input is shared with another
+    consumer; its gradient is accumulated into (or seeds) the join's buffer (dx None until the last producer)."""
     g, (co, ci, kh, kw) = st["geom"], st["wshape"]
     packed = st.get("packed")
     M = g.N * g.Ho * g.Wo
@@ -350,11 +374,15 @@ def _conv_bwd(dy, st, need_x: bool, need_w: bool, sink=None):
     dx = dw = None
     cols = st["cols"]
     if need_x:
+        acc = x_join.buf if x_join is not None else None  # accumulate into the other consumer's gradient
+        beta = 1.0 if acc is not None else 0.0
+        dst2 = acc.view(g.N * g.H * g.W, g.C) if acc is not None else None
         if cols is not None and cols.data_ptr() == st["x"].data_ptr():  # 1x1 / stride 1: dX = dY . W
             if packed is not None and packed["dgrad"] is not None:  # W^T [Cin, Cout] from the pack: plain NT
-                dx = gemm(dyb, packed["dgrad"], out_dtype=torch.bfloat16).view(g.N, g.H, g.W, g.C)
+                dx = gemm(dyb, packed["dgrad"], out_dtype=torch.bfloat16, out=dst2, beta=beta)
             else:
-                dx = gemm(dyb, st["wm"], tb=True, out_dtype=torch.bfloat16).view(g.N, g.H, g.W, g.C)
+                dx = gemm(dyb, st["wm"], tb=True, out_dtype=torch.bfloat16, out=dst2, beta=beta)
+            dx = dx.view(g.N, g.H, g.W, g.C)
         elif g.stride == 1 and co % 8 == 0 and kh == kw and g.pad <= kh - 1 and g.C == ci:
             # stride 1: dX = conv(dY, W flipped, ci<->co, pad KH-1-pad), implicit GEMM (no col2im)
             gd = N.ConvGeom(N=g.N, H=g.Ho, W=g.Wo, C=co, KH=kh, KW=kw, stride=1, pad=kh - 1 - g.pad, Ho=g.H, Wo=g.W,
@@ -364,15 +392,18 @@ def _conv_bwd(dy, st, need_x: bool, need_w: bool, sink=None):
             else:
                 wd = st.get("w_master").flip(2, 3).permute(1, 2, 3, 0).reshape(ci, -1).to(torch.bfloat16).contiguous()
             dx = gemm(dyb.view(g.N, g.Ho, g.Wo, co), wd, conv=1, geom=gd, mnk=(g.N * g.H * g.W, ci, gd.K),
-                      out_dtype=torch.bfloat16).view(g.N, g.H, g.W, g.C)
+                      out_dtype=torch.bfloat16, out=dst2, beta=beta).view(g.N, g.H, g.W, g.C)
         else:
             wm = st["wm"]
             dcols = gemm(dyb, wm, tb=True, out_dtype=torch.bfloat16)  # [M, Kp] = dY . Wm
             kp = wm.shape[1]
             gc = N.ConvGeom(N=g.N, H=g.H, W=g.W, C=g.C, KH=g.KH, KW=g.KW, stride=g.stride, pad=g.pad, Ho=g.Ho,
                             Wo=g.Wo, K=g.K, Kp=kp)
-            dx = torch.empty(g.N, g.H, g.W, g.C, dtype=torch.bfloat16, device=dy.device)
-            N.check(N.lib().dca_ops_col2im(N.ptr(dcols), N.ptr(dx), gc, N.stream(dy.device)), "col2im")
+            dx = acc if acc is not None else torch.empty(g.N, g.H, g.W, g.C, dtype=torch.bfloat16, device=dy.device)
+            N.check(N.lib().dca_ops_col2im(N.ptr(dcols), N.ptr(dx), gc, int(acc is not None), N.stream(dy.device)),
+                    "col2im")
+        if x_join is not None:
+            dx = x_join.contribute(dx if acc is None else acc)
     if need_w:
         dst = sink if sink is not None else torch.empty(co, ci, kh, kw, dtype=torch.float32, device=dy.device)
         beta = 1.0 if sink is not None else 0.0
@@ -414,7 +445,7 @@ class _ConvBNAct(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, w, r, gamma, beta, running_mean, running_var, stride, pad, eps, momentum, relu, res_mode, fp8,
-                fp8_state, emit, packed, sinks):
+                fp8_state, emit, packed, sinks, x_join, r_join):
         co = w.shape[0]
         g = _geom(x, w, stride, pad)
         M = g.N * g.Ho * g.Wo
@@ -439,6 +470,7 @@ class _ConvBNAct(torch.autograd.Function):
             emit.q, emit.src_ptr = q, out.data_ptr()
         ctx.st = st
         ctx.sinks = sinks
+        ctx.joins = (x_join, r_join)
         ctx.save_for_backward(y, r, gamma, beta, stats)
         ctx.relu, ctx.res_mode = relu, res_mode
         return out
@@ -452,22 +484,28 @@ class _ConvBNAct(torch.autograd.Function):
         if sg:
             sg[1]()
             sb[1]()
+        x_join, r_join = ctx.joins
+        if r_join is not None and dr is not None:  # the identity gradient seeds the block input's shared buffer
+            dr = r_join.contribute(dr)
         dx, dw = _conv_bwd(dy_conv, ctx.st, ctx.needs_input_grad[0], ctx.needs_input_grad[1] or sw is not None,
-                           sink=sw[0] if sw else None)
+                           sink=sw[0] if sw else None, x_join=x_join if ctx.needs_input_grad[0] else None)
         if sw:
             sw[1]()
-        ctx.st = ctx.sinks = None
-        return dx, dw, dr, dgamma, dbeta, None, None, None, None, None, None, None, None, None, None, None, None, None
+        ctx.st = ctx.sinks = ctx.joins = None
+        return (dx, dw, dr, dgamma, dbeta, None, None, None, None, None, None, None, None, None, None, None, None, None,
+                None, None)
 
 
 def conv_bn_act(x, conv: torch.nn.Conv2d, bn: torch.nn.BatchNorm2d, r=None, relu=True, fp8=False, res_mode=None,
                 fp8_state: Optional[Fp8Delayed] = None, emit: Optional[Fp8Delayed] = None, packed=None,
-                direct_grads: bool = False):
+                direct_grads: bool = False, x_join: Optional[GradJoin] = None, r_join: Optional[GradJoin] = None):
     """Training-mode act(bn(conv(x))) for NHWC bf16 x, conv without bias; with a residual r: res_mode 2 (default,
     ResNet: act(bn + r)) or 1 (NetResDeep: act(bn) + r).  fp8: forward GEMM in fp8 e4m3 (fp8_state: this conv's
     delayed-scaling input state); emit: also produce the fp8 copy of the output that the consumer of ``emit`` reads.
     packed: the conv's WeightPack entry.  direct_grads: the conv weight and BN affine parameters are used once
-    per step, so their gradients may be written straight into FlatBucketDDP's flat buffer (``grad_sink``)."""
+    per step, so their gradients may be written straight into FlatBucketDDP's flat buffer (``grad_sink``).
+    x_join / r_join: the input x / the residual r is also consumed elsewhere (GradJoin): its gradient is summed
+    inside the producing kernels instead of by an autograd add."""
     if res_mode is None:
         res_mode = 2 if r is not None else 0
     if conv.bias is not None or not bn.training:
@@ -481,7 +519,8 @@ def conv_bn_act(x, conv: torch.nn.Conv2d, bn: torch.nn.BatchNorm2d, r=None, relu
         if sw is not None and sg is not None and sb is not None:
             sinks = (sw, sg, sb)
     return _ConvBNAct.apply(x, conv.weight, r, bn.weight, bn.bias, bn.running_mean, bn.running_var, conv.stride[0],
-                            conv.padding[0], bn.eps, momentum, relu, res_mode, fp8, fp8_state, emit, packed, sinks)
+                            conv.padding[0], bn.eps, momentum, relu, res_mode, fp8, fp8_state, emit, packed, sinks,
+                            x_join if torch.is_grad_enabled() else None, r_join if torch.is_grad_enabled() else None)
 
 
 def conv2d(x, w, b=None, stride=1, pad=0, relu=False, fp8=False):

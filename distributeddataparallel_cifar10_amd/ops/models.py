@@ -79,11 +79,11 @@ class OpsModel(nn.Module):
             self._fp8 = {}
         return self._fp8.setdefault(id(conv), F.Fp8Delayed())
 
-    def _conv_bn(self, h, conv, bn, relu=True, r=None, consumer=None):
+    def _conv_bn(self, h, conv, bn, relu=True, r=None, consumer=None, x_join=None, r_join=None):
         # every ResNet conv / BN is applied once per step: gradients may go straight into the flat DDP buffer
         return F.conv_bn_act(h, conv, bn, r=r, relu=relu, fp8=self._fp8_ok(conv), fp8_state=self._state(conv),
                              emit=self._state(consumer) if consumer is not None else None,
-                             packed=self._pack.get(conv), direct_grads=True)
+                             packed=self._pack.get(conv), direct_grads=True, x_join=x_join, r_join=r_join)
 
     def _resnet(self, h):
         m = self.module
@@ -92,9 +92,15 @@ class OpsModel(nn.Module):
         blocks = [b for stage in (m.layer1, m.layer2, m.layer3, m.layer4) for b in stage]
         for i, b in enumerate(blocks):
             nxt = blocks[i + 1].conv1 if i + 1 < len(blocks) else None
-            idt = h if b.downsample is None else self._conv_bn(h, b.downsample[0], b.downsample[1], relu=False)
-            out = self._conv_bn(h, b.conv1, b.bn1)
+            # the block input feeds conv1 and the identity / downsample path: one shared gradient buffer
+            join = F.GradJoin(2)
+            if b.downsample is None:
+                idt = h
+            else:
+                idt = self._conv_bn(h, b.downsample[0], b.downsample[1], relu=False, x_join=join)
+            out = self._conv_bn(h, b.conv1, b.bn1, x_join=join)
             out = self._conv_bn(out, b.conv2, b.bn2, consumer=b.conv3)
-            h = self._conv_bn(out, b.conv3, b.bn3, relu=True, r=idt, consumer=nxt)  # relu(bn3(conv3) + identity)
+            h = self._conv_bn(out, b.conv3, b.bn3, relu=True, r=idt, consumer=nxt,
+                              r_join=join if b.downsample is None else None)  # relu(bn3(conv3) + identity)
         feat = F.global_avg_pool(h)
         return F.linear(feat.to(torch.bfloat16), m.fc.weight, m.fc.bias, out_dtype=torch.float32, fp8=self.fp8)
