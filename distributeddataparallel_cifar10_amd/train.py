@@ -113,9 +113,13 @@ def load_dataset(cfg: TrainConfig):
 
 
 def resolve_engine(cfg: TrainConfig, device: torch.device, model: nn.Module) -> str:
+    """auto: NetResDeep on the fused engine, other models (ResNet family) on the ops-layer HIP kernels, on a GPU;
+    stock torch ops on the CPU."""
     if cfg.engine != "auto":
         return cfg.engine
-    return "fused" if device.type == "cuda" and _is_netresdeep(model) else "torch"
+    if device.type != "cuda":
+        return "torch"
+    return "fused" if _is_netresdeep(model) else "ops"
 
 
 def _is_netresdeep(model: nn.Module) -> bool:
@@ -235,7 +239,7 @@ def build_model_for_rank(cfg: TrainConfig, rank: int, world_size: int, device: t
         if device.type == "cuda":
             model = model.to(memory_format=torch.channels_last)
         if cfg.engine == "fused":
-            raise ValueError("the fused engine implements NetResDeep only; use --engine torch/auto for resnet50")
+            raise ValueError("the fused engine implements NetResDeep only; use --engine ops/torch/auto for resnet50")
     else:
         model = NetResDeep().to(device)
     meta = None

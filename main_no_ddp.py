@@ -8,8 +8,8 @@ CrossEntropyLoss, 99 epochs, the same log lines, no checkpoint.
 Deliberate deviation: the reference trains at import time (module-level driver without a ``__main__`` guard);
 here the driver runs only when executed as a script, so the functions can be imported.
 
-On a GPU the step runs on the native engine (device-resident data, one hipGraph replay per step); on the CPU it
-runs stock PyTorch ops.  Optional flags: see --help.
+On a GPU the step runs on the native engine (NetResDeep: device-resident data, one hipGraph replay per step) or
+on the ops-layer HIP kernels (other models, ``--engine ops``); on the CPU it runs stock PyTorch ops.  Optional flags: see --help.
 """
 from __future__ import annotations
 
@@ -42,10 +42,15 @@ def prepare(batch_size=32, pin_memory=False, num_workers=0):
 def training_loop(model, train_loader):
     """Reference main_no_ddp.py:36-59 (no checkpoint)."""
     from distributeddataparallel_cifar10_amd.parallel.ddp import FusedDDPTrainer
-    if isinstance(model, torch.nn.Module) and resolve_engine(_cfg, device, model) == "fused":
+    kind = resolve_engine(_cfg, device, model) if isinstance(model, torch.nn.Module) else None
+    if kind == "fused":
         n_idx = len(train_loader) * train_loader.batch_size
         model = FusedDDPTrainer(model, train_loader.data, train_loader.labels, batch_max=train_loader.batch_size,
                                 lr=_cfg.lr, dtype=_cfg.dtype, max_indices=max(n_idx, train_loader.batch_size))
+    elif kind == "ops":  # the ops-layer HIP kernels (flat parameters, packed weights, HIP SGD)
+        from distributeddataparallel_cifar10_amd.ops.models import OpsModel
+        from distributeddataparallel_cifar10_amd.parallel.flat_ddp import FlatBucketDDP
+        model = FlatBucketDDP(OpsModel(model, fp8=_cfg.fp8), bucket_cap_mb=_cfg.bucket_mb)
     try:
         return _train_loop(model, train_loader, 0, _cfg)
     finally:

@@ -410,3 +410,15 @@ def test_wgrad_transposed_read_kernel(gpu, M, N, K, splits):
     ref = a.float().t() @ b.float()
     out = gemm(a, b, ta=True, tb=True, splits=splits)
     assert _rel(out, ref) < 1e-5, _rel(out, ref)
+
+
+def test_main_no_ddp_resnet50_auto_ops(gpu):
+    """--model resnet50 on a GPU resolves to the ops engine (HIP kernels, packed weights, gradient sinks)."""
+    import subprocess
+    import sys
+    import os
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([sys.executable, "main_no_ddp.py", "--synthetic", "256", "--epochs", "1", "--max-steps", "3",
+                        "--model", "resnet50"], cwd=root, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    assert "Epoch 1, Training loss" in r.stdout and "training time:" in r.stdout
