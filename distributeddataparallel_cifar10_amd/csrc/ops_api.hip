@@ -136,6 +136,7 @@ int dca_ops_gemm(const GemmArgs* a, void* stream) {
   const bool wgrad = !g.fp8 && g.ta && (g.tb || g.conv == 2) && g.M % 8 == 0 && g.N % 8 == 0 && g.lda % 8 == 0 &&
                      (g.conv == 2 || g.ldb % 8 == 0) && g.ws != nullptr && getenv_wgrad_ok();
   if (wgrad) {
+    REQUIRE(g.conv != 2 || (long)g.cN * g.cHo * g.cWo < (1L << 24), "gemm: weight-gradient pixel count >= 2^24");
     const int bm = g.M <= 64 ? 64 : 128, bn = g.N <= 64 ? 64 : 128;
     const long items = (long)((g.M + bm - 1) / bm) * ((g.N + bn - 1) / bn) * g.splits;
     REQUIRE(items < (1L << 31), "gemm: too many work items");

@@ -28,6 +28,21 @@ namespace ops {
 
 typedef short s16x4 __attribute__((ext_vector_type(4)));
 
+// q = p / d, r = p % d for 0 <= p < 2^24 via a float reciprocal and one correction step (the pixel decode of the
+// implicit-im2col gather runs per row per K-tile: integer division would make the loader VALU-bound)
+__device__ __forceinline__ int fdivmod(int p, int d, float inv, int& r) {
+  int q = (int)((float)p * inv);
+  r = p - q * d;
+  if (r < 0) {
+    --q;
+    r += d;
+  } else if (r >= d) {
+    ++q;
+    r -= d;
+  }
+  return q;
+}
+
 __device__ __forceinline__ s16x4 lds_tr16(const char* p) {
   return __builtin_amdgcn_ds_read_tr16_b64_v4i16((s16x4 __attribute__((address_space(3)))*)(p));
 }
@@ -72,6 +87,7 @@ __global__ void __launch_bounds__(256) k_wgrad(GemmArgs g) {
     ckw = tap - ckh * g.cKW;
   }
 
+  const float inv_wo = 1.f / (float)g.cWo, inv_ho = 1.f / (float)g.cHo;
   uint4 sa[T::NA], sb[T::NB];
   auto load = [&](int kt) {
     const int k0 = k_begin + kt * T::BK;
@@ -89,7 +105,9 @@ __global__ void __launch_bounds__(256) k_wgrad(GemmArgs g) {
       size_t off = 0;
       if (g.conv == 2) {
         const int p = ok ? k : k_begin;
-        const int ow = p % g.cWo, t = p / g.cWo, oh = t % g.cHo, img = t / g.cHo;
+        int ow, oh;
+        const int t = fdivmod(p, g.cWo, inv_wo, ow);
+        const int img = fdivmod(t, g.cHo, inv_ho, oh);
         const int h = oh * g.cS - g.cP + ckh, w = ow * g.cS - g.cP + ckw;
         ok = ok && h >= 0 && h < g.cH && w >= 0 && w < g.cW;
         off = ok ? ((size_t)(img * g.cH + h) * g.cW + w) * g.cC + cc : 0;
