@@ -100,6 +100,7 @@ class FlatBucketDDP(nn.Module):
                 if s <= o < e:
                     self._bucket_of[p] = bi
         self._pending = [0] * len(self.buckets)
+        self._ready = set()
         self._works: list = []
         self._callback_queued = False
         self.bucket_fire_order: List[int] = []  # for tests: order in which buckets were launched
@@ -162,6 +163,11 @@ class FlatBucketDDP(nn.Module):
         def ready():
             if self.world_size == 1:
                 return
+            # idempotent per step: a kernel-written (sink) gradient reports readiness itself, and autograd may
+            # still run the parameter's AccumulateGrad with an undefined gradient, firing the hook as well
+            if p in self._ready:
+                return
+            self._ready.add(p)
             if not self._callback_queued:
                 torch.autograd.Variable._execution_engine.queue_callback(self._finish_backward)
                 self._callback_queued = True
@@ -198,6 +204,7 @@ class FlatBucketDDP(nn.Module):
 
     def _reset_pending(self) -> None:
         self._pending = [b[2] for b in self.buckets]
+        self._ready = set()
 
     # ---- module API -------------------------------------------------------------------------------------------
     def forward(self, *args, **kwargs):
