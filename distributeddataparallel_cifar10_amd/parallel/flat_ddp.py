@@ -101,6 +101,7 @@ class FlatBucketDDP(nn.Module):
                     self._bucket_of[p] = bi
         self._pending = [0] * len(self.buckets)
         self._ready = set()
+        self._fused_opt = None  # FlatSGD(overlap=True): each bucket is updated as soon as it is reduced
         self._works: list = []
         self._callback_queued = False
         self.bucket_fire_order: List[int] = []  # for tests: order in which buckets were launched
@@ -161,7 +162,7 @@ class FlatBucketDDP(nn.Module):
 
     def _make_ready(self, p):
         def ready():
-            if self.world_size == 1:
+            if self.world_size == 1 and self._fused_opt is None:
                 return
             # idempotent per step: a kernel-written (sink) gradient reports readiness itself, and autograd may
             # still run the parameter's AccumulateGrad with an undefined gradient, firing the hook as well
@@ -180,22 +181,51 @@ class FlatBucketDDP(nn.Module):
     def _launch(self, bi: int) -> None:
         s, e, _ = self.buckets[bi]
         seg = self.flat_grad[s:e]
-        if self.xgmi is not None:  # own xGMI all-reduce on the comm stream, average fused, no host sync
+        if self.world_size == 1:  # nothing to reduce: only the fused optimizer update (side stream on a GPU)
+            if seg.is_cuda:
+                cs = self._side_stream()
+                cs.wait_stream(torch.cuda.current_stream(seg.device))
+                with torch.cuda.stream(cs):
+                    self._fused_opt._update_slice(s, e)
+            else:
+                self._fused_opt._update_slice(s, e)
+        elif self.xgmi is not None:  # own xGMI all-reduce on the comm stream, average fused, no host sync
             cs = self._comm_stream
             cs.wait_stream(torch.cuda.current_stream(seg.device))
             self.xgmi.all_reduce_(seg, average=True, algo=self._algo, wire=self._wire, stream=cs)
+            if self._fused_opt is not None:  # the bucket's SGD update right behind its all-reduce
+                with torch.cuda.stream(cs):
+                    self._fused_opt._update_slice(s, e)
         else:
             seg.div_(self.world_size)  # average: pre-divide, then sum
-            self._works.append(dist.all_reduce(seg, group=self.process_group, async_op=True))
+            work = dist.all_reduce(seg, group=self.process_group, async_op=True)
+            if self._fused_opt is not None:
+                if seg.is_cuda:  # ordered behind the collective on a side stream, overlapping the backward
+                    with torch.cuda.stream(self._side_stream()):
+                        work.wait()  # RCCL: a stream-level wait on the side stream, the host does not block
+                        self._fused_opt._update_slice(s, e)
+                    work = None
+                else:
+                    self._works.append((work, s, e))
+                    work = None
+            if work is not None:
+                self._works.append((work, None, None))
         self.bucket_fire_order.append(bi)
+
+    def _side_stream(self):
+        if self._comm_stream is None:
+            self._comm_stream = torch.cuda.Stream(self.flat.device)
+        return self._comm_stream
 
     def _finish_backward(self) -> None:
         # parameters that received no gradient this step: reduce their (zero) slices too, in bucket order
         for bi, left in enumerate(self._pending):
             if left:
                 self._launch(bi)
-        for w in self._works:
+        for w, s, e in self._works:
             w.wait()
+            if s is not None:  # CPU: the fused update of a bucket after its (gloo) all-reduce
+                self._fused_opt._update_slice(s, e)
         if self._comm_stream is not None:
             torch.cuda.current_stream(self.flat_grad.device).wait_stream(self._comm_stream)
         self._works = []
@@ -233,16 +263,46 @@ class FlatSGD(torch.optim.Optimizer):
     """``optim.SGD`` over the flat buffer in one or two fused ops.
 
     Default = reference ``main.py:27`` (lr only).  ``momentum`` / ``weight_decay`` follow torch.optim.SGD's
-    formulas (buf = m * buf + (g + wd * p); p -= lr * buf), e.g. the ppe_main_ddp.py setting SGD(1e-3, 0.9)."""
+    formulas (buf = m * buf + (g + wd * p); p -= lr * buf), e.g. the ppe_main_ddp.py setting SGD(1e-3, 0.9).
 
-    def __init__(self, ddp: FlatBucketDDP, lr: float = 1e-2, momentum: float = 0.0, weight_decay: float = 0.0):
+    ``overlap=True`` (BASELINE config 5, "fused SGD + all-reduce overlap"): every gradient bucket is updated as
+    soon as it is complete -- right behind its all-reduce on the comm stream (HIP SGD kernel), or on a side
+    stream with one rank -- so the update overlaps the rest of the backward; ``step()`` then has nothing left
+    to do.  The momentum buffer starts at zero, so its first update equals the gradient (torch's semantics)."""
+
+    def __init__(self, ddp: FlatBucketDDP, lr: float = 1e-2, momentum: float = 0.0, weight_decay: float = 0.0,
+                 overlap: bool = False):
         super().__init__(list(ddp.module.parameters()), dict(lr=lr, momentum=momentum, weight_decay=weight_decay))
         self.ddp = ddp
         self._buf = None
+        self.overlap = overlap
+        if overlap:
+            if ddp._fused_opt is not None:
+                raise ValueError("FlatBucketDDP already has a fused optimizer")
+            if momentum:
+                self._buf = torch.zeros_like(ddp.flat)
+            ddp._fused_opt = self
+
+    @torch.no_grad()
+    def _update_slice(self, s: int, e: int) -> None:
+        g = self.param_groups[0]
+        p, grad = self.ddp.flat[s:e], self.ddp.flat_grad[s:e]
+        buf = self._buf[s:e] if self._buf is not None else None
+        if p.is_cuda:
+            from ..ops.functional import sgd_step_
+            sgd_step_(p, grad, g["lr"], g["momentum"], g["weight_decay"], buf=buf, first=None)
+            return
+        d = grad.add(p, alpha=g["weight_decay"]) if g["weight_decay"] else grad
+        if buf is not None:
+            buf.mul_(g["momentum"]).add_(d)
+            d = buf
+        p.add_(d, alpha=-g["lr"])
 
     @torch.no_grad()
     def step(self, closure=None):
         loss = closure() if closure is not None else None
+        if self.overlap:  # already applied bucket by bucket during the backward
+            return loss
         g = self.param_groups[0]
         if self.ddp.flat.is_cuda:  # one HIP kernel over the flat buffer (ops/functional.py sgd_step_)
             from ..ops.functional import sgd_step_

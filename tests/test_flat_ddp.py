@@ -137,3 +137,54 @@ def test_flat_ddp_single_process_zero_grad_none():
     F.cross_entropy(ddp(x), y).backward()
     assert all(p.grad.data_ptr() >= ddp.flat_grad.data_ptr() for p in m.parameters())
     assert torch.allclose(ddp.flat_grad, g1, atol=1e-6)
+
+
+def _fused_sgd_worker(rank, ws, port, q):
+    import traceback
+    try:
+        import os
+        import torch.distributed as dist
+        os.environ["MASTER_ADDR"] = "127.0.0.1"
+        os.environ["MASTER_PORT"] = str(port)
+        if ws > 1:
+            dist.init_process_group("gloo", rank=rank, world_size=ws)
+        import torch.nn as nn
+        from distributeddataparallel_cifar10_amd.parallel.flat_ddp import FlatBucketDDP, FlatSGD
+        torch.manual_seed(0)
+        a = nn.Sequential(nn.Conv2d(3, 8, 3, padding=1), nn.ReLU(), nn.Flatten(), nn.Linear(8 * 8 * 8, 10))
+        b = nn.Sequential(nn.Conv2d(3, 8, 3, padding=1), nn.ReLU(), nn.Flatten(), nn.Linear(8 * 8 * 8, 10))
+        b.load_state_dict(a.state_dict())
+        da = FlatBucketDDP(a, bucket_cap_mb=0.005, first_bucket_mb=0.002)
+        db = FlatBucketDDP(b, bucket_cap_mb=0.005, first_bucket_mb=0.002)
+        assert len(da.buckets) >= 2
+        oa = FlatSGD(da, lr=0.05, momentum=0.9, weight_decay=1e-3)
+        ob = FlatSGD(db, lr=0.05, momentum=0.9, weight_decay=1e-3, overlap=True)
+        for step in range(4):
+            g = torch.Generator().manual_seed(10 * step + rank)
+            x, y = torch.randn(4, 3, 8, 8, generator=g), torch.randint(0, 10, (4,), generator=g)
+            for d, o in ((da, oa), (db, ob)):
+                o.zero_grad()
+                nn.functional.cross_entropy(d(x), y).backward()
+                o.step()
+            torch.testing.assert_close(db.flat, da.flat, rtol=1e-6, atol=1e-7, msg=f"step {step}")
+        q.put((rank, None))
+    except Exception:
+        q.put((rank, traceback.format_exc()))
+
+
+@pytest.mark.parametrize("ws", [1, 2])
+def test_fused_overlapped_sgd_matches_step(ws):
+    """FlatSGD(overlap=True): per-bucket updates issued during the backward (behind each bucket's all-reduce)
+    give the same parameters as one SGD step after the backward (momentum + weight decay, 4 steps)."""
+    import torch.multiprocessing as mp
+    port = 29600 + ws
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_fused_sgd_worker, args=(r, ws, port, q)) for r in range(ws)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=300) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+    bad = [r for r in res if r[1]]
+    assert not bad, "\n".join(f"rank {r}:\n{e}" for r, e in bad)

@@ -422,3 +422,29 @@ def test_main_no_ddp_resnet50_auto_ops(gpu):
                         "--model", "resnet50"], cwd=root, capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stderr[-3000:]
     assert "Epoch 1, Training loss" in r.stdout and "training time:" in r.stdout
+
+
+def test_ops_resnet_overlapped_sgd_matches(gpu):
+    """FlatSGD(overlap=True) on the GPU (bucket updates on the side stream during the backward, momentum) gives
+    the same parameters as the post-backward flat SGD, step for step."""
+    import copy
+    from distributeddataparallel_cifar10_amd.models.resnet50 import ResNet
+    from distributeddataparallel_cifar10_amd.ops import OpsModel, cross_entropy
+    from distributeddataparallel_cifar10_amd.parallel.flat_ddp import FlatBucketDDP, FlatSGD
+    torch.manual_seed(4)
+    a = ResNet([1, 1, 1, 1], num_classes=10).to(gpu)
+    b = copy.deepcopy(a)
+    da = FlatBucketDDP(OpsModel(a), bucket_cap_mb=1.0, first_bucket_mb=0.2)
+    db = FlatBucketDDP(OpsModel(b), bucket_cap_mb=1.0, first_bucket_mb=0.2)
+    oa = FlatSGD(da, lr=0.05, momentum=0.9, weight_decay=1e-4)
+    ob = FlatSGD(db, lr=0.05, momentum=0.9, weight_decay=1e-4, overlap=True)
+    x = torch.randn(4, 3, 64, 64, device=gpu)
+    y = torch.randint(0, 10, (4,), device=gpu)
+    for step in range(3):
+        for d, o in ((da, oa), (db, ob)):
+            o.zero_grad()
+            cross_entropy(d(x), y).backward()
+            o.step()
+        torch.cuda.synchronize()
+        assert sorted(db.bucket_fire_order) == list(range(len(db.buckets)))
+        assert torch.equal(da.flat, db.flat), (step, _rel(db.flat, da.flat))
