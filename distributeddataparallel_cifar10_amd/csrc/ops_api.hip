@@ -75,7 +75,8 @@ int dca_ops_gemm(const GemmArgs* a, void* stream) {
   hipStream_t st = (hipStream_t)stream;
   REQUIRE(g.M > 0 && g.N > 0 && g.K > 0, "gemm: empty problem");
   REQUIRE(!g.fp8 || (!g.ta && !g.tb), "gemm: fp8 operands must be K-contiguous (ta = tb = 0)");
-  REQUIRE(!g.fp8 || (g.K % 16 == 0 && g.lda % 16 == 0 && g.ldb % 16 == 0), "gemm: fp8 needs K, lda, ldb % 16 == 0");
+  REQUIRE(!g.fp8 || (g.K % 16 == 0 && (g.conv == 1 || g.lda % 16 == 0) && g.ldb % 16 == 0),
+          "gemm: fp8 needs K, lda, ldb % 16 == 0");
   REQUIRE(g.conv == 1 || g.ta || g.lda >= g.K, "gemm: lda < K");
   REQUIRE(g.conv == 2 || !g.tb || g.ldb >= g.N, "gemm: ldb < N (transposed B)");
   REQUIRE(g.conv == 2 || g.tb || g.ldb >= g.K, "gemm: ldb < K");
@@ -83,7 +84,8 @@ int dca_ops_gemm(const GemmArgs* a, void* stream) {
   REQUIRE(g.ldc >= g.N, "gemm: ldc < N");
   REQUIRE(g.conv >= 0 && g.conv <= 2, "gemm: bad conv mode");
   if (g.conv) {
-    REQUIRE(!g.fp8 && g.cC % 8 == 0 && g.cC > 0, "gemm: implicit conv needs bf16 and C % 8 == 0");
+    REQUIRE(g.cC > 0 && (g.fp8 ? (g.conv == 1 && g.cC % 16 == 0) : g.cC % 8 == 0),
+            "gemm: implicit conv needs C % 8 == 0 (bf16) or an fp8 forward with C % 16 == 0");
     REQUIRE(g.cHo == (g.cH + 2 * g.cP - g.cKH) / g.cS + 1 && g.cWo == (g.cW + 2 * g.cP - g.cKW) / g.cS + 1,
             "gemm: inconsistent conv geometry");
     const long pix = (long)g.cN * g.cHo * g.cWo, kc = (long)g.cKH * g.cKW * g.cC;
@@ -159,10 +161,11 @@ int dca_ops_gemm(const GemmArgs* a, void* stream) {
   g.single = g.k_per_split <= 4 * kt ? 1 : 0;  // short K: one operand buffer, twice the workgroups per CU
   // K-contiguous operands with 16-B aligned rows: direct global -> LDS staging (k_gemm_glds)
   const int esz = g.fp8 ? 1 : 2;
-  // (measured, bench/gemm_bench.py: +18..100 % on plain NT GEMMs; implicit convs only when C % 64 == 0 (one
-  // tap per K-tile: a wave-uniform decode); short-K narrow tiles stay on the single-buffer register kernel)
+  // (measured, bench/gemm_bench.py: +18..100 % on plain NT GEMMs; bf16 implicit convs only when C % 64 == 0 (one
+  // tap per K-tile: a wave-uniform decode) and opted in; fp8 implicit convs always (the register-staged fp8
+  // kernel needs 219 VGPRs: one wave per SIMD); short-K narrow tiles stay on the single-buffer register kernel)
   const bool glds = getenv_glds_ok() && !g.ta && !g.tb && !(narrow && g.single) &&
-                    (g.conv == 1 ? (g.cC % 64 == 0 && getenv_glds_conv())
+                    (g.conv == 1 ? (g.fp8 || (g.cC % 64 == 0 && getenv_glds_conv()))
                                  : (g.conv == 0 && (long)g.lda * esz % 16 == 0 && (long)g.K * esz % 16 == 0)) &&
                     (long)g.ldb * esz % 16 == 0 && ((uintptr_t)g.A & 15) == 0 && ((uintptr_t)g.B & 15) == 0;
   if (glds) {

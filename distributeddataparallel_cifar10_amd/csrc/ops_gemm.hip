@@ -185,15 +185,17 @@ __device__ __forceinline__ void conv_rows(ConvRows& cr, const GemmArgs& g, int m
     cr.iw[i] = ow * g.cS - g.cP;
   }
 }
-__device__ __forceinline__ void load_conv_a(Stage& s, const unsigned short* x, const ConvRows& cr, const GemmArgs& g,
-                                            int k0, int k_end) {
-  const int k = k0 + (threadIdx.x & 7) * 8;  // 8 channels of one tap (C % 8 == 0)
+// ESZ = 2: 8 bf16 channels of one tap per 16-B chunk (C % 8 == 0); ESZ = 1: 16 fp8 channels (C % 16 == 0)
+template <int ESZ>
+__device__ __forceinline__ void load_conv_a(Stage& s, const char* x, const ConvRows& cr, const GemmArgs& g, int k0,
+                                            int k_end) {
+  const int k = k0 + (threadIdx.x & 7) * (16 / ESZ);  // one tap per chunk
   const int tap = k / g.cC, c = k - tap * g.cC, kh = tap / g.cKW, kw = tap - kh * g.cKW;
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     const int h = cr.ih[i] + kh, w = cr.iw[i] + kw;
     const bool ok = k < k_end && h >= 0 && h < g.cH && w >= 0 && w < g.cW;
-    const long off = ok ? ((long)(cr.nh[i] + h) * g.cW + w) * g.cC + c : 0;
+    const long off = ok ? (((long)(cr.nh[i] + h) * g.cW + w) * g.cC + c) * ESZ : 0;
     const uint4 v = *(const uint4*)(x + off);
     s.v[i] = ok ? v : uint4{0u, 0u, 0u, 0u};
   }
@@ -420,7 +422,7 @@ __global__ void __launch_bounds__(GT) k_gemm(GemmArgs g) {
   using SB = StageT<BN_ / 32>;
   auto load = [&](Stage& sa, SB& sb, int kt) {
     const int k0 = k_begin + kt * KT;
-    if (g.conv == 1) load_conv_a(sa, (const unsigned short*)g.A, cr, g, k0, k_end);
+    if (g.conv == 1) load_conv_a<ESZ>(sa, (const char*)g.A, cr, g, k0, k_end);
     else if (g.ta) load_t(sa, (const unsigned short*)g.A, m0, g.M, g.lda, k0, k_end);
     else load_nt<ESZ>(sa, (const char*)g.A, m0, g.M, (size_t)g.lda * ESZ, k0 * ESZ, k_end * ESZ);
     if constexpr (BN_ == 128) {
@@ -587,18 +589,18 @@ __global__ void __launch_bounds__(GT) k_gemm_glds(GemmArgs g) {
       if (g.conv == 1) {
         int c, kh, kw;
         if (c64) {  // the whole K-tile is one tap: wave-uniform decode, per-lane channel offset only
-          c = tc0 + ((kb - kb0) >> 1);
+          c = tc0 + (kb - kb0) / ESZ;
           kh = tkh;
           kw = tkw;
         } else {
-          const int k = kb >> 1, tap = k / g.cC;
+          const int k = kb / ESZ, tap = k / g.cC;
           c = k - tap * g.cC;
           kh = tap / g.cKW;
           kw = tap - kh * g.cKW;
         }
         const int h = ih[i] + kh, w = iw[i] + kw;
         if (kb < kb_end && h >= 0 && h < g.cH && w >= 0 && w < g.cW)
-          src = (const unsigned short*)g.A + ((size_t)(nh[i] + h) * g.cW + w) * g.cC + c;
+          src = (const char*)g.A + (((size_t)(nh[i] + h) * g.cW + w) * g.cC + c) * ESZ;
       } else if (kb < kb_end) {
         src = arow[i] + kb;
       }

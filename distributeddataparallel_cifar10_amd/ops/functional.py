@@ -334,6 +334,15 @@ def _conv_fwd(x, w, b, stride, pad, relu, fp8, col_stats=None, shift=None, fp8_s
     if packed is not None and packed["kp"] != g.K:
         raise ValueError("conv: packed weight does not match the input channels")
     use_fp8 = fp8 and g.Kp % 16 == 0 and (packed is None or packed["q8"] is not None)
+    if use_fp8 and not direct and g.C % 16 == 0 and packed is not None:
+        # fp8 implicit conv: the NHWC input's fp8 copy (emitted by its producer) gathered on the fly
+        qx, ax, delayed = _fp8_operand(x, fp8_state)
+        y = gemm(qx, packed["q8"], conv=1, geom=g, mnk=(M, co, g.K), bias=b, relu=relu, out_dtype=torch.bfloat16,
+                 amax_a=ax, amax_b=packed["amax"], col_stats=col_stats, stats_shift=shift)
+        if delayed:
+            fp8_state.amax_prev.copy_(fp8_state.amax_out.view(torch.float32))
+        st["wm"] = packed["fwd"]
+        return y.view(g.N, g.Ho, g.Wo, co), st
     if direct or use_fp8 or not _implicit_ok(g):
         if direct:
             cols = x.view(M, g.K)

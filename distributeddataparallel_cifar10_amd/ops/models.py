@@ -13,12 +13,15 @@ switches to channels-last bf16 once, and runs:
   -> fc.  The bf16 (and fp8) GEMM operands of all convolutions are rebuilt from the fp32 weights by one
   ``WeightPack`` launch per step, and the conv / BN parameter gradients are written straight into the flat
   gradient buffer of ``FlatBucketDDP`` when the model is wrapped in it (``functional.grad_sink``).
-  With ``fp8=True`` the 1x1 convolutions (Cin >= 128) and fc run their forward GEMM in fp8 e4m3 on the
-  MX-scaled MFMA (fp8 rate): weights are quantised per step with a device-side amax; activations are emitted in
+  With ``fp8=True`` the 3x3 convolutions (implicit GEMM over an fp8 NHWC copy of the input), fc, and optionally
+  the 1x1 convolutions (``DCA_FP8_MIN_CIN``) run their forward GEMM in fp8 e4m3 on the MX-scaled MFMA (fp8 rate):
+  weights are quantised per step (WeightPack, device-side amax); activations are emitted in
   fp8 directly by the producing BN kernel with delayed scaling (previous step's amax, ``functional.Fp8Delayed``);
   gradients and the backward stay bf16 (BASELINE config 5).
 """
 from __future__ import annotations
+
+import os
 
 import torch
 import torch.nn as nn
@@ -67,10 +70,21 @@ class OpsModel(nn.Module):
         z = F.linear(flat, w1, m.fc1.bias, relu=True, out_dtype=torch.bfloat16)
         return F.linear(z, m.fc2.weight, m.fc2.bias, out_dtype=torch.float32)
 
+    # fp8 pays where the GEMM is MFMA-bound: the 3x3 convolutions (K = 9 Cin).  For the 1x1 convolutions the fp8
+    # copy the producer must write costs more than the faster GEMM saves (measured at batch 256: 1x1 fp8 from
+    # Cin >= 256 / 512 / 1024 / never -> 7659 / 7681 / 7729 / 7763 img/s, bf16 7708), so they stay bf16 unless
+    # DCA_FP8_MIN_CIN (>= 128) asks for them.
+    FP8_MIN_CIN = int(os.environ.get("DCA_FP8_MIN_CIN", "0")) or None
+
     def _fp8_ok(self, conv) -> bool:
-        """fp8 forward for 1x1 stride-1 convolutions with K = Cin >= 128 (the fp8 K-tile is 128 deep)."""
-        return (self.fp8 and conv.kernel_size == (1, 1) and conv.stride == (1, 1) and conv.padding == (0, 0)
-                and conv.in_channels >= 128)
+        """fp8 forward GEMM for 1x1 stride-1 convolutions with K = Cin >= FP8_MIN_CIN (the fp8 K-tile is 128
+        deep) and for 3x3 convolutions (K = 9 Cin, implicit GEMM over the input's fp8 copy; Cin % 16 == 0)."""
+        if not self.fp8:
+            return False
+        if conv.kernel_size == (3, 3):
+            return conv.in_channels % 16 == 0 and conv.in_channels >= 64
+        return (self.FP8_MIN_CIN is not None and conv.kernel_size == (1, 1) and conv.stride == (1, 1)
+                and conv.padding == (0, 0) and conv.in_channels >= max(128, self.FP8_MIN_CIN))
 
     def _state(self, conv):
         if not self._fp8_ok(conv):
@@ -98,7 +112,7 @@ class OpsModel(nn.Module):
                 idt = h
             else:
                 idt = self._conv_bn(h, b.downsample[0], b.downsample[1], relu=False, x_join=join)
-            out = self._conv_bn(h, b.conv1, b.bn1, x_join=join)
+            out = self._conv_bn(h, b.conv1, b.bn1, x_join=join, consumer=b.conv2)
             out = self._conv_bn(out, b.conv2, b.bn2, consumer=b.conv3)
             h = self._conv_bn(out, b.conv3, b.bn3, relu=True, r=idt, consumer=nxt,
                               r_join=join if b.downsample is None else None)  # relu(bn3(conv3) + identity)

@@ -448,3 +448,30 @@ def test_ops_resnet_overlapped_sgd_matches(gpu):
         torch.cuda.synchronize()
         assert sorted(db.bucket_fire_order) == list(range(len(db.buckets)))
         assert torch.equal(da.flat, db.flat), (step, _rel(db.flat, da.flat))
+
+
+@pytest.mark.parametrize("s", [1, 2])
+def test_conv_bn_act_fp8_implicit_3x3(gpu, s):
+    """fp8 forward of a 3x3 conv as an implicit GEMM over the input's fp8 copy (packed fp8 weights), with BN in
+    the epilogue, vs torch fp32: forward within fp8 tolerance, backward (bf16) unaffected in structure."""
+    from distributeddataparallel_cifar10_amd.ops import conv_bn_act
+    from distributeddataparallel_cifar10_amd.ops import functional as F
+    g = torch.Generator(device=gpu).manual_seed(11 + s)
+    n, h, ci, co = 4, 14, 64, 32
+    conv = torch.nn.Conv2d(ci, co, 3, stride=s, padding=1, bias=False).to(gpu)
+    bn = torch.nn.BatchNorm2d(co).to(gpu)
+    rconv, rbn = torch.nn.Conv2d(ci, co, 3, stride=s, padding=1, bias=False).to(gpu), torch.nn.BatchNorm2d(co).to(gpu)
+    rconv.load_state_dict(conv.state_dict())
+    rbn.load_state_dict(bn.state_dict())
+    pack = F.WeightPack([conv], [conv])
+    pack.pack()
+    x = _bf(torch.randn(n, h, h, ci, device=gpu, generator=g)).requires_grad_()
+    y = conv_bn_act(x, conv, bn, relu=True, fp8=True, packed=pack.get(conv))
+    dy = _bf(torch.randn(y.shape, device=gpu, generator=g))
+    y.backward(dy)
+    xr = x.detach().float().permute(0, 3, 1, 2).requires_grad_()
+    z = torch.relu(rbn(rconv(xr)))
+    z.backward(dy.float().permute(0, 3, 1, 2))
+    assert _rel(y.float().permute(0, 3, 1, 2), z) < 0.08
+    assert _rel(x.grad.float().permute(0, 3, 1, 2), xr.grad) < 0.2
+    assert _rel(conv.weight.grad, rconv.weight.grad) < 0.2
