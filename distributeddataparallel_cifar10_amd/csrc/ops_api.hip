@@ -44,12 +44,10 @@ inline bool getenv_glds_ok() {
   static const bool v = getenv_flag("DCA_OPS_GLDS");
   return v;
 }
-// implicit-conv glds measured neutral vs the register-staged gather (profiles/gemm_bench_*_r1c.log): opt-in
+// bf16 implicit-conv glds (C % 64 == 0): neutral at batch 64, +2..6 % per conv GEMM at batch 256
+// (DCA_OPS_GLDS_CONV=0 turns it off)
 inline bool getenv_glds_conv() {
-  static const bool v = [] {
-    const char* e = getenv("DCA_OPS_GLDS_CONV");
-    return e && e[0] == '1';
-  }();
+  static const bool v = getenv_flag("DCA_OPS_GLDS_CONV");
   return v;
 }
 inline bool getenv_wgrad_ok() {
@@ -162,7 +160,7 @@ int dca_ops_gemm(const GemmArgs* a, void* stream) {
   // K-contiguous operands with 16-B aligned rows: direct global -> LDS staging (k_gemm_glds)
   const int esz = g.fp8 ? 1 : 2;
   // (measured, bench/gemm_bench.py: +18..100 % on plain NT GEMMs; bf16 implicit convs only when C % 64 == 0 (one
-  // tap per K-tile: a wave-uniform decode) and opted in; fp8 implicit convs always (the register-staged fp8
+  // tap per K-tile: a wave-uniform decode); fp8 implicit convs always (the register-staged fp8
   // kernel needs 219 VGPRs: one wave per SIMD); short-K narrow tiles stay on the single-buffer register kernel)
   const bool glds = getenv_glds_ok() && !g.ta && !g.tb && !(narrow && g.single) &&
                     (g.conv == 1 ? (g.fp8 || (g.cC % 64 == 0 && getenv_glds_conv()))
