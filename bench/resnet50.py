@@ -35,6 +35,9 @@ def main() -> int:
                     help="torch: stock conv/BN (MIOpen) under bf16 autocast; ops: the framework's HIP kernels "
                          "(MFMA GEMM convs, fused BN+ReLU+residual, fused CE, HIP SGD)")
     ap.add_argument("--fp8", action="store_true", help="ops path: fp8 e4m3 forward GEMMs for 1x1 convs and fc")
+    ap.add_argument("--graph", type=int, default=0,
+                    help="1: capture the whole training step (forward, backward, SGD) in a HIP graph and replay it "
+                         "(one rank: no collectives inside the capture)")
     ap.add_argument("--overlap-sgd", type=int, default=0,
                     help="1: each gradient bucket's SGD update runs right behind its all-reduce during the backward "
                          "(FlatSGD overlap=True; measured 4.6 %% slower on 1 GPU, where there is no all-reduce to hide "
@@ -74,10 +77,26 @@ def main() -> int:
     for _ in range(a.warmup):
         step()
     torch.cuda.synchronize()
+    run = step
+    if a.graph:
+        if world > 1:
+            raise SystemExit("--graph: one rank only")
+        g_ = torch.cuda.CUDAGraph()
+        s_ = torch.cuda.Stream()
+        s_.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s_):
+            step()  # one more eager step on the capture stream (allocator warm-up)
+        torch.cuda.current_stream().wait_stream(s_)
+        with torch.cuda.graph(g_):
+            static_loss = step()
+
+        def run():
+            g_.replay()
+            return static_loss
     dist.barrier()
     t0 = time.perf_counter()
     for _ in range(a.steps):
-        loss = step()
+        loss = run()
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
     t = torch.tensor([dt], device=dev, dtype=torch.float64)
@@ -92,7 +111,8 @@ def main() -> int:
                           "config": {"model": "ResNet-50", "per_rank_batch": a.batch, "image": a.image,
                                      "parallelism": f"dp{world}", "optimizer": "SGD(0.1, momentum 0.9)" +
                                      (", per-bucket updates overlapped with the backward" if a.overlap_sgd else ""),
-                                     "path": ("FlatBucketDDP + ops HIP kernels" + (" (fp8 fwd GEMMs)" if a.fp8 else " (bf16)"))
+                                     "path": ("FlatBucketDDP + ops HIP kernels" + (" (fp8 fwd GEMMs)" if a.fp8 else " (bf16)")
+                                              + (", step replayed as a HIP graph" if a.graph else ""))
                                      if a.path == "ops" else "FlatBucketDDP + stock conv (MIOpen), bf16 autocast"}}),
               flush=True)
     dist.destroy_process_group()
