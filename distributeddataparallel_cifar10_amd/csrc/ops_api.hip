@@ -50,6 +50,22 @@ inline bool getenv_glds_conv() {
   static const bool v = getenv_flag("DCA_OPS_GLDS_CONV");
   return v;
 }
+// single-buffer weight-gradient kernel: the loop is latency-bound, so more resident workgroups per CU win
+// (batch-256 census: M = 64 weight gradients 845 -> 580 us, 835 -> 556 us; DCA_OPS_WGRAD_SINGLE=0 turns it off)
+inline bool getenv_wgrad_single() {
+  static const bool v = getenv_flag("DCA_OPS_WGRAD_SINGLE");
+  return v;
+}
+// glds single-buffer mode (32 KiB LDS: ~1.5x the resident workgroups) for short K.  Batch-256 census vs
+// double-buffered: K <= 576 0.78-0.91x time, K = 1152 0.93x, K = 1024-4608 0.97-1.23x.
+// DCA_OPS_GLDS_SINGLE = 0: never, 1: always, unset: K-tiles per split <= 9.
+inline int getenv_glds_single() {
+  static const int v = [] {
+    const char* e = getenv("DCA_OPS_GLDS_SINGLE");
+    return e ? (e[0] == '1' ? 1 : 0) : -1;
+  }();
+  return v;
+}
 inline bool getenv_wgrad_ok() {
   static const int v = [] {
     const char* e = getenv("DCA_OPS_WGRAD");
@@ -141,8 +157,11 @@ int dca_ops_gemm(const GemmArgs* a, void* stream) {
     const long items = (long)((g.M + bm - 1) / bm) * ((g.N + bn - 1) / bn) * g.splits;
     REQUIRE(items < (1L << 31), "gemm: too many work items");
     const dim3 grid((unsigned)items);
-    constexpr int l00 = WgradTile<64, 64, 2>::LDS, l01 = WgradTile<64, 128, 1>::LDS;
-    constexpr int l10 = WgradTile<128, 64, 4>::LDS, l11 = WgradTile<128, 128, 2>::LDS;
+    // single LDS buffer: more resident workgroups per CU for these latency-bound loops
+    g.single = getenv_wgrad_single() ? 1 : 0;
+    const int sh = g.single ? 1 : 0;
+    const int l00 = WgradTile<64, 64, 2>::LDS >> sh, l01 = WgradTile<64, 128, 1>::LDS >> sh;
+    const int l10 = WgradTile<128, 64, 4>::LDS >> sh, l11 = WgradTile<128, 128, 2>::LDS >> sh;
     if (bm == 64 && bn == 64) hipLaunchKernelGGL((k_wgrad<64, 64, 2>), grid, dim3(256), l00, st, g);
     else if (bm == 64) hipLaunchKernelGGL((k_wgrad<64, 128, 1>), grid, dim3(256), l01, st, g);
     else if (bn == 64) hipLaunchKernelGGL((k_wgrad<128, 64, 4>), grid, dim3(256), l10, st, g);
@@ -167,12 +186,16 @@ int dca_ops_gemm(const GemmArgs* a, void* stream) {
                                  : (g.conv == 0 && (long)g.lda * esz % 16 == 0 && (long)g.K * esz % 16 == 0)) &&
                     (long)g.ldb * esz % 16 == 0 && ((uintptr_t)g.A & 15) == 0 && ((uintptr_t)g.B & 15) == 0;
   if (glds) {
+    const int gs = getenv_glds_single();
+    g.single = gs >= 0 ? gs : (g.k_per_split <= 9 * kt ? 1 : 0);
+    const int l64 = g.single ? GemmTile<64>::LDS_SINGLE : GemmTile<64>::LDS;
+    const int l128 = g.single ? GemmTile<128>::LDS_SINGLE : GemmTile<128>::LDS;
     if (narrow) {
-      if (g.fp8) hipLaunchKernelGGL((k_gemm_glds<true, 64>), grid, dim3(GT), GemmTile<64>::LDS, st, g);
-      else hipLaunchKernelGGL((k_gemm_glds<false, 64>), grid, dim3(GT), GemmTile<64>::LDS, st, g);
+      if (g.fp8) hipLaunchKernelGGL((k_gemm_glds<true, 64>), grid, dim3(GT), l64, st, g);
+      else hipLaunchKernelGGL((k_gemm_glds<false, 64>), grid, dim3(GT), l64, st, g);
     } else {
-      if (g.fp8) hipLaunchKernelGGL((k_gemm_glds<true, 128>), grid, dim3(GT), GemmTile<128>::LDS, st, g);
-      else hipLaunchKernelGGL((k_gemm_glds<false, 128>), grid, dim3(GT), GemmTile<128>::LDS, st, g);
+      if (g.fp8) hipLaunchKernelGGL((k_gemm_glds<true, 128>), grid, dim3(GT), l128, st, g);
+      else hipLaunchKernelGGL((k_gemm_glds<false, 128>), grid, dim3(GT), l128, st, g);
     }
   } else if (narrow) {
     const int lds = g.single ? GemmTile<64>::LDS_SINGLE : GemmTile<64>::LDS;

@@ -621,10 +621,11 @@ __global__ void __launch_bounds__(GT) k_gemm_glds(GemmArgs g) {
 #pragma unroll
     for (int n = 0; n < T::NF; ++n) acc[m][n] = f32x4{0.f, 0.f, 0.f, 0.f};
 
+  const bool single = g.single != 0;  // one buffer: tile k+1 is issued after tile k's closing barrier
   if (nk > 0) issue(0, 0);
   for (int kt = 0; kt < nk; ++kt) {
-    const int buf = kt & 1;
-    if (kt + 1 < nk) {
+    const int buf = single ? 0 : kt & 1;
+    if (kt + 1 < nk && !single) {
       issue(kt + 1, buf ^ 1);  // the buffer every wave finished reading before the previous closing barrier
       wait_vmcnt<NI>();         // this thread's loads of tile kt have landed (tile kt+1's still in flight)
     } else {
@@ -673,6 +674,7 @@ __global__ void __launch_bounds__(GT) k_gemm_glds(GemmArgs g) {
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();  // every wave is done reading buf before it is refilled
     asm volatile("" ::: "memory");
+    if (single && kt + 1 < nk) issue(kt + 1, 0);
   }
   gemm_epilogue<BN_>(g, acc, smem, m0, n0, tm, ksplit);
 }

@@ -142,8 +142,9 @@ __global__ void __launch_bounds__(256) k_wgrad(GemmArgs g) {
     store(0);
   }
   __syncthreads();
+  const bool single = g.single != 0;  // one LDS buffer: half the LDS, twice the workgroups per CU
   for (int kt = 0; kt < nk; ++kt) {
-    const int buf = kt & 1;
+    const int buf = single ? 0 : (kt & 1);
     if (kt + 1 < nk) load(kt + 1);
     const char* la = smem + buf * T::BUF;
     const char* lb = la + T::A_BYTES;
@@ -169,7 +170,10 @@ __global__ void __launch_bounds__(256) k_wgrad(GemmArgs g) {
         for (int j = 0; j < T::FN; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
     }
-    if (kt + 1 < nk) store(buf ^ 1);
+    if (kt + 1 < nk) {
+      if (single) __syncthreads();  // every wave is done reading the buffer it is about to overwrite
+      store(single ? 0 : buf ^ 1);
+    }
     __syncthreads();
   }
 
