@@ -74,6 +74,14 @@ inline bool getenv_wgrad_ok() {
   return v != 0;
 }
 inline int nparts_rows(long M) { return (int)((M + dca::ops::BN_ROWS - 1) / dca::ops::BN_ROWS); }
+// BN kernels: 16 channel lanes (256 contiguous bytes per row and wave instruction) when C % 128 == 0, else 8
+#define BN_LAUNCH(kern, C, rows, st, ...)                                                              \
+  do {                                                                                                 \
+    if ((C) % 128 == 0)                                                                                \
+      hipLaunchKernelGGL((kern<16>), dim3((C) / 128, rows), dim3(256), 0, st, __VA_ARGS__);            \
+    else                                                                                               \
+      hipLaunchKernelGGL((kern<8>), dim3(((C) + 63) / 64, rows), dim3(256), 0, st, __VA_ARGS__);       \
+  } while (0)
 }  // namespace
 
 using namespace dca::ops;
@@ -245,7 +253,7 @@ int dca_ops_bn_fwd(const void* x, const void* r, void* out, float* part, float* 
                      (int)M, C);
   hipLaunchKernelGGL(k_bn_finalize, dim3((C + 15) / 16), dim3(256), 0, st, (const float2*)part, nparts, (int)M, C,
                      rm, rv, (float2*)stats, eps, momentum);
-  hipLaunchKernelGGL(k_bn_apply, dim3((C + 63) / 64, nparts_rows(M)), dim3(256), 0, st, (const bf16_t*)x, (const bf16_t*)r,
+  BN_LAUNCH(k_bn_apply, C, nparts_rows(M), st, (const bf16_t*)x, (const bf16_t*)r,
                      (bf16_t*)out, (const float2*)stats, gamma, beta, M, C, relu, res_mode, (uint8_t*)nullptr,
                      (const float*)nullptr, (unsigned*)nullptr);
   OPCK(hipGetLastError());
@@ -267,7 +275,7 @@ int dca_ops_bn_fwd_parts(const void* x, const void* r, void* out, const float* p
   if (q) OPCK(hipMemsetAsync(amax_out, 0, sizeof(unsigned), st));
   hipLaunchKernelGGL(k_bn_finalize, dim3((C + 15) / 16), dim3(256), 0, st, (const float2*)part, nparts, (int)M, C,
                      rm, rv, (float2*)stats, eps, momentum);
-  hipLaunchKernelGGL(k_bn_apply, dim3((C + 63) / 64, nparts_rows(M)), dim3(256), 0, st, (const bf16_t*)x, (const bf16_t*)r,
+  BN_LAUNCH(k_bn_apply, C, nparts_rows(M), st, (const bf16_t*)x, (const bf16_t*)r,
                      (bf16_t*)out, (const float2*)stats, gamma, beta, M, C, relu, res_mode, (uint8_t*)q, amax_prev,
                      amax_out);
   OPCK(hipGetLastError());
@@ -281,12 +289,12 @@ int dca_ops_bn_bwd(const void* dy, const void* x, const void* r, const float* st
   REQUIRE(res_mode != 2 || (r != nullptr && dr != nullptr), "bn bwd: residual tensors missing");
   hipStream_t st = (hipStream_t)stream;
   const int nparts = (int)((M + BN_ROWS - 1) / BN_ROWS);
-  hipLaunchKernelGGL(k_bn_bwd_stats, dim3((C + 63) / 64, nparts), dim3(256), 0, st, (const bf16_t*)dy,
+  BN_LAUNCH(k_bn_bwd_stats, C, nparts, st, (const bf16_t*)dy,
                      (const bf16_t*)x, (const bf16_t*)r, (const float2*)stats, gamma, beta, (float2*)part, (int)M, C,
                      relu, res_mode);
   hipLaunchKernelGGL(k_bn_bwd_finalize, dim3((C + 15) / 16), dim3(256), 0, st, (const float2*)part, nparts, C,
                      dgamma, dbeta, (float2*)sums, accumulate);
-  hipLaunchKernelGGL(k_bn_bwd_apply, dim3((C + 63) / 64, nparts_rows(M)), dim3(256), 0, st, (const bf16_t*)dy, (const bf16_t*)x,
+  BN_LAUNCH(k_bn_bwd_apply, C, nparts_rows(M), st, (const bf16_t*)dy, (const bf16_t*)x,
                      (const bf16_t*)r, (const float2*)stats, gamma, beta, (const float2*)sums, (bf16_t*)dx,
                      (bf16_t*)dr, M, C, relu, res_mode);
   OPCK(hipGetLastError());

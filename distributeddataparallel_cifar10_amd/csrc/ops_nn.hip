@@ -128,6 +128,7 @@ __global__ void __launch_bounds__(256) k_col2im(const bf16_t* __restrict__ dcols
 // the batch mean: a single pass without cancellation trouble), then one finalize.
 // ---------------------------------------------------------------------------------------------------------
 constexpr int BN_ROWS = 256;  // rows per partial block (threads: 64 channel lanes x 4 row lanes)
+constexpr int BN_U = 4;        // rows per thread with their loads in flight together (apply / backward kernels)
 
 // grid (ceil(C/64), ceil(M/BN_ROWS)); part[blockIdx.y][C] = (sum, sumsq)
 __global__ void __launch_bounds__(256) k_bn_stats(const bf16_t* __restrict__ x, const float* __restrict__ shift,
@@ -215,14 +216,15 @@ __global__ void __launch_bounds__(256) k_bn_finalize(const float2* __restrict__ 
 // Optionally also emits an fp8 e4m3 copy of the output for an fp8 consumer GEMM, with DELAYED scaling: the scale
 // 448 / amax comes from the previous step's amax of this tensor (amax_prev), and this step's amax is recorded in
 // amax_out for the next step -- no extra pass over the activation, no host sync.
+template <int CL>
 __global__ void __launch_bounds__(256) k_bn_apply(const bf16_t* __restrict__ x, const bf16_t* __restrict__ r,
                                                   bf16_t* __restrict__ out, const float2* __restrict__ stats,
                                                   const float* __restrict__ gamma, const float* __restrict__ beta,
                                                   long M, int C, int relu, int res_mode, uint8_t* __restrict__ q,
                                                   const float* __restrict__ amax_prev, unsigned* __restrict__ amax_out) {
-  // grid (ceil(C/64), ceil(M/BN_ROWS)): 8 channel groups x 32 row lanes, z = x * sc + sh per channel
+  // grid (ceil(C/(8 CL)), ceil(M/BN_ROWS)): CL channel groups of 8 x 256/CL row lanes, z = x * sc + sh per channel
   __shared__ float red[256];
-  const int cgl = threadIdx.x & 7, rl = threadIdx.x >> 3, c0 = blockIdx.x * 64 + cgl * 8;
+  const int cgl = threadIdx.x % CL, rl = threadIdx.x / CL, c0 = blockIdx.x * (8 * CL) + cgl * 8;
   const long r0 = (long)blockIdx.y * BN_ROWS;
   float qs = 1.f, amax = 0.f;
   if (q) qs = *amax_prev > 0.f ? 448.f / *amax_prev : 1.f;
@@ -235,11 +237,22 @@ __global__ void __launch_bounds__(256) k_bn_apply(const bf16_t* __restrict__ x, 
       sh[j] = beta[c0 + j] - st.x * sc[j];
     }
     const long rend = M < r0 + BN_ROWS ? M : r0 + BN_ROWS;
-    for (long row = r0 + rl; row < rend; row += 32) {
+    for (long base = r0 + rl; base < rend; base += (256 / CL) * BN_U) {
+    uint4 X[BN_U], R[BN_U];
+#pragma unroll
+    for (int u = 0; u < BN_U; ++u) {  // all loads in flight first (clamped rows)
+      const long rw = base + (256 / CL) * u, o = (rw < rend ? rw : rend - 1) * C + c0;
+      X[u] = *(const uint4*)(x + o);
+      if (res_mode) R[u] = *(const uint4*)(r + o);
+    }
+#pragma unroll
+    for (int u = 0; u < BN_U; ++u) {
+      const long row = base + (256 / CL) * u;
+      if (row >= rend) break;
       const long o = row * C + c0;
       float v[8], rv[8];
-      unpack8(*(const uint4*)(x + o), v);
-      if (res_mode) unpack8(*(const uint4*)(r + o), rv);
+      unpack8(X[u], v);
+      if (res_mode) unpack8(R[u], rv);
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         float z = v[j] * sc[j] + sh[j];
@@ -268,6 +281,7 @@ __global__ void __launch_bounds__(256) k_bn_apply(const bf16_t* __restrict__ x, 
         *(uint2*)(q + o) = uint2{(unsigned)w[0], (unsigned)w[1]};
       }
     }
+    }
   }
   if (q) {
     red[threadIdx.x] = amax;
@@ -283,12 +297,13 @@ __global__ void __launch_bounds__(256) k_bn_apply(const bf16_t* __restrict__ x, 
 // dz = dy * act'(.) recomputed from x (and r); partial sums of dz and dz * xhat per channel.
 // grid (ceil(C/64), ceil(M/BN_ROWS)); 256 threads = 8 channel groups (8 channels, one 16-B load per tensor per
 // row) x 32 row lanes; all rows' loads of a thread are independent (issued back to back).
+template <int CL>
 __global__ void __launch_bounds__(256) k_bn_bwd_stats(const bf16_t* __restrict__ dy, const bf16_t* __restrict__ x,
                                                       const bf16_t* __restrict__ r, const float2* __restrict__ stats,
                                                       const float* __restrict__ gamma, const float* __restrict__ beta,
                                                       float2* __restrict__ part, int M, int C, int relu, int res_mode) {
-  __shared__ float2 red[32][64];
-  const int cgl = threadIdx.x & 7, rl = threadIdx.x >> 3, c0 = blockIdx.x * 64 + cgl * 8;
+  __shared__ float2 red[256 / CL][8 * CL];
+  const int cgl = threadIdx.x % CL, rl = threadIdx.x / CL, c0 = blockIdx.x * (8 * CL) + cgl * 8;
   const int r0 = blockIdx.y * BN_ROWS;
   float s[8], q[8], mu[8], is[8], ga[8], be[8];
 #pragma unroll
@@ -301,33 +316,46 @@ __global__ void __launch_bounds__(256) k_bn_bwd_stats(const bf16_t* __restrict__
     be[j] = beta[c];
   }
   if (c0 < C) {
-    for (int row = r0 + rl; row < min(M, r0 + BN_ROWS); row += 32) {
-      const long o = (long)row * C + c0;
-      float xv[8], dv[8], rv[8];
-      unpack8(*(const uint4*)(x + o), xv);
-      unpack8(*(const uint4*)(dy + o), dv);
-      if (res_mode == 2) unpack8(*(const uint4*)(r + o), rv);
+    const int rend = min(M, r0 + BN_ROWS);
+    // BN_U rows per thread in flight: every load issued (clamped rows, unconditional) before any is used
+    for (int base = r0 + rl; base < rend; base += (256 / CL) * BN_U) {
+      uint4 X[BN_U], D[BN_U], R[BN_U];
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const float xh = (xv[j] - mu[j]) * is[j];
-        float d = dv[j];
-        if (relu) {
-          float z = xh * ga[j] + be[j];
-          if (res_mode == 2) z += rv[j];
-          d = z > 0.f ? d : 0.f;
+      for (int u = 0; u < BN_U; ++u) {
+        const long o = (long)min(base + (256 / CL) * u, rend - 1) * C + c0;
+        X[u] = *(const uint4*)(x + o);
+        D[u] = *(const uint4*)(dy + o);
+        if (res_mode == 2) R[u] = *(const uint4*)(r + o);
+      }
+#pragma unroll
+      for (int u = 0; u < BN_U; ++u) {
+        if (base + (256 / CL) * u >= rend) break;
+        float xv[8], dv[8], rv[8];
+        unpack8(X[u], xv);
+        unpack8(D[u], dv);
+        if (res_mode == 2) unpack8(R[u], rv);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float xh = (xv[j] - mu[j]) * is[j];
+          float d = dv[j];
+          if (relu) {
+            float z = xh * ga[j] + be[j];
+            if (res_mode == 2) z += rv[j];
+            d = z > 0.f ? d : 0.f;
+          }
+          s[j] += d;
+          q[j] += d * xh;
         }
-        s[j] += d;
-        q[j] += d * xh;
       }
     }
   }
 #pragma unroll
   for (int j = 0; j < 8; ++j) red[rl][cgl * 8 + j] = float2{s[j], q[j]};
   __syncthreads();
-  const int c = blockIdx.x * 64 + threadIdx.x;
-  if (threadIdx.x < 64 && c < C) {
+  const int c = blockIdx.x * (8 * CL) + threadIdx.x;
+  if (threadIdx.x < 8 * CL && c < C) {
     float2 a = red[0][threadIdx.x];
-    for (int k = 1; k < 32; ++k) {
+    for (int k = 1; k < 256 / CL; ++k) {
       a.x += red[k][threadIdx.x].x;
       a.y += red[k][threadIdx.x].y;
     }
@@ -352,12 +380,13 @@ __global__ void __launch_bounds__(256) k_bn_bwd_finalize(const float2* __restric
 // dx = gamma * invstd * (dz - mean(dz) - xhat * mean(dz * xhat)); res_mode 2 also writes dr = dz.
 // grid (ceil(C/64), ceil(M/BN_ROWS)): 8 channel groups x 32 row lanes, per-channel coefficients folded once per
 // thread (dx = A*dz + B*x + D), one 16-B load / store per tensor per row.
+template <int CL>
 __global__ void __launch_bounds__(256) k_bn_bwd_apply(const bf16_t* __restrict__ dy, const bf16_t* __restrict__ x,
                                                       const bf16_t* __restrict__ r, const float2* __restrict__ stats,
                                                       const float* __restrict__ gamma, const float* __restrict__ beta,
                                                       const float2* __restrict__ sums, bf16_t* __restrict__ dx,
                                                       bf16_t* __restrict__ dr, long M, int C, int relu, int res_mode) {
-  const int cgl = threadIdx.x & 7, rl = threadIdx.x >> 3, c0 = blockIdx.x * 64 + cgl * 8;
+  const int cgl = threadIdx.x % CL, rl = threadIdx.x / CL, c0 = blockIdx.x * (8 * CL) + cgl * 8;
   if (c0 >= C) return;
   const long r0 = (long)blockIdx.y * BN_ROWS;
   const float inv_m = 1.f / (float)M;
@@ -375,25 +404,38 @@ __global__ void __launch_bounds__(256) k_bn_bwd_apply(const bf16_t* __restrict__
     cd[j] = -ca[j] * sm.x * inv_m - cb[j] * mu[j];
   }
   const long rend = M < r0 + BN_ROWS ? M : r0 + BN_ROWS;
-  for (long row = r0 + rl; row < rend; row += 32) {
-    const long o = row * C + c0;
-    float xv[8], d[8], rv[8];
-    unpack8(*(const uint4*)(x + o), xv);
-    unpack8(*(const uint4*)(dy + o), d);
-    if (res_mode == 2) unpack8(*(const uint4*)(r + o), rv);
+  for (long base = r0 + rl; base < rend; base += (256 / CL) * BN_U) {
+    uint4 X[BN_U], D[BN_U], R[BN_U];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      float dz = d[j];
-      if (relu) {
-        float z = (xv[j] - mu[j]) * is[j] * ga[j] + be[j];
-        if (res_mode == 2) z += rv[j];
-        dz = z > 0.f ? dz : 0.f;
-      }
-      rv[j] = dz;
-      d[j] = ca[j] * dz + cb[j] * xv[j] + cd[j];
+    for (int u = 0; u < BN_U; ++u) {  // all loads in flight first (clamped rows)
+      const long row = base + (256 / CL) * u, o = (row < rend ? row : rend - 1) * C + c0;
+      X[u] = *(const uint4*)(x + o);
+      D[u] = *(const uint4*)(dy + o);
+      if (res_mode == 2) R[u] = *(const uint4*)(r + o);
     }
-    *(uint4*)(dx + o) = pack8(d);
-    if (res_mode == 2) *(uint4*)(dr + o) = pack8(rv);
+#pragma unroll
+    for (int u = 0; u < BN_U; ++u) {
+      const long row = base + (256 / CL) * u;
+      if (row >= rend) break;
+      const long o = row * C + c0;
+      float xv[8], d[8], rv[8];
+      unpack8(X[u], xv);
+      unpack8(D[u], d);
+      if (res_mode == 2) unpack8(R[u], rv);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        float dz = d[j];
+        if (relu) {
+          float z = (xv[j] - mu[j]) * is[j] * ga[j] + be[j];
+          if (res_mode == 2) z += rv[j];
+          dz = z > 0.f ? dz : 0.f;
+        }
+        rv[j] = dz;
+        d[j] = ca[j] * dz + cb[j] * xv[j] + cd[j];
+      }
+      *(uint4*)(dx + o) = pack8(d);
+      if (res_mode == 2) *(uint4*)(dr + o) = pack8(rv);
+    }
   }
 }
 
