@@ -59,6 +59,12 @@ inline bool getenv_wgrad_single() {
 // glds single-buffer mode (32 KiB LDS: ~1.5x the resident workgroups) for short K.  Batch-256 census vs
 // double-buffered: K <= 576 0.78-0.91x time, K = 1152 0.93x, K = 1024-4608 0.97-1.23x.
 // DCA_OPS_GLDS_SINGLE = 0: never, 1: always, unset: K-tiles per split <= 9.
+// narrow (128 x 64) short-K GEMMs on the single-buffer glds kernel: 0.89-0.90x the register-staged time at
+// batch 256 (802816 x 64 x {64, 256}); DCA_OPS_GLDS_NARROW=0 turns it off
+inline bool getenv_glds_narrow() {
+  static const bool v = getenv_flag("DCA_OPS_GLDS_NARROW");
+  return v;
+}
 inline int getenv_glds_single() {
   static const int v = [] {
     const char* e = getenv("DCA_OPS_GLDS_SINGLE");
@@ -189,7 +195,7 @@ int dca_ops_gemm(const GemmArgs* a, void* stream) {
   // (measured, bench/gemm_bench.py: +18..100 % on plain NT GEMMs; bf16 implicit convs only when C % 64 == 0 (one
   // tap per K-tile: a wave-uniform decode); fp8 implicit convs always (the register-staged fp8
   // kernel needs 219 VGPRs: one wave per SIMD); short-K narrow tiles stay on the single-buffer register kernel)
-  const bool glds = getenv_glds_ok() && !g.ta && !g.tb && !(narrow && g.single) &&
+  const bool glds = getenv_glds_ok() && !g.ta && !g.tb && !(narrow && g.single && !getenv_glds_narrow()) &&
                     (g.conv == 1 ? (g.fp8 || (g.cC % 64 == 0 && getenv_glds_conv()))
                                  : (g.conv == 0 && (long)g.lda * esz % 16 == 0 && (long)g.K * esz % 16 == 0)) &&
                     (long)g.ldb * esz % 16 == 0 && ((uintptr_t)g.A & 15) == 0 && ((uintptr_t)g.B & 15) == 0;
