@@ -65,6 +65,22 @@ inline bool getenv_glds_narrow() {
   static const bool v = getenv_flag("DCA_OPS_GLDS_NARROW");
   return v;
 }
+inline int getenv_glds_waves() {  // 0: automatic; DCA_OPS_GLDS_WAVES = 4 or 8 forces it
+  static const int v = [] {
+    const char* e = getenv("DCA_OPS_GLDS_WAVES");
+    const int n = e ? atoi(e) : 0;
+    return n == 4 || n == 8 ? n : 0;
+  }();
+  return v;
+}
+inline int getenv_glds_stages() {
+  static const int v = [] {
+    const char* e = getenv("DCA_OPS_GLDS_STAGES");
+    const int n = e ? atoi(e) : 2;
+    return n < 2 ? 2 : (n > 4 ? 4 : n);
+  }();
+  return v;
+}
 inline int getenv_glds_single() {
   static const int v = [] {
     const char* e = getenv("DCA_OPS_GLDS_SINGLE");
@@ -137,14 +153,18 @@ int dca_ops_gemm(const GemmArgs* a, void* stream) {
       OPCK(hipFuncSetAttribute((const void*)k_wgrad<64, 128, 1>, hipFuncAttributeMaxDynamicSharedMemorySize, l01));
       OPCK(hipFuncSetAttribute((const void*)k_wgrad<128, 64, 4>, hipFuncAttributeMaxDynamicSharedMemorySize, l10));
       OPCK(hipFuncSetAttribute((const void*)k_wgrad<128, 128, 2>, hipFuncAttributeMaxDynamicSharedMemorySize, l11));
-      OPCK(hipFuncSetAttribute((const void*)k_gemm_glds<false, 128>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                               GemmTile<128>::LDS));
-      OPCK(hipFuncSetAttribute((const void*)k_gemm_glds<true, 128>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                               GemmTile<128>::LDS));
-      OPCK(hipFuncSetAttribute((const void*)k_gemm_glds<false, 64>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                               GemmTile<64>::LDS));
-      OPCK(hipFuncSetAttribute((const void*)k_gemm_glds<true, 64>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                               GemmTile<64>::LDS));
+#define GLDS_ATTR(F8, BNV, NWV)                                                                          \
+  OPCK(hipFuncSetAttribute((const void*)k_gemm_glds<F8, BNV, NWV>, hipFuncAttributeMaxDynamicSharedMemorySize, \
+                           4 * GemmTile<BNV>::BUF))
+      GLDS_ATTR(false, 128, 4);
+      GLDS_ATTR(true, 128, 4);
+      GLDS_ATTR(false, 64, 4);
+      GLDS_ATTR(true, 64, 4);
+      GLDS_ATTR(false, 128, 8);
+      GLDS_ATTR(true, 128, 8);
+      GLDS_ATTR(false, 64, 8);
+      GLDS_ATTR(true, 64, 8);
+#undef GLDS_ATTR
     }
     g_lds_set = true;
   }
@@ -202,14 +222,33 @@ int dca_ops_gemm(const GemmArgs* a, void* stream) {
   if (glds) {
     const int gs = getenv_glds_single();
     g.single = gs >= 0 ? gs : (g.k_per_split <= 9 * kt ? 1 : 0);
-    const int l64 = g.single ? GemmTile<64>::LDS_SINGLE : GemmTile<64>::LDS;
-    const int l128 = g.single ? GemmTile<128>::LDS_SINGLE : GemmTile<128>::LDS;
+    g.stages = g.single ? 1 : getenv_glds_stages();
+    const int l64b = g.single ? GemmTile<64>::LDS_SINGLE : g.stages * GemmTile<64>::BUF;
+    const int l128b = g.single ? GemmTile<128>::LDS_SINGLE : g.stages * GemmTile<128>::BUF;
+    // 8 waves (4 per SIMD at 2 workgroups per CU) for the double-buffered long-K loops: 0.92-0.95x time on the
+    // batch-256 long-K convs; the single-buffer short-K launches keep 4 (8 measured 1.13-1.41x there)
+    const int gw = getenv_glds_waves();
+    const bool w8 = gw ? gw == 8 : !g.single;
+    const dim3 blk(w8 ? 512 : 256);
+    // the epilogue's column-statistics combine uses (threads / (BN / 8)) x BN float2 of LDS
+    const int red64 = (w8 ? 512 : 256) / 8 * 64 * 8, red128 = (w8 ? 512 : 256) / 16 * 128 * 8;
+    const int l64 = std::max(l64b, red64), l128 = std::max(l128b, red128);
     if (narrow) {
-      if (g.fp8) hipLaunchKernelGGL((k_gemm_glds<true, 64>), grid, dim3(GT), l64, st, g);
-      else hipLaunchKernelGGL((k_gemm_glds<false, 64>), grid, dim3(GT), l64, st, g);
+      if (g.fp8) {
+        if (w8) hipLaunchKernelGGL((k_gemm_glds<true, 64, 8>), grid, blk, l64, st, g);
+        else hipLaunchKernelGGL((k_gemm_glds<true, 64, 4>), grid, blk, l64, st, g);
+      } else {
+        if (w8) hipLaunchKernelGGL((k_gemm_glds<false, 64, 8>), grid, blk, l64, st, g);
+        else hipLaunchKernelGGL((k_gemm_glds<false, 64, 4>), grid, blk, l64, st, g);
+      }
     } else {
-      if (g.fp8) hipLaunchKernelGGL((k_gemm_glds<true, 128>), grid, dim3(GT), l128, st, g);
-      else hipLaunchKernelGGL((k_gemm_glds<false, 128>), grid, dim3(GT), l128, st, g);
+      if (g.fp8) {
+        if (w8) hipLaunchKernelGGL((k_gemm_glds<true, 128, 8>), grid, blk, l128, st, g);
+        else hipLaunchKernelGGL((k_gemm_glds<true, 128, 4>), grid, blk, l128, st, g);
+      } else {
+        if (w8) hipLaunchKernelGGL((k_gemm_glds<false, 128, 8>), grid, blk, l128, st, g);
+        else hipLaunchKernelGGL((k_gemm_glds<false, 128, 4>), grid, blk, l128, st, g);
+      }
     }
   } else if (narrow) {
     const int lds = g.single ? GemmTile<64>::LDS_SINGLE : GemmTile<64>::LDS;

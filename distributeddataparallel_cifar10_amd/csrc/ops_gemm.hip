@@ -66,6 +66,7 @@ struct GemmArgs {
   // single = 1: one LDS operand buffer (2 barriers per K-tile) so short-K GEMMs run with half the LDS and
   // twice the workgroups per CU (set by the launcher when a split has <= 4 K-tiles)
   int single;
+  int stages;  // k_gemm_glds: LDS buffers in the K pipeline (2..4; tiles in flight = stages - 1), when !single
 };
 
 __device__ __forceinline__ float amax_scale(const unsigned* a) {
@@ -253,11 +254,17 @@ struct GemmTile {
 // K loop: register prefetch of tile k+1 during the MFMAs of tile k, written to the other LDS buffer after them.
 // (A two-tile-deep prefetch measured neutral to 20 % slower: 196 VGPRs = 1 wave per SIMD, bench/gemm_bench.py.)
 // Shared epilogue of the GEMM kernels (acc = this wave's 64 x BN_/2 fp32 fragments of the 128 x BN_ tile).
-template <int BN_>
-__device__ __forceinline__ void gemm_epilogue(const GemmArgs& g, f32x4 (&acc)[4][BN_ / 32], char* smem, int m0,
-                                              int n0, int tm, int ksplit) {
-  using T = GemmTile<BN_>;
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, wr = wave >> 1, wc = wave & 1;
+template <int BN_, int NW>
+struct WaveGrid {  // NW waves as 2 (rows of 64) x NW/2 (column slices) over the 128 x BN_ tile
+  static constexpr int WC = NW / 2, WCW = BN_ / WC, NF = WCW / 16, NT = NW * 64;
+  static_assert(NF >= 1, "bad wave grid");
+};
+
+template <int BN_, int NW = 4>
+__device__ __forceinline__ void gemm_epilogue(const GemmArgs& g, f32x4 (&acc)[4][WaveGrid<BN_, NW>::NF], char* smem,
+                                              int m0, int n0, int tm, int ksplit) {
+  using T = WaveGrid<BN_, NW>;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, wr = wave / T::WC, wc = wave % T::WC;
   // Epilogue.  Split-K partials go straight to the fp32 slab.  Otherwise the 128x128 fp32 tile is staged in
   // LDS (the K-loop buffers are free: 64 KiB exactly; 16-column groups XOR-swizzled by (row >> 2) & 3 so the
   // fragment writes of one instruction hit distinct banks), then written back row-contiguously, 16 B per lane,
@@ -281,7 +288,7 @@ __device__ __forceinline__ void gemm_epilogue(const GemmArgs& g, f32x4 (&acc)[4]
   float* ct = (float*)smem;
   auto cidx = [](int r, int c) { return r * BN_ + (c ^ (((r >> 2) & 3) << 4)); };
   const float alpha = gemm_alpha(g);
-  constexpr int CG = BN_ / 8, RL = GT / CG;  // column groups of 8, row lanes
+  constexpr int CG = BN_ / 8, RL = T::NT / CG;  // column groups of 8, row lanes
   const int cg = threadIdx.x % CG, col0 = n0 + cg * 8;
   float bias8[8], shift8[8], s1[8], s2[8];
 #pragma unroll
@@ -526,19 +533,21 @@ __device__ __forceinline__ void wait_vmcnt() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
 
-template <bool FP8, int BN_>
-__global__ void __launch_bounds__(GT) k_gemm_glds(GemmArgs g) {
+template <bool FP8, int BN_, int NW>
+__global__ void __launch_bounds__(NW * 64) k_gemm_glds(GemmArgs g) {
   using T = GemmTile<BN_>;
+  using Wg = WaveGrid<BN_, NW>;
+  constexpr int RA = GBM / NW, RB = BN_ / NW;  // A / B tile rows staged by each wave
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int ntm = (g.M + GBM - 1) / GBM, ntn = (g.N + BN_ - 1) / BN_;
   const int tile = xcd_remap(blockIdx.x, ntm * ntn);
   const int tm = tile / ntn, tn = tile % ntn;
   const int m0 = tm * GBM, n0 = tn * BN_;
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, wr = wave >> 1, wc = wave & 1;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, wr = wave / Wg::WC, wc = wave % Wg::WC;
   constexpr int ESZ = FP8 ? 1 : 2;
   constexpr int KT = GBK_BYTES / ESZ;
-  constexpr int NBI = BN_ / 32;      // B wave instructions (8 rows each) per tile
-  constexpr int NI = 4 + NBI;        // glds per thread per tile
+  constexpr int NAI = RA / 8, NBI = RB / 8;  // A / B wave instructions (8 rows each) per tile
+  constexpr int NI = NAI + NBI;              // glds per thread per tile
   const int ksplit = blockIdx.y;
   const int k_begin = ksplit * g.k_per_split;
   const int k_end = min(g.K, k_begin + g.k_per_split);
@@ -546,11 +555,11 @@ __global__ void __launch_bounds__(GT) k_gemm_glds(GemmArgs g) {
   const int lr = lane >> 3, lj = lane & 7;
 
   // per-lane rows: A row wave*32 + i*8 + lr, B row wave*(BN_/4) + i*8 + lr
-  const char* arow[4];
-  int nh[4], ih[4], iw[4];
+  const char* arow[NAI];
+  int nh[NAI], ih[NAI], iw[NAI];
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    int m = m0 + wave * 32 + i * 8 + lr;
+  for (int i = 0; i < NAI; ++i) {
+    int m = m0 + wave * RA + i * 8 + lr;
     m = m < g.M ? m : g.M - 1;
     arow[i] = (const char*)g.A + (size_t)m * g.lda * ESZ;
     if (g.conv == 1) {
@@ -563,7 +572,7 @@ __global__ void __launch_bounds__(GT) k_gemm_glds(GemmArgs g) {
   const char* brow[NBI];
 #pragma unroll
   for (int i = 0; i < NBI; ++i) {
-    int n = n0 + wave * (BN_ / 4) + i * 8 + lr;
+    int n = n0 + wave * RB + i * 8 + lr;
     n = n < g.N ? n : g.N - 1;
     brow[i] = (const char*)g.B + (size_t)n * g.ldb * ESZ;
   }
@@ -582,8 +591,8 @@ __global__ void __launch_bounds__(GT) k_gemm_glds(GemmArgs g) {
       tkw = tap - tkh * g.cKW;
     }
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int r = wave * 32 + i * 8 + lr;
+    for (int i = 0; i < NAI; ++i) {
+      const int r = wave * RA + i * 8 + lr;
       const int kb = kb0 + ((lj ^ ((r >> 1) & 7)) << 4);
       const void* src = g_gemm_zero16;
       if (g.conv == 1) {
@@ -604,32 +613,35 @@ __global__ void __launch_bounds__(GT) k_gemm_glds(GemmArgs g) {
       } else if (kb < kb_end) {
         src = arow[i] + kb;
       }
-      glds16(src, la + (wave * 32 + i * 8) * 128);
+      glds16(src, la + (wave * RA + i * 8) * 128);
     }
 #pragma unroll
     for (int i = 0; i < NBI; ++i) {
-      const int r = wave * (BN_ / 4) + i * 8 + lr;
+      const int r = wave * RB + i * 8 + lr;
       const int kb = kb0 + ((lj ^ ((r >> 1) & 7)) << 4);
       glds16(kb < kb_end ? (const void*)(brow[i] + kb) : (const void*)g_gemm_zero16,
-             lb + (wave * (BN_ / 4) + i * 8) * 128);
+             lb + (wave * RB + i * 8) * 128);
     }
   };
 
-  f32x4 acc[4][T::NF];
+  f32x4 acc[4][Wg::NF];
 #pragma unroll
   for (int m = 0; m < 4; ++m)
 #pragma unroll
-    for (int n = 0; n < T::NF; ++n) acc[m][n] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int n = 0; n < Wg::NF; ++n) acc[m][n] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  const bool single = g.single != 0;  // one buffer: tile k+1 is issued after tile k's closing barrier
-  if (nk > 0) issue(0, 0);
+  // S LDS buffers, S - 1 tiles in flight.  S = 1 (single): tile k is issued after tile k-1's closing barrier.
+  const int S = g.single ? 1 : (g.stages >= 2 && g.stages <= 4 ? g.stages : 2);
+  for (int t0 = 0; t0 < S - 1 && t0 < nk; ++t0) issue(t0, t0);
   for (int kt = 0; kt < nk; ++kt) {
-    const int buf = single ? 0 : kt & 1;
-    if (kt + 1 < nk && !single) {
-      issue(kt + 1, buf ^ 1);  // the buffer every wave finished reading before the previous closing barrier
-      wait_vmcnt<NI>();         // this thread's loads of tile kt have landed (tile kt+1's still in flight)
-    } else {
-      wait_vmcnt<0>();
+    const int buf = kt % S;
+    const int nt = kt + S - 1;
+    if (nt < nk) issue(nt, nt % S);  // into the buffer every wave finished reading before the last barrier
+    switch (min(nk - 1, nt) - kt) {   // this thread's loads of tile kt have landed (later tiles' in flight)
+      case 0: wait_vmcnt<0>(); break;
+      case 1: wait_vmcnt<NI>(); break;
+      case 2: wait_vmcnt<2 * NI>(); break;
+      default: wait_vmcnt<3 * NI>(); break;
     }
     __builtin_amdgcn_s_barrier();  // ... and every thread's
     asm volatile("" ::: "memory");
@@ -638,21 +650,21 @@ __global__ void __launch_bounds__(GT) k_gemm_glds(GemmArgs g) {
     if constexpr (!FP8) {
 #pragma unroll
       for (int s = 0; s < 2; ++s) {
-        s16x8 af[4], bfr[T::NF];
+        s16x8 af[4], bfr[Wg::NF];
 #pragma unroll
         for (int m = 0; m < 4; ++m)
           af[m] = *(const s16x8*)(la + lds_off(wr * 64 + m * 16 + (lane & 15), s * 4 + (lane >> 4)));
 #pragma unroll
-        for (int n = 0; n < T::NF; ++n)
-          bfr[n] = *(const s16x8*)(lb + lds_off(wc * T::WCW + n * 16 + (lane & 15), s * 4 + (lane >> 4)));
+        for (int n = 0; n < Wg::NF; ++n)
+          bfr[n] = *(const s16x8*)(lb + lds_off(wc * Wg::WCW + n * 16 + (lane & 15), s * 4 + (lane >> 4)));
 #pragma unroll
         for (int m = 0; m < 4; ++m)
 #pragma unroll
-          for (int n = 0; n < T::NF; ++n)
+          for (int n = 0; n < Wg::NF; ++n)
             acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[m], bfr[n], acc[m][n], 0, 0, 0);
       }
     } else {
-      i32x8 af[4], bfr[T::NF];
+      i32x8 af[4], bfr[Wg::NF];
 #pragma unroll
       for (int m = 0; m < 4; ++m) {
         const int row = wr * 64 + m * 16 + (lane & 15), c = 2 * (lane >> 4);
@@ -660,23 +672,22 @@ __global__ void __launch_bounds__(GT) k_gemm_glds(GemmArgs g) {
         af[m] = i32x8{(int)lo.x, (int)lo.y, (int)lo.z, (int)lo.w, (int)hi.x, (int)hi.y, (int)hi.z, (int)hi.w};
       }
 #pragma unroll
-      for (int n = 0; n < T::NF; ++n) {
-        const int row = wc * T::WCW + n * 16 + (lane & 15), c = 2 * (lane >> 4);
+      for (int n = 0; n < Wg::NF; ++n) {
+        const int row = wc * Wg::WCW + n * 16 + (lane & 15), c = 2 * (lane >> 4);
         const uint4 lo = *(const uint4*)(lb + lds_off(row, c)), hi = *(const uint4*)(lb + lds_off(row, c + 1));
         bfr[n] = i32x8{(int)lo.x, (int)lo.y, (int)lo.z, (int)lo.w, (int)hi.x, (int)hi.y, (int)hi.z, (int)hi.w};
       }
 #pragma unroll
       for (int m = 0; m < 4; ++m)
 #pragma unroll
-        for (int n = 0; n < T::NF; ++n)
+        for (int n = 0; n < Wg::NF; ++n)
           acc[m][n] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(af[m], bfr[n], acc[m][n], 0, 0, 0, 127, 0, 127);
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();  // every wave is done reading buf before it is refilled
     asm volatile("" ::: "memory");
-    if (single && kt + 1 < nk) issue(kt + 1, 0);
   }
-  gemm_epilogue<BN_>(g, acc, smem, m0, n0, tm, ksplit);
+  gemm_epilogue<BN_, NW>(g, acc, smem, m0, n0, tm, ksplit);
 }
 
 // Split-K combine: C = alpha * sum_s ws[s] (+bias) (+beta*C) (ReLU).  256 threads = 64 consecutive elements x 4

@@ -31,6 +31,7 @@ class GemmArgs(ctypes.Structure):
         ("cS", c_int), ("cP", c_int), ("cHo", c_int), ("cWo", c_int), ("col_stats", c_void_p),
         ("stats_shift", c_void_p), ("amax_a", c_void_p), ("amax_b", c_void_p),
         ("wperm_C", c_int), ("wperm_Cpad", c_int), ("wperm_T", c_int), ("single", c_int),
+        ("stages", c_int),
     ]
 
 
