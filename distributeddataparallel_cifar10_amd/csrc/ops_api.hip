@@ -65,6 +65,13 @@ inline bool getenv_glds_narrow() {
   static const bool v = getenv_flag("DCA_OPS_GLDS_NARROW");
   return v;
 }
+inline bool getenv_glds_conv_any() {  // experiment: glds (per-lane tap decode) for every implicit conv
+  static const bool v = [] {
+    const char* e = getenv("DCA_OPS_GLDS_CONV_ANY");
+    return e && e[0] == '1';
+  }();
+  return v;
+}
 inline int getenv_glds_waves() {  // 0: automatic; DCA_OPS_GLDS_WAVES = 4 or 8 forces it
   static const int v = [] {
     const char* e = getenv("DCA_OPS_GLDS_WAVES");
@@ -216,7 +223,7 @@ int dca_ops_gemm(const GemmArgs* a, void* stream) {
   // tap per K-tile: a wave-uniform decode); fp8 implicit convs always (the register-staged fp8
   // kernel needs 219 VGPRs: one wave per SIMD); short-K narrow tiles stay on the single-buffer register kernel)
   const bool glds = getenv_glds_ok() && !g.ta && !g.tb && !(narrow && g.single && !getenv_glds_narrow()) &&
-                    (g.conv == 1 ? (g.fp8 || (g.cC % 64 == 0 && getenv_glds_conv()))
+                    (g.conv == 1 ? (g.fp8 || (g.cC % 64 == 0 && getenv_glds_conv()) || getenv_glds_conv_any())
                                  : (g.conv == 0 && (long)g.lda * esz % 16 == 0 && (long)g.K * esz % 16 == 0)) &&
                     (long)g.ldb * esz % 16 == 0 && ((uintptr_t)g.A & 15) == 0 && ((uintptr_t)g.B & 15) == 0;
   if (glds) {
@@ -434,5 +441,13 @@ int dca_ops_pack_weights(const void* descs, int nd, int blocks_per_layer, unsign
 }
 
 int dca_ops_pack_desc_size() { return (int)sizeof(PackDesc); }
+
+int dca_ops_nchw_to_nhwc8(const float* x, void* y, int N, int C, long HW, void* stream) {
+  REQUIRE(C > 0 && C <= 8, "nchw_to_nhwc8: 1..8 channels");
+  hipLaunchKernelGGL(k_nchw_to_nhwc8, dim3(grid_for((long)N * HW)), dim3(256), 0, (hipStream_t)stream, x, (bf16_t*)y,
+                     N, C, HW);
+  OPCK(hipGetLastError());
+  return 0;
+}
 
 }  // extern "C"

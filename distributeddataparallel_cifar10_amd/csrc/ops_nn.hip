@@ -728,5 +728,19 @@ __global__ void __launch_bounds__(256) k_pack_fp8(const PackDesc* __restrict__ d
   }
 }
 
+// Network input: NCHW fp32 [N][C][HW] (C <= 8) -> NHWC bf16 [N][HW][8], channels C..7 zero (the 8-channel-padded
+// stem input of the implicit-GEMM stem).  One thread per pixel: C strided fp32 reads, one 16-B store.
+__global__ void __launch_bounds__(256) k_nchw_to_nhwc8(const float* __restrict__ x, bf16_t* __restrict__ y, int N,
+                                                       int C, long HW) {
+  const long total = (long)N * HW;
+  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < total; i += (long)gridDim.x * 256) {
+    const long n = i / HW, p = i - n * HW;
+    float v[8];
+#pragma unroll
+    for (int c = 0; c < 8; ++c) v[c] = c < C ? x[(n * C + c) * HW + p] : 0.f;
+    *(uint4*)(y + i * 8) = pack8(v);
+  }
+}
+
 }  // namespace ops
 }  // namespace dca

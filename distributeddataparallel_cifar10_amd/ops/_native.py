@@ -74,6 +74,7 @@ def _declare(lib):
     lib.dca_ops_fp8_alpha.argtypes = [c_void_p, c_void_p, c_float, c_void_p, c_void_p]
     lib.dca_ops_pack_weights.argtypes = [c_void_p, c_int, c_int, c_void_p, c_int, c_void_p]
     lib.dca_ops_pack_desc_size.restype = c_int
+    lib.dca_ops_nchw_to_nhwc8.argtypes = [c_void_p, c_void_p, c_int, c_int, c_long, c_void_p]
     return lib
 
 

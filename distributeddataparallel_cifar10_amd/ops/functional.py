@@ -259,6 +259,19 @@ class WeightPack:
                 "pack_weights")
 
 
+def nchw_to_nhwc8(x: torch.Tensor) -> torch.Tensor:
+    """Network input NCHW fp32 (C <= 8) -> NHWC bf16 with the channels zero-padded to 8, in one kernel (the
+    implicit-GEMM stem's operand).  The input needs no gradient."""
+    _dev_check(x)
+    if x.dtype != torch.float32 or x.dim() != 4 or x.shape[1] > 8:
+        raise ValueError("nchw_to_nhwc8: NCHW fp32 with at most 8 channels")
+    x = x.contiguous()
+    n, c, h, w = x.shape
+    y = torch.empty(n, h, w, 8, dtype=torch.bfloat16, device=x.device)
+    N.check(N.lib().dca_ops_nchw_to_nhwc8(N.ptr(x), N.ptr(y), n, c, h * w, N.stream(x.device)), "nchw_to_nhwc8")
+    return y
+
+
 def grad_sink(p: torch.Tensor):
     """(flat gradient view, ready callback) that FlatBucketDDP attaches to its parameters, or None.  A kernel
     that owns a parameter's whole gradient for the step writes (accumulates) it straight into the view and

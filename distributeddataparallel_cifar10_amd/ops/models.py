@@ -46,10 +46,13 @@ class OpsModel(nn.Module):
             h = x.permute(0, 2, 3, 1).to(torch.bfloat16).contiguous()  # NCHW fp32 -> NHWC bf16
             return self._netresdeep(h)
         # ResNet: the 3-channel input is zero-padded to 8 channels so the 7x7 stem is an implicit GEMM
-        h = x.permute(0, 2, 3, 1)
-        if h.shape[-1] % 8:
-            h = torch.nn.functional.pad(h, (0, 8 - h.shape[-1] % 8))
-        h = h.to(torch.bfloat16).contiguous()
+        if x.shape[1] <= 8 and x.dtype == torch.float32 and not x.requires_grad:
+            h = F.nchw_to_nhwc8(x)  # one kernel
+        else:
+            h = x.permute(0, 2, 3, 1)
+            if h.shape[-1] % 8:
+                h = torch.nn.functional.pad(h, (0, 8 - h.shape[-1] % 8))
+            h = h.to(torch.bfloat16).contiguous()
         if self._pack is None:
             convs = [m for m in self.module.modules() if isinstance(m, nn.Conv2d)]
             self._pack = F.WeightPack(convs, [c for c in convs if self._fp8_ok(c)])

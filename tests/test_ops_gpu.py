@@ -475,3 +475,11 @@ def test_conv_bn_act_fp8_implicit_3x3(gpu, s):
     assert _rel(y.float().permute(0, 3, 1, 2), z) < 0.08
     assert _rel(x.grad.float().permute(0, 3, 1, 2), xr.grad) < 0.2
     assert _rel(conv.weight.grad, rconv.weight.grad) < 0.2
+
+
+def test_nchw_to_nhwc8(gpu):
+    from distributeddataparallel_cifar10_amd.ops import functional as F
+    x = torch.randn(3, 3, 17, 19, device=gpu)
+    y = F.nchw_to_nhwc8(x)
+    ref = TF.pad(x.permute(0, 2, 3, 1), (0, 5)).to(torch.bfloat16)
+    assert y.shape == (3, 17, 19, 8) and torch.equal(y, ref)
