@@ -1,13 +1,21 @@
 set -o pipefail
 mkdir -p gpurun_out
-timeout -k 10 600 python -u -m pytest tests/test_ops_gpu.py -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/pytest_ops.log 2>&1 &&
-DCA_OPS_GLDS_CONV_ANY=1 timeout -k 10 600 python -u -m pytest tests/test_ops_gpu.py -m gpu -x -q --timeout 120 --timeout-method thread -k "conv or resnet" > gpurun_out/pytest_any.log 2>&1 &&
 timeout -k 10 300 python bench/r50_gemm_census.py --batch 256 > gpurun_out/census_a.log 2>&1 &&
-DCA_OPS_GLDS_CONV_ANY=1 timeout -k 10 300 python bench/r50_gemm_census.py --batch 256 > gpurun_out/census_b.log 2>&1 &&
-timeout -k 10 300 python bench/resnet50.py --steps 10 --warmup 3 > gpurun_out/r50.log 2>&1
+DCA_OPS_REG_SINGLE_NK=9 timeout -k 10 300 python bench/r50_gemm_census.py --batch 256 > gpurun_out/census_b.log 2>&1 &&
+DCA_OPS_REG_SINGLE_NK=100 timeout -k 10 300 python bench/r50_gemm_census.py --batch 256 > gpurun_out/census_c.log 2>&1
 rc=$?
-tail -1 gpurun_out/pytest_ops.log; tail -1 gpurun_out/pytest_any.log
-grep "392\|3211264" gpurun_out/census_a.log | cut -c1-120; grep "392\|3211264" gpurun_out/census_b.log | cut -c1-120
-tail -1 gpurun_out/census_a.log; tail -1 gpurun_out/census_b.log
-tail -1 gpurun_out/r50.log | cut -c60-140
+python3 - <<'PY'
+import json
+def load(p):
+    d={}
+    for l in open(p):
+        if l.startswith('{"kind"'):
+            r=json.loads(l); d[(r["kind"],r["M"],r["N"],r["K"])]=r["us"]
+        elif l.startswith('{"total'): d["total"]=json.loads(l)["total_gemm_us"]
+    return d
+a=load('gpurun_out/census_a.log'); b=load('gpurun_out/census_b.log'); c=load('gpurun_out/census_c.log')
+for k in sorted(a, key=lambda k: -a[k] if k!="total" else 0):
+    if k!="total" and (abs(b.get(k,0)/a[k]-1) > 0.05 or abs(c.get(k,0)/a[k]-1) > 0.05): print(k, a[k], round(b.get(k,0)/a[k],2), round(c.get(k,0)/a[k],2))
+print("total", a["total"], b["total"], c["total"])
+PY
 exit $rc

@@ -72,6 +72,13 @@ inline bool getenv_glds_conv_any() {  // experiment: glds (per-lane tap decode) 
   }();
   return v;
 }
+inline int getenv_reg_single_nk() {  // register-staged kernel: single-buffer up to this many K-tiles per split
+  static const int v = [] {
+    const char* e = getenv("DCA_OPS_REG_SINGLE_NK");
+    return e ? atoi(e) : 4;
+  }();
+  return v;
+}
 inline int getenv_glds_waves() {  // 0: automatic; DCA_OPS_GLDS_WAVES = 4 or 8 forces it
   static const int v = [] {
     const char* e = getenv("DCA_OPS_GLDS_WAVES");
@@ -216,7 +223,7 @@ int dca_ops_gemm(const GemmArgs* a, void* stream) {
   const int bn = narrow ? 64 : 128;
   const int tiles = ((g.M + GBM - 1) / GBM) * ((g.N + bn - 1) / bn);
   const dim3 grid(tiles, g.splits);
-  g.single = g.k_per_split <= 4 * kt ? 1 : 0;  // short K: one operand buffer, twice the workgroups per CU
+  g.single = g.k_per_split <= getenv_reg_single_nk() * kt ? 1 : 0;  // short K: one buffer, 2x workgroups per CU
   // K-contiguous operands with 16-B aligned rows: direct global -> LDS staging (k_gemm_glds)
   const int esz = g.fp8 ? 1 : 2;
   // (measured, bench/gemm_bench.py: +18..100 % on plain NT GEMMs; bf16 implicit convs only when C % 64 == 0 (one
