@@ -1,11 +1,8 @@
 set -o pipefail
 mkdir -p gpurun_out
-timeout -k 10 300 python bench/resnet50.py --steps 10 --warmup 3 > gpurun_out/r50_b256.log 2>&1 &&
-DCA_FP8_MIN_CIN=256 timeout -k 10 300 python bench/resnet50.py --steps 10 --warmup 3 --fp8 > gpurun_out/r50_fp8_256.log 2>&1 &&
-DCA_FP8_MIN_CIN=512 timeout -k 10 300 python bench/resnet50.py --steps 10 --warmup 3 --fp8 > gpurun_out/r50_fp8_512.log 2>&1 &&
-DCA_FP8_MIN_CIN=1024 timeout -k 10 300 python bench/resnet50.py --steps 10 --warmup 3 --fp8 > gpurun_out/r50_fp8_1024.log 2>&1 &&
-DCA_FP8_MIN_CIN=99999 timeout -k 10 300 python bench/resnet50.py --steps 10 --warmup 3 --fp8 > gpurun_out/r50_fp8_none.log 2>&1 &&
-timeout -k 10 300 python bench/resnet50.py --steps 10 --warmup 3 > gpurun_out/r50_b256_2.log 2>&1
+timeout -k 10 300 python bench/resnet50.py --steps 6 --warmup 2 --batch 512 > gpurun_out/r50_512.log 2>&1 &&
+timeout -k 10 300 python bench/resnet50.py --steps 8 --warmup 2 --batch 384 > gpurun_out/r50_384.log 2>&1 &&
+timeout -k 10 300 python bench/resnet50.py --steps 12 --warmup 3 --batch 128 > gpurun_out/r50_128.log 2>&1
 rc=$?
-for f in r50_b256 r50_fp8_256 r50_fp8_512 r50_fp8_1024 r50_fp8_none r50_b256_2; do echo -n "$f "; tail -1 gpurun_out/$f.log | cut -c60-110; done
+for f in r50_512 r50_384 r50_128; do echo -n "$f "; tail -1 gpurun_out/$f.log | cut -c60-160; done
 exit $rc

@@ -533,8 +533,8 @@ def conv_bn_act(x, conv: torch.nn.Conv2d, bn: torch.nn.BatchNorm2d, r=None, relu
     if conv.bias is not None or not bn.training:
         raise ValueError("conv_bn_act: conv without bias, BN in training mode")
     momentum = bn.momentum if bn.track_running_stats else 0.0
-    if bn.track_running_stats:
-        bn.num_batches_tracked.add_(1)
+    if bn.track_running_stats and not getattr(bn, "_dca_counted", False):
+        bn.num_batches_tracked.add_(1)  # (a model that batches these increments marks its BNs _dca_counted)
     sinks = None
     if direct_grads and torch.is_grad_enabled():
         sw, sg, sb = grad_sink(conv.weight), grad_sink(bn.weight), grad_sink(bn.bias)

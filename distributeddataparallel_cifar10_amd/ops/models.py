@@ -56,7 +56,13 @@ class OpsModel(nn.Module):
         if self._pack is None:
             convs = [m for m in self.module.modules() if isinstance(m, nn.Conv2d)]
             self._pack = F.WeightPack(convs, [c for c in convs if self._fp8_ok(c)])
+            self._bns = [m for m in self.module.modules()
+                         if isinstance(m, nn.BatchNorm2d) and m.track_running_stats]
+            for m in self._bns:
+                m._dca_counted = True
         self._pack.pack()  # every conv's bf16 / fp8 GEMM operands from this step's fp32 weights: one launch
+        if self.training and self._bns:  # every BN's num_batches_tracked += 1 in one launch (each BN runs once)
+            torch._foreach_add_([m.num_batches_tracked for m in self._bns], 1)
         return self._resnet(h)
 
     # reference model/resnet.py:15-22, 33-37

@@ -483,3 +483,17 @@ def test_nchw_to_nhwc8(gpu):
     y = F.nchw_to_nhwc8(x)
     ref = TF.pad(x.permute(0, 2, 3, 1), (0, 5)).to(torch.bfloat16)
     assert y.shape == (3, 17, 19, 8) and torch.equal(y, ref)
+
+
+def test_ops_resnet_counts_batches_once_per_forward(gpu):
+    """The batched num_batches_tracked increment: every BN counts exactly one batch per forward."""
+    from distributeddataparallel_cifar10_amd.models.resnet50 import ResNet
+    from distributeddataparallel_cifar10_amd.ops import OpsModel, cross_entropy
+    net = ResNet([1, 1, 1, 1], num_classes=10).to(gpu)
+    m = OpsModel(net)
+    x = torch.randn(2, 3, 64, 64, device=gpu)
+    y = torch.randint(0, 10, (2,), device=gpu)
+    for _ in range(3):
+        cross_entropy(m(x), y).backward()
+    counts = {int(b.num_batches_tracked) for b in net.modules() if isinstance(b, torch.nn.BatchNorm2d)}
+    assert counts == {3}, counts
