@@ -1,21 +1,10 @@
 set -o pipefail
 mkdir -p gpurun_out
-timeout -k 10 300 python bench/r50_gemm_census.py --batch 256 > gpurun_out/census_a.log 2>&1 &&
-DCA_OPS_REG_SINGLE_NK=9 timeout -k 10 300 python bench/r50_gemm_census.py --batch 256 > gpurun_out/census_b.log 2>&1 &&
-DCA_OPS_REG_SINGLE_NK=100 timeout -k 10 300 python bench/r50_gemm_census.py --batch 256 > gpurun_out/census_c.log 2>&1
+timeout -k 10 600 python -u -m pytest tests/test_ops_gpu.py -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/pytest_ops.log 2>&1 &&
+timeout -k 10 300 python bench/r50_gemm_census.py --batch 256 > gpurun_out/census256.log 2>&1 &&
+timeout -k 10 300 python bench/resnet50.py --steps 10 --warmup 3 > gpurun_out/r50.log 2>&1 &&
+timeout -k 10 300 python bench/resnet50.py --steps 10 --warmup 3 --fp8 > gpurun_out/r50_fp8.log 2>&1
 rc=$?
-python3 - <<'PY'
-import json
-def load(p):
-    d={}
-    for l in open(p):
-        if l.startswith('{"kind"'):
-            r=json.loads(l); d[(r["kind"],r["M"],r["N"],r["K"])]=r["us"]
-        elif l.startswith('{"total'): d["total"]=json.loads(l)["total_gemm_us"]
-    return d
-a=load('gpurun_out/census_a.log'); b=load('gpurun_out/census_b.log'); c=load('gpurun_out/census_c.log')
-for k in sorted(a, key=lambda k: -a[k] if k!="total" else 0):
-    if k!="total" and (abs(b.get(k,0)/a[k]-1) > 0.05 or abs(c.get(k,0)/a[k]-1) > 0.05): print(k, a[k], round(b.get(k,0)/a[k],2), round(c.get(k,0)/a[k],2))
-print("total", a["total"], b["total"], c["total"])
-PY
+tail -3 gpurun_out/pytest_ops.log; tail -1 gpurun_out/census256.log
+for f in r50 r50_fp8; do echo -n "$f "; tail -1 gpurun_out/$f.log | cut -c60-140; done
 exit $rc

@@ -144,13 +144,21 @@ int dca_ops_gemm(const GemmArgs* a, void* stream) {
   if (g.conv) {
     REQUIRE(g.cC > 0 && (g.fp8 ? (g.conv == 1 && g.cC % 16 == 0) : g.cC % 8 == 0),
             "gemm: implicit conv needs C % 8 == 0 (bf16) or an fp8 forward with C % 16 == 0");
-    REQUIRE(g.cHo == (g.cH + 2 * g.cP - g.cKH) / g.cS + 1 && g.cWo == (g.cW + 2 * g.cP - g.cKW) / g.cS + 1,
+    // a sub-pixel input-gradient class (orow_S > 0) relies on the gather's bounds checks for its one-sided
+    // padding, so its output grid is only bounded; otherwise the usual convolution arithmetic
+    REQUIRE(g.orow_S > 0 ? (g.conv == 1 && g.cHo >= 1 && g.cWo >= 1 && g.cHo <= g.cH && g.cWo <= g.cW)
+                         : (g.cHo == (g.cH + 2 * g.cP - g.cKH) / g.cS + 1 && g.cWo == (g.cW + 2 * g.cP - g.cKW) / g.cS + 1),
             "gemm: inconsistent conv geometry");
     const long pix = (long)g.cN * g.cHo * g.cWo, kc = (long)g.cKH * g.cKW * g.cC;
     REQUIRE(g.conv != 1 || (g.M == pix && g.K == kc && !g.ta), "gemm: conv A shape mismatch");
     REQUIRE(g.conv != 2 || (g.K == pix && g.N == kc && !g.tb), "gemm: conv B shape mismatch");
   }
   REQUIRE(!g.col_stats || (g.stats_shift && g.splits <= 1), "gemm: column stats need a shift and no split-K");
+  REQUIRE(g.orow_S <= 0 || (g.splits <= 1 && g.wperm_T <= 0 && g.orow_Ho > 0 && g.orow_Wo > 0 &&
+                            (long)g.orow_Ho * g.orow_Wo > 0 && g.M % ((long)g.orow_Ho * g.orow_Wo) == 0 &&
+                            g.orow_S * (g.orow_Ho - 1) + g.orow_ph < g.orow_H &&
+                            g.orow_S * (g.orow_Wo - 1) + g.orow_pw < g.orow_W),
+          "gemm: output row remap needs the epilogue path and a consistent pixel grid");
   if (!g_lds_set) {
     OPCK(hipFuncSetAttribute((const void*)k_gemm<false, 128>, hipFuncAttributeMaxDynamicSharedMemorySize,
                              GemmTile<128>::LDS));
@@ -456,5 +464,14 @@ int dca_ops_nchw_to_nhwc8(const float* x, void* y, int N, int C, long HW, void* 
   OPCK(hipGetLastError());
   return 0;
 }
+
+int dca_ops_pack_gather(const void* descs, int nd, int blocks, void* stream) {
+  REQUIRE(nd > 0 && blocks > 0, "pack_gather: empty");
+  hipLaunchKernelGGL(k_pack_gather, dim3(blocks, nd), dim3(256), 0, (hipStream_t)stream, (const GatherDesc*)descs);
+  OPCK(hipGetLastError());
+  return 0;
+}
+
+int dca_ops_gather_desc_size() { return (int)sizeof(GatherDesc); }
 
 }  // extern "C"

@@ -67,6 +67,10 @@ struct GemmArgs {
   // twice the workgroups per CU (set by the launcher when a split has <= 4 K-tiles)
   int single;
   int stages;  // k_gemm_glds: LDS buffers in the K pipeline (2..4; tiles in flight = stages - 1), when !single
+  // output row remap (orow_S > 0): GEMM row m = pixel (n, i, j) of an orow_Ho x orow_Wo grid is stored at row
+  // (n * orow_H + orow_S * i + orow_ph) * orow_W + orow_S * j + orow_pw of C -- the sub-pixel (parity class)
+  // input gradients of a strided convolution written straight into dX
+  int orow_S, orow_ph, orow_pw, orow_H, orow_W, orow_Ho, orow_Wo;
 };
 
 __device__ __forceinline__ float amax_scale(const unsigned* a) {
@@ -317,7 +321,12 @@ __device__ __forceinline__ void gemm_epilogue(const GemmArgs& g, f32x4 (&acc)[4]
       const f32x4 a0 = *(const f32x4*)(ct + cidx(lr, cg * 8)), a1 = *(const f32x4*)(ct + cidx(lr, cg * 8 + 4));
       const float av[8] = {a0[0], a0[1], a0[2], a0[3], a1[0], a1[1], a1[2], a1[3]};
       float v[8];
-      const size_t o = (size_t)row * g.ldc + col0;
+      size_t orow = (size_t)row;
+      if (g.orow_S > 0) {
+        const int j = row % g.orow_Wo, t = row / g.orow_Wo, i = t % g.orow_Ho, n = t / g.orow_Ho;
+        orow = ((size_t)n * g.orow_H + g.orow_S * i + g.orow_ph) * g.orow_W + g.orow_S * j + g.orow_pw;
+      }
+      const size_t o = orow * g.ldc + col0;
       float old[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
       if (g.beta != 0.f) {  // accumulate into the existing output: one 16-B (two for fp32) load per row chunk
         if (full8 && g.out_bf16) {

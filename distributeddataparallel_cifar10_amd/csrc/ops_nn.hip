@@ -742,5 +742,18 @@ __global__ void __launch_bounds__(256) k_nchw_to_nhwc8(const float* __restrict__
   }
 }
 
+// Gathered bf16 copies of fp32 weights: out[i] = bf16(w[idx[i]]) -- the per-parity-class input-gradient matrices
+// of strided convolutions (index tables built once on the host).  grid (blocks, descriptors).
+struct GatherDesc {
+  const float* w;
+  const int* idx;
+  bf16_t* out;
+  long n;
+};
+__global__ void __launch_bounds__(256) k_pack_gather(const GatherDesc* __restrict__ descs) {
+  const GatherDesc d = descs[blockIdx.y];
+  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < d.n; i += (long)gridDim.x * 256) d.out[i] = f2bf_rne(d.w[d.idx[i]]);
+}
+
 }  // namespace ops
 }  // namespace dca

@@ -31,7 +31,8 @@ class GemmArgs(ctypes.Structure):
         ("cS", c_int), ("cP", c_int), ("cHo", c_int), ("cWo", c_int), ("col_stats", c_void_p),
         ("stats_shift", c_void_p), ("amax_a", c_void_p), ("amax_b", c_void_p),
         ("wperm_C", c_int), ("wperm_Cpad", c_int), ("wperm_T", c_int), ("single", c_int),
-        ("stages", c_int),
+        ("stages", c_int), ("orow_S", c_int), ("orow_ph", c_int), ("orow_pw", c_int), ("orow_H", c_int),
+        ("orow_W", c_int), ("orow_Ho", c_int), ("orow_Wo", c_int),
     ]
 
 
@@ -43,6 +44,11 @@ class PackDesc(ctypes.Structure):
     """Mirror of csrc/ops_nn.hip::PackDesc (one layer of the per-step weight pack)."""
     _fields_ = [("w", c_void_p), ("fwd", c_void_p), ("dgrad", c_void_p), ("q8", c_void_p), ("amax", c_void_p),
                 ("co", c_int), ("ci", c_int), ("ci_pad", c_int), ("kh", c_int), ("kw", c_int), ("kp", c_int)]
+
+
+class GatherDesc(ctypes.Structure):
+    """Mirror of csrc/ops_nn.hip::GatherDesc."""
+    _fields_ = [("w", c_void_p), ("idx", c_void_p), ("out", c_void_p), ("n", c_long)]
 
 
 class PoolGeom(ctypes.Structure):
@@ -74,6 +80,8 @@ def _declare(lib):
     lib.dca_ops_fp8_alpha.argtypes = [c_void_p, c_void_p, c_float, c_void_p, c_void_p]
     lib.dca_ops_pack_weights.argtypes = [c_void_p, c_int, c_int, c_void_p, c_int, c_void_p]
     lib.dca_ops_pack_desc_size.restype = c_int
+    lib.dca_ops_pack_gather.argtypes = [c_void_p, c_int, c_int, c_void_p]
+    lib.dca_ops_gather_desc_size.restype = c_int
     lib.dca_ops_nchw_to_nhwc8.argtypes = [c_void_p, c_void_p, c_int, c_int, c_long, c_void_p]
     return lib
 
@@ -97,8 +105,9 @@ def lib():
         handle = _declare(ctypes.CDLL(path, mode=ctypes.RTLD_GLOBAL))
         if handle.dca_ops_abi_version() != ABI_VERSION:
             raise RuntimeError(f"{path}: ABI {handle.dca_ops_abi_version()} != {ABI_VERSION} (stale build?)")
-        if handle.dca_ops_pack_desc_size() != ctypes.sizeof(PackDesc):
-            raise RuntimeError(f"{path}: PackDesc layout mismatch")
+        if handle.dca_ops_pack_desc_size() != ctypes.sizeof(PackDesc) or \
+                handle.dca_ops_gather_desc_size() != ctypes.sizeof(GatherDesc):
+            raise RuntimeError(f"{path}: descriptor layout mismatch")
         _lib = handle
         return _lib
 

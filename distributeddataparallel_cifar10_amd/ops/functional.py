@@ -32,7 +32,7 @@ def gemm(a: torch.Tensor, b: torch.Tensor, *, ta: bool = False, tb: bool = False
          beta: float = 0.0, splits: int = 0, alpha_dev: Optional[torch.Tensor] = None, conv: int = 0,
          geom=None, col_stats: Optional[torch.Tensor] = None, stats_shift: Optional[torch.Tensor] = None,
          mnk=None, amax_a: Optional[torch.Tensor] = None, amax_b: Optional[torch.Tensor] = None,
-         wperm=None) -> torch.Tensor:
+         wperm=None, orow=None) -> torch.Tensor:
     """C[M,N] = alpha * A(m,k) B(n,k) (+bias) (+beta*out) (ReLU).
 
     A is [M,K] (ta=False) or [K,M] (ta=True); B is [N,K] (tb=False) or [K,N] (tb=True).  bf16 operands, or
@@ -41,7 +41,9 @@ def gemm(a: torch.Tensor, b: torch.Tensor, *, ta: bool = False, tb: bool = False
     the GEMM shape).  col_stats [ceil(M/128), N, 2] fp32 receives per-tile BN partial sums of the output.
     amax_a / amax_b: fp8 per-tensor amax bits (int32 [1]) of the operands, folded into alpha on the device.
     wperm = (C, Cpad, T): weight-gradient output written straight into torch's [M, C, KH, KW] fp32 layout
-    (``out``), GEMM column n = tap * Cpad + c; padded channels dropped."""
+    (``out``), GEMM column n = tap * Cpad + c; padded channels dropped.
+    orow = (S, ph, pw, H, W, Ho, Wo): row m = pixel (n, i, j) of an Ho x Wo grid goes to row
+    (n H + S i + ph) W + S j + pw of ``out`` ([N H W, N_gemm]): a strided conv's sub-pixel input gradient."""
     _dev_check(a, b, bias, out)
     fp8 = a.dtype == torch.uint8
     if fp8 != (b.dtype == torch.uint8) or (not fp8 and (a.dtype != torch.bfloat16 or b.dtype != torch.bfloat16)):
@@ -59,6 +61,10 @@ def gemm(a: torch.Tensor, b: torch.Tensor, *, ta: bool = False, tb: bool = False
         if out is None or out.dtype != torch.float32 or not out.is_contiguous() \
                 or out.numel() != M * wperm[0] * wperm[2]:
             raise ValueError("gemm: weight-layout output must be contiguous fp32 [M, C, KH, KW]")
+    elif orow is not None:
+        if out is None or out.dim() != 2 or out.shape[1] != Nn or not out.is_contiguous() \
+                or out.shape[0] != M // (orow[5] * orow[6]) * orow[3] * orow[4]:
+            raise ValueError("gemm: remapped output must be contiguous [N*H*W, N_gemm]")
     else:
         if out is None:
             out = torch.empty(M, Nn, dtype=out_dtype, device=a.device)
@@ -67,7 +73,7 @@ def gemm(a: torch.Tensor, b: torch.Tensor, *, ta: bool = False, tb: bool = False
     if bias is not None and (bias.dtype != torch.float32 or bias.numel() != Nn):
         raise ValueError("gemm: bias must be fp32 [N]")
     tiles = math.ceil(M / 128) * math.ceil(Nn / 128)
-    if col_stats is not None:
+    if col_stats is not None or orow is not None:
         splits = 1
     if splits <= 0:
         splits = 1
@@ -89,6 +95,9 @@ def gemm(a: torch.Tensor, b: torch.Tensor, *, ta: bool = False, tb: bool = False
                       amax_b=amax_b.data_ptr() if amax_b is not None else None)
     if wperm is not None:
         args.wperm_C, args.wperm_Cpad, args.wperm_T = (int(v) for v in wperm)
+    if orow is not None:
+        (args.orow_S, args.orow_ph, args.orow_pw, args.orow_H, args.orow_W, args.orow_Ho,
+         args.orow_Wo) = (int(v) for v in orow)
     if conv:
         for f in ("N", "H", "W", "C", "KH", "KW", "Ho", "Wo"):
             setattr(args, "c" + f, getattr(geom, f))
@@ -223,8 +232,12 @@ class WeightPack:
             kp = kh * kw * ci_pad
             e = dict(ci_pad=ci_pad, kp=kp, fwd=torch.empty(co, kp, dtype=torch.bfloat16, device=dev), dgrad=None,
                      q8=None, amax=None)
-            if c.stride[0] == 1 and ci_pad == ci and co % 8 == 0 and (kh > 1 or c.padding[0] == 0):
+            if ci_pad == ci and co % 8 == 0 and ((c.stride[0] == 1 and (kh > 1 or c.padding[0] == 0))
+                                                 or (c.stride[0] == 2 and kh == 1 and c.padding[0] == 0)):
                 e["dgrad"] = torch.empty(ci, kh * kw * co, dtype=torch.bfloat16, device=dev)
+            e["classes"] = None
+            if c.stride == (2, 2) and kh > 1 and kh == kw and ci_pad == ci and co % 8 == 0:
+                e["classes"] = self._parity_classes(c, dev)
             if id(c) in fp8_ids:
                 e["q8"] = torch.empty(co, kp, dtype=torch.uint8, device=dev)
                 e["amax"] = self.amax[j:j + 1]
@@ -233,6 +246,39 @@ class WeightPack:
         self.n_fp8 = n_fp8
         self._key = None
         self._descs = None
+        self._gkey = None
+        self._n_gather = 0
+
+    @staticmethod
+    def _parity_classes(c, dev):
+        """Sub-pixel decomposition of a stride-2 conv's input gradient: input pixels of parity (ph, pw) receive
+        dY only through the taps kh with (ph + pad - kh) even, from dY row i + (ph + pad - kh) / 2.  Each class
+        is a stride-1 implicit conv over dY (taps ordered by that offset, pad = -min offset) with the matrix
+        [Cin][(a_h KWc + a_w) Cout + co] = w[co][ci][kh_a][kw_a]; returns [(ph, pw, KHc, KWc, pad, out, idx)]."""
+        import numpy as np
+        co, ci, k, _ = c.weight.shape
+        p = c.padding[0]
+
+        def taps(par):
+            t = sorted(((par + p - kk) // 2, kk) for kk in range(k) if (par + p - kk) % 2 == 0)
+            return [kk for _, kk in t], -t[0][0]
+
+        out = []
+        for ph in (0, 1):
+            for pw in (0, 1):
+                (kh_l, pad_h), (kw_l, pad_w) = taps(ph), taps(pw)
+                if pad_h != pad_w:
+                    return None
+                o_, c_, ah, aw = np.meshgrid(np.arange(co), np.arange(ci), np.arange(len(kh_l)), np.arange(len(kw_l)),
+                                             indexing="ij")
+                src = ((o_ * ci + c_) * k + np.asarray(kh_l)[ah]) * k + np.asarray(kw_l)[aw]  # w[co][ci][kh][kw]
+                col = (ah * len(kw_l) + aw) * co + o_
+                idx = np.empty((ci, len(kh_l) * len(kw_l) * co), dtype=np.int32)
+                idx[c_, col] = src
+                out.append((ph, pw, len(kh_l), len(kw_l), pad_h,
+                            torch.empty(idx.shape, dtype=torch.bfloat16, device=dev),
+                            torch.from_numpy(idx.reshape(-1)).to(dev)))
+        return out
 
     def get(self, conv):
         return self.entries.get(id(conv))
@@ -257,6 +303,19 @@ class WeightPack:
         N.check(N.lib().dca_ops_pack_weights(N.ptr(self._descs), len(self.convs), self.BLOCKS_PER_LAYER,
                                              N.ptr(self.amax), self.n_fp8, N.stream(self.amax.device)),
                 "pack_weights")
+        if key != self._gkey:
+            gl = [(c, cl) for c in self.convs for cl in (self.entries[id(c)]["classes"] or [])]
+            self._n_gather = len(gl)
+            if gl:
+                arr = (N.GatherDesc * len(gl))()
+                for i, (c, cl) in enumerate(gl):
+                    arr[i] = N.GatherDesc(w=c.weight.data_ptr(), idx=cl[6].data_ptr(), out=cl[5].data_ptr(),
+                                          n=cl[5].numel())
+                self._gdescs = torch.frombuffer(bytearray(bytes(arr)), dtype=torch.uint8).to(self.amax.device)
+            self._gkey = key
+        if self._n_gather:
+            N.check(N.lib().dca_ops_pack_gather(N.ptr(self._gdescs), self._n_gather, 64, N.stream(self.amax.device)),
+                    "pack_gather")
 
 
 def nchw_to_nhwc8(x: torch.Tensor) -> torch.Tensor:
@@ -415,6 +474,23 @@ def _conv_bwd(dy, st, need_x: bool, need_w: bool, sink=None, x_join: Optional[Gr
                 wd = st.get("w_master").flip(2, 3).permute(1, 2, 3, 0).reshape(ci, -1).to(torch.bfloat16).contiguous()
             dx = gemm(dyb.view(g.N, g.Ho, g.Wo, co), wd, conv=1, geom=gd, mnk=(g.N * g.H * g.W, ci, gd.K),
                       out_dtype=torch.bfloat16, out=dst2, beta=beta).view(g.N, g.H, g.W, g.C)
+        elif (packed is not None and g.stride == 2 and g.H % 2 == 0 and g.W % 2 == 0 and g.C == ci
+              and (packed.get("classes") or (kh == 1 and g.pad == 0 and packed["dgrad"] is not None))):
+            # sub-pixel decomposition: each parity class of input pixels is a stride-1 implicit conv over dY whose
+            # GEMM epilogue writes straight into its rows of dX (no dY.W^T column matrix, no col2im)
+            classes = packed["classes"] or [(0, 0, 1, 1, 0, packed["dgrad"], None)]
+            if acc is None:
+                dx = (torch.empty if len(classes) == 4 else torch.zeros)(g.N, g.H, g.W, g.C, dtype=torch.bfloat16,
+                                                                          device=dy.device)
+            else:
+                dx = acc
+            dy4 = dyb.view(g.N, g.Ho, g.Wo, co)
+            for ph, pw, nkh, nkw, pad_c, wc, _ in classes:
+                ho_c, wo_c = (g.H - ph + 1) // 2, (g.W - pw + 1) // 2
+                gc = N.ConvGeom(N=g.N, H=g.Ho, W=g.Wo, C=co, KH=nkh, KW=nkw, stride=1, pad=pad_c, Ho=ho_c, Wo=wo_c,
+                                K=nkh * nkw * co, Kp=nkh * nkw * co)
+                gemm(dy4, wc, conv=1, geom=gc, mnk=(g.N * ho_c * wo_c, ci, gc.K), out=dx.view(-1, ci), beta=beta,
+                     orow=(2, ph, pw, g.H, g.W, ho_c, wo_c))
         else:
             wm = st["wm"]
             dcols = gemm(dyb, wm, tb=True, out_dtype=torch.bfloat16)  # [M, Kp] = dY . Wm

@@ -497,3 +497,39 @@ def test_ops_resnet_counts_batches_once_per_forward(gpu):
         cross_entropy(m(x), y).backward()
     counts = {int(b.num_batches_tracked) for b in net.modules() if isinstance(b, torch.nn.BatchNorm2d)}
     assert counts == {3}, counts
+
+
+@pytest.mark.parametrize("k,p", [(3, 1), (1, 0)])
+def test_strided_conv_subpixel_input_grad(gpu, k, p):
+    """Stride-2 conv input gradient by parity classes (implicit stride-1 convs over dY, GEMM epilogue rows
+    remapped into dX) with the packed class matrices, vs torch fp32; and accumulating into a GradJoin buffer."""
+    from distributeddataparallel_cifar10_amd.ops import conv_bn_act
+    from distributeddataparallel_cifar10_amd.ops import functional as F
+    g = torch.Generator(device=gpu).manual_seed(21 + k)
+    n, h, ci, co = 2, 14, 64, 128
+    conv = torch.nn.Conv2d(ci, co, k, stride=2, padding=p, bias=False).to(gpu)
+    bn = torch.nn.BatchNorm2d(co).to(gpu)
+    rconv, rbn = torch.nn.Conv2d(ci, co, k, stride=2, padding=p, bias=False).to(gpu), torch.nn.BatchNorm2d(co).to(gpu)
+    rconv.load_state_dict(conv.state_dict())
+    rbn.load_state_dict(bn.state_dict())
+    pack = F.WeightPack([conv])
+    pack.pack()
+    e = pack.get(conv)
+    assert (e["classes"] is not None) == (k > 1) and (k > 1 or e["dgrad"] is not None)
+    x = _bf(torch.randn(n, h, h, ci, device=gpu, generator=g)).requires_grad_()
+    y = conv_bn_act(x, conv, bn, relu=True, packed=e)
+    dy = _bf(torch.randn(y.shape, device=gpu, generator=g))
+    y.backward(dy)
+    xr = x.detach().float().permute(0, 3, 1, 2).requires_grad_()
+    with torch.no_grad():
+        rconv.weight.copy_(_bf(rconv.weight).float())
+    torch.relu(rbn(rconv(xr))).backward(dy.float().permute(0, 3, 1, 2))
+    assert _rel(x.grad.float().permute(0, 3, 1, 2), xr.grad) < 3e-2
+    # accumulate mode: a GradJoin whose buffer already holds another consumer's gradient
+    join = F.GradJoin(2)
+    seed = _bf(torch.randn(n, h, h, ci, device=gpu, generator=g))
+    join.contribute(seed.clone())
+    x2 = x.detach().clone().requires_grad_()
+    y2 = conv_bn_act(x2, conv, bn, relu=True, packed=e, x_join=join)
+    y2.backward(dy)
+    assert _rel(x2.grad.float(), seed.float() + x.grad.float()) < 2e-2
