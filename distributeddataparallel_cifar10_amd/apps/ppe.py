@@ -11,7 +11,8 @@ workflow runs on MI355X:
   ``detection_collate`` makes ``(images, bboxes[N,5] = (batch_idx, x1, y1, x2, y2), labels[N,3], paths)``.
 * ``ResNet101ROI``: the ResNet-101 trunk (``models/resnet50.py``) + ROI-align over the stride-16 features
   (bilinear ``grid_sample``, 4x4 bins) + a 3-way multi-label head.  This is the ``model(data, bboxes)`` contract
-  of ``ppe_main_ddp.py:146``.
+  of ``ppe_main_ddp.py:146``.  On GPU every conv / BN / pool / fc runs on the ops layer's HIP kernels
+  (``OpsModel.begin/stem/blocks/head``); ``engine="torch"`` keeps the stock torch modules.
 * ``train`` (``:128-182``): SGD(1e-3, momentum 0.9) via ``FlatSGD``, BCE-with-logits, progress print every 100
   iterations, ``model-ep{E}.pth`` every 5 epochs (rank 0), validation loss per epoch, loss-curve PNG.
 * ``eval_model`` / ``compute_map`` / ``plot_graph`` (``:186-231``): per-class AP (area under the interpolated
@@ -142,8 +143,12 @@ def preprocess_img(x: torch.Tensor) -> torch.Tensor:
 class ResNet101ROI(nn.Module):
     """ResNet-101 trunk to stride 16 (layer1-3) + ROI-align of every box + layer4 + multi-label head."""
 
-    def __init__(self, num_classes: int = 3, bins: int = 4, layers: Sequence[int] = (3, 4, 23, 3)):
+    def __init__(self, num_classes: int = 3, bins: int = 4, layers: Sequence[int] = (3, 4, 23, 3),
+                 engine: str = "auto"):
         super().__init__()
+        if engine not in ("auto", "ops", "torch"):
+            raise ValueError(f"engine {engine!r}: auto | ops | torch")
+        self.engine = engine  # auto: the ops layer's HIP kernels on GPU, torch modules on CPU
         r = ResNet(list(layers), num_classes=1000, zero_init_residual=False)  # (1,1,1,1) for tests
         self.stem = nn.Sequential(r.conv1, r.bn1, r.relu, r.maxpool)
         self.layer1, self.layer2, self.layer3, self.layer4 = r.layer1, r.layer2, r.layer3, r.layer4
@@ -164,9 +169,29 @@ class ResNet101ROI(nn.Module):
         return F.grid_sample(feat[bi], grid, mode="bilinear", padding_mode="border", align_corners=False)
 
     def forward(self, x: torch.Tensor, boxes: torch.Tensor) -> torch.Tensor:
+        if x.is_cuda and self.engine != "torch":
+            return self._forward_ops(x, boxes)
+        if self.engine == "ops":
+            raise RuntimeError("ResNet101ROI(engine='ops') needs a GPU input")
         f = self.layer3(self.layer2(self.layer1(self.stem(x))))          # stride 16
         r = self.layer4(self.roi_align(f, boxes.to(f.dtype), 16.0))     # [N,2048,2,2]
         return self.fc(torch.flatten(F.adaptive_avg_pool2d(r, 1), 1))
+
+    def _forward_ops(self, x: torch.Tensor, boxes: torch.Tensor) -> torch.Tensor:
+        """The same network on the ops layer's HIP kernels (implicit-GEMM MFMA convs with the BN statistics in
+        the epilogue, fused BN + ReLU + residual, pools, fc) over NHWC bf16 activations.  Only the ROI gather
+        (bilinear ``grid_sample`` of a few boxes per image) stays in torch.  Training-mode BN trains; eval mode
+        is the inference path (running statistics, under no_grad)."""
+        ops = self.__dict__.get("_ops")
+        if ops is None:  # kept out of the module tree: OpsModel wraps this module (no state_dict cycle)
+            from ..ops import OpsModel
+            ops = self.__dict__["_ops"] = OpsModel(self)
+        h = ops.begin(x)
+        h = ops.stem(h, self.stem[0], self.stem[1])
+        h = ops.blocks(h, [*self.layer1, *self.layer2, *self.layer3])             # stride 16, NHWC bf16
+        r = self.roi_align(h.permute(0, 3, 1, 2).float(), boxes.float(), 16.0)  # [N,1024,bins,bins] fp32
+        h = ops.blocks(r.permute(0, 2, 3, 1).to(torch.bfloat16).contiguous(), self.layer4)
+        return ops.head(h, self.fc)
 
 
 def freeze_backbone(model: nn.Module) -> None:
@@ -176,8 +201,8 @@ def freeze_backbone(model: nn.Module) -> None:
 
 
 def build_model(load_model: Optional[str] = None, num_classes: int = 3,
-                layers: Sequence[int] = (3, 4, 23, 3)) -> nn.Module:
-    m = ResNet101ROI(num_classes, layers=layers)
+                layers: Sequence[int] = (3, 4, 23, 3), engine: str = "auto") -> nn.Module:
+    m = ResNet101ROI(num_classes, layers=layers, engine=engine)
     if load_model and os.path.exists(load_model):
         sd = torch.load(load_model, map_location="cpu", weights_only=True)
         sd = {k: v for k, v in sd.items() if not (k.startswith("fc.") and v.shape[0] != num_classes)}

@@ -125,7 +125,7 @@ using namespace dca::ops;
 extern "C" {
 
 const char* dca_ops_last_error() { return g_err.c_str(); }
-int dca_ops_abi_version() { return 5; }
+int dca_ops_abi_version() { return 6; }
 
 // Must match ops/_native.py::GemmArgs.
 int dca_ops_gemm(const GemmArgs* a, void* stream) {
@@ -345,6 +345,21 @@ int dca_ops_bn_fwd_parts(const void* x, const void* r, void* out, const float* p
   BN_LAUNCH(k_bn_apply, C, nparts_rows(M), st, (const bf16_t*)x, (const bf16_t*)r,
                      (bf16_t*)out, (const float2*)stats, gamma, beta, M, C, relu, res_mode, (uint8_t*)q, amax_prev,
                      amax_out);
+  OPCK(hipGetLastError());
+  return 0;
+}
+
+// BatchNorm in eval mode (inference) fused with ReLU / residual: normalises with the running statistics.
+// stats: [C] float2 scratch (mean, invstd).  No running-stat update.
+int dca_ops_bn_eval(const void* x, const void* r, void* out, float* stats, const float* gamma, const float* beta,
+                    const float* rm, const float* rv, long M, int C, float eps, int relu, int res_mode, void* stream) {
+  REQUIRE(C % 8 == 0, "bn: C must be a multiple of 8");
+  REQUIRE(res_mode == 0 || r != nullptr, "bn: residual missing");
+  hipStream_t st = (hipStream_t)stream;
+  hipLaunchKernelGGL(k_bn_eval_stats, dim3((C + 255) / 256), dim3(256), 0, st, rm, rv, (float2*)stats, C, eps);
+  BN_LAUNCH(k_bn_apply, C, nparts_rows(M), st, (const bf16_t*)x, (const bf16_t*)r,
+                     (bf16_t*)out, (const float2*)stats, gamma, beta, M, C, relu, res_mode, (uint8_t*)nullptr,
+                     (const float*)nullptr, (unsigned*)nullptr);
   OPCK(hipGetLastError());
   return 0;
 }

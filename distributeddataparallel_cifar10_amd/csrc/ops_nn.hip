@@ -212,6 +212,15 @@ __global__ void __launch_bounds__(256) k_bn_finalize(const float2* __restrict__ 
 }
 
 
+// Inference (BatchNorm2d in eval mode): the running statistics are the normalisation statistics.
+// stats[c] = (running_mean, rsqrt(running_var + eps)); grid ceil(C/256), 256 threads.
+__global__ void __launch_bounds__(256) k_bn_eval_stats(const float* __restrict__ running_mean,
+                                                       const float* __restrict__ running_var,
+                                                       float2* __restrict__ stats, int C, float eps) {
+  const int c = blockIdx.x * 256 + threadIdx.x;
+  if (c < C) stats[c] = float2{running_mean[c], rsqrtf(running_var[c] + eps)};
+}
+
 // out = fused(x); vectorised by 8 channels (C % 8 == 0)
 // Optionally also emits an fp8 e4m3 copy of the output for an fp8 consumer GEMM, with DELAYED scaling: the scale
 // 448 / amax comes from the previous step's amax of this tensor (amax_prev), and this step's amax is recorded in

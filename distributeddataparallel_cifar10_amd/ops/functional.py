@@ -597,7 +597,8 @@ class _ConvBNAct(torch.autograd.Function):
 def conv_bn_act(x, conv: torch.nn.Conv2d, bn: torch.nn.BatchNorm2d, r=None, relu=True, fp8=False, res_mode=None,
                 fp8_state: Optional[Fp8Delayed] = None, emit: Optional[Fp8Delayed] = None, packed=None,
                 direct_grads: bool = False, x_join: Optional[GradJoin] = None, r_join: Optional[GradJoin] = None):
-    """Training-mode act(bn(conv(x))) for NHWC bf16 x, conv without bias; with a residual r: res_mode 2 (default,
+    """act(bn(conv(x))) for NHWC bf16 x, conv without bias (BN in eval mode: inference under no_grad, running
+    statistics); with a residual r: res_mode 2 (default,
     ResNet: act(bn + r)) or 1 (NetResDeep: act(bn) + r).  fp8: forward GEMM in fp8 e4m3 (fp8_state: this conv's
     delayed-scaling input state); emit: also produce the fp8 copy of the output that the consumer of ``emit`` reads.
     packed: the conv's WeightPack entry.  direct_grads: the conv weight and BN affine parameters are used once
@@ -606,8 +607,13 @@ def conv_bn_act(x, conv: torch.nn.Conv2d, bn: torch.nn.BatchNorm2d, r=None, relu
     inside the producing kernels instead of by an autograd add."""
     if res_mode is None:
         res_mode = 2 if r is not None else 0
-    if conv.bias is not None or not bn.training:
-        raise ValueError("conv_bn_act: conv without bias, BN in training mode")
+    if conv.bias is not None:
+        raise ValueError("conv_bn_act: conv without bias")
+    if not bn.training:  # inference: running statistics, no autograd
+        _check_inference(conv.weight)
+        with torch.no_grad():
+            y, _ = _conv_fwd(x, conv.weight, None, conv.stride[0], conv.padding[0], False, False, packed=packed)
+            return _bn_eval(y, r, bn, relu, res_mode)
     momentum = bn.momentum if bn.track_running_stats else 0.0
     if bn.track_running_stats and not getattr(bn, "_dca_counted", False):
         bn.num_batches_tracked.add_(1)  # (a model that batches these increments marks its BNs _dca_counted)
@@ -676,15 +682,42 @@ def _bn_backward(dy, x, r, gamma, beta, stats, relu, res_mode, dgamma_out=None, 
     return dx, dr, dgamma, dbeta
 
 
+def _check_inference(p: torch.Tensor) -> None:
+    if torch.is_grad_enabled() and p.requires_grad:
+        raise RuntimeError("ops layer: eval-mode BatchNorm is the inference path; run it under torch.no_grad() "
+                           "(training-mode BN for gradients)")
+
+
+def _bn_eval(x, r, bn: torch.nn.BatchNorm2d, relu, res_mode):
+    """Eval-mode BatchNorm2d (normalised with the running statistics) + ReLU / residual over NHWC bf16 x, the
+    same k_bn_apply pass as training with the statistics taken from the running buffers (torch BatchNorm2d eval
+    semantics; reference model/resnet.py:28 in ``model.eval()``)."""
+    if not bn.track_running_stats or bn.running_mean is None:
+        raise NotImplementedError("ops eval BatchNorm needs running statistics")
+    x = x.contiguous()
+    C = x.shape[-1]
+    M = x.numel() // C
+    r = r.contiguous() if r is not None else None
+    out = torch.empty_like(x)
+    stats = torch.empty(C, 2, dtype=torch.float32, device=x.device)
+    N.check(N.lib().dca_ops_bn_eval(N.ptr(x), N.ptr(r), N.ptr(out), N.ptr(stats), N.ptr(bn.weight), N.ptr(bn.bias),
+                                    N.ptr(bn.running_mean), N.ptr(bn.running_var), M, C, float(bn.eps), int(relu),
+                                    int(res_mode), N.stream(x.device)), "bn_eval")
+    return out
+
+
 def batch_norm_act(x, bn: torch.nn.BatchNorm2d, r=None, relu=True, res_mode=0):
-    """Training-mode BatchNorm2d `bn` over NHWC x (running stats updated in place; num_batches_tracked += 1)."""
+    """BatchNorm2d `bn` over NHWC x.  Training mode: batch statistics, running stats updated in place,
+    num_batches_tracked += 1.  Eval mode: running statistics (inference, under no_grad)."""
     if res_mode and r is None:
         raise ValueError("batch_norm_act: residual mode needs r")
-    momentum = bn.momentum if bn.training and bn.track_running_stats else 0.0
-    if bn.training and bn.track_running_stats:
+    if not bn.training:  # inference: running statistics, no autograd
+        _check_inference(bn.weight)
+        with torch.no_grad():
+            return _bn_eval(x, r if res_mode else None, bn, relu, res_mode)
+    momentum = bn.momentum if bn.track_running_stats else 0.0
+    if bn.track_running_stats:
         bn.num_batches_tracked.add_(1)
-    if not bn.training:
-        raise NotImplementedError("batch_norm_act implements training mode (eval uses torch)")
     return _BatchNormAct.apply(x, r if res_mode else None, bn.weight, bn.bias, bn.running_mean, bn.running_var,
                                bn.eps, momentum, relu, res_mode)
 

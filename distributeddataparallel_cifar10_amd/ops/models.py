@@ -45,7 +45,14 @@ class OpsModel(nn.Module):
         if self.kind == "netresdeep":
             h = x.permute(0, 2, 3, 1).to(torch.bfloat16).contiguous()  # NCHW fp32 -> NHWC bf16
             return self._netresdeep(h)
-        # ResNet: the 3-channel input is zero-padded to 8 channels so the 7x7 stem is an implicit GEMM
+        return self._resnet(self.begin(x))
+
+    def begin(self, x: torch.Tensor) -> torch.Tensor:
+        """Per-step entry of a ResNet-family forward: NCHW fp32 input -> NHWC bf16 (the 3-channel input
+        zero-padded to 8 channels so the 7x7 stem is an implicit GEMM), every conv's GEMM operands packed from
+        this step's fp32 weights (one launch), every BN's num_batches_tracked += 1 (one launch, training only).
+        Models that compose the stages themselves (``apps/ppe.py``'s ROI head) call this, then ``stem`` /
+        ``blocks`` / ``head``."""
         if x.shape[1] <= 8 and x.dtype == torch.float32 and not x.requires_grad:
             h = F.nchw_to_nhwc8(x)  # one kernel
         else:
@@ -61,9 +68,9 @@ class OpsModel(nn.Module):
             for m in self._bns:
                 m._dca_counted = True
         self._pack.pack()  # every conv's bf16 / fp8 GEMM operands from this step's fp32 weights: one launch
-        if self.training and self._bns:  # every BN's num_batches_tracked += 1 in one launch (each BN runs once)
+        if self.training and self.module.training and self._bns:  # each BN runs once per step: one launch
             torch._foreach_add_([m.num_batches_tracked for m in self._bns], 1)
-        return self._resnet(h)
+        return h
 
     # reference model/resnet.py:15-22, 33-37
     def _netresdeep(self, h):
@@ -108,11 +115,14 @@ class OpsModel(nn.Module):
                              emit=self._state(consumer) if consumer is not None else None,
                              packed=self._pack.get(conv), direct_grads=True, x_join=x_join, r_join=r_join)
 
-    def _resnet(self, h):
-        m = self.module
-        h = self._conv_bn(h, m.conv1, m.bn1)
-        h = F.max_pool2d(h, 3, 2, 1)
-        blocks = [b for stage in (m.layer1, m.layer2, m.layer3, m.layer4) for b in stage]
+    def stem(self, h, conv, bn):
+        """7x7/2 conv -> BN + ReLU -> 3x3/2 max pool (torchvision ResNet stem)."""
+        h = self._conv_bn(h, conv, bn)
+        return F.max_pool2d(h, 3, 2, 1)
+
+    def blocks(self, h, blocks):
+        """Bottleneck blocks in sequence over NHWC bf16 ``h``."""
+        blocks = list(blocks)
         for i, b in enumerate(blocks):
             nxt = blocks[i + 1].conv1 if i + 1 < len(blocks) else None
             # the block input feeds conv1 and the identity / downsample path: one shared gradient buffer
@@ -125,5 +135,15 @@ class OpsModel(nn.Module):
             out = self._conv_bn(out, b.conv2, b.bn2, consumer=b.conv3)
             h = self._conv_bn(out, b.conv3, b.bn3, relu=True, r=idt, consumer=nxt,
                               r_join=join if b.downsample is None else None)  # relu(bn3(conv3) + identity)
+        return h
+
+    def head(self, h, fc):
+        """Global average pool -> fc (fp32 logits)."""
         feat = F.global_avg_pool(h)
-        return F.linear(feat.to(torch.bfloat16), m.fc.weight, m.fc.bias, out_dtype=torch.float32, fp8=self.fp8)
+        return F.linear(feat.to(torch.bfloat16), fc.weight, fc.bias, out_dtype=torch.float32, fp8=self.fp8)
+
+    def _resnet(self, h):
+        m = self.module
+        h = self.stem(h, m.conv1, m.bn1)
+        h = self.blocks(h, [b for stage in (m.layer1, m.layer2, m.layer3, m.layer4) for b in stage])
+        return self.head(h, m.fc)

@@ -221,6 +221,36 @@ def test_ops_resnet_step(gpu, fp8):
     assert not bad, bad
 
 
+@pytest.mark.parametrize("kind", ["resnet", "netresdeep"])
+def test_ops_eval_inference(gpu, kind):
+    """Eval-mode forward (inference: BN normalised with the running statistics, k_bn_eval_stats + k_bn_apply)
+    on the ops path vs stock fp32 PyTorch in eval mode, with non-trivial running statistics; running buffers
+    and num_batches_tracked untouched; the eval path refuses to run under autograd."""
+    import copy
+    from distributeddataparallel_cifar10_amd.models.netresdeep import NetResDeep
+    from distributeddataparallel_cifar10_amd.models.resnet50 import ResNet
+    from distributeddataparallel_cifar10_amd.ops import OpsModel
+    torch.manual_seed(0)
+    net = (ResNet([1, 1, 1, 1], num_classes=10, zero_init_residual=False) if kind == "resnet" else NetResDeep()).to(gpu)
+    for mod in net.modules():
+        if isinstance(mod, torch.nn.BatchNorm2d):
+            mod.running_mean.uniform_(-0.2, 0.2)
+            mod.running_var.uniform_(0.5, 2.0)
+            mod.weight.data.uniform_(0.5, 1.5)
+            mod.bias.data.uniform_(-0.2, 0.2)
+    ref = copy.deepcopy(net).eval()
+    ops = OpsModel(net).eval()
+    x = torch.randn(8, 3, 96 if kind == "resnet" else 32, 96 if kind == "resnet" else 32, device=gpu)
+    bufs = [b.clone() for b in net.buffers()]
+    with torch.no_grad():
+        y, yref = ops(x), ref(x)
+    assert y.dtype == torch.float32 and y.shape == yref.shape
+    assert _rel(y, yref) < 3e-2, _rel(y, yref)
+    assert all(torch.equal(a, b) for a, b in zip(bufs, net.buffers()))
+    with pytest.raises(RuntimeError, match="no_grad"):
+        ops(x)
+
+
 @pytest.mark.parametrize("fp8", [False, True])
 def test_ops_resnet_trains(gpu, fp8):
     """20 SGD steps on one fixed batch through the ops path (FlatBucketDDP + HIP SGD with momentum) fit it."""

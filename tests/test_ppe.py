@@ -149,3 +149,49 @@ def test_ppe_train_on_gpu(tmp_path):
     assert np.isfinite(tl) and np.isfinite(vl)
     mAP, *aps = ppe.eval_model(model, dl, str(tmp_path), ["rc", "nc", "ma"], dev)
     assert 0.0 <= mAP <= 1.0
+
+
+def _rel(a, b):
+    a, b = a.double(), b.double()
+    return ((a - b).norm() / b.norm().clamp_min(1e-30)).item()
+
+
+@pytest.mark.gpu
+def test_ppe_roi_ops_matches_torch():
+    """ResNet101ROI on the ops layer's HIP kernels (the GPU default) vs the same weights on stock fp32 torch
+    (engine='torch'): training-mode logits, loss and parameter gradients; then eval-mode (inference BN with the
+    running statistics) logits.  Gradient bar: within 2x stock bf16 autocast's own error (+0.02)."""
+    import copy
+    from distributeddataparallel_cifar10_amd.runtime import native  # noqa: F401
+    dev = torch.device("cuda", 0)
+    torch.manual_seed(0)
+    m = ppe.build_model(None, 3, layers=(1, 1, 1, 1)).to(dev)
+    ref = copy.deepcopy(m)
+    ref.engine = "torch"
+    amp = copy.deepcopy(ref)
+    ds = ppe.SyntheticPPE(4, seed=0)
+    imgs, boxes, labels, _ = ds.detection_collate([ds[i] for i in range(4)])
+    x = ppe.preprocess_img(imgs.to(dev).float())
+    b, l = boxes.to(dev).float(), labels.to(dev).float()
+    out = m(x, b)
+    oref = ref(x, b)
+    assert out.dtype == torch.float32 and out.shape == oref.shape
+    assert _rel(out.detach(), oref.detach()) < 5e-2, _rel(out.detach(), oref.detach())
+    loss = torch.nn.functional.binary_cross_entropy_with_logits(out, l)
+    lref = torch.nn.functional.binary_cross_entropy_with_logits(oref, l)
+    loss.backward()
+    lref.backward()
+    with torch.autocast("cuda", dtype=torch.bfloat16):  # stock bf16's own error on the same step sets the bar
+        lamp = torch.nn.functional.binary_cross_entropy_with_logits(amp(x, b).float(), l)
+    lamp.backward()
+    assert abs(loss.item() - lref.item()) < 2e-2 * max(1.0, abs(lref.item()))
+    for (n, p), (_, q), (_, r) in zip(m.named_parameters(), ref.named_parameters(), amp.named_parameters()):
+        assert p.grad is not None, n
+        assert _rel(p.grad, q.grad) <= 2 * _rel(r.grad, q.grad) + 0.02, (n, _rel(p.grad, q.grad), _rel(r.grad, q.grad))
+    for a, c in zip(m.buffers(), ref.buffers()):  # BN running stats / counters updated alike
+        assert torch.allclose(a.double(), c.double(), rtol=3e-2, atol=3e-2)
+    m.eval()
+    ref.eval()
+    with torch.no_grad():
+        e, eref = m(x, b), ref(x, b)
+    assert _rel(e, eref) < 5e-2, _rel(e, eref)
