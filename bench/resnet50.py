@@ -118,11 +118,12 @@ def main() -> int:
         print(json.dumps({"metric": metric, "value": round(v, 1), "mode": "inference" if a.infer else "training",
                           "unit": "images/sec", "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
                           "ms_per_step": round(1e3 * dt / a.steps, 3), "higher_is_better": True, "scaling": "weak",
-                          "dtype": a.dtype, "data": "synthetic", "loss": float(loss),
+                          "dtype": a.dtype, "data": "synthetic", "loss": float(loss.detach()),
                           "config": {"model": "ResNet-50", "per_rank_batch": a.batch, "image": a.image,
-                                     "parallelism": f"dp{world}", "optimizer": "SGD(0.1, momentum 0.9)" +
+                                     "parallelism": f"dp{world}",
+                                     "optimizer": None if a.infer else "SGD(0.1, momentum 0.9)" +
                                      (", per-bucket updates overlapped with the backward" if a.overlap_sgd else ""),
-                                     "path": ("FlatBucketDDP + ops HIP kernels" + (" (fp8 fwd GEMMs)" if a.fp8 else " (bf16)")
+                                     "path": (("eval-mode forward, ops HIP kernels" if a.infer else "FlatBucketDDP + ops HIP kernels") + (" (fp8 fwd GEMMs)" if a.fp8 else " (bf16)")
                                               + (", step replayed as a HIP graph" if a.graph else ""))
                                      if a.path == "ops" else "FlatBucketDDP + stock conv (MIOpen), bf16 autocast"}}),
               flush=True)
