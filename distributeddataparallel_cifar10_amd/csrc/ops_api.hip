@@ -383,20 +383,36 @@ int dca_ops_bn_bwd(const void* dy, const void* x, const void* r, const float* st
   return 0;
 }
 
+// 32-bit pool indexing when every element offset of the input and output (plus one grid stride of slack for the
+// loop counter) stays below 2^31
+inline bool pool_idx32(const PoolGeom& g) {
+  const long in = (long)g.N * g.H * g.W * g.C, out = (long)g.N * g.Ho * g.Wo * g.C;
+  return std::max(in, out) + 8192L * 256 < (1L << 31);
+}
+
 int dca_ops_maxpool_fwd(const void* x, void* y, void* arg, const PoolGeom* geom, void* stream) {
   const PoolGeom g = *geom;
   REQUIRE(g.K * g.K <= 255 && g.K > 0 && g.S > 0, "maxpool: bad window");
-  hipLaunchKernelGGL(k_maxpool_fwd, dim3(grid_for((long)g.N * g.Ho * g.Wo * g.C / ((g.C & 7) == 0 ? 8 : 1))), dim3(256), 0,
-                     (hipStream_t)stream,
-                     (const bf16_t*)x, (bf16_t*)y, (uint8_t*)arg, g);
+  const dim3 grid(grid_for((long)g.N * g.Ho * g.Wo * g.C / ((g.C & 7) == 0 ? 8 : 1)));
+  if (pool_idx32(g))
+    hipLaunchKernelGGL(k_maxpool_fwd<unsigned>, grid, dim3(256), 0, (hipStream_t)stream,
+                       (const bf16_t*)x, (bf16_t*)y, (uint8_t*)arg, g);
+  else
+    hipLaunchKernelGGL(k_maxpool_fwd<long>, grid, dim3(256), 0, (hipStream_t)stream,
+                       (const bf16_t*)x, (bf16_t*)y, (uint8_t*)arg, g);
   OPCK(hipGetLastError());
   return 0;
 }
 
 int dca_ops_maxpool_bwd(const void* dy, const void* arg, void* dx, const PoolGeom* geom, void* stream) {
   const PoolGeom g = *geom;
-  hipLaunchKernelGGL(k_maxpool_bwd, dim3(grid_for((long)g.N * g.H * g.W * g.C / ((g.C & 7) == 0 ? 8 : 1))), dim3(256), 0, (hipStream_t)stream,
-                     (const bf16_t*)dy, (const uint8_t*)arg, (bf16_t*)dx, g);
+  const dim3 grid(grid_for((long)g.N * g.H * g.W * g.C / ((g.C & 7) == 0 ? 8 : 1)));
+  if (pool_idx32(g))
+    hipLaunchKernelGGL(k_maxpool_bwd<unsigned>, grid, dim3(256), 0, (hipStream_t)stream,
+                       (const bf16_t*)dy, (const uint8_t*)arg, (bf16_t*)dx, g);
+  else
+    hipLaunchKernelGGL(k_maxpool_bwd<long>, grid, dim3(256), 0, (hipStream_t)stream,
+                       (const bf16_t*)dy, (const uint8_t*)arg, (bf16_t*)dx, g);
   OPCK(hipGetLastError());
   return 0;
 }

@@ -456,15 +456,18 @@ struct PoolGeom {
 };
 
 // C % 8 == 0: one thread per output pixel and 8 channels (16-B loads, 8-B argmax stores); else per element
+// IT: index type.  unsigned (32-bit) when every element offset of x and y fits -- the per-thread index decode is
+// then 32-bit division instead of the 64-bit division sequence, which made the ResNet-50 pools ALU-bound.
+template <typename IT>
 __global__ void __launch_bounds__(256) k_maxpool_fwd(const bf16_t* __restrict__ x, bf16_t* __restrict__ y,
                                                      uint8_t* __restrict__ arg, PoolGeom g) {
   const int vec = (g.C & 7) == 0 ? 8 : 1;
-  const int cgs = g.C / vec;
-  const long total = (long)g.N * g.Ho * g.Wo * cgs;
-  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < total; i += (long)gridDim.x * 256) {
+  const IT cgs = (IT)(g.C / vec), Wo = (IT)g.Wo, Ho = (IT)g.Ho;
+  const IT total = (IT)g.N * Ho * Wo * cgs;
+  for (IT i = (IT)blockIdx.x * 256 + threadIdx.x; i < total; i += (IT)gridDim.x * 256) {
     const int c = (int)(i % cgs) * vec;
-    const long p = i / cgs;
-    const int ow = (int)(p % g.Wo), oh = (int)((p / g.Wo) % g.Ho), n = (int)(p / ((long)g.Wo * g.Ho));
+    const IT p = i / cgs, pr = p / Wo;
+    const int ow = (int)(p - pr * Wo), oh = (int)(pr % Ho), n = (int)(pr / Ho);
     float best[8];
     int bi[8];
 #pragma unroll
@@ -478,7 +481,7 @@ __global__ void __launch_bounds__(256) k_maxpool_fwd(const bf16_t* __restrict__ 
       for (int kw = 0; kw < g.K; ++kw) {
         const int w = ow * g.S - g.P + kw;
         if (w < 0 || w >= g.W) continue;
-        const long xo = (((long)n * g.H + h) * g.W + w) * g.C + c;
+        const IT xo = (((IT)n * g.H + h) * g.W + w) * g.C + c;
         float v[8];
         if (vec == 8) unpack8(*(const uint4*)(x + xo), v);
         else v[0] = ld_bf(x + xo);
@@ -491,7 +494,7 @@ __global__ void __launch_bounds__(256) k_maxpool_fwd(const bf16_t* __restrict__ 
         }
       }
     }
-    const long o = p * g.C + c;
+    const IT o = p * g.C + c;
     if (vec == 8) {
       *(uint4*)(y + o) = pack8(best);
       *(uint2*)(arg + o) = uint2{(unsigned)bi[0] | ((unsigned)bi[1] << 8) | ((unsigned)bi[2] << 16) | ((unsigned)bi[3] << 24),
@@ -504,15 +507,16 @@ __global__ void __launch_bounds__(256) k_maxpool_fwd(const bf16_t* __restrict__ 
 }
 
 // one thread per input pixel and 8 channels (C % 8 == 0: 16-B dy loads, 8-B argmax loads), else per element
+template <typename IT>
 __global__ void __launch_bounds__(256) k_maxpool_bwd(const bf16_t* __restrict__ dy, const uint8_t* __restrict__ arg,
                                                      bf16_t* __restrict__ dx, PoolGeom g) {
   const int vec = (g.C & 7) == 0 ? 8 : 1;
-  const int cgs = g.C / vec;
-  const long total = (long)g.N * g.H * g.W * cgs;
-  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < total; i += (long)gridDim.x * 256) {
+  const IT cgs = (IT)(g.C / vec), W = (IT)g.W, H = (IT)g.H;
+  const IT total = (IT)g.N * H * W * cgs;
+  for (IT i = (IT)blockIdx.x * 256 + threadIdx.x; i < total; i += (IT)gridDim.x * 256) {
     const int c = (int)(i % cgs) * vec;
-    const long p = i / cgs;
-    const int w = (int)(p % g.W), h = (int)((p / g.W) % g.H), n = (int)(p / ((long)g.W * g.H));
+    const IT p = i / cgs, pr = p / W;
+    const int w = (int)(p - pr * W), h = (int)(pr % H), n = (int)(pr / H);
     float s[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
     for (int kh = 0; kh < g.K; ++kh) {
       const int th = h + g.P - kh;
@@ -524,7 +528,7 @@ __global__ void __launch_bounds__(256) k_maxpool_bwd(const bf16_t* __restrict__ 
         if (tw < 0 || tw % g.S) continue;
         const int ow = tw / g.S;
         if (ow >= g.Wo) continue;
-        const long o = (((long)n * g.Ho + oh) * g.Wo + ow) * g.C + c;
+        const IT o = (((IT)n * g.Ho + oh) * g.Wo + ow) * g.C + c;
         const int tap = kh * g.K + kw;
         if (vec == 8) {
           float d[8];
@@ -540,7 +544,7 @@ __global__ void __launch_bounds__(256) k_maxpool_bwd(const bf16_t* __restrict__ 
         }
       }
     }
-    const long xo = p * g.C + c;
+    const IT xo = p * g.C + c;
     if (vec == 8) *(uint4*)(dx + xo) = pack8(s);
     else dx[xo] = f2bf_rne(s[0]);
   }
