@@ -506,6 +506,69 @@ __global__ void __launch_bounds__(256) k_maxpool_fwd(const bf16_t* __restrict__ 
   }
 }
 
+// 3x3 / stride 2 / pad 1 with H = 2 Ho, W = 2 Wo, C % 8 == 0 (the ResNet stem pool): one thread per OUTPUT
+// pixel and 8 channels writes the 2x2 input block (2oh..2oh+1, 2ow..2ow+1).  Even input rows/cols are reached only
+// by the centre tap of their own output; odd ones also by the next output's first tap.  Every dy / argmax record
+// is loaded once per thread (4 loads -> 4 stores, instead of 2.25 loads per store in the input-driven kernel).
+// Sums are taken in ascending tap order, as in k_maxpool_bwd.
+template <typename IT>
+__global__ void __launch_bounds__(256) k_maxpool_bwd_k3s2(const bf16_t* __restrict__ dy,
+                                                          const uint8_t* __restrict__ arg, bf16_t* __restrict__ dx,
+                                                          PoolGeom g) {
+  const IT cgs = (IT)(g.C >> 3), Wo = (IT)g.Wo, Ho = (IT)g.Ho;
+  const IT total = (IT)g.N * Ho * Wo * cgs;
+  for (IT i = (IT)blockIdx.x * 256 + threadIdx.x; i < total; i += (IT)gridDim.x * 256) {
+    const int c = (int)(i % cgs) * 8;
+    const IT p = i / cgs, pr = p / Wo;
+    const int ow = (int)(p - pr * Wo), oh = (int)(pr % Ho), n = (int)(pr / Ho);
+    const bool hr = oh + 1 < g.Ho, hc = ow + 1 < g.Wo;
+    // records (oh, ow), (oh, ow+1), (oh+1, ow), (oh+1, ow+1); missing neighbours read the own record with an
+    // impossible tap (255) so all loads are unconditional
+    const IT o00 = p * g.C + c;
+    const IT o01 = hc ? o00 + g.C : o00;
+    const IT o10 = hr ? o00 + (IT)g.Wo * g.C : o00;
+    const IT o11 = hr && hc ? o00 + ((IT)g.Wo + 1) * g.C : o00;
+    float d00[8], d01[8], d10[8], d11[8];
+    unpack8(*(const uint4*)(dy + o00), d00);
+    unpack8(*(const uint4*)(dy + o01), d01);
+    unpack8(*(const uint4*)(dy + o10), d10);
+    unpack8(*(const uint4*)(dy + o11), d11);
+    const uint2 a00 = *(const uint2*)(arg + o00), a01 = *(const uint2*)(arg + o01);
+    const uint2 a10 = *(const uint2*)(arg + o10), a11 = *(const uint2*)(arg + o11);
+    const unsigned m01 = hc ? 0u : 0xffu, m10 = hr ? 0u : 0xffu, m11 = hr && hc ? 0u : 0xffu;
+    float e00[8], e01[8], e10[8], e11[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int sh = (j & 3) * 8;
+      const unsigned t00 = ((j < 4 ? a00.x : a00.y) >> sh) & 0xffu;
+      const unsigned t01 = (((j < 4 ? a01.x : a01.y) >> sh) & 0xffu) | m01;
+      const unsigned t10 = (((j < 4 ? a10.x : a10.y) >> sh) & 0xffu) | m10;
+      const unsigned t11 = (((j < 4 ? a11.x : a11.y) >> sh) & 0xffu) | m11;
+      e00[j] = t00 == 4u ? d00[j] : 0.f;
+      float s = 0.f;
+      s += t01 == 3u ? d01[j] : 0.f;
+      s += t00 == 5u ? d00[j] : 0.f;
+      e01[j] = s;
+      s = 0.f;
+      s += t10 == 1u ? d10[j] : 0.f;
+      s += t00 == 7u ? d00[j] : 0.f;
+      e10[j] = s;
+      s = 0.f;
+      s += t11 == 0u ? d11[j] : 0.f;
+      s += t10 == 2u ? d10[j] : 0.f;
+      s += t01 == 6u ? d01[j] : 0.f;
+      s += t00 == 8u ? d00[j] : 0.f;
+      e11[j] = s;
+    }
+    const IT x00 = (((IT)n * g.H + 2 * oh) * g.W + 2 * ow) * g.C + c;
+    const IT xr = (IT)g.W * g.C;
+    *(uint4*)(dx + x00) = pack8(e00);
+    *(uint4*)(dx + x00 + g.C) = pack8(e01);
+    *(uint4*)(dx + x00 + xr) = pack8(e10);
+    *(uint4*)(dx + x00 + xr + g.C) = pack8(e11);
+  }
+}
+
 // one thread per input pixel and 8 channels (C % 8 == 0: 16-B dy loads, 8-B argmax loads), else per element
 template <typename IT>
 __global__ void __launch_bounds__(256) k_maxpool_bwd(const bf16_t* __restrict__ dy, const uint8_t* __restrict__ arg,

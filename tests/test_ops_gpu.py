@@ -133,7 +133,8 @@ def test_batch_norm_act(gpu, res_mode, relu):
     assert int(bn.num_batches_tracked) == int(ref_bn.num_batches_tracked) == 1
 
 
-@pytest.mark.parametrize("k,s,p,h", [(2, 2, 0, 16), (3, 2, 1, 15), (2, 2, 0, 7)])
+# (3, 2, 1, even h) with c % 8 == 0 takes the output-driven k_maxpool_bwd_k3s2 backward (h = 14: odd Ho edge)
+@pytest.mark.parametrize("k,s,p,h", [(2, 2, 0, 16), (3, 2, 1, 15), (2, 2, 0, 7), (3, 2, 1, 16), (3, 2, 1, 14)])
 @pytest.mark.parametrize("c", [24, 5])
 def test_max_pool(gpu, k, s, p, h, c):
     from distributeddataparallel_cifar10_amd.ops import max_pool2d
@@ -144,6 +145,21 @@ def test_max_pool(gpu, k, s, p, h, c):
     y.backward(dy)
     xr = x.detach().float().permute(0, 3, 1, 2).requires_grad_()
     yr = TF.max_pool2d(xr, k, s, p)
+    yr.backward(dy.float().permute(0, 3, 1, 2))
+    assert torch.equal(y.float().permute(0, 3, 1, 2), yr)
+    assert _rel(x.grad.float().permute(0, 3, 1, 2), xr.grad) < 1e-2
+
+
+def test_max_pool_resnet_stem_shape(gpu):
+    """The ResNet stem pool (3x3/2/1, 112 -> 56, 64 channels) through the output-driven backward."""
+    from distributeddataparallel_cifar10_amd.ops import max_pool2d
+    g = torch.Generator(device=gpu).manual_seed(5)
+    x = _bf(torch.randn(3, 112, 112, 64, device=gpu, generator=g)).requires_grad_()
+    y = max_pool2d(x, 3, 2, 1)
+    dy = _bf(torch.randn(y.shape, device=gpu, generator=g))
+    y.backward(dy)
+    xr = x.detach().float().permute(0, 3, 1, 2).requires_grad_()
+    yr = TF.max_pool2d(xr, 3, 2, 1)
     yr.backward(dy.float().permute(0, 3, 1, 2))
     assert torch.equal(y.float().permute(0, 3, 1, 2), yr)
     assert _rel(x.grad.float().permute(0, 3, 1, 2), xr.grad) < 1e-2
