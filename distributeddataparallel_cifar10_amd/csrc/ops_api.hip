@@ -40,7 +40,7 @@ inline bool getenv_flag(const char* name) {
   const char* e = getenv(name);
   return !(e && e[0] == '0');
 }
-// output-driven 3x3/2 max-pool backward (DCA_OPS_POOL_K3S2=0: the input-driven generic kernel)
+// 3x3/2 max-pool specialisations: unrolled forward, output-driven backward (DCA_OPS_POOL_K3S2=0: generic kernels)
 inline bool getenv_pool_k3s2() {
   static const bool v = getenv_flag("DCA_OPS_POOL_K3S2");
   return v;
@@ -398,6 +398,18 @@ inline bool pool_idx32(const PoolGeom& g) {
 int dca_ops_maxpool_fwd(const void* x, void* y, void* arg, const PoolGeom* geom, void* stream) {
   const PoolGeom g = *geom;
   REQUIRE(g.K * g.K <= 255 && g.K > 0 && g.S > 0, "maxpool: bad window");
+  if (g.K == 3 && g.S == 2 && g.P == 1 && g.H == 2 * g.Ho && g.W == 2 * g.Wo && g.C % 8 == 0 &&
+      getenv_pool_k3s2()) {
+    const dim3 grid(grid_for((long)g.N * g.Ho * g.Wo * g.C / 8));
+    if (pool_idx32(g))
+      hipLaunchKernelGGL(k_maxpool_fwd_k3s2<unsigned>, grid, dim3(256), 0, (hipStream_t)stream,
+                         (const bf16_t*)x, (bf16_t*)y, (uint8_t*)arg, g);
+    else
+      hipLaunchKernelGGL(k_maxpool_fwd_k3s2<long>, grid, dim3(256), 0, (hipStream_t)stream,
+                         (const bf16_t*)x, (bf16_t*)y, (uint8_t*)arg, g);
+    OPCK(hipGetLastError());
+    return 0;
+  }
   const dim3 grid(grid_for((long)g.N * g.Ho * g.Wo * g.C / ((g.C & 7) == 0 ? 8 : 1)));
   if (pool_idx32(g))
     hipLaunchKernelGGL(k_maxpool_fwd<unsigned>, grid, dim3(256), 0, (hipStream_t)stream,

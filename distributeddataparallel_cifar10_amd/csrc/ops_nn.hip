@@ -506,6 +506,57 @@ __global__ void __launch_bounds__(256) k_maxpool_fwd(const bf16_t* __restrict__ 
   }
 }
 
+// 3x3 / stride 2 / pad 1 forward with H = 2 Ho, W = 2 Wo, C % 8 == 0: the generic kernel's runtime tap loops issue
+// their 9 loads one after another (a memory latency each); here all 9 are unrolled and in flight together.  Only
+// the top row / left column of a window can fall into the padding (H = 2 Ho): those taps load the window centre
+// and are skipped in the compare, which runs in the same tap order (first max wins, NaN propagates).
+template <typename IT>
+__global__ void __launch_bounds__(256) k_maxpool_fwd_k3s2(const bf16_t* __restrict__ x, bf16_t* __restrict__ y,
+                                                          uint8_t* __restrict__ arg, PoolGeom g) {
+  const IT cgs = (IT)(g.C >> 3), Wo = (IT)g.Wo, Ho = (IT)g.Ho;
+  const IT total = (IT)g.N * Ho * Wo * cgs;
+  for (IT i = (IT)blockIdx.x * 256 + threadIdx.x; i < total; i += (IT)gridDim.x * 256) {
+    const int c = (int)(i % cgs) * 8;
+    const IT p = i / cgs, pr = p / Wo;
+    const int ow = (int)(p - pr * Wo), oh = (int)(pr % Ho), n = (int)(pr / Ho);
+    const IT ctr = (((IT)n * g.H + 2 * oh) * g.W + 2 * ow) * g.C + c;  // window centre (always in range)
+    const IT rs = (IT)g.W * g.C;
+    const bool top = oh > 0, left = ow > 0;
+    uint4 u[9];
+#pragma unroll
+    for (int kh = 0; kh < 3; ++kh)
+#pragma unroll
+      for (int kw = 0; kw < 3; ++kw) {
+        const bool ok = (kh > 0 || top) && (kw > 0 || left);
+        const IT o = ok ? ctr + (IT)(kh * rs) - rs + (IT)(kw * g.C) - (IT)g.C : ctr;
+        u[kh * 3 + kw] = *(const uint4*)(x + o);
+      }
+    float best[8];
+    int bi[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      best[j] = -INFINITY;
+      bi[j] = 0;
+    }
+#pragma unroll
+    for (int t = 0; t < 9; ++t) {
+      if (!((t >= 3 || top) && (t % 3 > 0 || left))) continue;
+      float v[8];
+      unpack8(u[t], v);
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+        if (v[j] > best[j] || (v[j] != v[j] && best[j] == best[j])) {
+          best[j] = v[j];
+          bi[j] = t;
+        }
+    }
+    const IT o = p * g.C + c;
+    *(uint4*)(y + o) = pack8(best);
+    *(uint2*)(arg + o) = uint2{(unsigned)bi[0] | ((unsigned)bi[1] << 8) | ((unsigned)bi[2] << 16) | ((unsigned)bi[3] << 24),
+                               (unsigned)bi[4] | ((unsigned)bi[5] << 8) | ((unsigned)bi[6] << 16) | ((unsigned)bi[7] << 24)};
+  }
+}
+
 // 3x3 / stride 2 / pad 1 with H = 2 Ho, W = 2 Wo, C % 8 == 0 (the ResNet stem pool): one thread per OUTPUT
 // pixel and 8 channels writes the 2x2 input block (2oh..2oh+1, 2ow..2ow+1).  Even input rows/cols are reached only
 // by the centre tap of their own output; odd ones also by the next output's first tap.  Every dy / argmax record
