@@ -454,8 +454,12 @@ int dca_ops_avgpool_fwd(const void* x, float* y, int N, int HW, int C, void* str
 }
 
 int dca_ops_avgpool_bwd(const float* dy, void* dx, int N, int HW, int C, void* stream) {
-  hipLaunchKernelGGL(k_avgpool_bwd, dim3(grid_for((long)N * HW * C)), dim3(256), 0, (hipStream_t)stream, dy,
-                     (bf16_t*)dx, N, HW, C);
+  if (C % 8 == 0 && (long)N * HW * C + 8192L * 256 * 8 < (1L << 31))
+    hipLaunchKernelGGL(k_avgpool_bwd8, dim3(grid_for((long)N * HW * C / 8)), dim3(256), 0, (hipStream_t)stream, dy,
+                       (bf16_t*)dx, N, HW, C);
+  else
+    hipLaunchKernelGGL(k_avgpool_bwd, dim3(grid_for((long)N * HW * C)), dim3(256), 0, (hipStream_t)stream, dy,
+                       (bf16_t*)dx, N, HW, C);
   OPCK(hipGetLastError());
   return 0;
 }

@@ -673,6 +673,18 @@ __global__ void __launch_bounds__(256) k_avgpool_fwd(const bf16_t* __restrict__ 
   for (int p = 0; p < HW; ++p) s += ld_bf(x + ((long)n * HW + p) * C + c);
   y[(long)n * C + c] = s / HW;
 }
+// C % 8 == 0: one thread per pixel and 8 channels (two 16-B dy loads, one 16-B store), 32-bit index decode
+__global__ void __launch_bounds__(256) k_avgpool_bwd8(const float* __restrict__ dy, bf16_t* __restrict__ dx, int N,
+                                                      int HW, int C) {
+  const unsigned cg = (unsigned)C >> 3, per_n = (unsigned)HW * cg, total = (unsigned)N * per_n;
+  const float hw = (float)HW;
+  for (unsigned i = blockIdx.x * 256u + threadIdx.x; i < total; i += gridDim.x * 256u) {
+    const unsigned n = i / per_n, c = (i % cg) * 8u;
+    const f32x4 a = *(const f32x4*)(dy + n * (unsigned)C + c), b = *(const f32x4*)(dy + n * (unsigned)C + c + 4);
+    float v[8] = {a[0] / hw, a[1] / hw, a[2] / hw, a[3] / hw, b[0] / hw, b[1] / hw, b[2] / hw, b[3] / hw};
+    *(uint4*)(dx + 8ul * i) = pack8(v);
+  }
+}
 __global__ void __launch_bounds__(256) k_avgpool_bwd(const float* __restrict__ dy, bf16_t* __restrict__ dx, int N,
                                                      int HW, int C) {
   const long total = (long)N * HW * C;
