@@ -323,8 +323,10 @@ int dca_ops_bn_fwd(const void* x, const void* r, void* out, float* part, float* 
   const int nparts = (int)((M + BN_ROWS - 1) / BN_ROWS);
   hipLaunchKernelGGL(k_bn_stats, dim3((C + 63) / 64, nparts), dim3(256), 0, st, (const bf16_t*)x, rm, (float2*)part,
                      (int)M, C);
-  hipLaunchKernelGGL(k_bn_finalize, dim3((C + 15) / 16), dim3(256), 0, st, (const float2*)part, nparts, (int)M, C,
-                     rm, rv, (float2*)stats, eps, momentum);
+#define FIN(CW) hipLaunchKernelGGL(k_bn_finalize<CW>, dim3((C + CW - 1) / CW), dim3(256), 0, st, (const float2*)part, \
+                                   nparts, (int)M, C, rm, rv, (float2*)stats, eps, momentum)
+  BN_FIN_DISPATCH(C, FIN);
+#undef FIN
   BN_LAUNCH(k_bn_apply, C, nparts_rows(M), st, (const bf16_t*)x, (const bf16_t*)r,
                      (bf16_t*)out, (const float2*)stats, gamma, beta, M, C, relu, res_mode, (uint8_t*)nullptr,
                      (const float*)nullptr, (unsigned*)nullptr);
@@ -345,8 +347,10 @@ int dca_ops_bn_fwd_parts(const void* x, const void* r, void* out, const float* p
   REQUIRE(!q || (amax_prev && amax_out), "bn: fp8 output needs amax_prev and amax_out");
   hipStream_t st = (hipStream_t)stream;
   if (q) OPCK(hipMemsetAsync(amax_out, 0, sizeof(unsigned), st));
-  hipLaunchKernelGGL(k_bn_finalize, dim3((C + 15) / 16), dim3(256), 0, st, (const float2*)part, nparts, (int)M, C,
-                     rm, rv, (float2*)stats, eps, momentum);
+#define FIN(CW) hipLaunchKernelGGL(k_bn_finalize<CW>, dim3((C + CW - 1) / CW), dim3(256), 0, st, (const float2*)part, \
+                                   nparts, (int)M, C, rm, rv, (float2*)stats, eps, momentum)
+  BN_FIN_DISPATCH(C, FIN);
+#undef FIN
   BN_LAUNCH(k_bn_apply, C, nparts_rows(M), st, (const bf16_t*)x, (const bf16_t*)r,
                      (bf16_t*)out, (const float2*)stats, gamma, beta, M, C, relu, res_mode, (uint8_t*)q, amax_prev,
                      amax_out);
@@ -379,8 +383,10 @@ int dca_ops_bn_bwd(const void* dy, const void* x, const void* r, const float* st
   BN_LAUNCH(k_bn_bwd_stats, C, nparts, st, (const bf16_t*)dy,
                      (const bf16_t*)x, (const bf16_t*)r, (const float2*)stats, gamma, beta, (float2*)part, (int)M, C,
                      relu, res_mode);
-  hipLaunchKernelGGL(k_bn_bwd_finalize, dim3((C + 15) / 16), dim3(256), 0, st, (const float2*)part, nparts, C,
-                     dgamma, dbeta, (float2*)sums, accumulate);
+#define FIN(CW) hipLaunchKernelGGL(k_bn_bwd_finalize<CW>, dim3((C + CW - 1) / CW), dim3(256), 0, st, \
+                                   (const float2*)part, nparts, C, dgamma, dbeta, (float2*)sums, accumulate)
+  BN_FIN_DISPATCH(C, FIN);
+#undef FIN
   BN_LAUNCH(k_bn_bwd_apply, C, nparts_rows(M), st, (const bf16_t*)dy, (const bf16_t*)x,
                      (const bf16_t*)r, (const float2*)stats, gamma, beta, (const float2*)sums, (bf16_t*)dx,
                      (bf16_t*)dr, M, C, relu, res_mode);
