@@ -203,7 +203,8 @@ __device__ __forceinline__ float2 reduce_parts(const float2* __restrict__ part, 
     if ((C) >= 2048) { CALL(16); }     \
     else if ((C) >= 1024) { CALL(8); } \
     else if ((C) >= 512) { CALL(4); }  \
-    else { CALL(2); }                  \
+    else if ((C) >= 256) { CALL(2); }  \
+    else { CALL(1); }                  \
   } while (0)
 
 template <int CW>
