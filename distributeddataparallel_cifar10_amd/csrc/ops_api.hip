@@ -516,6 +516,7 @@ int dca_ops_fp8_alpha(const unsigned* amax_a, const unsigned* amax_b, float extr
 // descs: device array of nd PackDesc (ops/functional.py WeightPack); amax: n_amax device words zeroed first.
 int dca_ops_pack_weights(const void* descs, int nd, int blocks_per_layer, unsigned* amax, int n_amax, void* stream) {
   REQUIRE(nd > 0 && blocks_per_layer > 0, "pack_weights: empty");
+  REQUIRE(blocks_per_layer <= 4096, "pack_weights: at most 4096 blocks per layer (32-bit grid-stride indices)");
   hipStream_t st = (hipStream_t)stream;
   if (n_amax > 0) OPCK(hipMemsetAsync(amax, 0, sizeof(unsigned) * n_amax, st));
   const dim3 grid(blocks_per_layer, nd);

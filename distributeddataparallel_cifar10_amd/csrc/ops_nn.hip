@@ -825,37 +825,39 @@ struct PackDesc {
   int co, ci, ci_pad, kh, kw, kp;
 };
 
-__device__ __forceinline__ bool pack_src(const PackDesc& d, long i, long& src, int& n, int& c, int& a, int& b) {
-  n = (int)(i / d.kp);
-  const int k = (int)(i - (long)n * d.kp);
+// Index math is 32-bit: a layer's weight count is far below 2^31 (asserted on the host), and the 64-bit division
+// sequences made this launch ALU-bound.
+__device__ __forceinline__ bool pack_src(const PackDesc& d, unsigned i, unsigned& src, int& n, int& c, int& a,
+                                         int& b) {
+  n = (int)(i / (unsigned)d.kp);
+  const int k = (int)(i - (unsigned)n * d.kp);
   const int tap = k / d.ci_pad;
   c = k - tap * d.ci_pad;
   a = tap / d.kw;
   b = tap - a * d.kw;
   if (c >= d.ci || tap >= d.kh * d.kw) return false;
-  src = (((long)n * d.ci + c) * d.kh + a) * d.kw + b;
+  src = (((unsigned)n * d.ci + c) * d.kh + a) * d.kw + b;
   return true;
 }
 
 __global__ void __launch_bounds__(256) k_pack_weights(const PackDesc* __restrict__ descs) {
   const PackDesc d = descs[blockIdx.y];
-  const long total = (long)d.co * d.kp;
+  const unsigned total = (unsigned)d.co * d.kp;
   float m = 0.f;
-  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < total; i += (long)gridDim.x * 256) {
-    long src;
+  for (unsigned i = blockIdx.x * 256u + threadIdx.x; i < total; i += gridDim.x * 256u) {
+    unsigned src;
     int n, c, a, b;
     const float v = pack_src(d, i, src, n, c, a, b) ? d.w[src] : 0.f;
     d.fwd[i] = f2bf_rne(v);
     m = fmaxf(m, fabsf(v));
   }
   if (d.dgrad) {  // second pass in the dgrad matrix's own order: coalesced writes, gathered (L2-resident) reads
-    const int taps = d.kh * d.kw;
-    const long dtot = (long)d.ci * taps * d.co;
-    for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < dtot; i += (long)gridDim.x * 256) {
-      const int n = (int)(i % d.co);
-      const long r = i / d.co;
-      const int tflip = (int)(r % taps), c = (int)(r / taps);
-      d.dgrad[i] = f2bf_rne(d.w[((long)n * d.ci + c) * taps + (taps - 1 - tflip)]);
+    const unsigned taps = d.kh * d.kw, co = d.co;
+    const unsigned dtot = (unsigned)d.ci * taps * co;
+    for (unsigned i = blockIdx.x * 256u + threadIdx.x; i < dtot; i += gridDim.x * 256u) {
+      const unsigned r = i / co, n = i - r * co;
+      const unsigned c = r / taps, tflip = r - c * taps;
+      d.dgrad[i] = f2bf_rne(d.w[(n * d.ci + c) * taps + (taps - 1 - tflip)]);
     }
   }
   if (d.q8) {
@@ -875,9 +877,9 @@ __global__ void __launch_bounds__(256) k_pack_fp8(const PackDesc* __restrict__ d
   if (!d.q8) return;
   const float amax = __uint_as_float(*d.amax);
   const float sc = amax > 0.f ? 448.f / amax : 1.f;
-  const long total = (long)d.co * d.kp;
-  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < total; i += (long)gridDim.x * 256) {
-    long src;
+  const unsigned total = (unsigned)d.co * d.kp;
+  for (unsigned i = blockIdx.x * 256u + threadIdx.x; i < total; i += gridDim.x * 256u) {
+    unsigned src;
     int n, c, a, b;
     const float v = pack_src(d, i, src, n, c, a, b) ? fminf(fmaxf(d.w[src] * sc, -448.f), 448.f) : 0.f;
     d.q8[i] = (uint8_t)(__builtin_amdgcn_cvt_pk_fp8_f32(v, 0.f, 0, false) & 0xff);

@@ -292,6 +292,8 @@ class WeightPack:
                 co, ci, kh, kw = c.weight.shape
                 if not c.weight.is_contiguous():
                     raise ValueError("WeightPack: conv weights must be contiguous")
+                if max(co * e["kp"], ci * kh * kw * co) + 4096 * 256 >= 2 ** 31:
+                    raise ValueError("WeightPack: layer too large for the 32-bit pack kernel indices")
                 arr[i] = N.PackDesc(w=c.weight.data_ptr(), fwd=e["fwd"].data_ptr(),
                                     dgrad=e["dgrad"].data_ptr() if e["dgrad"] is not None else None,
                                     q8=e["q8"].data_ptr() if e["q8"] is not None else None,
