@@ -851,13 +851,31 @@ __global__ void __launch_bounds__(256) k_pack_weights(const PackDesc* __restrict
     d.fwd[i] = f2bf_rne(v);
     m = fmaxf(m, fabsf(v));
   }
-  if (d.dgrad) {  // second pass in the dgrad matrix's own order: coalesced writes, gathered (L2-resident) reads
-    const unsigned taps = d.kh * d.kw, co = d.co;
-    const unsigned dtot = (unsigned)d.ci * taps * co;
-    for (unsigned i = blockIdx.x * 256u + threadIdx.x; i < dtot; i += gridDim.x * 256u) {
-      const unsigned r = i / co, n = i - r * co;
-      const unsigned c = r / taps, tflip = r - c * taps;
-      d.dgrad[i] = f2bf_rne(d.w[(n * d.ci + c) * taps + (taps - 1 - tflip)]);
+  if (d.dgrad) {
+    // second pass: dgrad[c*taps + tflip][n] = w[n][c][taps-1-tflip] is a transpose of the [Cout][Cin*taps] weight
+    // matrix (taps flipped inside each channel group), done through 32 x 32 LDS tiles so both the fp32 reads and
+    // the bf16 writes are coalesced (a direct gather reads one cache line per element).
+    __shared__ float tile[32][33];
+    const unsigned taps = d.kh * d.kw, co = d.co, R = (unsigned)d.ci * taps;
+    const unsigned tn = (co + 31) / 32, tr = (R + 31) / 32;
+    const unsigned tx = threadIdx.x & 31, ty = threadIdx.x >> 5;
+    for (unsigned t = blockIdx.x; t < tn * tr; t += gridDim.x) {  // block-uniform trip count
+      const unsigned n0 = (t / tr) * 32, r0 = (t % tr) * 32;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const unsigned n = n0 + ty + 8 * j, r = r0 + tx;
+        tile[ty + 8 * j][tx] = n < co && r < R ? d.w[n * R + r] : 0.f;
+      }
+      __syncthreads();
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const unsigned r = r0 + ty + 8 * j, n = n0 + tx;
+        if (r < R && n < co) {
+          const unsigned c = r / taps, tap = r - c * taps;
+          d.dgrad[(c * taps + (taps - 1 - tap)) * co + n] = f2bf_rne(tile[tx][ty + 8 * j]);
+        }
+      }
+      __syncthreads();
     }
   }
   if (d.q8) {

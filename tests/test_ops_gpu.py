@@ -397,6 +397,12 @@ def test_weight_pack(gpu):
         convs[1].weight.mul_(-2.0)
     pack.pack()
     assert torch.equal(e1["fwd"], F._weight_matrix(convs[1].weight.detach(), 288))
+    # partial 32 x 32 transpose tiles in both dimensions (Cout = 40, Cin * taps = 216)
+    conv3 = torch.nn.Conv2d(24, 40, 3, padding=1, bias=False).to(gpu)
+    pack3 = F.WeightPack([conv3])
+    pack3.pack()
+    w3 = conv3.weight.detach()
+    assert torch.equal(pack3.get(conv3)["dgrad"], w3.flip(2, 3).permute(1, 2, 3, 0).reshape(24, -1).to(torch.bfloat16))
 
 
 def test_weight_grad_layout_remap(gpu):
