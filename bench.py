@@ -2,36 +2,43 @@
 
 Metric/config from BASELINE.json: "images/sec (whole node) CIFAR-10 ResNet at 1/2/4/8 MI355X; scaling efficiency",
 NetResDeep(n_chans1=32, n_blocks=10), per-rank batch 32 (reference main.py:61), SGD lr 1e-2, one process per GPU,
-gradient all-reduce = one-shot xGMI peer reads fused with SGD (RCCL fallback).  Synthetic CIFAR-shaped uint8 data (no datasets offline), random-init weights.
+gradient all-reduce = one-shot xGMI peer reads fused with SGD (RCCL fallback).  Synthetic CIFAR-shaped uint8 data
+(no datasets offline), random-init weights.
 
-Each step is the FULL training step (stem+10 blocks forward, loss, backward, gradient all-reduce, SGD update,
-BN running stats) replayed as hipGraphs (16 steps per launch) by the native engine.  W warm-up steps, then K timed steps bracketed by
-barrier + device sync on both sides; the slowest rank's time is reported.
+Each step is the FULL training step (stem + 10 blocks forward, loss, backward, gradient all-reduce, SGD update,
+BN running stats) replayed as hipGraphs (16 steps per launch) by the native engine.  The graphs are captured during
+warm-up (never inside the timed region).  W warm-up steps, then K timed steps bracketed by barrier + device sync on
+both sides; the slowest rank's time is reported.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--dtype bf16|fp32]
+Launch modes (reference main.py:80-85 launches its ranks itself with mp.spawn; so does this):
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--dtype bf16|fp32]     # N>1: spawns N ranks itself
     python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 --master-port P bench.py --gpus N
+    python bench.py --sweep 1,2,4,8                                               # one fresh rank group per N,
+                                                                                  # + scaling-efficiency summary
+The parent of a self-launch never touches the GPU (ranks are spawned before any HIP call).
+DCA_BENCH_SHARE_GPU=1 (rehearsal on a 1-GPU box): every rank on GPU 0, gloo process group, xGMI all-reduce.
 """
 from __future__ import annotations
 
 import argparse
 import json
 import os
+import socket
 import sys
+import tempfile
 import time
-
-import numpy as np
-import torch
-import torch.distributed as dist
 
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 
 BASELINE_METRIC = "images/sec (whole node) CIFAR-10 ResNet at 1/2/4/8 MI355X; scaling efficiency"
-# Practical bar measured this round: the reference training step as-is (PyTorch-ROCm eager + stock DDP,
-# host data pipeline) on one MI355X -> profiles/reference_eager_mi355x.log.  BASELINE.md publishes no number.
-REF_EAGER_IPS_PER_GPU = 10958.3
+# Practical bar (BASELINE.md publishes no number): the reference training step as-is -- PyTorch-ROCm eager + stock
+# DDP + its host data pipeline -- on one MI355X, measured per precision (bench/reference_eager.py):
+#   fp32 (the reference's own precision): profiles/reference_eager_mi355x.log
+#   bf16 (the same step under torch.autocast bf16): profiles/reference_eager_bf16_mi355x.log
+REF_EAGER_IPS_PER_GPU = {"fp32": 10958.3, "bf16": None}
 
 
-def main() -> int:
+def _args(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=300)
@@ -42,24 +49,34 @@ def main() -> int:
     ap.add_argument("--engine", default="auto", choices=["auto", "persistent", "multikernel"])
     ap.add_argument("--allreduce", default="auto", choices=["auto", "xgmi", "rccl"],
                     help="gradient all-reduce for N>1: one-shot xGMI peer reads (default inside a node) or RCCL")
-    a = ap.parse_args()
+    ap.add_argument("--sweep", default=None, metavar="N1,N2,..",
+                    help="run each N in a fresh spawned rank group; print per-N lines and a scaling summary")
+    ap.add_argument("--result-file", default=None, help=argparse.SUPPRESS)  # rank 0 -> parent (sweep)
+    return ap.parse_args(argv)
+
+
+def _free_port() -> int:
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def run_rank(a) -> dict | None:
+    """One rank of the benchmark (rank / world from the launcher env).  Returns rank 0's result dict."""
+    import numpy as np
+    import torch
+    import torch.distributed as dist
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != a.gpus:
-        if world == 1 and a.gpus > 1:
-            print(f"bench.py: --gpus {a.gpus} needs torch.distributed.run with {a.gpus} processes", file=sys.stderr)
-            return 2
-    # Rehearsal hook (tests / 1-GPU boxes): DCA_BENCH_SHARE_GPU=1 puts every rank on GPU 0 with a gloo process
-    # group (RCCL refuses two ranks per device); the gradient all-reduce is still the engine's xGMI path.
     share = os.environ.get("DCA_BENCH_SHARE_GPU") == "1"
     dev_index = 0 if share else local_rank
     torch.cuda.set_device(dev_index)
     dev = torch.device("cuda", dev_index)
     os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
     os.environ.setdefault("MASTER_PORT", "29511")
-    if share:
+    if share:  # RCCL refuses two ranks per device; the gradient all-reduce is still the engine's xGMI path
         dist.init_process_group("gloo", rank=rank, world_size=world)
     else:
         dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
@@ -75,55 +92,126 @@ def main() -> int:
     trainer = FusedDDPTrainer(model, data.to(dev), labels.to(dev), batch_max=a.batch, lr=1e-2, dtype=a.dtype,
                               rows=a.rows, max_indices=(a.warmup + a.steps) * a.batch, persistent=persistent,
                               comm=a.allreduce)
+    eng = trainer.engine
     sampler = torch.utils.data.distributed.DistributedSampler(range(50000), num_replicas=world, rank=rank)
     order = np.resize(np.fromiter(iter(sampler), dtype=np.int32), (a.warmup + a.steps) * a.batch)
-    trainer.engine.set_indices(order)
-    trainer.engine.set_cursor(0)
-    trainer.engine.read_loss(reset=True)
+    eng.set_indices(order)
+    eng.set_cursor(0)
+    eng.precapture(a.batch)  # graph capture + instantiate happen here, outside the timed region
+    eng.read_loss(reset=True)
 
-    trainer.engine.run(a.batch, a.warmup)
-    trainer.engine.sync()
+    eng.run(a.batch, a.warmup)
+    eng.sync()
+    eng.comm_time(reset=True)
     dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    trainer.engine.run(a.batch, a.steps)
-    trainer.engine.sync()
+    eng.run(a.batch, a.steps)
+    eng.sync()
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
     dist.barrier()
-    t = torch.tensor([dt], device="cpu" if share else dev, dtype=torch.float64)
-    dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    dt = float(t.item())
-    loss_sum, nsteps = trainer.engine.read_loss()
-    ok = np.isfinite(loss_sum)
+    comm_us, comm_calls = eng.comm_time()
+    on = "cpu" if share else dev
+    mine = torch.tensor([dt, comm_us / max(comm_calls, 1)], device=on, dtype=torch.float64)
+    every = [torch.zeros_like(mine) for _ in range(world)]
+    dist.all_gather(every, mine)
+    per_rank = [(float(t[0].item()), float(t[1].item())) for t in every]
+    dt = max(p[0] for p in per_rank)
+    loss_sum, nsteps = eng.read_loss()
+    ok = bool(np.isfinite(loss_sum))
     value = world * a.batch * a.steps / dt
+    ref = REF_EAGER_IPS_PER_GPU.get(a.dtype)
+    res = {
+        "metric": BASELINE_METRIC,
+        "value": round(value, 1),
+        "unit": "images/sec",
+        "n_gpus": world,
+        "steps": a.steps,
+        "warmup": a.warmup,
+        "ms_per_step": round(1e3 * dt / a.steps, 5),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": round(value / (ref * world), 3) if ref else None,
+        "dtype": a.dtype,
+        "engine": "persistent" if eng.cfg.persistent else "multikernel",
+        "allreduce": trainer.comm,
+        "per_rank_ms_per_step": [round(1e3 * p[0] / a.steps, 5) for p in per_rank],
+        "allreduce_us_per_step": ([round(p[1], 2) for p in per_rank] if trainer.comm == "xgmi" else None),
+        "data": "synthetic (CIFAR-10-shaped uint8 3x32x32, 50000 samples, random labels; random-init weights)",
+        "config": {"model": "NetResDeep(n_chans1=32, n_blocks=10)", "global_batch": a.batch * world,
+                   "per_rank_batch": a.batch, "seq_len": None, "image": "3x32x32",
+                   "parallelism": f"dp{world}", "optimizer": "SGD(lr=1e-2)",
+                   "baseline": (f"reference main.py step as-is, PyTorch-ROCm eager ({a.dtype}) on 1x MI355X, "
+                                f"{ref} img/s/GPU (bench/reference_eager.py)") if ref else
+                               f"no {a.dtype} reference measurement"},
+        "loss_finite": ok,
+        "mean_loss": loss_sum / max(nsteps, 1),
+    }
     if rank == 0:
-        print(json.dumps({
-            "metric": BASELINE_METRIC,
-            "value": round(value, 1),
-            "unit": "images/sec",
-            "n_gpus": world,
-            "steps": a.steps,
-            "warmup": a.warmup,
-            "ms_per_step": round(1e3 * dt / a.steps, 5),
-            "higher_is_better": True,
-            "scaling": "weak",
-            "vs_baseline": round(value / (REF_EAGER_IPS_PER_GPU * world), 3),
-            "dtype": a.dtype,
-            "engine": "persistent" if trainer.engine.cfg.persistent else "multikernel",
-            "allreduce": trainer.comm,
-            "data": "synthetic (CIFAR-10-shaped uint8 3x32x32, 50000 samples, random labels; random-init weights)",
-            "config": {"model": "NetResDeep(n_chans1=32, n_blocks=10)", "global_batch": a.batch * world,
-                       "per_rank_batch": a.batch, "seq_len": None, "image": "3x32x32",
-                       "parallelism": f"dp{world}", "optimizer": "SGD(lr=1e-2)",
-                       "baseline": "reference main.py step as-is, PyTorch-ROCm eager on 1x MI355X "
-                                   f"({REF_EAGER_IPS_PER_GPU} img/s/GPU, profiles/reference_eager_mi355x.log)"},
-            "loss_finite": bool(ok),
-            "mean_loss": loss_sum / max(nsteps, 1),
-        }), flush=True)
+        print(json.dumps(res), flush=True)
+        if a.result_file:
+            with open(a.result_file, "w") as f:
+                json.dump(res, f)
     trainer.close()
     dist.destroy_process_group()
-    return 0 if ok else 1
+    if not ok:
+        raise SystemExit(1)
+    return res if rank == 0 else None
+
+
+def _spawned(local_rank: int, world: int, port: int, argv: list) -> None:
+    """mp.spawn target: one rank of a self-launched group (reference main.py:84 mp.spawn(main, nprocs=...))."""
+    os.environ.update({"RANK": str(local_rank), "LOCAL_RANK": str(local_rank), "WORLD_SIZE": str(world),
+                       "LOCAL_WORLD_SIZE": str(world), "MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port)})
+    run_rank(_args(argv))
+
+
+def launch(n: int, argv: list) -> None:
+    """Run an n-rank group: in this process for n == 1, else as n spawned processes (no GPU call in the parent)."""
+    if n == 1:
+        os.environ.setdefault("WORLD_SIZE", "1")
+        run_rank(_args(argv))
+        return
+    import torch.multiprocessing as mp
+    mp.spawn(_spawned, args=(n, _free_port(), argv), nprocs=n, join=True)
+
+
+def sweep(ns: list, argv: list) -> int:
+    """One fresh rank group per N (1-rank groups too run in a child, so every N starts from a clean process)."""
+    import torch.multiprocessing as mp
+    results = {}
+    for n in ns:
+        with tempfile.NamedTemporaryFile(suffix=".json", delete=False) as f:
+            path = f.name
+        sub = [x for x in argv if x != "--sweep"] + ["--gpus", str(n), "--result-file", path]
+        mp.spawn(_spawned, args=(n, _free_port(), sub), nprocs=n, join=True)
+        with open(path) as f:
+            results[n] = json.load(f)
+        os.unlink(path)
+    base = results[min(results)]["value"] / min(results)
+    print(json.dumps({"metric": BASELINE_METRIC, "sweep": {str(n): r["value"] for n, r in results.items()},
+                      "scaling_efficiency": {str(n): round(r["value"] / (n * base), 4) for n, r in results.items()},
+                      "ms_per_step": {str(n): r["ms_per_step"] for n, r in results.items()},
+                      "dtype": results[min(results)]["dtype"], "unit": "images/sec"}), flush=True)
+    return 0
+
+
+def main() -> int:
+    argv = sys.argv[1:]
+    a = _args(argv)
+    if a.sweep:
+        i = argv.index("--sweep")
+        return sweep([int(x) for x in a.sweep.split(",")], argv[:i] + argv[i + 2:])
+    if "WORLD_SIZE" in os.environ:  # started by torch.distributed.run (or another launcher)
+        world = int(os.environ["WORLD_SIZE"])
+        if world != a.gpus:
+            print(f"bench.py: --gpus {a.gpus} but the launcher started {world} ranks", file=sys.stderr)
+            return 2
+        run_rank(a)
+        return 0
+    launch(a.gpus, argv)
+    return 0
 
 
 if __name__ == "__main__":

@@ -47,7 +47,7 @@ class FakeCifar(torch.utils.data.Dataset):
         return img, self.targets[i]
 
 
-def run(mode: str, steps: int, warmup: int, bs: int) -> dict:
+def run(mode: str, steps: int, warmup: int, bs: int, dtype: str = "fp32") -> dict:
     dev = torch.device("cuda", 0)
     model = NetResDeep().to(dev)
     model = nn.parallel.DistributedDataParallel(model, device_ids=[0], output_device=0)
@@ -78,8 +78,9 @@ def run(mode: str, steps: int, warmup: int, bs: int) -> dict:
     def step():
         imgs, labels = nxt()
         imgs, labels = imgs.to(dev), labels.to(dev)
-        out = model(imgs)
-        loss = loss_fn(out, labels)
+        with torch.autocast("cuda", torch.bfloat16, enabled=dtype == "bf16"):  # bf16: AMP, fp32 master weights
+            out = model(imgs)
+            loss = loss_fn(out.float(), labels)
         opt.zero_grad()
         loss.backward()
         opt.step()
@@ -94,7 +95,7 @@ def run(mode: str, steps: int, warmup: int, bs: int) -> dict:
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
     return {"metric": "reference_eager_images_per_sec", "data": mode, "value": steps * bs / dt,
-            "ms_per_step": 1e3 * dt / steps, "steps": steps, "batch": bs, "n_gpus": 1, "dtype": "fp32"}
+            "ms_per_step": 1e3 * dt / steps, "steps": steps, "batch": bs, "n_gpus": 1, "dtype": dtype}
 
 
 def main():
@@ -103,13 +104,15 @@ def main():
     ap.add_argument("--warmup", type=int, default=30)
     ap.add_argument("--batch", type=int, default=32)
     ap.add_argument("--modes", default="device,host")
+    ap.add_argument("--dtypes", default="fp32", help="comma list of fp32 / bf16 (torch.autocast bf16)")
     a = ap.parse_args()
     os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
     os.environ.setdefault("MASTER_PORT", "29533")
     dist.init_process_group("nccl", rank=0, world_size=1)
     torch.cuda.set_device(0)
-    for m in a.modes.split(","):
-        print(json.dumps(run(m, a.steps, a.warmup, a.batch)), flush=True)
+    for d in a.dtypes.split(","):
+        for m in a.modes.split(","):
+            print(json.dumps(run(m, a.steps, a.warmup, a.batch, d)), flush=True)
     dist.destroy_process_group()
 
 

@@ -9,6 +9,11 @@ Also calibrates the launch floor with graphs of empty / load-only kernels (dca_m
 """
 from __future__ import annotations
 
+
+def _mcheck(lib, rc, what):
+    if rc != 0:
+        raise RuntimeError(f"{what} failed: {lib.dca_micro_last_error().decode(errors='replace')}")
+
 import ctypes
 import json
 import os
@@ -34,7 +39,7 @@ def microbench(lib):
     for kind, name in kinds:
         for grid in (128, 256):
             us = ctypes.c_float()
-            native.check(lib.dca_microbench(kind, 23, grid, 200, ctypes.byref(us)), "microbench")
+            _mcheck(lib, lib.dca_microbench(kind, 23, grid, 200, ctypes.byref(us)), "microbench")
             out[f"{name}/grid{grid}"] = round(us.value, 3)
     return out
 
@@ -133,7 +138,7 @@ def main():
         entry.update(phases)
         res["kernels"].append(entry)
         print(json.dumps(entry), flush=True)
-    res["microbench_us_per_kernel"] = microbench(native.load())
+    res["microbench_us_per_kernel"] = microbench(native.load_micro())
     print(json.dumps({"microbench_us_per_kernel": res["microbench_us_per_kernel"]}), flush=True)
     eng.close()
 

@@ -9,6 +9,11 @@ import json
 import os
 import sys
 
+
+def _mcheck(lib, rc, what):
+    if rc != 0:
+        raise RuntimeError(f"{what} failed: {lib.dca_micro_last_error().decode(errors='replace')}")
+
 import torch
 import torch.distributed as dist
 
@@ -46,11 +51,11 @@ def single_process(ws_list=(1, 2, 3), iters=500):
     what the all-reduce adds per step, free of the cross-process scheduling of a shared GPU."""
     import ctypes
     from distributeddataparallel_cifar10_amd.runtime import native
-    lib = native.require_native()
+    lib = native.load_micro()
     torch.cuda.init()
     for w in ws_list:
         us, err = ctypes.c_float(), ctypes.c_int()
-        native.check(lib.dca_microbench_xgmi(w, iters, ctypes.byref(us), ctypes.byref(err)), "microbench_xgmi")
+        _mcheck(lib, lib.dca_microbench_xgmi(w, iters, ctypes.byref(us), ctypes.byref(err)), "microbench_xgmi")
         print(json.dumps({"ranks_in_process": w, "us_per_allreduce": round(us.value, 2), "timeout": bool(err.value),
                           "bytes": 76140 * 4}), flush=True)
 

@@ -22,7 +22,8 @@ workflow runs on MI355X:
 
 Deliberate fixes: ``-freeze`` really freezes (``requires_grad``, applied before the DDP
 wrap); k-fold calls ``train`` with the right arguments; validation runs in eval mode and averages every val batch
-(the reference kept only the last); predictions are thresholded on sigmoid probabilities.
+(the reference kept only the last).  ``pre_generate_labels`` keeps the reference's raw-logit threshold and 0/1
+"scores" by default (probabilities are added as "probs").
 """
 from __future__ import annotations
 
@@ -293,6 +294,8 @@ def train(data_loader, data_loader_eval, model, save_dir: str, num_epoch: int, r
             if max_iters and it >= max_iters:
                 break
         train_losses.append(float(loss.item()))
+        if hasattr(model, "check_comm"):  # FlatBucketDDP over xGMI: a peer timeout must raise, not diverge
+            model.check_comm()
         if (epoch % 5 == 0 or epoch == 100) and rank == 0:
             torch.save(inner.state_dict(), os.path.join(save_dir, "model-ep{}.pth".format(epoch)))
             print("model is saved in", save_dir)
@@ -375,9 +378,14 @@ def k_fold_cv(dataset, k: int, load_model: Optional[str], save_dir: str, num_epo
 
 
 def pre_generate_labels(model, dataset, model_name: Optional[str], out_dir: str = "outputs",
-                        json_path: str = "PPE_preds_160.json", threshold: float = 0.5, device=None):
+                        json_path: str = "PPE_preds_160.json", threshold: float = 0.5, device=None,
+                        threshold_probs: bool = False):
     """Reference ppe_main_ddp.py:310-396: predict every box, draw the boxes with their active attributes onto
-    the image, write the images and a JSON of boxes / scores."""
+    the image, write the images and a JSON of boxes / scores.
+
+    As the reference (its sigmoid is commented out), an attribute is on when its RAW LOGIT exceeds `threshold`,
+    and the JSON "scores" are those 0/1 decisions; "probs" adds the sigmoid probabilities.
+    ``threshold_probs=True`` thresholds the probabilities instead (logit > logit(threshold))."""
     from PIL import Image, ImageDraw
     device = device or next(model.parameters()).device
     if model_name:
@@ -391,16 +399,18 @@ def pre_generate_labels(model, dataset, model_name: Optional[str], out_dir: str 
         for i in range(len(dataset)):
             img, boxes, _, path = dataset[i]
             bb = torch.cat([torch.zeros(len(boxes), 1), boxes], 1)
-            p = torch.sigmoid(model(preprocess_img(img[None].to(device)), bb.to(device))).float().cpu().numpy()
+            logits = model(preprocess_img(img[None].to(device)), bb.to(device)).float().cpu()
+            probs = torch.sigmoid(logits).numpy()
+            p = ((probs if threshold_probs else logits.numpy()) > threshold).astype(np.int64)
             name = os.path.splitext(os.path.basename(str(path)))[0]
-            out[name] = {"bboxes": boxes.tolist(), "scores": p.tolist()}
+            out[name] = {"bboxes": boxes.tolist(), "scores": p.tolist(), "probs": probs.tolist()}
             canvas = Image.fromarray(img.permute(1, 2, 0).clamp(0, 255).byte().numpy())
             draw = ImageDraw.Draw(canvas)
             for (x1, y1, x2, y2), s in zip(boxes.tolist(), p):
                 if x2 - x1 == 10 and y2 - y1 == 10:  # padding box of person-free frames
                     continue
                 draw.rectangle([x1, y1, x2, y2], outline=(0, 255, 0), width=2)
-                draw.text((x1, max(y1 - 10, 0)), "h" + "".join(f"_{a}" for a, v in zip(attrs, s) if v > threshold),
+                draw.text((x1, max(y1 - 10, 0)), "h" + "".join(f"_{a}" for a, v in zip(attrs, s) if v),
                           fill=(255, 0, 0))
             canvas.save(os.path.join(out_dir, f"{name}.jpg"))
     with open(json_path, "w") as f:

@@ -6,6 +6,7 @@
     SGD, fp8 quantisation) -> ``_lib/libdca_ops.so``
   * ``csrc/comm_api.hip`` (generic xGMI one-shot / two-shot all-reduce for any model's flat buckets)
     -> ``_lib/libdca_comm.so``
+  * on request only (``build micro``): ``bench/micro/engine_micro.hip`` calibration kernels -> ``_lib/libdca_micro.so``
 hipcc cross-compiles without
 a GPU, so this runs on the CPU-only build host too.  The library links the HIP runtime and RCCL by SONAME
 (``libamdhip64.so.7``, ``librccl.so.1``); loaded after ``import torch`` it binds to the copies torch already
@@ -25,10 +26,13 @@ LIB_DIR = os.path.join(PKG_DIR, "_lib")
 ENGINE_LIB = os.path.join(LIB_DIR, "libdca_engine.so")
 OPS_LIB = os.path.join(LIB_DIR, "libdca_ops.so")
 COMM_LIB = os.path.join(LIB_DIR, "libdca_comm.so")
-_ENTRY = {"ops": ("ops_api.hip", OPS_LIB), "comm": ("comm_api.hip", COMM_LIB)}
+MICRO_LIB = os.path.join(LIB_DIR, "libdca_micro.so")
+_ENTRY = {"ops": ("ops_api.hip", OPS_LIB), "comm": ("comm_api.hip", COMM_LIB),
+          # calibration micro-benchmarks (bench/micro): diagnostic, never loaded by the framework itself
+          "micro": (os.path.join(os.path.dirname(PKG_DIR), "bench", "micro", "engine_micro.hip"), MICRO_LIB)}
 ARCH = os.environ.get("DCA_OFFLOAD_ARCH", "gfx950")
 # Variants: "" = production; "stamps" = diagnostic build with in-kernel phase stamps (-DDCA_STAMPS).
-VARIANTS = {"": [], "stamps": ["-DDCA_STAMPS"], "ops": [], "comm": []}
+VARIANTS = {"": [], "stamps": ["-DDCA_STAMPS"], "ops": [], "comm": [], "micro": []}
 
 
 def lib_path(variant: str = "") -> str:
@@ -50,7 +54,8 @@ def _sources():
 
 def _digest(variant: str = "") -> str:
     h = hashlib.sha256((ARCH + "|" + variant).encode())
-    for p in _sources():
+    extra = [_ENTRY["micro"][0]] if variant == "micro" else []
+    for p in _sources() + extra:
         with open(p, "rb") as f:
             h.update(os.path.basename(p).encode())
             h.update(f.read())
@@ -94,5 +99,6 @@ def build_all(force: bool = False, verbose: bool = False, variants=("", "ops", "
 
 
 if __name__ == "__main__":
-    for v in (["", "ops", "comm", "stamps"] if "--all" in sys.argv else ["", "ops", "comm"]):
+    wanted = [a for a in sys.argv[1:] if not a.startswith("--")]
+    for v in wanted or (["", "ops", "comm", "stamps", "micro"] if "--all" in sys.argv else ["", "ops", "comm"]):
         print(build(force="--force" in sys.argv, verbose=True, variant=v))

@@ -70,6 +70,7 @@ struct DcaInit {
   int comm_mode;        // world_size > 1: 0 = RCCL inside the step; 1 = external (host drives the all-reduce
                         // between dca_engine_run_part(.., 1) and (.., 2); test/debug path, no RCCL communicator);
                         // 2 = xGMI one-shot (peer-to-peer reads of IPC-mapped gradient slabs, fused with SGD)
+  int force_comm;       // comm_mode 0 at world_size 1: still run the RCCL all-reduce + averaging SGD (tests)
 };
 
 }  // extern "C"
@@ -95,6 +96,8 @@ struct Engine {
   unsigned long long ar_deadline = 300ull * 100000000ull;  // 300 s in 100 MHz ticks (a peer may be in host code)
   std::map<int, hipGraphExec_t> graphs;
   bool persistent = false;
+  bool comm_on = false;  // the step ends with a gradient collective (world_size > 1, or force_comm)
+  int resident = 0;      // persistent engine: workgroups guaranteed co-resident (occupancy x CUs)
   int pk_waves = 8;
   int xpack = 0;  // experimental one-XCD placement of the persistent kernel (env DCA_PK_XPACK=1)
   int staged_b = 0;  // persistent engine: batch slots of the current staging parity that hold the next batch
@@ -155,6 +158,7 @@ static int alloc_workspace(Engine* e) {
       {"LOSS", 16},                  {"STAMPS", 32 * 256 * 8 * 2 * 8},
       {"GRAN", 2 * 64 * 64 * 8},     {"EPOCH", 16},                   {"ERR", 16},
       {"TSLAB", bmax * WSLAB_N * 4}, {"BNG", 64 * 4}, {"IDS", 64 * 4}, {"W1B", 65536 * 2}, {"XCC", 64 * 8}, {"SIMG", 2 * 64 * 3072}, {"SLAB", 2 * 64 * 4}, {"GH", bmax * 8192 * 4}, {"SWF", 2 * 3 * 64 * 4 * 2},
+      {"COMMT", 16},
   };
   size_t total = 0;
   for (auto& r : regs) total += align_up(r.bytes, 256);
@@ -244,7 +248,7 @@ static int enqueue_xgmi_sgd(Engine* e, const Ctx& cx) {
 static int enqueue_step_persistent(Engine* e, int B, int part) {
   Ctx cx = e->base;
   cx.B = B;
-  const bool multi = e->in.world_size > 1;
+  const bool multi = e->comm_on;
   const bool rccl_overlap = e->split && multi && part == 0 && e->in.comm_mode == 0;  // fc all-reduce overlapped with the trunk backward
   if (part != 2) {
     pk::PkArgs pa = e->pa;
@@ -316,7 +320,7 @@ static int enqueue_step(Engine* e, int B, int part = 0) {
     size_t lds = (i == 0) ? e->s_dgrad0 : e->s_dgrad;
     lds = std::max(lds, (i < NBLK - 1) ? e->s_wgrad : e->s_fc);
     hipLaunchKernelGGL(e->kbwd, dim3(nparts + extra), blk, lds, e->st, cx, i);
-    if (i == NBLK - 1 && e->in.world_size > 1 && part == 0 && e->in.comm_mode == 0) {  // bucket A ready: overlap its all-reduce with the trunk bwd
+    if (i == NBLK - 1 && e->comm_on && part == 0 && e->in.comm_mode == 0) {  // bucket A ready: overlap its all-reduce with the trunk bwd
       HIPCK(hipEventRecord(e->evA, e->st));
       HIPCK(hipStreamWaitEvent(e->cst, e->evA, 0));
       NCCK(ncclAllReduce(cx.grads, cx.grads, BUCKET_A_END, ncclFloat32, ncclSum, e->comm, e->cst));
@@ -324,8 +328,8 @@ static int enqueue_step(Engine* e, int B, int part = 0) {
   }
   const int nother = cx.fuse_sgd ? 64 : 0;
   hipLaunchKernelGGL(e->kred, dim3(N_TRUNK_RED_WG + N_STEM_RED_WG + nother + 1), blk, 0, e->st, cx, nslab, nparts);
-  if (e->in.world_size > 1 && part == 0 && e->in.comm_mode == 2) return enqueue_xgmi_sgd(e, cx);
-  if (e->in.world_size > 1 && part == 0) {
+  if (e->comm_on && part == 0 && e->in.comm_mode == 2) return enqueue_xgmi_sgd(e, cx);
+  if (e->comm_on && part == 0) {
     HIPCK(hipEventRecord(e->evB, e->st));
     HIPCK(hipStreamWaitEvent(e->cst, e->evB, 0));
     NCCK(ncclAllReduce(cx.grads + OFF_CONVW, cx.grads + OFF_CONVW, FLAT_N - OFF_CONVW, ncclFloat32, ncclSum, e->comm,
@@ -340,152 +344,6 @@ static int enqueue_step(Engine* e, int B, int part = 0) {
 
 }  // namespace dca
 
-namespace dca {
-__global__ void k_mb_empty(int) {}
-// Memory round-trip calibration kernels (8 float4 = 32 KiB per workgroup unless noted):
-//   1: all WGs read the same 32 KiB (never written) + serial LDS reduce by thread 0
-//   2: one float per thread, WG-private, then store
-//   3: WG-private 32 KiB (never written), per-thread sums stored
-//   4: WG-private 32 KiB written by the PREVIOUS kernel at the same WG index (ping-pong)
-//   5: like 4 but reading the region written by WG (w+1) % grid (another XCD under round-robin dispatch)
-//   6: every WG reads the same 32 KiB that WG 0 of the previous kernel wrote (BN-partials pattern)
-__global__ void __launch_bounds__(NT) k_mb_load(const f32x4* src, f32x4* dst, int kind) {
-  const int t = threadIdx.x, w = blockIdx.x, g = gridDim.x;
-  if (kind == 2) {
-    const float v = ((const float*)src)[w * NT + t];
-    ((float*)dst)[w * NT + t] = v + 1.f;
-    return;
-  }
-  const int base = kind == 1 || kind == 6 ? 0 : (kind == 5 ? ((w + 1) % g) : w) * 2048;
-  f32x4 v[8];
-#pragma unroll
-  for (int m = 0; m < 8; ++m) v[m] = src[base + t + NT * m];
-  if (kind == 1) {
-    float s = 0.f;
-#pragma unroll
-    for (int m = 0; m < 8; ++m) s += v[m].x + v[m].y + v[m].z + v[m].w;
-    __shared__ float r[NT];
-    r[t] = s;
-    __syncthreads();
-    if (t == 0) {
-      float a = 0.f;
-      for (int k = 0; k < NT; ++k) a += r[k];
-      ((float*)dst)[w] = a;
-    }
-    return;
-  }
-  if (kind == 3) {
-    f32x4 s = v[0];
-#pragma unroll
-    for (int m = 1; m < 8; ++m) s += v[m];
-    dst[w * NT + t] = s;
-    return;
-  }
-  if (kind == 6 && w != 0) {
-    f32x4 s = v[0];
-#pragma unroll
-    for (int m = 1; m < 8; ++m) s += v[m];
-    dst[4096 + w * NT + t] = s;  // scratch, away from the region the next kernel reads
-    return;
-  }
-#pragma unroll
-  for (int m = 0; m < 8; ++m) dst[(kind == 6 ? 0 : w * 2048) + t + NT * m] = v[m] + 1.f;
-}
-// In-kernel all-gather of 64 floats per workgroup among G co-resident workgroups, `rounds` times
-// (the BN-statistics exchange of a persistent design).  Data-as-flag granules {tag, value} (8-byte relaxed
-// agent-scope atomic stores/loads, i.e. sc1 write-through / L2-bypassing): no fences needed.  Parity
-// double-buffered by round.  Every spin is bounded; a timeout sets *err and the kernel still completes.
-template <int NTH>
-__global__ void __launch_bounds__(NTH) k_mb_xchg(unsigned long long* gran, unsigned* err, int rounds, int sleep) {
-  const int t = threadIdx.x, w = blockIdx.x, G = gridDim.x;
-  __shared__ float red[64];
-  float keep = 0.f;
-  for (int r = 0; r < rounds; ++r) {
-    const unsigned long long tag = (unsigned long long)(r + 1) << 32;
-    unsigned long long* buf = gran + (size_t)(r & 1) * G * 64;
-    if (t < 64) {
-      const float v = (float)(w + t) + keep;
-      __hip_atomic_store(buf + w * 64 + t, tag | __float_as_uint(v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      float acc = 0.f;
-      for (unsigned spins = 0;; ++spins) {
-        bool ok = true;
-        acc = 0.f;
-        for (int k = 0; k < G; ++k) {
-          const unsigned long long x = __hip_atomic_load(buf + k * 64 + t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          ok &= (x & 0xffffffff00000000ull) == tag;
-          acc += __uint_as_float((unsigned)x);
-        }
-        if (__all(ok)) break;
-        if (spins > (1u << 20)) {
-          atomicOr(err, 1u);
-          break;
-        }
-        if (sleep) __builtin_amdgcn_s_sleep(1);
-      }
-      red[t] = acc;
-    }
-    __syncthreads();
-    keep = red[t & 63] * 1e-9f;
-    __syncthreads();
-  }
-  if (t == 0 && keep == 12345.f) err[1] = 1;  // keep the chain live
-}
-// Same exchange, but the sweep is spread over all waves of the workgroup and uses plain (non-volatile)
-// sc1 buffer loads, so every wave has all of its granule loads in flight at once.
-template <int NTH>
-__global__ void __launch_bounds__(NTH) k_mb_xchg2(unsigned long long* gran, unsigned* err, int rounds) {
-  constexpr int NW = NTH / 64, KMAX = 8;
-  const int t = threadIdx.x, lane = t & 63, wave = t >> 6, w = blockIdx.x, G = gridDim.x;
-  __shared__ float red[NW][64];
-  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(gran, (short)0, 2 * G * 64 * 8, 0x00020000);
-  float keep = 0.f;
-  for (int r = 0; r < rounds; ++r) {
-    const unsigned tag = (unsigned)(r + 1);
-    const int boff = (r & 1) * G * 64;
-    if (wave == 0) {
-      const float v = (float)(w + lane) + keep;
-      __hip_atomic_store(gran + boff + w * 64 + lane, ((unsigned long long)tag << 32) | __float_as_uint(v),
-                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    float acc = 0.f;
-    for (unsigned spins = 0;; ++spins) {
-      bool ok = true;
-      acc = 0.f;
-      unsigned lo[KMAX], hi[KMAX];
-#pragma unroll
-      for (int kk = 0; kk < KMAX; ++kk) {
-        const int k = wave + NW * kk;
-        if (k < G) {
-          const auto x = __builtin_amdgcn_raw_buffer_load_b64(rs, (boff + k * 64 + lane) * 8, 0, 16);
-          lo[kk] = x[0];
-          hi[kk] = x[1];
-        } else {
-          lo[kk] = 0u;
-          hi[kk] = tag;
-        }
-      }
-#pragma unroll
-      for (int kk = 0; kk < KMAX; ++kk) {
-        ok &= hi[kk] == tag;
-        acc += __uint_as_float(lo[kk]);
-      }
-      if (__all(ok)) break;
-      if (spins > (1u << 20)) {
-        atomicOr(err, 1u);
-        break;
-      }
-    }
-    red[wave][lane] = acc;
-    __syncthreads();
-    float s = 0.f;
-#pragma unroll
-    for (int k = 0; k < NW; ++k) s += red[k][lane];
-    keep = s * 1e-9f;
-    __syncthreads();
-  }
-  if (t == 0 && keep == 12345.f) err[1] = 1;
-}
-}  // namespace dca
 
 using dca::Engine;
 
@@ -493,7 +351,7 @@ extern "C" {
 
 const char* dca_last_error() { return g_err.c_str(); }
 
-int dca_abi_version() { return 3; }  // bump with every DcaInit / signature change
+int dca_abi_version() { return 4; }  // bump with every DcaInit / signature change
 
 int dca_nccl_unique_id(char* out128) {
   ncclUniqueId id;
@@ -504,21 +362,21 @@ int dca_nccl_unique_id(char* out128) {
 }
 
 static int prime_ids(Engine* e);
+static void engine_free(Engine* e);
 
-int dca_engine_create(const DcaInit* in, int n_indices, void** out) {
-  Engine* e = new Engine();
+// Body of dca_engine_create; on failure the caller frees whatever was acquired (engine_free handles a partially
+// built engine), so every early return of HIPCK / NCCK is leak-free.
+static int engine_init(Engine* e, const DcaInit* in, int n_indices) {
   e->in = *in;
   e->bf = in->bf16 != 0;
   e->R = in->rows;
   e->RW = e->bf ? 16 : 8;
   if (in->bmax < 1 || in->bmax > dca::BMAX_LIMIT) {
     g_err = "batch_max must be in [1, 64]";
-    delete e;
     return -1;
   }
   if (e->R != 2 && e->R != 4) {
     g_err = "rows must be 2 or 4";
-    delete e;
     return -1;
   }
   e->TPI = 16 / e->R;
@@ -528,6 +386,9 @@ int dca_engine_create(const DcaInit* in, int n_indices, void** out) {
     return -1;
   }
   e->pk_waves = 8;
+  // comm_on: the step ends with a gradient collective + the averaging SGD kernel.  force_comm runs that path at
+  // world_size 1 (a 1-rank RCCL communicator) so the graph-captured collective is testable on one GPU.
+  e->comm_on = in->world_size > 1 || (in->force_comm && in->comm_mode == 0);
   {
     const char* xp = getenv("DCA_PK_XPACK");
     e->xpack = xp && xp[0] == '1';
@@ -539,27 +400,43 @@ int dca_engine_create(const DcaInit* in, int n_indices, void** out) {
   }
   if (e->persistent && !e->bf) {
     g_err = "the persistent engine is bf16-only (fp32 MFMA needs all CUs: use the multi-kernel engine)";
-    delete e;
     return -1;
   }
   if (e->bf && e->R == 4) dca::bind_kernels<true, 4, 16>(e);
   else if (e->bf) dca::bind_kernels<true, 2, 16>(e);
   else if (e->R == 4) dca::bind_kernels<false, 4, 8>(e);
   else dca::bind_kernels<false, 2, 8>(e);
-  if (dca::set_lds_limits(e)) { delete e; return -1; }
+  if (dca::set_lds_limits(e)) return -1;
+  if (e->persistent) {
+    // Co-residency: the persistent step spins on in-kernel exchanges, so every one of its bmax workgroups must be
+    // resident at once.  The occupancy answer can be one block per CU high near register edges (MI355X guide,
+    // Residency): require a margin of one block per CU below it.
+    int dev = 0, ncu = 0, per_cu = 0;
+    HIPCK(hipGetDevice(&dev));
+    HIPCK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
+    HIPCK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)dca::pk::k_pk_step<8>, 64 * 8,
+                                                      dca::pk::Plan::TOTAL));
+    const int resident = (per_cu > 1 ? per_cu - 1 : per_cu) * ncu;
+    if (resident < in->bmax) {
+      g_err = "persistent engine: " + std::to_string(in->bmax) + " workgroups cannot all be resident (" +
+              std::to_string(per_cu) + " per CU x " + std::to_string(ncu) + " CUs); use the multi-kernel engine";
+      return -1;
+    }
+    e->resident = resident;
+  }
   HIPCK(hipStreamCreateWithFlags(&e->st, hipStreamNonBlocking));
   HIPCK(hipStreamCreateWithFlags(&e->cst, hipStreamNonBlocking));
   HIPCK(hipEventCreateWithFlags(&e->evA, hipEventDisableTiming));
   HIPCK(hipEventCreateWithFlags(&e->evB, hipEventDisableTiming));
   HIPCK(hipEventCreateWithFlags(&e->evC, hipEventDisableTiming));
-  if (dca::alloc_workspace(e)) { delete e; return -1; }
+  if (dca::alloc_workspace(e)) return -1;
   e->n_indices = n_indices;
   HIPCK(hipMalloc(&e->indices, sizeof(int) * (size_t)std::max(n_indices, 1)));
   HIPCK(hipMemset(e->indices, 0, sizeof(int) * (size_t)std::max(n_indices, 1)));
   dca::Ctx& c = e->base;
   c.ws = in->world_size;
   c.rank = in->rank;
-  c.fuse_sgd = in->world_size == 1 ? 1 : 0;
+  c.fuse_sgd = e->comm_on ? 0 : 1;
   c.lr = in->lr;
   c.bn_mom = in->bn_mom;
   c.bn_eps = in->bn_eps;
@@ -574,6 +451,7 @@ int dca_engine_create(const DcaInit* in, int n_indices, void** out) {
   c.indices = e->indices;
   c.n_data = in->n_data;
   c.n_idx = std::max(n_indices, 1);
+  e->peers.ticks = (unsigned long long*)e->regions["COMMT"];
   if (in->world_size > 1 && in->comm_mode == 2) {
     if (in->world_size > dca::xg::MAXR) {
       g_err = "xGMI all-reduce: world_size > 8 (one node) -- use RCCL";
@@ -589,36 +467,51 @@ int dca_engine_create(const DcaInit* in, int n_indices, void** out) {
     const char* dl = getenv("DCA_XGMI_TIMEOUT_S");
     if (dl) e->ar_deadline = (unsigned long long)(atof(dl) * 1e8);
   }
-  if (in->world_size > 1 && in->comm_mode == 0) {
+  if (e->comm_on && in->comm_mode == 0) {
     ncclUniqueId id;
-    memcpy(&id, in->nccl_id, 128);
+    if (in->world_size == 1) NCCK(ncclGetUniqueId(&id));  // force_comm: a private 1-rank communicator
+    else memcpy(&id, in->nccl_id, 128);
     NCCK(ncclCommInitRank(&e->comm, in->world_size, id, in->rank));
   }
   if (prime_ids(e)) return -1;
   HIPCK(hipStreamSynchronize(e->st));
+  return 0;
+}
+
+int dca_engine_create(const DcaInit* in, int n_indices, void** out) {
+  Engine* e = new Engine();
+  if (engine_init(e, in, n_indices)) {
+    const std::string err = g_err;
+    engine_free(e);
+    g_err = err;
+    return -1;
+  }
   *out = e;
   return 0;
 }
 
-int dca_engine_destroy(void* h) {
-  Engine* e = (Engine*)h;
-  if (!e) return 0;
-  (void)hipStreamSynchronize(e->st);
-  (void)hipStreamSynchronize(e->cst);
+// Release everything an Engine holds; safe on a partially initialised engine.
+static void engine_free(Engine* e) {
+  if (e->st) (void)hipStreamSynchronize(e->st);
+  if (e->cst) (void)hipStreamSynchronize(e->cst);
   for (auto& kv : e->graphs) (void)hipGraphExecDestroy(kv.second);
   if (e->comm) (void)ncclCommDestroy(e->comm);
   for (int q = 0; q < dca::xg::MAXR; ++q)
     if (e->peers_open && q != e->in.rank && q < e->in.world_size && e->peers.base[q])
       (void)hipIpcCloseMemHandle(e->peers.base[q]);
   if (e->xregion) (void)hipFree(e->xregion);
-  (void)hipFree(e->wsp);
-  (void)hipFree(e->indices);
-  (void)hipEventDestroy(e->evA);
-  (void)hipEventDestroy(e->evB);
-  (void)hipEventDestroy(e->evC);
-  (void)hipStreamDestroy(e->st);
-  (void)hipStreamDestroy(e->cst);
+  if (e->wsp) (void)hipFree(e->wsp);
+  if (e->indices) (void)hipFree(e->indices);
+  if (e->evA) (void)hipEventDestroy(e->evA);
+  if (e->evB) (void)hipEventDestroy(e->evB);
+  if (e->evC) (void)hipEventDestroy(e->evC);
+  if (e->st) (void)hipStreamDestroy(e->st);
+  if (e->cst) (void)hipStreamDestroy(e->cst);
   delete e;
+}
+
+int dca_engine_destroy(void* h) {
+  if (h) engine_free((Engine*)h);
   return 0;
 }
 
@@ -693,6 +586,39 @@ int dca_engine_read_loss(void* h, double* loss, int* steps, int reset) {
 // Enqueue `nsteps` training steps of batch B.  use_graph: replay a captured hipGraph (captured on first use).
 constexpr int GRAPH_CHUNK = 16;  // steps per graph replay
 
+// The executable graph of `chunk` consecutive steps of batch B (captured and instantiated on first use).
+static hipGraphExec_t capture_graph(Engine* e, int B, int chunk) {
+  const int key = B * 1024 + chunk;
+  auto it = e->graphs.find(key);
+  if (it != e->graphs.end()) return it->second;
+  hipGraph_t g;
+  hipError_t ec = hipStreamBeginCapture(e->st, hipStreamCaptureModeThreadLocal);
+  if (ec != hipSuccess) {
+    g_err = std::string("hipStreamBeginCapture: ") + hipGetErrorString(ec);
+    return nullptr;
+  }
+  int rc = 0;
+  for (int s = 0; s < chunk && !rc; ++s) rc = dca::enqueue_step(e, B);
+  ec = hipStreamEndCapture(e->st, &g);
+  if (rc) {
+    if (ec == hipSuccess) (void)hipGraphDestroy(g);
+    return nullptr;
+  }
+  if (ec != hipSuccess) {
+    g_err = std::string("hipStreamEndCapture: ") + hipGetErrorString(ec);
+    return nullptr;
+  }
+  hipGraphExec_t ex;
+  ec = hipGraphInstantiate(&ex, g, nullptr, nullptr, 0);
+  (void)hipGraphDestroy(g);
+  if (ec != hipSuccess) {
+    g_err = std::string("hipGraphInstantiate: ") + hipGetErrorString(ec);
+    return nullptr;
+  }
+  e->graphs.emplace(key, ex);
+  return ex;
+}
+
 int dca_engine_run(void* h, int B, int nsteps, int use_graph) {
   Engine* e = (Engine*)h;
   if (B < 1 || B > e->in.bmax) {
@@ -717,27 +643,39 @@ int dca_engine_run(void* h, int B, int nsteps, int use_graph) {
   for (const int chunk : {GRAPH_CHUNK, 1}) {
     const int reps = (nsteps - done) / chunk;
     if (reps == 0) continue;
-    const int key = B * 1024 + chunk;
-    auto it = e->graphs.find(key);
-    if (it == e->graphs.end()) {
-      hipGraph_t g;
-      HIPCK(hipStreamBeginCapture(e->st, hipStreamCaptureModeThreadLocal));
-      int rc = 0;
-      for (int s = 0; s < chunk && !rc; ++s) rc = dca::enqueue_step(e, B);
-      const hipError_t ec = hipStreamEndCapture(e->st, &g);
-      if (rc) return -1;
-      if (ec != hipSuccess) {
-        g_err = std::string("hipStreamEndCapture: ") + hipGetErrorString(ec);
-        return -1;
-      }
-      hipGraphExec_t ex;
-      HIPCK(hipGraphInstantiate(&ex, g, nullptr, nullptr, 0));
-      HIPCK(hipGraphDestroy(g));
-      it = e->graphs.emplace(key, ex).first;
-    }
-    for (int r = 0; r < reps; ++r) HIPCK(hipGraphLaunch(it->second, e->st));
+    hipGraphExec_t ex = capture_graph(e, B, chunk);
+    if (ex == nullptr) return -1;
+    for (int r = 0; r < reps; ++r) HIPCK(hipGraphLaunch(ex, e->st));
     done += reps * chunk;
   }
+  return 0;
+}
+
+// Capture (without running) the graphs dca_engine_run replays for batch B, so a later timed run never pays
+// capture + instantiate.  Synchronous.
+int dca_engine_precapture(void* h, int B) {
+  Engine* e = (Engine*)h;
+  if (B < 1 || B > e->in.bmax) {
+    g_err = "batch out of range";
+    return -1;
+  }
+  if (e->in.world_size > 1 && e->in.comm_mode == 1) return 0;  // external all-reduce: eager only
+  for (const int chunk : {GRAPH_CHUNK, 1})
+    if (capture_graph(e, B, chunk) == nullptr) return -1;
+  HIPCK(hipStreamSynchronize(e->st));
+  return 0;
+}
+
+// Time spent inside the gradient all-reduce kernel (xGMI path: workgroup 0 of k_xgmi_ar_sgd, entry to exit,
+// including the wait for the slowest peer), summed since the last reset: microseconds and calls.
+int dca_engine_comm_time(void* h, double* us, long long* calls, int reset) {
+  Engine* e = (Engine*)h;
+  HIPCK(hipStreamSynchronize(e->st));
+  unsigned long long v[2] = {0, 0};
+  HIPCK(hipMemcpy(v, e->peers.ticks, sizeof(v), hipMemcpyDeviceToHost));
+  *us = (double)v[0] / 100.0;  // s_memrealtime: 100 MHz
+  *calls = (long long)v[1];
+  if (reset) HIPCK(hipMemset(e->peers.ticks, 0, sizeof(v)));
   return 0;
 }
 
@@ -863,157 +801,5 @@ void* dca_engine_region(void* h, const char* name) {
 
 size_t dca_engine_workspace_bytes(void* h) { return ((Engine*)h)->ws_bytes; }
 
-// Persistent-exchange calibration: G workgroups of `nth` threads, `rounds` all-gather rounds.
-// Writes the kernel time (us, median of `iters`) and the timeout flag.
-int dca_microbench_xchg(int G, int nth, int rounds, int iters, int sleep, float* us, int* err_out) {
-  hipStream_t s;
-  HIPCK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
-  unsigned long long* gran;
-  unsigned* err;
-  HIPCK(hipMalloc(&gran, (size_t)2 * G * 64 * 8));
-  HIPCK(hipMalloc(&err, 16));
-  HIPCK(hipMemset(err, 0, 16));
-  hipEvent_t a, b;
-  HIPCK(hipEventCreate(&a));
-  HIPCK(hipEventCreate(&b));
-  float best = 1e30f;
-  for (int it = 0; it < iters; ++it) {
-    HIPCK(hipMemsetAsync(gran, 0, (size_t)2 * G * 64 * 8, s));
-    HIPCK(hipEventRecord(a, s));
-    if (sleep == 2 && nth == 1024) hipLaunchKernelGGL(dca::k_mb_xchg2<1024>, dim3(G), dim3(1024), 0, s, gran, err, rounds);
-    else if (sleep == 2) hipLaunchKernelGGL(dca::k_mb_xchg2<256>, dim3(G), dim3(256), 0, s, gran, err, rounds);
-    else if (nth == 1024) hipLaunchKernelGGL(dca::k_mb_xchg<1024>, dim3(G), dim3(1024), 0, s, gran, err, rounds, sleep);
-    else hipLaunchKernelGGL(dca::k_mb_xchg<256>, dim3(G), dim3(256), 0, s, gran, err, rounds, sleep);
-    HIPCK(hipEventRecord(b, s));
-    HIPCK(hipEventSynchronize(b));
-    float ms = 0.f;
-    HIPCK(hipEventElapsedTime(&ms, a, b));
-    best = std::min(best, ms);
-  }
-  unsigned herr[2];
-  HIPCK(hipMemcpy(herr, err, 8, hipMemcpyDeviceToHost));
-  *us = best * 1e3f;
-  *err_out = (int)herr[0];
-  (void)hipFree(gran);
-  (void)hipFree(err);
-  (void)hipEventDestroy(a);
-  (void)hipEventDestroy(b);
-  (void)hipStreamDestroy(s);
-  return 0;
-}
-
-// xGMI all-reduce protocol cost without peers in other processes: W ranks simulated in THIS process, one
-// stream and one uncached region each (so all ranks' kernels are co-resident, as on W separate GPUs), `iters`
-// all-reduces of FLAT_N floats per rank.  Writes mean microseconds per all-reduce; *err_out = timeout flag.
-int dca_microbench_xgmi(int W, int iters, float* us, int* err_out) {
-  // W <= 3: with GPU_MAX_HW_QUEUES=4 a 4th user stream can share a hardware queue with another, which serialises
-  // two ranks' kernels and deadlocks the flag wait until its deadline (measured: the W=4 run never finished).
-  if (W < 1 || W > dca::xg::MAXR || W > 3 || iters < 1) {
-    g_err = "microbench_xgmi: 1 <= W <= 3 (co-resident streams per process), iters >= 1";
-    return -1;
-  }
-  hipStream_t st[3];
-  char* reg[3];
-  float *src, *dst;
-  unsigned* err;
-  dca::xg::Peers P{};
-  for (int q = 0; q < W; ++q) {
-    HIPCK(hipStreamCreateWithFlags(&st[q], hipStreamNonBlocking));
-    HIPCK(hipExtMallocWithFlags((void**)&reg[q], dca::xg::REGION_BYTES, hipDeviceMallocUncached));
-    HIPCK(hipMemset(reg[q], 0, dca::xg::REGION_BYTES));
-    P.base[q] = reg[q];
-  }
-  HIPCK(hipMalloc(&src, sizeof(float) * dca::FLAT_ALLOC * W));
-  HIPCK(hipMalloc(&dst, sizeof(float) * dca::FLAT_ALLOC * W));
-  HIPCK(hipMemset(src, 0, sizeof(float) * dca::FLAT_ALLOC * W));
-  HIPCK(hipMalloc(&err, 16));
-  HIPCK(hipMemset(err, 0, 16));
-  HIPCK(hipDeviceSynchronize());
-  hipEvent_t a, b;
-  HIPCK(hipEventCreate(&a));
-  HIPCK(hipEventCreate(&b));
-  float best = 1e30f;
-  for (int rep = 0; rep < 3; ++rep) {
-    HIPCK(hipDeviceSynchronize());
-    HIPCK(hipEventRecord(a, st[0]));
-    for (int q = 1; q < W; ++q) HIPCK(hipStreamWaitEvent(st[q], a, 0));
-    for (int i = 0; i < iters; ++i)
-      for (int q = 0; q < W; ++q) {
-        dca::Ctx cx{};
-        cx.ws = W;
-        cx.rank = q;
-        hipLaunchKernelGGL(dca::xg::k_xgmi_ar_sgd<true>, dim3(dca::xg::AR_NB), dim3(dca::xg::AR_T), 0, st[q], cx, P,
-                           (const float*)(src + (size_t)q * dca::FLAT_ALLOC), dst + (size_t)q * dca::FLAT_ALLOC, err,
-                           0, 2ull * 100000000ull);
-      }
-    for (int q = 1; q < W; ++q) {
-      hipEvent_t e;
-      HIPCK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-      HIPCK(hipEventRecord(e, st[q]));
-      HIPCK(hipStreamWaitEvent(st[0], e, 0));
-      (void)hipEventDestroy(e);
-    }
-    HIPCK(hipEventRecord(b, st[0]));
-    HIPCK(hipEventSynchronize(b));
-    float ms = 0.f;
-    HIPCK(hipEventElapsedTime(&ms, a, b));
-    best = std::min(best, 1e3f * ms / (float)iters);
-  }
-  unsigned h = 0;
-  HIPCK(hipMemcpy(&h, err, sizeof(unsigned), hipMemcpyDeviceToHost));
-  *us = best;
-  *err_out = h ? 1 : 0;
-  for (int q = 0; q < W; ++q) {
-    (void)hipStreamDestroy(st[q]);
-    (void)hipFree(reg[q]);
-  }
-  (void)hipFree(src);
-  (void)hipFree(dst);
-  (void)hipFree(err);
-  (void)hipEventDestroy(a);
-  (void)hipEventDestroy(b);
-  return 0;
-}
-
-// Launch-floor calibration: a hipGraph of `nk` dependent kernels of `kind` (0 empty; 1..6 see k_mb_load)
-// with `grid` workgroups, replayed `iters` times.  Writes microseconds per kernel to *us.
-int dca_microbench(int kind, int nk, int grid, int iters, float* us) {
-  hipStream_t s;
-  HIPCK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
-  char* buf;
-  const size_t half = (size_t)(grid + 1) * 2048 * 16 + (1 << 16);
-  HIPCK(hipMalloc(&buf, 2 * half));
-  HIPCK(hipMemset(buf, 0, 2 * half));
-  hipGraph_t g;
-  HIPCK(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
-  for (int k = 0; k < nk; ++k) {
-    const bool odd = (k & 1) && kind >= 4;
-    const dca::f32x4* src = (const dca::f32x4*)(buf + (odd ? half : 0));
-    dca::f32x4* dst = (dca::f32x4*)(buf + (odd ? 0 : half));
-    if (kind == 0) hipLaunchKernelGGL(dca::k_mb_empty, dim3(grid), dim3(dca::NT), 0, s, k);
-    else hipLaunchKernelGGL(dca::k_mb_load, dim3(grid), dim3(dca::NT), 0, s, src, dst, kind);
-  }
-  HIPCK(hipStreamEndCapture(s, &g));
-  hipGraphExec_t ex;
-  HIPCK(hipGraphInstantiate(&ex, g, nullptr, nullptr, 0));
-  hipEvent_t a, b;
-  HIPCK(hipEventCreate(&a));
-  HIPCK(hipEventCreate(&b));
-  for (int w = 0; w < 3; ++w) HIPCK(hipGraphLaunch(ex, s));
-  HIPCK(hipEventRecord(a, s));
-  for (int it = 0; it < iters; ++it) HIPCK(hipGraphLaunch(ex, s));
-  HIPCK(hipEventRecord(b, s));
-  HIPCK(hipEventSynchronize(b));
-  float ms = 0.f;
-  HIPCK(hipEventElapsedTime(&ms, a, b));
-  *us = 1e3f * ms / (float)(iters * nk);
-  (void)hipGraphExecDestroy(ex);
-  (void)hipGraphDestroy(g);
-  (void)hipEventDestroy(a);
-  (void)hipEventDestroy(b);
-  (void)hipFree(buf);
-  (void)hipStreamDestroy(s);
-  return 0;
-}
 
 }  // extern "C"

@@ -42,7 +42,8 @@ static_assert(MAXR * AR_NB * 4 <= (int)FLAG_BYTES, "flag area too small");
 static_assert(FLAT_N % 4 == 0, "flat buffer must be float4 granular");
 
 struct Peers {
-  char* base[MAXR];  // every rank's shared region, mapped into this process (own one at base[rank])
+  char* base[MAXR];           // every rank's shared region, mapped into this process (own one at base[rank])
+  unsigned long long* ticks;  // optional [2]: s_memrealtime ticks spent in the kernel by workgroup 0, calls
 };
 
 typedef unsigned v4u __attribute__((ext_vector_type(4)));
@@ -68,6 +69,7 @@ __global__ void __launch_bounds__(AR_T) k_xgmi_ar_sgd(Ctx cx, Peers P, const flo
   const bool live = v < AR_V4;
   int* myflags = (int*)P.base[me];
   __shared__ int s_ep;
+  const unsigned long long t_in = __builtin_amdgcn_s_memrealtime();
   if (t == 0) s_ep = flag_load(myflags + me * AR_NB + b) + 1;
   const f32x4 g = live ? *(const f32x4*)(src + 4 * v) : f32x4{0.f, 0.f, 0.f, 0.f};
   __syncthreads();
@@ -91,6 +93,10 @@ __global__ void __launch_bounds__(AR_T) k_xgmi_ar_sgd(Ctx cx, Peers P, const flo
     }
   }
   __syncthreads();
+  if (b == 0 && t == 0 && P.ticks != nullptr) {  // exposed all-reduce time of this rank (metrics)
+    atomicAdd(P.ticks, __builtin_amdgcn_s_memrealtime() - t_in);
+    atomicAdd(P.ticks + 1, 1ull);
+  }
   if (!live) return;
   // All W loads in flight at once (one per peer link), cache-bypassing: unconditional loads (ranks >= W re-read
   // rank 0, which is never summed) so the compiler issues them back to back instead of branching around each one.

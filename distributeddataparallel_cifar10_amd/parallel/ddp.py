@@ -105,6 +105,11 @@ class FusedDDPTrainer:
             eng.close()
         return None
 
+    def check_comm(self) -> None:
+        """Raise if the engine recorded an exchange / all-reduce timeout (synchronous; called at epoch ends)."""
+        if self.engine is not None:
+            self.engine.check_errors()
+
     def close(self):
         if self.engine is None:
             return

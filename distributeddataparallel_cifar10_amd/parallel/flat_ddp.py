@@ -105,6 +105,9 @@ class FlatBucketDDP(nn.Module):
         self._works: list = []
         self._callback_queued = False
         self.bucket_fire_order: List[int] = []  # for tests: order in which buckets were launched
+        self._sync_next_forward = True
+        self.timing = False  # True: record the comm-stream span of every step (comm_time(); metrics)
+        self._comm_events: list = []
         self._sync_module_states()  # CC3
         self.comm, self.xgmi, self._comm_stream = "process_group" if self.world_size > 1 else "none", None, None
         self._wire, self._algo = wire, algo
@@ -181,6 +184,12 @@ class FlatBucketDDP(nn.Module):
     def _launch(self, bi: int) -> None:
         s, e, _ = self.buckets[bi]
         seg = self.flat_grad[s:e]
+        if self.timing and seg.is_cuda and self.world_size > 1 and not self.bucket_fire_order:
+            ev = torch.cuda.Event(enable_timing=True)  # first bucket of the step: comm span starts
+            cs = self._side_stream()
+            cs.wait_stream(torch.cuda.current_stream(seg.device))
+            ev.record(cs)
+            self._comm_events.append([ev, None])
         if self.world_size == 1:  # nothing to reduce: only the fused optimizer update (side stream on a GPU)
             if seg.is_cuda:
                 cs = self._side_stream()
@@ -227,6 +236,10 @@ class FlatBucketDDP(nn.Module):
             if s is not None:  # CPU: the fused update of a bucket after its (gloo) all-reduce
                 self._fused_opt._update_slice(s, e)
         if self._comm_stream is not None:
+            if self._comm_events and self._comm_events[-1][1] is None:
+                ev = torch.cuda.Event(enable_timing=True)
+                ev.record(self._comm_stream)
+                self._comm_events[-1][1] = ev
             torch.cuda.current_stream(self.flat_grad.device).wait_stream(self._comm_stream)
         self._works = []
         self._callback_queued = False
@@ -238,14 +251,32 @@ class FlatBucketDDP(nn.Module):
 
     # ---- module API -------------------------------------------------------------------------------------------
     def forward(self, *args, **kwargs):
-        if self.world_size > 1 and self.broadcast_buffers:
-            self._broadcast_buffers_now()  # CC4
+        # CC4 with torch DDP's exact rule (nn/parallel/distributed.py require_forward_param_sync): a forward
+        # broadcasts rank 0's buffers unless the PREVIOUS forward ran without autograd, so in an eval loop under
+        # no_grad only the first batch runs a collective (a rank evaluating alone must use .module)
+        if self.world_size > 1 and self.broadcast_buffers and self._sync_next_forward:
+            self._broadcast_buffers_now()
         self._reset_pending()
         self.bucket_fire_order = []
-        return self.module(*args, **kwargs)
+        out = self.module(*args, **kwargs)
+        self._sync_next_forward = torch.is_grad_enabled()
+        return out
 
     def zero_grad(self, set_to_none: bool = False) -> None:  # grads stay views of the flat buffer
         self.flat_grad.zero_()
+
+    def comm_time(self, reset: bool = True) -> tuple:
+        """(microseconds, steps) the gradient collectives spanned on the comm stream -- first bucket launched to
+        backward finished -- over the timed steps since the last reset (``timing=True``; synchronises)."""
+        tot, n = 0.0, 0
+        for a, b in self._comm_events:
+            if b is not None:
+                b.synchronize()
+                tot += a.elapsed_time(b) * 1e3
+                n += 1
+        if reset:
+            self._comm_events = []
+        return tot, n
 
     def check_comm(self) -> None:
         """Raise if the xGMI all-reduce recorded a peer timeout (synchronous; call at log points)."""

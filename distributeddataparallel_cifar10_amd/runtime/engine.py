@@ -63,6 +63,7 @@ class _DcaInit(ctypes.Structure):
         ("debug", ctypes.c_int),
         ("pk_waves", ctypes.c_int),
         ("comm_mode", ctypes.c_int),
+        ("force_comm", ctypes.c_int),
     ]
 
 
@@ -118,6 +119,8 @@ class EngineConfig:
                                  # "external" (host all-reduce between step parts; tests / any torch backend)
     bn_momentum: float = 0.1
     bn_eps: float = 1e-5
+    force_comm: bool = False     # comm="rccl" at world_size 1: still run the graph-captured RCCL all-reduce and the
+                                 # averaging SGD kernel (a 1-rank communicator) -- exercises that path on one GPU
 
 
 class NetResDeepEngine:
@@ -164,7 +167,7 @@ class NetResDeepEngine:
             bn_mom=float(cfg.bn_momentum), bn_eps=float(cfg.bn_eps), world_size=int(cfg.world_size),
             rank=int(cfg.rank), nccl_id=ctypes.cast(self._nccl_id, ctypes.c_char_p),
             persistent=1 if cfg.persistent else 0, debug=1 if cfg.debug else 0, pk_waves=int(cfg.pk_waves),
-            comm_mode={"rccl": 0, "external": 1, "xgmi": 2}[cfg.comm],
+            comm_mode={"rccl": 0, "external": 1, "xgmi": 2}[cfg.comm], force_comm=1 if cfg.force_comm else 0,
         )
         self._init = init
         self.max_indices = int(max_indices or self.data.shape[0])
@@ -199,19 +202,28 @@ class NetResDeepEngine:
             raise ValueError("need one 64-byte handle per rank")
         native.check(self.lib.dca_engine_ipc_open(self.h, blob, int(self.cfg.world_size)), "dca_engine_ipc_open")
 
-    def xgmi_selftest(self, timeout_s: float = 20.0) -> bool:
-        """Collective: all-reduce a rank-dependent pattern through the xGMI protocol and check the sum exactly.
-        Every rank must call it (it advances the shared epochs like a training step does)."""
+    def xgmi_selftest(self, timeout_s: float = 20.0, rounds: int = 4) -> bool:
+        """Collective: `rounds` consecutive all-reduces of rank- and round-dependent patterns through the xGMI
+        protocol, each checked exactly.  Consecutive rounds alternate the slab parity and advance every
+        workgroup's epoch, so a stale read of a previous round's slab (wrong parity, epoch reuse, a peer's L2
+        holding an old line) shows up as a wrong sum.  Every rank must call it (it advances the shared epochs like
+        a training step does)."""
         n, w, r = FLAT_N, self.cfg.world_size, self.cfg.rank
         base = torch.arange(n, device=self.device, dtype=torch.float32).remainder_(997.0)
-        src = base * float(r + 1)
-        dst = torch.empty_like(src)
-        torch.cuda.synchronize(self.device)
-        timed_out = ctypes.c_int()
-        native.check(self.lib.dca_engine_ipc_selftest(self.h, src.data_ptr(), dst.data_ptr(), float(timeout_s),
-                                                       ctypes.byref(timed_out)), "dca_engine_ipc_selftest")
-        expect = base * float(w * (w + 1) // 2)
-        return not timed_out.value and bool(torch.equal(dst, expect))
+        dst = torch.empty_like(base)
+        ok = True
+        for k in range(int(rounds)):
+            # pattern_k(rank) = (rank + 1) * sign_k * (base + 7 k): integers, exact in fp32 after the sum
+            sign = -1.0 if k % 2 else 1.0
+            pat = (base + 7.0 * k) * sign
+            src = pat * float(r + 1)
+            dst.fill_(float("nan"))
+            torch.cuda.synchronize(self.device)
+            timed_out = ctypes.c_int()
+            native.check(self.lib.dca_engine_ipc_selftest(self.h, src.data_ptr(), dst.data_ptr(), float(timeout_s),
+                                                           ctypes.byref(timed_out)), "dca_engine_ipc_selftest")
+            ok = ok and not timed_out.value and bool(torch.equal(dst, pat * float(w * (w + 1) // 2)))
+        return ok
 
     def xgmi_bench(self, iters: int = 200) -> float:
         """Collective: mean microseconds per xGMI all-reduce of the flat gradient (protocol + data, no SGD)."""
@@ -254,6 +266,19 @@ class NetResDeepEngine:
             torch.cuda.synchronize(self.device)
             native.check(self.lib.dca_engine_run_part(self.h, int(batch), 2), "run_part(2)")
         self.sync()
+
+    def precapture(self, batch: int) -> None:
+        """Capture the step graphs ``run(batch, ...)`` replays (16-step and 1-step chunks) without running them, so
+        a timed region never includes graph capture / instantiation."""
+        native.check(self.lib.dca_engine_precapture(self.h, int(batch)), "dca_engine_precapture")
+
+    def comm_time(self, reset: bool = False) -> tuple[float, int]:
+        """(microseconds, calls) spent in the xGMI gradient all-reduce kernel (publish + wait for the slowest peer)
+        since the last reset; (0.0, 0) on paths without it (world_size 1, RCCL).  Synchronises."""
+        us, calls = ctypes.c_double(), ctypes.c_longlong()
+        native.check(self.lib.dca_engine_comm_time(self.h, ctypes.byref(us), ctypes.byref(calls), int(reset)),
+                     "dca_engine_comm_time")
+        return float(us.value), int(calls.value)
 
     def check_errors(self, reset: bool = True) -> None:
         """Raise if a persistent-kernel BN exchange timed out (a workgroup was not co-resident)."""

@@ -16,7 +16,7 @@ import torch  # noqa: F401  (must be imported before the native library, see mod
 
 from .. import build as _build
 
-ABI_VERSION = 3  # csrc/engine.hip dca_abi_version(): DcaInit layout / C signatures
+ABI_VERSION = 4  # csrc/engine.hip dca_abi_version(): DcaInit layout / C signatures
 _lock = threading.Lock()
 _lib = None
 
@@ -48,12 +48,23 @@ def _declare(lib):
     lib.dca_engine_ipc_handle.argtypes = [c_void_p, ctypes.c_char_p]
     lib.dca_engine_ipc_open.argtypes = [c_void_p, ctypes.c_char_p, c_int]
     lib.dca_engine_ipc_selftest.argtypes = [c_void_p, c_void_p, c_void_p, ctypes.c_float, ctypes.POINTER(c_int)]
-    lib.dca_microbench_xgmi.argtypes = [c_int, c_int, ctypes.POINTER(ctypes.c_float), ctypes.POINTER(c_int)]
     lib.dca_engine_ipc_bench.argtypes = [c_void_p, c_void_p, c_void_p, c_int, ctypes.POINTER(ctypes.c_float)]
     lib.dca_engine_errors.argtypes = [c_void_p, ctypes.POINTER(ctypes.c_uint), c_int]  # flags[2]
-    lib.dca_microbench.argtypes = [c_int, c_int, c_int, c_int, ctypes.POINTER(ctypes.c_float)]
-    lib.dca_microbench_xchg.argtypes = [c_int, c_int, c_int, c_int, c_int, ctypes.POINTER(ctypes.c_float),
-                                        ctypes.POINTER(c_int)]
+    lib.dca_engine_precapture.argtypes = [c_void_p, c_int]
+    lib.dca_engine_comm_time.argtypes = [c_void_p, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_longlong),
+                                         c_int]
+    return lib
+
+
+def load_micro():
+    """The calibration micro-benchmark library (bench/micro/engine_micro.hip; benchmarks only)."""
+    path = _build.build(variant="micro")
+    lib = ctypes.CDLL(path, mode=ctypes.RTLD_GLOBAL)
+    c_int, fp, ip = ctypes.c_int, ctypes.POINTER(ctypes.c_float), ctypes.POINTER(ctypes.c_int)
+    lib.dca_micro_last_error.restype = ctypes.c_char_p
+    lib.dca_microbench_xgmi.argtypes = [c_int, c_int, fp, ip]
+    lib.dca_microbench.argtypes = [c_int, c_int, c_int, c_int, fp]
+    lib.dca_microbench_xchg.argtypes = [c_int, c_int, c_int, c_int, c_int, fp, ip]
     return lib
 
 

@@ -42,7 +42,7 @@ class TrainConfig:
     data_path: str = "data/CIFAR-10/"
     synthetic: int = 0               # >0: use N synthetic CIFAR-shaped samples instead of the dataset
     engine: str = "auto"             # auto | fused | torch
-    dtype: str = "bf16"              # fused engine compute precision (bf16 MFMA or exact fp32 MFMA)
+    dtype: str = "fp32"              # compute precision: fp32 = the reference's numerics (default), bf16 = MFMA bf16
     max_steps: Optional[int] = None  # per-epoch step cap (smoke tests / benchmarking)
     checkpoint: bool = True
     checkpoint_path: Optional[str] = None
@@ -75,7 +75,8 @@ def add_cli_args(ap: argparse.ArgumentParser, batch_default: int = 32) -> argpar
                     help="fused: NetResDeep native engine; ops: the framework's HIP layer kernels (any supported "
                          "model) + FlatBucketDDP; torch: stock PyTorch ops + FlatBucketDDP")
     ap.add_argument("--fp8", action="store_true", help="ops engine: fp8 e4m3 forward GEMMs (1x1 convs, fc)")
-    ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
+    ap.add_argument("--dtype", default="fp32", choices=["bf16", "fp32"],
+                    help="fp32 (default): the reference's precision; bf16: bf16 MFMA operands, fp32 accumulation")
     ap.add_argument("--no-checkpoint", action="store_true")
     ap.add_argument("--checkpoint-path", default=None)
     ap.add_argument("--resume", default=None)
@@ -112,14 +113,20 @@ def load_dataset(cfg: TrainConfig):
     return load_cifar10(cfg.data_path, train=True)
 
 
+FUSED_BATCH_MAX = 64  # csrc/common.h BMAX_LIMIT: per-rank batch the fused NetResDeep engine supports
+
+
 def resolve_engine(cfg: TrainConfig, device: torch.device, model: nn.Module) -> str:
-    """auto: NetResDeep on the fused engine, other models (ResNet family) on the ops-layer HIP kernels, on a GPU;
-    stock torch ops on the CPU."""
+    """auto: NetResDeep on the fused engine (per-rank batch <= 64), other models (ResNet family) and larger
+    NetResDeep batches on the ops-layer HIP kernels, on a GPU; stock torch ops on the CPU."""
+    if cfg.engine == "fused" and cfg.batch_size > FUSED_BATCH_MAX:
+        raise ValueError(f"--engine fused supports --batch-size <= {FUSED_BATCH_MAX} per rank "
+                         f"(got {cfg.batch_size}); use --engine ops or auto")
     if cfg.engine != "auto":
         return cfg.engine
     if device.type != "cuda":
         return "torch"
-    return "fused" if _is_netresdeep(model) else "ops"
+    return "fused" if _is_netresdeep(model) and cfg.batch_size <= FUSED_BATCH_MAX else "ops"
 
 
 def _is_netresdeep(model: nn.Module) -> bool:
@@ -161,6 +168,10 @@ def train_loop(model, train_loader: DeviceLoader, rank: int, cfg: Optional[Train
                 and not _is_netresdeep(unwrap(model)))  # generic models train in bf16; NetResDeep torch path = fp32
     if cfg.check_sync:
         assert_params_in_sync(unwrap(model))
+    if cfg.metrics_json and hasattr(model, "timing"):
+        model.timing = True  # FlatBucketDDP: record the comm-stream span per step
+    if cfg.metrics_json and fused:
+        model.engine.comm_time(reset=True)
     stack = ExitStack()
     prof = stack.enter_context(_profiler(cfg.profile, train_loader.device)) if cfg.profile else None
     start_time = time.time()
@@ -168,11 +179,15 @@ def train_loop(model, train_loader: DeviceLoader, rank: int, cfg: Optional[Train
         train_loader.set_epoch(epoch)
         t0 = time.perf_counter()
         if fused:
-            idx = train_loader.indices()[:steps_per_epoch * train_loader.batch_size]
+            bs = train_loader.batch_size
+            idx = train_loader.indices()[:steps_per_epoch * bs]
             if cfg.fail_at_step is not None and global_step < cfg.fail_at_step <= global_step + steps_per_epoch:
+                done = cfg.fail_at_step - global_step - 1  # steps before the failing one still run, as on the
+                if done:                                   # generic path (the failure is raised AT that step)
+                    model.engine.run_epoch(idx[:done * bs], bs)
                 raise _Fault(f"injected failure at step {cfg.fail_at_step} (rank {rank})")
             with record_function(f"epoch{epoch}:engine"):
-                loss_sum, nsteps = model.engine.run_epoch(idx, train_loader.batch_size)
+                loss_sum, nsteps = model.engine.run_epoch(idx, bs)
         else:
             loss_sum, nsteps = 0.0, 0
             for imgs, labels in train_loader:
@@ -192,10 +207,14 @@ def train_loop(model, train_loader: DeviceLoader, rank: int, cfg: Optional[Train
                 nsteps += 1
         global_step += nsteps
         dt = time.perf_counter() - t0
+        if hasattr(model, "check_comm"):  # a peer timeout of the xGMI all-reduce must not go unnoticed
+            model.check_comm()            # (rank-divergent gradients): raise before anything is saved
         mean = loss_sum / n_batches  # reference divides by len(train_loader) (main.py:44)
         history.append(mean)
-        mlog.write(epoch=epoch, loss=mean, steps=nsteps, seconds=dt,
-                   images_per_sec=nsteps * train_loader.batch_size / max(dt, 1e-9))
+        comm_us, comm_n = _comm_time(model) if cfg.metrics_json else (0.0, 0)
+        mlog.write(epoch=epoch, loss=mean, steps=nsteps, seconds=dt, step_ms=1e3 * dt / max(nsteps, 1),
+                   images_per_sec=nsteps * train_loader.batch_size / max(dt, 1e-9),
+                   allreduce_us_per_step=(comm_us / comm_n) if comm_n else None)
         if should_log(epoch):
             print(epoch_line(epoch, mean), flush=True)
             if cfg.checkpoint:
@@ -208,6 +227,16 @@ def train_loop(model, train_loader: DeviceLoader, rank: int, cfg: Optional[Train
         _export_profile(prof, cfg.profile, rank, train_loader.device)
     print(time_line(total), flush=True)
     return {"losses": history, "seconds": total, "steps": global_step}
+
+
+def _comm_time(model) -> tuple:
+    """(microseconds, steps) spent in the gradient all-reduce since the last call (per-rank metric)."""
+    from .parallel.ddp import FusedDDPTrainer
+    if isinstance(model, FusedDDPTrainer):
+        return model.engine.comm_time(reset=True)
+    if hasattr(model, "comm_time"):
+        return model.comm_time(reset=True)
+    return 0.0, 0
 
 
 def _profiler(out_dir: str, device: torch.device):
@@ -260,6 +289,3 @@ def build_model_for_rank(cfg: TrainConfig, rank: int, world_size: int, device: t
                                dtype=cfg.dtype, max_indices=max(n_idx, loader.batch_size), comm=cfg.allreduce)
     return FlatBucketDDP(model, bucket_cap_mb=cfg.bucket_mb)
 
-
-def unwrap_model(model) -> nn.Module:
-    return unwrap(model)

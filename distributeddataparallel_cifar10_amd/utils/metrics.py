@@ -14,8 +14,6 @@ import os
 import time
 from typing import Optional
 
-import torch
-
 
 def epoch_line(epoch: int, mean_loss: float) -> str:
     return "Epoch {}, Training loss {}".format(epoch, mean_loss)
@@ -44,27 +42,3 @@ class MetricsLog:
         rec.setdefault("time", time.time())
         with open(self.path, "a") as f:
             f.write(json.dumps(rec) + "\n")
-
-
-class DeviceTimer:
-    """Wall time of device work between start() and stop() (HIP events; host clock on CPU)."""
-
-    def __init__(self, device=None):
-        self.cuda = device is not None and torch.device(device).type == "cuda"
-        self.device = device
-
-    def start(self):
-        if self.cuda:
-            self.e0 = torch.cuda.Event(enable_timing=True)
-            self.e1 = torch.cuda.Event(enable_timing=True)
-            self.e0.record()
-        self.t0 = time.perf_counter()
-        return self
-
-    def stop(self) -> float:
-        """Seconds elapsed (synchronises)."""
-        if self.cuda:
-            self.e1.record()
-            self.e1.synchronize()
-            return self.e0.elapsed_time(self.e1) / 1e3
-        return time.perf_counter() - self.t0

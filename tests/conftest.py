@@ -2,6 +2,7 @@
 
 Markers:
   gpu  -- needs an MI355X (run with ``pytest -m gpu``); everything else runs on the CPU (``-m "not gpu"``).
+  multigpu -- one rank per GPU across >= 2 devices (also ``gpu``; skipped on a 1-GPU box).
 Multi-process tests use the gloo backend on 127.0.0.1.
 """
 import os
@@ -20,6 +21,7 @@ os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: requires an AMD Instinct GPU (MI355X, gfx950)")
     config.addinivalue_line("markers", "slow: long-running CPU test")
+    config.addinivalue_line("markers", "multigpu: needs >= 2 MI355X on one node (also marked gpu; skips below 2)")
 
 
 def free_port() -> int:

@@ -82,3 +82,47 @@ def _case_sync_check(rank, ws):
 def test_check_sync_detects_divergence(port):
     from test_flat_ddp import _spawn
     _spawn(_case_sync_check, port, ws=2)
+
+
+def test_train_loop_checks_comm_every_epoch():
+    """train_loop calls the DDP wrapper's check_comm() at every epoch end (before any checkpoint), so a recorded
+    all-reduce timeout stops training instead of silently diverging the ranks."""
+    import pytest
+    from distributeddataparallel_cifar10_amd.data.loader import DeviceLoader
+    from distributeddataparallel_cifar10_amd.data.synthetic import synthetic_cifar
+    from distributeddataparallel_cifar10_amd.models.netresdeep import NetResDeep
+    from distributeddataparallel_cifar10_amd.parallel.flat_ddp import FlatBucketDDP
+    from distributeddataparallel_cifar10_amd.train import TrainConfig, train_loop
+
+    class Boom(RuntimeError):
+        pass
+
+    ddp = FlatBucketDDP(NetResDeep())
+    calls = []
+
+    def check():
+        calls.append(1)
+        raise Boom("peer timeout")
+
+    ddp.check_comm = check
+    data, labels = synthetic_cifar(64, seed=0)
+    loader = DeviceLoader(data, labels, batch_size=32, world_size=1, rank=0, device="cpu")
+    with pytest.raises(Boom):
+        train_loop(ddp, loader, 0, TrainConfig(epochs=2, max_steps=1, checkpoint=False))
+    assert calls == [1]
+
+
+def test_resolve_engine_large_batch_falls_back():
+    """The fused NetResDeep engine supports per-rank batch <= 64: auto picks the ops kernels above that, an
+    explicit --engine fused raises a clear error instead of failing inside the native engine."""
+    import pytest
+    import torch
+    from distributeddataparallel_cifar10_amd.models.netresdeep import NetResDeep
+    from distributeddataparallel_cifar10_amd.train import TrainConfig, resolve_engine
+    cuda = torch.device("cuda", 0)
+    m = NetResDeep()
+    assert resolve_engine(TrainConfig(batch_size=64), cuda, m) == "fused"
+    assert resolve_engine(TrainConfig(batch_size=128), cuda, m) == "ops"
+    assert resolve_engine(TrainConfig(batch_size=128), torch.device("cpu"), m) == "torch"
+    with pytest.raises(ValueError, match="batch-size"):
+        resolve_engine(TrainConfig(batch_size=128, engine="fused"), cuda, m)

@@ -112,9 +112,11 @@ def test_engine_ddp_two_ranks_one_gpu(gpu, port, dtype, persistent, split, monke
     assert not bad, "\n".join(f"rank {r}:\n{e}" for r, e in bad)
 
 
-def _xgmi_worker(rank, ws, port, dtype, persistent, q):
-    """One rank of the fused trainer with the one-shot xGMI all-reduce (all ranks share GPU 0: the IPC-mapped
-    slabs are then peers on the same device, which exercises the whole protocol -- epochs, parities, flags)."""
+def _xgmi_worker(rank, ws, port, dtype, persistent, q, comm="xgmi", own_device=False):
+    """One rank of the fused trainer with the one-shot xGMI all-reduce.  By default all ranks share GPU 0: the
+    IPC-mapped slabs are then peers on the same device, which exercises the whole protocol -- epochs, parities,
+    flags.  own_device=True (tests/test_multigpu.py): rank r on GPU r, so the slabs and flags cross xGMI, and
+    comm="rccl" runs the graph-captured RCCL all-reduce instead."""
     try:
         os.environ["MASTER_ADDR"] = "127.0.0.1"
         os.environ["MASTER_PORT"] = str(port)
@@ -125,8 +127,8 @@ def _xgmi_worker(rank, ws, port, dtype, persistent, q):
         from distributeddataparallel_cifar10_amd.models.netresdeep import NetResDeep
         from distributeddataparallel_cifar10_amd.parallel.ddp import FusedDDPTrainer
         from distributeddataparallel_cifar10_amd.utils.oracle import reference_step
-        torch.cuda.set_device(0)
-        dev = torch.device("cuda", 0)
+        dev = torch.device("cuda", rank if own_device else 0)
+        torch.cuda.set_device(dev)
         data, labels = synthetic_cifar(NDATA, seed=5)
         order = [distributed_indices(NDATA, ws, r) for r in range(ws)]
         torch.manual_seed(100 + rank)
@@ -136,8 +138,8 @@ def _xgmi_worker(rank, ws, port, dtype, persistent, q):
         ref0 = copy.deepcopy(model)
         model = model.to(dev)
         tr = FusedDDPTrainer(model, data.to(dev), labels.to(dev), batch_max=32, dtype=dtype, persistent=persistent,
-                             comm="xgmi", max_indices=len(order[rank]))
-        assert tr.comm == "xgmi", "fell back to RCCL: the xGMI path did not come up"
+                             comm=comm, max_indices=len(order[rank]))
+        assert tr.comm == comm, f"asked for {comm}, got {tr.comm} (the xGMI path did not come up?)"
         eng = tr.engine
         eng.set_indices(order[rank])
         eng.set_cursor(0)
@@ -219,3 +221,25 @@ def test_bench_two_ranks_shared_gpu(gpu, port):
     assert out["n_gpus"] == 2 and out["steps"] == 48 and out["allreduce"] == "xgmi" and out["loss_finite"]
     assert out["config"]["global_batch"] == 64 and out["config"]["parallelism"] == "dp2"
     assert out["value"] > 0
+
+
+def test_bench_self_launch_sweep_shared_gpu(gpu):
+    """``python bench.py --sweep 1,2`` (no torchrun): bench.py spawns each rank group itself (reference
+    main.py:84 mp.spawn), rank 0 prints the per-N JSON line (whole-job value, per-rank step times, the xGMI
+    all-reduce time per step) and the parent prints the scaling summary.  Rehearsed with the ranks sharing this
+    box's one GPU (DCA_BENCH_SHARE_GPU=1)."""
+    import json
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, DCA_BENCH_SHARE_GPU="1", DCA_XGMI_TIMEOUT_S="60")
+    env.pop("WORLD_SIZE", None)
+    cmd = [sys.executable, "bench.py", "--sweep", "1,2", "--steps", "48", "--warmup", "16"]
+    r = subprocess.run(cmd, cwd=root, env=env, capture_output=True, text=True, timeout=400)
+    assert r.returncode == 0, r.stderr[-4000:]
+    recs = [json.loads(ln) for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(recs) == 3, r.stdout
+    one, two, summary = recs
+    assert one["n_gpus"] == 1 and two["n_gpus"] == 2 and two["allreduce"] == "xgmi" and two["loss_finite"]
+    assert len(two["per_rank_ms_per_step"]) == 2 and all(v > 0 for v in two["allreduce_us_per_step"])
+    assert set(summary["scaling_efficiency"]) == {"1", "2"} and summary["scaling_efficiency"]["1"] == 1.0

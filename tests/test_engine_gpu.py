@@ -123,3 +123,53 @@ def test_split_mode_matches_oracle(gpu, monkeypatch):
     res = compare_one_step("bf16", 4, 32, True, seed=7, verbose=False, persistent=True)
     bad = {k: v for k, v in res.items() if v > 5e-2}
     assert not bad, bad
+
+
+@pytest.mark.parametrize("persistent,split", [(True, "0"), (True, "1"), (False, "0")])
+def test_rccl_path_world_size_one(gpu, persistent, split, monkeypatch):
+    """comm="rccl" with force_comm at world_size 1: the graph-captured ncclAllReduce (a 1-rank communicator), the
+    split-mode stream/event wiring and the averaging SGD kernel all run, and give the same training step as the
+    fused-SGD world_size-1 engine (an all-reduce over one rank is the identity)."""
+    import copy
+    from distributeddataparallel_cifar10_amd.data.synthetic import synthetic_cifar
+    from distributeddataparallel_cifar10_amd.models.netresdeep import NetResDeep
+    from distributeddataparallel_cifar10_amd.runtime.engine import EngineConfig, NetResDeepEngine
+    monkeypatch.setenv("DCA_PK_SPLIT", split)
+    data, labels = synthetic_cifar(256, seed=3)
+    torch.manual_seed(11)
+    m0 = NetResDeep()
+    out = []
+    for force in (False, True):
+        m = copy.deepcopy(m0).to(gpu)
+        eng = NetResDeepEngine(m, data.to(gpu), labels.to(gpu),
+                               EngineConfig(batch_max=32, dtype="bf16", persistent=persistent, comm="rccl",
+                                            force_comm=force))
+        eng.set_indices(list(range(256)))
+        eng.set_cursor(0)
+        eng.read_loss(reset=True)
+        eng.run(32, 5)  # graph replay incl. the captured collective
+        loss, steps = eng.read_loss()
+        assert steps == 5
+        out.append((loss, {k: v.detach().cpu().clone() for k, v in m.state_dict().items()}))
+        eng.close()
+    (l0, s0), (l1, s1) = out
+    assert abs(l0 - l1) <= 1e-6 * abs(l0), (l0, l1)
+    for k in s0:
+        assert torch.allclose(s0[k].double(), s1[k].double(), rtol=1e-6, atol=1e-7), k
+
+
+def test_precapture_keeps_graphs_out_of_timed_runs(gpu):
+    """precapture() builds both graph chunk sizes; a later run with any step count only replays."""
+    from distributeddataparallel_cifar10_amd.data.synthetic import synthetic_cifar
+    from distributeddataparallel_cifar10_amd.models.netresdeep import NetResDeep
+    from distributeddataparallel_cifar10_amd.runtime.engine import EngineConfig, NetResDeepEngine
+    data, labels = synthetic_cifar(1024, seed=1)
+    eng = NetResDeepEngine(NetResDeep().to(gpu), data.to(gpu), labels.to(gpu), EngineConfig(batch_max=32))
+    eng.set_indices(list(range(1024)))
+    eng.set_cursor(0)
+    eng.precapture(32)
+    eng.read_loss(reset=True)
+    eng.run(32, 21)  # 16 + 5 x 1
+    loss, steps = eng.read_loss()
+    eng.close()
+    assert steps == 21 and loss == loss

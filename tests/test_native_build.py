@@ -71,7 +71,7 @@ def test_graft_build_and_abi():
     lib.dca_abi_version.restype = ctypes.c_int
     assert lib.dca_abi_version() > 0
     for sym in ("dca_engine_create", "dca_engine_run", "dca_engine_destroy", "dca_engine_errors",
-                "dca_nccl_unique_id", "dca_microbench"):
+                "dca_nccl_unique_id", "dca_engine_precapture", "dca_engine_comm_time"):
         assert hasattr(lib, sym), sym
 
 

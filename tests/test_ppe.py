@@ -108,6 +108,8 @@ def test_train_eval_kfold_pregenerate(tmp_path):
     j = json.load(open(tmp_path / "p.json"))
     k = next(iter(j))
     assert len(j[k]["bboxes"]) == len(j[k]["scores"]) and len(j[k]["scores"][0]) == 3
+    assert {v for row in j[k]["scores"] for v in row} <= {0, 1}  # reference: 0/1 decisions on raw logits
+    assert len(j[k]["probs"]) == len(j[k]["scores"])
 
 
 def test_synthetic_is_learnable():

@@ -192,3 +192,36 @@ def _ops_ddp_worker(rank, ws, port, q):
 
 def test_ops_resnet_flat_ddp_xgmi(gpu, port):
     _spawn(_ops_ddp_worker, 2, port)
+
+
+def _timeout_worker(rank, ws, port, q):
+    try:
+        dev = _init(rank, ws, port)
+        from distributeddataparallel_cifar10_amd.parallel.xgmi import XgmiComm
+        comm = XgmiComm.create(4096, device=dev, timeout_s=2.0)
+        assert comm is not None
+        t = torch.ones(4096, device=dev)
+        if rank == 0:  # rank 1 never arrives: the flag wait expires, the error word is set, check() raises
+            comm.all_reduce_(t, average=False)
+            torch.cuda.synchronize()
+            raised = False
+            try:
+                comm.check()
+            except RuntimeError:
+                raised = True
+            assert raised, "a peer timeout was not reported"
+        dist.barrier()
+        comm.close()
+        q.put((rank, None))
+    except Exception:
+        q.put((rank, traceback.format_exc()))
+    finally:
+        if dist.is_initialized():
+            dist.destroy_process_group()
+
+
+def test_xgmi_peer_timeout_is_reported(gpu, port):
+    """Fault injection: a rank that stops stepping makes its peer's all-reduce time out; the error word is set
+    and check() -- which train_loop / the PPE trainer call at every epoch end -- raises instead of letting the
+    ranks' parameters silently diverge."""
+    _spawn(_timeout_worker, 2, port)
