@@ -59,7 +59,7 @@ def compare_one_step(dtype: str, rows: int, B: int, graph: bool, seed: int = 0, 
     eng.run(B, 1, graph=graph)
     eng.sync()
     r = reference_step(ref, data[idx], labels[idx], lr=1e-2, bf16_operands=(dtype == "bf16"),
-                       fc1_bf16=bool(persistent))
+                       fc1_bf16=bool(persistent) and dtype == "bf16")
     out = {}
 
     def rep(name, a, b):
@@ -127,7 +127,7 @@ def trajectory(dtype: str, rows: int, B: int, steps: int, seed: int = 1, persist
         losses_e.append(lsum)
         sel = idx[s * B:(s + 1) * B]
         losses_r.append(reference_step(ref, data[sel], labels[sel], bf16_operands=(dtype == "bf16"),
-                                       fc1_bf16=bool(persistent))["loss"])
+                                       fc1_bf16=bool(persistent) and dtype == "bf16")["loss"])
     sd, rsd = model.state_dict(), ref.state_dict()
     perr = max(rel(sd[k], rsd[k]) for k in rsd if rsd[k].dtype != torch.int64)
     eng.close()

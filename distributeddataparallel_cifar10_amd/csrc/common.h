@@ -87,7 +87,12 @@ struct Ctx {
   void* w1b;                   // [32][2048] bf16 copy of fc1.weight (persistent engine's head; kept by every SGD)
   void* swf;                   // [2 co half][3 k group][64 lanes][4] bf16 conv1 weights as 16x16x16 MFMA B fragments
   unsigned long long* stamps;  // [32 kernel slots][256 wg][8 stamps][2] (diagnostic DCA_STAMPS builds only)
+  // sliced persistent engine (netresdeep_pks.hip): bf16 hi / lo splits of the conv weights, u16 offsets
+  //   [0, 9216) fwd hi [tap][co][ci] | [9216, 18432) fwd lo | [18432, 27648) dgrad hi [8 - tap][ci][co] |
+  //   [27648, 36864) dgrad lo | [36864, 38400) conv1 MFMA B fragments hi (swf_slot order) | [38400, 39936) lo
+  unsigned short* pkw;
 };
+constexpr int PKW_N = 39936;
 
 // In-kernel phase stamps (diagnostic build, -DDCA_STAMPS): thread 0 of each workgroup records
 // (s_memtime, s_memrealtime) at phase boundaries.  Never compiled into the production library.

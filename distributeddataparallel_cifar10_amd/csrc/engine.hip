@@ -18,6 +18,7 @@
 
 #include "netresdeep_kernels.hip"
 #include "netresdeep_persistent.hip"
+#include "netresdeep_pks.hip"
 #include "xgmi_allreduce.hip"
 
 namespace {
@@ -96,6 +97,8 @@ struct Engine {
   unsigned long long ar_deadline = 300ull * 100000000ull;  // 300 s in 100 MHz ticks (a peer may be in host code)
   std::map<int, hipGraphExec_t> graphs;
   bool persistent = false;
+  bool sliced = false;   // persistent engine, image-sliced kernel (netresdeep_pks.hip; default)
+  pks::Args qa{};
   bool comm_on = false;  // the step ends with a gradient collective (world_size > 1, or force_comm)
   int resident = 0;      // persistent engine: workgroups guaranteed co-resident (occupancy x CUs)
   int pk_waves = 8;
@@ -157,8 +160,9 @@ static int alloc_workspace(Engine* e) {
       {"RS_BASE", 64 * 4},           {"CURSOR", 16},                  {"STEPS", 16},
       {"LOSS", 16},                  {"STAMPS", 32 * 256 * 8 * 2 * 8},
       {"GRAN", 2 * 64 * 64 * 8},     {"EPOCH", 16},                   {"ERR", 16},
-      {"TSLAB", bmax * WSLAB_N * 4}, {"BNG", 64 * 4}, {"IDS", 64 * 4}, {"W1B", 65536 * 2}, {"XCC", 64 * 8}, {"SIMG", 2 * 64 * 3072}, {"SLAB", 2 * 64 * 4}, {"GH", bmax * 8192 * 4}, {"SWF", 2 * 3 * 64 * 4 * 2},
-      {"COMMT", 16},
+      {"TSLAB", bmax * pks::S * WSLAB_N * 4}, {"BNG", 64 * 4}, {"IDS", 64 * 4}, {"W1B", 65536 * 2}, {"XCC", 64 * 8}, {"SIMG", 2 * 64 * 3072}, {"SLAB", 2 * 64 * 4}, {"GH", bmax * 8192 * 4}, {"SWF", 2 * 3 * 64 * 4 * 2},
+      {"COMMT", 16}, {"PKW", PKW_N * 2},
+      {"PKS_GRAN", 2 * (size_t)pks::LMAX * pks::GSTR * 8}, {"PKS_YH", 10 * (size_t)pks::LMAX * 2 * 512 * 4},
   };
   size_t total = 0;
   for (auto& r : regs) total += align_up(r.bytes, 256);
@@ -210,6 +214,17 @@ static int alloc_workspace(Engine* e) {
   e->pa.gh = (float*)e->regions["GH"];
   e->pa.slab = (int*)e->regions["SLAB"];
   e->pa.debug = e->in.debug;
+  c.pkw = (unsigned short*)e->regions["PKW"];
+  pks::Args& qa = e->qa;
+  qa.gran = (unsigned long long*)e->regions["PKS_GRAN"];
+  qa.epoch = e->pa.epoch;
+  qa.err = e->pa.err;
+  qa.tslab = e->pa.tslab;
+  qa.bng = e->pa.bng;
+  qa.simg = e->pa.simg;
+  qa.slab = e->pa.slab;
+  qa.yh = (float*)e->regions["PKS_YH"];
+  qa.debug = e->in.debug;
   return 0;
 }
 
@@ -222,6 +237,10 @@ static int set_lds_limits(Engine* e) {
   HIPCK(hipFuncSetAttribute((const void*)e->kbwd, hipFuncAttributeMaxDynamicSharedMemorySize, (int)dg));
   HIPCK(hipFuncSetAttribute((const void*)pk::k_pk_step<8>, hipFuncAttributeMaxDynamicSharedMemorySize,
                             pk::Plan::TOTAL));
+  HIPCK(hipFuncSetAttribute((const void*)pks::k_pks_step<0>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            pks::Plan<0>::TOTAL));
+  HIPCK(hipFuncSetAttribute((const void*)pks::k_pks_step<1>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            pks::Plan<1>::TOTAL));
 
   return 0;
 }
@@ -245,10 +264,29 @@ static int enqueue_xgmi_sgd(Engine* e, const Ctx& cx) {
 // Persistent path: one launch for the whole trunk, one for reduction + SGD.
 // `part`: 0 = the whole step; 1 = compute up to (not including) the gradient all-reduce; 2 = what follows it
 // (averaging SGD + CC4 base).  Parts 1/2 exist for comm_mode 1, where the host runs the all-reduce in between.
+// grid of the sliced step: S workgroups per image, image slots rounded up to a multiple of 8 (see k_pks_step)
+static int pks_grid(int B) { return (B + 7) / 8 * 8 * pks::S; }
+
 static int enqueue_step_persistent(Engine* e, int B, int part) {
   Ctx cx = e->base;
   cx.B = B;
   const bool multi = e->comm_on;
+  if (e->sliced && part != 2) {
+    if (e->bf)
+      hipLaunchKernelGGL(pks::k_pks_step<0>, dim3(pks_grid(B)), dim3(pks::NTH), pks::Plan<0>::TOTAL, e->st, cx, e->qa);
+    else
+      hipLaunchKernelGGL(pks::k_pks_step<1>, dim3(pks_grid(B)), dim3(pks::NTH), pks::Plan<1>::TOTAL, e->st, cx, e->qa);
+    hipLaunchKernelGGL(pks::k_pks_reduce, dim3(pk::R_GRID), dim3(256), 0, e->st, cx, e->pa, B * pks::S);
+  }
+  if (e->sliced) {
+    if (multi) {
+      if (part == 0 && e->in.comm_mode == 2) return enqueue_xgmi_sgd(e, cx);
+      if (part == 0) NCCK(ncclAllReduce(cx.grads, cx.grads, FLAT_N, ncclFloat32, ncclSum, e->comm, e->st));
+      if (part != 1) hipLaunchKernelGGL(e->kapply, dim3(64), dim3(NT), 0, e->st, cx, 1);
+    }
+    HIPCK(hipGetLastError());
+    return 0;
+  }
   const bool rccl_overlap = e->split && multi && part == 0 && e->in.comm_mode == 0;  // fc all-reduce overlapped with the trunk backward
   if (part != 2) {
     pk::PkArgs pa = e->pa;
@@ -398,8 +436,12 @@ static int engine_init(Engine* e, const DcaInit* in, int n_indices) {
     const char* sp = getenv("DCA_PK_SPLIT");
     e->split = sp && sp[0] == '1';
   }
-  if (e->persistent && !e->bf) {
-    g_err = "the persistent engine is bf16-only (fp32 MFMA needs all CUs: use the multi-kernel engine)";
+  {
+    const char* ps = getenv("DCA_PKS");  // DCA_PKS=0: the one-workgroup-per-image kernel (bf16 only)
+    e->sliced = e->persistent && !(ps && ps[0] == '0');
+  }
+  if (e->persistent && !e->sliced && !e->bf) {
+    g_err = "the one-workgroup-per-image persistent kernel is bf16-only (use the sliced kernel: unset DCA_PKS)";
     return -1;
   }
   if (e->bf && e->R == 4) dca::bind_kernels<true, 4, 16>(e);
@@ -414,11 +456,19 @@ static int engine_init(Engine* e, const DcaInit* in, int n_indices) {
     int dev = 0, ncu = 0, per_cu = 0;
     HIPCK(hipGetDevice(&dev));
     HIPCK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
-    HIPCK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)dca::pk::k_pk_step<8>, 64 * 8,
-                                                      dca::pk::Plan::TOTAL));
+    if (!e->sliced)
+      HIPCK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)dca::pk::k_pk_step<8>, 64 * 8,
+                                                        dca::pk::Plan::TOTAL));
+    else if (e->bf)
+      HIPCK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)dca::pks::k_pks_step<0>, dca::pks::NTH,
+                                                        dca::pks::Plan<0>::TOTAL));
+    else
+      HIPCK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)dca::pks::k_pks_step<1>, dca::pks::NTH,
+                                                        dca::pks::Plan<1>::TOTAL));
     const int resident = (per_cu > 1 ? per_cu - 1 : per_cu) * ncu;
-    if (resident < in->bmax) {
-      g_err = "persistent engine: " + std::to_string(in->bmax) + " workgroups cannot all be resident (" +
+    const int need = e->sliced ? dca::pks_grid(in->bmax) : in->bmax;
+    if (resident < need) {
+      g_err = "persistent engine: " + std::to_string(need) + " workgroups cannot all be resident (" +
               std::to_string(per_cu) + " per CU x " + std::to_string(ncu) + " CUs); use the multi-kernel engine";
       return -1;
     }
@@ -800,6 +850,12 @@ void* dca_engine_region(void* h, const char* name) {
 }
 
 size_t dca_engine_workspace_bytes(void* h) { return ((Engine*)h)->ws_bytes; }
+
+// 0: multi-kernel engine; 1: persistent, one workgroup per image; 2: persistent, image-sliced (S per image)
+int dca_engine_kind(void* h) {
+  Engine* e = (Engine*)h;
+  return e->sliced ? 2 : (e->persistent ? 1 : 0);
+}
 
 
 }  // extern "C"

@@ -1,0 +1,1248 @@
+// Image-sliced persistent NetResDeep training step for CDNA4 (gfx950 / MI355X): ONE launch per step, every image
+// split over S = 4 workgroups of 4 image rows (one wave per row), so a batch of 32 runs on 128 CUs instead of the
+// 32 of the one-workgroup-per-image kernel (netresdeep_persistent.hip), and each CU's serial work per block is a
+// quarter.
+//
+//   stem (+ 1 halo pooled row each side, recomputed, no exchange) -> 10 forward blocks -> head -> 10 backward
+//   blocks -> stem backward; then k_pks_reduce (slab reduction + SGD + bookkeeping).
+//
+// Cross-workgroup traffic, all as data-as-flag granules {tag, f32} written by ONE sc1 store (8 or 16 B) and read
+// by sc1 loads (MI355X guide, Guideline 16 R2; no fences), double-buffered by round parity, every spin bounded:
+//   * per block, one round: the 64 BatchNorm partial sums of every workgroup (all-to-all sweep) PLUS the two
+//     boundary rows of the conv output (forward: y) or of the BN-masked gradient (backward: dz) for the
+//     neighbouring slices' halos -- the halo rides in the same round, so slicing adds no extra hand-off latency;
+//   * once, in the head: the 32 fc1 partial sums of the S slices of an image.
+// The halo row of x is kept by the halo waves themselves (x_{i+1} = relu(bn(y_i)) + x_i needs only the neighbour's
+// y_i row and the global BN statistics).  The backward recovers x_i = x_{i+1} - relu(bn(y_i)) (reversible
+// residual) instead of storing every block input.
+//
+// Precision P: 0 = bf16 MFMA operands (fp32 accumulate, BatchNorm / loss / SGD in fp32); 1 = fp32-accurate
+// "3xbf16": every operand a = a_hi + a_lo (two bf16), every product a_hi*b_hi + a_hi*b_lo + a_lo*b_hi on
+// v_mfma_f32_16x16x32_bf16 (relative product error ~2^-17, i.e. ~16 mantissa bits, finer than the TF32 that
+// cuDNN uses for the reference's fp32 convolutions by default on Ampere and later), fc1 in plain fp32.
+//
+// Element ownership (C layout of v_mfma_f32_16x16x32_bf16): thread (wave w, lane l = 16q + c) owns
+//   pixel (image row 4s + w, col 4q + i), channel 16h + c   for h in {0,1}, i in {0..3}   (8 values)
+//
+// Reference semantics: model/resnet.py:5-37 (one shared ResBlock applied 10x, skip after the ReLU),
+// main.py:27-39 (SGD, CrossEntropy mean), BatchNorm2d training statistics + 10 running-stat EMAs per forward.
+
+namespace dca {
+namespace pks {
+
+constexpr int S = 4;                   // workgroups (row slices) per image
+constexpr int RS = 16 / S;             // image rows per slice
+constexpr int NW = RS;                 // waves per workgroup: one image row each
+constexpr int NTH = 64 * NW;           // threads per workgroup
+constexpr int GSTR = 64 + 2 * 512;     // granules per workgroup per round: 64 BN sums | top row | bottom row
+constexpr int LMAX = 64 * S;           // logical workgroups (batch <= 64)
+constexpr int NNT = (18 + NW - 1) / NW;  // wgrad tile columns (ci half x tap) per wave
+constexpr int RND_HEAD = 10;           // rounds: 0..9 forward BN, 10 head (fc1 partials), 11..20 backward BN
+constexpr unsigned SPIN_LIMIT = 1u << 18;
+constexpr int RB = 80;                 // bf16 record: 32 channels (64 B) + 16 B pad (staggers the banks)
+
+struct Args {
+  unsigned long long* gran;  // [2][LMAX][GSTR] granules
+  int* epoch;                // device scalar, advanced by the reduce kernel after every step
+  unsigned* err;             // bit r: exchange round r timed out
+  float* tslab;              // [LMAX][WSLAB_N] trunk wgrad per workgroup (fragment order, read by k_pks_reduce)
+  float* bng;                // [64] dgamma | dbeta (written by logical workgroup 0)
+  uint8_t* simg;             // [2][64][3072] batch images staged by the previous step (parity = epoch & 1)
+  int* slab;                 // [2][64] their labels
+  float* yh;                 // [10][LMAX][2][512] halo rows of y received in the forward (for the backward)
+  int debug;                 // also store X / DY / G for the numerical diagnostics
+};
+
+// ---- LDS plan (bytes; every region 16-byte aligned) ---------------------------------------------------------
+template <int P>
+struct Plan {
+  static constexpr int NP = P + 1;                       // precision planes: hi (+ lo)
+  static constexpr int O_CRED = 0;                       // [2][NW][64] f32 combine scratch
+  static constexpr int O_STAT = O_CRED + 2 * NW * 64 * 4;  // [10][64] f32: mean | invstd
+  static constexpr int O_SCSH = O_STAT + 2560;           // [10][64] f32: BN scale | shift of every block
+  static constexpr int O_MISC = O_SCSH + 2560;           // [1280] f32 step constants (layout: k_pks_step)
+  static constexpr int O_U = O_MISC + 5120;              // phase union
+  // trunk, forward and backward
+  static constexpr int WT_PL = 288 * RB;                 // conv weight records [tap][co | ci] x 32
+  static constexpr int U_WT = 0;
+  static constexpr int XR_PL = (RS + 2) * 18 * RB;       // conv input records, rows -1..RS, cols -1..16
+  static constexpr int U_XR = U_WT + NP * WT_PL;
+  static constexpr int U_XR_END = U_XR + NP * XR_PL;
+  static constexpr int DYT_S = RS * 16 + 8;              // dy, channel-major (wgrad A operand)
+  static constexpr int DYT_PL = 32 * DYT_S * 2;
+  static constexpr int U_DYT = U_XR_END;
+  static constexpr int XT_S = (RS + 2) * 16 + 8;         // x, channel-major, 3 column-shifted copies
+  static constexpr int XT_PL = 3 * 32 * XT_S * 2;
+  static constexpr int U_XT = U_DYT + NP * DYT_PL;
+  static constexpr int BWD_END = U_XT + NP * XT_PL;
+  // stem (start of the step; WT and XR live)
+  static constexpr int XIN_ROWS = 2 * RS + 6, XIN_COLS = 34;  // input rows 8s-3 .. 8s+10, cols -1..32
+  static constexpr int XIN_PL = XIN_ROWS * XIN_COLS * 8;      // NHWC4 bf16 pixels
+  static constexpr int U_XIN = U_XR_END;
+  static constexpr int X0S = 36;
+  static constexpr int U_X0 = U_XIN + NP * XIN_PL;             // [RS + 2][16][X0S] f32 pooled stem output
+  static constexpr int U_SCODE = U_X0 + (RS + 2) * 16 * X0S * 4;  // [RS][16][32] u8 stem pool codes
+  static constexpr int STEM_END = U_SCODE + RS * 16 * 32;
+  // head (WT live -- it receives the dgrad weights meanwhile -- XR / dyT / xT free)
+  static constexpr int X10S = 33;
+  static constexpr int U_X10 = U_XR;                           // [RS][16][X10S] f32
+  static constexpr int W1S = P == 1 ? 516 : 520;               // fc1 slice row stride (elements)
+  static constexpr int W1_BYTES = 32 * W1S * (P == 1 ? 4 : 2); // [32 rows][512 local features] (f32 | bf16)
+  static constexpr int U_W1 = U_XR_END;
+  static constexpr int U_PCODE = U_W1 + W1_BYTES;              // [512] u8 pool argmax
+  static constexpr int U_DP = U_PCODE + 512;                   // [512] f32 dL/dpooled
+  static constexpr int U_PL = U_DP + 2048;                     // [512] f32 pooled features
+  static constexpr int U_HP = U_PL + 2048;                     // [32] fc1 partials | [32, 64) dh
+  static constexpr int HEAD_END = U_HP + 256;
+  // stem backward (WT / XR free)
+  static constexpr int DSP = 2 * RS * 32 + 8;                  // d(conv1 out), channel-major, own conv rows
+  static constexpr int DST_PL = 32 * DSP * 2;
+  static constexpr int U_DST = 0;
+  static constexpr int XSR = 2 * RS + 2;                       // input rows 8s-1 .. 8s+8
+  static constexpr int XS_S = 40;
+  static constexpr int XS_PL = 9 * XSR * XS_S * 2;             // [3 kw][3 ci][XSR][XS_S] shifted input copies
+  static constexpr int U_XS = U_DST + NP * DST_PL;
+  static constexpr int SBWD_END = U_XS + NP * XS_PL;
+  static constexpr int UNION = pk::cmax(pk::cmax(BWD_END, STEM_END), pk::cmax(HEAD_END, SBWD_END));
+  static constexpr int TOTAL = O_U + UNION;
+};
+static_assert(Plan<1>::TOTAL <= 160 * 1024, "LDS budget");
+static_assert(Plan<0>::X10S * 4 * RS * 16 <= Plan<0>::XR_PL, "x10 fits the XR region");
+
+// ---- helpers ------------------------------------------------------------------------------------------------
+__device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+__device__ __forceinline__ void pin(float& x) { asm volatile("" : "+v"(x)); }
+__device__ __forceinline__ void pin(unsigned& x) { asm volatile("" : "+v"(x)); }
+__device__ __forceinline__ void pin(int& x) { asm volatile("" : "+v"(x)); }
+__device__ __forceinline__ void pin(uint2& x) { asm volatile("" : "+v"(x.x), "+v"(x.y)); }
+__device__ __forceinline__ void pin(uint4& x) { asm volatile("" : "+v"(x.x), "+v"(x.y), "+v"(x.z), "+v"(x.w)); }
+
+typedef unsigned v4u __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ unsigned short bf_lo(float v, unsigned short hi) {
+  return bfbits(v - __uint_as_float((unsigned)hi << 16));
+}
+// one value into channel `ch` of record `rec` (both planes)
+template <int P>
+__device__ __forceinline__ void st1r(char* xr, int plane, int rec, int ch, float v) {
+  const unsigned short hi = bfbits(v);
+  *(unsigned short*)(xr + rec * RB + ch * 2) = hi;
+  if constexpr (P == 1) *(unsigned short*)(xr + plane + rec * RB + ch * 2) = bf_lo(v, hi);
+}
+template <int P>
+__device__ __forceinline__ f32x4 mma3(const bf16x8& ah, const bf16x8& al, const bf16x8& bh, const bf16x8& bl,
+                                      f32x4 acc) {
+  acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, bh, acc, 0, 0, 0);
+  if constexpr (P == 1) {
+    acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, bl, acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al, bh, acc, 0, 0, 0);
+  }
+  return acc;
+}
+template <int P>
+__device__ __forceinline__ f32x4 mma3s(const s4v& ah, const s4v& al, const s4v& bh, const s4v& bl, f32x4 acc) {
+  acc = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(ah, bh, acc, 0, 0, 0);
+  if constexpr (P == 1) {
+    acc = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(ah, bl, acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(al, bh, acc, 0, 0, 0);
+  }
+  return acc;
+}
+
+// 3x3 conv of one output row (wave w = slice row w) on MFMA, both channel halves.  xr: (RS+2) x 18 records,
+// wt: 288 records (tap-major); P=1 reads the lo planes at +XR_PL / +WT_PL.
+template <int P>
+__device__ __forceinline__ void conv_row(const char* xr, const char* wt, f32x4 (&acc)[2], int w, int lane) {
+  using PL = Plan<P>;
+  const int c = lane & 15, q = lane >> 4;
+  const char* abase = xr + (w * 18 + c) * RB + q * 16;
+  const char* bbase = wt + c * RB + q * 16;
+  acc[0] = z4();
+  acc[1] = z4();
+#pragma unroll
+  for (int tap = 0; tap < 9; ++tap) {
+    const int kh = tap / 3, kw = tap % 3;
+    const bf16x8 b0 = *(const bf16x8*)(bbase + (tap * 32) * RB);
+    const bf16x8 b1 = *(const bf16x8*)(bbase + (tap * 32 + 16) * RB);
+    const bf16x8 a = *(const bf16x8*)(abase + (kh * 18 + kw) * RB);
+    bf16x8 b0l = b0, b1l = b1, al = a;
+    if constexpr (P == 1) {
+      b0l = *(const bf16x8*)(bbase + PL::WT_PL + (tap * 32) * RB);
+      b1l = *(const bf16x8*)(bbase + PL::WT_PL + (tap * 32 + 16) * RB);
+      al = *(const bf16x8*)(abase + PL::XR_PL + (kh * 18 + kw) * RB);
+    }
+    acc[0] = mma3<P>(a, al, b0, b0l, acc[0]);
+    acc[1] = mma3<P>(a, al, b1, b1l, acc[1]);
+  }
+}
+
+// per-workgroup channel sums of per-thread C-layout partials (a0/b0: channel c, a1/b1: channel 16 + c), delivered
+// to the publishing threads: thread t < 64 returns slot t (t < 32: sum of a for channel t, else sum of b for
+// channel t - 32).  One LDS barrier.
+__device__ __forceinline__ float wg_csum(float a0, float a1, float b0, float b1, float* cred) {
+  const int t = threadIdx.x, w = t >> 6, lane = t & 63, c = lane & 15;
+  a0 += __shfl_xor(a0, 16);
+  a0 += __shfl_xor(a0, 32);
+  a1 += __shfl_xor(a1, 16);
+  a1 += __shfl_xor(a1, 32);
+  b0 += __shfl_xor(b0, 16);
+  b0 += __shfl_xor(b0, 32);
+  b1 += __shfl_xor(b1, 16);
+  b1 += __shfl_xor(b1, 32);
+  float* r = cred + NW * 64;  // disjoint from the sweep combine area
+  if (lane < 16) {
+    r[w * 64 + c] = a0;
+    r[w * 64 + 16 + c] = a1;
+    r[w * 64 + 32 + c] = b0;
+    r[w * 64 + 48 + c] = b1;
+  }
+  lds_barrier();
+  float v = 0.f;
+  if (t < 64) {
+#pragma unroll
+    for (int k = 0; k < NW; ++k) v += r[k * 64 + t];
+  }
+  return v;
+}
+
+__device__ __forceinline__ unsigned tagof(int epoch, int round) { return (unsigned)(epoch * 64 + round + 1); }
+__device__ __forceinline__ unsigned long long* gslot(const Args& pa, int round, int L) {
+  return pa.gran + ((size_t)(round & 1) * LMAX + L) * GSTR;
+}
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t grsrc(const Args& pa, int round) {
+  return __builtin_amdgcn_make_buffer_rsrc(pa.gran + (size_t)(round & 1) * LMAX * GSTR, (short)0,
+                                           LMAX * GSTR * 8, 0x00020000);
+}
+// one granule, one sc1 store
+__device__ __forceinline__ void gput(unsigned long long* g, unsigned tag, float v) {
+  __hip_atomic_store(g, ((unsigned long long)tag << 32) | __float_as_uint(v), __ATOMIC_RELAXED,
+                     __HIP_MEMORY_SCOPE_AGENT);
+}
+// publish this lane's 8 values of a boundary row (which: 0 = my top row, 1 = my bottom row): 4 x 16-B sc1
+// stores, each holding two whole granules
+__device__ __forceinline__ void publish_row(const Args& pa, int round, int L, int which, unsigned tag,
+                                            const float (&v)[2][4], int lane) {
+  const __amdgpu_buffer_rsrc_t rs = grsrc(pa, round);
+  const int base = (L * GSTR + 64 + which * 512) * 8;
+#pragma unroll
+  for (int h = 0; h < 2; ++h)
+#pragma unroll
+    for (int p = 0; p < 2; ++p) {
+      const v4u x = v4u{__float_as_uint(v[h][2 * p]), tag, __float_as_uint(v[h][2 * p + 1]), tag};
+      __builtin_amdgcn_raw_buffer_store_b128(x, rs, base + (h * 256 + lane * 4 + 2 * p) * 8, 0, 16);
+    }
+}
+// one poll pass over the 8 granules of a neighbour's boundary row this lane needs; true when all carry `tag`
+__device__ __forceinline__ bool poll_row(const Args& pa, int round, int Lsrc, int which, unsigned tag,
+                                         float (&v)[2][4], int lane) {
+  const __amdgpu_buffer_rsrc_t rs = grsrc(pa, round);
+  const int base = (Lsrc * GSTR + 64 + which * 512) * 8;
+  v4u x[2][2];
+#pragma unroll
+  for (int h = 0; h < 2; ++h)
+#pragma unroll
+    for (int p = 0; p < 2; ++p)
+      x[h][p] = __builtin_amdgcn_raw_buffer_load_b128(rs, base + (h * 256 + lane * 4 + 2 * p) * 8, 0, 16);
+  bool ok = true;
+#pragma unroll
+  for (int h = 0; h < 2; ++h)
+#pragma unroll
+    for (int p = 0; p < 2; ++p) {
+      ok &= x[h][p][1] == tag && x[h][p][3] == tag;
+      v[h][2 * p] = __uint_as_float(x[h][p][0]);
+      v[h][2 * p + 1] = __uint_as_float(x[h][p][2]);
+    }
+  return ok;
+}
+
+// BN sweep pass: lane l reads slots 2(l & 31), 2(l & 31) + 1 of workgroups 2w + (l >> 5) + 2 NW k (one 16-B sc1
+// load = two granules), k < KS; sums in k order.  Slots past the grid read a valid (clamped) granule and count 0.
+template <int KS>
+__device__ __forceinline__ bool sweep_pass(const __amdgpu_buffer_rsrc_t rs, int w, int lane, int G, unsigned tag,
+                                           float& s0, float& s1) {
+  const int j = lane & 31, hf = lane >> 5;
+  v4u x[KS];
+#pragma unroll
+  for (int k = 0; k < KS; ++k) {
+    const int Lk = 2 * w + hf + 2 * NW * k, Lc = Lk < G ? Lk : G - 1;
+    x[k] = __builtin_amdgcn_raw_buffer_load_b128(rs, (Lc * GSTR + 2 * j) * 8, 0, 16);
+  }
+  bool ok = true;
+  s0 = 0.f;
+  s1 = 0.f;
+#pragma unroll
+  for (int k = 0; k < KS; ++k) {
+    const bool valid = 2 * w + hf + 2 * NW * k < G;
+    ok &= !valid || (x[k][1] == tag && x[k][3] == tag);
+    s0 += valid ? __uint_as_float(x[k][0]) : 0.f;
+    s1 += valid ? __uint_as_float(x[k][2]) : 0.f;
+  }
+  return ok;
+}
+template <int KS>
+__device__ __forceinline__ void sweep_wait(const Args& pa, int round, int w, int lane, int G, unsigned tag,
+                                           float& s0, float& s1) {
+  const __amdgpu_buffer_rsrc_t rs = grsrc(pa, round);
+  for (unsigned spins = 0;; ++spins) {
+    asm volatile("" ::: "memory");  // the loads are re-issued every pass
+    if (__all(sweep_pass<KS>(rs, w, lane, G, tag, s0, s1))) return;
+    if (spins >= SPIN_LIMIT) {
+      if (lane == 0) atomicOr(pa.err, 1u << (round & 31));
+      return;
+    }
+  }
+}
+// All-to-all BN exchange wait + (halo waves) the neighbour's boundary row.  On return cred[0 .. NW*64) holds every
+// wave's partial totals (the caller's barrier makes them visible): tot(slot) = sum_k cred[k * 64 + slot].
+__device__ __forceinline__ void xchg_wait(const Args& pa, int round, int epoch, int G, float* cred, bool halo,
+                                          int Lsrc, int which, float (&hv)[2][4]) {
+  const int t = threadIdx.x, lane = t & 63;
+  const int w = __builtin_amdgcn_readfirstlane(t >> 6);
+  const unsigned tag = tagof(epoch, round);
+  float s0, s1;
+  if (G <= 2 * NW * 8) sweep_wait<8>(pa, round, w, lane, G, tag, s0, s1);
+  else if (G <= 2 * NW * 16) sweep_wait<16>(pa, round, w, lane, G, tag, s0, s1);
+  else sweep_wait<32>(pa, round, w, lane, G, tag, s0, s1);
+  s0 += __shfl_xor(s0, 32);  // the two half-waves read different workgroups
+  s1 += __shfl_xor(s1, 32);
+  if (lane < 32) {
+    cred[w * 64 + 2 * lane] = s0;
+    cred[w * 64 + 2 * lane + 1] = s1;
+  }
+  if (halo) {
+    for (unsigned spins = 0;; ++spins) {
+      asm volatile("" ::: "memory");
+      if (__all(poll_row(pa, round, Lsrc, which, tag, hv, lane))) break;
+      if (spins >= SPIN_LIMIT) {
+        if (lane == 0) atomicOr(pa.err, 1u << (round & 31));
+        break;
+      }
+    }
+  }
+}
+__device__ __forceinline__ float slot_total(const float* cred, int slot) {
+  float a = 0.f;
+#pragma unroll
+  for (int k = 0; k < NW; ++k) a += cred[k * 64 + slot];
+  return a;
+}
+
+// tiled global activation layout of one image row: element (col 4q + i, ch 16h + c) at h*256 + (16q + c)*4 + i
+__device__ __forceinline__ void st8(float* p, int lane, const float (&v)[2][4]) {
+#pragma unroll
+  for (int h = 0; h < 2; ++h) *(f32x4*)(p + h * 256 + lane * 4) = f32x4{v[h][0], v[h][1], v[h][2], v[h][3]};
+}
+__device__ __forceinline__ void ld8(const float* p, int lane, float (&v)[2][4]) {
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const f32x4 u = *(const f32x4*)(p + h * 256 + lane * 4);
+    v[h][0] = u[0];
+    v[h][1] = u[1];
+    v[h][2] = u[2];
+    v[h][3] = u[3];
+  }
+}
+
+// wgrad of one application, accumulated in registers: D[co][ci,tap] += sum over this slice's pixels of
+// dy[p][co] x[p + tap][ci].  Wave w owns tile columns nt = w, w + NW, ... (ci half x tap), both co halves; K steps
+// of 32 pixels = two image rows.
+template <int P>
+__device__ __forceinline__ void wgrad_acc(const unsigned short* dyT, const unsigned short* xT, f32x4 (&wacc)[NNT][2],
+                                          int w, int lane) {
+  using PL = Plan<P>;
+  const int c = lane & 15, q = lane >> 4;
+  constexpr int DYO = PL::DYT_PL / 2, XTO = PL::XT_PL / 2;  // lo-plane offsets (elements)
+#pragma unroll
+  for (int s = 0; s < RS / 2; ++s) {
+    const int row = 2 * s + (q >> 1), c0 = 8 * (q & 1);
+    const int ao0 = c * PL::DYT_S + row * 16 + c0, ao1 = (16 + c) * PL::DYT_S + row * 16 + c0;
+    const bf16x8 a0 = *(const bf16x8*)(dyT + ao0);
+    const bf16x8 a1 = *(const bf16x8*)(dyT + ao1);
+    bf16x8 a0l = a0, a1l = a1;
+    if constexpr (P == 1) {
+      a0l = *(const bf16x8*)(dyT + DYO + ao0);
+      a1l = *(const bf16x8*)(dyT + DYO + ao1);
+    }
+#pragma unroll
+    for (int j = 0; j < NNT; ++j) {
+      const int nt = w + NW * j;
+      if (nt < 18) {
+        const int tap = nt >> 1, cih = nt & 1, kh = tap / 3, kw = tap % 3;
+        const int bo = (kw * 32 + 16 * cih + c) * PL::XT_S + (row + kh) * 16 + c0;
+        const bf16x8 b = *(const bf16x8*)(xT + bo);
+        bf16x8 bl = b;
+        if constexpr (P == 1) bl = *(const bf16x8*)(xT + XTO + bo);
+        wacc[j][0] = mma3<P>(a0, a0l, b, bl, wacc[j][0]);
+        wacc[j][1] = mma3<P>(a1, a1l, b, bl, wacc[j][1]);
+      }
+    }
+  }
+}
+// one lane's 4 consecutive columns (4q .. 4q+3) of x, channel ch, into the three column-shifted copies of xT row
+// `xrow` (copy kw holds x[col + kw - 1] at col)
+__device__ __forceinline__ void xt_put(unsigned short* xT, int XT_S, int xrow, int ch, int q, unsigned b0, unsigned b1,
+                                       unsigned b2, unsigned b3) {
+  const int rowoff = xrow * 16 + 4 * q;
+  unsigned short* p1 = xT + (32 + ch) * XT_S + rowoff;
+  *(uint2*)p1 = uint2{b0 | (b1 << 16), b2 | (b3 << 16)};
+  unsigned short* p0 = xT + ch * XT_S + rowoff;
+  p0[1] = (unsigned short)b0;
+  *(unsigned*)(p0 + 2) = b1 | (b2 << 16);
+  if (q < 3) p0[4] = (unsigned short)b3;
+  unsigned short* p2 = xT + (64 + ch) * XT_S + rowoff;
+  if (q > 0) p2[-1] = (unsigned short)b0;
+  *(unsigned*)p2 = b1 | (b2 << 16);
+  p2[2] = (unsigned short)b3;
+}
+template <int P>
+__device__ __forceinline__ void xt_row(unsigned short* xT, int xrow, int q, int c, const float (&x)[2][4]) {
+  using PL = Plan<P>;
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const int ch = 16 * h + c;
+    unsigned hb[4], lb[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const unsigned short hi = bfbits(x[h][i]);
+      hb[i] = hi;
+      lb[i] = P == 1 ? bf_lo(x[h][i], hi) : 0u;
+    }
+    xt_put(xT, PL::XT_S, xrow, ch, q, hb[0], hb[1], hb[2], hb[3]);
+    if constexpr (P == 1) xt_put(xT + PL::XT_PL / 2, PL::XT_S, xrow, ch, q, lb[0], lb[1], lb[2], lb[3]);
+  }
+}
+// a row of records (x or dy, both channel halves) of this lane into XR row `xrow`
+template <int P>
+__device__ __forceinline__ void xr_row(char* XR, int xrow, int q, int c, const float (&v)[2][4]) {
+  using PL = Plan<P>;
+#pragma unroll
+  for (int h = 0; h < 2; ++h)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) st1r<P>(XR, PL::XR_PL, xrow * 18 + 4 * q + i + 1, 16 * h + c, v[h][i]);
+}
+
+// weight staging: NP planes of 1152 16-B chunks, loaded to registers (all in flight), stored as records
+template <int P>
+struct WStage {
+  static constexpr int M = (1152 + NTH - 1) / NTH;
+  uint4 v[P + 1][M];
+};
+template <int P>
+__device__ __forceinline__ void wstage_load(WStage<P>& ws, const unsigned short* src) {
+#pragma unroll
+  for (int p = 0; p <= P; ++p)
+#pragma unroll
+    for (int m = 0; m < WStage<P>::M; ++m) {
+      const int idx = threadIdx.x + NTH * m;
+      ws.v[p][m] = ((const uint4*)(src + p * 9216))[idx < 1152 ? idx : 1151];
+    }
+#pragma unroll
+  for (int p = 0; p <= P; ++p)
+#pragma unroll
+    for (int m = 0; m < WStage<P>::M; ++m) pin(ws.v[p][m]);
+}
+// the same without forcing the wait: for prefetches issued before an exchange (the spin loop's memory clobber
+// keeps them above it, their wait lands at first use)
+template <int P>
+__device__ __forceinline__ void wstage_prefetch(WStage<P>& ws, const unsigned short* src) {
+#pragma unroll
+  for (int p = 0; p <= P; ++p)
+#pragma unroll
+    for (int m = 0; m < WStage<P>::M; ++m) {
+      const int idx = threadIdx.x + NTH * m;
+      ws.v[p][m] = ((const uint4*)(src + p * 9216))[idx < 1152 ? idx : 1151];
+    }
+}
+template <int P>
+__device__ __forceinline__ void wstage_store(const WStage<P>& ws, char* wt) {
+#pragma unroll
+  for (int p = 0; p <= P; ++p)
+#pragma unroll
+    for (int m = 0; m < WStage<P>::M; ++m) {
+      const int idx = threadIdx.x + NTH * m;
+      if (idx < 1152) *(uint4*)(wt + p * Plan<P>::WT_PL + (idx >> 2) * RB + (idx & 3) * 16) = ws.v[p][m];
+    }
+}
+
+constexpr int P_KSHIFT = 906;  // misc: [10][32] BN shifts (last step's batch means)
+constexpr int P_LABEL = 1240;  // misc: this image's label
+
+// ============================================================================================================
+template <int P>
+__global__ void __launch_bounds__(NTH) k_pks_step(Ctx cx, Args pa) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  using PL = Plan<P>;
+  const int t = threadIdx.x, w = t >> 6, lane = t & 63, c = lane & 15, q = lane >> 4;
+  // Placement (speed only, never correctness): blocks b and b + 8 share an XCD under the observed round-robin
+  // dispatch, so the S slices of an image get block ids 8 apart and their halo hand-offs stay in one L2.
+  const int b = blockIdx.x, s = (b >> 3) % S, n = (b >> 3) / S * 8 + (b & 7);
+  const int B = cx.B;
+  if (n >= B) return;
+  const int L = n * S + s, G = B * S;
+  const int row = s * RS + w;  // image row of this wave
+  const bool halo = (w == 0 && s > 0) || (w == NW - 1 && s < S - 1);  // this wave keeps a neighbour row
+  const int hwhich = w == 0 ? 0 : 1;                  // the boundary row this wave publishes: 0 top, 1 bottom
+  const int hsrc = w == 0 ? L - 1 : L + 1;            // ... and whose boundary row it receives
+  const int hxrow = w == 0 ? 0 : RS + 1;              // XR / xT row of the received halo
+  float* cred = (float*)(smem + PL::O_CRED);
+  float* stat = (float*)(smem + PL::O_STAT);
+  float* scsh = (float*)(smem + PL::O_SCSH);
+  float* misc = (float*)(smem + PL::O_MISC);
+  char* U = smem + PL::O_U;
+  char* WT = U + PL::U_WT;
+  char* XR = U + PL::U_XR;
+  const int epoch = *pa.epoch;
+  const int par = epoch & 1;
+  const uint8_t* my_img = pa.simg + (size_t)(par * 64 + n) * 3072;
+  const int next_id = sample_id(cx, B + n);
+  const float Ntot = (float)B * 256.f;
+  const unsigned short* pkw = (const unsigned short*)cx.pkw;
+  DCA_STAMP(cx, 0, L, 0);
+
+  float x[2][4];        // this wave's row of the current block input (forward), x_{i+1} (backward)
+  float xo[2][4] = {};  // halo waves: the neighbour row of the same
+  float y[2][4];        // conv output of the current block
+
+  // ======================= stem: gather + normalise + conv1 + bias + ReLU + 2x2 max-pool ======================
+  // Pooled rows 4s-1 .. 4s+4 (own + one halo row each side, recomputed here: the input image is read-only).
+  // Input staged as bf16 NHWC4 pixels (3 channels + a zero): an MFMA K-group of 4 is one tap of one pixel
+  // (v_mfma_f32_16x16x16_bf16, K = (tap, channel), 3 MFMAs cover the 9 taps; taps 9..11 have zero weights).
+  {
+    uint2* xin4 = (uint2*)(U + PL::U_XIN);
+    float* x0i = (float*)(U + PL::U_X0);
+    uint8_t* scl = (uint8_t*)(U + PL::U_SCODE);
+    // step constants -> misc (as netresdeep_persistent.hip): k < 64: BN gamma|beta -> misc[320 + k]; k >= 64 ->
+    // misc[384 + k]: running mean|var [448,512) (rank 0's base under DDP, CC4), fc1 bias [512,544), W2
+    // [544,864), b2 [864,874), conv1 bias [874,906), BN shifts [906,1226)
+    constexpr int NKC = 842, KCM = (NKC + NTH - 1) / NTH;
+    float kc[KCM];
+#pragma unroll
+    for (int m = 0; m < KCM; ++m) {
+      const int k = min(t + NTH * m, NKC - 1);
+      const float* rsm = cx.ws > 1 ? cx.rs_base : cx.rm;
+      const float* rsv = cx.ws > 1 ? cx.rs_base + 32 : cx.rv;
+      const float* src = k < 64 ? cx.params + OFF_BNW + k
+                       : k < 96 ? rsm + (k - 64)
+                       : k < 128 ? rsv + (k - 96)
+                       : k < 160 ? cx.params + OFF_FC1B + (k - 128)
+                       : k < 480 ? cx.params + OFF_FC2W + (k - 160)
+                       : k < 490 ? cx.params + OFF_FC2B + (k - 480)
+                       : k < 522 ? cx.params + OFF_C1B + (k - 490)
+                                 : (const float*)cx.STATS + 2 * (k - 522);
+      kc[m] = *src;
+    }
+    int lab = pa.slab[par * 64 + n];
+    // input words: thread t < 112 -> xin4 row j = t >> 3 (image row 8s-3+j), 4 columns 4 (t & 7) .., 3 channels
+    const int jr = (t >> 3) < 14 ? (t >> 3) : 13, yimg = 8 * s - 3 + jr, xq = t & 7;
+    const bool ivalid = t < 112 && yimg >= 0 && yimg < 32;
+    const unsigned* imw = (const unsigned*)my_img;
+    const int yc = yimg < 0 ? 0 : (yimg > 31 ? 31 : yimg);
+    unsigned iw0 = imw[yc * 8 + xq], iw1 = imw[256 + yc * 8 + xq], iw2 = imw[512 + yc * 8 + xq];
+    WStage<P> wst;
+    wstage_load<P>(wst, pkw);  // forward trunk weights [tap][co][ci] (hi, lo)
+    uint2 bwr[P + 1][2][3];    // conv1 B fragments: lane (co = 16h + c, k-group q) of MFMA m
+#pragma unroll
+    for (int p = 0; p <= P; ++p)
+#pragma unroll
+      for (int h = 0; h < 2; ++h)
+#pragma unroll
+        for (int m = 0; m < 3; ++m) bwr[p][h][m] = ((const uint2*)(pkw + 36864 + p * 1536))[(h * 3 + m) * 64 + lane];
+#pragma unroll
+    for (int m = 0; m < KCM; ++m) pin(kc[m]);
+    pin(lab);
+    pin(iw0);
+    pin(iw1);
+    pin(iw2);
+#pragma unroll
+    for (int p = 0; p <= P; ++p)
+#pragma unroll
+      for (int h = 0; h < 2; ++h)
+#pragma unroll
+        for (int m = 0; m < 3; ++m) pin(bwr[p][h][m]);
+#pragma unroll
+    for (int m = 0; m < KCM; ++m) {
+      const int k = t + NTH * m;
+      if (k < NKC) misc[(k < 64 ? 320 : 384) + k] = k >= 522 && !(fabsf(kc[m]) < 1e30f) ? 0.f : kc[m];
+    }
+    if (t == 0) misc[P_LABEL] = __int_as_float(lab);
+    if (t < 112) {
+#pragma unroll
+      for (int b2 = 0; b2 < 4; ++b2) {
+        const float v0 = ivalid ? norm_px((iw0 >> (8 * b2)) & 255u, 0) : 0.f;
+        const float v1 = ivalid ? norm_px((iw1 >> (8 * b2)) & 255u, 1) : 0.f;
+        const float v2 = ivalid ? norm_px((iw2 >> (8 * b2)) & 255u, 2) : 0.f;
+        const unsigned short h0 = bfbits(v0), h1 = bfbits(v1), h2 = bfbits(v2);
+        const int px = jr * 34 + 4 * xq + 1 + b2;
+        xin4[px] = uint2{(unsigned)h0 | ((unsigned)h1 << 16), (unsigned)h2};
+        if constexpr (P == 1)
+          xin4[PL::XIN_PL / 8 + px] = uint2{(unsigned)bf_lo(v0, h0) | ((unsigned)bf_lo(v1, h1) << 16),
+                                            (unsigned)bf_lo(v2, h2)};
+      }
+    } else if (t < 112 + 28) {  // columns 0 and 33 of the 14 rows
+      const int k = t - 112, px = (k >> 1) * 34 + ((k & 1) ? 33 : 0);
+      xin4[px] = uint2{0u, 0u};
+      if constexpr (P == 1) xin4[PL::XIN_PL / 8 + px] = uint2{0u, 0u};
+    }
+    wstage_store<P>(wst, WT);
+    for (int idx = t; idx < PL::NP * PL::XR_PL / 16; idx += NTH) ((uint4*)XR)[idx] = uint4{0u, 0u, 0u, 0u};
+    lds_barrier();
+    DCA_STAMP(cx, 0, L, 2);
+    s4v bw[P + 1][2][3];
+#pragma unroll
+    for (int p = 0; p <= P; ++p)
+#pragma unroll
+      for (int h = 0; h < 2; ++h)
+#pragma unroll
+        for (int m = 0; m < 3; ++m) bw[p][h][m] = __builtin_bit_cast(s4v, bwr[p][h][m]);
+    const float* sb = misc + 874;
+    // units: (pooled row 4s-1+ur, column half), ur = 0..RS+1; wave w takes units w, w + NW, ...
+#pragma unroll 1
+    for (int u = w; u < 2 * (RS + 2); u += NW) {
+      const int ur = u >> 1, chalf = u & 1, pr = 4 * s - 1 + ur;
+      if (pr < 0 || pr > 15) continue;  // wave-uniform: the image border (XR rows stay zero)
+      f32x4 acc[2][2];
+#pragma unroll
+      for (int rw = 0; rw < 2; ++rw) {
+        acc[rw][0] = z4();
+        acc[rw][1] = z4();
+#pragma unroll
+        for (int m = 0; m < 3; ++m) {
+          const int tap = 4 * m + q, tc = tap < 9 ? tap : 0, kh = tc / 3, kw = tc % 3;
+          const int px = (2 * ur + rw + kh) * 34 + 16 * chalf + c + kw;
+          const s4v a = __builtin_bit_cast(s4v, xin4[px]);
+          s4v al = a;
+          if constexpr (P == 1) al = __builtin_bit_cast(s4v, xin4[PL::XIN_PL / 8 + px]);
+          acc[rw][0] = mma3s<P>(a, al, bw[0][0][m], bw[P][0][m], acc[rw][0]);
+          acc[rw][1] = mma3s<P>(a, al, bw[0][1][m], bw[P][1][m], acc[rw][1]);
+        }
+      }
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int co = 16 * h + c;
+        const float bias = sb[co];
+#pragma unroll
+        for (int pp = 0; pp < 2; ++pp) {
+          const float v00 = fmaxf(acc[0][h][2 * pp] + bias, 0.f), v01 = fmaxf(acc[0][h][2 * pp + 1] + bias, 0.f);
+          const float v10 = fmaxf(acc[1][h][2 * pp] + bias, 0.f), v11 = fmaxf(acc[1][h][2 * pp + 1] + bias, 0.f);
+          float best = v00;
+          int code = 0;
+          if (v01 > best) { best = v01; code = 1; }
+          if (v10 > best) { best = v10; code = 2; }
+          if (v11 > best) { best = v11; code = 3; }
+          if (best > 0.f) code |= 4;
+          const int pc = 8 * chalf + 2 * q + pp;
+          x0i[(ur * 16 + pc) * PL::X0S + co] = best;
+          if (ur >= 1 && ur <= RS) scl[((ur - 1) * 16 + pc) * 32 + co] = (uint8_t)code;
+          st1r<P>(XR, PL::XR_PL, ur * 18 + pc + 1, co, best);
+        }
+      }
+    }
+    lds_barrier();
+    DCA_STAMP(cx, 0, L, 3);
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      unsigned cw = 0;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        x[h][i] = x0i[((w + 1) * 16 + 4 * q + i) * PL::X0S + 16 * h + c];
+        if (halo) xo[h][i] = x0i[(hxrow * 16 + 4 * q + i) * PL::X0S + 16 * h + c];
+        cw |= (unsigned)scl[(w * 16 + 4 * q + i) * 32 + 16 * h + c] << (8 * i);
+      }
+      // stem pool codes, read back by this very thread in the stem backward
+      *(unsigned*)(cx.SCODE + (size_t)n * 8192 + row * 512 + h * 256 + lane * 4) = cw;
+    }
+    if (pa.debug) st8(cx.X + (size_t)n * 8192 + row * 512, lane, x);
+  }
+  DCA_STAMP(cx, 0, L, 1);
+
+  // ======================= forward: 10 applications of the shared ResBlock ===================================
+  // fc1 weights of this slice's 512 pooled features (local index u = ch*16 + pr*8 + pw <-> global feature
+  // ch*64 + (2s + pr)*8 + pw: per row, 32 runs of 16 contiguous elements), loaded into registers before the last
+  // exchange so its wait hides the latency, then staged in LDS for fc1 (reduction over features) and its
+  // transpose dp (reduction over rows)
+  constexpr int W1M = P == 1 ? 16 : 8;  // 16-B chunks per thread: 32 rows x 512 x (4 | 2) B / 16 B / 256
+  uint4 w1r[W1M];
+  WStage<P> wst_d;  // dgrad weights, staged into WT during the head
+#pragma unroll 1
+  for (int i = 0; i < NBLK; ++i) {
+    f32x4 acc[2];
+    conv_row<P>(XR, WT, acc, w, lane);
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+      for (int i2 = 0; i2 < 4; ++i2) y[h][i2] = acc[h][i2];
+    if (i == 5) DCA_STAMP(cx, 6, L, 0);
+    // shifted one-pass sums S1 = sum(y - K), S2 = sum((y - K)^2); K = this block's batch mean of the previous
+    // step (0 at the first), identical in every workgroup, so the partials combine exactly
+    const float K0 = misc[P_KSHIFT + i * 32 + c], K1 = misc[P_KSHIFT + i * 32 + 16 + c];
+    float a0 = 0.f, a1 = 0.f, b0 = 0.f, b1 = 0.f;
+#pragma unroll
+    for (int i2 = 0; i2 < 4; ++i2) {
+      const float d0 = y[0][i2] - K0, d1 = y[1][i2] - K1;
+      a0 += d0;
+      a1 += d1;
+      b0 += d0 * d0;
+      b1 += d1 * d1;
+    }
+    const float pv = wg_csum(a0, a1, b0, b1, cred);
+    const unsigned tag = tagof(epoch, i);
+    if (t < 64) gput(gslot(pa, i, L) + t, tag, pv);
+    if (halo) publish_row(pa, i, L, hwhich, tag, y, lane);
+    // meanwhile: this block's y (and, debug, x) for the backward / diagnostics
+    st8(cx.Y + (size_t)i * B * 8192 + (size_t)n * 8192 + row * 512, lane, y);
+    if (i == NBLK - 1) {
+      // chunk k = t + 256 m: row j, run ch, piece pc (P=1: 4 pieces of 4 floats, P=0: 2 of 8 bf16)
+#pragma unroll
+      for (int m = 0; m < W1M; ++m) {
+        const int k = t + NTH * m;
+        if constexpr (P == 1) {
+          const int j = k >> 7, ch = (k >> 2) & 31, pc = k & 3;
+          w1r[m] = *(const uint4*)(cx.params + OFF_FC1W + j * 2048 + ch * 64 + 16 * s + 4 * pc);
+        } else {
+          const int j = k >> 6, ch = (k >> 1) & 31, pc = k & 1;
+          w1r[m] = *(const uint4*)((const unsigned short*)cx.w1b + j * 2048 + ch * 64 + 16 * s + 8 * pc);
+        }
+      }
+      wstage_prefetch<P>(wst_d, pkw + 18432);  // dgrad weights [tap'][ci][co] (hi, lo)
+    }
+    float yo[2][4];
+    if (i == 5) DCA_STAMP(cx, 6, L, 1);
+    xchg_wait(pa, i, epoch, G, cred, halo, hsrc, hwhich ^ 1, yo);
+    if (i == 5) DCA_STAMP(cx, 6, L, 2);
+    lds_barrier();
+    if (i == 5) DCA_STAMP(cx, 6, L, 3);
+    if (halo) st8(pa.yh + ((size_t)(i * LMAX + L) * 2 + hwhich) * 512, lane, yo);
+    // every thread finalises the statistics of its own two channels (same sums, same order everywhere)
+    float scv[2], shv[2];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int ch = 16 * h + c;
+      const float S1 = slot_total(cred, ch), S2 = slot_total(cred, 32 + ch);
+      const float dm = S1 / Ntot;
+      const float mean = misc[P_KSHIFT + i * 32 + ch] + dm;
+      const float var = fmaxf(S2 / Ntot - dm * dm, 0.f);
+      const float invstd = rsqrtf(var + cx.bn_eps);
+      scv[h] = misc[320 + ch] * invstd;
+      shv[h] = misc[352 + ch] - mean * scv[h];
+      if (w == 0 && q == 0) {
+        stat[i * 64 + ch] = mean;
+        stat[i * 64 + 32 + ch] = invstd;
+        scsh[i * 64 + ch] = scv[h];
+        scsh[i * 64 + 32 + ch] = shv[h];
+        if (L == 0) {  // BN running statistics (10 EMAs per forward) and the batch stats for the next step
+          const float unb = var * Ntot / (Ntot - 1.f), mo = cx.bn_mom;
+          misc[448 + ch] = misc[448 + ch] * (1.f - mo) + mean * mo;
+          misc[480 + ch] = misc[480 + ch] * (1.f - mo) + unb * mo;
+          cx.STATS[i * 32 + ch] = make_float2(mean, invstd);
+        }
+      }
+    }
+    // x_{i+1} = relu(bn(y_i)) + x_i, own row and (halo waves) the neighbour row
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+      for (int i2 = 0; i2 < 4; ++i2) {
+        x[h][i2] = fmaxf(__builtin_fmaf(y[h][i2], scv[h], shv[h]), 0.f) + x[h][i2];
+        if (halo) xo[h][i2] = fmaxf(__builtin_fmaf(yo[h][i2], scv[h], shv[h]), 0.f) + xo[h][i2];
+      }
+    if (i < NBLK - 1) {
+      xr_row<P>(XR, w + 1, q, c, x);
+      if (halo) xr_row<P>(XR, hxrow, q, c, xo);
+      if (pa.debug) st8(cx.X + (size_t)(i + 1) * B * 8192 + (size_t)n * 8192 + row * 512, lane, x);
+      lds_barrier();
+    }
+    DCA_STAMP(cx, 1 + i / 8, L, i % 8);
+  }
+  if (L == 0 && t < 32) {
+    cx.rm[t] = misc[448 + t];
+    cx.rv[t] = misc[480 + t];
+  }
+
+  // ======================= head ==============================================================================
+  // x10 (registers) -> LDS -> 2x2 max-pool -> fc1 partial over this slice's 512 features -> the S slices of the
+  // image exchange their partials -> fc1 + ReLU, fc2, cross-entropy (mean over the batch) and their backward
+  // (every slice, redundantly) -> dp = W1^T dh for this slice's features -> max-pool backward -> g = dL/dx10.
+  float g[2][4];
+  {
+    float* x10 = (float*)(U + PL::U_X10);
+    uint8_t* pcode = (uint8_t*)(U + PL::U_PCODE);
+    float* dpl = (float*)(U + PL::U_DP);
+    float* pl = (float*)(U + PL::U_PL);
+    float* hp = (float*)(U + PL::U_HP);
+    char* w1l = U + PL::U_W1;
+    wstage_store<P>(wst_d, WT);  // every conv read of WT is done (block 9's conv preceded its exchange)
+#pragma unroll
+    for (int m = 0; m < W1M; ++m) {
+      const int k = t + NTH * m;
+      if constexpr (P == 1) {
+        const int j = k >> 7, ch = (k >> 2) & 31, pc = k & 3;
+        *(uint4*)(w1l + (j * PL::W1S + ch * 16 + 4 * pc) * 4) = w1r[m];
+      } else {
+        const int j = k >> 6, ch = (k >> 1) & 31, pc = k & 1;
+        *(uint4*)(w1l + (j * PL::W1S + ch * 16 + 8 * pc) * 2) = w1r[m];
+      }
+    }
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+      for (int i2 = 0; i2 < 4; ++i2) x10[(w * 16 + 4 * q + i2) * PL::X10S + 16 * h + c] = x[h][i2];
+    lds_barrier();
+    // pool: thread t -> channel ch = t >> 3, local pool row pr = (t >> 2) & 1, pool cols 2 (t & 3) + {0, 1}
+    {
+      const int ch = t >> 3, pr = (t >> 2) & 1;
+      float pv[2];
+#pragma unroll
+      for (int k = 0; k < 2; ++k) {
+        const int pc = 2 * (t & 3) + k;
+        float v[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e)  // window order (0,0) (0,1) (1,0) (1,1): first maximum wins
+          v[e] = x10[((2 * pr + (e >> 1)) * 16 + 2 * pc + (e & 1)) * PL::X10S + ch];
+        float best = v[0];
+        unsigned id = 0;
+        if (v[1] > best) { best = v[1]; id = 1; }
+        if (v[2] > best) { best = v[2]; id = 2; }
+        if (v[3] > best) { best = v[3]; id = 3; }
+        pv[k] = best;
+        pcode[2 * t + k] = (uint8_t)id;  // local feature u = ch*16 + pr*8 + pc = 2t + k
+      }
+      *(float2*)(pl + 2 * t) = make_float2(pv[0], pv[1]);
+      // fc1 input for the weight gradient: global feature ch*64 + (2s + pr)*8 + pc
+      *(float2*)(cx.HP + (size_t)n * 2048 + ch * 64 + (2 * s + pr) * 8 + 2 * (t & 3)) = make_float2(pv[0], pv[1]);
+    }
+    lds_barrier();
+    // fc1 partial over this slice's features: thread (row j = t >> 3, part k = t & 7) sums features u = 8m + k,
+    // then 3 xor-shuffles over the 8 parts (fixed order: identical in every workgroup)
+    {
+      const int j = t >> 3, k = t & 7;
+      float a = 0.f;
+#pragma unroll 8
+      for (int m = 0; m < 64; ++m) {
+        const int u = 8 * m + k;
+        const float wv = P == 1 ? ((const float*)w1l)[j * PL::W1S + u]
+                                : __uint_as_float((unsigned)((const unsigned short*)w1l)[j * PL::W1S + u] << 16);
+        a += wv * pl[u];
+      }
+      a += __shfl_xor(a, 1);
+      a += __shfl_xor(a, 2);
+      a += __shfl_xor(a, 4);
+      if (k == 0) hp[j] = a;
+    }
+    lds_barrier();
+    DCA_STAMP(cx, 3, L, 1);
+    const unsigned tag = tagof(epoch, RND_HEAD);
+    if (t < 32) gput(gslot(pa, RND_HEAD, L) + t, tag, hp[t]);
+    if (w == 0) {
+      // the image's S partials, summed in slice order (bitwise identical in every slice); fc1 bias + ReLU, fc2,
+      // softmax cross-entropy and dh, lane-parallel with shuffles
+      float hh = 0.f;
+      {
+        const __amdgpu_buffer_rsrc_t rs = grsrc(pa, RND_HEAD);
+        const int sl = lane & 31;
+        for (unsigned spins = 0;; ++spins) {
+          asm volatile("" ::: "memory");
+          bool ok = true;
+          float a = 0.f;
+#pragma unroll
+          for (int s2 = 0; s2 < S; ++s2) {
+            const auto xg = __builtin_amdgcn_raw_buffer_load_b64(rs, ((n * S + s2) * GSTR + sl) * 8, 0, 16);
+            ok &= xg[1] == tag;
+            a += __uint_as_float(xg[0]);
+          }
+          hh = a;
+          if (__all(ok)) break;
+          if (spins >= SPIN_LIMIT) {
+            if (lane == 0) atomicOr(pa.err, 1u << RND_HEAD);
+            break;
+          }
+        }
+      }
+      DCA_STAMP(cx, 3, L, 2);
+      hh += misc[512 + (lane & 31)];
+      const float hr = fmaxf(hh, 0.f);
+      const int o = lane < 10 ? lane : 0;
+      float logit = misc[864 + o];
+#pragma unroll
+      for (int jj = 0; jj < 32; ++jj)
+        logit += misc[544 + o * 32 + jj] * __int_as_float(__builtin_amdgcn_readlane(__float_as_int(hr), jj));
+      float lg[10];
+#pragma unroll
+      for (int oo = 0; oo < 10; ++oo) lg[oo] = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(logit), oo));
+      float mx = lg[0];
+#pragma unroll
+      for (int oo = 1; oo < 10; ++oo) mx = fmaxf(mx, lg[oo]);
+      float ex[10], se = 0.f;
+#pragma unroll
+      for (int oo = 0; oo < 10; ++oo) {
+        ex[oo] = __expf(lg[oo] - mx);
+        se += ex[oo];
+      }
+      const float lse = mx + __logf(se), rse = 1.f / se;
+      const int label = __float_as_int(misc[P_LABEL]);
+      float lt = lg[0];
+#pragma unroll
+      for (int oo = 1; oo < 10; ++oo) lt = label == oo ? lg[oo] : lt;
+      const float invB = 1.f / (float)B;
+      float sd = 0.f, dl = 0.f;
+#pragma unroll
+      for (int oo = 0; oo < 10; ++oo) {
+        const float dlo = (ex[oo] * rse - (oo == label ? 1.f : 0.f)) * invB;
+        sd += misc[544 + oo * 32 + (lane & 31)] * dlo;
+        dl = lane == oo ? dlo : dl;
+      }
+      const float dh = hh > 0.f ? sd : 0.f;
+      if (lane < 32) hp[32 + lane] = dh;
+      if (s == 0) {
+        if (lane == 0) cx.HLOSS[n] = lse - lt;
+        if (lane < 32) {
+          cx.HDH[n * 32 + lane] = dh;
+          cx.HH[n * 32 + lane] = hr;
+        }
+        if (lane < 10) cx.HDL[n * 10 + lane] = dl;
+      }
+    }
+    lds_barrier();
+    DCA_STAMP(cx, 3, L, 3);
+    {  // dp = W1^T dh for this thread's two local features u = 2t, 2t + 1
+      float d0 = 0.f, d1 = 0.f;
+#pragma unroll 8
+      for (int j = 0; j < 32; ++j) {
+        const float dhj = hp[32 + j];
+        float w0, w1;
+        if constexpr (P == 1) {
+          const float2 wv = *(const float2*)((const float*)w1l + j * PL::W1S + 2 * t);
+          w0 = wv.x;
+          w1 = wv.y;
+        } else {
+          const unsigned u = *(const unsigned*)((const unsigned short*)w1l + j * PL::W1S + 2 * t);
+          w0 = __uint_as_float(u << 16);
+          w1 = __uint_as_float(u & 0xffff0000u);
+        }
+        d0 += dhj * w0;
+        d1 += dhj * w1;
+      }
+      *(float2*)(dpl + 2 * t) = make_float2(d0, d1);
+    }
+    lds_barrier();
+    // g = max-pool backward of dp, routed by the saved argmax (this thread's pixels)
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+      for (int i2 = 0; i2 < 4; ++i2) {
+        const int col = 4 * q + i2, u = (16 * h + c) * 16 + (w >> 1) * 8 + (col >> 1);
+        const unsigned pos = (unsigned)((w & 1) * 2 + (col & 1));
+        g[h][i2] = pcode[u] == pos ? dpl[u] : 0.f;
+      }
+    if (pa.debug) st8(cx.G + (size_t)n * 8192 + row * 512, lane, g);
+  }
+  DCA_STAMP(cx, 3, L, 0);
+
+  // ======================= backward: 10 applications, newest first ===========================================
+  unsigned short* dyT = (unsigned short*)(U + PL::U_DYT);
+  unsigned short* xT = (unsigned short*)(U + PL::U_XT);
+  lds_barrier();  // every wave is done with the head's LDS (X10 / DP overlap XR)
+  for (int idx = t; idx < PL::NP * PL::XR_PL / 16; idx += NTH) ((uint4*)XR)[idx] = uint4{0u, 0u, 0u, 0u};
+  for (int idx = t; idx < PL::NP * PL::XT_PL / 16; idx += NTH) ((uint4*)xT)[idx] = uint4{0u, 0u, 0u, 0u};
+  f32x4 wacc[NNT][2];
+#pragma unroll
+  for (int j = 0; j < NNT; ++j) wacc[j][0] = wacc[j][1] = z4();
+  float dgam = 0.f, dbet = 0.f;
+  float yv[2][4], yo[2][4] = {};  // y_i of this row / of the halo row
+  ld8(cx.Y + (size_t)(NBLK - 1) * B * 8192 + (size_t)n * 8192 + row * 512, lane, yv);
+  if (halo) ld8(pa.yh + ((size_t)((NBLK - 1) * LMAX + L) * 2 + hwhich) * 512, lane, yo);
+  unsigned codew[2];     // stem-backward prefetch (during block 0)
+  unsigned imgw = 0;
+  uint4 nxt = uint4{0u, 0u, 0u, 0u};
+  int nxt_lab = 0;
+  lds_barrier();
+#pragma unroll 1
+  for (int i = NBLK - 1; i >= 0; --i) {
+    // recover x_i = x_{i+1} - relu(bn(y_i)) (same fma, same scale / shift as the forward); BN-backward inputs
+    float dz[2][4], xh[2][4], xho[2][4];
+    float sa[2] = {0.f, 0.f}, sbv[2] = {0.f, 0.f};
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int ch = 16 * h + c;
+      const float mean = stat[i * 64 + ch], inv = stat[i * 64 + 32 + ch];
+      const float sc = scsh[i * 64 + ch], sh = scsh[i * 64 + 32 + ch];
+#pragma unroll
+      for (int i2 = 0; i2 < 4; ++i2) {
+        const float z = __builtin_fmaf(yv[h][i2], sc, sh);
+        x[h][i2] = x[h][i2] - fmaxf(z, 0.f);
+        xh[h][i2] = (yv[h][i2] - mean) * inv;
+        dz[h][i2] = z > 0.f ? g[h][i2] : 0.f;
+        sa[h] += dz[h][i2];
+        sbv[h] += dz[h][i2] * xh[h][i2];
+        if (halo) {
+          const float zo = __builtin_fmaf(yo[h][i2], sc, sh);
+          xo[h][i2] = xo[h][i2] - fmaxf(zo, 0.f);
+          xho[h][i2] = (yo[h][i2] - mean) * inv;
+        }
+      }
+    }
+    const int rnd = RND_HEAD + 1 + (NBLK - 1 - i);
+    const unsigned tag = tagof(epoch, rnd);
+    if (i == 5) DCA_STAMP(cx, 7, L, 0);
+    const float pv = wg_csum(sa[0], sa[1], sbv[0], sbv[1], cred);
+    if (t < 64) gput(gslot(pa, rnd, L) + t, tag, pv);
+    if (halo) publish_row(pa, rnd, L, hwhich, tag, dz, lane);
+    if (i == 5) DCA_STAMP(cx, 7, L, 1);
+    // while the exchange is in flight: the weight gradient of the PREVIOUS application (block i + 1), whose dy /
+    // x tiles are still staged; then the barrier retires every wave's reads of them before x_i replaces them
+    if (i < NBLK - 1) wgrad_acc<P>(dyT, xT, wacc, w, lane);
+    if (i == 5) DCA_STAMP(cx, 7, L, 2);
+    if (i > 0) {  // prefetch y_{i-1}; lands while this block's exchange and convolutions run
+      ld8(cx.Y + (size_t)(i - 1) * B * 8192 + (size_t)n * 8192 + row * 512, lane, yv);
+    } else {      // last block: what the stem backward needs (pool codes, raw input words, next batch's image)
+#pragma unroll
+      for (int h = 0; h < 2; ++h)
+        codew[h] = *(const unsigned*)(cx.SCODE + (size_t)n * 8192 + row * 512 + h * 256 + lane * 4);
+      {
+        const int ci = t / 80, rem = t % 80, xr_ = rem >> 3, yimg = 8 * s - 1 + xr_;
+        const int yc = yimg < 0 ? 0 : (yimg > 31 ? 31 : yimg);
+        imgw = ((const unsigned*)my_img)[(ci < 3 ? ci : 2) * 256 + yc * 8 + (rem & 7)];
+      }
+      if (t < 48) nxt = ((const uint4*)(cx.data + (size_t)next_id * 3072 + 768 * s))[t];
+      if (t == 48) nxt_lab = cx.labels[next_id];
+    }
+    lds_barrier();
+    xt_row<P>(xT, w + 1, q, c, x);
+    if (halo) xt_row<P>(xT, hxrow, q, c, xo);
+    float dzo[2][4];
+    if (i == 5) DCA_STAMP(cx, 7, L, 3);
+    xchg_wait(pa, rnd, epoch, G, cred, halo, hsrc, hwhich ^ 1, dzo);
+    if (i == 5) DCA_STAMP(cx, 7, L, 4);
+    if (halo && i > 0) ld8(pa.yh + ((size_t)((i - 1) * LMAX + L) * 2 + hwhich) * 512, lane, yo);
+    lds_barrier();
+    if (i == 5) DCA_STAMP(cx, 7, L, 5);
+    if (L == 0 && t < 32) {  // BN affine gradients: dbeta = sum dz, dgamma = sum dz * xhat
+      dbet += slot_total(cred, t);
+      dgam += slot_total(cred, 32 + t);
+    }
+    float dyv[2][4], dyo[2][4];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int ch = 16 * h + c;
+      const float Sa = slot_total(cred, ch), Sb = slot_total(cred, 32 + ch);
+      const float k1 = misc[320 + ch] * stat[i * 64 + 32 + ch] / Ntot;
+#pragma unroll
+      for (int i2 = 0; i2 < 4; ++i2) {
+        dyv[h][i2] = k1 * (Ntot * dz[h][i2] - Sa - xh[h][i2] * Sb);
+        if (halo) dyo[h][i2] = k1 * (Ntot * dzo[h][i2] - Sa - xho[h][i2] * Sb);
+      }
+    }
+    xr_row<P>(XR, w + 1, q, c, dyv);
+    if (halo) xr_row<P>(XR, hxrow, q, c, dyo);
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int ch = 16 * h + c;
+      unsigned hb[4], lb[4];
+#pragma unroll
+      for (int i2 = 0; i2 < 4; ++i2) {
+        const unsigned short hi = bfbits(dyv[h][i2]);
+        hb[i2] = hi;
+        lb[i2] = P == 1 ? bf_lo(dyv[h][i2], hi) : 0u;
+      }
+      *(uint2*)(dyT + ch * PL::DYT_S + w * 16 + 4 * q) = uint2{hb[0] | (hb[1] << 16), hb[2] | (hb[3] << 16)};
+      if constexpr (P == 1)
+        *(uint2*)(dyT + PL::DYT_PL / 2 + ch * PL::DYT_S + w * 16 + 4 * q) =
+            uint2{lb[0] | (lb[1] << 16), lb[2] | (lb[3] << 16)};
+    }
+    if (pa.debug) {
+      st8(cx.DY + (size_t)i * B * 8192 + (size_t)n * 8192 + row * 512, lane, dyv);
+      st8(cx.X + (size_t)i * B * 8192 + (size_t)n * 8192 + row * 512, lane, x);
+    }
+    lds_barrier();
+    if (i == 5) DCA_STAMP(cx, 7, L, 6);
+    // dgrad: g_i = g_{i+1} + conv(dy, W^T flipped)
+    {
+      f32x4 acc[2];
+      conv_row<P>(XR, WT, acc, w, lane);
+#pragma unroll
+      for (int h = 0; h < 2; ++h)
+#pragma unroll
+        for (int i2 = 0; i2 < 4; ++i2) g[h][i2] += acc[h][i2];
+    }
+    if (pa.debug && (i == 2 || i == 1)) st8(cx.G + (size_t)(i == 2 ? 0 : 1) * B * 8192 + (size_t)n * 8192 + row * 512,
+                                            lane, g);
+    DCA_STAMP(cx, 4 + (NBLK - 1 - i) / 8, L, (NBLK - 1 - i) % 8);
+  }
+  if (L == 0 && t < 32) {
+    pa.bng[t] = dgam;
+    pa.bng[32 + t] = dbet;
+  }
+
+  // ======================= stem backward: max-pool bwd (saved argmax) -> ReLU mask -> conv1 wgrad ============
+  lds_barrier();  // every wave is done with XR / WT (the last dgrad); dyT / xT stay for the last wgrad
+  wgrad_acc<P>(dyT, xT, wacc, w, lane);  // application 0
+  {
+    unsigned short* dsT = (unsigned short*)(U + PL::U_DST);
+    unsigned short* xs = (unsigned short*)(U + PL::U_XS);
+    // d(conv1 output) of this wave's two conv rows: every 2x2 window written whole (value at the argmax if the
+    // ReLU was active, zeros elsewhere)
+    float db0 = 0.f, db1 = 0.f;
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+      for (int i2 = 0; i2 < 4; ++i2) {
+        const unsigned code = (codew[h] >> (8 * i2)) & 255u, pos = code & 3u;
+        const float val = (code & 4u) ? g[h][i2] : 0.f;
+        const unsigned short vh = bfbits(val);
+        const unsigned vb = vh, vl = P == 1 ? (unsigned)bf_lo(val, vh) : 0u;
+        const int ch = 16 * h + c, so = ch * PL::DSP + (2 * w) * 32 + 2 * (4 * q + i2);
+        *(unsigned*)(dsT + so) = (pos == 0 ? vb : 0u) | ((pos == 1 ? vb : 0u) << 16);
+        *(unsigned*)(dsT + so + 32) = (pos == 2 ? vb : 0u) | ((pos == 3 ? vb : 0u) << 16);
+        if constexpr (P == 1) {
+          *(unsigned*)(dsT + PL::DST_PL / 2 + so) = (pos == 0 ? vl : 0u) | ((pos == 1 ? vl : 0u) << 16);
+          *(unsigned*)(dsT + PL::DST_PL / 2 + so + 32) = (pos == 2 ? vl : 0u) | ((pos == 3 ? vl : 0u) << 16);
+        }
+        if (h == 0) db0 += val;
+        else db1 += val;
+      }
+    // three column-shifted copies of the normalised input rows 8s-1 .. 8s+8 (copy kw holds x[col + kw - 1])
+    if (t < 240) {
+      const int ci = t / 80, rem = t % 80, xr_ = rem >> 3, x0 = 4 * (rem & 7), yimg = 8 * s - 1 + xr_;
+      const bool valid = yimg >= 0 && yimg < 32;
+      unsigned hb[4], lb[4];
+#pragma unroll
+      for (int b2 = 0; b2 < 4; ++b2) {
+        const float v = valid ? norm_px((imgw >> (8 * b2)) & 255u, ci) : 0.f;
+        const unsigned short hi = bfbits(v);
+        hb[b2] = hi;
+        lb[b2] = P == 1 ? bf_lo(v, hi) : 0u;
+      }
+#pragma unroll
+      for (int p = 0; p <= P; ++p) {
+        const unsigned* bb = p ? lb : hb;
+        unsigned short* base = xs + p * (PL::XS_PL / 2);
+        unsigned short* p1 = base + ((3 + ci) * PL::XSR + xr_) * PL::XS_S + x0;  // kw = 1
+        *(uint2*)p1 = uint2{bb[0] | (bb[1] << 16), bb[2] | (bb[3] << 16)};
+        unsigned short* p0 = base + ((0 + ci) * PL::XSR + xr_) * PL::XS_S + x0;  // kw = 0: col c holds x[c - 1]
+        p0[1] = (unsigned short)bb[0];
+        *(unsigned*)(p0 + 2) = bb[1] | (bb[2] << 16);
+        if (x0 + 4 < 32) p0[4] = (unsigned short)bb[3];
+        if (x0 == 0) p0[0] = 0;
+        unsigned short* p2 = base + ((6 + ci) * PL::XSR + xr_) * PL::XS_S + x0;  // kw = 2: col c holds x[c + 1]
+        if (x0 > 0) p2[-1] = (unsigned short)bb[0];
+        *(unsigned*)p2 = bb[1] | (bb[2] << 16);
+        p2[2] = (unsigned short)bb[3];
+        if (x0 == 28) p2[3] = 0;
+      }
+    }
+    // conv1 bias gradient partial of this workgroup (also the barrier before the MFMAs)
+    const float dbv = wg_csum(db0, db1, 0.f, 0.f, cred);
+    float* ss = cx.SSLAB + (size_t)L * SSLAB_N;
+    if (t < 32) ss[1024 + t] = dbv;
+    // D[co][k] = sum over this slice's conv pixels of ds[p][co] * im2col[p][k]; K step = one conv row (32 px).
+    // Wave w: tile w (mt = co half, nt = k tile); k >= 27 columns are discarded by the reduce
+    {
+      const int mt = w & 1, nt = w >> 1;
+      const int kidx = 16 * nt + c, kk = kidx < 27 ? kidx : 0, ci = kk / 9, kh = (kk % 9) / 3, kw = kk % 3;
+      const unsigned short* abase = dsT + (16 * mt + c) * PL::DSP + 8 * q;
+      const unsigned short* bbase = xs + ((kw * 3 + ci) * PL::XSR + kh) * PL::XS_S + 8 * q;
+      f32x4 acc2 = z4();
+#pragma unroll
+      for (int sr = 0; sr < 2 * RS; ++sr) {
+        const bf16x8 a = *(const bf16x8*)(abase + sr * 32);
+        const bf16x8 bb = *(const bf16x8*)(bbase + sr * PL::XS_S);
+        bf16x8 al = a, bl = bb;
+        if constexpr (P == 1) {
+          al = *(const bf16x8*)(abase + PL::DST_PL / 2 + sr * 32);
+          bl = *(const bf16x8*)(bbase + PL::XS_PL / 2 + sr * PL::XS_S);
+        }
+        acc2 = mma3<P>(a, al, bb, bl, acc2);
+      }
+      st4(ss + ((w * 64 + lane) << 2), acc2);
+    }
+  }
+  // the next batch's image n (this slice's quarter) and label, staged into the other parity
+  if (t < 48) ((uint4*)(pa.simg + (size_t)((par ^ 1) * 64 + n) * 3072 + 768 * s))[t] = nxt;
+  if (t == 48 && s == 0) pa.slab[(par ^ 1) * 64 + n] = nxt_lab;
+  // trunk wgrad slab (accumulated over the 10 applications): tile tt = 2 nt + mt, the layout k_pks_reduce reads
+#pragma unroll
+  for (int j = 0; j < NNT; ++j) {
+    const int nt = w + NW * j;
+    if (nt < 18) {
+      st4(pa.tslab + (size_t)L * WSLAB_N + (((2 * nt) * 64 + lane) << 2), wacc[j][0]);
+      st4(pa.tslab + (size_t)L * WSLAB_N + (((2 * nt + 1) * 64 + lane) << 2), wacc[j][1]);
+    }
+  }
+  DCA_STAMP(cx, 5, L, 7);
+}
+
+// ============================================================================================================
+// Reduction + SGD after the sliced step: the trunk / stem slabs of all B x S workgroups (deterministic order),
+// then the fc gradients and the bookkeeping of netresdeep_persistent.hip (k_pk_reduce's roles).
+// Grid pk::R_GRID x 256.
+// ============================================================================================================
+__device__ __forceinline__ void red_trunk_stem(const Ctx& cx, const float* tslab, int bid, int nslab, f32x4* red) {
+  const int t = threadIdx.x;
+  const bool stem = bid >= pk::R_TRUNK;
+  const int chunk = stem ? bid - pk::R_TRUNK : bid;
+  const int slot = t & 63, grp = t >> 6, e0 = chunk * 256 + slot * 4;
+  const float* src = stem ? cx.SSLAB : tslab;
+  const int stride = stem ? SSLAB_N : WSLAB_N, lim = stem ? SSLAB_N : WSLAB_N;
+  int pix[4];
+  float pold[4];
+#pragma unroll
+  for (int ii = 0; ii < 4; ++ii) {
+    const int e = e0 + ii;
+    int pidx = -1;
+    if (e < lim) {
+      if (!stem) {
+        const int tt = e >> 8, ln = (e >> 2) & 63, mt = tt & 1, nt = tt >> 1, tap = nt >> 1, cih = nt & 1;
+        pidx = OFF_CONVW + (16 * mt + 4 * (ln >> 4) + ii) * 288 + (16 * cih + (ln & 15)) * 9 + tap;
+      } else if (e < 1024) {
+        const int tt = e >> 8, ln = (e >> 2) & 63, mt = tt & 1, nt = tt >> 1, k = 16 * nt + (ln & 15);
+        if (k < 27) pidx = OFF_C1W + (16 * mt + 4 * (ln >> 4) + ii) * 27 + k;
+      } else if (e < 1056) {
+        pidx = OFF_C1B + (e - 1024);
+      }
+    }
+    pix[ii] = pidx;
+    pold[ii] = cx.params[pidx >= 0 ? pidx : 0];
+  }
+  f32x4 sacc = z4();
+  const int ec = e0 < lim ? e0 : lim - 4;
+  for (int k0 = 0; k0 < nslab; k0 += 64) {  // 16 slabs per thread in flight, fixed order
+    f32x4 v[16];
+#pragma unroll
+    for (int u = 0; u < 16; ++u) {
+      const int k = k0 + grp + 4 * u;
+      v[u] = ld4(src + (size_t)(k < nslab ? k : nslab - 1) * stride + ec);
+    }
+#pragma unroll
+    for (int u = 0; u < 16; ++u)
+      if (k0 + grp + 4 * u < nslab) sacc += v[u];
+  }
+  red[t] = sacc;
+  __syncthreads();
+  if (t < 64 && e0 < lim) {
+    const f32x4 tot = red[t] + red[64 + t] + red[128 + t] + red[192 + t];
+#pragma unroll
+    for (int ii = 0; ii < 4; ++ii) {
+      const int pidx = pix[ii];
+      if (pidx < 0) continue;
+      const float wv = pk::sgd_put_pre(cx, pidx, tot[ii], pold[ii]);
+      if (cx.fuse_sgd) derive_param<true>(cx, pidx, wv);
+    }
+  }
+}
+
+__global__ void __launch_bounds__(256) k_pks_reduce(Ctx cx, pk::PkArgs pa, int nslab) {
+  __shared__ f32x4 red[256];
+  __shared__ float stage[64 * 32 + 64 * 64];
+  const int bid = blockIdx.x;
+  if (bid < pk::R_TRUNK + pk::R_STEM) {
+    red_trunk_stem(cx, pa.tslab, bid, nslab, red);
+  } else if (bid < pk::R_TRUNK + pk::R_STEM + pk::R_FC) {
+    pk::pk_red_fc1(cx, bid - pk::R_TRUNK - pk::R_STEM, stage);
+  } else {
+    pk::pk_red_fc_small(cx, stage);
+    __syncthreads();
+    pk::pk_bookkeeping(cx, pa, (float*)red);
+  }
+}
+
+}  // namespace pks
+}  // namespace dca

@@ -108,7 +108,7 @@ class EngineConfig:
     lr: float = 1e-2
     dtype: str = "bf16"          # "bf16": bf16 MFMA (fp32 accumulate/storage); "fp32": exact fp32 MFMA
     rows: int = 4                # multi-kernel engine: trunk rows per workgroup tile (2 or 4)
-    persistent: Optional[bool] = None  # one-launch persistent trunk kernel (default: on for bf16)
+    persistent: Optional[bool] = None  # one-launch persistent step kernel (default: on; image-sliced)
     debug: bool = False          # persistent engine: also store per-block dy / residual grads (diagnostics)
     pk_waves: int = 8            # persistent engine: waves per workgroup (8: 2 image rows per wave)
     world_size: int = 1
@@ -133,9 +133,7 @@ class NetResDeepEngine:
         if cfg.dtype not in ("bf16", "fp32"):
             raise ValueError("dtype must be 'bf16' or 'fp32'")
         if cfg.persistent is None:
-            cfg.persistent = cfg.dtype == "bf16"
-        if cfg.persistent and cfg.dtype != "bf16":
-            raise ValueError("the persistent engine is bf16-only; use persistent=False for fp32")
+            cfg.persistent = True  # the image-sliced persistent kernel (bf16 and fp32)
         if getattr(model, "n_chans1", 32) != 32 or getattr(model, "n_blocks", 10) != 10:
             raise ValueError("the fused engine is specialised for NetResDeep(n_chans1=32, n_blocks=10)")
         self.lib = native.require_native()
@@ -176,6 +174,7 @@ class NetResDeepEngine:
             native.check(self.lib.dca_engine_create(ctypes.byref(init), self.max_indices, ctypes.byref(h)),
                          "dca_engine_create")
         self.h = h
+        self.kind = int(self.lib.dca_engine_kind(h))  # 0 multi-kernel, 1 persistent per image, 2 sliced
         self.derive()
         self._n_indices = 0
 
@@ -333,7 +332,7 @@ class NetResDeepEngine:
         [row][h][lane = 16q + c][i] holding element (row, col = 4q + i, ch = 16h + c) (netresdeep_persistent.hip: tl),
         with X in bf16.
         """
-        if self.cfg.persistent and name == "X":  # block inputs are kept as bf16 (only used as a bf16 operand)
+        if self.kind == 1 and name == "X":  # block inputs are kept as bf16 (only used as a bf16 operand)
             raw = self.region(name, count * batch * 4096).view(torch.bfloat16).float()
             return tile_to_nhwc(raw, count, batch)
         raw = self.region(name, count * batch * 8192)
