@@ -42,7 +42,10 @@ def _cfg(dtype, rows, B, persistent):
 
 
 def compare_one_step(dtype: str, rows: int, B: int, graph: bool, seed: int = 0, verbose: bool = True,
-                     persistent: bool = False) -> dict:
+                     persistent: bool = False, forced: bool = False) -> dict:
+    """One engine step vs the oracle.  forced=True feeds the engine's own stem output and conv outputs into the
+    oracle (utils/oracle.py reference_step(force=...)), so the backward comparison is free of ReLU / max-pool mask
+    flips and measures arithmetic error only."""
     torch.manual_seed(seed)
     dev = torch.device("cuda", 0)
     ndata = 2 * B + 8
@@ -58,8 +61,14 @@ def compare_one_step(dtype: str, rows: int, B: int, graph: bool, seed: int = 0, 
     eng.read_loss(reset=True)
     eng.run(B, 1, graph=graph)
     eng.sync()
+    force = None
+    if forced:
+        to_nchw = lambda t: t.permute(0, 3, 1, 2).contiguous().cpu()  # noqa: E731
+        force = {"x0": to_nchw(eng.activations("X", 1, B)[0]),
+                 "c1": eng.region("C1", B * 32 * 1024).view(B, 32, 32, 32).cpu(),
+                 "y": [to_nchw(t) for t in eng.activations("Y", 10, B)]}
     r = reference_step(ref, data[idx], labels[idx], lr=1e-2, bf16_operands=(dtype == "bf16"),
-                       fc1_bf16=bool(persistent) and dtype == "bf16")
+                       fc1_bf16=bool(persistent) and dtype == "bf16", force=force)
     out = {}
 
     def rep(name, a, b):
@@ -129,9 +138,13 @@ def trajectory(dtype: str, rows: int, B: int, steps: int, seed: int = 1, persist
         losses_r.append(reference_step(ref, data[sel], labels[sel], bf16_operands=(dtype == "bf16"),
                                        fc1_bf16=bool(persistent) and dtype == "bf16")["loss"])
     sd, rsd = model.state_dict(), ref.state_dict()
-    perr = max(rel(sd[k], rsd[k]) for k in rsd if rsd[k].dtype != torch.int64)
+    keys = [k for k in rsd if rsd[k].dtype != torch.int64]
+    perr = max(rel(sd[k], rsd[k]) for k in keys)
+    a = torch.cat([sd[k].detach().double().cpu().reshape(-1) for k in keys])
+    b = torch.cat([rsd[k].detach().double().reshape(-1) for k in keys])
     eng.close()
-    return {"losses_engine": losses_e, "losses_ref": losses_r, "max_param_rel_err": perr}
+    return {"losses_engine": losses_e, "losses_ref": losses_r, "max_param_rel_err": perr,
+            "param_rel_l2": ((a - b).norm() / b.norm()).item()}
 
 
 def main():

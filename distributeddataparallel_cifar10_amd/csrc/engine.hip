@@ -163,6 +163,7 @@ static int alloc_workspace(Engine* e) {
       {"TSLAB", bmax * pks::S * WSLAB_N * 4}, {"BNG", 64 * 4}, {"IDS", 64 * 4}, {"W1B", 65536 * 2}, {"XCC", 64 * 8}, {"SIMG", 2 * 64 * 3072}, {"SLAB", 2 * 64 * 4}, {"GH", bmax * 8192 * 4}, {"SWF", 2 * 3 * 64 * 4 * 2},
       {"COMMT", 16}, {"PKW", PKW_N * 2},
       {"PKS_GRAN", 2 * (size_t)pks::LMAX * pks::GSTR * 8}, {"PKS_YH", 10 * (size_t)pks::LMAX * 2 * 512 * 4},
+      {"C1", e->in.debug ? bmax * 32 * 1024 * 4 : 16},
   };
   size_t total = 0;
   for (auto& r : regs) total += align_up(r.bytes, 256);
@@ -224,7 +225,10 @@ static int alloc_workspace(Engine* e) {
   qa.simg = e->pa.simg;
   qa.slab = e->pa.slab;
   qa.yh = (float*)e->regions["PKS_YH"];
+  qa.c1 = (float*)e->regions["C1"];
   qa.debug = e->in.debug;
+  qa.gap = 0;  // exchange polling: s_sleep(1) units between passes (0 measured best; DCA_PKS_POLL_GAP)
+  if (const char* pp = getenv("DCA_PKS_POLL_GAP")) qa.gap = atoi(pp);
   return 0;
 }
 

@@ -1,7 +1,7 @@
 // Image-sliced persistent NetResDeep training step for CDNA4 (gfx950 / MI355X): ONE launch per step, every image
-// split over S = 4 workgroups of 4 image rows (one wave per row), so a batch of 32 runs on 128 CUs instead of the
-// 32 of the one-workgroup-per-image kernel (netresdeep_persistent.hip), and each CU's serial work per block is a
-// quarter.
+// split over S = 4 workgroups of 4 image rows, so a batch of 32 runs on 128 CUs instead of the 32 of the
+// one-workgroup-per-image kernel (netresdeep_persistent.hip).  A workgroup has 8 waves: wave (row w, channel half
+// h) owns one image row and 16 of the 32 channels, so every latency-bound phase of a block is short.
 //
 //   stem (+ 1 halo pooled row each side, recomputed, no exchange) -> 10 forward blocks -> head -> 10 backward
 //   blocks -> stem backward; then k_pks_reduce (slab reduction + SGD + bookkeeping).
@@ -21,8 +21,9 @@
 // v_mfma_f32_16x16x32_bf16 (relative product error ~2^-17, i.e. ~16 mantissa bits, finer than the TF32 that
 // cuDNN uses for the reference's fp32 convolutions by default on Ampere and later), fc1 in plain fp32.
 //
-// Element ownership (C layout of v_mfma_f32_16x16x32_bf16): thread (wave w, lane l = 16q + c) owns
-//   pixel (image row 4s + w, col 4q + i), channel 16h + c   for h in {0,1}, i in {0..3}   (8 values)
+// Element ownership (C layout of v_mfma_f32_16x16x32_bf16): thread (wave 4h + w, lane l = 16q + c) owns
+//   pixel (image row 4s + w, col 4q + i), channel 16h + c   for i in {0..3}   (4 values)
+// Global activations keep the tiled row layout [row][h][lane][i] (one f32x4 per thread and row).
 //
 // Reference semantics: model/resnet.py:5-37 (one shared ResBlock applied 10x, skip after the ReLU),
 // main.py:27-39 (SGD, CrossEntropy mean), BatchNorm2d training statistics + 10 running-stat EMAs per forward.
@@ -32,13 +33,13 @@ namespace pks {
 
 constexpr int S = 4;                   // workgroups (row slices) per image
 constexpr int RS = 16 / S;             // image rows per slice
-constexpr int NW = RS;                 // waves per workgroup: one image row each
+constexpr int NW = 2 * RS;             // waves per workgroup: (row, channel half)
 constexpr int NTH = 64 * NW;           // threads per workgroup
 constexpr int GSTR = 64 + 2 * 512;     // granules per workgroup per round: 64 BN sums | top row | bottom row
 constexpr int LMAX = 64 * S;           // logical workgroups (batch <= 64)
 constexpr int NNT = (18 + NW - 1) / NW;  // wgrad tile columns (ci half x tap) per wave
 constexpr int RND_HEAD = 10;           // rounds: 0..9 forward BN, 10 head (fc1 partials), 11..20 backward BN
-constexpr unsigned SPIN_LIMIT = 1u << 18;
+constexpr unsigned SPIN_LIMIT = 1u << 17;
 constexpr int RB = 80;                 // bf16 record: 32 channels (64 B) + 16 B pad (staggers the banks)
 
 struct Args {
@@ -50,7 +51,9 @@ struct Args {
   uint8_t* simg;             // [2][64][3072] batch images staged by the previous step (parity = epoch & 1)
   int* slab;                 // [2][64] their labels
   float* yh;                 // [10][LMAX][2][512] halo rows of y received in the forward (for the backward)
-  int debug;                 // also store X / DY / G for the numerical diagnostics
+  float* c1;                 // debug: [B][32][32][32] conv1 pre-activation (NCHW), for the flip-aware oracle
+  int debug;                 // also store X / DY / G / C1 for the numerical diagnostics
+  int gap;                   // sweep: s_sleep(1) units before re-issuing a failed pass (env DCA_PKS_POLL_GAP)
 };
 
 // ---- LDS plan (bytes; every region 16-byte aligned) ---------------------------------------------------------
@@ -102,12 +105,17 @@ struct Plan {
   static constexpr int XS_S = 40;
   static constexpr int XS_PL = 9 * XSR * XS_S * 2;             // [3 kw][3 ci][XSR][XS_S] shifted input copies
   static constexpr int U_XS = U_DST + NP * DST_PL;
-  static constexpr int SBWD_END = U_XS + NP * XS_PL;
+  static constexpr int U_SRED = U_XS + NP * XS_PL;             // [NW][64][4] f32 stem-wgrad partials (written
+                                                               // after the barrier that retires the last wgrad)
+  static constexpr int SBWD_END = U_SRED + NW * 64 * 16;
   static constexpr int UNION = pk::cmax(pk::cmax(BWD_END, STEM_END), pk::cmax(HEAD_END, SBWD_END));
   static constexpr int TOTAL = O_U + UNION;
 };
 static_assert(Plan<1>::TOTAL <= 160 * 1024, "LDS budget");
 static_assert(Plan<0>::X10S * 4 * RS * 16 <= Plan<0>::XR_PL, "x10 fits the XR region");
+// dsT / xs are written while other waves may still run the last wgrad (dyT / xT); SRED only after the barrier
+static_assert(Plan<0>::U_SRED <= Plan<0>::U_DYT, "stem-backward staging clear of dyT / xT (last wgrad)");
+static_assert(Plan<1>::U_SRED <= Plan<1>::U_DYT, "stem-backward staging clear of dyT / xT (last wgrad)");
 
 // ---- helpers ------------------------------------------------------------------------------------------------
 __device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
@@ -149,58 +157,50 @@ __device__ __forceinline__ f32x4 mma3s(const s4v& ah, const s4v& al, const s4v& 
   return acc;
 }
 
-// 3x3 conv of one output row (wave w = slice row w) on MFMA, both channel halves.  xr: (RS+2) x 18 records,
+// 3x3 conv of one output row (slice row w), output channels 16h .. 16h+15, on MFMA.  xr: (RS+2) x 18 records,
 // wt: 288 records (tap-major); P=1 reads the lo planes at +XR_PL / +WT_PL.
 template <int P>
-__device__ __forceinline__ void conv_row(const char* xr, const char* wt, f32x4 (&acc)[2], int w, int lane) {
+__device__ __forceinline__ f32x4 conv_row(const char* xr, const char* wt, int w, int h, int lane) {
   using PL = Plan<P>;
   const int c = lane & 15, q = lane >> 4;
   const char* abase = xr + (w * 18 + c) * RB + q * 16;
-  const char* bbase = wt + c * RB + q * 16;
-  acc[0] = z4();
-  acc[1] = z4();
+  const char* bbase = wt + (16 * h + c) * RB + q * 16;
+  f32x4 acc = z4();
 #pragma unroll
   for (int tap = 0; tap < 9; ++tap) {
     const int kh = tap / 3, kw = tap % 3;
-    const bf16x8 b0 = *(const bf16x8*)(bbase + (tap * 32) * RB);
-    const bf16x8 b1 = *(const bf16x8*)(bbase + (tap * 32 + 16) * RB);
+    const bf16x8 b = *(const bf16x8*)(bbase + (tap * 32) * RB);
     const bf16x8 a = *(const bf16x8*)(abase + (kh * 18 + kw) * RB);
-    bf16x8 b0l = b0, b1l = b1, al = a;
+    bf16x8 bl = b, al = a;
     if constexpr (P == 1) {
-      b0l = *(const bf16x8*)(bbase + PL::WT_PL + (tap * 32) * RB);
-      b1l = *(const bf16x8*)(bbase + PL::WT_PL + (tap * 32 + 16) * RB);
+      bl = *(const bf16x8*)(bbase + PL::WT_PL + (tap * 32) * RB);
       al = *(const bf16x8*)(abase + PL::XR_PL + (kh * 18 + kw) * RB);
     }
-    acc[0] = mma3<P>(a, al, b0, b0l, acc[0]);
-    acc[1] = mma3<P>(a, al, b1, b1l, acc[1]);
+    acc = mma3<P>(a, al, b, bl, acc);
   }
+  return acc;
 }
 
-// per-workgroup channel sums of per-thread C-layout partials (a0/b0: channel c, a1/b1: channel 16 + c), delivered
-// to the publishing threads: thread t < 64 returns slot t (t < 32: sum of a for channel t, else sum of b for
-// channel t - 32).  One LDS barrier.
-__device__ __forceinline__ float wg_csum(float a0, float a1, float b0, float b1, float* cred) {
-  const int t = threadIdx.x, w = t >> 6, lane = t & 63, c = lane & 15;
-  a0 += __shfl_xor(a0, 16);
-  a0 += __shfl_xor(a0, 32);
-  a1 += __shfl_xor(a1, 16);
-  a1 += __shfl_xor(a1, 32);
-  b0 += __shfl_xor(b0, 16);
-  b0 += __shfl_xor(b0, 32);
-  b1 += __shfl_xor(b1, 16);
-  b1 += __shfl_xor(b1, 32);
-  float* r = cred + NW * 64;  // disjoint from the sweep combine area
+// per-workgroup channel sums of per-thread partials (a, b: channel 16h + c of wave 4h + w), delivered to the
+// publishing threads: thread t < 64 returns slot t (t < 32: sum of a for channel t, else sum of b for channel
+// t - 32).  One LDS barrier.
+__device__ __forceinline__ float wg_csum(float a, float b, float* cred) {
+  const int t = threadIdx.x, wv = t >> 6, lane = t & 63, c = lane & 15;
+  a += __shfl_xor(a, 16);
+  a += __shfl_xor(a, 32);
+  b += __shfl_xor(b, 16);
+  b += __shfl_xor(b, 32);
+  float* r = cred + NW * 64;  // [NW][32], disjoint from the sweep combine area
   if (lane < 16) {
-    r[w * 64 + c] = a0;
-    r[w * 64 + 16 + c] = a1;
-    r[w * 64 + 32 + c] = b0;
-    r[w * 64 + 48 + c] = b1;
+    r[wv * 32 + c] = a;
+    r[wv * 32 + 16 + c] = b;
   }
   lds_barrier();
   float v = 0.f;
   if (t < 64) {
+    const int ch = t & 31, hh = ch >> 4, off = (t >> 5) * 16 + (ch & 15);
 #pragma unroll
-    for (int k = 0; k < NW; ++k) v += r[k * 64 + t];
+    for (int w = 0; w < RS; ++w) v += r[(4 * hh + w) * 32 + off];
   }
   return v;
 }
@@ -218,74 +218,80 @@ __device__ __forceinline__ void gput(unsigned long long* g, unsigned tag, float 
   __hip_atomic_store(g, ((unsigned long long)tag << 32) | __float_as_uint(v), __ATOMIC_RELAXED,
                      __HIP_MEMORY_SCOPE_AGENT);
 }
-// publish this lane's 8 values of a boundary row (which: 0 = my top row, 1 = my bottom row): 4 x 16-B sc1
-// stores, each holding two whole granules
-__device__ __forceinline__ void publish_row(const Args& pa, int round, int L, int which, unsigned tag,
-                                            const float (&v)[2][4], int lane) {
+// publish this lane's 4 values (channel half h) of a boundary row (which: 0 = my top row, 1 = my bottom row):
+// 2 x 16-B sc1 stores, each holding two whole granules
+__device__ __forceinline__ void publish_row(const Args& pa, int round, int L, int which, int h, unsigned tag,
+                                            const float (&v)[4], int lane) {
   const __amdgpu_buffer_rsrc_t rs = grsrc(pa, round);
-  const int base = (L * GSTR + 64 + which * 512) * 8;
+  const int base = (L * GSTR + 64 + which * 512 + h * 256 + lane * 4) * 8;
 #pragma unroll
-  for (int h = 0; h < 2; ++h)
-#pragma unroll
-    for (int p = 0; p < 2; ++p) {
-      const v4u x = v4u{__float_as_uint(v[h][2 * p]), tag, __float_as_uint(v[h][2 * p + 1]), tag};
-      __builtin_amdgcn_raw_buffer_store_b128(x, rs, base + (h * 256 + lane * 4 + 2 * p) * 8, 0, 16);
-    }
+  for (int p = 0; p < 2; ++p) {
+    const v4u x = v4u{__float_as_uint(v[2 * p]), tag, __float_as_uint(v[2 * p + 1]), tag};
+    __builtin_amdgcn_raw_buffer_store_b128(x, rs, base + 2 * p * 8, 0, 16);
+  }
 }
-// one poll pass over the 8 granules of a neighbour's boundary row this lane needs; true when all carry `tag`
-__device__ __forceinline__ bool poll_row(const Args& pa, int round, int Lsrc, int which, unsigned tag,
-                                         float (&v)[2][4], int lane) {
+// one poll pass over the 4 granules of a neighbour's boundary row this lane needs; true when all carry `tag`
+__device__ __forceinline__ bool poll_row(const Args& pa, int round, int Lsrc, int which, int h, unsigned tag,
+                                         float (&v)[4], int lane) {
   const __amdgpu_buffer_rsrc_t rs = grsrc(pa, round);
-  const int base = (Lsrc * GSTR + 64 + which * 512) * 8;
-  v4u x[2][2];
+  const int base = (Lsrc * GSTR + 64 + which * 512 + h * 256 + lane * 4) * 8;
+  v4u x[2];
 #pragma unroll
-  for (int h = 0; h < 2; ++h)
-#pragma unroll
-    for (int p = 0; p < 2; ++p)
-      x[h][p] = __builtin_amdgcn_raw_buffer_load_b128(rs, base + (h * 256 + lane * 4 + 2 * p) * 8, 0, 16);
+  for (int p = 0; p < 2; ++p) x[p] = __builtin_amdgcn_raw_buffer_load_b128(rs, base + 2 * p * 8, 0, 16);
   bool ok = true;
 #pragma unroll
-  for (int h = 0; h < 2; ++h)
-#pragma unroll
-    for (int p = 0; p < 2; ++p) {
-      ok &= x[h][p][1] == tag && x[h][p][3] == tag;
-      v[h][2 * p] = __uint_as_float(x[h][p][0]);
-      v[h][2 * p + 1] = __uint_as_float(x[h][p][2]);
-    }
+  for (int p = 0; p < 2; ++p) {
+    ok &= x[p][1] == tag && x[p][3] == tag;
+    v[2 * p] = __uint_as_float(x[p][0]);
+    v[2 * p + 1] = __uint_as_float(x[p][2]);
+  }
   return ok;
 }
 
-// BN sweep pass: lane l reads slots 2(l & 31), 2(l & 31) + 1 of workgroups 2w + (l >> 5) + 2 NW k (one 16-B sc1
-// load = two granules), k < KS; sums in k order.  Slots past the grid read a valid (clamped) granule and count 0.
+// BN sweep: lane l of wave wv reads slots 2(l & 31), 2(l & 31) + 1 of workgroups 2 wv + (l >> 5) + 2 NW k (one
+// 16-B sc1 load = two granules), k < KS; sums in k order.  Slots past the grid read a valid (clamped) granule
+// and count 0.
 template <int KS>
-__device__ __forceinline__ bool sweep_pass(const __amdgpu_buffer_rsrc_t rs, int w, int lane, int G, unsigned tag,
-                                           float& s0, float& s1) {
+__device__ __forceinline__ void sweep_issue(const __amdgpu_buffer_rsrc_t rs, int wv, int lane, int G, v4u (&x)[KS]) {
   const int j = lane & 31, hf = lane >> 5;
-  v4u x[KS];
+  asm volatile("" ::: "memory");  // re-issued every pass (never hoisted out of the spin)
 #pragma unroll
   for (int k = 0; k < KS; ++k) {
-    const int Lk = 2 * w + hf + 2 * NW * k, Lc = Lk < G ? Lk : G - 1;
+    const int Lk = 2 * wv + hf + 2 * NW * k, Lc = Lk < G ? Lk : G - 1;
     x[k] = __builtin_amdgcn_raw_buffer_load_b128(rs, (Lc * GSTR + 2 * j) * 8, 0, 16);
   }
+}
+template <int KS>
+__device__ __forceinline__ bool sweep_eval(const v4u (&x)[KS], int wv, int lane, int G, unsigned tag, float& s0,
+                                           float& s1) {
+  const int hf = lane >> 5;
   bool ok = true;
   s0 = 0.f;
   s1 = 0.f;
 #pragma unroll
   for (int k = 0; k < KS; ++k) {
-    const bool valid = 2 * w + hf + 2 * NW * k < G;
+    const bool valid = 2 * wv + hf + 2 * NW * k < G;
     ok &= !valid || (x[k][1] == tag && x[k][3] == tag);
     s0 += valid ? __uint_as_float(x[k][0]) : 0.f;
     s1 += valid ? __uint_as_float(x[k][2]) : 0.f;
   }
-  return ok;
+  return __all(ok);
 }
+__device__ __forceinline__ void sleep_units(int n) {
+  for (int k = 0; k < n; ++k) __builtin_amdgcn_s_sleep(1);  // 64 cycles each
+}
+// One pass in flight, re-issued as soon as it fails.  (Two staggered passes in flight were measured slower:
+// 103.6 vs 95.9 us per step at batch 32 -- the polling traffic of 128 workgroups, not the round trip, is what
+// the exchange waits on; profiles/bench_poll_r2.log.)
 template <int KS>
-__device__ __forceinline__ void sweep_wait(const Args& pa, int round, int w, int lane, int G, unsigned tag,
+__device__ __forceinline__ void sweep_wait(const Args& pa, int round, int wv, int lane, int G, unsigned tag,
                                            float& s0, float& s1) {
   const __amdgpu_buffer_rsrc_t rs = grsrc(pa, round);
+  v4u xa[KS];
   for (unsigned spins = 0;; ++spins) {
-    asm volatile("" ::: "memory");  // the loads are re-issued every pass
-    if (__all(sweep_pass<KS>(rs, w, lane, G, tag, s0, s1))) return;
+    sweep_issue<KS>(rs, wv, lane, G, xa);
+    if (sweep_eval<KS>(xa, wv, lane, G, tag, s0, s1)) return;
+    sleep_units(pa.gap);
     if (spins >= SPIN_LIMIT) {
       if (lane == 0) atomicOr(pa.err, 1u << (round & 31));
       return;
@@ -295,24 +301,24 @@ __device__ __forceinline__ void sweep_wait(const Args& pa, int round, int w, int
 // All-to-all BN exchange wait + (halo waves) the neighbour's boundary row.  On return cred[0 .. NW*64) holds every
 // wave's partial totals (the caller's barrier makes them visible): tot(slot) = sum_k cred[k * 64 + slot].
 __device__ __forceinline__ void xchg_wait(const Args& pa, int round, int epoch, int G, float* cred, bool halo,
-                                          int Lsrc, int which, float (&hv)[2][4]) {
+                                          int Lsrc, int which, int h, float (&hv)[4]) {
   const int t = threadIdx.x, lane = t & 63;
-  const int w = __builtin_amdgcn_readfirstlane(t >> 6);
+  const int wv = __builtin_amdgcn_readfirstlane(t >> 6);
   const unsigned tag = tagof(epoch, round);
   float s0, s1;
-  if (G <= 2 * NW * 8) sweep_wait<8>(pa, round, w, lane, G, tag, s0, s1);
-  else if (G <= 2 * NW * 16) sweep_wait<16>(pa, round, w, lane, G, tag, s0, s1);
-  else sweep_wait<32>(pa, round, w, lane, G, tag, s0, s1);
+  if (G <= 2 * NW * 4) sweep_wait<4>(pa, round, wv, lane, G, tag, s0, s1);
+  else if (G <= 2 * NW * 8) sweep_wait<8>(pa, round, wv, lane, G, tag, s0, s1);
+  else sweep_wait<16>(pa, round, wv, lane, G, tag, s0, s1);
   s0 += __shfl_xor(s0, 32);  // the two half-waves read different workgroups
   s1 += __shfl_xor(s1, 32);
   if (lane < 32) {
-    cred[w * 64 + 2 * lane] = s0;
-    cred[w * 64 + 2 * lane + 1] = s1;
+    cred[wv * 64 + 2 * lane] = s0;
+    cred[wv * 64 + 2 * lane + 1] = s1;
   }
   if (halo) {
     for (unsigned spins = 0;; ++spins) {
       asm volatile("" ::: "memory");
-      if (__all(poll_row(pa, round, Lsrc, which, tag, hv, lane))) break;
+      if (__all(poll_row(pa, round, Lsrc, which, h, tag, hv, lane))) break;
       if (spins >= SPIN_LIMIT) {
         if (lane == 0) atomicOr(pa.err, 1u << (round & 31));
         break;
@@ -327,28 +333,24 @@ __device__ __forceinline__ float slot_total(const float* cred, int slot) {
   return a;
 }
 
-// tiled global activation layout of one image row: element (col 4q + i, ch 16h + c) at h*256 + (16q + c)*4 + i
-__device__ __forceinline__ void st8(float* p, int lane, const float (&v)[2][4]) {
-#pragma unroll
-  for (int h = 0; h < 2; ++h) *(f32x4*)(p + h * 256 + lane * 4) = f32x4{v[h][0], v[h][1], v[h][2], v[h][3]};
+// this thread's 4 values of one image row in the tiled global layout [h][lane][i]
+__device__ __forceinline__ void st4r(float* rowp, int h, int lane, const float (&v)[4]) {
+  *(f32x4*)(rowp + h * 256 + lane * 4) = f32x4{v[0], v[1], v[2], v[3]};
 }
-__device__ __forceinline__ void ld8(const float* p, int lane, float (&v)[2][4]) {
-#pragma unroll
-  for (int h = 0; h < 2; ++h) {
-    const f32x4 u = *(const f32x4*)(p + h * 256 + lane * 4);
-    v[h][0] = u[0];
-    v[h][1] = u[1];
-    v[h][2] = u[2];
-    v[h][3] = u[3];
-  }
+__device__ __forceinline__ void ld4r(const float* rowp, int h, int lane, float (&v)[4]) {
+  const f32x4 u = *(const f32x4*)(rowp + h * 256 + lane * 4);
+  v[0] = u[0];
+  v[1] = u[1];
+  v[2] = u[2];
+  v[3] = u[3];
 }
 
 // wgrad of one application, accumulated in registers: D[co][ci,tap] += sum over this slice's pixels of
-// dy[p][co] x[p + tap][ci].  Wave w owns tile columns nt = w, w + NW, ... (ci half x tap), both co halves; K steps
-// of 32 pixels = two image rows.
+// dy[p][co] x[p + tap][ci].  Wave wv owns tile columns nt = wv, wv + NW, ... (ci half x tap), both co halves; K
+// steps of 32 pixels = two image rows.
 template <int P>
 __device__ __forceinline__ void wgrad_acc(const unsigned short* dyT, const unsigned short* xT, f32x4 (&wacc)[NNT][2],
-                                          int w, int lane) {
+                                          int wv, int lane) {
   using PL = Plan<P>;
   const int c = lane & 15, q = lane >> 4;
   constexpr int DYO = PL::DYT_PL / 2, XTO = PL::XT_PL / 2;  // lo-plane offsets (elements)
@@ -365,7 +367,7 @@ __device__ __forceinline__ void wgrad_acc(const unsigned short* dyT, const unsig
     }
 #pragma unroll
     for (int j = 0; j < NNT; ++j) {
-      const int nt = w + NW * j;
+      const int nt = wv + NW * j;
       if (nt < 18) {
         const int tap = nt >> 1, cih = nt & 1, kh = tap / 3, kw = tap % 3;
         const int bo = (kw * 32 + 16 * cih + c) * PL::XT_S + (row + kh) * 16 + c0;
@@ -395,30 +397,24 @@ __device__ __forceinline__ void xt_put(unsigned short* xT, int XT_S, int xrow, i
   p2[2] = (unsigned short)b3;
 }
 template <int P>
-__device__ __forceinline__ void xt_row(unsigned short* xT, int xrow, int q, int c, const float (&x)[2][4]) {
+__device__ __forceinline__ void xt_row(unsigned short* xT, int xrow, int q, int ch, const float (&x)[4]) {
   using PL = Plan<P>;
+  unsigned hb[4], lb[4];
 #pragma unroll
-  for (int h = 0; h < 2; ++h) {
-    const int ch = 16 * h + c;
-    unsigned hb[4], lb[4];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const unsigned short hi = bfbits(x[h][i]);
-      hb[i] = hi;
-      lb[i] = P == 1 ? bf_lo(x[h][i], hi) : 0u;
-    }
-    xt_put(xT, PL::XT_S, xrow, ch, q, hb[0], hb[1], hb[2], hb[3]);
-    if constexpr (P == 1) xt_put(xT + PL::XT_PL / 2, PL::XT_S, xrow, ch, q, lb[0], lb[1], lb[2], lb[3]);
+  for (int i = 0; i < 4; ++i) {
+    const unsigned short hi = bfbits(x[i]);
+    hb[i] = hi;
+    lb[i] = P == 1 ? bf_lo(x[i], hi) : 0u;
   }
+  xt_put(xT, PL::XT_S, xrow, ch, q, hb[0], hb[1], hb[2], hb[3]);
+  if constexpr (P == 1) xt_put(xT + PL::XT_PL / 2, PL::XT_S, xrow, ch, q, lb[0], lb[1], lb[2], lb[3]);
 }
-// a row of records (x or dy, both channel halves) of this lane into XR row `xrow`
+// this lane's 4 records-entries (channel ch, cols 4q .. 4q+3) of XR row `xrow`
 template <int P>
-__device__ __forceinline__ void xr_row(char* XR, int xrow, int q, int c, const float (&v)[2][4]) {
+__device__ __forceinline__ void xr_row(char* XR, int xrow, int q, int ch, const float (&v)[4]) {
   using PL = Plan<P>;
 #pragma unroll
-  for (int h = 0; h < 2; ++h)
-#pragma unroll
-    for (int i = 0; i < 4; ++i) st1r<P>(XR, PL::XR_PL, xrow * 18 + 4 * q + i + 1, 16 * h + c, v[h][i]);
+  for (int i = 0; i < 4; ++i) st1r<P>(XR, PL::XR_PL, xrow * 18 + 4 * q + i + 1, ch, v[i]);
 }
 
 // weight staging: NP planes of 1152 16-B chunks, loaded to registers (all in flight), stored as records
@@ -472,7 +468,8 @@ template <int P>
 __global__ void __launch_bounds__(NTH) k_pks_step(Ctx cx, Args pa) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   using PL = Plan<P>;
-  const int t = threadIdx.x, w = t >> 6, lane = t & 63, c = lane & 15, q = lane >> 4;
+  const int t = threadIdx.x, wv = t >> 6, lane = t & 63, c = lane & 15, q = lane >> 4;
+  const int w = wv & (RS - 1), hh = wv / RS, ch = 16 * hh + c;  // image row (in the slice), channel half, channel
   // Placement (speed only, never correctness): blocks b and b + 8 share an XCD under the observed round-robin
   // dispatch, so the S slices of an image get block ids 8 apart and their halo hand-offs stay in one L2.
   const int b = blockIdx.x, s = (b >> 3) % S, n = (b >> 3) / S * 8 + (b & 7);
@@ -480,7 +477,7 @@ __global__ void __launch_bounds__(NTH) k_pks_step(Ctx cx, Args pa) {
   if (n >= B) return;
   const int L = n * S + s, G = B * S;
   const int row = s * RS + w;  // image row of this wave
-  const bool halo = (w == 0 && s > 0) || (w == NW - 1 && s < S - 1);  // this wave keeps a neighbour row
+  const bool halo = (w == 0 && s > 0) || (w == RS - 1 && s < S - 1);  // this wave keeps a neighbour row
   const int hwhich = w == 0 ? 0 : 1;                  // the boundary row this wave publishes: 0 top, 1 bottom
   const int hsrc = w == 0 ? L - 1 : L + 1;            // ... and whose boundary row it receives
   const int hxrow = w == 0 ? 0 : RS + 1;              // XR / xT row of the received halo
@@ -497,11 +494,12 @@ __global__ void __launch_bounds__(NTH) k_pks_step(Ctx cx, Args pa) {
   const int next_id = sample_id(cx, B + n);
   const float Ntot = (float)B * 256.f;
   const unsigned short* pkw = (const unsigned short*)cx.pkw;
+  const size_t img8 = (size_t)n * 8192 + (size_t)row * 512;  // this row inside an image of a block's tensor
   DCA_STAMP(cx, 0, L, 0);
 
-  float x[2][4];        // this wave's row of the current block input (forward), x_{i+1} (backward)
-  float xo[2][4] = {};  // halo waves: the neighbour row of the same
-  float y[2][4];        // conv output of the current block
+  float x[4];        // this thread's values of the current block input (forward), x_{i+1} (backward)
+  float xo[4] = {};  // halo waves: the neighbour row of the same
+  float y[4];        // conv output of the current block
 
   // ======================= stem: gather + normalise + conv1 + bias + ReLU + 2x2 max-pool ======================
   // Pooled rows 4s-1 .. 4s+4 (own + one halo row each side, recomputed here: the input image is read-only).
@@ -595,9 +593,9 @@ __global__ void __launch_bounds__(NTH) k_pks_step(Ctx cx, Args pa) {
 #pragma unroll
         for (int m = 0; m < 3; ++m) bw[p][h][m] = __builtin_bit_cast(s4v, bwr[p][h][m]);
     const float* sb = misc + 874;
-    // units: (pooled row 4s-1+ur, column half), ur = 0..RS+1; wave w takes units w, w + NW, ...
+    // units: (pooled row 4s-1+ur, column half), ur = 0..RS+1; wave wv takes units wv, wv + NW, ...
 #pragma unroll 1
-    for (int u = w; u < 2 * (RS + 2); u += NW) {
+    for (int u = wv; u < 2 * (RS + 2); u += NW) {
       const int ur = u >> 1, chalf = u & 1, pr = 4 * s - 1 + ur;
       if (pr < 0 || pr > 15) continue;  // wave-uniform: the image border (XR rows stay zero)
       f32x4 acc[2][2];
@@ -615,6 +613,16 @@ __global__ void __launch_bounds__(NTH) k_pks_step(Ctx cx, Args pa) {
           acc[rw][0] = mma3s<P>(a, al, bw[0][0][m], bw[P][0][m], acc[rw][0]);
           acc[rw][1] = mma3s<P>(a, al, bw[0][1][m], bw[P][1][m], acc[rw][1]);
         }
+      }
+      if (pa.debug && ur >= 1 && ur <= RS) {  // conv1 + bias before the ReLU, own rows (NCHW)
+#pragma unroll
+        for (int rw = 0; rw < 2; ++rw)
+#pragma unroll
+          for (int h = 0; h < 2; ++h)
+#pragma unroll
+            for (int i2 = 0; i2 < 4; ++i2)
+              pa.c1[(((size_t)n * 32 + 16 * h + c) * 32 + 2 * pr + rw) * 32 + 16 * chalf + 4 * q + i2] =
+                  acc[rw][h][i2] + sb[16 * h + c];
       }
 #pragma unroll
       for (int h = 0; h < 2; ++h) {
@@ -639,130 +647,132 @@ __global__ void __launch_bounds__(NTH) k_pks_step(Ctx cx, Args pa) {
     }
     lds_barrier();
     DCA_STAMP(cx, 0, L, 3);
+    unsigned cw = 0;
 #pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      unsigned cw = 0;
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        x[h][i] = x0i[((w + 1) * 16 + 4 * q + i) * PL::X0S + 16 * h + c];
-        if (halo) xo[h][i] = x0i[(hxrow * 16 + 4 * q + i) * PL::X0S + 16 * h + c];
-        cw |= (unsigned)scl[(w * 16 + 4 * q + i) * 32 + 16 * h + c] << (8 * i);
-      }
-      // stem pool codes, read back by this very thread in the stem backward
-      *(unsigned*)(cx.SCODE + (size_t)n * 8192 + row * 512 + h * 256 + lane * 4) = cw;
+    for (int i = 0; i < 4; ++i) {
+      x[i] = x0i[((w + 1) * 16 + 4 * q + i) * PL::X0S + ch];
+      if (halo) xo[i] = x0i[(hxrow * 16 + 4 * q + i) * PL::X0S + ch];
+      cw |= (unsigned)scl[(w * 16 + 4 * q + i) * 32 + ch] << (8 * i);
     }
-    if (pa.debug) st8(cx.X + (size_t)n * 8192 + row * 512, lane, x);
+    // stem pool codes, read back by this very thread in the stem backward
+    *(unsigned*)(cx.SCODE + img8 + hh * 256 + lane * 4) = cw;
+    if (pa.debug) st4r(cx.X + img8, hh, lane, x);
   }
   DCA_STAMP(cx, 0, L, 1);
 
   // ======================= forward: 10 applications of the shared ResBlock ===================================
   // fc1 weights of this slice's 512 pooled features (local index u = ch*16 + pr*8 + pw <-> global feature
-  // ch*64 + (2s + pr)*8 + pw: per row, 32 runs of 16 contiguous elements), loaded into registers before the last
-  // exchange so its wait hides the latency, then staged in LDS for fc1 (reduction over features) and its
-  // transpose dp (reduction over rows)
-  constexpr int W1M = P == 1 ? 16 : 8;  // 16-B chunks per thread: 32 rows x 512 x (4 | 2) B / 16 B / 256
+  // ch*64 + (2s + pr)*8 + pw: per row, 32 runs of 16 contiguous elements): loaded into registers at block 6 (the
+  // exchange waits hide the latency), stored at block 7 into their LDS region (unused by the forward), read by
+  // fc1 (reduction over features) and its transpose dp (reduction over rows).  The dgrad weights are prefetched
+  // at block 8 and staged into WT at the head.
+  constexpr int W1M = P == 1 ? 4096 / NTH : 2048 / NTH;  // 16-B chunks per thread
   uint4 w1r[W1M];
   WStage<P> wst_d;  // dgrad weights, staged into WT during the head
 #pragma unroll 1
   for (int i = 0; i < NBLK; ++i) {
-    f32x4 acc[2];
-    conv_row<P>(XR, WT, acc, w, lane);
+    {
+      const f32x4 acc = conv_row<P>(XR, WT, w, hh, lane);
 #pragma unroll
-    for (int h = 0; h < 2; ++h)
-#pragma unroll
-      for (int i2 = 0; i2 < 4; ++i2) y[h][i2] = acc[h][i2];
+      for (int i2 = 0; i2 < 4; ++i2) y[i2] = acc[i2];
+    }
     if (i == 5) DCA_STAMP(cx, 6, L, 0);
     // shifted one-pass sums S1 = sum(y - K), S2 = sum((y - K)^2); K = this block's batch mean of the previous
     // step (0 at the first), identical in every workgroup, so the partials combine exactly
-    const float K0 = misc[P_KSHIFT + i * 32 + c], K1 = misc[P_KSHIFT + i * 32 + 16 + c];
-    float a0 = 0.f, a1 = 0.f, b0 = 0.f, b1 = 0.f;
+    const float K = misc[P_KSHIFT + i * 32 + ch];
+    float a = 0.f, bsq = 0.f;
 #pragma unroll
     for (int i2 = 0; i2 < 4; ++i2) {
-      const float d0 = y[0][i2] - K0, d1 = y[1][i2] - K1;
-      a0 += d0;
-      a1 += d1;
-      b0 += d0 * d0;
-      b1 += d1 * d1;
+      const float d = y[i2] - K;
+      a += d;
+      bsq += d * d;
     }
-    const float pv = wg_csum(a0, a1, b0, b1, cred);
+    const float pv = wg_csum(a, bsq, cred);
     const unsigned tag = tagof(epoch, i);
     if (t < 64) gput(gslot(pa, i, L) + t, tag, pv);
-    if (halo) publish_row(pa, i, L, hwhich, tag, y, lane);
-    // meanwhile: this block's y (and, debug, x) for the backward / diagnostics
-    st8(cx.Y + (size_t)i * B * 8192 + (size_t)n * 8192 + row * 512, lane, y);
-    if (i == NBLK - 1) {
-      // chunk k = t + 256 m: row j, run ch, piece pc (P=1: 4 pieces of 4 floats, P=0: 2 of 8 bf16)
+    if (halo) publish_row(pa, i, L, hwhich, hh, tag, y, lane);
+    // meanwhile: this block's y for the backward / diagnostics
+    st4r(cx.Y + (size_t)i * B * 8192 + img8, hh, lane, y);
+    if (i == NBLK - 4) {
+      // chunk k = t + NTH m: row j, run ch, piece pc (P=1: 4 pieces of 4 floats, P=0: 2 of 8 bf16)
 #pragma unroll
       for (int m = 0; m < W1M; ++m) {
         const int k = t + NTH * m;
         if constexpr (P == 1) {
-          const int j = k >> 7, ch = (k >> 2) & 31, pc = k & 3;
-          w1r[m] = *(const uint4*)(cx.params + OFF_FC1W + j * 2048 + ch * 64 + 16 * s + 4 * pc);
+          const int j = k >> 7, chh = (k >> 2) & 31, pc = k & 3;
+          w1r[m] = *(const uint4*)(cx.params + OFF_FC1W + j * 2048 + chh * 64 + 16 * s + 4 * pc);
         } else {
-          const int j = k >> 6, ch = (k >> 1) & 31, pc = k & 1;
-          w1r[m] = *(const uint4*)((const unsigned short*)cx.w1b + j * 2048 + ch * 64 + 16 * s + 8 * pc);
+          const int j = k >> 6, chh = (k >> 1) & 31, pc = k & 1;
+          w1r[m] = *(const uint4*)((const unsigned short*)cx.w1b + j * 2048 + chh * 64 + 16 * s + 8 * pc);
         }
       }
-      wstage_prefetch<P>(wst_d, pkw + 18432);  // dgrad weights [tap'][ci][co] (hi, lo)
     }
-    float yo[2][4];
+    if (i == NBLK - 2) wstage_prefetch<P>(wst_d, pkw + 18432);  // dgrad weights [tap'][ci][co] (hi, lo)
+    float yo[4];
     if (i == 5) DCA_STAMP(cx, 6, L, 1);
-    xchg_wait(pa, i, epoch, G, cred, halo, hsrc, hwhich ^ 1, yo);
+    xchg_wait(pa, i, epoch, G, cred, halo, hsrc, hwhich ^ 1, hh, yo);
     if (i == 5) DCA_STAMP(cx, 6, L, 2);
     lds_barrier();
     if (i == 5) DCA_STAMP(cx, 6, L, 3);
-    if (halo) st8(pa.yh + ((size_t)(i * LMAX + L) * 2 + hwhich) * 512, lane, yo);
-    // every thread finalises the statistics of its own two channels (same sums, same order everywhere)
-    float scv[2], shv[2];
+    if (halo) st4r(pa.yh + ((size_t)(i * LMAX + L) * 2 + hwhich) * 512, hh, lane, yo);
+    // every thread finalises the statistics of its own channel (same sums, same order everywhere)
+    const float S1 = slot_total(cred, ch), S2 = slot_total(cred, 32 + ch);
+    const float dm = S1 / Ntot;
+    const float mean = K + dm;
+    const float var = fmaxf(S2 / Ntot - dm * dm, 0.f);
+    const float invstd = rsqrtf(var + cx.bn_eps);
+    const float scv = misc[320 + ch] * invstd;
+    const float shv = misc[352 + ch] - mean * scv;
+    if (w == 0 && q == 0) {
+      stat[i * 64 + ch] = mean;
+      stat[i * 64 + 32 + ch] = invstd;
+      scsh[i * 64 + ch] = scv;
+      scsh[i * 64 + 32 + ch] = shv;
+      if (L == 0) {  // BN running statistics (10 EMAs per forward) and the batch stats for the next step
+        const float unb = var * Ntot / (Ntot - 1.f), mo = cx.bn_mom;
+        misc[448 + ch] = misc[448 + ch] * (1.f - mo) + mean * mo;
+        misc[480 + ch] = misc[480 + ch] * (1.f - mo) + unb * mo;
+        cx.STATS[i * 32 + ch] = make_float2(mean, invstd);
+        if (i == NBLK - 1) {
+          cx.rm[ch] = misc[448 + ch];
+          cx.rv[ch] = misc[480 + ch];
+        }
+      }
+    }
+    if (i == NBLK - 3) {  // the fc1 slice into LDS (its region is free during the forward)
+      char* w1l = U + PL::U_W1;
 #pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      const int ch = 16 * h + c;
-      const float S1 = slot_total(cred, ch), S2 = slot_total(cred, 32 + ch);
-      const float dm = S1 / Ntot;
-      const float mean = misc[P_KSHIFT + i * 32 + ch] + dm;
-      const float var = fmaxf(S2 / Ntot - dm * dm, 0.f);
-      const float invstd = rsqrtf(var + cx.bn_eps);
-      scv[h] = misc[320 + ch] * invstd;
-      shv[h] = misc[352 + ch] - mean * scv[h];
-      if (w == 0 && q == 0) {
-        stat[i * 64 + ch] = mean;
-        stat[i * 64 + 32 + ch] = invstd;
-        scsh[i * 64 + ch] = scv[h];
-        scsh[i * 64 + 32 + ch] = shv[h];
-        if (L == 0) {  // BN running statistics (10 EMAs per forward) and the batch stats for the next step
-          const float unb = var * Ntot / (Ntot - 1.f), mo = cx.bn_mom;
-          misc[448 + ch] = misc[448 + ch] * (1.f - mo) + mean * mo;
-          misc[480 + ch] = misc[480 + ch] * (1.f - mo) + unb * mo;
-          cx.STATS[i * 32 + ch] = make_float2(mean, invstd);
+      for (int m = 0; m < W1M; ++m) {
+        const int k = t + NTH * m;
+        if constexpr (P == 1) {
+          const int j = k >> 7, chh = (k >> 2) & 31, pc = k & 3;
+          *(uint4*)(w1l + (j * PL::W1S + chh * 16 + 4 * pc) * 4) = w1r[m];
+        } else {
+          const int j = k >> 6, chh = (k >> 1) & 31, pc = k & 1;
+          *(uint4*)(w1l + (j * PL::W1S + chh * 16 + 8 * pc) * 2) = w1r[m];
         }
       }
     }
     // x_{i+1} = relu(bn(y_i)) + x_i, own row and (halo waves) the neighbour row
 #pragma unroll
-    for (int h = 0; h < 2; ++h)
-#pragma unroll
-      for (int i2 = 0; i2 < 4; ++i2) {
-        x[h][i2] = fmaxf(__builtin_fmaf(y[h][i2], scv[h], shv[h]), 0.f) + x[h][i2];
-        if (halo) xo[h][i2] = fmaxf(__builtin_fmaf(yo[h][i2], scv[h], shv[h]), 0.f) + xo[h][i2];
-      }
+    for (int i2 = 0; i2 < 4; ++i2) {
+      x[i2] = fmaxf(__builtin_fmaf(y[i2], scv, shv), 0.f) + x[i2];
+      if (halo) xo[i2] = fmaxf(__builtin_fmaf(yo[i2], scv, shv), 0.f) + xo[i2];
+    }
     if (i < NBLK - 1) {
-      xr_row<P>(XR, w + 1, q, c, x);
-      if (halo) xr_row<P>(XR, hxrow, q, c, xo);
-      if (pa.debug) st8(cx.X + (size_t)(i + 1) * B * 8192 + (size_t)n * 8192 + row * 512, lane, x);
+      xr_row<P>(XR, w + 1, q, ch, x);
+      if (halo) xr_row<P>(XR, hxrow, q, ch, xo);
+      if (pa.debug) st4r(cx.X + (size_t)(i + 1) * B * 8192 + img8, hh, lane, x);
       lds_barrier();
     }
     DCA_STAMP(cx, 1 + i / 8, L, i % 8);
-  }
-  if (L == 0 && t < 32) {
-    cx.rm[t] = misc[448 + t];
-    cx.rv[t] = misc[480 + t];
   }
 
   // ======================= head ==============================================================================
   // x10 (registers) -> LDS -> 2x2 max-pool -> fc1 partial over this slice's 512 features -> the S slices of the
   // image exchange their partials -> fc1 + ReLU, fc2, cross-entropy (mean over the batch) and their backward
   // (every slice, redundantly) -> dp = W1^T dh for this slice's features -> max-pool backward -> g = dL/dx10.
-  float g[2][4];
+  float g[4];
   {
     float* x10 = (float*)(U + PL::U_X10);
     uint8_t* pcode = (uint8_t*)(U + PL::U_PCODE);
@@ -772,24 +782,11 @@ __global__ void __launch_bounds__(NTH) k_pks_step(Ctx cx, Args pa) {
     char* w1l = U + PL::U_W1;
     wstage_store<P>(wst_d, WT);  // every conv read of WT is done (block 9's conv preceded its exchange)
 #pragma unroll
-    for (int m = 0; m < W1M; ++m) {
-      const int k = t + NTH * m;
-      if constexpr (P == 1) {
-        const int j = k >> 7, ch = (k >> 2) & 31, pc = k & 3;
-        *(uint4*)(w1l + (j * PL::W1S + ch * 16 + 4 * pc) * 4) = w1r[m];
-      } else {
-        const int j = k >> 6, ch = (k >> 1) & 31, pc = k & 1;
-        *(uint4*)(w1l + (j * PL::W1S + ch * 16 + 8 * pc) * 2) = w1r[m];
-      }
-    }
-#pragma unroll
-    for (int h = 0; h < 2; ++h)
-#pragma unroll
-      for (int i2 = 0; i2 < 4; ++i2) x10[(w * 16 + 4 * q + i2) * PL::X10S + 16 * h + c] = x[h][i2];
+    for (int i2 = 0; i2 < 4; ++i2) x10[(w * 16 + 4 * q + i2) * PL::X10S + ch] = x[i2];
     lds_barrier();
-    // pool: thread t -> channel ch = t >> 3, local pool row pr = (t >> 2) & 1, pool cols 2 (t & 3) + {0, 1}
-    {
-      const int ch = t >> 3, pr = (t >> 2) & 1;
+    // pool: thread t < 256 -> channel t >> 3, local pool row pr = (t >> 2) & 1, pool cols 2 (t & 3) + {0, 1}
+    if (t < 256) {
+      const int pch = t >> 3, pr = (t >> 2) & 1;
       float pv[2];
 #pragma unroll
       for (int k = 0; k < 2; ++k) {
@@ -797,7 +794,7 @@ __global__ void __launch_bounds__(NTH) k_pks_step(Ctx cx, Args pa) {
         float v[4];
 #pragma unroll
         for (int e = 0; e < 4; ++e)  // window order (0,0) (0,1) (1,0) (1,1): first maximum wins
-          v[e] = x10[((2 * pr + (e >> 1)) * 16 + 2 * pc + (e & 1)) * PL::X10S + ch];
+          v[e] = x10[((2 * pr + (e >> 1)) * 16 + 2 * pc + (e & 1)) * PL::X10S + pch];
         float best = v[0];
         unsigned id = 0;
         if (v[1] > best) { best = v[1]; id = 1; }
@@ -808,34 +805,35 @@ __global__ void __launch_bounds__(NTH) k_pks_step(Ctx cx, Args pa) {
       }
       *(float2*)(pl + 2 * t) = make_float2(pv[0], pv[1]);
       // fc1 input for the weight gradient: global feature ch*64 + (2s + pr)*8 + pc
-      *(float2*)(cx.HP + (size_t)n * 2048 + ch * 64 + (2 * s + pr) * 8 + 2 * (t & 3)) = make_float2(pv[0], pv[1]);
+      *(float2*)(cx.HP + (size_t)n * 2048 + pch * 64 + (2 * s + pr) * 8 + 2 * (t & 3)) = make_float2(pv[0], pv[1]);
     }
     lds_barrier();
-    // fc1 partial over this slice's features: thread (row j = t >> 3, part k = t & 7) sums features u = 8m + k,
-    // then 3 xor-shuffles over the 8 parts (fixed order: identical in every workgroup)
+    // fc1 partial over this slice's features: thread (row j = t >> 4, part k = t & 15) sums features u = 16m + k,
+    // then 4 xor-shuffles over the 16 parts (fixed order: identical in every workgroup)
     {
-      const int j = t >> 3, k = t & 7;
+      const int j = t >> 4, k = t & 15;
       float a = 0.f;
 #pragma unroll 8
-      for (int m = 0; m < 64; ++m) {
-        const int u = 8 * m + k;
-        const float wv = P == 1 ? ((const float*)w1l)[j * PL::W1S + u]
-                                : __uint_as_float((unsigned)((const unsigned short*)w1l)[j * PL::W1S + u] << 16);
-        a += wv * pl[u];
+      for (int m = 0; m < 32; ++m) {
+        const int u = 16 * m + k;
+        const float wvv = P == 1 ? ((const float*)w1l)[j * PL::W1S + u]
+                                 : __uint_as_float((unsigned)((const unsigned short*)w1l)[j * PL::W1S + u] << 16);
+        a += wvv * pl[u];
       }
       a += __shfl_xor(a, 1);
       a += __shfl_xor(a, 2);
       a += __shfl_xor(a, 4);
+      a += __shfl_xor(a, 8);
       if (k == 0) hp[j] = a;
     }
     lds_barrier();
     DCA_STAMP(cx, 3, L, 1);
     const unsigned tag = tagof(epoch, RND_HEAD);
     if (t < 32) gput(gslot(pa, RND_HEAD, L) + t, tag, hp[t]);
-    if (w == 0) {
+    if (wv == 0) {
       // the image's S partials, summed in slice order (bitwise identical in every slice); fc1 bias + ReLU, fc2,
       // softmax cross-entropy and dh, lane-parallel with shuffles
-      float hh = 0.f;
+      float hsum = 0.f;
       {
         const __amdgpu_buffer_rsrc_t rs = grsrc(pa, RND_HEAD);
         const int sl = lane & 31;
@@ -849,7 +847,7 @@ __global__ void __launch_bounds__(NTH) k_pks_step(Ctx cx, Args pa) {
             ok &= xg[1] == tag;
             a += __uint_as_float(xg[0]);
           }
-          hh = a;
+          hsum = a;
           if (__all(ok)) break;
           if (spins >= SPIN_LIMIT) {
             if (lane == 0) atomicOr(pa.err, 1u << RND_HEAD);
@@ -858,8 +856,8 @@ __global__ void __launch_bounds__(NTH) k_pks_step(Ctx cx, Args pa) {
         }
       }
       DCA_STAMP(cx, 3, L, 2);
-      hh += misc[512 + (lane & 31)];
-      const float hr = fmaxf(hh, 0.f);
+      hsum += misc[512 + (lane & 31)];
+      const float hr = fmaxf(hsum, 0.f);
       const int o = lane < 10 ? lane : 0;
       float logit = misc[864 + o];
 #pragma unroll
@@ -890,7 +888,7 @@ __global__ void __launch_bounds__(NTH) k_pks_step(Ctx cx, Args pa) {
         sd += misc[544 + oo * 32 + (lane & 31)] * dlo;
         dl = lane == oo ? dlo : dl;
       }
-      const float dh = hh > 0.f ? sd : 0.f;
+      const float dh = hsum > 0.f ? sd : 0.f;
       if (lane < 32) hp[32 + lane] = dh;
       if (s == 0) {
         if (lane == 0) cx.HLOSS[n] = lse - lt;
@@ -903,54 +901,42 @@ __global__ void __launch_bounds__(NTH) k_pks_step(Ctx cx, Args pa) {
     }
     lds_barrier();
     DCA_STAMP(cx, 3, L, 3);
-    {  // dp = W1^T dh for this thread's two local features u = 2t, 2t + 1
-      float d0 = 0.f, d1 = 0.f;
+    {  // dp = W1^T dh for this thread's local feature u = t
+      float d0 = 0.f;
 #pragma unroll 8
       for (int j = 0; j < 32; ++j) {
-        const float dhj = hp[32 + j];
-        float w0, w1;
-        if constexpr (P == 1) {
-          const float2 wv = *(const float2*)((const float*)w1l + j * PL::W1S + 2 * t);
-          w0 = wv.x;
-          w1 = wv.y;
-        } else {
-          const unsigned u = *(const unsigned*)((const unsigned short*)w1l + j * PL::W1S + 2 * t);
-          w0 = __uint_as_float(u << 16);
-          w1 = __uint_as_float(u & 0xffff0000u);
-        }
-        d0 += dhj * w0;
-        d1 += dhj * w1;
+        const float wvv = P == 1 ? ((const float*)w1l)[j * PL::W1S + t]
+                                 : __uint_as_float((unsigned)((const unsigned short*)w1l)[j * PL::W1S + t] << 16);
+        d0 += hp[32 + j] * wvv;
       }
-      *(float2*)(dpl + 2 * t) = make_float2(d0, d1);
+      dpl[t] = d0;
     }
     lds_barrier();
     // g = max-pool backward of dp, routed by the saved argmax (this thread's pixels)
 #pragma unroll
-    for (int h = 0; h < 2; ++h)
-#pragma unroll
-      for (int i2 = 0; i2 < 4; ++i2) {
-        const int col = 4 * q + i2, u = (16 * h + c) * 16 + (w >> 1) * 8 + (col >> 1);
-        const unsigned pos = (unsigned)((w & 1) * 2 + (col & 1));
-        g[h][i2] = pcode[u] == pos ? dpl[u] : 0.f;
-      }
-    if (pa.debug) st8(cx.G + (size_t)n * 8192 + row * 512, lane, g);
+    for (int i2 = 0; i2 < 4; ++i2) {
+      const int col = 4 * q + i2, u = ch * 16 + (w >> 1) * 8 + (col >> 1);
+      const unsigned pos = (unsigned)((w & 1) * 2 + (col & 1));
+      g[i2] = pcode[u] == pos ? dpl[u] : 0.f;
+    }
+    if (pa.debug) st4r(cx.G + img8, hh, lane, g);
   }
   DCA_STAMP(cx, 3, L, 0);
 
   // ======================= backward: 10 applications, newest first ===========================================
   unsigned short* dyT = (unsigned short*)(U + PL::U_DYT);
   unsigned short* xT = (unsigned short*)(U + PL::U_XT);
-  lds_barrier();  // every wave is done with the head's LDS (X10 / DP overlap XR)
+  lds_barrier();  // every wave is done with the head's LDS (X10 / W1 / DP overlap XR / dyT / xT)
   for (int idx = t; idx < PL::NP * PL::XR_PL / 16; idx += NTH) ((uint4*)XR)[idx] = uint4{0u, 0u, 0u, 0u};
   for (int idx = t; idx < PL::NP * PL::XT_PL / 16; idx += NTH) ((uint4*)xT)[idx] = uint4{0u, 0u, 0u, 0u};
   f32x4 wacc[NNT][2];
 #pragma unroll
   for (int j = 0; j < NNT; ++j) wacc[j][0] = wacc[j][1] = z4();
   float dgam = 0.f, dbet = 0.f;
-  float yv[2][4], yo[2][4] = {};  // y_i of this row / of the halo row
-  ld8(cx.Y + (size_t)(NBLK - 1) * B * 8192 + (size_t)n * 8192 + row * 512, lane, yv);
-  if (halo) ld8(pa.yh + ((size_t)((NBLK - 1) * LMAX + L) * 2 + hwhich) * 512, lane, yo);
-  unsigned codew[2];     // stem-backward prefetch (during block 0)
+  float yv[4], yo[4] = {};  // y_i of this row / of the halo row
+  ld4r(cx.Y + (size_t)(NBLK - 1) * B * 8192 + img8, hh, lane, yv);
+  if (halo) ld4r(pa.yh + ((size_t)((NBLK - 1) * LMAX + L) * 2 + hwhich) * 512, hh, lane, yo);
+  unsigned codew = 0;  // stem-backward prefetch (during block 0)
   unsigned imgw = 0;
   uint4 nxt = uint4{0u, 0u, 0u, 0u};
   int nxt_lab = 0;
@@ -958,45 +944,39 @@ __global__ void __launch_bounds__(NTH) k_pks_step(Ctx cx, Args pa) {
 #pragma unroll 1
   for (int i = NBLK - 1; i >= 0; --i) {
     // recover x_i = x_{i+1} - relu(bn(y_i)) (same fma, same scale / shift as the forward); BN-backward inputs
-    float dz[2][4], xh[2][4], xho[2][4];
-    float sa[2] = {0.f, 0.f}, sbv[2] = {0.f, 0.f};
+    float dz[4], xh[4], xho[4];
+    float sa = 0.f, sbv = 0.f;
+    const float mean = stat[i * 64 + ch], inv = stat[i * 64 + 32 + ch];
+    const float sc = scsh[i * 64 + ch], sh = scsh[i * 64 + 32 + ch];
 #pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      const int ch = 16 * h + c;
-      const float mean = stat[i * 64 + ch], inv = stat[i * 64 + 32 + ch];
-      const float sc = scsh[i * 64 + ch], sh = scsh[i * 64 + 32 + ch];
-#pragma unroll
-      for (int i2 = 0; i2 < 4; ++i2) {
-        const float z = __builtin_fmaf(yv[h][i2], sc, sh);
-        x[h][i2] = x[h][i2] - fmaxf(z, 0.f);
-        xh[h][i2] = (yv[h][i2] - mean) * inv;
-        dz[h][i2] = z > 0.f ? g[h][i2] : 0.f;
-        sa[h] += dz[h][i2];
-        sbv[h] += dz[h][i2] * xh[h][i2];
-        if (halo) {
-          const float zo = __builtin_fmaf(yo[h][i2], sc, sh);
-          xo[h][i2] = xo[h][i2] - fmaxf(zo, 0.f);
-          xho[h][i2] = (yo[h][i2] - mean) * inv;
-        }
+    for (int i2 = 0; i2 < 4; ++i2) {
+      const float z = __builtin_fmaf(yv[i2], sc, sh);
+      x[i2] = x[i2] - fmaxf(z, 0.f);
+      xh[i2] = (yv[i2] - mean) * inv;
+      dz[i2] = z > 0.f ? g[i2] : 0.f;
+      sa += dz[i2];
+      sbv += dz[i2] * xh[i2];
+      if (halo) {
+        const float zo = __builtin_fmaf(yo[i2], sc, sh);
+        xo[i2] = xo[i2] - fmaxf(zo, 0.f);
+        xho[i2] = (yo[i2] - mean) * inv;
       }
     }
     const int rnd = RND_HEAD + 1 + (NBLK - 1 - i);
     const unsigned tag = tagof(epoch, rnd);
     if (i == 5) DCA_STAMP(cx, 7, L, 0);
-    const float pv = wg_csum(sa[0], sa[1], sbv[0], sbv[1], cred);
+    const float pv = wg_csum(sa, sbv, cred);
     if (t < 64) gput(gslot(pa, rnd, L) + t, tag, pv);
-    if (halo) publish_row(pa, rnd, L, hwhich, tag, dz, lane);
+    if (halo) publish_row(pa, rnd, L, hwhich, hh, tag, dz, lane);
     if (i == 5) DCA_STAMP(cx, 7, L, 1);
     // while the exchange is in flight: the weight gradient of the PREVIOUS application (block i + 1), whose dy /
     // x tiles are still staged; then the barrier retires every wave's reads of them before x_i replaces them
-    if (i < NBLK - 1) wgrad_acc<P>(dyT, xT, wacc, w, lane);
+    if (i < NBLK - 1) wgrad_acc<P>(dyT, xT, wacc, wv, lane);
     if (i == 5) DCA_STAMP(cx, 7, L, 2);
     if (i > 0) {  // prefetch y_{i-1}; lands while this block's exchange and convolutions run
-      ld8(cx.Y + (size_t)(i - 1) * B * 8192 + (size_t)n * 8192 + row * 512, lane, yv);
+      ld4r(cx.Y + (size_t)(i - 1) * B * 8192 + img8, hh, lane, yv);
     } else {      // last block: what the stem backward needs (pool codes, raw input words, next batch's image)
-#pragma unroll
-      for (int h = 0; h < 2; ++h)
-        codew[h] = *(const unsigned*)(cx.SCODE + (size_t)n * 8192 + row * 512 + h * 256 + lane * 4);
+      codew = *(const unsigned*)(cx.SCODE + img8 + hh * 256 + lane * 4);
       {
         const int ci = t / 80, rem = t % 80, xr_ = rem >> 3, yimg = 8 * s - 1 + xr_;
         const int yc = yimg < 0 ? 0 : (yimg > 31 ? 31 : yimg);
@@ -1006,42 +986,38 @@ __global__ void __launch_bounds__(NTH) k_pks_step(Ctx cx, Args pa) {
       if (t == 48) nxt_lab = cx.labels[next_id];
     }
     lds_barrier();
-    xt_row<P>(xT, w + 1, q, c, x);
-    if (halo) xt_row<P>(xT, hxrow, q, c, xo);
-    float dzo[2][4];
+    xt_row<P>(xT, w + 1, q, ch, x);
+    if (halo) xt_row<P>(xT, hxrow, q, ch, xo);
+    float dzo[4];
     if (i == 5) DCA_STAMP(cx, 7, L, 3);
-    xchg_wait(pa, rnd, epoch, G, cred, halo, hsrc, hwhich ^ 1, dzo);
+    xchg_wait(pa, rnd, epoch, G, cred, halo, hsrc, hwhich ^ 1, hh, dzo);
     if (i == 5) DCA_STAMP(cx, 7, L, 4);
-    if (halo && i > 0) ld8(pa.yh + ((size_t)((i - 1) * LMAX + L) * 2 + hwhich) * 512, lane, yo);
+    if (halo && i > 0) ld4r(pa.yh + ((size_t)((i - 1) * LMAX + L) * 2 + hwhich) * 512, hh, lane, yo);
     lds_barrier();
     if (i == 5) DCA_STAMP(cx, 7, L, 5);
     if (L == 0 && t < 32) {  // BN affine gradients: dbeta = sum dz, dgamma = sum dz * xhat
       dbet += slot_total(cred, t);
       dgam += slot_total(cred, 32 + t);
     }
-    float dyv[2][4], dyo[2][4];
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      const int ch = 16 * h + c;
+    float dyv[4], dyo[4];
+    {
       const float Sa = slot_total(cred, ch), Sb = slot_total(cred, 32 + ch);
-      const float k1 = misc[320 + ch] * stat[i * 64 + 32 + ch] / Ntot;
+      const float k1 = misc[320 + ch] * inv / Ntot;
 #pragma unroll
       for (int i2 = 0; i2 < 4; ++i2) {
-        dyv[h][i2] = k1 * (Ntot * dz[h][i2] - Sa - xh[h][i2] * Sb);
-        if (halo) dyo[h][i2] = k1 * (Ntot * dzo[h][i2] - Sa - xho[h][i2] * Sb);
+        dyv[i2] = k1 * (Ntot * dz[i2] - Sa - xh[i2] * Sb);
+        if (halo) dyo[i2] = k1 * (Ntot * dzo[i2] - Sa - xho[i2] * Sb);
       }
     }
-    xr_row<P>(XR, w + 1, q, c, dyv);
-    if (halo) xr_row<P>(XR, hxrow, q, c, dyo);
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      const int ch = 16 * h + c;
+    xr_row<P>(XR, w + 1, q, ch, dyv);
+    if (halo) xr_row<P>(XR, hxrow, q, ch, dyo);
+    {
       unsigned hb[4], lb[4];
 #pragma unroll
       for (int i2 = 0; i2 < 4; ++i2) {
-        const unsigned short hi = bfbits(dyv[h][i2]);
+        const unsigned short hi = bfbits(dyv[i2]);
         hb[i2] = hi;
-        lb[i2] = P == 1 ? bf_lo(dyv[h][i2], hi) : 0u;
+        lb[i2] = P == 1 ? bf_lo(dyv[i2], hi) : 0u;
       }
       *(uint2*)(dyT + ch * PL::DYT_S + w * 16 + 4 * q) = uint2{hb[0] | (hb[1] << 16), hb[2] | (hb[3] << 16)};
       if constexpr (P == 1)
@@ -1049,22 +1025,18 @@ __global__ void __launch_bounds__(NTH) k_pks_step(Ctx cx, Args pa) {
             uint2{lb[0] | (lb[1] << 16), lb[2] | (lb[3] << 16)};
     }
     if (pa.debug) {
-      st8(cx.DY + (size_t)i * B * 8192 + (size_t)n * 8192 + row * 512, lane, dyv);
-      st8(cx.X + (size_t)i * B * 8192 + (size_t)n * 8192 + row * 512, lane, x);
+      st4r(cx.DY + (size_t)i * B * 8192 + img8, hh, lane, dyv);
+      st4r(cx.X + (size_t)i * B * 8192 + img8, hh, lane, x);
     }
     lds_barrier();
     if (i == 5) DCA_STAMP(cx, 7, L, 6);
     // dgrad: g_i = g_{i+1} + conv(dy, W^T flipped)
     {
-      f32x4 acc[2];
-      conv_row<P>(XR, WT, acc, w, lane);
+      const f32x4 acc = conv_row<P>(XR, WT, w, hh, lane);
 #pragma unroll
-      for (int h = 0; h < 2; ++h)
-#pragma unroll
-        for (int i2 = 0; i2 < 4; ++i2) g[h][i2] += acc[h][i2];
+      for (int i2 = 0; i2 < 4; ++i2) g[i2] += acc[i2];
     }
-    if (pa.debug && (i == 2 || i == 1)) st8(cx.G + (size_t)(i == 2 ? 0 : 1) * B * 8192 + (size_t)n * 8192 + row * 512,
-                                            lane, g);
+    if (pa.debug && (i == 2 || i == 1)) st4r(cx.G + (size_t)(i == 2 ? 0 : 1) * B * 8192 + img8, hh, lane, g);
     DCA_STAMP(cx, 4 + (NBLK - 1 - i) / 8, L, (NBLK - 1 - i) % 8);
   }
   if (L == 0 && t < 32) {
@@ -1074,31 +1046,29 @@ __global__ void __launch_bounds__(NTH) k_pks_step(Ctx cx, Args pa) {
 
   // ======================= stem backward: max-pool bwd (saved argmax) -> ReLU mask -> conv1 wgrad ============
   lds_barrier();  // every wave is done with XR / WT (the last dgrad); dyT / xT stay for the last wgrad
-  wgrad_acc<P>(dyT, xT, wacc, w, lane);  // application 0
+  wgrad_acc<P>(dyT, xT, wacc, wv, lane);  // application 0
   {
     unsigned short* dsT = (unsigned short*)(U + PL::U_DST);
     unsigned short* xs = (unsigned short*)(U + PL::U_XS);
-    // d(conv1 output) of this wave's two conv rows: every 2x2 window written whole (value at the argmax if the
-    // ReLU was active, zeros elsewhere)
-    float db0 = 0.f, db1 = 0.f;
+    float* sred = (float*)(U + PL::U_SRED);
+    // d(conv1 output) of this row's two conv rows, channel ch: every 2x2 window written whole (value at the
+    // argmax if the ReLU was active, zeros elsewhere)
+    float db = 0.f;
 #pragma unroll
-    for (int h = 0; h < 2; ++h)
-#pragma unroll
-      for (int i2 = 0; i2 < 4; ++i2) {
-        const unsigned code = (codew[h] >> (8 * i2)) & 255u, pos = code & 3u;
-        const float val = (code & 4u) ? g[h][i2] : 0.f;
-        const unsigned short vh = bfbits(val);
-        const unsigned vb = vh, vl = P == 1 ? (unsigned)bf_lo(val, vh) : 0u;
-        const int ch = 16 * h + c, so = ch * PL::DSP + (2 * w) * 32 + 2 * (4 * q + i2);
-        *(unsigned*)(dsT + so) = (pos == 0 ? vb : 0u) | ((pos == 1 ? vb : 0u) << 16);
-        *(unsigned*)(dsT + so + 32) = (pos == 2 ? vb : 0u) | ((pos == 3 ? vb : 0u) << 16);
-        if constexpr (P == 1) {
-          *(unsigned*)(dsT + PL::DST_PL / 2 + so) = (pos == 0 ? vl : 0u) | ((pos == 1 ? vl : 0u) << 16);
-          *(unsigned*)(dsT + PL::DST_PL / 2 + so + 32) = (pos == 2 ? vl : 0u) | ((pos == 3 ? vl : 0u) << 16);
-        }
-        if (h == 0) db0 += val;
-        else db1 += val;
+    for (int i2 = 0; i2 < 4; ++i2) {
+      const unsigned code = (codew >> (8 * i2)) & 255u, pos = code & 3u;
+      const float val = (code & 4u) ? g[i2] : 0.f;
+      const unsigned short vh = bfbits(val);
+      const unsigned vb = vh, vl = P == 1 ? (unsigned)bf_lo(val, vh) : 0u;
+      const int so = ch * PL::DSP + (2 * w) * 32 + 2 * (4 * q + i2);
+      *(unsigned*)(dsT + so) = (pos == 0 ? vb : 0u) | ((pos == 1 ? vb : 0u) << 16);
+      *(unsigned*)(dsT + so + 32) = (pos == 2 ? vb : 0u) | ((pos == 3 ? vb : 0u) << 16);
+      if constexpr (P == 1) {
+        *(unsigned*)(dsT + PL::DST_PL / 2 + so) = (pos == 0 ? vl : 0u) | ((pos == 1 ? vl : 0u) << 16);
+        *(unsigned*)(dsT + PL::DST_PL / 2 + so + 32) = (pos == 2 ? vl : 0u) | ((pos == 3 ? vl : 0u) << 16);
       }
+      db += val;
+    }
     // three column-shifted copies of the normalised input rows 8s-1 .. 8s+8 (copy kw holds x[col + kw - 1])
     if (t < 240) {
       const int ci = t / 80, rem = t % 80, xr_ = rem >> 3, x0 = 4 * (rem & 7), yimg = 8 * s - 1 + xr_;
@@ -1130,19 +1100,20 @@ __global__ void __launch_bounds__(NTH) k_pks_step(Ctx cx, Args pa) {
       }
     }
     // conv1 bias gradient partial of this workgroup (also the barrier before the MFMAs)
-    const float dbv = wg_csum(db0, db1, 0.f, 0.f, cred);
+    const float dbv = wg_csum(db, 0.f, cred);
     float* ss = cx.SSLAB + (size_t)L * SSLAB_N;
     if (t < 32) ss[1024 + t] = dbv;
     // D[co][k] = sum over this slice's conv pixels of ds[p][co] * im2col[p][k]; K step = one conv row (32 px).
-    // Wave w: tile w (mt = co half, nt = k tile); k >= 27 columns are discarded by the reduce
+    // Wave wv: tile wv & 3 (mt = co half, nt = k tile), conv rows 4 (wv >> 2) .. +3; k >= 27 columns are
+    // discarded by the reduce
     {
-      const int mt = w & 1, nt = w >> 1;
+      const int tile = wv & 3, mt = tile & 1, nt = tile >> 1, sr0 = 4 * (wv >> 2);
       const int kidx = 16 * nt + c, kk = kidx < 27 ? kidx : 0, ci = kk / 9, kh = (kk % 9) / 3, kw = kk % 3;
       const unsigned short* abase = dsT + (16 * mt + c) * PL::DSP + 8 * q;
       const unsigned short* bbase = xs + ((kw * 3 + ci) * PL::XSR + kh) * PL::XS_S + 8 * q;
       f32x4 acc2 = z4();
 #pragma unroll
-      for (int sr = 0; sr < 2 * RS; ++sr) {
+      for (int sr = sr0; sr < sr0 + 4; ++sr) {
         const bf16x8 a = *(const bf16x8*)(abase + sr * 32);
         const bf16x8 bb = *(const bf16x8*)(bbase + sr * PL::XS_S);
         bf16x8 al = a, bl = bb;
@@ -1152,7 +1123,12 @@ __global__ void __launch_bounds__(NTH) k_pks_step(Ctx cx, Args pa) {
         }
         acc2 = mma3<P>(a, al, bb, bl, acc2);
       }
-      st4(ss + ((w * 64 + lane) << 2), acc2);
+      st4(sred + ((wv * 64 + lane) << 2), acc2);
+    }
+    lds_barrier();
+    if (t < 256) {
+      const int tile = t >> 6, ln = t & 63;
+      st4(ss + ((tile * 64 + ln) << 2), ld4(sred + ((tile * 64 + ln) << 2)) + ld4(sred + (((tile + 4) * 64 + ln) << 2)));
     }
   }
   // the next batch's image n (this slice's quarter) and label, staged into the other parity
@@ -1161,7 +1137,7 @@ __global__ void __launch_bounds__(NTH) k_pks_step(Ctx cx, Args pa) {
   // trunk wgrad slab (accumulated over the 10 applications): tile tt = 2 nt + mt, the layout k_pks_reduce reads
 #pragma unroll
   for (int j = 0; j < NNT; ++j) {
-    const int nt = w + NW * j;
+    const int nt = wv + NW * j;
     if (nt < 18) {
       st4(pa.tslab + (size_t)L * WSLAB_N + (((2 * nt) * 64 + lane) << 2), wacc[j][0]);
       st4(pa.tslab + (size_t)L * WSLAB_N + (((2 * nt + 1) * 64 + lane) << 2), wacc[j][1]);

@@ -52,21 +52,36 @@ def _conv(mod, x, bf16_operands: bool):
     return mod(x)
 
 
+def _forced(t: torch.Tensor, value) -> torch.Tensor:
+    """Straight-through: the forward takes `value`, the gradient flows to `t` unchanged."""
+    if value is None:
+        return t
+    return t + (value.to(t.dtype) - t).detach()
+
+
 def reference_step(model, imgs_u8: torch.Tensor, labels: torch.Tensor, lr: float = 1e-2, apply_sgd: bool = True,
-                   bf16_operands: bool = False, fc1_bf16: bool = False):
+                   bf16_operands: bool = False, fc1_bf16: bool = False, force: dict | None = None):
     """One SGD step of `model` (mutated in place).  Returns a dict of intermediates and gradients.
 
     bf16_operands=True emulates the engine's bf16 mode (bf16 MFMA operands, fp32 everything else), so the
     comparison isolates kernel bugs from bf16 rounding; fc1_bf16=True additionally rounds the fc1 weight the
-    persistent engine reads (its head keeps a bf16 copy of fc1.weight)."""
+    persistent engine reads (its head keeps a bf16 copy of fc1.weight).
+
+    force={"c1": NCHW conv1 output (pre-ReLU), "x0": NCHW stem output, "y": [10 NCHW conv outputs]} (the
+    engine's own forward, any subset): every forced tensor
+    enters the graph straight-through, so BatchNorm statistics, ReLU masks and max-pool argmaxes downstream of it
+    are the engine's.  The backward then differs from the engine's only by arithmetic, not by the mask flips that
+    near-zero pre-activations cause between two independently rounded forwards (flip-aware comparison)."""
+    force = force or {}
     x = normalize_u8(imgs_u8)
     blk = model.resblocks[0]
-    out0 = F.max_pool2d(torch.relu(_conv(model.conv1, x, bf16_operands)), 2)
+    c1 = _forced(_conv(model.conv1, x, bf16_operands), force.get("c1"))
+    out0 = _forced(F.max_pool2d(torch.relu(c1), 2), force.get("x0"))
     xs, ys = [out0], []
     out0.retain_grad()
     cur = out0
-    for _ in range(len(model.resblocks)):
-        y = _conv(blk.conv, cur, bf16_operands)
+    for i in range(len(model.resblocks)):
+        y = _forced(_conv(blk.conv, cur, bf16_operands), force["y"][i] if "y" in force else None)
         y.retain_grad()
         ys.append(y)
         nxt = torch.relu(blk.batch_norm(y)) + cur

@@ -73,7 +73,7 @@ def _worker(rank, port, dtype, persistent, q):
         eng.run_external(B, STEPS, allreduce)
         loss, steps = eng.read_loss()
         assert steps == STEPS
-        sim = _simulate(ref0, data, labels, order, 1e-2, dtype == "bf16", persistent)[rank]
+        sim = _simulate(ref0, data, labels, order, 1e-2, dtype == "bf16", persistent and dtype == "bf16")[rank]
         tol = 1e-3 if dtype == "fp32" else 3e-2
         sd, rsd = model.state_dict(), sim.state_dict()
         for k in ("fc1.weight", "fc2.bias", "resblocks.0.conv.weight", "resblocks.0.batch_norm.weight",
@@ -96,10 +96,13 @@ def _worker(rank, port, dtype, persistent, q):
             dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("dtype,persistent,split", [("bf16", True, "0"), ("bf16", True, "1"), ("fp32", False, "0"),
-                                                    ("bf16", False, "0")])
-def test_engine_ddp_two_ranks_one_gpu(gpu, port, dtype, persistent, split, monkeypatch):
-    monkeypatch.setenv("DCA_PK_SPLIT", split)  # inherited by the spawned ranks
+@pytest.mark.parametrize("dtype,persistent,kernel", [("bf16", True, "sliced"), ("fp32", True, "sliced"),
+                                                     ("bf16", True, "per-image-split"), ("fp32", False, "multi"),
+                                                     ("bf16", False, "multi")])
+def test_engine_ddp_two_ranks_one_gpu(gpu, port, dtype, persistent, kernel, monkeypatch):
+    # inherited by the spawned ranks: the one-workgroup-per-image kernel in its two-phase (split) mode
+    monkeypatch.setenv("DCA_PKS", "0" if kernel == "per-image-split" else "1")
+    monkeypatch.setenv("DCA_PK_SPLIT", "1" if kernel == "per-image-split" else "0")
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     procs = [ctx.Process(target=_worker, args=(r, port, dtype, persistent, q)) for r in range(WS)]
@@ -161,7 +164,7 @@ def _xgmi_worker(rank, ws, port, dtype, persistent, q, comm="xgmi", own_device=F
                         v.copy_(snap[k])
                 sel = order[r][s * B:(s + 1) * B]
                 out = reference_step(models[r], data[sel], labels[sel], lr=1e-2, apply_sgd=False,
-                                     bf16_operands=dtype == "bf16", fc1_bf16=persistent)
+                                     bf16_operands=dtype == "bf16", fc1_bf16=persistent and dtype == "bf16")
                 grads.append(out["grads"])
             with torch.no_grad():
                 for r in range(ws):
@@ -189,7 +192,8 @@ def _xgmi_worker(rank, ws, port, dtype, persistent, q, comm="xgmi", own_device=F
             dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("ws,dtype,persistent", [(2, "bf16", True), (4, "bf16", True), (2, "fp32", False)])
+@pytest.mark.parametrize("ws,dtype,persistent", [(2, "bf16", True), (4, "bf16", True), (2, "fp32", True),
+                                                 (2, "fp32", False)])
 def test_xgmi_allreduce_ranks_one_gpu(gpu, port, ws, dtype, persistent):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()

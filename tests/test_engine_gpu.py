@@ -1,9 +1,10 @@
 """Native engine on a real MI355X: numerics of the HIP kernels vs the plain PyTorch fp32 oracle, end-to-end entry
 points, and that the in-tree native library (not an eager fallback) is what runs.
 
-Tolerances are relative L2 errors per tensor (ReLU-mask flips at |z|~0 make max-error meaningless):
-  fp32 engine (exact fp32 MFMA, different summation order) <= 1e-2 per tensor, trajectory <= 1e-3;
-  bf16 engine (bf16 MFMA operands, fp32 accumulation; oracle rounds the same operands) <= 5e-2, trajectory <= 3e-2.
+Tolerances are relative L2 errors per tensor:
+  independent forwards (ReLU / max-pool mask flips at |z|~0 dominate): fp32 <= 1e-2, bf16 <= 5e-2 per tensor;
+  flip-aware (the oracle forced onto the engine's forward): fp32 (3xbf16 MFMA) <= 1e-4, bf16 <= 3e-3;
+  8-step trajectory, whole parameter vector: fp32 <= 1e-4, bf16 <= 3e-2.
 """
 import json
 import os
@@ -36,27 +37,49 @@ def test_native_library_loaded_in_tree(gpu):
 
 
 @pytest.mark.parametrize("dtype,persistent,B,graph", [
-    ("fp32", False, 32, True),
-    ("bf16", False, 32, True),
+    ("fp32", True, 32, True),   # image-sliced persistent kernel, fp32-accurate (3xbf16) MFMA
     ("bf16", True, 32, True),
     ("bf16", True, 32, False),
     ("bf16", True, 16, True),   # ragged last batch of an epoch
-    ("fp32", False, 20, True),
+    ("fp32", True, 20, True),
+    ("fp32", True, 64, True),   # main_no_ddp.py's batch
+    ("fp32", False, 32, True),  # multi-kernel engine (exact fp32 MFMA)
+    ("bf16", False, 32, True),
 ])
 def test_one_step_matches_oracle(gpu, dtype, persistent, B, graph):
+    """Independent forwards: ReLU / max-pool masks may flip where a pre-activation is ~0, so the backward is
+    compared in relative L2 at a loose bound; the flip-aware test below pins the arithmetic."""
     from engine_diag import compare_one_step
     res = compare_one_step(dtype, 4, B, graph, seed=B, verbose=False, persistent=persistent)
     tol = 1e-2 if dtype == "fp32" else 5e-2
     bad = {k: v for k, v in res.items() if v > tol}
     assert not bad, bad
     assert res["state:resblocks.0.batch_norm.num_batches_tracked"] == 0.0  # nbt += 10 per step
+    if dtype == "fp32" and persistent:  # forward activations before any mask can flip: 3xbf16 accuracy
+        assert max(res[f"x{i}"] for i in range(10)) < 1e-4 and max(res[f"y{i}"] for i in range(10)) < 1e-4, res
 
 
-@pytest.mark.parametrize("dtype,persistent,tol", [("fp32", False, 1e-3), ("bf16", True, 3e-2)])
+@pytest.mark.parametrize("dtype,B,tol", [("fp32", 32, 1e-4), ("fp32", 20, 1e-4), ("fp32", 64, 1e-4),
+                                          ("bf16", 32, 3e-3)])
+def test_one_step_flip_aware(gpu, dtype, B, tol):
+    """The oracle's forward is forced onto the engine's own conv1 output, stem output and 10 conv outputs
+    (straight-through), so BatchNorm statistics, ReLU masks and max-pool argmaxes are the engine's and the
+    backward differs by arithmetic only: every activation gradient, every parameter gradient and the updated
+    state within `tol` relative L2 (fp32 mode: 3xbf16 products, ~2^-17 each)."""
+    from engine_diag import compare_one_step
+    res = compare_one_step(dtype, 4, B, True, seed=3 + B, verbose=False, persistent=True, forced=True)
+    bad = {k: v for k, v in res.items() if v > tol}
+    assert not bad, bad
+
+
+@pytest.mark.parametrize("dtype,persistent,tol", [("fp32", True, 1e-4), ("bf16", True, 3e-2),
+                                                  ("fp32", False, 1e-4)])
 def test_trajectory_matches_oracle(gpu, dtype, persistent, tol):
+    """8 steps, both sides independent: losses and the whole parameter vector (relative L2) track the fp32
+    oracle; the worst single tensor (a bias fed by a few mask flips) within 20x."""
     from engine_diag import trajectory
     tr = trajectory(dtype, 4, 32, 8, persistent=persistent)
-    assert tr["max_param_rel_err"] < tol, tr
+    assert tr["param_rel_l2"] < tol and tr["max_param_rel_err"] < 20 * tol, tr
     for le, lr in zip(tr["losses_engine"], tr["losses_ref"]):
         assert abs(le - lr) < 5 * tol * max(1.0, abs(lr)), (le, lr)
 
@@ -119,6 +142,7 @@ def test_split_mode_matches_oracle(gpu, monkeypatch):
     """Two-phase persistent step (phase 1: stem/forward/head, phase 2: backward; fc gradients in their own
     kernel) gives the same step as the fused kernel."""
     from engine_diag import compare_one_step
+    monkeypatch.setenv("DCA_PKS", "0")  # the one-workgroup-per-image kernel
     monkeypatch.setenv("DCA_PK_SPLIT", "1")
     res = compare_one_step("bf16", 4, 32, True, seed=7, verbose=False, persistent=True)
     bad = {k: v for k, v in res.items() if v > 5e-2}
@@ -127,6 +151,8 @@ def test_split_mode_matches_oracle(gpu, monkeypatch):
 
 @pytest.mark.parametrize("persistent,split", [(True, "0"), (True, "1"), (False, "0")])
 def test_rccl_path_world_size_one(gpu, persistent, split, monkeypatch):
+    if split == "1":  # the two-phase mode belongs to the one-workgroup-per-image kernel
+        monkeypatch.setenv("DCA_PKS", "0")
     """comm="rccl" with force_comm at world_size 1: the graph-captured ncclAllReduce (a 1-rank communicator), the
     split-mode stream/event wiring and the averaging SGD kernel all run, and give the same training step as the
     fused-SGD world_size-1 engine (an all-reduce over one rank is the identity)."""
