@@ -18,8 +18,8 @@
 
 #include "netresdeep_kernels.hip"
 #include "netresdeep_persistent.hip"
-#include "netresdeep_pks.hip"
 #include "xgmi_allreduce.hip"
+#include "netresdeep_pks.hip"
 
 namespace {
 
@@ -275,16 +275,28 @@ static int enqueue_step_persistent(Engine* e, int B, int part) {
   Ctx cx = e->base;
   cx.B = B;
   const bool multi = e->comm_on;
-  if (e->sliced && part != 2) {
-    if (e->bf)
-      hipLaunchKernelGGL(pks::k_pks_step<0>, dim3(pks_grid(B)), dim3(pks::NTH), pks::Plan<0>::TOTAL, e->st, cx, e->qa);
-    else
-      hipLaunchKernelGGL(pks::k_pks_step<1>, dim3(pks_grid(B)), dim3(pks::NTH), pks::Plan<1>::TOTAL, e->st, cx, e->qa);
-    hipLaunchKernelGGL(pks::k_pks_reduce, dim3(pk::R_GRID), dim3(256), 0, e->st, cx, e->pa, B * pks::S);
-  }
   if (e->sliced) {
-    if (multi) {
-      if (part == 0 && e->in.comm_mode == 2) return enqueue_xgmi_sgd(e, cx);
+    // step kernel, then ONE kernel for reduction + all-reduce + SGD (mode: see k_pks_reduce_ar)
+    const bool xgmi = multi && e->in.comm_mode == 2;
+    if (xgmi && !e->peers_open) {
+      g_err = "xGMI all-reduce: peers not mapped (call dca_engine_ipc_open first)";
+      return -1;
+    }
+    if (part != 2) {
+      if (e->bf)
+        hipLaunchKernelGGL(pks::k_pks_step<0>, dim3(pks_grid(B)), dim3(pks::NTH), pks::Plan<0>::TOTAL, e->st, cx,
+                           e->qa);
+      else
+        hipLaunchKernelGGL(pks::k_pks_step<1>, dim3(pks_grid(B)), dim3(pks::NTH), pks::Plan<1>::TOTAL, e->st, cx,
+                           e->qa);
+      pks::RedAr ra{};
+      ra.peers = e->peers;
+      ra.err = e->pa.err + 1;
+      ra.deadline = e->ar_deadline;
+      ra.mode = !multi ? 0 : (xgmi ? 2 : 1);
+      hipLaunchKernelGGL(pks::k_pks_reduce_ar, dim3(pks::NSEG), dim3(256), 0, e->st, cx, e->pa, B * pks::S, ra);
+    }
+    if (multi && !xgmi) {  // RCCL (comm_mode 0, captured) or the host (comm_mode 1, between parts 1 and 2)
       if (part == 0) NCCK(ncclAllReduce(cx.grads, cx.grads, FLAT_N, ncclFloat32, ncclSum, e->comm, e->st));
       if (part != 1) hipLaunchKernelGGL(e->kapply, dim3(64), dim3(NT), 0, e->st, cx, 1);
     }
@@ -512,11 +524,13 @@ static int engine_init(Engine* e, const DcaInit* in, int n_indices) {
       return -1;
     }
     // uncached device memory: peers read it over xGMI and no L2 may hold a stale line of it
-    if (hipExtMallocWithFlags((void**)&e->xregion, dca::xg::REGION_BYTES, hipDeviceMallocUncached) != hipSuccess) {
+    // two halves: [0, REGION_BYTES) k_xgmi_ar_sgd (multi-kernel / per-image engines); [REGION_BYTES, 2x) the
+    // sliced engine's fused reduce + all-reduce (own flags and slabs: their epochs never mix)
+    if (hipExtMallocWithFlags((void**)&e->xregion, 2 * dca::xg::REGION_BYTES, hipDeviceMallocUncached) != hipSuccess) {
       (void)hipGetLastError();
-      HIPCK(hipMalloc(&e->xregion, dca::xg::REGION_BYTES));
+      HIPCK(hipMalloc(&e->xregion, 2 * dca::xg::REGION_BYTES));
     }
-    HIPCK(hipMemset(e->xregion, 0, dca::xg::REGION_BYTES));
+    HIPCK(hipMemset(e->xregion, 0, 2 * dca::xg::REGION_BYTES));
     HIPCK(hipDeviceSynchronize());
     const char* dl = getenv("DCA_XGMI_TIMEOUT_S");
     if (dl) e->ar_deadline = (unsigned long long)(atof(dl) * 1e8);
@@ -780,7 +794,20 @@ int dca_engine_ipc_selftest(void* h, const float* src, float* dst, float timeout
   }
   HIPCK(hipMemsetAsync(e->pa.err + 1, 0, sizeof(unsigned), e->st));
   const unsigned long long dl = (unsigned long long)((double)timeout_s * 1e8);
-  if (e->bf)
+  if (e->sliced) {  // the path a sliced training step uses: per-segment exchange inside the fused reduce kernel
+    dca::pks::RedAr ra{};
+    ra.peers = e->peers;
+    ra.peers.ticks = nullptr;
+    ra.err = e->pa.err + 1;
+    ra.deadline = dl;
+    ra.st_src = src;
+    ra.st_dst = dst;
+    ra.st_n = dca::FLAT_N;
+    ra.mode = 3;
+    dca::Ctx cx = e->base;
+    cx.B = 1;
+    hipLaunchKernelGGL(dca::pks::k_pks_reduce_ar, dim3(dca::pks::NSEG), dim3(256), 0, e->st, cx, e->pa, 1, ra);
+  } else if (e->bf)
     hipLaunchKernelGGL(dca::xg::k_xgmi_ar_sgd<true>, dim3(dca::xg::AR_NB), dim3(dca::xg::AR_T), 0, e->st,
                        e->base, e->peers, src, dst, e->pa.err + 1, 0, dl);
   else

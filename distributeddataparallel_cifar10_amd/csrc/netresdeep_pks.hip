@@ -1146,77 +1146,272 @@ __global__ void __launch_bounds__(NTH) k_pks_step(Ctx cx, Args pa) {
   DCA_STAMP(cx, 5, L, 7);
 }
 
+
 // ============================================================================================================
-// Reduction + SGD after the sliced step: the trunk / stem slabs of all B x S workgroups (deterministic order),
-// then the fc gradients and the bookkeeping of netresdeep_persistent.hip (k_pk_reduce's roles).
-// Grid pk::R_GRID x 256.
+// Reduction + gradient all-reduce + SGD in ONE kernel (sliced engine).  Every workgroup owns one segment of the
+// gradient: a chunk of the trunk conv (36 x 256, slab fragment order), of conv1 (5 x 256), a 64-column block
+// of fc1 (32 x 2048) or the small tail (fc1 / fc2 biases, fc2 weight, BN affine, the CC4 running-stat segment;
+// 492 floats).  It reduces its segment over the B x S workgroup slabs (deterministic order), then
+//   mode 0 (world size 1): SGD, fused;
+//   mode 1 (RCCL): writes the gradient only (ncclAllReduce + k_apply_sgd follow in the graph);
+//   mode 2 (xGMI): exchanges THIS segment one-shot with the peers (write-through slab + per-segment flags in the
+//     second half of every rank's IPC region, peers read all W slabs, sum in rank order -- bitwise identical on
+//     every rank), then the averaging SGD: 74 concurrent small all-reduces instead of one all-reduce launch after
+//     the reduction (reference: DDP's single NCCL bucket after the whole backward, main.py:63);
+//   mode 3: the same exchange on a caller pattern (collective self-test of this path).
+// Memory ordering as in xgmi_allreduce.hip (system-coherent stores to uncached memory, s_waitcnt vmcnt(0) +
+// barrier before the flag, cache-bypassing loads; per-segment epochs, slab parity = epoch & 1).
 // ============================================================================================================
-__device__ __forceinline__ void red_trunk_stem(const Ctx& cx, const float* tslab, int bid, int nslab, f32x4* red) {
-  const int t = threadIdx.x;
-  const bool stem = bid >= pk::R_TRUNK;
-  const int chunk = stem ? bid - pk::R_TRUNK : bid;
-  const int slot = t & 63, grp = t >> 6, e0 = chunk * 256 + slot * 4;
-  const float* src = stem ? cx.SSLAB : tslab;
-  const int stride = stem ? SSLAB_N : WSLAB_N, lim = stem ? SSLAB_N : WSLAB_N;
-  int pix[4];
-  float pold[4];
-#pragma unroll
-  for (int ii = 0; ii < 4; ++ii) {
-    const int e = e0 + ii;
-    int pidx = -1;
-    if (e < lim) {
-      if (!stem) {
-        const int tt = e >> 8, ln = (e >> 2) & 63, mt = tt & 1, nt = tt >> 1, tap = nt >> 1, cih = nt & 1;
-        pidx = OFF_CONVW + (16 * mt + 4 * (ln >> 4) + ii) * 288 + (16 * cih + (ln & 15)) * 9 + tap;
-      } else if (e < 1024) {
-        const int tt = e >> 8, ln = (e >> 2) & 63, mt = tt & 1, nt = tt >> 1, k = 16 * nt + (ln & 15);
-        if (k < 27) pidx = OFF_C1W + (16 * mt + 4 * (ln >> 4) + ii) * 27 + k;
-      } else if (e < 1056) {
-        pidx = OFF_C1B + (e - 1024);
-      }
-    }
-    pix[ii] = pidx;
-    pold[ii] = cx.params[pidx >= 0 ? pidx : 0];
-  }
-  f32x4 sacc = z4();
-  const int ec = e0 < lim ? e0 : lim - 4;
-  for (int k0 = 0; k0 < nslab; k0 += 64) {  // 16 slabs per thread in flight, fixed order
-    f32x4 v[16];
-#pragma unroll
-    for (int u = 0; u < 16; ++u) {
-      const int k = k0 + grp + 4 * u;
-      v[u] = ld4(src + (size_t)(k < nslab ? k : nslab - 1) * stride + ec);
-    }
-#pragma unroll
-    for (int u = 0; u < 16; ++u)
-      if (k0 + grp + 4 * u < nslab) sacc += v[u];
-  }
-  red[t] = sacc;
-  __syncthreads();
-  if (t < 64 && e0 < lim) {
-    const f32x4 tot = red[t] + red[64 + t] + red[128 + t] + red[192 + t];
-#pragma unroll
-    for (int ii = 0; ii < 4; ++ii) {
-      const int pidx = pix[ii];
-      if (pidx < 0) continue;
-      const float wv = pk::sgd_put_pre(cx, pidx, tot[ii], pold[ii]);
-      if (cx.fuse_sgd) derive_param<true>(cx, pidx, wv);
-    }
-  }
+constexpr int NSEG = pk::R_TRUNK + pk::R_STEM + pk::R_FC + 1;  // 74
+constexpr int SEG_SMALL_LEN = 492;                            // 32 + 320 + 10 + 64 + 64 (+2 pad)
+static_assert(NSEG <= xg::AR_NB, "one flag per segment");
+__device__ __forceinline__ int seg_off(int b) {
+  return b < 36 ? b * 256 : b < 41 ? 9216 + (b - 36) * 256 : b < 73 ? 10496 + (b - 41) * 2048 : 76032;
+}
+__device__ __forceinline__ int seg_len(int b) { return b < 41 ? 256 : b < 73 ? 2048 : SEG_SMALL_LEN; }
+static_assert(76032 + SEG_SMALL_LEN <= (int)xg::SLAB_FLOATS, "segments fit one slab");
+
+struct RedAr {
+  xg::Peers peers;            // every rank's IPC region; this kernel uses its SECOND half (xg::REGION_BYTES on)
+  unsigned* err;              // bit 31: a peer wait expired
+  unsigned long long deadline;  // s_memrealtime ticks
+  const float* st_src;        // mode 3: the pattern (st_n floats, slab offsets)
+  float* st_dst;
+  int st_n;
+  int mode;
+};
+
+__device__ __forceinline__ char* rbase(const RedAr& ra, int q) { return ra.peers.base[q] + xg::REGION_BYTES; }
+__device__ __forceinline__ float* rslab(const RedAr& ra, int q, int par) {
+  return (float*)(rbase(ra, q) + xg::FLAG_BYTES) + (size_t)par * xg::SLAB_FLOATS;
 }
 
-__global__ void __launch_bounds__(256) k_pks_reduce(Ctx cx, pk::PkArgs pa, int nslab) {
+// one-shot exchange of segment b (segv[0 .. len), len % 4 == 0) with every peer; on return segv holds the sum
+__device__ void seg_exchange(const Ctx& cx, const RedAr& ra, int b, float* segv, int len, int off) {
+  const int t = threadIdx.x, W = cx.ws, me = cx.rank;
+  int* myflags = (int*)rbase(ra, me);
+  __shared__ int s_ep;
+  const unsigned long long t_in = __builtin_amdgcn_s_memrealtime();
+  if (t == 0) s_ep = xg::flag_load(myflags + me * xg::AR_NB + b) + 1;
+  __syncthreads();
+  const int ep = s_ep, par = ep & 1;
+  constexpr int SYS = 17;  // sc0 | sc1: write-through store / cache-bypassing load
+  const __amdgpu_buffer_rsrc_t mine =
+      __builtin_amdgcn_make_buffer_rsrc(rslab(ra, me, par), (short)0, (int)(xg::SLAB_FLOATS * 4), 0x00020000);
+  for (int k = 4 * t; k < len; k += 1024)
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(xg::v4u, *(const f32x4*)(segv + k)), mine,
+                                           4 * (off + k), 0, SYS);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this thread's slab stores are performed
+  __syncthreads();                                    // ... and every thread's
+  if (t < W) xg::flag_store((int*)rbase(ra, t) + me * xg::AR_NB + b, ep);
+  if (t < W) {
+    const int* f = myflags + t * xg::AR_NB + b;
+    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+    while (xg::flag_load(f) < ep) {
+      __builtin_amdgcn_s_sleep(1);
+      if (__builtin_amdgcn_s_memrealtime() - t0 > ra.deadline) {
+        atomicOr(ra.err, 0x80000000u);
+        break;
+      }
+    }
+  }
+  __syncthreads();
+  if (b == 0 && t == 0 && ra.peers.ticks != nullptr) {  // exposed all-reduce time of this rank (metrics)
+    atomicAdd(ra.peers.ticks, __builtin_amdgcn_s_memrealtime() - t_in);
+    atomicAdd(ra.peers.ticks + 1, 1ull);
+  }
+  for (int k = 4 * t; k < len; k += 1024) {
+    f32x4 part[xg::MAXR];
+#pragma unroll
+    for (int q = 0; q < xg::MAXR; ++q) {  // all loads in flight, one per peer link; ranks >= W re-read rank 0
+      const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(rslab(ra, q < W ? q : 0, par), (short)0,
+                                                                          (int)(xg::SLAB_FLOATS * 4), 0x00020000);
+      part[q] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, 4 * (off + k), 0, SYS));
+    }
+    f32x4 sum = part[0];
+#pragma unroll
+    for (int q = 1; q < xg::MAXR; ++q) sum += q < W ? part[q] : z4();
+    *(f32x4*)(segv + k) = sum;
+  }
+  __syncthreads();
+}
+
+__global__ void __launch_bounds__(256) k_pks_reduce_ar(Ctx cx, pk::PkArgs pa, int nslab, RedAr ra) {
+  __shared__ __attribute__((aligned(16))) float segv[2048];
+  __shared__ int segp[2048];  // parameter index; -1 none; -2 - k: CC4 running-stat slot k
   __shared__ f32x4 red[256];
   __shared__ float stage[64 * 32 + 64 * 64];
-  const int bid = blockIdx.x;
-  if (bid < pk::R_TRUNK + pk::R_STEM) {
-    red_trunk_stem(cx, pa.tslab, bid, nslab, red);
-  } else if (bid < pk::R_TRUNK + pk::R_STEM + pk::R_FC) {
-    pk::pk_red_fc1(cx, bid - pk::R_TRUNK - pk::R_STEM, stage);
-  } else {
-    pk::pk_red_fc_small(cx, stage);
+  const int b = blockIdx.x, t = threadIdx.x, B = cx.B;
+  const int len = seg_len(b), off = seg_off(b);
+  const int mode = ra.mode;
+  if (mode == 3) {
+    for (int k = t; k < len; k += 256) {
+      segv[k] = off + k < ra.st_n ? ra.st_src[off + k] : 0.f;
+      segp[k] = -1;
+    }
+  } else if (b < pk::R_TRUNK + pk::R_STEM) {
+    // trunk / stem chunk: 256 outputs in slab fragment order, summed over the nslab workgroup slabs
+    const bool stem = b >= pk::R_TRUNK;
+    const int chunk = stem ? b - pk::R_TRUNK : b;
+    const int slot = t & 63, grp = t >> 6, e0 = chunk * 256 + slot * 4;
+    const float* src = stem ? cx.SSLAB : pa.tslab;
+    const int stride = stem ? SSLAB_N : WSLAB_N, lim = stem ? SSLAB_N : WSLAB_N;
+    f32x4 sacc = z4();
+    const int ec = e0 < lim ? e0 : lim - 4;
+    for (int k0 = 0; k0 < nslab; k0 += 64) {  // 16 slabs per thread in flight, fixed order
+      f32x4 v[16];
+#pragma unroll
+      for (int u = 0; u < 16; ++u) {
+        const int k = k0 + grp + 4 * u;
+        v[u] = ld4(src + (size_t)(k < nslab ? k : nslab - 1) * stride + ec);
+      }
+#pragma unroll
+      for (int u = 0; u < 16; ++u)
+        if (k0 + grp + 4 * u < nslab) sacc += v[u];
+    }
+    red[t] = sacc;
     __syncthreads();
-    pk::pk_bookkeeping(cx, pa, (float*)red);
+    if (t < 64) {
+      const f32x4 tot = red[t] + red[64 + t] + red[128 + t] + red[192 + t];
+#pragma unroll
+      for (int ii = 0; ii < 4; ++ii) {
+        const int e = e0 + ii;
+        int pidx = -1;
+        if (e < lim) {
+          if (!stem) {
+            const int tt = e >> 8, ln = (e >> 2) & 63, mt = tt & 1, nt = tt >> 1, tap = nt >> 1, cih = nt & 1;
+            pidx = OFF_CONVW + (16 * mt + 4 * (ln >> 4) + ii) * 288 + (16 * cih + (ln & 15)) * 9 + tap;
+          } else if (e < 1024) {
+            const int tt = e >> 8, ln = (e >> 2) & 63, mt = tt & 1, nt = tt >> 1, k = 16 * nt + (ln & 15);
+            if (k < 27) pidx = OFF_C1W + (16 * mt + 4 * (ln >> 4) + ii) * 27 + k;
+          } else if (e < 1056) {
+            pidx = OFF_C1B + (e - 1024);
+          }
+        }
+        segv[slot * 4 + ii] = e < lim ? tot[ii] : 0.f;
+        segp[slot * 4 + ii] = pidx;
+      }
+    }
+  } else if (b < NSEG - 1) {
+    // fc1 block f: dW1[j][64f + kk .. +7] = sum_b dh[b][j] p[b][k]
+    const int f = b - pk::R_TRUNK - pk::R_STEM;
+    float* dh_s = stage;           // [B][32]
+    float* p_s = stage + 64 * 32;  // [B][64]
+    const int j = t >> 3, kk = 8 * (t & 7);
+    f32x4 dh4[2], p4[4];
+#pragma unroll
+    for (int m = 0; m < 2; ++m) {
+      const int idx = t + 256 * m;
+      dh4[m] = ld4(cx.HDH + 4 * (idx < B * 8 ? idx : 0));
+    }
+#pragma unroll
+    for (int m = 0; m < 4; ++m) {
+      const int idx = t + 256 * m, ic = idx < B * 16 ? idx : 0, bb = ic >> 4, k4 = ic & 15;
+      p4[m] = ld4(cx.HP + (size_t)bb * 2048 + 64 * f + 4 * k4);
+    }
+#pragma unroll
+    for (int m = 0; m < 2; ++m)
+      if (t + 256 * m < B * 8) st4(dh_s + 4 * (t + 256 * m), dh4[m]);
+#pragma unroll
+    for (int m = 0; m < 4; ++m)
+      if (t + 256 * m < B * 16) st4(p_s + 4 * (t + 256 * m), p4[m]);
+    __syncthreads();
+    f32x4 a0 = z4(), a1 = z4();
+#pragma unroll 8
+    for (int bb = 0; bb < B; ++bb) {
+      const float dh = dh_s[bb * 32 + j];
+      a0 += dh * ld4(p_s + bb * 64 + kk);
+      a1 += dh * ld4(p_s + bb * 64 + kk + 4);
+    }
+    const int lo = j * 64 + kk, pb = OFF_FC1W + j * 2048 + 64 * f + kk;
+    st4(segv + lo, a0);
+    st4(segv + lo + 4, a1);
+#pragma unroll
+    for (int ii = 0; ii < 8; ++ii) segp[lo + ii] = pb + ii;
+  } else {
+    // small tail: fc1 bias [0,32), fc2 weight [32,352), fc2 bias [352,362), BN gamma|beta [362,426),
+    // CC4 running mean|var [426,490) (rank 0's buffers; the others contribute 0), pad
+    float* hh_s = stage;            // [B][32]
+    float* dl_s = stage + 64 * 32;  // [B][16]
+    float* dh_s = dl_s + 64 * 16;   // [B][32]
+    for (int idx = t; idx < B * 32; idx += 256) {
+      hh_s[idx] = cx.HH[idx];
+      dh_s[idx] = cx.HDH[idx];
+    }
+    for (int idx = t; idx < B * 10; idx += 256) dl_s[(idx / 10) * 16 + idx % 10] = cx.HDL[idx];
+    __syncthreads();
+    for (int idx = t; idx < SEG_SMALL_LEN; idx += 256) {
+      float sv = 0.f;
+      int pidx = -1;
+      if (idx < 32) {
+#pragma unroll 8
+        for (int bb = 0; bb < B; ++bb) sv += dh_s[bb * 32 + idx];
+        pidx = OFF_FC1B + idx;
+      } else if (idx < 352) {
+        const int o = (idx - 32) >> 5, jj = (idx - 32) & 31;
+#pragma unroll 8
+        for (int bb = 0; bb < B; ++bb) sv += dl_s[bb * 16 + o] * hh_s[bb * 32 + jj];
+        pidx = OFF_FC2W + o * 32 + jj;
+      } else if (idx < 362) {
+        const int o = idx - 352;
+#pragma unroll 8
+        for (int bb = 0; bb < B; ++bb) sv += dl_s[bb * 16 + o];
+        pidx = OFF_FC2B + o;
+      } else if (idx < 426) {
+        const int k = idx - 362;  // 0..31 dgamma, 32..63 dbeta
+        sv = pa.bng[k];
+        pidx = (k < 32 ? OFF_BNW : OFF_BNB) + (k & 31);
+      } else if (idx < 490) {
+        const int k = idx - 426;
+        sv = cx.rank == 0 ? (k < 32 ? cx.rm[k] : cx.rv[k - 32]) : 0.f;
+        pidx = -2 - k;
+      }
+      segv[idx] = sv;
+      segp[idx] = pidx;
+    }
+  }
+  __syncthreads();
+  if (mode >= 2) seg_exchange(cx, ra, b, segv, len, off);
+  for (int k = t; k < len; k += 256) {
+    const int pidx = segp[k];
+    const float g = segv[k];
+    if (mode == 3) {
+      if (off + k < ra.st_n) ra.st_dst[off + k] = g;
+      continue;
+    }
+    if (pidx >= 0) {
+      cx.grads[pidx] = g;
+      if (mode == 1) continue;
+      const float oldp = cx.params[pidx];
+      float wv;
+      if (mode == 0) {
+        wv = __builtin_fmaf(-cx.lr, g, oldp);
+      } else {
+        wv = oldp;
+        wv -= cx.lr * g * cx.inv_ws;  // same rounding as k_apply_sgd / k_xgmi_ar_sgd
+      }
+      cx.params[pidx] = wv;
+      derive_param<true>(cx, pidx, wv);
+    } else if (pidx <= -2) {  // CC4: rank 0's running stats become every rank's base (rides the all-reduce)
+      const int kk = -2 - pidx;
+      if (mode == 1) cx.grads[OFF_RS + kk] = g;
+      else if (mode == 2) cx.rs_base[kk] = g;
+    }
+  }
+  if (b == NSEG - 1 && mode != 3) {  // bookkeeping
+    __syncthreads();
+    float* lred = (float*)red;
+    lred[t] = t < B ? cx.HLOSS[t] : 0.f;
+    __syncthreads();
+    if (t == 0) {
+      float sl = 0.f;
+      for (int k = 0; k < B; ++k) sl += lred[k];
+      *cx.loss_acc += (double)(sl / (float)B);
+      *cx.cursor += B;
+      *cx.step_count += 1;
+      *cx.nbt += NBLK;  // BatchNorm num_batches_tracked: +1 per application
+      *pa.epoch += 1;
+    }
   }
 }
 
