@@ -280,9 +280,9 @@ __device__ __forceinline__ bool sweep_eval(const v4u (&x)[KS], int wv, int lane,
 __device__ __forceinline__ void sleep_units(int n) {
   for (int k = 0; k < n; ++k) __builtin_amdgcn_s_sleep(1);  // 64 cycles each
 }
-// One pass in flight, re-issued as soon as it fails.  (Two staggered passes in flight were measured slower:
-// 103.6 vs 95.9 us per step at batch 32 -- the polling traffic of 128 workgroups, not the round trip, is what
-// the exchange waits on; profiles/bench_poll_r2.log.)
+// One full pass in flight, re-issued as soon as it fails.  Measured alternatives (profiles/bench_poll_r2.log):
+// two staggered full passes in flight 103.6 vs 95.9 us per step (more polling traffic); polling one sentinel
+// granule per workgroup between full passes 100.6 vs 98.1 (one more round trip).
 template <int KS>
 __device__ __forceinline__ void sweep_wait(const Args& pa, int round, int wv, int lane, int G, unsigned tag,
                                            float& s0, float& s1) {
