@@ -5,24 +5,26 @@ all-reduce launched from gradient hooks so it overlaps the backward) + FlatSGD (
 bf16 autocast.  Prints one JSON line (whole-job images/sec, slowest rank).
 
     python bench/resnet50.py [--batch 256] [--steps 30] [--warmup 5]
+    python bench/resnet50.py --gpus 8                      # spawns 8 ranks itself (reference main.py:80-85)
+    python bench/resnet50.py --sweep 1,2,4,8               # one fresh rank group per N + scaling efficiency
     python -m torch.distributed.run --nproc-per-node 8 --master-addr 127.0.0.1 bench/resnet50.py --gpus 8
+    python bench/resnet50.py --path torch                  # stock PyTorch (MIOpen convs, channels_last, autocast)
+The parent of a self-launch never touches the GPU (ranks are spawned before any HIP call).
 """
 from __future__ import annotations
 
 import argparse
 import json
 import os
+import socket
 import sys
+import tempfile
 import time
-
-import torch
-import torch.distributed as dist
-import torch.nn.functional as F
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 
-def main() -> int:
+def _args(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--batch", type=int, default=256, help="per-rank batch (288 GB HBM per GPU: large per-GPU batches)")
@@ -45,7 +47,26 @@ def main() -> int:
     ap.add_argument("--infer", action="store_true",
                     help="inference (serving) throughput: eval-mode forward under no_grad, BN with the running "
                          "statistics (ops path: k_bn_eval_stats + k_bn_apply), no backward / optimizer")
-    a = ap.parse_args()
+    ap.add_argument("--channels-last", type=int, default=1,
+                    help="torch path: model and input in channels_last (NHWC) memory format")
+    ap.add_argument("--sweep", default=None, metavar="N1,N2,..",
+                    help="run each N in a fresh spawned rank group; print per-N lines and a scaling summary")
+    ap.add_argument("--result-file", default=None, help=argparse.SUPPRESS)
+    return ap.parse_args(argv)
+
+
+def _free_port() -> int:
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def run_rank(a) -> None:
+    """One rank (rank / world from the launcher env)."""
+    import torch
+    import torch.distributed as dist
+    import torch.nn.functional as F
+
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -58,13 +79,22 @@ def main() -> int:
     from distributeddataparallel_cifar10_amd.parallel.flat_ddp import FlatBucketDDP, FlatSGD
     torch.manual_seed(rank)
     model = resnet50().to(dev)
+    cl = a.path == "torch" and bool(a.channels_last)
+    if cl:
+        model = model.to(memory_format=torch.channels_last)
     if a.path == "ops":
         from distributeddataparallel_cifar10_amd.ops import OpsModel, cross_entropy
         model = OpsModel(model, fp8=a.fp8)
-    ddp = FlatBucketDDP(model, bucket_cap_mb=a.bucket_mb, first_bucket_mb=1.0)
-    opt = FlatSGD(ddp, lr=0.1, momentum=0.9, overlap=bool(a.overlap_sgd))
+    if a.path == "torch":  # stock PyTorch end to end: torch DDP + torch.optim.SGD
+        ddp = torch.nn.parallel.DistributedDataParallel(model, device_ids=[local])
+        opt = torch.optim.SGD(model.parameters(), lr=0.1, momentum=0.9)
+    else:
+        ddp = FlatBucketDDP(model, bucket_cap_mb=a.bucket_mb, first_bucket_mb=1.0)
+        opt = FlatSGD(ddp, lr=0.1, momentum=0.9, overlap=bool(a.overlap_sgd))
     g = torch.Generator(device=dev).manual_seed(1234 + rank)
     x = torch.randn(a.batch, 3, a.image, a.image, device=dev, generator=g)
+    if cl:
+        x = x.contiguous(memory_format=torch.channels_last)
     y = torch.randint(0, 1000, (a.batch,), device=dev, generator=g)
     amp = torch.autocast("cuda", dtype=torch.bfloat16, enabled=a.dtype == "bf16" and a.path == "torch")
     ce = cross_entropy if a.path == "ops" else F.cross_entropy
@@ -125,9 +155,57 @@ def main() -> int:
                                      (", per-bucket updates overlapped with the backward" if a.overlap_sgd else ""),
                                      "path": (("eval-mode forward, ops HIP kernels" if a.infer else "FlatBucketDDP + ops HIP kernels") + (" (fp8 fwd GEMMs)" if a.fp8 else " (bf16)")
                                               + (", step replayed as a HIP graph" if a.graph else ""))
-                                     if a.path == "ops" else "FlatBucketDDP + stock conv (MIOpen), bf16 autocast"}}),
+                                     if a.path == "ops" else "stock PyTorch: torch DDP + MIOpen convs + torch.optim.SGD, bf16 autocast" +
+                                     (", channels_last" if cl else ", NCHW")}}),
               flush=True)
+        if a.result_file:
+            with open(a.result_file, "w") as f:
+                json.dump({"value": v, "ms_per_step": round(1e3 * dt / a.steps, 3)}, f)
     dist.destroy_process_group()
+
+
+def _spawned(local_rank: int, world: int, port: int, argv: list) -> None:
+    os.environ.update({"RANK": str(local_rank), "LOCAL_RANK": str(local_rank), "WORLD_SIZE": str(world),
+                       "LOCAL_WORLD_SIZE": str(world), "MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port)})
+    run_rank(_args(argv))
+
+
+def main() -> int:
+    argv = sys.argv[1:]
+    a = _args(argv)
+    if a.sweep:
+        import torch.multiprocessing as mp
+        i = argv.index("--sweep")
+        rest = argv[:i] + argv[i + 2:]
+        res = {}
+        for n in [int(x) for x in a.sweep.split(",")]:
+            with tempfile.NamedTemporaryFile(suffix=".json", delete=False) as f:
+                path = f.name
+            mp.spawn(_spawned, args=(n, _free_port(), rest + ["--gpus", str(n), "--result-file", path]), nprocs=n,
+                     join=True)
+            with open(path) as f:
+                res[n] = json.load(f)
+            os.unlink(path)
+        n0 = min(res)
+        base = res[n0]["value"] / n0
+        print(json.dumps({"metric": "images/sec (whole node) ResNet-50 synthetic 3x224x224 DDP",
+                          "sweep": {str(n): round(r["value"], 1) for n, r in res.items()},
+                          "scaling_efficiency": {str(n): round(r["value"] / (n * base), 4) for n, r in res.items()},
+                          "ms_per_step": {str(n): r["ms_per_step"] for n, r in res.items()}}), flush=True)
+        return 0
+    if "WORLD_SIZE" in os.environ:  # started by torch.distributed.run
+        if int(os.environ["WORLD_SIZE"]) != a.gpus:
+            print(f"resnet50.py: --gpus {a.gpus} but the launcher started {os.environ['WORLD_SIZE']} ranks",
+                  file=sys.stderr)
+            return 2
+        run_rank(a)
+        return 0
+    if a.gpus == 1:
+        os.environ.setdefault("WORLD_SIZE", "1")
+        run_rank(a)
+        return 0
+    import torch.multiprocessing as mp
+    mp.spawn(_spawned, args=(a.gpus, _free_port(), argv), nprocs=a.gpus, join=True)
     return 0
 
 

@@ -537,6 +537,11 @@ __device__ __forceinline__ void glds16(const void* src, char* lds_wave_base) {
   __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
                                    (__attribute__((address_space(3))) void*)lds_wave_base, 16, 0, 0);
 }
+// 16 B per lane from a buffer descriptor straight into LDS (wave-linear at lds_wave_base); an offset past the
+// descriptor's range loads zeros
+__device__ __forceinline__ void blds16(__amdgpu_buffer_rsrc_t rs, char* lds_wave_base, unsigned voff, unsigned soff) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (__attribute__((address_space(3))) void*)lds_wave_base, 16, voff, soff, 0, 0);
+}
 template <int N>
 __device__ __forceinline__ void wait_vmcnt() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
@@ -588,7 +593,103 @@ __global__ void __launch_bounds__(NW * 64) k_gemm_glds(GemmArgs g) {
   const int kb_end = k_end * ESZ;
 
   const bool c64 = g.conv == 1 && g.cC % KT == 0;
+
+  // Fast path (plain K-contiguous operands, or the implicit conv with C % 64 == 0): buffer_load ... lds with the
+  // per-lane byte offsets computed once here, so a K-tile costs one add per load (plus, for the conv, a tap
+  // validity test against a per-row mask) and the tap / channel position advances without divisions.  The
+  // profile of the general path (profiles/gemm_pmc_r2.txt): ~7 VALU and ~8 SALU per MFMA on the 3x3 conv, the
+  // issue bound of that kernel.  Out-of-range lanes (rows past M / N, padding taps, the K tail) get an offset
+  // past the descriptor's range, which loads zeros.
+  constexpr unsigned OOB = 0x80000000u;
+  const long long a_bytes = g.conv == 1 ? (long long)g.cN * g.cH * g.cW * g.cC * ESZ
+                                        : ((long long)(g.M - 1) * g.lda + g.K) * ESZ;
+  const long long b_bytes = ((long long)(g.N - 1) * g.ldb + g.K) * ESZ;
+  const int ntaps = g.cKH * g.cKW;
+  const bool fast = a_bytes < OOB && b_bytes < OOB && (g.conv == 0 || (c64 && ntaps <= 32));
+  const __amdgpu_buffer_rsrc_t ars = __builtin_amdgcn_make_buffer_rsrc((void*)g.A, (short)0, (int)(fast ? a_bytes : 0),
+                                                                       0x00020000);
+  const __amdgpu_buffer_rsrc_t brs = __builtin_amdgcn_make_buffer_rsrc((void*)g.B, (short)0, (int)(fast ? b_bytes : 0),
+                                                                       0x00020000);
+  unsigned aoff[NAI], amask[NAI], boff[NBI];
+  int s_tap = 0, s_kh = 0, s_kw = 0, s_c0b = 0, s_tapoff = 0;  // conv: position of the next tile to issue
+  if (fast) {
+#pragma unroll
+    for (int i = 0; i < NAI; ++i) {
+      const int r = wave * RA + i * 8 + lr, m = m0 + r;
+      const unsigned cb = (unsigned)(lj ^ ((r >> 1) & 7)) << 4;
+      if (g.conv == 1) {
+        amask[i] = 0u;
+        aoff[i] = 0u;
+        if (m < g.M) {
+          const int ow = m % g.cWo, t = m / g.cWo, oh = t % g.cHo, n = t / g.cHo;
+          const int ih0 = oh * g.cS - g.cP, iw0 = ow * g.cS - g.cP;
+          const long long ro = (((long long)n * g.cH + ih0) * g.cW + iw0) * g.cC * ESZ;
+          aoff[i] = (unsigned)(ro + cb);  // wraps for padding rows; only used when the tap is valid
+          for (int kh = 0; kh < g.cKH; ++kh)
+            for (int kw = 0; kw < g.cKW; ++kw)
+              if (ih0 + kh >= 0 && ih0 + kh < g.cH && iw0 + kw >= 0 && iw0 + kw < g.cW) amask[i] |= 1u << (kh * g.cKW + kw);
+        }
+      } else {
+        aoff[i] = m < g.M ? (unsigned)((long long)m * g.lda * ESZ) + cb : OOB;
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < NBI; ++i) {
+      const int r = wave * RB + i * 8 + lr, n = n0 + r;
+      boff[i] = n < g.N ? (unsigned)((long long)n * g.ldb * ESZ) + ((unsigned)(lj ^ ((r >> 1) & 7)) << 4) : OOB;
+    }
+    if (g.conv == 1) {
+      s_tap = k_begin / g.cC;
+      s_c0b = (k_begin - s_tap * g.cC) * ESZ;
+      s_kh = s_tap / g.cKW;
+      s_kw = s_tap - s_kh * g.cKW;
+      s_tapoff = (s_kh * g.cW + s_kw) * g.cC * ESZ;
+    }
+  }
+  auto lane_cb = [&](int r) { return (int)((unsigned)(lj ^ ((r >> 1) & 7)) << 4); };
+  auto issue_fast = [&](int kt, int buf) {
+    const int kb0 = (k_begin + kt * KT) * ESZ;
+    const bool tail = kb_end - kb0 < GBK_BYTES;  // (uniform) the last, partial K-tile
+    char* la = smem + buf * T::BUF;
+    char* lb = la + G_TILE_BYTES;
+    if (g.conv == 1) {
+      const unsigned sadd = (unsigned)(s_tapoff + s_c0b), bit = 1u << s_tap;
+#pragma unroll
+      for (int i = 0; i < NAI; ++i) {
+        bool ok = (amask[i] & bit) != 0u;
+        if (tail) ok = ok && kb0 + lane_cb(wave * RA + i * 8 + lr) < kb_end;
+        blds16(ars, la + (wave * RA + i * 8) * 128, ok ? aoff[i] + sadd : OOB, 0u);
+      }
+      s_c0b += GBK_BYTES;
+      if (s_c0b == g.cC * ESZ) {
+        s_c0b = 0;
+        ++s_tap;
+        if (++s_kw == g.cKW) {
+          s_kw = 0;
+          ++s_kh;
+        }
+        s_tapoff = (s_kh * g.cW + s_kw) * g.cC * ESZ;
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < NAI; ++i) {
+        unsigned v = aoff[i];
+        if (tail && kb0 + lane_cb(wave * RA + i * 8 + lr) >= kb_end) v = OOB;
+        blds16(ars, la + (wave * RA + i * 8) * 128, v, (unsigned)kb0);
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < NBI; ++i) {
+      unsigned v = boff[i];
+      if (tail && kb0 + lane_cb(wave * RB + i * 8 + lr) >= kb_end) v = OOB;
+      blds16(brs, lb + (wave * RB + i * 8) * 128, v, (unsigned)kb0);
+    }
+  };
   auto issue = [&](int kt, int buf) {
+    if (fast) {
+      issue_fast(kt, buf);
+      return;
+    }
     const int kb0 = (k_begin + kt * KT) * ESZ;
     char* la = smem + buf * T::BUF;
     char* lb = la + G_TILE_BYTES;
