@@ -1236,19 +1236,49 @@ __device__ void seg_exchange(const Ctx& cx, const RedAr& ra, int b, float* segv,
   __syncthreads();
 }
 
+// parameter index of element k of segment b: >= 0 a parameter; -1 none; -2 - k: CC4 running-stat slot k
+__device__ __forceinline__ int seg_pidx(const Ctx& cx, int b, int k) {
+  if (b < pk::R_TRUNK + pk::R_STEM) {  // slab fragment order
+    const bool stem = b >= pk::R_TRUNK;
+    const int e = (stem ? b - pk::R_TRUNK : b) * 256 + k, ii = k & 3;
+    if (e >= (stem ? SSLAB_N : WSLAB_N)) return -1;
+    const int tt = e >> 8, ln = (e >> 2) & 63, mt = tt & 1, nt = tt >> 1;
+    if (!stem) return OFF_CONVW + (16 * mt + 4 * (ln >> 4) + ii) * 288 + (16 * (nt & 1) + (ln & 15)) * 9 + (nt >> 1);
+    if (e < 1024) {
+      const int kk = 16 * nt + (ln & 15);
+      return kk < 27 ? OFF_C1W + (16 * mt + 4 * (ln >> 4) + ii) * 27 + kk : -1;
+    }
+    return e < 1056 ? OFF_C1B + (e - 1024) : -1;
+  }
+  if (b < NSEG - 1) return OFF_FC1W + (k >> 6) * 2048 + 64 * (b - pk::R_TRUNK - pk::R_STEM) + (k & 63);
+  if (k < 32) return OFF_FC1B + k;
+  if (k < 352) return OFF_FC2W + ((k - 32) >> 5) * 32 + ((k - 32) & 31);
+  if (k < 362) return OFF_FC2B + (k - 352);
+  if (k < 426) return ((k - 362) < 32 ? OFF_BNW : OFF_BNB) + ((k - 362) & 31);
+  if (k < 490) return -2 - (k - 426);
+  return -1;
+}
+
 __global__ void __launch_bounds__(256) k_pks_reduce_ar(Ctx cx, pk::PkArgs pa, int nslab, RedAr ra) {
   __shared__ __attribute__((aligned(16))) float segv[2048];
-  __shared__ int segp[2048];  // parameter index; -1 none; -2 - k: CC4 running-stat slot k
   __shared__ f32x4 red[256];
   __shared__ float stage[64 * 32 + 64 * 64];
   const int b = blockIdx.x, t = threadIdx.x, B = cx.B;
   const int len = seg_len(b), off = seg_off(b);
   const int mode = ra.mode;
+  // this thread's SGD elements (k = t + 256 i): parameter indices and old values loaded first, so their latency
+  // hides under the slab reduction (a dependent read after it cost 1.5 us per step)
+  constexpr int KMAX = 2048 / 256;
+  int pid[KMAX];
+  float pold[KMAX];
+#pragma unroll
+  for (int i = 0; i < KMAX; ++i) {
+    const int k = t + 256 * i;
+    pid[i] = k < len && mode != 3 ? seg_pidx(cx, b, k) : -1;
+    pold[i] = cx.params[pid[i] >= 0 ? pid[i] : 0];
+  }
   if (mode == 3) {
-    for (int k = t; k < len; k += 256) {
-      segv[k] = off + k < ra.st_n ? ra.st_src[off + k] : 0.f;
-      segp[k] = -1;
-    }
+    for (int k = t; k < len; k += 256) segv[k] = off + k < ra.st_n ? ra.st_src[off + k] : 0.f;
   } else if (b < pk::R_TRUNK + pk::R_STEM) {
     // trunk / stem chunk: 256 outputs in slab fragment order, summed over the nslab workgroup slabs
     const bool stem = b >= pk::R_TRUNK;
@@ -1274,23 +1304,7 @@ __global__ void __launch_bounds__(256) k_pks_reduce_ar(Ctx cx, pk::PkArgs pa, in
     if (t < 64) {
       const f32x4 tot = red[t] + red[64 + t] + red[128 + t] + red[192 + t];
 #pragma unroll
-      for (int ii = 0; ii < 4; ++ii) {
-        const int e = e0 + ii;
-        int pidx = -1;
-        if (e < lim) {
-          if (!stem) {
-            const int tt = e >> 8, ln = (e >> 2) & 63, mt = tt & 1, nt = tt >> 1, tap = nt >> 1, cih = nt & 1;
-            pidx = OFF_CONVW + (16 * mt + 4 * (ln >> 4) + ii) * 288 + (16 * cih + (ln & 15)) * 9 + tap;
-          } else if (e < 1024) {
-            const int tt = e >> 8, ln = (e >> 2) & 63, mt = tt & 1, nt = tt >> 1, k = 16 * nt + (ln & 15);
-            if (k < 27) pidx = OFF_C1W + (16 * mt + 4 * (ln >> 4) + ii) * 27 + k;
-          } else if (e < 1056) {
-            pidx = OFF_C1B + (e - 1024);
-          }
-        }
-        segv[slot * 4 + ii] = e < lim ? tot[ii] : 0.f;
-        segp[slot * 4 + ii] = pidx;
-      }
+      for (int ii = 0; ii < 4; ++ii) segv[slot * 4 + ii] = e0 + ii < lim ? tot[ii] : 0.f;
     }
   } else if (b < NSEG - 1) {
     // fc1 block f: dW1[j][64f + kk .. +7] = sum_b dh[b][j] p[b][k]
@@ -1323,11 +1337,9 @@ __global__ void __launch_bounds__(256) k_pks_reduce_ar(Ctx cx, pk::PkArgs pa, in
       a0 += dh * ld4(p_s + bb * 64 + kk);
       a1 += dh * ld4(p_s + bb * 64 + kk + 4);
     }
-    const int lo = j * 64 + kk, pb = OFF_FC1W + j * 2048 + 64 * f + kk;
+    const int lo = j * 64 + kk;
     st4(segv + lo, a0);
     st4(segv + lo + 4, a1);
-#pragma unroll
-    for (int ii = 0; ii < 8; ++ii) segp[lo + ii] = pb + ii;
   } else {
     // small tail: fc1 bias [0,32), fc2 weight [32,352), fc2 bias [352,362), BN gamma|beta [362,426),
     // CC4 running mean|var [426,490) (rank 0's buffers; the others contribute 0), pad
@@ -1340,40 +1352,35 @@ __global__ void __launch_bounds__(256) k_pks_reduce_ar(Ctx cx, pk::PkArgs pa, in
     }
     for (int idx = t; idx < B * 10; idx += 256) dl_s[(idx / 10) * 16 + idx % 10] = cx.HDL[idx];
     __syncthreads();
-    for (int idx = t; idx < SEG_SMALL_LEN; idx += 256) {
+    for (int idx = t; idx < SEG_SMALL_LEN; idx += 256) {  // (parameter indices: seg_pidx)
       float sv = 0.f;
-      int pidx = -1;
       if (idx < 32) {
 #pragma unroll 8
         for (int bb = 0; bb < B; ++bb) sv += dh_s[bb * 32 + idx];
-        pidx = OFF_FC1B + idx;
       } else if (idx < 352) {
         const int o = (idx - 32) >> 5, jj = (idx - 32) & 31;
 #pragma unroll 8
         for (int bb = 0; bb < B; ++bb) sv += dl_s[bb * 16 + o] * hh_s[bb * 32 + jj];
-        pidx = OFF_FC2W + o * 32 + jj;
       } else if (idx < 362) {
         const int o = idx - 352;
 #pragma unroll 8
         for (int bb = 0; bb < B; ++bb) sv += dl_s[bb * 16 + o];
-        pidx = OFF_FC2B + o;
       } else if (idx < 426) {
-        const int k = idx - 362;  // 0..31 dgamma, 32..63 dbeta
-        sv = pa.bng[k];
-        pidx = (k < 32 ? OFF_BNW : OFF_BNB) + (k & 31);
+        sv = pa.bng[idx - 362];  // 0..31 dgamma, 32..63 dbeta
       } else if (idx < 490) {
         const int k = idx - 426;
         sv = cx.rank == 0 ? (k < 32 ? cx.rm[k] : cx.rv[k - 32]) : 0.f;
-        pidx = -2 - k;
       }
       segv[idx] = sv;
-      segp[idx] = pidx;
     }
   }
   __syncthreads();
   if (mode >= 2) seg_exchange(cx, ra, b, segv, len, off);
-  for (int k = t; k < len; k += 256) {
-    const int pidx = segp[k];
+#pragma unroll
+  for (int i = 0; i < KMAX; ++i) {
+    const int k = t + 256 * i;
+    if (k >= len) break;
+    const int pidx = pid[i];
     const float g = segv[k];
     if (mode == 3) {
       if (off + k < ra.st_n) ra.st_dst[off + k] = g;
@@ -1382,7 +1389,7 @@ __global__ void __launch_bounds__(256) k_pks_reduce_ar(Ctx cx, pk::PkArgs pa, in
     if (pidx >= 0) {
       cx.grads[pidx] = g;
       if (mode == 1) continue;
-      const float oldp = cx.params[pidx];
+      const float oldp = pold[i];
       float wv;
       if (mode == 0) {
         wv = __builtin_fmaf(-cx.lr, g, oldp);
