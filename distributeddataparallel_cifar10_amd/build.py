@@ -52,8 +52,13 @@ def _sources():
     return sorted(os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith((".hip", ".h", ".cpp")))
 
 
+def _extra(variant: str) -> list:
+    """Diagnostic builds only: extra hipcc flags from DCA_HIPCC_EXTRA (e.g. -DDCA_DETAIL_FWD=9 for the stamps)."""
+    return os.environ.get("DCA_HIPCC_EXTRA", "").split() if variant == "stamps" else []
+
+
 def _digest(variant: str = "") -> str:
-    h = hashlib.sha256((ARCH + "|" + variant).encode())
+    h = hashlib.sha256((ARCH + "|" + variant + "|" + " ".join(_extra(variant))).encode())
     extra = [_ENTRY["micro"][0]] if variant == "micro" else []
     for p in _sources() + extra:
         with open(p, "rb") as f:
@@ -75,7 +80,7 @@ def build(force: bool = False, verbose: bool = False, variant: str = "") -> str:
     tmp = out + f".tmp{os.getpid()}"
     cmd = [
         _hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
-        "-Wall", "-Wno-unused-function", "-Wno-unused-variable", *VARIANTS[variant],
+        "-Wall", "-Wno-unused-function", "-Wno-unused-variable", *VARIANTS[variant], *_extra(variant),
         os.path.join(CSRC, _ENTRY[variant][0] if variant in _ENTRY else "engine.hip"), "-o", tmp,
         *([] if variant in _ENTRY else ["-lrccl"]),
     ]

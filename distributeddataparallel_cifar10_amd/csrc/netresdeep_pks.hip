@@ -29,6 +29,13 @@
 // main.py:27-39 (SGD, CrossEntropy mean), BatchNorm2d training statistics + 10 running-stat EMAs per forward.
 
 namespace dca {
+// stamps build: which forward / backward block gets the detailed stamps (slots 6 / 7)
+#ifndef DCA_DETAIL_FWD
+#define DCA_DETAIL_FWD 5
+#endif
+#ifndef DCA_DETAIL_BWD
+#define DCA_DETAIL_BWD 5
+#endif
 namespace pks {
 
 constexpr int S = 4;                   // workgroups (row slices) per image
@@ -460,6 +467,28 @@ __device__ __forceinline__ void wstage_store(const WStage<P>& ws, char* wt) {
     }
 }
 
+// fc1 slice of slice s: 32 rows x 512 local features (u = ch*16 + pr*8 + pw <-> global ch*64 + (2s + pr)*8 + pw),
+// row j at w1l + j * W1S elements; one lane-linear 1 KB LDS-DMA per bf16 row (P=0) / half f32 row (P=1)
+template <int P>
+__device__ __forceinline__ void w1_dma(const Ctx& cx, char* w1l, int s, int wv, int lane) {
+  constexpr int IPR = P == 1 ? 2 : 1, NI = 32 * IPR / NW;
+#pragma unroll
+  for (int m = 0; m < NI; ++m) {
+    const int ins = wv * NI + m, j = ins / IPR, h = ins % IPR;
+    const void* src;
+    if constexpr (P == 1) {
+      const int u = 256 * h + 4 * lane;
+      src = cx.params + OFF_FC1W + j * 2048 + (u >> 4) * 64 + (2 * s + ((u >> 3) & 1)) * 8 + (u & 7);
+    } else {
+      const int u = 8 * lane;
+      src = (const unsigned short*)cx.w1b + j * 2048 + (u >> 4) * 64 + (2 * s + ((u >> 3) & 1)) * 8;
+    }
+    __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
+                                     (__attribute__((address_space(3))) void*)(w1l + j * Plan<P>::W1S * (P == 1 ? 4 : 2) + h * 1024),
+                                     16, 0, 0);
+  }
+}
+
 constexpr int P_KSHIFT = 906;  // misc: [10][32] BN shifts (last step's batch means)
 constexpr int P_LABEL = 1240;  // misc: this image's label
 
@@ -662,12 +691,10 @@ __global__ void __launch_bounds__(NTH) k_pks_step(Ctx cx, Args pa) {
 
   // ======================= forward: 10 applications of the shared ResBlock ===================================
   // fc1 weights of this slice's 512 pooled features (local index u = ch*16 + pr*8 + pw <-> global feature
-  // ch*64 + (2s + pr)*8 + pw: per row, 32 runs of 16 contiguous elements): loaded into registers at block 6 (the
-  // exchange waits hide the latency), stored at block 7 into their LDS region (unused by the forward), read by
+  // ch*64 + (2s + pr)*8 + pw: per row, 32 runs of 16 contiguous elements): copied into their LDS region (unused by
+  // the forward) by LDS-DMA right after block 6's exchange, read by
   // fc1 (reduction over features) and its transpose dp (reduction over rows).  The dgrad weights are prefetched
   // at block 8 and staged into WT at the head.
-  constexpr int W1M = P == 1 ? 4096 / NTH : 2048 / NTH;  // 16-B chunks per thread
-  uint4 w1r[W1M];
   WStage<P> wst_d;  // dgrad weights, staged into WT during the head
 #pragma unroll 1
   for (int i = 0; i < NBLK; ++i) {
@@ -676,7 +703,7 @@ __global__ void __launch_bounds__(NTH) k_pks_step(Ctx cx, Args pa) {
 #pragma unroll
       for (int i2 = 0; i2 < 4; ++i2) y[i2] = acc[i2];
     }
-    if (i == 5) DCA_STAMP(cx, 6, L, 0);
+    if (i == DCA_DETAIL_FWD) DCA_STAMP(cx, 6, L, 0);
     // shifted one-pass sums S1 = sum(y - K), S2 = sum((y - K)^2); K = this block's batch mean of the previous
     // step (0 at the first), identical in every workgroup, so the partials combine exactly
     const float K = misc[P_KSHIFT + i * 32 + ch];
@@ -693,27 +720,17 @@ __global__ void __launch_bounds__(NTH) k_pks_step(Ctx cx, Args pa) {
     if (halo) publish_row(pa, i, L, hwhich, hh, tag, y, lane);
     // meanwhile: this block's y for the backward / diagnostics
     st4r(cx.Y + (size_t)i * B * 8192 + img8, hh, lane, y);
-    if (i == NBLK - 4) {
-      // chunk k = t + NTH m: row j, run ch, piece pc (P=1: 4 pieces of 4 floats, P=0: 2 of 8 bf16)
-#pragma unroll
-      for (int m = 0; m < W1M; ++m) {
-        const int k = t + NTH * m;
-        if constexpr (P == 1) {
-          const int j = k >> 7, chh = (k >> 2) & 31, pc = k & 3;
-          w1r[m] = *(const uint4*)(cx.params + OFF_FC1W + j * 2048 + chh * 64 + 16 * s + 4 * pc);
-        } else {
-          const int j = k >> 6, chh = (k >> 1) & 31, pc = k & 1;
-          w1r[m] = *(const uint4*)((const unsigned short*)cx.w1b + j * 2048 + chh * 64 + 16 * s + 8 * pc);
-        }
-      }
-    }
     if (i == NBLK - 2) wstage_prefetch<P>(wst_d, pkw + 18432);  // dgrad weights [tap'][ci][co] (hi, lo)
     float yo[4];
-    if (i == 5) DCA_STAMP(cx, 6, L, 1);
+    if (i == DCA_DETAIL_FWD) DCA_STAMP(cx, 6, L, 1);
     xchg_wait(pa, i, epoch, G, cred, halo, hsrc, hwhich ^ 1, hh, yo);
-    if (i == 5) DCA_STAMP(cx, 6, L, 2);
+    if (i == DCA_DETAIL_FWD) DCA_STAMP(cx, 6, L, 2);
+    // the fc1 slice for the head, straight into its LDS region (free during the forward) by LDS-DMA, issued right
+    // AFTER an exchange: vmcnt is in order, so loads in flight when a sweep starts hold up its first pass (register
+    // loads before the exchange + an LDS store a block later cost ~1.4 us in each of the two blocks, stamps)
+    if (i == NBLK - 4) w1_dma<P>(cx, U + PL::U_W1, s, wv, lane);
     lds_barrier();
-    if (i == 5) DCA_STAMP(cx, 6, L, 3);
+    if (i == DCA_DETAIL_FWD) DCA_STAMP(cx, 6, L, 3);
     if (halo) st4r(pa.yh + ((size_t)(i * LMAX + L) * 2 + hwhich) * 512, hh, lane, yo);
     // every thread finalises the statistics of its own channel (same sums, same order everywhere)
     const float S1 = slot_total(cred, ch), S2 = slot_total(cred, 32 + ch);
@@ -736,20 +753,6 @@ __global__ void __launch_bounds__(NTH) k_pks_step(Ctx cx, Args pa) {
         if (i == NBLK - 1) {
           cx.rm[ch] = misc[448 + ch];
           cx.rv[ch] = misc[480 + ch];
-        }
-      }
-    }
-    if (i == NBLK - 3) {  // the fc1 slice into LDS (its region is free during the forward)
-      char* w1l = U + PL::U_W1;
-#pragma unroll
-      for (int m = 0; m < W1M; ++m) {
-        const int k = t + NTH * m;
-        if constexpr (P == 1) {
-          const int j = k >> 7, chh = (k >> 2) & 31, pc = k & 3;
-          *(uint4*)(w1l + (j * PL::W1S + chh * 16 + 4 * pc) * 4) = w1r[m];
-        } else {
-          const int j = k >> 6, chh = (k >> 1) & 31, pc = k & 1;
-          *(uint4*)(w1l + (j * PL::W1S + chh * 16 + 8 * pc) * 2) = w1r[m];
         }
       }
     }
@@ -964,15 +967,15 @@ __global__ void __launch_bounds__(NTH) k_pks_step(Ctx cx, Args pa) {
     }
     const int rnd = RND_HEAD + 1 + (NBLK - 1 - i);
     const unsigned tag = tagof(epoch, rnd);
-    if (i == 5) DCA_STAMP(cx, 7, L, 0);
+    if (i == DCA_DETAIL_BWD) DCA_STAMP(cx, 7, L, 0);
     const float pv = wg_csum(sa, sbv, cred);
     if (t < 64) gput(gslot(pa, rnd, L) + t, tag, pv);
     if (halo) publish_row(pa, rnd, L, hwhich, hh, tag, dz, lane);
-    if (i == 5) DCA_STAMP(cx, 7, L, 1);
+    if (i == DCA_DETAIL_BWD) DCA_STAMP(cx, 7, L, 1);
     // while the exchange is in flight: the weight gradient of the PREVIOUS application (block i + 1), whose dy /
     // x tiles are still staged; then the barrier retires every wave's reads of them before x_i replaces them
     if (i < NBLK - 1) wgrad_acc<P>(dyT, xT, wacc, wv, lane);
-    if (i == 5) DCA_STAMP(cx, 7, L, 2);
+    if (i == DCA_DETAIL_BWD) DCA_STAMP(cx, 7, L, 2);
     if (i > 0) {  // prefetch y_{i-1}; lands while this block's exchange and convolutions run
       ld4r(cx.Y + (size_t)(i - 1) * B * 8192 + img8, hh, lane, yv);
     } else {      // last block: what the stem backward needs (pool codes, raw input words, next batch's image)
@@ -989,12 +992,12 @@ __global__ void __launch_bounds__(NTH) k_pks_step(Ctx cx, Args pa) {
     xt_row<P>(xT, w + 1, q, ch, x);
     if (halo) xt_row<P>(xT, hxrow, q, ch, xo);
     float dzo[4];
-    if (i == 5) DCA_STAMP(cx, 7, L, 3);
+    if (i == DCA_DETAIL_BWD) DCA_STAMP(cx, 7, L, 3);
     xchg_wait(pa, rnd, epoch, G, cred, halo, hsrc, hwhich ^ 1, hh, dzo);
-    if (i == 5) DCA_STAMP(cx, 7, L, 4);
+    if (i == DCA_DETAIL_BWD) DCA_STAMP(cx, 7, L, 4);
     if (halo && i > 0) ld4r(pa.yh + ((size_t)((i - 1) * LMAX + L) * 2 + hwhich) * 512, hh, lane, yo);
     lds_barrier();
-    if (i == 5) DCA_STAMP(cx, 7, L, 5);
+    if (i == DCA_DETAIL_BWD) DCA_STAMP(cx, 7, L, 5);
     if (L == 0 && t < 32) {  // BN affine gradients: dbeta = sum dz, dgamma = sum dz * xhat
       dbet += slot_total(cred, t);
       dgam += slot_total(cred, 32 + t);
@@ -1029,7 +1032,7 @@ __global__ void __launch_bounds__(NTH) k_pks_step(Ctx cx, Args pa) {
       st4r(cx.X + (size_t)i * B * 8192 + img8, hh, lane, x);
     }
     lds_barrier();
-    if (i == 5) DCA_STAMP(cx, 7, L, 6);
+    if (i == DCA_DETAIL_BWD) DCA_STAMP(cx, 7, L, 6);
     // dgrad: g_i = g_{i+1} + conv(dy, W^T flipped)
     {
       const f32x4 acc = conv_row<P>(XR, WT, w, hh, lane);
