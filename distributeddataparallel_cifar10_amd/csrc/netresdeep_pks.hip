@@ -718,13 +718,12 @@ __global__ void __launch_bounds__(NTH) k_pks_step(Ctx cx, Args pa) {
     const unsigned tag = tagof(epoch, i);
     if (t < 64) gput(gslot(pa, i, L) + t, tag, pv);
     if (halo) publish_row(pa, i, L, hwhich, hh, tag, y, lane);
-    // meanwhile: this block's y for the backward / diagnostics
-    st4r(cx.Y + (size_t)i * B * 8192 + img8, hh, lane, y);
     if (i == NBLK - 2) wstage_prefetch<P>(wst_d, pkw + 18432);  // dgrad weights [tap'][ci][co] (hi, lo)
     float yo[4];
     if (i == DCA_DETAIL_FWD) DCA_STAMP(cx, 6, L, 1);
     xchg_wait(pa, i, epoch, G, cred, halo, hsrc, hwhich ^ 1, hh, yo);
     if (i == DCA_DETAIL_FWD) DCA_STAMP(cx, 6, L, 2);
+    st4r(cx.Y + (size_t)i * B * 8192 + img8, hh, lane, y);  // this block's y for the backward (after the sweep)
     // the fc1 slice for the head, straight into its LDS region (free during the forward) by LDS-DMA, issued right
     // AFTER an exchange: vmcnt is in order, so loads in flight when a sweep starts hold up its first pass (register
     // loads before the exchange + an LDS store a block later cost ~1.4 us in each of the two blocks, stamps)
@@ -976,7 +975,16 @@ __global__ void __launch_bounds__(NTH) k_pks_step(Ctx cx, Args pa) {
     // x tiles are still staged; then the barrier retires every wave's reads of them before x_i replaces them
     if (i < NBLK - 1) wgrad_acc<P>(dyT, xT, wacc, wv, lane);
     if (i == DCA_DETAIL_BWD) DCA_STAMP(cx, 7, L, 2);
-    if (i > 0) {  // prefetch y_{i-1}; lands while this block's exchange and convolutions run
+    lds_barrier();
+    xt_row<P>(xT, w + 1, q, ch, x);
+    if (halo) xt_row<P>(xT, hxrow, q, ch, xo);
+    float dzo[4];
+    if (i == DCA_DETAIL_BWD) DCA_STAMP(cx, 7, L, 3);
+    xchg_wait(pa, rnd, epoch, G, cred, halo, hsrc, hwhich ^ 1, hh, dzo);
+    if (i == DCA_DETAIL_BWD) DCA_STAMP(cx, 7, L, 4);
+    // loads for the next block, issued AFTER the exchange (vmcnt is in order: a load in flight when a sweep
+    // starts holds up its first pass); they land during this block's dgrad
+    if (i > 0) {  // y_{i-1}
       ld4r(cx.Y + (size_t)(i - 1) * B * 8192 + img8, hh, lane, yv);
     } else {      // last block: what the stem backward needs (pool codes, raw input words, next batch's image)
       codew = *(const unsigned*)(cx.SCODE + img8 + hh * 256 + lane * 4);
@@ -988,13 +996,6 @@ __global__ void __launch_bounds__(NTH) k_pks_step(Ctx cx, Args pa) {
       if (t < 48) nxt = ((const uint4*)(cx.data + (size_t)next_id * 3072 + 768 * s))[t];
       if (t == 48) nxt_lab = cx.labels[next_id];
     }
-    lds_barrier();
-    xt_row<P>(xT, w + 1, q, ch, x);
-    if (halo) xt_row<P>(xT, hxrow, q, ch, xo);
-    float dzo[4];
-    if (i == DCA_DETAIL_BWD) DCA_STAMP(cx, 7, L, 3);
-    xchg_wait(pa, rnd, epoch, G, cred, halo, hsrc, hwhich ^ 1, hh, dzo);
-    if (i == DCA_DETAIL_BWD) DCA_STAMP(cx, 7, L, 4);
     if (halo && i > 0) ld4r(pa.yh + ((size_t)((i - 1) * LMAX + L) * 2 + hwhich) * 512, hh, lane, yo);
     lds_barrier();
     if (i == DCA_DETAIL_BWD) DCA_STAMP(cx, 7, L, 5);
