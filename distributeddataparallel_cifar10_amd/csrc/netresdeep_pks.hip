@@ -775,6 +775,7 @@ __global__ void __launch_bounds__(NTH) k_pks_step(Ctx cx, Args pa) {
   // image exchange their partials -> fc1 + ReLU, fc2, cross-entropy (mean over the batch) and their backward
   // (every slice, redundantly) -> dp = W1^T dh for this slice's features -> max-pool backward -> g = dL/dx10.
   float g[4];
+  float yv[4], yo[4] = {};  // y_i of this row / of the halo row (backward)
   {
     float* x10 = (float*)(U + PL::U_X10);
     uint8_t* pcode = (uint8_t*)(U + PL::U_PCODE);
@@ -810,6 +811,10 @@ __global__ void __launch_bounds__(NTH) k_pks_step(Ctx cx, Args pa) {
       *(float2*)(cx.HP + (size_t)n * 2048 + pch * 64 + (2 * s + pr) * 8 + 2 * (t & 3)) = make_float2(pv[0], pv[1]);
     }
     lds_barrier();
+    // block 9's y for the first backward block, loaded now: the fc1 partial below hides the latency (the head
+    // exchange is polled by wave 0 only, after that)
+    ld4r(cx.Y + (size_t)(NBLK - 1) * B * 8192 + img8, hh, lane, yv);
+    if (halo) ld4r(pa.yh + ((size_t)((NBLK - 1) * LMAX + L) * 2 + hwhich) * 512, hh, lane, yo);
     // fc1 partial over this slice's features: thread (row j = t >> 4, part k = t & 15) sums features u = 16m + k,
     // then 4 xor-shuffles over the 16 parts (fixed order: identical in every workgroup)
     {
@@ -935,9 +940,6 @@ __global__ void __launch_bounds__(NTH) k_pks_step(Ctx cx, Args pa) {
 #pragma unroll
   for (int j = 0; j < NNT; ++j) wacc[j][0] = wacc[j][1] = z4();
   float dgam = 0.f, dbet = 0.f;
-  float yv[4], yo[4] = {};  // y_i of this row / of the halo row
-  ld4r(cx.Y + (size_t)(NBLK - 1) * B * 8192 + img8, hh, lane, yv);
-  if (halo) ld4r(pa.yh + ((size_t)((NBLK - 1) * LMAX + L) * 2 + hwhich) * 512, hh, lane, yo);
   unsigned codew = 0;  // stem-backward prefetch (during block 0)
   unsigned imgw = 0;
   uint4 nxt = uint4{0u, 0u, 0u, 0u};
