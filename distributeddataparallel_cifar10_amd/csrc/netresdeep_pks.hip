@@ -1162,19 +1162,23 @@ __global__ void __launch_bounds__(NTH) k_pks_step(Ctx cx, Args pa) {
 //   mode 1 (RCCL): writes the gradient only (ncclAllReduce + k_apply_sgd follow in the graph);
 //   mode 2 (xGMI): exchanges THIS segment one-shot with the peers (write-through slab + per-segment flags in the
 //     second half of every rank's IPC region, peers read all W slabs, sum in rank order -- bitwise identical on
-//     every rank), then the averaging SGD: 74 concurrent small all-reduces instead of one all-reduce launch after
+//     every rank), then the averaging SGD: 106 concurrent small all-reduces instead of one all-reduce launch after
 //     the reduction (reference: DDP's single NCCL bucket after the whole backward, main.py:63);
 //   mode 3: the same exchange on a caller pattern (collective self-test of this path).
 // Memory ordering as in xgmi_allreduce.hip (system-coherent stores to uncached memory, s_waitcnt vmcnt(0) +
 // barrier before the flag, cache-bypassing loads; per-segment epochs, slab parity = epoch & 1).
 // ============================================================================================================
-constexpr int NSEG = pk::R_TRUNK + pk::R_STEM + pk::R_FC + 1;  // 74
-constexpr int SEG_SMALL_LEN = 492;                            // 32 + 320 + 10 + 64 + 64 (+2 pad)
-static_assert(NSEG <= xg::AR_NB, "one flag per segment");
+// segments: 36 trunk + 5 stem chunks of 256, fc1 as 64 blocks of 16 rows x 64 features (1024), one small tail.
+// 106 workgroups: each reads one float4 per peer per thread at most (one round of xGMI loads in flight)
+constexpr int R_FC1 = 2 * pk::R_FC;
+constexpr int NSEG = pk::R_TRUNK + pk::R_STEM + R_FC1 + 1;  // 106
+constexpr int SEG_SMALL_LEN = 492;                         // 32 + 320 + 10 + 64 + 64 (+2 pad)
+constexpr int SEG_MAX = 1024;
+static_assert((size_t)NSEG * xg::MAXR * 4 <= xg::FLAG_BYTES, "one flag per segment and rank");
 __device__ __forceinline__ int seg_off(int b) {
-  return b < 36 ? b * 256 : b < 41 ? 9216 + (b - 36) * 256 : b < 73 ? 10496 + (b - 41) * 2048 : 76032;
+  return b < 36 ? b * 256 : b < 41 ? 9216 + (b - 36) * 256 : b < 105 ? 10496 + (b - 41) * 1024 : 76032;
 }
-__device__ __forceinline__ int seg_len(int b) { return b < 41 ? 256 : b < 73 ? 2048 : SEG_SMALL_LEN; }
+__device__ __forceinline__ int seg_len(int b) { return b < 41 ? 256 : b < 105 ? 1024 : SEG_SMALL_LEN; }
 static_assert(76032 + SEG_SMALL_LEN <= (int)xg::SLAB_FLOATS, "segments fit one slab");
 
 struct RedAr {
@@ -1198,7 +1202,7 @@ __device__ void seg_exchange(const Ctx& cx, const RedAr& ra, int b, float* segv,
   int* myflags = (int*)rbase(ra, me);
   __shared__ int s_ep;
   const unsigned long long t_in = __builtin_amdgcn_s_memrealtime();
-  if (t == 0) s_ep = xg::flag_load(myflags + me * xg::AR_NB + b) + 1;
+  if (t == 0) s_ep = xg::flag_load(myflags + me * NSEG + b) + 1;
   __syncthreads();
   const int ep = s_ep, par = ep & 1;
   constexpr int SYS = 17;  // sc0 | sc1: write-through store / cache-bypassing load
@@ -1209,9 +1213,9 @@ __device__ void seg_exchange(const Ctx& cx, const RedAr& ra, int b, float* segv,
                                            4 * (off + k), 0, SYS);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this thread's slab stores are performed
   __syncthreads();                                    // ... and every thread's
-  if (t < W) xg::flag_store((int*)rbase(ra, t) + me * xg::AR_NB + b, ep);
+  if (t < W) xg::flag_store((int*)rbase(ra, t) + me * NSEG + b, ep);
   if (t < W) {
-    const int* f = myflags + t * xg::AR_NB + b;
+    const int* f = myflags + t * NSEG + b;
     const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
     while (xg::flag_load(f) < ep) {
       __builtin_amdgcn_s_sleep(1);
@@ -1256,7 +1260,10 @@ __device__ __forceinline__ int seg_pidx(const Ctx& cx, int b, int k) {
     }
     return e < 1056 ? OFF_C1B + (e - 1024) : -1;
   }
-  if (b < NSEG - 1) return OFF_FC1W + (k >> 6) * 2048 + 64 * (b - pk::R_TRUNK - pk::R_STEM) + (k & 63);
+  if (b < NSEG - 1) {
+    const int fb = b - pk::R_TRUNK - pk::R_STEM;  // fc1 block: features 64 (fb >> 1) .., rows 16 (fb & 1) ..
+    return OFF_FC1W + (16 * (fb & 1) + (k >> 6)) * 2048 + 64 * (fb >> 1) + (k & 63);
+  }
   if (k < 32) return OFF_FC1B + k;
   if (k < 352) return OFF_FC2W + ((k - 32) >> 5) * 32 + ((k - 32) & 31);
   if (k < 362) return OFF_FC2B + (k - 352);
@@ -1266,7 +1273,7 @@ __device__ __forceinline__ int seg_pidx(const Ctx& cx, int b, int k) {
 }
 
 __global__ void __launch_bounds__(256) k_pks_reduce_ar(Ctx cx, pk::PkArgs pa, int nslab, RedAr ra) {
-  __shared__ __attribute__((aligned(16))) float segv[2048];
+  __shared__ __attribute__((aligned(16))) float segv[SEG_MAX];
   __shared__ f32x4 red[256];
   __shared__ float stage[64 * 32 + 64 * 64];
   const int b = blockIdx.x, t = threadIdx.x, B = cx.B;
@@ -1274,7 +1281,7 @@ __global__ void __launch_bounds__(256) k_pks_reduce_ar(Ctx cx, pk::PkArgs pa, in
   const int mode = ra.mode;
   // this thread's SGD elements (k = t + 256 i): parameter indices and old values loaded first, so their latency
   // hides under the slab reduction (a dependent read after it cost 1.5 us per step)
-  constexpr int KMAX = 2048 / 256;
+  constexpr int KMAX = SEG_MAX / 256;
   int pid[KMAX];
   float pold[KMAX];
 #pragma unroll
@@ -1313,11 +1320,11 @@ __global__ void __launch_bounds__(256) k_pks_reduce_ar(Ctx cx, pk::PkArgs pa, in
       for (int ii = 0; ii < 4; ++ii) segv[slot * 4 + ii] = e0 + ii < lim ? tot[ii] : 0.f;
     }
   } else if (b < NSEG - 1) {
-    // fc1 block f: dW1[j][64f + kk .. +7] = sum_b dh[b][j] p[b][k]
-    const int f = b - pk::R_TRUNK - pk::R_STEM;
+    // fc1 block: dW1[j][64f + kk .. +3] = sum_b dh[b][j] p[b][64f + kk ..], rows j = 16 h .. 16 h + 15
+    const int fb = b - pk::R_TRUNK - pk::R_STEM, f = fb >> 1, j0 = 16 * (fb & 1);
     float* dh_s = stage;           // [B][32]
     float* p_s = stage + 64 * 32;  // [B][64]
-    const int j = t >> 3, kk = 8 * (t & 7);
+    const int jl = t >> 4, kk = 4 * (t & 15);
     f32x4 dh4[2], p4[4];
 #pragma unroll
     for (int m = 0; m < 2; ++m) {
@@ -1336,16 +1343,10 @@ __global__ void __launch_bounds__(256) k_pks_reduce_ar(Ctx cx, pk::PkArgs pa, in
     for (int m = 0; m < 4; ++m)
       if (t + 256 * m < B * 16) st4(p_s + 4 * (t + 256 * m), p4[m]);
     __syncthreads();
-    f32x4 a0 = z4(), a1 = z4();
+    f32x4 a0 = z4();
 #pragma unroll 8
-    for (int bb = 0; bb < B; ++bb) {
-      const float dh = dh_s[bb * 32 + j];
-      a0 += dh * ld4(p_s + bb * 64 + kk);
-      a1 += dh * ld4(p_s + bb * 64 + kk + 4);
-    }
-    const int lo = j * 64 + kk;
-    st4(segv + lo, a0);
-    st4(segv + lo + 4, a1);
+    for (int bb = 0; bb < B; ++bb) a0 += dh_s[bb * 32 + j0 + jl] * ld4(p_s + bb * 64 + kk);
+    st4(segv + jl * 64 + kk, a0);
   } else {
     // small tail: fc1 bias [0,32), fc2 weight [32,352), fc2 bias [352,362), BN gamma|beta [362,426),
     // CC4 running mean|var [426,490) (rank 0's buffers; the others contribute 0), pad

@@ -57,3 +57,19 @@ def test_bench_one_rank_per_gpu(gpu, port, allreduce):
     assert len(lines) == 1, r.stdout
     out = json.loads(lines[0])
     assert out["n_gpus"] == n and out["allreduce"] == allreduce and out["loss_finite"]
+
+
+@needs2
+def test_resnet50_bench_self_launch(gpu):
+    """bench/resnet50.py --gpus N spawns one rank per GPU itself (FlatBucketDDP over xGMI, ops kernels); small
+    batch / image so it finishes quickly."""
+    n = min(_ngpu(), 8)
+    cmd = [sys.executable, "bench/resnet50.py", "--gpus", str(n), "--batch", "16", "--image", "64", "--steps", "3",
+           "--warmup", "1"]
+    r = subprocess.run(cmd, cwd=ROOT, env=dict(os.environ, DCA_XGMI_TIMEOUT_S="60"), capture_output=True, text=True,
+                       timeout=600)
+    assert r.returncode == 0, r.stderr[-4000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    out = json.loads(lines[0])
+    assert out["n_gpus"] == n and out["value"] > 0 and out["loss"] == out["loss"]

@@ -74,7 +74,10 @@ def test_quantize_fp8_and_scaled_gemm(gpu):
 
 @pytest.mark.parametrize("n,h,c,co,k,s,p,bias", [(2, 16, 32, 32, 3, 1, 1, False), (3, 32, 3, 32, 3, 1, 1, True),
                                                   (2, 14, 16, 24, 7, 2, 3, False), (2, 9, 64, 48, 1, 2, 0, False),
-                                                  (4, 8, 64, 128, 1, 1, 0, False), (2, 10, 3, 16, 3, 2, 1, False)])
+                                                  (4, 8, 64, 128, 1, 1, 0, False), (2, 10, 3, 16, 3, 2, 1, False),
+                                                  # C % 64 == 0 3x3: the implicit-conv buffer-load fast path (padding
+                                                  # taps, a partial last M tile; stride 1 dgrad runs it too)
+                                                  (2, 12, 64, 64, 3, 1, 1, False), (2, 13, 128, 64, 3, 2, 1, False)])
 def test_conv2d_fwd_bwd(gpu, n, h, c, co, k, s, p, bias):
     from distributeddataparallel_cifar10_amd.ops import conv2d
     g = torch.Generator(device=gpu).manual_seed(n * h + c)
