@@ -241,6 +241,17 @@ __device__ __forceinline__ int xcd_remap(int orig, int nwg) {
   return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (orig >> 3);
 }
 
+// (tm, tn) of the t-th tile in grouped order: bands of GROUP tile rows, column-major inside a band, so the tiles
+// one XCD runs together (consecutive t after xcd_remap) cover a compact block of C: with 32 x 32 tiles an XCD's
+// 64 co-resident tiles share 8 A row-tiles and 8 B column-tiles instead of 2 and 32
+constexpr int TILE_GROUP = 8;
+__device__ __forceinline__ void tile_coords(int t, int ntm, int ntn, int& tm, int& tn) {
+  const int per = TILE_GROUP * ntn, band = t / per, first = band * TILE_GROUP;
+  const int rows = ntm - first < TILE_GROUP ? ntm - first : TILE_GROUP, r = t - band * per;
+  tm = first + r % rows;
+  tn = r / rows;
+}
+
 template <int BN_>
 struct GemmTile {
   static constexpr int B_BYTES = BN_ * GBK_BYTES;              // B tile per buffer
@@ -413,7 +424,8 @@ __global__ void __launch_bounds__(GT) k_gemm(GemmArgs g) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int ntm = (g.M + GBM - 1) / GBM, ntn = (g.N + BN_ - 1) / BN_;
   const int tile = xcd_remap(blockIdx.x, ntm * ntn);
-  const int tm = tile / ntn, tn = tile % ntn;
+  int tm, tn;
+  tile_coords(tile, ntm, ntn, tm, tn);
   const int m0 = tm * GBM, n0 = tn * BN_;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, wr = wave >> 1, wc = wave & 1;
   constexpr int ESZ = FP8 ? 1 : 2;
@@ -555,7 +567,8 @@ __global__ void __launch_bounds__(NW * 64) k_gemm_glds(GemmArgs g) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int ntm = (g.M + GBM - 1) / GBM, ntn = (g.N + BN_ - 1) / BN_;
   const int tile = xcd_remap(blockIdx.x, ntm * ntn);
-  const int tm = tile / ntn, tn = tile % ntn;
+  int tm, tn;
+  tile_coords(tile, ntm, ntn, tm, tn);
   const int m0 = tm * GBM, n0 = tn * BN_;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, wr = wave / Wg::WC, wc = wave % Wg::WC;
   constexpr int ESZ = FP8 ? 1 : 2;
