@@ -130,7 +130,7 @@ using namespace dca::ops;
 extern "C" {
 
 const char* dca_ops_last_error() { return g_err.c_str(); }
-int dca_ops_abi_version() { return 6; }
+int dca_ops_abi_version() { return 7; }
 
 // Must match ops/_native.py::GemmArgs.
 int dca_ops_gemm(const GemmArgs* a, void* stream) {
@@ -159,6 +159,10 @@ int dca_ops_gemm(const GemmArgs* a, void* stream) {
     REQUIRE(g.conv != 2 || (g.K == pix && g.N == kc && !g.tb), "gemm: conv B shape mismatch");
   }
   REQUIRE(!g.col_stats || (g.stats_shift && g.splits <= 1), "gemm: column stats need a shift and no split-K");
+  REQUIRE(!g.bnb_part || (g.bnb_x && g.bnb_stats && g.bnb_gamma && g.bnb_beta && !g.col_stats && g.splits <= 1 &&
+                          g.out_bf16 && g.N % 8 == 0 && g.ldc % 8 == 0 && g.wperm_T <= 0 && !g.fp8),
+          "gemm: fused BN-backward statistics need a bf16 output with N % 8 == 0 and no split-K");
+  REQUIRE(!g.bnb_part || (g.beta == 0.f && !g.bias && !g.relu), "gemm: fused BN-backward statistics: plain output");
   REQUIRE(g.orow_S <= 0 || (g.splits <= 1 && g.wperm_T <= 0 && g.orow_Ho > 0 && g.orow_Wo > 0 &&
                             (long)g.orow_Ho * g.orow_Wo > 0 && g.M % ((long)g.orow_Ho * g.orow_Wo) == 0 &&
                             g.orow_S * (g.orow_Ho - 1) + g.orow_ph < g.orow_H &&
@@ -171,6 +175,10 @@ int dca_ops_gemm(const GemmArgs* a, void* stream) {
                              GemmTile<128>::LDS));
     OPCK(hipFuncSetAttribute((const void*)k_gemm<false, 64>, hipFuncAttributeMaxDynamicSharedMemorySize,
                              GemmTile<64>::LDS));
+    OPCK(hipFuncSetAttribute((const void*)k_gemm<false, 128, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                             GemmTile<128>::LDS));
+    OPCK(hipFuncSetAttribute((const void*)k_gemm<false, 64, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                             GemmTile<64>::LDS));
     OPCK(hipFuncSetAttribute((const void*)k_gemm<true, 64>, hipFuncAttributeMaxDynamicSharedMemorySize,
                              GemmTile<64>::LDS));
     {
@@ -182,7 +190,10 @@ int dca_ops_gemm(const GemmArgs* a, void* stream) {
       OPCK(hipFuncSetAttribute((const void*)k_wgrad<128, 128, 2>, hipFuncAttributeMaxDynamicSharedMemorySize, l11));
 #define GLDS_ATTR(F8, BNV, NWV)                                                                          \
   OPCK(hipFuncSetAttribute((const void*)k_gemm_glds<F8, BNV, NWV>, hipFuncAttributeMaxDynamicSharedMemorySize, \
-                           4 * GemmTile<BNV>::BUF))
+                           4 * GemmTile<BNV>::BUF));                                                          \
+  if (!F8)                                                                                                   \
+    OPCK(hipFuncSetAttribute((const void*)k_gemm_glds<false, BNV, NWV, true>,                               \
+                             hipFuncAttributeMaxDynamicSharedMemorySize, 4 * GemmTile<BNV>::BUF))
       GLDS_ATTR(false, 128, 4);
       GLDS_ATTR(true, 128, 4);
       GLDS_ATTR(false, 64, 4);
@@ -264,6 +275,9 @@ int dca_ops_gemm(const GemmArgs* a, void* stream) {
       if (g.fp8) {
         if (w8) hipLaunchKernelGGL((k_gemm_glds<true, 64, 8>), grid, blk, l64, st, g);
         else hipLaunchKernelGGL((k_gemm_glds<true, 64, 4>), grid, blk, l64, st, g);
+      } else if (g.bnb_part) {
+        if (w8) hipLaunchKernelGGL((k_gemm_glds<false, 64, 8, true>), grid, blk, l64, st, g);
+        else hipLaunchKernelGGL((k_gemm_glds<false, 64, 4, true>), grid, blk, l64, st, g);
       } else {
         if (w8) hipLaunchKernelGGL((k_gemm_glds<false, 64, 8>), grid, blk, l64, st, g);
         else hipLaunchKernelGGL((k_gemm_glds<false, 64, 4>), grid, blk, l64, st, g);
@@ -272,6 +286,9 @@ int dca_ops_gemm(const GemmArgs* a, void* stream) {
       if (g.fp8) {
         if (w8) hipLaunchKernelGGL((k_gemm_glds<true, 128, 8>), grid, blk, l128, st, g);
         else hipLaunchKernelGGL((k_gemm_glds<true, 128, 4>), grid, blk, l128, st, g);
+      } else if (g.bnb_part) {
+        if (w8) hipLaunchKernelGGL((k_gemm_glds<false, 128, 8, true>), grid, blk, l128, st, g);
+        else hipLaunchKernelGGL((k_gemm_glds<false, 128, 4, true>), grid, blk, l128, st, g);
       } else {
         if (w8) hipLaunchKernelGGL((k_gemm_glds<false, 128, 8>), grid, blk, l128, st, g);
         else hipLaunchKernelGGL((k_gemm_glds<false, 128, 4>), grid, blk, l128, st, g);
@@ -280,10 +297,12 @@ int dca_ops_gemm(const GemmArgs* a, void* stream) {
   } else if (narrow) {
     const int lds = g.single ? GemmTile<64>::LDS_SINGLE : GemmTile<64>::LDS;
     if (g.fp8) hipLaunchKernelGGL((k_gemm<true, 64>), grid, dim3(GT), lds, st, g);
+    else if (g.bnb_part) hipLaunchKernelGGL((k_gemm<false, 64, true>), grid, dim3(GT), lds, st, g);
     else hipLaunchKernelGGL((k_gemm<false, 64>), grid, dim3(GT), lds, st, g);
   } else {
     const int lds = g.single ? GemmTile<128>::LDS_SINGLE : GemmTile<128>::LDS;
     if (g.fp8) hipLaunchKernelGGL((k_gemm<true, 128>), grid, dim3(GT), lds, st, g);
+    else if (g.bnb_part) hipLaunchKernelGGL((k_gemm<false, 128, true>), grid, dim3(GT), lds, st, g);
     else hipLaunchKernelGGL((k_gemm<false, 128>), grid, dim3(GT), lds, st, g);
   }
   if (g.splits > 1 || g.wperm_T > 0)
@@ -390,6 +409,23 @@ int dca_ops_bn_bwd(const void* dy, const void* x, const void* r, const float* st
   BN_LAUNCH(k_bn_bwd_apply, C, nparts_rows(M), st, (const bf16_t*)dy, (const bf16_t*)x,
                      (const bf16_t*)r, (const float2*)stats, gamma, beta, (const float2*)sums, (bf16_t*)dx,
                      (bf16_t*)dr, M, C, relu, res_mode);
+  OPCK(hipGetLastError());
+  return 0;
+}
+
+// The same backward when the statistics pass already ran in the producer of dy (the dgrad GEMM epilogue,
+// GemmArgs::bnb_part): nparts partial rows [nparts][C] of (sum dz, sum dz * xhat) -> finalize -> apply.
+int dca_ops_bn_bwd_parts(const void* dy, const void* x, const float* stats, const float* gamma, const float* beta,
+                         const float* part, int nparts, float* sums, float* dgamma, float* dbeta, void* dx, long M,
+                         int C, int accumulate, void* stream) {
+  REQUIRE(C % 8 == 0 && nparts > 0, "bn: C must be a multiple of 8");
+  hipStream_t st = (hipStream_t)stream;
+#define FIN(CW) hipLaunchKernelGGL(k_bn_bwd_finalize<CW>, dim3((C + CW - 1) / CW), dim3(256), 0, st, \
+                                   (const float2*)part, nparts, C, dgamma, dbeta, (float2*)sums, accumulate)
+  BN_FIN_DISPATCH(C, FIN);
+#undef FIN
+  BN_LAUNCH(k_bn_bwd_apply, C, nparts_rows(M), st, (const bf16_t*)dy, (const bf16_t*)x, (const bf16_t*)nullptr,
+            (const float2*)stats, gamma, beta, (const float2*)sums, (bf16_t*)dx, (bf16_t*)nullptr, M, C, 1, 0);
   OPCK(hipGetLastError());
   return 0;
 }

@@ -240,6 +240,34 @@ def test_ops_resnet_step(gpu, fp8):
     assert not bad, bad
 
 
+def test_ops_bn_backward_stats_fused_in_dgrad(gpu, monkeypatch):
+    """bn1 -> conv2 and bn2 -> conv3 of every bottleneck: the BN-backward statistics summed in conv2's / conv3's
+    dgrad GEMM epilogue (BnLink, DCA_OPS_BNB_FUSE=1) give the same gradients as the separate statistics pass
+    (stride-1 3x3, the 4 parity classes of the stride-2 3x3, and the 1x1 dgrad), up to fp32 summation order."""
+    import copy
+    from distributeddataparallel_cifar10_amd.models.resnet50 import ResNet
+    from distributeddataparallel_cifar10_amd.ops import OpsModel, cross_entropy
+    from distributeddataparallel_cifar10_amd.ops import functional as OF
+    torch.manual_seed(0)
+    net = ResNet([2, 1, 1, 1], num_classes=10, zero_init_residual=False).to(gpu)
+    x = torch.randn(4, 3, 96, 96, device=gpu)
+    y = torch.randint(0, 10, (4,), device=gpu)
+    grads = []
+    for fuse in (False, True):
+        monkeypatch.setattr(OF, "_BNB_FUSE", fuse)
+        m = copy.deepcopy(net)
+        cross_entropy(OpsModel(m)(x), y).backward()
+        grads.append({n: p.grad.clone() for n, p in m.named_parameters()})
+    rows = [(n, _rel(grads[1][n], g)) for n, g in grads[0].items()]
+    print("\n".join(f"{n:40s} {e:.2e}" for n, e in rows))
+    # the last bottleneck's own BN parameters see the fused sums directly (fp32 summation order only); upstream
+    # gradients also carry the bf16 rounding flips that those last-bit differences cause through the backward
+    direct = [(n, e) for n, e in rows if n.startswith("layer4.0.bn") or n.startswith("fc.")]
+    assert all(e < 1e-3 for _, e in direct), direct
+    bad = [(n, e) for n, e in rows if e > 0.1]
+    assert not bad, bad
+
+
 @pytest.mark.parametrize("kind", ["resnet", "netresdeep"])
 def test_ops_eval_inference(gpu, kind):
     """Eval-mode forward (inference: BN normalised with the running statistics, k_bn_eval_stats + k_bn_apply)
