@@ -1197,12 +1197,14 @@ __device__ __forceinline__ float* rslab(const RedAr& ra, int q, int par) {
 }
 
 // one-shot exchange of segment b (segv[0 .. len), len % 4 == 0) with every peer; on return segv holds the sum
-__device__ void seg_exchange(const Ctx& cx, const RedAr& ra, int b, float* segv, int len, int off) {
+// ep0: this segment's last epoch (own flag), loaded by the caller at kernel start so its latency hides under the
+// reduction (thread 0's value; broadcast here)
+__device__ void seg_exchange(const Ctx& cx, const RedAr& ra, int b, float* segv, int len, int off, int ep0) {
   const int t = threadIdx.x, W = cx.ws, me = cx.rank;
   int* myflags = (int*)rbase(ra, me);
   __shared__ int s_ep;
   const unsigned long long t_in = __builtin_amdgcn_s_memrealtime();
-  if (t == 0) s_ep = xg::flag_load(myflags + me * NSEG + b) + 1;
+  if (t == 0) s_ep = ep0 + 1;
   __syncthreads();
   const int ep = s_ep, par = ep & 1;
   constexpr int SYS = 17;  // sc0 | sc1: write-through store / cache-bypassing load
@@ -1281,6 +1283,8 @@ __global__ void __launch_bounds__(256) k_pks_reduce_ar(Ctx cx, pk::PkArgs pa, in
   const int mode = ra.mode;
   // this thread's SGD elements (k = t + 256 i): parameter indices and old values loaded first, so their latency
   // hides under the slab reduction (a dependent read after it cost 1.5 us per step)
+  // this segment's exchange epoch (own flag), loaded now: the latency of the uncached read hides under the reduction
+  const int ep0 = mode >= 2 && t == 0 ? xg::flag_load((const int*)rbase(ra, cx.rank) + cx.rank * NSEG + b) : 0;
   constexpr int KMAX = SEG_MAX / 256;
   int pid[KMAX];
   float pold[KMAX];
@@ -1382,7 +1386,7 @@ __global__ void __launch_bounds__(256) k_pks_reduce_ar(Ctx cx, pk::PkArgs pa, in
     }
   }
   __syncthreads();
-  if (mode >= 2) seg_exchange(cx, ra, b, segv, len, off);
+  if (mode >= 2) seg_exchange(cx, ra, b, segv, len, off, ep0);
 #pragma unroll
   for (int i = 0; i < KMAX; ++i) {
     const int k = t + 256 * i;
