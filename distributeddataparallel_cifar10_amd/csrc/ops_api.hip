@@ -107,6 +107,13 @@ inline int getenv_glds_single() {
   }();
   return v;
 }
+inline int getenv_pp() {  // ping-pong 256 x 256 GEMM (k_gemm_pp): DCA_OPS_PP = 0 never, 1 whenever eligible,
+  static const int v = [] {  // 2 (default) by the shape rule at the launch site
+    const char* e = getenv("DCA_OPS_PP");
+    return e ? atoi(e) : 2;
+  }();
+  return v;
+}
 inline bool getenv_wgrad_ok() {
   static const int v = [] {
     const char* e = getenv("DCA_OPS_WGRAD");
@@ -204,6 +211,7 @@ int dca_ops_gemm(const GemmArgs* a, void* stream) {
       GLDS_ATTR(true, 64, 8);
 #undef GLDS_ATTR
     }
+    OPCK(hipFuncSetAttribute((const void*)k_gemm_pp, hipFuncAttributeMaxDynamicSharedMemorySize, PP_LDS));
     g_lds_set = true;
   }
   const int kt = GBK_BYTES / (g.fp8 ? 1 : 2);
@@ -241,6 +249,30 @@ int dca_ops_gemm(const GemmArgs* a, void* stream) {
     hipLaunchKernelGGL(k_gemm_splitk_reduce, dim3(grid_for((long)g.M * g.N, RED_EL, 4096)), dim3(256), 0, st, g);
     OPCK(hipGetLastError());
     return 0;
+  }
+  // ping-pong 256 x 256 kernel: bf16, K-contiguous operands (plain or the C % 64 implicit conv), no split-K / row
+  // remap / fused BN-backward statistics, 16-B aligned rows, operands addressable with 32-bit offsets
+  {
+    const long long ab = g.conv == 1 ? (long long)g.cN * g.cH * g.cW * g.cC * 2 : ((long long)(g.M - 1) * g.lda + g.K) * 2;
+    const long long bb = ((long long)(g.N - 1) * g.ldb + g.K) * 2;
+    // shape rule (no wasted MFMA columns, >= 160 of the 256 CUs busy, K >= 1024 to amortise the pipeline fill and
+    // the 256-row epilogue): measured 4096^3 779 -> 1037 TF, 3x3 conv 256x14x14x256 109 -> 81.6 us; the ResNet-50
+    // batch-256 census (profiles/gemm_pingpong_r2.log) loses on N = 128 (+54 %), 98-tile grids (+38 %) and
+    // K = 256 (+20 %), wins on 50176 x 256 x {1024, 2304} (-8 %, -21 %)
+    const long pp_tiles = (long)((g.M + PP_BM - 1) / PP_BM) * ((g.N + PP_BN - 1) / PP_BN);
+    const int ppk = getenv_pp();
+    const bool pp_shape = ppk == 1 || (ppk == 2 && g.N % PP_BN == 0 && pp_tiles >= 160 && g.K >= 1024);
+    const bool pp = pp_shape && !g.fp8 && !g.ta && !g.tb && g.splits == 1 && g.wperm_T <= 0 && g.orow_S <= 0 &&
+                    !g.bnb_part && g.M >= 256 && g.N >= 128 && g.K >= 256 && ab < (1LL << 31) && bb < (1LL << 31) &&
+                    (long)g.ldb * 2 % 16 == 0 && ((uintptr_t)g.A & 15) == 0 && ((uintptr_t)g.B & 15) == 0 &&
+                    (g.conv == 1 ? (g.cC % 64 == 0 && g.cKH * g.cKW <= 32)
+                                 : (g.conv == 0 && (long)g.lda * 2 % 16 == 0 && (long)g.K * 2 % 16 == 0));
+    if (pp) {
+      const unsigned tiles = (unsigned)(((g.M + PP_BM - 1) / PP_BM) * ((g.N + PP_BN - 1) / PP_BN));
+      hipLaunchKernelGGL(k_gemm_pp, dim3(tiles), dim3(PP_NT), PP_LDS, st, g);
+      OPCK(hipGetLastError());
+      return 0;
+    }
   }
   // narrow N (<= 64) with a K-contiguous B operand: the 128x64 tile
   const bool narrow = g.N <= 64 && !g.tb && g.conv != 2;

@@ -878,6 +878,282 @@ __global__ void __launch_bounds__(NW * 64) k_gemm_glds(GemmArgs g) {
   gemm_epilogue<BN_, NW, BNB>(g, acc, smem, m0, n0, tm, ksplit);
 }
 
+// ---------------------------------------------------------------------------------------------------------
+// k_gemm_pp: 256 x 256 output tile, 512 threads as two wave groups that ping-pong (bf16, K-contiguous operands or
+// the C % 64 implicit conv; no split-K / row remap).  Group r (waves 4r .. 4r+3) owns rows 128r .., wave (r, c)
+// a 128 x 64 sub-tile (32 accumulators of 16 x 16).  Every K-tile is two k32 steps; per step a group first reads
+// its A / B fragments from LDS (L) and then issues its 32 MFMAs (M).  Group 1 starts one barrier late, so in
+// every barrier interval one group runs MFMAs while the other reads fragments and issues LDS-DMA: each SIMD holds
+// one wave of each group (waves w and w + 4), so its MFMA pipe is fed by whichever group is in M.
+// Interval I_j (between barriers j and j + 1): group 0 runs L(s) in I_2s and M(s) in I_2s+1, group 1 L(s) in
+// I_2s+1 and M(s) in I_2s+2 (step s = 2 kt + h).  Staging, two LDS buffers (tile kt in buffer kt & 1):
+//   * tile kt + 1 is issued in I_4kt (group 0 before L(2kt), group 1 in M(2kt - 1)); its buffer last held tile
+//     kt - 1, read for the last time in I_4kt-1 and retired there (lgkmcnt(0) before that barrier);
+//   * every issuing thread waits vmcnt(0) before the barrier ending I_4kt+3 (group 0 after M(2kt + 1), group 1
+//     after L(2kt + 1)), so tile kt + 1 is complete and visible when group 0 reads it in I_4kt+4.
+// Operand addressing as k_gemm_glds' fast path (per-lane offsets computed once, incremental tap for the conv).
+// ---------------------------------------------------------------------------------------------------------
+constexpr int PP_BM = 256, PP_BN = 256, PP_NT = 512;
+constexpr int PP_TILE = PP_BM * GBK_BYTES;       // 32 KiB per operand and buffer
+constexpr int PP_LDS = 2 * 2 * PP_TILE;          // 128 KiB
+
+__global__ void __launch_bounds__(PP_NT) k_gemm_pp(GemmArgs g) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int ntm = (g.M + PP_BM - 1) / PP_BM, ntn = (g.N + PP_BN - 1) / PP_BN;
+  const int tile = xcd_remap(blockIdx.x, ntm * ntn);
+  int tm, tn;
+  tile_coords(tile, ntm, ntn, tm, tn);
+  const int m0 = tm * PP_BM, n0 = tn * PP_BN;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, wr = wave >> 2, wc = wave & 3;
+  constexpr int ESZ = 2, KT = GBK_BYTES / ESZ;
+  const int k_begin = 0, k_end = g.K, nk = (g.K + KT - 1) / KT;
+  const int lr = lane >> 3, lj = lane & 7;
+  constexpr int NI = 4;  // glds per thread and operand per K-tile (wave: rows 32 wave .. + 32)
+  constexpr unsigned OOB = 0x80000000u;
+  const long long a_bytes = g.conv == 1 ? (long long)g.cN * g.cH * g.cW * g.cC * ESZ
+                                        : ((long long)(g.M - 1) * g.lda + g.K) * ESZ;
+  const long long b_bytes = ((long long)(g.N - 1) * g.ldb + g.K) * ESZ;
+  const __amdgpu_buffer_rsrc_t ars = __builtin_amdgcn_make_buffer_rsrc((void*)g.A, (short)0, (int)a_bytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t brs = __builtin_amdgcn_make_buffer_rsrc((void*)g.B, (short)0, (int)b_bytes, 0x00020000);
+  unsigned aoff[NI], amask[NI], boff[NI];
+  int s_tap = 0, s_kh = 0, s_kw = 0, s_c0b = 0, s_tapoff = 0;
+#pragma unroll
+  for (int i = 0; i < NI; ++i) {
+    const int r = wave * 32 + i * 8 + lr, m = m0 + r;
+    const unsigned cb = (unsigned)(lj ^ ((r >> 1) & 7)) << 4;
+    if (g.conv == 1) {
+      amask[i] = 0u;
+      aoff[i] = 0u;
+      if (m < g.M) {
+        const int ow = m % g.cWo, t = m / g.cWo, oh = t % g.cHo, n = t / g.cHo;
+        const int ih0 = oh * g.cS - g.cP, iw0 = ow * g.cS - g.cP;
+        aoff[i] = (unsigned)((((long long)n * g.cH + ih0) * g.cW + iw0) * g.cC * ESZ + cb);
+        for (int kh = 0; kh < g.cKH; ++kh)
+          for (int kw = 0; kw < g.cKW; ++kw)
+            if (ih0 + kh >= 0 && ih0 + kh < g.cH && iw0 + kw >= 0 && iw0 + kw < g.cW) amask[i] |= 1u << (kh * g.cKW + kw);
+      }
+    } else {
+      amask[i] = 0u;
+      aoff[i] = m < g.M ? (unsigned)((long long)m * g.lda * ESZ) + cb : OOB;
+    }
+    const int n = n0 + r;
+    boff[i] = n < g.N ? (unsigned)((long long)n * g.ldb * ESZ) + cb : OOB;
+  }
+  auto lane_cb = [&](int r) { return (int)((unsigned)(lj ^ ((r >> 1) & 7)) << 4); };
+  // this thread's LDS-DMA of tile kt into buffer kt & 1 (tiles issued in increasing order: the conv tap state)
+  auto issue = [&](int kt) {
+    const int kb0 = (k_begin + kt * KT) * ESZ;
+    const bool tail = k_end * ESZ - kb0 < GBK_BYTES;
+    char* la = smem + (kt & 1) * 2 * PP_TILE;
+    char* lb = la + PP_TILE;
+    if (g.conv == 1) {
+      const unsigned sadd = (unsigned)(s_tapoff + s_c0b), bit = 1u << s_tap;
+#pragma unroll
+      for (int i = 0; i < NI; ++i) {
+        bool ok = (amask[i] & bit) != 0u;
+        if (tail) ok = ok && kb0 + lane_cb(wave * 32 + i * 8 + lr) < k_end * ESZ;
+        blds16(ars, la + (wave * 32 + i * 8) * 128, ok ? aoff[i] + sadd : OOB, 0u);
+      }
+      s_c0b += GBK_BYTES;
+      if (s_c0b == g.cC * ESZ) {
+        s_c0b = 0;
+        ++s_tap;
+        if (++s_kw == g.cKW) {
+          s_kw = 0;
+          ++s_kh;
+        }
+        s_tapoff = (s_kh * g.cW + s_kw) * g.cC * ESZ;
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < NI; ++i) {
+        unsigned v = aoff[i];
+        if (tail && kb0 + lane_cb(wave * 32 + i * 8 + lr) >= k_end * ESZ) v = OOB;
+        blds16(ars, la + (wave * 32 + i * 8) * 128, v, (unsigned)kb0);
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < NI; ++i) {
+      unsigned v = boff[i];
+      if (tail && kb0 + lane_cb(wave * 32 + i * 8 + lr) >= k_end * ESZ) v = OOB;
+      blds16(brs, lb + (wave * 32 + i * 8) * 128, v, (unsigned)kb0);
+    }
+  };
+  auto bar = [] {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+  };
+
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int m = 0; m < 8; ++m)
+#pragma unroll
+    for (int n = 0; n < 4; ++n) acc[m][n] = f32x4{0.f, 0.f, 0.f, 0.f};
+  s16x8 af[8], bfr[4];
+  auto load_frags = [&](int kt, int h) {
+    const char* la = smem + (kt & 1) * 2 * PP_TILE;
+    const char* lb = la + PP_TILE;
+#pragma unroll
+    for (int m = 0; m < 8; ++m) af[m] = *(const s16x8*)(la + lds_off(wr * 128 + m * 16 + (lane & 15), h * 4 + (lane >> 4)));
+#pragma unroll
+    for (int n = 0; n < 4; ++n) bfr[n] = *(const s16x8*)(lb + lds_off(wc * 64 + n * 16 + (lane & 15), h * 4 + (lane >> 4)));
+  };
+  auto mfmas = [&] {
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int m = 0; m < 8; ++m)
+#pragma unroll
+      for (int n = 0; n < 4; ++n) acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[m], bfr[n], acc[m][n], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+  };
+
+  // prologue: tile 0 complete and visible to everyone
+  if (nk > 0) issue(0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  bar();
+  if (wr == 0) {
+#pragma unroll 1
+    for (int st = 0; st < 2 * nk; ++st) {
+      const int kt = st >> 1, h = st & 1;
+      if (h == 0 && kt + 1 < nk) issue(kt + 1);  // I_4kt: buffer (kt+1) & 1 retired in I_4kt-1
+      load_frags(kt, h);
+      bar();                                      // end of L(st)
+      mfmas();
+      if (h == 1) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // my part of tile kt + 1 landed
+      bar();                                      // end of M(st)
+    }
+    bar();  // group 1 runs one barrier behind
+  } else {
+    if (nk > 1) issue(1);  // I_0: group 1's part of tile 1 (group 0 issued its part before L(0))
+    bar();                 // end of I_0
+#pragma unroll 1
+    for (int st = 0; st < 2 * nk; ++st) {
+      const int kt = st >> 1, h = st & 1;
+      load_frags(kt, h);
+      if (h == 1) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // my part of tile kt + 1 landed (I_4kt+3)
+      bar();                                      // end of L(st)
+      if (h == 1 && kt + 2 < nk) issue(kt + 2);  // I_4kt+4: tile kt + 2 into buffer kt & 1, retired in I_4kt+3
+      mfmas();
+      bar();                                      // end of M(st)
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+
+  // epilogue: four 64-row quarters staged in LDS (fp32, 64 KiB), written row-contiguously, 16 B per lane, with
+  // alpha / bias / beta / ReLU and the optional BN column statistics (one partial row per 128 output rows)
+  float* ct = (float*)smem;
+  auto cidx = [](int r, int c) { return r * PP_BN + (c ^ (((r >> 2) & 3) << 4)); };
+  const float alpha = gemm_alpha(g);
+  constexpr int CG = PP_BN / 8, RL = PP_NT / CG;  // 32 column groups, 16 row lanes
+  const int cg = threadIdx.x % CG, col0 = n0 + cg * 8;
+  float bias8[8], shift8[8], s1[8], s2[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    const int col = min(col0 + e, g.N - 1);
+    bias8[e] = g.bias ? g.bias[col] : 0.f;
+    shift8[e] = g.col_stats ? g.stats_shift[col] : 0.f;
+    s1[e] = s2[e] = 0.f;
+  }
+  const bool full8 = col0 + 8 <= g.N && (g.ldc & 7) == 0;
+#pragma unroll  // (compile-time accumulator indices: a runtime index would put acc in scratch)
+  for (int q = 0; q < 4; ++q) {
+    if (wr == (q >> 1)) {
+#pragma unroll
+      for (int m = 0; m < 4; ++m)
+#pragma unroll
+        for (int n = 0; n < 4; ++n)
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+            ct[cidx(m * 16 + (lane >> 4) * 4 + j, wc * 64 + n * 16 + (lane & 15))] = acc[(q & 1) * 4 + m][n][j];
+    }
+    __syncthreads();
+    for (int r = 0; r < 64 / RL; ++r) {
+      const int lrow = threadIdx.x / CG + RL * r, row = m0 + q * 64 + lrow;
+      if (row >= g.M || col0 >= g.N) continue;
+      const f32x4 a0 = *(const f32x4*)(ct + cidx(lrow, cg * 8)), a1 = *(const f32x4*)(ct + cidx(lrow, cg * 8 + 4));
+      const float av[8] = {a0[0], a0[1], a0[2], a0[3], a1[0], a1[1], a1[2], a1[3]};
+      const size_t o = (size_t)row * g.ldc + col0;
+      float old[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+      if (g.beta != 0.f) {
+        if (full8 && g.out_bf16) {
+          const uint4 u = *(const uint4*)((const unsigned short*)g.C + o);
+          const unsigned w4[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+          for (int e = 0; e < 8; ++e) old[e] = __uint_as_float((w4[e >> 1] >> ((e & 1) * 16)) << 16);
+        } else {
+          for (int e = 0; e < 8 && col0 + e < g.N; ++e)
+            old[e] = g.out_bf16 ? bf2f(((const unsigned short*)g.C)[o + e]) : ((const float*)g.C)[o + e];
+        }
+      }
+      float v[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        float x = av[e] * alpha + bias8[e] + g.beta * old[e];
+        if (g.relu) x = x > 0.f ? x : 0.f;
+        v[e] = x;
+      }
+      if (g.out_bf16) {
+        unsigned short hb[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) hb[e] = f2bf_rne(v[e]);
+        if (g.col_stats) {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            const float d = bf2f(hb[e]) - shift8[e];
+            s1[e] += d;
+            s2[e] += d * d;
+          }
+        }
+        if (full8) {
+          *(uint4*)((unsigned short*)g.C + o) =
+              uint4{hb[0] | ((unsigned)hb[1] << 16), hb[2] | ((unsigned)hb[3] << 16), hb[4] | ((unsigned)hb[5] << 16),
+                    hb[6] | ((unsigned)hb[7] << 16)};
+        } else {
+          for (int e = 0; e < 8 && col0 + e < g.N; ++e) ((unsigned short*)g.C)[o + e] = hb[e];
+        }
+      } else {
+        if (g.col_stats) {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            const float d = v[e] - shift8[e];
+            s1[e] += d;
+            s2[e] += d * d;
+          }
+        }
+        if (full8) {
+          *(f32x4*)((float*)g.C + o) = f32x4{v[0], v[1], v[2], v[3]};
+          *(f32x4*)((float*)g.C + o + 4) = f32x4{v[4], v[5], v[6], v[7]};
+        } else {
+          for (int e = 0; e < 8 && col0 + e < g.N; ++e) ((float*)g.C)[o + e] = v[e];
+        }
+      }
+    }
+    __syncthreads();
+    if (g.col_stats && (q & 1)) {  // one partial row per 128 output rows (the k_bn_finalize layout)
+      float2* red = (float2*)smem;  // [RL][PP_BN]
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        red[(threadIdx.x / CG) * PP_BN + cg * 8 + e] = float2{s1[e], s2[e]};
+        s1[e] = s2[e] = 0.f;
+      }
+      __syncthreads();
+      if (threadIdx.x < PP_BN) {
+        const int col = n0 + threadIdx.x;
+        float2 t = red[threadIdx.x];
+        for (int k = 1; k < RL; ++k) {
+          t.x += red[k * PP_BN + threadIdx.x].x;
+          t.y += red[k * PP_BN + threadIdx.x].y;
+        }
+        const int prow = 2 * tm + (q >> 1);
+        if (col < g.N && prow * 128 < g.M) g.col_stats[(size_t)prow * g.N + col] = t;
+      }
+      __syncthreads();
+    }
+  }
+}
+
 // Split-K combine: C = alpha * sum_s ws[s] (+bias) (+beta*C) (ReLU).  256 threads = 64 consecutive elements x 4
 // split lanes (lane l sums slabs l, l+4, ...; the 4 partials are added in lane order: deterministic), so
 // thousands of slabs of a small weight gradient are read by many threads with 256-B row segments.

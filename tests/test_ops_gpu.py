@@ -1,5 +1,7 @@
 """Unit tests of the ops-layer HIP kernels (csrc/ops_*.hip) against plain PyTorch fp32 references of the same op
 (layer 1: one test family per kernel family, random + ragged shapes, asymmetric operands)."""
+import os
+
 import pytest
 import torch
 import torch.nn.functional as TF
@@ -32,6 +34,22 @@ def test_gemm_bf16(gpu, M, N, K, ta, tb):
     assert _rel(out, ref) < 1e-5, _rel(out, ref)
     out2 = gemm(A, B, ta=bool(ta), tb=bool(tb), bias=bias, relu=True, out_dtype=torch.bfloat16, splits=3)
     assert _rel(out2.float(), ref.clamp_min(0)) < 1e-2
+
+
+def test_gemm_pingpong_matches_torch(gpu):
+    """The ping-pong 256 x 256 GEMM (DCA_OPS_PP=1, read once per process: run in a child) on plain NT shapes with
+    M / N / K tails, bias + ReLU, fused BN column statistics, and implicit 3x3 / 1x1 convolutions (padding, stride
+    2) against torch fp32."""
+    import json
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([sys.executable, os.path.join(root, "tests", "_pp_check.py")], capture_output=True, text=True,
+                       env=dict(os.environ, DCA_OPS_PP="1"), timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    res = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
+    bad = {k: v for k, v in res.items() if v > (1e-2 if "bf16" in k or "colstats" in k else 2e-3)}
+    assert not bad, (bad, res)
 
 
 def test_gemm_identity_layout(gpu):
