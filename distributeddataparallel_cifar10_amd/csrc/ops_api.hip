@@ -211,7 +211,10 @@ int dca_ops_gemm(const GemmArgs* a, void* stream) {
       GLDS_ATTR(true, 64, 8);
 #undef GLDS_ATTR
     }
-    OPCK(hipFuncSetAttribute((const void*)k_gemm_pp, hipFuncAttributeMaxDynamicSharedMemorySize, PP_LDS));
+    OPCK(hipFuncSetAttribute((const void*)k_gemm_pp<256>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                             PpTile<256>::LDS));
+    OPCK(hipFuncSetAttribute((const void*)k_gemm_pp<128>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                             PpTile<128>::LDS));
     g_lds_set = true;
   }
   const int kt = GBK_BYTES / (g.fp8 ? 1 : 2);
@@ -259,17 +262,21 @@ int dca_ops_gemm(const GemmArgs* a, void* stream) {
     // the 256-row epilogue): measured 4096^3 779 -> 1037 TF, 3x3 conv 256x14x14x256 109 -> 81.6 us; the ResNet-50
     // batch-256 census (profiles/gemm_pingpong_r2.log) loses on N = 128 (+54 %), 98-tile grids (+38 %) and
     // K = 256 (+20 %), wins on 50176 x 256 x {1024, 2304} (-8 %, -21 %)
-    const long pp_tiles = (long)((g.M + PP_BM - 1) / PP_BM) * ((g.N + PP_BN - 1) / PP_BN);
+    // N % 256 != 0 (e.g. 128): the 256 x 128 tile
+    const int ppbn = g.N % 256 == 0 ? 256 : 128;
+    const long pp_tiles = (long)((g.M + PP_BM - 1) / PP_BM) * ((g.N + ppbn - 1) / ppbn);
     const int ppk = getenv_pp();
-    const bool pp_shape = ppk == 1 || (ppk == 2 && g.N % PP_BN == 0 && pp_tiles >= 160 && g.K >= 1024);
+    // (the 256 x 128 tile measured slower than the 128 x 128 kernels on every ResNet-50 N = 128 shape, +12-18 %:
+    // 16 MFMAs per barrier interval do not cover the other group's fragment loads; DCA_OPS_PP=1 only)
+    const bool pp_shape = ppk == 1 || (ppk == 2 && ppbn == 256 && g.N % 256 == 0 && pp_tiles >= 160 && g.K >= 1024);
     const bool pp = pp_shape && !g.fp8 && !g.ta && !g.tb && g.splits == 1 && g.wperm_T <= 0 && g.orow_S <= 0 &&
                     !g.bnb_part && g.M >= 256 && g.N >= 128 && g.K >= 256 && ab < (1LL << 31) && bb < (1LL << 31) &&
                     (long)g.ldb * 2 % 16 == 0 && ((uintptr_t)g.A & 15) == 0 && ((uintptr_t)g.B & 15) == 0 &&
                     (g.conv == 1 ? (g.cC % 64 == 0 && g.cKH * g.cKW <= 32)
                                  : (g.conv == 0 && (long)g.lda * 2 % 16 == 0 && (long)g.K * 2 % 16 == 0));
     if (pp) {
-      const unsigned tiles = (unsigned)(((g.M + PP_BM - 1) / PP_BM) * ((g.N + PP_BN - 1) / PP_BN));
-      hipLaunchKernelGGL(k_gemm_pp, dim3(tiles), dim3(PP_NT), PP_LDS, st, g);
+      if (ppbn == 256) hipLaunchKernelGGL(k_gemm_pp<256>, dim3((unsigned)pp_tiles), dim3(PP_NT), PpTile<256>::LDS, st, g);
+      else hipLaunchKernelGGL(k_gemm_pp<128>, dim3((unsigned)pp_tiles), dim3(PP_NT), PpTile<128>::LDS, st, g);
       OPCK(hipGetLastError());
       return 0;
     }

@@ -893,18 +893,29 @@ __global__ void __launch_bounds__(NW * 64) k_gemm_glds(GemmArgs g) {
 //     after L(2kt + 1)), so tile kt + 1 is complete and visible when group 0 reads it in I_4kt+4.
 // Operand addressing as k_gemm_glds' fast path (per-lane offsets computed once, incremental tap for the conv).
 // ---------------------------------------------------------------------------------------------------------
-constexpr int PP_BM = 256, PP_BN = 256, PP_NT = 512;
-constexpr int PP_TILE = PP_BM * GBK_BYTES;       // 32 KiB per operand and buffer
-constexpr int PP_LDS = 2 * 2 * PP_TILE;          // 128 KiB
+constexpr int PP_BM = 256, PP_NT = 512;
+constexpr int PP_TILE = PP_BM * GBK_BYTES;  // A: 32 KiB per buffer
+template <int BN>
+struct PpTile {  // BN = 256: a group's 4 waves side by side (128 x 64 each); BN = 128: 2 x 2 waves of 64 x 64
+  static constexpr int WMG = BN == 256 ? 1 : 2, WNG = 4 / WMG, MF = 8 / WMG;
+  static constexpr int BTILE = BN * GBK_BYTES, BUF = PP_TILE + BTILE, LDS = 2 * BUF;
+  static constexpr int NIB = BN / 64;  // B glds per thread and K-tile (wave: B rows (BN / 8) wave ..)
+  static_assert(LDS >= 64 * BN * 4, "epilogue staging fits");
+};
+constexpr int PP_LDS = PpTile<256>::LDS;  // 128 KiB
 
+template <int PP_BN>
 __global__ void __launch_bounds__(PP_NT) k_gemm_pp(GemmArgs g) {
+  using TT = PpTile<PP_BN>;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int ntm = (g.M + PP_BM - 1) / PP_BM, ntn = (g.N + PP_BN - 1) / PP_BN;
   const int tile = xcd_remap(blockIdx.x, ntm * ntn);
   int tm, tn;
   tile_coords(tile, ntm, ntn, tm, tn);
   const int m0 = tm * PP_BM, n0 = tn * PP_BN;
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, wr = wave >> 2, wc = wave & 3;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, wr = wave >> 2;
+  const int wi = (wave & 3) / TT::WNG, wj = (wave & 3) % TT::WNG;  // wave position inside its group
+  const int wrow = wr * 128 + wi * (128 / TT::WMG), wcol = wj * 64;
   constexpr int ESZ = 2, KT = GBK_BYTES / ESZ;
   const int k_begin = 0, k_end = g.K, nk = (g.K + KT - 1) / KT;
   const int lr = lane >> 3, lj = lane & 7;
@@ -915,7 +926,7 @@ __global__ void __launch_bounds__(PP_NT) k_gemm_pp(GemmArgs g) {
   const long long b_bytes = ((long long)(g.N - 1) * g.ldb + g.K) * ESZ;
   const __amdgpu_buffer_rsrc_t ars = __builtin_amdgcn_make_buffer_rsrc((void*)g.A, (short)0, (int)a_bytes, 0x00020000);
   const __amdgpu_buffer_rsrc_t brs = __builtin_amdgcn_make_buffer_rsrc((void*)g.B, (short)0, (int)b_bytes, 0x00020000);
-  unsigned aoff[NI], amask[NI], boff[NI];
+  unsigned aoff[NI], amask[NI], boff[TT::NIB];
   int s_tap = 0, s_kh = 0, s_kw = 0, s_c0b = 0, s_tapoff = 0;
 #pragma unroll
   for (int i = 0; i < NI; ++i) {
@@ -936,15 +947,18 @@ __global__ void __launch_bounds__(PP_NT) k_gemm_pp(GemmArgs g) {
       amask[i] = 0u;
       aoff[i] = m < g.M ? (unsigned)((long long)m * g.lda * ESZ) + cb : OOB;
     }
-    const int n = n0 + r;
-    boff[i] = n < g.N ? (unsigned)((long long)n * g.ldb * ESZ) + cb : OOB;
+  }
+#pragma unroll
+  for (int i = 0; i < TT::NIB; ++i) {
+    const int r = wave * (PP_BN / 8) + i * 8 + lr, n = n0 + r;
+    boff[i] = n < g.N ? (unsigned)((long long)n * g.ldb * ESZ) + ((unsigned)(lj ^ ((r >> 1) & 7)) << 4) : OOB;
   }
   auto lane_cb = [&](int r) { return (int)((unsigned)(lj ^ ((r >> 1) & 7)) << 4); };
   // this thread's LDS-DMA of tile kt into buffer kt & 1 (tiles issued in increasing order: the conv tap state)
   auto issue = [&](int kt) {
     const int kb0 = (k_begin + kt * KT) * ESZ;
     const bool tail = k_end * ESZ - kb0 < GBK_BYTES;
-    char* la = smem + (kt & 1) * 2 * PP_TILE;
+    char* la = smem + (kt & 1) * TT::BUF;
     char* lb = la + PP_TILE;
     if (g.conv == 1) {
       const unsigned sadd = (unsigned)(s_tapoff + s_c0b), bit = 1u << s_tap;
@@ -973,10 +987,11 @@ __global__ void __launch_bounds__(PP_NT) k_gemm_pp(GemmArgs g) {
       }
     }
 #pragma unroll
-    for (int i = 0; i < NI; ++i) {
+    for (int i = 0; i < TT::NIB; ++i) {
+      const int r = wave * (PP_BN / 8) + i * 8;
       unsigned v = boff[i];
-      if (tail && kb0 + lane_cb(wave * 32 + i * 8 + lr) >= k_end * ESZ) v = OOB;
-      blds16(brs, lb + (wave * 32 + i * 8) * 128, v, (unsigned)kb0);
+      if (tail && kb0 + lane_cb(r + lr) >= k_end * ESZ) v = OOB;
+      blds16(brs, lb + r * 128, v, (unsigned)kb0);
     }
   };
   auto bar = [] {
@@ -985,24 +1000,25 @@ __global__ void __launch_bounds__(PP_NT) k_gemm_pp(GemmArgs g) {
     asm volatile("" ::: "memory");
   };
 
-  f32x4 acc[8][4];
+  constexpr int MF = TT::MF;
+  f32x4 acc[MF][4];
 #pragma unroll
-  for (int m = 0; m < 8; ++m)
+  for (int m = 0; m < MF; ++m)
 #pragma unroll
     for (int n = 0; n < 4; ++n) acc[m][n] = f32x4{0.f, 0.f, 0.f, 0.f};
-  s16x8 af[8], bfr[4];
+  s16x8 af[MF], bfr[4];
   auto load_frags = [&](int kt, int h) {
-    const char* la = smem + (kt & 1) * 2 * PP_TILE;
+    const char* la = smem + (kt & 1) * TT::BUF;
     const char* lb = la + PP_TILE;
 #pragma unroll
-    for (int m = 0; m < 8; ++m) af[m] = *(const s16x8*)(la + lds_off(wr * 128 + m * 16 + (lane & 15), h * 4 + (lane >> 4)));
+    for (int m = 0; m < MF; ++m) af[m] = *(const s16x8*)(la + lds_off(wrow + m * 16 + (lane & 15), h * 4 + (lane >> 4)));
 #pragma unroll
-    for (int n = 0; n < 4; ++n) bfr[n] = *(const s16x8*)(lb + lds_off(wc * 64 + n * 16 + (lane & 15), h * 4 + (lane >> 4)));
+    for (int n = 0; n < 4; ++n) bfr[n] = *(const s16x8*)(lb + lds_off(wcol + n * 16 + (lane & 15), h * 4 + (lane >> 4)));
   };
   auto mfmas = [&] {
     __builtin_amdgcn_s_setprio(1);
 #pragma unroll
-    for (int m = 0; m < 8; ++m)
+    for (int m = 0; m < MF; ++m)
 #pragma unroll
       for (int n = 0; n < 4; ++n) acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[m], bfr[n], acc[m][n], 0, 0, 0);
     __builtin_amdgcn_s_setprio(0);
@@ -1059,14 +1075,16 @@ __global__ void __launch_bounds__(PP_NT) k_gemm_pp(GemmArgs g) {
   const bool full8 = col0 + 8 <= g.N && (g.ldc & 7) == 0;
 #pragma unroll  // (compile-time accumulator indices: a runtime index would put acc in scratch)
   for (int q = 0; q < 4; ++q) {
-    if (wr == (q >> 1)) {
+    // quarter q = rows 64 q ..: group q >> 1; BN = 256: its accumulators (q & 1) * 4 ..; BN = 128: wave wi = q & 1
+    if (wr == (q >> 1) && (TT::WMG == 1 || wi == (q & 1))) {
 #pragma unroll
       for (int m = 0; m < 4; ++m)
 #pragma unroll
         for (int n = 0; n < 4; ++n)
 #pragma unroll
           for (int j = 0; j < 4; ++j)
-            ct[cidx(m * 16 + (lane >> 4) * 4 + j, wc * 64 + n * 16 + (lane & 15))] = acc[(q & 1) * 4 + m][n][j];
+            ct[cidx(m * 16 + (lane >> 4) * 4 + j, wcol + n * 16 + (lane & 15))] =
+                acc[TT::WMG == 1 ? (q & 1) * 4 + m : m][n][j];
     }
     __syncthreads();
     for (int r = 0; r < 64 / RL; ++r) {

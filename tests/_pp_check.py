@@ -22,7 +22,7 @@ def main():
     g = torch.Generator(device=dev).manual_seed(0)
     bf = torch.bfloat16
     out = {}
-    for M, N, K in [(256, 256, 256), (1000, 384, 520), (777, 130, 1000), (4096, 512, 2048)]:
+    for M, N, K in [(256, 256, 256), (1000, 384, 520), (777, 130, 1000), (4096, 512, 2048), (2048, 128, 1152)]:
         a = torch.randn(M, K, device=dev, generator=g).to(bf)
         b = torch.randn(N, K, device=dev, generator=g).to(bf)
         bias = torch.randn(N, device=dev, generator=g)
