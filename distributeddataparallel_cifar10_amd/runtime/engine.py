@@ -132,7 +132,8 @@ class NetResDeepEngine:
             raise ValueError("comm must be 'rccl', 'external' or 'xgmi'")
         if cfg.dtype not in ("bf16", "fp32"):
             raise ValueError("dtype must be 'bf16' or 'fp32'")
-        if cfg.persistent is None:
+        auto_engine = cfg.persistent is None
+        if auto_engine:
             cfg.persistent = True  # the image-sliced persistent kernel (bf16 and fp32)
         if getattr(model, "n_chans1", 32) != 32 or getattr(model, "n_blocks", 10) != 10:
             raise ValueError("the fused engine is specialised for NetResDeep(n_chans1=32, n_blocks=10)")
@@ -171,8 +172,14 @@ class NetResDeepEngine:
         self.max_indices = int(max_indices or self.data.shape[0])
         h = ctypes.c_void_p()
         with torch.cuda.device(dev):
-            native.check(self.lib.dca_engine_create(ctypes.byref(init), self.max_indices, ctypes.byref(h)),
-                         "dca_engine_create")
+            rc = self.lib.dca_engine_create(ctypes.byref(init), self.max_indices, ctypes.byref(h))
+            if rc != 0 and auto_engine and "cannot all be resident" in native.last_error():
+                # the persistent step's workgroups do not fit the device at once (co-residency check at create
+                # time): the multi-kernel engine instead, same numerics contract
+                cfg.persistent = False
+                init.persistent = 0
+                rc = self.lib.dca_engine_create(ctypes.byref(init), self.max_indices, ctypes.byref(h))
+            native.check(rc, "dca_engine_create")
         self.h = h
         self.kind = int(self.lib.dca_engine_kind(h))  # 0 multi-kernel, 1 persistent per image, 2 sliced
         self.derive()

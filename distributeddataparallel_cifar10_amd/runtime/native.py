@@ -109,6 +109,10 @@ def require_native():
     return load(build_if_missing=True)
 
 
+def last_error() -> str:
+    return load(build_if_missing=False).dca_last_error().decode(errors="replace")
+
+
 def check(rc: int, what: str):
     if rc != 0:
         lib = load(build_if_missing=False)
