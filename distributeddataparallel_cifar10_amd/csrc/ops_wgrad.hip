@@ -87,34 +87,62 @@ __global__ void __launch_bounds__(256) k_wgrad(GemmArgs g) {
     ckw = tap - ckh * g.cKW;
   }
 
+  // Loader state per row slot i (rows k = k0 + r + RS i of K-tile k0): row pointers advanced by one K-tile per
+  // tile, and for the implicit im2col B the row's pixel decode (img, oh, ow) advanced by 64 pixels with scalar
+  // deltas -- no per-tile division or 64-bit multiply (the loader was ~7 VALU per MFMA, PMC, VALU-bound).
+  // Every load is unconditional from a valid address and selected to zero afterwards.
+  constexpr int RSA = 256 / T::CA, RSB = 256 / T::CB;
+  const unsigned short* pa[T::NA];
+  const unsigned short* pb[T::NB];
+  int bimg[T::NB], boh[T::NB], bow[T::NB];
+#pragma unroll
+  for (int i = 0; i < T::NA; ++i) pa[i] = A + (size_t)(k_begin + ra + RSA * i) * g.lda + (a_in ? ma : 0);
   const float inv_wo = 1.f / (float)g.cWo, inv_ho = 1.f / (float)g.cHo;
+  const int hw = g.cHo * g.cWo, d_img = T::BK / hw, d_rem = T::BK - d_img * hw, d_oh = d_rem / g.cWo,
+            d_ow = d_rem - d_oh * g.cWo;
+#pragma unroll
+  for (int i = 0; i < T::NB; ++i) {
+    const int k = min(k_begin + rb + RSB * i, g.K - 1);
+    if (g.conv == 2) {
+      const int t = fdivmod(k, g.cWo, inv_wo, bow[i]);
+      bimg[i] = fdivmod(t, g.cHo, inv_ho, boh[i]);
+      pb[i] = B;
+    } else {
+      bimg[i] = boh[i] = bow[i] = 0;
+      pb[i] = B + (size_t)(k_begin + rb + RSB * i) * g.ldb + (b_in ? nb : 0);
+    }
+  }
   uint4 sa[T::NA], sb[T::NB];
   auto load = [&](int kt) {
     const int k0 = k_begin + kt * T::BK;
 #pragma unroll
     for (int i = 0; i < T::NA; ++i) {
-      const int k = k0 + ra + (256 / T::CA) * i;
-      const bool ok = a_in && k < k_end;
-      const uint4 v = *(const uint4*)(A + (ok ? (size_t)k * g.lda + ma : 0));
+      const bool ok = a_in && k0 + ra + RSA * i < k_end;
+      const uint4 v = *(const uint4*)(ok ? pa[i] : A);
       sa[i] = ok ? v : uint4{0u, 0u, 0u, 0u};
+      pa[i] += (size_t)T::BK * g.lda;
     }
 #pragma unroll
     for (int i = 0; i < T::NB; ++i) {
-      const int k = k0 + rb + (256 / T::CB) * i;
-      bool ok = b_in && k < k_end;
-      size_t off = 0;
+      bool ok = b_in && k0 + rb + RSB * i < k_end;
+      const unsigned short* src;
       if (g.conv == 2) {
-        const int p = ok ? k : k_begin;
-        int ow, oh;
-        const int t = fdivmod(p, g.cWo, inv_wo, ow);
-        const int img = fdivmod(t, g.cHo, inv_ho, oh);
-        const int h = oh * g.cS - g.cP + ckh, w = ow * g.cS - g.cP + ckw;
+        const int h = boh[i] * g.cS - g.cP + ckh, w = bow[i] * g.cS - g.cP + ckw;
         ok = ok && h >= 0 && h < g.cH && w >= 0 && w < g.cW;
-        off = ok ? ((size_t)(img * g.cH + h) * g.cW + w) * g.cC + cc : 0;
+        src = B + ((size_t)(bimg[i] * g.cH + h) * g.cW + w) * g.cC + cc;
+        // next tile: 64 pixels on
+        bow[i] += d_ow;
+        const int c1 = bow[i] >= g.cWo;
+        bow[i] -= c1 ? g.cWo : 0;
+        boh[i] += d_oh + c1;
+        const int c2 = boh[i] >= g.cHo;
+        boh[i] -= c2 ? g.cHo : 0;
+        bimg[i] += d_img + c2;
       } else {
-        off = ok ? (size_t)k * g.ldb + nb : 0;
+        src = pb[i];
+        pb[i] += (size_t)T::BK * g.ldb;
       }
-      const uint4 v = *(const uint4*)(B + off);
+      const uint4 v = *(const uint4*)(ok ? src : B);
       sb[i] = ok ? v : uint4{0u, 0u, 0u, 0u};
     }
   };
