@@ -87,16 +87,12 @@ __global__ void __launch_bounds__(256) k_wgrad(GemmArgs g) {
     ckw = tap - ckh * g.cKW;
   }
 
-  // Loader state per row slot i (rows k = k0 + r + RS i of K-tile k0): row pointers advanced by one K-tile per
-  // tile, and for the implicit im2col B the row's pixel decode (img, oh, ow) advanced by 64 pixels with scalar
-  // deltas -- no per-tile division or 64-bit multiply (the loader was ~7 VALU per MFMA, PMC, VALU-bound).
+  // Loader state per row slot i (rows k = k0 + r + RS i of K-tile k0): for the implicit im2col B the row's pixel
+  // decode (img, oh, ow) advanced by 64 pixels with scalar deltas -- no per-tile division (the loader was ~7 VALU
+  // per MFMA, PMC, VALU-bound); plain rows keep one multiply (measured: pointer stepping was no faster).
   // Every load is unconditional from a valid address and selected to zero afterwards.
   constexpr int RSA = 256 / T::CA, RSB = 256 / T::CB;
-  const unsigned short* pa[T::NA];
-  const unsigned short* pb[T::NB];
   int bimg[T::NB], boh[T::NB], bow[T::NB];
-#pragma unroll
-  for (int i = 0; i < T::NA; ++i) pa[i] = A + (size_t)(k_begin + ra + RSA * i) * g.lda + (a_in ? ma : 0);
   const float inv_wo = 1.f / (float)g.cWo, inv_ho = 1.f / (float)g.cHo;
   const int hw = g.cHo * g.cWo, d_img = T::BK / hw, d_rem = T::BK - d_img * hw, d_oh = d_rem / g.cWo,
             d_ow = d_rem - d_oh * g.cWo;
@@ -106,10 +102,8 @@ __global__ void __launch_bounds__(256) k_wgrad(GemmArgs g) {
     if (g.conv == 2) {
       const int t = fdivmod(k, g.cWo, inv_wo, bow[i]);
       bimg[i] = fdivmod(t, g.cHo, inv_ho, boh[i]);
-      pb[i] = B;
     } else {
       bimg[i] = boh[i] = bow[i] = 0;
-      pb[i] = B + (size_t)(k_begin + rb + RSB * i) * g.ldb + (b_in ? nb : 0);
     }
   }
   uint4 sa[T::NA], sb[T::NB];
@@ -117,10 +111,10 @@ __global__ void __launch_bounds__(256) k_wgrad(GemmArgs g) {
     const int k0 = k_begin + kt * T::BK;
 #pragma unroll
     for (int i = 0; i < T::NA; ++i) {
-      const bool ok = a_in && k0 + ra + RSA * i < k_end;
-      const uint4 v = *(const uint4*)(ok ? pa[i] : A);
+      const int k = k0 + ra + RSA * i;
+      const bool ok = a_in && k < k_end;
+      const uint4 v = *(const uint4*)(A + (ok ? (size_t)k * g.lda + ma : 0));
       sa[i] = ok ? v : uint4{0u, 0u, 0u, 0u};
-      pa[i] += (size_t)T::BK * g.lda;
     }
 #pragma unroll
     for (int i = 0; i < T::NB; ++i) {
@@ -139,8 +133,7 @@ __global__ void __launch_bounds__(256) k_wgrad(GemmArgs g) {
         boh[i] -= c2 ? g.cHo : 0;
         bimg[i] += d_img + c2;
       } else {
-        src = pb[i];
-        pb[i] += (size_t)T::BK * g.ldb;
+        src = B + (ok ? (size_t)(k0 + rb + RSB * i) * g.ldb + nb : 0);
       }
       const uint4 v = *(const uint4*)(ok ? src : B);
       sb[i] = ok ? v : uint4{0u, 0u, 0u, 0u};
