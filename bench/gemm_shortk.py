@@ -1,0 +1,62 @@
+"""Short-K / wide-output GEMMs of ResNet-50 at batch 256 (the 1x1 expand / reduce convolutions and their dgrads):
+time per call with the fused BatchNorm column statistics the forward uses, against the HBM floor of the call
+(A read once + C written once).
+
+    python bench/gemm_shortk.py [--no-stats]        # one JSON line per shape
+Dispatch knobs (DCA_OPS_*) are read once per process, so A/B runs use one process per setting.
+"""
+import argparse
+import json
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from distributeddataparallel_cifar10_amd import ops  # noqa: E402
+
+SHAPES = [(802816, 256, 64), (50176, 1024, 256), (200704, 512, 128), (802816, 64, 256), (200704, 128, 512),
+          (12544, 2048, 512), (50176, 256, 1024), (802816, 128, 256)]
+
+
+def timeit(fn, iters=20):
+    for _ in range(3):
+        fn()
+    torch.cuda.synchronize()
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    a.record()
+    for _ in range(iters):
+        fn()
+    b.record()
+    torch.cuda.synchronize()
+    return a.elapsed_time(b) * 1e3 / iters
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--no-stats", action="store_true")
+    ap.add_argument("--tag", default=os.environ.get("DCA_TAG", "default"))
+    a = ap.parse_args()
+    dev = torch.device("cuda", 0)
+    bf = torch.bfloat16
+    for M, N, K in SHAPES:
+        x = torch.randn(M, K, device=dev).to(bf)
+        w = torch.randn(N, K, device=dev).to(bf)
+        kw = {}
+        if not a.no_stats:
+            kw = dict(col_stats=torch.zeros((M + 127) // 128, N, 2, device=dev),
+                      stats_shift=torch.zeros(N, device=dev))
+        y = ops.gemm(x, w, out_dtype=bf, **kw)
+        ref = (x.float() @ w.float().t())
+        err = ((y.float() - ref).norm() / ref.norm()).item()
+        us = timeit(lambda: ops.gemm(x, w, out_dtype=bf, **kw))
+        floor_us = 2 * (M * K + M * N) / 5.0e6  # at 5 TB/s
+        print(json.dumps({"tag": a.tag, "shape": f"{M}x{N}x{K}", "stats": not a.no_stats, "us": round(us, 1),
+                          "tflops": round(2 * M * N * K / us / 1e6, 1),
+                          "gbps": round(2 * (M * K + M * N) / us / 1e3, 1), "floor_us_5tbs": round(floor_us, 1),
+                          "rel_err": round(err, 5)}), flush=True)
+        del x, w, y, ref
+
+
+if __name__ == "__main__":
+    main()

@@ -107,6 +107,20 @@ inline int getenv_glds_single() {
   }();
   return v;
 }
+inline int getenv_stream() {  // persistent short-K GEMM (k_gemm_stream): DCA_OPS_STREAM = 0 never, 1 whenever
+  static const int v = [] {    // eligible, 2 (default) by the shape rule at the launch site
+    const char* e = getenv("DCA_OPS_STREAM");
+    return e ? atoi(e) : 2;
+  }();
+  return v;
+}
+inline int getenv_stream_cpol() {
+  static const int v = [] {
+    const char* e = getenv("DCA_OPS_STREAM_CPOL");
+    return e ? atoi(e) : 2;
+  }();
+  return v;
+}
 inline int getenv_pp() {  // ping-pong 256 x 256 GEMM (k_gemm_pp): DCA_OPS_PP = 0 never, 1 whenever eligible,
   static const int v = [] {  // 2 (default) by the shape rule at the launch site
     const char* e = getenv("DCA_OPS_PP");
@@ -215,6 +229,10 @@ int dca_ops_gemm(const GemmArgs* a, void* stream) {
                              PpTile<256>::LDS));
     OPCK(hipFuncSetAttribute((const void*)k_gemm_pp<128>, hipFuncAttributeMaxDynamicSharedMemorySize,
                              PpTile<128>::LDS));
+    OPCK(hipFuncSetAttribute((const void*)k_gemm_stream<0>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                             2 * ST_BUF + 2 * 2048 * 4));
+    OPCK(hipFuncSetAttribute((const void*)k_gemm_stream<2>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                             2 * ST_BUF + 2 * 2048 * 4));
     g_lds_set = true;
   }
   const int kt = GBK_BYTES / (g.fp8 ? 1 : 2);
@@ -252,6 +270,38 @@ int dca_ops_gemm(const GemmArgs* a, void* stream) {
     hipLaunchKernelGGL(k_gemm_splitk_reduce, dim3(grid_for((long)g.M * g.N, RED_EL, 4096)), dim3(256), 0, st, g);
     OPCK(hipGetLastError());
     return 0;
+  }
+  // persistent short-K stream kernel (k_gemm_stream): plain NT bf16 -> bf16, N % 128 == 0, K % 64 == 0; by default
+  // for K <= 512 and M >= 16384 (the output-heavy 1x1 convolutions and their input gradients)
+  {
+    const int sk = getenv_stream();
+    const long long ab = ((long long)(g.M - 1) * g.lda + g.K) * 2, bb = ((long long)(g.N - 1) * g.ldb + g.K) * 2;
+    const long long cbytes = (long long)g.M * g.ldc * 2;
+    const bool st_ok = sk != 0 && !g.fp8 && g.conv == 0 && !g.ta && !g.tb && g.splits == 1 && g.wperm_T <= 0 &&
+                       g.orow_S <= 0 && !g.bnb_part && g.beta == 0.f && g.out_bf16 && g.N % 128 == 0 &&
+                       g.N <= 2048 && g.K % 64 == 0 && g.K > 0 && g.M > 0 && g.lda % 8 == 0 && g.ldb % 8 == 0 &&
+                       g.ldc % 8 == 0 && g.lda >= g.K && g.ldb >= g.K && g.ldc >= g.N &&
+                       ((uintptr_t)g.A & 15) == 0 && ((uintptr_t)g.B & 15) == 0 && ((uintptr_t)g.C & 15) == 0 &&
+                       ab < (1LL << 31) && bb < (1LL << 31) && cbytes < (1LL << 31) &&
+                       (long long)((g.M + GBM - 1) / GBM) * g.N * 8 < (1LL << 31) &&
+                       (sk == 1 || (g.K <= 512 && g.M >= 16384));
+    if (st_ok) {
+      static int ncu = 0;
+      if (!ncu) {
+        int dev = 0;
+        OPCK(hipGetDevice(&dev));
+        OPCK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
+      }
+      const long tiles = (long)((g.M + GBM - 1) / GBM) * (g.N / GBM);
+      long grid = std::min<long>(2L * ncu, (tiles + 7) / 8 * 8);  // two resident workgroups per CU
+      grid = std::max<long>(8, grid / 8 * 8);
+      const int lds = 2 * ST_BUF + 2 * g.N * 4;
+      // output stores non-temporal by default (802816 x 256 x 64: 175 -> 157 us); DCA_OPS_STREAM_CPOL=0 plain
+      if (getenv_stream_cpol() == 2) hipLaunchKernelGGL(k_gemm_stream<2>, dim3((unsigned)grid), dim3(ST_NT), lds, st, g);
+      else hipLaunchKernelGGL(k_gemm_stream<0>, dim3((unsigned)grid), dim3(ST_NT), lds, st, g);
+      OPCK(hipGetLastError());
+      return 0;
+    }
   }
   // ping-pong 256 x 256 kernel: bf16, K-contiguous operands (plain or the C % 64 implicit conv), no split-K / row
   // remap / fused BN-backward statistics, 16-B aligned rows, operands addressable with 32-bit offsets

@@ -1172,6 +1172,164 @@ __global__ void __launch_bounds__(PP_NT) k_gemm_pp(GemmArgs g) {
   }
 }
 
+// ---------------------------------------------------------------------------------------------------------
+// k_gemm_stream: persistent kernel for the short-K, output-heavy GEMMs of channels-last 1x1 convolutions (ResNet-50
+// at batch 256: M = 5e4..8e5 pixels, N = 128..2048, K = 64..256).  Those calls move ~3x more bytes out than in and
+// have 1-4 K-tiles per 128 x 128 tile, so the one-tile-per-workgroup kernels serialise load -> MFMA -> LDS-staged
+// epilogue and reach 1.6-2.8 TB/s (profiles/gemm_shortk_r2.log).  Here a workgroup walks a static list of tiles as
+// one flat stream of K-tiles, double-buffered by LDS-DMA, so the next tile's operands are in flight during this
+// tile's MFMAs and epilogue.
+//   * 4 waves, each 128 (M) x 32 (N).  The MFMA operands are swapped (weights = src0, activations = src1), so a
+//     lane's accumulators are consecutive output COLUMNS of one row, and the 32 weight rows of a wave slab are
+//     staged in LDS in the order n = 8 (i >> 2) + 4 f + (i & 3) (fragment f, MFMA row i): lane (q, j) then holds
+//     columns 8q .. 8q + 7 of row j of every 16-row fragment -- one 16-B bf16 store per row, no LDS staging.
+//   * Epilogue straight from registers: alpha, bias, ReLU, bf16, buffer stores (rows past M dropped by the
+//     descriptor); the BN column statistics are summed over the wave's 128 rows in registers and 16-lane xor
+//     shuffles and written by lane j = 0 to col_stats[tm][n] (same layout as the other kernels).
+//   * vmcnt is in issue order for loads, stores and LDS-DMA alike: after an epilogue the wait is vmcnt(12) (its
+//     8 C + 4 statistics stores stay in flight) before the next tile's DMA is issued.
+//   * XCD-aware static schedule: workgroup b runs on XCD b % 8; XCD x owns tiles [x T / 8, (x + 1) T / 8) in the
+//     grouped order, dealt round-robin to its workgroups, so its co-resident tiles share A row-tiles in its L2.
+// Requirements (checked by the launcher): bf16 NT operands, N % 128 == 0, K % 64 == 0, bf16 output, beta == 0,
+// 16-B aligned rows, operand / output byte ranges < 2^31.
+// ---------------------------------------------------------------------------------------------------------
+constexpr int ST_NT = 256;
+constexpr int ST_BUF = 2 * G_TILE_BYTES;  // A + B tile, 128 rows x 128 B each
+constexpr int ST_NST = 12;                // stores per epilogue and lane: 8 output rows + 4 x 16 B of statistics
+typedef unsigned st_v4u __attribute__((ext_vector_type(4)));
+
+template <int CPOL>
+__global__ void __launch_bounds__(ST_NT) k_gemm_stream(GemmArgs g) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  constexpr unsigned OOB = 0x80000000u;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, j = lane & 15, q = lane >> 4;
+  const int ntm = (g.M + GBM - 1) / GBM, ntn = g.N / GBM, T = ntm * ntn, nk = g.K / 64;
+  float* sbias = (float*)(smem + 2 * ST_BUF);  // [N] bias | [N] statistics shift
+  float* sshift = sbias + g.N;
+  for (int c = threadIdx.x; c < g.N; c += ST_NT) {
+    sbias[c] = g.bias ? g.bias[c] : 0.f;
+    sshift[c] = g.col_stats ? g.stats_shift[c] : 0.f;
+  }
+  const float alpha = gemm_alpha(g);
+  __syncthreads();  // (also drains these loads: the pipeline's vmcnt accounting starts from zero)
+  const int nxwg = gridDim.x >> 3, xcd = blockIdx.x & 7, loc = blockIdx.x >> 3;
+  const int t_beg = (int)((long long)xcd * T / 8), t_end = (int)((long long)(xcd + 1) * T / 8);
+  const int my_tiles = t_end - t_beg > loc ? (t_end - t_beg - loc + nxwg - 1) / nxwg : 0;
+  const int steps = my_tiles * nk;
+  const __amdgpu_buffer_rsrc_t ars = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)g.A, (short)0, (int)(((long long)(g.M - 1) * g.lda + g.K) * 2), 0x00020000);
+  const __amdgpu_buffer_rsrc_t brs = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)g.B, (short)0, (int)(((long long)(g.N - 1) * g.ldb + g.K) * 2), 0x00020000);
+  const __amdgpu_buffer_rsrc_t crs = __builtin_amdgcn_make_buffer_rsrc(
+      g.C, (short)0, (int)((long long)g.M * g.ldc * 2), 0x00020000);
+  const __amdgpu_buffer_rsrc_t srs = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)g.col_stats, (short)0, g.col_stats ? (int)((long long)ntm * g.N * 8) : 0, 0x00020000);
+  const unsigned lda2 = (unsigned)g.lda * 2u, ldb2 = (unsigned)g.ldb * 2u;
+
+  auto issue = [&](int s) {
+    const int k = s / nk, kt = s - k * nk;
+    int tm, tn;
+    tile_coords(t_beg + loc + k * nxwg, ntm, ntn, tm, tn);
+    char* la = smem + (s & 1) * ST_BUF;
+    char* lb = la + G_TILE_BYTES;
+    const unsigned kb0 = (unsigned)kt * 128u;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int r = 32 * w + 8 * i + (lane >> 3);  // LDS row of this lane's chunk (A and B)
+      const unsigned cb = (unsigned)((lane & 7) ^ ((r >> 1) & 7)) << 4;
+      const int m = tm * GBM + r;
+      blds16(ars, la + (32 * w + 8 * i) * 128, m < g.M ? (unsigned)m * lda2 + cb : OOB, kb0);
+      const int jj = 8 * (i & 1) + (lane >> 3);  // LDS row 32w + 16f + jj holds weight row 8 (jj >> 2) + 4f + (jj & 3)
+      const int n = tn * GBM + 32 * w + 8 * (jj >> 2) + 4 * (i >> 1) + (jj & 3);
+      blds16(brs, lb + (32 * w + 8 * i) * 128, (unsigned)n * ldb2 + cb, kb0);
+    }
+  };
+
+  f32x4 acc[8][2];
+#pragma unroll
+  for (int m = 0; m < 8; ++m) acc[m][0] = acc[m][1] = f32x4{0.f, 0.f, 0.f, 0.f};
+  bool after_epi = false;
+  if (steps > 0) issue(0);
+  for (int s = 0; s < steps; ++s) {
+    if (after_epi) {  // outstanding: this step's DMA, then the previous epilogue's stores
+      wait_vmcnt<ST_NST>();
+      if (s + 1 < steps) issue(s + 1);
+    } else if (s + 1 < steps) {
+      issue(s + 1);
+      wait_vmcnt<8>();
+    } else {
+      wait_vmcnt<0>();
+    }
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    const char* la = smem + (s & 1) * ST_BUF;
+    const char* lb = la + G_TILE_BYTES;
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2) {
+      s16x8 xf[8], wf[2];
+#pragma unroll
+      for (int m = 0; m < 8; ++m) xf[m] = *(const s16x8*)(la + lds_off(16 * m + j, 4 * s2 + q));
+#pragma unroll
+      for (int f = 0; f < 2; ++f) wf[f] = *(const s16x8*)(lb + lds_off(32 * w + 16 * f + j, 4 * s2 + q));
+#pragma unroll
+      for (int m = 0; m < 8; ++m)
+#pragma unroll
+        for (int f = 0; f < 2; ++f) acc[m][f] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[f], xf[m], acc[m][f], 0, 0, 0);
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();  // every wave is done reading this buffer before it is refilled
+    asm volatile("" ::: "memory");
+    const int k = s / nk;
+    after_epi = s - k * nk == nk - 1;
+    if (!after_epi) continue;
+    // ---- epilogue of tile k: lane (q, j) owns columns c0 .. c0 + 7 of rows tm*128 + 16 m + j
+    int tm, tn;
+    tile_coords(t_beg + loc + k * nxwg, ntm, ntn, tm, tn);
+    const int c0 = tn * GBM + 32 * w + 8 * q;
+    float b8[8], sh8[8], s1[8], s2v[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      b8[e] = sbias[c0 + e];
+      sh8[e] = sshift[c0 + e];
+      s1[e] = s2v[e] = 0.f;
+    }
+#pragma unroll
+    for (int m = 0; m < 8; ++m) {
+      const int row = tm * GBM + 16 * m + j;
+      unsigned short h[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        float x = acc[m][e >> 2][e & 3] * alpha + b8[e];
+        if (g.relu) x = x > 0.f ? x : 0.f;
+        h[e] = f2bf_rne(x);
+        const float d = row < g.M ? bf2f(h[e]) - sh8[e] : 0.f;  // statistics of the values as stored
+        s1[e] += d;
+        s2v[e] += d * d;
+      }
+      const st_v4u pk = st_v4u{h[0] | ((unsigned)h[1] << 16), h[2] | ((unsigned)h[3] << 16),
+                               h[4] | ((unsigned)h[5] << 16), h[6] | ((unsigned)h[7] << 16)};
+      __builtin_amdgcn_raw_buffer_store_b128(pk, crs, row < g.M ? ((unsigned)row * (unsigned)g.ldc + c0) * 2u : OOB,
+                                             0, CPOL);
+      acc[m][0] = acc[m][1] = f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+#pragma unroll
+      for (int x = 1; x < 16; x <<= 1) {
+        s1[e] += __shfl_xor(s1[e], x);
+        s2v[e] += __shfl_xor(s2v[e], x);
+      }
+    }
+    const unsigned so = j == 0 ? ((unsigned)tm * (unsigned)g.N + c0) * 8u : OOB;
+#pragma unroll
+    for (int p = 0; p < 4; ++p)
+      __builtin_amdgcn_raw_buffer_store_b128(
+          st_v4u{__float_as_uint(s1[2 * p]), __float_as_uint(s2v[2 * p]), __float_as_uint(s1[2 * p + 1]),
+                 __float_as_uint(s2v[2 * p + 1])},
+          srs, so + 16u * p, 0, 0);
+  }
+}
+
 // Split-K combine: C = alpha * sum_s ws[s] (+bias) (+beta*C) (ReLU).  256 threads = 64 consecutive elements x 4
 // split lanes (lane l sums slabs l, l+4, ...; the 4 partials are added in lane order: deterministic), so
 // thousands of slabs of a small weight gradient are read by many threads with 256-B row segments.

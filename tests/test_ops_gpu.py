@@ -52,6 +52,23 @@ def test_gemm_pingpong_matches_torch(gpu):
     assert not bad, (bad, res)
 
 
+def test_gemm_stream_matches_torch(gpu):
+    """The persistent short-K GEMM (DCA_OPS_STREAM=1, read once per process: run in a child) on plain NT shapes
+    with M tails, 1-8 K-tiles, padded strides, bias + ReLU and the fused BN column statistics, against torch fp32;
+    plus an exact layout check (A = I)."""
+    import json
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([sys.executable, os.path.join(root, "tests", "_stream_check.py")], capture_output=True,
+                       text=True, env=dict(os.environ, DCA_OPS_STREAM="1"), timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    res = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
+    assert res.pop("identity_exact_err") == 0.0, res
+    bad = {k: v for k, v in res.items() if not v <= 1e-2}
+    assert not bad, (bad, res)
+
+
 def test_gemm_identity_layout(gpu):
     """A = I with an asymmetric B must return B^T exactly (catches row/col swaps in the C write)."""
     from distributeddataparallel_cifar10_amd.ops import gemm
