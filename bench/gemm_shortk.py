@@ -36,14 +36,19 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--no-stats", action="store_true")
     ap.add_argument("--tag", default=os.environ.get("DCA_TAG", "default"))
+    ap.add_argument("--shape", default=None, help="MxNxK: only this shape")
+    ap.add_argument("--beta", action="store_true", help="accumulate into the output (C += A B^T), no statistics")
     a = ap.parse_args()
+    shapes = [tuple(int(v) for v in a.shape.split("x"))] if a.shape else SHAPES
     dev = torch.device("cuda", 0)
     bf = torch.bfloat16
-    for M, N, K in SHAPES:
+    for M, N, K in shapes:
         x = torch.randn(M, K, device=dev).to(bf)
         w = torch.randn(N, K, device=dev).to(bf)
         kw = {}
-        if not a.no_stats:
+        if a.beta:
+            kw = dict(out=torch.zeros(M, N, device=dev, dtype=bf), beta=1.0)
+        elif not a.no_stats:
             kw = dict(col_stats=torch.zeros((M + 127) // 128, N, 2, device=dev),
                       stats_shift=torch.zeros(N, device=dev))
         y = ops.gemm(x, w, out_dtype=bf, **kw)
@@ -51,9 +56,9 @@ def main():
         err = ((y.float() - ref).norm() / ref.norm()).item()
         us = timeit(lambda: ops.gemm(x, w, out_dtype=bf, **kw))
         floor_us = 2 * (M * K + M * N) / 5.0e6  # at 5 TB/s
-        print(json.dumps({"tag": a.tag, "shape": f"{M}x{N}x{K}", "stats": not a.no_stats, "us": round(us, 1),
+        print(json.dumps({"tag": a.tag, "shape": f"{M}x{N}x{K}", "stats": not a.no_stats and not a.beta, "beta": a.beta, "us": round(us, 1),
                           "tflops": round(2 * M * N * K / us / 1e6, 1),
-                          "gbps": round(2 * (M * K + M * N) / us / 1e3, 1), "floor_us_5tbs": round(floor_us, 1),
+                          "gbps": round(2 * (M * K + (2 if a.beta else 1) * M * N) / us / 1e3, 1), "floor_us_5tbs": round(floor_us, 1),
                           "rel_err": round(err, 5)}), flush=True)
         del x, w, y, ref
 

@@ -272,19 +272,20 @@ int dca_ops_gemm(const GemmArgs* a, void* stream) {
     return 0;
   }
   // persistent short-K stream kernel (k_gemm_stream): plain NT bf16 -> bf16, N % 128 == 0, K % 64 == 0; by default
-  // for K <= 512 and M >= 16384 (the output-heavy 1x1 convolutions and their input gradients)
+  // for K <= 512 and M >= 16384, accumulating (beta) calls only for K <= 128 (profiles/gemm_shortk_r2.log)
+  // (the output-heavy 1x1 convolutions and their input gradients)
   {
     const int sk = getenv_stream();
     const long long ab = ((long long)(g.M - 1) * g.lda + g.K) * 2, bb = ((long long)(g.N - 1) * g.ldb + g.K) * 2;
     const long long cbytes = (long long)g.M * g.ldc * 2;
     const bool st_ok = sk != 0 && !g.fp8 && g.conv == 0 && !g.ta && !g.tb && g.splits == 1 && g.wperm_T <= 0 &&
-                       g.orow_S <= 0 && !g.bnb_part && g.beta == 0.f && g.out_bf16 && g.N % 128 == 0 &&
+                       g.orow_S <= 0 && !g.bnb_part && !g.relu && g.out_bf16 && g.N % 128 == 0 &&
                        g.N <= 2048 && g.K % 64 == 0 && g.K > 0 && g.M > 0 && g.lda % 8 == 0 && g.ldb % 8 == 0 &&
                        g.ldc % 8 == 0 && g.lda >= g.K && g.ldb >= g.K && g.ldc >= g.N &&
                        ((uintptr_t)g.A & 15) == 0 && ((uintptr_t)g.B & 15) == 0 && ((uintptr_t)g.C & 15) == 0 &&
                        ab < (1LL << 31) && bb < (1LL << 31) && cbytes < (1LL << 31) &&
                        (long long)((g.M + GBM - 1) / GBM) * g.N * 8 < (1LL << 31) &&
-                       (sk == 1 || (g.K <= 512 && g.M >= 16384));
+                       (sk == 1 || (g.K <= 512 && g.M >= 16384 && (g.beta == 0.f || g.K <= 128)));
     if (st_ok) {
       static int ncu = 0;
       if (!ncu) {
@@ -293,7 +294,9 @@ int dca_ops_gemm(const GemmArgs* a, void* stream) {
         OPCK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
       }
       const long tiles = (long)((g.M + GBM - 1) / GBM) * (g.N / GBM);
-      long grid = std::min<long>(2L * ncu, (tiles + 7) / 8 * 8);  // two resident workgroups per CU
+      static const int dbg = getenv("DCA_OPS_STREAM_DBG") ? atoi(getenv("DCA_OPS_STREAM_DBG")) : 0;
+      g.single = dbg;
+      long grid = std::min<long>((dbg & 1 ? 1L : 2L) * ncu, (tiles + 7) / 8 * 8);  // two resident workgroups per CU
       grid = std::max<long>(8, grid / 8 * 8);
       const int lds = 2 * ST_BUF + 2 * g.N * 4;
       // output stores non-temporal by default (802816 x 256 x 64: 175 -> 157 us); DCA_OPS_STREAM_CPOL=0 plain

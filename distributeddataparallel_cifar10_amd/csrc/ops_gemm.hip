@@ -20,6 +20,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <type_traits>
+
 namespace dca {
 namespace ops {
 
@@ -1183,14 +1185,16 @@ __global__ void __launch_bounds__(PP_NT) k_gemm_pp(GemmArgs g) {
 //     lane's accumulators are consecutive output COLUMNS of one row, and the 32 weight rows of a wave slab are
 //     staged in LDS in the order n = 8 (i >> 2) + 4 f + (i & 3) (fragment f, MFMA row i): lane (q, j) then holds
 //     columns 8q .. 8q + 7 of row j of every 16-row fragment -- one 16-B bf16 store per row, no LDS staging.
-//   * Epilogue straight from registers: alpha, bias, ReLU, bf16, buffer stores (rows past M dropped by the
-//     descriptor); the BN column statistics are summed over the wave's 128 rows in registers and 16-lane xor
-//     shuffles and written by lane j = 0 to col_stats[tm][n] (same layout as the other kernels).
+//   * Epilogue straight from registers: alpha, bias, + beta * C_old (the residual-join input gradients),
+//     bf16 (packed cvt), buffer stores (rows past M dropped by the
+//     descriptor); the BN column statistics are summed over the wave's 128 rows in packed-fp32 registers and a
+//     16-lane DPP row reduction, and written by lane j = 15 to col_stats[tm][n] (same layout as the other kernels).
+//     The accumulators start from the MFMA's zero C operand on a tile's first K-tile (no per-tile clearing).
 //   * vmcnt is in issue order for loads, stores and LDS-DMA alike: after an epilogue the wait is vmcnt(12) (its
 //     8 C + 4 statistics stores stay in flight) before the next tile's DMA is issued.
 //   * XCD-aware static schedule: workgroup b runs on XCD b % 8; XCD x owns tiles [x T / 8, (x + 1) T / 8) in the
 //     grouped order, dealt round-robin to its workgroups, so its co-resident tiles share A row-tiles in its L2.
-// Requirements (checked by the launcher): bf16 NT operands, N % 128 == 0, K % 64 == 0, bf16 output, beta == 0,
+// Requirements (checked by the launcher): bf16 NT operands, N % 128 == 0, K % 64 == 0, bf16 output, no ReLU,
 // 16-B aligned rows, operand / output byte ranges < 2^31.
 // ---------------------------------------------------------------------------------------------------------
 constexpr int ST_NT = 256;
@@ -1245,24 +1249,18 @@ __global__ void __launch_bounds__(ST_NT) k_gemm_stream(GemmArgs g) {
     }
   };
 
+  // DPP sum over the 16 lanes of a row (lane j = 15 of each row ends with the total)
+  auto rowsum16 = [](float x) {
+    x += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, x), 0x111, 0xf, 0xf, true));
+    x += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, x), 0x112, 0xf, 0xf, true));
+    x += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, x), 0x114, 0xf, 0xf, true));
+    x += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, x), 0x118, 0xf, 0xf, true));
+    return x;
+  };
   f32x4 acc[8][2];
-#pragma unroll
-  for (int m = 0; m < 8; ++m) acc[m][0] = acc[m][1] = f32x4{0.f, 0.f, 0.f, 0.f};
-  bool after_epi = false;
-  if (steps > 0) issue(0);
-  for (int s = 0; s < steps; ++s) {
-    if (after_epi) {  // outstanding: this step's DMA, then the previous epilogue's stores
-      wait_vmcnt<ST_NST>();
-      if (s + 1 < steps) issue(s + 1);
-    } else if (s + 1 < steps) {
-      issue(s + 1);
-      wait_vmcnt<8>();
-    } else {
-      wait_vmcnt<0>();
-    }
-    __builtin_amdgcn_s_barrier();
-    asm volatile("" ::: "memory");
-    const char* la = smem + (s & 1) * ST_BUF;
+  // one K-tile from LDS buffer `buf`; FIRST: the tile's first K-tile (accumulators start from the MFMA's zero C)
+  auto compute = [&](int buf, auto first) {
+    const char* la = smem + buf * ST_BUF;
     const char* lb = la + G_TILE_BYTES;
 #pragma unroll
     for (int s2 = 0; s2 < 2; ++s2) {
@@ -1274,59 +1272,123 @@ __global__ void __launch_bounds__(ST_NT) k_gemm_stream(GemmArgs g) {
 #pragma unroll
       for (int m = 0; m < 8; ++m)
 #pragma unroll
-        for (int f = 0; f < 2; ++f) acc[m][f] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[f], xf[m], acc[m][f], 0, 0, 0);
+        for (int f = 0; f < 2; ++f)
+          acc[m][f] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+              wf[f], xf[m], (decltype(first)::value && s2 == 0) ? f32x4{0.f, 0.f, 0.f, 0.f} : acc[m][f], 0, 0, 0);
     }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();  // every wave is done reading this buffer before it is refilled
-    asm volatile("" ::: "memory");
-    const int k = s / nk;
-    after_epi = s - k * nk == nk - 1;
-    if (!after_epi) continue;
-    // ---- epilogue of tile k: lane (q, j) owns columns c0 .. c0 + 7 of rows tm*128 + 16 m + j
-    int tm, tn;
-    tile_coords(t_beg + loc + k * nxwg, ntm, ntn, tm, tn);
+  };
+  // epilogue of tile (tm, tn): lane (q, j) owns columns c0 .. c0 + 7 of rows tm*128 + 16 m + j.  FULL: no row past M.
+  st_v4u old[8];  // beta != 0: this tile's C_old rows (lane (q, j): row 16 m + j, columns c0 .. c0 + 7)
+  auto load_old = [&](int tm, int tn) {
     const int c0 = tn * GBM + 32 * w + 8 * q;
-    float b8[8], sh8[8], s1[8], s2v[8];
 #pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      b8[e] = sbias[c0 + e];
-      sh8[e] = sshift[c0 + e];
-      s1[e] = s2v[e] = 0.f;
+    for (int m = 0; m < 8; ++m) {
+      const int row = tm * GBM + 16 * m + j;
+      old[m] = __builtin_amdgcn_raw_buffer_load_b128(
+          crs, row < g.M ? ((unsigned)row * (unsigned)g.ldc + c0) * 2u : OOB, 0, 0);
+    }
+  };
+  // more: the DMA of the next step was issued after the C_old loads (still in flight)
+  auto epilogue = [&](int tm, int tn, bool more, auto full, auto acc_old) {
+    constexpr bool FULL = decltype(full)::value, BETA = decltype(acc_old)::value;
+    const int c0 = tn * GBM + 32 * w + 8 * q;
+    if constexpr (BETA) {  // C_old was loaded ahead of the tile's last K-step, before the DMA of the next step
+      if (more) wait_vmcnt<8>();
+      else wait_vmcnt<0>();
+    }
+    typedef float f2 __attribute__((ext_vector_type(2)));
+    f2 b2[4], sh2[4], s1[4], sq[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      b2[e] = *(const f2*)(sbias + c0 + 2 * e);
+      sh2[e] = *(const f2*)(sshift + c0 + 2 * e);
+      s1[e] = sq[e] = f2{0.f, 0.f};
     }
 #pragma unroll
     for (int m = 0; m < 8; ++m) {
       const int row = tm * GBM + 16 * m + j;
-      unsigned short h[8];
+      const bool in = FULL || row < g.M;
+      unsigned pk[4];
 #pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        float x = acc[m][e >> 2][e & 3] * alpha + b8[e];
-        if (g.relu) x = x > 0.f ? x : 0.f;
-        h[e] = f2bf_rne(x);
-        const float d = row < g.M ? bf2f(h[e]) - sh8[e] : 0.f;  // statistics of the values as stored
+      for (int e = 0; e < 4; ++e) {  // columns 2e, 2e + 1 = fragment e >> 1, elements 2 (e & 1) + {0, 1}
+        const f32x4& a = acc[m][e >> 1];
+        f2 x = f2{a[2 * (e & 1)], a[2 * (e & 1) + 1]} * alpha + b2[e];
+        if constexpr (BETA)
+          x += f2{__uint_as_float(old[m][e] << 16), __uint_as_float(old[m][e] & 0xffff0000u)} * g.beta;
+        typedef __bf16 bf2 __attribute__((ext_vector_type(2)));
+        pk[e] = __builtin_bit_cast(unsigned, __builtin_convertvector(x, bf2));
+        // statistics of the values as stored (bf16)
+        f2 d = f2{__uint_as_float(pk[e] << 16), __uint_as_float(pk[e] & 0xffff0000u)} - sh2[e];
+        if (!FULL && !in) d = f2{0.f, 0.f};
         s1[e] += d;
-        s2v[e] += d * d;
+        sq[e] += d * d;
       }
-      const st_v4u pk = st_v4u{h[0] | ((unsigned)h[1] << 16), h[2] | ((unsigned)h[3] << 16),
-                               h[4] | ((unsigned)h[5] << 16), h[6] | ((unsigned)h[7] << 16)};
-      __builtin_amdgcn_raw_buffer_store_b128(pk, crs, row < g.M ? ((unsigned)row * (unsigned)g.ldc + c0) * 2u : OOB,
+      __builtin_amdgcn_raw_buffer_store_b128(st_v4u{pk[0], pk[1], pk[2], pk[3]}, crs,
+                                             in && !(g.single & 2) ? ((unsigned)row * (unsigned)g.ldc + c0) * 2u : OOB,
                                              0, CPOL);
-      acc[m][0] = acc[m][1] = f32x4{0.f, 0.f, 0.f, 0.f};
     }
+    float r1[8], r2[8];
 #pragma unroll
-    for (int e = 0; e < 8; ++e) {
-#pragma unroll
-      for (int x = 1; x < 16; x <<= 1) {
-        s1[e] += __shfl_xor(s1[e], x);
-        s2v[e] += __shfl_xor(s2v[e], x);
-      }
+    for (int e = 0; e < 4; ++e) {
+      r1[2 * e] = rowsum16(s1[e][0]);
+      r1[2 * e + 1] = rowsum16(s1[e][1]);
+      r2[2 * e] = rowsum16(sq[e][0]);
+      r2[2 * e + 1] = rowsum16(sq[e][1]);
     }
-    const unsigned so = j == 0 ? ((unsigned)tm * (unsigned)g.N + c0) * 8u : OOB;
+    const unsigned so = j == 15 ? ((unsigned)tm * (unsigned)g.N + c0) * 8u : OOB;
 #pragma unroll
     for (int p = 0; p < 4; ++p)
       __builtin_amdgcn_raw_buffer_store_b128(
-          st_v4u{__float_as_uint(s1[2 * p]), __float_as_uint(s2v[2 * p]), __float_as_uint(s1[2 * p + 1]),
-                 __float_as_uint(s2v[2 * p + 1])},
+          st_v4u{__float_as_uint(r1[2 * p]), __float_as_uint(r2[2 * p]), __float_as_uint(r1[2 * p + 1]),
+                 __float_as_uint(r2[2 * p + 1])},
           srs, so + 16u * p, 0, 0);
+  };
+
+  // the stream: step s = (tile k, K-tile kt), s = k * nk + kt; DMA of step s + 1 in flight during step s
+  // beta != 0: the tile's C_old rows are loaded at the top of its last K-step, ahead of the next step's DMA, so
+  // their latency hides under that step's MFMAs
+  const bool bta = g.beta != 0.f;
+  if (steps > 0) issue(0);
+  for (int k = 0; k < my_tiles; ++k) {
+    int tm, tn;
+    tile_coords(t_beg + loc + k * nxwg, ntm, ntn, tm, tn);
+    for (int kt = 0; kt < nk; ++kt) {
+      const int s = k * nk + kt;
+      const bool lo = bta && kt == nk - 1;
+      if (kt == 0 && k > 0) {  // outstanding: this step's DMA, then the previous epilogue's stores
+        wait_vmcnt<ST_NST>();
+        if (lo) load_old(tm, tn);
+        if (s + 1 < steps) issue(s + 1);
+      } else if (lo) {  // outstanding: this step's DMA | C_old (8) | next DMA (8)
+        load_old(tm, tn);
+        if (s + 1 < steps) {
+          issue(s + 1);
+          wait_vmcnt<16>();
+        } else {
+          wait_vmcnt<8>();
+        }
+      } else if (s + 1 < steps) {
+        issue(s + 1);
+        wait_vmcnt<8>();
+      } else {
+        wait_vmcnt<0>();
+      }
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+      if (kt == 0) compute(s & 1, std::true_type{});
+      else compute(s & 1, std::false_type{});
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();  // every wave is done reading this buffer before it is refilled
+      asm volatile("" ::: "memory");
+    }
+    const bool full = tm * GBM + GBM <= g.M, more = (k + 1) * nk < steps;
+    if (bta) {
+      if (full) epilogue(tm, tn, more, std::true_type{}, std::true_type{});
+      else epilogue(tm, tn, more, std::false_type{}, std::true_type{});
+    } else {
+      if (full) epilogue(tm, tn, more, std::true_type{}, std::false_type{});
+      else epilogue(tm, tn, more, std::false_type{}, std::false_type{});
+    }
   }
 }
 

@@ -1,6 +1,6 @@
 """Run under DCA_OPS_STREAM=1 (tests/test_ops_gpu.py::test_gemm_stream_matches_torch): the persistent short-K GEMM
 (csrc/ops_gemm.hip k_gemm_stream) against torch fp32 on plain NT shapes -- M tails, one to eight K-tiles, padded
-row strides, bias + ReLU, the fused BN column statistics -- and the exact layout check (A = I).  One JSON line."""
+row strides, bias, beta accumulation, the fused BN column statistics -- and the exact layout check (A = I).  One JSON line."""
 import json
 import os
 import sys
@@ -28,8 +28,11 @@ def main():
         bias = torch.randn(N, device=dev, generator=g)
         ref = a.float() @ b.float().t()
         out[f"nt{M}x{N}x{K}_bf16"] = rel(ops.gemm(a, b, out_dtype=bf), ref)
-        out[f"nt{M}x{N}x{K}_bf16_bias_relu"] = rel(ops.gemm(a, b, bias=bias, relu=True, out_dtype=bf),
-                                                  torch.relu(ref + bias))
+        out[f"nt{M}x{N}x{K}_bf16_bias"] = rel(ops.gemm(a, b, bias=bias, out_dtype=bf), ref + bias)
+        c0 = torch.randn(M, N, device=dev, generator=g).to(bf)
+        c1 = c0.clone()
+        ops.gemm(a, b, out_dtype=bf, out=c1, beta=1.0)
+        out[f"nt{M}x{N}x{K}_beta"] = rel(c1, ref + c0.float())
         shift = torch.randn(N, device=dev, generator=g) * 0.1
         parts = torch.full(((M + 127) // 128, N, 2), float("nan"), device=dev)
         y = ops.gemm(a, b, out_dtype=bf, col_stats=parts, stats_shift=shift)
