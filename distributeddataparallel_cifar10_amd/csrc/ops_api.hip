@@ -114,11 +114,8 @@ inline int getenv_stream() {  // persistent short-K GEMM (k_gemm_stream): DCA_OP
   }();
   return v;
 }
-inline int getenv_stream_cpol() {
-  static const int v = [] {
-    const char* e = getenv("DCA_OPS_STREAM_CPOL");
-    return e ? atoi(e) : 2;
-  }();
+inline bool getenv_stream_conv() {  // implicit 3x3 convolutions (N = 64 / 128) on k_gemm_stream; DCA_OPS_STREAM_CONV=0 off
+  static const bool v = getenv_flag("DCA_OPS_STREAM_CONV");
   return v;
 }
 inline int getenv_pp() {  // ping-pong 256 x 256 GEMM (k_gemm_pp): DCA_OPS_PP = 0 never, 1 whenever eligible,
@@ -229,9 +226,11 @@ int dca_ops_gemm(const GemmArgs* a, void* stream) {
                              PpTile<256>::LDS));
     OPCK(hipFuncSetAttribute((const void*)k_gemm_pp<128>, hipFuncAttributeMaxDynamicSharedMemorySize,
                              PpTile<128>::LDS));
-    OPCK(hipFuncSetAttribute((const void*)k_gemm_stream<0>, hipFuncAttributeMaxDynamicSharedMemorySize,
+    OPCK(hipFuncSetAttribute((const void*)k_gemm_stream<2, false>, hipFuncAttributeMaxDynamicSharedMemorySize,
                              2 * ST_BUF + 2 * 2048 * 4));
-    OPCK(hipFuncSetAttribute((const void*)k_gemm_stream<2>, hipFuncAttributeMaxDynamicSharedMemorySize,
+    OPCK(hipFuncSetAttribute((const void*)k_gemm_stream<2, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                             2 * ST_BUF + 2 * 2048 * 4));
+    OPCK(hipFuncSetAttribute((const void*)k_gemm_stream<1, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
                              2 * ST_BUF + 2 * 2048 * 4));
     g_lds_set = true;
   }
@@ -271,21 +270,29 @@ int dca_ops_gemm(const GemmArgs* a, void* stream) {
     OPCK(hipGetLastError());
     return 0;
   }
-  // persistent short-K stream kernel (k_gemm_stream): plain NT bf16 -> bf16, N % 128 == 0, K % 64 == 0; by default
-  // for K <= 512 and M >= 16384, accumulating (beta) calls only for K <= 128 (profiles/gemm_shortk_r2.log)
-  // (the output-heavy 1x1 convolutions and their input gradients)
+  // persistent stream kernel (k_gemm_stream), bf16 -> bf16, K % 64 == 0, no split / remap / ReLU:
+  //   plain NT, N % 128 == 0: by default for K <= 512 and M >= 16384, accumulating (beta) calls only for K <= 128
+  //     (the output-heavy 1x1 convolutions and their input gradients; profiles/gemm_shortk_r2.log);
+  //   implicit conv with C % 64 == 0, N = 128: M >= 16384 (ResNet-50's layer-2 3x3 convolutions and their input
+  //     gradients: 129.5 -> 117.9 us at batch 256); N = 64 only when forced (DCA_OPS_STREAM=1): its 16-column waves
+  //     read 9 fragments per 8 MFMAs from LDS and lose to the one-tile kernel (218.5 vs 176.4 us)
   {
     const int sk = getenv_stream();
-    const long long ab = ((long long)(g.M - 1) * g.lda + g.K) * 2, bb = ((long long)(g.N - 1) * g.ldb + g.K) * 2;
+    const bool conv = g.conv == 1;
+    const long long ab = conv ? (long long)g.cN * g.cH * g.cW * g.cC * 2 : ((long long)(g.M - 1) * g.lda + g.K) * 2;
+    const long long bb = ((long long)(g.N - 1) * g.ldb + g.K) * 2;
     const long long cbytes = (long long)g.M * g.ldc * 2;
-    const bool st_ok = sk != 0 && !g.fp8 && g.conv == 0 && !g.ta && !g.tb && g.splits == 1 && g.wperm_T <= 0 &&
-                       g.orow_S <= 0 && !g.bnb_part && !g.relu && g.out_bf16 && g.N % 128 == 0 &&
-                       g.N <= 2048 && g.K % 64 == 0 && g.K > 0 && g.M > 0 && g.lda % 8 == 0 && g.ldb % 8 == 0 &&
-                       g.ldc % 8 == 0 && g.lda >= g.K && g.ldb >= g.K && g.ldc >= g.N &&
+    const int nf = g.N % 128 == 0 ? 2 : 1;
+    const bool shape_ok = conv ? (g.cC % 64 == 0 && g.cKH * g.cKW <= 32 && (g.N == 64 || g.N == 128) && g.orow_S <= 0 &&
+                                  (sk == 1 || (sk == 2 && getenv_stream_conv() && g.N == 128 && g.M >= 16384)))
+                               : (g.conv == 0 && !g.ta && g.N % 128 == 0 && g.lda % 8 == 0 && g.lda >= g.K &&
+                                  (sk == 1 || (g.K <= 512 && g.M >= 16384 && (g.beta == 0.f || g.K <= 128))));
+    const bool st_ok = sk != 0 && shape_ok && !g.fp8 && !g.tb && g.splits == 1 && g.wperm_T <= 0 && g.orow_S <= 0 &&
+                       !g.bnb_part && !g.relu && g.out_bf16 && g.N % 64 == 0 && g.N <= 2048 && g.K % 64 == 0 &&
+                       g.K > 0 && g.M > 0 && g.ldb % 8 == 0 && g.ldc % 8 == 0 && g.ldb >= g.K && g.ldc >= g.N &&
                        ((uintptr_t)g.A & 15) == 0 && ((uintptr_t)g.B & 15) == 0 && ((uintptr_t)g.C & 15) == 0 &&
                        ab < (1LL << 31) && bb < (1LL << 31) && cbytes < (1LL << 31) &&
-                       (long long)((g.M + GBM - 1) / GBM) * g.N * 8 < (1LL << 31) &&
-                       (sk == 1 || (g.K <= 512 && g.M >= 16384 && (g.beta == 0.f || g.K <= 128)));
+                       (long long)((g.M + GBM - 1) / GBM) * g.N * 8 < (1LL << 31);
     if (st_ok) {
       static int ncu = 0;
       if (!ncu) {
@@ -293,15 +300,17 @@ int dca_ops_gemm(const GemmArgs* a, void* stream) {
         OPCK(hipGetDevice(&dev));
         OPCK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
       }
-      const long tiles = (long)((g.M + GBM - 1) / GBM) * (g.N / GBM);
-      static const int dbg = getenv("DCA_OPS_STREAM_DBG") ? atoi(getenv("DCA_OPS_STREAM_DBG")) : 0;
-      g.single = dbg;
-      long grid = std::min<long>((dbg & 1 ? 1L : 2L) * ncu, (tiles + 7) / 8 * 8);  // two resident workgroups per CU
+      const long tiles = (long)((g.M + GBM - 1) / GBM) * (g.N / (64 * nf));
+      long grid = std::min<long>(2L * ncu, (tiles + 7) / 8 * 8);  // two resident workgroups per CU
       grid = std::max<long>(8, grid / 8 * 8);
       const int lds = 2 * ST_BUF + 2 * g.N * 4;
-      // output stores non-temporal by default (802816 x 256 x 64: 175 -> 157 us); DCA_OPS_STREAM_CPOL=0 plain
-      if (getenv_stream_cpol() == 2) hipLaunchKernelGGL(k_gemm_stream<2>, dim3((unsigned)grid), dim3(ST_NT), lds, st, g);
-      else hipLaunchKernelGGL(k_gemm_stream<0>, dim3((unsigned)grid), dim3(ST_NT), lds, st, g);
+      const dim3 gr((unsigned)grid), bl(ST_NT);
+      if (conv) {
+        if (nf == 2) hipLaunchKernelGGL((k_gemm_stream<2, true>), gr, bl, lds, st, g);
+        else hipLaunchKernelGGL((k_gemm_stream<1, true>), gr, bl, lds, st, g);
+      } else {
+        hipLaunchKernelGGL((k_gemm_stream<2, false>), gr, bl, lds, st, g);
+      }
       OPCK(hipGetLastError());
       return 0;
     }

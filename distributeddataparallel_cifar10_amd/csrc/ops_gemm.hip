@@ -1181,7 +1181,7 @@ __global__ void __launch_bounds__(PP_NT) k_gemm_pp(GemmArgs g) {
 // epilogue and reach 1.6-2.8 TB/s (profiles/gemm_shortk_r2.log).  Here a workgroup walks a static list of tiles as
 // one flat stream of K-tiles, double-buffered by LDS-DMA, so the next tile's operands are in flight during this
 // tile's MFMAs and epilogue.
-//   * 4 waves, each 128 (M) x 32 (N).  The MFMA operands are swapped (weights = src0, activations = src1), so a
+//   * 4 waves, each 128 (M) x 32 (N) (or 128 x 16: 64-column tiles).  The MFMA operands are swapped (weights = src0, activations = src1), so a
 //     lane's accumulators are consecutive output COLUMNS of one row, and the 32 weight rows of a wave slab are
 //     staged in LDS in the order n = 8 (i >> 2) + 4 f + (i & 3) (fragment f, MFMA row i): lane (q, j) then holds
 //     columns 8q .. 8q + 7 of row j of every 16-row fragment -- one 16-B bf16 store per row, no LDS staging.
@@ -1190,24 +1190,35 @@ __global__ void __launch_bounds__(PP_NT) k_gemm_pp(GemmArgs g) {
 //     descriptor); the BN column statistics are summed over the wave's 128 rows in packed-fp32 registers and a
 //     16-lane DPP row reduction, and written by lane j = 15 to col_stats[tm][n] (same layout as the other kernels).
 //     The accumulators start from the MFMA's zero C operand on a tile's first K-tile (no per-tile clearing).
-//   * vmcnt is in issue order for loads, stores and LDS-DMA alike: after an epilogue the wait is vmcnt(12) (its
-//     8 C + 4 statistics stores stay in flight) before the next tile's DMA is issued.
+//   * vmcnt is in issue order for loads, stores and LDS-DMA alike: after an epilogue the wait is vmcnt(NST) (its
+//     8 C + statistics stores stay in flight) before the next tile's DMA is issued.
+//   * Implicit convolutions (C % 64 == 0, one tap per K-step) use the same stream: the 3x3 convolutions of
+//     ResNet-50's layers 1-2 (N = 64 / 128) were issue-bound on the one-tile kernel (16 VALU + 12 SALU per MFMA,
+//     profiles/gemm_stream_pmc_r2.txt).
 //   * XCD-aware static schedule: workgroup b runs on XCD b % 8; XCD x owns tiles [x T / 8, (x + 1) T / 8) in the
 //     grouped order, dealt round-robin to its workgroups, so its co-resident tiles share A row-tiles in its L2.
-// Requirements (checked by the launcher): bf16 NT operands, N % 128 == 0, K % 64 == 0, bf16 output, no ReLU,
-// 16-B aligned rows, operand / output byte ranges < 2^31.
+// Requirements (checked by the launcher): bf16 NT operands (or the C % 64 implicit conv), N % 64 == 0 (NF = 1) or
+// N % 128 == 0 (NF = 2), K % 64 == 0, bf16 output, no ReLU, 16-B aligned rows, operand / output byte ranges < 2^31,
+// at most 32 taps.
 // ---------------------------------------------------------------------------------------------------------
 constexpr int ST_NT = 256;
 constexpr int ST_BUF = 2 * G_TILE_BYTES;  // A + B tile, 128 rows x 128 B each
-constexpr int ST_NST = 12;                // stores per epilogue and lane: 8 output rows + 4 x 16 B of statistics
 typedef unsigned st_v4u __attribute__((ext_vector_type(4)));
+typedef unsigned st_v2u __attribute__((ext_vector_type(2)));
 
-template <int CPOL>
-__global__ void __launch_bounds__(ST_NT) k_gemm_stream(GemmArgs g) {
+// NF: 16-column MFMA fragments per wave (2: 128-column tiles, 1: 64-column tiles -- the 64-channel convolutions).
+// CONV: A is the implicit im2col of an NHWC input with C % 64 == 0 (one tap per K-step; per-row tap-validity masks
+// computed once per tile, padding taps load zeros through an offset past the descriptor).
+template <int NF, bool CONV>
+__global__ void __launch_bounds__(ST_NT, 2) k_gemm_stream(GemmArgs g) {
+  constexpr int WN = 16 * NF, TN = 4 * WN;  // columns per wave / per tile
+  constexpr int NBI = WN / 8;               // B DMA instructions per wave and K-step
+  constexpr int NI = 4 + NBI;               // DMA instructions per lane and K-step
+  constexpr int NST = 8 + 2 * NF;           // stores per lane and epilogue: 8 output rows + the statistics
   extern __shared__ __attribute__((aligned(16))) char smem[];
   constexpr unsigned OOB = 0x80000000u;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, j = lane & 15, q = lane >> 4;
-  const int ntm = (g.M + GBM - 1) / GBM, ntn = g.N / GBM, T = ntm * ntn, nk = g.K / 64;
+  const int ntm = (g.M + GBM - 1) / GBM, ntn = g.N / TN, T = ntm * ntn, nk = g.K / 64;
   float* sbias = (float*)(smem + 2 * ST_BUF);  // [N] bias | [N] statistics shift
   float* sshift = sbias + g.N;
   for (int c = threadIdx.x; c < g.N; c += ST_NT) {
@@ -1220,8 +1231,8 @@ __global__ void __launch_bounds__(ST_NT) k_gemm_stream(GemmArgs g) {
   const int t_beg = (int)((long long)xcd * T / 8), t_end = (int)((long long)(xcd + 1) * T / 8);
   const int my_tiles = t_end - t_beg > loc ? (t_end - t_beg - loc + nxwg - 1) / nxwg : 0;
   const int steps = my_tiles * nk;
-  const __amdgpu_buffer_rsrc_t ars = __builtin_amdgcn_make_buffer_rsrc(
-      (void*)g.A, (short)0, (int)(((long long)(g.M - 1) * g.lda + g.K) * 2), 0x00020000);
+  const long long a_bytes = CONV ? (long long)g.cN * g.cH * g.cW * g.cC * 2 : ((long long)(g.M - 1) * g.lda + g.K) * 2;
+  const __amdgpu_buffer_rsrc_t ars = __builtin_amdgcn_make_buffer_rsrc((void*)g.A, (short)0, (int)a_bytes, 0x00020000);
   const __amdgpu_buffer_rsrc_t brs = __builtin_amdgcn_make_buffer_rsrc(
       (void*)g.B, (short)0, (int)(((long long)(g.N - 1) * g.ldb + g.K) * 2), 0x00020000);
   const __amdgpu_buffer_rsrc_t crs = __builtin_amdgcn_make_buffer_rsrc(
@@ -1229,23 +1240,55 @@ __global__ void __launch_bounds__(ST_NT) k_gemm_stream(GemmArgs g) {
   const __amdgpu_buffer_rsrc_t srs = __builtin_amdgcn_make_buffer_rsrc(
       (void*)g.col_stats, (short)0, g.col_stats ? (int)((long long)ntm * g.N * 8) : 0, 0x00020000);
   const unsigned lda2 = (unsigned)g.lda * 2u, ldb2 = (unsigned)g.ldb * 2u;
+  const int cpt = CONV ? g.cC / 64 : 1;  // K-steps per tap
 
+  // issue side: A row offsets (and conv tap masks) of the tile whose K-steps are being issued
+  unsigned aoff[4], amask[4];
+  int itm = 0, itn = 0;
   auto issue = [&](int s) {
     const int k = s / nk, kt = s - k * nk;
-    int tm, tn;
-    tile_coords(t_beg + loc + k * nxwg, ntm, ntn, tm, tn);
+    if (kt == 0) {
+      tile_coords(t_beg + loc + k * nxwg, ntm, ntn, itm, itn);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int r = 32 * w + 8 * i + (lane >> 3), m = itm * GBM + r;
+        const unsigned cb = (unsigned)((lane & 7) ^ ((r >> 1) & 7)) << 4;
+        if constexpr (CONV) {
+          amask[i] = 0u;
+          aoff[i] = 0u;
+          if (m < g.M) {
+            const int ow = m % g.cWo, t2 = m / g.cWo, oh = t2 % g.cHo, n = t2 / g.cHo;
+            const int ih0 = oh * g.cS - g.cP, iw0 = ow * g.cS - g.cP;
+            aoff[i] = (unsigned)((((long long)n * g.cH + ih0) * g.cW + iw0) * g.cC * 2) + cb;  // wraps for padding
+            for (int kh = 0; kh < g.cKH; ++kh)
+              for (int kw = 0; kw < g.cKW; ++kw)
+                if (ih0 + kh >= 0 && ih0 + kh < g.cH && iw0 + kw >= 0 && iw0 + kw < g.cW)
+                  amask[i] |= 1u << (kh * g.cKW + kw);
+          }
+        } else {
+          aoff[i] = m < g.M ? (unsigned)m * lda2 + cb : OOB;
+        }
+      }
+    }
     char* la = smem + (s & 1) * ST_BUF;
     char* lb = la + G_TILE_BYTES;
     const unsigned kb0 = (unsigned)kt * 128u;
+    if constexpr (CONV) {
+      const int tap = kt / cpt, kh = tap / g.cKW, kw = tap - kh * g.cKW;
+      const unsigned toff = (unsigned)(((kh * g.cW + kw) * g.cC + (kt - tap * cpt) * 64) * 2);
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int r = 32 * w + 8 * i + (lane >> 3);  // LDS row of this lane's chunk (A and B)
+      for (int i = 0; i < 4; ++i)
+        blds16(ars, la + (32 * w + 8 * i) * 128, (amask[i] >> tap) & 1u ? aoff[i] + toff : OOB, 0u);
+    } else {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) blds16(ars, la + (32 * w + 8 * i) * 128, aoff[i], kb0);
+    }
+#pragma unroll
+    for (int ib = 0; ib < NBI; ++ib) {  // LDS row WN w + 16 f + i holds weight row 4 NF (i >> 2) + 4 f + (i & 3)
+      const int rl = 8 * ib + (lane >> 3), f = rl >> 4, i = rl & 15, r = WN * w + rl;
       const unsigned cb = (unsigned)((lane & 7) ^ ((r >> 1) & 7)) << 4;
-      const int m = tm * GBM + r;
-      blds16(ars, la + (32 * w + 8 * i) * 128, m < g.M ? (unsigned)m * lda2 + cb : OOB, kb0);
-      const int jj = 8 * (i & 1) + (lane >> 3);  // LDS row 32w + 16f + jj holds weight row 8 (jj >> 2) + 4f + (jj & 3)
-      const int n = tn * GBM + 32 * w + 8 * (jj >> 2) + 4 * (i >> 1) + (jj & 3);
-      blds16(brs, lb + (32 * w + 8 * i) * 128, (unsigned)n * ldb2 + cb, kb0);
+      const int n = itn * TN + WN * w + 4 * NF * (i >> 2) + 4 * f + (i & 3);
+      blds16(brs, lb + (WN * w + 8 * ib) * 128, (unsigned)n * ldb2 + cb, kb0);
     }
   };
 
@@ -1257,49 +1300,56 @@ __global__ void __launch_bounds__(ST_NT) k_gemm_stream(GemmArgs g) {
     x += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, x), 0x118, 0xf, 0xf, true));
     return x;
   };
-  f32x4 acc[8][2];
-  // one K-tile from LDS buffer `buf`; FIRST: the tile's first K-tile (accumulators start from the MFMA's zero C)
+  f32x4 acc[8][NF];
+  // one K-step from LDS buffer `buf`; FIRST: the tile's first K-step (accumulators start from the MFMA's zero C)
   auto compute = [&](int buf, auto first) {
     const char* la = smem + buf * ST_BUF;
     const char* lb = la + G_TILE_BYTES;
 #pragma unroll
     for (int s2 = 0; s2 < 2; ++s2) {
-      s16x8 xf[8], wf[2];
+      s16x8 xf[8], wf[NF];
 #pragma unroll
       for (int m = 0; m < 8; ++m) xf[m] = *(const s16x8*)(la + lds_off(16 * m + j, 4 * s2 + q));
 #pragma unroll
-      for (int f = 0; f < 2; ++f) wf[f] = *(const s16x8*)(lb + lds_off(32 * w + 16 * f + j, 4 * s2 + q));
+      for (int f = 0; f < NF; ++f) wf[f] = *(const s16x8*)(lb + lds_off(WN * w + 16 * f + j, 4 * s2 + q));
 #pragma unroll
       for (int m = 0; m < 8; ++m)
 #pragma unroll
-        for (int f = 0; f < 2; ++f)
+        for (int f = 0; f < NF; ++f)
           acc[m][f] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
               wf[f], xf[m], (decltype(first)::value && s2 == 0) ? f32x4{0.f, 0.f, 0.f, 0.f} : acc[m][f], 0, 0, 0);
     }
   };
-  // epilogue of tile (tm, tn): lane (q, j) owns columns c0 .. c0 + 7 of rows tm*128 + 16 m + j.  FULL: no row past M.
-  st_v4u old[8];  // beta != 0: this tile's C_old rows (lane (q, j): row 16 m + j, columns c0 .. c0 + 7)
+  typedef float f2 __attribute__((ext_vector_type(2)));
+  typedef __bf16 bf2 __attribute__((ext_vector_type(2)));
+  st_v4u old[8];  // beta != 0: this tile's C_old rows (lane (q, j): row 16 m + j, columns c0 .. c0 + 4 NF - 1)
   auto load_old = [&](int tm, int tn) {
-    const int c0 = tn * GBM + 32 * w + 8 * q;
+    const int c0 = tn * TN + WN * w + 4 * NF * q;
 #pragma unroll
     for (int m = 0; m < 8; ++m) {
       const int row = tm * GBM + 16 * m + j;
-      old[m] = __builtin_amdgcn_raw_buffer_load_b128(
-          crs, row < g.M ? ((unsigned)row * (unsigned)g.ldc + c0) * 2u : OOB, 0, 0);
+      const unsigned o = row < g.M ? ((unsigned)row * (unsigned)g.ldc + c0) * 2u : OOB;
+      if constexpr (NF == 2) {
+        old[m] = __builtin_amdgcn_raw_buffer_load_b128(crs, o, 0, 0);
+      } else {
+        const st_v2u v = __builtin_amdgcn_raw_buffer_load_b64(crs, o, 0, 0);
+        old[m] = st_v4u{v[0], v[1], 0u, 0u};
+      }
     }
   };
-  // more: the DMA of the next step was issued after the C_old loads (still in flight)
+  // epilogue of tile (tm, tn): lane (q, j) owns columns c0 .. c0 + 4 NF - 1 of rows tm*128 + 16 m + j.
+  // more: the DMA of the next K-step was issued after the C_old loads.  FULL: no row past M.
   auto epilogue = [&](int tm, int tn, bool more, auto full, auto acc_old) {
     constexpr bool FULL = decltype(full)::value, BETA = decltype(acc_old)::value;
-    const int c0 = tn * GBM + 32 * w + 8 * q;
-    if constexpr (BETA) {  // C_old was loaded ahead of the tile's last K-step, before the DMA of the next step
-      if (more) wait_vmcnt<8>();
+    constexpr int NP = 2 * NF;  // column pairs per lane
+    const int c0 = tn * TN + WN * w + 4 * NF * q;
+    if constexpr (BETA) {
+      if (more) wait_vmcnt<NI>();
       else wait_vmcnt<0>();
     }
-    typedef float f2 __attribute__((ext_vector_type(2)));
-    f2 b2[4], sh2[4], s1[4], sq[4];
+    f2 b2[NP], sh2[NP], s1[NP], sq[NP];
 #pragma unroll
-    for (int e = 0; e < 4; ++e) {
+    for (int e = 0; e < NP; ++e) {
       b2[e] = *(const f2*)(sbias + c0 + 2 * e);
       sh2[e] = *(const f2*)(sshift + c0 + 2 * e);
       s1[e] = sq[e] = f2{0.f, 0.f};
@@ -1308,14 +1358,13 @@ __global__ void __launch_bounds__(ST_NT) k_gemm_stream(GemmArgs g) {
     for (int m = 0; m < 8; ++m) {
       const int row = tm * GBM + 16 * m + j;
       const bool in = FULL || row < g.M;
-      unsigned pk[4];
+      unsigned pk[NP];
 #pragma unroll
-      for (int e = 0; e < 4; ++e) {  // columns 2e, 2e + 1 = fragment e >> 1, elements 2 (e & 1) + {0, 1}
+      for (int e = 0; e < NP; ++e) {  // columns 2e, 2e + 1 = fragment e >> 1, elements 2 (e & 1) + {0, 1}
         const f32x4& a = acc[m][e >> 1];
         f2 x = f2{a[2 * (e & 1)], a[2 * (e & 1) + 1]} * alpha + b2[e];
         if constexpr (BETA)
           x += f2{__uint_as_float(old[m][e] << 16), __uint_as_float(old[m][e] & 0xffff0000u)} * g.beta;
-        typedef __bf16 bf2 __attribute__((ext_vector_type(2)));
         pk[e] = __builtin_bit_cast(unsigned, __builtin_convertvector(x, bf2));
         // statistics of the values as stored (bf16)
         f2 d = f2{__uint_as_float(pk[e] << 16), __uint_as_float(pk[e] & 0xffff0000u)} - sh2[e];
@@ -1323,13 +1372,13 @@ __global__ void __launch_bounds__(ST_NT) k_gemm_stream(GemmArgs g) {
         s1[e] += d;
         sq[e] += d * d;
       }
-      __builtin_amdgcn_raw_buffer_store_b128(st_v4u{pk[0], pk[1], pk[2], pk[3]}, crs,
-                                             in && !(g.single & 2) ? ((unsigned)row * (unsigned)g.ldc + c0) * 2u : OOB,
-                                             0, CPOL);
+      const unsigned o = in ? ((unsigned)row * (unsigned)g.ldc + c0) * 2u : OOB;
+      if constexpr (NF == 2) __builtin_amdgcn_raw_buffer_store_b128(st_v4u{pk[0], pk[1], pk[2], pk[3]}, crs, o, 0, 2);
+      else __builtin_amdgcn_raw_buffer_store_b64(st_v2u{pk[0], pk[1]}, crs, o, 0, 2);  // (nt: streamed output)
     }
-    float r1[8], r2[8];
+    float r1[2 * NP], r2[2 * NP];
 #pragma unroll
-    for (int e = 0; e < 4; ++e) {
+    for (int e = 0; e < NP; ++e) {
       r1[2 * e] = rowsum16(s1[e][0]);
       r1[2 * e + 1] = rowsum16(s1[e][1]);
       r2[2 * e] = rowsum16(sq[e][0]);
@@ -1337,14 +1386,14 @@ __global__ void __launch_bounds__(ST_NT) k_gemm_stream(GemmArgs g) {
     }
     const unsigned so = j == 15 ? ((unsigned)tm * (unsigned)g.N + c0) * 8u : OOB;
 #pragma unroll
-    for (int p = 0; p < 4; ++p)
+    for (int p = 0; p < NP; ++p)
       __builtin_amdgcn_raw_buffer_store_b128(
           st_v4u{__float_as_uint(r1[2 * p]), __float_as_uint(r2[2 * p]), __float_as_uint(r1[2 * p + 1]),
                  __float_as_uint(r2[2 * p + 1])},
           srs, so + 16u * p, 0, 0);
   };
 
-  // the stream: step s = (tile k, K-tile kt), s = k * nk + kt; DMA of step s + 1 in flight during step s
+  // the stream: step s = (tile k, K-step kt), s = k * nk + kt; the DMA of step s + 1 is in flight during step s.
   // beta != 0: the tile's C_old rows are loaded at the top of its last K-step, ahead of the next step's DMA, so
   // their latency hides under that step's MFMAs
   const bool bta = g.beta != 0.f;
@@ -1356,20 +1405,20 @@ __global__ void __launch_bounds__(ST_NT) k_gemm_stream(GemmArgs g) {
       const int s = k * nk + kt;
       const bool lo = bta && kt == nk - 1;
       if (kt == 0 && k > 0) {  // outstanding: this step's DMA, then the previous epilogue's stores
-        wait_vmcnt<ST_NST>();
+        wait_vmcnt<NST>();
         if (lo) load_old(tm, tn);
         if (s + 1 < steps) issue(s + 1);
-      } else if (lo) {  // outstanding: this step's DMA | C_old (8) | next DMA (8)
+      } else if (lo) {  // outstanding: this step's DMA | C_old (8) | next DMA (NI)
         load_old(tm, tn);
         if (s + 1 < steps) {
           issue(s + 1);
-          wait_vmcnt<16>();
+          wait_vmcnt<8 + NI>();
         } else {
           wait_vmcnt<8>();
         }
       } else if (s + 1 < steps) {
         issue(s + 1);
-        wait_vmcnt<8>();
+        wait_vmcnt<NI>();
       } else {
         wait_vmcnt<0>();
       }

@@ -40,6 +40,28 @@ def main():
         out[f"nt{M}x{N}x{K}_colstats"] = max(rel(parts[..., 0].sum(0), d.sum(0)),
                                              rel(parts[..., 1].sum(0), (d * d).sum(0)))
         out[f"nt{M}x{N}x{K}_colstats_y"] = rel(y, ref)
+    # implicit convolutions (C % 64 == 0, N = 64 / 128): padding, stride 2, 1x1, M tails, BN statistics, beta
+    from distributeddataparallel_cifar10_amd.ops import functional as F
+    for n, h, c, co, k, st, pd in [(2, 14, 64, 64, 3, 1, 1), (3, 15, 128, 128, 3, 2, 1), (4, 9, 64, 128, 3, 1, 1),
+                                   (2, 11, 128, 64, 1, 1, 0), (1, 57, 64, 64, 3, 1, 1)]:
+        x = torch.randn(n, h, h, c, device=dev, generator=g).to(bf)
+        wt = torch.randn(co, c, k, k, device=dev, generator=g) * 0.05
+        geo = F._geom(x, wt, st, pd)
+        wm = F._weight_matrix(wt, geo.K)
+        Mc = geo.N * geo.Ho * geo.Wo
+        ref = torch.nn.functional.conv2d(x.float().permute(0, 3, 1, 2), wt.to(bf).float(), stride=st, padding=pd)
+        ref = ref.permute(0, 2, 3, 1).reshape(Mc, co)
+        shift = torch.randn(co, device=dev, generator=g) * 0.1
+        parts = torch.full(((Mc + 127) // 128, co, 2), float("nan"), device=dev)
+        y = ops.gemm(x, wm, conv=1, geom=geo, mnk=(Mc, co, geo.K), out_dtype=bf, col_stats=parts, stats_shift=shift)
+        tag = f"conv{n}x{h}x{c}->{co}_k{k}s{st}"
+        out[tag] = rel(y, ref)
+        d = y.float() - shift
+        out[tag + "_colstats"] = max(rel(parts[..., 0].sum(0), d.sum(0)), rel(parts[..., 1].sum(0), (d * d).sum(0)))
+        c0 = torch.randn(Mc, co, device=dev, generator=g).to(bf)
+        c1 = c0.clone()
+        ops.gemm(x, wm, conv=1, geom=geo, mnk=(Mc, co, geo.K), out_dtype=bf, out=c1, beta=1.0)
+        out[tag + "_beta"] = rel(c1, ref + c0.float())
     # padded leading dimensions (views into wider buffers)
     a_w = torch.randn(3000, 192, device=dev, generator=g).to(bf)
     b_w = torch.randn(256, 136, device=dev, generator=g).to(bf)
