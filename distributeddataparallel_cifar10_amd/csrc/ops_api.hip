@@ -226,12 +226,14 @@ int dca_ops_gemm(const GemmArgs* a, void* stream) {
                              PpTile<256>::LDS));
     OPCK(hipFuncSetAttribute((const void*)k_gemm_pp<128>, hipFuncAttributeMaxDynamicSharedMemorySize,
                              PpTile<128>::LDS));
-    OPCK(hipFuncSetAttribute((const void*)k_gemm_stream<2, false>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                             2 * ST_BUF + 2 * 2048 * 4));
-    OPCK(hipFuncSetAttribute((const void*)k_gemm_stream<2, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                             2 * ST_BUF + 2 * 2048 * 4));
-    OPCK(hipFuncSetAttribute((const void*)k_gemm_stream<1, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                             2 * ST_BUF + 2 * 2048 * 4));
+    OPCK(hipFuncSetAttribute((const void*)k_gemm_stream<2, 1, false>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                             2 * (2 * G_TILE_BYTES + 8192) + 2 * 2048 * 4));
+    OPCK(hipFuncSetAttribute((const void*)k_gemm_stream<2, 1, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                             2 * (2 * G_TILE_BYTES + 8192) + 2 * 2048 * 4));
+    OPCK(hipFuncSetAttribute((const void*)k_gemm_stream<2, 2, false>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                             2 * (2 * G_TILE_BYTES + 8192) + 2 * 2048 * 4));
+    OPCK(hipFuncSetAttribute((const void*)k_gemm_stream<2, 2, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                             2 * (2 * G_TILE_BYTES + 8192) + 2 * 2048 * 4));
     g_lds_set = true;
   }
   const int kt = GBK_BYTES / (g.fp8 ? 1 : 2);
@@ -273,19 +275,21 @@ int dca_ops_gemm(const GemmArgs* a, void* stream) {
   // persistent stream kernel (k_gemm_stream), bf16 -> bf16, K % 64 == 0, no split / remap / ReLU:
   //   plain NT, N % 128 == 0: by default for K <= 512 and M >= 16384, accumulating (beta) calls only for K <= 128
   //     (the output-heavy 1x1 convolutions and their input gradients; profiles/gemm_shortk_r2.log);
+  //   N = 64: 256 x 64 tiles (802816 x 64 x 256: 123.4 -> 109.1 us);
   //   implicit conv with C % 64 == 0, N = 128: M >= 16384 (ResNet-50's layer-2 3x3 convolutions and their input
-  //     gradients: 129.5 -> 117.9 us at batch 256); N = 64 only when forced (DCA_OPS_STREAM=1): its 16-column waves
-  //     read 9 fragments per 8 MFMAs from LDS and lose to the one-tile kernel (218.5 vs 176.4 us)
+  //     gradients: 129.5 -> 117.5 us at batch 256).  The N = 64 conv stays on the one-tile kernel unless forced
+  //     (DCA_OPS_STREAM=1): 174 us there, 218 us with 128 x 64 stream tiles, 283 us with 256 x 64
   {
     const int sk = getenv_stream();
     const bool conv = g.conv == 1;
     const long long ab = conv ? (long long)g.cN * g.cH * g.cW * g.cC * 2 : ((long long)(g.M - 1) * g.lda + g.K) * 2;
     const long long bb = ((long long)(g.N - 1) * g.ldb + g.K) * 2;
     const long long cbytes = (long long)g.M * g.ldc * 2;
-    const int nf = g.N % 128 == 0 ? 2 : 1;
+    const int mw = g.N % 128 == 0 ? 1 : 2;  // 128 x 128 tiles, or 256 x 64 for N % 128 == 64
     const bool shape_ok = conv ? (g.cC % 64 == 0 && g.cKH * g.cKW <= 32 && (g.N == 64 || g.N == 128) && g.orow_S <= 0 &&
                                   (sk == 1 || (sk == 2 && getenv_stream_conv() && g.N == 128 && g.M >= 16384)))
-                               : (g.conv == 0 && !g.ta && g.N % 128 == 0 && g.lda % 8 == 0 && g.lda >= g.K &&
+                               : (g.conv == 0 && !g.ta && g.lda % 8 == 0 && g.lda >= g.K &&
+                                  (g.N % 128 == 0 || g.N == 64) &&
                                   (sk == 1 || (g.K <= 512 && g.M >= 16384 && (g.beta == 0.f || g.K <= 128))));
     const bool st_ok = sk != 0 && shape_ok && !g.fp8 && !g.tb && g.splits == 1 && g.wperm_T <= 0 && g.orow_S <= 0 &&
                        !g.bnb_part && !g.relu && g.out_bf16 && g.N % 64 == 0 && g.N <= 2048 && g.K % 64 == 0 &&
@@ -300,16 +304,17 @@ int dca_ops_gemm(const GemmArgs* a, void* stream) {
         OPCK(hipGetDevice(&dev));
         OPCK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
       }
-      const long tiles = (long)((g.M + GBM - 1) / GBM) * (g.N / (64 * nf));
+      const long tiles = (long)((g.M + GBM * mw - 1) / (GBM * mw)) * (g.N / (128 / mw));
       long grid = std::min<long>(2L * ncu, (tiles + 7) / 8 * 8);  // two resident workgroups per CU
       grid = std::max<long>(8, grid / 8 * 8);
-      const int lds = 2 * ST_BUF + 2 * g.N * 4;
+      const int lds = 2 * (GBM * mw * 128 + (128 / mw) * 128) + 2 * g.N * 4;  // 2 x (A | B) + bias | shift
       const dim3 gr((unsigned)grid), bl(ST_NT);
       if (conv) {
-        if (nf == 2) hipLaunchKernelGGL((k_gemm_stream<2, true>), gr, bl, lds, st, g);
-        else hipLaunchKernelGGL((k_gemm_stream<1, true>), gr, bl, lds, st, g);
+        if (mw == 1) hipLaunchKernelGGL((k_gemm_stream<2, 1, true>), gr, bl, lds, st, g);
+        else hipLaunchKernelGGL((k_gemm_stream<2, 2, true>), gr, bl, lds, st, g);
       } else {
-        hipLaunchKernelGGL((k_gemm_stream<2, false>), gr, bl, lds, st, g);
+        if (mw == 1) hipLaunchKernelGGL((k_gemm_stream<2, 1, false>), gr, bl, lds, st, g);
+        else hipLaunchKernelGGL((k_gemm_stream<2, 2, false>), gr, bl, lds, st, g);
       }
       OPCK(hipGetLastError());
       return 0;

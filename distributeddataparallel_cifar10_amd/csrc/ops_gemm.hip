@@ -1206,20 +1206,26 @@ constexpr int ST_BUF = 2 * G_TILE_BYTES;  // A + B tile, 128 rows x 128 B each
 typedef unsigned st_v4u __attribute__((ext_vector_type(4)));
 typedef unsigned st_v2u __attribute__((ext_vector_type(2)));
 
-// NF: 16-column MFMA fragments per wave (2: 128-column tiles, 1: 64-column tiles -- the 64-channel convolutions).
+// NF: 16-column MFMA fragments per wave.  MW: waves along M -- the tile is 128 MW rows x 64 NF (4 / MW) columns and
+// wave (wm, wn) owns rows 128 wm .., so each wave's statistics are exactly one 128-row partial row of col_stats
+// (MW = 2, NF = 2: 256 x 64 tiles for the 64-channel layers, 10 fragment reads per 16 MFMAs).
 // CONV: A is the implicit im2col of an NHWC input with C % 64 == 0 (one tap per K-step; per-row tap-validity masks
 // computed once per tile, padding taps load zeros through an offset past the descriptor).
-template <int NF, bool CONV>
+template <int NF, int MW, bool CONV>
 __global__ void __launch_bounds__(ST_NT, 2) k_gemm_stream(GemmArgs g) {
-  constexpr int WN = 16 * NF, TN = 4 * WN;  // columns per wave / per tile
-  constexpr int NBI = WN / 8;               // B DMA instructions per wave and K-step
-  constexpr int NI = 4 + NBI;               // DMA instructions per lane and K-step
+  constexpr int NWN = 4 / MW, WN = 16 * NF, TN = NWN * WN, TM = GBM * MW;  // waves along N, columns per wave / tile
+  constexpr int NAI = 4 * MW;               // A DMA instructions per wave and K-step (TM rows, 8 per instruction)
+  constexpr int NBI = TN / 32;              // B DMA instructions per wave and K-step (TN rows over 4 waves)
+  constexpr int NI = NAI + NBI;             // DMA instructions per lane and K-step
+  constexpr int BUF = TM * 128 + TN * 128;  // LDS bytes per buffer: A | B
   constexpr int NST = 8 + 2 * NF;           // stores per lane and epilogue: 8 output rows + the statistics
   extern __shared__ __attribute__((aligned(16))) char smem[];
   constexpr unsigned OOB = 0x80000000u;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, j = lane & 15, q = lane >> 4;
-  const int ntm = (g.M + GBM - 1) / GBM, ntn = g.N / TN, T = ntm * ntn, nk = g.K / 64;
-  float* sbias = (float*)(smem + 2 * ST_BUF);  // [N] bias | [N] statistics shift
+  const int wm = w / NWN, wn = w % NWN;
+  const int ntm = (g.M + TM - 1) / TM, ntn = g.N / TN, T = ntm * ntn, nk = g.K / 64;
+  const int nstat = (g.M + GBM - 1) / GBM;  // col_stats rows (128-row blocks)
+  float* sbias = (float*)(smem + 2 * BUF);  // [N] bias | [N] statistics shift
   float* sshift = sbias + g.N;
   for (int c = threadIdx.x; c < g.N; c += ST_NT) {
     sbias[c] = g.bias ? g.bias[c] : 0.f;
@@ -1238,20 +1244,20 @@ __global__ void __launch_bounds__(ST_NT, 2) k_gemm_stream(GemmArgs g) {
   const __amdgpu_buffer_rsrc_t crs = __builtin_amdgcn_make_buffer_rsrc(
       g.C, (short)0, (int)((long long)g.M * g.ldc * 2), 0x00020000);
   const __amdgpu_buffer_rsrc_t srs = __builtin_amdgcn_make_buffer_rsrc(
-      (void*)g.col_stats, (short)0, g.col_stats ? (int)((long long)ntm * g.N * 8) : 0, 0x00020000);
+      (void*)g.col_stats, (short)0, g.col_stats ? (int)((long long)nstat * g.N * 8) : 0, 0x00020000);
   const unsigned lda2 = (unsigned)g.lda * 2u, ldb2 = (unsigned)g.ldb * 2u;
   const int cpt = CONV ? g.cC / 64 : 1;  // K-steps per tap
 
   // issue side: A row offsets (and conv tap masks) of the tile whose K-steps are being issued
-  unsigned aoff[4], amask[4];
+  unsigned aoff[NAI], amask[NAI];
   int itm = 0, itn = 0;
   auto issue = [&](int s) {
     const int k = s / nk, kt = s - k * nk;
     if (kt == 0) {
       tile_coords(t_beg + loc + k * nxwg, ntm, ntn, itm, itn);
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int r = 32 * w + 8 * i + (lane >> 3), m = itm * GBM + r;
+      for (int i = 0; i < NAI; ++i) {
+        const int r = 8 * NAI * w + 8 * i + (lane >> 3), m = itm * TM + r;
         const unsigned cb = (unsigned)((lane & 7) ^ ((r >> 1) & 7)) << 4;
         if constexpr (CONV) {
           amask[i] = 0u;
@@ -1270,25 +1276,25 @@ __global__ void __launch_bounds__(ST_NT, 2) k_gemm_stream(GemmArgs g) {
         }
       }
     }
-    char* la = smem + (s & 1) * ST_BUF;
-    char* lb = la + G_TILE_BYTES;
+    char* la = smem + (s & 1) * BUF;
+    char* lb = la + TM * 128;
     const unsigned kb0 = (unsigned)kt * 128u;
     if constexpr (CONV) {
       const int tap = kt / cpt, kh = tap / g.cKW, kw = tap - kh * g.cKW;
       const unsigned toff = (unsigned)(((kh * g.cW + kw) * g.cC + (kt - tap * cpt) * 64) * 2);
 #pragma unroll
-      for (int i = 0; i < 4; ++i)
-        blds16(ars, la + (32 * w + 8 * i) * 128, (amask[i] >> tap) & 1u ? aoff[i] + toff : OOB, 0u);
+      for (int i = 0; i < NAI; ++i)
+        blds16(ars, la + (8 * NAI * w + 8 * i) * 128, (amask[i] >> tap) & 1u ? aoff[i] + toff : OOB, 0u);
     } else {
 #pragma unroll
-      for (int i = 0; i < 4; ++i) blds16(ars, la + (32 * w + 8 * i) * 128, aoff[i], kb0);
+      for (int i = 0; i < NAI; ++i) blds16(ars, la + (8 * NAI * w + 8 * i) * 128, aoff[i], kb0);
     }
 #pragma unroll
-    for (int ib = 0; ib < NBI; ++ib) {  // LDS row WN w + 16 f + i holds weight row 4 NF (i >> 2) + 4 f + (i & 3)
-      const int rl = 8 * ib + (lane >> 3), f = rl >> 4, i = rl & 15, r = WN * w + rl;
+    for (int ib = 0; ib < NBI; ++ib) {  // LDS row WN v + 16 f + i holds weight row WN v + 4 NF (i >> 2) + 4 f + (i & 3)
+      const int r = 8 * NBI * w + 8 * ib + (lane >> 3), v = r / WN, rl = r % WN, f = rl >> 4, i = rl & 15;
       const unsigned cb = (unsigned)((lane & 7) ^ ((r >> 1) & 7)) << 4;
-      const int n = itn * TN + WN * w + 4 * NF * (i >> 2) + 4 * f + (i & 3);
-      blds16(brs, lb + (WN * w + 8 * ib) * 128, (unsigned)n * ldb2 + cb, kb0);
+      const int n = itn * TN + WN * v + 4 * NF * (i >> 2) + 4 * f + (i & 3);
+      blds16(brs, lb + (8 * NBI * w + 8 * ib) * 128, (unsigned)n * ldb2 + cb, kb0);
     }
   };
 
@@ -1303,15 +1309,15 @@ __global__ void __launch_bounds__(ST_NT, 2) k_gemm_stream(GemmArgs g) {
   f32x4 acc[8][NF];
   // one K-step from LDS buffer `buf`; FIRST: the tile's first K-step (accumulators start from the MFMA's zero C)
   auto compute = [&](int buf, auto first) {
-    const char* la = smem + buf * ST_BUF;
-    const char* lb = la + G_TILE_BYTES;
+    const char* la = smem + buf * BUF;
+    const char* lb = la + TM * 128;
 #pragma unroll
     for (int s2 = 0; s2 < 2; ++s2) {
       s16x8 xf[8], wf[NF];
 #pragma unroll
-      for (int m = 0; m < 8; ++m) xf[m] = *(const s16x8*)(la + lds_off(16 * m + j, 4 * s2 + q));
+      for (int m = 0; m < 8; ++m) xf[m] = *(const s16x8*)(la + lds_off(GBM * wm + 16 * m + j, 4 * s2 + q));
 #pragma unroll
-      for (int f = 0; f < NF; ++f) wf[f] = *(const s16x8*)(lb + lds_off(WN * w + 16 * f + j, 4 * s2 + q));
+      for (int f = 0; f < NF; ++f) wf[f] = *(const s16x8*)(lb + lds_off(WN * wn + 16 * f + j, 4 * s2 + q));
 #pragma unroll
       for (int m = 0; m < 8; ++m)
 #pragma unroll
@@ -1324,10 +1330,10 @@ __global__ void __launch_bounds__(ST_NT, 2) k_gemm_stream(GemmArgs g) {
   typedef __bf16 bf2 __attribute__((ext_vector_type(2)));
   st_v4u old[8];  // beta != 0: this tile's C_old rows (lane (q, j): row 16 m + j, columns c0 .. c0 + 4 NF - 1)
   auto load_old = [&](int tm, int tn) {
-    const int c0 = tn * TN + WN * w + 4 * NF * q;
+    const int c0 = tn * TN + WN * wn + 4 * NF * q;
 #pragma unroll
     for (int m = 0; m < 8; ++m) {
-      const int row = tm * GBM + 16 * m + j;
+      const int row = tm * TM + GBM * wm + 16 * m + j;
       const unsigned o = row < g.M ? ((unsigned)row * (unsigned)g.ldc + c0) * 2u : OOB;
       if constexpr (NF == 2) {
         old[m] = __builtin_amdgcn_raw_buffer_load_b128(crs, o, 0, 0);
@@ -1342,7 +1348,7 @@ __global__ void __launch_bounds__(ST_NT, 2) k_gemm_stream(GemmArgs g) {
   auto epilogue = [&](int tm, int tn, bool more, auto full, auto acc_old) {
     constexpr bool FULL = decltype(full)::value, BETA = decltype(acc_old)::value;
     constexpr int NP = 2 * NF;  // column pairs per lane
-    const int c0 = tn * TN + WN * w + 4 * NF * q;
+    const int c0 = tn * TN + WN * wn + 4 * NF * q;
     if constexpr (BETA) {
       if (more) wait_vmcnt<NI>();
       else wait_vmcnt<0>();
@@ -1356,7 +1362,7 @@ __global__ void __launch_bounds__(ST_NT, 2) k_gemm_stream(GemmArgs g) {
     }
 #pragma unroll
     for (int m = 0; m < 8; ++m) {
-      const int row = tm * GBM + 16 * m + j;
+      const int row = tm * TM + GBM * wm + 16 * m + j;
       const bool in = FULL || row < g.M;
       unsigned pk[NP];
 #pragma unroll
@@ -1384,7 +1390,7 @@ __global__ void __launch_bounds__(ST_NT, 2) k_gemm_stream(GemmArgs g) {
       r2[2 * e] = rowsum16(sq[e][0]);
       r2[2 * e + 1] = rowsum16(sq[e][1]);
     }
-    const unsigned so = j == 15 ? ((unsigned)tm * (unsigned)g.N + c0) * 8u : OOB;
+    const unsigned so = j == 15 ? ((unsigned)(tm * MW + wm) * (unsigned)g.N + c0) * 8u : OOB;
 #pragma unroll
     for (int p = 0; p < NP; ++p)
       __builtin_amdgcn_raw_buffer_store_b128(
@@ -1430,7 +1436,7 @@ __global__ void __launch_bounds__(ST_NT, 2) k_gemm_stream(GemmArgs g) {
       __builtin_amdgcn_s_barrier();  // every wave is done reading this buffer before it is refilled
       asm volatile("" ::: "memory");
     }
-    const bool full = tm * GBM + GBM <= g.M, more = (k + 1) * nk < steps;
+    const bool full = tm * TM + GBM * wm + GBM <= g.M, more = (k + 1) * nk < steps;
     if (bta) {
       if (full) epilogue(tm, tn, more, std::true_type{}, std::true_type{});
       else epilogue(tm, tn, more, std::false_type{}, std::true_type{});

@@ -21,7 +21,7 @@ def main():
     g = torch.Generator(device=dev).manual_seed(0)
     bf = torch.bfloat16
     out = {}
-    for M, N, K in [(128, 128, 64), (1000, 256, 64), (4097, 512, 128), (300, 1024, 256), (20000, 128, 512),
+    for M, N, K in [(128, 128, 64), (1000, 256, 64), (4097, 512, 128), (300, 1024, 256), (20000, 128, 512), (5000, 64, 128),
                     (70000, 256, 64)]:
         a = torch.randn(M, K, device=dev, generator=g).to(bf)
         b = (torch.randn(N, K, device=dev, generator=g) * torch.linspace(0.5, 2.0, K, device=dev)).to(bf)
