@@ -823,10 +823,12 @@ __global__ void __launch_bounds__(NW * 64) k_gemm_glds(GemmArgs g) {
   // S LDS buffers, S - 1 tiles in flight.  S = 1 (single): tile k is issued after tile k-1's closing barrier.
   const int S = g.single ? 1 : (g.stages >= 2 && g.stages <= 4 ? g.stages : 2);
   for (int t0 = 0; t0 < S - 1 && t0 < nk; ++t0) issue(t0, t0);
-  for (int kt = 0; kt < nk; ++kt) {
-    const int buf = kt % S;
+  // buffer indices stepped incrementally: kt % S with a runtime S compiled to ~40 SALU of signed division per
+  // K-tile (the loop's issue bound on short-N shapes, profiles/gemm_stream_pmc_r2.txt)
+  int buf = 0, ibuf = S - 1;  // kt % S, (kt + S - 1) % S
+  for (int kt = 0; kt < nk; ++kt, buf = buf + 1 == S ? 0 : buf + 1, ibuf = ibuf + 1 == S ? 0 : ibuf + 1) {
     const int nt = kt + S - 1;
-    if (nt < nk) issue(nt, nt % S);  // into the buffer every wave finished reading before the last barrier
+    if (nt < nk) issue(nt, ibuf);  // into the buffer every wave finished reading before the last barrier
     switch (min(nk - 1, nt) - kt) {   // this thread's loads of tile kt have landed (later tiles' in flight)
       case 0: wait_vmcnt<0>(); break;
       case 1: wait_vmcnt<NI>(); break;
@@ -1251,8 +1253,11 @@ __global__ void __launch_bounds__(ST_NT, 2) k_gemm_stream(GemmArgs g) {
   // issue side: A row offsets (and conv tap masks) of the tile whose K-steps are being issued
   unsigned aoff[NAI], amask[NAI];
   int itm = 0, itn = 0;
+  // issue() is called for s = 0, 1, 2, ... in order: the (tile, K-step, tap) position advances incrementally
+  // (no per-step division: runtime divisions compile to ~20 SALU each)
+  int i_k = 0, i_kt = 0, i_tap = 0, i_cs = 0, i_toff = 0;
   auto issue = [&](int s) {
-    const int k = s / nk, kt = s - k * nk;
+    const int k = i_k, kt = i_kt;
     if (kt == 0) {
       tile_coords(t_beg + loc + k * nxwg, ntm, ntn, itm, itn);
 #pragma unroll
@@ -1280,11 +1285,21 @@ __global__ void __launch_bounds__(ST_NT, 2) k_gemm_stream(GemmArgs g) {
     char* lb = la + TM * 128;
     const unsigned kb0 = (unsigned)kt * 128u;
     if constexpr (CONV) {
-      const int tap = kt / cpt, kh = tap / g.cKW, kw = tap - kh * g.cKW;
-      const unsigned toff = (unsigned)(((kh * g.cW + kw) * g.cC + (kt - tap * cpt) * 64) * 2);
+      const int tap = i_tap;
+      const unsigned toff = (unsigned)i_toff;
 #pragma unroll
       for (int i = 0; i < NAI; ++i)
         blds16(ars, la + (8 * NAI * w + 8 * i) * 128, (amask[i] >> tap) & 1u ? aoff[i] + toff : OOB, 0u);
+      // next K-step: 64 more channels of this tap, or the next tap (kw, then kh), or tap 0 of the next tile
+      if (++i_cs < cpt) {
+        i_toff += 128;
+      } else {
+        i_cs = 0;
+        ++i_tap;
+        const int kh = i_tap / g.cKW;  // (once per tap)
+        i_toff = ((kh * g.cW + (i_tap - kh * g.cKW)) * g.cC) * 2;
+      }
+      if (kt + 1 == nk) i_tap = i_cs = i_toff = 0;
     } else {
 #pragma unroll
       for (int i = 0; i < NAI; ++i) blds16(ars, la + (8 * NAI * w + 8 * i) * 128, aoff[i], kb0);
@@ -1295,6 +1310,10 @@ __global__ void __launch_bounds__(ST_NT, 2) k_gemm_stream(GemmArgs g) {
       const unsigned cb = (unsigned)((lane & 7) ^ ((r >> 1) & 7)) << 4;
       const int n = itn * TN + WN * v + 4 * NF * (i >> 2) + 4 * f + (i & 3);
       blds16(brs, lb + (8 * NBI * w + 8 * ib) * 128, (unsigned)n * ldb2 + cb, kb0);
+    }
+    if (++i_kt == nk) {
+      i_kt = 0;
+      ++i_k;
     }
   };
 
