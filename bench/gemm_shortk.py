@@ -38,10 +38,27 @@ def main():
     ap.add_argument("--tag", default=os.environ.get("DCA_TAG", "default"))
     ap.add_argument("--shape", default=None, help="MxNxK: only this shape")
     ap.add_argument("--beta", action="store_true", help="accumulate into the output (C += A B^T), no statistics")
+    ap.add_argument("--conv", default=None,
+                    help="NxHxCxCO[xKxSxP]: an implicit convolution forward instead (default 3x3, stride 1, pad 1)")
     a = ap.parse_args()
     shapes = [tuple(int(v) for v in a.shape.split("x"))] if a.shape else SHAPES
     dev = torch.device("cuda", 0)
     bf = torch.bfloat16
+    if a.conv:
+        from distributeddataparallel_cifar10_amd.ops import functional as F
+        v = [int(t) for t in a.conv.split("x")]
+        n, h, c, co = v[:4]
+        kk, st, pd = v[4:7] if len(v) >= 7 else (3, 1, 1)
+        x = torch.randn(n, h, h, c, device=dev).to(bf)
+        wt = torch.randn(co, c, kk, kk, device=dev) * 0.05
+        geo = F._geom(x, wt, st, pd)
+        wm = F._weight_matrix(wt, geo.K)
+        M = n * geo.Ho * geo.Wo
+        kw = dict(col_stats=torch.zeros((M + 127) // 128, co, 2, device=dev), stats_shift=torch.zeros(co, device=dev))
+        us = timeit(lambda: ops.gemm(x, wm, conv=1, geom=geo, mnk=(M, co, geo.K), out_dtype=bf, **kw))
+        print(json.dumps({"tag": a.tag, "conv3x3": a.conv, "us": round(us, 1),
+                          "tflops": round(2 * M * co * geo.K / us / 1e6, 1)}), flush=True)
+        return
     for M, N, K in shapes:
         x = torch.randn(M, K, device=dev).to(bf)
         w = torch.randn(N, K, device=dev).to(bf)
