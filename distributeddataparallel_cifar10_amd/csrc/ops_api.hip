@@ -287,6 +287,7 @@ int dca_ops_gemm(const GemmArgs* a, void* stream) {
     const long long cbytes = (long long)g.M * g.ldc * 2;
     const int mw = g.N % 128 == 0 ? 1 : 2;  // 128 x 128 tiles, or 256 x 64 for N % 128 == 64
     const bool shape_ok = conv ? (g.cC % 64 == 0 && g.cKH * g.cKW <= 32 && (g.N == 64 || g.N == 128) && g.orow_S <= 0 &&
+                                  g.M < (1 << 24) &&
                                   (sk == 1 || (sk == 2 && getenv_stream_conv() && g.N == 128 && g.M >= 16384)))
                                : (g.conv == 0 && !g.ta && g.lda % 8 == 0 && g.lda >= g.K &&
                                   (g.N % 128 == 0 || g.N == 64) &&

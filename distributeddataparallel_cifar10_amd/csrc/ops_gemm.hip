@@ -611,6 +611,32 @@ __global__ void __launch_bounds__(GT) k_gemm(GemmArgs g) {
 // Out-of-range chunks (K tail, conv padding) load from a zeroed global word.
 // ---------------------------------------------------------------------------------------------------------
 __device__ __attribute__((aligned(16))) unsigned char g_gemm_zero16[16];
+// x / d and x % d for 0 <= x < 2^24 by a float reciprocal and one correction (a runtime-divisor integer division
+// is ~20-40 instructions; these decodes run once per tile row)
+__device__ __forceinline__ int fdiv_rc(int x, int d, float inv, int& r) {
+  int q = (int)((float)x * inv);
+  r = x - q * d;
+  if (r < 0) {
+    --q;
+    r += d;
+  }
+  if (r >= d) {
+    ++q;
+    r -= d;
+  }
+  return q;
+}
+// valid-tap mask of an implicit-conv row whose window starts at (ih0, iw0): bit kh * KW + kw, from the valid
+// kh / kw ranges (rep = sum over kh of 1 << kh * KW spreads the kw bits over the kernel rows)
+__device__ __forceinline__ unsigned tap_mask(int ih0, int iw0, int H, int W, int KH, int KW, unsigned rep) {
+  const int khlo = ih0 < 0 ? -ih0 : 0, khhi = min(KH, H - ih0);
+  const int kwlo = iw0 < 0 ? -iw0 : 0, kwhi = min(KW, W - iw0);
+  const unsigned long long rows =
+      khhi > khlo ? ((1ull << (khhi * KW)) - 1ull) & ~((1ull << (khlo * KW)) - 1ull) : 0ull;
+  const unsigned cols = kwhi > kwlo ? ((1u << kwhi) - 1u) & ~((1u << kwlo) - 1u) : 0u;
+  return (unsigned)rows & (cols * rep);
+}
+
 
 __device__ __forceinline__ void glds16(const void* src, char* lds_wave_base) {
   __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
@@ -648,6 +674,14 @@ __global__ void __launch_bounds__(NW * 64) k_gemm_glds(GemmArgs g) {
   const int nk = (k_end - k_begin + KT - 1) / KT;
   const int lr = lane >> 3, lj = lane & 7;
 
+  const bool c64 = g.conv == 1 && g.cC % KT == 0;
+  constexpr unsigned OOB = 0x80000000u;
+  const long long a_bytes = g.conv == 1 ? (long long)g.cN * g.cH * g.cW * g.cC * ESZ
+                                        : ((long long)(g.M - 1) * g.lda + g.K) * ESZ;
+  const long long b_bytes = ((long long)(g.N - 1) * g.ldb + g.K) * ESZ;
+  const int ntaps = g.cKH * g.cKW;
+  const bool fast = a_bytes < OOB && b_bytes < OOB && (g.conv == 0 || (c64 && ntaps <= 32 && g.M < (1 << 24)));
+
   // per-lane rows: A row wave*32 + i*8 + lr, B row wave*(BN_/4) + i*8 + lr
   const char* arow[NAI];
   int nh[NAI], ih[NAI], iw[NAI];
@@ -656,7 +690,7 @@ __global__ void __launch_bounds__(NW * 64) k_gemm_glds(GemmArgs g) {
     int m = m0 + wave * RA + i * 8 + lr;
     m = m < g.M ? m : g.M - 1;
     arow[i] = (const char*)g.A + (size_t)m * g.lda * ESZ;
-    if (g.conv == 1) {
+    if (g.conv == 1 && !fast) {
       const int ow = m % g.cWo, t = m / g.cWo, oh = t % g.cHo, n = t / g.cHo;
       nh[i] = n * g.cH;
       ih[i] = oh * g.cS - g.cP;
@@ -672,20 +706,12 @@ __global__ void __launch_bounds__(NW * 64) k_gemm_glds(GemmArgs g) {
   }
   const int kb_end = k_end * ESZ;
 
-  const bool c64 = g.conv == 1 && g.cC % KT == 0;
-
   // Fast path (plain K-contiguous operands, or the implicit conv with C % 64 == 0): buffer_load ... lds with the
   // per-lane byte offsets computed once here, so a K-tile costs one add per load (plus, for the conv, a tap
   // validity test against a per-row mask) and the tap / channel position advances without divisions.  The
   // profile of the general path (profiles/gemm_pmc_r2.txt): ~7 VALU and ~8 SALU per MFMA on the 3x3 conv, the
   // issue bound of that kernel.  Out-of-range lanes (rows past M / N, padding taps, the K tail) get an offset
   // past the descriptor's range, which loads zeros.
-  constexpr unsigned OOB = 0x80000000u;
-  const long long a_bytes = g.conv == 1 ? (long long)g.cN * g.cH * g.cW * g.cC * ESZ
-                                        : ((long long)(g.M - 1) * g.lda + g.K) * ESZ;
-  const long long b_bytes = ((long long)(g.N - 1) * g.ldb + g.K) * ESZ;
-  const int ntaps = g.cKH * g.cKW;
-  const bool fast = a_bytes < OOB && b_bytes < OOB && (g.conv == 0 || (c64 && ntaps <= 32));
   const __amdgpu_buffer_rsrc_t ars = __builtin_amdgcn_make_buffer_rsrc((void*)g.A, (short)0, (int)(fast ? a_bytes : 0),
                                                                        0x00020000);
   const __amdgpu_buffer_rsrc_t brs = __builtin_amdgcn_make_buffer_rsrc((void*)g.B, (short)0, (int)(fast ? b_bytes : 0),
@@ -693,22 +719,21 @@ __global__ void __launch_bounds__(NW * 64) k_gemm_glds(GemmArgs g) {
   unsigned aoff[NAI], amask[NAI], boff[NBI];
   int s_tap = 0, s_kh = 0, s_kw = 0, s_c0b = 0, s_tapoff = 0;  // conv: position of the next tile to issue
   if (fast) {
+    const float inv_wo = g.conv == 1 ? 1.f / (float)g.cWo : 0.f, inv_ho = g.conv == 1 ? 1.f / (float)g.cHo : 0.f;
+    unsigned rep = 0u;
+    if (g.conv == 1)
+      for (int kh = 0; kh < g.cKH; ++kh) rep |= 1u << (kh * g.cKW);
 #pragma unroll
     for (int i = 0; i < NAI; ++i) {
       const int r = wave * RA + i * 8 + lr, m = m0 + r;
       const unsigned cb = (unsigned)(lj ^ ((r >> 1) & 7)) << 4;
-      if (g.conv == 1) {
-        amask[i] = 0u;
-        aoff[i] = 0u;
-        if (m < g.M) {
-          const int ow = m % g.cWo, t = m / g.cWo, oh = t % g.cHo, n = t / g.cHo;
-          const int ih0 = oh * g.cS - g.cP, iw0 = ow * g.cS - g.cP;
-          const long long ro = (((long long)n * g.cH + ih0) * g.cW + iw0) * g.cC * ESZ;
-          aoff[i] = (unsigned)(ro + cb);  // wraps for padding rows; only used when the tap is valid
-          for (int kh = 0; kh < g.cKH; ++kh)
-            for (int kw = 0; kw < g.cKW; ++kw)
-              if (ih0 + kh >= 0 && ih0 + kh < g.cH && iw0 + kw >= 0 && iw0 + kw < g.cW) amask[i] |= 1u << (kh * g.cKW + kw);
-        }
+      if (g.conv == 1) {  // float-reciprocal row decode, range-based tap mask (no per-tap loop)
+        int ow, oh;
+        const int t = fdiv_rc(m < g.M ? m : 0, g.cWo, inv_wo, ow), n = fdiv_rc(t, g.cHo, inv_ho, oh);
+        const int ih0 = oh * g.cS - g.cP, iw0 = ow * g.cS - g.cP;
+        const long long ro = (((long long)n * g.cH + ih0) * g.cW + iw0) * g.cC * ESZ;
+        aoff[i] = (unsigned)(ro + cb);  // wraps for padding rows; only used when the tap is valid
+        amask[i] = m < g.M ? tap_mask(ih0, iw0, g.cH, g.cW, g.cKH, g.cKW, rep) : 0u;
       } else {
         aoff[i] = m < g.M ? (unsigned)((long long)m * g.lda * ESZ) + cb : OOB;
       }
@@ -1249,6 +1274,10 @@ __global__ void __launch_bounds__(ST_NT, 2) k_gemm_stream(GemmArgs g) {
       (void*)g.col_stats, (short)0, g.col_stats ? (int)((long long)nstat * g.N * 8) : 0, 0x00020000);
   const unsigned lda2 = (unsigned)g.lda * 2u, ldb2 = (unsigned)g.ldb * 2u;
   const int cpt = CONV ? g.cC / 64 : 1;  // K-steps per tap
+  const float inv_wo = CONV ? 1.f / (float)g.cWo : 0.f, inv_ho = CONV ? 1.f / (float)g.cHo : 0.f;
+  unsigned rep = 0u;  // bit kh * KW set for every kh: spreads a kw mask over the kernel rows
+  if constexpr (CONV)
+    for (int kh = 0; kh < g.cKH; ++kh) rep |= 1u << (kh * g.cKW);
 
   // issue side: A row offsets (and conv tap masks) of the tile whose K-steps are being issued
   unsigned aoff[NAI], amask[NAI];
@@ -1265,17 +1294,14 @@ __global__ void __launch_bounds__(ST_NT, 2) k_gemm_stream(GemmArgs g) {
         const int r = 8 * NAI * w + 8 * i + (lane >> 3), m = itm * TM + r;
         const unsigned cb = (unsigned)((lane & 7) ^ ((r >> 1) & 7)) << 4;
         if constexpr (CONV) {
-          amask[i] = 0u;
-          aoff[i] = 0u;
-          if (m < g.M) {
-            const int ow = m % g.cWo, t2 = m / g.cWo, oh = t2 % g.cHo, n = t2 / g.cHo;
-            const int ih0 = oh * g.cS - g.cP, iw0 = ow * g.cS - g.cP;
-            aoff[i] = (unsigned)((((long long)n * g.cH + ih0) * g.cW + iw0) * g.cC * 2) + cb;  // wraps for padding
-            for (int kh = 0; kh < g.cKH; ++kh)
-              for (int kw = 0; kw < g.cKW; ++kw)
-                if (ih0 + kh >= 0 && ih0 + kh < g.cH && iw0 + kw >= 0 && iw0 + kw < g.cW)
-                  amask[i] |= 1u << (kh * g.cKW + kw);
-          }
+          // row decode by float-reciprocal division (exact after one correction: m < 2^24, launcher-checked) and
+          // the tap mask from the valid kh / kw ranges: rows(kh) & (cols(kw) x rep) -- the per-tap loop and two
+          // integer divisions per row were ~200 VALU per K-step (PMC, profiles/gemm_stream_pmc_r2.txt)
+          int ow, oh;
+          const int t2 = fdiv_rc(m < g.M ? m : 0, g.cWo, inv_wo, ow), n = fdiv_rc(t2, g.cHo, inv_ho, oh);
+          const int ih0 = oh * g.cS - g.cP, iw0 = ow * g.cS - g.cP;
+          aoff[i] = (unsigned)((((long long)n * g.cH + ih0) * g.cW + iw0) * g.cC * 2) + cb;  // wraps for padding
+          amask[i] = m < g.M ? tap_mask(ih0, iw0, g.cH, g.cW, g.cKH, g.cKW, rep) : 0u;
         } else {
           aoff[i] = m < g.M ? (unsigned)m * lda2 + cb : OOB;
         }
