@@ -164,6 +164,7 @@ int dca_ops_gemm(const GemmArgs* a, void* stream) {
   REQUIRE(g.conv == 1 || !g.ta || g.lda >= g.M, "gemm: lda < M (transposed A)");
   REQUIRE(g.ldc >= g.N, "gemm: ldc < N");
   REQUIRE(g.conv >= 0 && g.conv <= 2, "gemm: bad conv mode");
+  REQUIRE(g.conv != 1 || g.K < (1 << 24), "gemm: implicit conv K >= 2^24");
   if (g.conv) {
     REQUIRE(g.cC > 0 && (g.fp8 ? (g.conv == 1 && g.cC % 16 == 0) : g.cC % 8 == 0),
             "gemm: implicit conv needs C % 8 == 0 (bf16) or an fp8 forward with C % 16 == 0");
@@ -340,7 +341,7 @@ int dca_ops_gemm(const GemmArgs* a, void* stream) {
     const bool pp = pp_shape && !g.fp8 && !g.ta && !g.tb && g.splits == 1 && g.wperm_T <= 0 && g.orow_S <= 0 &&
                     !g.bnb_part && g.M >= 256 && g.N >= 128 && g.K >= 256 && ab < (1LL << 31) && bb < (1LL << 31) &&
                     (long)g.ldb * 2 % 16 == 0 && ((uintptr_t)g.A & 15) == 0 && ((uintptr_t)g.B & 15) == 0 &&
-                    (g.conv == 1 ? (g.cC % 64 == 0 && g.cKH * g.cKW <= 32)
+                    (g.conv == 1 ? (g.cC % 64 == 0 && g.cKH * g.cKW <= 32 && g.M < (1 << 24))
                                  : (g.conv == 0 && (long)g.lda * 2 % 16 == 0 && (long)g.K * 2 % 16 == 0));
     if (pp) {
       if (ppbn == 256) hipLaunchKernelGGL(k_gemm_pp<256>, dim3((unsigned)pp_tiles), dim3(PP_NT), PpTile<256>::LDS, st, g);

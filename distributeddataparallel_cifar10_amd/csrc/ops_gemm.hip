@@ -185,6 +185,32 @@ __device__ __forceinline__ void store_t(const Stage& s, char* lds) {
   }
 }
 
+// x / d and x % d for 0 <= x < 2^24 by a float reciprocal and one correction (a runtime-divisor integer division
+// is ~20-40 instructions; these decodes run once per tile row)
+__device__ __forceinline__ int fdiv_rc(int x, int d, float inv, int& r) {
+  int q = (int)((float)x * inv);
+  r = x - q * d;
+  if (r < 0) {
+    --q;
+    r += d;
+  }
+  if (r >= d) {
+    ++q;
+    r -= d;
+  }
+  return q;
+}
+// valid-tap mask of an implicit-conv row whose window starts at (ih0, iw0): bit kh * KW + kw, from the valid
+// kh / kw ranges (rep = sum over kh of 1 << kh * KW spreads the kw bits over the kernel rows)
+__device__ __forceinline__ unsigned tap_mask(int ih0, int iw0, int H, int W, int KH, int KW, unsigned rep) {
+  const int khlo = ih0 < 0 ? -ih0 : 0, khhi = min(KH, H - ih0);
+  const int kwlo = iw0 < 0 ? -iw0 : 0, kwhi = min(KW, W - iw0);
+  const unsigned long long rows =
+      khhi > khlo ? ((1ull << (khhi * KW)) - 1ull) & ~((1ull << (khlo * KW)) - 1ull) : 0ull;
+  const unsigned cols = kwhi > kwlo ? ((1u << kwhi) - 1u) & ~((1u << kwlo) - 1u) : 0u;
+  return (unsigned)rows & (cols * rep);
+}
+
 // Implicit-GEMM gathers.  Per-thread row decompositions are computed once per tile (the rows a thread loads
 // are fixed across the K loop); every load is unconditional from a clamped address, then selected to zero.
 struct ConvRows {  // conv = 1: the 4 output pixels (A rows) this thread loads
@@ -195,7 +221,13 @@ __device__ __forceinline__ void conv_rows(ConvRows& cr, const GemmArgs& g, int m
   for (int i = 0; i < 4; ++i) {
     int m = m0 + ((threadIdx.x + GT * i) >> 3);
     m = m < g.M ? m : g.M - 1;
-    const int ow = m % g.cWo, t = m / g.cWo, oh = t % g.cHo, n = t / g.cHo;
+    int ow, t, oh, n;
+    if (g.M < (1 << 24)) {  // float-reciprocal decode (runtime-divisor divisions are ~20-40 instructions each)
+      t = fdiv_rc(m, g.cWo, 1.f / (float)g.cWo, ow);
+      n = fdiv_rc(t, g.cHo, 1.f / (float)g.cHo, oh);
+    } else {
+      ow = m % g.cWo, t = m / g.cWo, oh = t % g.cHo, n = t / g.cHo;
+    }
     cr.nh[i] = n * g.cH;
     cr.ih[i] = oh * g.cS - g.cP;
     cr.iw[i] = ow * g.cS - g.cP;
@@ -206,7 +238,8 @@ template <int ESZ>
 __device__ __forceinline__ void load_conv_a(Stage& s, const char* x, const ConvRows& cr, const GemmArgs& g, int k0,
                                             int k_end) {
   const int k = k0 + (threadIdx.x & 7) * (16 / ESZ);  // one tap per chunk
-  const int tap = k / g.cC, c = k - tap * g.cC, kh = tap / g.cKW, kw = tap - kh * g.cKW;
+  int c, kw;  // (K < 2^24: checked by the launcher for implicit convs)
+  const int tap = fdiv_rc(k, g.cC, 1.f / (float)g.cC, c), kh = fdiv_rc(tap, g.cKW, 1.f / (float)g.cKW, kw);
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     const int h = cr.ih[i] + kh, w = cr.iw[i] + kw;
@@ -611,31 +644,6 @@ __global__ void __launch_bounds__(GT) k_gemm(GemmArgs g) {
 // Out-of-range chunks (K tail, conv padding) load from a zeroed global word.
 // ---------------------------------------------------------------------------------------------------------
 __device__ __attribute__((aligned(16))) unsigned char g_gemm_zero16[16];
-// x / d and x % d for 0 <= x < 2^24 by a float reciprocal and one correction (a runtime-divisor integer division
-// is ~20-40 instructions; these decodes run once per tile row)
-__device__ __forceinline__ int fdiv_rc(int x, int d, float inv, int& r) {
-  int q = (int)((float)x * inv);
-  r = x - q * d;
-  if (r < 0) {
-    --q;
-    r += d;
-  }
-  if (r >= d) {
-    ++q;
-    r -= d;
-  }
-  return q;
-}
-// valid-tap mask of an implicit-conv row whose window starts at (ih0, iw0): bit kh * KW + kw, from the valid
-// kh / kw ranges (rep = sum over kh of 1 << kh * KW spreads the kw bits over the kernel rows)
-__device__ __forceinline__ unsigned tap_mask(int ih0, int iw0, int H, int W, int KH, int KW, unsigned rep) {
-  const int khlo = ih0 < 0 ? -ih0 : 0, khhi = min(KH, H - ih0);
-  const int kwlo = iw0 < 0 ? -iw0 : 0, kwhi = min(KW, W - iw0);
-  const unsigned long long rows =
-      khhi > khlo ? ((1ull << (khhi * KW)) - 1ull) & ~((1ull << (khlo * KW)) - 1ull) : 0ull;
-  const unsigned cols = kwhi > kwlo ? ((1u << kwhi) - 1u) & ~((1u << kwlo) - 1u) : 0u;
-  return (unsigned)rows & (cols * rep);
-}
 
 
 __device__ __forceinline__ void glds16(const void* src, char* lds_wave_base) {
@@ -957,21 +965,20 @@ __global__ void __launch_bounds__(PP_NT) k_gemm_pp(GemmArgs g) {
   const __amdgpu_buffer_rsrc_t brs = __builtin_amdgcn_make_buffer_rsrc((void*)g.B, (short)0, (int)b_bytes, 0x00020000);
   unsigned aoff[NI], amask[NI], boff[TT::NIB];
   int s_tap = 0, s_kh = 0, s_kw = 0, s_c0b = 0, s_tapoff = 0;
+  const float inv_wo = g.conv == 1 ? 1.f / (float)g.cWo : 0.f, inv_ho = g.conv == 1 ? 1.f / (float)g.cHo : 0.f;
+  unsigned rep = 0u;
+  if (g.conv == 1)
+    for (int kh = 0; kh < g.cKH; ++kh) rep |= 1u << (kh * g.cKW);
 #pragma unroll
   for (int i = 0; i < NI; ++i) {
     const int r = wave * 32 + i * 8 + lr, m = m0 + r;
     const unsigned cb = (unsigned)(lj ^ ((r >> 1) & 7)) << 4;
-    if (g.conv == 1) {
-      amask[i] = 0u;
-      aoff[i] = 0u;
-      if (m < g.M) {
-        const int ow = m % g.cWo, t = m / g.cWo, oh = t % g.cHo, n = t / g.cHo;
-        const int ih0 = oh * g.cS - g.cP, iw0 = ow * g.cS - g.cP;
-        aoff[i] = (unsigned)((((long long)n * g.cH + ih0) * g.cW + iw0) * g.cC * ESZ + cb);
-        for (int kh = 0; kh < g.cKH; ++kh)
-          for (int kw = 0; kw < g.cKW; ++kw)
-            if (ih0 + kh >= 0 && ih0 + kh < g.cH && iw0 + kw >= 0 && iw0 + kw < g.cW) amask[i] |= 1u << (kh * g.cKW + kw);
-      }
+    if (g.conv == 1) {  // float-reciprocal row decode (M < 2^24: launcher), range-built tap mask
+      int ow, oh;
+      const int t = fdiv_rc(m < g.M ? m : 0, g.cWo, inv_wo, ow), n = fdiv_rc(t, g.cHo, inv_ho, oh);
+      const int ih0 = oh * g.cS - g.cP, iw0 = ow * g.cS - g.cP;
+      aoff[i] = (unsigned)((((long long)n * g.cH + ih0) * g.cW + iw0) * g.cC * ESZ + cb);
+      amask[i] = m < g.M ? tap_mask(ih0, iw0, g.cH, g.cW, g.cKH, g.cKW, rep) : 0u;
     } else {
       amask[i] = 0u;
       aoff[i] = m < g.M ? (unsigned)((long long)m * g.lda * ESZ) + cb : OOB;
