@@ -652,7 +652,7 @@ int dca_engine_read_loss(void* h, double* loss, int* steps, int reset) {
 }
 
 // Enqueue `nsteps` training steps of batch B.  use_graph: replay a captured hipGraph (captured on first use).
-constexpr int GRAPH_CHUNK = 16;  // steps per graph replay
+constexpr int GRAPH_CHUNK = 16;  // steps per graph replay (remainders: 8 / 4 / 2 / 1-step graphs, <= 4 extra launches)
 
 // The executable graph of `chunk` consecutive steps of batch B (captured and instantiated on first use).
 static hipGraphExec_t capture_graph(Engine* e, int B, int chunk) {
@@ -708,7 +708,7 @@ int dca_engine_run(void* h, int B, int nsteps, int use_graph) {
   // gap between graph launches on the GPU (rocprofv3, profiles/), inside a graph consecutive kernels are
   // back to back.
   int done = 0;
-  for (const int chunk : {GRAPH_CHUNK, 1}) {
+  for (const int chunk : {GRAPH_CHUNK, 8, 4, 2, 1}) {
     const int reps = (nsteps - done) / chunk;
     if (reps == 0) continue;
     hipGraphExec_t ex = capture_graph(e, B, chunk);
@@ -728,7 +728,7 @@ int dca_engine_precapture(void* h, int B) {
     return -1;
   }
   if (e->in.world_size > 1 && e->in.comm_mode == 1) return 0;  // external all-reduce: eager only
-  for (const int chunk : {GRAPH_CHUNK, 1})
+  for (const int chunk : {GRAPH_CHUNK, 8, 4, 2, 1})
     if (capture_graph(e, B, chunk) == nullptr) return -1;
   HIPCK(hipStreamSynchronize(e->st));
   return 0;

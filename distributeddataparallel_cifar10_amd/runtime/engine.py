@@ -274,7 +274,7 @@ class NetResDeepEngine:
         self.sync()
 
     def precapture(self, batch: int) -> None:
-        """Capture the step graphs ``run(batch, ...)`` replays (16-step and 1-step chunks) without running them, so
+        """Capture the step graphs ``run(batch, ...)`` replays (16 / 8 / 4 / 2 / 1-step chunks) without running them, so
         a timed region never includes graph capture / instantiation."""
         native.check(self.lib.dca_engine_precapture(self.h, int(batch)), "dca_engine_precapture")
 
