@@ -683,6 +683,13 @@ static hipGraphExec_t capture_graph(Engine* e, int B, int chunk) {
     g_err = std::string("hipGraphInstantiate: ") + hipGetErrorString(ec);
     return nullptr;
   }
+  // upload now (stream-ordered), so the first replay -- possibly inside a timed region -- does not pay it
+  ec = hipGraphUpload(ex, e->st);
+  if (ec != hipSuccess) {
+    (void)hipGraphExecDestroy(ex);
+    g_err = std::string("hipGraphUpload: ") + hipGetErrorString(ec);
+    return nullptr;
+  }
   e->graphs.emplace(key, ex);
   return ex;
 }
