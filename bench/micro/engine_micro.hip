@@ -165,6 +165,321 @@ __global__ void __launch_bounds__(NTH) k_mb_xchg2(unsigned long long* gran, unsi
   }
   if (t == 0 && keep == 12345.f) err[1] = 1;
 }
+
+// BN-statistics exchange variants of the sliced engine, with emulated per-round compute and jitter (512-thread
+// workgroups, 64 fp32 partials per workgroup and round, every workgroup needs the 64 sums over all G):
+//   V0: one hop, 8-byte {value, tag} granules, every workgroup sweeps G x 512 B (the round-2 engine);
+//   V1: one hop, 4-byte self-tagged values (tag in the 2 low mantissa bits), sweep G x 256 B;
+//   V2: two hops, 8-byte granules: group k = L % 8 (one XCD under round-robin dispatch) is summed by its leader
+//       (L = k, sweeps G / 8 x 512 B) and published as a group record; every workgroup sweeps the 8 records (4 KB);
+//   V3: V2 with 4-byte self-tagged values (leader sweeps G / 8 x 256 B, everyone 8 x 256 B).
+// work / jitter in 10-ns ticks (s_memrealtime): round r of workgroup L "computes" work + hash(L, r) % jitter.
+__device__ __forceinline__ unsigned mb_tag4(int r) { return 1u + (unsigned)((r >> 1) % 3); }
+__device__ __forceinline__ void mb_st4(unsigned* p, unsigned tag4, float v) {
+  __hip_atomic_store(p, (__float_as_uint(v) & ~3u) | tag4, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void mb_st8(unsigned long long* p, unsigned tag, float v) {
+  __hip_atomic_store(p, ((unsigned long long)tag << 32) | __float_as_uint(v), __ATOMIC_RELAXED,
+                     __HIP_MEMORY_SCOPE_AGENT);
+}
+// 8-byte granule sweep: lanes 32 hf + j read slots 2j, 2j+1 of unit (2 wv + hf + 16 k); result per wave in cred
+template <int KS>
+__device__ bool mb_sweep8(const unsigned long long* base, int nunit, int ustride, int wv, int lane, unsigned tag,
+                          float* cred, unsigned* err) {
+  const int j = lane & 31, hf = lane >> 5;
+  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)base, (short)0, 0x7ffffff0, 0x00020000);
+  float s0 = 0.f, s1 = 0.f;
+  for (unsigned spins = 0;; ++spins) {
+    asm volatile("" ::: "memory");
+    typedef unsigned v4u_ __attribute__((ext_vector_type(4)));
+    v4u_ x[KS];
+#pragma unroll
+    for (int k = 0; k < KS; ++k) {
+      const int u = 2 * wv + hf + 16 * k, uc = u < nunit ? u : nunit - 1;
+      x[k] = __builtin_amdgcn_raw_buffer_load_b128(rs, (uc * ustride + 2 * j) * 8, 0, 16);
+    }
+    bool ok = true;
+    s0 = s1 = 0.f;
+#pragma unroll
+    for (int k = 0; k < KS; ++k) {
+      const bool valid = 2 * wv + hf + 16 * k < nunit;
+      ok &= !valid || (x[k][1] == tag && x[k][3] == tag);
+      s0 += valid ? __uint_as_float(x[k][0]) : 0.f;
+      s1 += valid ? __uint_as_float(x[k][2]) : 0.f;
+    }
+    if (__all(ok)) break;
+    if (spins > (1u << 20)) {
+      if (lane == 0) atomicOr(err, 1u);
+      break;
+    }
+  }
+  s0 += __shfl_xor(s0, 32);
+  s1 += __shfl_xor(s1, 32);
+  if (lane < 32) {
+    cred[wv * 64 + 2 * lane] = s0;
+    cred[wv * 64 + 2 * lane + 1] = s1;
+  }
+  return true;
+}
+// 4-byte self-tagged sweep: lanes 16 sub + q read slots 4q .. 4q+3 of unit (4 wv + sub + 32 k)
+template <int KS>
+__device__ bool mb_sweep4(const unsigned* base, int nunit, int ustride, int wv, int lane, unsigned tag4, float* cred,
+                          unsigned* err) {
+  const int q = lane & 15, sub = lane >> 4;
+  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)base, (short)0, 0x7ffffff0, 0x00020000);
+  float s[4];
+  for (unsigned spins = 0;; ++spins) {
+    asm volatile("" ::: "memory");
+    typedef unsigned v4u_ __attribute__((ext_vector_type(4)));
+    v4u_ x[KS];
+#pragma unroll
+    for (int k = 0; k < KS; ++k) {
+      const int u = 4 * wv + sub + 32 * k, uc = u < nunit ? u : nunit - 1;
+      x[k] = __builtin_amdgcn_raw_buffer_load_b128(rs, (uc * ustride + 4 * q) * 4, 0, 16);
+    }
+    bool ok = true;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) s[i] = 0.f;
+#pragma unroll
+    for (int k = 0; k < KS; ++k) {
+      const bool valid = 4 * wv + sub + 32 * k < nunit;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        ok &= !valid || (x[k][i] & 3u) == tag4;
+        s[i] += valid ? __uint_as_float(x[k][i]) : 0.f;
+      }
+    }
+    if (__all(ok)) break;
+    if (spins > (1u << 20)) {
+      if (lane == 0) atomicOr(err, 1u);
+      break;
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    s[i] += __shfl_xor(s[i], 16);
+    s[i] += __shfl_xor(s[i], 32);
+  }
+  if (lane < 16) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) cred[wv * 64 + 4 * q + i] = s[i];
+  }
+  return true;
+}
+__device__ __forceinline__ unsigned mb_xcc_id() {
+  unsigned v;
+  asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID, 0, 4)" : "=s"(v));
+  return v;
+}
+// V4: census of the workgroups' XCDs (HW_REG_XCC_ID) at kernel start; per round the members of one XCD hand their
+// partials to that XCD's leader through the XCD's L2 (plain granule stores, sc1 = L1-bypassing loads served by the
+// shared L2), the leaders publish XCD records write-through (sc1), every workgroup sweeps the <= 8 records.
+__device__ void mb_bnx_v4(unsigned* buf, unsigned* err, int rounds, int work, int jitter) {
+  const int t = threadIdx.x, lane = t & 63, wv = t >> 6, L = blockIdx.x, G = gridDim.x;
+  __shared__ float cred[8 * 64];
+  __shared__ int xcl[256];
+  __shared__ int mlist[256];
+  __shared__ int s_info[16];  // [2] this workgroup leads its XCD, [8 + v] members of xcc v
+  unsigned long long* cen = (unsigned long long*)buf + (size_t)2 * 256 * 64 + 2 * 8 * 64;
+  const unsigned myx = mb_xcc_id();
+  if (t == 0) mb_st8(cen + L, 1u, __uint_as_float(myx));
+  for (int k = t; k < G; k += 512) {
+    unsigned long long x;
+    for (unsigned spins = 0;; ++spins) {
+      x = __hip_atomic_load(cen + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if ((x >> 32) == 1u) break;
+      if (spins > (1u << 20)) {
+        atomicOr(err, 1u);
+        break;
+      }
+    }
+    xcl[k] = (int)(unsigned)x & 7;
+  }
+  __syncthreads();
+  if (t < 8) {
+    int n = 0;
+    for (int k = 0; k < G; ++k) n += xcl[k] == t;
+    s_info[8 + t] = n;
+  }
+  if (t < G && xcl[t] == (int)myx) {
+    int m = 0;
+    for (int k = 0; k < t; ++k) m += xcl[k] == (int)myx;
+    mlist[m] = t;
+    if (t == L) s_info[2] = m == 0;
+  }
+  __syncthreads();
+  const int nm = s_info[8 + myx] < 32 ? s_info[8 + myx] : 32;  // (<= 32 members per XCD for G <= 256)
+  const bool leader = s_info[2] != 0;
+  float keep = 0.f;
+  for (int r = 0; r < rounds; ++r) {
+    {
+      unsigned h = (unsigned)L * 2654435761u ^ (unsigned)r * 40503u;
+      h ^= h >> 13;
+      h *= 0x5bd1e995u;
+      h ^= h >> 15;
+      const unsigned long long dl = (unsigned long long)work + (jitter > 0 ? h % (unsigned)jitter : 0u);
+      const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+      while (__builtin_amdgcn_s_memrealtime() - t0 < dl) __builtin_amdgcn_s_sleep(1);
+    }
+    const float v = (float)((L + lane) & 7) + keep;
+    const int par = r & 1;
+    const unsigned tag = (unsigned)(r + 1);
+    unsigned long long* A8 = (unsigned long long*)buf + (size_t)par * 256 * 64;
+    unsigned long long* B8 = (unsigned long long*)buf + (size_t)2 * 256 * 64 + par * 8 * 64;
+    if (wv == 0)  // plain 8-byte store: stays in this XCD's L2, where the leader's sc1 loads read it
+      __hip_atomic_store(A8 + L * 64 + lane, ((unsigned long long)tag << 32) | __float_as_uint(v), __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_WORKGROUP);
+    if (leader) {
+      const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)A8, (short)0, 0x7ffffff0, 0x00020000);
+      const int j = lane & 31, hf = lane >> 5;
+      float s0 = 0.f, s1 = 0.f;
+      for (unsigned spins = 0;; ++spins) {
+        asm volatile("" ::: "memory");
+        typedef unsigned v4u_ __attribute__((ext_vector_type(4)));
+        v4u_ x[2];
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {
+          const int u = 2 * wv + hf + 16 * k, uc = mlist[u < nm ? u : nm - 1];
+          x[k] = __builtin_amdgcn_raw_buffer_load_b128(rs, (uc * 64 + 2 * j) * 8, 0, 16);
+        }
+        bool ok = true;
+        s0 = s1 = 0.f;
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {
+          const bool valid = 2 * wv + hf + 16 * k < nm;
+          ok &= !valid || (x[k][1] == tag && x[k][3] == tag);
+          s0 += valid ? __uint_as_float(x[k][0]) : 0.f;
+          s1 += valid ? __uint_as_float(x[k][2]) : 0.f;
+        }
+        if (__all(ok)) break;
+        if (spins > (1u << 20)) {
+          if (lane == 0) atomicOr(err, 1u);
+          break;
+        }
+      }
+      s0 += __shfl_xor(s0, 32);
+      s1 += __shfl_xor(s1, 32);
+      if (lane < 32) {
+        cred[wv * 64 + 2 * lane] = s0;
+        cred[wv * 64 + 2 * lane + 1] = s1;
+      }
+      __syncthreads();
+      if (wv == 0) {
+        float s = 0.f;
+        for (int k = 0; k < 8; ++k) s += cred[k * 64 + lane];
+        mb_st8(B8 + myx * 64 + lane, tag, s);
+      }
+      __syncthreads();
+    }
+    // every workgroup: the records of the XCDs that have members (waves 0..3: xcc 2 wv + hf)
+    if (wv < 4) {
+      const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)B8, (short)0, 0x7ffffff0, 0x00020000);
+      const int j = lane & 31, hf = lane >> 5, xv = 2 * wv + hf;
+      const bool valid = s_info[8 + xv] > 0;
+      float s0 = 0.f, s1 = 0.f;
+      for (unsigned spins = 0;; ++spins) {
+        asm volatile("" ::: "memory");
+        typedef unsigned v4u_ __attribute__((ext_vector_type(4)));
+        const v4u_ x = __builtin_amdgcn_raw_buffer_load_b128(rs, (xv * 64 + 2 * j) * 8, 0, 16);
+        const bool ok = !valid || (x[1] == tag && x[3] == tag);
+        s0 = valid ? __uint_as_float(x[0]) : 0.f;
+        s1 = valid ? __uint_as_float(x[2]) : 0.f;
+        if (__all(ok)) break;
+        if (spins > (1u << 20)) {
+          if (lane == 0) atomicOr(err, 1u);
+          break;
+        }
+      }
+      s0 += __shfl_xor(s0, 32);
+      s1 += __shfl_xor(s1, 32);
+      if (lane < 32) {
+        cred[wv * 64 + 2 * lane] = s0;
+        cred[wv * 64 + 2 * lane + 1] = s1;
+      }
+    }
+    __syncthreads();
+    float s = 0.f;
+    for (int k = 0; k < 4; ++k) s += cred[k * 64 + lane];
+    keep = s * 1e-9f;
+    __syncthreads();
+  }
+  if (t == 0 && keep == 12345.f) err[1] = 1;
+}
+
+template <int V>
+__global__ void __launch_bounds__(512) k_mb_bnx(unsigned* buf, unsigned* err, int rounds, int work, int jitter) {
+  if constexpr (V == 4) {
+    mb_bnx_v4(buf, err, rounds, work, jitter);
+    return;
+  }
+  const int t = threadIdx.x, lane = t & 63, wv = t >> 6, L = blockIdx.x, G = gridDim.x;
+  __shared__ float cred[8 * 64];
+  const int NG = 8, M = (G + NG - 1) / NG, grp = L % NG;
+  float keep = 0.f;
+  for (int r = 0; r < rounds; ++r) {
+    {  // emulated compute of this round
+      unsigned h = (unsigned)L * 2654435761u ^ (unsigned)r * 40503u;
+      h ^= h >> 13;
+      h *= 0x5bd1e995u;
+      h ^= h >> 15;
+      const unsigned long long dl = (unsigned long long)work + (jitter > 0 ? h % (unsigned)jitter : 0u);
+      const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+      while (__builtin_amdgcn_s_memrealtime() - t0 < dl) __builtin_amdgcn_s_sleep(1);
+    }
+    const float v = (float)((L + lane) & 7) + keep;
+    const int par = r & 1;
+    const unsigned tag = (unsigned)(r + 1), tag4 = mb_tag4(r);
+    unsigned long long* A8 = (unsigned long long*)buf + (size_t)par * 256 * 64;
+    unsigned* A4 = buf + (size_t)par * 256 * 64;
+    unsigned long long* B8 = (unsigned long long*)buf + (size_t)2 * 256 * 64 + par * NG * 64;
+    unsigned* B4 = buf + (size_t)2 * 256 * 64 + par * NG * 64;
+    int nred = 8;  // waves whose cred rows hold the final partials
+    if (wv == 0) {
+      if (V == 0 || V == 2) mb_st8(A8 + L * 64 + lane, tag, v);
+      else mb_st4(A4 + L * 64 + lane, tag4, v);
+    }
+    if (V == 0) {
+      if (G <= 64) mb_sweep8<4>(A8, G, 64, wv, lane, tag, cred, err);
+      else if (G <= 128) mb_sweep8<8>(A8, G, 64, wv, lane, tag, cred, err);
+      else mb_sweep8<16>(A8, G, 64, wv, lane, tag, cred, err);
+    } else if (V == 1) {
+      if (G <= 64) mb_sweep4<2>(A4, G, 64, wv, lane, tag4, cred, err);
+      else if (G <= 128) mb_sweep4<4>(A4, G, 64, wv, lane, tag4, cred, err);
+      else mb_sweep4<8>(A4, G, 64, wv, lane, tag4, cred, err);
+    } else {
+      if (L < NG) {  // group leader: sum the group's M members (units L + 8 m), publish the group record
+        if (V == 2) {
+          if (M <= 16) mb_sweep8<1>(A8 + grp * 64, M, NG * 64, wv, lane, tag, cred, err);
+          else mb_sweep8<2>(A8 + grp * 64, M, NG * 64, wv, lane, tag, cred, err);
+        } else {
+          if (wv < 4 || M > 16) mb_sweep4<1>(A4 + grp * 64, M, NG * 64, wv, lane, tag4, cred, err);
+        }
+        __syncthreads();
+        if (wv == 0) {
+          const int nw = V == 2 ? 8 : (M > 16 ? 8 : 4);
+          float s = 0.f;
+          for (int k = 0; k < nw; ++k) s += cred[k * 64 + lane];
+          if (V == 2) mb_st8(B8 + grp * 64 + lane, tag, s);
+          else mb_st4(B4 + grp * 64 + lane, tag4, s);
+        }
+        __syncthreads();
+      }
+      if (V == 2) {
+        if (wv < 4) mb_sweep8<1>(B8, NG, 64, wv, lane, tag, cred, err);
+        nred = 4;
+      } else {
+        if (wv < 2) mb_sweep4<1>(B4, NG, 64, wv, lane, tag4, cred, err);
+        nred = 2;
+      }
+    }
+    __syncthreads();
+    float s = 0.f;
+    for (int k = 0; k < nred; ++k) s += cred[k * 64 + lane];
+    keep = s * 1e-9f;
+    __syncthreads();
+  }
+  if (t == 0 && keep == 12345.f) err[1] = 1;
+}
 }  // namespace dca
 
 extern "C" {
@@ -203,6 +518,54 @@ int dca_microbench_xchg(int G, int nth, int rounds, int iters, int sleep, float*
   *us = best * 1e3f;
   *err_out = (int)herr[0];
   (void)hipFree(gran);
+  (void)hipFree(err);
+  (void)hipEventDestroy(a);
+  (void)hipEventDestroy(b);
+  (void)hipStreamDestroy(s);
+  return 0;
+}
+
+// BN-exchange variants (k_mb_bnx): G workgroups, `rounds` rounds, emulated work / jitter in 10-ns ticks.
+// Writes the best kernel time over `iters` (us) and the timeout flag.
+int dca_microbench_bnx(int variant, int G, int rounds, int work, int jitter, int iters, float* us, int* err_out) {
+  if (G < 8 || G > 256 || G % 8 || variant < 0 || variant > 4) {
+    g_err = "microbench_bnx: G in [8, 256], multiple of 8; variant 0..4";
+    return -1;
+  }
+  hipStream_t s;
+  HIPCK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+  const size_t bytes = (size_t)2 * 256 * 64 * 8 + 2 * 8 * 64 * 8 + 256 * 8;
+  unsigned* buf;
+  unsigned* err;
+  HIPCK(hipMalloc(&buf, bytes));
+  HIPCK(hipMalloc(&err, 16));
+  HIPCK(hipMemset(err, 0, 16));
+  hipEvent_t a, b;
+  HIPCK(hipEventCreate(&a));
+  HIPCK(hipEventCreate(&b));
+  float best = 1e30f;
+  for (int it = 0; it < iters; ++it) {
+    HIPCK(hipMemsetAsync(buf, 0, bytes, s));
+    HIPCK(hipEventRecord(a, s));
+    switch (variant) {
+      case 0: hipLaunchKernelGGL(dca::k_mb_bnx<0>, dim3(G), dim3(512), 0, s, buf, err, rounds, work, jitter); break;
+      case 1: hipLaunchKernelGGL(dca::k_mb_bnx<1>, dim3(G), dim3(512), 0, s, buf, err, rounds, work, jitter); break;
+      case 2: hipLaunchKernelGGL(dca::k_mb_bnx<2>, dim3(G), dim3(512), 0, s, buf, err, rounds, work, jitter); break;
+      case 4: hipLaunchKernelGGL(dca::k_mb_bnx<4>, dim3(G), dim3(512), 0, s, buf, err, rounds, work, jitter); break;
+      default: hipLaunchKernelGGL(dca::k_mb_bnx<3>, dim3(G), dim3(512), 0, s, buf, err, rounds, work, jitter); break;
+    }
+    HIPCK(hipGetLastError());
+    HIPCK(hipEventRecord(b, s));
+    HIPCK(hipEventSynchronize(b));
+    float ms = 0.f;
+    HIPCK(hipEventElapsedTime(&ms, a, b));
+    best = std::min(best, ms);
+  }
+  unsigned herr[2];
+  HIPCK(hipMemcpy(herr, err, 8, hipMemcpyDeviceToHost));
+  *us = best * 1e3f;
+  *err_out = (int)herr[0];
+  (void)hipFree(buf);
   (void)hipFree(err);
   (void)hipEventDestroy(a);
   (void)hipEventDestroy(b);

@@ -66,6 +66,7 @@ def load_micro():
     lib.dca_microbench_xgmi.argtypes = [c_int, c_int, fp, ip]
     lib.dca_microbench.argtypes = [c_int, c_int, c_int, c_int, fp]
     lib.dca_microbench_xchg.argtypes = [c_int, c_int, c_int, c_int, c_int, fp, ip]
+    lib.dca_microbench_bnx.argtypes = [c_int, c_int, c_int, c_int, c_int, c_int, fp, ip]
     return lib
 
 
