@@ -51,6 +51,8 @@ def _args(argv=None):
                     help="gradient all-reduce for N>1: one-shot xGMI peer reads (default inside a node) or RCCL")
     ap.add_argument("--sweep", default=None, metavar="N1,N2,..",
                     help="run each N in a fresh spawned rank group; print per-N lines and a scaling summary")
+    ap.add_argument("--no-fp32", action="store_true",
+                    help="bf16 runs: skip the second, fp32 (reference precision) timing in the same invocation")
     ap.add_argument("--result-file", default=None, help=argparse.SUPPRESS)  # rank 0 -> parent (sweep)
     return ap.parse_args(argv)
 
@@ -86,40 +88,48 @@ def run_rank(a) -> dict | None:
     from distributeddataparallel_cifar10_amd.parallel.ddp import FusedDDPTrainer
 
     data, labels = synthetic_cifar(50000, seed=0)
-    torch.manual_seed(1234 + rank)  # ranks init differently; the DDP wrap broadcasts rank 0's weights (CC3)
-    model = NetResDeep().to(dev)
-    persistent = None if a.engine == "auto" else a.engine == "persistent"
-    trainer = FusedDDPTrainer(model, data.to(dev), labels.to(dev), batch_max=a.batch, lr=1e-2, dtype=a.dtype,
-                              rows=a.rows, max_indices=(a.warmup + a.steps) * a.batch, persistent=persistent,
-                              comm=a.allreduce)
-    eng = trainer.engine
+    data, labels = data.to(dev), labels.to(dev)
     sampler = torch.utils.data.distributed.DistributedSampler(range(50000), num_replicas=world, rank=rank)
     order = np.resize(np.fromiter(iter(sampler), dtype=np.int32), (a.warmup + a.steps) * a.batch)
-    eng.set_indices(order)
-    eng.set_cursor(0)
-    eng.precapture(a.batch)  # graph capture + instantiate happen here, outside the timed region
-    eng.read_loss(reset=True)
 
-    eng.run(a.batch, a.warmup)
-    eng.sync()
-    eng.comm_time(reset=True)
-    dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    eng.run(a.batch, a.steps)
-    eng.sync()
-    torch.cuda.synchronize()
-    dt = time.perf_counter() - t0
-    dist.barrier()
-    comm_us, comm_calls = eng.comm_time()
-    on = "cpu" if share else dev
-    mine = torch.tensor([dt, comm_us / max(comm_calls, 1)], device=on, dtype=torch.float64)
-    every = [torch.zeros_like(mine) for _ in range(world)]
-    dist.all_gather(every, mine)
-    per_rank = [(float(t[0].item()), float(t[1].item())) for t in every]
-    dt = max(p[0] for p in per_rank)
-    loss_sum, nsteps = eng.read_loss()
-    ok = bool(np.isfinite(loss_sum))
+    def timed(dtype: str):
+        """W warm-up + K timed steps of a fresh model / engine in `dtype`; the slowest rank's seconds."""
+        torch.manual_seed(1234 + rank)  # ranks init differently; the DDP wrap broadcasts rank 0's weights (CC3)
+        model = NetResDeep().to(dev)
+        persistent = None if a.engine == "auto" else a.engine == "persistent"
+        trainer = FusedDDPTrainer(model, data, labels, batch_max=a.batch, lr=1e-2, dtype=dtype, rows=a.rows,
+                                  max_indices=(a.warmup + a.steps) * a.batch, persistent=persistent,
+                                  comm=a.allreduce)
+        eng = trainer.engine
+        eng.set_indices(order)
+        eng.set_cursor(0)
+        eng.precapture(a.batch)  # graph capture + instantiate happen here, outside the timed region
+        eng.read_loss(reset=True)
+        eng.run(a.batch, a.warmup)
+        eng.sync()
+        eng.comm_time(reset=True)
+        dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        eng.run(a.batch, a.steps)
+        eng.sync()
+        torch.cuda.synchronize()
+        dt = time.perf_counter() - t0
+        dist.barrier()
+        comm_us, comm_calls = eng.comm_time()
+        on = "cpu" if share else dev
+        mine = torch.tensor([dt, comm_us / max(comm_calls, 1)], device=on, dtype=torch.float64)
+        every = [torch.zeros_like(mine) for _ in range(world)]
+        dist.all_gather(every, mine)
+        per_rank = [(float(t[0].item()), float(t[1].item())) for t in every]
+        loss_sum, nsteps = eng.read_loss()
+        out = {"dt": max(p[0] for p in per_rank), "per_rank": per_rank, "loss": loss_sum / max(nsteps, 1),
+               "ok": bool(np.isfinite(loss_sum)), "engine": eng.kind_name, "comm": trainer.comm}
+        trainer.close()
+        return out
+
+    main_run = timed(a.dtype)
+    dt, per_rank, ok = main_run["dt"], main_run["per_rank"], main_run["ok"]
     value = world * a.batch * a.steps / dt
     ref = REF_EAGER_IPS_PER_GPU.get(a.dtype)
     res = {
@@ -134,10 +144,11 @@ def run_rank(a) -> dict | None:
         "scaling": "weak",
         "vs_baseline": round(value / (ref * world), 3) if ref else None,
         "dtype": a.dtype,
-        "engine": "persistent" if eng.cfg.persistent else "multikernel",
-        "allreduce": trainer.comm,
+        "engine": main_run["engine"],
+        "allreduce": main_run["comm"],
         "per_rank_ms_per_step": [round(1e3 * p[0] / a.steps, 5) for p in per_rank],
-        "allreduce_us_per_step": ([round(p[1], 2) for p in per_rank] if trainer.comm == "xgmi" else None),
+        # exposed gradient-exchange wait per step, mean over the gradient segments (xGMI path only)
+        "allreduce_us_per_step": ([round(p[1], 2) for p in per_rank] if main_run["comm"] == "xgmi" else None),
         "data": "synthetic (CIFAR-10-shaped uint8 3x32x32, 50000 samples, random labels; random-init weights)",
         "config": {"model": "NetResDeep(n_chans1=32, n_blocks=10)", "global_batch": a.batch * world,
                    "per_rank_batch": a.batch, "seq_len": None, "image": "3x32x32",
@@ -146,14 +157,24 @@ def run_rank(a) -> dict | None:
                                 f"{ref} img/s/GPU (bench/reference_eager.py)") if ref else
                                f"no {a.dtype} reference measurement"},
         "loss_finite": ok,
-        "mean_loss": loss_sum / max(nsteps, 1),
+        "mean_loss": main_run["loss"],
     }
+    if a.dtype == "bf16" and not a.no_fp32:
+        # the reference's precision, timed in the same invocation (same steps / warm-up / ranks).  The sliced
+        # engine's fp32 is "3xbf16": every MFMA operand split into bf16 hi + lo, products hi*hi + hi*lo + lo*hi,
+        # fp32 accumulation / BatchNorm / loss / SGD (measured against the fp32 oracle: tests/test_engine_gpu.py)
+        f = timed("fp32")
+        fv = world * a.batch * a.steps / f["dt"]
+        res.update({"fp32_value": round(fv, 1), "fp32_ms_per_step": round(1e3 * f["dt"] / a.steps, 5),
+                    "fp32_mode": "3xbf16" if f["engine"] == "sliced" else "fp32-mfma",
+                    "fp32_engine": f["engine"], "fp32_vs_baseline": round(fv / (REF_EAGER_IPS_PER_GPU["fp32"] * world), 3),
+                    "fp32_loss_finite": f["ok"]})
+        ok = ok and f["ok"]
     if rank == 0:
         print(json.dumps(res), flush=True)
         if a.result_file:
             with open(a.result_file, "w") as f:
                 json.dump(res, f)
-    trainer.close()
     dist.destroy_process_group()
     if not ok:
         raise SystemExit(1)
@@ -184,13 +205,15 @@ def sweep(ns: list, argv: list) -> int:
     for n in ns:
         with tempfile.NamedTemporaryFile(suffix=".json", delete=False) as f:
             path = f.name
-        sub = [x for x in argv if x != "--sweep"] + ["--gpus", str(n), "--result-file", path]
+        sub = argv + ["--gpus", str(n), "--result-file", path]
         mp.spawn(_spawned, args=(n, _free_port(), sub), nprocs=n, join=True)
         with open(path) as f:
             results[n] = json.load(f)
         os.unlink(path)
     base = results[min(results)]["value"] / min(results)
+    fp32 = {str(n): r["fp32_value"] for n, r in results.items() if "fp32_value" in r}
     print(json.dumps({"metric": BASELINE_METRIC, "sweep": {str(n): r["value"] for n, r in results.items()},
+                      **({"fp32_sweep": fp32} if fp32 else {}),
                       "scaling_efficiency": {str(n): round(r["value"] / (n * base), 4) for n, r in results.items()},
                       "ms_per_step": {str(n): r["ms_per_step"] for n, r in results.items()},
                       "dtype": results[min(results)]["dtype"], "unit": "images/sec"}), flush=True)
@@ -201,8 +224,15 @@ def main() -> int:
     argv = sys.argv[1:]
     a = _args(argv)
     if a.sweep:
-        i = argv.index("--sweep")
-        return sweep([int(x) for x in a.sweep.split(",")], argv[:i] + argv[i + 2:])
+        rest, skip = [], False
+        for x in argv:  # drop both "--sweep N1,N2" and "--sweep=N1,N2"
+            if skip:
+                skip = False
+            elif x == "--sweep":
+                skip = True
+            elif not x.startswith("--sweep="):
+                rest.append(x)
+        return sweep([int(x) for x in a.sweep.split(",")], rest)
     if "WORLD_SIZE" in os.environ:  # started by torch.distributed.run (or another launcher)
         world = int(os.environ["WORLD_SIZE"])
         if world != a.gpus:

@@ -104,6 +104,7 @@ struct Engine {
   int pk_waves = 8;
   int xpack = 0;  // experimental one-XCD placement of the persistent kernel (env DCA_PK_XPACK=1)
   int staged_b = 0;  // persistent engine: batch slots of the current staging parity that hold the next batch
+  int last_b = 0;    // batch size of the last enqueued step (sliced engine: BN slots are re-zeroed when it changes)
   int split = 0;     // persistent engine: two-phase step (fc all-reduce overlapped); default on when world_size > 1
   pk::PkArgs pa{};
   std::map<std::string, void*> regions;
@@ -163,6 +164,7 @@ static int alloc_workspace(Engine* e) {
       {"TSLAB", bmax * pks::S * WSLAB_N * 4}, {"BNG", 64 * 4}, {"IDS", 64 * 4}, {"W1B", 65536 * 2}, {"XCC", 64 * 8}, {"SIMG", 2 * 64 * 3072}, {"SLAB", 2 * 64 * 4}, {"GH", bmax * 8192 * 4}, {"SWF", 2 * 3 * 64 * 4 * 2},
       {"COMMT", 16}, {"PKW", PKW_N * 2},
       {"PKS_GRAN", 2 * (size_t)pks::LMAX * pks::GSTR * 8}, {"PKS_YH", 10 * (size_t)pks::LMAX * 2 * 512 * 4},
+      {"PKS_BNX", 2 * (size_t)pks::LMAX * 64 * 4},
       {"C1", e->in.debug ? bmax * 32 * 1024 * 4 : 16},
   };
   size_t total = 0;
@@ -218,6 +220,7 @@ static int alloc_workspace(Engine* e) {
   c.pkw = (unsigned short*)e->regions["PKW"];
   pks::Args& qa = e->qa;
   qa.gran = (unsigned long long*)e->regions["PKS_GRAN"];
+  qa.bnx = (unsigned*)e->regions["PKS_BNX"];
   qa.epoch = e->pa.epoch;
   qa.err = e->pa.err;
   qa.tslab = e->pa.tslab;
@@ -605,6 +608,11 @@ static int prime_ids(Engine* e) {
 static int ensure_staged(Engine* e, int B) {
   if (e->persistent && B > e->staged_b && prime_ids(e)) return -1;
   if (e->persistent) e->staged_b = B;
+  // sliced engine: a workgroup absent from the last steps (smaller batch) left BN slots whose 2-bit tags could
+  // match again; zeroed slots (tag 0) never match (bn_tag)
+  if (e->sliced && B != e->last_b)
+    HIPCK(hipMemsetAsync(e->qa.bnx, 0, 2 * (size_t)dca::pks::LMAX * 64 * 4, e->st));
+  e->last_b = B;
   return 0;
 }
 

@@ -1381,15 +1381,15 @@ __device__ __forceinline__ void derive_param(const Ctx& cx, int e, float w) {
     const unsigned short hi = bfbits(w), lo = bfbits(w - __uint_as_float((unsigned)hi << 16));
     if (e >= OFF_CONVW && e < OFF_CONVW + 9216) {
       const int r = e - OFF_CONVW, co = r / 288, ci = (r / 9) % 32, tap = r % 9;
-      const int fo = (tap * 32 + co) * 32 + ci, dofs = 18432 + ((8 - tap) * 32 + ci) * 32 + co;
+      const int fo = (tap * 32 + co) * PKW_REC + ci, dofs = PKW_DGRAD + ((8 - tap) * 32 + ci) * PKW_REC + co;
       cx.pkw[fo] = hi;
-      cx.pkw[9216 + fo] = lo;
+      cx.pkw[PKW_PLANE + fo] = lo;
       cx.pkw[dofs] = hi;
-      cx.pkw[9216 + dofs] = lo;
+      cx.pkw[PKW_PLANE + dofs] = lo;
     } else if (e >= OFF_C1W && e < OFF_C1W + 864) {
       const int r = e - OFF_C1W, slot = swf_slot(r / 27, r % 27);
-      cx.pkw[36864 + slot] = hi;
-      cx.pkw[38400 + slot] = lo;
+      cx.pkw[PKW_STEM + slot] = hi;
+      cx.pkw[PKW_STEM + 1536 + slot] = lo;
     }
   }
 }

@@ -18,8 +18,8 @@
 //
 // Precision P: 0 = bf16 MFMA operands (fp32 accumulate, BatchNorm / loss / SGD in fp32); 1 = fp32-accurate
 // "3xbf16": every operand a = a_hi + a_lo (two bf16), every product a_hi*b_hi + a_hi*b_lo + a_lo*b_hi on
-// v_mfma_f32_16x16x32_bf16 (relative product error ~2^-17, i.e. ~16 mantissa bits, finer than the TF32 that
-// cuDNN uses for the reference's fp32 convolutions by default on Ampere and later), fc1 in plain fp32.
+// v_mfma_f32_16x16x32_bf16 (relative product error ~2^-17, not IEEE fp32 products), fc1 in plain fp32.  Measured
+// against the plain-PyTorch fp32 oracle: <= 1e-5 per tensor (flip-aware), 8-step trajectory <= 1e-4.
 //
 // Element ownership (C layout of v_mfma_f32_16x16x32_bf16): thread (wave 4h + w, lane l = 16q + c) owns
 //   pixel (image row 4s + w, col 4q + i), channel 16h + c   for i in {0..3}   (4 values)
@@ -42,7 +42,7 @@ constexpr int S = 4;                   // workgroups (row slices) per image
 constexpr int RS = 16 / S;             // image rows per slice
 constexpr int NW = 2 * RS;             // waves per workgroup: (row, channel half)
 constexpr int NTH = 64 * NW;           // threads per workgroup
-constexpr int GSTR = 64 + 2 * 512;     // granules per workgroup per round: 64 BN sums | top row | bottom row
+constexpr int GSTR = 64 + 2 * 512;     // granules per workgroup per round: 64 (head partials) | top row | bottom row
 constexpr int LMAX = 64 * S;           // logical workgroups (batch <= 64)
 constexpr int NNT = (18 + NW - 1) / NW;  // wgrad tile columns (ci half x tap) per wave
 constexpr int RND_HEAD = 10;           // rounds: 0..9 forward BN, 10 head (fc1 partials), 11..20 backward BN
@@ -50,7 +50,8 @@ constexpr unsigned SPIN_LIMIT = 1u << 17;
 constexpr int RB = 80;                 // bf16 record: 32 channels (64 B) + 16 B pad (staggers the banks)
 
 struct Args {
-  unsigned long long* gran;  // [2][LMAX][GSTR] granules
+  unsigned long long* gran;  // [2][LMAX][GSTR] granules (halo rows, head partials)
+  unsigned* bnx;             // [2][LMAX][64] BatchNorm partials, 4-byte self-tagged values (see bn_tag)
   int* epoch;                // device scalar, advanced by the reduce kernel after every step
   unsigned* err;             // bit r: exchange round r timed out
   float* tslab;              // [LMAX][WSLAB_N] trunk wgrad per workgroup (fragment order, read by k_pks_reduce)
@@ -255,32 +256,47 @@ __device__ __forceinline__ bool poll_row(const Args& pa, int round, int Lsrc, in
   return ok;
 }
 
-// BN sweep: lane l of wave wv reads slots 2(l & 31), 2(l & 31) + 1 of workgroups 2 wv + (l >> 5) + 2 NW k (one
-// 16-B sc1 load = two granules), k < KS; sums in k order.  Slots past the grid read a valid (clamped) granule
-// and count 0.
+// BatchNorm partials travel as 4-byte self-tagged fp32 values: the 2 low mantissa bits of every value carry the
+// tag (a <= 3 ulp perturbation of a partial sum, identical for every reader), so one 16-B sc1 load returns four
+// validated values -- half the bytes per sweep pass of {value, tag} granules (profiles/bnx_variants_r3.log: 1.73 vs
+// 2.05 us per exchange round at 128 workgroups).  Slot parity = round & 1; consecutive writes of a slot carry
+// consecutive tags of the cycle 1, 2, 3 (each parity is written 10 times per step: c = 10 epoch + k, tag =
+// 1 + c mod 3), so a reader can never accept the previous write; 0 never matches (the host zeroes the buffer
+// whenever the batch size changes, so slots of workgroups absent from earlier steps are never stale-valid).
+__device__ __forceinline__ unsigned bn_tag(int epoch, int rnd) {
+  const int k = rnd < RND_HEAD ? rnd >> 1 : 5 + ((rnd - RND_HEAD - 1) >> 1);
+  return 1u + (unsigned)((epoch * 10 + k) % 3);
+}
+__device__ __forceinline__ void bn_put(const Args& pa, int rnd, int L, int slot, unsigned tag, float v) {
+  __hip_atomic_store(pa.bnx + ((size_t)(rnd & 1) * LMAX + L) * 64 + slot, (__float_as_uint(v) & ~3u) | tag,
+                     __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// BN sweep: lane 16 sub + q4 of wave wv reads slots 4 q4 .. 4 q4 + 3 of workgroups 4 wv + sub + 32 k (one 16-B sc1
+// load), k < KS; sums in k order.  Slots past the grid read a valid (clamped) address and count 0.
 template <int KS>
 __device__ __forceinline__ void sweep_issue(const __amdgpu_buffer_rsrc_t rs, int wv, int lane, int G, v4u (&x)[KS]) {
-  const int j = lane & 31, hf = lane >> 5;
+  const int q4 = lane & 15, sub = lane >> 4;
   asm volatile("" ::: "memory");  // re-issued every pass (never hoisted out of the spin)
 #pragma unroll
   for (int k = 0; k < KS; ++k) {
-    const int Lk = 2 * wv + hf + 2 * NW * k, Lc = Lk < G ? Lk : G - 1;
-    x[k] = __builtin_amdgcn_raw_buffer_load_b128(rs, (Lc * GSTR + 2 * j) * 8, 0, 16);
+    const int Lk = 4 * wv + sub + 4 * NW * k, Lc = Lk < G ? Lk : G - 1;
+    x[k] = __builtin_amdgcn_raw_buffer_load_b128(rs, (Lc * 64 + 4 * q4) * 4, 0, 16);
   }
 }
 template <int KS>
-__device__ __forceinline__ bool sweep_eval(const v4u (&x)[KS], int wv, int lane, int G, unsigned tag, float& s0,
-                                           float& s1) {
-  const int hf = lane >> 5;
+__device__ __forceinline__ bool sweep_eval(const v4u (&x)[KS], int wv, int lane, int G, unsigned tag, float (&sv)[4]) {
+  const int sub = lane >> 4;
   bool ok = true;
-  s0 = 0.f;
-  s1 = 0.f;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) sv[e] = 0.f;
 #pragma unroll
   for (int k = 0; k < KS; ++k) {
-    const bool valid = 2 * wv + hf + 2 * NW * k < G;
-    ok &= !valid || (x[k][1] == tag && x[k][3] == tag);
-    s0 += valid ? __uint_as_float(x[k][0]) : 0.f;
-    s1 += valid ? __uint_as_float(x[k][2]) : 0.f;
+    const bool valid = 4 * wv + sub + 4 * NW * k < G;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      ok &= !valid || (x[k][e] & 3u) == tag;
+      sv[e] += valid ? __uint_as_float(x[k][e]) : 0.f;
+    }
   }
   return __all(ok);
 }
@@ -292,12 +308,13 @@ __device__ __forceinline__ void sleep_units(int n) {
 // granule per workgroup between full passes 100.6 vs 98.1 (one more round trip).
 template <int KS>
 __device__ __forceinline__ void sweep_wait(const Args& pa, int round, int wv, int lane, int G, unsigned tag,
-                                           float& s0, float& s1) {
-  const __amdgpu_buffer_rsrc_t rs = grsrc(pa, round);
+                                           float (&sv)[4]) {
+  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(pa.bnx + (size_t)(round & 1) * LMAX * 64,
+                                                                      (short)0, LMAX * 64 * 4, 0x00020000);
   v4u xa[KS];
   for (unsigned spins = 0;; ++spins) {
     sweep_issue<KS>(rs, wv, lane, G, xa);
-    if (sweep_eval<KS>(xa, wv, lane, G, tag, s0, s1)) return;
+    if (sweep_eval<KS>(xa, wv, lane, G, tag, sv)) return;
     sleep_units(pa.gap);
     if (spins >= SPIN_LIMIT) {
       if (lane == 0) atomicOr(pa.err, 1u << (round & 31));
@@ -312,16 +329,18 @@ __device__ __forceinline__ void xchg_wait(const Args& pa, int round, int epoch, 
   const int t = threadIdx.x, lane = t & 63;
   const int wv = __builtin_amdgcn_readfirstlane(t >> 6);
   const unsigned tag = tagof(epoch, round);
-  float s0, s1;
-  if (G <= 2 * NW * 4) sweep_wait<4>(pa, round, wv, lane, G, tag, s0, s1);
-  else if (G <= 2 * NW * 8) sweep_wait<8>(pa, round, wv, lane, G, tag, s0, s1);
-  else sweep_wait<16>(pa, round, wv, lane, G, tag, s0, s1);
-  s0 += __shfl_xor(s0, 32);  // the two half-waves read different workgroups
-  s1 += __shfl_xor(s1, 32);
-  if (lane < 32) {
-    cred[wv * 64 + 2 * lane] = s0;
-    cred[wv * 64 + 2 * lane + 1] = s1;
+  float sv[4];
+  const unsigned btag = bn_tag(epoch, round);
+  if (G <= 4 * NW) sweep_wait<1>(pa, round, wv, lane, G, btag, sv);
+  else if (G <= 8 * NW) sweep_wait<2>(pa, round, wv, lane, G, btag, sv);
+  else if (G <= 16 * NW) sweep_wait<4>(pa, round, wv, lane, G, btag, sv);
+  else sweep_wait<8>(pa, round, wv, lane, G, btag, sv);
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {  // the four 16-lane groups read different workgroups
+    sv[e] += __shfl_xor(sv[e], 16);
+    sv[e] += __shfl_xor(sv[e], 32);
   }
+  if (lane < 16) *(f32x4*)(cred + wv * 64 + 4 * lane) = f32x4{sv[0], sv[1], sv[2], sv[3]};
   if (halo) {
     for (unsigned spins = 0;; ++spins) {
       asm volatile("" ::: "memory");
@@ -424,47 +443,20 @@ __device__ __forceinline__ void xr_row(char* XR, int xrow, int q, int ch, const 
   for (int i = 0; i < 4; ++i) st1r<P>(XR, PL::XR_PL, xrow * 18 + 4 * q + i + 1, ch, v[i]);
 }
 
-// weight staging: NP planes of 1152 16-B chunks, loaded to registers (all in flight), stored as records
+// weight staging: the NP planes (hi, lo) of one conv weight, stored in global memory in the LDS record layout
+// (common.h PKW_*), copied into WT by LDS-DMA -- no registers, no scratch; the issuing waves' vmcnt covers it.
+// 1 KB per wave instruction, chunks dealt round-robin to the waves; P = 0's 22.5 KB end in a half chunk.
 template <int P>
-struct WStage {
-  static constexpr int M = (1152 + NTH - 1) / NTH;
-  uint4 v[P + 1][M];
-};
-template <int P>
-__device__ __forceinline__ void wstage_load(WStage<P>& ws, const unsigned short* src) {
+__device__ __forceinline__ void wt_dma(char* wt, const unsigned short* src, int wv, int lane) {
+  constexpr int BYTES = (P + 1) * PKW_PLANE * 2, NCH = (BYTES + 1023) / 1024;
+  static_assert(BYTES == (P + 1) * Plan<P>::WT_PL, "record layout of pkw matches the LDS weight planes");
 #pragma unroll
-  for (int p = 0; p <= P; ++p)
-#pragma unroll
-    for (int m = 0; m < WStage<P>::M; ++m) {
-      const int idx = threadIdx.x + NTH * m;
-      ws.v[p][m] = ((const uint4*)(src + p * 9216))[idx < 1152 ? idx : 1151];
-    }
-#pragma unroll
-  for (int p = 0; p <= P; ++p)
-#pragma unroll
-    for (int m = 0; m < WStage<P>::M; ++m) pin(ws.v[p][m]);
-}
-// the same without forcing the wait: for prefetches issued before an exchange (the spin loop's memory clobber
-// keeps them above it, their wait lands at first use)
-template <int P>
-__device__ __forceinline__ void wstage_prefetch(WStage<P>& ws, const unsigned short* src) {
-#pragma unroll
-  for (int p = 0; p <= P; ++p)
-#pragma unroll
-    for (int m = 0; m < WStage<P>::M; ++m) {
-      const int idx = threadIdx.x + NTH * m;
-      ws.v[p][m] = ((const uint4*)(src + p * 9216))[idx < 1152 ? idx : 1151];
-    }
-}
-template <int P>
-__device__ __forceinline__ void wstage_store(const WStage<P>& ws, char* wt) {
-#pragma unroll
-  for (int p = 0; p <= P; ++p)
-#pragma unroll
-    for (int m = 0; m < WStage<P>::M; ++m) {
-      const int idx = threadIdx.x + NTH * m;
-      if (idx < 1152) *(uint4*)(wt + p * Plan<P>::WT_PL + (idx >> 2) * RB + (idx & 3) * 16) = ws.v[p][m];
-    }
+  for (int m = 0; m < (NCH + NW - 1) / NW; ++m) {
+    const int ck = wv + NW * m;
+    if (ck < NCH && ck * 1024 + lane * 16 < BYTES)
+      __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)((const char*)src + ck * 1024 + lane * 16),
+                                       (__attribute__((address_space(3))) void*)(wt + ck * 1024), 16, 0, 0);
+  }
 }
 
 // fc1 slice of slice s: 32 rows x 512 local features (u = ch*16 + pr*8 + pw <-> global ch*64 + (2s + pr)*8 + pw),
@@ -565,15 +557,14 @@ __global__ void __launch_bounds__(NTH) k_pks_step(Ctx cx, Args pa) {
     const unsigned* imw = (const unsigned*)my_img;
     const int yc = yimg < 0 ? 0 : (yimg > 31 ? 31 : yimg);
     unsigned iw0 = imw[yc * 8 + xq], iw1 = imw[256 + yc * 8 + xq], iw2 = imw[512 + yc * 8 + xq];
-    WStage<P> wst;
-    wstage_load<P>(wst, pkw);  // forward trunk weights [tap][co][ci] (hi, lo)
-    uint2 bwr[P + 1][2][3];    // conv1 B fragments: lane (co = 16h + c, k-group q) of MFMA m
+    wt_dma<P>(WT, pkw, wv, lane);  // forward trunk weights, records [tap][co] x ci (hi, lo)
+    uint2 bwr[P + 1][2][3];        // conv1 B fragments: lane (co = 16h + c, k-group q) of MFMA m
 #pragma unroll
     for (int p = 0; p <= P; ++p)
 #pragma unroll
       for (int h = 0; h < 2; ++h)
 #pragma unroll
-        for (int m = 0; m < 3; ++m) bwr[p][h][m] = ((const uint2*)(pkw + 36864 + p * 1536))[(h * 3 + m) * 64 + lane];
+        for (int m = 0; m < 3; ++m) bwr[p][h][m] = ((const uint2*)(pkw + PKW_STEM + p * 1536))[(h * 3 + m) * 64 + lane];
 #pragma unroll
     for (int m = 0; m < KCM; ++m) pin(kc[m]);
     pin(lab);
@@ -610,8 +601,8 @@ __global__ void __launch_bounds__(NTH) k_pks_step(Ctx cx, Args pa) {
       xin4[px] = uint2{0u, 0u};
       if constexpr (P == 1) xin4[PL::XIN_PL / 8 + px] = uint2{0u, 0u};
     }
-    wstage_store<P>(wst, WT);
     for (int idx = t; idx < PL::NP * PL::XR_PL / 16; idx += NTH) ((uint4*)XR)[idx] = uint4{0u, 0u, 0u, 0u};
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's weight DMA has landed in LDS
     lds_barrier();
     DCA_STAMP(cx, 0, L, 2);
     s4v bw[P + 1][2][3];
@@ -693,9 +684,8 @@ __global__ void __launch_bounds__(NTH) k_pks_step(Ctx cx, Args pa) {
   // fc1 weights of this slice's 512 pooled features (local index u = ch*16 + pr*8 + pw <-> global feature
   // ch*64 + (2s + pr)*8 + pw: per row, 32 runs of 16 contiguous elements): copied into their LDS region (unused by
   // the forward) by LDS-DMA right after block 6's exchange, read by
-  // fc1 (reduction over features) and its transpose dp (reduction over rows).  The dgrad weights are prefetched
-  // at block 8 and staged into WT at the head.
-  WStage<P> wst_d;  // dgrad weights, staged into WT during the head
+  // fc1 (reduction over features) and its transpose dp (reduction over rows).  The dgrad weights replace the
+  // forward ones in WT by LDS-DMA right after block 9's exchange (block 9's conv was WT's last reader).
 #pragma unroll 1
   for (int i = 0; i < NBLK; ++i) {
     {
@@ -716,9 +706,8 @@ __global__ void __launch_bounds__(NTH) k_pks_step(Ctx cx, Args pa) {
     }
     const float pv = wg_csum(a, bsq, cred);
     const unsigned tag = tagof(epoch, i);
-    if (t < 64) gput(gslot(pa, i, L) + t, tag, pv);
+    if (t < 64) bn_put(pa, i, L, t, bn_tag(epoch, i), pv);
     if (halo) publish_row(pa, i, L, hwhich, hh, tag, y, lane);
-    if (i == NBLK - 2) wstage_prefetch<P>(wst_d, pkw + 18432);  // dgrad weights [tap'][ci][co] (hi, lo)
     float yo[4];
     if (i == DCA_DETAIL_FWD) DCA_STAMP(cx, 6, L, 1);
     xchg_wait(pa, i, epoch, G, cred, halo, hsrc, hwhich ^ 1, hh, yo);
@@ -728,6 +717,7 @@ __global__ void __launch_bounds__(NTH) k_pks_step(Ctx cx, Args pa) {
     // AFTER an exchange: vmcnt is in order, so loads in flight when a sweep starts hold up its first pass (register
     // loads before the exchange + an LDS store a block later cost ~1.4 us in each of the two blocks, stamps)
     if (i == NBLK - 4) w1_dma<P>(cx, U + PL::U_W1, s, wv, lane);
+    if (i == NBLK - 1) wt_dma<P>(WT, pkw + PKW_DGRAD, wv, lane);  // dgrad weights, records [8 - tap][ci] x co
     lds_barrier();
     if (i == DCA_DETAIL_FWD) DCA_STAMP(cx, 6, L, 3);
     if (halo) st4r(pa.yh + ((size_t)(i * LMAX + L) * 2 + hwhich) * 512, hh, lane, yo);
@@ -783,7 +773,6 @@ __global__ void __launch_bounds__(NTH) k_pks_step(Ctx cx, Args pa) {
     float* pl = (float*)(U + PL::U_PL);
     float* hp = (float*)(U + PL::U_HP);
     char* w1l = U + PL::U_W1;
-    wstage_store<P>(wst_d, WT);  // every conv read of WT is done (block 9's conv preceded its exchange)
 #pragma unroll
     for (int i2 = 0; i2 < 4; ++i2) x10[(w * 16 + 4 * q + i2) * PL::X10S + ch] = x[i2];
     lds_barrier();
@@ -933,6 +922,7 @@ __global__ void __launch_bounds__(NTH) k_pks_step(Ctx cx, Args pa) {
   // ======================= backward: 10 applications, newest first ===========================================
   unsigned short* dyT = (unsigned short*)(U + PL::U_DYT);
   unsigned short* xT = (unsigned short*)(U + PL::U_XT);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the dgrad weight DMA (block 9) has landed
   lds_barrier();  // every wave is done with the head's LDS (X10 / W1 / DP overlap XR / dyT / xT)
   for (int idx = t; idx < PL::NP * PL::XR_PL / 16; idx += NTH) ((uint4*)XR)[idx] = uint4{0u, 0u, 0u, 0u};
   for (int idx = t; idx < PL::NP * PL::XT_PL / 16; idx += NTH) ((uint4*)xT)[idx] = uint4{0u, 0u, 0u, 0u};
@@ -970,7 +960,7 @@ __global__ void __launch_bounds__(NTH) k_pks_step(Ctx cx, Args pa) {
     const unsigned tag = tagof(epoch, rnd);
     if (i == DCA_DETAIL_BWD) DCA_STAMP(cx, 7, L, 0);
     const float pv = wg_csum(sa, sbv, cred);
-    if (t < 64) gput(gslot(pa, rnd, L) + t, tag, pv);
+    if (t < 64) bn_put(pa, rnd, L, t, bn_tag(epoch, rnd), pv);
     if (halo) publish_row(pa, rnd, L, hwhich, hh, tag, dz, lane);
     if (i == DCA_DETAIL_BWD) DCA_STAMP(cx, 7, L, 1);
     // while the exchange is in flight: the weight gradient of the PREVIOUS application (block i + 1), whose dy /
@@ -1232,18 +1222,12 @@ __device__ void seg_exchange(const Ctx& cx, const RedAr& ra, int b, float* segv,
     atomicAdd(ra.peers.ticks, __builtin_amdgcn_s_memrealtime() - t_in);
     atomicAdd(ra.peers.ticks + 1, 1ull);
   }
-  for (int k = 4 * t; k < len; k += 1024) {
-    f32x4 part[xg::MAXR];
-#pragma unroll
-    for (int q = 0; q < xg::MAXR; ++q) {  // all loads in flight, one per peer link; ranks >= W re-read rank 0
-      const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(rslab(ra, q < W ? q : 0, par), (short)0,
+  for (int k = 4 * t; k < len; k += 1024) {  // exactly W loads in flight, one per peer link (rank_sum.h)
+    *(f32x4*)(segv + k) = rank_sum(W, [&](int q) {
+      const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(rslab(ra, q, par), (short)0,
                                                                           (int)(xg::SLAB_FLOATS * 4), 0x00020000);
-      part[q] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, 4 * (off + k), 0, SYS));
-    }
-    f32x4 sum = part[0];
-#pragma unroll
-    for (int q = 1; q < xg::MAXR; ++q) sum += q < W ? part[q] : z4();
-    *(f32x4*)(segv + k) = sum;
+      return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, 4 * (off + k), 0, SYS));
+    });
   }
   __syncthreads();
 }

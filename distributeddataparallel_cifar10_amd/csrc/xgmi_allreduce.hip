@@ -27,6 +27,7 @@
 // epoch ep.  Parities alternate, so epoch ep+1's writes never touch what epoch ep's readers read.
 #pragma once
 #include "common.h"
+#include "rank_sum.h"
 
 namespace dca {
 namespace xg {
@@ -98,18 +99,12 @@ __global__ void __launch_bounds__(AR_T) k_xgmi_ar_sgd(Ctx cx, Peers P, const flo
     atomicAdd(P.ticks + 1, 1ull);
   }
   if (!live) return;
-  // All W loads in flight at once (one per peer link), cache-bypassing: unconditional loads (ranks >= W re-read
-  // rank 0, which is never summed) so the compiler issues them back to back instead of branching around each one.
-  f32x4 part[MAXR];
-#pragma unroll
-  for (int q = 0; q < MAXR; ++q) {
+  // exactly W loads in flight at once (one per peer link), cache-bypassing, summed in rank order (rank_sum.h)
+  const f32x4 s = rank_sum(W, [&](int q) {
     const __amdgpu_buffer_rsrc_t rs =
-        __builtin_amdgcn_make_buffer_rsrc(slab(P, q < W ? q : 0, par), (short)0, (int)(SLAB_FLOATS * 4), 0x00020000);
-    part[q] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, 16 * v, 0, SYS));
-  }
-  f32x4 s = part[0];
-#pragma unroll
-  for (int q = 1; q < MAXR; ++q) s += q < W ? part[q] : f32x4{0.f, 0.f, 0.f, 0.f};
+        __builtin_amdgcn_make_buffer_rsrc(slab(P, q, par), (short)0, (int)(SLAB_FLOATS * 4), 0x00020000);
+    return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, 16 * v, 0, SYS));
+  });
   if (!sgd) {
     *(f32x4*)(sum_out + 4 * v) = s;
     return;

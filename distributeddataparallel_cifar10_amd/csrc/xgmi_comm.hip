@@ -39,6 +39,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "rank_sum.h"
+
 namespace dca {
 namespace comm {
 
@@ -144,16 +146,26 @@ __device__ __forceinline__ void exchange(const Args& a, bool out, int ep) {
   __syncthreads();
 }
 
-// Sum float4 v over all W ranks' slabs (rank order), all W loads in flight at once (one per peer link).
+// Sum float4 v over all W ranks' slabs (rank order), exactly W loads in flight at once (one per peer link).
 template <bool BF>
 __device__ __forceinline__ f4 gather_sum(const __amdgpu_buffer_rsrc_t* rs, int W, long long v) {
-  f4 part[MAXR];
+  return rank_sum(W, [&](int q) { return slab_get<BF>(rs[q], v); });
+}
+// Two-shot all-gather: element i of every other rank's piece b, exactly W - 1 peer loads in flight per thread.
+template <bool BF, int NR>
+__device__ __forceinline__ void allgather_n(const Args& a, const __amdgpu_buffer_rsrc_t* rout, const long long* lo,
+                                            const long long* hi, long long len) {
+  for (long long i = threadIdx.x; i < len; i += T) {
+    f4 got[NR];
 #pragma unroll
-  for (int q = 0; q < MAXR; ++q) part[q] = slab_get<BF>(rs[q < W ? q : 0], v);
-  f4 s = part[0];
+    for (int q = 0; q < NR; ++q) {
+      const long long v = lo[q] + i < hi[q] ? lo[q] + i : lo[q];  // clamped: unconditional loads
+      if (q != a.me) got[q] = slab_get<BF>(rout[q], v);
+    }
 #pragma unroll
-  for (int q = 1; q < MAXR; ++q) s += q < W ? part[q] : f4{0.f, 0.f, 0.f, 0.f};
-  return s;
+    for (int q = 0; q < NR; ++q)
+      if (q != a.me && lo[q] + i < hi[q]) store_dst(a.dst, lo[q] + i, a.n, got[q]);
+  }
 }
 
 template <bool BF, bool TWO>
@@ -169,7 +181,7 @@ __global__ void __launch_bounds__(T) k_allreduce(Args a) {
   const long long sb = (nv * 4) * wire;  // slab bytes in use
   __amdgpu_buffer_rsrc_t rin[MAXR];
 #pragma unroll
-  for (int q = 0; q < MAXR; ++q) rin[q] = rsrc(in_slab(a, q < W ? q : 0, par), sb);
+  for (int q = 0; q < MAXR; ++q) rin[q] = rsrc(in_slab(a, q < W ? q : me, par), sb);  // q >= W: never read
 
   if (!TWO) {
     const long long piece = (nv + a.nb - 1) / a.nb, lo = b * piece, hi = lo + piece < nv ? lo + piece : nv;
@@ -211,7 +223,7 @@ __global__ void __launch_bounds__(T) k_allreduce(Args a) {
   long long lo[MAXR], hi[MAXR], len = 0;
 #pragma unroll
   for (int q = 0; q < MAXR; ++q) {
-    rout[q] = rsrc(out_slab(a, q < W ? q : 0, par), sb);
+    rout[q] = rsrc(out_slab(a, q < W ? q : me, par), sb);  // q >= W: never read
     if (q < W) {
       range(q, lo[q], hi[q]);
       len = hi[q] - lo[q] > len ? hi[q] - lo[q] : len;
@@ -219,16 +231,15 @@ __global__ void __launch_bounds__(T) k_allreduce(Args a) {
       lo[q] = hi[q] = 0;
     }
   }
-  for (long long i = t; i < len; i += T) {
-    f4 got[MAXR];
-#pragma unroll
-    for (int q = 0; q < MAXR; ++q) {
-      const long long v = lo[q] + i < hi[q] ? lo[q] + i : lo[0];  // clamped: unconditional loads
-      got[q] = slab_get<BF>(rout[q], v);
-    }
-#pragma unroll
-    for (int q = 0; q < MAXR; ++q)
-      if (q < W && q != me && lo[q] + i < hi[q]) store_dst(a.dst, lo[q] + i, a.n, got[q]);
+  switch (W) {  // wave-uniform: exactly the W - 1 peers are read
+    case 1: break;
+    case 2: allgather_n<BF, 2>(a, rout, lo, hi, len); break;
+    case 3: allgather_n<BF, 3>(a, rout, lo, hi, len); break;
+    case 4: allgather_n<BF, 4>(a, rout, lo, hi, len); break;
+    case 5: allgather_n<BF, 5>(a, rout, lo, hi, len); break;
+    case 6: allgather_n<BF, 6>(a, rout, lo, hi, len); break;
+    case 7: allgather_n<BF, 7>(a, rout, lo, hi, len); break;
+    default: allgather_n<BF, 8>(a, rout, lo, hi, len); break;
   }
 }
 

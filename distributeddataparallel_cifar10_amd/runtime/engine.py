@@ -11,6 +11,7 @@ accumulated on the device and read only at log points.
 from __future__ import annotations
 
 import ctypes
+import warnings
 from dataclasses import dataclass
 from typing import Optional
 
@@ -36,6 +37,8 @@ LAYOUT = {
     "conv1.weight": (75180, (32, 3, 3, 3)),
     "conv1.bias": (76044, (32,)),
 }
+# engine kinds reported by dca_engine_kind (also written into bench / metrics output)
+KIND_NAMES = {0: "multikernel", 1: "persistent-per-image", 2: "sliced"}
 # gradient buckets (contiguous slices of the flat gradient buffer, ordered by gradient-ready time)
 BUCKETS = (("fc", 0, BUCKET_A_END), ("trunk+stem+bn_stats", BUCKET_A_END, FLAT_N))
 
@@ -176,12 +179,16 @@ class NetResDeepEngine:
             if rc != 0 and auto_engine and "cannot all be resident" in native.last_error():
                 # the persistent step's workgroups do not fit the device at once (co-residency check at create
                 # time): the multi-kernel engine instead, same numerics contract
+                reason = native.last_error()
                 cfg.persistent = False
                 init.persistent = 0
                 rc = self.lib.dca_engine_create(ctypes.byref(init), self.max_indices, ctypes.byref(h))
+                warnings.warn(f"NetResDeepEngine: persistent step not co-resident ({reason}); using the multi-kernel "
+                              f"engine (exact fp32 MFMA for dtype fp32, a different numerics path)", RuntimeWarning)
             native.check(rc, "dca_engine_create")
         self.h = h
         self.kind = int(self.lib.dca_engine_kind(h))  # 0 multi-kernel, 1 persistent per image, 2 sliced
+        self.kind_name = KIND_NAMES.get(self.kind, str(self.kind))
         self.derive()
         self._n_indices = 0
 

@@ -76,7 +76,9 @@ def add_cli_args(ap: argparse.ArgumentParser, batch_default: int = 32) -> argpar
                          "model) + FlatBucketDDP; torch: stock PyTorch ops + FlatBucketDDP")
     ap.add_argument("--fp8", action="store_true", help="ops engine: fp8 e4m3 forward GEMMs (1x1 convs, fc)")
     ap.add_argument("--dtype", default="fp32", choices=["bf16", "fp32"],
-                    help="fp32 (default): the reference's precision; bf16: bf16 MFMA operands, fp32 accumulation")
+                    help="fp32 (default): fp32-accurate, the reference's dtype (the sliced engine computes every "
+                         "product as 3 bf16 MFMA products, ~2^-17 relative error; the multi-kernel engine exact fp32 "
+                         "MFMA); bf16: bf16 MFMA operands, fp32 accumulation")
     ap.add_argument("--no-checkpoint", action="store_true")
     ap.add_argument("--checkpoint-path", default=None)
     ap.add_argument("--resume", default=None)
