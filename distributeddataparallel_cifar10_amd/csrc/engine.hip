@@ -17,7 +17,6 @@
 #include <string>
 
 #include "netresdeep_kernels.hip"
-#include "netresdeep_persistent.hip"
 #include "xgmi_allreduce.hip"
 #include "netresdeep_pks.hip"
 
@@ -65,9 +64,9 @@ struct DcaInit {
   int world_size;
   int rank;
   const char* nccl_id;  // 128 bytes (world_size > 1)
-  int persistent;       // 1: one-launch persistent trunk kernel (bf16 only)
-  int debug;            // persistent engine: also store DY / G for diagnostics
-  int pk_waves;         // persistent engine: waves per workgroup (8; 0 = default)
+  int persistent;       // 1: the one-launch image-sliced persistent step kernel (netresdeep_pks.hip)
+  int debug;            // persistent engine: also store X / DY / G / conv1 pre-activations for diagnostics
+  int pk_waves;         // unused (kept for ABI layout; must be 0 or 8)
   int comm_mode;        // world_size > 1: 0 = RCCL inside the step; 1 = external (host drives the all-reduce
                         // between dca_engine_run_part(.., 1) and (.., 2); test/debug path, no RCCL communicator);
                         // 2 = xGMI one-shot (peer-to-peer reads of IPC-mapped gradient slabs, fused with SGD)
@@ -96,17 +95,12 @@ struct Engine {
   bool peers_open = false;
   unsigned long long ar_deadline = 300ull * 100000000ull;  // 300 s in 100 MHz ticks (a peer may be in host code)
   std::map<int, hipGraphExec_t> graphs;
-  bool persistent = false;
-  bool sliced = false;   // persistent engine, image-sliced kernel (netresdeep_pks.hip; default)
+  bool persistent = false;  // the image-sliced persistent step kernel (netresdeep_pks.hip; default)
   pks::Args qa{};
   bool comm_on = false;  // the step ends with a gradient collective (world_size > 1, or force_comm)
   int resident = 0;      // persistent engine: workgroups guaranteed co-resident (occupancy x CUs)
-  int pk_waves = 8;
-  int xpack = 0;  // experimental one-XCD placement of the persistent kernel (env DCA_PK_XPACK=1)
   int staged_b = 0;  // persistent engine: batch slots of the current staging parity that hold the next batch
-  int last_b = 0;    // batch size of the last enqueued step (sliced engine: BN slots are re-zeroed when it changes)
-  int split = 0;     // persistent engine: two-phase step (fc all-reduce overlapped); default on when world_size > 1
-  pk::PkArgs pa{};
+  int last_b = 0;    // batch size of the last enqueued step (BN slots are re-zeroed when it changes)
   std::map<std::string, void*> regions;
   // dynamic LDS sizes
   size_t s_stem = 0, s_fwd = 0, s_head1 = 0, s_head2 = 0, s_dgrad = 0, s_dgrad0 = 0, s_wgrad = 0, s_fc = 0;
@@ -160,8 +154,9 @@ static int alloc_workspace(Engine* e) {
       {"WT_F", 9216 * esz},          {"WT_D", 9216 * esz},            {"SW", 1024 * esz},
       {"RS_BASE", 64 * 4},           {"CURSOR", 16},                  {"STEPS", 16},
       {"LOSS", 16},                  {"STAMPS", 32 * 256 * 8 * 2 * 8},
-      {"GRAN", 2 * 64 * 64 * 8},     {"EPOCH", 16},                   {"ERR", 16},
-      {"TSLAB", bmax * pks::S * WSLAB_N * 4}, {"BNG", 64 * 4}, {"IDS", 64 * 4}, {"W1B", 65536 * 2}, {"XCC", 64 * 8}, {"SIMG", 2 * 64 * 3072}, {"SLAB", 2 * 64 * 4}, {"GH", bmax * 8192 * 4}, {"SWF", 2 * 3 * 64 * 4 * 2},
+      {"EPOCH", 16},                 {"ERR", 16},
+      {"TSLAB", bmax * pks::S * WSLAB_N * 4}, {"BNG", 64 * 4}, {"W1B", 65536 * 2}, {"SIMG", 2 * 64 * 3072},
+      {"SLAB", 2 * 64 * 4},
       {"COMMT", 16}, {"PKW", PKW_N * 2},
       {"PKS_GRAN", 2 * (size_t)pks::LMAX * pks::GSTR * 8}, {"PKS_YH", 10 * (size_t)pks::LMAX * 2 * 512 * 4},
       {"PKS_BNX", 2 * (size_t)pks::LMAX * 64 * 4},
@@ -204,29 +199,25 @@ static int alloc_workspace(Engine* e) {
   c.loss_acc = (double*)e->regions["LOSS"];
   c.pstride = (int)pstride;
   c.stamps = (unsigned long long*)e->regions["STAMPS"];
-  c.w1b = e->regions["W1B"];
-  c.swf = e->regions["SWF"];
-  e->pa.gran = (unsigned long long*)e->regions["GRAN"];
-  e->pa.epoch = (int*)e->regions["EPOCH"];
-  e->pa.err = (unsigned*)e->regions["ERR"];
-  e->pa.tslab = (float*)e->regions["TSLAB"];
-  e->pa.bng = (float*)e->regions["BNG"];
-  e->pa.ids = (int*)e->regions["IDS"];
-  e->pa.xcc = (unsigned long long*)e->regions["XCC"];
-  e->pa.simg = (uint8_t*)e->regions["SIMG"];
-  e->pa.gh = (float*)e->regions["GH"];
-  e->pa.slab = (int*)e->regions["SLAB"];
-  e->pa.debug = e->in.debug;
-  c.pkw = (unsigned short*)e->regions["PKW"];
+  // derived weight copies: each engine writes only the layouts its kernels read (derive_param skips null ones)
+  c.swf = nullptr;
+  if (e->persistent) {
+    c.w1b = e->regions["W1B"];
+    c.pkw = (unsigned short*)e->regions["PKW"];
+    c.wt_f = c.wt_d = c.sw = nullptr;
+  } else {
+    c.w1b = nullptr;
+    c.pkw = nullptr;
+  }
   pks::Args& qa = e->qa;
   qa.gran = (unsigned long long*)e->regions["PKS_GRAN"];
   qa.bnx = (unsigned*)e->regions["PKS_BNX"];
-  qa.epoch = e->pa.epoch;
-  qa.err = e->pa.err;
-  qa.tslab = e->pa.tslab;
-  qa.bng = e->pa.bng;
-  qa.simg = e->pa.simg;
-  qa.slab = e->pa.slab;
+  qa.epoch = (int*)e->regions["EPOCH"];
+  qa.err = (unsigned*)e->regions["ERR"];
+  qa.tslab = (float*)e->regions["TSLAB"];
+  qa.bng = (float*)e->regions["BNG"];
+  qa.simg = (uint8_t*)e->regions["SIMG"];
+  qa.slab = (int*)e->regions["SLAB"];
   qa.yh = (float*)e->regions["PKS_YH"];
   qa.c1 = (float*)e->regions["C1"];
   qa.debug = e->in.debug;
@@ -242,8 +233,6 @@ static int set_lds_limits(Engine* e) {
   HIPCK(hipFuncSetAttribute((const void*)e->khead1, hipFuncAttributeMaxDynamicSharedMemorySize, (int)e->s_head1));
   HIPCK(hipFuncSetAttribute((const void*)e->khead2, hipFuncAttributeMaxDynamicSharedMemorySize, (int)e->s_head2));
   HIPCK(hipFuncSetAttribute((const void*)e->kbwd, hipFuncAttributeMaxDynamicSharedMemorySize, (int)dg));
-  HIPCK(hipFuncSetAttribute((const void*)pk::k_pk_step<8>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                            pk::Plan::TOTAL));
   HIPCK(hipFuncSetAttribute((const void*)pks::k_pks_step<0>, hipFuncAttributeMaxDynamicSharedMemorySize,
                             pks::Plan<0>::TOTAL));
   HIPCK(hipFuncSetAttribute((const void*)pks::k_pks_step<1>, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -260,17 +249,18 @@ static int enqueue_xgmi_sgd(Engine* e, const Ctx& cx) {
   }
   if (e->bf)
     hipLaunchKernelGGL(xg::k_xgmi_ar_sgd<true>, dim3(xg::AR_NB), dim3(xg::AR_T), 0, e->st, cx, e->peers,
-                       (const float*)cx.grads, (float*)nullptr, e->pa.err + 1, 1, e->ar_deadline);
+                       (const float*)cx.grads, (float*)nullptr, e->qa.err + 1, 1, e->ar_deadline);
   else
     hipLaunchKernelGGL(xg::k_xgmi_ar_sgd<false>, dim3(xg::AR_NB), dim3(xg::AR_T), 0, e->st, cx, e->peers,
-                       (const float*)cx.grads, (float*)nullptr, e->pa.err + 1, 1, e->ar_deadline);
+                       (const float*)cx.grads, (float*)nullptr, e->qa.err + 1, 1, e->ar_deadline);
   HIPCK(hipGetLastError());
   return 0;
 }
 
-// Persistent path: one launch for the whole trunk, one for reduction + SGD.
-// `part`: 0 = the whole step; 1 = compute up to (not including) the gradient all-reduce; 2 = what follows it
-// (averaging SGD + CC4 base).  Parts 1/2 exist for comm_mode 1, where the host runs the all-reduce in between.
+// Persistent path: the sliced step kernel, then ONE kernel for reduction + all-reduce + SGD (mode: see
+// k_pks_reduce_ar).  `part`: 0 = the whole step; 1 = compute up to (not including) the gradient all-reduce;
+// 2 = what follows it (averaging SGD + CC4 base).  Parts 1/2 exist for comm_mode 1, where the host runs the
+// all-reduce in between.
 // grid of the sliced step: S workgroups per image, image slots rounded up to a multiple of 8 (see k_pks_step)
 static int pks_grid(int B) { return (B + 7) / 8 * 8 * pks::S; }
 
@@ -278,77 +268,27 @@ static int enqueue_step_persistent(Engine* e, int B, int part) {
   Ctx cx = e->base;
   cx.B = B;
   const bool multi = e->comm_on;
-  if (e->sliced) {
-    // step kernel, then ONE kernel for reduction + all-reduce + SGD (mode: see k_pks_reduce_ar)
-    const bool xgmi = multi && e->in.comm_mode == 2;
-    if (xgmi && !e->peers_open) {
-      g_err = "xGMI all-reduce: peers not mapped (call dca_engine_ipc_open first)";
-      return -1;
-    }
-    if (part != 2) {
-      if (e->bf)
-        hipLaunchKernelGGL(pks::k_pks_step<0>, dim3(pks_grid(B)), dim3(pks::NTH), pks::Plan<0>::TOTAL, e->st, cx,
-                           e->qa);
-      else
-        hipLaunchKernelGGL(pks::k_pks_step<1>, dim3(pks_grid(B)), dim3(pks::NTH), pks::Plan<1>::TOTAL, e->st, cx,
-                           e->qa);
-      pks::RedAr ra{};
-      ra.peers = e->peers;
-      ra.err = e->pa.err + 1;
-      ra.deadline = e->ar_deadline;
-      ra.mode = !multi ? 0 : (xgmi ? 2 : 1);
-      hipLaunchKernelGGL(pks::k_pks_reduce_ar, dim3(pks::NSEG), dim3(256), 0, e->st, cx, e->pa, B * pks::S, ra);
-    }
-    if (multi && !xgmi) {  // RCCL (comm_mode 0, captured) or the host (comm_mode 1, between parts 1 and 2)
-      if (part == 0) NCCK(ncclAllReduce(cx.grads, cx.grads, FLAT_N, ncclFloat32, ncclSum, e->comm, e->st));
-      if (part != 1) hipLaunchKernelGGL(e->kapply, dim3(64), dim3(NT), 0, e->st, cx, 1);
-    }
-    HIPCK(hipGetLastError());
-    return 0;
+  const bool xgmi = multi && e->in.comm_mode == 2;
+  if (xgmi && !e->peers_open) {
+    g_err = "xGMI all-reduce: peers not mapped (call dca_engine_ipc_open first)";
+    return -1;
   }
-  const bool rccl_overlap = e->split && multi && part == 0 && e->in.comm_mode == 0;  // fc all-reduce overlapped with the trunk backward
   if (part != 2) {
-    pk::PkArgs pa = e->pa;
-    // Packing the image workgroups onto one XCD (grid 8 x B, see pk_img) keeps the BN exchange inside one L2,
-    // but measured slower end to end (119 vs 105 us/step: every workgroup then shares one L2 and its
-    // bandwidth); opt-in for experiments only (DCA_PK_XPACK=1).
-    pa.xpack = (B <= 32 && e->xpack) ? 1 : 0;
-    const dim3 grid(pa.xpack ? 8 * B : B), blk(64 * 8);
-    if (!e->split) {
-      pa.phase = 0;
-      hipLaunchKernelGGL(pk::k_pk_step<8>, grid, blk, pk::Plan::TOTAL, e->st, cx, pa);
-      hipLaunchKernelGGL(pk::k_pk_reduce, dim3(pk::R_GRID), dim3(256), 0, e->st, cx, e->pa, 1);
-    } else {
-      // Split mode: phase 1 (stem, forward, head) | phase 2 (backward).  The fc gradients -- bucket A, 86 % of
-      // the gradient bytes -- are final after phase 1, so with RCCL they are reduced and all-reduced on the
-      // comm stream while phase 2 runs; bucket B (trunk, BN, stem, CC4 segment) follows the slab reduction.
-      pa.phase = 1;
-      hipLaunchKernelGGL(pk::k_pk_step<8>, grid, blk, pk::Plan::TOTAL, e->st, cx, pa);
-      if (rccl_overlap) {
-        HIPCK(hipEventRecord(e->evA, e->st));
-        HIPCK(hipStreamWaitEvent(e->cst, e->evA, 0));
-        hipLaunchKernelGGL(pk::k_pk_fc, dim3(pk::R_FC + 1), dim3(256), 0, e->cst, cx);
-        NCCK(ncclAllReduce(cx.grads, cx.grads, BUCKET_A_END, ncclFloat32, ncclSum, e->comm, e->cst));
-      }
-      pa.phase = 2;
-      hipLaunchKernelGGL(pk::k_pk_step<8>, grid, blk, pk::Plan::TOTAL, e->st, cx, pa);
-      hipLaunchKernelGGL(pk::k_pk_reduce, dim3(pk::R_TRUNK + pk::R_STEM + 1), dim3(256), 0, e->st, cx, e->pa, 0);
-      if (!rccl_overlap) hipLaunchKernelGGL(pk::k_pk_fc, dim3(pk::R_FC + 1), dim3(256), 0, e->st, cx);
-    }
+    if (e->bf)
+      hipLaunchKernelGGL(pks::k_pks_step<0>, dim3(pks_grid(B)), dim3(pks::NTH), pks::Plan<0>::TOTAL, e->st, cx,
+                         e->qa);
+    else
+      hipLaunchKernelGGL(pks::k_pks_step<1>, dim3(pks_grid(B)), dim3(pks::NTH), pks::Plan<1>::TOTAL, e->st, cx,
+                         e->qa);
+    pks::RedAr ra{};
+    ra.peers = e->peers;
+    ra.err = e->qa.err + 1;
+    ra.deadline = e->ar_deadline;
+    ra.mode = !multi ? 0 : (xgmi ? 2 : 1);
+    hipLaunchKernelGGL(pks::k_pks_reduce_ar, dim3(pks::NSEG), dim3(256), 0, e->st, cx, e->qa, B * pks::S, ra);
   }
-  if (multi) {
-    if (rccl_overlap) {  // bucket B on the comm stream, after bucket A (one communicator, one stream: ordered)
-      HIPCK(hipEventRecord(e->evB, e->st));
-      HIPCK(hipStreamWaitEvent(e->cst, e->evB, 0));
-      NCCK(ncclAllReduce(cx.grads + OFF_CONVW, cx.grads + OFF_CONVW, FLAT_N - OFF_CONVW, ncclFloat32, ncclSum,
-                         e->comm, e->cst));
-      HIPCK(hipEventRecord(e->evC, e->cst));
-      HIPCK(hipStreamWaitEvent(e->st, e->evC, 0));
-    } else if (part == 0 && e->in.comm_mode == 2) {
-      return enqueue_xgmi_sgd(e, cx);
-    } else if (part == 0) {
-      NCCK(ncclAllReduce(cx.grads, cx.grads, FLAT_N, ncclFloat32, ncclSum, e->comm, e->st));
-    }
+  if (multi && !xgmi) {  // RCCL (comm_mode 0, captured) or the host (comm_mode 1, between parts 1 and 2)
+    if (part == 0) NCCK(ncclAllReduce(cx.grads, cx.grads, FLAT_N, ncclFloat32, ncclSum, e->comm, e->st));
     if (part != 1) hipLaunchKernelGGL(e->kapply, dim3(64), dim3(NT), 0, e->st, cx, 1);
   }
   HIPCK(hipGetLastError());
@@ -442,27 +382,9 @@ static int engine_init(Engine* e, const DcaInit* in, int n_indices) {
     g_err = "persistent engine: pk_waves must be 8";
     return -1;
   }
-  e->pk_waves = 8;
   // comm_on: the step ends with a gradient collective + the averaging SGD kernel.  force_comm runs that path at
   // world_size 1 (a 1-rank RCCL communicator) so the graph-captured collective is testable on one GPU.
   e->comm_on = in->world_size > 1 || (in->force_comm && in->comm_mode == 0);
-  {
-    const char* xp = getenv("DCA_PK_XPACK");
-    e->xpack = xp && xp[0] == '1';
-    // Split mode (phase 1 | phase 2, fc all-reduce overlapped with the trunk backward): +7.7 us/step at
-    // world_size 1 (kernel boundary + state restore, profiles/bench_split_ws1.log), which the overlap repays
-    // only if RCCL needs more than that for the 264 KB fc bucket.  Opt-in: DCA_PK_SPLIT=1.
-    const char* sp = getenv("DCA_PK_SPLIT");
-    e->split = sp && sp[0] == '1';
-  }
-  {
-    const char* ps = getenv("DCA_PKS");  // DCA_PKS=0: the one-workgroup-per-image kernel (bf16 only)
-    e->sliced = e->persistent && !(ps && ps[0] == '0');
-  }
-  if (e->persistent && !e->sliced && !e->bf) {
-    g_err = "the one-workgroup-per-image persistent kernel is bf16-only (use the sliced kernel: unset DCA_PKS)";
-    return -1;
-  }
   if (e->bf && e->R == 4) dca::bind_kernels<true, 4, 16>(e);
   else if (e->bf) dca::bind_kernels<true, 2, 16>(e);
   else if (e->R == 4) dca::bind_kernels<false, 4, 8>(e);
@@ -475,17 +397,14 @@ static int engine_init(Engine* e, const DcaInit* in, int n_indices) {
     int dev = 0, ncu = 0, per_cu = 0;
     HIPCK(hipGetDevice(&dev));
     HIPCK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
-    if (!e->sliced)
-      HIPCK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)dca::pk::k_pk_step<8>, 64 * 8,
-                                                        dca::pk::Plan::TOTAL));
-    else if (e->bf)
+    if (e->bf)
       HIPCK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)dca::pks::k_pks_step<0>, dca::pks::NTH,
                                                         dca::pks::Plan<0>::TOTAL));
     else
       HIPCK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)dca::pks::k_pks_step<1>, dca::pks::NTH,
                                                         dca::pks::Plan<1>::TOTAL));
     const int resident = (per_cu > 1 ? per_cu - 1 : per_cu) * ncu;
-    const int need = e->sliced ? dca::pks_grid(in->bmax) : in->bmax;
+    const int need = dca::pks_grid(in->bmax);
     if (resident < need) {
       g_err = "persistent engine: " + std::to_string(need) + " workgroups cannot all be resident (" +
               std::to_string(per_cu) + " per CU x " + std::to_string(ncu) + " CUs); use the multi-kernel engine";
@@ -599,7 +518,8 @@ int dca_engine_derive(void* h) {
 // persistent engine: the batch ids of the next step are produced by the previous step; re-derive them whenever
 // the host moves the cursor or replaces the index list
 static int prime_ids(Engine* e) {
-  hipLaunchKernelGGL(dca::pk::k_pk_prime_ids, dim3(64), dim3(256), 0, e->st, e->base, e->pa);
+  if (!e->persistent) return 0;  // the multi-kernel engine gathers its batch inside the stem kernel
+  hipLaunchKernelGGL(dca::pks::k_pks_prime, dim3(64), dim3(256), 0, e->st, e->base, e->qa);
   HIPCK(hipGetLastError());
   e->staged_b = 64;
   return 0;
@@ -610,7 +530,7 @@ static int ensure_staged(Engine* e, int B) {
   if (e->persistent) e->staged_b = B;
   // sliced engine: a workgroup absent from the last steps (smaller batch) left BN slots whose 2-bit tags could
   // match again; zeroed slots (tag 0) never match (bn_tag)
-  if (e->sliced && B != e->last_b)
+  if (e->persistent && B != e->last_b)
     HIPCK(hipMemsetAsync(e->qa.bnx, 0, 2 * (size_t)dca::pks::LMAX * 64 * 4, e->st));
   e->last_b = B;
   return 0;
@@ -641,8 +561,8 @@ int dca_engine_set_cursor(void* h, int v) {
 int dca_engine_errors(void* h, unsigned* flags, int reset) {
   Engine* e = (Engine*)h;
   HIPCK(hipStreamSynchronize(e->st));
-  HIPCK(hipMemcpy(flags, e->pa.err, 2 * sizeof(unsigned), hipMemcpyDeviceToHost));
-  if (reset) HIPCK(hipMemset(e->pa.err, 0, 2 * sizeof(unsigned)));
+  HIPCK(hipMemcpy(flags, e->qa.err, 2 * sizeof(unsigned), hipMemcpyDeviceToHost));
+  if (reset) HIPCK(hipMemset(e->qa.err, 0, 2 * sizeof(unsigned)));
   return 0;
 }
 
@@ -807,13 +727,13 @@ int dca_engine_ipc_selftest(void* h, const float* src, float* dst, float timeout
     g_err = "ipc_selftest: peers not mapped";
     return -1;
   }
-  HIPCK(hipMemsetAsync(e->pa.err + 1, 0, sizeof(unsigned), e->st));
+  HIPCK(hipMemsetAsync(e->qa.err + 1, 0, sizeof(unsigned), e->st));
   const unsigned long long dl = (unsigned long long)((double)timeout_s * 1e8);
-  if (e->sliced) {  // the path a sliced training step uses: per-segment exchange inside the fused reduce kernel
+  if (e->persistent) {  // the path a sliced training step uses: per-segment exchange inside the fused reduce kernel
     dca::pks::RedAr ra{};
     ra.peers = e->peers;
     ra.peers.ticks = nullptr;
-    ra.err = e->pa.err + 1;
+    ra.err = e->qa.err + 1;
     ra.deadline = dl;
     ra.st_src = src;
     ra.st_dst = dst;
@@ -821,18 +741,18 @@ int dca_engine_ipc_selftest(void* h, const float* src, float* dst, float timeout
     ra.mode = 3;
     dca::Ctx cx = e->base;
     cx.B = 1;
-    hipLaunchKernelGGL(dca::pks::k_pks_reduce_ar, dim3(dca::pks::NSEG), dim3(256), 0, e->st, cx, e->pa, 1, ra);
+    hipLaunchKernelGGL(dca::pks::k_pks_reduce_ar, dim3(dca::pks::NSEG), dim3(256), 0, e->st, cx, e->qa, 1, ra);
   } else if (e->bf)
     hipLaunchKernelGGL(dca::xg::k_xgmi_ar_sgd<true>, dim3(dca::xg::AR_NB), dim3(dca::xg::AR_T), 0, e->st,
-                       e->base, e->peers, src, dst, e->pa.err + 1, 0, dl);
+                       e->base, e->peers, src, dst, e->qa.err + 1, 0, dl);
   else
     hipLaunchKernelGGL(dca::xg::k_xgmi_ar_sgd<false>, dim3(dca::xg::AR_NB), dim3(dca::xg::AR_T), 0, e->st,
-                       e->base, e->peers, src, dst, e->pa.err + 1, 0, dl);
+                       e->base, e->peers, src, dst, e->qa.err + 1, 0, dl);
   HIPCK(hipGetLastError());
   HIPCK(hipStreamSynchronize(e->st));
   unsigned f = 0;
-  HIPCK(hipMemcpy(&f, e->pa.err + 1, sizeof(unsigned), hipMemcpyDeviceToHost));
-  HIPCK(hipMemset(e->pa.err + 1, 0, sizeof(unsigned)));
+  HIPCK(hipMemcpy(&f, e->qa.err + 1, sizeof(unsigned), hipMemcpyDeviceToHost));
+  HIPCK(hipMemset(e->qa.err + 1, 0, sizeof(unsigned)));
   *timed_out = (f & 0x80000000u) ? 1 : 0;
   return 0;
 }
@@ -852,10 +772,10 @@ int dca_engine_ipc_bench(void* h, const float* src, float* dst, int iters, float
   for (int i = 0; i < iters; ++i) {
     if (e->bf)
       hipLaunchKernelGGL(dca::xg::k_xgmi_ar_sgd<true>, dim3(dca::xg::AR_NB), dim3(dca::xg::AR_T), 0, e->st,
-                         e->base, e->peers, src, dst, e->pa.err + 1, 0, e->ar_deadline);
+                         e->base, e->peers, src, dst, e->qa.err + 1, 0, e->ar_deadline);
     else
       hipLaunchKernelGGL(dca::xg::k_xgmi_ar_sgd<false>, dim3(dca::xg::AR_NB), dim3(dca::xg::AR_T), 0, e->st,
-                         e->base, e->peers, src, dst, e->pa.err + 1, 0, e->ar_deadline);
+                         e->base, e->peers, src, dst, e->qa.err + 1, 0, e->ar_deadline);
   }
   HIPCK(hipEventRecord(b, e->st));
   HIPCK(hipEventSynchronize(b));
@@ -897,10 +817,11 @@ void* dca_engine_region(void* h, const char* name) {
 
 size_t dca_engine_workspace_bytes(void* h) { return ((Engine*)h)->ws_bytes; }
 
-// 0: multi-kernel engine; 1: persistent, one workgroup per image; 2: persistent, image-sliced (S per image)
+// 0: multi-kernel engine; 2: persistent, image-sliced (S workgroups per image).  (1, the retired
+// one-workgroup-per-image kernel, is never returned.)
 int dca_engine_kind(void* h) {
   Engine* e = (Engine*)h;
-  return e->sliced ? 2 : (e->persistent ? 1 : 0);
+  return e->persistent ? 2 : 0;
 }
 
 

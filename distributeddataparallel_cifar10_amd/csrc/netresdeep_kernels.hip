@@ -1364,18 +1364,22 @@ __global__ void __launch_bounds__(NT) k_reduce(Ctx cx, int nslab, int nsslab) {
 
 // Kernel-layout copies of flat parameter e (value w): bf16 fc1 for the persistent head, the forward / dgrad
 // conv weight tiles, the stem weight (plain and as MFMA B fragments).  Other parameters have no copy.
+// Each engine sets only the copies its kernels read; the others are null (kernel-argument pointers, so these tests
+// are uniform branches).
 template <bool BF>
 __device__ __forceinline__ void derive_param(const Ctx& cx, int e, float w) {
   if (e < OFF_FC1W + 65536) {
-    ((unsigned short*)cx.w1b)[e - OFF_FC1W] = bfbits(w);  // bf16 fc1 copy (persistent engine's head)
+    if (cx.w1b) ((unsigned short*)cx.w1b)[e - OFF_FC1W] = bfbits(w);  // bf16 fc1 copy (sliced engine's head)
   } else if (e >= OFF_CONVW && e < OFF_CONVW + 9216) {
-    const int r = e - OFF_CONVW, co = r / 288, ci = (r / 9) % 32, tap = r % 9;
-    put_w<BF>(cx.wt_f, (tap * 32 + co) * 32 + ci, w);
-    put_w<BF>(cx.wt_d, ((8 - tap) * 32 + ci) * 32 + co, w);
+    if (cx.wt_f) {
+      const int r = e - OFF_CONVW, co = r / 288, ci = (r / 9) % 32, tap = r % 9;
+      put_w<BF>(cx.wt_f, (tap * 32 + co) * 32 + ci, w);
+      put_w<BF>(cx.wt_d, ((8 - tap) * 32 + ci) * 32 + co, w);
+    }
   } else if (e >= OFF_C1W && e < OFF_C1W + 864) {
     const int r = e - OFF_C1W, co = r / 27, k = r % 27;
-    put_w<BF>(cx.sw, co * 32 + k, w);
-    ((unsigned short*)cx.swf)[swf_slot(co, k)] = bfbits(w);
+    if (cx.sw) put_w<BF>(cx.sw, co * 32 + k, w);
+    if (cx.swf) ((unsigned short*)cx.swf)[swf_slot(co, k)] = bfbits(w);
   }
   if (cx.pkw != nullptr) {  // hi / lo bf16 splits for the sliced persistent engine
     const unsigned short hi = bfbits(w), lo = bfbits(w - __uint_as_float((unsigned)hi << 16));
@@ -1410,8 +1414,8 @@ __global__ void __launch_bounds__(NT) k_apply_sgd(Ctx cx, int mode) {
     if (mode) cx.rs_base[gid] = cx.grads[OFF_RS + gid];
     else cx.rs_base[gid] = gid < 32 ? cx.rm[gid] : cx.rv[gid - 32];
   }
-  if (!mode && gid < 32 * 5) put_w<BF>(cx.sw, (gid / 5) * 32 + 27 + gid % 5, 0.f);
-  if (!mode && gid < 2 * 3 * 64 * 4) {  // the never-written zero slots of the stem fragments (4th channel, taps 9..11)
+  if (!mode && gid < 32 * 5 && cx.sw) put_w<BF>(cx.sw, (gid / 5) * 32 + 27 + gid % 5, 0.f);
+  if (!mode && gid < 2 * 3 * 64 * 4 && cx.swf) {  // never-written zero slots of the stem fragments (4th channel, taps 9..11)
     const int ci = gid & 3, lane = (gid >> 2) & 63, m = (gid >> 8) % 3, tap = 4 * m + (lane >> 4);
     if (ci == 3 || tap >= 9) ((unsigned short*)cx.swf)[gid] = 0;
   }

@@ -1,6 +1,6 @@
 // Image-sliced persistent NetResDeep training step for CDNA4 (gfx950 / MI355X): ONE launch per step, every image
-// split over S = 4 workgroups of 4 image rows, so a batch of 32 runs on 128 CUs instead of the 32 of the
-// one-workgroup-per-image kernel (netresdeep_persistent.hip).  A workgroup has 8 waves: wave (row w, channel half
+// split over S = 4 workgroups of 4 image rows, so a batch of 32 runs on 128 CUs instead of the 32 of a
+// one-workgroup-per-image design (rounds 1-2; retired).  A workgroup has 8 waves: wave (row w, channel half
 // h) owns one image row and 16 of the 32 channels, so every latency-bound phase of a block is short.
 //
 //   stem (+ 1 halo pooled row each side, recomputed, no exchange) -> 10 forward blocks -> head -> 10 backward
@@ -48,6 +48,7 @@ constexpr int NNT = (18 + NW - 1) / NW;  // wgrad tile columns (ci half x tap) p
 constexpr int RND_HEAD = 10;           // rounds: 0..9 forward BN, 10 head (fc1 partials), 11..20 backward BN
 constexpr unsigned SPIN_LIMIT = 1u << 17;
 constexpr int RB = 80;                 // bf16 record: 32 channels (64 B) + 16 B pad (staggers the banks)
+constexpr int cmax(int a, int b) { return a > b ? a : b; }
 
 struct Args {
   unsigned long long* gran;  // [2][LMAX][GSTR] granules (halo rows, head partials)
@@ -116,7 +117,7 @@ struct Plan {
   static constexpr int U_SRED = U_XS + NP * XS_PL;             // [NW][64][4] f32 stem-wgrad partials (written
                                                                // after the barrier that retires the last wgrad)
   static constexpr int SBWD_END = U_SRED + NW * 64 * 16;
-  static constexpr int UNION = pk::cmax(pk::cmax(BWD_END, STEM_END), pk::cmax(HEAD_END, SBWD_END));
+  static constexpr int UNION = cmax(cmax(BWD_END, STEM_END), cmax(HEAD_END, SBWD_END));
   static constexpr int TOTAL = O_U + UNION;
 };
 static_assert(Plan<1>::TOTAL <= 160 * 1024, "LDS budget");
@@ -530,7 +531,7 @@ __global__ void __launch_bounds__(NTH) k_pks_step(Ctx cx, Args pa) {
     uint2* xin4 = (uint2*)(U + PL::U_XIN);
     float* x0i = (float*)(U + PL::U_X0);
     uint8_t* scl = (uint8_t*)(U + PL::U_SCODE);
-    // step constants -> misc (as netresdeep_persistent.hip): k < 64: BN gamma|beta -> misc[320 + k]; k >= 64 ->
+    // step constants -> misc: k < 64: BN gamma|beta -> misc[320 + k]; k >= 64 ->
     // misc[384 + k]: running mean|var [448,512) (rank 0's base under DDP, CC4), fc1 bias [512,544), W2
     // [544,864), b2 [864,874), conv1 bias [874,906), BN shifts [906,1226)
     constexpr int NKC = 842, KCM = (NKC + NTH - 1) / NTH;
@@ -1143,6 +1144,15 @@ __global__ void __launch_bounds__(NTH) k_pks_step(Ctx cx, Args pa) {
 }
 
 
+// The first batch after the host moved the cursor or replaced the index list (grid 64 x 256): image and label of
+// batch position b into the current staging parity (every later batch is staged by the step before it).
+__global__ void __launch_bounds__(256) k_pks_prime(Ctx cx, Args pa) {
+  const int t = threadIdx.x, b = blockIdx.x, par = *pa.epoch & 1, id = sample_id(cx, b);
+  if (t < 192)
+    ((uint4*)(pa.simg + (size_t)(par * 64 + b) * 3072))[t] = ((const uint4*)(cx.data + (size_t)id * 3072))[t];
+  if (t == 192) pa.slab[par * 64 + b] = cx.labels[id];
+}
+
 // ============================================================================================================
 // Reduction + gradient all-reduce + SGD in ONE kernel (sliced engine).  Every workgroup owns one segment of the
 // gradient: a chunk of the trunk conv (36 x 256, slab fragment order), of conv1 (5 x 256), a 64-column block
@@ -1160,8 +1170,8 @@ __global__ void __launch_bounds__(NTH) k_pks_step(Ctx cx, Args pa) {
 // ============================================================================================================
 // segments: 36 trunk + 5 stem chunks of 256, fc1 as 64 blocks of 16 rows x 64 features (1024), one small tail.
 // 106 workgroups: each reads one float4 per peer per thread at most (one round of xGMI loads in flight)
-constexpr int R_FC1 = 2 * pk::R_FC;
-constexpr int NSEG = pk::R_TRUNK + pk::R_STEM + R_FC1 + 1;  // 106
+constexpr int R_TRUNK = 36, R_STEM = 5, R_FC1 = 64;  // segments: trunk / stem chunks of 256, fc1 blocks of 1024
+constexpr int NSEG = R_TRUNK + R_STEM + R_FC1 + 1;  // 106
 constexpr int SEG_SMALL_LEN = 492;                         // 32 + 320 + 10 + 64 + 64 (+2 pad)
 constexpr int SEG_MAX = 1024;
 static_assert((size_t)NSEG * xg::MAXR * 4 <= xg::FLAG_BYTES, "one flag per segment and rank");
@@ -1234,9 +1244,9 @@ __device__ void seg_exchange(const Ctx& cx, const RedAr& ra, int b, float* segv,
 
 // parameter index of element k of segment b: >= 0 a parameter; -1 none; -2 - k: CC4 running-stat slot k
 __device__ __forceinline__ int seg_pidx(const Ctx& cx, int b, int k) {
-  if (b < pk::R_TRUNK + pk::R_STEM) {  // slab fragment order
-    const bool stem = b >= pk::R_TRUNK;
-    const int e = (stem ? b - pk::R_TRUNK : b) * 256 + k, ii = k & 3;
+  if (b < R_TRUNK + R_STEM) {  // slab fragment order
+    const bool stem = b >= R_TRUNK;
+    const int e = (stem ? b - R_TRUNK : b) * 256 + k, ii = k & 3;
     if (e >= (stem ? SSLAB_N : WSLAB_N)) return -1;
     const int tt = e >> 8, ln = (e >> 2) & 63, mt = tt & 1, nt = tt >> 1;
     if (!stem) return OFF_CONVW + (16 * mt + 4 * (ln >> 4) + ii) * 288 + (16 * (nt & 1) + (ln & 15)) * 9 + (nt >> 1);
@@ -1247,7 +1257,7 @@ __device__ __forceinline__ int seg_pidx(const Ctx& cx, int b, int k) {
     return e < 1056 ? OFF_C1B + (e - 1024) : -1;
   }
   if (b < NSEG - 1) {
-    const int fb = b - pk::R_TRUNK - pk::R_STEM;  // fc1 block: features 64 (fb >> 1) .., rows 16 (fb & 1) ..
+    const int fb = b - R_TRUNK - R_STEM;  // fc1 block: features 64 (fb >> 1) .., rows 16 (fb & 1) ..
     return OFF_FC1W + (16 * (fb & 1) + (k >> 6)) * 2048 + 64 * (fb >> 1) + (k & 63);
   }
   if (k < 32) return OFF_FC1B + k;
@@ -1258,7 +1268,7 @@ __device__ __forceinline__ int seg_pidx(const Ctx& cx, int b, int k) {
   return -1;
 }
 
-__global__ void __launch_bounds__(256) k_pks_reduce_ar(Ctx cx, pk::PkArgs pa, int nslab, RedAr ra) {
+__global__ void __launch_bounds__(256) k_pks_reduce_ar(Ctx cx, Args pa, int nslab, RedAr ra) {
   __shared__ __attribute__((aligned(16))) float segv[SEG_MAX];
   __shared__ f32x4 red[256];
   __shared__ float stage[64 * 32 + 64 * 64];
@@ -1280,10 +1290,10 @@ __global__ void __launch_bounds__(256) k_pks_reduce_ar(Ctx cx, pk::PkArgs pa, in
   }
   if (mode == 3) {
     for (int k = t; k < len; k += 256) segv[k] = off + k < ra.st_n ? ra.st_src[off + k] : 0.f;
-  } else if (b < pk::R_TRUNK + pk::R_STEM) {
+  } else if (b < R_TRUNK + R_STEM) {
     // trunk / stem chunk: 256 outputs in slab fragment order, summed over the nslab workgroup slabs
-    const bool stem = b >= pk::R_TRUNK;
-    const int chunk = stem ? b - pk::R_TRUNK : b;
+    const bool stem = b >= R_TRUNK;
+    const int chunk = stem ? b - R_TRUNK : b;
     const int slot = t & 63, grp = t >> 6, e0 = chunk * 256 + slot * 4;
     const float* src = stem ? cx.SSLAB : pa.tslab;
     const int stride = stem ? SSLAB_N : WSLAB_N, lim = stem ? SSLAB_N : WSLAB_N;
@@ -1309,7 +1319,7 @@ __global__ void __launch_bounds__(256) k_pks_reduce_ar(Ctx cx, pk::PkArgs pa, in
     }
   } else if (b < NSEG - 1) {
     // fc1 block: dW1[j][64f + kk .. +3] = sum_b dh[b][j] p[b][64f + kk ..], rows j = 16 h .. 16 h + 15
-    const int fb = b - pk::R_TRUNK - pk::R_STEM, f = fb >> 1, j0 = 16 * (fb & 1);
+    const int fb = b - R_TRUNK - R_STEM, f = fb >> 1, j0 = 16 * (fb & 1);
     float* dh_s = stage;           // [B][32]
     float* p_s = stage + 64 * 32;  // [B][64]
     const int jl = t >> 4, kk = 4 * (t & 15);

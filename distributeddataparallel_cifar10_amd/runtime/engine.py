@@ -38,7 +38,7 @@ LAYOUT = {
     "conv1.bias": (76044, (32,)),
 }
 # engine kinds reported by dca_engine_kind (also written into bench / metrics output)
-KIND_NAMES = {0: "multikernel", 1: "persistent-per-image", 2: "sliced"}
+KIND_NAMES = {0: "multikernel", 2: "sliced"}
 # gradient buckets (contiguous slices of the flat gradient buffer, ordered by gradient-ready time)
 BUCKETS = (("fc", 0, BUCKET_A_END), ("trunk+stem+bn_stats", BUCKET_A_END, FLAT_N))
 
@@ -93,7 +93,7 @@ def tile_to_nhwc(raw: torch.Tensor, count: int, batch: int) -> torch.Tensor:
     """Fragment-tiled activations of the persistent engine -> NHWC [count, batch, 16, 16, 32].
 
     Tiled index of element (row, col = 4q + i, ch = 16h + c): row*512 + h*256 + (16q + c)*4 + i
-    (csrc/netresdeep_persistent.hip: tl)."""
+    (csrc/netresdeep_pks.hip: st4r / ld4r)."""
     t = raw.reshape(count, batch, 16, 2, 4, 16, 4)  # [.., row, h, q, c, i]
     return t.permute(0, 1, 2, 4, 6, 3, 5).reshape(count, batch, 16, 16, 32)  # [.., row, q, i, h, c]
 
@@ -113,7 +113,7 @@ class EngineConfig:
     rows: int = 4                # multi-kernel engine: trunk rows per workgroup tile (2 or 4)
     persistent: Optional[bool] = None  # one-launch persistent step kernel (default: on; image-sliced)
     debug: bool = False          # persistent engine: also store per-block dy / residual grads (diagnostics)
-    pk_waves: int = 8            # persistent engine: waves per workgroup (8: 2 image rows per wave)
+    pk_waves: int = 8            # (ABI field; the sliced kernel always runs 8 waves per workgroup)
     world_size: int = 1
     rank: int = 0
     comm: str = "rccl"           # world_size > 1: "rccl" (all-reduce inside the graph-captured step),
@@ -187,7 +187,7 @@ class NetResDeepEngine:
                               f"engine (exact fp32 MFMA for dtype fp32, a different numerics path)", RuntimeWarning)
             native.check(rc, "dca_engine_create")
         self.h = h
-        self.kind = int(self.lib.dca_engine_kind(h))  # 0 multi-kernel, 1 persistent per image, 2 sliced
+        self.kind = int(self.lib.dca_engine_kind(h))  # 0 multi-kernel, 2 sliced persistent
         self.kind_name = KIND_NAMES.get(self.kind, str(self.kind))
         self.derive()
         self._n_indices = 0
@@ -343,12 +343,8 @@ class NetResDeepEngine:
         """Per-block activation region (X, Y, DY, G) as NHWC [count, batch, 16, 16, 32].
 
         The multi-kernel engine stores NHWC directly.  The persistent engine stores the MFMA fragment-tiled layout
-        [row][h][lane = 16q + c][i] holding element (row, col = 4q + i, ch = 16h + c) (netresdeep_persistent.hip: tl),
-        with X in bf16.
+        [row][h][lane = 16q + c][i] holding element (row, col = 4q + i, ch = 16h + c) (netresdeep_pks.hip: st4r).
         """
-        if self.kind == 1 and name == "X":  # block inputs are kept as bf16 (only used as a bf16 operand)
-            raw = self.region(name, count * batch * 4096).view(torch.bfloat16).float()
-            return tile_to_nhwc(raw, count, batch)
         raw = self.region(name, count * batch * 8192)
         if not self.cfg.persistent:
             return raw.view(count, batch, 16, 16, 32)

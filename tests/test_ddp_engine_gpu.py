@@ -97,12 +97,8 @@ def _worker(rank, port, dtype, persistent, q):
 
 
 @pytest.mark.parametrize("dtype,persistent,kernel", [("bf16", True, "sliced"), ("fp32", True, "sliced"),
-                                                     ("bf16", True, "per-image-split"), ("fp32", False, "multi"),
-                                                     ("bf16", False, "multi")])
-def test_engine_ddp_two_ranks_one_gpu(gpu, port, dtype, persistent, kernel, monkeypatch):
-    # inherited by the spawned ranks: the one-workgroup-per-image kernel in its two-phase (split) mode
-    monkeypatch.setenv("DCA_PKS", "0" if kernel == "per-image-split" else "1")
-    monkeypatch.setenv("DCA_PK_SPLIT", "1" if kernel == "per-image-split" else "0")
+                                                     ("fp32", False, "multi"), ("bf16", False, "multi")])
+def test_engine_ddp_two_ranks_one_gpu(gpu, port, dtype, persistent, kernel):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     procs = [ctx.Process(target=_worker, args=(r, port, dtype, persistent, q)) for r in range(WS)]

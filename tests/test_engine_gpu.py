@@ -138,29 +138,15 @@ def test_bench_contract(gpu):
     assert rec["n_gpus"] == 1 and rec["value"] > 0 and rec["loss_finite"]
 
 
-def test_split_mode_matches_oracle(gpu, monkeypatch):
-    """Two-phase persistent step (phase 1: stem/forward/head, phase 2: backward; fc gradients in their own
-    kernel) gives the same step as the fused kernel."""
-    from engine_diag import compare_one_step
-    monkeypatch.setenv("DCA_PKS", "0")  # the one-workgroup-per-image kernel
-    monkeypatch.setenv("DCA_PK_SPLIT", "1")
-    res = compare_one_step("bf16", 4, 32, True, seed=7, verbose=False, persistent=True)
-    bad = {k: v for k, v in res.items() if v > 5e-2}
-    assert not bad, bad
-
-
-@pytest.mark.parametrize("persistent,split", [(True, "0"), (True, "1"), (False, "0")])
-def test_rccl_path_world_size_one(gpu, persistent, split, monkeypatch):
-    if split == "1":  # the two-phase mode belongs to the one-workgroup-per-image kernel
-        monkeypatch.setenv("DCA_PKS", "0")
+@pytest.mark.parametrize("persistent", [True, False])
+def test_rccl_path_world_size_one(gpu, persistent):
     """comm="rccl" with force_comm at world_size 1: the graph-captured ncclAllReduce (a 1-rank communicator), the
-    split-mode stream/event wiring and the averaging SGD kernel all run, and give the same training step as the
-    fused-SGD world_size-1 engine (an all-reduce over one rank is the identity)."""
+    stream/event wiring and the averaging SGD kernel all run, and give the same training step as the fused-SGD
+    world_size-1 engine (an all-reduce over one rank is the identity)."""
     import copy
     from distributeddataparallel_cifar10_amd.data.synthetic import synthetic_cifar
     from distributeddataparallel_cifar10_amd.models.netresdeep import NetResDeep
     from distributeddataparallel_cifar10_amd.runtime.engine import EngineConfig, NetResDeepEngine
-    monkeypatch.setenv("DCA_PK_SPLIT", split)
     data, labels = synthetic_cifar(256, seed=3)
     torch.manual_seed(11)
     m0 = NetResDeep()
