@@ -88,14 +88,20 @@ struct Ctx {
   void* swf;                   // [2 co half][3 k group][64 lanes][4] bf16 conv1 weights as 16x16x16 MFMA B fragments
   unsigned long long* stamps;  // [32 kernel slots][256 wg][8 stamps][2] (diagnostic DCA_STAMPS builds only)
   // sliced persistent engine (netresdeep_pks.hip): bf16 hi / lo splits of the conv weights in the kernel's LDS
-  // record layout (record = 32 bf16 + 8 pad, 80 B), so a plane is staged by a straight LDS-DMA copy; u16 offsets
-  //   [0, 11520) fwd hi, record tap*32 + co, element ci | [11520, 23040) fwd lo |
-  //   [23040, 34560) dgrad hi, record (8 - tap)*32 + ci, element co | [34560, 46080) dgrad lo |
-  //   [46080, 47616) conv1 MFMA B fragments hi (swf_slot order) | [47616, 49152) lo
+  // record layout (record = 32 bf16, 64 B, 16-B chunks swizzled: pkw_elem), so a plane is staged by a straight
+  // LDS-DMA copy; u16 offsets
+  //   [0, 9216) fwd hi, record tap*32 + co, element ci | [9216, 18432) fwd lo |
+  //   [18432, 27648) dgrad hi, record (8 - tap)*32 + ci, element co | [27648, 36864) dgrad lo |
+  //   [36864, 38400) conv1 MFMA B fragments hi (swf_slot order) | [38400, 39936) lo
   unsigned short* pkw;
 };
-constexpr int PKW_REC = 40;             // u16 per record
-constexpr int PKW_PLANE = 288 * PKW_REC;  // 11520
+constexpr int PKW_REC = 32;             // u16 per record
+constexpr int PKW_PLANE = 288 * PKW_REC;  // 9216
+// u16 offset of element e of record r (chunk e >> 3 at position (e >> 3) ^ 2((r >> 2) & 1): netresdeep_pks.hip
+// rec_chunk)
+__host__ __device__ inline int pkw_elem(int r, int e) {
+  return r * PKW_REC + ((((e >> 3) ^ ((r >> 1) & 2)) << 3) | (e & 7));
+}
 constexpr int PKW_DGRAD = 2 * PKW_PLANE;
 constexpr int PKW_STEM = 4 * PKW_PLANE;   // 46080
 constexpr int PKW_N = PKW_STEM + 2 * 1536;

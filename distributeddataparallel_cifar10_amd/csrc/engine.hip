@@ -285,7 +285,7 @@ static int enqueue_step_persistent(Engine* e, int B, int part) {
     ra.err = e->qa.err + 1;
     ra.deadline = e->ar_deadline;
     ra.mode = !multi ? 0 : (xgmi ? 2 : 1);
-    hipLaunchKernelGGL(pks::k_pks_reduce_ar, dim3(pks::NSEG), dim3(256), 0, e->st, cx, e->qa, B * pks::S, ra);
+    hipLaunchKernelGGL(pks::k_pks_reduce_ar, dim3(pks::NSEG + 1), dim3(256), 0, e->st, cx, e->qa, B * pks::S, ra);
   }
   if (multi && !xgmi) {  // RCCL (comm_mode 0, captured) or the host (comm_mode 1, between parts 1 and 2)
     if (part == 0) NCCK(ncclAllReduce(cx.grads, cx.grads, FLAT_N, ncclFloat32, ncclSum, e->comm, e->st));

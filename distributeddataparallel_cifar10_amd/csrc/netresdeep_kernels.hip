@@ -1385,7 +1385,7 @@ __device__ __forceinline__ void derive_param(const Ctx& cx, int e, float w) {
     const unsigned short hi = bfbits(w), lo = bfbits(w - __uint_as_float((unsigned)hi << 16));
     if (e >= OFF_CONVW && e < OFF_CONVW + 9216) {
       const int r = e - OFF_CONVW, co = r / 288, ci = (r / 9) % 32, tap = r % 9;
-      const int fo = (tap * 32 + co) * PKW_REC + ci, dofs = PKW_DGRAD + ((8 - tap) * 32 + ci) * PKW_REC + co;
+      const int fo = pkw_elem(tap * 32 + co, ci), dofs = PKW_DGRAD + pkw_elem((8 - tap) * 32 + ci, co);
       cx.pkw[fo] = hi;
       cx.pkw[PKW_PLANE + fo] = lo;
       cx.pkw[dofs] = hi;

@@ -47,7 +47,7 @@ constexpr int LMAX = 64 * S;           // logical workgroups (batch <= 64)
 constexpr int NNT = (18 + NW - 1) / NW;  // wgrad tile columns (ci half x tap) per wave
 constexpr int RND_HEAD = 10;           // rounds: 0..9 forward BN, 10 head (fc1 partials), 11..20 backward BN
 constexpr unsigned SPIN_LIMIT = 1u << 17;
-constexpr int RB = 80;                 // bf16 record: 32 channels (64 B) + 16 B pad (staggers the banks)
+constexpr int RB = 64;                 // bf16 record: 32 channels, 16-B chunks swizzled (rec_chunk)
 constexpr int cmax(int a, int b) { return a > b ? a : b; }
 
 struct Args {
@@ -98,9 +98,10 @@ struct Plan {
   // head (WT live -- it receives the dgrad weights meanwhile -- XR / dyT / xT free)
   static constexpr int X10S = 33;
   static constexpr int U_X10 = U_XR;                           // [RS][16][X10S] f32
+  static constexpr int X10_BYTES = RS * 16 * X10S * 4;
   static constexpr int W1S = P == 1 ? 516 : 520;               // fc1 slice row stride (elements)
   static constexpr int W1_BYTES = 32 * W1S * (P == 1 ? 4 : 2); // [32 rows][512 local features] (f32 | bf16)
-  static constexpr int U_W1 = U_XR_END;
+  static constexpr int U_W1 = (cmax(U_XR_END, U_X10 + X10_BYTES) + 15) / 16 * 16;
   static constexpr int U_PCODE = U_W1 + W1_BYTES;              // [512] u8 pool argmax
   static constexpr int U_DP = U_PCODE + 512;                   // [512] f32 dL/dpooled
   static constexpr int U_PL = U_DP + 2048;                     // [512] f32 pooled features
@@ -121,7 +122,7 @@ struct Plan {
   static constexpr int TOTAL = O_U + UNION;
 };
 static_assert(Plan<1>::TOTAL <= 160 * 1024, "LDS budget");
-static_assert(Plan<0>::X10S * 4 * RS * 16 <= Plan<0>::XR_PL, "x10 fits the XR region");
+static_assert(Plan<0>::U_W1 >= Plan<0>::U_X10 + Plan<0>::X10_BYTES, "x10 clear of the fc1 slice");
 // dsT / xs are written while other waves may still run the last wgrad (dyT / xT); SRED only after the barrier
 static_assert(Plan<0>::U_SRED <= Plan<0>::U_DYT, "stem-backward staging clear of dyT / xT (last wgrad)");
 static_assert(Plan<1>::U_SRED <= Plan<1>::U_DYT, "stem-backward staging clear of dyT / xT (last wgrad)");
@@ -139,12 +140,19 @@ typedef unsigned v4u __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ unsigned short bf_lo(float v, unsigned short hi) {
   return bfbits(v - __uint_as_float((unsigned)hi << 16));
 }
+// Record layout of the conv operands (inputs XR, weights WT): record r = 32 bf16 channels = four 16-B chunks; chunk
+// q of record r sits at chunk position q ^ 2((r >> 2) & 1).  An MFMA operand read (ds_read_b128, lane 16q + c
+// reads chunk q of record base + c) then touches 16 distinct 16-B bank groups in each of the instruction's four
+// 16-lane groups, for ANY base (an unswizzled record stride cannot: 80-B records conflicted 2-way).
+__device__ __forceinline__ int rec_chunk(int rec, int q) { return ((rec << 6) | (q << 4)) ^ ((rec & 4) << 3); }
+__device__ __forceinline__ int rec_elem(int rec, int ch) { return rec_chunk(rec, ch >> 3) + ((ch & 7) << 1); }
 // one value into channel `ch` of record `rec` (both planes)
 template <int P>
 __device__ __forceinline__ void st1r(char* xr, int plane, int rec, int ch, float v) {
   const unsigned short hi = bfbits(v);
-  *(unsigned short*)(xr + rec * RB + ch * 2) = hi;
-  if constexpr (P == 1) *(unsigned short*)(xr + plane + rec * RB + ch * 2) = bf_lo(v, hi);
+  const int o = rec_elem(rec, ch);
+  *(unsigned short*)(xr + o) = hi;
+  if constexpr (P == 1) *(unsigned short*)(xr + plane + o) = bf_lo(v, hi);
 }
 template <int P>
 __device__ __forceinline__ f32x4 mma3(const bf16x8& ah, const bf16x8& al, const bf16x8& bh, const bf16x8& bl,
@@ -166,24 +174,39 @@ __device__ __forceinline__ f32x4 mma3s(const s4v& ah, const s4v& al, const s4v& 
   return acc;
 }
 
+// The B fragments of one conv weight (9 taps, lane 16q + c: record tap*32 + 16h + c, chunk q).  P = 0 keeps them
+// in registers for a whole pass (forward / backward): the conv then reads only its A operand from LDS.
+__device__ __forceinline__ int wrec_off(int h, int lane) {
+  return rec_chunk(16 * h + (lane & 15), lane >> 4);  // + tap * 32 * RB (a multiple of 8 records: same swizzle)
+}
+__device__ __forceinline__ void load_bfrag(const char* wt, int h, int lane, bf16x8 (&bw)[9]) {
+  const char* bb = wt + wrec_off(h, lane);
+#pragma unroll
+  for (int tap = 0; tap < 9; ++tap) bw[tap] = *(const bf16x8*)(bb + tap * 32 * RB);
+}
 // 3x3 conv of one output row (slice row w), output channels 16h .. 16h+15, on MFMA.  xr: (RS+2) x 18 records,
-// wt: 288 records (tap-major); P=1 reads the lo planes at +XR_PL / +WT_PL.
+// wt: 288 records (tap-major); P=1 reads the lo planes at +XR_PL / +WT_PL and the B operands from LDS, P=0 takes
+// its B operands from registers (bw).
 template <int P>
-__device__ __forceinline__ f32x4 conv_row(const char* xr, const char* wt, int w, int h, int lane) {
+__device__ __forceinline__ f32x4 conv_row(const char* xr, const char* wt, const bf16x8 (&bw)[9], int w, int h,
+                                          int lane) {
   using PL = Plan<P>;
   const int c = lane & 15, q = lane >> 4;
-  const char* abase = xr + (w * 18 + c) * RB + q * 16;
-  const char* bbase = wt + (16 * h + c) * RB + q * 16;
+  const char* bbase = wt + wrec_off(h, lane);
   f32x4 acc = z4();
 #pragma unroll
   for (int tap = 0; tap < 9; ++tap) {
     const int kh = tap / 3, kw = tap % 3;
-    const bf16x8 b = *(const bf16x8*)(bbase + (tap * 32) * RB);
-    const bf16x8 a = *(const bf16x8*)(abase + (kh * 18 + kw) * RB);
-    bf16x8 bl = b, al = a;
+    const int ao = rec_chunk((w + kh) * 18 + kw + c, q);
+    const bf16x8 a = *(const bf16x8*)(xr + ao);
+    bf16x8 b, bl, al = a;
     if constexpr (P == 1) {
-      bl = *(const bf16x8*)(bbase + PL::WT_PL + (tap * 32) * RB);
-      al = *(const bf16x8*)(abase + PL::XR_PL + (kh * 18 + kw) * RB);
+      b = *(const bf16x8*)(bbase + tap * 32 * RB);
+      bl = *(const bf16x8*)(bbase + PL::WT_PL + tap * 32 * RB);
+      al = *(const bf16x8*)(xr + PL::XR_PL + ao);
+    } else {
+      b = bw[tap];
+      bl = b;
     }
     acc = mma3<P>(a, al, b, bl, acc);
   }
@@ -361,6 +384,16 @@ __device__ __forceinline__ float slot_total(const float* cred, int slot) {
 }
 
 // this thread's 4 values of one image row in the tiled global layout [h][lane][i]
+// Write-through (sc1) 16-B store: the line leaves the XCD's L2 instead of staying dirty there.  Used for the bulk
+// data this kernel writes (per-block y, halo rows, weight-gradient slabs, pooled features, the next batch): dirty
+// L2 lines are written back at the kernel boundary (MI355X guide "boundary": + dirty bytes / ~6 TB/s), ~15 MB
+// per step here, which the following reduction kernel would wait for.
+__device__ __forceinline__ void st4_wt(void* p, f32x4 v) {
+  asm volatile("global_store_dwordx4 %0, %1, off sc1\n\ts_nop 1" ::"v"(p), "v"(v) : "memory");
+}
+__device__ __forceinline__ void st4r_wt(float* rowp, int h, int lane, const float (&v)[4]) {
+  st4_wt(rowp + h * 256 + lane * 4, f32x4{v[0], v[1], v[2], v[3]});
+}
 __device__ __forceinline__ void st4r(float* rowp, int h, int lane, const float (&v)[4]) {
   *(f32x4*)(rowp + h * 256 + lane * 4) = f32x4{v[0], v[1], v[2], v[3]};
 }
@@ -687,10 +720,12 @@ __global__ void __launch_bounds__(NTH) k_pks_step(Ctx cx, Args pa) {
   // the forward) by LDS-DMA right after block 6's exchange, read by
   // fc1 (reduction over features) and its transpose dp (reduction over rows).  The dgrad weights replace the
   // forward ones in WT by LDS-DMA right after block 9's exchange (block 9's conv was WT's last reader).
+  bf16x8 bw[9];  // P = 0: this wave's B fragments of the conv weight (forward here, dgrad in the backward)
+  if constexpr (P == 0) load_bfrag(WT, hh, lane, bw);
 #pragma unroll 1
   for (int i = 0; i < NBLK; ++i) {
     {
-      const f32x4 acc = conv_row<P>(XR, WT, w, hh, lane);
+      const f32x4 acc = conv_row<P>(XR, WT, bw, w, hh, lane);
 #pragma unroll
       for (int i2 = 0; i2 < 4; ++i2) y[i2] = acc[i2];
     }
@@ -713,7 +748,7 @@ __global__ void __launch_bounds__(NTH) k_pks_step(Ctx cx, Args pa) {
     if (i == DCA_DETAIL_FWD) DCA_STAMP(cx, 6, L, 1);
     xchg_wait(pa, i, epoch, G, cred, halo, hsrc, hwhich ^ 1, hh, yo);
     if (i == DCA_DETAIL_FWD) DCA_STAMP(cx, 6, L, 2);
-    st4r(cx.Y + (size_t)i * B * 8192 + img8, hh, lane, y);  // this block's y for the backward (after the sweep)
+    st4r_wt(cx.Y + (size_t)i * B * 8192 + img8, hh, lane, y);  // this block's y for the backward (after the sweep)
     // the fc1 slice for the head, straight into its LDS region (free during the forward) by LDS-DMA, issued right
     // AFTER an exchange: vmcnt is in order, so loads in flight when a sweep starts hold up its first pass (register
     // loads before the exchange + an LDS store a block later cost ~1.4 us in each of the two blocks, stamps)
@@ -721,7 +756,7 @@ __global__ void __launch_bounds__(NTH) k_pks_step(Ctx cx, Args pa) {
     if (i == NBLK - 1) wt_dma<P>(WT, pkw + PKW_DGRAD, wv, lane);  // dgrad weights, records [8 - tap][ci] x co
     lds_barrier();
     if (i == DCA_DETAIL_FWD) DCA_STAMP(cx, 6, L, 3);
-    if (halo) st4r(pa.yh + ((size_t)(i * LMAX + L) * 2 + hwhich) * 512, hh, lane, yo);
+    if (halo) st4r_wt(pa.yh + ((size_t)(i * LMAX + L) * 2 + hwhich) * 512, hh, lane, yo);
     // every thread finalises the statistics of its own channel (same sums, same order everywhere)
     const float S1 = slot_total(cred, ch), S2 = slot_total(cred, 32 + ch);
     const float dm = S1 / Ntot;
@@ -925,6 +960,7 @@ __global__ void __launch_bounds__(NTH) k_pks_step(Ctx cx, Args pa) {
   unsigned short* xT = (unsigned short*)(U + PL::U_XT);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the dgrad weight DMA (block 9) has landed
   lds_barrier();  // every wave is done with the head's LDS (X10 / W1 / DP overlap XR / dyT / xT)
+  if constexpr (P == 0) load_bfrag(WT, hh, lane, bw);  // dgrad B fragments
   for (int idx = t; idx < PL::NP * PL::XR_PL / 16; idx += NTH) ((uint4*)XR)[idx] = uint4{0u, 0u, 0u, 0u};
   for (int idx = t; idx < PL::NP * PL::XT_PL / 16; idx += NTH) ((uint4*)xT)[idx] = uint4{0u, 0u, 0u, 0u};
   f32x4 wacc[NNT][2];
@@ -1029,7 +1065,7 @@ __global__ void __launch_bounds__(NTH) k_pks_step(Ctx cx, Args pa) {
     if (i == DCA_DETAIL_BWD) DCA_STAMP(cx, 7, L, 6);
     // dgrad: g_i = g_{i+1} + conv(dy, W^T flipped)
     {
-      const f32x4 acc = conv_row<P>(XR, WT, w, hh, lane);
+      const f32x4 acc = conv_row<P>(XR, WT, bw, w, hh, lane);
 #pragma unroll
       for (int i2 = 0; i2 < 4; ++i2) g[i2] += acc[i2];
     }
@@ -1125,19 +1161,19 @@ __global__ void __launch_bounds__(NTH) k_pks_step(Ctx cx, Args pa) {
     lds_barrier();
     if (t < 256) {
       const int tile = t >> 6, ln = t & 63;
-      st4(ss + ((tile * 64 + ln) << 2), ld4(sred + ((tile * 64 + ln) << 2)) + ld4(sred + (((tile + 4) * 64 + ln) << 2)));
+      st4_wt(ss + ((tile * 64 + ln) << 2), ld4(sred + ((tile * 64 + ln) << 2)) + ld4(sred + (((tile + 4) * 64 + ln) << 2)));
     }
   }
   // the next batch's image n (this slice's quarter) and label, staged into the other parity
-  if (t < 48) ((uint4*)(pa.simg + (size_t)((par ^ 1) * 64 + n) * 3072 + 768 * s))[t] = nxt;
+  if (t < 48) st4_wt((uint4*)(pa.simg + (size_t)((par ^ 1) * 64 + n) * 3072 + 768 * s) + t, __builtin_bit_cast(f32x4, nxt));
   if (t == 48 && s == 0) pa.slab[(par ^ 1) * 64 + n] = nxt_lab;
   // trunk wgrad slab (accumulated over the 10 applications): tile tt = 2 nt + mt, the layout k_pks_reduce reads
 #pragma unroll
   for (int j = 0; j < NNT; ++j) {
     const int nt = wv + NW * j;
     if (nt < 18) {
-      st4(pa.tslab + (size_t)L * WSLAB_N + (((2 * nt) * 64 + lane) << 2), wacc[j][0]);
-      st4(pa.tslab + (size_t)L * WSLAB_N + (((2 * nt + 1) * 64 + lane) << 2), wacc[j][1]);
+      st4_wt(pa.tslab + (size_t)L * WSLAB_N + (((2 * nt) * 64 + lane) << 2), wacc[j][0]);
+      st4_wt(pa.tslab + (size_t)L * WSLAB_N + (((2 * nt + 1) * 64 + lane) << 2), wacc[j][1]);
     }
   }
   DCA_STAMP(cx, 5, L, 7);
@@ -1268,13 +1304,45 @@ __device__ __forceinline__ int seg_pidx(const Ctx& cx, int b, int k) {
   return -1;
 }
 
+// Grid NSEG + 1: workgroup NSEG is the step's bookkeeping (batch-mean loss, cursor, step / BN-batch counters,
+// epoch), independent of every segment, so it runs beside them instead of after the tail segment's work.
+__device__ __forceinline__ void pks_bookkeeping(const Ctx& cx, const Args& pa) {
+  const int t = threadIdx.x, B = cx.B;
+  if (t >= 64) return;
+  float l = t < B ? cx.HLOSS[t] : 0.f;  // B <= 64
+  double acc = 0.0;
+  int cur = 0, stp = 0, ep = 0;
+  long long nb = 0;
+  if (t == 0) {  // issued together with the loss loads: one memory round trip, not five dependent ones
+    acc = *cx.loss_acc;
+    cur = *cx.cursor;
+    stp = *cx.step_count;
+    nb = *cx.nbt;
+    ep = *pa.epoch;
+  }
+#pragma unroll
+  for (int m = 1; m < 64; m <<= 1) l += __shfl_xor(l, m);  // fixed tree: identical every step
+  if (t == 0) {
+    *cx.loss_acc = acc + (double)(l / (float)B);
+    *cx.cursor = cur + B;
+    *cx.step_count = stp + 1;
+    *cx.nbt = nb + NBLK;  // BatchNorm num_batches_tracked: +1 per application
+    *pa.epoch = ep + 1;
+  }
+}
+
 __global__ void __launch_bounds__(256) k_pks_reduce_ar(Ctx cx, Args pa, int nslab, RedAr ra) {
   __shared__ __attribute__((aligned(16))) float segv[SEG_MAX];
   __shared__ f32x4 red[256];
   __shared__ float stage[64 * 32 + 64 * 64];
   const int b = blockIdx.x, t = threadIdx.x, B = cx.B;
-  const int len = seg_len(b), off = seg_off(b);
   const int mode = ra.mode;
+  if (b == NSEG) {
+    if (mode != 3) pks_bookkeeping(cx, pa);
+    return;
+  }
+  const int len = seg_len(b), off = seg_off(b);
+  DCA_STAMP(cx, 8, b, 0);
   // this thread's SGD elements (k = t + 256 i): parameter indices and old values loaded first, so their latency
   // hides under the slab reduction (a dependent read after it cost 1.5 us per step)
   // this segment's exchange epoch (own flag), loaded now: the latency of the uncached read hides under the reduction
@@ -1299,15 +1367,15 @@ __global__ void __launch_bounds__(256) k_pks_reduce_ar(Ctx cx, Args pa, int nsla
     const int stride = stem ? SSLAB_N : WSLAB_N, lim = stem ? SSLAB_N : WSLAB_N;
     f32x4 sacc = z4();
     const int ec = e0 < lim ? e0 : lim - 4;
-    for (int k0 = 0; k0 < nslab; k0 += 64) {  // 16 slabs per thread in flight, fixed order
-      f32x4 v[16];
+    for (int k0 = 0; k0 < nslab; k0 += 128) {  // 32 slabs per thread in flight (all of batch 32), fixed order
+      f32x4 v[32];
 #pragma unroll
-      for (int u = 0; u < 16; ++u) {
+      for (int u = 0; u < 32; ++u) {
         const int k = k0 + grp + 4 * u;
         v[u] = ld4(src + (size_t)(k < nslab ? k : nslab - 1) * stride + ec);
       }
 #pragma unroll
-      for (int u = 0; u < 16; ++u)
+      for (int u = 0; u < 32; ++u)
         if (k0 + grp + 4 * u < nslab) sacc += v[u];
     }
     red[t] = sacc;
@@ -1380,7 +1448,9 @@ __global__ void __launch_bounds__(256) k_pks_reduce_ar(Ctx cx, Args pa, int nsla
     }
   }
   __syncthreads();
+  DCA_STAMP(cx, 8, b, 1);
   if (mode >= 2) seg_exchange(cx, ra, b, segv, len, off, ep0);
+  DCA_STAMP(cx, 8, b, 2);
 #pragma unroll
   for (int i = 0; i < KMAX; ++i) {
     const int k = t + 256 * i;
@@ -1410,21 +1480,7 @@ __global__ void __launch_bounds__(256) k_pks_reduce_ar(Ctx cx, Args pa, int nsla
       else if (mode == 2) cx.rs_base[kk] = g;
     }
   }
-  if (b == NSEG - 1 && mode != 3) {  // bookkeeping
-    __syncthreads();
-    float* lred = (float*)red;
-    lred[t] = t < B ? cx.HLOSS[t] : 0.f;
-    __syncthreads();
-    if (t == 0) {
-      float sl = 0.f;
-      for (int k = 0; k < B; ++k) sl += lred[k];
-      *cx.loss_acc += (double)(sl / (float)B);
-      *cx.cursor += B;
-      *cx.step_count += 1;
-      *cx.nbt += NBLK;  // BatchNorm num_batches_tracked: +1 per application
-      *pa.epoch += 1;
-    }
-  }
+  DCA_STAMP(cx, 8, b, 3);
 }
 
 }  // namespace pks

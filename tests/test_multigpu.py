@@ -1,9 +1,15 @@
-"""Cross-device data parallelism: one rank per GPU on a multi-GPU MI355X node (skipped below 2 devices, so the
-1-GPU tier collects and skips them; on an 8-GPU node they run unchanged).
+"""Cross-device data parallelism: one rank per GPU on a multi-GPU MI355X node (the ``multigpu`` tests skip below
+2 devices, so the 1-GPU tier collects and skips them; on an 8-GPU node they run unchanged).
 
-* the fused trainer's DDP step against the single-process oracle simulation with the slabs / flags crossing xGMI
-  (comm="xgmi") and with the graph-captured RCCL all-reduce (comm="rccl"); bitwise-equal parameters on all ranks;
-* the driver's own bench command (torch.distributed.run, one rank per GPU) with both all-reduce paths.
+* the fused trainer's DDP step against the single-process simulation of reference DDP (bf16 and fp32), with the
+  slabs / flags crossing xGMI (comm="xgmi") and with the graph-captured RCCL all-reduce (comm="rccl");
+  bitwise-equal parameters on all ranks;
+* the driver's exact command (``python bench.py --gpus N``, ranks self-launched) and its torchrun form, both
+  all-reduce paths, plus ``--sweep 1,2,N`` with its scaling-efficiency summary;
+* ResNet (ops kernels) under FlatBucketDDP + XgmiComm against the host-averaged per-rank reference.
+
+The ``shared`` variants run the same commands with every rank on GPU 0 (DCA_BENCH_SHARE_GPU=1: gloo process
+group, the engine's xGMI path between ranks on one device), so the 1-GPU tier exercises them every round.
 """
 import json
 import os
@@ -14,7 +20,7 @@ import pytest
 import torch
 import torch.multiprocessing as mp
 
-pytestmark = [pytest.mark.gpu, pytest.mark.multigpu]
+pytestmark = pytest.mark.gpu
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
@@ -22,17 +28,33 @@ def _ngpu() -> int:
     return torch.cuda.device_count()
 
 
-needs2 = pytest.mark.skipif(_ngpu() < 2, reason="needs >= 2 GPUs (one rank per device)")
+needs2 = [pytest.mark.multigpu, pytest.mark.skipif(_ngpu() < 2, reason="needs >= 2 GPUs (one rank per device)")]
 
 
-@needs2
+def _json_lines(out: str) -> list:
+    return [json.loads(ln) for ln in out.splitlines() if ln.startswith("{")]
+
+
+def _bench(args, shared=False, timeout=420):
+    env = dict(os.environ, DCA_XGMI_TIMEOUT_S="60")
+    env.pop("DCA_BENCH_SHARE_GPU", None)
+    if shared:
+        env["DCA_BENCH_SHARE_GPU"] = "1"
+    r = subprocess.run([sys.executable, *args], cwd=ROOT, env=env, capture_output=True, text=True, timeout=timeout)
+    assert r.returncode == 0, r.stderr[-4000:]
+    return _json_lines(r.stdout)
+
+
+@pytest.mark.parametrize("dtype", ["bf16", "fp32"])
 @pytest.mark.parametrize("comm", ["xgmi", "rccl"])
-def test_ddp_engine_cross_device(gpu, port, comm):
+@pytest.mark.multigpu
+@pytest.mark.skipif(_ngpu() < 2, reason="needs >= 2 GPUs (one rank per device)")
+def test_ddp_engine_cross_device(gpu, port, comm, dtype):
     from test_ddp_engine_gpu import _xgmi_worker
     ws = min(_ngpu(), 8)
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    procs = [ctx.Process(target=_xgmi_worker, args=(r, ws, port, "bf16", True, q, comm, True)) for r in range(ws)]
+    procs = [ctx.Process(target=_xgmi_worker, args=(r, ws, port, dtype, True, q, comm, True)) for r in range(ws)]
     for p in procs:
         p.start()
     res = [q.get(timeout=600) for _ in procs]
@@ -42,34 +64,87 @@ def test_ddp_engine_cross_device(gpu, port, comm):
     assert not bad, "\n".join(f"rank {r}:\n{e}" for r, e in bad)
 
 
-@needs2
-@pytest.mark.parametrize("allreduce", ["xgmi", "rccl"])
-def test_bench_one_rank_per_gpu(gpu, port, allreduce):
+def _check_bench_line(out, n, allreduce=None):
+    assert out["n_gpus"] == n and out["value"] > 0 and out["loss_finite"], out
+    assert out["config"]["parallelism"] == f"dp{n}" and out["config"]["global_batch"] == 32 * n
+    if allreduce is not None:
+        assert out["allreduce"] == allreduce, out
+    if n > 1 and out["allreduce"] == "xgmi":
+        assert len(out["allreduce_us_per_step"]) == n
+    assert out["fp32_value"] > 0 and out["fp32_loss_finite"] and out["fp32_mode"] in ("3xbf16", "fp32-mfma")
+
+
+@pytest.mark.multigpu
+@pytest.mark.skipif(_ngpu() < 2, reason="needs >= 2 GPUs (one rank per device)")
+def test_bench_driver_command(gpu):
+    """The driver's command verbatim: ``python bench.py --gpus N --steps K --warmup W`` (bench.py spawns the N
+    ranks itself); bf16 value plus the fp32 (reference precision) timing of the same invocation."""
     n = min(_ngpu(), 8)
-    env = dict(os.environ, DCA_XGMI_TIMEOUT_S="60")
-    env.pop("DCA_BENCH_SHARE_GPU", None)
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(n), "--master-addr",
-           "127.0.0.1", "--master-port", str(port), "bench.py", "--gpus", str(n), "--steps", "64", "--warmup", "32",
-           "--allreduce", allreduce]
-    r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=400)
-    assert r.returncode == 0, r.stderr[-4000:]
-    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
-    assert len(lines) == 1, r.stdout
-    out = json.loads(lines[0])
-    assert out["n_gpus"] == n and out["allreduce"] == allreduce and out["loss_finite"]
+    lines = _bench(["bench.py", "--gpus", str(n), "--steps", "48", "--warmup", "16"])
+    assert len(lines) == 1, lines
+    _check_bench_line(lines[0], n)
 
 
-@needs2
+@pytest.mark.parametrize("allreduce", ["xgmi", "rccl"])
+@pytest.mark.multigpu
+@pytest.mark.skipif(_ngpu() < 2, reason="needs >= 2 GPUs (one rank per device)")
+def test_bench_torchrun_one_rank_per_gpu(gpu, port, allreduce):
+    n = min(_ngpu(), 8)
+    lines = _bench(["-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(n), "--master-addr",
+                    "127.0.0.1", "--master-port", str(port), "bench.py", "--gpus", str(n), "--steps", "48",
+                    "--warmup", "16", "--allreduce", allreduce])
+    assert len(lines) == 1, lines
+    _check_bench_line(lines[0], n, allreduce)
+
+
+@pytest.mark.multigpu
+@pytest.mark.skipif(_ngpu() < 2, reason="needs >= 2 GPUs (one rank per device)")
+def test_bench_sweep(gpu):
+    """``--sweep 1,2,N``: one fresh rank group per N and the scaling summary the headline metric asks for."""
+    n = min(_ngpu(), 8)
+    ns = sorted({1, 2, n})
+    lines = _bench(["bench.py", "--sweep", ",".join(map(str, ns)), "--steps", "48", "--warmup", "16", "--no-fp32"],
+                   timeout=900)
+    per_n, summary = lines[:-1], lines[-1]
+    assert [ln["n_gpus"] for ln in per_n] == ns and all(ln["loss_finite"] for ln in per_n)
+    assert set(summary["scaling_efficiency"]) == {str(k) for k in ns}
+    assert summary["scaling_efficiency"]["1"] == 1.0
+    assert all(0.0 < v for v in summary["scaling_efficiency"].values())
+
+
+@pytest.mark.multigpu
+@pytest.mark.skipif(_ngpu() < 2, reason="needs >= 2 GPUs (one rank per device)")
+def test_resnet_flat_ddp_xgmi_cross_device(gpu, port):
+    """ResNet (ops kernels, small batch / image) under FlatBucketDDP + XgmiComm, one rank per GPU, against the
+    per-rank reference with host-averaged gradients."""
+    from test_xgmi_comm_gpu import _ops_ddp_worker, _spawn
+    _spawn(_ops_ddp_worker, min(_ngpu(), 8), port, own_device=True)
+
+
+@pytest.mark.multigpu
+@pytest.mark.skipif(_ngpu() < 2, reason="needs >= 2 GPUs (one rank per device)")
 def test_resnet50_bench_self_launch(gpu):
     """bench/resnet50.py --gpus N spawns one rank per GPU itself (FlatBucketDDP over xGMI, ops kernels); small
     batch / image so it finishes quickly."""
     n = min(_ngpu(), 8)
-    cmd = [sys.executable, "bench/resnet50.py", "--gpus", str(n), "--batch", "16", "--image", "64", "--steps", "3",
-           "--warmup", "1"]
-    r = subprocess.run(cmd, cwd=ROOT, env=dict(os.environ, DCA_XGMI_TIMEOUT_S="60"), capture_output=True, text=True,
-                       timeout=600)
-    assert r.returncode == 0, r.stderr[-4000:]
-    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
-    assert len(lines) == 1, r.stdout
-    out = json.loads(lines[0])
-    assert out["n_gpus"] == n and out["value"] > 0 and out["loss"] == out["loss"]
+    lines = _bench(["bench/resnet50.py", "--gpus", str(n), "--batch", "16", "--image", "64", "--steps", "3",
+                    "--warmup", "1"], timeout=600)
+    assert len(lines) == 1, lines
+    assert lines[0]["n_gpus"] == n and lines[0]["value"] > 0 and lines[0]["loss"] == lines[0]["loss"]
+
+
+# ---- shared-GPU rehearsals of the same commands (run on the 1-GPU tier) ----------------------------------------
+def test_bench_driver_command_shared_gpu(gpu):
+    """``python bench.py --gpus 2`` with both ranks on GPU 0: self-launch, gloo rendezvous, the engine's xGMI
+    gradient exchange between the ranks, slowest-rank timing and the fp32 second timing."""
+    lines = _bench(["bench.py", "--gpus", "2", "--steps", "32", "--warmup", "8"], shared=True)
+    assert len(lines) == 1, lines
+    _check_bench_line(lines[0], 2, "xgmi")
+
+
+def test_bench_sweep_shared_gpu(gpu):
+    lines = _bench(["bench.py", "--sweep=1,2", "--steps", "32", "--warmup", "8", "--no-fp32"], shared=True,
+                   timeout=600)
+    per_n, summary = lines[:-1], lines[-1]
+    assert [ln["n_gpus"] for ln in per_n] == [1, 2] and all(ln["loss_finite"] for ln in per_n)
+    assert set(summary["scaling_efficiency"]) == {"1", "2"}

@@ -35,10 +35,10 @@ def _expect(xs, wire, scale):
     return s.bfloat16().float() if wire == "bf16" else s
 
 
-def _spawn(target, ws, *args):
+def _spawn(target, ws, *args, **kw):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    procs = [ctx.Process(target=target, args=(r, ws, *args, q)) for r in range(ws)]
+    procs = [ctx.Process(target=target, args=(r, ws, *args, q), kwargs=kw) for r in range(ws)]
     for p in procs:
         p.start()
     res = [q.get(timeout=600) for _ in procs]
@@ -48,12 +48,14 @@ def _spawn(target, ws, *args):
     assert not bad, "\n".join(f"rank {r}:\n{e}" for r, e in bad)
 
 
-def _init(rank, ws, port):
+def _init(rank, ws, port, own_device=False):
+    """gloo process group; every rank on GPU 0 (shared-GPU rehearsal) or, own_device, rank r on GPU r."""
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=ws)
-    torch.cuda.set_device(0)
-    return torch.device("cuda", 0)
+    dev = rank if own_device else 0
+    torch.cuda.set_device(dev)
+    return torch.device("cuda", dev)
 
 
 def _collective_worker(rank, ws, port, q):
@@ -144,11 +146,12 @@ def test_flat_ddp_xgmi_matches_averaged_grads(gpu, port, ws, algo, wire):
     _spawn(_ddp_worker, ws, port, algo, wire)
 
 
-def _ops_ddp_worker(rank, ws, port, q):
+def _ops_ddp_worker(rank, ws, port, q, own_device=False):
     """OpsModel ResNet under FlatBucketDDP on the xGMI path: conv / BN gradients arrive through the grad sinks
-    (written by the kernels, buckets fired by the sink callbacks), block-input gradients through GradJoin."""
+    (written by the kernels, buckets fired by the sink callbacks), block-input gradients through GradJoin.  Checked
+    against a per-rank reference whose gradients are averaged on the host in rank order (CC5 simulated)."""
     try:
-        dev = _init(rank, ws, port)
+        dev = _init(rank, ws, port, own_device)
         import copy
         from distributeddataparallel_cifar10_amd.models.resnet50 import ResNet
         from distributeddataparallel_cifar10_amd.ops import OpsModel, cross_entropy
