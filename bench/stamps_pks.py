@@ -76,12 +76,13 @@ def main():
                           "last_pub_to_first_done_us": round(float(D.min() - P.max()) / 100.0, 2),
                           "done_spread_us": round(float(D.max() - D.min()) / 100.0, 2),
                           "pub_to_done_med_us": round(float(np.median(D - P)) / 100.0, 2)}), flush=True)
-    # reduction kernel (slot 8, workgroup = gradient segment): 0 start, 1 segment summed, 2 exchanged, 3 end
+    # reduction kernel (slot 8, workgroup = gradient segment): 0 start, 1 segment summed, 2 exchanged, 3 end;
+    # fc workers of the step kernel (slot 9, fc1 block 0..63, 64 = fc tail): 0 start, 1 head seen + computed, ...
     red = raw.reshape(32, 256, 8, 2)[8]
     step_end = rte.max()
-    groups = {"trunk": range(0, 36), "stem": range(36, 41), "fc1": range(41, 105), "tail": range(105, 106)}
-    r0 = red[:106, 0, 1].astype(np.int64)
-    r3 = red[:106, 3, 1].astype(np.int64)
+    groups = {"trunk": range(0, 144), "stem": range(144, 161), "bn_tail": range(161, 162)}
+    r0 = red[:162, 0, 1].astype(np.int64)
+    r3 = red[:162, 3, 1].astype(np.int64)
     if (r0 != 0).all():
         print(json.dumps({"reduce_gap_after_step_us": round(float(r0.min() - step_end) / 100.0, 2),
                           "reduce_span_us": round(float(r3.max() - r0.min()) / 100.0, 2),
@@ -93,6 +94,11 @@ def main():
                               "sgd_us": round(float(seg[2]), 2),
                               "end_after_first_start_us": round(float(x[:, 3, 1].max() - r0.min()) / 100.0, 2)}),
                   flush=True)
+    fcw = raw.reshape(32, 256, 8, 2)[9][:65].astype(np.int64)
+    if (fcw[:, 3, 1] != 0).all():
+        print(json.dumps({"fc_workers": 65, "compute_us": round(float(np.median(fcw[:, 1, 1] - fcw[:, 0, 1])) / 100.0, 2),
+                          "last_end_before_step_end_us": round(float(step_end - fcw[:, 3, 1].max()) / 100.0, 2)}),
+              flush=True)
     eng.close()
 
 

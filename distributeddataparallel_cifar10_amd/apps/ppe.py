@@ -23,7 +23,8 @@ workflow runs on MI355X:
 Deliberate fixes: ``-freeze`` really freezes (``requires_grad``, applied before the DDP
 wrap); k-fold calls ``train`` with the right arguments; validation runs in eval mode and averages every val batch
 (the reference kept only the last).  ``pre_generate_labels`` keeps the reference's raw-logit threshold and 0/1
-"scores" by default (probabilities are added as "probs").
+"scores" (as floats 0.0 / 1.0, like its ``pred.astype(np.float)``); ``with_probs=True`` adds the sigmoid
+probabilities as "probs" (an extension).
 """
 from __future__ import annotations
 
@@ -379,12 +380,12 @@ def k_fold_cv(dataset, k: int, load_model: Optional[str], save_dir: str, num_epo
 
 def pre_generate_labels(model, dataset, model_name: Optional[str], out_dir: str = "outputs",
                         json_path: str = "PPE_preds_160.json", threshold: float = 0.5, device=None,
-                        threshold_probs: bool = False):
+                        threshold_probs: bool = False, with_probs: bool = False):
     """Reference ppe_main_ddp.py:310-396: predict every box, draw the boxes with their active attributes onto
     the image, write the images and a JSON of boxes / scores.
 
     As the reference (its sigmoid is commented out), an attribute is on when its RAW LOGIT exceeds `threshold`,
-    and the JSON "scores" are those 0/1 decisions; "probs" adds the sigmoid probabilities.
+    and the JSON "scores" are those decisions as 0.0 / 1.0; ``with_probs`` adds the sigmoid probabilities.
     ``threshold_probs=True`` thresholds the probabilities instead (logit > logit(threshold))."""
     from PIL import Image, ImageDraw
     device = device or next(model.parameters()).device
@@ -403,7 +404,11 @@ def pre_generate_labels(model, dataset, model_name: Optional[str], out_dir: str 
             probs = torch.sigmoid(logits).numpy()
             p = ((probs if threshold_probs else logits.numpy()) > threshold).astype(np.int64)
             name = os.path.splitext(os.path.basename(str(path)))[0]
-            out[name] = {"bboxes": boxes.tolist(), "scores": p.tolist(), "probs": probs.tolist()}
+            # the reference writes pred.astype(np.float): 0.0 / 1.0 (ppe_main_ddp.py:368); probabilities only
+            # on request (an extension of the reference's format)
+            out[name] = {"bboxes": boxes.tolist(), "scores": p.astype(np.float64).tolist()}
+            if with_probs:
+                out[name]["probs"] = probs.tolist()
             canvas = Image.fromarray(img.permute(1, 2, 0).clamp(0, 255).byte().numpy())
             draw = ImageDraw.Draw(canvas)
             for (x1, y1, x2, y2), s in zip(boxes.tolist(), p):

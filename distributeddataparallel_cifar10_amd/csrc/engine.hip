@@ -101,6 +101,12 @@ struct Engine {
   int resident = 0;      // persistent engine: workgroups guaranteed co-resident (occupancy x CUs)
   int staged_b = 0;  // persistent engine: batch slots of the current staging parity that hold the next batch
   int last_b = 0;    // batch size of the last enqueued step (BN slots are re-zeroed when it changes)
+  int seg_ch = 64;   // gradient-segment layout (pks::seg_layout): trunk / conv1 chunk size
+  int fc_in_step = 1;  // the fc1 / fc-tail gradient segments run on the step kernel's fc workers (pks::N_FCW extra
+                       // workgroups beside the backward); off: in the reduction kernel.  Off whenever the step and
+                       // its fc workers would exceed the co-resident budget, and when xGMI peers share this device
+  int shared_device = 0;  // set by the host: xGMI peers on this device (shared-GPU rehearsal): no fc workers and
+                          // the coarse 107-segment layout, so a spinning reduction grid leaves CUs for a peer's step
   std::map<std::string, void*> regions;
   // dynamic LDS sizes
   size_t s_stem = 0, s_fwd = 0, s_head1 = 0, s_head2 = 0, s_dgrad = 0, s_dgrad0 = 0, s_wgrad = 0, s_fc = 0;
@@ -159,7 +165,7 @@ static int alloc_workspace(Engine* e) {
       {"SLAB", 2 * 64 * 4},
       {"COMMT", 16}, {"PKW", PKW_N * 2},
       {"PKS_GRAN", 2 * (size_t)pks::LMAX * pks::GSTR * 8}, {"PKS_YH", 10 * (size_t)pks::LMAX * 2 * 512 * 4},
-      {"PKS_BNX", 2 * (size_t)pks::LMAX * 64 * 4},
+      {"PKS_BNX", 2 * (size_t)pks::LMAX * 64 * 4}, {"PKS_HDONE", (size_t)pks::LMAX * 8},
       {"C1", e->in.debug ? bmax * 32 * 1024 * 4 : 16},
   };
   size_t total = 0;
@@ -212,6 +218,7 @@ static int alloc_workspace(Engine* e) {
   pks::Args& qa = e->qa;
   qa.gran = (unsigned long long*)e->regions["PKS_GRAN"];
   qa.bnx = (unsigned*)e->regions["PKS_BNX"];
+  qa.hdone = (unsigned long long*)e->regions["PKS_HDONE"];
   qa.epoch = (int*)e->regions["EPOCH"];
   qa.err = (unsigned*)e->regions["ERR"];
   qa.tslab = (float*)e->regions["TSLAB"];
@@ -274,18 +281,20 @@ static int enqueue_step_persistent(Engine* e, int B, int part) {
     return -1;
   }
   if (part != 2) {
-    if (e->bf)
-      hipLaunchKernelGGL(pks::k_pks_step<0>, dim3(pks_grid(B)), dim3(pks::NTH), pks::Plan<0>::TOTAL, e->st, cx,
-                         e->qa);
-    else
-      hipLaunchKernelGGL(pks::k_pks_step<1>, dim3(pks_grid(B)), dim3(pks::NTH), pks::Plan<1>::TOTAL, e->st, cx,
-                         e->qa);
     pks::RedAr ra{};
     ra.peers = e->peers;
     ra.err = e->qa.err + 1;
     ra.deadline = e->ar_deadline;
     ra.mode = !multi ? 0 : (xgmi ? 2 : 1);
-    hipLaunchKernelGGL(pks::k_pks_reduce_ar, dim3(pks::NSEG + 1), dim3(256), 0, e->st, cx, e->qa, B * pks::S, ra);
+    ra.fc_in_step = (e->fc_in_step && !e->shared_device && pks_grid(B) + pks::N_FCW <= e->resident) ? 1 : 0;
+    ra.seg_ch = e->shared_device ? 256 : e->seg_ch;
+    const dim3 grid(pks_grid(B) + (ra.fc_in_step ? pks::N_FCW : 0));
+    if (e->bf)
+      hipLaunchKernelGGL(pks::k_pks_step<0>, grid, dim3(pks::NTH), pks::Plan<0>::TOTAL, e->st, cx, e->qa, ra);
+    else
+      hipLaunchKernelGGL(pks::k_pks_step<1>, grid, dim3(pks::NTH), pks::Plan<1>::TOTAL, e->st, cx, e->qa, ra);
+    hipLaunchKernelGGL(pks::k_pks_reduce_ar, dim3(pks::reduce_segments(ra.fc_in_step, ra.seg_ch) + 1), dim3(256), 0, e->st,
+                       cx, e->qa, B * pks::S, ra);
   }
   if (multi && !xgmi) {  // RCCL (comm_mode 0, captured) or the host (comm_mode 1, between parts 1 and 2)
     if (part == 0) NCCK(ncclAllReduce(cx.grads, cx.grads, FLAT_N, ncclFloat32, ncclSum, e->comm, e->st));
@@ -411,6 +420,8 @@ static int engine_init(Engine* e, const DcaInit* in, int n_indices) {
       return -1;
     }
     e->resident = resident;
+    if (const char* fo = getenv("DCA_PKS_FC_IN_STEP")) e->fc_in_step = fo[0] != '0';
+    if (const char* sc = getenv("DCA_PKS_SEG_CH")) e->seg_ch = atoi(sc) == 256 ? 256 : 64;
   }
   HIPCK(hipStreamCreateWithFlags(&e->st, hipStreamNonBlocking));
   HIPCK(hipStreamCreateWithFlags(&e->cst, hipStreamNonBlocking));
@@ -739,9 +750,12 @@ int dca_engine_ipc_selftest(void* h, const float* src, float* dst, float timeout
     ra.st_dst = dst;
     ra.st_n = dca::FLAT_N;
     ra.mode = 3;
+    ra.fc_in_step = 0;  // every segment in the reduction kernel
+    ra.seg_ch = e->shared_device ? 256 : e->seg_ch;
     dca::Ctx cx = e->base;
     cx.B = 1;
-    hipLaunchKernelGGL(dca::pks::k_pks_reduce_ar, dim3(dca::pks::NSEG), dim3(256), 0, e->st, cx, e->qa, 1, ra);
+    hipLaunchKernelGGL(dca::pks::k_pks_reduce_ar, dim3(dca::pks::seg_layout(ra.seg_ch).nseg), dim3(256), 0, e->st, cx,
+                       e->qa, 1, ra);
   } else if (e->bf)
     hipLaunchKernelGGL(dca::xg::k_xgmi_ar_sgd<true>, dim3(dca::xg::AR_NB), dim3(dca::xg::AR_T), 0, e->st,
                        e->base, e->peers, src, dst, e->qa.err + 1, 0, dl);
@@ -802,6 +816,18 @@ int dca_engine_sync(void* h) {
   Engine* e = (Engine*)h;
   HIPCK(hipStreamSynchronize(e->st));
   HIPCK(hipStreamSynchronize(e->cst));
+  return 0;
+}
+
+// Sliced engine: the host reports that xGMI peers share this device (shared-GPU rehearsal): no fc workers in the
+// step kernel and the coarse gradient-segment layout (see Engine::shared_device).  Collective in effect: every
+// rank must make the same call before stepping.  Drops the captured graphs.
+int dca_engine_set_shared_device(void* h, int shared) {
+  Engine* e = (Engine*)h;
+  HIPCK(hipStreamSynchronize(e->st));
+  for (auto& kv : e->graphs) (void)hipGraphExecDestroy(kv.second);
+  e->graphs.clear();
+  e->shared_device = shared ? 1 : 0;
   return 0;
 }
 

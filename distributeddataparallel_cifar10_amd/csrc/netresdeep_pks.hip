@@ -53,6 +53,7 @@ constexpr int cmax(int a, int b) { return a > b ? a : b; }
 struct Args {
   unsigned long long* gran;  // [2][LMAX][GSTR] granules (halo rows, head partials)
   unsigned* bnx;             // [2][LMAX][64] BatchNorm partials, 4-byte self-tagged values (see bn_tag)
+  unsigned long long* hdone; // [LMAX] head-done granules {tagof(epoch, RND_HDONE), 0} (fc workers' start signal)
   int* epoch;                // device scalar, advanced by the reduce kernel after every step
   unsigned* err;             // bit r: exchange round r timed out
   float* tslab;              // [LMAX][WSLAB_N] trunk wgrad per workgroup (fragment order, read by k_pks_reduce)
@@ -296,54 +297,52 @@ __device__ __forceinline__ void bn_put(const Args& pa, int rnd, int L, int slot,
                      __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 // BN sweep: lane 16 sub + q4 of wave wv reads slots 4 q4 .. 4 q4 + 3 of workgroups 4 wv + sub + 32 k (one 16-B sc1
-// load), k < KS; sums in k order.  Slots past the grid read a valid (clamped) address and count 0.
-template <int KS>
-__device__ __forceinline__ void sweep_issue(const __amdgpu_buffer_rsrc_t rs, int wv, int lane, int G, v4u (&x)[KS]) {
-  const int q4 = lane & 15, sub = lane >> 4;
-  asm volatile("" ::: "memory");  // re-issued every pass (never hoisted out of the spin)
-#pragma unroll
-  for (int k = 0; k < KS; ++k) {
-    const int Lk = 4 * wv + sub + 4 * NW * k, Lc = Lk < G ? Lk : G - 1;
-    x[k] = __builtin_amdgcn_raw_buffer_load_b128(rs, (Lc * 64 + 4 * q4) * 4, 0, 16);
-  }
+// load), k < KS.  A pass re-reads only the loads whose four values were not all valid yet (per lane: exec-masked;
+// per wave: skipped once no lane needs it), so after the first pass the polling traffic is the stragglers' slots
+// only and every later pass is a short round trip.  The values are summed once at the end, in k order: the same
+// sums in every workgroup, whatever order they arrived in.
+__device__ __forceinline__ void sleep_units(int n) {
+  for (int k = 0; k < n; ++k) __builtin_amdgcn_s_sleep(1);  // 64 cycles each
 }
 template <int KS>
-__device__ __forceinline__ bool sweep_eval(const v4u (&x)[KS], int wv, int lane, int G, unsigned tag, float (&sv)[4]) {
-  const int sub = lane >> 4;
-  bool ok = true;
+__device__ __forceinline__ void sweep_wait(const Args& pa, int round, int wv, int lane, int G, unsigned tag,
+                                           float (&sv)[4]) {
+  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(pa.bnx + (size_t)(round & 1) * LMAX * 64,
+                                                                      (short)0, LMAX * 64 * 4, 0x00020000);
+  const int q4 = lane & 15, sub = lane >> 4;
+  v4u xa[KS];
+  unsigned need = 0;  // bit k: load k of this lane still lacks a valid value
+#pragma unroll
+  for (int k = 0; k < KS; ++k) {
+    xa[k] = v4u{0u, 0u, 0u, 0u};
+    if (4 * wv + sub + 4 * NW * k < G) need |= 1u << k;
+  }
+  for (unsigned spins = 0;; ++spins) {
+    asm volatile("" ::: "memory");  // re-issued every pass (never hoisted out of the spin)
+#pragma unroll
+    for (int k = 0; k < KS; ++k)
+      if (need & (1u << k))
+        xa[k] = __builtin_amdgcn_raw_buffer_load_b128(rs, ((4 * wv + sub + 4 * NW * k) * 64 + 4 * q4) * 4, 0, 16);
+#pragma unroll
+    for (int k = 0; k < KS; ++k) {
+      const bool ok = (xa[k][0] & 3u) == tag && (xa[k][1] & 3u) == tag && (xa[k][2] & 3u) == tag &&
+                      (xa[k][3] & 3u) == tag;
+      if (ok) need &= ~(1u << k);
+    }
+    if (__all(need == 0)) break;
+    sleep_units(pa.gap);
+    if (spins >= SPIN_LIMIT) {
+      if (lane == 0) atomicOr(pa.err, 1u << (round & 31));
+      break;
+    }
+  }
 #pragma unroll
   for (int e = 0; e < 4; ++e) sv[e] = 0.f;
 #pragma unroll
   for (int k = 0; k < KS; ++k) {
     const bool valid = 4 * wv + sub + 4 * NW * k < G;
 #pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      ok &= !valid || (x[k][e] & 3u) == tag;
-      sv[e] += valid ? __uint_as_float(x[k][e]) : 0.f;
-    }
-  }
-  return __all(ok);
-}
-__device__ __forceinline__ void sleep_units(int n) {
-  for (int k = 0; k < n; ++k) __builtin_amdgcn_s_sleep(1);  // 64 cycles each
-}
-// One full pass in flight, re-issued as soon as it fails.  Measured alternatives (profiles/bench_poll_r2.log):
-// two staggered full passes in flight 103.6 vs 95.9 us per step (more polling traffic); polling one sentinel
-// granule per workgroup between full passes 100.6 vs 98.1 (one more round trip).
-template <int KS>
-__device__ __forceinline__ void sweep_wait(const Args& pa, int round, int wv, int lane, int G, unsigned tag,
-                                           float (&sv)[4]) {
-  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(pa.bnx + (size_t)(round & 1) * LMAX * 64,
-                                                                      (short)0, LMAX * 64 * 4, 0x00020000);
-  v4u xa[KS];
-  for (unsigned spins = 0;; ++spins) {
-    sweep_issue<KS>(rs, wv, lane, G, xa);
-    if (sweep_eval<KS>(xa, wv, lane, G, tag, sv)) return;
-    sleep_units(pa.gap);
-    if (spins >= SPIN_LIMIT) {
-      if (lane == 0) atomicOr(pa.err, 1u << (round & 31));
-      return;
-    }
+    for (int e = 0; e < 4; ++e) sv[e] += valid ? __uint_as_float(xa[k][e]) : 0.f;
   }
 }
 // All-to-all BN exchange wait + (halo waves) the neighbour's boundary row.  On return cred[0 .. NW*64) holds every
@@ -390,6 +389,13 @@ __device__ __forceinline__ float slot_total(const float* cred, int slot) {
 // per step here, which the following reduction kernel would wait for.
 __device__ __forceinline__ void st4_wt(void* p, f32x4 v) {
   asm volatile("global_store_dwordx4 %0, %1, off sc1\n\ts_nop 1" ::"v"(p), "v"(v) : "memory");
+}
+__device__ __forceinline__ void st2_wt(float* p, float a, float b) {
+  typedef float f2_ __attribute__((ext_vector_type(2)));
+  asm volatile("global_store_dwordx2 %0, %1, off sc1" ::"v"(p), "v"(f2_{a, b}) : "memory");
+}
+__device__ __forceinline__ void st1_wt(float* p, float v) {
+  __hip_atomic_store((unsigned*)p, __float_as_uint(v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 __device__ __forceinline__ void st4r_wt(float* rowp, int h, int lane, const float (&v)[4]) {
   st4_wt(rowp + h * 256 + lane * 4, f32x4{v[0], v[1], v[2], v[3]});
@@ -515,14 +521,377 @@ __device__ __forceinline__ void w1_dma(const Ctx& cx, char* w1l, int s, int wv, 
   }
 }
 
+// ============================================================================================================
+// Gradient segments: reduction + gradient all-reduce + SGD.  Every segment is one slice of the gradient: a 64-element
+// chunk of the trunk conv or of conv1 (slab fragment order, summed over the B x S workgroup slabs), a 16-row x
+// 64-feature block of fc1 (1024), the fc tail (fc1 bias, fc2 weight and bias; 362) or the BN tail (BN affine and
+// the CC4 running-stat segment; 128).  A segment is
+//   mode 0 (world size 1): reduced, then SGD (fused);
+//   mode 1 (RCCL): reduced and written to the gradient only (ncclAllReduce + k_apply_sgd follow in the graph);
+//   mode 2 (xGMI): reduced, exchanged one-shot with the peers (write-through slab + per-segment flags in the second
+//     half of every rank's IPC region, peers read all W slabs, sum in rank order -- bitwise identical on every
+//     rank), then the averaging SGD: ~227 concurrent small all-reduces instead of one all-reduce launch after the
+//     reduction (reference: DDP's single NCCL bucket after the whole backward, main.py:63);
+//   mode 3: the same exchange on a caller pattern (collective self-test of this path).
+// The fc1 blocks and the fc tail are final after the head: with `fc_in_step` the step kernel runs them on 65
+// extra workgroups ("fc workers", on CUs the 128 step workgroups leave idle) beside the trunk backward --
+// including their xGMI exchange, i.e. 86.6 % of the gradient bytes all-reduced while the backward runs (the
+// reference's DDP bucket becomes ready only after the last backward op: zero overlap).  k_pks_reduce_ar
+// then handles the trunk, conv1 and BN-tail segments.
+// Memory ordering as in xgmi_allreduce.hip (system-coherent stores to uncached memory, s_waitcnt vmcnt(0) +
+// barrier before the flag, cache-bypassing loads; per-segment epochs, slab parity = epoch & 1).
+// ============================================================================================================
+// Segment layout, chosen per launch: trunk / conv1 chunks of `ch` = 64 elements (B x S slabs of 256 B per
+// workgroup; 227 segments) or 256 (41 chunks, 107 segments: the layout for ranks sharing one device, whose reduction
+// grid must leave room for another rank's step kernel -- a CU holding a reduction workgroup has too few VGPRs left
+// for a step workgroup).  256-element chunks read 128 KB through one CU (3.9 us, profiles/stamps_pks_bf16_r3f.log).
+constexpr int R_FC1 = 64;
+constexpr int FCT_LEN = 364, BNT_LEN = 128;        // fc tail 362 (+2 pad), BN tail
+constexpr int SEG_MAX = 1024;
+constexpr int NSEG_MAX = WSLAB_N / 64 + (SSLAB_N + 63) / 64 + R_FC1 + 2;  // 227: flag-array stride per rank
+constexpr int N_FCW = R_FC1 + 1;                   // fc workers of the step kernel
+constexpr int RND_HDONE = 30;                      // tag round of the head-done granules (fc workers' start)
+struct SegLayout {
+  int ch, r_trunk, r_ts, fct, bnt, nseg, off_fc1, off_fct, off_bnt;
+};
+__host__ __device__ constexpr SegLayout seg_layout(int ch) {
+  return SegLayout{ch,
+                   WSLAB_N / ch,
+                   WSLAB_N / ch + (SSLAB_N + ch - 1) / ch,
+                   WSLAB_N / ch + (SSLAB_N + ch - 1) / ch + R_FC1,
+                   WSLAB_N / ch + (SSLAB_N + ch - 1) / ch + R_FC1 + 1,
+                   WSLAB_N / ch + (SSLAB_N + ch - 1) / ch + R_FC1 + 2,
+                   (WSLAB_N / ch + (SSLAB_N + ch - 1) / ch) * ch,
+                   (WSLAB_N / ch + (SSLAB_N + ch - 1) / ch) * ch + R_FC1 * 1024,
+                   (WSLAB_N / ch + (SSLAB_N + ch - 1) / ch) * ch + R_FC1 * 1024 + FCT_LEN};
+}
+static_assert(WSLAB_N % 256 == 0, "trunk slab splits into whole chunks");
+static_assert(seg_layout(64).nseg == NSEG_MAX && seg_layout(256).nseg <= NSEG_MAX, "flag stride");
+static_assert((size_t)NSEG_MAX * xg::MAXR * 4 <= xg::FLAG_BYTES, "one flag per segment and rank");
+static_assert(seg_layout(64).off_bnt + BNT_LEN >= FLAT_N && seg_layout(256).off_bnt + BNT_LEN >= FLAT_N &&
+                  seg_layout(256).off_bnt + BNT_LEN <= (int)xg::SLAB_FLOATS,
+              "segments cover the flat buffer (self-test) and fit one slab");
+__device__ __forceinline__ int seg_off(const SegLayout& G, int b) {
+  return b < G.r_ts ? b * G.ch : b < G.fct ? G.off_fc1 + (b - G.r_ts) * 1024 : b == G.fct ? G.off_fct : G.off_bnt;
+}
+__device__ __forceinline__ int seg_len(const SegLayout& G, int b) {
+  return b < G.r_ts ? G.ch : b < G.fct ? 1024 : b == G.fct ? FCT_LEN : BNT_LEN;
+}
+
+struct RedAr {
+  xg::Peers peers;            // every rank's IPC region; the segments use its SECOND half (xg::REGION_BYTES on)
+  unsigned* err;              // bit 31: a peer wait expired
+  unsigned long long deadline;  // s_memrealtime ticks
+  const float* st_src;        // mode 3: the pattern (st_n floats, slab offsets)
+  float* st_dst;
+  int st_n;
+  int mode;
+  int fc_in_step;             // the fc1 / fc-tail segments run on the step kernel's fc workers
+  int seg_ch;                 // segment layout (seg_layout): 64 or 256
+};
+
+__device__ __forceinline__ char* rbase(const RedAr& ra, int q) { return ra.peers.base[q] + xg::REGION_BYTES; }
+__device__ __forceinline__ float* rslab(const RedAr& ra, int q, int par) {
+  return (float*)(rbase(ra, q) + xg::FLAG_BYTES) + (size_t)par * xg::SLAB_FLOATS;
+}
+
+// one-shot exchange of segment b (segv[0 .. len), len % 4 == 0) with every peer; on return segv holds the sum
+// ep0: this segment's last epoch (own flag), loaded by the caller early so its latency hides under the reduction
+// (thread 0's value; broadcast here through *s_ep)
+template <int NTH>
+__device__ void seg_exchange(const Ctx& cx, const RedAr& ra, int b, float* segv, int len, int off, int ep0, int* s_ep) {
+  const int t = threadIdx.x, W = cx.ws, me = cx.rank;
+  int* myflags = (int*)rbase(ra, me);
+  const unsigned long long t_in = __builtin_amdgcn_s_memrealtime();
+  if (t == 0) *s_ep = ep0 + 1;
+  __syncthreads();
+  const int ep = *s_ep, par = ep & 1;
+  constexpr int SYS = 17;  // sc0 | sc1: write-through store / cache-bypassing load
+  const __amdgpu_buffer_rsrc_t mine =
+      __builtin_amdgcn_make_buffer_rsrc(rslab(ra, me, par), (short)0, (int)(xg::SLAB_FLOATS * 4), 0x00020000);
+  for (int k = 4 * t; k < len; k += 4 * NTH)
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(xg::v4u, *(const f32x4*)(segv + k)), mine,
+                                           4 * (off + k), 0, SYS);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this thread's slab stores are performed
+  __syncthreads();                                    // ... and every thread's
+  if (t < W) xg::flag_store((int*)rbase(ra, t) + me * NSEG_MAX + b, ep);
+  if (t < W) {
+    const int* f = myflags + t * NSEG_MAX + b;
+    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+    while (xg::flag_load(f) < ep) {
+      __builtin_amdgcn_s_sleep(1);
+      if (__builtin_amdgcn_s_memrealtime() - t0 > ra.deadline) {
+        atomicOr(ra.err, 0x80000000u);
+        break;
+      }
+    }
+  }
+  __syncthreads();
+  if (t == 0 && b < seg_layout(ra.seg_ch).r_ts && ra.peers.ticks != nullptr) {  // exposed exchange wait, summed over the segments the
+    atomicAdd(ra.peers.ticks, __builtin_amdgcn_s_memrealtime() - t_in);  // reduction kernel exchanges (metrics)
+    if (b == 0) atomicAdd(ra.peers.ticks + 1, 1ull);
+  }
+  for (int k = 4 * t; k < len; k += 4 * NTH) {  // exactly W loads in flight, one per peer link (rank_sum.h)
+    *(f32x4*)(segv + k) = rank_sum(W, [&](int q) {
+      const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(rslab(ra, q, par), (short)0,
+                                                                          (int)(xg::SLAB_FLOATS * 4), 0x00020000);
+      return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, 4 * (off + k), 0, SYS));
+    });
+  }
+  __syncthreads();
+}
+
+// parameter index of element k of segment b: >= 0 a parameter; -1 none; -2 - k: CC4 running-stat slot k
+__device__ __forceinline__ int seg_pidx(const SegLayout& G, int b, int k) {
+  if (b < G.r_ts) {  // slab fragment order
+    const bool stem = b >= G.r_trunk;
+    const int e = (stem ? b - G.r_trunk : b) * G.ch + k, ii = k & 3;
+    if (e >= (stem ? SSLAB_N : WSLAB_N)) return -1;
+    const int tt = e >> 8, ln = (e >> 2) & 63, mt = tt & 1, nt = tt >> 1;
+    if (!stem) return OFF_CONVW + (16 * mt + 4 * (ln >> 4) + ii) * 288 + (16 * (nt & 1) + (ln & 15)) * 9 + (nt >> 1);
+    if (e < 1024) {
+      const int kk = 16 * nt + (ln & 15);
+      return kk < 27 ? OFF_C1W + (16 * mt + 4 * (ln >> 4) + ii) * 27 + kk : -1;
+    }
+    return e < 1056 ? OFF_C1B + (e - 1024) : -1;
+  }
+  if (b < G.fct) {
+    const int fb = b - G.r_ts;  // fc1 block: features 64 (fb >> 1) .., rows 16 (fb & 1) ..
+    return OFF_FC1W + (16 * (fb & 1) + (k >> 6)) * 2048 + 64 * (fb >> 1) + (k & 63);
+  }
+  if (b == G.fct) {
+    if (k < 32) return OFF_FC1B + k;
+    if (k < 352) return OFF_FC2W + ((k - 32) >> 5) * 32 + ((k - 32) & 31);
+    return k < 362 ? OFF_FC2B + (k - 352) : -1;
+  }
+  return k < 64 ? (k < 32 ? OFF_BNW : OFF_BNB) + (k & 31) : -2 - (k - 64);
+}
+
+// 16-B load bypassing L1 (sc1): the head outputs are read by the fc workers inside the launch that writes them
+__device__ __forceinline__ f32x4 ld4_sc1(const float* base, int bytes, int off_floats) {
+  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)base, (short)0, bytes, 0x00020000);
+  return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, 4 * off_floats, 0, 16));
+}
+
+// trunk / stem chunk b of CH outputs in slab fragment order, summed over the nslab workgroup slabs: thread (grp,
+// slot) sums float4 `slot` of slabs grp, grp + NG, ... (all in flight for batch 32), fixed order
+template <int NTH, int CH>
+__device__ __forceinline__ void seg_chunk(const Ctx& cx, const Args& pa, const SegLayout& Ls, int b, int nslab,
+                                          float* segv, f32x4* red) {
+  constexpr int NS = CH / 4, NG = NTH / NS, NU = 128 / NG;
+  const int t = threadIdx.x;
+  const bool stem = b >= Ls.r_trunk;
+  const int chunk = stem ? b - Ls.r_trunk : b;
+  const int slot = t % NS, grp = t / NS, e0 = chunk * CH + slot * 4;
+  const float* src = stem ? cx.SSLAB : pa.tslab;
+  const int stride = stem ? SSLAB_N : WSLAB_N;
+  const int ec = e0 < stride ? e0 : stride - 4;  // conv1's last 256-chunk is partial (1088 = 4.25 x 256)
+  f32x4 sacc = z4();
+  for (int k0 = 0; k0 < nslab; k0 += 128) {
+    f32x4 v[NU];
+#pragma unroll
+    for (int u = 0; u < NU; ++u) {
+      const int k = k0 + grp + NG * u;
+      v[u] = ld4(src + (size_t)(k < nslab ? k : nslab - 1) * stride + ec);
+    }
+#pragma unroll
+    for (int u = 0; u < NU; ++u)
+      if (k0 + grp + NG * u < nslab) sacc += v[u];
+  }
+  red[t] = sacc;
+  __syncthreads();
+  if (t < NS) {
+    f32x4 tot = red[t];
+#pragma unroll
+    for (int g = 1; g < NG; ++g) tot += red[NS * g + t];
+    *(f32x4*)(segv + slot * 4) = e0 < stride ? tot : z4();
+  }
+}
+
+// Segment b on this workgroup (NTH threads): reduce / compute into segv, exchange (mode 2), SGD.  LDS: segv
+// [SEG_MAX], red [NTH] f32x4, stage [64 * 32 + 64 * 64] floats, *s_ep.
+template <int NTH>
+__device__ void seg_process(const Ctx& cx, const Args& pa, const RedAr& ra, int b, int nslab, float* segv,
+                            f32x4* red, float* stage, int* s_ep, int sslot, int swg) {
+  const int t = threadIdx.x, B = cx.B;
+  const int mode = ra.mode;
+  const SegLayout Ls = seg_layout(ra.seg_ch);
+  const int len = seg_len(Ls, b), off = seg_off(Ls, b);
+  // this segment's exchange epoch (own flag), and this thread's SGD elements (k = t + NTH i): parameter indices
+  // and old values, loaded first so their latency hides under the reduction
+  const int ep0 = mode >= 2 && t == 0 ? xg::flag_load((const int*)rbase(ra, cx.rank) + cx.rank * NSEG_MAX + b) : 0;
+  constexpr int KMAX = SEG_MAX / NTH;
+  int pid[KMAX];
+  float pold[KMAX];
+#pragma unroll
+  for (int i = 0; i < KMAX; ++i) {
+    const int k = t + NTH * i;
+    pid[i] = k < len && mode != 3 ? seg_pidx(Ls, b, k) : -1;
+    pold[i] = cx.params[pid[i] >= 0 ? pid[i] : 0];
+  }
+  if (mode == 3) {
+    for (int k = t; k < len; k += NTH) segv[k] = off + k < ra.st_n ? ra.st_src[off + k] : 0.f;
+  } else if (b < Ls.r_ts) {
+    if (Ls.ch == 64) seg_chunk<NTH, 64>(cx, pa, Ls, b, nslab, segv, red);
+    else seg_chunk<NTH, 256>(cx, pa, Ls, b, nslab, segv, red);
+  } else if (b < Ls.fct) {
+    // fc1 block: dW1[j][64f + kk .. +3] = sum_b dh[b][j] p[b][64f + kk ..], rows j = 16 h .. 16 h + 15
+    const int fb = b - Ls.r_ts, f = fb >> 1, j0 = 16 * (fb & 1);
+    float* dh_s = stage;           // [B][32]
+    float* p_s = stage + 64 * 32;  // [B][64]
+    constexpr int MD = (64 * 8 + NTH - 1) / NTH, MP = (64 * 16 + NTH - 1) / NTH;
+    f32x4 dh4[MD], p4[MP];
+#pragma unroll
+    for (int m = 0; m < MD; ++m) {
+      const int idx = t + NTH * m;
+      dh4[m] = ld4_sc1(cx.HDH, 64 * 32 * 4, 4 * (idx < B * 8 ? idx : 0));
+    }
+#pragma unroll
+    for (int m = 0; m < MP; ++m) {
+      const int idx = t + NTH * m, ic = idx < B * 16 ? idx : 0, bb = ic >> 4, k4 = ic & 15;
+      p4[m] = ld4_sc1(cx.HP, 64 * 2048 * 4, bb * 2048 + 64 * f + 4 * k4);
+    }
+#pragma unroll
+    for (int m = 0; m < MD; ++m)
+      if (t + NTH * m < B * 8) st4(dh_s + 4 * (t + NTH * m), dh4[m]);
+#pragma unroll
+    for (int m = 0; m < MP; ++m)
+      if (t + NTH * m < B * 16) st4(p_s + 4 * (t + NTH * m), p4[m]);
+    __syncthreads();
+    if (t < 256) {
+      const int jl = t >> 4, kk = 4 * (t & 15);
+      f32x4 a0 = z4();
+#pragma unroll 8
+      for (int bb = 0; bb < B; ++bb) a0 += dh_s[bb * 32 + j0 + jl] * ld4(p_s + bb * 64 + kk);
+      st4(segv + jl * 64 + kk, a0);
+    }
+  } else if (b == Ls.fct) {
+    // fc tail: fc1 bias [0,32), fc2 weight [32,352), fc2 bias [352,362), pad
+    float* hh_s = stage;            // [B][32]
+    float* dl_s = stage + 64 * 32;  // [B][16]
+    float* dh_s = dl_s + 64 * 16;   // [B][32]
+    for (int idx = t; idx < B * 8; idx += NTH) {
+      st4(hh_s + 4 * idx, ld4_sc1(cx.HH, 64 * 32 * 4, 4 * idx));
+      st4(dh_s + 4 * idx, ld4_sc1(cx.HDH, 64 * 32 * 4, 4 * idx));
+    }
+    for (int idx = t; idx < B * 10; idx += NTH) {
+      const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)cx.HDL, (short)0, 64 * 16 * 4, 0x00020000);
+      dl_s[(idx / 10) * 16 + idx % 10] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs, 4 * idx, 0, 16));
+    }
+    __syncthreads();
+    for (int idx = t; idx < FCT_LEN; idx += NTH) {  // (parameter indices: seg_pidx)
+      float sv = 0.f;
+      if (idx < 32) {
+#pragma unroll 8
+        for (int bb = 0; bb < B; ++bb) sv += dh_s[bb * 32 + idx];
+      } else if (idx < 352) {
+        const int o = (idx - 32) >> 5, jj = (idx - 32) & 31;
+#pragma unroll 8
+        for (int bb = 0; bb < B; ++bb) sv += dl_s[bb * 16 + o] * hh_s[bb * 32 + jj];
+      } else if (idx < 362) {
+        const int o = idx - 352;
+#pragma unroll 8
+        for (int bb = 0; bb < B; ++bb) sv += dl_s[bb * 16 + o];
+      }
+      segv[idx] = sv;
+    }
+  } else {
+    // BN tail: gamma | beta gradients [0, 64), CC4 running mean | var [64, 128) (rank 0's buffers; others 0)
+    for (int idx = t; idx < BNT_LEN; idx += NTH) {
+      float sv;
+      if (idx < 64) {
+        sv = pa.bng[idx];
+      } else {
+        const int k = idx - 64;
+        sv = cx.rank == 0 ? (k < 32 ? cx.rm[k] : cx.rv[k - 32]) : 0.f;
+      }
+      segv[idx] = sv;
+    }
+  }
+  __syncthreads();
+  DCA_STAMP(cx, sslot, swg, 1);
+  if (mode >= 2) seg_exchange<NTH>(cx, ra, b, segv, len, off, ep0, s_ep);
+  DCA_STAMP(cx, sslot, swg, 2);
+#pragma unroll
+  for (int i = 0; i < KMAX; ++i) {
+    const int k = t + NTH * i;
+    if (k >= len) break;
+    const int pidx = pid[i];
+    const float g = segv[k];
+    if (mode == 3) {
+      if (off + k < ra.st_n) ra.st_dst[off + k] = g;
+      continue;
+    }
+    if (pidx >= 0) {
+      cx.grads[pidx] = g;
+      if (mode == 1) continue;
+      const float oldp = pold[i];
+      float wv;
+      if (mode == 0) {
+        wv = __builtin_fmaf(-cx.lr, g, oldp);
+      } else {
+        wv = oldp;
+        wv -= cx.lr * g * cx.inv_ws;  // same rounding as k_apply_sgd / k_xgmi_ar_sgd
+      }
+      cx.params[pidx] = wv;
+      derive_param<true>(cx, pidx, wv);
+    } else if (pidx <= -2) {  // CC4: rank 0's running stats become every rank's base (rides the all-reduce)
+      const int kk = -2 - pidx;
+      if (mode == 1) cx.grads[OFF_RS + kk] = g;
+      else if (mode == 2) cx.rs_base[kk] = g;
+    }
+  }
+  DCA_STAMP(cx, sslot, swg, 3);
+}
+
+// fc worker fb (0 .. R_FC1 - 1: fc1 block fb; R_FC1: fc tail) of the step kernel: waits until every main workgroup
+// has published its head-done granule (its pooled features HP and, slice 0, the image's dh / h / dlogits are
+// written through and drained), then runs the segment (compute, xGMI exchange, SGD) beside the trunk backward.
+template <int P>
+__device__ void fc_worker(const Ctx& cx, const Args& pa, const RedAr& ra, int fb, char* smem) {
+  const int t = threadIdx.x, lane = t & 63, G = cx.B * S;
+  const int epoch = *pa.epoch;
+  DCA_STAMP(cx, 9, fb, 0);
+  if (t < 64) {  // ONE wave polls (sleeping between passes): the CU's other work is the step's, on other CUs
+    const unsigned tag = tagof(epoch, RND_HDONE);
+    for (unsigned spins = 0;; ++spins) {
+      bool ok = true;
+      for (int k = lane; k < G; k += 64)
+        ok &= (unsigned)(__hip_atomic_load(pa.hdone + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >> 32) == tag;
+      if (__all(ok)) break;
+      if (spins >= SPIN_LIMIT) {
+        if (lane == 0) atomicOr(pa.err, 1u << 30);
+        break;
+      }
+      __builtin_amdgcn_s_sleep(8);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  __syncthreads();
+  float* segv = (float*)smem;
+  f32x4* red = (f32x4*)(smem + SEG_MAX * 4);
+  float* stage = (float*)(smem + SEG_MAX * 4 + NTH * 16);
+  int* s_ep = (int*)(smem + SEG_MAX * 4 + NTH * 16 + (64 * 32 + 64 * 64) * 4);
+  const SegLayout Ls = seg_layout(ra.seg_ch);
+  seg_process<NTH>(cx, pa, ra, fb < R_FC1 ? Ls.r_ts + fb : Ls.fct, G, segv, red, stage, s_ep, 9, fb);
+}
+
 constexpr int P_KSHIFT = 906;  // misc: [10][32] BN shifts (last step's batch means)
 constexpr int P_LABEL = 1240;  // misc: this image's label
 
 // ============================================================================================================
 template <int P>
-__global__ void __launch_bounds__(NTH) k_pks_step(Ctx cx, Args pa) {
+__global__ void __launch_bounds__(NTH) k_pks_step(Ctx cx, Args pa, RedAr ra) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   using PL = Plan<P>;
+  {  // workgroups past the main grid are the fc workers (only launched with ra.fc_in_step)
+    const int gmain = (cx.B + 7) / 8 * 8 * S;
+    if ((int)blockIdx.x >= gmain) {
+      fc_worker<P>(cx, pa, ra, (int)blockIdx.x - gmain, smem);
+      return;
+    }
+  }
   const int t = threadIdx.x, wv = t >> 6, lane = t & 63, c = lane & 15, q = lane >> 4;
   const int w = wv & (RS - 1), hh = wv / RS, ch = 16 * hh + c;  // image row (in the slice), channel half, channel
   // Placement (speed only, never correctness): blocks b and b + 8 share an XCD under the observed round-robin
@@ -833,7 +1202,7 @@ __global__ void __launch_bounds__(NTH) k_pks_step(Ctx cx, Args pa) {
       }
       *(float2*)(pl + 2 * t) = make_float2(pv[0], pv[1]);
       // fc1 input for the weight gradient: global feature ch*64 + (2s + pr)*8 + pc
-      *(float2*)(cx.HP + (size_t)n * 2048 + pch * 64 + (2 * s + pr) * 8 + 2 * (t & 3)) = make_float2(pv[0], pv[1]);
+      st2_wt(cx.HP + (size_t)n * 2048 + pch * 64 + (2 * s + pr) * 8 + 2 * (t & 3), pv[0], pv[1]);
     }
     lds_barrier();
     // block 9's y for the first backward block, loaded now: the fc1 partial below hides the latency (the head
@@ -922,13 +1291,13 @@ __global__ void __launch_bounds__(NTH) k_pks_step(Ctx cx, Args pa) {
       }
       const float dh = hsum > 0.f ? sd : 0.f;
       if (lane < 32) hp[32 + lane] = dh;
-      if (s == 0) {
-        if (lane == 0) cx.HLOSS[n] = lse - lt;
+      if (s == 0) {  // write-through (sc1): the fc workers read them inside this launch
+        if (lane == 0) st1_wt(cx.HLOSS + n, lse - lt);
         if (lane < 32) {
-          cx.HDH[n * 32 + lane] = dh;
-          cx.HH[n * 32 + lane] = hr;
+          st1_wt(cx.HDH + n * 32 + lane, dh);
+          st1_wt(cx.HH + n * 32 + lane, hr);
         }
-        if (lane < 10) cx.HDL[n * 10 + lane] = dl;
+        if (lane < 10) st1_wt(cx.HDL + n * 10 + lane, dl);
       }
     }
     lds_barrier();
@@ -1027,6 +1396,9 @@ __global__ void __launch_bounds__(NTH) k_pks_step(Ctx cx, Args pa) {
     }
     if (halo && i > 0) ld4r(pa.yh + ((size_t)((i - 1) * LMAX + L) * 2 + hwhich) * 512, hh, lane, yo);
     lds_barrier();
+    // head outputs done: every wave's head stores (write-through) were retired by its sweep's waits (vmcnt counts
+    // stores and loads in order) before this barrier -> one granule releases the fc workers
+    if (i == NBLK - 1 && ra.fc_in_step && t == 0) gput(pa.hdone + L, tagof(epoch, RND_HDONE), 0.f);
     if (i == DCA_DETAIL_BWD) DCA_STAMP(cx, 7, L, 5);
     if (L == 0 && t < 32) {  // BN affine gradients: dbeta = sum dz, dgamma = sum dz * xhat
       dbet += slot_total(cred, t);
@@ -1190,122 +1562,11 @@ __global__ void __launch_bounds__(256) k_pks_prime(Ctx cx, Args pa) {
 }
 
 // ============================================================================================================
-// Reduction + gradient all-reduce + SGD in ONE kernel (sliced engine).  Every workgroup owns one segment of the
-// gradient: a chunk of the trunk conv (36 x 256, slab fragment order), of conv1 (5 x 256), a 64-column block
-// of fc1 (32 x 2048) or the small tail (fc1 / fc2 biases, fc2 weight, BN affine, the CC4 running-stat segment;
-// 492 floats).  It reduces its segment over the B x S workgroup slabs (deterministic order), then
-//   mode 0 (world size 1): SGD, fused;
-//   mode 1 (RCCL): writes the gradient only (ncclAllReduce + k_apply_sgd follow in the graph);
-//   mode 2 (xGMI): exchanges THIS segment one-shot with the peers (write-through slab + per-segment flags in the
-//     second half of every rank's IPC region, peers read all W slabs, sum in rank order -- bitwise identical on
-//     every rank), then the averaging SGD: 106 concurrent small all-reduces instead of one all-reduce launch after
-//     the reduction (reference: DDP's single NCCL bucket after the whole backward, main.py:63);
-//   mode 3: the same exchange on a caller pattern (collective self-test of this path).
-// Memory ordering as in xgmi_allreduce.hip (system-coherent stores to uncached memory, s_waitcnt vmcnt(0) +
-// barrier before the flag, cache-bypassing loads; per-segment epochs, slab parity = epoch & 1).
+// The reduction kernel after the step: the trunk / conv1 chunks and the BN tail (plus the fc1 blocks and the fc
+// tail when the step kernel did not run them), each followed by its exchange and SGD; one more workgroup does the
+// step's bookkeeping.  mode 3 (self-test): every segment, no bookkeeping.
 // ============================================================================================================
-// segments: 36 trunk + 5 stem chunks of 256, fc1 as 64 blocks of 16 rows x 64 features (1024), one small tail.
-// 106 workgroups: each reads one float4 per peer per thread at most (one round of xGMI loads in flight)
-constexpr int R_TRUNK = 36, R_STEM = 5, R_FC1 = 64;  // segments: trunk / stem chunks of 256, fc1 blocks of 1024
-constexpr int NSEG = R_TRUNK + R_STEM + R_FC1 + 1;  // 106
-constexpr int SEG_SMALL_LEN = 492;                         // 32 + 320 + 10 + 64 + 64 (+2 pad)
-constexpr int SEG_MAX = 1024;
-static_assert((size_t)NSEG * xg::MAXR * 4 <= xg::FLAG_BYTES, "one flag per segment and rank");
-__device__ __forceinline__ int seg_off(int b) {
-  return b < 36 ? b * 256 : b < 41 ? 9216 + (b - 36) * 256 : b < 105 ? 10496 + (b - 41) * 1024 : 76032;
-}
-__device__ __forceinline__ int seg_len(int b) { return b < 41 ? 256 : b < 105 ? 1024 : SEG_SMALL_LEN; }
-static_assert(76032 + SEG_SMALL_LEN <= (int)xg::SLAB_FLOATS, "segments fit one slab");
-
-struct RedAr {
-  xg::Peers peers;            // every rank's IPC region; this kernel uses its SECOND half (xg::REGION_BYTES on)
-  unsigned* err;              // bit 31: a peer wait expired
-  unsigned long long deadline;  // s_memrealtime ticks
-  const float* st_src;        // mode 3: the pattern (st_n floats, slab offsets)
-  float* st_dst;
-  int st_n;
-  int mode;
-};
-
-__device__ __forceinline__ char* rbase(const RedAr& ra, int q) { return ra.peers.base[q] + xg::REGION_BYTES; }
-__device__ __forceinline__ float* rslab(const RedAr& ra, int q, int par) {
-  return (float*)(rbase(ra, q) + xg::FLAG_BYTES) + (size_t)par * xg::SLAB_FLOATS;
-}
-
-// one-shot exchange of segment b (segv[0 .. len), len % 4 == 0) with every peer; on return segv holds the sum
-// ep0: this segment's last epoch (own flag), loaded by the caller at kernel start so its latency hides under the
-// reduction (thread 0's value; broadcast here)
-__device__ void seg_exchange(const Ctx& cx, const RedAr& ra, int b, float* segv, int len, int off, int ep0) {
-  const int t = threadIdx.x, W = cx.ws, me = cx.rank;
-  int* myflags = (int*)rbase(ra, me);
-  __shared__ int s_ep;
-  const unsigned long long t_in = __builtin_amdgcn_s_memrealtime();
-  if (t == 0) s_ep = ep0 + 1;
-  __syncthreads();
-  const int ep = s_ep, par = ep & 1;
-  constexpr int SYS = 17;  // sc0 | sc1: write-through store / cache-bypassing load
-  const __amdgpu_buffer_rsrc_t mine =
-      __builtin_amdgcn_make_buffer_rsrc(rslab(ra, me, par), (short)0, (int)(xg::SLAB_FLOATS * 4), 0x00020000);
-  for (int k = 4 * t; k < len; k += 1024)
-    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(xg::v4u, *(const f32x4*)(segv + k)), mine,
-                                           4 * (off + k), 0, SYS);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this thread's slab stores are performed
-  __syncthreads();                                    // ... and every thread's
-  if (t < W) xg::flag_store((int*)rbase(ra, t) + me * NSEG + b, ep);
-  if (t < W) {
-    const int* f = myflags + t * NSEG + b;
-    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
-    while (xg::flag_load(f) < ep) {
-      __builtin_amdgcn_s_sleep(1);
-      if (__builtin_amdgcn_s_memrealtime() - t0 > ra.deadline) {
-        atomicOr(ra.err, 0x80000000u);
-        break;
-      }
-    }
-  }
-  __syncthreads();
-  if (b == 0 && t == 0 && ra.peers.ticks != nullptr) {  // exposed all-reduce time of this rank (metrics)
-    atomicAdd(ra.peers.ticks, __builtin_amdgcn_s_memrealtime() - t_in);
-    atomicAdd(ra.peers.ticks + 1, 1ull);
-  }
-  for (int k = 4 * t; k < len; k += 1024) {  // exactly W loads in flight, one per peer link (rank_sum.h)
-    *(f32x4*)(segv + k) = rank_sum(W, [&](int q) {
-      const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(rslab(ra, q, par), (short)0,
-                                                                          (int)(xg::SLAB_FLOATS * 4), 0x00020000);
-      return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, 4 * (off + k), 0, SYS));
-    });
-  }
-  __syncthreads();
-}
-
-// parameter index of element k of segment b: >= 0 a parameter; -1 none; -2 - k: CC4 running-stat slot k
-__device__ __forceinline__ int seg_pidx(const Ctx& cx, int b, int k) {
-  if (b < R_TRUNK + R_STEM) {  // slab fragment order
-    const bool stem = b >= R_TRUNK;
-    const int e = (stem ? b - R_TRUNK : b) * 256 + k, ii = k & 3;
-    if (e >= (stem ? SSLAB_N : WSLAB_N)) return -1;
-    const int tt = e >> 8, ln = (e >> 2) & 63, mt = tt & 1, nt = tt >> 1;
-    if (!stem) return OFF_CONVW + (16 * mt + 4 * (ln >> 4) + ii) * 288 + (16 * (nt & 1) + (ln & 15)) * 9 + (nt >> 1);
-    if (e < 1024) {
-      const int kk = 16 * nt + (ln & 15);
-      return kk < 27 ? OFF_C1W + (16 * mt + 4 * (ln >> 4) + ii) * 27 + kk : -1;
-    }
-    return e < 1056 ? OFF_C1B + (e - 1024) : -1;
-  }
-  if (b < NSEG - 1) {
-    const int fb = b - R_TRUNK - R_STEM;  // fc1 block: features 64 (fb >> 1) .., rows 16 (fb & 1) ..
-    return OFF_FC1W + (16 * (fb & 1) + (k >> 6)) * 2048 + 64 * (fb >> 1) + (k & 63);
-  }
-  if (k < 32) return OFF_FC1B + k;
-  if (k < 352) return OFF_FC2W + ((k - 32) >> 5) * 32 + ((k - 32) & 31);
-  if (k < 362) return OFF_FC2B + (k - 352);
-  if (k < 426) return ((k - 362) < 32 ? OFF_BNW : OFF_BNB) + ((k - 362) & 31);
-  if (k < 490) return -2 - (k - 426);
-  return -1;
-}
-
-// Grid NSEG + 1: workgroup NSEG is the step's bookkeeping (batch-mean loss, cursor, step / BN-batch counters,
-// epoch), independent of every segment, so it runs beside them instead of after the tail segment's work.
+// batch-mean loss, cursor, step / BN-batch counters, epoch: independent of every segment, so it runs beside them
 __device__ __forceinline__ void pks_bookkeeping(const Ctx& cx, const Args& pa) {
   const int t = threadIdx.x, B = cx.B;
   if (t >= 64) return;
@@ -1331,156 +1592,24 @@ __device__ __forceinline__ void pks_bookkeeping(const Ctx& cx, const Args& pa) {
   }
 }
 
+// grid: reduce_grid(ra) + 1
+__host__ __device__ inline int reduce_segments(int fc_in_step, int seg_ch) {
+  return fc_in_step ? seg_layout(seg_ch).r_ts + 1 : seg_layout(seg_ch).nseg;
+}
+
 __global__ void __launch_bounds__(256) k_pks_reduce_ar(Ctx cx, Args pa, int nslab, RedAr ra) {
   __shared__ __attribute__((aligned(16))) float segv[SEG_MAX];
   __shared__ f32x4 red[256];
   __shared__ float stage[64 * 32 + 64 * 64];
-  const int b = blockIdx.x, t = threadIdx.x, B = cx.B;
-  const int mode = ra.mode;
-  if (b == NSEG) {
-    if (mode != 3) pks_bookkeeping(cx, pa);
+  __shared__ int s_ep;
+  const int nred = reduce_segments(ra.fc_in_step, ra.seg_ch), b = blockIdx.x;
+  if (b >= nred) {
+    if (ra.mode != 3) pks_bookkeeping(cx, pa);
     return;
   }
-  const int len = seg_len(b), off = seg_off(b);
+  const int seg = !ra.fc_in_step || b < seg_layout(ra.seg_ch).r_ts ? b : seg_layout(ra.seg_ch).bnt;
   DCA_STAMP(cx, 8, b, 0);
-  // this thread's SGD elements (k = t + 256 i): parameter indices and old values loaded first, so their latency
-  // hides under the slab reduction (a dependent read after it cost 1.5 us per step)
-  // this segment's exchange epoch (own flag), loaded now: the latency of the uncached read hides under the reduction
-  const int ep0 = mode >= 2 && t == 0 ? xg::flag_load((const int*)rbase(ra, cx.rank) + cx.rank * NSEG + b) : 0;
-  constexpr int KMAX = SEG_MAX / 256;
-  int pid[KMAX];
-  float pold[KMAX];
-#pragma unroll
-  for (int i = 0; i < KMAX; ++i) {
-    const int k = t + 256 * i;
-    pid[i] = k < len && mode != 3 ? seg_pidx(cx, b, k) : -1;
-    pold[i] = cx.params[pid[i] >= 0 ? pid[i] : 0];
-  }
-  if (mode == 3) {
-    for (int k = t; k < len; k += 256) segv[k] = off + k < ra.st_n ? ra.st_src[off + k] : 0.f;
-  } else if (b < R_TRUNK + R_STEM) {
-    // trunk / stem chunk: 256 outputs in slab fragment order, summed over the nslab workgroup slabs
-    const bool stem = b >= R_TRUNK;
-    const int chunk = stem ? b - R_TRUNK : b;
-    const int slot = t & 63, grp = t >> 6, e0 = chunk * 256 + slot * 4;
-    const float* src = stem ? cx.SSLAB : pa.tslab;
-    const int stride = stem ? SSLAB_N : WSLAB_N, lim = stem ? SSLAB_N : WSLAB_N;
-    f32x4 sacc = z4();
-    const int ec = e0 < lim ? e0 : lim - 4;
-    for (int k0 = 0; k0 < nslab; k0 += 128) {  // 32 slabs per thread in flight (all of batch 32), fixed order
-      f32x4 v[32];
-#pragma unroll
-      for (int u = 0; u < 32; ++u) {
-        const int k = k0 + grp + 4 * u;
-        v[u] = ld4(src + (size_t)(k < nslab ? k : nslab - 1) * stride + ec);
-      }
-#pragma unroll
-      for (int u = 0; u < 32; ++u)
-        if (k0 + grp + 4 * u < nslab) sacc += v[u];
-    }
-    red[t] = sacc;
-    __syncthreads();
-    if (t < 64) {
-      const f32x4 tot = red[t] + red[64 + t] + red[128 + t] + red[192 + t];
-#pragma unroll
-      for (int ii = 0; ii < 4; ++ii) segv[slot * 4 + ii] = e0 + ii < lim ? tot[ii] : 0.f;
-    }
-  } else if (b < NSEG - 1) {
-    // fc1 block: dW1[j][64f + kk .. +3] = sum_b dh[b][j] p[b][64f + kk ..], rows j = 16 h .. 16 h + 15
-    const int fb = b - R_TRUNK - R_STEM, f = fb >> 1, j0 = 16 * (fb & 1);
-    float* dh_s = stage;           // [B][32]
-    float* p_s = stage + 64 * 32;  // [B][64]
-    const int jl = t >> 4, kk = 4 * (t & 15);
-    f32x4 dh4[2], p4[4];
-#pragma unroll
-    for (int m = 0; m < 2; ++m) {
-      const int idx = t + 256 * m;
-      dh4[m] = ld4(cx.HDH + 4 * (idx < B * 8 ? idx : 0));
-    }
-#pragma unroll
-    for (int m = 0; m < 4; ++m) {
-      const int idx = t + 256 * m, ic = idx < B * 16 ? idx : 0, bb = ic >> 4, k4 = ic & 15;
-      p4[m] = ld4(cx.HP + (size_t)bb * 2048 + 64 * f + 4 * k4);
-    }
-#pragma unroll
-    for (int m = 0; m < 2; ++m)
-      if (t + 256 * m < B * 8) st4(dh_s + 4 * (t + 256 * m), dh4[m]);
-#pragma unroll
-    for (int m = 0; m < 4; ++m)
-      if (t + 256 * m < B * 16) st4(p_s + 4 * (t + 256 * m), p4[m]);
-    __syncthreads();
-    f32x4 a0 = z4();
-#pragma unroll 8
-    for (int bb = 0; bb < B; ++bb) a0 += dh_s[bb * 32 + j0 + jl] * ld4(p_s + bb * 64 + kk);
-    st4(segv + jl * 64 + kk, a0);
-  } else {
-    // small tail: fc1 bias [0,32), fc2 weight [32,352), fc2 bias [352,362), BN gamma|beta [362,426),
-    // CC4 running mean|var [426,490) (rank 0's buffers; the others contribute 0), pad
-    float* hh_s = stage;            // [B][32]
-    float* dl_s = stage + 64 * 32;  // [B][16]
-    float* dh_s = dl_s + 64 * 16;   // [B][32]
-    for (int idx = t; idx < B * 32; idx += 256) {
-      hh_s[idx] = cx.HH[idx];
-      dh_s[idx] = cx.HDH[idx];
-    }
-    for (int idx = t; idx < B * 10; idx += 256) dl_s[(idx / 10) * 16 + idx % 10] = cx.HDL[idx];
-    __syncthreads();
-    for (int idx = t; idx < SEG_SMALL_LEN; idx += 256) {  // (parameter indices: seg_pidx)
-      float sv = 0.f;
-      if (idx < 32) {
-#pragma unroll 8
-        for (int bb = 0; bb < B; ++bb) sv += dh_s[bb * 32 + idx];
-      } else if (idx < 352) {
-        const int o = (idx - 32) >> 5, jj = (idx - 32) & 31;
-#pragma unroll 8
-        for (int bb = 0; bb < B; ++bb) sv += dl_s[bb * 16 + o] * hh_s[bb * 32 + jj];
-      } else if (idx < 362) {
-        const int o = idx - 352;
-#pragma unroll 8
-        for (int bb = 0; bb < B; ++bb) sv += dl_s[bb * 16 + o];
-      } else if (idx < 426) {
-        sv = pa.bng[idx - 362];  // 0..31 dgamma, 32..63 dbeta
-      } else if (idx < 490) {
-        const int k = idx - 426;
-        sv = cx.rank == 0 ? (k < 32 ? cx.rm[k] : cx.rv[k - 32]) : 0.f;
-      }
-      segv[idx] = sv;
-    }
-  }
-  __syncthreads();
-  DCA_STAMP(cx, 8, b, 1);
-  if (mode >= 2) seg_exchange(cx, ra, b, segv, len, off, ep0);
-  DCA_STAMP(cx, 8, b, 2);
-#pragma unroll
-  for (int i = 0; i < KMAX; ++i) {
-    const int k = t + 256 * i;
-    if (k >= len) break;
-    const int pidx = pid[i];
-    const float g = segv[k];
-    if (mode == 3) {
-      if (off + k < ra.st_n) ra.st_dst[off + k] = g;
-      continue;
-    }
-    if (pidx >= 0) {
-      cx.grads[pidx] = g;
-      if (mode == 1) continue;
-      const float oldp = pold[i];
-      float wv;
-      if (mode == 0) {
-        wv = __builtin_fmaf(-cx.lr, g, oldp);
-      } else {
-        wv = oldp;
-        wv -= cx.lr * g * cx.inv_ws;  // same rounding as k_apply_sgd / k_xgmi_ar_sgd
-      }
-      cx.params[pidx] = wv;
-      derive_param<true>(cx, pidx, wv);
-    } else if (pidx <= -2) {  // CC4: rank 0's running stats become every rank's base (rides the all-reduce)
-      const int kk = -2 - pidx;
-      if (mode == 1) cx.grads[OFF_RS + kk] = g;
-      else if (mode == 2) cx.rs_base[kk] = g;
-    }
-  }
-  DCA_STAMP(cx, 8, b, 3);
+  seg_process<256>(cx, pa, ra, seg, nslab, segv, red, stage, &s_ep, 8, b);
 }
 
 }  // namespace pks

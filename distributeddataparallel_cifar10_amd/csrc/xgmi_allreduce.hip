@@ -36,7 +36,7 @@ constexpr int MAXR = 8;                                  // ranks of one xGMI no
 constexpr int AR_T = 256;                                // threads per workgroup: one float4 each
 constexpr int AR_V4 = FLAT_N / 4;                        // 19035 float4 (FLAT_N is a multiple of 4)
 constexpr int AR_NB = (AR_V4 + AR_T - 1) / AR_T;         // 75 workgroups
-constexpr size_t FLAG_BYTES = 4096;                      // >= MAXR * AR_NB * 4
+constexpr size_t FLAG_BYTES = 8192;                      // >= MAXR * max(AR_NB, pks::NSEG) * 4
 constexpr size_t SLAB_FLOATS = (size_t)AR_NB * AR_T * 4;  // 76800 >= FLAT_N
 constexpr size_t REGION_BYTES = FLAG_BYTES + 2 * SLAB_FLOATS * 4;
 static_assert(MAXR * AR_NB * 4 <= (int)FLAG_BYTES, "flag area too small");

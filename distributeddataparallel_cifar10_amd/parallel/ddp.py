@@ -31,6 +31,14 @@ import torch.nn as nn
 from ..runtime.engine import EngineConfig, NetResDeepEngine, nccl_unique_id
 
 
+def _device_key(dev) -> str:
+    """Identity of the physical device (UUID when available), to detect ranks that share one GPU."""
+    try:
+        return str(torch.cuda.get_device_properties(dev).uuid)
+    except Exception:  # noqa: BLE001
+        return f"{os.uname().nodename}:{dev}"
+
+
 def broadcast_module_state(model: nn.Module, src: int = 0) -> None:
     """CC3: make every rank's parameters and buffers equal to rank `src`'s (reference DDP constructor)."""
     if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
@@ -85,6 +93,12 @@ class FusedDDPTrainer:
         handles = [None] * self.world_size
         dist.all_gather_object(handles, handle)
         ok = all(h is not None for h in handles)
+        # ranks sharing one device (the shared-GPU rehearsal): the step kernel's fc workers exchange with peers
+        # inside the step, so one rank's step could hold CUs another rank's step needs -> fc segments after the step
+        dev_ids = [None] * self.world_size
+        dist.all_gather_object(dev_ids, _device_key(data_u8.device))
+        if ok and eng is not None and len(set(dev_ids)) < len(dev_ids):
+            eng.set_shared_device(True)
         if ok:
             try:
                 eng.connect_peers(handles)

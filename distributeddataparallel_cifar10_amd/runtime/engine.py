@@ -192,6 +192,13 @@ class NetResDeepEngine:
         self.derive()
         self._n_indices = 0
 
+    def set_shared_device(self, shared: bool) -> None:
+        """Sliced engine, xGMI: peers share this device (shared-GPU rehearsal).  Then the fc gradient segments run
+        after the step (not on the step kernel's fc workers, which exchange with peers inside the step) and the
+        reduction grid stays small, so one rank's spinning kernels always leave CUs for a peer's step.  Every rank
+        must make the same call before stepping."""
+        native.check(self.lib.dca_engine_set_shared_device(self.h, 1 if shared else 0), "dca_engine_set_shared_device")
+
     # ---- state sync ---------------------------------------------------------------------------------------
     def derive(self):
         """Re-derive the kernel-layout weight copies after the fp32 params changed outside the engine."""

@@ -214,9 +214,14 @@ def train_loop(model, train_loader: DeviceLoader, rank: int, cfg: Optional[Train
         mean = loss_sum / n_batches  # reference divides by len(train_loader) (main.py:44)
         history.append(mean)
         comm_us, comm_n = _comm_time(model) if cfg.metrics_json else (0.0, 0)
+        eng = getattr(model, "engine", None)
         mlog.write(epoch=epoch, loss=mean, steps=nsteps, seconds=dt, step_ms=1e3 * dt / max(nsteps, 1),
                    images_per_sec=nsteps * train_loader.batch_size / max(dt, 1e-9),
-                   allreduce_us_per_step=(comm_us / comm_n) if comm_n else None)
+                   # exposed wait of the reduction kernel's gradient-segment exchanges, summed per step (xGMI)
+                   allreduce_us_per_step=(comm_us / comm_n) if comm_n else None,
+                   engine=getattr(eng, "kind_name", cfg.engine if not fused else None),
+                   dtype=cfg.dtype, fp32_mode=("3xbf16" if getattr(eng, "kind_name", "") == "sliced" else
+                                               "fp32-mfma") if cfg.dtype == "fp32" and fused else None)
         if should_log(epoch):
             print(epoch_line(epoch, mean), flush=True)
             if cfg.checkpoint:

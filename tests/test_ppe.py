@@ -108,7 +108,12 @@ def test_train_eval_kfold_pregenerate(tmp_path):
     j = json.load(open(tmp_path / "p.json"))
     k = next(iter(j))
     assert len(j[k]["bboxes"]) == len(j[k]["scores"]) and len(j[k]["scores"][0]) == 3
-    assert {v for row in j[k]["scores"] for v in row} <= {0, 1}  # reference: 0/1 decisions on raw logits
+    # reference: pred.astype(np.float) of the raw-logit decisions -> 0.0 / 1.0 floats, no "probs" key
+    assert {v for row in j[k]["scores"] for v in row} <= {0.0, 1.0}
+    assert all(isinstance(v, float) for row in j[k]["scores"] for v in row) and "probs" not in j[k]
+    out = ppe.pre_generate_labels(model, ppe.SyntheticPPE(2, seed=3), str(tmp_path / "run" / "model-ep0.pth"),
+                                  out_dir=str(tmp_path / "out2"), json_path=str(tmp_path / "p2.json"), with_probs=True)
+    j = json.load(open(tmp_path / "p2.json"))
     assert len(j[k]["probs"]) == len(j[k]["scores"])
 
 
