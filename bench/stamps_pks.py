@@ -49,7 +49,7 @@ def main():
     seq += [(f"fwd{i}", (1 + i // 8, i % 8)) for i in range(10)]
     seq += [("head.fc1part", (3, 1)), ("head.xchg", (3, 2)), ("head.ce", (3, 3)), ("head.end", (3, 0))]
     seq += [(f"bwd{9 - k}", (4 + k // 8, k % 8)) for k in range(10)]
-    seq += [("end", (5, 7))]
+    seq += [("end.wgrad0", (5, 2)), ("end.stem_staged", (5, 3)), ("end.stem_wgrad", (5, 4)), ("end", (5, 7))]
     prev = None
     total = 0.0
     for name, (sl, k) in seq:

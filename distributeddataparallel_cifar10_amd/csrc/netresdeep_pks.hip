@@ -263,23 +263,6 @@ __device__ __forceinline__ void publish_row(const Args& pa, int round, int L, in
     __builtin_amdgcn_raw_buffer_store_b128(x, rs, base + 2 * p * 8, 0, 16);
   }
 }
-// one poll pass over the 4 granules of a neighbour's boundary row this lane needs; true when all carry `tag`
-__device__ __forceinline__ bool poll_row(const Args& pa, int round, int Lsrc, int which, int h, unsigned tag,
-                                         float (&v)[4], int lane) {
-  const __amdgpu_buffer_rsrc_t rs = grsrc(pa, round);
-  const int base = (Lsrc * GSTR + 64 + which * 512 + h * 256 + lane * 4) * 8;
-  v4u x[2];
-#pragma unroll
-  for (int p = 0; p < 2; ++p) x[p] = __builtin_amdgcn_raw_buffer_load_b128(rs, base + 2 * p * 8, 0, 16);
-  bool ok = true;
-#pragma unroll
-  for (int p = 0; p < 2; ++p) {
-    ok &= x[p][1] == tag && x[p][3] == tag;
-    v[2 * p] = __uint_as_float(x[p][0]);
-    v[2 * p + 1] = __uint_as_float(x[p][2]);
-  }
-  return ok;
-}
 
 // BatchNorm partials travel as 4-byte self-tagged fp32 values: the 2 low mantissa bits of every value carry the
 // tag (a <= 3 ulp perturbation of a partial sum, identical for every reader), so one 16-B sc1 load returns four
@@ -304,21 +287,31 @@ __device__ __forceinline__ void bn_put(const Args& pa, int rnd, int L, int slot,
 __device__ __forceinline__ void sleep_units(int n) {
   for (int k = 0; k < n; ++k) __builtin_amdgcn_s_sleep(1);  // 64 cycles each
 }
+// Halo waves poll the neighbour slice's boundary row (2 x 16-B sc1 loads of {value, tag} granules) in the SAME
+// passes (need bit 8 .. 9): its data arrive with the BN partials instead of costing one more round trip after them.
 template <int KS>
 __device__ __forceinline__ void sweep_wait(const Args& pa, int round, int wv, int lane, int G, unsigned tag,
-                                           float (&sv)[4]) {
+                                           float (&sv)[4], bool halo, int Lsrc, int which, int h, unsigned htag,
+                                           float (&hv)[4]) {
   const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(pa.bnx + (size_t)(round & 1) * LMAX * 64,
                                                                       (short)0, LMAX * 64 * 4, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rh = grsrc(pa, round);
+  const int hbase = (Lsrc * GSTR + 64 + which * 512 + h * 256 + lane * 4) * 8;
   const int q4 = lane & 15, sub = lane >> 4;
-  v4u xa[KS];
-  unsigned need = 0;  // bit k: load k of this lane still lacks a valid value
+  v4u xa[KS], xh[2];
+  unsigned need = 0;  // bit k: load k of this lane still lacks a valid value; bits 8, 9: the halo row
 #pragma unroll
   for (int k = 0; k < KS; ++k) {
     xa[k] = v4u{0u, 0u, 0u, 0u};
     if (4 * wv + sub + 4 * NW * k < G) need |= 1u << k;
   }
+  xh[0] = xh[1] = v4u{0u, 0u, 0u, 0u};
+  if (halo) need |= 3u << 8;
   for (unsigned spins = 0;; ++spins) {
     asm volatile("" ::: "memory");  // re-issued every pass (never hoisted out of the spin)
+#pragma unroll
+    for (int p = 0; p < 2; ++p)
+      if (need & (1u << (8 + p))) xh[p] = __builtin_amdgcn_raw_buffer_load_b128(rh, hbase + 2 * p * 8, 0, 16);
 #pragma unroll
     for (int k = 0; k < KS; ++k)
       if (need & (1u << k))
@@ -329,6 +322,9 @@ __device__ __forceinline__ void sweep_wait(const Args& pa, int round, int wv, in
                       (xa[k][3] & 3u) == tag;
       if (ok) need &= ~(1u << k);
     }
+#pragma unroll
+    for (int p = 0; p < 2; ++p)
+      if (xh[p][1] == htag && xh[p][3] == htag) need &= ~(1u << (8 + p));
     if (__all(need == 0)) break;
     sleep_units(pa.gap);
     if (spins >= SPIN_LIMIT) {
@@ -344,6 +340,11 @@ __device__ __forceinline__ void sweep_wait(const Args& pa, int round, int wv, in
 #pragma unroll
     for (int e = 0; e < 4; ++e) sv[e] += valid ? __uint_as_float(xa[k][e]) : 0.f;
   }
+#pragma unroll
+  for (int p = 0; p < 2; ++p) {
+    hv[2 * p] = __uint_as_float(xh[p][0]);
+    hv[2 * p + 1] = __uint_as_float(xh[p][2]);
+  }
 }
 // All-to-all BN exchange wait + (halo waves) the neighbour's boundary row.  On return cred[0 .. NW*64) holds every
 // wave's partial totals (the caller's barrier makes them visible): tot(slot) = sum_k cred[k * 64 + slot].
@@ -354,26 +355,16 @@ __device__ __forceinline__ void xchg_wait(const Args& pa, int round, int epoch, 
   const unsigned tag = tagof(epoch, round);
   float sv[4];
   const unsigned btag = bn_tag(epoch, round);
-  if (G <= 4 * NW) sweep_wait<1>(pa, round, wv, lane, G, btag, sv);
-  else if (G <= 8 * NW) sweep_wait<2>(pa, round, wv, lane, G, btag, sv);
-  else if (G <= 16 * NW) sweep_wait<4>(pa, round, wv, lane, G, btag, sv);
-  else sweep_wait<8>(pa, round, wv, lane, G, btag, sv);
+  if (G <= 4 * NW) sweep_wait<1>(pa, round, wv, lane, G, btag, sv, halo, Lsrc, which, h, tag, hv);
+  else if (G <= 8 * NW) sweep_wait<2>(pa, round, wv, lane, G, btag, sv, halo, Lsrc, which, h, tag, hv);
+  else if (G <= 16 * NW) sweep_wait<4>(pa, round, wv, lane, G, btag, sv, halo, Lsrc, which, h, tag, hv);
+  else sweep_wait<8>(pa, round, wv, lane, G, btag, sv, halo, Lsrc, which, h, tag, hv);
 #pragma unroll
   for (int e = 0; e < 4; ++e) {  // the four 16-lane groups read different workgroups
     sv[e] += __shfl_xor(sv[e], 16);
     sv[e] += __shfl_xor(sv[e], 32);
   }
   if (lane < 16) *(f32x4*)(cred + wv * 64 + 4 * lane) = f32x4{sv[0], sv[1], sv[2], sv[3]};
-  if (halo) {
-    for (unsigned spins = 0;; ++spins) {
-      asm volatile("" ::: "memory");
-      if (__all(poll_row(pa, round, Lsrc, which, h, tag, hv, lane))) break;
-      if (spins >= SPIN_LIMIT) {
-        if (lane == 0) atomicOr(pa.err, 1u << (round & 31));
-        break;
-      }
-    }
-  }
 }
 __device__ __forceinline__ float slot_total(const float* cred, int slot) {
   float a = 0.f;
@@ -1452,6 +1443,7 @@ __global__ void __launch_bounds__(NTH) k_pks_step(Ctx cx, Args pa, RedAr ra) {
   // ======================= stem backward: max-pool bwd (saved argmax) -> ReLU mask -> conv1 wgrad ============
   lds_barrier();  // every wave is done with XR / WT (the last dgrad); dyT / xT stay for the last wgrad
   wgrad_acc<P>(dyT, xT, wacc, wv, lane);  // application 0
+  DCA_STAMP(cx, 5, L, 2);
   {
     unsigned short* dsT = (unsigned short*)(U + PL::U_DST);
     unsigned short* xs = (unsigned short*)(U + PL::U_XS);
@@ -1506,6 +1498,7 @@ __global__ void __launch_bounds__(NTH) k_pks_step(Ctx cx, Args pa, RedAr ra) {
     }
     // conv1 bias gradient partial of this workgroup (also the barrier before the MFMAs)
     const float dbv = wg_csum(db, 0.f, cred);
+    DCA_STAMP(cx, 5, L, 3);
     float* ss = cx.SSLAB + (size_t)L * SSLAB_N;
     if (t < 32) ss[1024 + t] = dbv;
     // D[co][k] = sum over this slice's conv pixels of ds[p][co] * im2col[p][k]; K step = one conv row (32 px).
@@ -1536,6 +1529,7 @@ __global__ void __launch_bounds__(NTH) k_pks_step(Ctx cx, Args pa, RedAr ra) {
       st4_wt(ss + ((tile * 64 + ln) << 2), ld4(sred + ((tile * 64 + ln) << 2)) + ld4(sred + (((tile + 4) * 64 + ln) << 2)));
     }
   }
+  DCA_STAMP(cx, 5, L, 4);
   // the next batch's image n (this slice's quarter) and label, staged into the other parity
   if (t < 48) st4_wt((uint4*)(pa.simg + (size_t)((par ^ 1) * 64 + n) * 3072 + 768 * s) + t, __builtin_bit_cast(f32x4, nxt));
   if (t == 48 && s == 0) pa.slab[(par ^ 1) * 64 + n] = nxt_lab;
