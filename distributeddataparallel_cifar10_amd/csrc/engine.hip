@@ -756,12 +756,16 @@ int dca_engine_ipc_selftest(void* h, const float* src, float* dst, float timeout
     cx.B = 1;
     hipLaunchKernelGGL(dca::pks::k_pks_reduce_ar, dim3(dca::pks::seg_layout(ra.seg_ch).nseg), dim3(256), 0, e->st, cx,
                        e->qa, 1, ra);
-  } else if (e->bf)
-    hipLaunchKernelGGL(dca::xg::k_xgmi_ar_sgd<true>, dim3(dca::xg::AR_NB), dim3(dca::xg::AR_T), 0, e->st,
-                       e->base, e->peers, src, dst, e->qa.err + 1, 0, dl);
-  else
-    hipLaunchKernelGGL(dca::xg::k_xgmi_ar_sgd<false>, dim3(dca::xg::AR_NB), dim3(dca::xg::AR_T), 0, e->st,
-                       e->base, e->peers, src, dst, e->qa.err + 1, 0, dl);
+  } else {
+    dca::xg::Peers P = e->peers;
+    P.ticks = nullptr;  // a self-test is not training-step communication (metrics)
+    if (e->bf)
+      hipLaunchKernelGGL(dca::xg::k_xgmi_ar_sgd<true>, dim3(dca::xg::AR_NB), dim3(dca::xg::AR_T), 0, e->st,
+                         e->base, P, src, dst, e->qa.err + 1, 0, dl);
+    else
+      hipLaunchKernelGGL(dca::xg::k_xgmi_ar_sgd<false>, dim3(dca::xg::AR_NB), dim3(dca::xg::AR_T), 0, e->st,
+                         e->base, P, src, dst, e->qa.err + 1, 0, dl);
+  }
   HIPCK(hipGetLastError());
   HIPCK(hipStreamSynchronize(e->st));
   unsigned f = 0;
@@ -783,13 +787,31 @@ int dca_engine_ipc_bench(void* h, const float* src, float* dst, int iters, float
   HIPCK(hipEventCreate(&a));
   HIPCK(hipEventCreate(&b));
   HIPCK(hipEventRecord(a, e->st));
+  dca::xg::Peers P = e->peers;
+  P.ticks = nullptr;  // benchmark traffic stays out of the training comm-time counters
   for (int i = 0; i < iters; ++i) {
-    if (e->bf)
+    if (e->persistent) {  // the exchange a sliced training step runs: every gradient segment, self-test mode
+      dca::pks::RedAr ra{};
+      ra.peers = P;
+      ra.err = e->qa.err + 1;
+      ra.deadline = e->ar_deadline;
+      ra.st_src = src;
+      ra.st_dst = dst;
+      ra.st_n = dca::FLAT_N;
+      ra.mode = 3;
+      ra.fc_in_step = 0;
+      ra.seg_ch = e->shared_device ? 256 : e->seg_ch;
+      dca::Ctx cx = e->base;
+      cx.B = 1;
+      hipLaunchKernelGGL(dca::pks::k_pks_reduce_ar, dim3(dca::pks::seg_layout(ra.seg_ch).nseg), dim3(256), 0, e->st,
+                         cx, e->qa, 1, ra);
+    } else if (e->bf) {
       hipLaunchKernelGGL(dca::xg::k_xgmi_ar_sgd<true>, dim3(dca::xg::AR_NB), dim3(dca::xg::AR_T), 0, e->st,
-                         e->base, e->peers, src, dst, e->qa.err + 1, 0, e->ar_deadline);
-    else
+                         e->base, P, src, dst, e->qa.err + 1, 0, e->ar_deadline);
+    } else {
       hipLaunchKernelGGL(dca::xg::k_xgmi_ar_sgd<false>, dim3(dca::xg::AR_NB), dim3(dca::xg::AR_T), 0, e->st,
-                         e->base, e->peers, src, dst, e->qa.err + 1, 0, e->ar_deadline);
+                         e->base, P, src, dst, e->qa.err + 1, 0, e->ar_deadline);
+    }
   }
   HIPCK(hipEventRecord(b, e->st));
   HIPCK(hipEventSynchronize(b));
