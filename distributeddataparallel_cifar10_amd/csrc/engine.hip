@@ -105,8 +105,9 @@ struct Engine {
   int fc_in_step = 1;  // the fc1 / fc-tail gradient segments run on the step kernel's fc workers (pks::N_FCW extra
                        // workgroups beside the backward); off: in the reduction kernel.  Off whenever the step and
                        // its fc workers would exceed the co-resident budget, and when xGMI peers share this device
-  int shared_device = 0;  // set by the host: xGMI peers on this device (shared-GPU rehearsal): no fc workers and
-                          // the coarse 107-segment layout, so a spinning reduction grid leaves CUs for a peer's step
+  int shared_device = 0;  // set by the host: number of xGMI ranks on this device (shared-GPU rehearsal; 0/1: not
+                          // shared): the coarse 107-segment layout, and fc workers only when every co-scheduled
+                          // grid fits (fc_in_step_for), so a spinning kernel always leaves CUs for a peer's step
   std::map<std::string, void*> regions;
   // dynamic LDS sizes
   size_t s_stem = 0, s_fwd = 0, s_head1 = 0, s_head2 = 0, s_dgrad = 0, s_dgrad0 = 0, s_wgrad = 0, s_fc = 0;
@@ -271,6 +272,17 @@ static int enqueue_xgmi_sgd(Engine* e, const Ctx& cx) {
 // grid of the sliced step: S workgroups per image, image slots rounded up to a multiple of 8 (see k_pks_step)
 static int pks_grid(int B) { return (B + 7) / 8 * 8 * pks::S; }
 
+// Whether the step at batch B runs the fc gradient segments on fc workers.  A step workgroup needs a whole CU
+// (VGPR-bound), and every workgroup of a peer's spinning step or reduction kernel may hold one: with n ranks on
+// the device, fc workers only when (n - 1) peer grids + this step fit the co-resident budget.
+static bool fc_in_step_for(const Engine* e, int B) {
+  const int gs = pks_grid(B) + pks::N_FCW;
+  if (!e->fc_in_step || gs > e->resident) return false;
+  if (e->shared_device <= 1) return true;
+  const int gr = pks::reduce_segments(1, 256) + 1;
+  return (e->shared_device - 1) * std::max(gs, gr) + gs <= e->resident;
+}
+
 static int enqueue_step_persistent(Engine* e, int B, int part) {
   Ctx cx = e->base;
   cx.B = B;
@@ -286,8 +298,8 @@ static int enqueue_step_persistent(Engine* e, int B, int part) {
     ra.err = e->qa.err + 1;
     ra.deadline = e->ar_deadline;
     ra.mode = !multi ? 0 : (xgmi ? 2 : 1);
-    ra.fc_in_step = (e->fc_in_step && !e->shared_device && pks_grid(B) + pks::N_FCW <= e->resident) ? 1 : 0;
-    ra.seg_ch = e->shared_device ? 256 : e->seg_ch;
+    ra.fc_in_step = fc_in_step_for(e, B) ? 1 : 0;
+    ra.seg_ch = e->shared_device > 1 ? 256 : e->seg_ch;
     const dim3 grid(pks_grid(B) + (ra.fc_in_step ? pks::N_FCW : 0));
     if (e->bf)
       hipLaunchKernelGGL(pks::k_pks_step<0>, grid, dim3(pks::NTH), pks::Plan<0>::TOTAL, e->st, cx, e->qa, ra);
@@ -751,7 +763,7 @@ int dca_engine_ipc_selftest(void* h, const float* src, float* dst, float timeout
     ra.st_n = dca::FLAT_N;
     ra.mode = 3;
     ra.fc_in_step = 0;  // every segment in the reduction kernel
-    ra.seg_ch = e->shared_device ? 256 : e->seg_ch;
+    ra.seg_ch = e->shared_device > 1 ? 256 : e->seg_ch;
     dca::Ctx cx = e->base;
     cx.B = 1;
     hipLaunchKernelGGL(dca::pks::k_pks_reduce_ar, dim3(dca::pks::seg_layout(ra.seg_ch).nseg), dim3(256), 0, e->st, cx,
@@ -800,7 +812,7 @@ int dca_engine_ipc_bench(void* h, const float* src, float* dst, int iters, float
       ra.st_n = dca::FLAT_N;
       ra.mode = 3;
       ra.fc_in_step = 0;
-      ra.seg_ch = e->shared_device ? 256 : e->seg_ch;
+      ra.seg_ch = e->shared_device > 1 ? 256 : e->seg_ch;
       dca::Ctx cx = e->base;
       cx.B = 1;
       hipLaunchKernelGGL(dca::pks::k_pks_reduce_ar, dim3(dca::pks::seg_layout(ra.seg_ch).nseg), dim3(256), 0, e->st,
@@ -841,16 +853,23 @@ int dca_engine_sync(void* h) {
   return 0;
 }
 
-// Sliced engine: the host reports that xGMI peers share this device (shared-GPU rehearsal): no fc workers in the
-// step kernel and the coarse gradient-segment layout (see Engine::shared_device).  Collective in effect: every
-// rank must make the same call before stepping.  Drops the captured graphs.
-int dca_engine_set_shared_device(void* h, int shared) {
+// Sliced engine: the host reports that `n` xGMI ranks share this device (shared-GPU rehearsal; the largest such
+// count over all devices, so every rank picks the same layout): the coarse gradient-segment layout and the
+// co-residency rule of fc_in_step_for.  Collective in effect: every rank must make the same call before
+// stepping.  Drops the captured graphs.
+int dca_engine_set_shared_device(void* h, int n) {
   Engine* e = (Engine*)h;
   HIPCK(hipStreamSynchronize(e->st));
   for (auto& kv : e->graphs) (void)hipGraphExecDestroy(kv.second);
   e->graphs.clear();
-  e->shared_device = shared ? 1 : 0;
+  e->shared_device = n > 1 ? n : 0;
   return 0;
+}
+
+// Sliced engine: 1 if a step at batch B runs the fc gradient segments on the step kernel's fc workers.
+int dca_engine_fc_in_step(void* h, int B) {
+  Engine* e = (Engine*)h;
+  return e->persistent && fc_in_step_for(e, B) ? 1 : 0;
 }
 
 // Handle of the engine stream (so Python can order torch work against it).

@@ -93,12 +93,13 @@ class FusedDDPTrainer:
         handles = [None] * self.world_size
         dist.all_gather_object(handles, handle)
         ok = all(h is not None for h in handles)
-        # ranks sharing one device (the shared-GPU rehearsal): the step kernel's fc workers exchange with peers
-        # inside the step, so one rank's step could hold CUs another rank's step needs -> fc segments after the step
+        # ranks sharing one device (the shared-GPU rehearsal): a rank's spinning kernels (the step's fc workers,
+        # the reduction) can hold CUs a peer's step needs -> the engine budgets its grids by the sharing count
         dev_ids = [None] * self.world_size
         dist.all_gather_object(dev_ids, _device_key(data_u8.device))
-        if ok and eng is not None and len(set(dev_ids)) < len(dev_ids):
-            eng.set_shared_device(True)
+        n_share = max(dev_ids.count(d) for d in dev_ids)
+        if ok and eng is not None and n_share > 1:
+            eng.set_shared_device(n_share)
         if ok:
             try:
                 eng.connect_peers(handles)

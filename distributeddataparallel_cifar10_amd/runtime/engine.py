@@ -192,12 +192,17 @@ class NetResDeepEngine:
         self.derive()
         self._n_indices = 0
 
-    def set_shared_device(self, shared: bool) -> None:
-        """Sliced engine, xGMI: peers share this device (shared-GPU rehearsal).  Then the fc gradient segments run
-        after the step (not on the step kernel's fc workers, which exchange with peers inside the step) and the
-        reduction grid stays small, so one rank's spinning kernels always leave CUs for a peer's step.  Every rank
-        must make the same call before stepping."""
-        native.check(self.lib.dca_engine_set_shared_device(self.h, 1 if shared else 0), "dca_engine_set_shared_device")
+    def set_shared_device(self, n: int) -> None:
+        """Sliced engine, xGMI: ``n`` ranks share one device (shared-GPU rehearsal; the largest count over all
+        devices, ``n <= 1``: not shared).  Then the reduction uses the coarse segment layout and the fc gradient
+        segments run on the step kernel's fc workers only when every co-scheduled grid fits on the device
+        (a rank's spinning kernels must always leave CUs for a peer's step).  Every rank must make the same
+        call before stepping."""
+        native.check(self.lib.dca_engine_set_shared_device(self.h, int(n)), "dca_engine_set_shared_device")
+
+    def fc_in_step(self, batch: int) -> bool:
+        """Whether a step at this batch size runs the fc gradient segments on the step kernel's fc workers."""
+        return bool(self.lib.dca_engine_fc_in_step(self.h, int(batch)))
 
     # ---- state sync ---------------------------------------------------------------------------------------
     def derive(self):

@@ -53,6 +53,7 @@ def _declare(lib):
     lib.dca_engine_precapture.argtypes = [c_void_p, c_int]
     lib.dca_engine_kind.argtypes = [c_void_p]
     lib.dca_engine_set_shared_device.argtypes = [c_void_p, c_int]
+    lib.dca_engine_fc_in_step.argtypes = [c_void_p, c_int]
     lib.dca_engine_comm_time.argtypes = [c_void_p, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_longlong),
                                          c_int]
     return lib

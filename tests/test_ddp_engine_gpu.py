@@ -111,11 +111,12 @@ def test_engine_ddp_two_ranks_one_gpu(gpu, port, dtype, persistent, kernel):
     assert not bad, "\n".join(f"rank {r}:\n{e}" for r, e in bad)
 
 
-def _xgmi_worker(rank, ws, port, dtype, persistent, q, comm="xgmi", own_device=False):
+def _xgmi_worker(rank, ws, port, dtype, persistent, q, comm="xgmi", own_device=False, batch=B, fc_workers=None):
     """One rank of the fused trainer with the one-shot xGMI all-reduce.  By default all ranks share GPU 0: the
     IPC-mapped slabs are then peers on the same device, which exercises the whole protocol -- epochs, parities,
     flags.  own_device=True (tests/test_multigpu.py): rank r on GPU r, so the slabs and flags cross xGMI, and
-    comm="rccl" runs the graph-captured RCCL all-reduce instead."""
+    comm="rccl" runs the graph-captured RCCL all-reduce instead.  fc_workers: assert whether the sliced step ran
+    the fc gradient segments (and their xGMI exchange) on its fc workers."""
     try:
         os.environ["MASTER_ADDR"] = "127.0.0.1"
         os.environ["MASTER_PORT"] = str(port)
@@ -140,13 +141,15 @@ def _xgmi_worker(rank, ws, port, dtype, persistent, q, comm="xgmi", own_device=F
                              comm=comm, max_indices=len(order[rank]))
         assert tr.comm == comm, f"asked for {comm}, got {tr.comm} (the xGMI path did not come up?)"
         eng = tr.engine
+        if fc_workers is not None:
+            assert eng.fc_in_step(batch) == fc_workers, (batch, fc_workers)
         eng.set_indices(order[rank])
         eng.set_cursor(0)
         eng.read_loss(reset=True)
         import time
         for s in range(STEPS):  # uneven producer timing: ranks reach each step's all-reduce at different times
             time.sleep(0.03 * ((rank + s) % ws))
-            eng.run(B, 1)  # graph-captured step, the all-reduce inside the graph
+            eng.run(batch, 1)  # graph-captured step, the all-reduce inside the graph
         loss, steps = eng.read_loss()
         assert steps == STEPS
         # single-process simulation of reference DDP over `ws` ranks
@@ -158,7 +161,7 @@ def _xgmi_worker(rank, ws, port, dtype, persistent, q, comm="xgmi", own_device=F
                 with torch.no_grad():
                     for k, v in models[r].named_buffers():
                         v.copy_(snap[k])
-                sel = order[r][s * B:(s + 1) * B]
+                sel = order[r][s * batch:(s + 1) * batch]
                 out = reference_step(models[r], data[sel], labels[sel], lr=1e-2, apply_sgd=False,
                                      bf16_operands=dtype == "bf16", fc1_bf16=persistent and dtype == "bf16")
                 grads.append(out["grads"])
@@ -194,6 +197,24 @@ def test_xgmi_allreduce_ranks_one_gpu(gpu, port, ws, dtype, persistent):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     procs = [ctx.Process(target=_xgmi_worker, args=(r, ws, port, dtype, persistent, q)) for r in range(ws)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=600) for _ in procs]
+    for p in procs:
+        p.join(timeout=120)
+    bad = [r for r in res if r[1]]
+    assert not bad, "\n".join(f"rank {r}:\n{e}" for r, e in bad)
+
+
+@pytest.mark.parametrize("dtype", ["bf16", "fp32"])
+def test_xgmi_fc_workers_two_ranks_one_gpu(gpu, port, dtype):
+    """Batch 8 on 2 ranks sharing the GPU: both steps with their fc workers (2 x 97 workgroups) and a peer's
+    reduction fit on the device together, so the fc workers' in-step xGMI exchange runs (the path of the
+    cross-device runs) and must match the DDP simulation bitwise-consistently on both ranks."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_xgmi_worker, args=(r, 2, port, dtype, True, q),
+                         kwargs=dict(batch=8, fc_workers=True)) for r in range(2)]
     for p in procs:
         p.start()
     res = [q.get(timeout=600) for _ in procs]
