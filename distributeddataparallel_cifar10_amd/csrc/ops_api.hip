@@ -456,7 +456,7 @@ int dca_ops_bn_fwd(const void* x, const void* r, void* out, float* part, float* 
 #undef FIN
   BN_LAUNCH(k_bn_apply, C, nparts_rows(M), st, (const bf16_t*)x, (const bf16_t*)r,
                      (bf16_t*)out, (const float2*)stats, gamma, beta, M, C, relu, res_mode, (uint8_t*)nullptr,
-                     (const float*)nullptr, (unsigned*)nullptr);
+                     (const float*)nullptr, (unsigned*)nullptr, (uint8_t*)nullptr);
   OPCK(hipGetLastError());
   return 0;
 }
@@ -465,13 +465,15 @@ int dca_ops_bn_fwd(const void* x, const void* r, void* out, float* part, float* 
 // over `nparts` partial rows + apply.
 // q / amax_prev / amax_out (optional): also write an fp8 copy of the output with delayed scaling (k_bn_apply);
 // amax_out is zeroed here first.
+// mask (optional, res_mode 2 + ReLU): [M C / 8] bytes, the ReLU mask for dca_ops_bn_bwd.
 int dca_ops_bn_fwd_parts(const void* x, const void* r, void* out, const float* part, int nparts, float* stats,
                          const float* gamma, const float* beta, float* rm, float* rv, long M, int C, float eps,
                          float momentum, int relu, int res_mode, void* q, const float* amax_prev, unsigned* amax_out,
-                         void* stream) {
+                         void* mask, void* stream) {
   REQUIRE(C % 8 == 0, "bn: C must be a multiple of 8");
   REQUIRE(res_mode == 0 || r != nullptr, "bn: residual missing");
   REQUIRE(!q || (amax_prev && amax_out), "bn: fp8 output needs amax_prev and amax_out");
+  REQUIRE(!mask || (relu && res_mode == 2), "bn: the stored mask is for ReLU(bn + r)");
   hipStream_t st = (hipStream_t)stream;
   if (q) OPCK(hipMemsetAsync(amax_out, 0, sizeof(unsigned), st));
 #define FIN(CW) hipLaunchKernelGGL(k_bn_finalize<CW>, dim3((C + CW - 1) / CW), dim3(256), 0, st, (const float2*)part, \
@@ -480,7 +482,7 @@ int dca_ops_bn_fwd_parts(const void* x, const void* r, void* out, const float* p
 #undef FIN
   BN_LAUNCH(k_bn_apply, C, nparts_rows(M), st, (const bf16_t*)x, (const bf16_t*)r,
                      (bf16_t*)out, (const float2*)stats, gamma, beta, M, C, relu, res_mode, (uint8_t*)q, amax_prev,
-                     amax_out);
+                     amax_out, (uint8_t*)mask);
   OPCK(hipGetLastError());
   return 0;
 }
@@ -495,28 +497,30 @@ int dca_ops_bn_eval(const void* x, const void* r, void* out, float* stats, const
   hipLaunchKernelGGL(k_bn_eval_stats, dim3((C + 255) / 256), dim3(256), 0, st, rm, rv, (float2*)stats, C, eps);
   BN_LAUNCH(k_bn_apply, C, nparts_rows(M), st, (const bf16_t*)x, (const bf16_t*)r,
                      (bf16_t*)out, (const float2*)stats, gamma, beta, M, C, relu, res_mode, (uint8_t*)nullptr,
-                     (const float*)nullptr, (unsigned*)nullptr);
+                     (const float*)nullptr, (unsigned*)nullptr, (uint8_t*)nullptr);
   OPCK(hipGetLastError());
   return 0;
 }
 
+// mask (optional): the forward's ReLU bit mask (dca_ops_bn_fwd_parts); r is then not read.
 int dca_ops_bn_bwd(const void* dy, const void* x, const void* r, const float* stats, const float* gamma,
                    const float* beta, float* part, float* sums, float* dgamma, float* dbeta, void* dx, void* dr,
-                   long M, int C, int relu, int res_mode, int accumulate, void* stream) {
+                   long M, int C, int relu, int res_mode, int accumulate, const void* mask, void* stream) {
   REQUIRE(C % 8 == 0, "bn: C must be a multiple of 8");
-  REQUIRE(res_mode != 2 || (r != nullptr && dr != nullptr), "bn bwd: residual tensors missing");
+  REQUIRE(res_mode != 2 || ((r != nullptr || mask != nullptr) && dr != nullptr), "bn bwd: residual tensors missing");
+  REQUIRE(!mask || (relu && res_mode == 2), "bn bwd: the stored mask is for ReLU(bn + r)");
   hipStream_t st = (hipStream_t)stream;
   const int nparts = (int)((M + BN_ROWS - 1) / BN_ROWS);
   BN_LAUNCH(k_bn_bwd_stats, C, nparts, st, (const bf16_t*)dy,
                      (const bf16_t*)x, (const bf16_t*)r, (const float2*)stats, gamma, beta, (float2*)part, (int)M, C,
-                     relu, res_mode);
+                     relu, res_mode, (const uint8_t*)mask);
 #define FIN(CW) hipLaunchKernelGGL(k_bn_bwd_finalize<CW>, dim3((C + CW - 1) / CW), dim3(256), 0, st, \
                                    (const float2*)part, nparts, C, dgamma, dbeta, (float2*)sums, accumulate)
   BN_FIN_DISPATCH(C, FIN);
 #undef FIN
   BN_LAUNCH(k_bn_bwd_apply, C, nparts_rows(M), st, (const bf16_t*)dy, (const bf16_t*)x,
                      (const bf16_t*)r, (const float2*)stats, gamma, beta, (const float2*)sums, (bf16_t*)dx,
-                     (bf16_t*)dr, M, C, relu, res_mode);
+                     (bf16_t*)dr, M, C, relu, res_mode, (const uint8_t*)mask);
   OPCK(hipGetLastError());
   return 0;
 }
@@ -533,7 +537,8 @@ int dca_ops_bn_bwd_parts(const void* dy, const void* x, const float* stats, cons
   BN_FIN_DISPATCH(C, FIN);
 #undef FIN
   BN_LAUNCH(k_bn_bwd_apply, C, nparts_rows(M), st, (const bf16_t*)dy, (const bf16_t*)x, (const bf16_t*)nullptr,
-            (const float2*)stats, gamma, beta, (const float2*)sums, (bf16_t*)dx, (bf16_t*)nullptr, M, C, 1, 0);
+            (const float2*)stats, gamma, beta, (const float2*)sums, (bf16_t*)dx, (bf16_t*)nullptr, M, C, 1, 0,
+            (const uint8_t*)nullptr);
   OPCK(hipGetLastError());
   return 0;
 }

@@ -246,7 +246,8 @@ __global__ void __launch_bounds__(256) k_bn_apply(const bf16_t* __restrict__ x, 
                                                   bf16_t* __restrict__ out, const float2* __restrict__ stats,
                                                   const float* __restrict__ gamma, const float* __restrict__ beta,
                                                   long M, int C, int relu, int res_mode, uint8_t* __restrict__ q,
-                                                  const float* __restrict__ amax_prev, unsigned* __restrict__ amax_out) {
+                                                  const float* __restrict__ amax_prev, unsigned* __restrict__ amax_out,
+                                                  uint8_t* __restrict__ mk) {
   // grid (ceil(C/(8 CL)), ceil(M/BN_ROWS)): CL channel groups of 8 x 256/CL row lanes, z = x * sc + sh per channel
   __shared__ float red[256];
   const int cgl = threadIdx.x % CL, rl = threadIdx.x / CL, c0 = blockIdx.x * (8 * CL) + cgl * 8;
@@ -288,6 +289,12 @@ __global__ void __launch_bounds__(256) k_bn_apply(const bf16_t* __restrict__ x, 
       }
       const uint4 ov = pack8(v);
       *(uint4*)(out + o) = ov;
+      if (mk) {  // ReLU mask, one bit per element (bit j: channel c0 + j), for the backward
+        unsigned b = 0;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) b |= (v[j] > 0.f ? 1u : 0u) << j;
+        mk[o >> 3] = (uint8_t)b;
+      }
       if (q) {
         float f[8];
         unpack8(ov, f);  // quantise the value as stored (bf16)
@@ -319,14 +326,16 @@ __global__ void __launch_bounds__(256) k_bn_apply(const bf16_t* __restrict__ x, 
   }
 }
 
-// dz = dy * act'(.) recomputed from x (and r); partial sums of dz and dz * xhat per channel.
+// dz = dy * act'(.) recomputed from x (and r) -- or, when the forward stored it (mk: res_mode 2 + ReLU), the ReLU
+// bit mask (1/16 of the bytes of r; exactly the forward's mask); partial sums of dz and dz * xhat per channel.
 // grid (ceil(C/64), ceil(M/BN_ROWS)); 256 threads = 8 channel groups (8 channels, one 16-B load per tensor per
 // row) x 32 row lanes; all rows' loads of a thread are independent (issued back to back).
 template <int CL>
 __global__ void __launch_bounds__(256) k_bn_bwd_stats(const bf16_t* __restrict__ dy, const bf16_t* __restrict__ x,
                                                       const bf16_t* __restrict__ r, const float2* __restrict__ stats,
                                                       const float* __restrict__ gamma, const float* __restrict__ beta,
-                                                      float2* __restrict__ part, int M, int C, int relu, int res_mode) {
+                                                      float2* __restrict__ part, int M, int C, int relu, int res_mode,
+                                                      const uint8_t* __restrict__ mk) {
   __shared__ float2 red[256 / CL][8 * CL];
   const int cgl = threadIdx.x % CL, rl = threadIdx.x / CL, c0 = blockIdx.x * (8 * CL) + cgl * 8;
   const int r0 = blockIdx.y * BN_ROWS;
@@ -345,12 +354,14 @@ __global__ void __launch_bounds__(256) k_bn_bwd_stats(const bf16_t* __restrict__
     // BN_U rows per thread in flight: every load issued (clamped rows, unconditional) before any is used
     for (int base = r0 + rl; base < rend; base += (256 / CL) * BN_U) {
       uint4 X[BN_U], D[BN_U], R[BN_U];
+      unsigned MB[BN_U];
 #pragma unroll
       for (int u = 0; u < BN_U; ++u) {
         const long o = (long)min(base + (256 / CL) * u, rend - 1) * C + c0;
         X[u] = *(const uint4*)(x + o);
         D[u] = *(const uint4*)(dy + o);
-        if (res_mode == 2) R[u] = *(const uint4*)(r + o);
+        if (mk) MB[u] = mk[o >> 3];
+        else if (res_mode == 2) R[u] = *(const uint4*)(r + o);
       }
 #pragma unroll
       for (int u = 0; u < BN_U; ++u) {
@@ -358,12 +369,14 @@ __global__ void __launch_bounds__(256) k_bn_bwd_stats(const bf16_t* __restrict__
         float xv[8], dv[8], rv[8];
         unpack8(X[u], xv);
         unpack8(D[u], dv);
-        if (res_mode == 2) unpack8(R[u], rv);
+        if (!mk && res_mode == 2) unpack8(R[u], rv);
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
           const float xh = (xv[j] - mu[j]) * is[j];
           float d = dv[j];
-          if (relu) {
+          if (mk) {
+            d = (MB[u] >> j) & 1u ? d : 0.f;
+          } else if (relu) {
             float z = xh * ga[j] + be[j];
             if (res_mode == 2) z += rv[j];
             d = z > 0.f ? d : 0.f;
@@ -411,7 +424,8 @@ __global__ void __launch_bounds__(256) k_bn_bwd_apply(const bf16_t* __restrict__
                                                       const bf16_t* __restrict__ r, const float2* __restrict__ stats,
                                                       const float* __restrict__ gamma, const float* __restrict__ beta,
                                                       const float2* __restrict__ sums, bf16_t* __restrict__ dx,
-                                                      bf16_t* __restrict__ dr, long M, int C, int relu, int res_mode) {
+                                                      bf16_t* __restrict__ dr, long M, int C, int relu, int res_mode,
+                                                      const uint8_t* __restrict__ mk) {
   const int cgl = threadIdx.x % CL, rl = threadIdx.x / CL, c0 = blockIdx.x * (8 * CL) + cgl * 8;
   if (c0 >= C) return;
   const long r0 = (long)blockIdx.y * BN_ROWS;
@@ -432,12 +446,14 @@ __global__ void __launch_bounds__(256) k_bn_bwd_apply(const bf16_t* __restrict__
   const long rend = M < r0 + BN_ROWS ? M : r0 + BN_ROWS;
   for (long base = r0 + rl; base < rend; base += (256 / CL) * BN_U) {
     uint4 X[BN_U], D[BN_U], R[BN_U];
+    unsigned MB[BN_U];
 #pragma unroll
     for (int u = 0; u < BN_U; ++u) {  // all loads in flight first (clamped rows)
       const long row = base + (256 / CL) * u, o = (row < rend ? row : rend - 1) * C + c0;
       X[u] = *(const uint4*)(x + o);
       D[u] = *(const uint4*)(dy + o);
-      if (res_mode == 2) R[u] = *(const uint4*)(r + o);
+      if (mk) MB[u] = mk[o >> 3];
+      else if (res_mode == 2) R[u] = *(const uint4*)(r + o);
     }
 #pragma unroll
     for (int u = 0; u < BN_U; ++u) {
@@ -447,11 +463,13 @@ __global__ void __launch_bounds__(256) k_bn_bwd_apply(const bf16_t* __restrict__
       float xv[8], d[8], rv[8];
       unpack8(X[u], xv);
       unpack8(D[u], d);
-      if (res_mode == 2) unpack8(R[u], rv);
+      if (!mk && res_mode == 2) unpack8(R[u], rv);
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         float dz = d[j];
-        if (relu) {
+        if (mk) {
+          dz = (MB[u] >> j) & 1u ? dz : 0.f;
+        } else if (relu) {
           float z = (xv[j] - mu[j]) * is[j] * ga[j] + be[j];
           if (res_mode == 2) z += rv[j];
           dz = z > 0.f ? dz : 0.f;

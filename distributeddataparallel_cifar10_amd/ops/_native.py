@@ -67,12 +67,12 @@ def _declare(lib):
                                    c_void_p, c_long, c_int, c_float, c_float, c_int, c_int, c_void_p]
     lib.dca_ops_bn_fwd_parts.argtypes = [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_void_p,
                                          c_void_p, c_void_p, c_long, c_int, c_float, c_float, c_int, c_int, c_void_p,
-                                         c_void_p, c_void_p, c_void_p]
+                                         c_void_p, c_void_p, c_void_p, c_void_p]
     lib.dca_ops_bn_eval.argtypes = [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                                     c_long, c_int, c_float, c_int, c_int, c_void_p]
     lib.dca_ops_bn_bwd.argtypes = [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                                    c_void_p, c_void_p, c_void_p, c_void_p, c_long, c_int, c_int, c_int, c_int,
-                                   c_void_p]
+                                   c_void_p, c_void_p]
     lib.dca_ops_bn_bwd_parts.argtypes = [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_void_p,
                                          c_void_p, c_void_p, c_void_p, c_long, c_int, c_int, c_void_p]
     lib.dca_ops_maxpool_fwd.argtypes = [c_void_p, c_void_p, c_void_p, P(PoolGeom), c_void_p]

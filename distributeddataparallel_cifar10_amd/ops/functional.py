@@ -621,11 +621,13 @@ class _ConvBNAct(torch.autograd.Function):
         q = None
         if emit is not None and emit.ready:  # fp8 copy of the output for the next (fp8) GEMM, delayed scaling
             q = torch.empty(out.shape, dtype=torch.uint8, device=x.device)
+        # ReLU(bn + r): the forward stores the ReLU mask as bits, so the backward reads M*C/8 bytes instead of r
+        mask = torch.empty(M * co // 8, dtype=torch.uint8, device=x.device) if relu and res_mode == 2 else None
         N.check(N.lib().dca_ops_bn_fwd_parts(N.ptr(y), N.ptr(r), N.ptr(out), N.ptr(part), nparts, N.ptr(stats),
                                              N.ptr(gamma), N.ptr(beta), N.ptr(running_mean), N.ptr(running_var), M, co,
                                              float(eps), float(momentum), int(relu), int(res_mode), N.ptr(q),
                                              N.ptr(emit.amax_prev) if q is not None else None,
-                                             N.ptr(emit.amax_out) if q is not None else None,
+                                             N.ptr(emit.amax_out) if q is not None else None, N.ptr(mask),
                                              N.stream(x.device)), "bn_fwd_parts")
         if q is not None:
             emit.q, emit.src_ptr = q, out.data_ptr()
@@ -635,19 +637,19 @@ class _ConvBNAct(torch.autograd.Function):
         ctx.links = (link_out if relu and res_mode == 0 else None, link_in)
         if ctx.links[0] is not None:
             ctx.links[0].publish(y, stats, gamma.detach(), beta.detach())
-        ctx.save_for_backward(y, r, gamma, beta, stats)
+        ctx.save_for_backward(y, r if mask is None else None, gamma, beta, stats, mask)
         ctx.relu, ctx.res_mode = relu, res_mode
         return out
 
     @staticmethod
     def backward(ctx, dout):
-        y, r, gamma, beta, stats = ctx.saved_tensors
+        y, r, gamma, beta, stats, mask = ctx.saved_tensors
         sw, sg, sb = ctx.sinks if ctx.sinks is not None else (None, None, None)
         link_out, link_in = ctx.links
         parts = link_out.take() if link_out is not None else (None, 0)
         dy_conv, dr, dgamma, dbeta = _bn_backward(dout, y, r, gamma, beta, stats, ctx.relu, ctx.res_mode,
                                                   dgamma_out=sg[0] if sg else None, dbeta_out=sb[0] if sb else None,
-                                                  parts=parts if parts[0] is not None else None)
+                                                  parts=parts if parts[0] is not None else None, mask=mask)
         if sg:
             sg[1]()
             sb[1]()
@@ -735,9 +737,11 @@ class _BatchNormAct(torch.autograd.Function):
         return dx, dr, dgamma, dbeta, None, None, None, None, None, None
 
 
-def _bn_backward(dy, x, r, gamma, beta, stats, relu, res_mode, dgamma_out=None, dbeta_out=None, parts=None):
+def _bn_backward(dy, x, r, gamma, beta, stats, relu, res_mode, dgamma_out=None, dbeta_out=None, parts=None,
+                 mask=None):
     """(dx, dr, dgamma, dbeta) of the fused BN + ReLU + residual.  dgamma_out / dbeta_out: flat gradient views
-    to accumulate into (then dgamma / dbeta are returned as None)."""
+    to accumulate into (then dgamma / dbeta are returned as None).  mask: the forward's ReLU bit mask (res_mode 2;
+    r is then not needed)."""
     dy = dy.to(torch.bfloat16).contiguous()
     C = x.shape[-1]
     M = x.numel() // C
@@ -758,7 +762,8 @@ def _bn_backward(dy, x, r, gamma, beta, stats, relu, res_mode, dgamma_out=None, 
         return (dx, None, None, None) if direct else (dx, None, dgamma, dbeta)
     N.check(N.lib().dca_ops_bn_bwd(N.ptr(dy), N.ptr(x), N.ptr(r), N.ptr(stats), N.ptr(gamma), N.ptr(beta),
                                    N.ptr(part), N.ptr(sums), N.ptr(dgamma), N.ptr(dbeta), N.ptr(dx), N.ptr(dr),
-                                   M, C, int(relu), int(res_mode), int(direct), N.stream(x.device)), "bn_bwd")
+                                   M, C, int(relu), int(res_mode), int(direct), N.ptr(mask), N.stream(x.device)),
+            "bn_bwd")
     if res_mode == 1:
         dr = dy
     if direct:
