@@ -125,6 +125,11 @@ inline int getenv_pp() {  // ping-pong 256 x 256 GEMM (k_gemm_pp): DCA_OPS_PP = 
   }();
   return v;
 }
+// weight gradients with M >= 256 on the ping-pong LDS-DMA kernel (k_wgrad_pp): DCA_OPS_WGRAD_PP=0 turns it off
+inline bool getenv_wgrad_pp() {
+  static const bool v = getenv_flag("DCA_OPS_WGRAD_PP");
+  return v;
+}
 inline bool getenv_wgrad_ok() {
   static const int v = [] {
     const char* e = getenv("DCA_OPS_WGRAD");
@@ -207,6 +212,14 @@ int dca_ops_gemm(const GemmArgs* a, void* stream) {
       OPCK(hipFuncSetAttribute((const void*)k_wgrad<64, 128, 1>, hipFuncAttributeMaxDynamicSharedMemorySize, l01));
       OPCK(hipFuncSetAttribute((const void*)k_wgrad<128, 64, 4>, hipFuncAttributeMaxDynamicSharedMemorySize, l10));
       OPCK(hipFuncSetAttribute((const void*)k_wgrad<128, 128, 2>, hipFuncAttributeMaxDynamicSharedMemorySize, l11));
+#define WPP_ATTR(PBN, SW) \
+  OPCK(hipFuncSetAttribute((const void*)k_wgrad_pp<PBN, SW>, hipFuncAttributeMaxDynamicSharedMemorySize, WpTile<PBN>::LDS))
+      WPP_ATTR(256, false);
+      WPP_ATTR(128, false);
+      WPP_ATTR(64, false);
+      WPP_ATTR(128, true);
+      WPP_ATTR(64, true);
+#undef WPP_ATTR
 #define GLDS_ATTR(F8, BNV, NWV)                                                                          \
   OPCK(hipFuncSetAttribute((const void*)k_gemm_glds<F8, BNV, NWV>, hipFuncAttributeMaxDynamicSharedMemorySize, \
                            4 * GemmTile<BNV>::BUF));                                                          \
@@ -256,6 +269,38 @@ int dca_ops_gemm(const GemmArgs* a, void* stream) {
                      (g.conv == 2 || g.ldb % 8 == 0) && g.ws != nullptr && getenv_wgrad_ok();
   if (wgrad) {
     REQUIRE(g.conv != 2 || (long)g.cN * g.cHo * g.cWo < (1L << 24), "gemm: weight-gradient pixel count >= 2^24");
+    // the ping-pong kernel: the larger of M (output channels) / N (input channels x taps) along its 256-row side
+    // (SW: N), the smaller one as a 256 / 128 / 64 column tile; both >= 64 and the larger >= 256; 32-bit operand
+    // offsets, 16-B aligned rows.  The split count is cut to about one workgroup per CU (one fits per CU)
+    const long long a_by = (long long)g.K * g.lda * 2;
+    const long long b_by = g.conv == 2 ? (long long)g.cN * g.cH * g.cW * g.cC * 2 : (long long)g.K * g.ldb * 2;
+    const bool sw = g.M < 256;
+    const int big = sw ? g.N : g.M, small = sw ? g.M : g.N;
+    if (getenv_wgrad_pp() && big >= 256 && small >= 64 && !(sw && small > 128) && a_by < (1LL << 31) &&
+        b_by < (1LL << 31) && ((uintptr_t)g.A & 15) == 0 && ((uintptr_t)g.B & 15) == 0 &&
+        (g.conv != 2 || g.cC % 8 == 0)) {
+      const int pbn = small <= 64 ? 64 : ((small % 256 == 0 || small > 1024) ? 256 : 128);
+      const long tiles = (long)((big + WP_BM - 1) / WP_BM) * ((small + pbn - 1) / pbn);
+      const long want = std::max<long>(1, (256 + tiles - 1) / tiles);
+      if (want < g.splits) {  // fewer, longer splits (the slab was sized for g.splits: smaller is fine)
+        int kps = (int)((g.K + want - 1) / want);
+        kps = (kps + WP_KT - 1) / WP_KT * WP_KT;
+        g.k_per_split = kps;
+        g.splits = (g.K + kps - 1) / kps;
+      }
+      const dim3 grid((unsigned)(tiles * g.splits)), blk(WP_NT);
+      if (sw) {
+        if (pbn == 64) hipLaunchKernelGGL((k_wgrad_pp<64, true>), grid, blk, WpTile<64>::LDS, st, g);
+        else hipLaunchKernelGGL((k_wgrad_pp<128, true>), grid, blk, WpTile<128>::LDS, st, g);
+      } else {
+        if (pbn == 256) hipLaunchKernelGGL((k_wgrad_pp<256, false>), grid, blk, WpTile<256>::LDS, st, g);
+        else if (pbn == 128) hipLaunchKernelGGL((k_wgrad_pp<128, false>), grid, blk, WpTile<128>::LDS, st, g);
+        else hipLaunchKernelGGL((k_wgrad_pp<64, false>), grid, blk, WpTile<64>::LDS, st, g);
+      }
+      hipLaunchKernelGGL(k_gemm_splitk_reduce, dim3(grid_for((long)g.M * g.N, RED_EL, 4096)), dim3(256), 0, st, g);
+      OPCK(hipGetLastError());
+      return 0;
+    }
     const int bm = g.M <= 64 ? 64 : 128, bn = g.N <= 64 ? 64 : 128;
     const long items = (long)((g.M + bm - 1) / bm) * ((g.N + bn - 1) / bn) * g.splits;
     REQUIRE(items < (1L << 31), "gemm: too many work items");

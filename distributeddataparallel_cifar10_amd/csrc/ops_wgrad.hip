@@ -212,5 +212,225 @@ __global__ void __launch_bounds__(256) k_wgrad(GemmArgs g) {
     }
 }
 
+// ---------------------------------------------------------------------------------------------------------
+// k_wgrad_pp: weight gradients on a 256 x PBN tile (PBN = 256 | 128 | 64), 512 threads as two wave groups on the
+// k_gemm_pp ping-pong schedule (one group issues its MFMAs while the other reads its fragments and issues LDS-DMA;
+// each SIMD holds one wave of each group), operands staged by LDS-DMA instead of a register pass (k_wgrad: 4 waves,
+// register-staged, one barrier per K-tile: ~400 TF on ResNet-50's shapes).
+//   * The 256-wide side is the larger GEMM dimension: SW = false -> rows = M (output channels, A = dY), columns = N
+//     (B = X or its implicit im2col); SW = true (M < 256 <= N, e.g. a 64-channel 3x3 conv, N = 576) -> rows = N
+//     (from B), columns = M (from A), and the epilogue writes the transposed fragment (4 consecutive n per lane: one
+//     16-B store).
+//   * K-tile = 64 pixel rows; an operand row of W channels is 2W bytes in LDS, stored row-linear with 16-B chunk c of
+//     row r at chunk position c ^ swz(r) (2 (r & 7) for rows of >= 256 B, 2 ((r >> 1) & 3) for 128-B rows): the DMA
+//     image stays wave-linear (1 KiB per wave instruction) because the swizzle is applied to the SOURCE chunk each
+//     lane loads.  Fragments by ds_read_b64_tr_b16 with k_wgrad's lane map (lanes 4q + p of 16-lane group g: row
+//     4g + q, +16 for the high half, columns 4p ..): the 32 lanes of one LDS cycle read 8 consecutive rows x 32 B,
+//     which the swizzle spreads over all 64 banks.
+//   * Group r owns rows 128 r ..; waves: PBN = 256 -> 128 x 64 (32 accumulators), 128 -> 2 x 2 of 64 x 64 (16),
+//     64 -> 4 x 1 of 32 x 64 (8).  Split-K over pixels into the fp32 slab (k_gemm_splitk_reduce remaps it).
+//   * Out-of-range chunks (M / N edges, K tail, conv padding) load through an offset past the descriptor: zeros.
+// ---------------------------------------------------------------------------------------------------------
+constexpr int WP_BM = 256, WP_NT = 512, WP_KT = 64;
+template <int PBN>
+struct WpTile {
+  static constexpr int WMG = PBN == 256 ? 1 : (PBN == 128 ? 2 : 4), WNG = 4 / WMG, MF = 8 / WMG;
+  static constexpr int R_RB = WP_BM * 2, C_RB = PBN * 2;            // LDS row bytes: row side | column side
+  static constexpr int R_CPR = R_RB / 16, C_CPR = C_RB / 16;        // 16-B chunks per row
+  static constexpr int R_RPI = 1024 / R_RB, C_RPI = 1024 / C_RB;    // rows per wave DMA instruction
+  static constexpr int R_BYTES = WP_KT * R_RB, C_BYTES = WP_KT * C_RB, BUF = R_BYTES + C_BYTES, LDS = 2 * BUF;
+  static constexpr int NIR = R_BYTES / 16 / WP_NT, NIC = C_BYTES / 16 / WP_NT;  // DMA per thread and K-tile
+  static_assert(NIR * WP_NT * 16 == R_BYTES && NIC * WP_NT * 16 == C_BYTES, "wgrad pp staging");
+};
+template <int RB>
+__device__ __forceinline__ int wp_swz(int r) { return RB >= 256 ? 2 * (r & 7) : 2 * ((r >> 1) & 3); }
+template <int RB>
+__device__ __forceinline__ int wp_off(int r, int colbyte) {
+  return r * RB + ((((colbyte >> 4) ^ wp_swz<RB>(r)) << 4) | (colbyte & 15));
+}
+
+// One operand side of k_wgrad_pp: NI DMA slots per thread and K-tile (fixed tile row and logical chunk each), plain
+// pixel-major rows (offset stepped by 64 rows per tile) or the implicit im2col of an NHWC input (pixel decode
+// stepped by 64 pixels per tile: k_wgrad's incremental decode, no division in the loop).
+template <int NI, int RB, int RPI>
+struct WpSide {
+  unsigned off[NI];
+  int row[NI], img[NI], oh[NI], ow[NI], kh[NI], kw[NI], cc[NI];
+  __device__ __forceinline__ void init(const GemmArgs& g, bool implicit, int e0, int extent, int ld, int k_begin,
+                                       int wave, int lane) {
+    constexpr int CPR = RB / 16;
+#pragma unroll
+    for (int i = 0; i < NI; ++i) {
+      const int r = (wave * NI + i) * RPI + lane / CPR, c = (lane % CPR) ^ wp_swz<RB>(r);
+      const int e = e0 + 8 * c;  // first channel (GEMM index) of this lane's chunk
+      row[i] = r;
+      img[i] = oh[i] = ow[i] = kh[i] = kw[i] = cc[i] = 0;
+      if (implicit) {
+        const int ee = e < extent ? e : 0, tap = ee / g.cC;
+        cc[i] = e < extent ? ee - tap * g.cC : -1;  // -1: past the extent (never valid)
+        kh[i] = tap / g.cKW;
+        kw[i] = tap - kh[i] * g.cKW;
+        const float inv_wo = 1.f / (float)g.cWo, inv_ho = 1.f / (float)g.cHo;
+        const int t = fdivmod(min(k_begin + r, g.K - 1), g.cWo, inv_wo, ow[i]);
+        img[i] = fdivmod(t, g.cHo, inv_ho, oh[i]);
+        off[i] = 0u;
+      } else {
+        off[i] = e < extent ? (unsigned)((long long)(k_begin + r) * ld * 2 + e * 2) : 0x80000000u;
+      }
+    }
+  }
+  __device__ __forceinline__ void issue(const GemmArgs& g, bool implicit, __amdgpu_buffer_rsrc_t rs, char* lds,
+                                        int kt, int k0, int k_end, int ld, int wave, int d_img, int d_oh, int d_ow) {
+    constexpr unsigned OOB = 0x80000000u;
+    if (implicit) {
+#pragma unroll
+      for (int i = 0; i < NI; ++i) {
+        const int h = oh[i] * g.cS - g.cP + kh[i], w = ow[i] * g.cS - g.cP + kw[i];
+        const bool ok = cc[i] >= 0 && k0 + row[i] < k_end && h >= 0 && h < g.cH && w >= 0 && w < g.cW;
+        blds16(rs, lds + (wave * NI + i) * 1024, ok ? (unsigned)((((img[i] * g.cH + h) * g.cW + w) * g.cC + cc[i]) * 2) : OOB,
+               0u);
+        ow[i] += d_ow;
+        const int c1 = ow[i] >= g.cWo;
+        ow[i] -= c1 ? g.cWo : 0;
+        oh[i] += d_oh + c1;
+        const int c2 = oh[i] >= g.cHo;
+        oh[i] -= c2 ? g.cHo : 0;
+        img[i] += d_img + c2;
+      }
+    } else {
+      const unsigned so = (unsigned)((long long)kt * WP_KT * ld * 2);
+#pragma unroll
+      for (int i = 0; i < NI; ++i) blds16(rs, lds + (wave * NI + i) * 1024, k0 + row[i] < k_end ? off[i] : OOB, so);
+    }
+  }
+};
+
+template <int PBN, bool SW>
+__global__ void __launch_bounds__(WP_NT) k_wgrad_pp(GemmArgs g) {
+  using T = WpTile<PBN>;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int RX = SW ? g.N : g.M, CX = SW ? g.M : g.N;  // extents of the row side / column side
+  const int ntm = (RX + WP_BM - 1) / WP_BM, ntn = (CX + PBN - 1) / PBN, ntiles = ntm * ntn;
+  const int work = xcd_remap(blockIdx.x, ntiles * g.splits);
+  const int tile = work % ntiles, ksplit = work / ntiles;
+  const int r0t = (tile / ntn) * WP_BM, c0t = (tile % ntn) * PBN;
+  const int k_begin = ksplit * g.k_per_split, k_end = min(g.K, k_begin + g.k_per_split);
+  const int nk = (k_end - k_begin + WP_KT - 1) / WP_KT;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, wr = wave >> 2;
+  const int wi = (wave & 3) / T::WNG, wj = (wave & 3) % T::WNG;
+  const int wrow = wr * 128 + wi * (128 / T::WMG), wcol = wj * 64;  // this wave's sub-tile in the 256 x PBN tile
+  const bool conv = g.conv == 2;  // B (the row side when SW) is the implicit im2col of an NHWC input
+  const long long a_bytes = (long long)g.K * g.lda * 2;
+  const long long b_bytes = conv ? (long long)g.cN * g.cH * g.cW * g.cC * 2 : (long long)g.K * g.ldb * 2;
+  const __amdgpu_buffer_rsrc_t ars = __builtin_amdgcn_make_buffer_rsrc((void*)g.A, (short)0, (int)a_bytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t brs = __builtin_amdgcn_make_buffer_rsrc((void*)g.B, (short)0, (int)b_bytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rrs = SW ? brs : ars, crs = SW ? ars : brs;
+  const int rld = SW ? g.ldb : g.lda, cld = SW ? g.lda : g.ldb;
+  const bool r_imp = SW && conv, c_imp = !SW && conv;
+  int d_img = 0, d_oh = 0, d_ow = 0;
+  if (conv) {
+    const int hw = g.cHo * g.cWo, rem = WP_KT % hw;
+    d_img = WP_KT / hw;
+    d_oh = rem / g.cWo;
+    d_ow = rem - d_oh * g.cWo;
+  }
+  WpSide<T::NIR, T::R_RB, T::R_RPI> rside;
+  WpSide<T::NIC, T::C_RB, T::C_RPI> cside;
+  rside.init(g, r_imp, r0t, RX, rld, k_begin, wave, lane);
+  cside.init(g, c_imp, c0t, CX, cld, k_begin, wave, lane);
+  // this thread's LDS-DMA of K-tile kt into buffer kt & 1 (every thread issues its tiles in increasing order)
+  auto issue = [&](int kt) {
+    const int k0 = k_begin + kt * WP_KT;
+    char* lr = smem + (kt & 1) * T::BUF;
+    rside.issue(g, r_imp, rrs, lr, kt, k0, k_end, rld, wave, d_img, d_oh, d_ow);
+    cside.issue(g, c_imp, crs, lr + T::R_BYTES, kt, k0, k_end, cld, wave, d_img, d_oh, d_ow);
+  };
+  auto bar = [] {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+  };
+
+  constexpr int MF = T::MF;
+  f32x4 acc[MF][4];
+#pragma unroll
+  for (int m = 0; m < MF; ++m)
+#pragma unroll
+    for (int n = 0; n < 4; ++n) acc[m][n] = f32x4{0.f, 0.f, 0.f, 0.f};
+  s16x8 af[MF], bfr[4];
+  const int grp = lane >> 4, q = (lane >> 2) & 3, p4 = (lane & 3) * 4;
+  auto load_frags = [&](int kt, int h) {
+    const char* lr = smem + (kt & 1) * T::BUF;
+    const char* lc = lr + T::R_BYTES;
+    const int r0 = h * 32 + 4 * grp + q;  // high half: r0 + 16 (same swizzle)
+#pragma unroll
+    for (int m = 0; m < MF; ++m) {
+      const char* pa = lr + wp_off<T::R_RB>(r0, (wrow + m * 16 + p4) * 2);
+      const s16x4 lo = lds_tr16(pa), hi = lds_tr16(pa + 16 * T::R_RB);
+      af[m] = s16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+    }
+#pragma unroll
+    for (int n = 0; n < 4; ++n) {
+      const char* pb = lc + wp_off<T::C_RB>(r0, (wcol + n * 16 + p4) * 2);
+      const s16x4 lo = lds_tr16(pb), hi = lds_tr16(pb + 16 * T::C_RB);
+      bfr[n] = s16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+    }
+  };
+  auto mfmas = [&] {
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int m = 0; m < MF; ++m)
+#pragma unroll
+      for (int n = 0; n < 4; ++n) acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[m], bfr[n], acc[m][n], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+  };
+
+  // the k_gemm_pp schedule (its comment block has the interval bookkeeping)
+  if (nk > 0) issue(0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  bar();
+  if (wr == 0) {
+#pragma unroll 1
+    for (int st = 0; st < 2 * nk; ++st) {
+      const int kt = st >> 1, h = st & 1;
+      if (h == 0 && kt + 1 < nk) issue(kt + 1);
+      load_frags(kt, h);
+      bar();
+      mfmas();
+      if (h == 1) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      bar();
+    }
+    bar();
+  } else {
+    if (nk > 1) issue(1);
+    bar();
+#pragma unroll 1
+    for (int st = 0; st < 2 * nk; ++st) {
+      const int kt = st >> 1, h = st & 1;
+      load_frags(kt, h);
+      if (h == 1) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      bar();
+      if (h == 1 && kt + 2 < nk) issue(kt + 2);
+      mfmas();
+      bar();
+    }
+  }
+
+  // slab [split][M][N] straight from the accumulators: fragment (row-side 4 (lane >> 4) + e, column-side lane & 15)
+#pragma unroll
+  for (int m = 0; m < MF; ++m)
+#pragma unroll
+    for (int n = 0; n < 4; ++n) {
+      const int cidx = c0t + wcol + n * 16 + (lane & 15), ridx = r0t + wrow + m * 16 + (lane >> 4) * 4;
+      if constexpr (SW) {  // (m = cidx, n = ridx .. ridx + 3): one 16-B store (N % 8 == 0)
+        if (cidx < g.M && ridx < g.N) *(f32x4*)(g.ws + ((size_t)ksplit * g.M + cidx) * g.N + ridx) = acc[m][n];
+      } else {
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          if (ridx + e < g.M && cidx < g.N) g.ws[((size_t)ksplit * g.M + ridx + e) * g.N + cidx] = acc[m][n][e];
+      }
+    }
+}
+
 }  // namespace ops
 }  // namespace dca

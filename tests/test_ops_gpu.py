@@ -530,6 +530,46 @@ def test_wgrad_transposed_read_kernel(gpu, M, N, K, splits):
     assert _rel(out, ref) < 1e-5, _rel(out, ref)
 
 
+@pytest.mark.parametrize("M,N,K,splits", [(256, 256, 4096, 4), (512, 384, 3000, 7), (264, 136, 777, 1),
+                                          (1024, 256, 50176, 64), (256, 1160, 200, 1), (256, 64, 4096, 4),
+                                          (64, 576, 5000, 8), (128, 1152, 3000, 5), (64, 264, 777, 1),
+                                          (120, 512, 640, 2)])
+def test_wgrad_pingpong_kernel(gpu, M, N, K, splits):
+    """Weight gradients on k_wgrad_pp (the larger of M / N along the 256-row side, the smaller as a 256 / 128 / 64
+    column tile; LDS-DMA with swizzled source chunks, transposed fragment reads, two ping-pong wave groups):
+    ragged M, N, K tails, split-K and the swapped (M < 256) form, vs fp32 torch."""
+    from distributeddataparallel_cifar10_amd.ops import gemm
+    g = torch.Generator(device=gpu).manual_seed(M * 7 + N + K)
+    a = _bf(torch.randn(K, M, device=gpu, generator=g))
+    b = _bf(torch.randn(K, N, device=gpu, generator=g) * torch.linspace(0.5, 2.0, N, device=gpu))
+    ref = a.float().t() @ b.float()
+    out = gemm(a, b, ta=True, tb=True, splits=splits)
+    assert _rel(out, ref) < 1e-5, _rel(out, ref)
+
+
+@pytest.mark.parametrize("n,h,c,co,k,s,p", [(3, 13, 64, 256, 3, 1, 1), (2, 14, 128, 512, 3, 2, 1),
+                                            (2, 12, 256, 264, 1, 2, 0), (4, 7, 512, 256, 3, 1, 1),
+                                            (3, 14, 64, 64, 3, 1, 1), (2, 15, 128, 128, 3, 2, 1),
+                                            (2, 20, 8, 64, 7, 2, 3)])
+def test_wgrad_pingpong_implicit_conv(gpu, n, h, c, co, k, s, p):
+    """Implicit-im2col weight gradients (conv = 2) on k_wgrad_pp, as its column side (Cout >= 256) or its row side
+    (swapped: Cout 64 / 128, incl. the 8-channel 7x7/2 stem): taps straddling tiles, zero padding, stride 2, ragged
+    pixel counts, written into torch's [Cout, Cin, KH, KW] layout."""
+    from distributeddataparallel_cifar10_amd.ops import functional as F
+    g = torch.Generator(device=gpu).manual_seed(n * h + c + co)
+    x = _bf(torch.randn(n, h, h, c, device=gpu, generator=g))
+    w = torch.empty(co, c, k, k, device=gpu)
+    geo = F._geom(x, w, s, p)
+    M = n * geo.Ho * geo.Wo
+    dy = _bf(torch.randn(M, co, device=gpu, generator=g))
+    ref = torch.nn.grad.conv2d_weight(x.float().permute(0, 3, 1, 2), w.shape,
+                                      dy.float().view(n, geo.Ho, geo.Wo, co).permute(0, 3, 1, 2), stride=s, padding=p)
+    out = torch.empty_like(w)
+    F.gemm(dy, x, ta=True, conv=2, geom=geo, mnk=(co, geo.K, M), splits=F._wgrad_splits(co, geo.K, M), out=out,
+           wperm=(c, c, k * k))
+    assert _rel(out, ref) < 1e-5, _rel(out, ref)
+
+
 def test_main_no_ddp_resnet50_auto_ops(gpu):
     """--model resnet50 on a GPU resolves to the ops engine (HIP kernels, packed weights, gradient sinks)."""
     import subprocess
