@@ -130,6 +130,13 @@ inline bool getenv_wgrad_pp() {
   static const bool v = getenv_flag("DCA_OPS_WGRAD_PP");
   return v;
 }
+inline bool getenv_wgrad_pp_all() {  // DCA_OPS_WGRAD_PP_ALL=1: also the forms the shape rule leaves on k_wgrad
+  static const bool v = [] {
+    const char* e = getenv("DCA_OPS_WGRAD_PP_ALL");
+    return e && e[0] == '1';
+  }();
+  return v;
+}
 inline bool getenv_wgrad_ok() {
   static const int v = [] {
     const char* e = getenv("DCA_OPS_WGRAD");
@@ -270,16 +277,22 @@ int dca_ops_gemm(const GemmArgs* a, void* stream) {
   if (wgrad) {
     REQUIRE(g.conv != 2 || (long)g.cN * g.cHo * g.cWo < (1L << 24), "gemm: weight-gradient pixel count >= 2^24");
     // the ping-pong kernel: the larger of M (output channels) / N (input channels x taps) along its 256-row side
-    // (SW: N), the smaller one as a 256 / 128 / 64 column tile; both >= 64 and the larger >= 256; 32-bit operand
-    // offsets, 16-B aligned rows.  The split count is cut to about one workgroup per CU (one fits per CU)
+    // (SW: N), the smaller one as a 256 / 128 column tile; 32-bit operand offsets, 16-B aligned rows.  The split
+    // count is cut to about one workgroup per CU (one fits per CU).  Shape rule from bench/wgrad_bench.py at batch
+    // 256 (profiles/wgrad_pp_r3.log): M >= 256, N >= 128 -> 0.71-0.92x the k_wgrad time (3x3 256x2304x50176 123.4
+    // -> 92.1 us); swapped only for plain (1x1) operands with 64 < M <= 128 (0.89-0.92x); the swapped implicit 3x3
+    // convolutions (1.5-1.7x) and the 64-wide column tile (1.0-1.7x) measured slower and stay on k_wgrad
     const long long a_by = (long long)g.K * g.lda * 2;
     const long long b_by = g.conv == 2 ? (long long)g.cN * g.cH * g.cW * g.cC * 2 : (long long)g.K * g.ldb * 2;
     const bool sw = g.M < 256;
     const int big = sw ? g.N : g.M, small = sw ? g.M : g.N;
-    if (getenv_wgrad_pp() && big >= 256 && small >= 64 && !(sw && small > 128) && a_by < (1LL << 31) &&
-        b_by < (1LL << 31) && ((uintptr_t)g.A & 15) == 0 && ((uintptr_t)g.B & 15) == 0 &&
-        (g.conv != 2 || g.cC % 8 == 0)) {
-      const int pbn = small <= 64 ? 64 : ((small % 256 == 0 || small > 1024) ? 256 : 128);
+    const bool all = getenv_wgrad_pp_all();  // every form the kernel has (tests / measurements)
+    const bool pp_shape = all ? (big >= 256 && small >= 64 && !(sw && small > 128))
+                              : (sw ? (g.conv != 2 && small > 64 && small <= 128 && big >= 256)
+                                    : (big >= 256 && small >= 128));
+    if (getenv_wgrad_pp() && pp_shape && a_by < (1LL << 31) && b_by < (1LL << 31) && ((uintptr_t)g.A & 15) == 0 &&
+        ((uintptr_t)g.B & 15) == 0 && (g.conv != 2 || g.cC % 8 == 0)) {
+      const int pbn = small <= 64 ? 64 : (sw ? 128 : ((small % 256 == 0 || small > 1024) ? 256 : 128));
       const long tiles = (long)((big + WP_BM - 1) / WP_BM) * ((small + pbn - 1) / pbn);
       const long want = std::max<long>(1, (256 + tiles - 1) / tiles);
       if (want < g.splits) {  // fewer, longer splits (the slab was sized for g.splits: smaller is fine)
@@ -289,13 +302,15 @@ int dca_ops_gemm(const GemmArgs* a, void* stream) {
         g.splits = (g.K + kps - 1) / kps;
       }
       const dim3 grid((unsigned)(tiles * g.splits)), blk(WP_NT);
-      if (sw) {
-        if (pbn == 64) hipLaunchKernelGGL((k_wgrad_pp<64, true>), grid, blk, WpTile<64>::LDS, st, g);
-        else hipLaunchKernelGGL((k_wgrad_pp<128, true>), grid, blk, WpTile<128>::LDS, st, g);
-      } else {
-        if (pbn == 256) hipLaunchKernelGGL((k_wgrad_pp<256, false>), grid, blk, WpTile<256>::LDS, st, g);
-        else if (pbn == 128) hipLaunchKernelGGL((k_wgrad_pp<128, false>), grid, blk, WpTile<128>::LDS, st, g);
+      if (pbn == 64) {
+        if (sw) hipLaunchKernelGGL((k_wgrad_pp<64, true>), grid, blk, WpTile<64>::LDS, st, g);
         else hipLaunchKernelGGL((k_wgrad_pp<64, false>), grid, blk, WpTile<64>::LDS, st, g);
+      } else if (sw) {
+        hipLaunchKernelGGL((k_wgrad_pp<128, true>), grid, blk, WpTile<128>::LDS, st, g);
+      } else if (pbn == 256) {
+        hipLaunchKernelGGL((k_wgrad_pp<256, false>), grid, blk, WpTile<256>::LDS, st, g);
+      } else {
+        hipLaunchKernelGGL((k_wgrad_pp<128, false>), grid, blk, WpTile<128>::LDS, st, g);
       }
       hipLaunchKernelGGL(k_gemm_splitk_reduce, dim3(grid_for((long)g.M * g.N, RED_EL, 4096)), dim3(256), 0, st, g);
       OPCK(hipGetLastError());

@@ -570,6 +570,21 @@ def test_wgrad_pingpong_implicit_conv(gpu, n, h, c, co, k, s, p):
     assert _rel(out, ref) < 1e-5, _rel(out, ref)
 
 
+def test_wgrad_pingpong_all_forms(gpu):
+    """Every k_wgrad_pp form (DCA_OPS_WGRAD_PP_ALL=1, read once per process: run in a child), including the 64-wide
+    column tile and the swapped implicit-conv row side that the default shape rule leaves on k_wgrad, vs torch."""
+    import json
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([sys.executable, os.path.join(root, "tests", "_wgrad_pp_check.py")], capture_output=True,
+                       text=True, env=dict(os.environ, DCA_OPS_WGRAD_PP_ALL="1"), timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    res = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
+    bad = {k: v for k, v in res.items() if not v < 1e-5}
+    assert not bad, (bad, res)
+
+
 def test_main_no_ddp_resnet50_auto_ops(gpu):
     """--model resnet50 on a GPU resolves to the ops engine (HIP kernels, packed weights, gradient sinks)."""
     import subprocess
