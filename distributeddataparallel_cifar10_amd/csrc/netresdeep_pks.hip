@@ -214,15 +214,23 @@ __device__ __forceinline__ f32x4 conv_row(const char* xr, const char* wt, const 
   return acc;
 }
 
+// a + a[lane ^ 16], then + the same of lane ^ 32: the value every lane of a 16-lane column group ends with, summed in
+// the order of two __shfl_xor steps (bitwise the same; fp addition is commutative) but on the gfx950 cross-row VALU
+// swaps (v_permlane16_swap / v_permlane32_swap) instead of two dependent ds_bpermute LDS round trips
+__device__ __forceinline__ float xsum_rows(float a) {
+  const auto p = __builtin_amdgcn_permlane16_swap(__float_as_uint(a), __float_as_uint(a), false, false);
+  a = __uint_as_float(p[0]) + __uint_as_float(p[1]);
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(a), __float_as_uint(a), false, false);
+  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+
 // per-workgroup channel sums of per-thread partials (a, b: channel 16h + c of wave 4h + w), delivered to the
 // publishing threads: thread t < 64 returns slot t (t < 32: sum of a for channel t, else sum of b for channel
 // t - 32).  One LDS barrier.
 __device__ __forceinline__ float wg_csum(float a, float b, float* cred) {
   const int t = threadIdx.x, wv = t >> 6, lane = t & 63, c = lane & 15;
-  a += __shfl_xor(a, 16);
-  a += __shfl_xor(a, 32);
-  b += __shfl_xor(b, 16);
-  b += __shfl_xor(b, 32);
+  a = xsum_rows(a);
+  b = xsum_rows(b);
   float* r = cred + NW * 64;  // [NW][32], disjoint from the sweep combine area
   if (lane < 16) {
     r[wv * 32 + c] = a;
@@ -361,8 +369,7 @@ __device__ __forceinline__ void xchg_wait(const Args& pa, int round, int epoch, 
   else sweep_wait<8>(pa, round, wv, lane, G, btag, sv, halo, Lsrc, which, h, tag, hv);
 #pragma unroll
   for (int e = 0; e < 4; ++e) {  // the four 16-lane groups read different workgroups
-    sv[e] += __shfl_xor(sv[e], 16);
-    sv[e] += __shfl_xor(sv[e], 32);
+    sv[e] = xsum_rows(sv[e]);
   }
   if (lane < 16) *(f32x4*)(cred + wv * 64 + 4 * lane) = f32x4{sv[0], sv[1], sv[2], sv[3]};
 }
