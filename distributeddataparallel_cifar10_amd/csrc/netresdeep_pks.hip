@@ -224,6 +224,17 @@ __device__ __forceinline__ float xsum_rows(float a) {
   return __uint_as_float(r[0]) + __uint_as_float(r[1]);
 }
 
+// sum over the 16 lanes of a row, every lane ending with it: the xor-1 / 2 / 4 / 8 butterfly of __shfl_xor (the same
+// pairings, so bitwise the same sums) on DPP lane moves -- quad_perm [1,0,3,2], [2,3,0,1], row_half_mirror,
+// row_mirror -- instead of four dependent ds_bpermute round trips
+__device__ __forceinline__ float xsum_row16(float a) {
+  a += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(a), 0xB1, 0xF, 0xF, false));
+  a += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(a), 0x4E, 0xF, 0xF, false));
+  a += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(a), 0x141, 0xF, 0xF, false));
+  a += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(a), 0x140, 0xF, 0xF, false));
+  return a;
+}
+
 // per-workgroup channel sums of per-thread partials (a, b: channel 16h + c of wave 4h + w), delivered to the
 // publishing threads: thread t < 64 returns slot t (t < 32: sum of a for channel t, else sum of b for channel
 // t - 32).  One LDS barrier.
@@ -231,17 +242,22 @@ __device__ __forceinline__ float wg_csum(float a, float b, float* cred) {
   const int t = threadIdx.x, wv = t >> 6, lane = t & 63, c = lane & 15;
   a = xsum_rows(a);
   b = xsum_rows(b);
-  float* r = cred + NW * 64;  // [NW][32], disjoint from the sweep combine area
+  // [2 halves][32: a | b of 16 channels][RS rows], disjoint from the sweep combine area: a publishing thread reads
+  // its RS row partials as one 16-B LDS read (summed in row order)
+  float* r = cred + NW * 64;
   if (lane < 16) {
-    r[wv * 32 + c] = a;
-    r[wv * 32 + 16 + c] = b;
+    r[((wv / RS) * 32 + c) * RS + wv % RS] = a;
+    r[((wv / RS) * 32 + 16 + c) * RS + wv % RS] = b;
   }
   lds_barrier();
   float v = 0.f;
   if (t < 64) {
     const int ch = t & 31, hh = ch >> 4, off = (t >> 5) * 16 + (ch & 15);
-#pragma unroll
-    for (int w = 0; w < RS; ++w) v += r[(4 * hh + w) * 32 + off];
+    const f32x4 x = *(const f32x4*)(r + (hh * 32 + off) * RS);
+    v = x[0];
+    v += x[1];
+    v += x[2];
+    v += x[3];
   }
   return v;
 }
@@ -355,7 +371,8 @@ __device__ __forceinline__ void sweep_wait(const Args& pa, int round, int wv, in
   }
 }
 // All-to-all BN exchange wait + (halo waves) the neighbour's boundary row.  On return cred[0 .. NW*64) holds every
-// wave's partial totals (the caller's barrier makes them visible): tot(slot) = sum_k cred[k * 64 + slot].
+// wave's partial totals slot-major (the caller's barrier makes them visible): tot(slot) = sum_k cred[slot * NW + k],
+// two 16-B LDS reads per slot.
 __device__ __forceinline__ void xchg_wait(const Args& pa, int round, int epoch, int G, float* cred, bool halo,
                                           int Lsrc, int which, int h, float (&hv)[4]) {
   const int t = threadIdx.x, lane = t & 63;
@@ -371,12 +388,22 @@ __device__ __forceinline__ void xchg_wait(const Args& pa, int round, int epoch, 
   for (int e = 0; e < 4; ++e) {  // the four 16-lane groups read different workgroups
     sv[e] = xsum_rows(sv[e]);
   }
-  if (lane < 16) *(f32x4*)(cred + wv * 64 + 4 * lane) = f32x4{sv[0], sv[1], sv[2], sv[3]};
+  if (lane < 16) {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) cred[(4 * lane + e) * NW + wv] = sv[e];
+  }
 }
 __device__ __forceinline__ float slot_total(const float* cred, int slot) {
-  float a = 0.f;
-#pragma unroll
-  for (int k = 0; k < NW; ++k) a += cred[k * 64 + slot];
+  static_assert(NW == 8 && RS == 4, "slot-major combine layout: 8 waves, 4 rows");
+  const f32x4 u = *(const f32x4*)(cred + slot * NW), w = *(const f32x4*)(cred + slot * NW + 4);
+  float a = u[0];  // wave order, as the per-wave sums were added before
+  a += u[1];
+  a += u[2];
+  a += u[3];
+  a += w[0];
+  a += w[1];
+  a += w[2];
+  a += w[3];
   return a;
 }
 
@@ -1219,10 +1246,7 @@ __global__ void __launch_bounds__(NTH) k_pks_step(Ctx cx, Args pa, RedAr ra) {
                                  : __uint_as_float((unsigned)((const unsigned short*)w1l)[j * PL::W1S + u] << 16);
         a += wvv * pl[u];
       }
-      a += __shfl_xor(a, 1);
-      a += __shfl_xor(a, 2);
-      a += __shfl_xor(a, 4);
-      a += __shfl_xor(a, 8);
+      a = xsum_row16(a);
       if (k == 0) hp[j] = a;
     }
     lds_barrier();

@@ -745,6 +745,14 @@ int dca_ops_nchw_to_nhwc8(const float* x, void* y, int N, int C, long HW, void* 
   return 0;
 }
 
+int dca_ops_nchw_to_s2d16(const float* x, void* y, int N, int C, int H, int W, int Hs, int Ws, int P, void* stream) {
+  REQUIRE(C > 0 && C <= 4 && P >= 0 && Hs > 0 && Ws > 0, "nchw_to_s2d16: 1..4 channels");
+  hipLaunchKernelGGL(k_nchw_to_s2d16, dim3(grid_for((long)N * Hs * Ws)), dim3(256), 0, (hipStream_t)stream, x,
+                     (bf16_t*)y, N, C, H, W, Hs, Ws, P);
+  OPCK(hipGetLastError());
+  return 0;
+}
+
 int dca_ops_pack_gather(const void* descs, int nd, int blocks, void* stream) {
   REQUIRE(nd > 0 && blocks > 0, "pack_gather: empty");
   hipLaunchKernelGGL(k_pack_gather, dim3(blocks, nd), dim3(256), 0, (hipStream_t)stream, (const GatherDesc*)descs);

@@ -936,8 +936,39 @@ __global__ void __launch_bounds__(256) k_nchw_to_nhwc8(const float* __restrict__
   }
 }
 
-// Gathered bf16 copies of fp32 weights: out[i] = bf16(w[idx[i]]) -- the per-parity-class input-gradient matrices
-// of strided convolutions (index tables built once on the host).  grid (blocks, descriptors).
+// Space-to-depth input of a stride-2 stem convolution (C <= 4 channels): y[n][Y][X][(2 ph + pw) C + c] =
+// x[n][c][2Y + ph - P][2X + pw - P] (zero outside the image; channels 4C .. 15 zero), 16 bf16 channels per pixel.
+// A KxK / 2 conv with padding P - 1 over x is then a ceil((K+1)/2)^2 stride-1 conv with no padding over y (ops
+// functional.stem_s2d_weight_index): ResNet's 7x7/2 stem becomes 4x4 taps x 16 channels = K 256 instead of
+// 7 x 7 x 8 = 392, with two 16-B chunks per tap instead of one.
+__global__ void __launch_bounds__(256) k_nchw_to_s2d16(const float* __restrict__ x, bf16_t* __restrict__ y, int N,
+                                                       int C, int H, int W, int Hs, int Ws, int P) {
+  const long total = (long)N * Hs * Ws;
+  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < total; i += (long)gridDim.x * 256) {
+    const long n = i / ((long)Hs * Ws);
+    const int rem = (int)(i - n * Hs * Ws), Y = rem / Ws, X = rem - Y * Ws;
+    float v[16];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) v[k] = 0.f;
+#pragma unroll
+    for (int ph = 0; ph < 2; ++ph)
+#pragma unroll
+      for (int pw = 0; pw < 2; ++pw) {
+        const int h = 2 * Y + ph - P, w = 2 * X + pw - P;
+        if (h < 0 || h >= H || w < 0 || w >= W) continue;
+#pragma unroll
+        for (int c = 0; c < 4; ++c)
+          if (c < C) v[(2 * ph + pw) * C + c] = x[((n * C + c) * H + h) * W + w];
+      }
+    uint4* o = (uint4*)(y + i * 16);
+    o[0] = pack8(v);
+    o[1] = pack8(v + 8);
+  }
+}
+
+// Gathered bf16 copies of fp32 weights: out[i] = bf16(w[idx[i]]), 0 where idx[i] < 0 -- the per-parity-class
+// input-gradient matrices of strided convolutions and the space-to-depth stem matrix (index tables built once on
+// the host).  grid (blocks, descriptors).
 struct GatherDesc {
   const float* w;
   const int* idx;
@@ -946,7 +977,10 @@ struct GatherDesc {
 };
 __global__ void __launch_bounds__(256) k_pack_gather(const GatherDesc* __restrict__ descs) {
   const GatherDesc d = descs[blockIdx.y];
-  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < d.n; i += (long)gridDim.x * 256) d.out[i] = f2bf_rne(d.w[d.idx[i]]);
+  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < d.n; i += (long)gridDim.x * 256) {
+    const int k = d.idx[i];
+    d.out[i] = f2bf_rne(k >= 0 ? d.w[k] : 0.f);
+  }
 }
 
 }  // namespace ops

@@ -88,6 +88,7 @@ def _declare(lib):
     lib.dca_ops_pack_gather.argtypes = [c_void_p, c_int, c_int, c_void_p]
     lib.dca_ops_gather_desc_size.restype = c_int
     lib.dca_ops_nchw_to_nhwc8.argtypes = [c_void_p, c_void_p, c_int, c_int, c_long, c_void_p]
+    lib.dca_ops_nchw_to_s2d16.argtypes = [c_void_p, c_void_p] + [c_int] * 7 + [c_void_p]
     return lib
 
 

@@ -231,9 +231,10 @@ class WeightPack:
 
     BLOCKS_PER_LAYER = 256
 
-    def __init__(self, convs, fp8_convs=()):
+    def __init__(self, convs, fp8_convs=(), s2d_convs=()):
         self.convs = list(convs)
         fp8_ids = {id(c) for c in fp8_convs}
+        s2d_ids = {id(c) for c in s2d_convs}
         self.entries = {}
         n_fp8 = sum(1 for c in self.convs if id(c) in fp8_ids)
         dev = self.convs[0].weight.device
@@ -255,6 +256,12 @@ class WeightPack:
                 e["q8"] = torch.empty(co, kp, dtype=torch.uint8, device=dev)
                 e["amax"] = self.amax[j:j + 1]
                 j += 1
+            e["s2d"] = None
+            if id(c) in s2d_ids:  # space-to-depth stem: [Co, 4 * 4 * 16] gathered from w (no dgrad: network input)
+                idx_f, idx_b = stem_s2d_index(c)
+                e.update(ci_pad=S2D_C, kp=S2D_TAPS * S2D_TAPS * S2D_C, dgrad=None, classes=None, q8=None, amax=None,
+                         fwd=torch.empty(co, S2D_TAPS * S2D_TAPS * S2D_C, dtype=torch.bfloat16, device=dev),
+                         s2d=dict(shape=(co, S2D_C, S2D_TAPS, S2D_TAPS), fwd_idx=idx_f, back_idx=idx_b))
             self.entries[id(c)] = e
         self.n_fp8 = n_fp8
         self._key = None
@@ -298,9 +305,10 @@ class WeightPack:
 
     def pack(self) -> None:
         key = tuple(c.weight.data_ptr() for c in self.convs)
-        if key != self._key:  # parameters re-pointed (e.g. into a flat DDP buffer): rebuild the descriptors
-            arr = (N.PackDesc * len(self.convs))()
-            for i, c in enumerate(self.convs):
+        packed = [c for c in self.convs if self.entries[id(c)]["s2d"] is None]
+        if key != self._key and packed:  # parameters re-pointed (e.g. into a flat DDP buffer): rebuild descriptors
+            arr = (N.PackDesc * len(packed))()
+            for i, c in enumerate(packed):
                 e = self.entries[id(c)]
                 co, ci, kh, kw = c.weight.shape
                 if not c.weight.is_contiguous():
@@ -315,17 +323,21 @@ class WeightPack:
             host = torch.frombuffer(bytearray(bytes(arr)), dtype=torch.uint8)
             self._descs = host.to(self.amax.device)
             self._key = key
-        N.check(N.lib().dca_ops_pack_weights(N.ptr(self._descs), len(self.convs), self.BLOCKS_PER_LAYER,
-                                             N.ptr(self.amax), self.n_fp8, N.stream(self.amax.device)),
-                "pack_weights")
+        if packed:
+            N.check(N.lib().dca_ops_pack_weights(N.ptr(self._descs), len(packed), self.BLOCKS_PER_LAYER,
+                                                 N.ptr(self.amax), self.n_fp8, N.stream(self.amax.device)),
+                    "pack_weights")
         if key != self._gkey:
-            gl = [(c, cl) for c in self.convs for cl in (self.entries[id(c)]["classes"] or [])]
+            # (weight, index table, output): strided-dgrad parity classes and space-to-depth stem matrices
+            gl = [(c, cl[6], cl[5]) for c in self.convs for cl in (self.entries[id(c)]["classes"] or [])]
+            gl += [(c, e["s2d"]["fwd_idx"], e["fwd"]) for c in self.convs
+                   for e in [self.entries[id(c)]] if e["s2d"] is not None]
             self._n_gather = len(gl)
             if gl:
                 arr = (N.GatherDesc * len(gl))()
-                for i, (c, cl) in enumerate(gl):
-                    arr[i] = N.GatherDesc(w=c.weight.data_ptr(), idx=cl[6].data_ptr(), out=cl[5].data_ptr(),
-                                          n=cl[5].numel())
+                for i, (c, idx, out) in enumerate(gl):
+                    arr[i] = N.GatherDesc(w=c.weight.data_ptr(), idx=idx.data_ptr(), out=out.data_ptr(),
+                                          n=out.numel())
                 self._gdescs = torch.frombuffer(bytearray(bytes(arr)), dtype=torch.uint8).to(self.amax.device)
             self._gkey = key
         if self._n_gather:
@@ -344,6 +356,66 @@ def nchw_to_nhwc8(x: torch.Tensor) -> torch.Tensor:
     y = torch.empty(n, h, w, 8, dtype=torch.bfloat16, device=x.device)
     N.check(N.lib().dca_ops_nchw_to_nhwc8(N.ptr(x), N.ptr(y), n, c, h * w, N.stream(x.device)), "nchw_to_nhwc8")
     return y
+
+
+def stem_s2d_ok(conv: torch.nn.Conv2d) -> bool:
+    """A 7x7 / 2 convolution with padding 3 over <= 4 input channels (the ResNet stem): it runs as a 4x4 stride-1
+    conv over the space-to-depth input (``nchw_to_s2d16``), K = 4 x 4 taps x 16 channels = 256 instead of
+    7 x 7 x 8 = 392."""
+    return (conv.kernel_size == (7, 7) and conv.stride == (2, 2) and conv.padding == (3, 3) and conv.in_channels <= 4
+            and conv.dilation == (1, 1) and conv.groups == 1 and conv.bias is None)
+
+
+S2D_TAPS, S2D_C, S2D_PAD = 4, 16, 4  # 4x4 taps of 16 channels; input shifted by padding + 1 = 4 (even)
+
+
+def stem_s2d_index(conv: torch.nn.Conv2d):
+    """Index tables between the stem weight w [Co, C, 7, 7] and its space-to-depth form w' [Co, 16, 4, 4] (torch
+    layout of the 4x4 conv; GEMM column (i * 4 + j) * 16 + ch of the forward matrix): channel ch = (2 ph + pw) C + c
+    of tap (i, j) holds w[:, c, 2i + ph - 1, 2j + pw - 1] (zero where that lies outside 0..6).
+    Returns (fwd [Co * 256] int32: source element of every forward-matrix entry, -1 for zero;
+             back [C * 49] int64: column of w'.view(Co, 256) that holds (c, kh, kw))."""
+    import numpy as np
+    co, ci = conv.weight.shape[:2]
+    fwd = np.full((co, S2D_TAPS, S2D_TAPS, S2D_C), -1, dtype=np.int32)
+    back = np.zeros((ci, 7, 7), dtype=np.int64)
+    for i in range(S2D_TAPS):
+        for j in range(S2D_TAPS):
+            for ph in (0, 1):
+                for pw in (0, 1):
+                    kh, kw = 2 * i + ph - 1, 2 * j + pw - 1
+                    if not (0 <= kh < 7 and 0 <= kw < 7):
+                        continue
+                    for c in range(ci):
+                        ch = (2 * ph + pw) * ci + c
+                        fwd[:, i, j, ch] = (np.arange(co) * ci + c) * 49 + kh * 7 + kw
+                        back[c, kh, kw] = ch * S2D_TAPS * S2D_TAPS + i * S2D_TAPS + j
+    dev = conv.weight.device
+    return torch.from_numpy(fwd.reshape(-1)).to(dev), torch.from_numpy(back.reshape(-1)).to(dev)
+
+
+def nchw_to_s2d16(x: torch.Tensor) -> torch.Tensor:
+    """Network input NCHW fp32 (C <= 4) -> the space-to-depth NHWC bf16 operand of the 7x7/2/3 stem
+    ([N, Ho + 3, Wo + 3, 16], one kernel).  The input needs no gradient."""
+    _dev_check(x)
+    if x.dtype != torch.float32 or x.dim() != 4 or x.shape[1] > 4:
+        raise ValueError("nchw_to_s2d16: NCHW fp32 with at most 4 channels")
+    x = x.contiguous()
+    n, c, h, w = x.shape
+    ho, wo = (h + 6 - 7) // 2 + 1, (w + 6 - 7) // 2 + 1
+    hs, ws = ho + S2D_TAPS - 1, wo + S2D_TAPS - 1
+    y = torch.empty(n, hs, ws, S2D_C, dtype=torch.bfloat16, device=x.device)
+    N.check(N.lib().dca_ops_nchw_to_s2d16(N.ptr(x), N.ptr(y), n, c, h, w, hs, ws, S2D_PAD, N.stream(x.device)),
+            "nchw_to_s2d16")
+    return y
+
+
+def _s2d_args(w, stride, pad, packed):
+    """(geometry weight, stride, pad) of a conv: its own, or for a space-to-depth stem entry the 4x4 / 1 / 0 conv
+    over the s2d input (a meta tensor carries the shape)."""
+    if packed is not None and packed.get("s2d") is not None:
+        return torch.empty(packed["s2d"]["shape"], device="meta"), 1, 0
+    return w, stride, pad
 
 
 def grad_sink(p: torch.Tensor):
@@ -608,11 +680,12 @@ class _ConvBNAct(torch.autograd.Function):
     def forward(ctx, x, w, r, gamma, beta, running_mean, running_var, stride, pad, eps, momentum, relu, res_mode, fp8,
                 fp8_state, emit, packed, sinks, x_join, r_join, link_out, link_in):
         co = w.shape[0]
-        g = _geom(x, w, stride, pad)
+        wg, stride, pad = _s2d_args(w, stride, pad, packed)
+        g = _geom(x, wg, stride, pad)
         M = g.N * g.Ho * g.Wo
         nparts = (M + 127) // 128
         part = torch.empty(nparts, co, 2, dtype=torch.float32, device=x.device)
-        y, st = _conv_fwd(x, w, None, stride, pad, False, fp8, col_stats=part, shift=running_mean,
+        y, st = _conv_fwd(x, wg, None, stride, pad, False, fp8, col_stats=part, shift=running_mean,
                           fp8_state=fp8_state, packed=packed)
         st["w_master"] = w.detach()
         r = r.contiguous() if r is not None else None
@@ -632,6 +705,7 @@ class _ConvBNAct(torch.autograd.Function):
         if q is not None:
             emit.q, emit.src_ptr = q, out.data_ptr()
         ctx.st = st
+        ctx.wshape = tuple(w.shape)
         ctx.sinks = sinks
         ctx.joins = (x_join, r_join)
         ctx.links = (link_out if relu and res_mode == 0 else None, link_in)
@@ -656,9 +730,17 @@ class _ConvBNAct(torch.autograd.Function):
         x_join, r_join = ctx.joins
         if r_join is not None and dr is not None:  # the identity gradient seeds the block input's shared buffer
             dr = r_join.contribute(dr)
+        s2d = (ctx.st.get("packed") or {}).get("s2d")
         dx, dw = _conv_bwd(dy_conv, ctx.st, ctx.needs_input_grad[0], ctx.needs_input_grad[1] or sw is not None,
-                           sink=sw[0] if sw else None, x_join=x_join if ctx.needs_input_grad[0] else None,
+                           sink=sw[0] if sw and s2d is None else None,
+                           x_join=x_join if ctx.needs_input_grad[0] else None,
                            bnb=link_in if ctx.needs_input_grad[0] else None)
+        if s2d is not None and dw is not None:  # [Co, 16, 4, 4] of the 4x4 conv -> the stem's [Co, C, 7, 7]
+            co = dw.shape[0]
+            dw = dw.view(co, -1).index_select(1, s2d["back_idx"]).view(sw[0].shape if sw else ctx.wshape)
+            if sw:
+                sw[0].add_(dw)
+                dw = None
         if sw:
             sw[1]()
         ctx.st = ctx.sinks = ctx.joins = ctx.links = None
@@ -688,7 +770,8 @@ def conv_bn_act(x, conv: torch.nn.Conv2d, bn: torch.nn.BatchNorm2d, r=None, relu
     if not bn.training:  # inference: running statistics, no autograd
         _check_inference(conv.weight)
         with torch.no_grad():
-            y, _ = _conv_fwd(x, conv.weight, None, conv.stride[0], conv.padding[0], False, False, packed=packed)
+            wg, stride, pad = _s2d_args(conv.weight, conv.stride[0], conv.padding[0], packed)
+            y, _ = _conv_fwd(x, wg, None, stride, pad, False, False, packed=packed)
             return _bn_eval(y, r, bn, relu, res_mode)
     momentum = bn.momentum if bn.track_running_stats else 0.0
     if bn.track_running_stats and not getattr(bn, "_dca_counted", False):

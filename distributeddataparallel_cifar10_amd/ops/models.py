@@ -10,7 +10,8 @@ switches to channels-last bf16 once, and runs:
   -> fc2 (fp32 logits).  fc1's columns are permuted from the reference's NCHW flatten order to NHWC.
 * ResNet-50/101: stem 7x7/2 conv -> BN + ReLU -> 3x3/2 max pool -> bottlenecks (1x1, 3x3, 1x1 convs, each BN
   fused with its ReLU; the last one with the residual add before the ReLU, res_mode 2) -> global average pool
-  -> fc.  The bf16 (and fp8) GEMM operands of all convolutions are rebuilt from the fp32 weights by one
+  -> fc.  The 7x7/2 stem runs as a 4x4 stride-1 conv over a space-to-depth copy of the input (K 256 instead of
+  392).  The bf16 (and fp8) GEMM operands of all convolutions are rebuilt from the fp32 weights by one
   ``WeightPack`` launch per step, and the conv / BN parameter gradients are written straight into the flat
   gradient buffer of ``FlatBucketDDP`` when the model is wrapped in it (``functional.grad_sink``).
   With ``fp8=True`` the 3x3 convolutions (implicit GEMM over an fp8 NHWC copy of the input), fc, and optionally
@@ -40,6 +41,7 @@ class OpsModel(nn.Module):
         self.fp8 = fp8
         self.kind = "netresdeep" if _is_netresdeep(model) else "resnet"
         self._pack = None
+        self._s2d = None
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         if self.kind == "netresdeep":
@@ -53,20 +55,30 @@ class OpsModel(nn.Module):
         this step's fp32 weights (one launch), every BN's num_batches_tracked += 1 (one launch, training only).
         Models that compose the stages themselves (``apps/ppe.py``'s ROI head) call this, then ``stem`` /
         ``blocks`` / ``head``."""
-        if x.shape[1] <= 8 and x.dtype == torch.float32 and not x.requires_grad:
+        if self._pack is None:
+            convs = [m for m in self.module.modules() if isinstance(m, nn.Conv2d)]
+            # the stem (the first conv: ResNet conv1, the PPE model's stem[0]) as a space-to-depth 4x4 conv when it
+            # is 7x7/2/3 over <= 4 channels (DCA_OPS_STEM_S2D=0: the 8-channel NHWC 7x7 implicit GEMM)
+            self._s2d = convs[0] if convs and self.kind == "resnet" and F.stem_s2d_ok(convs[0]) and \
+                os.environ.get("DCA_OPS_STEM_S2D", "1") != "0" else None
+            self._pack = F.WeightPack(convs, [c for c in convs if self._fp8_ok(c)],
+                                      [self._s2d] if self._s2d is not None else [])
+            self._bns = [m for m in self.module.modules()
+                         if isinstance(m, nn.BatchNorm2d) and m.track_running_stats]
+            for m in self._bns:
+                m._dca_counted = True
+        if self._s2d is not None:
+            if x.requires_grad:
+                raise NotImplementedError("OpsModel: no input gradient through the space-to-depth stem "
+                                          "(DCA_OPS_STEM_S2D=0)")
+            h = F.nchw_to_s2d16(x.detach().float())  # one kernel: the stem's space-to-depth operand
+        elif x.shape[1] <= 8 and x.dtype == torch.float32 and not x.requires_grad:
             h = F.nchw_to_nhwc8(x)  # one kernel
         else:
             h = x.permute(0, 2, 3, 1)
             if h.shape[-1] % 8:
                 h = torch.nn.functional.pad(h, (0, 8 - h.shape[-1] % 8))
             h = h.to(torch.bfloat16).contiguous()
-        if self._pack is None:
-            convs = [m for m in self.module.modules() if isinstance(m, nn.Conv2d)]
-            self._pack = F.WeightPack(convs, [c for c in convs if self._fp8_ok(c)])
-            self._bns = [m for m in self.module.modules()
-                         if isinstance(m, nn.BatchNorm2d) and m.track_running_stats]
-            for m in self._bns:
-                m._dca_counted = True
         self._pack.pack()  # every conv's bf16 / fp8 GEMM operands from this step's fp32 weights: one launch
         if self.training and self.module.training and self._bns:  # each BN runs once per step: one launch
             torch._foreach_add_([m.num_batches_tracked for m in self._bns], 1)
@@ -118,7 +130,10 @@ class OpsModel(nn.Module):
                              link_out=link_out, link_in=link_in)
 
     def stem(self, h, conv, bn):
-        """7x7/2 conv -> BN + ReLU -> 3x3/2 max pool (torchvision ResNet stem)."""
+        """7x7/2 conv -> BN + ReLU -> 3x3/2 max pool (torchvision ResNet stem).  ``h`` is what ``begin`` returned:
+        for the space-to-depth stem its [N, Ho + 3, Wo + 3, 16] operand (the conv then runs as 4x4 / 1)."""
+        if self._s2d is not None and conv is not self._s2d:
+            raise ValueError("OpsModel.stem: begin() prepared the space-to-depth input of this model's first conv")
         h = self._conv_bn(h, conv, bn)
         return F.max_pool2d(h, 3, 2, 1)
 
