@@ -71,9 +71,9 @@ template <int P>
 struct Plan {
   static constexpr int NP = P + 1;                       // precision planes: hi (+ lo)
   static constexpr int O_CRED = 0;                       // [2][NW][64] f32 combine scratch
-  static constexpr int O_STAT = O_CRED + 2 * NW * 64 * 4;  // [10][64] f32: mean | invstd
-  static constexpr int O_SCSH = O_STAT + 2560;           // [10][64] f32: BN scale | shift of every block
-  static constexpr int O_MISC = O_SCSH + 2560;           // [1280] f32 step constants (layout: k_pks_step)
+  static constexpr int O_STAT = O_CRED + 2 * NW * 64 * 4;  // [10][32] f32x4: mean, invstd, BN scale, shift of every
+                                                         // block (one 16-B LDS read per channel in the backward)
+  static constexpr int O_MISC = O_STAT + 5120;           // [1280] f32 step constants (layout: k_pks_step)
   static constexpr int O_U = O_MISC + 5120;              // phase union
   // trunk, forward and backward
   static constexpr int WT_PL = 288 * RB;                 // conv weight records [tap][co | ci] x 32
@@ -372,7 +372,8 @@ __device__ __forceinline__ void sweep_wait(const Args& pa, int round, int wv, in
 }
 // All-to-all BN exchange wait + (halo waves) the neighbour's boundary row.  On return cred[0 .. NW*64) holds every
 // wave's partial totals slot-major (the caller's barrier makes them visible): tot(slot) = sum_k cred[slot * NW + k],
-// two 16-B LDS reads per slot.
+// two 16-B LDS reads per slot.  (A conflict-free one-write-per-lane form, wave k of a slot at position k ^ (slot >> 3),
+// sums in a slot-dependent order: it moved the fp32 flip-aware batch-64 check past its 1e-4 bound, so not used.)
 __device__ __forceinline__ void xchg_wait(const Args& pa, int round, int epoch, int G, float* cred, bool halo,
                                           int Lsrc, int which, int h, float (&hv)[4]) {
   const int t = threadIdx.x, lane = t & 63;
@@ -931,8 +932,7 @@ __global__ void __launch_bounds__(NTH) k_pks_step(Ctx cx, Args pa, RedAr ra) {
   const int hsrc = w == 0 ? L - 1 : L + 1;            // ... and whose boundary row it receives
   const int hxrow = w == 0 ? 0 : RS + 1;              // XR / xT row of the received halo
   float* cred = (float*)(smem + PL::O_CRED);
-  float* stat = (float*)(smem + PL::O_STAT);
-  float* scsh = (float*)(smem + PL::O_SCSH);
+  f32x4* stat = (f32x4*)(smem + PL::O_STAT);
   float* misc = (float*)(smem + PL::O_MISC);
   char* U = smem + PL::O_U;
   char* WT = U + PL::U_WT;
@@ -1114,6 +1114,7 @@ __global__ void __launch_bounds__(NTH) k_pks_step(Ctx cx, Args pa, RedAr ra) {
   // the forward) by LDS-DMA right after block 6's exchange, read by
   // fc1 (reduction over features) and its transpose dp (reduction over rows).  The dgrad weights replace the
   // forward ones in WT by LDS-DMA right after block 9's exchange (block 9's conv was WT's last reader).
+  const float gam = misc[320 + ch], bet = misc[352 + ch];  // BN affine of this thread's channel (registers)
   bf16x8 bw[9];  // P = 0: this wave's B fragments of the conv weight (forward here, dgrad in the backward)
   if constexpr (P == 0) load_bfrag(WT, hh, lane, bw);
 #pragma unroll 1
@@ -1157,13 +1158,10 @@ __global__ void __launch_bounds__(NTH) k_pks_step(Ctx cx, Args pa, RedAr ra) {
     const float mean = K + dm;
     const float var = fmaxf(S2 / Ntot - dm * dm, 0.f);
     const float invstd = rsqrtf(var + cx.bn_eps);
-    const float scv = misc[320 + ch] * invstd;
-    const float shv = misc[352 + ch] - mean * scv;
+    const float scv = gam * invstd;
+    const float shv = bet - mean * scv;
     if (w == 0 && q == 0) {
-      stat[i * 64 + ch] = mean;
-      stat[i * 64 + 32 + ch] = invstd;
-      scsh[i * 64 + ch] = scv;
-      scsh[i * 64 + 32 + ch] = shv;
+      stat[i * 32 + ch] = f32x4{mean, invstd, scv, shv};
       if (L == 0) {  // BN running statistics (10 EMAs per forward) and the batch stats for the next step
         const float unb = var * Ntot / (Ntot - 1.f), mo = cx.bn_mom;
         misc[448 + ch] = misc[448 + ch] * (1.f - mo) + mean * mo;
@@ -1368,8 +1366,8 @@ __global__ void __launch_bounds__(NTH) k_pks_step(Ctx cx, Args pa, RedAr ra) {
     // recover x_i = x_{i+1} - relu(bn(y_i)) (same fma, same scale / shift as the forward); BN-backward inputs
     float dz[4], xh[4], xho[4];
     float sa = 0.f, sbv = 0.f;
-    const float mean = stat[i * 64 + ch], inv = stat[i * 64 + 32 + ch];
-    const float sc = scsh[i * 64 + ch], sh = scsh[i * 64 + 32 + ch];
+    const f32x4 st4 = stat[i * 32 + ch];
+    const float mean = st4[0], inv = st4[1], sc = st4[2], sh = st4[3];
 #pragma unroll
     for (int i2 = 0; i2 < 4; ++i2) {
       const float z = __builtin_fmaf(yv[i2], sc, sh);
@@ -1429,7 +1427,7 @@ __global__ void __launch_bounds__(NTH) k_pks_step(Ctx cx, Args pa, RedAr ra) {
     float dyv[4], dyo[4];
     {
       const float Sa = slot_total(cred, ch), Sb = slot_total(cred, 32 + ch);
-      const float k1 = misc[320 + ch] * inv / Ntot;
+      const float k1 = sc / Ntot;  // gamma * invstd: the forward's scale, bitwise
 #pragma unroll
       for (int i2 = 0; i2 < 4; ++i2) {
         dyv[i2] = k1 * (Ntot * dz[i2] - Sa - xh[i2] * Sb);
