@@ -1232,17 +1232,32 @@ __global__ void __launch_bounds__(NTH) k_pks_step(Ctx cx, Args pa, RedAr ra) {
     // exchange is polled by wave 0 only, after that)
     ld4r(cx.Y + (size_t)(NBLK - 1) * B * 8192 + img8, hh, lane, yv);
     if (halo) ld4r(pa.yh + ((size_t)((NBLK - 1) * LMAX + L) * 2 + hwhich) * 512, hh, lane, yo);
-    // fc1 partial over this slice's features: thread (row j = t >> 4, part k = t & 15) sums features u = 16m + k,
-    // then 4 xor-shuffles over the 16 parts (fixed order: identical in every workgroup)
+    // fc1 partial over this slice's features: thread (row j = t >> 4, part k = t & 15) sums features
+    // u = 64m + 4k .. +3 (one 8 / 16-B weight read and one 16-B feature read per 4 features), then the 16 parts by
+    // DPP (fixed order: identical in every workgroup)
     {
       const int j = t >> 4, k = t & 15;
       float a = 0.f;
-#pragma unroll 8
-      for (int m = 0; m < 32; ++m) {
-        const int u = 16 * m + k;
-        const float wvv = P == 1 ? ((const float*)w1l)[j * PL::W1S + u]
-                                 : __uint_as_float((unsigned)((const unsigned short*)w1l)[j * PL::W1S + u] << 16);
-        a += wvv * pl[u];
+#pragma unroll
+      for (int m = 0; m < 8; ++m) {
+        const int u0 = 64 * m + 4 * k;
+        float wv4[4];
+        if constexpr (P == 1) {
+          const f32x4 w4 = *(const f32x4*)((const float*)w1l + j * PL::W1S + u0);
+          wv4[0] = w4[0];
+          wv4[1] = w4[1];
+          wv4[2] = w4[2];
+          wv4[3] = w4[3];
+        } else {
+          const uint2 w4 = *(const uint2*)((const unsigned short*)w1l + j * PL::W1S + u0);
+          wv4[0] = __uint_as_float(w4.x << 16);
+          wv4[1] = __uint_as_float(w4.x & 0xffff0000u);
+          wv4[2] = __uint_as_float(w4.y << 16);
+          wv4[3] = __uint_as_float(w4.y & 0xffff0000u);
+        }
+        const f32x4 p4 = *(const f32x4*)(pl + u0);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) a += wv4[e] * p4[e];
       }
       a = xsum_row16(a);
       if (k == 0) hp[j] = a;
@@ -1282,8 +1297,12 @@ __global__ void __launch_bounds__(NTH) k_pks_step(Ctx cx, Args pa, RedAr ra) {
       const int o = lane < 10 ? lane : 0;
       float logit = misc[864 + o];
 #pragma unroll
-      for (int jj = 0; jj < 32; ++jj)
-        logit += misc[544 + o * 32 + jj] * __int_as_float(__builtin_amdgcn_readlane(__float_as_int(hr), jj));
+      for (int j4 = 0; j4 < 8; ++j4) {  // W2 row o as 8 x 16-B LDS reads (same summation order)
+        const f32x4 w4 = *(const f32x4*)(misc + 544 + o * 32 + 4 * j4);
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          logit += w4[e] * __int_as_float(__builtin_amdgcn_readlane(__float_as_int(hr), 4 * j4 + e));
+      }
       float lg[10];
 #pragma unroll
       for (int oo = 0; oo < 10; ++oo) lg[oo] = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(logit), oo));
@@ -1322,13 +1341,18 @@ __global__ void __launch_bounds__(NTH) k_pks_step(Ctx cx, Args pa, RedAr ra) {
     }
     lds_barrier();
     DCA_STAMP(cx, 3, L, 3);
-    {  // dp = W1^T dh for this thread's local feature u = t
+    {  // dp = W1^T dh for this thread's local feature u = t (dh read as 8 broadcast 16-B LDS reads)
       float d0 = 0.f;
-#pragma unroll 8
-      for (int j = 0; j < 32; ++j) {
-        const float wvv = P == 1 ? ((const float*)w1l)[j * PL::W1S + t]
-                                 : __uint_as_float((unsigned)((const unsigned short*)w1l)[j * PL::W1S + t] << 16);
-        d0 += hp[32 + j] * wvv;
+#pragma unroll
+      for (int j4 = 0; j4 < 8; ++j4) {
+        const f32x4 dh4 = *(const f32x4*)(hp + 32 + 4 * j4);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int j = 4 * j4 + e;
+          const float wvv = P == 1 ? ((const float*)w1l)[j * PL::W1S + t]
+                                   : __uint_as_float((unsigned)((const unsigned short*)w1l)[j * PL::W1S + t] << 16);
+          d0 += dh4[e] * wvv;
+        }
       }
       dpl[t] = d0;
     }
