@@ -1119,15 +1119,16 @@ __global__ void __launch_bounds__(NTH) k_pks_step(Ctx cx, Args pa, RedAr ra) {
   if constexpr (P == 0) load_bfrag(WT, hh, lane, bw);
 #pragma unroll 1
   for (int i = 0; i < NBLK; ++i) {
+    // shifted one-pass sums S1 = sum(y - K), S2 = sum((y - K)^2); K = this block's batch mean of the previous
+    // step (0 at the first), identical in every workgroup, so the partials combine exactly (read ahead of the conv:
+    // its LDS latency hides under the conv's)
+    const float K = misc[P_KSHIFT + i * 32 + ch];
     {
       const f32x4 acc = conv_row<P>(XR, WT, bw, w, hh, lane);
 #pragma unroll
       for (int i2 = 0; i2 < 4; ++i2) y[i2] = acc[i2];
     }
     if (i == DCA_DETAIL_FWD) DCA_STAMP(cx, 6, L, 0);
-    // shifted one-pass sums S1 = sum(y - K), S2 = sum((y - K)^2); K = this block's batch mean of the previous
-    // step (0 at the first), identical in every workgroup, so the partials combine exactly
-    const float K = misc[P_KSHIFT + i * 32 + ch];
     float a = 0.f, bsq = 0.f;
 #pragma unroll
     for (int i2 = 0; i2 < 4; ++i2) {
@@ -1385,12 +1386,13 @@ __global__ void __launch_bounds__(NTH) k_pks_step(Ctx cx, Args pa, RedAr ra) {
   uint4 nxt = uint4{0u, 0u, 0u, 0u};
   int nxt_lab = 0;
   lds_barrier();
+  f32x4 st4n = stat[(NBLK - 1) * 32 + ch];  // this channel's statistics of the next backward block, read ahead
 #pragma unroll 1
   for (int i = NBLK - 1; i >= 0; --i) {
     // recover x_i = x_{i+1} - relu(bn(y_i)) (same fma, same scale / shift as the forward); BN-backward inputs
     float dz[4], xh[4], xho[4];
     float sa = 0.f, sbv = 0.f;
-    const f32x4 st4 = stat[i * 32 + ch];
+    const f32x4 st4 = st4n;
     const float mean = st4[0], inv = st4[1], sc = st4[2], sh = st4[3];
 #pragma unroll
     for (int i2 = 0; i2 < 4; ++i2) {
@@ -1480,6 +1482,7 @@ __global__ void __launch_bounds__(NTH) k_pks_step(Ctx cx, Args pa, RedAr ra) {
     lds_barrier();
     if (i == DCA_DETAIL_BWD) DCA_STAMP(cx, 7, L, 6);
     // dgrad: g_i = g_{i+1} + conv(dy, W^T flipped)
+    if (i > 0) st4n = stat[(i - 1) * 32 + ch];
     {
       const f32x4 acc = conv_row<P>(XR, WT, bw, w, hh, lane);
 #pragma unroll
