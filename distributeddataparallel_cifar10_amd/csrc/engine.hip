@@ -15,6 +15,7 @@
 #include <cstring>
 #include <map>
 #include <string>
+#include <vector>
 
 #include "netresdeep_kernels.hip"
 #include "xgmi_allreduce.hip"
@@ -71,6 +72,8 @@ struct DcaInit {
                         // between dca_engine_run_part(.., 1) and (.., 2); test/debug path, no RCCL communicator);
                         // 2 = xGMI one-shot (peer-to-peer reads of IPC-mapped gradient slabs, fused with SGD)
   int force_comm;       // comm_mode 0 at world_size 1: still run the RCCL all-reduce + averaging SGD (tests)
+  int auto_engine;      // the persistent engine was chosen automatically: keep one workgroup of co-residency
+                        // slack (else the caller asked for it explicitly and may use every CU)
 };
 
 }  // extern "C"
@@ -88,6 +91,9 @@ struct Engine {
   size_t ws_bytes = 0;
   int* indices = nullptr;
   int n_indices = 0;
+  // dca_engine_run_checked: pinned host copies of the two error words per in-flight chunk + their events
+  unsigned* err_host = nullptr;  // [CHK_RING][2]
+  hipEvent_t chk_ev[4] = {};
   ncclComm_t comm = nullptr;
   // comm_mode 2 (xGMI one-shot): this rank's shared region and every rank's mapping of it
   char* xregion = nullptr;
@@ -98,7 +104,8 @@ struct Engine {
   bool persistent = false;  // the image-sliced persistent step kernel (netresdeep_pks.hip; default)
   pks::Args qa{};
   bool comm_on = false;  // the step ends with a gradient collective (world_size > 1, or force_comm)
-  int resident = 0;      // persistent engine: workgroups guaranteed co-resident (occupancy x CUs)
+  int resident = 0;      // persistent engine: step workgroups allowed in one grid (occupancy x CUs, minus a margin)
+  int cu_slots = 0;      // persistent engine: step workgroups the device holds at once (occupancy x CUs)
   int staged_b = 0;  // persistent engine: batch slots of the current staging parity that hold the next batch
   int last_b = 0;    // batch size of the last enqueued step (BN slots are re-zeroed when it changes)
   int seg_ch = 64;   // gradient-segment layout (pks::seg_layout): trunk / conv1 chunk size
@@ -272,15 +279,22 @@ static int enqueue_xgmi_sgd(Engine* e, const Ctx& cx) {
 // grid of the sliced step: S workgroups per image, image slots rounded up to a multiple of 8 (see k_pks_step)
 static int pks_grid(int B) { return (B + 7) / 8 * 8 * pks::S; }
 
-// Whether the step at batch B runs the fc gradient segments on fc workers.  A step workgroup needs a whole CU
-// (VGPR-bound), and every workgroup of a peer's spinning step or reduction kernel may hold one: with n ranks on
-// the device, fc workers only when (n - 1) peer grids + this step fit the co-resident budget.
+// Ranks sharing one device (shared-GPU rehearsal): a step workgroup needs a whole CU (256 VGPRs), and every
+// workgroup of a peer's spinning step or reduction kernel may hold one.  Each of the n ranks therefore gets a budget
+// of cu_slots / n CUs: its step grid (+ fc workers) and its reduction grid stay within it, so a late rank always
+// finds room for its step however the others are spread over their steps and reductions.
+static int share_budget(const Engine* e) { return e->shared_device > 1 ? e->cu_slots / e->shared_device : e->cu_slots; }
+
+// Whether the step at batch B runs the fc gradient segments on fc workers (the step grid + N_FCW fits the budget).
 static bool fc_in_step_for(const Engine* e, int B) {
   const int gs = pks_grid(B) + pks::N_FCW;
   if (!e->fc_in_step || gs > e->resident) return false;
-  if (e->shared_device <= 1) return true;
-  const int gr = pks::reduce_segments(1, 256) + 1;
-  return (e->shared_device - 1) * std::max(gs, gr) + gs <= e->resident;
+  return e->shared_device <= 1 || gs <= share_budget(e);
+}
+// Reduction grid: one workgroup per segment + the bookkeeping one; shared device: capped at the rank's budget
+// (k_pks_reduce_ar then loops over the segments).
+static int reduce_grid(const Engine* e, int nred_plus) {
+  return e->shared_device > 1 ? std::min(nred_plus, share_budget(e)) : nred_plus;
 }
 
 static int enqueue_step_persistent(Engine* e, int B, int part) {
@@ -300,13 +314,19 @@ static int enqueue_step_persistent(Engine* e, int B, int part) {
     ra.mode = !multi ? 0 : (xgmi ? 2 : 1);
     ra.fc_in_step = fc_in_step_for(e, B) ? 1 : 0;
     ra.seg_ch = e->shared_device > 1 ? 256 : e->seg_ch;
+    if (e->shared_device > 1 && pks_grid(B) > share_budget(e)) {
+      g_err = "shared-GPU rehearsal: " + std::to_string(e->shared_device) + " ranks x " + std::to_string(pks_grid(B)) +
+              " step workgroups (batch " + std::to_string(B) + ") exceed the device's " + std::to_string(e->cu_slots) +
+              " CUs; use a smaller per-rank batch";
+      return -1;
+    }
     const dim3 grid(pks_grid(B) + (ra.fc_in_step ? pks::N_FCW : 0));
     if (e->bf)
       hipLaunchKernelGGL(pks::k_pks_step<0>, grid, dim3(pks::NTH), pks::Plan<0>::TOTAL, e->st, cx, e->qa, ra);
     else
       hipLaunchKernelGGL(pks::k_pks_step<1>, grid, dim3(pks::NTH), pks::Plan<1>::TOTAL, e->st, cx, e->qa, ra);
-    hipLaunchKernelGGL(pks::k_pks_reduce_ar, dim3(pks::reduce_segments(ra.fc_in_step, ra.seg_ch) + 1), dim3(256), 0, e->st,
-                       cx, e->qa, B * pks::S, ra);
+    hipLaunchKernelGGL(pks::k_pks_reduce_ar, dim3(reduce_grid(e, pks::reduce_segments(ra.fc_in_step, ra.seg_ch) + 1)),
+                       dim3(256), pks::stage_floats(B) * 4, e->st, cx, e->qa, B * pks::S, ra);
   }
   if (multi && !xgmi) {  // RCCL (comm_mode 0, captured) or the host (comm_mode 1, between parts 1 and 2)
     if (part == 0) NCCK(ncclAllReduce(cx.grads, cx.grads, FLAT_N, ncclFloat32, ncclSum, e->comm, e->st));
@@ -369,7 +389,7 @@ extern "C" {
 
 const char* dca_last_error() { return g_err.c_str(); }
 
-int dca_abi_version() { return 4; }  // bump with every DcaInit / signature change
+int dca_abi_version() { return 5; }  // bump with every DcaInit / signature change
 
 int dca_nccl_unique_id(char* out128) {
   ncclUniqueId id;
@@ -424,8 +444,13 @@ static int engine_init(Engine* e, const DcaInit* in, int n_indices) {
     else
       HIPCK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)dca::pks::k_pks_step<1>, dca::pks::NTH,
                                                         dca::pks::Plan<1>::TOTAL));
-    const int resident = (per_cu > 1 ? per_cu - 1 : per_cu) * ncu;
+    // one step workgroup per CU (256 VGPRs): a grid of every CU would leave no slack for anything else on the
+    // device (another stream's kernel, another process), so an automatically chosen engine keeps a margin of one
+    // workgroup -- batch 64 (256 workgroups) then falls back to the multi-kernel engine with a warning; an
+    // explicit persistent=True may use every CU
+    const int resident = per_cu > 1 ? (per_cu - 1) * ncu : (in->auto_engine ? ncu - 1 : ncu);
     const int need = dca::pks_grid(in->bmax);
+    e->cu_slots = per_cu * ncu;
     if (resident < need) {
       g_err = "persistent engine: " + std::to_string(need) + " workgroups cannot all be resident (" +
               std::to_string(per_cu) + " per CU x " + std::to_string(ncu) + " CUs); use the multi-kernel engine";
@@ -440,6 +465,9 @@ static int engine_init(Engine* e, const DcaInit* in, int n_indices) {
   HIPCK(hipEventCreateWithFlags(&e->evA, hipEventDisableTiming));
   HIPCK(hipEventCreateWithFlags(&e->evB, hipEventDisableTiming));
   HIPCK(hipEventCreateWithFlags(&e->evC, hipEventDisableTiming));
+  for (auto& ev : e->chk_ev) HIPCK(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+  HIPCK(hipHostMalloc((void**)&e->err_host, 4 * 2 * sizeof(unsigned), hipHostMallocDefault));
+  memset(e->err_host, 0, 4 * 2 * sizeof(unsigned));
   if (dca::alloc_workspace(e)) return -1;
   e->n_indices = n_indices;
   HIPCK(hipMalloc(&e->indices, sizeof(int) * (size_t)std::max(n_indices, 1)));
@@ -515,6 +543,9 @@ static void engine_free(Engine* e) {
   if (e->xregion) (void)hipFree(e->xregion);
   if (e->wsp) (void)hipFree(e->wsp);
   if (e->indices) (void)hipFree(e->indices);
+  if (e->err_host) (void)hipHostFree(e->err_host);
+  for (auto& ev : e->chk_ev)
+    if (ev) (void)hipEventDestroy(ev);
   if (e->evA) (void)hipEventDestroy(e->evA);
   if (e->evB) (void)hipEventDestroy(e->evB);
   if (e->evC) (void)hipEventDestroy(e->evC);
@@ -677,6 +708,65 @@ int dca_engine_run(void* h, int B, int nsteps, int use_graph) {
   return 0;
 }
 
+// dca_engine_run with the device error words checked after EVERY graph chunk, without stalling the GPU: behind each
+// chunk an async copy of the two words into pinned host memory and an event; before launching chunk k + 2 the host
+// waits for chunk k's event (chunk k + 1 keeps the GPU busy meanwhile) and reads its words.  An exchange timeout
+// (BN exchange of the step, or a peer that stopped stepping in the xGMI all-reduce) therefore stops the run within
+// two 8-step chunks (< 16 steps) instead of at the epoch end; after the first timed-out wait the kernels do not wait
+// again (fail fast on the error word), so those steps are quick.  Returns 0, or 1 when an error word was set (*steps_done:
+// steps of the chunks enqueued before stopping; the words stay set for dca_engine_errors); -1 on a HIP error.
+// Synchronous: the stream is drained before returning.
+int dca_engine_run_checked(void* h, int B, int nsteps, int* steps_done) {
+  Engine* e = (Engine*)h;
+  constexpr int RING = 4;
+  *steps_done = 0;
+  if (B < 1 || B > e->in.bmax || nsteps < 0) {
+    g_err = "batch out of range";
+    return -1;
+  }
+  if (e->in.world_size > 1 && e->in.comm_mode == 1) {
+    g_err = "comm_mode 1 (external all-reduce): drive steps with dca_engine_run_part";
+    return -1;
+  }
+  if (nsteps > 0 && ensure_staged(e, B)) return -1;
+  int left = nsteps;
+  std::vector<int> order;  // graph chunk sizes in launch order (16s, then 8 / 4 / 2 / 1)
+  for (const int chunk : {8, 4, 2, 1})  // 8-step chunks: a failure is seen within < 16 steps (2 chunks in flight)
+    for (; left >= chunk; left -= chunk) order.push_back(chunk);
+  int launched = 0, rc = 0;
+  size_t k = 0, checked = 0;
+  auto check = [&](size_t j) -> int {  // chunk j's words (its event first)
+    hipEvent_t ev = e->chk_ev[j % RING];
+    if (hipEventSynchronize(ev) != hipSuccess) return -1;
+    const unsigned* w = e->err_host + 2 * (j % RING);
+    return (w[0] | w[1]) ? 1 : 0;
+  };
+  for (; k < order.size(); ++k) {
+    if (k >= 2) {  // keep <= 2 chunks in flight behind the check
+      const int r = check(checked++);
+      if (r < 0) HIPCK(hipGetLastError());
+      if (r) {
+        rc = 1;
+        break;
+      }
+    }
+    hipGraphExec_t ex = capture_graph(e, B, order[k]);
+    if (ex == nullptr) return -1;
+    HIPCK(hipGraphLaunch(ex, e->st));
+    HIPCK(hipMemcpyAsync(e->err_host + 2 * (k % RING), e->qa.err, 2 * sizeof(unsigned), hipMemcpyDeviceToHost, e->st));
+    HIPCK(hipEventRecord(e->chk_ev[k % RING], e->st));
+    launched += order[k];
+  }
+  while (rc == 0 && checked < k) {
+    const int r = check(checked++);
+    if (r < 0) HIPCK(hipGetLastError());
+    if (r) rc = 1;
+  }
+  HIPCK(hipStreamSynchronize(e->st));
+  *steps_done = launched;
+  return rc;
+}
+
 // Capture (without running) the graphs dca_engine_run replays for batch B, so a later timed run never pays
 // capture + instantiate.  Synchronous.
 int dca_engine_precapture(void* h, int B) {
@@ -766,8 +856,8 @@ int dca_engine_ipc_selftest(void* h, const float* src, float* dst, float timeout
     ra.seg_ch = e->shared_device > 1 ? 256 : e->seg_ch;
     dca::Ctx cx = e->base;
     cx.B = 1;
-    hipLaunchKernelGGL(dca::pks::k_pks_reduce_ar, dim3(dca::pks::seg_layout(ra.seg_ch).nseg), dim3(256), 0, e->st, cx,
-                       e->qa, 1, ra);
+    hipLaunchKernelGGL(dca::pks::k_pks_reduce_ar, dim3(dca::reduce_grid(e, dca::pks::seg_layout(ra.seg_ch).nseg)),
+                       dim3(256), dca::pks::stage_floats(1) * 4, e->st, cx, e->qa, 1, ra);
   } else {
     dca::xg::Peers P = e->peers;
     P.ticks = nullptr;  // a self-test is not training-step communication (metrics)
@@ -784,6 +874,50 @@ int dca_engine_ipc_selftest(void* h, const float* src, float* dst, float timeout
   HIPCK(hipMemcpy(&f, e->qa.err + 1, sizeof(unsigned), hipMemcpyDeviceToHost));
   HIPCK(hipMemset(e->qa.err + 1, 0, sizeof(unsigned)));
   *timed_out = (f & 0x80000000u) ? 1 : 0;
+  return 0;
+}
+
+// comm_mode 2, sliced engine: the same collective self-test through the STEP kernel's fc workers (the in-step
+// exchange of the fc1 blocks and the fc tail that runs beside the trunk backward): k_pks_step launched with batch 0,
+// i.e. N_FCW fc workers and no step workgroups, in self-test mode.  Only the fc segments' slab range is written to
+// dst: [*lo, *hi).  Each fc worker waits only for the same segment of its peers, so ranks sharing a device need no
+// co-residency budget here.  Collective; synchronous.
+int dca_engine_ipc_selftest_fc(void* h, const float* src, float* dst, float timeout_s, int* timed_out, int* lo,
+                               int* hi) {
+  Engine* e = (Engine*)h;
+  if (!e->peers_open || !e->persistent) {
+    g_err = "ipc_selftest_fc: needs the sliced engine with mapped peers";
+    return -1;
+  }
+  HIPCK(hipMemsetAsync(e->qa.err, 0, 2 * sizeof(unsigned), e->st));
+  dca::pks::RedAr ra{};
+  ra.peers = e->peers;
+  ra.peers.ticks = nullptr;
+  ra.err = e->qa.err + 1;
+  ra.deadline = (unsigned long long)((double)timeout_s * 1e8);
+  ra.st_src = src;
+  ra.st_dst = dst;
+  ra.st_n = dca::FLAT_N;
+  ra.mode = 3;
+  ra.fc_in_step = 1;
+  ra.seg_ch = e->shared_device > 1 ? 256 : e->seg_ch;
+  dca::Ctx cx = e->base;
+  cx.B = 0;  // no step workgroups: the whole grid is fc workers
+  if (e->bf)
+    hipLaunchKernelGGL(dca::pks::k_pks_step<0>, dim3(dca::pks::N_FCW), dim3(dca::pks::NTH), dca::pks::Plan<0>::TOTAL,
+                       e->st, cx, e->qa, ra);
+  else
+    hipLaunchKernelGGL(dca::pks::k_pks_step<1>, dim3(dca::pks::N_FCW), dim3(dca::pks::NTH), dca::pks::Plan<1>::TOTAL,
+                       e->st, cx, e->qa, ra);
+  HIPCK(hipGetLastError());
+  HIPCK(hipStreamSynchronize(e->st));
+  unsigned f[2] = {0, 0};
+  HIPCK(hipMemcpy(f, e->qa.err, sizeof(f), hipMemcpyDeviceToHost));
+  HIPCK(hipMemset(e->qa.err, 0, sizeof(f)));
+  *timed_out = ((f[1] & 0x80000000u) || f[0]) ? 1 : 0;
+  const dca::pks::SegLayout L = dca::pks::seg_layout(ra.seg_ch);
+  *lo = L.off_fc1;
+  *hi = std::min(L.off_fct + 362, (int)dca::FLAT_N);
   return 0;
 }
 
@@ -815,8 +949,8 @@ int dca_engine_ipc_bench(void* h, const float* src, float* dst, int iters, float
       ra.seg_ch = e->shared_device > 1 ? 256 : e->seg_ch;
       dca::Ctx cx = e->base;
       cx.B = 1;
-      hipLaunchKernelGGL(dca::pks::k_pks_reduce_ar, dim3(dca::pks::seg_layout(ra.seg_ch).nseg), dim3(256), 0, e->st,
-                         cx, e->qa, 1, ra);
+      hipLaunchKernelGGL(dca::pks::k_pks_reduce_ar, dim3(dca::reduce_grid(e, dca::pks::seg_layout(ra.seg_ch).nseg)),
+                         dim3(256), dca::pks::stage_floats(1) * 4, e->st, cx, e->qa, 1, ra);
     } else if (e->bf) {
       hipLaunchKernelGGL(dca::xg::k_xgmi_ar_sgd<true>, dim3(dca::xg::AR_NB), dim3(dca::xg::AR_T), 0, e->st,
                          e->base, P, src, dst, e->qa.err + 1, 0, e->ar_deadline);

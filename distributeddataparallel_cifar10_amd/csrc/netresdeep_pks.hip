@@ -262,7 +262,15 @@ __device__ __forceinline__ float wg_csum(float a, float b, float* cred) {
   return v;
 }
 
-__device__ __forceinline__ unsigned tagof(int epoch, int round) { return (unsigned)(epoch * 64 + round + 1); }
+// The step epoch (device scalar) runs 0 .. EPOCH_WRAP - 1 and wraps (pks_bookkeeping): EPOCH_WRAP is a multiple of 6,
+// so the epoch parity (staging) and the bn_tag cycle (epoch mod 3) continue seamlessly across the wrap, and
+// epoch * 64 + round + 1 < 2^32 never overflows (unsigned arithmetic throughout: no signed-overflow UB after hours of
+// stepping).  Consecutive epochs -- the only ones a granule can hold -- still give distinct tags at the wrap.
+constexpr unsigned EPOCH_WRAP = 6u << 23;
+static_assert((unsigned long long)EPOCH_WRAP * 64 + 64 < (1ull << 32), "granule tags fit 32 bits");
+__device__ __forceinline__ unsigned tagof(int epoch, int round) {
+  return (unsigned)epoch * 64u + (unsigned)round + 1u;
+}
 __device__ __forceinline__ unsigned long long* gslot(const Args& pa, int round, int L) {
   return pa.gran + ((size_t)(round & 1) * LMAX + L) * GSTR;
 }
@@ -295,10 +303,12 @@ __device__ __forceinline__ void publish_row(const Args& pa, int round, int L, in
 // consecutive tags of the cycle 1, 2, 3 (each parity is written 10 times per step: c = 10 epoch + k, tag =
 // 1 + c mod 3), so a reader can never accept the previous write; 0 never matches (the host zeroes the buffer
 // whenever the batch size changes, so slots of workgroups absent from earlier steps are never stale-valid).
-__device__ __forceinline__ unsigned bn_tag(int epoch, int rnd) {
-  const int k = rnd < RND_HEAD ? rnd >> 1 : 5 + ((rnd - RND_HEAD - 1) >> 1);
-  return 1u + (unsigned)((epoch * 10 + k) % 3);
+// (10 epoch + k) mod 3 = (epoch mod 3 + k) mod 3, in unsigned arithmetic (EPOCH_WRAP % 3 == 0 keeps the cycle).
+__host__ __device__ __forceinline__ unsigned bn_tag(int epoch, int rnd) {
+  const unsigned k = rnd < RND_HEAD ? (unsigned)rnd >> 1 : 5u + ((unsigned)(rnd - RND_HEAD - 1) >> 1);
+  return 1u + ((unsigned)epoch % 3u + k) % 3u;
 }
+static_assert(EPOCH_WRAP % 6 == 0, "epoch wrap keeps parity and the bn_tag cycle");
 __device__ __forceinline__ void bn_put(const Args& pa, int rnd, int L, int slot, unsigned tag, float v) {
   __hip_atomic_store(pa.bnx + ((size_t)(rnd & 1) * LMAX + L) * 64 + slot, (__float_as_uint(v) & ~3u) | tag,
                      __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -572,6 +582,10 @@ __device__ __forceinline__ void w1_dma(const Ctx& cx, char* w1l, int s, int wv, 
 // grid must leave room for another rank's step kernel -- a CU holding a reduction workgroup has too few VGPRs left
 // for a step workgroup).  256-element chunks read 128 KB through one CU (3.9 us, profiles/stamps_pks_bf16_r3f.log).
 constexpr int R_FC1 = 64;
+// LDS staging of the fc segments at batch B: fc1 block dh [B][32] + p [B][64]; fc tail h [B][32] + dlogits [B][16]
+// + dh [B][32].  Sized per launch (dynamic LDS of k_pks_reduce_ar): the reduction grids of ranks sharing a device
+// spin side by side and must leave a step workgroup's LDS free on every CU.
+__host__ __device__ constexpr int stage_floats(int B) { return B * 96; }
 constexpr int FCT_LEN = 364, BNT_LEN = 128;        // fc tail 362 (+2 pad), BN tail
 constexpr int SEG_MAX = 1024;
 constexpr int NSEG_MAX = WSLAB_N / 64 + (SSLAB_N + 63) / 64 + R_FC1 + 2;  // 227: flag-array stride per rank
@@ -629,7 +643,7 @@ __device__ void seg_exchange(const Ctx& cx, const RedAr& ra, int b, float* segv,
   const int t = threadIdx.x, W = cx.ws, me = cx.rank;
   int* myflags = (int*)rbase(ra, me);
   const unsigned long long t_in = __builtin_amdgcn_s_memrealtime();
-  if (t == 0) *s_ep = ep0 + 1;
+  if (t == 0) *s_ep = xg::next_ep(ep0);
   __syncthreads();
   const int ep = *s_ep, par = ep & 1;
   constexpr int SYS = 17;  // sc0 | sc1: write-through store / cache-bypassing load
@@ -641,10 +655,12 @@ __device__ void seg_exchange(const Ctx& cx, const RedAr& ra, int b, float* segv,
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this thread's slab stores are performed
   __syncthreads();                                    // ... and every thread's
   if (t < W) xg::flag_store((int*)rbase(ra, t) + me * NSEG_MAX + b, ep);
-  if (t < W) {
+  // fail fast: once any exchange of this rank timed out (a peer stopped stepping) the host is about to stop the run
+  // (dca_engine_run_checked); later exchanges do not wait the full deadline again
+  if (t < W && !(__hip_atomic_load(ra.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & 0x80000000u)) {
     const int* f = myflags + t * NSEG_MAX + b;
     const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
-    while (xg::flag_load(f) < ep) {
+    while (xg::flag_before(xg::flag_load(f), ep)) {
       __builtin_amdgcn_s_sleep(1);
       if (__builtin_amdgcn_s_memrealtime() - t0 > ra.deadline) {
         atomicOr(ra.err, 0x80000000u);
@@ -735,7 +751,7 @@ __device__ __forceinline__ void seg_chunk(const Ctx& cx, const Args& pa, const S
 }
 
 // Segment b on this workgroup (NTH threads): reduce / compute into segv, exchange (mode 2), SGD.  LDS: segv
-// [SEG_MAX], red [NTH] f32x4, stage [64 * 32 + 64 * 64] floats, *s_ep.
+// [SEG_MAX], red [NTH] f32x4, stage [stage_floats(B)], *s_ep.
 template <int NTH>
 __device__ void seg_process(const Ctx& cx, const Args& pa, const RedAr& ra, int b, int nslab, float* segv,
                             f32x4* red, float* stage, int* s_ep, int sslot, int swg) {
@@ -764,7 +780,7 @@ __device__ void seg_process(const Ctx& cx, const Args& pa, const RedAr& ra, int 
     // fc1 block: dW1[j][64f + kk .. +3] = sum_b dh[b][j] p[b][64f + kk ..], rows j = 16 h .. 16 h + 15
     const int fb = b - Ls.r_ts, f = fb >> 1, j0 = 16 * (fb & 1);
     float* dh_s = stage;           // [B][32]
-    float* p_s = stage + 64 * 32;  // [B][64]
+    float* p_s = stage + B * 32;   // [B][64]
     constexpr int MD = (64 * 8 + NTH - 1) / NTH, MP = (64 * 16 + NTH - 1) / NTH;
     f32x4 dh4[MD], p4[MP];
 #pragma unroll
@@ -794,8 +810,8 @@ __device__ void seg_process(const Ctx& cx, const Args& pa, const RedAr& ra, int 
   } else if (b == Ls.fct) {
     // fc tail: fc1 bias [0,32), fc2 weight [32,352), fc2 bias [352,362), pad
     float* hh_s = stage;            // [B][32]
-    float* dl_s = stage + 64 * 32;  // [B][16]
-    float* dh_s = dl_s + 64 * 16;   // [B][32]
+    float* dl_s = stage + B * 32;   // [B][16]
+    float* dh_s = dl_s + B * 16;    // [B][32]
     for (int idx = t; idx < B * 8; idx += NTH) {
       st4(hh_s + 4 * idx, ld4_sc1(cx.HH, 64 * 32 * 4, 4 * idx));
       st4(dh_s + 4 * idx, ld4_sc1(cx.HDH, 64 * 32 * 4, 4 * idx));
@@ -898,7 +914,7 @@ __device__ void fc_worker(const Ctx& cx, const Args& pa, const RedAr& ra, int fb
   float* segv = (float*)smem;
   f32x4* red = (f32x4*)(smem + SEG_MAX * 4);
   float* stage = (float*)(smem + SEG_MAX * 4 + NTH * 16);
-  int* s_ep = (int*)(smem + SEG_MAX * 4 + NTH * 16 + (64 * 32 + 64 * 64) * 4);
+  int* s_ep = (int*)(smem + SEG_MAX * 4 + NTH * 16 + stage_floats(cx.B) * 4);
   const SegLayout Ls = seg_layout(ra.seg_ch);
   seg_process<NTH>(cx, pa, ra, fb < R_FC1 ? Ls.r_ts + fb : Ls.fct, G, segv, red, stage, s_ep, 9, fb);
 }
@@ -1638,7 +1654,7 @@ __device__ __forceinline__ void pks_bookkeeping(const Ctx& cx, const Args& pa) {
     *cx.cursor = cur + B;
     *cx.step_count = stp + 1;
     *cx.nbt = nb + NBLK;  // BatchNorm num_batches_tracked: +1 per application
-    *pa.epoch = ep + 1;
+    *pa.epoch = (int)(((unsigned)ep + 1u) % EPOCH_WRAP);
   }
 }
 
@@ -1647,19 +1663,36 @@ __host__ __device__ inline int reduce_segments(int fc_in_step, int seg_ch) {
   return fc_in_step ? seg_layout(seg_ch).r_ts + 1 : seg_layout(seg_ch).nseg;
 }
 
+// dynamic LDS: stage_floats(cx.B) * 4 bytes (fc-segment staging)
+// Grid: nred + 1 workgroups (one segment each, the last one the bookkeeping), or -- ranks sharing one device
+// (shared-GPU rehearsal) -- at most the per-rank CU budget: workgroup b then runs segments b, b + grid, ... in turn
+// and the last workgroup also does the bookkeeping.  Every segment's exchange only waits for the SAME segment of the
+// peers, and each rank visits its segments in the same order, so the looped form cannot deadlock among reductions;
+// its point is that a rank's spinning reduction never holds more CUs than its step kernel (a step workgroup needs a
+// whole CU: 256 VGPRs), so a late peer always finds room for its step.
 __global__ void __launch_bounds__(256) k_pks_reduce_ar(Ctx cx, Args pa, int nslab, RedAr ra) {
   __shared__ __attribute__((aligned(16))) float segv[SEG_MAX];
   __shared__ f32x4 red[256];
-  __shared__ float stage[64 * 32 + 64 * 64];
+  extern __shared__ __attribute__((aligned(16))) float stage[];
   __shared__ int s_ep;
-  const int nred = reduce_segments(ra.fc_in_step, ra.seg_ch), b = blockIdx.x;
-  if (b >= nred) {
-    if (ra.mode != 3) pks_bookkeeping(cx, pa);
+  const int nred = reduce_segments(ra.fc_in_step, ra.seg_ch), b = blockIdx.x, nwg = gridDim.x;
+  const SegLayout Ls = seg_layout(ra.seg_ch);
+  if (nwg > nred) {
+    if (b >= nred) {
+      if (ra.mode != 3) pks_bookkeeping(cx, pa);
+      return;
+    }
+    const int seg = !ra.fc_in_step || b < Ls.r_ts ? b : Ls.bnt;
+    DCA_STAMP(cx, 8, b, 0);
+    seg_process<256>(cx, pa, ra, seg, nslab, segv, red, stage, &s_ep, 8, b);
     return;
   }
-  const int seg = !ra.fc_in_step || b < seg_layout(ra.seg_ch).r_ts ? b : seg_layout(ra.seg_ch).bnt;
-  DCA_STAMP(cx, 8, b, 0);
-  seg_process<256>(cx, pa, ra, seg, nslab, segv, red, stage, &s_ep, 8, b);
+  for (int k = b; k < nred; k += nwg) {
+    const int seg = !ra.fc_in_step || k < Ls.r_ts ? k : Ls.bnt;
+    seg_process<256>(cx, pa, ra, seg, nslab, segv, red, stage, &s_ep, 8, k);
+    __syncthreads();  // segv / red / stage are reused by the next segment
+  }
+  if (b == nwg - 1 && ra.mode != 3) pks_bookkeeping(cx, pa);
 }
 
 }  // namespace pks

@@ -55,6 +55,10 @@ __device__ __forceinline__ int flag_load(const int* p) {
 __device__ __forceinline__ void flag_store(int* p, int v) {
   __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
+// Epochs count calls and wrap modulo 2^32 (after ~2^31 steps a plain signed compare would overflow): "flag f has
+// not reached epoch ep yet" as a wrap-aware serial-number comparison; next_ep is the wrapping increment.
+__device__ __forceinline__ bool flag_before(int f, int ep) { return (int)((unsigned)f - (unsigned)ep) < 0; }
+__device__ __forceinline__ int next_ep(int f) { return (int)((unsigned)f + 1u); }
 __device__ __forceinline__ float* slab(const Peers& P, int q, int parity) {
   return (float*)(P.base[q] + FLAG_BYTES) + (size_t)parity * SLAB_FLOATS;
 }
@@ -71,7 +75,7 @@ __global__ void __launch_bounds__(AR_T) k_xgmi_ar_sgd(Ctx cx, Peers P, const flo
   int* myflags = (int*)P.base[me];
   __shared__ int s_ep;
   const unsigned long long t_in = __builtin_amdgcn_s_memrealtime();
-  if (t == 0) s_ep = flag_load(myflags + me * AR_NB + b) + 1;
+  if (t == 0) s_ep = next_ep(flag_load(myflags + me * AR_NB + b));
   const f32x4 g = live ? *(const f32x4*)(src + 4 * v) : f32x4{0.f, 0.f, 0.f, 0.f};
   __syncthreads();
   const int ep = s_ep, par = ep & 1;
@@ -82,10 +86,10 @@ __global__ void __launch_bounds__(AR_T) k_xgmi_ar_sgd(Ctx cx, Peers P, const flo
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this thread's slab store is performed
   __syncthreads();                                    // ... and every thread's of this workgroup
   if (t < W) flag_store((int*)P.base[t] + me * AR_NB + b, ep);
-  if (t < W) {
+  if (t < W && !(__hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & 0x80000000u)) {  // fail fast
     const int* f = myflags + t * AR_NB + b;
     const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
-    while (flag_load(f) < ep) {
+    while (flag_before(flag_load(f), ep)) {
       __builtin_amdgcn_s_sleep(1);
       if (__builtin_amdgcn_s_memrealtime() - t0 > deadline_ticks) {
         atomicOr(err, 0x80000000u);

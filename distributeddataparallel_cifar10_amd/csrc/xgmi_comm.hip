@@ -135,7 +135,9 @@ __device__ __forceinline__ void exchange(const Args& a, bool out, int ep) {
     __hip_atomic_store(f, ep, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     const int* mine = (out ? out_flags(a.base[a.me]) : in_flags(a.base[a.me])) + t * NB_MAX + b;
     const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
-    while (__hip_atomic_load(mine, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) < ep) {
+    // fail fast: after a timed-out wait (error word set, not yet read by the host) later calls do not wait again
+    const bool failed = __hip_atomic_load(a.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u;
+    while (!failed && (int)((unsigned)__hip_atomic_load(mine, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) - (unsigned)ep) < 0) {
       __builtin_amdgcn_s_sleep(1);
       if (__builtin_amdgcn_s_memrealtime() - t0 > a.deadline) {
         atomicOr(a.err, 1u);
@@ -174,7 +176,7 @@ __global__ void __launch_bounds__(T) k_allreduce(Args a) {
   const long long nv = (a.n + 3) / 4;
   __shared__ int s_ep;
   if (t == 0) s_ep = __hip_atomic_load(in_flags(a.base[me]) + me * NB_MAX + b, __ATOMIC_RELAXED,
-                                       __HIP_MEMORY_SCOPE_SYSTEM) + 1;
+                                       __HIP_MEMORY_SCOPE_SYSTEM) + 1u;  // wraps mod 2^32 (wrap-aware wait below)
   __syncthreads();
   const int ep = s_ep, par = ep & 1;
   const long long wire = BF ? 2 : 4;

@@ -58,9 +58,11 @@ class OpsModel(nn.Module):
         if self._pack is None:
             convs = [m for m in self.module.modules() if isinstance(m, nn.Conv2d)]
             # the stem (the first conv: ResNet conv1, the PPE model's stem[0]) as a space-to-depth 4x4 conv when it
-            # is 7x7/2/3 over <= 4 channels (DCA_OPS_STEM_S2D=0: the 8-channel NHWC 7x7 implicit GEMM)
+            # is 7x7/2/3 over <= 4 channels (DCA_OPS_STEM_S2D=0: the 8-channel NHWC 7x7 implicit GEMM).  Decided
+            # here, at the first step: an input that requires grad (no input gradient through the s2d stem) keeps
+            # the regular 7x7 path for the model's lifetime
             self._s2d = convs[0] if convs and self.kind == "resnet" and F.stem_s2d_ok(convs[0]) and \
-                os.environ.get("DCA_OPS_STEM_S2D", "1") != "0" else None
+                not x.requires_grad and os.environ.get("DCA_OPS_STEM_S2D", "1") != "0" else None
             self._pack = F.WeightPack(convs, [c for c in convs if self._fp8_ok(c)],
                                       [self._s2d] if self._s2d is not None else [])
             self._bns = [m for m in self.module.modules()
@@ -69,8 +71,9 @@ class OpsModel(nn.Module):
                 m._dca_counted = True
         if self._s2d is not None:
             if x.requires_grad:
-                raise NotImplementedError("OpsModel: no input gradient through the space-to-depth stem "
-                                          "(DCA_OPS_STEM_S2D=0)")
+                raise NotImplementedError("OpsModel: the first step's input did not require grad, so the stem "
+                                          "runs space-to-depth (no input gradient); build the model with a "
+                                          "requires_grad input first, or set DCA_OPS_STEM_S2D=0")
             h = F.nchw_to_s2d16(x.detach().float())  # one kernel: the stem's space-to-depth operand
         elif x.shape[1] <= 8 and x.dtype == torch.float32 and not x.requires_grad:
             h = F.nchw_to_nhwc8(x)  # one kernel

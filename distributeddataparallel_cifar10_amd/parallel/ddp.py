@@ -29,14 +29,7 @@ import torch.distributed as dist
 import torch.nn as nn
 
 from ..runtime.engine import EngineConfig, NetResDeepEngine, nccl_unique_id
-
-
-def _device_key(dev) -> str:
-    """Identity of the physical device (UUID when available), to detect ranks that share one GPU."""
-    try:
-        return str(torch.cuda.get_device_properties(dev).uuid)
-    except Exception:  # noqa: BLE001
-        return f"{os.uname().nodename}:{dev}"
+from .dist import device_share_count
 
 
 def broadcast_module_state(model: nn.Module, src: int = 0) -> None:
@@ -95,9 +88,8 @@ class FusedDDPTrainer:
         ok = all(h is not None for h in handles)
         # ranks sharing one device (the shared-GPU rehearsal): a rank's spinning kernels (the step's fc workers,
         # the reduction) can hold CUs a peer's step needs -> the engine budgets its grids by the sharing count
-        dev_ids = [None] * self.world_size
-        dist.all_gather_object(dev_ids, _device_key(data_u8.device))
-        n_share = max(dev_ids.count(d) for d in dev_ids)
+        n_share = device_share_count(data_u8.device)
+        self.n_share = n_share
         if ok and eng is not None and n_share > 1:
             eng.set_shared_device(n_share)
         if ok:

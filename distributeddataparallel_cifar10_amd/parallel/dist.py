@@ -53,6 +53,34 @@ def world() -> tuple[int, int]:
     return 0, 1
 
 
+def device_key(dev) -> Optional[str]:
+    """Identity of the physical device, to detect ranks that share one GPU: the device UUID, else the PCI
+    domain:bus:device address; None when neither is known (then nobody is counted as sharing).  The local ordinal
+    is never used: with one visible GPU per rank (HIP_VISIBLE_DEVICES) every rank is ``cuda:0``."""
+    try:
+        props = torch.cuda.get_device_properties(dev)
+    except Exception:  # noqa: BLE001
+        return None
+    uuid = str(getattr(props, "uuid", "") or "")
+    if uuid and uuid.strip("0-") != "":
+        return "uuid:" + uuid
+    bus = getattr(props, "pci_bus_id", None)
+    if bus is not None and (bus or getattr(props, "pci_device_id", 0)):
+        return f"pci:{getattr(props, 'pci_domain_id', 0)}:{bus}:{getattr(props, 'pci_device_id', 0)}"
+    return None
+
+
+def device_share_count(dev, group=None) -> int:
+    """Collective: the largest number of ranks of `group` on one physical device (1 = one rank per GPU).  Unknown
+    device identities count as unshared."""
+    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size(group) == 1:
+        return 1
+    keys = [None] * dist.get_world_size(group)
+    dist.all_gather_object(keys, device_key(dev), group=group)
+    known = [k for k in keys if k is not None]
+    return max((known.count(k) for k in known), default=1)
+
+
 def params_checksum(module: torch.nn.Module) -> float:
     """Sum of all parameters (float64) -- cheap cross-rank consistency check."""
     with torch.no_grad():

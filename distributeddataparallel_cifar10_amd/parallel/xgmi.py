@@ -26,6 +26,7 @@ import torch
 import torch.distributed as dist
 
 from .. import build as _build
+from .dist import device_share_count
 
 ABI_VERSION = 1
 _lock = threading.Lock()
@@ -70,7 +71,8 @@ class XgmiComm:
     """One rank's endpoint.  ``all_reduce_(t)`` sums (``average=True``: averages) a contiguous fp32 CUDA tensor
     of at most ``max_numel`` elements across the group, in place, on ``stream`` (default: current stream)."""
 
-    def __init__(self, max_numel: int, group=None, wire: str = "fp32", nb: int = 128, timeout_s: float = 30.0):
+    def __init__(self, max_numel: int, group=None, wire: str = "fp32", nb: Optional[int] = 128,
+                 timeout_s: float = 30.0):
         if wire not in ("fp32", "bf16"):
             raise ValueError("wire must be 'fp32' or 'bf16'")
         self.group = group
@@ -79,6 +81,8 @@ class XgmiComm:
         if self.world > 8:
             raise ValueError("the xGMI communicator spans one node (<= 8 ranks)")
         self.wire, self.timeout_s, self.max_numel = wire, float(timeout_s), int(max_numel)
+        nb = 128 if nb is None else int(nb)
+        self.nb = nb
         self.last_algo = None
         h = ctypes.c_void_p()
         slab = (self.max_numel + 3) // 4 * 4 * 4  # fp32 sized, so the wire format can be switched per call
@@ -100,6 +104,10 @@ class XgmiComm:
         """Collective: build, connect and self-test the communicator on every rank; None on EVERY rank if any
         rank failed (so all ranks agree on the fallback)."""
         world = dist.get_world_size(group) if dist.is_initialized() else 1
+        if kw.get("nb") is None:
+            # ranks sharing one device (the shared-GPU rehearsal): every rank's call spins until all have arrived,
+            # so the W grids must be co-resident together -- split the default 128 workgroups by the sharing count
+            kw["nb"] = max(8, 128 // device_share_count(device, group))
         comm, handle, err = None, None, None
         try:
             comm = cls(max_numel, group=group, **kw)

@@ -67,6 +67,7 @@ class _DcaInit(ctypes.Structure):
         ("pk_waves", ctypes.c_int),
         ("comm_mode", ctypes.c_int),
         ("force_comm", ctypes.c_int),
+        ("auto_engine", ctypes.c_int),
     ]
 
 
@@ -170,6 +171,7 @@ class NetResDeepEngine:
             rank=int(cfg.rank), nccl_id=ctypes.cast(self._nccl_id, ctypes.c_char_p),
             persistent=1 if cfg.persistent else 0, debug=1 if cfg.debug else 0, pk_waves=int(cfg.pk_waves),
             comm_mode={"rccl": 0, "external": 1, "xgmi": 2}[cfg.comm], force_comm=1 if cfg.force_comm else 0,
+            auto_engine=1 if auto_engine else 0,
         )
         self._init = init
         self.max_indices = int(max_indices or self.data.shape[0])
@@ -248,6 +250,16 @@ class NetResDeepEngine:
             native.check(self.lib.dca_engine_ipc_selftest(self.h, src.data_ptr(), dst.data_ptr(), float(timeout_s),
                                                            ctypes.byref(timed_out)), "dca_engine_ipc_selftest")
             ok = ok and not timed_out.value and bool(torch.equal(dst, pat * float(w * (w + 1) // 2)))
+            if self.cfg.persistent:  # the same exchange as the step kernel's fc workers run it (in-step bucket A)
+                dst.fill_(float("nan"))
+                torch.cuda.synchronize(self.device)
+                lo, hi = ctypes.c_int(), ctypes.c_int()
+                native.check(self.lib.dca_engine_ipc_selftest_fc(self.h, src.data_ptr(), dst.data_ptr(),
+                                                                  float(timeout_s), ctypes.byref(timed_out),
+                                                                  ctypes.byref(lo), ctypes.byref(hi)),
+                             "dca_engine_ipc_selftest_fc")
+                want = pat[lo.value:hi.value] * float(w * (w + 1) // 2)
+                ok = ok and not timed_out.value and bool(torch.equal(dst[lo.value:hi.value], want))
         return ok
 
     def xgmi_bench(self, iters: int = 200) -> float:
@@ -326,17 +338,35 @@ class NetResDeepEngine:
                      "read_loss")
         return loss.value, steps.value
 
+    def run_checked(self, batch: int, steps: int) -> int:
+        """`steps` graph-replayed steps with the device error words checked after every 16-step chunk (pipelined:
+        the GPU never waits for the check).  Synchronous.  Raises (``check_errors``) as soon as an exchange timed
+        out -- a rank that stopped stepping is noticed within two chunks, not at the epoch end.  Returns the steps
+        run."""
+        done = ctypes.c_int()
+        rc = self.lib.dca_engine_run_checked(self.h, int(batch), int(steps), ctypes.byref(done))
+        if rc < 0:
+            native.check(rc, "dca_engine_run_checked")
+        if rc == 1:
+            self.check_errors()  # raises (and resets the words)
+            raise RuntimeError("engine error word set, but check_errors found none")
+        return int(done.value)
+
     def run_epoch(self, indices, batch: int, graph: bool = True) -> tuple[float, int]:
-        """One pass over `indices` in batches of `batch` (ragged last batch kept, drop_last=False)."""
+        """One pass over `indices` in batches of `batch` (ragged last batch kept, drop_last=False).  With graphs
+        the error words are checked after every chunk (``run_checked``)."""
         n = len(indices)
         self.set_indices(indices)
         self.set_cursor(0)
         self.read_loss(reset=True)
         full, rem = divmod(n, batch)
-        if full:
-            self.run(batch, full, graph)
-        if rem:
-            self.run(rem, 1, graph)
+        for b, k in ((batch, full), (rem, 1 if rem else 0)):
+            if not k:
+                continue
+            if graph and not (self.cfg.world_size > 1 and self.cfg.comm == "external"):
+                self.run_checked(b, k)
+            else:
+                self.run(b, k, graph)
         return self.read_loss(reset=True)
 
     # ---- introspection (tests) --------------------------------------------------------------------------

@@ -16,7 +16,7 @@ import torch  # noqa: F401  (must be imported before the native library, see mod
 
 from .. import build as _build
 
-ABI_VERSION = 4  # csrc/engine.hip dca_abi_version(): DcaInit layout / C signatures
+ABI_VERSION = 5  # csrc/engine.hip dca_abi_version(): DcaInit layout / C signatures
 _lock = threading.Lock()
 _lib = None
 
@@ -38,6 +38,7 @@ def _declare(lib):
     lib.dca_engine_read_loss.argtypes = [c_void_p, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(c_int), c_int]
     lib.dca_engine_run.argtypes = [c_void_p, c_int, c_int, c_int]
     lib.dca_engine_run_part.argtypes = [c_void_p, c_int, c_int]
+    lib.dca_engine_run_checked.argtypes = [c_void_p, c_int, c_int, ctypes.POINTER(c_int)]
     lib.dca_engine_sync.argtypes = [c_void_p]
     lib.dca_engine_stream.argtypes = [c_void_p]
     lib.dca_engine_stream.restype = c_void_p
@@ -48,6 +49,8 @@ def _declare(lib):
     lib.dca_engine_ipc_handle.argtypes = [c_void_p, ctypes.c_char_p]
     lib.dca_engine_ipc_open.argtypes = [c_void_p, ctypes.c_char_p, c_int]
     lib.dca_engine_ipc_selftest.argtypes = [c_void_p, c_void_p, c_void_p, ctypes.c_float, ctypes.POINTER(c_int)]
+    lib.dca_engine_ipc_selftest_fc.argtypes = [c_void_p, c_void_p, c_void_p, ctypes.c_float, ctypes.POINTER(c_int),
+                                               ctypes.POINTER(c_int), ctypes.POINTER(c_int)]
     lib.dca_engine_ipc_bench.argtypes = [c_void_p, c_void_p, c_void_p, c_int, ctypes.POINTER(ctypes.c_float)]
     lib.dca_engine_errors.argtypes = [c_void_p, ctypes.POINTER(ctypes.c_uint), c_int]  # flags[2]
     lib.dca_engine_precapture.argtypes = [c_void_p, c_int]

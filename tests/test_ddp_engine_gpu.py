@@ -191,12 +191,19 @@ def _xgmi_worker(rank, ws, port, dtype, persistent, q, comm="xgmi", own_device=F
             dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("ws,dtype,persistent", [(2, "bf16", True), (4, "bf16", True), (2, "fp32", True),
-                                                 (2, "fp32", False)])
-def test_xgmi_allreduce_ranks_one_gpu(gpu, port, ws, dtype, persistent):
+@pytest.mark.parametrize("ws,dtype,persistent,batch", [(2, "bf16", True, B), (4, "bf16", True, B),
+                                                       (2, "fp32", True, B), (2, "fp32", False, B),
+                                                       (3, "fp32", True, 8), (8, "bf16", True, 8),
+                                                       (8, "fp32", True, 4), (8, "bf16", False, 4)])
+def test_xgmi_allreduce_ranks_one_gpu(gpu, port, ws, dtype, persistent, batch):
+    """ws=8 (the node's world size): the sliced engine's reduction exchange with 8 peers (rank_sum_n<8> in
+    seg_exchange), its fc-worker exchange with 8 peers (construction self-test, FusedDDPTrainer), CC4 through 8
+    ranks, the multi-kernel engine's k_xgmi_ar_sgd with 8 peers.  A per-rank batch of <= 8 keeps each rank's step
+    grid (32 workgroups, one CU each) within its 256 / 8 CU budget."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    procs = [ctx.Process(target=_xgmi_worker, args=(r, ws, port, dtype, persistent, q)) for r in range(ws)]
+    procs = [ctx.Process(target=_xgmi_worker, args=(r, ws, port, dtype, persistent, q),
+                         kwargs=dict(batch=batch)) for r in range(ws)]
     for p in procs:
         p.start()
     res = [q.get(timeout=600) for _ in procs]
@@ -264,3 +271,60 @@ def test_bench_self_launch_sweep_shared_gpu(gpu):
     assert one["n_gpus"] == 1 and two["n_gpus"] == 2 and two["allreduce"] == "xgmi" and two["loss_finite"]
     assert len(two["per_rank_ms_per_step"]) == 2 and all(v > 0 for v in two["allreduce_us_per_step"])
     assert set(summary["scaling_efficiency"]) == {"1", "2"} and summary["scaling_efficiency"]["1"] == 1.0
+
+
+def _stall_worker(rank, ws, port, q):
+    """Rank 1 stops after 3 steps (fault injection: a peer that stops stepping); rank 0's run_epoch must raise
+    within 16 steps of the stall, not at the epoch end (the error words are checked after every 8-step chunk and the
+    exchanges fail fast once one has timed out)."""
+    try:
+        os.environ["MASTER_ADDR"] = "127.0.0.1"
+        os.environ["MASTER_PORT"] = str(port)
+        os.environ["DCA_XGMI_TIMEOUT_S"] = "1"
+        dist.init_process_group("gloo", rank=rank, world_size=ws)
+        from distributeddataparallel_cifar10_amd.data.synthetic import synthetic_cifar
+        from distributeddataparallel_cifar10_amd.models.netresdeep import NetResDeep
+        from distributeddataparallel_cifar10_amd.parallel.ddp import FusedDDPTrainer
+        dev = torch.device("cuda", 0)
+        data, labels = synthetic_cifar(NDATA, seed=5)
+        torch.manual_seed(0)
+        tr = FusedDDPTrainer(NetResDeep().to(dev), data.to(dev), labels.to(dev), batch_max=32, dtype="bf16",
+                             comm="xgmi", max_indices=NDATA)
+        assert tr.comm == "xgmi"
+        eng = tr.engine
+        batch, good = 8, 3
+        if rank == 0:
+            raised = False
+            try:
+                eng.run_epoch(list(range(NDATA)), batch)  # 32 steps; the peer is gone after step 3
+            except RuntimeError as ex:
+                raised = "xGMI" in str(ex)
+            assert raised, "a peer that stopped stepping was not reported"
+            _, steps = eng.read_loss()
+            assert good < steps <= good + 16, steps
+        else:
+            eng.set_indices(list(range(NDATA)))
+            eng.set_cursor(0)
+            eng.run(batch, good)
+            eng.sync()
+        dist.barrier()
+        tr.close()
+        q.put((rank, None))
+    except Exception:
+        q.put((rank, traceback.format_exc()))
+    finally:
+        if dist.is_initialized():
+            dist.destroy_process_group()
+
+
+def test_peer_stall_raises_within_16_steps(gpu, port):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_stall_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=600) for _ in procs]
+    for p in procs:
+        p.join(timeout=120)
+    bad = [r for r in res if r[1]]
+    assert not bad, "\n".join(f"rank {r}:\n{e}" for r, e in bad)

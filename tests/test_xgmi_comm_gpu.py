@@ -64,6 +64,7 @@ def _collective_worker(rank, ws, port, q):
         from distributeddataparallel_cifar10_amd.parallel.xgmi import XgmiComm
         comm = XgmiComm.create(max(SIZES), device=dev, timeout_s=60.0)
         assert comm is not None, "xGMI communicator did not come up (self-test failed)"
+        assert comm.nb == max(8, 128 // ws), comm.nb  # shared-device grid budget
         it = 0
         for rep in range(2):  # every (size, algo, wire) twice: both slab parities, advancing epochs
             for n in SIZES:
@@ -98,8 +99,11 @@ def _collective_worker(rank, ws, port, q):
             dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("ws", [2, 4])
+@pytest.mark.parametrize("ws", [2, 3, 4, 8])
 def test_xgmi_comm_exact_sums(gpu, port, ws):
+    """ws=8 is the node's world size (reference main.py:80-84: one rank per GPU): every 8-peer branch of the kernel
+    (rank_sum_n<8>, the two-shot allgather_n<.., 8>) runs here; ws=3 the odd ones.  The communicator splits its
+    default grid by the number of ranks sharing the device (128 / n workgroups), so all W grids are co-resident."""
     _spawn(_collective_worker, ws, port)
 
 
@@ -141,7 +145,9 @@ def _ddp_worker(rank, ws, port, algo, wire, q):
             dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("ws,algo,wire", [(2, "auto", "fp32"), (4, "twoshot", "fp32"), (2, "oneshot", "bf16")])
+@pytest.mark.parametrize("ws,algo,wire", [(2, "auto", "fp32"), (4, "twoshot", "fp32"), (2, "oneshot", "bf16"),
+                                          (3, "auto", "fp32"), (8, "oneshot", "fp32"), (8, "oneshot", "bf16"),
+                                          (8, "twoshot", "fp32"), (8, "twoshot", "bf16")])
 def test_flat_ddp_xgmi_matches_averaged_grads(gpu, port, ws, algo, wire):
     _spawn(_ddp_worker, ws, port, algo, wire)
 
