@@ -109,6 +109,8 @@ struct Engine {
   int staged_b = 0;  // persistent engine: batch slots of the current staging parity that hold the next batch
   int last_b = 0;    // batch size of the last enqueued step (BN slots are re-zeroed when it changes)
   int seg_ch = 64;   // gradient-segment layout (pks::seg_layout): trunk / conv1 chunk size
+  int red_in_step = 1;  // with fc_in_step, world size 1 or xGMI, not shared: the remaining gradient segments and the
+                        // bookkeeping run at the end of the step kernel (pks::red_worker): one kernel per step
   int fc_in_step = 1;  // the fc1 / fc-tail gradient segments run on the step kernel's fc workers (pks::N_FCW extra
                        // workgroups beside the backward); off: in the reduction kernel.  Off whenever the step and
                        // its fc workers would exceed the co-resident budget, and when xGMI peers share this device
@@ -174,6 +176,7 @@ static int alloc_workspace(Engine* e) {
       {"COMMT", 16}, {"PKW", PKW_N * 2},
       {"PKS_GRAN", 2 * (size_t)pks::LMAX * pks::GSTR * 8}, {"PKS_YH", 10 * (size_t)pks::LMAX * 2 * 512 * 4},
       {"PKS_BNX", 2 * (size_t)pks::LMAX * 64 * 4}, {"PKS_HDONE", (size_t)pks::LMAX * 8},
+      {"PKS_SDONE", (size_t)(pks::LMAX + pks::N_FCW) * 8},
       {"C1", e->in.debug ? bmax * 32 * 1024 * 4 : 16},
   };
   size_t total = 0;
@@ -227,6 +230,7 @@ static int alloc_workspace(Engine* e) {
   qa.gran = (unsigned long long*)e->regions["PKS_GRAN"];
   qa.bnx = (unsigned*)e->regions["PKS_BNX"];
   qa.hdone = (unsigned long long*)e->regions["PKS_HDONE"];
+  qa.sdone = (unsigned long long*)e->regions["PKS_SDONE"];
   qa.epoch = (int*)e->regions["EPOCH"];
   qa.err = (unsigned*)e->regions["ERR"];
   qa.tslab = (float*)e->regions["TSLAB"];
@@ -314,6 +318,10 @@ static int enqueue_step_persistent(Engine* e, int B, int part) {
     ra.mode = !multi ? 0 : (xgmi ? 2 : 1);
     ra.fc_in_step = fc_in_step_for(e, B) ? 1 : 0;
     ra.seg_ch = e->shared_device > 1 ? 256 : e->seg_ch;
+    // in-step reduction: needs the fc workers (the BN tail / bookkeeping pool layout assumes them), the fused SGD
+    // or the xGMI exchange (RCCL and the host all-reduce follow a separate reduction kernel), and a device of our
+    // own (ranks sharing one keep the budgeted, looped reduction kernel)
+    ra.red_in_step = e->red_in_step && ra.fc_in_step && ra.mode != 1 && e->shared_device <= 1 && part == 0 ? 1 : 0;
     if (e->shared_device > 1 && pks_grid(B) > share_budget(e)) {
       g_err = "shared-GPU rehearsal: " + std::to_string(e->shared_device) + " ranks x " + std::to_string(pks_grid(B)) +
               " step workgroups (batch " + std::to_string(B) + ") exceed the device's " + std::to_string(e->cu_slots) +
@@ -325,8 +333,9 @@ static int enqueue_step_persistent(Engine* e, int B, int part) {
       hipLaunchKernelGGL(pks::k_pks_step<0>, grid, dim3(pks::NTH), pks::Plan<0>::TOTAL, e->st, cx, e->qa, ra);
     else
       hipLaunchKernelGGL(pks::k_pks_step<1>, grid, dim3(pks::NTH), pks::Plan<1>::TOTAL, e->st, cx, e->qa, ra);
-    hipLaunchKernelGGL(pks::k_pks_reduce_ar, dim3(reduce_grid(e, pks::reduce_segments(ra.fc_in_step, ra.seg_ch) + 1)),
-                       dim3(256), pks::stage_floats(B) * 4, e->st, cx, e->qa, B * pks::S, ra);
+    if (!ra.red_in_step)
+      hipLaunchKernelGGL(pks::k_pks_reduce_ar, dim3(reduce_grid(e, pks::reduce_segments(ra.fc_in_step, ra.seg_ch) + 1)),
+                         dim3(256), pks::stage_floats(B) * 4, e->st, cx, e->qa, B * pks::S, ra);
   }
   if (multi && !xgmi) {  // RCCL (comm_mode 0, captured) or the host (comm_mode 1, between parts 1 and 2)
     if (part == 0) NCCK(ncclAllReduce(cx.grads, cx.grads, FLAT_N, ncclFloat32, ncclSum, e->comm, e->st));
@@ -458,6 +467,7 @@ static int engine_init(Engine* e, const DcaInit* in, int n_indices) {
     }
     e->resident = resident;
     if (const char* fo = getenv("DCA_PKS_FC_IN_STEP")) e->fc_in_step = fo[0] != '0';
+    if (const char* ro = getenv("DCA_PKS_RED_IN_STEP")) e->red_in_step = ro[0] != '0';
     if (const char* sc = getenv("DCA_PKS_SEG_CH")) e->seg_ch = atoi(sc) == 256 ? 256 : 64;
   }
   HIPCK(hipStreamCreateWithFlags(&e->st, hipStreamNonBlocking));
@@ -903,12 +913,15 @@ int dca_engine_ipc_selftest_fc(void* h, const float* src, float* dst, float time
   ra.seg_ch = e->shared_device > 1 ? 256 : e->seg_ch;
   dca::Ctx cx = e->base;
   cx.B = 0;  // no step workgroups: the whole grid is fc workers
+  // one workgroup per fc segment, or (ranks sharing the device) the rank's CU budget: every rank's workgroup f waits
+  // for its peers' workgroup f, so all ranks' grids must be co-resident (a step-kernel workgroup takes a whole CU)
+  const dim3 grid(std::min(dca::pks::N_FCW, dca::share_budget(e)));
   if (e->bf)
-    hipLaunchKernelGGL(dca::pks::k_pks_step<0>, dim3(dca::pks::N_FCW), dim3(dca::pks::NTH), dca::pks::Plan<0>::TOTAL,
-                       e->st, cx, e->qa, ra);
+    hipLaunchKernelGGL(dca::pks::k_pks_step<0>, grid, dim3(dca::pks::NTH), dca::pks::Plan<0>::TOTAL, e->st, cx, e->qa,
+                       ra);
   else
-    hipLaunchKernelGGL(dca::pks::k_pks_step<1>, dim3(dca::pks::N_FCW), dim3(dca::pks::NTH), dca::pks::Plan<1>::TOTAL,
-                       e->st, cx, e->qa, ra);
+    hipLaunchKernelGGL(dca::pks::k_pks_step<1>, grid, dim3(dca::pks::NTH), dca::pks::Plan<1>::TOTAL, e->st, cx, e->qa,
+                       ra);
   HIPCK(hipGetLastError());
   HIPCK(hipStreamSynchronize(e->st));
   unsigned f[2] = {0, 0};

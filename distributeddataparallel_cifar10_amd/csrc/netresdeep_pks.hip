@@ -54,6 +54,7 @@ struct Args {
   unsigned long long* gran;  // [2][LMAX][GSTR] granules (halo rows, head partials)
   unsigned* bnx;             // [2][LMAX][64] BatchNorm partials, 4-byte self-tagged values (see bn_tag)
   unsigned long long* hdone; // [LMAX] head-done granules {tagof(epoch, RND_HDONE), 0} (fc workers' start signal)
+  unsigned long long* sdone; // [LMAX + N_FCW] slab-done granules {tagof(epoch, RND_SDONE), 0} (in-step reduction)
   int* epoch;                // device scalar, advanced by the reduce kernel after every step
   unsigned* err;             // bit r: exchange round r timed out
   float* tslab;              // [LMAX][WSLAB_N] trunk wgrad per workgroup (fragment order, read by k_pks_reduce)
@@ -238,8 +239,14 @@ __device__ __forceinline__ float xsum_row16(float a) {
 // per-workgroup channel sums of per-thread partials (a, b: channel 16h + c of wave 4h + w), delivered to the
 // publishing threads: thread t < 64 returns slot t (t < 32: sum of a for channel t, else sum of b for channel
 // t - 32).  One LDS barrier.
+// FRESH: re-derive the thread's LDS offsets here (an opaque copy of threadIdx.x) instead of letting the compiler keep
+// them live from the kernel's start -- the stem backward's call is the only use after the 20 blocks, and holding its
+// address through them spilled a VGPR to scratch.
+template <bool FRESH = false>
 __device__ __forceinline__ float wg_csum(float a, float b, float* cred) {
-  const int t = threadIdx.x, wv = t >> 6, lane = t & 63, c = lane & 15;
+  int t = threadIdx.x;
+  if constexpr (FRESH) asm volatile("v_mov_b32 %0, %1" : "=v"(t) : "v"(t));
+  const int wv = t >> 6, lane = t & 63, c = lane & 15;
   a = xsum_rows(a);
   b = xsum_rows(b);
   // [2 halves][32: a | b of 16 channels][RS rows], disjoint from the sweep combine area: a publishing thread reads
@@ -591,6 +598,7 @@ constexpr int SEG_MAX = 1024;
 constexpr int NSEG_MAX = WSLAB_N / 64 + (SSLAB_N + 63) / 64 + R_FC1 + 2;  // 227: flag-array stride per rank
 constexpr int N_FCW = R_FC1 + 1;                   // fc workers of the step kernel
 constexpr int RND_HDONE = 30;                      // tag round of the head-done granules (fc workers' start)
+constexpr int RND_SDONE = 31;                      // tag round of the slab-done granules (in-step reduction)
 struct SegLayout {
   int ch, r_trunk, r_ts, fct, bnt, nseg, off_fc1, off_fct, off_bnt;
 };
@@ -628,6 +636,8 @@ struct RedAr {
   int mode;
   int fc_in_step;             // the fc1 / fc-tail segments run on the step kernel's fc workers
   int seg_ch;                 // segment layout (seg_layout): 64 or 256
+  int red_in_step;            // the trunk / conv1 / BN-tail segments and the bookkeeping run at the end of the step
+                              // kernel (red_worker) instead of in k_pks_reduce_ar (needs fc_in_step)
 };
 
 __device__ __forceinline__ char* rbase(const RedAr& ra, int q) { return ra.peers.base[q] + xg::REGION_BYTES; }
@@ -728,13 +738,18 @@ __device__ __forceinline__ void seg_chunk(const Ctx& cx, const Args& pa, const S
   const float* src = stem ? cx.SSLAB : pa.tslab;
   const int stride = stem ? SSLAB_N : WSLAB_N;
   const int ec = e0 < stride ? e0 : stride - 4;  // conv1's last 256-chunk is partial (1088 = 4.25 x 256)
+  // sc1 loads: the slabs were written through (sc1) by workgroups on any XCD, possibly inside this very launch
+  // (red_worker); this CU's L2 may still hold last step's lines of them
+  const __amdgpu_buffer_rsrc_t rs =
+      __builtin_amdgcn_make_buffer_rsrc((void*)src, (short)0, nslab * stride * 4, 0x00020000);
   f32x4 sacc = z4();
   for (int k0 = 0; k0 < nslab; k0 += 128) {
     f32x4 v[NU];
 #pragma unroll
     for (int u = 0; u < NU; ++u) {
       const int k = k0 + grp + NG * u;
-      v[u] = ld4(src + (size_t)(k < nslab ? k : nslab - 1) * stride + ec);
+      v[u] = __builtin_bit_cast(
+          f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, ((k < nslab ? k : nslab - 1) * stride + ec) * 4, 0, 16));
     }
 #pragma unroll
     for (int u = 0; u < NU; ++u)
@@ -886,11 +901,39 @@ __device__ void seg_process(const Ctx& cx, const Args& pa, const RedAr& ra, int 
   DCA_STAMP(cx, sslot, swg, 3);
 }
 
+// batch-mean loss, cursor, step / BN-batch counters, epoch: independent of every segment, so it runs beside them
+__device__ __forceinline__ void pks_bookkeeping(const Ctx& cx, const Args& pa) {
+  const int t = threadIdx.x, B = cx.B;
+  if (t >= 64) return;
+  // B <= 64; sc1: written through by the slice-0 workgroups, possibly inside this launch (red_worker)
+  float l = t < B ? __uint_as_float(__hip_atomic_load((const unsigned*)cx.HLOSS + t, __ATOMIC_RELAXED,
+                                                      __HIP_MEMORY_SCOPE_AGENT)) : 0.f;
+  double acc = 0.0;
+  int cur = 0, stp = 0, ep = 0;
+  long long nb = 0;
+  if (t == 0) {  // issued together with the loss loads: one memory round trip, not five dependent ones
+    acc = *cx.loss_acc;
+    cur = *cx.cursor;
+    stp = *cx.step_count;
+    nb = *cx.nbt;
+    ep = *pa.epoch;
+  }
+#pragma unroll
+  for (int m = 1; m < 64; m <<= 1) l += __shfl_xor(l, m);  // fixed tree: identical every step
+  if (t == 0) {
+    *cx.loss_acc = acc + (double)(l / (float)B);
+    *cx.cursor = cur + B;
+    *cx.step_count = stp + 1;
+    *cx.nbt = nb + NBLK;  // BatchNorm num_batches_tracked: +1 per application
+    *pa.epoch = (int)(((unsigned)ep + 1u) % EPOCH_WRAP);
+  }
+}
+
 // fc worker fb (0 .. R_FC1 - 1: fc1 block fb; R_FC1: fc tail) of the step kernel: waits until every main workgroup
 // has published its head-done granule (its pooled features HP and, slice 0, the image's dh / h / dlogits are
 // written through and drained), then runs the segment (compute, xGMI exchange, SGD) beside the trunk backward.
 template <int P>
-__device__ void fc_worker(const Ctx& cx, const Args& pa, const RedAr& ra, int fb, char* smem) {
+__device__ void fc_segment(const Ctx& cx, const Args& pa, const RedAr& ra, int fb, char* smem) {
   const int t = threadIdx.x, lane = t & 63, G = cx.B * S;
   const int epoch = *pa.epoch;
   DCA_STAMP(cx, 9, fb, 0);
@@ -919,21 +962,74 @@ __device__ void fc_worker(const Ctx& cx, const Args& pa, const RedAr& ra, int fb
   seg_process<NTH>(cx, pa, ra, fb < R_FC1 ? Ls.r_ts + fb : Ls.fct, G, segv, red, stage, s_ep, 9, fb);
 }
 
+// In-step gradient reduction (ra.red_in_step; replaces k_pks_reduce_ar and the kernel boundary before it).  Every
+// member of the pool -- the G step workgroups (pool index L, once their trunk / conv1 slabs are written through) and
+// the fc workers (G + fb, once their fc segment is done) -- publishes a slab-done granule, waits for all of them
+// (so every slab is complete AND every workgroup of the launch has long read this step's epoch), then runs its
+// share of the remaining segments: v = 0 the BN tail (pool index 0 = logical workgroup 0, which itself wrote the
+// BN-affine gradients and the running statistics), v = 1 .. r_ts the trunk / conv1 chunks (sc1 slab loads), v =
+// r_ts + 1 the step's bookkeeping (loss, cursor, counters, epoch); each segment with its xGMI exchange (world size
+// > 1) and SGD, exactly as in k_pks_reduce_ar.  The slab hand-off is the guide's sc1-store / agent-granule form (no
+// release fence: the slabs are write-through; the readers' loads are sc1).
+__device__ void red_worker(const Ctx& cx, const Args& pa, const RedAr& ra, int epoch, int pidx, char* smem) {
+  const int t = threadIdx.x, lane = t & 63, G = cx.B * S;
+  const int nfcw = ra.fc_in_step ? N_FCW : 0, pool = G + nfcw;
+  const unsigned tag = tagof(epoch, RND_SDONE);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this thread's write-through slab / head stores are performed
+  __syncthreads();                                    // ... and every thread's of this workgroup
+  if (t == 0) gput(pa.sdone + (pidx < G ? pidx : LMAX + pidx - G), tag, 0.f);
+  const SegLayout Ls = seg_layout(ra.seg_ch);
+  const int nv = Ls.r_ts + 2;  // BN tail, r_ts chunks, bookkeeping
+  if (pidx >= nv) return;      // nothing to do (the granule above still counts this workgroup in)
+  // One wave polls every member's granule.  Step workgroups poll back to back (their wait is on the step's critical
+  // path, ~1 us); fc workers arrive ~30 us early and sleep between passes, so their polling does not load the memory
+  // system under the trunk backward's latency-bound exchanges.
+  const int nap = pidx >= G ? 8 : 0;
+  DCA_STAMP(cx, 10, pidx, 0);
+  if (t < 64) {
+    for (unsigned spins = 0;; ++spins) {
+      bool ok = true;
+      for (int k = lane; k < pool; k += 64) {
+        const unsigned long long* g = pa.sdone + (k < G ? k : LMAX + k - G);
+        ok &= (unsigned)(__hip_atomic_load(g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >> 32) == tag;
+      }
+      if (__all(ok)) break;
+      if (spins >= SPIN_LIMIT) {
+        if (lane == 0) atomicOr(pa.err, 1u << 29);
+        break;
+      }
+      sleep_units(nap);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  __syncthreads();
+  DCA_STAMP(cx, 10, pidx, 1);
+  float* segv = (float*)smem;
+  f32x4* red = (f32x4*)(smem + SEG_MAX * 4);
+  float* stage = (float*)(smem + SEG_MAX * 4 + NTH * 16);
+  int* s_ep = (int*)(smem + SEG_MAX * 4 + NTH * 16 + stage_floats(cx.B) * 4);
+  for (int v = pidx; v < nv; v += pool) {
+    if (v == nv - 1) {
+      pks_bookkeeping(cx, pa);
+      continue;
+    }
+    DCA_STAMP(cx, 8, v, 0);
+    seg_process<NTH>(cx, pa, ra, v == 0 ? Ls.bnt : v - 1, G, segv, red, stage, s_ep, 8, v);
+    __syncthreads();  // segv / red are reused by the next segment
+  }
+}
+
 constexpr int P_KSHIFT = 906;  // misc: [10][32] BN shifts (last step's batch means)
 constexpr int P_LABEL = 1240;  // misc: this image's label
 
 // ============================================================================================================
+// The step of one main workgroup (slice s of image n).  pidx / ep_out: its in-step reduction pool index and the step
+// epoch (left at -1 by the padding workgroups of a batch that is not a multiple of 8).
 template <int P>
-__global__ void __launch_bounds__(NTH) k_pks_step(Ctx cx, Args pa, RedAr ra) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
+__device__ __forceinline__ void step_main(const Ctx& cx, const Args& pa, const RedAr& ra, char* smem, int& pidx,
+                                          int& ep_out) {
   using PL = Plan<P>;
-  {  // workgroups past the main grid are the fc workers (only launched with ra.fc_in_step)
-    const int gmain = (cx.B + 7) / 8 * 8 * S;
-    if ((int)blockIdx.x >= gmain) {
-      fc_worker<P>(cx, pa, ra, (int)blockIdx.x - gmain, smem);
-      return;
-    }
-  }
   const int t = threadIdx.x, wv = t >> 6, lane = t & 63, c = lane & 15, q = lane >> 4;
   const int w = wv & (RS - 1), hh = wv / RS, ch = 16 * hh + c;  // image row (in the slice), channel half, channel
   // Placement (speed only, never correctness): blocks b and b + 8 share an XCD under the observed round-robin
@@ -1569,10 +1665,10 @@ __global__ void __launch_bounds__(NTH) k_pks_step(Ctx cx, Args pa, RedAr ra) {
       }
     }
     // conv1 bias gradient partial of this workgroup (also the barrier before the MFMAs)
-    const float dbv = wg_csum(db, 0.f, cred);
+    const float dbv = wg_csum<true>(db, 0.f, cred);
     DCA_STAMP(cx, 5, L, 3);
     float* ss = cx.SSLAB + (size_t)L * SSLAB_N;
-    if (t < 32) ss[1024 + t] = dbv;
+    if (t < 32) st1_wt(ss + 1024 + t, dbv);  // write-through: read by the reduction (possibly in this launch)
     // D[co][k] = sum over this slice's conv pixels of ds[p][co] * im2col[p][k]; K step = one conv row (32 px).
     // Wave wv: tile wv & 3 (mt = co half, nt = k tile), conv rows 4 (wv >> 2) .. +3; k >= 27 columns are
     // discarded by the reduce
@@ -1615,6 +1711,32 @@ __global__ void __launch_bounds__(NTH) k_pks_step(Ctx cx, Args pa, RedAr ra) {
     }
   }
   DCA_STAMP(cx, 5, L, 7);
+  pidx = L;
+  ep_out = epoch;
+}
+
+template <int P>
+__global__ void __launch_bounds__(NTH) k_pks_step(Ctx cx, Args pa, RedAr ra) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  int pidx = -1, ep = 0;
+  const int gmain = (cx.B + 7) / 8 * 8 * S;
+  if ((int)blockIdx.x >= gmain) {  // workgroups past the main grid are the fc workers (only with ra.fc_in_step)
+    const int fb = (int)blockIdx.x - gmain, nfw = (int)gridDim.x - gmain;
+    // one fc segment each in a training step (nfw == N_FCW); the self-test on a shared device launches fewer
+    // workers (its per-rank CU budget), which then take the segments in turn
+    for (int f = fb; f < N_FCW; f += nfw) {
+      if (f != fb) __syncthreads();
+      fc_segment<P>(cx, pa, ra, f, smem);
+    }
+    pidx = cx.B * S + fb;
+    ep = *pa.epoch;  // unchanged: the bookkeeping waits for this workgroup's slab-done granule
+  } else {
+    step_main<P>(cx, pa, ra, smem, pidx, ep);
+  }
+  if (pidx >= 0 && ra.red_in_step) {
+    __syncthreads();  // every wave is done with its LDS before red_worker reuses it
+    red_worker(cx, pa, ra, ep, pidx, smem);
+  }
 }
 
 
@@ -1632,32 +1754,6 @@ __global__ void __launch_bounds__(256) k_pks_prime(Ctx cx, Args pa) {
 // tail when the step kernel did not run them), each followed by its exchange and SGD; one more workgroup does the
 // step's bookkeeping.  mode 3 (self-test): every segment, no bookkeeping.
 // ============================================================================================================
-// batch-mean loss, cursor, step / BN-batch counters, epoch: independent of every segment, so it runs beside them
-__device__ __forceinline__ void pks_bookkeeping(const Ctx& cx, const Args& pa) {
-  const int t = threadIdx.x, B = cx.B;
-  if (t >= 64) return;
-  float l = t < B ? cx.HLOSS[t] : 0.f;  // B <= 64
-  double acc = 0.0;
-  int cur = 0, stp = 0, ep = 0;
-  long long nb = 0;
-  if (t == 0) {  // issued together with the loss loads: one memory round trip, not five dependent ones
-    acc = *cx.loss_acc;
-    cur = *cx.cursor;
-    stp = *cx.step_count;
-    nb = *cx.nbt;
-    ep = *pa.epoch;
-  }
-#pragma unroll
-  for (int m = 1; m < 64; m <<= 1) l += __shfl_xor(l, m);  // fixed tree: identical every step
-  if (t == 0) {
-    *cx.loss_acc = acc + (double)(l / (float)B);
-    *cx.cursor = cur + B;
-    *cx.step_count = stp + 1;
-    *cx.nbt = nb + NBLK;  // BatchNorm num_batches_tracked: +1 per application
-    *pa.epoch = (int)(((unsigned)ep + 1u) % EPOCH_WRAP);
-  }
-}
-
 // grid: reduce_grid(ra) + 1
 __host__ __device__ inline int reduce_segments(int fc_in_step, int seg_ch) {
   return fc_in_step ? seg_layout(seg_ch).r_ts + 1 : seg_layout(seg_ch).nseg;

@@ -108,6 +108,7 @@ class FlatBucketDDP(nn.Module):
         self._sync_next_forward = True
         self.timing = False  # True: record the comm-stream span of every step (comm_time(); metrics)
         self._comm_events: list = []
+        self._flat_buffers = self._rehome_buffers(dev)
         self._sync_module_states()  # CC3
         self.comm, self.xgmi, self._comm_stream = "process_group" if self.world_size > 1 else "none", None, None
         self._wire, self._algo = wire, algo
@@ -134,21 +135,49 @@ class FlatBucketDDP(nn.Module):
             dist.broadcast(self.flat, 0, group=self.process_group)
         self._broadcast_buffers_now()
 
-    def _broadcast_buffers_now(self) -> None:
-        bufs = [b for b in self.module.buffers()]
-        if not bufs or self.world_size == 1:
-            return
-        by_dtype = {}
-        for b in bufs:
-            by_dtype.setdefault(b.dtype, []).append(b)
+    def _rehome_buffers(self, dev) -> list:
+        """Module buffers (BN running mean / var, num_batches_tracked) become views of ONE flat tensor per dtype,
+        like the parameters: CC4 is then one in-place broadcast per dtype -- no concatenation before it and no
+        per-buffer copy after it (torch DDP coalesces into a temporary and copies back).  A buffer shared by
+        several modules (NetResDeep's one ResBlock applied 10x) is re-homed once and stays shared.  Buffers on
+        another device than the parameters keep their own storage (broadcast as they are)."""
+        seen, groups = {}, {}
+        for mod in self.module.modules():
+            for name, b in mod._buffers.items():
+                if b is None:
+                    continue
+                key = id(b)
+                if key not in seen:
+                    seen[key] = (b, [])
+                    if b.device == dev:
+                        groups.setdefault(b.dtype, []).append(key)
+                seen[key][1].append((mod, name))
+        flats = []
         with torch.no_grad():
-            for group in by_dtype.values():  # one coalesced broadcast per dtype
-                flat = torch.cat([b.reshape(-1) for b in group])
-                dist.broadcast(flat, 0, group=self.process_group)
+            for dtype, keys in groups.items():
+                total = sum(seen[k][0].numel() for k in keys)
+                flat = torch.empty(total, dtype=dtype, device=dev)
                 o = 0
-                for b in group:
-                    b.copy_(flat[o:o + b.numel()].view_as(b))
-                    o += b.numel()
+                for k in keys:
+                    b, users = seen[k]
+                    n = b.numel()
+                    v = flat[o:o + n].view_as(b)
+                    v.copy_(b)
+                    for mod, name in users:
+                        mod._buffers[name] = v
+                    o += n
+                flats.append(flat)
+        self._loose_buffers = [seen[k][0] for k in seen if seen[k][0].device != dev]
+        return flats
+
+    def _broadcast_buffers_now(self) -> None:
+        if self.world_size == 1:
+            return
+        with torch.no_grad():
+            for flat in self._flat_buffers:  # one in-place broadcast per dtype (the buffers are views of it)
+                dist.broadcast(flat, 0, group=self.process_group)
+            for b in self._loose_buffers:
+                dist.broadcast(b, 0, group=self.process_group)
 
     def _make_hook(self, p):
         ready = self._make_ready(p)

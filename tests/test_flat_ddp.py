@@ -94,6 +94,44 @@ def _case_buffer_broadcast_every_forward(rank, ws):
     assert int(bn.num_batches_tracked) == 10
 
 
+def _case_flat_buffers_one_broadcast_per_dtype(rank, ws):
+    """Buffers are views of one flat tensor per dtype (like the parameters), so CC4 is one in-place broadcast per
+    dtype: 2 collectives (fp32 running stats, int64 counters) and no concatenation / copy-back per forward.  The
+    ResNet's BN buffers and NetResDeep's shared ResBlock (one BN applied 10x) both stay intact."""
+    from distributeddataparallel_cifar10_amd.models.resnet50 import ResNet
+    torch.manual_seed(0)
+    for m in (NetResDeep(), ResNet([1, 1, 1, 1], num_classes=10)):
+        ddp = FlatBucketDDP(m)
+        bufs = list(m.buffers())
+        flats = {f.dtype: f for f in ddp._flat_buffers}
+        assert set(flats) == {torch.float32, torch.int64} and len(ddp._flat_buffers) == 2
+        assert sum(f.numel() for f in flats.values()) == sum(b.numel() for b in bufs)
+        for b in bufs:  # every buffer lives inside its dtype's flat tensor
+            f = flats[b.dtype]
+            assert f.data_ptr() <= b.data_ptr() < f.data_ptr() + f.numel() * f.element_size()
+        if isinstance(m, NetResDeep):  # the 10 applications still share one BN module
+            assert len({id(blk.batch_norm) for blk in m.resblocks}) == 1
+        with torch.no_grad():  # ranks diverge between forwards (SURVEY.md Q8)
+            for b in bufs:
+                b.fill_(rank + 1)
+        calls = []
+        real = dist.broadcast
+
+        def counting(t, src, group=None, async_op=False):
+            calls.append((str(t.dtype), t.numel()))
+            return real(t, src, group=group, async_op=async_op)
+
+        dist.broadcast = counting
+        try:
+            ddp.eval()
+            with torch.no_grad():
+                ddp(torch.randn(2, 3, 32, 32))  # eval forward: CC4 only, buffers untouched by the BN itself
+        finally:
+            dist.broadcast = real
+        assert sorted(calls) == sorted((str(f.dtype), f.numel()) for f in flats.values()), calls
+        assert all(bool((b == 1).all()) for b in bufs)  # rank 0's buffers everywhere
+
+
 def _case_matches_torch_ddp(rank, ws):
     torch.manual_seed(3)
     base = NetResDeep()
@@ -121,7 +159,7 @@ def _case_matches_torch_ddp(rank, ws):
 
 
 @pytest.mark.parametrize("case", [_case_init_broadcast_and_grad_average, _case_buffer_broadcast_every_forward,
-                                  _case_matches_torch_ddp])
+                                  _case_matches_torch_ddp, _case_flat_buffers_one_broadcast_per_dtype])
 def test_flat_ddp_gloo(case, port):
     _spawn(case, port)
 
