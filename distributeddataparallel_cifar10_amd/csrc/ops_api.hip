@@ -160,7 +160,7 @@ using namespace dca::ops;
 extern "C" {
 
 const char* dca_ops_last_error() { return g_err.c_str(); }
-int dca_ops_abi_version() { return 7; }
+int dca_ops_abi_version() { return 8; }
 
 // Must match ops/_native.py::GemmArgs.
 int dca_ops_gemm(const GemmArgs* a, void* stream) {
@@ -661,29 +661,89 @@ int dca_ops_maxpool_bwd(const void* dy, const void* arg, void* dx, const PoolGeo
   return 0;
 }
 
-int dca_ops_avgpool_fwd(const void* x, float* y, int N, int HW, int C, void* stream) {
-  hipLaunchKernelGGL(k_avgpool_fwd, dim3((C + 255) / 256, N), dim3(256), 0, (hipStream_t)stream, (const bf16_t*)x, y,
-                     N, HW, C);
-  OPCK(hipGetLastError());
-  return 0;
-}
-
-int dca_ops_avgpool_bwd(const float* dy, void* dx, int N, int HW, int C, void* stream) {
-  if (C % 8 == 0 && (long)N * HW * C + 8192L * 256 * 8 < (1L << 31))
-    hipLaunchKernelGGL(k_avgpool_bwd8, dim3(grid_for((long)N * HW * C / 8)), dim3(256), 0, (hipStream_t)stream, dy,
-                       (bf16_t*)dx, N, HW, C);
+// y: fp32 [N][C], or bf16 with out_bf16 (the fc GEMM operand directly)
+int dca_ops_avgpool_fwd(const void* x, void* y, int N, int HW, int C, int out_bf16, void* stream) {
+  const dim3 grid((C + 255) / 256, N);
+  if (out_bf16)
+    hipLaunchKernelGGL(k_avgpool_fwd<bf16_t>, grid, dim3(256), 0, (hipStream_t)stream, (const bf16_t*)x, (bf16_t*)y,
+                       N, HW, C);
   else
-    hipLaunchKernelGGL(k_avgpool_bwd, dim3(grid_for((long)N * HW * C)), dim3(256), 0, (hipStream_t)stream, dy,
-                       (bf16_t*)dx, N, HW, C);
+    hipLaunchKernelGGL(k_avgpool_fwd<float>, grid, dim3(256), 0, (hipStream_t)stream, (const bf16_t*)x, (float*)y, N,
+                       HW, C);
   OPCK(hipGetLastError());
   return 0;
 }
 
+// dy: fp32 [N][C], or bf16 with dy_bf16
+int dca_ops_avgpool_bwd(const void* dy, void* dx, int N, int HW, int C, int dy_bf16, void* stream) {
+  const bool v8 = C % 8 == 0 && (long)N * HW * C + 8192L * 256 * 8 < (1L << 31);
+  REQUIRE(v8 || !dy_bf16, "avgpool_bwd: a bf16 dy needs C % 8 == 0");
+  if (v8 && dy_bf16)
+    hipLaunchKernelGGL(k_avgpool_bwd8<bf16_t>, dim3(grid_for((long)N * HW * C / 8)), dim3(256), 0, (hipStream_t)stream,
+                       (const bf16_t*)dy, (bf16_t*)dx, N, HW, C);
+  else if (v8)
+    hipLaunchKernelGGL(k_avgpool_bwd8<float>, dim3(grid_for((long)N * HW * C / 8)), dim3(256), 0, (hipStream_t)stream,
+                       (const float*)dy, (bf16_t*)dx, N, HW, C);
+  else
+    hipLaunchKernelGGL(k_avgpool_bwd, dim3(grid_for((long)N * HW * C)), dim3(256), 0, (hipStream_t)stream,
+                       (const float*)dy, (bf16_t*)dx, N, HW, C);
+  OPCK(hipGetLastError());
+  return 0;
+}
+
+// loss_mean / ticket (optional, both or neither): the batch-mean loss written in the same launch
 int dca_ops_cross_entropy(const float* logits, const long* labels, float* loss, float* dlogits, int B, int K,
-                          float grad_scale, void* stream) {
+                          float grad_scale, float* loss_mean, unsigned* ticket, void* stream) {
   REQUIRE(B > 0 && K > 0, "cross_entropy: empty input");
+  REQUIRE((loss_mean == nullptr) == (ticket == nullptr), "cross_entropy: loss_mean needs a ticket word");
   hipLaunchKernelGGL(k_cross_entropy, dim3(B), dim3(64), 0, (hipStream_t)stream, logits, labels, loss, dlogits, B, K,
-                     grad_scale);
+                     grad_scale, loss_mean, ticket);
+  OPCK(hipGetLastError());
+  return 0;
+}
+
+// zero `bytes` bytes on the stream (a gradient buffer before the backward): the runtime's fill, no ATen kernel
+int dca_ops_zero(void* p, long bytes, void* stream) {
+  OPCK(hipMemsetAsync(p, 0, (size_t)bytes, (hipStream_t)stream));
+  return 0;
+}
+
+int dca_ops_scale_dev(const float* x, const float* s, float* out, long n, void* stream) {
+  hipLaunchKernelGGL(k_scale_dev, dim3(grid_for(n, 256, 2048)), dim3(256), 0, (hipStream_t)stream, x, s, out, n);
+  OPCK(hipGetLastError());
+  return 0;
+}
+
+int dca_ops_cast_bf16(const float* x, void* y, long n, void* stream) {
+  hipLaunchKernelGGL(k_cast_bf16, dim3(grid_for(n, 256, 2048)), dim3(256), 0, (hipStream_t)stream, x, (bf16_t*)y, n);
+  OPCK(hipGetLastError());
+  return 0;
+}
+
+// ptrs: device array of n int64 pointers
+int dca_ops_add_i64(void* ptrs, int n, void* stream) {
+  REQUIRE(n > 0, "add_i64: empty");
+  hipLaunchKernelGGL(k_add_i64, dim3(1), dim3(64), 0, (hipStream_t)stream, (long long* const*)ptrs, n);
+  OPCK(hipGetLastError());
+  return 0;
+}
+
+// dy [R][N] (dy_bf16: bf16, else fp32), y: optional ReLU mask source [R][N] (y_bf16: bf16, else fp32); dyb: optional
+// bf16 copy of the masked dy; db [N] fp32 column sums; part: nblk * N floats; ticket: a zeroed device word.
+int dca_ops_dy_prep(const void* dy, int dy_bf16, const void* y, int y_bf16, void* dyb, float* part, float* db,
+                    unsigned* ticket, long R, int N, int nblk, void* stream) {
+  REQUIRE(R > 0 && N > 0 && nblk > 0 && R < (1L << 31), "dy_prep: bad shape");
+  const int rpb = (int)((R + nblk - 1) / nblk);
+  hipStream_t st = (hipStream_t)stream;
+  const dim3 g(nblk), b(256);
+#define DYP(TD, TY) \
+  hipLaunchKernelGGL((k_dy_prep<TD, TY>), g, b, 0, st, (const TD*)dy, (const TY*)y, (bf16_t*)dyb, part, db, ticket, \
+                     (int)R, N, rpb)
+  if (dy_bf16 && y_bf16) DYP(bf16_t, bf16_t);
+  else if (dy_bf16) DYP(bf16_t, float);
+  else if (y_bf16) DYP(float, bf16_t);
+  else DYP(float, float);
+#undef DYP
   OPCK(hipGetLastError());
   return 0;
 }

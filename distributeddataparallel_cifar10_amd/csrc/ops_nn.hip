@@ -700,23 +700,38 @@ __global__ void __launch_bounds__(256) k_maxpool_bwd(const bf16_t* __restrict__ 
 }
 
 // global average pool [N][HW][C] -> [N][C] (fp32 out) and its backward (broadcast / HW, bf16 out)
-__global__ void __launch_bounds__(256) k_avgpool_fwd(const bf16_t* __restrict__ x, float* __restrict__ y, int N,
+// TO: float (fp32 features) or bf16_t (the bf16 operand of the following fc GEMM, no separate cast pass)
+template <typename TO>
+__global__ void __launch_bounds__(256) k_avgpool_fwd(const bf16_t* __restrict__ x, TO* __restrict__ y, int N,
                                                      int HW, int C) {
   const int c = blockIdx.x * 256 + threadIdx.x, n = blockIdx.y;
   if (c >= C) return;
   float s = 0.f;
   for (int p = 0; p < HW; ++p) s += ld_bf(x + ((long)n * HW + p) * C + c);
-  y[(long)n * C + c] = s / HW;
+  if constexpr (sizeof(TO) == 2) y[(long)n * C + c] = f2bf_rne(s / HW);
+  else y[(long)n * C + c] = s / HW;
 }
-// C % 8 == 0: one thread per pixel and 8 channels (two 16-B dy loads, one 16-B store), 32-bit index decode
-__global__ void __launch_bounds__(256) k_avgpool_bwd8(const float* __restrict__ dy, bf16_t* __restrict__ dx, int N,
+// C % 8 == 0: one thread per pixel and 8 channels (dy: two 16-B fp32 loads or one 16-B bf16 load, one 16-B store),
+// 32-bit index decode
+template <typename TD>
+__global__ void __launch_bounds__(256) k_avgpool_bwd8(const TD* __restrict__ dy, bf16_t* __restrict__ dx, int N,
                                                       int HW, int C) {
   const unsigned cg = (unsigned)C >> 3, per_n = (unsigned)HW * cg, total = (unsigned)N * per_n;
   const float hw = (float)HW;
   for (unsigned i = blockIdx.x * 256u + threadIdx.x; i < total; i += gridDim.x * 256u) {
     const unsigned n = i / per_n, c = (i % cg) * 8u;
-    const f32x4 a = *(const f32x4*)(dy + n * (unsigned)C + c), b = *(const f32x4*)(dy + n * (unsigned)C + c + 4);
-    float v[8] = {a[0] / hw, a[1] / hw, a[2] / hw, a[3] / hw, b[0] / hw, b[1] / hw, b[2] / hw, b[3] / hw};
+    float v[8];
+    if constexpr (sizeof(TD) == 2) {
+      unpack8(*(const uint4*)(dy + n * (unsigned)C + c), v);
+    } else {
+      const f32x4 a = *(const f32x4*)(dy + n * (unsigned)C + c), b = *(const f32x4*)(dy + n * (unsigned)C + c + 4);
+      for (int j = 0; j < 4; ++j) {
+        v[j] = a[j];
+        v[4 + j] = b[j];
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] /= hw;
     *(uint4*)(dx + 8ul * i) = pack8(v);
   }
 }
@@ -733,9 +748,14 @@ __global__ void __launch_bounds__(256) k_avgpool_bwd(const float* __restrict__ d
 // ---------------------------------------------------------------------------------------------------------
 // Cross-entropy (mean over the batch): per-row loss and dlogits = (softmax - onehot) / B.  One wave per row.
 // ---------------------------------------------------------------------------------------------------------
+// loss_mean (optional): the batch mean of the row losses, computed by the last row's workgroup to finish (agent-scope
+// ticket; the rows' losses are stored write-through and read back with sc1 loads -- the guide's in-launch
+// reduction), summed in a fixed order (bitwise reproducible), so the mean needs no separate reduction kernel.
+// *ticket must be 0 at launch; the last workgroup resets it.
 __global__ void __launch_bounds__(64) k_cross_entropy(const float* __restrict__ logits, const long* __restrict__ labels,
                                                       float* __restrict__ loss, float* __restrict__ dlogits, int B,
-                                                      int K, float grad_scale) {
+                                                      int K, float grad_scale, float* __restrict__ loss_mean,
+                                                      unsigned* __restrict__ ticket) {
   const int b = blockIdx.x, l = threadIdx.x;
   const float* row = logits + (long)b * K;
   float m = -INFINITY;
@@ -747,12 +767,99 @@ __global__ void __launch_bounds__(64) k_cross_entropy(const float* __restrict__ 
   long y = labels[b];
   y = y < 0 ? 0 : (y >= K ? K - 1 : y);
   const float lse = m + __logf(s);
-  if (l == 0) loss[b] = lse - row[y];
+  if (l == 0) __hip_atomic_store(loss + b, lse - row[y], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   if (dlogits) {
     const float inv = 1.f / s;
     for (int k = l; k < K; k += 64)
       dlogits[(long)b * K + k] = (__expf(row[k] - m) * inv - (k == y ? 1.f : 0.f)) * grad_scale;
   }
+  if (loss_mean == nullptr) return;
+  __shared__ unsigned s_last;
+  if (l == 0) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the write-through loss store is performed
+    s_last = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (unsigned)(B - 1);
+  }
+  __syncthreads();
+  if (!s_last) return;
+  float a = 0.f;
+  for (int r = l; r < B; r += 64) a += __hip_atomic_load(loss + r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  for (int o = 32; o; o >>= 1) a += __shfl_xor(a, o);
+  if (l == 0) {
+    *loss_mean = a / (float)B;
+    __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
+// out[i] = x[i] * s[0] (s: a device scalar, e.g. the incoming gradient of a loss)
+__global__ void __launch_bounds__(256) k_scale_dev(const float* __restrict__ x, const float* __restrict__ sp,
+                                                  float* __restrict__ out, long n) {
+  const float sc = *sp;
+  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long)gridDim.x * 256) out[i] = x[i] * sc;
+}
+
+__global__ void __launch_bounds__(256) k_cast_bf16(const float* __restrict__ x, bf16_t* __restrict__ y, long n) {
+  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long)gridDim.x * 256) y[i] = f2bf_rne(x[i]);
+}
+
+// *ptrs[i] += 1 for i < n (BatchNorm num_batches_tracked of every BN of a model: one launch per step)
+__global__ void __launch_bounds__(64) k_add_i64(long long* const* __restrict__ ptrs, int n) {
+  for (int i = threadIdx.x; i < n; i += 64) *ptrs[i] += 1;
+}
+
+// Preamble of a GEMM layer's backward: dy [R][N] (fp32 or bf16) with an optional ReLU mask (y > 0, y [R][N] bf16 or
+// fp32) -> dyb [R][N] bf16 (the GEMMs' operand; optional) and db [N] fp32 = the column sums (the bias gradient).
+// Block b takes rows [b * rpb, (b + 1) * rpb) and writes its column partials write-through; the last block to finish
+// (agent ticket) sums the partials in block order -- one launch, bitwise reproducible.  *ticket is 0 at launch and
+// reset by the last block.
+template <typename TD, typename TY>
+__global__ void __launch_bounds__(256) k_dy_prep(const TD* __restrict__ dy, const TY* __restrict__ y,
+                                                bf16_t* __restrict__ dyb, float* __restrict__ part,
+                                                float* __restrict__ db, unsigned* __restrict__ ticket, int R, int N,
+                                                int rpb) {
+  __shared__ float red[256];
+  __shared__ unsigned s_last;
+  const int t = threadIdx.x;
+  const int cpp = N < 256 ? N : 256, rl = 256 / cpp, cl = t % cpp, rlane = t / cpp;
+  const long r0 = (long)blockIdx.x * rpb, r1 = r0 + rpb < R ? r0 + rpb : R;
+  for (int c0 = 0; c0 < N; c0 += cpp) {
+    const int c = c0 + cl;
+    float acc = 0.f;
+    if (rlane < rl && c < N) {
+      for (long r = r0 + rlane; r < r1; r += rl) {
+        float v;
+        if constexpr (sizeof(TD) == 2) v = bf2f(dy[r * N + c]);
+        else v = dy[r * N + c];
+        if (y != nullptr) {
+          float yv;
+          if constexpr (sizeof(TY) == 2) yv = bf2f(y[r * N + c]);
+          else yv = y[r * N + c];
+          v = yv > 0.f ? v : 0.f;
+        }
+        if (dyb != nullptr) dyb[r * N + c] = f2bf_rne(v);
+        acc += v;
+      }
+    }
+    red[t] = acc;
+    __syncthreads();
+    if (t < cpp && c0 + t < N) {
+      float a = 0.f;
+      for (int k = 0; k < rl; ++k) a += red[k * cpp + t];
+      __hip_atomic_store(part + (long)blockIdx.x * N + c0 + t, a, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    __syncthreads();
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (t == 0) s_last = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1;
+  __syncthreads();
+  if (!s_last) return;
+  for (int c = t; c < N; c += 256) {
+    float a = 0.f;
+    for (unsigned b = 0; b < gridDim.x; ++b)
+      a += __hip_atomic_load(part + (long)b * N + c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    db[c] = a;
+  }
+  if (t == 0) __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // ---------------------------------------------------------------------------------------------------------

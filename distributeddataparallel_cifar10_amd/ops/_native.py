@@ -13,7 +13,7 @@ import torch
 
 from .. import build as _build
 
-ABI_VERSION = 7
+ABI_VERSION = 8
 _lock = threading.Lock()
 _lib = None
 
@@ -77,9 +77,16 @@ def _declare(lib):
                                          c_void_p, c_void_p, c_void_p, c_long, c_int, c_int, c_void_p]
     lib.dca_ops_maxpool_fwd.argtypes = [c_void_p, c_void_p, c_void_p, P(PoolGeom), c_void_p]
     lib.dca_ops_maxpool_bwd.argtypes = [c_void_p, c_void_p, c_void_p, P(PoolGeom), c_void_p]
-    lib.dca_ops_avgpool_fwd.argtypes = [c_void_p, c_void_p, c_int, c_int, c_int, c_void_p]
-    lib.dca_ops_avgpool_bwd.argtypes = [c_void_p, c_void_p, c_int, c_int, c_int, c_void_p]
-    lib.dca_ops_cross_entropy.argtypes = [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_float, c_void_p]
+    lib.dca_ops_avgpool_fwd.argtypes = [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p]
+    lib.dca_ops_avgpool_bwd.argtypes = [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p]
+    lib.dca_ops_cross_entropy.argtypes = [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_float, c_void_p,
+                                          c_void_p, c_void_p]
+    lib.dca_ops_zero.argtypes = [c_void_p, ctypes.c_long, c_void_p]
+    lib.dca_ops_scale_dev.argtypes = [c_void_p, c_void_p, c_void_p, ctypes.c_long, c_void_p]
+    lib.dca_ops_cast_bf16.argtypes = [c_void_p, c_void_p, ctypes.c_long, c_void_p]
+    lib.dca_ops_add_i64.argtypes = [c_void_p, c_int, c_void_p]
+    lib.dca_ops_dy_prep.argtypes = [c_void_p, c_int, c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p,
+                                    ctypes.c_long, c_int, c_int, c_void_p]
     lib.dca_ops_sgd.argtypes = [c_void_p, c_void_p, c_void_p, c_long, c_float, c_float, c_float, c_void_p, c_void_p]
     lib.dca_ops_quant_fp8.argtypes = [c_void_p, c_int, c_long, c_void_p, c_void_p, c_void_p]
     lib.dca_ops_fp8_alpha.argtypes = [c_void_p, c_void_p, c_float, c_void_p, c_void_p]

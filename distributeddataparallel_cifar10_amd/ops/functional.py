@@ -153,14 +153,51 @@ def _wgrad_splits(M: int, Nn: int, K: int) -> int:
     return max(1, s)
 
 
+def dy_prep(dy: torch.Tensor, y: Optional[torch.Tensor] = None, want_bf16: bool = True, want_db: bool = True):
+    """Backward preamble of a GEMM layer in one launch: dy [.., N] (fp32 / bf16) masked by ReLU(y > 0) when y is
+    given -> (dy as a bf16 GEMM operand or None, db = column sums fp32 [N] or None).  Replaces the cast, the mask
+    multiply and the bias-gradient reduction (three ATen kernels)."""
+    _dev_check(dy, y)
+    dy = dy.contiguous()
+    n = dy.shape[-1]
+    r = dy.numel() // n
+    dyb = torch.empty(dy.shape, dtype=torch.bfloat16, device=dy.device) if want_bf16 else None
+    db = torch.empty(n, dtype=torch.float32, device=dy.device) if want_db else None
+    if not want_db:  # a plain cast / mask: still one launch (the column sums go to a scratch vector)
+        db = torch.empty(n, dtype=torch.float32, device=dy.device)
+    nblk = max(1, min(256, (r + 63) // 64))
+    part = torch.empty(nblk * n, dtype=torch.float32, device=dy.device)
+    if y is not None:
+        y = y.contiguous()
+    N.check(N.lib().dca_ops_dy_prep(N.ptr(dy), int(dy.dtype == torch.bfloat16), N.ptr(y),
+                                    int(y is not None and y.dtype == torch.bfloat16), N.ptr(dyb), N.ptr(part),
+                                    N.ptr(db), N.ptr(_ticket(dy.device)), r, n, nblk, N.stream(dy.device)), "dy_prep")
+    return dyb, (db if want_db else None)
+
+
+def add_one_i64(ptrs: torch.Tensor, n: int) -> None:
+    """``*ptrs[i] += 1`` for the n int64 counters whose addresses ``ptrs`` (a device int64 tensor) holds: every
+    BatchNorm's num_batches_tracked in one launch."""
+    N.check(N.lib().dca_ops_add_i64(N.ptr(ptrs), int(n), N.stream(ptrs.device)), "add_i64")
+
+
+def cast_bf16(x: torch.Tensor) -> torch.Tensor:
+    """fp32 -> bf16 (RNE) on the ops kernels (a weight operand outside the WeightPack)."""
+    _dev_check(x)
+    x = x.contiguous()
+    y = torch.empty(x.shape, dtype=torch.bfloat16, device=x.device)
+    N.check(N.lib().dca_ops_cast_bf16(N.ptr(x), N.ptr(y), x.numel(), N.stream(x.device)), "cast_bf16")
+    return y
+
+
 # ------------------------------------------------------------------------------------------------------------
 # Linear (x [B, in] bf16, w [out, in] fp32 master) -> fp32 or bf16
 # ------------------------------------------------------------------------------------------------------------
 class _Linear(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, w, b, relu, out_dtype, fp8):
-        xb = x.contiguous()
-        wb = w.to(torch.bfloat16).contiguous()
+        xb = x.contiguous() if x.dtype == torch.bfloat16 else cast_bf16(x.float())
+        wb = cast_bf16(w.detach())
         if fp8:
             qx, ax = quantize_fp8(xb)
             qw, aw = quantize_fp8(wb)
@@ -174,17 +211,14 @@ class _Linear(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dy):
         xb, wb, y = ctx.saved_tensors
-        if ctx.relu:
-            dy = dy * (y > 0)
-        dyb = dy.to(torch.bfloat16).contiguous()
-        dx = dw = db = None
+        want_db = ctx.has_b and ctx.needs_input_grad[2]
+        dyb, db = dy_prep(dy, y if ctx.relu else None, want_db=want_db)  # ReLU mask, bf16 operand, bias grad
+        dx = dw = None
         if ctx.needs_input_grad[0]:
             dx = gemm(dyb, wb, tb=True, out_dtype=torch.bfloat16)  # dX = dY . W
         if ctx.needs_input_grad[1]:
             M, Nn, K = wb.shape[0], wb.shape[1], xb.shape[0]
             dw = gemm(dyb, xb, ta=True, tb=True, splits=_wgrad_splits(M, Nn, K))  # dW = dY^T . X (fp32)
-        if ctx.has_b and ctx.needs_input_grad[2]:
-            db = dy.float().sum(0)
         return dx, dw, db, None, None, None
 
 
@@ -643,10 +677,10 @@ class _Conv2d(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dy):
         (y,) = ctx.saved_tensors
-        if ctx.relu:
-            dy = dy * (y > 0)
+        db = None
+        if ctx.relu or (ctx.has_b and ctx.needs_input_grad[2]):  # ReLU mask + bias gradient: one launch
+            dy, db = dy_prep(dy, y if ctx.relu else None, want_db=ctx.has_b and ctx.needs_input_grad[2])
         dx, dw = _conv_bwd(dy, ctx.st, ctx.needs_input_grad[0], ctx.needs_input_grad[1])
-        db = dy.float().sum((0, 1, 2)) if ctx.has_b and ctx.needs_input_grad[2] else None
         ctx.st = None
         return dx, dw, db, None, None, None, None
 
@@ -927,47 +961,69 @@ def max_pool2d(x, k=2, s=None, p=0):
 
 class _AvgPool(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x):
-        x = x.contiguous()
+    def forward(ctx, x, out_bf16):
         n, h, w, c = x.shape
-        y = torch.empty(n, c, dtype=torch.float32, device=x.device)
-        N.check(N.lib().dca_ops_avgpool_fwd(N.ptr(x), N.ptr(y), n, h * w, c, N.stream(x.device)), "avgpool_fwd")
+        y = torch.empty(n, c, dtype=torch.bfloat16 if out_bf16 else torch.float32, device=x.device)
+        N.check(N.lib().dca_ops_avgpool_fwd(N.ptr(x), N.ptr(y), n, h * w, c, int(out_bf16), N.stream(x.device)),
+                "avgpool_fwd")
         ctx.shape = (n, h, w, c)
         return y
 
     @staticmethod
     def backward(ctx, dy):
         n, h, w, c = ctx.shape
-        dy = dy.float().contiguous()
+        bf = dy.dtype == torch.bfloat16 and c % 8 == 0
+        dy = dy.contiguous() if bf else dy.float().contiguous()
         dx = torch.empty(n, h, w, c, dtype=torch.bfloat16, device=dy.device)
-        N.check(N.lib().dca_ops_avgpool_bwd(N.ptr(dy), N.ptr(dx), n, h * w, c, N.stream(dy.device)), "avgpool_bwd")
-        return dx
+        N.check(N.lib().dca_ops_avgpool_bwd(N.ptr(dy), N.ptr(dx), n, h * w, c, int(bf), N.stream(dy.device)),
+                "avgpool_bwd")
+        return dx, None
 
 
-def global_avg_pool(x):
-    """[N, H, W, C] bf16 -> [N, C] fp32 mean over H, W."""
-    return _AvgPool.apply(x)
+def global_avg_pool(x, out_dtype=torch.float32):
+    """[N, H, W, C] bf16 -> [N, C] mean over H, W (fp32, or bf16: the fc GEMM operand without a cast pass)."""
+    return _AvgPool.apply(x, out_dtype == torch.bfloat16)
 
 
 # ------------------------------------------------------------------------------------------------------------
 # Cross-entropy (mean) with the softmax gradient computed in the same kernel
 # ------------------------------------------------------------------------------------------------------------
+_TICKETS = {}
+
+
+def _ticket(dev) -> torch.Tensor:
+    """A zeroed device word for the in-launch "last workgroup" reductions (k_cross_entropy's mean, k_dy_prep's column
+    sums).  The last workgroup resets it, so one word per device serves every launch of one stream in turn; a ring
+    of them keeps launches that may overlap (other streams, graph replays) on different words."""
+    ring = _TICKETS.get(dev)
+    if ring is None:
+        ring = _TICKETS[dev] = [torch.zeros(64, dtype=torch.int32, device=dev), 0]
+    ring[1] = (ring[1] + 1) % 64
+    return ring[0][ring[1]:ring[1] + 1]
+
+
 class _CrossEntropy(torch.autograd.Function):
     @staticmethod
     def forward(ctx, logits, labels):
         logits = logits.float().contiguous()
         B, K = logits.shape
         loss = torch.empty(B, dtype=torch.float32, device=logits.device)
+        mean = torch.empty((), dtype=torch.float32, device=logits.device)
         dl = torch.empty_like(logits) if logits.requires_grad else None
         N.check(N.lib().dca_ops_cross_entropy(N.ptr(logits), N.ptr(labels.long().contiguous()), N.ptr(loss),
-                                              N.ptr(dl), B, K, 1.0 / B, N.stream(logits.device)), "cross_entropy")
+                                              N.ptr(dl), B, K, 1.0 / B, N.ptr(mean), N.ptr(_ticket(logits.device)),
+                                              N.stream(logits.device)), "cross_entropy")
         ctx.save_for_backward(dl)
-        return loss.mean()
+        return mean
 
     @staticmethod
     def backward(ctx, g):
         (dl,) = ctx.saved_tensors
-        return dl * g, None
+        out = torch.empty_like(dl)
+        g = g.float().contiguous()
+        N.check(N.lib().dca_ops_scale_dev(N.ptr(dl), N.ptr(g), N.ptr(out), dl.numel(), N.stream(dl.device)),
+                "scale_dev")
+        return out, None
 
 
 def cross_entropy(logits, labels):

@@ -69,6 +69,7 @@ class OpsModel(nn.Module):
                          if isinstance(m, nn.BatchNorm2d) and m.track_running_stats]
             for m in self._bns:
                 m._dca_counted = True
+            self._nbt_key = None
         if self._s2d is not None:
             if x.requires_grad:
                 raise NotImplementedError("OpsModel: the first step's input did not require grad, so the stem "
@@ -84,7 +85,11 @@ class OpsModel(nn.Module):
             h = h.to(torch.bfloat16).contiguous()
         self._pack.pack()  # every conv's bf16 / fp8 GEMM operands from this step's fp32 weights: one launch
         if self.training and self.module.training and self._bns:  # each BN runs once per step: one launch
-            torch._foreach_add_([m.num_batches_tracked for m in self._bns], 1)
+            key = tuple(m.num_batches_tracked.data_ptr() for m in self._bns)
+            if key != self._nbt_key:  # the counters moved (e.g. into FlatBucketDDP's flat int64 buffer)
+                self._nbt_ptrs = torch.tensor(list(key), dtype=torch.int64).to(h.device)
+                self._nbt_key = key
+            F.add_one_i64(self._nbt_ptrs, len(key))
         return h
 
     # reference model/resnet.py:15-22, 33-37
@@ -162,8 +167,8 @@ class OpsModel(nn.Module):
 
     def head(self, h, fc):
         """Global average pool -> fc (fp32 logits)."""
-        feat = F.global_avg_pool(h)
-        return F.linear(feat.to(torch.bfloat16), fc.weight, fc.bias, out_dtype=torch.float32, fp8=self.fp8)
+        feat = F.global_avg_pool(h, out_dtype=torch.bfloat16)  # the fc operand directly (no cast pass)
+        return F.linear(feat, fc.weight, fc.bias, out_dtype=torch.float32, fp8=self.fp8)
 
     def _resnet(self, h):
         m = self.module

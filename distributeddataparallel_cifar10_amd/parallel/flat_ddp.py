@@ -39,6 +39,16 @@ import torch.distributed as dist
 import torch.nn as nn
 
 
+def _zero_flat(t: torch.Tensor) -> None:
+    """Zero a flat (contiguous) gradient buffer: on a GPU one runtime fill on the current stream (no ATen kernel in
+    the training step), else torch's zero_."""
+    if t.is_cuda:
+        from ..ops import _native as N
+        N.check(N.lib().dca_ops_zero(N.ptr(t), t.numel() * t.element_size(), N.stream(t.device)), "zero")
+    else:
+        t.zero_()
+
+
 def _dist_on(group=None) -> bool:
     return dist.is_available() and dist.is_initialized() and dist.get_world_size(group) > 1
 
@@ -292,7 +302,7 @@ class FlatBucketDDP(nn.Module):
         return out
 
     def zero_grad(self, set_to_none: bool = False) -> None:  # grads stay views of the flat buffer
-        self.flat_grad.zero_()
+        _zero_flat(self.flat_grad)
 
     def comm_time(self, reset: bool = True) -> tuple:
         """(microseconds, steps) the gradient collectives spanned on the comm stream -- first bucket launched to
@@ -385,4 +395,4 @@ class FlatSGD(torch.optim.Optimizer):
         return loss
 
     def zero_grad(self, set_to_none: bool = True) -> None:
-        self.ddp.flat_grad.zero_()
+        _zero_flat(self.ddp.flat_grad)
