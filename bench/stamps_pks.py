@@ -94,18 +94,21 @@ def main():
                               "sgd_us": round(float(seg[2]), 2),
                               "end_after_first_start_us": round(float(x[:, 3, 1].max() - r0.min()) / 100.0, 2)}),
                   flush=True)
-    # in-step reduction (red_worker; slot 10, pool member p: 0 entry, 1 every slab seen; slot 8, task v: 0 BN tail,
-    # 1 .. 161 trunk / conv1 chunks -- 0 start, 1 summed, 2 exchanged, 3 end)
-    pw = raw.reshape(32, 256, 8, 2)[10][:193].astype(np.int64)
-    if (pw[:G, 1, 1] != 0).all():
-        tasks = red[:162].astype(np.int64)
-        print(json.dumps({"red_in_step": True,
-                          "main_entry_spread_us": round(float(pw[:G, 0, 1].max() - pw[:G, 0, 1].min()) / 100.0, 2),
-                          "last_entry_to_seen_med_us": round(float(np.median(pw[:G, 1, 1]) - pw[:G, 0, 1].max()) / 100.0, 2),
+    # in-step reduction (red_worker; slot 10, reducer r = fc worker / extra: 0 entry, 1 every slab-done granule
+    # seen; slot 8, task v: 0 BN tail, 1 .. r_ts trunk / conv1 chunks -- 0 start, 1 summed, 2 exchanged, 3 end)
+    pw = raw.reshape(32, 256, 8, 2)[10].astype(np.int64)
+    nred = int((pw[:, 1, 1] != 0).sum())
+    if nred:
+        seen = pw[:nred, 1, 1]
+        tasks = red[:nred - 1].astype(np.int64)  # the last task index is the bookkeeping (no stamps)
+        tasks = tasks[tasks[:, 3, 1] != 0]
+        print(json.dumps({"red_in_step": True, "reducers": nred,
+                          "last_main_end_to_first_seen_us": round(float(seen.min() - step_end) / 100.0, 2),
+                          "last_main_end_to_last_seen_us": round(float(seen.max() - step_end) / 100.0, 2),
                           "sum_us": round(float(np.median(tasks[:, 1, 1] - tasks[:, 0, 1])) / 100.0, 2),
                           "exchange_us": round(float(np.median(tasks[:, 2, 1] - tasks[:, 1, 1])) / 100.0, 2),
                           "sgd_us": round(float(np.median(tasks[:, 3, 1] - tasks[:, 2, 1])) / 100.0, 2),
-                          "last_task_end_after_last_entry_us": round(float(tasks[:, 3, 1].max() - pw[:G, 0, 1].max()) / 100.0, 2)}),
+                          "last_task_end_after_last_main_end_us": round(float(tasks[:, 3, 1].max() - step_end) / 100.0, 2)}),
               flush=True)
     fcw = raw.reshape(32, 256, 8, 2)[9][:65].astype(np.int64)
     if (fcw[:, 3, 1] != 0).all():

@@ -108,9 +108,10 @@ struct Engine {
   int cu_slots = 0;      // persistent engine: step workgroups the device holds at once (occupancy x CUs)
   int staged_b = 0;  // persistent engine: batch slots of the current staging parity that hold the next batch
   int last_b = 0;    // batch size of the last enqueued step (BN slots are re-zeroed when it changes)
-  int seg_ch = 64;   // gradient-segment layout (pks::seg_layout): trunk / conv1 chunk size
-  int red_in_step = 1;  // with fc_in_step, world size 1 or xGMI, not shared: the remaining gradient segments and the
-                        // bookkeeping run at the end of the step kernel (pks::red_worker): one kernel per step
+  int seg_ch = 128;  // gradient-segment layout (pks::seg_layout): trunk / conv1 chunk size (256 on a shared device)
+  int red_in_step = 0;  // DCA_PKS_RED_IN_STEP=1 (with fc_in_step, world size 1 or xGMI, not shared): the remaining
+                        // gradient segments and the bookkeeping run at the end of the step kernel (pks::red_worker):
+                        // one kernel per step.  Off by default: measured slower (docs/ARCHITECTURE.md)
   int fc_in_step = 1;  // the fc1 / fc-tail gradient segments run on the step kernel's fc workers (pks::N_FCW extra
                        // workgroups beside the backward); off: in the reduction kernel.  Off whenever the step and
                        // its fc workers would exceed the co-resident budget, and when xGMI peers share this device
@@ -175,8 +176,8 @@ static int alloc_workspace(Engine* e) {
       {"SLAB", 2 * 64 * 4},
       {"COMMT", 16}, {"PKW", PKW_N * 2},
       {"PKS_GRAN", 2 * (size_t)pks::LMAX * pks::GSTR * 8}, {"PKS_YH", 10 * (size_t)pks::LMAX * 2 * 512 * 4},
-      {"PKS_BNX", 2 * (size_t)pks::LMAX * 64 * 4}, {"PKS_HDONE", (size_t)pks::LMAX * 8},
-      {"PKS_SDONE", (size_t)(pks::LMAX + pks::N_FCW) * 8},
+      {"PKS_BNX", 2 * (size_t)pks::LMAX * 64 * 4},
+      {"PKS_HDONE", (size_t)pks::LMAX * 8 + 2 * 8 * 64 * 4},  // + the in-step arrival counters (pks::sdone_cnt)
       {"C1", e->in.debug ? bmax * 32 * 1024 * 4 : 16},
   };
   size_t total = 0;
@@ -230,7 +231,6 @@ static int alloc_workspace(Engine* e) {
   qa.gran = (unsigned long long*)e->regions["PKS_GRAN"];
   qa.bnx = (unsigned*)e->regions["PKS_BNX"];
   qa.hdone = (unsigned long long*)e->regions["PKS_HDONE"];
-  qa.sdone = (unsigned long long*)e->regions["PKS_SDONE"];
   qa.epoch = (int*)e->regions["EPOCH"];
   qa.err = (unsigned*)e->regions["ERR"];
   qa.tslab = (float*)e->regions["TSLAB"];
@@ -252,9 +252,13 @@ static int set_lds_limits(Engine* e) {
   HIPCK(hipFuncSetAttribute((const void*)e->khead1, hipFuncAttributeMaxDynamicSharedMemorySize, (int)e->s_head1));
   HIPCK(hipFuncSetAttribute((const void*)e->khead2, hipFuncAttributeMaxDynamicSharedMemorySize, (int)e->s_head2));
   HIPCK(hipFuncSetAttribute((const void*)e->kbwd, hipFuncAttributeMaxDynamicSharedMemorySize, (int)dg));
-  HIPCK(hipFuncSetAttribute((const void*)pks::k_pks_step<0>, hipFuncAttributeMaxDynamicSharedMemorySize,
+  HIPCK(hipFuncSetAttribute((const void*)pks::k_pks_step<0, false>, hipFuncAttributeMaxDynamicSharedMemorySize,
                             pks::Plan<0>::TOTAL));
-  HIPCK(hipFuncSetAttribute((const void*)pks::k_pks_step<1>, hipFuncAttributeMaxDynamicSharedMemorySize,
+  HIPCK(hipFuncSetAttribute((const void*)pks::k_pks_step<1, false>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            pks::Plan<1>::TOTAL));
+  HIPCK(hipFuncSetAttribute((const void*)pks::k_pks_step<0, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            pks::Plan<0>::TOTAL));
+  HIPCK(hipFuncSetAttribute((const void*)pks::k_pks_step<1, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
                             pks::Plan<1>::TOTAL));
 
   return 0;
@@ -321,19 +325,30 @@ static int enqueue_step_persistent(Engine* e, int B, int part) {
     // in-step reduction: needs the fc workers (the BN tail / bookkeeping pool layout assumes them), the fused SGD
     // or the xGMI exchange (RCCL and the host all-reduce follow a separate reduction kernel), and a device of our
     // own (ranks sharing one keep the budgeted, looped reduction kernel)
-    ra.red_in_step = e->red_in_step && ra.fc_in_step && ra.mode != 1 && e->shared_device <= 1 && part == 0 ? 1 : 0;
+    const bool red = e->red_in_step && ra.fc_in_step && ra.mode != 1 && e->shared_device <= 1 && part == 0 &&
+                     ra.seg_ch == 128;
+    // extra reducers: enough that every reduction task (BN tail, trunk / conv1 chunks, bookkeeping) has its own
+    // workgroup beside the 65 fc workers, within the co-resident budget
+    int nrx = 0;
+    if (red) {
+      const int tasks = pks::seg_layout(ra.seg_ch).r_ts + 2;
+      nrx = std::max(0, std::min({tasks - pks::N_FCW, e->resident - pks_grid(B) - pks::N_FCW, pks::NRX_MAX}));
+      ra.fc_in_step |= nrx << 8;  // (pks::red_nrx)
+    }
     if (e->shared_device > 1 && pks_grid(B) > share_budget(e)) {
       g_err = "shared-GPU rehearsal: " + std::to_string(e->shared_device) + " ranks x " + std::to_string(pks_grid(B)) +
               " step workgroups (batch " + std::to_string(B) + ") exceed the device's " + std::to_string(e->cu_slots) +
               " CUs; use a smaller per-rank batch";
       return -1;
     }
-    const dim3 grid(pks_grid(B) + (ra.fc_in_step ? pks::N_FCW : 0));
+    const dim3 grid(pks_grid(B) + (ra.fc_in_step ? pks::N_FCW : 0) + nrx);
     if (e->bf)
-      hipLaunchKernelGGL(pks::k_pks_step<0>, grid, dim3(pks::NTH), pks::Plan<0>::TOTAL, e->st, cx, e->qa, ra);
+      hipLaunchKernelGGL((red ? pks::k_pks_step<0, true> : pks::k_pks_step<0, false>), grid, dim3(pks::NTH),
+                         pks::Plan<0>::TOTAL, e->st, cx, e->qa, ra);
     else
-      hipLaunchKernelGGL(pks::k_pks_step<1>, grid, dim3(pks::NTH), pks::Plan<1>::TOTAL, e->st, cx, e->qa, ra);
-    if (!ra.red_in_step)
+      hipLaunchKernelGGL((red ? pks::k_pks_step<1, true> : pks::k_pks_step<1, false>), grid, dim3(pks::NTH),
+                         pks::Plan<1>::TOTAL, e->st, cx, e->qa, ra);
+    if (!red)
       hipLaunchKernelGGL(pks::k_pks_reduce_ar, dim3(reduce_grid(e, pks::reduce_segments(ra.fc_in_step, ra.seg_ch) + 1)),
                          dim3(256), pks::stage_floats(B) * 4, e->st, cx, e->qa, B * pks::S, ra);
   }
@@ -448,10 +463,10 @@ static int engine_init(Engine* e, const DcaInit* in, int n_indices) {
     HIPCK(hipGetDevice(&dev));
     HIPCK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
     if (e->bf)
-      HIPCK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)dca::pks::k_pks_step<0>, dca::pks::NTH,
+      HIPCK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)dca::pks::k_pks_step<0, false>, dca::pks::NTH,
                                                         dca::pks::Plan<0>::TOTAL));
     else
-      HIPCK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)dca::pks::k_pks_step<1>, dca::pks::NTH,
+      HIPCK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)dca::pks::k_pks_step<1, false>, dca::pks::NTH,
                                                         dca::pks::Plan<1>::TOTAL));
     // one step workgroup per CU (256 VGPRs): a grid of every CU would leave no slack for anything else on the
     // device (another stream's kernel, another process), so an automatically chosen engine keeps a margin of one
@@ -468,7 +483,10 @@ static int engine_init(Engine* e, const DcaInit* in, int n_indices) {
     e->resident = resident;
     if (const char* fo = getenv("DCA_PKS_FC_IN_STEP")) e->fc_in_step = fo[0] != '0';
     if (const char* ro = getenv("DCA_PKS_RED_IN_STEP")) e->red_in_step = ro[0] != '0';
-    if (const char* sc = getenv("DCA_PKS_SEG_CH")) e->seg_ch = atoi(sc) == 256 ? 256 : 64;
+    if (const char* sc = getenv("DCA_PKS_SEG_CH")) {
+      const int v = atoi(sc);
+      e->seg_ch = v == 64 || v == 256 ? v : 128;
+    }
   }
   HIPCK(hipStreamCreateWithFlags(&e->st, hipStreamNonBlocking));
   HIPCK(hipStreamCreateWithFlags(&e->cst, hipStreamNonBlocking));
@@ -594,8 +612,10 @@ static int ensure_staged(Engine* e, int B) {
   if (e->persistent) e->staged_b = B;
   // sliced engine: a workgroup absent from the last steps (smaller batch) left BN slots whose 2-bit tags could
   // match again; zeroed slots (tag 0) never match (bn_tag)
-  if (e->persistent && B != e->last_b)
+  if (e->persistent && B != e->last_b) {
     HIPCK(hipMemsetAsync(e->qa.bnx, 0, 2 * (size_t)dca::pks::LMAX * 64 * 4, e->st));
+    HIPCK(hipMemsetAsync(e->qa.hdone + dca::pks::LMAX, 0, 2 * 8 * 64 * 4, e->st));  // in-step arrival counters
+  }
   e->last_b = B;
   return 0;
 }
@@ -917,10 +937,10 @@ int dca_engine_ipc_selftest_fc(void* h, const float* src, float* dst, float time
   // for its peers' workgroup f, so all ranks' grids must be co-resident (a step-kernel workgroup takes a whole CU)
   const dim3 grid(std::min(dca::pks::N_FCW, dca::share_budget(e)));
   if (e->bf)
-    hipLaunchKernelGGL(dca::pks::k_pks_step<0>, grid, dim3(dca::pks::NTH), dca::pks::Plan<0>::TOTAL, e->st, cx, e->qa,
+    hipLaunchKernelGGL((dca::pks::k_pks_step<0, false>), grid, dim3(dca::pks::NTH), dca::pks::Plan<0>::TOTAL, e->st, cx, e->qa,
                        ra);
   else
-    hipLaunchKernelGGL(dca::pks::k_pks_step<1>, grid, dim3(dca::pks::NTH), dca::pks::Plan<1>::TOTAL, e->st, cx, e->qa,
+    hipLaunchKernelGGL((dca::pks::k_pks_step<1, false>), grid, dim3(dca::pks::NTH), dca::pks::Plan<1>::TOTAL, e->st, cx, e->qa,
                        ra);
   HIPCK(hipGetLastError());
   HIPCK(hipStreamSynchronize(e->st));

@@ -53,8 +53,9 @@ constexpr int cmax(int a, int b) { return a > b ? a : b; }
 struct Args {
   unsigned long long* gran;  // [2][LMAX][GSTR] granules (halo rows, head partials)
   unsigned* bnx;             // [2][LMAX][64] BatchNorm partials, 4-byte self-tagged values (see bn_tag)
-  unsigned long long* hdone; // [LMAX] head-done granules {tagof(epoch, RND_HDONE), 0} (fc workers' start signal)
-  unsigned long long* sdone; // [LMAX + N_FCW] slab-done granules {tagof(epoch, RND_SDONE), 0} (in-step reduction)
+  unsigned long long* hdone; // [LMAX] head-done granules {tagof(epoch, RND_HDONE), 0} (fc workers' start signal),
+                             // then the in-step reduction's arrival counters (sdone_cnt; no field of their own: one
+                             // more kernel-argument pointer pushed the 256-VGPR step kernel into scratch spills)
   int* epoch;                // device scalar, advanced by the reduce kernel after every step
   unsigned* err;             // bit r: exchange round r timed out
   float* tslab;              // [LMAX][WSLAB_N] trunk wgrad per workgroup (fragment order, read by k_pks_reduce)
@@ -440,6 +441,13 @@ __device__ __forceinline__ void st2_wt(float* p, float a, float b) {
 __device__ __forceinline__ void st1_wt(float* p, float v) {
   __hip_atomic_store((unsigned*)p, __float_as_uint(v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
+// write-through only when a reader in the same launch needs it (wt: wave-uniform); a plain store otherwise (measured:
+// the write-through form of these few values cost ~0.5 us per step when nothing in the launch reads them)
+template <bool WT>
+__device__ __forceinline__ void st1_maybe_wt(float* p, float v) {
+  if constexpr (WT) st1_wt(p, v);
+  else *p = v;
+}
 __device__ __forceinline__ void st4r_wt(float* rowp, int h, int lane, const float (&v)[4]) {
   st4_wt(rowp + h * 256 + lane * 4, f32x4{v[0], v[1], v[2], v[3]});
 }
@@ -614,7 +622,11 @@ __host__ __device__ constexpr SegLayout seg_layout(int ch) {
                    (WSLAB_N / ch + (SSLAB_N + ch - 1) / ch) * ch + R_FC1 * 1024 + FCT_LEN};
 }
 static_assert(WSLAB_N % 256 == 0, "trunk slab splits into whole chunks");
-static_assert(seg_layout(64).nseg == NSEG_MAX && seg_layout(256).nseg <= NSEG_MAX, "flag stride");
+static_assert(seg_layout(64).nseg == NSEG_MAX && seg_layout(128).nseg <= NSEG_MAX && seg_layout(256).nseg <= NSEG_MAX,
+              "flag stride");
+static_assert(seg_layout(128).off_bnt + BNT_LEN >= FLAT_N && seg_layout(128).off_bnt + BNT_LEN <= (int)xg::SLAB_FLOATS,
+              "the 128-element layout covers the flat buffer and fits one slab");
+constexpr int NRX_MAX = 256;                       // extra reducer workgroups of the step kernel, upper bound
 static_assert((size_t)NSEG_MAX * xg::MAXR * 4 <= xg::FLAG_BYTES, "one flag per segment and rank");
 static_assert(seg_layout(64).off_bnt + BNT_LEN >= FLAT_N && seg_layout(256).off_bnt + BNT_LEN >= FLAT_N &&
                   seg_layout(256).off_bnt + BNT_LEN <= (int)xg::SLAB_FLOATS,
@@ -634,11 +646,13 @@ struct RedAr {
   float* st_dst;
   int st_n;
   int mode;
-  int fc_in_step;             // the fc1 / fc-tail segments run on the step kernel's fc workers
-  int seg_ch;                 // segment layout (seg_layout): 64 or 256
-  int red_in_step;            // the trunk / conv1 / BN-tail segments and the bookkeeping run at the end of the step
-                              // kernel (red_worker) instead of in k_pks_reduce_ar (needs fc_in_step)
+  int fc_in_step;             // nonzero: the fc1 / fc-tail segments run on the step kernel's fc workers; bits 8..:
+                              // the in-step reduction's extra reducer count (red_nrx; k_pks_step<P, true> only).  No
+                              // fields of their own: a larger kernel argument pushed the 256-VGPR step kernel into
+                              // scratch spills
+  int seg_ch;                 // segment layout (seg_layout): 64, 128 or 256
 };
+__device__ __forceinline__ int red_nrx(const RedAr& ra) { return ra.fc_in_step >> 8; }
 
 __device__ __forceinline__ char* rbase(const RedAr& ra, int q) { return ra.peers.base[q] + xg::REGION_BYTES; }
 __device__ __forceinline__ float* rslab(const RedAr& ra, int q, int par) {
@@ -727,7 +741,9 @@ __device__ __forceinline__ f32x4 ld4_sc1(const float* base, int bytes, int off_f
 
 // trunk / stem chunk b of CH outputs in slab fragment order, summed over the nslab workgroup slabs: thread (grp,
 // slot) sums float4 `slot` of slabs grp, grp + NG, ... (all in flight for batch 32), fixed order
-template <int NTH, int CH>
+// SC1: the slabs may have been written inside this launch (in-step reduction): sc1 loads; after a kernel boundary
+// plain loads (measured 0.6 us per step faster in k_pks_reduce_ar)
+template <int NTH, int CH, bool SC1>
 __device__ __forceinline__ void seg_chunk(const Ctx& cx, const Args& pa, const SegLayout& Ls, int b, int nslab,
                                           float* segv, f32x4* red) {
   constexpr int NS = CH / 4, NG = NTH / NS, NU = 128 / NG;
@@ -748,8 +764,11 @@ __device__ __forceinline__ void seg_chunk(const Ctx& cx, const Args& pa, const S
 #pragma unroll
     for (int u = 0; u < NU; ++u) {
       const int k = k0 + grp + NG * u;
-      v[u] = __builtin_bit_cast(
-          f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, ((k < nslab ? k : nslab - 1) * stride + ec) * 4, 0, 16));
+      const int kc = k < nslab ? k : nslab - 1;
+      if constexpr (SC1)
+        v[u] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, (kc * stride + ec) * 4, 0, 16));
+      else
+        v[u] = ld4(src + (size_t)kc * stride + ec);
     }
 #pragma unroll
     for (int u = 0; u < NU; ++u)
@@ -767,7 +786,7 @@ __device__ __forceinline__ void seg_chunk(const Ctx& cx, const Args& pa, const S
 
 // Segment b on this workgroup (NTH threads): reduce / compute into segv, exchange (mode 2), SGD.  LDS: segv
 // [SEG_MAX], red [NTH] f32x4, stage [stage_floats(B)], *s_ep.
-template <int NTH>
+template <int NTH, bool SC1 = false>
 __device__ void seg_process(const Ctx& cx, const Args& pa, const RedAr& ra, int b, int nslab, float* segv,
                             f32x4* red, float* stage, int* s_ep, int sslot, int swg) {
   const int t = threadIdx.x, B = cx.B;
@@ -789,8 +808,10 @@ __device__ void seg_process(const Ctx& cx, const Args& pa, const RedAr& ra, int 
   if (mode == 3) {
     for (int k = t; k < len; k += NTH) segv[k] = off + k < ra.st_n ? ra.st_src[off + k] : 0.f;
   } else if (b < Ls.r_ts) {
-    if (Ls.ch == 64) seg_chunk<NTH, 64>(cx, pa, Ls, b, nslab, segv, red);
-    else seg_chunk<NTH, 256>(cx, pa, Ls, b, nslab, segv, red);
+    if constexpr (SC1) seg_chunk<NTH, 128, true>(cx, pa, Ls, b, nslab, segv, red);  // in-step: 128-element layout
+    else if (Ls.ch == 64) seg_chunk<NTH, 64, false>(cx, pa, Ls, b, nslab, segv, red);
+    else if (Ls.ch == 128) seg_chunk<NTH, 128, false>(cx, pa, Ls, b, nslab, segv, red);
+    else seg_chunk<NTH, 256, false>(cx, pa, Ls, b, nslab, segv, red);
   } else if (b < Ls.fct) {
     // fc1 block: dW1[j][64f + kk .. +3] = sum_b dh[b][j] p[b][64f + kk ..], rows j = 16 h .. 16 h + 15
     const int fb = b - Ls.r_ts, f = fb >> 1, j0 = 16 * (fb & 1);
@@ -857,10 +878,12 @@ __device__ void seg_process(const Ctx& cx, const Args& pa, const RedAr& ra, int 
     for (int idx = t; idx < BNT_LEN; idx += NTH) {
       float sv;
       if (idx < 64) {
-        sv = pa.bng[idx];
+        sv = __hip_atomic_load(pa.bng + idx, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // (as rm / rv below)
       } else {
         const int k = idx - 64;
-        sv = cx.rank == 0 ? (k < 32 ? cx.rm[k] : cx.rv[k - 32]) : 0.f;
+        // sc1: written through by logical workgroup 0, possibly inside this launch (in-step reduction)
+        sv = cx.rank == 0 ? __hip_atomic_load(k < 32 ? cx.rm + k : cx.rv + (k - 32), __ATOMIC_RELAXED,
+                                              __HIP_MEMORY_SCOPE_AGENT) : 0.f;
       }
       segv[idx] = sv;
     }
@@ -909,14 +932,14 @@ __device__ __forceinline__ void pks_bookkeeping(const Ctx& cx, const Args& pa) {
   float l = t < B ? __uint_as_float(__hip_atomic_load((const unsigned*)cx.HLOSS + t, __ATOMIC_RELAXED,
                                                       __HIP_MEMORY_SCOPE_AGENT)) : 0.f;
   double acc = 0.0;
-  int cur = 0, stp = 0, ep = 0;
+  int cur = 0, stp = 0;
   long long nb = 0;
+  const int ep = *pa.epoch;  // every lane (the counter reset below needs its parity)
   if (t == 0) {  // issued together with the loss loads: one memory round trip, not five dependent ones
     acc = *cx.loss_acc;
     cur = *cx.cursor;
     stp = *cx.step_count;
     nb = *cx.nbt;
-    ep = *pa.epoch;
   }
 #pragma unroll
   for (int m = 1; m < 64; m <<= 1) l += __shfl_xor(l, m);  // fixed tree: identical every step
@@ -927,6 +950,9 @@ __device__ __forceinline__ void pks_bookkeeping(const Ctx& cx, const Args& pa) {
     *cx.nbt = nb + NBLK;  // BatchNorm num_batches_tracked: +1 per application
     *pa.epoch = (int)(((unsigned)ep + 1u) % EPOCH_WRAP);
   }
+  if (t < 8)  // the next step's arrival counters (in-step reduction; see sdone_cnt): everyone has arrived at this one
+    __hip_atomic_store((unsigned*)(pa.hdone + LMAX) + ((((ep & 1) ^ 1) * 8 + t) * 64), 0u, __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // fc worker fb (0 .. R_FC1 - 1: fc1 block fb; R_FC1: fc tail) of the step kernel: waits until every main workgroup
@@ -962,60 +988,72 @@ __device__ void fc_segment(const Ctx& cx, const Args& pa, const RedAr& ra, int f
   seg_process<NTH>(cx, pa, ra, fb < R_FC1 ? Ls.r_ts + fb : Ls.fct, G, segv, red, stage, s_ep, 9, fb);
 }
 
-// In-step gradient reduction (ra.red_in_step; replaces k_pks_reduce_ar and the kernel boundary before it).  Every
-// member of the pool -- the G step workgroups (pool index L, once their trunk / conv1 slabs are written through) and
-// the fc workers (G + fb, once their fc segment is done) -- publishes a slab-done granule, waits for all of them
-// (so every slab is complete AND every workgroup of the launch has long read this step's epoch), then runs its
-// share of the remaining segments: v = 0 the BN tail (pool index 0 = logical workgroup 0, which itself wrote the
-// BN-affine gradients and the running statistics), v = 1 .. r_ts the trunk / conv1 chunks (sc1 slab loads), v =
-// r_ts + 1 the step's bookkeeping (loss, cursor, counters, epoch); each segment with its xGMI exchange (world size
-// > 1) and SGD, exactly as in k_pks_reduce_ar.  The slab hand-off is the guide's sc1-store / agent-granule form (no
-// release fence: the slabs are write-through; the readers' loads are sc1).
-__device__ void red_worker(const Ctx& cx, const Args& pa, const RedAr& ra, int epoch, int pidx, char* smem) {
-  const int t = threadIdx.x, lane = t & 63, G = cx.B * S;
-  const int nfcw = ra.fc_in_step ? N_FCW : 0, pool = G + nfcw;
-  const unsigned tag = tagof(epoch, RND_SDONE);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this thread's write-through slab / head stores are performed
+// In-step gradient reduction (k_pks_step<P, true>; replaces k_pks_reduce_ar and the kernel boundary before it).  The
+// step workgroups only announce their trunk / conv1 slabs (write-through, then a slab-done granule: sdone_publish)
+// and exit as before; the reduction runs on the REDUCERS -- the fc workers once their fc segment is done (~30 us
+// before the step ends) and red_nrx(ra) extra workgroups of the same launch on the CUs the step leaves free.  A reducer
+// publishes its own granule (so every workgroup of the launch has read this step's epoch before the bookkeeping
+// advances it), waits for all of them, then runs task v = its reducer index (+ the reducer count, ...): v = 0 the BN
+// tail, 1 .. r_ts the trunk / conv1 chunks (sc1 slab loads), r_ts + 1 the bookkeeping (loss, cursor, counters,
+// epoch); each segment with its xGMI exchange (world size > 1) and SGD, exactly as in k_pks_reduce_ar.  The step
+// workgroups' code (and register allocation) is unchanged: they never run a segment.  The slab hand-off is the
+// guide's sc1-store / agent-granule form (no release fence: the slabs are write-through; the readers' loads are sc1).
+// Arrival counters: 2 epoch parities x SDN shards (one 256-B line each, so the arrivals' atomics spread over
+// channels instead of queueing on one word: one word takes ~88 atomics per us, MI355X guide "dequeue").  Member w adds 1
+// to shard w % SDN of this step's parity once its write-through stores are performed; the reducers poll the SDN
+// shards until they sum to the member count.  The bookkeeping (which runs only after every member arrived) zeroes
+// the other parity's shards for the next step; every reduction path runs the bookkeeping, so a step of either kind
+// leaves the counters of the following one at zero.
+constexpr int SDN = 8, SD_STRIDE = 64;
+__device__ __forceinline__ unsigned* sdone_base(const Args& pa) { return (unsigned*)(pa.hdone + LMAX); }
+__device__ __forceinline__ unsigned* sdone_cnt(const Args& pa, int par, int shard) {
+  return sdone_base(pa) + (par * SDN + shard) * SD_STRIDE;
+}
+__device__ __forceinline__ void sdone_publish(const Args& pa, int who, int epoch) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this thread's write-through stores are performed
   __syncthreads();                                    // ... and every thread's of this workgroup
-  if (t == 0) gput(pa.sdone + (pidx < G ? pidx : LMAX + pidx - G), tag, 0.f);
+  if (threadIdx.x == 0)
+    __hip_atomic_fetch_add(sdone_cnt(pa, epoch & 1, who % SDN), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// r: reducer index (fc worker fb = r, extra e = N_FCW + e)
+__device__ void red_worker(const Ctx& cx, const Args& pa, const RedAr& ra, int epoch, int r, char* smem) {
+  const int t = threadIdx.x, lane = t & 63, G = cx.B * S;
+  const int nred = N_FCW + red_nrx(ra);
+  const unsigned all = (unsigned)(G + nred);
+  sdone_publish(pa, G + r, epoch);
   const SegLayout Ls = seg_layout(ra.seg_ch);
   const int nv = Ls.r_ts + 2;  // BN tail, r_ts chunks, bookkeeping
-  if (pidx >= nv) return;      // nothing to do (the granule above still counts this workgroup in)
-  // One wave polls every member's granule.  Step workgroups poll back to back (their wait is on the step's critical
-  // path, ~1 us); fc workers arrive ~30 us early and sleep between passes, so their polling does not load the memory
-  // system under the trunk backward's latency-bound exchanges.
-  const int nap = pidx >= G ? 8 : 0;
-  DCA_STAMP(cx, 10, pidx, 0);
-  if (t < 64) {
+  if (r >= nv) return;         // nothing to do (its arrival still counts)
+  DCA_STAMP(cx, 10, r, 0);
+  if (t < 64) {  // one wave polls the shards, sleeping between passes until the step workgroups are near the end
     for (unsigned spins = 0;; ++spins) {
-      bool ok = true;
-      for (int k = lane; k < pool; k += 64) {
-        const unsigned long long* g = pa.sdone + (k < G ? k : LMAX + k - G);
-        ok &= (unsigned)(__hip_atomic_load(g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >> 32) == tag;
-      }
-      if (__all(ok)) break;
+      unsigned got = lane < SDN ? __hip_atomic_load(sdone_cnt(pa, epoch & 1, lane), __ATOMIC_RELAXED,
+                                                    __HIP_MEMORY_SCOPE_AGENT) : 0u;
+      for (int o = 4; o; o >>= 1) got += __shfl_xor(got, o);
+      got = __shfl(got, 0);
+      if (got >= all) break;
       if (spins >= SPIN_LIMIT) {
         if (lane == 0) atomicOr(pa.err, 1u << 29);
         break;
       }
-      sleep_units(nap);
+      if (got + (unsigned)G / 2 < all) sleep_units(8);  // far from the end
     }
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   }
   __syncthreads();
-  DCA_STAMP(cx, 10, pidx, 1);
+  DCA_STAMP(cx, 10, r, 1);
   float* segv = (float*)smem;
   f32x4* red = (f32x4*)(smem + SEG_MAX * 4);
   float* stage = (float*)(smem + SEG_MAX * 4 + NTH * 16);
   int* s_ep = (int*)(smem + SEG_MAX * 4 + NTH * 16 + stage_floats(cx.B) * 4);
-  for (int v = pidx; v < nv; v += pool) {
+  for (int v = r; v < nv; v += nred) {
     if (v == nv - 1) {
       pks_bookkeeping(cx, pa);
       continue;
     }
     DCA_STAMP(cx, 8, v, 0);
-    seg_process<NTH>(cx, pa, ra, v == 0 ? Ls.bnt : v - 1, G, segv, red, stage, s_ep, 8, v);
+    seg_process<NTH, true>(cx, pa, ra, v == 0 ? Ls.bnt : v - 1, G, segv, red, stage, s_ep, 8, v);
     __syncthreads();  // segv / red are reused by the next segment
   }
 }
@@ -1024,11 +1062,9 @@ constexpr int P_KSHIFT = 906;  // misc: [10][32] BN shifts (last step's batch me
 constexpr int P_LABEL = 1240;  // misc: this image's label
 
 // ============================================================================================================
-// The step of one main workgroup (slice s of image n).  pidx / ep_out: its in-step reduction pool index and the step
-// epoch (left at -1 by the padding workgroups of a batch that is not a multiple of 8).
-template <int P>
-__device__ __forceinline__ void step_main(const Ctx& cx, const Args& pa, const RedAr& ra, char* smem, int& pidx,
-                                          int& ep_out) {
+// The step of one main workgroup (slice s of image n).  RIS: the launch runs the in-step reduction.
+template <int P, bool RIS>
+__device__ __forceinline__ void step_main(const Ctx& cx, const Args& pa, const RedAr& ra, char* smem) {
   using PL = Plan<P>;
   const int t = threadIdx.x, wv = t >> 6, lane = t & 63, c = lane & 15, q = lane >> 4;
   const int w = wv & (RS - 1), hh = wv / RS, ch = 16 * hh + c;  // image row (in the slice), channel half, channel
@@ -1281,8 +1317,9 @@ __device__ __forceinline__ void step_main(const Ctx& cx, const Args& pa, const R
         misc[480 + ch] = misc[480 + ch] * (1.f - mo) + unb * mo;
         cx.STATS[i * 32 + ch] = make_float2(mean, invstd);
         if (i == NBLK - 1) {
-          cx.rm[ch] = misc[448 + ch];
-          cx.rv[ch] = misc[480 + ch];
+          // write-through when the BN-tail reducer reads them in this launch (in-step reduction)
+          st1_maybe_wt<RIS>(cx.rm + ch, misc[448 + ch]);
+          st1_maybe_wt<RIS>(cx.rv + ch, misc[480 + ch]);
         }
       }
     }
@@ -1604,8 +1641,8 @@ __device__ __forceinline__ void step_main(const Ctx& cx, const Args& pa, const R
     DCA_STAMP(cx, 4 + (NBLK - 1 - i) / 8, L, (NBLK - 1 - i) % 8);
   }
   if (L == 0 && t < 32) {
-    pa.bng[t] = dgam;
-    pa.bng[32 + t] = dbet;
+    st1_maybe_wt<RIS>(pa.bng + t, dgam);  // (as rm / rv)
+    st1_maybe_wt<RIS>(pa.bng + 32 + t, dbet);
   }
 
   // ======================= stem backward: max-pool bwd (saved argmax) -> ReLU mask -> conv1 wgrad ============
@@ -1665,10 +1702,10 @@ __device__ __forceinline__ void step_main(const Ctx& cx, const Args& pa, const R
       }
     }
     // conv1 bias gradient partial of this workgroup (also the barrier before the MFMAs)
-    const float dbv = wg_csum<true>(db, 0.f, cred);
+    const float dbv = wg_csum(db, 0.f, cred);
     DCA_STAMP(cx, 5, L, 3);
     float* ss = cx.SSLAB + (size_t)L * SSLAB_N;
-    if (t < 32) st1_wt(ss + 1024 + t, dbv);  // write-through: read by the reduction (possibly in this launch)
+    if (t < 32) st1_maybe_wt<RIS>(ss + 1024 + t, dbv);  // (as rm / rv)
     // D[co][k] = sum over this slice's conv pixels of ds[p][co] * im2col[p][k]; K step = one conv row (32 px).
     // Wave wv: tile wv & 3 (mt = co half, nt = k tile), conv rows 4 (wv >> 2) .. +3; k >= 27 columns are
     // discarded by the reduce
@@ -1701,7 +1738,9 @@ __device__ __forceinline__ void step_main(const Ctx& cx, const Args& pa, const R
   // the next batch's image n (this slice's quarter) and label, staged into the other parity
   if (t < 48) st4_wt((uint4*)(pa.simg + (size_t)((par ^ 1) * 64 + n) * 3072 + 768 * s) + t, __builtin_bit_cast(f32x4, nxt));
   if (t == 48 && s == 0) pa.slab[(par ^ 1) * 64 + n] = nxt_lab;
-  // trunk wgrad slab (accumulated over the 10 applications): tile tt = 2 nt + mt, the layout k_pks_reduce reads
+  // trunk wgrad slab (accumulated over the 10 applications): tile tt = 2 nt + mt, the layout the reduction reads.
+  // (Issued here, last: stored right after application 0's wgrad instead, the write-through stores held up the stem
+  // backward's own waits -- vmcnt retires in order -- and the step was no faster.)
 #pragma unroll
   for (int j = 0; j < NNT; ++j) {
     const int nt = wv + NW * j;
@@ -1711,31 +1750,33 @@ __device__ __forceinline__ void step_main(const Ctx& cx, const Args& pa, const R
     }
   }
   DCA_STAMP(cx, 5, L, 7);
-  pidx = L;
-  ep_out = epoch;
+  if constexpr (RIS) sdone_publish(pa, L, epoch);  // the reducers of this launch take it from here
 }
 
-template <int P>
+// RIS (compile time): the in-step reduction's code exists only in the RIS instantiations, so the
+// default kernel's register allocation is the one without it
+template <int P, bool RIS>
 __global__ void __launch_bounds__(NTH) k_pks_step(Ctx cx, Args pa, RedAr ra) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  int pidx = -1, ep = 0;
   const int gmain = (cx.B + 7) / 8 * 8 * S;
-  if ((int)blockIdx.x >= gmain) {  // workgroups past the main grid are the fc workers (only with ra.fc_in_step)
-    const int fb = (int)blockIdx.x - gmain, nfw = (int)gridDim.x - gmain;
+  if ((int)blockIdx.x < gmain) {
+    step_main<P, RIS>(cx, pa, ra, smem);
+    return;
+  }
+  // past the main grid: the fc workers (only with ra.fc_in_step), then the extra reducers (RIS)
+  const int fb = (int)blockIdx.x - gmain, nfw = min((int)gridDim.x - gmain, N_FCW);
+  if (fb < N_FCW) {
     // one fc segment each in a training step (nfw == N_FCW); the self-test on a shared device launches fewer
     // workers (its per-rank CU budget), which then take the segments in turn
     for (int f = fb; f < N_FCW; f += nfw) {
       if (f != fb) __syncthreads();
       fc_segment<P>(cx, pa, ra, f, smem);
     }
-    pidx = cx.B * S + fb;
-    ep = *pa.epoch;  // unchanged: the bookkeeping waits for this workgroup's slab-done granule
-  } else {
-    step_main<P>(cx, pa, ra, smem, pidx, ep);
   }
-  if (pidx >= 0 && ra.red_in_step) {
-    __syncthreads();  // every wave is done with its LDS before red_worker reuses it
-    red_worker(cx, pa, ra, ep, pidx, smem);
+  if constexpr (RIS) {
+    const int epoch = *pa.epoch;  // unchanged until every workgroup has arrived (red_worker)
+    __syncthreads();              // the fc segment's LDS is reused
+    red_worker(cx, pa, ra, epoch, fb, smem);
   }
 }
 

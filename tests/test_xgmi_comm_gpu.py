@@ -14,7 +14,8 @@ import traceback
 import pytest
 import torch
 import torch.distributed as dist
-import torch.multiprocessing as mp
+
+from _ranks import spawn_ranks
 
 pytestmark = pytest.mark.gpu
 SIZES = [1, 5, 4099, 262147, 1 << 20]
@@ -35,17 +36,11 @@ def _expect(xs, wire, scale):
     return s.bfloat16().float() if wire == "bf16" else s
 
 
-def _spawn(target, ws, *args, **kw):
-    ctx = mp.get_context("spawn")
-    q = ctx.Queue()
-    procs = [ctx.Process(target=target, args=(r, ws, *args, q), kwargs=kw) for r in range(ws)]
-    for p in procs:
-        p.start()
-    res = [q.get(timeout=600) for _ in procs]
-    for p in procs:
-        p.join(timeout=120)
-    bad = [r for r in res if r[1]]
-    assert not bad, "\n".join(f"rank {r}:\n{e}" for r, e in bad)
+def _spawn(target, ws, *args, own_device=False, **kw):
+    """ws rank processes (all on GPU 0 unless own_device); see tests/_ranks.py."""
+    if own_device:
+        kw["own_device"] = True
+    spawn_ranks(target, ws, lambda r: (r, ws, *args), kw, shared=not own_device)
 
 
 def _init(rank, ws, port, own_device=False):
