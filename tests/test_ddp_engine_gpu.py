@@ -189,15 +189,14 @@ def _xgmi_worker(rank, ws, port, dtype, persistent, q, comm="xgmi", own_device=F
 @pytest.mark.parametrize("ws,dtype,persistent,batch", [(2, "bf16", True, B), (4, "bf16", True, B),
                                                        (2, "fp32", True, B), (2, "fp32", False, B),
                                                        (3, "fp32", True, 8), (4, "fp32", True, 8),
-                                                       (8, "bf16", True, 8), (8, "bf16", False, 4)])
+                                                       (8, "bf16", True, 8), (8, "fp32", True, 4),
+                                                       (8, "bf16", False, 4)])
 def test_xgmi_allreduce_ranks_one_gpu(gpu, port, ws, dtype, persistent, batch):
     """ws=8 (the node's world size): the sliced engine's reduction exchange with 8 peers (rank_sum_n<8> in
     seg_exchange), its fc-worker exchange with 8 peers (construction self-test, FusedDDPTrainer), CC4 through 8
     ranks, the multi-kernel engine's k_xgmi_ar_sgd with 8 peers.  A per-rank batch of <= 8 keeps each rank's step
-    grid (32 workgroups, one CU each) within its 256 / 8 CU budget.  (fp32 -- the 3xbf16 kernel, 150 KB of LDS per
-    workgroup -- with 8 ranks on one device hit an illegal-instruction queue abort in two of the eight processes
-    during their start-up, before any exchange; see docs/STATUS.md.  The fp32 kernel's exchanges run here with 3 and
-    4 ranks; its 8-peer code is the same seg_exchange instantiation as bf16's.)"""
+    grid (32 workgroups, one CU each) within its 256 / 8 CU budget, and every rank has one hardware queue
+    (tests/_ranks.py: with the default 4 per process, 8 processes oversubscribed the hardware scheduler)."""
     spawn_ranks(_xgmi_worker, ws, lambda r: (r, ws, port, dtype, persistent), dict(batch=batch))
 
 
