@@ -720,6 +720,15 @@ int dca_ops_cast_bf16(const float* x, void* y, long n, void* stream) {
   return 0;
 }
 
+int dca_ops_gather_cols(const float* src, int S, const long* idx, int L, float* out, int rows, int accumulate,
+                        void* stream) {
+  REQUIRE(rows > 0 && L > 0 && (long)rows * L < (1L << 31), "gather_cols: bad shape");
+  hipLaunchKernelGGL(k_gather_cols, dim3(grid_for((long)rows * L, 256, 1024)), dim3(256), 0, (hipStream_t)stream, src, S,
+                     idx, L, out, rows, accumulate);
+  OPCK(hipGetLastError());
+  return 0;
+}
+
 // ptrs: device array of n int64 pointers
 int dca_ops_add_i64(void* ptrs, int n, void* stream) {
   REQUIRE(n > 0, "add_i64: empty");
@@ -731,14 +740,14 @@ int dca_ops_add_i64(void* ptrs, int n, void* stream) {
 // dy [R][N] (dy_bf16: bf16, else fp32), y: optional ReLU mask source [R][N] (y_bf16: bf16, else fp32); dyb: optional
 // bf16 copy of the masked dy; db [N] fp32 column sums; part: nblk * N floats; ticket: a zeroed device word.
 int dca_ops_dy_prep(const void* dy, int dy_bf16, const void* y, int y_bf16, void* dyb, float* part, float* db,
-                    unsigned* ticket, long R, int N, int nblk, void* stream) {
+                    unsigned* ticket, long R, int N, int nblk, int accumulate, void* stream) {
   REQUIRE(R > 0 && N > 0 && nblk > 0 && R < (1L << 31), "dy_prep: bad shape");
   const int rpb = (int)((R + nblk - 1) / nblk);
   hipStream_t st = (hipStream_t)stream;
   const dim3 g(nblk), b(256);
 #define DYP(TD, TY) \
   hipLaunchKernelGGL((k_dy_prep<TD, TY>), g, b, 0, st, (const TD*)dy, (const TY*)y, (bf16_t*)dyb, part, db, ticket, \
-                     (int)R, N, rpb)
+                     (int)R, N, rpb, accumulate)
   if (dy_bf16 && y_bf16) DYP(bf16_t, bf16_t);
   else if (dy_bf16) DYP(bf16_t, float);
   else if (y_bf16) DYP(float, bf16_t);

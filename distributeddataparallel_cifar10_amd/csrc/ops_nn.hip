@@ -801,6 +801,18 @@ __global__ void __launch_bounds__(256) k_cast_bf16(const float* __restrict__ x, 
   for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long)gridDim.x * 256) y[i] = f2bf_rne(x[i]);
 }
 
+// out[r * L + j] (+)= src[r * S + idx[j]] (fp32; e.g. the space-to-depth stem's weight gradient remapped to torch's
+// layout, accumulated into the flat DDP gradient view)
+__global__ void __launch_bounds__(256) k_gather_cols(const float* __restrict__ src, int S, const long* __restrict__ idx,
+                                                    int L, float* __restrict__ out, int rows, int accumulate) {
+  const long total = (long)rows * L;
+  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < total; i += (long)gridDim.x * 256) {
+    const long r = i / L, j = i % L;
+    const float v = src[r * S + idx[j]];
+    out[i] = accumulate ? out[i] + v : v;
+  }
+}
+
 // *ptrs[i] += 1 for i < n (BatchNorm num_batches_tracked of every BN of a model: one launch per step)
 __global__ void __launch_bounds__(64) k_add_i64(long long* const* __restrict__ ptrs, int n) {
   for (int i = threadIdx.x; i < n; i += 64) *ptrs[i] += 1;
@@ -815,7 +827,7 @@ template <typename TD, typename TY>
 __global__ void __launch_bounds__(256) k_dy_prep(const TD* __restrict__ dy, const TY* __restrict__ y,
                                                 bf16_t* __restrict__ dyb, float* __restrict__ part,
                                                 float* __restrict__ db, unsigned* __restrict__ ticket, int R, int N,
-                                                int rpb) {
+                                                int rpb, int accumulate) {
   __shared__ float red[256];
   __shared__ unsigned s_last;
   const int t = threadIdx.x;
@@ -857,7 +869,7 @@ __global__ void __launch_bounds__(256) k_dy_prep(const TD* __restrict__ dy, cons
     float a = 0.f;
     for (unsigned b = 0; b < gridDim.x; ++b)
       a += __hip_atomic_load(part + (long)b * N + c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    db[c] = a;
+    db[c] = accumulate ? db[c] + a : a;  // accumulate: straight into a flat DDP gradient view (grad sink)
   }
   if (t == 0) __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }

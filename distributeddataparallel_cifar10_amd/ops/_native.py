@@ -86,7 +86,8 @@ def _declare(lib):
     lib.dca_ops_cast_bf16.argtypes = [c_void_p, c_void_p, ctypes.c_long, c_void_p]
     lib.dca_ops_add_i64.argtypes = [c_void_p, c_int, c_void_p]
     lib.dca_ops_dy_prep.argtypes = [c_void_p, c_int, c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p,
-                                    ctypes.c_long, c_int, c_int, c_void_p]
+                                    ctypes.c_long, c_int, c_int, c_int, c_void_p]
+    lib.dca_ops_gather_cols.argtypes = [c_void_p, c_int, c_void_p, c_int, c_void_p, c_int, c_int, c_void_p]
     lib.dca_ops_sgd.argtypes = [c_void_p, c_void_p, c_void_p, c_long, c_float, c_float, c_float, c_void_p, c_void_p]
     lib.dca_ops_quant_fp8.argtypes = [c_void_p, c_int, c_long, c_void_p, c_void_p, c_void_p]
     lib.dca_ops_fp8_alpha.argtypes = [c_void_p, c_void_p, c_float, c_void_p, c_void_p]

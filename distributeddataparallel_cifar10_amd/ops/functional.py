@@ -153,17 +153,20 @@ def _wgrad_splits(M: int, Nn: int, K: int) -> int:
     return max(1, s)
 
 
-def dy_prep(dy: torch.Tensor, y: Optional[torch.Tensor] = None, want_bf16: bool = True, want_db: bool = True):
+def dy_prep(dy: torch.Tensor, y: Optional[torch.Tensor] = None, want_bf16: bool = True, want_db: bool = True,
+            db_into: Optional[torch.Tensor] = None):
     """Backward preamble of a GEMM layer in one launch: dy [.., N] (fp32 / bf16) masked by ReLU(y > 0) when y is
     given -> (dy as a bf16 GEMM operand or None, db = column sums fp32 [N] or None).  Replaces the cast, the mask
-    multiply and the bias-gradient reduction (three ATen kernels)."""
+    multiply and the bias-gradient reduction (three ATen kernels).  db_into: accumulate the column sums into this
+    fp32 view instead (a flat DDP gradient sink)."""
     _dev_check(dy, y)
     dy = dy.contiguous()
     n = dy.shape[-1]
     r = dy.numel() // n
     dyb = torch.empty(dy.shape, dtype=torch.bfloat16, device=dy.device) if want_bf16 else None
-    db = torch.empty(n, dtype=torch.float32, device=dy.device) if want_db else None
-    if not want_db:  # a plain cast / mask: still one launch (the column sums go to a scratch vector)
+    if db_into is not None:
+        db = db_into
+    else:  # (without want_db: still one launch, the column sums go to a scratch vector)
         db = torch.empty(n, dtype=torch.float32, device=dy.device)
     nblk = max(1, min(256, (r + 63) // 64))
     part = torch.empty(nblk * n, dtype=torch.float32, device=dy.device)
@@ -171,8 +174,24 @@ def dy_prep(dy: torch.Tensor, y: Optional[torch.Tensor] = None, want_bf16: bool 
         y = y.contiguous()
     N.check(N.lib().dca_ops_dy_prep(N.ptr(dy), int(dy.dtype == torch.bfloat16), N.ptr(y),
                                     int(y is not None and y.dtype == torch.bfloat16), N.ptr(dyb), N.ptr(part),
-                                    N.ptr(db), N.ptr(_ticket(dy.device)), r, n, nblk, N.stream(dy.device)), "dy_prep")
-    return dyb, (db if want_db else None)
+                                    N.ptr(db), N.ptr(_ticket(dy.device)), r, n, nblk, int(db_into is not None),
+                                    N.stream(dy.device)), "dy_prep")
+    return dyb, (db if want_db and db_into is None else None)
+
+
+def zeros_bf16(*shape, device) -> torch.Tensor:
+    """A zeroed bf16 tensor by one runtime fill (no ATen fill kernel in the step)."""
+    t = torch.empty(*shape, dtype=torch.bfloat16, device=device)
+    N.check(N.lib().dca_ops_zero(N.ptr(t), t.numel() * 2, N.stream(device)), "zero")
+    return t
+
+
+def gather_cols(src: torch.Tensor, idx: torch.Tensor, out: torch.Tensor, accumulate: bool) -> None:
+    """out[r, j] (+)= src[r, idx[j]] for 2-D fp32 src [rows, S] / out [rows, L] (contiguous), one launch."""
+    rows, S = src.shape
+    L = idx.numel()
+    N.check(N.lib().dca_ops_gather_cols(N.ptr(src), S, N.ptr(idx), L, N.ptr(out), rows, int(accumulate),
+                                        N.stream(src.device)), "gather_cols")
 
 
 def add_one_i64(ptrs: torch.Tensor, n: int) -> None:
@@ -195,7 +214,7 @@ def cast_bf16(x: torch.Tensor) -> torch.Tensor:
 # ------------------------------------------------------------------------------------------------------------
 class _Linear(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, w, b, relu, out_dtype, fp8):
+    def forward(ctx, x, w, b, relu, out_dtype, fp8, sinks):
         xb = x.contiguous() if x.dtype == torch.bfloat16 else cast_bf16(x.float())
         wb = cast_bf16(w.detach())
         if fp8:
@@ -205,25 +224,42 @@ class _Linear(torch.autograd.Function):
         else:
             y = gemm(xb, wb, bias=b, relu=relu, out_dtype=out_dtype)
         ctx.save_for_backward(xb, wb, y if relu else None)
-        ctx.relu, ctx.has_b = relu, b is not None
+        ctx.relu, ctx.has_b, ctx.sinks = relu, b is not None, sinks
         return y
 
     @staticmethod
     def backward(ctx, dy):
         xb, wb, y = ctx.saved_tensors
-        want_db = ctx.has_b and ctx.needs_input_grad[2]
-        dyb, db = dy_prep(dy, y if ctx.relu else None, want_db=want_db)  # ReLU mask, bf16 operand, bias grad
+        sw, sb = ctx.sinks if ctx.sinks is not None else (None, None)
+        want_db = ctx.has_b and (ctx.needs_input_grad[2] or sb is not None)
+        # ReLU mask, bf16 operand and the bias gradient (into its flat DDP view when sunk) in one launch
+        dyb, db = dy_prep(dy, y if ctx.relu else None, want_db=want_db, db_into=sb[0] if sb is not None else None)
         dx = dw = None
         if ctx.needs_input_grad[0]:
             dx = gemm(dyb, wb, tb=True, out_dtype=torch.bfloat16)  # dX = dY . W
-        if ctx.needs_input_grad[1]:
+        if ctx.needs_input_grad[1] or sw is not None:
             M, Nn, K = wb.shape[0], wb.shape[1], xb.shape[0]
-            dw = gemm(dyb, xb, ta=True, tb=True, splits=_wgrad_splits(M, Nn, K))  # dW = dY^T . X (fp32)
-        return dx, dw, db, None, None, None
+            splits = _wgrad_splits(M, Nn, K)
+            if sw is not None:  # dW = dY^T . X accumulated by the GEMM's reduce pass into the flat gradient view
+                gemm(dyb, xb, ta=True, tb=True, splits=splits, out=sw[0], beta=1.0)
+            else:
+                dw = gemm(dyb, xb, ta=True, tb=True, splits=splits)  # dW = dY^T . X (fp32)
+        for sink in (sw, sb):
+            if sink is not None:
+                sink[1]()
+        ctx.sinks = None
+        return dx, dw, db, None, None, None, None
 
 
 def linear(x, w, b=None, relu=False, out_dtype=torch.float32, fp8=False):
-    return _Linear.apply(x, w, b, relu, out_dtype, fp8)
+    """x [B, in] -> [B, out].  Under FlatBucketDDP (grad sinks on w and b) the weight and bias gradients are written
+    straight into the flat gradient buffer by the backward's kernels (no autograd accumulate kernels)."""
+    sinks = None
+    if torch.is_grad_enabled() and b is not None:
+        sw, sb = grad_sink(w), grad_sink(b)
+        if sw is not None and sb is not None and sw[0].is_contiguous():
+            sinks = (sw, sb)
+    return _Linear.apply(x, w, b, relu, out_dtype, fp8, sinks)
 
 
 # ------------------------------------------------------------------------------------------------------------
@@ -617,8 +653,8 @@ def _conv_bwd(dy, st, need_x: bool, need_w: bool, sink=None, x_join: Optional[Gr
             # GEMM epilogue writes straight into its rows of dX (no dY.W^T column matrix, no col2im)
             classes = packed["classes"] or [(0, 0, 1, 1, 0, packed["dgrad"], None)]
             if acc is None:
-                dx = (torch.empty if len(classes) == 4 else torch.zeros)(g.N, g.H, g.W, g.C, dtype=torch.bfloat16,
-                                                                          device=dy.device)
+                dx = torch.empty(g.N, g.H, g.W, g.C, dtype=torch.bfloat16, device=dy.device) if len(classes) == 4 \
+                    else zeros_bf16(g.N, g.H, g.W, g.C, device=dy.device)
             else:
                 dx = acc
             dy4 = dyb.view(g.N, g.Ho, g.Wo, co)
@@ -771,10 +807,14 @@ class _ConvBNAct(torch.autograd.Function):
                            bnb=link_in if ctx.needs_input_grad[0] else None)
         if s2d is not None and dw is not None:  # [Co, 16, 4, 4] of the 4x4 conv -> the stem's [Co, C, 7, 7]
             co = dw.shape[0]
-            dw = dw.view(co, -1).index_select(1, s2d["back_idx"]).view(sw[0].shape if sw else ctx.wshape)
-            if sw:
-                sw[0].add_(dw)
+            src = dw.reshape(co, -1).contiguous()
+            if sw:  # one gather-accumulate launch straight into the flat gradient view
+                gather_cols(src, s2d["back_idx"], sw[0].view(co, -1), accumulate=True)
                 dw = None
+            else:
+                out = torch.empty(ctx.wshape, dtype=torch.float32, device=src.device)
+                gather_cols(src, s2d["back_idx"], out.view(co, -1), accumulate=False)
+                dw = out
         if sw:
             sw[1]()
         ctx.st = ctx.sinks = ctx.joins = ctx.links = None
