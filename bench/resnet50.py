@@ -98,6 +98,7 @@ def run_rank(a) -> None:
     y = torch.randint(0, 1000, (a.batch,), device=dev, generator=g)
     amp = torch.autocast("cuda", dtype=torch.bfloat16, enabled=a.dtype == "bf16" and a.path == "torch")
     ce = cross_entropy if a.path == "ops" else F.cross_entropy
+    one = torch.ones((), device=dev)  # the loss's seed gradient, allocated once (autograd would fill one per step)
 
     def step():
         if a.infer:
@@ -106,7 +107,7 @@ def run_rank(a) -> None:
         with amp:
             loss = ce(ddp(x), y)
         opt.zero_grad()
-        loss.backward()
+        loss.backward(one)
         opt.step()
         return loss
 

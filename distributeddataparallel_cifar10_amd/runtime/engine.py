@@ -11,6 +11,7 @@ accumulated on the device and read only at log points.
 from __future__ import annotations
 
 import ctypes
+import os
 import warnings
 from dataclasses import dataclass
 from typing import Optional
@@ -171,7 +172,9 @@ class NetResDeepEngine:
             rank=int(cfg.rank), nccl_id=ctypes.cast(self._nccl_id, ctypes.c_char_p),
             persistent=1 if cfg.persistent else 0, debug=1 if cfg.debug else 0, pk_waves=int(cfg.pk_waves),
             comm_mode={"rccl": 0, "external": 1, "xgmi": 2}[cfg.comm], force_comm=1 if cfg.force_comm else 0,
-            auto_engine=1 if auto_engine else 0,
+            # the automatic choice keeps one CU of co-residency slack (batch 64 -> multi-kernel engine);
+            # DCA_PKS_ALLOW_FULL_DEVICE=1 lets it use all 256 CUs (nothing else may then run on the GPU)
+            auto_engine=1 if auto_engine and os.environ.get("DCA_PKS_ALLOW_FULL_DEVICE") != "1" else 0,
         )
         self._init = init
         self.max_indices = int(max_indices or self.data.shape[0])

@@ -202,7 +202,7 @@ def train_loop(model, train_loader: DeviceLoader, rank: int, cfg: Optional[Train
                     loss = loss_fn(outputs.float(), labels)
                 optimizer.zero_grad()
                 with record_function("backward+allreduce"):
-                    loss.backward()
+                    loss.backward(_seed_grad(loss))
                 with record_function("optimizer"):
                     optimizer.step()
                 loss_sum += loss.item()
@@ -234,6 +234,18 @@ def train_loop(model, train_loader: DeviceLoader, rank: int, cfg: Optional[Train
         _export_profile(prof, cfg.profile, rank, train_loader.device)
     print(time_line(total), flush=True)
     return {"losses": history, "seconds": total, "steps": global_step}
+
+
+_SEEDS = {}
+
+
+def _seed_grad(loss: torch.Tensor) -> torch.Tensor:
+    """The scalar loss's seed gradient (1.0), allocated once per device and dtype: ``loss.backward()`` would launch
+    a fill kernel for it every step."""
+    key = (loss.device, loss.dtype)
+    if key not in _SEEDS:
+        _SEEDS[key] = torch.ones((), device=loss.device, dtype=loss.dtype)
+    return _SEEDS[key]
 
 
 def _comm_time(model) -> tuple:
