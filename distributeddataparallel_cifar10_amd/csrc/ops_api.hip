@@ -738,13 +738,14 @@ int dca_ops_add_i64(void* ptrs, int n, void* stream) {
 }
 
 // dy [R][N] (dy_bf16: bf16, else fp32), y: optional ReLU mask source [R][N] (y_bf16: bf16, else fp32); dyb: optional
-// bf16 copy of the masked dy; db [N] fp32 column sums; part: nblk * N floats; ticket: a zeroed device word.
+// bf16 copy of the masked dy; db [N] fp32 column sums; part: nchunk * N floats; ticket: ceil(N / 64) zeroed device
+// words.
 int dca_ops_dy_prep(const void* dy, int dy_bf16, const void* y, int y_bf16, void* dyb, float* part, float* db,
-                    unsigned* ticket, long R, int N, int nblk, int accumulate, void* stream) {
-  REQUIRE(R > 0 && N > 0 && nblk > 0 && R < (1L << 31), "dy_prep: bad shape");
-  const int rpb = (int)((R + nblk - 1) / nblk);
+                    unsigned* ticket, long R, int N, int nchunk, int accumulate, void* stream) {
+  REQUIRE(R > 0 && N > 0 && nchunk > 0 && nchunk <= 65535 && R < (1L << 31), "dy_prep: bad shape");
+  const int rpb = (int)((R + nchunk - 1) / nchunk);
   hipStream_t st = (hipStream_t)stream;
-  const dim3 g(nblk), b(256);
+  const dim3 g((N + 63) / 64, nchunk), b(256);
 #define DYP(TD, TY) \
   hipLaunchKernelGGL((k_dy_prep<TD, TY>), g, b, 0, st, (const TD*)dy, (const TY*)y, (bf16_t*)dyb, part, db, ticket, \
                      (int)R, N, rpb, accumulate)

@@ -820,9 +820,11 @@ __global__ void __launch_bounds__(64) k_add_i64(long long* const* __restrict__ p
 
 // Preamble of a GEMM layer's backward: dy [R][N] (fp32 or bf16) with an optional ReLU mask (y > 0, y [R][N] bf16 or
 // fp32) -> dyb [R][N] bf16 (the GEMMs' operand; optional) and db [N] fp32 = the column sums (the bias gradient).
-// Block b takes rows [b * rpb, (b + 1) * rpb) and writes its column partials write-through; the last block to finish
-// (agent ticket) sums the partials in block order -- one launch, bitwise reproducible.  *ticket is 0 at launch and
-// reset by the last block.
+// 2-D grid: blockIdx.x = a 64-column block (one wave-wide coalesced row segment), blockIdx.y = a chunk of rpb rows;
+// the 256 threads are 64 columns x 4 row lanes.  Each block writes its 64 column partials write-through; the last
+// block of a column block to finish (that column block's agent ticket) sums the gridDim.y partials in chunk order --
+// one launch, bitwise reproducible, enough workgroups to fill the chip.  ticket[gridDim.x] is zero at launch and
+// reset by the last blocks.
 template <typename TD, typename TY>
 __global__ void __launch_bounds__(256) k_dy_prep(const TD* __restrict__ dy, const TY* __restrict__ y,
                                                 bf16_t* __restrict__ dyb, float* __restrict__ part,
@@ -830,48 +832,52 @@ __global__ void __launch_bounds__(256) k_dy_prep(const TD* __restrict__ dy, cons
                                                 int rpb, int accumulate) {
   __shared__ float red[256];
   __shared__ unsigned s_last;
-  const int t = threadIdx.x;
-  const int cpp = N < 256 ? N : 256, rl = 256 / cpp, cl = t % cpp, rlane = t / cpp;
-  const long r0 = (long)blockIdx.x * rpb, r1 = r0 + rpb < R ? r0 + rpb : R;
-  for (int c0 = 0; c0 < N; c0 += cpp) {
-    const int c = c0 + cl;
-    float acc = 0.f;
-    if (rlane < rl && c < N) {
-      for (long r = r0 + rlane; r < r1; r += rl) {
-        float v;
-        if constexpr (sizeof(TD) == 2) v = bf2f(dy[r * N + c]);
-        else v = dy[r * N + c];
-        if (y != nullptr) {
-          float yv;
-          if constexpr (sizeof(TY) == 2) yv = bf2f(y[r * N + c]);
-          else yv = y[r * N + c];
-          v = yv > 0.f ? v : 0.f;
-        }
-        if (dyb != nullptr) dyb[r * N + c] = f2bf_rne(v);
-        acc += v;
+  const int t = threadIdx.x, cl = t & 63, rlane = t >> 6;
+  const int c = blockIdx.x * 64 + cl;
+  const long r0 = (long)blockIdx.y * rpb, r1 = r0 + rpb < R ? r0 + rpb : R;
+  float acc = 0.f;
+  if (c < N) {
+#pragma unroll 4
+    for (long r = r0 + rlane; r < r1; r += 4) {
+      float v;
+      if constexpr (sizeof(TD) == 2) v = bf2f(dy[r * N + c]);
+      else v = dy[r * N + c];
+      if (y != nullptr) {
+        float yv;
+        if constexpr (sizeof(TY) == 2) yv = bf2f(y[r * N + c]);
+        else yv = y[r * N + c];
+        v = yv > 0.f ? v : 0.f;
       }
+      if (dyb != nullptr) dyb[r * N + c] = f2bf_rne(v);
+      acc += v;
     }
-    red[t] = acc;
-    __syncthreads();
-    if (t < cpp && c0 + t < N) {
-      float a = 0.f;
-      for (int k = 0; k < rl; ++k) a += red[k * cpp + t];
-      __hip_atomic_store(part + (long)blockIdx.x * N + c0 + t, a, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    __syncthreads();
   }
+  red[t] = acc;
+  __syncthreads();
+  if (t < 64 && c < N)
+    __hip_atomic_store(part + (long)blockIdx.y * N + c, red[t] + red[t + 64] + red[t + 128] + red[t + 192],
+                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  if (t == 0) s_last = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1;
+  if (t == 0)
+    s_last = __hip_atomic_fetch_add(ticket + blockIdx.x, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+             gridDim.y - 1;
   __syncthreads();
   if (!s_last) return;
-  for (int c = t; c < N; c += 256) {
-    float a = 0.f;
-    for (unsigned b = 0; b < gridDim.x; ++b)
-      a += __hip_atomic_load(part + (long)b * N + c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    db[c] = accumulate ? db[c] + a : a;  // accumulate: straight into a flat DDP gradient view (grad sink)
+  // last block of this column block: 4 lanes per column each sum a quarter of the chunks, combined in fixed order
+  const int gy = gridDim.y, q = (gy + 3) >> 2, b0 = rlane * q, b1 = b0 + q < gy ? b0 + q : gy;
+  float a = 0.f;
+  if (c < N) {
+#pragma unroll 8
+    for (int b = b0; b < b1; ++b) a += __hip_atomic_load(part + (long)b * N + c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
-  if (t == 0) __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  red[t] = a;
+  __syncthreads();
+  if (t < 64 && c < N) {
+    const float s = ((red[t] + red[t + 64]) + red[t + 128]) + red[t + 192];
+    db[c] = accumulate ? db[c] + s : s;  // accumulate: straight into a flat DDP gradient view (grad sink)
+  }
+  if (t == 0) __hip_atomic_store(ticket + blockIdx.x, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // ---------------------------------------------------------------------------------------------------------

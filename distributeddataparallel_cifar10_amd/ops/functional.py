@@ -168,13 +168,14 @@ def dy_prep(dy: torch.Tensor, y: Optional[torch.Tensor] = None, want_bf16: bool 
         db = db_into
     else:  # (without want_db: still one launch, the column sums go to a scratch vector)
         db = torch.empty(n, dtype=torch.float32, device=dy.device)
-    nblk = max(1, min(256, (r + 63) // 64))
-    part = torch.empty(nblk * n, dtype=torch.float32, device=dy.device)
+    ncb = (n + 63) // 64  # 64-column blocks
+    nchunk = max(1, min((1024 + ncb - 1) // ncb, (r + 15) // 16))  # ~1024 workgroups, >= 16 rows each
+    part = torch.empty(nchunk * n, dtype=torch.float32, device=dy.device)
     if y is not None:
         y = y.contiguous()
     N.check(N.lib().dca_ops_dy_prep(N.ptr(dy), int(dy.dtype == torch.bfloat16), N.ptr(y),
                                     int(y is not None and y.dtype == torch.bfloat16), N.ptr(dyb), N.ptr(part),
-                                    N.ptr(db), N.ptr(_ticket(dy.device)), r, n, nblk, int(db_into is not None),
+                                    N.ptr(db), N.ptr(_ticket(dy.device, ncb)), r, n, nchunk, int(db_into is not None),
                                     N.stream(dy.device)), "dy_prep")
     return dyb, (db if want_db and db_into is None else None)
 
@@ -1031,15 +1032,23 @@ def global_avg_pool(x, out_dtype=torch.float32):
 _TICKETS = {}
 
 
-def _ticket(dev) -> torch.Tensor:
-    """A zeroed device word for the in-launch "last workgroup" reductions (k_cross_entropy's mean, k_dy_prep's column
-    sums).  The last workgroup resets it, so one word per device serves every launch of one stream in turn; a ring
-    of them keeps launches that may overlap (other streams, graph replays) on different words."""
+_TICKET_WORDS = 4096
+
+
+def _ticket(dev, n: int = 1) -> torch.Tensor:
+    """n consecutive zeroed device words for the in-launch "last workgroup" reductions (k_cross_entropy's mean, one
+    per 64-column block of k_dy_prep's column sums).  The last workgroups reset them, so the words serve every
+    launch of one stream in turn; handing them out round-robin from a ring of 4096 keeps launches that may overlap
+    (other streams, graph replays) on different words."""
+    assert 0 < n <= _TICKET_WORDS // 8, n
     ring = _TICKETS.get(dev)
     if ring is None:
-        ring = _TICKETS[dev] = [torch.zeros(64, dtype=torch.int32, device=dev), 0]
-    ring[1] = (ring[1] + 1) % 64
-    return ring[0][ring[1]:ring[1] + 1]
+        ring = _TICKETS[dev] = [torch.zeros(_TICKET_WORDS, dtype=torch.int32, device=dev), 0]
+    if ring[1] + n > _TICKET_WORDS:
+        ring[1] = 0
+    start = ring[1]
+    ring[1] += n
+    return ring[0][start:start + n]
 
 
 class _CrossEntropy(torch.autograd.Function):

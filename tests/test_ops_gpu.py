@@ -222,6 +222,30 @@ def test_avg_pool_and_cross_entropy(gpu):
     assert _rel(logits.grad, lr_.grad) < 1e-4
 
 
+@pytest.mark.parametrize("R,N,dyt,yt", [(256, 1000, torch.float32, torch.float32), (33, 10, torch.float32, None),
+                                         (5000, 64, torch.bfloat16, torch.bfloat16), (1, 130, torch.bfloat16, None),
+                                         (2048, 2048, torch.float32, torch.bfloat16), (70000, 24, torch.bfloat16, None)])
+def test_dy_prep(gpu, R, N, dyt, yt):
+    """k_dy_prep (2-D grid, per-column-block tickets): masked bf16 operand and bias gradient, plain and accumulated
+    into a sink, repeated launches (tickets reset by the last blocks)."""
+    from distributeddataparallel_cifar10_amd.ops.functional import dy_prep
+    g = torch.Generator(device=gpu).manual_seed(R + N)
+    dy = torch.randn(R, N, device=gpu, generator=g).to(dyt)
+    y = torch.randn(R, N, device=gpu, generator=g).to(yt) if yt is not None else None
+    ref = dy.float() * (y.float() > 0) if y is not None else dy.float()
+    for _ in range(3):
+        dyb, db = dy_prep(dy, y)
+        assert torch.equal(dyb, ref.to(torch.bfloat16))
+        assert _rel(db, ref.double().sum(0)) < 1e-5
+    sink = torch.randn(N, device=gpu, generator=g)
+    want = sink.double() + ref.double().sum(0)
+    dyb, db = dy_prep(dy, y, want_bf16=False, db_into=sink)
+    assert dyb is None and db is None
+    assert _rel(sink, want) < 1e-5
+    db1 = dy_prep(dy, y)[1]
+    assert torch.equal(db1, dy_prep(dy, y)[1])  # fixed summation order: bitwise reproducible
+
+
 @pytest.mark.parametrize("mu,wd", [(0.0, 0.0), (0.9, 1e-4)])
 def test_sgd(gpu, mu, wd):
     from distributeddataparallel_cifar10_amd.ops import sgd_step_
