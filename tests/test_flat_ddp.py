@@ -130,6 +130,10 @@ def _case_flat_buffers_one_broadcast_per_dtype(rank, ws):
             dist.broadcast = real
         assert sorted(calls) == sorted((str(f.dtype), f.numel()) for f in flats.values()), calls
         assert all(bool((b == 1).all()) for b in bufs)  # rank 0's buffers everywhere
+        with torch.profiler.profile(activities=[torch.profiler.ProfilerActivity.CPU]) as prof:
+            ddp._broadcast_buffers_now()  # CC4 alone: no cat, no per-buffer copy-back
+        ops = [e.name for e in prof.events()]
+        assert not [n for n in ops if n in ("aten::copy_", "aten::cat", "aten::_foreach_copy_", "aten::stack")], ops
 
 
 def _case_matches_torch_ddp(rank, ws):
