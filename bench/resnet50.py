@@ -157,7 +157,9 @@ def run_rank(a) -> None:
                                      "path": (("eval-mode forward, ops HIP kernels" if a.infer else "FlatBucketDDP + ops HIP kernels") + (" (fp8 fwd GEMMs)" if a.fp8 else " (bf16)")
                                               + (", step replayed as a HIP graph" if a.graph else ""))
                                      if a.path == "ops" else "stock PyTorch: torch DDP + MIOpen convs + torch.optim.SGD, bf16 autocast" +
-                                     (", channels_last" if cl else ", NCHW")}}),
+                                     (", channels_last" if cl else ", NCHW")},
+                          "comm": getattr(ddp, "comm", None),
+                          "xgmi_calibration": getattr(getattr(ddp, "xgmi", None), "calibration", None)}),
               flush=True)
         if a.result_file:
             with open(a.result_file, "w") as f:

@@ -84,6 +84,10 @@ class XgmiComm:
         nb = 128 if nb is None else int(nb)
         self.nb = nb
         self.last_algo = None
+        # auto choice between one-shot and two-shot: the library's modelled crossover until calibrate() measured
+        # this node's own (bytes on the wire: one-shot below, two-shot from there)
+        self.crossover_bytes: Optional[int] = None
+        self.calibration = None
         h = ctypes.c_void_p()
         slab = (self.max_numel + 3) // 4 * 4 * 4  # fp32 sized, so the wire format can be switched per call
         _check(lib().dca_comm_create(self.rank, self.world, slab, int(nb), ctypes.byref(h)), "create")
@@ -133,6 +137,8 @@ class XgmiComm:
                                 device="cpu" if dist.get_backend(group) == "gloo" else device)
             dist.all_reduce(flag, op=dist.ReduceOp.MIN, group=group)
             ok = int(flag.item()) == 1
+        if ok and world > 2 and os.environ.get("DCA_XGMI_CALIBRATE", "1") != "0":
+            comm.calibrate(device)
         if ok:
             return comm
         if err is not None and verbose:
@@ -159,6 +165,54 @@ class XgmiComm:
                 good &= bool(torch.equal(t, ref))
         return good and self.errors() == 0
 
+    def calibrate(self, device=None, reps: int = 5) -> Optional[int]:
+        """Collective: measure the one-shot / two-shot crossover on this node instead of trusting the library's
+        model (L = 5 us per flag round trip, B = 350 GB/s per GPU; comm_api.hip).  Every rank times both algorithms
+        on the same bucket sizes (64 KiB x 4^k up to the slab, on the comm's wire format); the per-size time is the
+        MAX over ranks (one all-reduce of the timing vector), so every rank derives the same crossover: the smallest
+        size from which two-shot wins at every larger measured size too.  W <= 2: one-shot always moves no more
+        bytes, nothing to measure."""
+        if self.world <= 2:
+            return None
+        wire_b = 2 if self.wire == "bf16" else 4
+        sizes, n = [], 16384
+        while n <= self.max_numel:
+            sizes.append(n)
+            n *= 4
+        if not sizes:
+            return None
+        buf = torch.zeros(sizes[-1], device=device, dtype=torch.float32)
+        st = torch.cuda.current_stream(buf.device)
+        times = []
+        for n in sizes:
+            t = buf[:n]
+            for algo in ("oneshot", "twoshot"):
+                for _ in range(2):
+                    self.all_reduce_(t, average=False, algo=algo)
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record(st)
+                for _ in range(reps):
+                    self.all_reduce_(t, average=False, algo=algo)
+                e1.record(st)
+                e1.synchronize()
+                times.append(e0.elapsed_time(e1) * 1e3 / reps)  # us per call
+        self.check()
+        tv = torch.tensor(times, dtype=torch.float64,
+                          device="cpu" if dist.get_backend(self.group) == "gloo" else buf.device)
+        dist.all_reduce(tv, op=dist.ReduceOp.MAX, group=self.group)
+        tv = tv.cpu().tolist()
+        one, two = tv[0::2], tv[1::2]
+        cross = None
+        for i in range(len(sizes) - 1, -1, -1):  # walk down while two-shot keeps winning
+            if two[i] < one[i]:
+                cross = sizes[i] * wire_b
+            else:
+                break
+        self.crossover_bytes = cross if cross is not None else (1 << 62)  # never: one-shot everywhere measured
+        self.calibration = {"bytes": [n * wire_b for n in sizes], "oneshot_us": one, "twoshot_us": two,
+                            "crossover_bytes": cross, "world": self.world}
+        return cross
+
     # ---- the collective ---------------------------------------------------------------------------------------
     def all_reduce_(self, t: torch.Tensor, average: bool = True, algo: str = "auto", wire: Optional[str] = None,
                     stream: Optional[torch.cuda.Stream] = None) -> torch.Tensor:
@@ -169,6 +223,9 @@ class XgmiComm:
         if t.data_ptr() % 16:
             raise ValueError("xGMI all-reduce needs a 16-byte aligned tensor")
         st = stream if stream is not None else torch.cuda.current_stream(t.device)
+        if algo == "auto" and self.crossover_bytes is not None:  # the measured crossover (calibrate())
+            algo = "twoshot" if t.numel() * (2 if (wire or self.wire) == "bf16" else 4) >= self.crossover_bytes \
+                else "oneshot"
         used = ctypes.c_int()
         _check(lib().dca_comm_allreduce(self._h, ctypes.c_void_p(t.data_ptr()), ctypes.c_void_p(t.data_ptr()),
                                         t.numel(), 1 if (wire or self.wire) == "bf16" else 0, ALGOS[algo],

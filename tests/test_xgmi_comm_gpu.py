@@ -60,6 +60,15 @@ def _collective_worker(rank, ws, port, q):
         comm = XgmiComm.create(max(SIZES), device=dev, timeout_s=60.0)
         assert comm is not None, "xGMI communicator did not come up (self-test failed)"
         assert comm.nb == max(8, 128 // ws), comm.nb  # shared-device grid budget
+        if ws > 2:  # the auto crossover is measured at creation, identically on every rank
+            cal = comm.calibration
+            assert cal is not None and len(cal["oneshot_us"]) == len(cal["bytes"]) == len(cal["twoshot_us"])
+            assert all(v > 0 for v in cal["oneshot_us"] + cal["twoshot_us"]), cal
+            seen = [None] * ws
+            dist.all_gather_object(seen, comm.crossover_bytes)
+            assert len(set(seen)) == 1, seen
+            if rank == 0:
+                print(f"\n[ws={ws}] xGMI calibration (shared device): {cal}", flush=True)
         it = 0
         for rep in range(2):  # every (size, algo, wire) twice: both slab parities, advancing epochs
             for n in SIZES:
