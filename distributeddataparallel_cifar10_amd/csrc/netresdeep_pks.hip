@@ -1650,6 +1650,12 @@ __device__ __forceinline__ void step_main(const Ctx& cx, const Args& pa, const R
   wgrad_acc<P>(dyT, xT, wacc, wv, lane);  // application 0
   DCA_STAMP(cx, 5, L, 2);
   {
+    // the lane indices re-derived from an opaque copy of threadIdx.x: nothing this phase addresses is held live
+    // (and spilled) through the 20 blocks
+    int tf = threadIdx.x;
+    asm volatile("v_mov_b32 %0, %1" : "=v"(tf) : "v"(tf));
+    const int t = tf, wv = tf >> 6, lane = tf & 63, c = lane & 15, q = lane >> 4;
+    const int w = wv & (RS - 1), ch = 16 * (wv / RS) + c;
     unsigned short* dsT = (unsigned short*)(U + PL::U_DST);
     unsigned short* xs = (unsigned short*)(U + PL::U_XS);
     float* sred = (float*)(U + PL::U_SRED);
@@ -1702,7 +1708,7 @@ __device__ __forceinline__ void step_main(const Ctx& cx, const Args& pa, const R
       }
     }
     // conv1 bias gradient partial of this workgroup (also the barrier before the MFMAs)
-    const float dbv = wg_csum(db, 0.f, cred);
+    const float dbv = wg_csum<true>(db, 0.f, cred);
     DCA_STAMP(cx, 5, L, 3);
     float* ss = cx.SSLAB + (size_t)L * SSLAB_N;
     if (t < 32) st1_maybe_wt<RIS>(ss + 1024 + t, dbv);  // (as rm / rv)
@@ -1741,9 +1747,11 @@ __device__ __forceinline__ void step_main(const Ctx& cx, const Args& pa, const R
   // trunk wgrad slab (accumulated over the 10 applications): tile tt = 2 nt + mt, the layout the reduction reads.
   // (Issued here, last: stored right after application 0's wgrad instead, the write-through stores held up the stem
   // backward's own waits -- vmcnt retires in order -- and the step was no faster.)
+  int wvf = wv;  // opaque copy: the slab offsets are re-derived here, not held live (spilled) since the forward
+  asm volatile("v_mov_b32 %0, %1" : "=v"(wvf) : "v"(wvf));
 #pragma unroll
   for (int j = 0; j < NNT; ++j) {
-    const int nt = wv + NW * j;
+    const int nt = wvf + NW * j;
     if (nt < 18) {
       st4_wt(pa.tslab + (size_t)L * WSLAB_N + (((2 * nt) * 64 + lane) << 2), wacc[j][0]);
       st4_wt(pa.tslab + (size_t)L * WSLAB_N + (((2 * nt + 1) * 64 + lane) << 2), wacc[j][1]);
