@@ -195,12 +195,22 @@ def launch(n: int, argv: list) -> None:
         run_rank(_args(argv))
         return
     import torch.multiprocessing as mp
+    _share_queues()
     mp.spawn(_spawned, args=(n, _free_port(), argv), nprocs=n, join=True)
+
+
+def _share_queues() -> None:
+    """Shared-GPU rehearsal: one hardware queue per rank process (inherited at spawn).  Eight processes with the
+    default four queues each oversubscribe the device's hardware scheduler, which then time-slices the queues and
+    stalls the ranks' spinning exchange kernels (tests/_ranks.py)."""
+    if os.environ.get("DCA_BENCH_SHARE_GPU") == "1":
+        os.environ["GPU_MAX_HW_QUEUES"] = "1"
 
 
 def sweep(ns: list, argv: list) -> int:
     """One fresh rank group per N (1-rank groups too run in a child, so every N starts from a clean process)."""
     import torch.multiprocessing as mp
+    _share_queues()
     results = {}
     for n in ns:
         with tempfile.NamedTemporaryFile(suffix=".json", delete=False) as f:
