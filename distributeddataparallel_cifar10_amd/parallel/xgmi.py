@@ -202,15 +202,22 @@ class XgmiComm:
         dist.all_reduce(tv, op=dist.ReduceOp.MAX, group=self.group)
         tv = tv.cpu().tolist()
         one, two = tv[0::2], tv[1::2]
-        cross = None
-        for i in range(len(sizes) - 1, -1, -1):  # walk down while two-shot keeps winning
-            if two[i] < one[i]:
-                cross = sizes[i] * wire_b
-            else:
-                break
+        cross = self.pick_crossover([n * wire_b for n in sizes], one, two)
         self.crossover_bytes = cross if cross is not None else (1 << 62)  # never: one-shot everywhere measured
         self.calibration = {"bytes": [n * wire_b for n in sizes], "oneshot_us": one, "twoshot_us": two,
                             "crossover_bytes": cross, "world": self.world}
+        return cross
+
+    @staticmethod
+    def pick_crossover(sizes_bytes, oneshot_us, twoshot_us) -> Optional[int]:
+        """The smallest measured size from which two-shot is faster at that size and every larger one (None: it
+        never is).  A two-shot win at a small size followed by a loss above it is noise, not a crossover."""
+        cross = None
+        for i in range(len(sizes_bytes) - 1, -1, -1):  # walk down while two-shot keeps winning
+            if twoshot_us[i] < oneshot_us[i]:
+                cross = int(sizes_bytes[i])
+            else:
+                break
         return cross
 
     # ---- the collective ---------------------------------------------------------------------------------------

@@ -230,3 +230,16 @@ def test_fused_overlapped_sgd_matches_step(ws):
         p.join(timeout=60)
     bad = [r for r in res if r[1]]
     assert not bad, "\n".join(f"rank {r}:\n{e}" for r, e in bad)
+
+
+def test_xgmi_crossover_pick():
+    """XgmiComm.calibrate's decision rule (CPU): two-shot from the smallest size where it wins at that size and
+    every larger one; an isolated small-size win is noise; no win means one-shot everywhere."""
+    from distributeddataparallel_cifar10_amd.parallel.xgmi import XgmiComm
+    sizes = [1 << 16, 1 << 18, 1 << 20, 1 << 22]
+    pick = XgmiComm.pick_crossover
+    assert pick(sizes, [10, 20, 40, 80], [12, 18, 30, 50]) == 1 << 18
+    assert pick(sizes, [10, 20, 40, 80], [9, 25, 30, 50]) == 1 << 20   # the 64 KiB win is not a crossover
+    assert pick(sizes, [10, 20, 40, 80], [11, 21, 41, 81]) is None
+    assert pick(sizes, [10, 20, 40, 80], [9, 19, 39, 79]) == 1 << 16
+    assert pick(sizes, [10, 20, 40, 80], [9, 19, 39, 81]) is None       # loses at the largest size
