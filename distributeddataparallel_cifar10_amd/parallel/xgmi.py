@@ -196,11 +196,16 @@ class XgmiComm:
                 e1.record(st)
                 e1.synchronize()
                 times.append(e0.elapsed_time(e1) * 1e3 / reps)  # us per call
-        self.check()
+        if self.errors(reset=False):  # a peer wait expired: no timing is trusted (and check() will still report it)
+            times = [float("inf")] * len(times)
+        # every rank reaches this all-reduce, failed or not, so no rank is left waiting in it
         tv = torch.tensor(times, dtype=torch.float64,
                           device="cpu" if dist.get_backend(self.group) == "gloo" else buf.device)
         dist.all_reduce(tv, op=dist.ReduceOp.MAX, group=self.group)
         tv = tv.cpu().tolist()
+        if any(v == float("inf") for v in tv):
+            self.calibration = {"failed": True, "world": self.world}
+            return None  # the library's modelled crossover stays in use
         one, two = tv[0::2], tv[1::2]
         cross = self.pick_crossover([n * wire_b for n in sizes], one, two)
         self.crossover_bytes = cross if cross is not None else (1 << 62)  # never: one-shot everywhere measured
