@@ -1,0 +1,340 @@
+// BatchNorm pass micro-benchmark (ResNet-50 batch-256 shapes): the production kernels of csrc/ops_nn.hip against
+// variants of the backward-statistics / backward-apply / apply passes (rows per workgroup, rows in flight per
+// thread, non-temporal loads and stores).  Standalone: hipcc --offload-arch=gfx950 -O3 bn_micro.hip -o bn_micro
+// Output: one line per (kernel, shape, variant): median us over 20 launches and the bytes moved per us.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <functional>
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
+
+#include "../../distributeddataparallel_cifar10_amd/csrc/ops_nn.hip"
+
+using namespace dca::ops;
+
+#define CK(x)                                                                        \
+  do {                                                                               \
+    hipError_t e_ = (x);                                                             \
+    if (e_ != hipSuccess) {                                                          \
+      fprintf(stderr, "%s:%d %s\n", __FILE__, __LINE__, hipGetErrorString(e_));      \
+      exit(1);                                                                       \
+    }                                                                                \
+  } while (0)
+
+typedef unsigned v4u_t __attribute__((ext_vector_type(4)));
+
+template <bool NT>
+__device__ __forceinline__ uint4 ld16(const bf16_t* p) {
+  if constexpr (NT) {
+    const v4u_t v = __builtin_nontemporal_load((const v4u_t*)p);
+    return uint4{v.x, v.y, v.z, v.w};
+  } else {
+    return *(const uint4*)p;
+  }
+}
+template <bool NT>
+__device__ __forceinline__ void st16(bf16_t* p, uint4 v) {
+  if constexpr (NT) __builtin_nontemporal_store(v4u_t{v.x, v.y, v.z, v.w}, (v4u_t*)p);
+  else *(uint4*)p = v;
+}
+
+// backward statistics with the stored mask (bn3) or the recomputed ReLU (bn1 / bn2)
+template <int CL, int ROWS, int U, bool NT>
+__global__ void __launch_bounds__(256) v_bwd_stats(const bf16_t* __restrict__ dy, const bf16_t* __restrict__ x,
+                                                   const float2* __restrict__ stats, const float* __restrict__ gamma,
+                                                   const float* __restrict__ beta, float2* __restrict__ part, int M,
+                                                   int C, const uint8_t* __restrict__ mk) {
+  __shared__ float2 red[256 / CL][8 * CL];
+  const int cgl = threadIdx.x % CL, rl = threadIdx.x / CL, c0 = blockIdx.x * (8 * CL) + cgl * 8;
+  const int r0 = blockIdx.y * ROWS;
+  float s[8], q[8], mu[8], is[8], ga[8], be[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int c = min(c0 + j, C - 1);
+    s[j] = q[j] = 0.f;
+    mu[j] = stats[c].x;
+    is[j] = stats[c].y;
+    ga[j] = gamma[c];
+    be[j] = beta[c];
+  }
+  if (c0 < C) {
+    const int rend = min(M, r0 + ROWS);
+    for (int base = r0 + rl; base < rend; base += (256 / CL) * U) {
+      uint4 X[U], D[U];
+      unsigned MB[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const long o = (long)min(base + (256 / CL) * u, rend - 1) * C + c0;
+        X[u] = ld16<NT>(x + o);
+        D[u] = ld16<NT>(dy + o);
+        if (mk) MB[u] = mk[o >> 3];
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        if (base + (256 / CL) * u >= rend) break;
+        float xv[8], dv[8];
+        unpack8(X[u], xv);
+        unpack8(D[u], dv);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float xh = (xv[j] - mu[j]) * is[j];
+          float d = dv[j];
+          if (mk) d = (MB[u] >> j) & 1u ? d : 0.f;
+          else d = xh * ga[j] + be[j] > 0.f ? d : 0.f;
+          s[j] += d;
+          q[j] += d * xh;
+        }
+      }
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < 8; ++j) red[rl][cgl * 8 + j] = float2{s[j], q[j]};
+  __syncthreads();
+  const int c = blockIdx.x * (8 * CL) + threadIdx.x;
+  if (threadIdx.x < 8 * CL && c < C) {
+    float2 a = red[0][threadIdx.x];
+    for (int k = 1; k < 256 / CL; ++k) {
+      a.x += red[k][threadIdx.x].x;
+      a.y += red[k][threadIdx.x].y;
+    }
+    part[(long)blockIdx.y * C + c] = a;
+  }
+}
+
+// backward apply: dx = ca dz + cb x + cd; with the mask (bn3) also dr = dz
+template <int CL, int ROWS, int U, bool NT>
+__global__ void __launch_bounds__(256) v_bwd_apply(const bf16_t* __restrict__ dy, const bf16_t* __restrict__ x,
+                                                   const float2* __restrict__ stats, const float* __restrict__ gamma,
+                                                   const float* __restrict__ beta, const float2* __restrict__ sums,
+                                                   bf16_t* __restrict__ dx, bf16_t* __restrict__ dr, long M, int C,
+                                                   const uint8_t* __restrict__ mk) {
+  const int cgl = threadIdx.x % CL, rl = threadIdx.x / CL, c0 = blockIdx.x * (8 * CL) + cgl * 8;
+  if (c0 >= C) return;
+  const long r0 = (long)blockIdx.y * ROWS;
+  const float inv_m = 1.f / (float)M;
+  float mu[8], is[8], ga[8], be[8], ca[8], cb[8], cd[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const float2 st = stats[c0 + j], sm = sums[c0 + j];
+    mu[j] = st.x;
+    is[j] = st.y;
+    ga[j] = gamma[c0 + j];
+    be[j] = beta[c0 + j];
+    ca[j] = ga[j] * is[j];
+    cb[j] = -ca[j] * is[j] * sm.y * inv_m;
+    cd[j] = -ca[j] * sm.x * inv_m - cb[j] * mu[j];
+  }
+  const long rend = M < r0 + ROWS ? M : r0 + ROWS;
+  for (long base = r0 + rl; base < rend; base += (256 / CL) * U) {
+    uint4 X[U], D[U];
+    unsigned MB[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const long row = base + (256 / CL) * u, o = (row < rend ? row : rend - 1) * C + c0;
+      X[u] = ld16<NT>(x + o);
+      D[u] = ld16<NT>(dy + o);
+      if (mk) MB[u] = mk[o >> 3];
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const long row = base + (256 / CL) * u;
+      if (row >= rend) break;
+      const long o = row * C + c0;
+      float xv[8], d[8], rv[8];
+      unpack8(X[u], xv);
+      unpack8(D[u], d);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        float dz = d[j];
+        if (mk) dz = (MB[u] >> j) & 1u ? dz : 0.f;
+        else dz = (xv[j] - mu[j]) * is[j] * ga[j] + be[j] > 0.f ? dz : 0.f;
+        rv[j] = dz;
+        d[j] = ca[j] * dz + cb[j] * xv[j] + cd[j];
+      }
+      st16<NT>(dx + o, pack8(d));
+      if (mk && dr) st16<NT>(dr + o, pack8(rv));
+    }
+  }
+}
+
+// forward apply: out = relu(x sc + sh (+ r)); with r also the mask
+template <int CL, int ROWS, int U, bool NT>
+__global__ void __launch_bounds__(256) v_apply(const bf16_t* __restrict__ x, const bf16_t* __restrict__ r,
+                                               bf16_t* __restrict__ out, const float2* __restrict__ stats,
+                                               const float* __restrict__ gamma, const float* __restrict__ beta, long M,
+                                               int C, uint8_t* __restrict__ mk) {
+  const int cgl = threadIdx.x % CL, rl = threadIdx.x / CL, c0 = blockIdx.x * (8 * CL) + cgl * 8;
+  if (c0 >= C) return;
+  const long r0 = (long)blockIdx.y * ROWS;
+  float sc[8], sh[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const float2 st = stats[c0 + j];
+    sc[j] = st.y * gamma[c0 + j];
+    sh[j] = beta[c0 + j] - st.x * sc[j];
+  }
+  const long rend = M < r0 + ROWS ? M : r0 + ROWS;
+  for (long base = r0 + rl; base < rend; base += (256 / CL) * U) {
+    uint4 X[U], R[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const long rw = base + (256 / CL) * u, o = (rw < rend ? rw : rend - 1) * C + c0;
+      X[u] = ld16<NT>(x + o);
+      if (r) R[u] = ld16<NT>(r + o);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const long row = base + (256 / CL) * u;
+      if (row >= rend) break;
+      const long o = row * C + c0;
+      float v[8], rv[8];
+      unpack8(X[u], v);
+      if (r) unpack8(R[u], rv);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        float z = v[j] * sc[j] + sh[j];
+        if (r) z += rv[j];
+        v[j] = z > 0.f ? z : 0.f;
+      }
+      st16<NT>(out + o, pack8(v));
+      if (mk) {
+        unsigned b = 0;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) b |= (v[j] > 0.f ? 1u : 0u) << j;
+        mk[o >> 3] = (uint8_t)b;
+      }
+    }
+  }
+}
+
+struct Bufs {
+  bf16_t *a, *b, *c, *d;
+  uint8_t* mk;
+  float2 *stats, *sums, *part;
+  float *gamma, *beta;
+};
+
+static float time_us(const std::function<void()>& f) {
+  hipEvent_t e0, e1;
+  CK(hipEventCreate(&e0));
+  CK(hipEventCreate(&e1));
+  std::vector<float> v;
+  for (int i = 0; i < 2; ++i) f();
+  for (int i = 0; i < 10; ++i) {
+    CK(hipEventRecord(e0, 0));
+    f();
+    CK(hipEventRecord(e1, 0));
+    CK(hipEventSynchronize(e1));
+    float ms;
+    CK(hipEventElapsedTime(&ms, e0, e1));
+    v.push_back(ms * 1e3f);
+  }
+  std::sort(v.begin(), v.end());
+  CK(hipEventDestroy(e0));
+  CK(hipEventDestroy(e1));
+  return v[v.size() / 2];
+}
+
+// one timed (kernel, variant) cell; the per-shape driver interleaves the variants over several rounds and keeps
+// each cell's best round, so clock / cache drift does not favour whichever variant runs first
+struct Cell {
+  const char* k;
+  const char* v;
+  double bytes;
+  std::function<void()> f;
+  float best = 1e30f;
+};
+
+template <int CL, int ROWS, int U, bool NT>
+static void add_variants(std::vector<Cell>& cells, const Bufs& B, long M, int C, bool bn3, const char* tag) {
+  const dim3 g((C + 8 * CL - 1) / (8 * CL), (unsigned)((M + ROWS - 1) / ROWS)), b(256);
+  const double e = (double)M * C;
+  const uint8_t* mk = bn3 ? B.mk : nullptr;
+  cells.push_back({"bwd_stats", tag, e * 4 + (bn3 ? e / 8 : 0), [=] {
+    hipLaunchKernelGGL((v_bwd_stats<CL, ROWS, U, NT>), g, b, 0, 0, B.a, B.b, B.stats, B.gamma, B.beta, B.part, (int)M,
+                       C, mk);
+  }});
+  cells.push_back({"bwd_apply", tag, e * (bn3 ? 8 : 6) + (bn3 ? e / 8 : 0), [=] {
+    hipLaunchKernelGGL((v_bwd_apply<CL, ROWS, U, NT>), g, b, 0, 0, B.a, B.b, B.stats, B.gamma, B.beta, B.sums, B.c,
+                       bn3 ? B.d : nullptr, M, C, mk);
+  }});
+  cells.push_back({"apply", tag, e * (bn3 ? 6 : 4) + (bn3 ? e / 8 : 0), [=] {
+    hipLaunchKernelGGL((v_apply<CL, ROWS, U, NT>), g, b, 0, 0, B.a, bn3 ? B.b : nullptr, B.c, B.stats, B.gamma,
+                       B.beta, M, C, bn3 ? B.mk : nullptr);
+  }});
+}
+
+template <int CL>
+static void run_shape(const Bufs& B, long M, int C, bool bn3) {
+  std::vector<Cell> cells;
+  const int nparts = (int)((M + BN_ROWS - 1) / BN_ROWS);
+  const dim3 g((C + 8 * CL - 1) / (8 * CL), nparts), b(256);
+  const double e = (double)M * C;
+  // production kernels (ops_nn.hip) as the baseline
+  cells.push_back({"bwd_stats", "prod", e * 4 + (bn3 ? e / 8 : 0), [=] {
+    if (bn3)
+      hipLaunchKernelGGL((k_bn_bwd_stats<CL, BWD_MASK, false>), g, b, 0, 0, B.a, B.b, (const bf16_t*)nullptr, B.stats,
+                         B.gamma, B.beta, B.part, (int)M, C, B.mk);
+    else
+      hipLaunchKernelGGL((k_bn_bwd_stats<CL, BWD_RELU, false>), g, b, 0, 0, B.a, B.b, (const bf16_t*)nullptr, B.stats,
+                         B.gamma, B.beta, B.part, (int)M, C, (const uint8_t*)nullptr);
+  }});
+  cells.push_back({"bwd_apply", "prod", e * (bn3 ? 8 : 6) + (bn3 ? e / 8 : 0), [=] {
+    if (bn3)
+      hipLaunchKernelGGL((k_bn_bwd_apply<CL, BWD_MASK, 256, false>), g, b, 0, 0, B.a, B.b, (const bf16_t*)nullptr,
+                         B.stats, B.gamma, B.beta, B.sums, B.c, B.d, M, C, B.mk);
+    else
+      hipLaunchKernelGGL((k_bn_bwd_apply<CL, BWD_RELU, 256, false>), g, b, 0, 0, B.a, B.b, (const bf16_t*)nullptr,
+                         B.stats, B.gamma, B.beta, B.sums, B.c, (bf16_t*)nullptr, M, C, (const uint8_t*)nullptr);
+  }});
+  cells.push_back({"apply", "prod", e * (bn3 ? 6 : 4) + (bn3 ? e / 8 : 0), [=] {
+    hipLaunchKernelGGL((k_bn_apply<CL>), g, b, 0, 0, B.a, bn3 ? B.b : nullptr, B.c, B.stats, B.gamma, B.beta, M, C, 1,
+                       bn3 ? 2 : 0, (uint8_t*)nullptr, (const float*)nullptr, (unsigned*)nullptr,
+                       bn3 ? B.mk : nullptr);
+  }});
+  add_variants<CL, 256, 4, false>(cells, B, M, C, bn3, "r256u4");
+  add_variants<CL, 256, 4, true>(cells, B, M, C, bn3, "r256u4nt");
+  add_variants<CL, 128, 4, true>(cells, B, M, C, bn3, "r128u4nt");
+  add_variants<CL, 128, 8, true>(cells, B, M, C, bn3, "r128u8nt");
+  add_variants<CL, 512, 8, true>(cells, B, M, C, bn3, "r512u8nt");
+  for (int round = 0; round < 5; ++round)
+    for (Cell& c : cells) c.best = std::min(c.best, time_us(c.f));
+  for (const Cell& c : cells)
+    printf("{\"k\":\"%s\",\"M\":%ld,\"C\":%d,\"bn3\":%d,\"v\":\"%s\",\"us\":%.1f,\"TBs\":%.2f}\n", c.k, M, C,
+           bn3, c.v, c.best, c.bytes / c.best / 1e6);
+  fflush(stdout);
+}
+
+int main() {
+  const long EMAX = 802816L * 256;
+  Bufs B;
+  CK(hipMalloc(&B.a, EMAX * 2));
+  CK(hipMalloc(&B.b, EMAX * 2));
+  CK(hipMalloc(&B.c, EMAX * 2));
+  CK(hipMalloc(&B.d, EMAX * 2));
+  CK(hipMalloc(&B.mk, EMAX / 8));
+  CK(hipMalloc(&B.stats, 4096 * 8));
+  CK(hipMalloc(&B.sums, 4096 * 8));
+  CK(hipMalloc(&B.part, (EMAX / 64) * 8 + 4096 * 8));
+  CK(hipMalloc(&B.gamma, 4096 * 4));
+  CK(hipMalloc(&B.beta, 4096 * 4));
+  CK(hipMemset(B.a, 0x3c, EMAX * 2));  // bf16 ~1.0-ish patterns: finite math
+  CK(hipMemset(B.b, 0x3c, EMAX * 2));
+  CK(hipMemset(B.mk, 0x5a, EMAX / 8));
+  CK(hipMemset(B.stats, 0, 4096 * 8));
+  CK(hipMemset(B.sums, 0, 4096 * 8));
+  CK(hipMemset(B.gamma, 0, 4096 * 4));
+  CK(hipMemset(B.beta, 0, 4096 * 4));
+  struct S { long M; int C; bool bn3; };
+  const S shapes[] = {{802816, 256, true}, {200704, 512, true}, {50176, 1024, true}, {12544, 2048, true},
+                      {802816, 64, false}, {200704, 128, false}, {50176, 256, false}, {12544, 512, false},
+                      {802816, 128, false}, {200704, 256, false}};
+  for (const S& s : shapes) {
+    if (s.C % 128 == 0) run_shape<16>(B, s.M, s.C, s.bn3);
+    else run_shape<8>(B, s.M, s.C, s.bn3);
+  }
+  CK(hipDeviceSynchronize());
+  return 0;
+}

@@ -146,13 +146,65 @@ inline bool getenv_wgrad_ok() {
 }
 inline int nparts_rows(long M) { return (int)((M + dca::ops::BN_ROWS - 1) / dca::ops::BN_ROWS); }
 // BN kernels: 16 channel lanes (256 contiguous bytes per row and wave instruction) when C % 128 == 0, else 8
-#define BN_LAUNCH(kern, C, rows, st, ...)                                                              \
-  do {                                                                                                 \
-    if ((C) % 128 == 0)                                                                                \
-      hipLaunchKernelGGL((kern<16>), dim3((C) / 128, rows), dim3(256), 0, st, __VA_ARGS__);            \
-    else                                                                                               \
-      hipLaunchKernelGGL((kern<8>), dim3(((C) + 63) / 64, rows), dim3(256), 0, st, __VA_ARGS__);       \
-  } while (0)
+
+// Per-shape policy of the large BN passes (bench/micro/bn_micro.hip, profiles/bn_micro_r4s.log; same box, ResNet-50
+// batch-256 shapes): tensors of >= 2^26 elements stream with non-temporal loads / stores (statistics 181.6 -> 145.5 us,
+// residual apply 251.6 -> 209.5 us at 802816 x 256); the 16-lane backward apply of >= 2^25 elements also takes 128
+// rows per workgroup (twice the workgroups: 104.5 -> 84.2 us at 50176 x 1024).  Smaller tensors keep the default
+// cache policy and 256 rows (they are re-read while still in the Infinity Cache).  DCA_OPS_BN_TUNE=0: the round-3
+// shape (256 rows, default policy) everywhere.
+using namespace dca::ops;
+inline bool getenv_bn_tune() {
+  static const bool v = getenv_flag("DCA_OPS_BN_TUNE");
+  return v;
+}
+inline bool bn_nt(long M, int C) { return getenv_bn_tune() && C % 128 == 0 && (long)M * C >= (1L << 26); }
+inline bool bn_bwd_apply_fine(long M, int C) {
+  return getenv_bn_tune() && C % 128 == 0 && (long)M * C >= (1L << 25);
+}
+inline int bn_bwd_mode(int relu, int res_mode, const void* mask) {
+  if (mask) return BWD_MASK;
+  if (relu) return res_mode == 2 ? BWD_RES : BWD_RELU;
+  return BWD_PLAIN;
+}
+template <int CL, typename... A>
+void bn_stats_launch(int mode, bool nt, dim3 g, hipStream_t st, A... a) {
+#define BST(MO)                                                                                  \
+  if (nt) hipLaunchKernelGGL((k_bn_bwd_stats<CL, MO, true>), g, dim3(256), 0, st, a...);         \
+  else hipLaunchKernelGGL((k_bn_bwd_stats<CL, MO, false>), g, dim3(256), 0, st, a...)
+  switch (mode) {
+    case BWD_PLAIN: BST(BWD_PLAIN); break;
+    case BWD_RELU: BST(BWD_RELU); break;
+    case BWD_RES: BST(BWD_RES); break;
+    default: BST(BWD_MASK); break;
+  }
+#undef BST
+}
+template <int CL, typename... A>
+void bn_bwd_apply_launch(int mode, bool fine, long M, int C, hipStream_t st, A... a) {
+  const unsigned gx = (unsigned)((C + 8 * CL - 1) / (8 * CL));
+  const dim3 g128(gx, (unsigned)((M + 127) / 128)), g256(gx, (unsigned)((M + 255) / 256));
+#define BAP(MO)                                                                                          \
+  if (fine) hipLaunchKernelGGL((k_bn_bwd_apply<CL, MO, 128, true>), g128, dim3(256), 0, st, a...);      \
+  else hipLaunchKernelGGL((k_bn_bwd_apply<CL, MO, 256, false>), g256, dim3(256), 0, st, a...)
+  switch (mode) {
+    case BWD_PLAIN: BAP(BWD_PLAIN); break;
+    case BWD_RELU: BAP(BWD_RELU); break;
+    case BWD_RES: BAP(BWD_RES); break;
+    default: BAP(BWD_MASK); break;
+  }
+#undef BAP
+}
+template <typename... A>
+void bn_apply_launch(long M, int C, hipStream_t st, A... a) {
+  if (C % 128 != 0) {
+    hipLaunchKernelGGL((k_bn_apply<8>), dim3((C + 63) / 64, nparts_rows(M)), dim3(256), 0, st, a...);
+  } else if (bn_nt(M, C)) {
+    hipLaunchKernelGGL((k_bn_apply<16, 128, true>), dim3(C / 128, (unsigned)((M + 127) / 128)), dim3(256), 0, st, a...);
+  } else {
+    hipLaunchKernelGGL((k_bn_apply<16>), dim3(C / 128, nparts_rows(M)), dim3(256), 0, st, a...);
+  }
+}
 }  // namespace
 
 using namespace dca::ops;
@@ -514,7 +566,7 @@ int dca_ops_bn_fwd(const void* x, const void* r, void* out, float* part, float* 
                                    nparts, (int)M, C, rm, rv, (float2*)stats, eps, momentum)
   BN_FIN_DISPATCH(C, FIN);
 #undef FIN
-  BN_LAUNCH(k_bn_apply, C, nparts_rows(M), st, (const bf16_t*)x, (const bf16_t*)r,
+  bn_apply_launch(M, C, st, (const bf16_t*)x, (const bf16_t*)r,
                      (bf16_t*)out, (const float2*)stats, gamma, beta, M, C, relu, res_mode, (uint8_t*)nullptr,
                      (const float*)nullptr, (unsigned*)nullptr, (uint8_t*)nullptr);
   OPCK(hipGetLastError());
@@ -540,7 +592,7 @@ int dca_ops_bn_fwd_parts(const void* x, const void* r, void* out, const float* p
                                    nparts, (int)M, C, rm, rv, (float2*)stats, eps, momentum)
   BN_FIN_DISPATCH(C, FIN);
 #undef FIN
-  BN_LAUNCH(k_bn_apply, C, nparts_rows(M), st, (const bf16_t*)x, (const bf16_t*)r,
+  bn_apply_launch(M, C, st, (const bf16_t*)x, (const bf16_t*)r,
                      (bf16_t*)out, (const float2*)stats, gamma, beta, M, C, relu, res_mode, (uint8_t*)q, amax_prev,
                      amax_out, (uint8_t*)mask);
   OPCK(hipGetLastError());
@@ -555,7 +607,7 @@ int dca_ops_bn_eval(const void* x, const void* r, void* out, float* stats, const
   REQUIRE(res_mode == 0 || r != nullptr, "bn: residual missing");
   hipStream_t st = (hipStream_t)stream;
   hipLaunchKernelGGL(k_bn_eval_stats, dim3((C + 255) / 256), dim3(256), 0, st, rm, rv, (float2*)stats, C, eps);
-  BN_LAUNCH(k_bn_apply, C, nparts_rows(M), st, (const bf16_t*)x, (const bf16_t*)r,
+  bn_apply_launch(M, C, st, (const bf16_t*)x, (const bf16_t*)r,
                      (bf16_t*)out, (const float2*)stats, gamma, beta, M, C, relu, res_mode, (uint8_t*)nullptr,
                      (const float*)nullptr, (unsigned*)nullptr, (uint8_t*)nullptr);
   OPCK(hipGetLastError());
@@ -569,18 +621,30 @@ int dca_ops_bn_bwd(const void* dy, const void* x, const void* r, const float* st
   REQUIRE(C % 8 == 0, "bn: C must be a multiple of 8");
   REQUIRE(res_mode != 2 || ((r != nullptr || mask != nullptr) && dr != nullptr), "bn bwd: residual tensors missing");
   REQUIRE(!mask || (relu && res_mode == 2), "bn bwd: the stored mask is for ReLU(bn + r)");
+  REQUIRE(res_mode != 2 || relu, "bn bwd: a residual join without ReLU is not supported");
   hipStream_t st = (hipStream_t)stream;
   const int nparts = (int)((M + BN_ROWS - 1) / BN_ROWS);
-  BN_LAUNCH(k_bn_bwd_stats, C, nparts, st, (const bf16_t*)dy,
-                     (const bf16_t*)x, (const bf16_t*)r, (const float2*)stats, gamma, beta, (float2*)part, (int)M, C,
-                     relu, res_mode, (const uint8_t*)mask);
+  const int mode = bn_bwd_mode(relu, res_mode, mask);
+  if (C % 128 == 0)
+    bn_stats_launch<16>(mode, bn_nt(M, C), dim3(C / 128, nparts), st, (const bf16_t*)dy, (const bf16_t*)x,
+                        (const bf16_t*)r, (const float2*)stats, gamma, beta, (float2*)part, (int)M, C,
+                        (const uint8_t*)mask);
+  else
+    bn_stats_launch<8>(mode, false, dim3((C + 63) / 64, nparts), st, (const bf16_t*)dy, (const bf16_t*)x,
+                       (const bf16_t*)r, (const float2*)stats, gamma, beta, (float2*)part, (int)M, C,
+                       (const uint8_t*)mask);
 #define FIN(CW) hipLaunchKernelGGL(k_bn_bwd_finalize<CW>, dim3((C + CW - 1) / CW), dim3(256), 0, st, \
                                    (const float2*)part, nparts, C, dgamma, dbeta, (float2*)sums, accumulate)
   BN_FIN_DISPATCH(C, FIN);
 #undef FIN
-  BN_LAUNCH(k_bn_bwd_apply, C, nparts_rows(M), st, (const bf16_t*)dy, (const bf16_t*)x,
-                     (const bf16_t*)r, (const float2*)stats, gamma, beta, (const float2*)sums, (bf16_t*)dx,
-                     (bf16_t*)dr, M, C, relu, res_mode, (const uint8_t*)mask);
+  if (C % 128 == 0)
+    bn_bwd_apply_launch<16>(mode, bn_bwd_apply_fine(M, C), M, C, st, (const bf16_t*)dy, (const bf16_t*)x,
+                            (const bf16_t*)r, (const float2*)stats, gamma, beta, (const float2*)sums, (bf16_t*)dx,
+                            (bf16_t*)dr, M, C, (const uint8_t*)mask);
+  else
+    bn_bwd_apply_launch<8>(mode, false, M, C, st, (const bf16_t*)dy, (const bf16_t*)x, (const bf16_t*)r,
+                           (const float2*)stats, gamma, beta, (const float2*)sums, (bf16_t*)dx, (bf16_t*)dr, M, C,
+                           (const uint8_t*)mask);
   OPCK(hipGetLastError());
   return 0;
 }
@@ -596,9 +660,14 @@ int dca_ops_bn_bwd_parts(const void* dy, const void* x, const float* stats, cons
                                    (const float2*)part, nparts, C, dgamma, dbeta, (float2*)sums, accumulate)
   BN_FIN_DISPATCH(C, FIN);
 #undef FIN
-  BN_LAUNCH(k_bn_bwd_apply, C, nparts_rows(M), st, (const bf16_t*)dy, (const bf16_t*)x, (const bf16_t*)nullptr,
-            (const float2*)stats, gamma, beta, (const float2*)sums, (bf16_t*)dx, (bf16_t*)nullptr, M, C, 1, 0,
-            (const uint8_t*)nullptr);
+  if (C % 128 == 0)
+    bn_bwd_apply_launch<16>(BWD_RELU, bn_bwd_apply_fine(M, C), M, C, st, (const bf16_t*)dy, (const bf16_t*)x,
+                            (const bf16_t*)nullptr, (const float2*)stats, gamma, beta, (const float2*)sums,
+                            (bf16_t*)dx, (bf16_t*)nullptr, M, C, (const uint8_t*)nullptr);
+  else
+    bn_bwd_apply_launch<8>(BWD_RELU, false, M, C, st, (const bf16_t*)dy, (const bf16_t*)x, (const bf16_t*)nullptr,
+                           (const float2*)stats, gamma, beta, (const float2*)sums, (bf16_t*)dx, (bf16_t*)nullptr, M,
+                           C, (const uint8_t*)nullptr);
   OPCK(hipGetLastError());
   return 0;
 }

@@ -130,6 +130,29 @@ __global__ void __launch_bounds__(256) k_col2im(const bf16_t* __restrict__ dcols
 constexpr int BN_ROWS = 256;  // rows per partial block (threads: 64 channel lanes x 4 row lanes)
 constexpr int BN_U = 4;        // rows per thread with their loads in flight together (apply / backward kernels)
 
+// 16-B activation loads / stores, optionally non-temporal (NT): the large BN passes stream tensors far bigger than
+// the Infinity Cache, where keeping them out of the caches measured 8-20 % faster (bench/micro/bn_micro.hip); the
+// smaller ones are re-read while still cache-resident and stay on the default policy
+typedef unsigned bn_v4u __attribute__((ext_vector_type(4)));
+template <bool NT>
+__device__ __forceinline__ uint4 bn_ld16(const bf16_t* p) {
+  if constexpr (NT) {
+    const bn_v4u v = __builtin_nontemporal_load((const bn_v4u*)p);
+    return uint4{v.x, v.y, v.z, v.w};
+  } else {
+    return *(const uint4*)p;
+  }
+}
+template <bool NT>
+__device__ __forceinline__ void bn_st16(bf16_t* p, uint4 v) {
+  if constexpr (NT) __builtin_nontemporal_store(bn_v4u{v.x, v.y, v.z, v.w}, (bn_v4u*)p);
+  else *(uint4*)p = v;
+}
+// How a BN backward recovers dz from dy (compile time, so each pass carries only its own loads and registers):
+//   BWD_PLAIN no activation; BWD_RELU ReLU recomputed from x; BWD_RES ReLU(bn(x) + r) recomputed (reads r);
+//   BWD_MASK the forward's stored ReLU bit mask.  BWD_RES / BWD_MASK (res_mode 2) also produce dr = dz.
+enum { BWD_PLAIN = 0, BWD_RELU = 1, BWD_RES = 2, BWD_MASK = 3 };
+
 // grid (ceil(C/64), ceil(M/BN_ROWS)); part[blockIdx.y][C] = (sum, sumsq)
 __global__ void __launch_bounds__(256) k_bn_stats(const bf16_t* __restrict__ x, const float* __restrict__ shift,
                                                   float2* __restrict__ part, int M, int C) {
@@ -241,17 +264,17 @@ __global__ void __launch_bounds__(256) k_bn_eval_stats(const float* __restrict__
 // Optionally also emits an fp8 e4m3 copy of the output for an fp8 consumer GEMM, with DELAYED scaling: the scale
 // 448 / amax comes from the previous step's amax of this tensor (amax_prev), and this step's amax is recorded in
 // amax_out for the next step -- no extra pass over the activation, no host sync.
-template <int CL>
+template <int CL, int ROWS = BN_ROWS, bool NT = false>
 __global__ void __launch_bounds__(256) k_bn_apply(const bf16_t* __restrict__ x, const bf16_t* __restrict__ r,
                                                   bf16_t* __restrict__ out, const float2* __restrict__ stats,
                                                   const float* __restrict__ gamma, const float* __restrict__ beta,
                                                   long M, int C, int relu, int res_mode, uint8_t* __restrict__ q,
                                                   const float* __restrict__ amax_prev, unsigned* __restrict__ amax_out,
                                                   uint8_t* __restrict__ mk) {
-  // grid (ceil(C/(8 CL)), ceil(M/BN_ROWS)): CL channel groups of 8 x 256/CL row lanes, z = x * sc + sh per channel
+  // grid (ceil(C/(8 CL)), ceil(M/ROWS)): CL channel groups of 8 x 256/CL row lanes, z = x * sc + sh per channel
   __shared__ float red[256];
   const int cgl = threadIdx.x % CL, rl = threadIdx.x / CL, c0 = blockIdx.x * (8 * CL) + cgl * 8;
-  const long r0 = (long)blockIdx.y * BN_ROWS;
+  const long r0 = (long)blockIdx.y * ROWS;
   float qs = 1.f, amax = 0.f;
   if (q) qs = *amax_prev > 0.f ? 448.f / *amax_prev : 1.f;
   if (c0 < C) {
@@ -262,14 +285,14 @@ __global__ void __launch_bounds__(256) k_bn_apply(const bf16_t* __restrict__ x, 
       sc[j] = st.y * gamma[c0 + j];
       sh[j] = beta[c0 + j] - st.x * sc[j];
     }
-    const long rend = M < r0 + BN_ROWS ? M : r0 + BN_ROWS;
+    const long rend = M < r0 + ROWS ? M : r0 + ROWS;
     for (long base = r0 + rl; base < rend; base += (256 / CL) * BN_U) {
     uint4 X[BN_U], R[BN_U];
 #pragma unroll
     for (int u = 0; u < BN_U; ++u) {  // all loads in flight first (clamped rows)
       const long rw = base + (256 / CL) * u, o = (rw < rend ? rw : rend - 1) * C + c0;
-      X[u] = *(const uint4*)(x + o);
-      if (res_mode) R[u] = *(const uint4*)(r + o);
+      X[u] = bn_ld16<NT>(x + o);
+      if (res_mode) R[u] = bn_ld16<NT>(r + o);
     }
 #pragma unroll
     for (int u = 0; u < BN_U; ++u) {
@@ -288,7 +311,7 @@ __global__ void __launch_bounds__(256) k_bn_apply(const bf16_t* __restrict__ x, 
         v[j] = z;
       }
       const uint4 ov = pack8(v);
-      *(uint4*)(out + o) = ov;
+      bn_st16<NT>(out + o, ov);
       if (mk) {  // ReLU mask, one bit per element (bit j: channel c0 + j), for the backward
         unsigned b = 0;
 #pragma unroll
@@ -326,15 +349,15 @@ __global__ void __launch_bounds__(256) k_bn_apply(const bf16_t* __restrict__ x, 
   }
 }
 
-// dz = dy * act'(.) recomputed from x (and r) -- or, when the forward stored it (mk: res_mode 2 + ReLU), the ReLU
-// bit mask (1/16 of the bytes of r; exactly the forward's mask); partial sums of dz and dz * xhat per channel.
-// grid (ceil(C/64), ceil(M/BN_ROWS)); 256 threads = 8 channel groups (8 channels, one 16-B load per tensor per
-// row) x 32 row lanes; all rows' loads of a thread are independent (issued back to back).
-template <int CL>
+// dz = dy * act'(.) recomputed from x (and r) -- or, when the forward stored it (BWD_MASK), the ReLU bit mask
+// (1/16 of the bytes of r; exactly the forward's mask); partial sums of dz and dz * xhat per channel.
+// grid (ceil(C/(8 CL)), ceil(M/BN_ROWS)); 256 threads = CL channel groups (8 channels, one 16-B load per tensor per
+// row) x 256/CL row lanes; all rows' loads of a thread are independent (issued back to back).
+template <int CL, int MODE, bool NT>
 __global__ void __launch_bounds__(256) k_bn_bwd_stats(const bf16_t* __restrict__ dy, const bf16_t* __restrict__ x,
                                                       const bf16_t* __restrict__ r, const float2* __restrict__ stats,
                                                       const float* __restrict__ gamma, const float* __restrict__ beta,
-                                                      float2* __restrict__ part, int M, int C, int relu, int res_mode,
+                                                      float2* __restrict__ part, int M, int C,
                                                       const uint8_t* __restrict__ mk) {
   __shared__ float2 red[256 / CL][8 * CL];
   const int cgl = threadIdx.x % CL, rl = threadIdx.x / CL, c0 = blockIdx.x * (8 * CL) + cgl * 8;
@@ -358,10 +381,10 @@ __global__ void __launch_bounds__(256) k_bn_bwd_stats(const bf16_t* __restrict__
 #pragma unroll
       for (int u = 0; u < BN_U; ++u) {
         const long o = (long)min(base + (256 / CL) * u, rend - 1) * C + c0;
-        X[u] = *(const uint4*)(x + o);
-        D[u] = *(const uint4*)(dy + o);
-        if (mk) MB[u] = mk[o >> 3];
-        else if (res_mode == 2) R[u] = *(const uint4*)(r + o);
+        X[u] = bn_ld16<NT>(x + o);
+        D[u] = bn_ld16<NT>(dy + o);
+        if constexpr (MODE == BWD_MASK) MB[u] = mk[o >> 3];
+        if constexpr (MODE == BWD_RES) R[u] = bn_ld16<NT>(r + o);
       }
 #pragma unroll
       for (int u = 0; u < BN_U; ++u) {
@@ -369,16 +392,16 @@ __global__ void __launch_bounds__(256) k_bn_bwd_stats(const bf16_t* __restrict__
         float xv[8], dv[8], rv[8];
         unpack8(X[u], xv);
         unpack8(D[u], dv);
-        if (!mk && res_mode == 2) unpack8(R[u], rv);
+        if constexpr (MODE == BWD_RES) unpack8(R[u], rv);
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
           const float xh = (xv[j] - mu[j]) * is[j];
           float d = dv[j];
-          if (mk) {
+          if constexpr (MODE == BWD_MASK) {
             d = (MB[u] >> j) & 1u ? d : 0.f;
-          } else if (relu) {
+          } else if constexpr (MODE != BWD_PLAIN) {
             float z = xh * ga[j] + be[j];
-            if (res_mode == 2) z += rv[j];
+            if constexpr (MODE == BWD_RES) z += rv[j];
             d = z > 0.f ? d : 0.f;
           }
           s[j] += d;
@@ -416,19 +439,19 @@ __global__ void __launch_bounds__(256) k_bn_bwd_finalize(const float2* __restric
   dbeta[c] = accumulate ? dbeta[c] + a.x : a.x;
 }
 
-// dx = gamma * invstd * (dz - mean(dz) - xhat * mean(dz * xhat)); res_mode 2 also writes dr = dz.
-// grid (ceil(C/64), ceil(M/BN_ROWS)): 8 channel groups x 32 row lanes, per-channel coefficients folded once per
+// dx = gamma * invstd * (dz - mean(dz) - xhat * mean(dz * xhat)); BWD_RES / BWD_MASK also write dr = dz.
+// grid (ceil(C/(8 CL)), ceil(M/ROWS)): CL channel groups x 256/CL row lanes, per-channel coefficients folded once per
 // thread (dx = A*dz + B*x + D), one 16-B load / store per tensor per row.
-template <int CL>
+template <int CL, int MODE, int ROWS, bool NT>
 __global__ void __launch_bounds__(256) k_bn_bwd_apply(const bf16_t* __restrict__ dy, const bf16_t* __restrict__ x,
                                                       const bf16_t* __restrict__ r, const float2* __restrict__ stats,
                                                       const float* __restrict__ gamma, const float* __restrict__ beta,
                                                       const float2* __restrict__ sums, bf16_t* __restrict__ dx,
-                                                      bf16_t* __restrict__ dr, long M, int C, int relu, int res_mode,
+                                                      bf16_t* __restrict__ dr, long M, int C,
                                                       const uint8_t* __restrict__ mk) {
   const int cgl = threadIdx.x % CL, rl = threadIdx.x / CL, c0 = blockIdx.x * (8 * CL) + cgl * 8;
   if (c0 >= C) return;
-  const long r0 = (long)blockIdx.y * BN_ROWS;
+  const long r0 = (long)blockIdx.y * ROWS;
   const float inv_m = 1.f / (float)M;
   float mu[8], is[8], ga[8], be[8], ca[8], cb[8], cd[8];
 #pragma unroll
@@ -443,17 +466,17 @@ __global__ void __launch_bounds__(256) k_bn_bwd_apply(const bf16_t* __restrict__
     cb[j] = -ca[j] * is[j] * sm.y * inv_m;
     cd[j] = -ca[j] * sm.x * inv_m - cb[j] * mu[j];
   }
-  const long rend = M < r0 + BN_ROWS ? M : r0 + BN_ROWS;
+  const long rend = M < r0 + ROWS ? M : r0 + ROWS;
   for (long base = r0 + rl; base < rend; base += (256 / CL) * BN_U) {
     uint4 X[BN_U], D[BN_U], R[BN_U];
     unsigned MB[BN_U];
 #pragma unroll
     for (int u = 0; u < BN_U; ++u) {  // all loads in flight first (clamped rows)
       const long row = base + (256 / CL) * u, o = (row < rend ? row : rend - 1) * C + c0;
-      X[u] = *(const uint4*)(x + o);
-      D[u] = *(const uint4*)(dy + o);
-      if (mk) MB[u] = mk[o >> 3];
-      else if (res_mode == 2) R[u] = *(const uint4*)(r + o);
+      X[u] = bn_ld16<NT>(x + o);
+      D[u] = bn_ld16<NT>(dy + o);
+      if constexpr (MODE == BWD_MASK) MB[u] = mk[o >> 3];
+      if constexpr (MODE == BWD_RES) R[u] = bn_ld16<NT>(r + o);
     }
 #pragma unroll
     for (int u = 0; u < BN_U; ++u) {
@@ -463,22 +486,22 @@ __global__ void __launch_bounds__(256) k_bn_bwd_apply(const bf16_t* __restrict__
       float xv[8], d[8], rv[8];
       unpack8(X[u], xv);
       unpack8(D[u], d);
-      if (!mk && res_mode == 2) unpack8(R[u], rv);
+      if constexpr (MODE == BWD_RES) unpack8(R[u], rv);
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         float dz = d[j];
-        if (mk) {
+        if constexpr (MODE == BWD_MASK) {
           dz = (MB[u] >> j) & 1u ? dz : 0.f;
-        } else if (relu) {
+        } else if constexpr (MODE != BWD_PLAIN) {
           float z = (xv[j] - mu[j]) * is[j] * ga[j] + be[j];
-          if (res_mode == 2) z += rv[j];
+          if constexpr (MODE == BWD_RES) z += rv[j];
           dz = z > 0.f ? dz : 0.f;
         }
         rv[j] = dz;
         d[j] = ca[j] * dz + cb[j] * xv[j] + cd[j];
       }
-      *(uint4*)(dx + o) = pack8(d);
-      if (res_mode == 2) *(uint4*)(dr + o) = pack8(rv);
+      bn_st16<NT>(dx + o, pack8(d));
+      if constexpr (MODE == BWD_RES || MODE == BWD_MASK) bn_st16<NT>(dr + o, pack8(rv));
     }
   }
 }
