@@ -146,6 +146,8 @@ inline bool getenv_wgrad_ok() {
 }
 inline int nparts_rows(long M) { return (int)((M + dca::ops::BN_ROWS - 1) / dca::ops::BN_ROWS); }
 // BN kernels: 16 channel lanes (256 contiguous bytes per row and wave instruction) when C % 128 == 0, else 8
+// finalize threads per workgroup: 1024 when one workgroup reduces one channel's partial rows (C < 256)
+#define BN_FIN_NTH(CW) ((CW) == 1 ? 1024 : 256)
 
 // Per-shape policy of the large BN passes (bench/micro/bn_micro.hip, profiles/bn_micro_r4s.log; same box, ResNet-50
 // batch-256 shapes): tensors of >= 2^26 elements stream with non-temporal loads / stores (statistics 181.6 -> 145.5 us,
@@ -562,7 +564,7 @@ int dca_ops_bn_fwd(const void* x, const void* r, void* out, float* part, float* 
   const int nparts = (int)((M + BN_ROWS - 1) / BN_ROWS);
   hipLaunchKernelGGL(k_bn_stats, dim3((C + 63) / 64, nparts), dim3(256), 0, st, (const bf16_t*)x, rm, (float2*)part,
                      (int)M, C);
-#define FIN(CW) hipLaunchKernelGGL(k_bn_finalize<CW>, dim3((C + CW - 1) / CW), dim3(256), 0, st, (const float2*)part, \
+#define FIN(CW) hipLaunchKernelGGL((k_bn_finalize<CW, BN_FIN_NTH(CW)>), dim3((C + CW - 1) / CW), dim3(BN_FIN_NTH(CW)), 0, st, (const float2*)part, \
                                    nparts, (int)M, C, rm, rv, (float2*)stats, eps, momentum)
   BN_FIN_DISPATCH(C, FIN);
 #undef FIN
@@ -588,7 +590,7 @@ int dca_ops_bn_fwd_parts(const void* x, const void* r, void* out, const float* p
   REQUIRE(!mask || (relu && res_mode == 2), "bn: the stored mask is for ReLU(bn + r)");
   hipStream_t st = (hipStream_t)stream;
   if (q) OPCK(hipMemsetAsync(amax_out, 0, sizeof(unsigned), st));
-#define FIN(CW) hipLaunchKernelGGL(k_bn_finalize<CW>, dim3((C + CW - 1) / CW), dim3(256), 0, st, (const float2*)part, \
+#define FIN(CW) hipLaunchKernelGGL((k_bn_finalize<CW, BN_FIN_NTH(CW)>), dim3((C + CW - 1) / CW), dim3(BN_FIN_NTH(CW)), 0, st, (const float2*)part, \
                                    nparts, (int)M, C, rm, rv, (float2*)stats, eps, momentum)
   BN_FIN_DISPATCH(C, FIN);
 #undef FIN
@@ -633,7 +635,7 @@ int dca_ops_bn_bwd(const void* dy, const void* x, const void* r, const float* st
     bn_stats_launch<8>(mode, false, dim3((C + 63) / 64, nparts), st, (const bf16_t*)dy, (const bf16_t*)x,
                        (const bf16_t*)r, (const float2*)stats, gamma, beta, (float2*)part, (int)M, C,
                        (const uint8_t*)mask);
-#define FIN(CW) hipLaunchKernelGGL(k_bn_bwd_finalize<CW>, dim3((C + CW - 1) / CW), dim3(256), 0, st, \
+#define FIN(CW) hipLaunchKernelGGL((k_bn_bwd_finalize<CW, BN_FIN_NTH(CW)>), dim3((C + CW - 1) / CW), dim3(BN_FIN_NTH(CW)), 0, st, \
                                    (const float2*)part, nparts, C, dgamma, dbeta, (float2*)sums, accumulate)
   BN_FIN_DISPATCH(C, FIN);
 #undef FIN
@@ -656,7 +658,7 @@ int dca_ops_bn_bwd_parts(const void* dy, const void* x, const float* stats, cons
                          int C, int accumulate, void* stream) {
   REQUIRE(C % 8 == 0 && nparts > 0, "bn: C must be a multiple of 8");
   hipStream_t st = (hipStream_t)stream;
-#define FIN(CW) hipLaunchKernelGGL(k_bn_bwd_finalize<CW>, dim3((C + CW - 1) / CW), dim3(256), 0, st, \
+#define FIN(CW) hipLaunchKernelGGL((k_bn_bwd_finalize<CW, BN_FIN_NTH(CW)>), dim3((C + CW - 1) / CW), dim3(BN_FIN_NTH(CW)), 0, st, \
                                    (const float2*)part, nparts, C, dgamma, dbeta, (float2*)sums, accumulate)
   BN_FIN_DISPATCH(C, FIN);
 #undef FIN

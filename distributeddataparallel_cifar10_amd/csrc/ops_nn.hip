@@ -185,9 +185,11 @@ __global__ void __launch_bounds__(256) k_bn_stats(const bf16_t* __restrict__ x, 
 // Sum of the per-tile partials of channel c.  A workgroup covers CW channels x (256 / CW) partial lanes: few
 // channels per workgroup (narrow layers) keep enough workgroups and short serial loops -- the reduction is
 // latency-bound (layer-1 BNs of ResNet-50 at batch 256: 6272 partials x 64 channels).  Tree combine in LDS.
-template <int CW>
+// NTH threads per workgroup (256; 1024 for the one-channel-per-workgroup form, whose 64-128 workgroups otherwise
+// walk thousands of partial rows in 3-4 dependent load rounds).
+template <int CW, int NTH = 256>
 __device__ __forceinline__ float2 reduce_parts(const float2* __restrict__ part, int nparts, int C, int c, float2* red) {
-  constexpr int PL = 256 / CW;
+  constexpr int PL = NTH / CW;
   const int pl = threadIdx.x / CW, cl = threadIdx.x % CW;
   float sx = 0.f, sy = 0.f;
   if (c < C) {
@@ -230,13 +232,13 @@ __device__ __forceinline__ float2 reduce_parts(const float2* __restrict__ part, 
     else { CALL(1); }                  \
   } while (0)
 
-template <int CW>
-__global__ void __launch_bounds__(256) k_bn_finalize(const float2* __restrict__ part, int nparts, int M, int C,
+template <int CW, int NTH = 256>
+__global__ void __launch_bounds__(NTH) k_bn_finalize(const float2* __restrict__ part, int nparts, int M, int C,
                                                      float* __restrict__ running_mean, float* __restrict__ running_var,
                                                      float2* __restrict__ stats, float eps, float momentum) {
-  __shared__ float2 red[256];
+  __shared__ float2 red[NTH];
   const int c = blockIdx.x * CW + (threadIdx.x % CW);
-  const float2 a = reduce_parts<CW>(part, nparts, C, c, red);
+  const float2 a = reduce_parts<CW, NTH>(part, nparts, C, c, red);
   if (threadIdx.x >= CW || c >= C) return;
   const float k = running_mean[c];
   const float dm = a.x / M;
@@ -426,13 +428,13 @@ __global__ void __launch_bounds__(256) k_bn_bwd_stats(const bf16_t* __restrict__
 
 // dgamma = sum(dz * xhat), dbeta = sum(dz) (written, or added when accumulate: shared modules); sums for dx.
 // grid ceil(C/16), 256 threads.
-template <int CW>
-__global__ void __launch_bounds__(256) k_bn_bwd_finalize(const float2* __restrict__ part, int nparts, int C,
+template <int CW, int NTH = 256>
+__global__ void __launch_bounds__(NTH) k_bn_bwd_finalize(const float2* __restrict__ part, int nparts, int C,
                                                          float* __restrict__ dgamma, float* __restrict__ dbeta,
                                                          float2* __restrict__ sums, int accumulate) {
-  __shared__ float2 red[256];
+  __shared__ float2 red[NTH];
   const int c = blockIdx.x * CW + (threadIdx.x % CW);
-  const float2 a = reduce_parts<CW>(part, nparts, C, c, red);
+  const float2 a = reduce_parts<CW, NTH>(part, nparts, C, c, red);
   if (threadIdx.x >= CW || c >= C) return;
   sums[c] = a;
   dgamma[c] = accumulate ? dgamma[c] + a.y : a.y;
