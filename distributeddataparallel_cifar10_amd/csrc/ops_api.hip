@@ -214,7 +214,7 @@ using namespace dca::ops;
 extern "C" {
 
 const char* dca_ops_last_error() { return g_err.c_str(); }
-int dca_ops_abi_version() { return 8; }
+int dca_ops_abi_version() { return 9; }
 
 // Must match ops/_native.py::GemmArgs.
 int dca_ops_gemm(const GemmArgs* a, void* stream) {
@@ -248,6 +248,11 @@ int dca_ops_gemm(const GemmArgs* a, void* stream) {
                           g.out_bf16 && g.N % 8 == 0 && g.ldc % 8 == 0 && g.wperm_T <= 0 && !g.fp8),
           "gemm: fused BN-backward statistics need a bf16 output with N % 8 == 0 and no split-K");
   REQUIRE(!g.bnb_part || (g.beta == 0.f && !g.bias && !g.relu), "gemm: fused BN-backward statistics: plain output");
+  REQUIRE(!g.beta_mask || (g.beta_src && g.beta_src != g.C && g.beta != 0.f && g.out_bf16 && !g.ta && !g.bnb_part &&
+                           g.splits <= 1 && g.wperm_T <= 0 && g.orow_S <= 0 && g.N % 8 == 0 && g.ldc % 8 == 0 &&
+                           ((uintptr_t)g.beta_src & 15) == 0),
+          "gemm: a masked accumulation source needs a separate 16-B aligned bf16 source, beta != 0 and a plain "
+          "bf16 output with N, ldc % 8 == 0");
   REQUIRE(g.orow_S <= 0 || (g.splits <= 1 && g.wperm_T <= 0 && g.orow_Ho > 0 && g.orow_Wo > 0 &&
                             (long)g.orow_Ho * g.orow_Wo > 0 && g.M % ((long)g.orow_Ho * g.orow_Wo) == 0 &&
                             g.orow_S * (g.orow_Ho - 1) + g.orow_ph < g.orow_H &&
@@ -408,6 +413,7 @@ int dca_ops_gemm(const GemmArgs* a, void* stream) {
                                   (g.N % 128 == 0 || g.N == 64) &&
                                   (sk == 1 || (g.K <= 512 && g.M >= 16384 && (g.beta == 0.f || g.K <= 128))));
     const bool st_ok = sk != 0 && shape_ok && !g.fp8 && !g.tb && g.splits == 1 && g.wperm_T <= 0 && g.orow_S <= 0 &&
+                       !(conv && g.beta_mask) &&
                        !g.bnb_part && !g.relu && g.out_bf16 && g.N % 64 == 0 && g.N <= 2048 && g.K % 64 == 0 &&
                        g.K > 0 && g.M > 0 && g.ldb % 8 == 0 && g.ldc % 8 == 0 && g.ldb >= g.K && g.ldc >= g.N &&
                        ((uintptr_t)g.A & 15) == 0 && ((uintptr_t)g.B & 15) == 0 && ((uintptr_t)g.C & 15) == 0 &&
@@ -435,6 +441,12 @@ int dca_ops_gemm(const GemmArgs* a, void* stream) {
       OPCK(hipGetLastError());
       return 0;
     }
+  }
+  if (g.beta_mask) {  // the other kernels read C_old from C: materialise the masked source there first
+    hipLaunchKernelGGL(k_masked_copy, dim3(grid_for((long)g.M * (g.N / 8), 256, 4096)), dim3(256), 0, st,
+                       (const unsigned short*)g.beta_src, g.beta_mask, (unsigned short*)g.C, g.M, g.N, g.ldc);
+    g.beta_mask = nullptr;
+    g.beta_src = nullptr;
   }
   // ping-pong 256 x 256 kernel: bf16, K-contiguous operands (plain or the C % 64 implicit conv), no split-K / row
   // remap / fused BN-backward statistics, 16-B aligned rows, operands addressable with 32-bit offsets
@@ -621,7 +633,8 @@ int dca_ops_bn_bwd(const void* dy, const void* x, const void* r, const float* st
                    const float* beta, float* part, float* sums, float* dgamma, float* dbeta, void* dx, void* dr,
                    long M, int C, int relu, int res_mode, int accumulate, const void* mask, void* stream) {
   REQUIRE(C % 8 == 0, "bn: C must be a multiple of 8");
-  REQUIRE(res_mode != 2 || ((r != nullptr || mask != nullptr) && dr != nullptr), "bn bwd: residual tensors missing");
+  // dr (= dz) may be omitted with the mask: the residual's consumer then reads dy and the mask itself
+  REQUIRE(res_mode != 2 || mask != nullptr || (r != nullptr && dr != nullptr), "bn bwd: residual tensors missing");
   REQUIRE(!mask || (relu && res_mode == 2), "bn bwd: the stored mask is for ReLU(bn + r)");
   REQUIRE(res_mode != 2 || relu, "bn bwd: a residual join without ReLU is not supported");
   hipStream_t st = (hipStream_t)stream;

@@ -82,6 +82,12 @@ struct GemmArgs {
   const float* bnb_gamma;
   const float* bnb_beta;
   float2* bnb_part;
+  // masked accumulation source (beta != 0, bf16 output): C = alpha A B + beta * (beta_src * mask) instead of
+  // beta * C_old -- the residual gradient dout * [ReLU(bn3 + r) > 0] of a bottleneck, read from dout and the bn3
+  // forward's bit mask (bit j of byte e / 8: element e of beta_src's [M][ldc] layout) so bn3's backward never writes
+  // it out.  k_gemm_stream applies it in the epilogue; other kernels get a masked copy into C first (dca_ops_gemm).
+  const void* beta_src;
+  const unsigned char* beta_mask;
 };
 
 __device__ __forceinline__ float amax_scale(const unsigned* a) {
@@ -1279,6 +1285,12 @@ __global__ void __launch_bounds__(ST_NT, 2) k_gemm_stream(GemmArgs g) {
       g.C, (short)0, (int)((long long)g.M * g.ldc * 2), 0x00020000);
   const __amdgpu_buffer_rsrc_t srs = __builtin_amdgcn_make_buffer_rsrc(
       (void*)g.col_stats, (short)0, g.col_stats ? (int)((long long)nstat * g.N * 8) : 0, 0x00020000);
+  // beta != 0: C_old from C, or (masked source) from beta_src with the bit mask
+  const bool mold = !CONV && g.beta_mask != nullptr;  // (plain GEMMs only: the launcher never sends it a conv)
+  const __amdgpu_buffer_rsrc_t ors = __builtin_amdgcn_make_buffer_rsrc(
+      mold ? (void*)g.beta_src : g.C, (short)0, (int)((long long)g.M * g.ldc * 2), 0x00020000);
+  const __amdgpu_buffer_rsrc_t mrs = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)g.beta_mask, (short)0, mold ? (int)((long long)g.M * g.ldc / 8) : 0, 0x00020000);
   const unsigned lda2 = (unsigned)g.lda * 2u, ldb2 = (unsigned)g.ldb * 2u;
   const int cpt = CONV ? g.cC / 64 : 1;  // K-steps per tap
   const float inv_wo = CONV ? 1.f / (float)g.cWo : 0.f, inv_ho = CONV ? 1.f / (float)g.cHo : 0.f;
@@ -1381,6 +1393,7 @@ __global__ void __launch_bounds__(ST_NT, 2) k_gemm_stream(GemmArgs g) {
   typedef float f2 __attribute__((ext_vector_type(2)));
   typedef __bf16 bf2 __attribute__((ext_vector_type(2)));
   st_v4u old[8];  // beta != 0: this tile's C_old rows (lane (q, j): row 16 m + j, columns c0 .. c0 + 4 NF - 1)
+  unsigned omk[8];  // masked source: the mask byte of those columns (c0 % 8 == 0 for NF = 2, 0 or 4 for NF = 1)
   auto load_old = [&](int tm, int tn) {
     const int c0 = tn * TN + WN * wn + 4 * NF * q;
 #pragma unroll
@@ -1388,10 +1401,18 @@ __global__ void __launch_bounds__(ST_NT, 2) k_gemm_stream(GemmArgs g) {
       const int row = tm * TM + GBM * wm + 16 * m + j;
       const unsigned o = row < g.M ? ((unsigned)row * (unsigned)g.ldc + c0) * 2u : OOB;
       if constexpr (NF == 2) {
-        old[m] = __builtin_amdgcn_raw_buffer_load_b128(crs, o, 0, 0);
+        old[m] = __builtin_amdgcn_raw_buffer_load_b128(ors, o, 0, 0);
       } else {
-        const st_v2u v = __builtin_amdgcn_raw_buffer_load_b64(crs, o, 0, 0);
+        const st_v2u v = __builtin_amdgcn_raw_buffer_load_b64(ors, o, 0, 0);
         old[m] = st_v4u{v[0], v[1], 0u, 0u};
+      }
+    }
+    if (mold) {  // issued after the 8 C_old loads: the waits below count 16
+#pragma unroll
+      for (int m = 0; m < 8; ++m) {
+        const int row = tm * TM + GBM * wm + 16 * m + j;
+        const unsigned o = row < g.M ? ((unsigned)row * (unsigned)g.ldc + c0) >> 3 : OOB;
+        omk[m] = __builtin_amdgcn_raw_buffer_load_b8(mrs, o, 0, 0);
       }
     }
   };
@@ -1421,8 +1442,14 @@ __global__ void __launch_bounds__(ST_NT, 2) k_gemm_stream(GemmArgs g) {
       for (int e = 0; e < NP; ++e) {  // columns 2e, 2e + 1 = fragment e >> 1, elements 2 (e & 1) + {0, 1}
         const f32x4& a = acc[m][e >> 1];
         f2 x = f2{a[2 * (e & 1)], a[2 * (e & 1) + 1]} * alpha + b2[e];
-        if constexpr (BETA)
-          x += f2{__uint_as_float(old[m][e] << 16), __uint_as_float(old[m][e] & 0xffff0000u)} * g.beta;
+        if constexpr (BETA) {
+          f2 ov = f2{__uint_as_float(old[m][e] << 16), __uint_as_float(old[m][e] & 0xffff0000u)};
+          if (mold) {
+            const unsigned b = omk[m] >> ((c0 & 7) + 2 * e);
+            ov = f2{(b & 1u) ? ov[0] : 0.f, (b & 2u) ? ov[1] : 0.f};
+          }
+          x += ov * g.beta;
+        }
         pk[e] = __builtin_bit_cast(unsigned, __builtin_convertvector(x, bf2));
         // statistics of the values as stored (bf16)
         f2 d = f2{__uint_as_float(pk[e] << 16), __uint_as_float(pk[e] & 0xffff0000u)} - sh2[e];
@@ -1470,9 +1497,11 @@ __global__ void __launch_bounds__(ST_NT, 2) k_gemm_stream(GemmArgs g) {
         load_old(tm, tn);
         if (s + 1 < steps) {
           issue(s + 1);
-          wait_vmcnt<8 + NI>();
+          if (mold) wait_vmcnt<16 + NI>();
+          else wait_vmcnt<8 + NI>();
         } else {
-          wait_vmcnt<8>();
+          if (mold) wait_vmcnt<16>();
+          else wait_vmcnt<8>();
         }
       } else if (s + 1 < steps) {
         issue(s + 1);
@@ -1504,6 +1533,24 @@ __global__ void __launch_bounds__(ST_NT, 2) k_gemm_stream(GemmArgs g) {
 // thousands of slabs of a small weight gradient are read by many threads with 256-B row segments.
 // With wperm_T > 0 the column is remapped to torch's weight layout (see GemmArgs) and padded channels dropped.
 constexpr int RED_EL = 64, RED_LANES = 4;
+// Masked accumulation source for the GEMM kernels without the epilogue form (dca_ops_gemm): C[m][n] =
+// beta_src[m][n] * bit(m * ldc + n) over the M x N output (bf16), before a plain beta = 1 GEMM.
+__global__ void __launch_bounds__(256) k_masked_copy(const unsigned short* __restrict__ src,
+                                                     const unsigned char* __restrict__ mk,
+                                                     unsigned short* __restrict__ dst, int M, int N, int ldc) {
+  const long total = (long)M * (N / 8);
+  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < total; i += (long)gridDim.x * 256) {
+    const long row = i / (N / 8), c8 = (i % (N / 8)) * 8, o = row * ldc + c8;
+    const uint4 v = *(const uint4*)(src + o);
+    const unsigned b = mk[o >> 3];
+    unsigned w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+      w[k] = ((b >> (2 * k)) & 1u ? (w[k] & 0xffffu) : 0u) | ((b >> (2 * k + 1)) & 1u ? (w[k] & 0xffff0000u) : 0u);
+    *(uint4*)(dst + o) = uint4{w[0], w[1], w[2], w[3]};
+  }
+}
+
 __global__ void __launch_bounds__(256) k_gemm_splitk_reduce(GemmArgs g) {
   __shared__ float red[RED_LANES][RED_EL];
   const size_t total = (size_t)g.M * g.N;

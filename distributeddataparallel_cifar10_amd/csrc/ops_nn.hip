@@ -503,7 +503,9 @@ __global__ void __launch_bounds__(256) k_bn_bwd_apply(const bf16_t* __restrict__
         d[j] = ca[j] * dz + cb[j] * xv[j] + cd[j];
       }
       bn_st16<NT>(dx + o, pack8(d));
-      if constexpr (MODE == BWD_RES || MODE == BWD_MASK) bn_st16<NT>(dr + o, pack8(rv));
+      if constexpr (MODE == BWD_RES) bn_st16<NT>(dr + o, pack8(rv));
+      if constexpr (MODE == BWD_MASK)
+        if (dr) bn_st16<NT>(dr + o, pack8(rv));  // (none: the consumer takes dout and the mask instead)
     }
   }
 }

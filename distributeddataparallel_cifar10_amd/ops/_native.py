@@ -13,7 +13,7 @@ import torch
 
 from .. import build as _build
 
-ABI_VERSION = 8
+ABI_VERSION = 9
 _lock = threading.Lock()
 _lib = None
 
@@ -34,6 +34,7 @@ class GemmArgs(ctypes.Structure):
         ("stages", c_int), ("orow_S", c_int), ("orow_ph", c_int), ("orow_pw", c_int), ("orow_H", c_int),
         ("orow_W", c_int), ("orow_Ho", c_int), ("orow_Wo", c_int), ("bnb_x", c_void_p), ("bnb_stats", c_void_p),
         ("bnb_gamma", c_void_p), ("bnb_beta", c_void_p), ("bnb_part", c_void_p),
+        ("beta_src", c_void_p), ("beta_mask", c_void_p),
     ]
 
 

@@ -39,7 +39,8 @@ def gemm(a: torch.Tensor, b: torch.Tensor, *, ta: bool = False, tb: bool = False
          beta: float = 0.0, splits: int = 0, alpha_dev: Optional[torch.Tensor] = None, conv: int = 0,
          geom=None, col_stats: Optional[torch.Tensor] = None, stats_shift: Optional[torch.Tensor] = None,
          mnk=None, amax_a: Optional[torch.Tensor] = None, amax_b: Optional[torch.Tensor] = None,
-         wperm=None, orow=None, bnb=None) -> torch.Tensor:
+         wperm=None, orow=None, bnb=None, beta_src: Optional[torch.Tensor] = None,
+         beta_mask: Optional[torch.Tensor] = None) -> torch.Tensor:
     """C[M,N] = alpha * A(m,k) B(n,k) (+bias) (+beta*out) (ReLU).
 
     A is [M,K] (ta=False) or [K,M] (ta=True); B is [N,K] (tb=False) or [K,N] (tb=True).  bf16 operands, or
@@ -115,6 +116,11 @@ def gemm(a: torch.Tensor, b: torch.Tensor, *, ta: bool = False, tb: bool = False
         bx, bst, bga, bbe, bpart = bnb
         args.bnb_x, args.bnb_stats, args.bnb_gamma, args.bnb_beta, args.bnb_part = (
             bx.data_ptr(), bst.data_ptr(), bga.data_ptr(), bbe.data_ptr(), bpart.data_ptr())
+    if beta_mask is not None:  # C = A B + beta * (beta_src * mask bits): beta_src has C's [M, ldc] layout
+        if beta_src is None or beta_src.dtype != torch.bfloat16 or not beta_src.is_contiguous() \
+                or beta_src.numel() != M * Nn or beta_mask.numel() * 8 != M * Nn or out.stride(0) != Nn:
+            raise ValueError("gemm: masked accumulation source must be a contiguous bf16 [M, N] tensor + M*N/8 bytes")
+        args.beta_src, args.beta_mask = beta_src.data_ptr(), beta_mask.data_ptr()
     N.check(N.lib().dca_ops_gemm(args, N.stream(a.device)), "gemm")
     return out
 
@@ -502,9 +508,27 @@ class GradJoin:
     first producer writes the gradient buffer and returns None; later producers accumulate into it inside their
     own kernel (GEMM beta = 1, col2im accumulate); the last one returns the sum."""
 
-    def __init__(self, n: int = 2):
+    def __init__(self, n: int = 2, defer_ok: bool = False):
         self.buf = None
         self.left = n
+        # defer_ok: the first producer may register (dout, ReLU bit mask) instead of writing dout * mask; the
+        # next producer (a 1x1 conv's dgrad GEMM) then takes it as its masked accumulation source
+        self.defer_ok = defer_ok
+        self.masked = None
+
+    def defer_masked(self, src, mask):
+        """First producer: the gradient is src * mask (bits); nothing written.  Returns None (not the last)."""
+        if self.buf is not None or self.masked is not None or not self.defer_ok:
+            raise RuntimeError("GradJoin: a masked contribution must come first, once, and be allowed")
+        self.masked = (src, mask)
+        self.left -= 1
+        if self.left <= 0:
+            raise RuntimeError("GradJoin: the masked contribution needs a later producer")
+        return None
+
+    def take_masked(self):
+        m, self.masked = self.masked, None
+        return m
 
     def contribute(self, t):
         """Register a producer's result (the buffer itself when it accumulated); returns what that producer
@@ -601,6 +625,13 @@ def _conv_fwd(x, w, b, stride, pad, relu, fp8, col_stats=None, shift=None, fp8_s
     return y.view(g.N, g.Ho, g.Wo, co), st
 
 
+def _unmask(src: torch.Tensor, mask: torch.Tensor) -> torch.Tensor:
+    """src * mask bits (bit j of byte e / 8 = element e) as a new bf16 tensor: the masked-copy kernel through a
+    zero-K-free path (a 1x1 GEMM would need weights), used only when a deferred join meets a non-1x1 consumer."""
+    bits = (mask.view(-1, 1) >> torch.arange(8, device=mask.device, dtype=torch.uint8)) & 1
+    return (src.reshape(-1) * bits.view(-1).to(src.dtype)).view_as(src).contiguous()
+
+
 def _conv_bwd(dy, st, need_x: bool, need_w: bool, sink=None, x_join: Optional[GradJoin] = None, bnb=None):
     """(dx, dw) of a conv from dY [N,Ho,Wo,Cout] (any dtype) and the forward state.  The weight gradient is
     written by the GEMM's reduce pass directly in torch's [Cout, Cin, KH, KW] layout -- into ``sink`` (a flat
@@ -616,9 +647,13 @@ def _conv_bwd(dy, st, need_x: bool, need_w: bool, sink=None, x_join: Optional[Gr
     cols = st["cols"]
     if need_x:
         acc = x_join.buf if x_join is not None else None  # accumulate into the other consumer's gradient
-        beta = 1.0 if acc is not None else 0.0
+        masked = x_join.take_masked() if x_join is not None and x_join.masked is not None else None
+        if masked is not None and not (cols is not None and cols.data_ptr() == st["x"].data_ptr()):
+            acc = _unmask(*masked)  # (only the 1x1 dgrad below takes the masked source in its epilogue)
+            masked = None
+        beta = 1.0 if acc is not None or masked is not None else 0.0
         dst2 = acc.view(g.N * g.H * g.W, g.C) if acc is not None else None
-        if acc is not None or bnb is None or not bnb.ready or g.C % 8:
+        if acc is not None or masked is not None or bnb is None or not bnb.ready or g.C % 8:
             bnb = None
 
         def bnb_args(rows, off):  # this GEMM's slice of the link's partial rows
@@ -630,10 +665,13 @@ def _conv_bwd(dy, st, need_x: bool, need_w: bool, sink=None, x_join: Optional[Gr
         if cols is not None and cols.data_ptr() == st["x"].data_ptr():  # 1x1 / stride 1: dX = dY . W
             if bnb is not None:
                 bnb.rows_total = (M + 127) // 128
+            msrc, mbits = (masked[0].view(M, g.C), masked[1]) if masked is not None else (None, None)
             if packed is not None and packed["dgrad"] is not None:  # W^T [Cin, Cout] from the pack: plain NT
-                dx = gemm(dyb, packed["dgrad"], out_dtype=torch.bfloat16, out=dst2, beta=beta, bnb=bnb_args(M, 0))
+                dx = gemm(dyb, packed["dgrad"], out_dtype=torch.bfloat16, out=dst2, beta=beta, bnb=bnb_args(M, 0),
+                          beta_src=msrc, beta_mask=mbits)
             else:
-                dx = gemm(dyb, st["wm"], tb=True, out_dtype=torch.bfloat16, out=dst2, beta=beta, bnb=bnb_args(M, 0))
+                dx = gemm(dyb, st["wm"], tb=True, out_dtype=torch.bfloat16, out=dst2, beta=beta, bnb=bnb_args(M, 0),
+                          beta_src=msrc, beta_mask=mbits)
             dx = dx.view(g.N, g.H, g.W, g.C)
         elif g.stride == 1 and co % 8 == 0 and kh == kw and g.pad <= kh - 1 and g.C == ci:
             # stride 1: dX = conv(dY, W flipped, ci<->co, pad KH-1-pad), implicit GEMM (no col2im)
@@ -686,7 +724,7 @@ def _conv_bwd(dy, st, need_x: bool, need_w: bool, sink=None, x_join: Optional[Gr
         if bnb is not None:
             bnb.nparts = bnb.rows_total
         if x_join is not None:
-            dx = x_join.contribute(dx if acc is None else acc)
+            dx = x_join.contribute(dx if acc is None else acc)  # (a masked source: dx is the fresh sum)
     if need_w:
         dst = sink if sink is not None else torch.empty(co, ci, kh, kw, dtype=torch.float32, device=dy.device)
         beta = 1.0 if sink is not None else 0.0
@@ -792,14 +830,19 @@ class _ConvBNAct(torch.autograd.Function):
         sw, sg, sb = ctx.sinks if ctx.sinks is not None else (None, None, None)
         link_out, link_in = ctx.links
         parts = link_out.take() if link_out is not None else (None, 0)
+        x_join, r_join = ctx.joins
+        defer = r_join is not None and mask is not None and r_join.defer_ok and ctx.res_mode == 2
+        dout = dout.to(torch.bfloat16).contiguous()
         dy_conv, dr, dgamma, dbeta = _bn_backward(dout, y, r, gamma, beta, stats, ctx.relu, ctx.res_mode,
                                                   dgamma_out=sg[0] if sg else None, dbeta_out=sb[0] if sb else None,
-                                                  parts=parts if parts[0] is not None else None, mask=mask)
+                                                  parts=parts if parts[0] is not None else None, mask=mask,
+                                                  want_dr=not defer)
         if sg:
             sg[1]()
             sb[1]()
-        x_join, r_join = ctx.joins
-        if r_join is not None and dr is not None:  # the identity gradient seeds the block input's shared buffer
+        if defer:  # the identity gradient dout * mask is taken by conv1's dgrad epilogue: never written
+            dr = r_join.defer_masked(dout, mask)
+        elif r_join is not None and dr is not None:  # the identity gradient seeds the block input's shared buffer
             dr = r_join.contribute(dr)
         s2d = (ctx.st.get("packed") or {}).get("s2d")
         dx, dw = _conv_bwd(dy_conv, ctx.st, ctx.needs_input_grad[0], ctx.needs_input_grad[1] or sw is not None,
@@ -896,7 +939,7 @@ class _BatchNormAct(torch.autograd.Function):
 
 
 def _bn_backward(dy, x, r, gamma, beta, stats, relu, res_mode, dgamma_out=None, dbeta_out=None, parts=None,
-                 mask=None):
+                 mask=None, want_dr: bool = True):
     """(dx, dr, dgamma, dbeta) of the fused BN + ReLU + residual.  dgamma_out / dbeta_out: flat gradient views
     to accumulate into (then dgamma / dbeta are returned as None).  mask: the forward's ReLU bit mask (res_mode 2;
     r is then not needed)."""
@@ -909,7 +952,8 @@ def _bn_backward(dy, x, r, gamma, beta, stats, relu, res_mode, dgamma_out=None, 
     dgamma = dgamma_out if direct else torch.empty(C, dtype=torch.float32, device=x.device)
     dbeta = dbeta_out if direct else torch.empty_like(dgamma)
     dx = torch.empty_like(x)
-    dr = torch.empty_like(x) if res_mode == 2 else None
+    # without dr (mask given): the residual's consumer reads dy and the mask itself (GradJoin.defer_masked)
+    dr = torch.empty_like(x) if res_mode == 2 and (want_dr or mask is None) else None
     if parts is not None:  # statistics already summed per tile by the dgrad GEMM that produced dy (BnLink)
         if not relu or res_mode != 0:
             raise ValueError("bn backward: fused statistics are for BN + ReLU without a residual")

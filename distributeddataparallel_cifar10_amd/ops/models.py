@@ -29,6 +29,9 @@ import torch.nn as nn
 
 from . import functional as F
 
+# DCA_OPS_MASKED_JOIN=0: bn3's backward writes the identity gradient dout * mask as before (A/B comparisons)
+_MASKED_JOIN = os.environ.get("DCA_OPS_MASKED_JOIN", "1") != "0"
+
 
 def _is_netresdeep(m: nn.Module) -> bool:
     return hasattr(m, "resblocks") and hasattr(m, "fc1") and hasattr(m, "fc2")
@@ -151,7 +154,13 @@ class OpsModel(nn.Module):
         for i, b in enumerate(blocks):
             nxt = blocks[i + 1].conv1 if i + 1 < len(blocks) else None
             # the block input feeds conv1 and the identity / downsample path: one shared gradient buffer
-            join = F.GradJoin(2)
+            c1 = b.conv1
+            # identity blocks whose conv1 dgrad runs on the stream GEMM (1x1, K = conv1 width <= 128, >= 16384
+            # pixels): bn3's backward skips writing dout * mask, the dgrad epilogue reads dout and the mask
+            defer = (b.downsample is None and _MASKED_JOIN and tuple(c1.kernel_size) == (1, 1)
+                     and tuple(c1.stride) == (1, 1) and c1.out_channels <= 128
+                     and h.shape[0] * h.shape[1] * h.shape[2] >= 16384)
+            join = F.GradJoin(2, defer_ok=defer)
             if b.downsample is None:
                 idt = h
             else:

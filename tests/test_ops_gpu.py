@@ -299,6 +299,45 @@ def test_ops_resnet_step(gpu, fp8):
     assert not bad, bad
 
 
+@pytest.mark.parametrize("M,N,K", [(20000, 256, 64), (16384, 128, 128), (777, 256, 64), (20000, 256, 256)])
+def test_gemm_masked_accumulation_source(gpu, M, N, K):
+    """C = A B^T + src * mask bits: in the stream GEMM's epilogue (K <= 128, M >= 16384) or through the masked
+    copy before the other kernels (small M, K = 256); against fp32 PyTorch."""
+    from distributeddataparallel_cifar10_amd.ops.functional import gemm
+    g = torch.Generator(device=gpu).manual_seed(M + K)
+    a = _bf(torch.randn(M, K, device=gpu, generator=g))
+    b = _bf(torch.randn(N, K, device=gpu, generator=g))
+    src = _bf(torch.randn(M, N, device=gpu, generator=g))
+    mask = torch.randint(0, 256, (M * N // 8,), device=gpu, generator=g, dtype=torch.int32).to(torch.uint8)
+    bits = ((mask.view(-1, 1).int() >> torch.arange(8, device=gpu)) & 1).view(M, N).float()
+    out = gemm(a, b, out_dtype=torch.bfloat16, beta=1.0, beta_src=src, beta_mask=mask)
+    ref = a.float() @ b.float().t() + src.float() * bits
+    assert _rel(out.float(), ref) < 1e-2
+    assert torch.equal(src, src.clone())  # the source is read, never written
+
+
+def test_ops_resnet_masked_identity_gradient_bitwise(gpu, monkeypatch):
+    """Identity blocks whose conv1 dgrad runs on the stream GEMM take the residual gradient dout * mask in that
+    GEMM's epilogue instead of bn3's backward writing it: every gradient is bitwise the one of the written path
+    (the masked value is exact in bf16 either way)."""
+    import copy
+    from distributeddataparallel_cifar10_amd.models.resnet50 import ResNet
+    from distributeddataparallel_cifar10_amd.ops import OpsModel, cross_entropy
+    from distributeddataparallel_cifar10_amd.ops import models as M_
+    torch.manual_seed(0)
+    net = ResNet([2, 1, 1, 1], num_classes=10, zero_init_residual=False).to(gpu)
+    other = copy.deepcopy(net)
+    x = torch.randn(8, 3, 192, 192, device=gpu)  # layer 1: 8 x 48 x 48 = 18432 pixels (stream GEMM eligible)
+    y = torch.randint(0, 10, (8,), device=gpu)
+    grads = []
+    for m, on in ((net, True), (other, False)):
+        monkeypatch.setattr(M_, "_MASKED_JOIN", on)
+        cross_entropy(OpsModel(m)(x), y).backward()
+        grads.append([p.grad.clone() for p in m.parameters()])
+    for (n, _), g1, g2 in zip(net.named_parameters(), *grads):
+        assert torch.equal(g1, g2), n
+
+
 def test_ops_bn_backward_stats_fused_in_dgrad(gpu, monkeypatch):
     """bn1 -> conv2 and bn2 -> conv3 of every bottleneck: the BN-backward statistics summed in conv2's / conv3's
     dgrad GEMM epilogue (BnLink, DCA_OPS_BNB_FUSE=1) give the same gradients as the separate statistics pass
