@@ -635,7 +635,9 @@ int dca_ops_bn_bwd(const void* dy, const void* x, const void* r, const float* st
   REQUIRE(C % 8 == 0, "bn: C must be a multiple of 8");
   // dr (= dz) may be omitted with the mask: the residual's consumer then reads dy and the mask itself
   REQUIRE(res_mode != 2 || mask != nullptr || (r != nullptr && dr != nullptr), "bn bwd: residual tensors missing");
-  REQUIRE(!mask || (relu && res_mode == 2), "bn bwd: the stored mask is for ReLU(bn + r)");
+  // mask: ReLU(bn + r)'s own stored mask (relu, res_mode 2), or -- a plain BN whose output is that r (ResNet
+  // downsample branch: no relu, res_mode 0) -- the consumer's mask applied to the consumer's dout, passed as dy
+  REQUIRE(!mask || (relu && res_mode == 2) || (!relu && res_mode == 0), "bn bwd: unsupported mask use");
   REQUIRE(res_mode != 2 || relu, "bn bwd: a residual join without ReLU is not supported");
   hipStream_t st = (hipStream_t)stream;
   const int nparts = (int)((M + BN_ROWS - 1) / BN_ROWS);

@@ -407,7 +407,7 @@ __global__ void __launch_bounds__(256) k_bn_bwd_stats(const bf16_t* __restrict__
             d = z > 0.f ? d : 0.f;
           }
           s[j] += d;
-          q[j] += d * xh;
+          q[j] = __builtin_fmaf(d, xh, q[j]);  // explicit: the same rounding in every MODE instantiation
         }
       }
     }
@@ -500,7 +500,9 @@ __global__ void __launch_bounds__(256) k_bn_bwd_apply(const bf16_t* __restrict__
           dz = z > 0.f ? dz : 0.f;
         }
         rv[j] = dz;
-        d[j] = ca[j] * dz + cb[j] * xv[j] + cd[j];
+        // explicit FMAs: every MODE instantiation rounds alike (a select folded into a product can otherwise be
+        // contracted differently, so BWD_MASK on dout and BWD_PLAIN on the written dout * mask differed in dx)
+        d[j] = __builtin_fmaf(ca[j], dz, __builtin_fmaf(cb[j], xv[j], cd[j]));
       }
       bn_st16<NT>(dx + o, pack8(d));
       if constexpr (MODE == BWD_RES) bn_st16<NT>(dr + o, pack8(rv));

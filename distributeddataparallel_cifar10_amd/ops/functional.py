@@ -23,6 +23,7 @@ from . import _native as N
 # at ResNet-50 batch 256 (8,417 vs 8,755 img/s: the epilogue's extra x reads and registers cost the dgrad GEMMs
 # more than the ~0.84 ms of statistics passes it removes); DCA_OPS_BNB_FUSE=1 turns it on
 _BNB_FUSE = os.environ.get("DCA_OPS_BNB_FUSE", "0") == "1"
+_BWD_TRACE = None  # diagnostics: a list to record the order of the fused conv-BN backward calls
 
 
 def _dev_check(*ts):
@@ -543,6 +544,16 @@ class GradJoin:
         return self.buf if self.left == 0 else None
 
 
+class ResidualLink:
+    """ReLU(bn3 + r) of a downsample bottleneck -> the downsample branch that produced r.  bn3's backward leaves
+    (dout, its forward ReLU bit mask) here and returns no gradient for r, so dL/dr = dout * mask is never written;
+    the downsample BN's backward (called by autograd with no gradient: its forward disables grad materialisation)
+    reads dout and the mask instead (k_bn_bwd_* in BWD_MASK mode)."""
+
+    def __init__(self):
+        self.dout = self.mask = None
+
+
 class Fp8Delayed:
     """Delayed-scaling fp8 state of ONE activation tensor feeding ONE fp8 GEMM (Transformer-Engine style).
 
@@ -787,7 +798,10 @@ class _ConvBNAct(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, w, r, gamma, beta, running_mean, running_var, stride, pad, eps, momentum, relu, res_mode, fp8,
-                fp8_state, emit, packed, sinks, x_join, r_join, link_out, link_in):
+                fp8_state, emit, packed, sinks, x_join, r_join, link_out, link_in, res_in):
+        ctx.res_in = res_in
+        if res_in is not None:  # the consumer may hand this output's gradient over res_in instead of autograd
+            ctx.set_materialize_grads(False)
         co = w.shape[0]
         wg, stride, pad = _s2d_args(w, stride, pad, packed)
         g = _geom(x, wg, stride, pad)
@@ -827,20 +841,34 @@ class _ConvBNAct(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dout):
         y, r, gamma, beta, stats, mask = ctx.saved_tensors
+        in_mask = None
+        if dout is None:  # (res_in: grad materialisation is off) the consumer's bn3 left dout and its mask
+            rl = ctx.res_in
+            if rl is None or rl.dout is None:
+                ctx.st = ctx.sinks = ctx.joins = ctx.links = ctx.res_in = None
+                return (None,) * 23
+            dout, in_mask, rl.dout, rl.mask = rl.dout, rl.mask, None, None
+        if _BWD_TRACE is not None:
+            _BWD_TRACE.append((tuple(y.shape), in_mask is not None))
         sw, sg, sb = ctx.sinks if ctx.sinks is not None else (None, None, None)
         link_out, link_in = ctx.links
         parts = link_out.take() if link_out is not None else (None, 0)
         x_join, r_join = ctx.joins
-        defer = r_join is not None and mask is not None and r_join.defer_ok and ctx.res_mode == 2
+        res_link = isinstance(r_join, ResidualLink) and mask is not None and ctx.res_mode == 2
+        defer = (not res_link and r_join is not None and mask is not None and r_join.defer_ok
+                 and ctx.res_mode == 2)
         dout = dout.to(torch.bfloat16).contiguous()
         dy_conv, dr, dgamma, dbeta = _bn_backward(dout, y, r, gamma, beta, stats, ctx.relu, ctx.res_mode,
                                                   dgamma_out=sg[0] if sg else None, dbeta_out=sb[0] if sb else None,
-                                                  parts=parts if parts[0] is not None else None, mask=mask,
-                                                  want_dr=not defer)
+                                                  parts=parts if parts[0] is not None else None,
+                                                  mask=mask if in_mask is None else in_mask,
+                                                  want_dr=not (defer or res_link))
         if sg:
             sg[1]()
             sb[1]()
-        if defer:  # the identity gradient dout * mask is taken by conv1's dgrad epilogue: never written
+        if res_link:  # dL/dr = dout * mask goes to the downsample branch through the link: never written
+            r_join.dout, r_join.mask, dr = dout, mask, None
+        elif defer:  # the identity gradient dout * mask is taken by conv1's dgrad epilogue: never written
             dr = r_join.defer_masked(dout, mask)
         elif r_join is not None and dr is not None:  # the identity gradient seeds the block input's shared buffer
             dr = r_join.contribute(dr)
@@ -861,15 +889,16 @@ class _ConvBNAct(torch.autograd.Function):
                 dw = out
         if sw:
             sw[1]()
-        ctx.st = ctx.sinks = ctx.joins = ctx.links = None
+        ctx.st = ctx.sinks = ctx.joins = ctx.links = ctx.res_in = None
         return (dx, dw, dr, dgamma, dbeta, None, None, None, None, None, None, None, None, None, None, None, None, None,
-                None, None, None, None)
+                None, None, None, None, None)
 
 
 def conv_bn_act(x, conv: torch.nn.Conv2d, bn: torch.nn.BatchNorm2d, r=None, relu=True, fp8=False, res_mode=None,
                 fp8_state: Optional[Fp8Delayed] = None, emit: Optional[Fp8Delayed] = None, packed=None,
                 direct_grads: bool = False, x_join: Optional[GradJoin] = None, r_join: Optional[GradJoin] = None,
-                link_out: Optional[BnLink] = None, link_in: Optional[BnLink] = None):
+                link_out: Optional[BnLink] = None, link_in: Optional[BnLink] = None,
+                res_in: Optional[ResidualLink] = None):
     """act(bn(conv(x))) for NHWC bf16 x, conv without bias (BN in eval mode: inference under no_grad, running
     statistics); with a residual r: res_mode 2 (default,
     ResNet: act(bn + r)) or 1 (NetResDeep: act(bn) + r).  fp8: forward GEMM in fp8 e4m3 (fp8_state: this conv's
@@ -903,7 +932,8 @@ def conv_bn_act(x, conv: torch.nn.Conv2d, bn: torch.nn.BatchNorm2d, r=None, relu
                             conv.padding[0], bn.eps, momentum, relu, res_mode, fp8, fp8_state, emit, packed, sinks,
                             x_join if torch.is_grad_enabled() else None, r_join if torch.is_grad_enabled() else None,
                             link_out if torch.is_grad_enabled() and _BNB_FUSE else None,
-                            link_in if torch.is_grad_enabled() and _BNB_FUSE else None)
+                            link_in if torch.is_grad_enabled() and _BNB_FUSE else None,
+                            res_in if torch.is_grad_enabled() else None)
 
 
 def conv2d(x, w, b=None, stride=1, pad=0, relu=False, fp8=False):

@@ -31,6 +31,7 @@ from . import functional as F
 
 # DCA_OPS_MASKED_JOIN=0: bn3's backward writes the identity gradient dout * mask as before (A/B comparisons)
 _MASKED_JOIN = os.environ.get("DCA_OPS_MASKED_JOIN", "1") != "0"
+_RES_LINK = os.environ.get("DCA_OPS_RES_LINK", "1") != "0"  # downsample blocks: the residual gradient over a link
 
 
 def _is_netresdeep(m: nn.Module) -> bool:
@@ -133,12 +134,12 @@ class OpsModel(nn.Module):
         return self._fp8.setdefault(id(conv), F.Fp8Delayed())
 
     def _conv_bn(self, h, conv, bn, relu=True, r=None, consumer=None, x_join=None, r_join=None, link_out=None,
-                 link_in=None):
+                 link_in=None, res_in=None):
         # every ResNet conv / BN is applied once per step: gradients may go straight into the flat DDP buffer
         return F.conv_bn_act(h, conv, bn, r=r, relu=relu, fp8=self._fp8_ok(conv), fp8_state=self._state(conv),
                              emit=self._state(consumer) if consumer is not None else None,
                              packed=self._pack.get(conv), direct_grads=True, x_join=x_join, r_join=r_join,
-                             link_out=link_out, link_in=link_in)
+                             link_out=link_out, link_in=link_in, res_in=res_in)
 
     def stem(self, h, conv, bn):
         """7x7/2 conv -> BN + ReLU -> 3x3/2 max pool (torchvision ResNet stem).  ``h`` is what ``begin`` returned:
@@ -161,17 +162,18 @@ class OpsModel(nn.Module):
                      and tuple(c1.stride) == (1, 1) and c1.out_channels <= 128
                      and h.shape[0] * h.shape[1] * h.shape[2] >= 16384)
             join = F.GradJoin(2, defer_ok=defer)
+            rlink = F.ResidualLink() if b.downsample is not None and _MASKED_JOIN and _RES_LINK else None
             if b.downsample is None:
                 idt = h
             else:
-                idt = self._conv_bn(h, b.downsample[0], b.downsample[1], relu=False, x_join=join)
+                idt = self._conv_bn(h, b.downsample[0], b.downsample[1], relu=False, x_join=join, res_in=rlink)
             # bn1 -> conv2 and bn2 -> conv3 are single-consumer BN + ReLU layers: their backward statistics come
             # out of conv2's / conv3's dgrad GEMM epilogue (BnLink)
             l1, l2 = F.BnLink(), F.BnLink()
             out = self._conv_bn(h, b.conv1, b.bn1, x_join=join, consumer=b.conv2, link_out=l1)
             out = self._conv_bn(out, b.conv2, b.bn2, consumer=b.conv3, link_in=l1, link_out=l2)
             h = self._conv_bn(out, b.conv3, b.bn3, relu=True, r=idt, consumer=nxt, link_in=l2,
-                              r_join=join if b.downsample is None else None)  # relu(bn3(conv3) + identity)
+                              r_join=join if b.downsample is None else rlink)  # relu(bn3(conv3) + identity)
         return h
 
     def head(self, h, fc):

@@ -318,8 +318,9 @@ def test_gemm_masked_accumulation_source(gpu, M, N, K):
 
 def test_ops_resnet_masked_identity_gradient_bitwise(gpu, monkeypatch):
     """Identity blocks whose conv1 dgrad runs on the stream GEMM take the residual gradient dout * mask in that
-    GEMM's epilogue instead of bn3's backward writing it: every gradient is bitwise the one of the written path
-    (the masked value is exact in bf16 either way)."""
+    GEMM's epilogue instead of bn3's backward writing it, and downsample blocks hand it to the downsample BN's
+    backward as (dout, mask) (ResidualLink): every gradient is bitwise the one of the written path (the masked
+    value is exact in bf16 either way; the BN backward kernels use explicit FMAs, so every mode rounds alike)."""
     import copy
     from distributeddataparallel_cifar10_amd.models.resnet50 import ResNet
     from distributeddataparallel_cifar10_amd.ops import OpsModel, cross_entropy
