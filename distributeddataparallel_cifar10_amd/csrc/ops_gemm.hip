@@ -87,7 +87,7 @@ struct GemmArgs {
   // forward's bit mask (bit j of byte e / 8: element e of beta_src's [M][ldc] layout) so bn3's backward never writes
   // it out.  k_gemm_stream applies it in the epilogue; other kernels get a masked copy into C first (dca_ops_gemm).
   const void* beta_src;
-  const unsigned char* beta_mask;
+  const uint8_t* beta_mask;
 };
 
 __device__ __forceinline__ float amax_scale(const unsigned* a) {

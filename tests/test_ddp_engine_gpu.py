@@ -189,7 +189,7 @@ def _xgmi_worker(rank, ws, port, dtype, persistent, q, comm="xgmi", own_device=F
 @pytest.mark.parametrize("ws,dtype,persistent,batch", [(2, "bf16", True, B), (4, "bf16", True, B),
                                                        (2, "fp32", True, B), (2, "fp32", False, B),
                                                        (3, "fp32", True, 8), (4, "fp32", True, 8),
-                                                       (8, "bf16", True, 8), (8, "fp32", True, 4),
+                                                       (8, "bf16", True, 4), (8, "fp32", True, 4),
                                                        (8, "bf16", False, 4)])
 def test_xgmi_allreduce_ranks_one_gpu(gpu, port, ws, dtype, persistent, batch):
     """ws=8 (the node's world size): the sliced engine's reduction exchange with 8 peers (rank_sum_n<8> in

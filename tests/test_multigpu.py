@@ -145,12 +145,14 @@ def test_bench_sweep_shared_gpu(gpu):
 
 def test_bench_driver_command_shared_gpu_8_ranks(gpu):
     """``python bench.py --gpus 8`` -- the driver's N=8 command -- rehearsed with all 8 ranks on GPU 0 at a per-rank
-    batch of 8 (each rank's step grid within its 256 / 8 CU budget): self-launch of 8 ranks, the engine's xGMI
-    exchange with 8 peers in every gradient segment, CC4 through 8 ranks, slowest-rank timing, fp32 second timing."""
-    lines = _bench(["bench.py", "--gpus", "8", "--batch", "8", "--steps", "32", "--warmup", "8"], shared=True,
+    batch of 4 (each rank's 16-workgroup step grid at half its 256 / 8 CU budget: at batch 8 the grid filled the
+    budget exactly and a rank's BN exchange once timed out while a peer's kernels held CUs): self-launch of 8 ranks,
+    the engine's xGMI exchange with 8 peers in every gradient segment, CC4 through 8 ranks, slowest-rank timing,
+    fp32 second timing."""
+    lines = _bench(["bench.py", "--gpus", "8", "--batch", "4", "--steps", "32", "--warmup", "8"], shared=True,
                    timeout=600)
     assert len(lines) == 1, lines
     out = lines[0]
     assert out["n_gpus"] == 8 and out["allreduce"] == "xgmi" and out["loss_finite"] and out["fp32_loss_finite"]
-    assert out["config"]["global_batch"] == 64 and out["config"]["parallelism"] == "dp8"
+    assert out["config"]["global_batch"] == 32 and out["config"]["parallelism"] == "dp8"
     assert len(out["per_rank_ms_per_step"]) == 8 and len(out["allreduce_us_per_step"]) == 8
