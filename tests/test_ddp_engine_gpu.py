@@ -194,8 +194,9 @@ def _xgmi_worker(rank, ws, port, dtype, persistent, q, comm="xgmi", own_device=F
 def test_xgmi_allreduce_ranks_one_gpu(gpu, port, ws, dtype, persistent, batch):
     """ws=8 (the node's world size): the sliced engine's reduction exchange with 8 peers (rank_sum_n<8> in
     seg_exchange), its fc-worker exchange with 8 peers (construction self-test, FusedDDPTrainer), CC4 through 8
-    ranks, the multi-kernel engine's k_xgmi_ar_sgd with 8 peers.  A per-rank batch of <= 8 keeps each rank's step
-    grid (32 workgroups, one CU each) within its 256 / 8 CU budget, and every rank has one hardware queue
+    ranks, the multi-kernel engine's k_xgmi_ar_sgd with 8 peers.  A per-rank batch of 4 keeps each rank's step
+    grid (16 workgroups, one CU each) at half its 256 / 8 CU budget (batch 8 fills it exactly: no slack while a
+    peer's kernels still hold CUs), and every rank has one hardware queue
     (tests/_ranks.py: with the default 4 per process, 8 processes oversubscribed the hardware scheduler)."""
     spawn_ranks(_xgmi_worker, ws, lambda r: (r, ws, port, dtype, persistent), dict(batch=batch))
 
