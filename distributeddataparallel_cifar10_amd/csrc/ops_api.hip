@@ -411,7 +411,8 @@ int dca_ops_gemm(const GemmArgs* a, void* stream) {
                                   (sk == 1 || (sk == 2 && getenv_stream_conv() && g.N == 128 && g.M >= 16384)))
                                : (g.conv == 0 && !g.ta && g.lda % 8 == 0 && g.lda >= g.K &&
                                   (g.N % 128 == 0 || g.N == 64) &&
-                                  (sk == 1 || (g.K <= 512 && g.M >= 16384 && (g.beta == 0.f || g.K <= 128))));
+                                  (sk == 1 || (g.K <= 512 && g.M >= 16384 &&
+                                               (g.beta == 0.f || g.K <= 128 || (g.beta_mask && g.K <= 256)))));
     const bool st_ok = sk != 0 && shape_ok && !g.fp8 && !g.tb && g.splits == 1 && g.wperm_T <= 0 && g.orow_S <= 0 &&
                        !(conv && g.beta_mask) &&
                        !g.bnb_part && !g.relu && g.out_bf16 && g.N % 64 == 0 && g.N <= 2048 && g.K % 64 == 0 &&

@@ -156,10 +156,12 @@ class OpsModel(nn.Module):
             nxt = blocks[i + 1].conv1 if i + 1 < len(blocks) else None
             # the block input feeds conv1 and the identity / downsample path: one shared gradient buffer
             c1 = b.conv1
-            # identity blocks whose conv1 dgrad runs on the stream GEMM (1x1, K = conv1 width <= 128, >= 16384
+            # identity blocks whose conv1 dgrad runs on the stream GEMM (1x1, K = conv1 width <= 256, >= 16384
             # pixels): bn3's backward skips writing dout * mask, the dgrad epilogue reads dout and the mask
+            # (layer 3, K = 256: 83.2 us on the stream kernel with the masked source against 83.8 us on glds with
+            # a written C_old, bench/gemm_beta_k256.py)
             defer = (b.downsample is None and _MASKED_JOIN and tuple(c1.kernel_size) == (1, 1)
-                     and tuple(c1.stride) == (1, 1) and c1.out_channels <= 128
+                     and tuple(c1.stride) == (1, 1) and c1.out_channels <= 256
                      and h.shape[0] * h.shape[1] * h.shape[2] >= 16384)
             join = F.GradJoin(2, defer_ok=defer)
             rlink = F.ResidualLink() if b.downsample is not None and _MASKED_JOIN and _RES_LINK else None
