@@ -49,6 +49,9 @@ def _args(argv=None):
     ap.add_argument("--engine", default="auto", choices=["auto", "persistent", "multikernel"])
     ap.add_argument("--allreduce", default="auto", choices=["auto", "xgmi", "rccl"],
                     help="gradient all-reduce for N>1: one-shot xGMI peer reads (default inside a node) or RCCL")
+    ap.add_argument("--loopback", action="store_true",
+                    help="--gpus 1 --allreduce xgmi: run the xGMI gradient exchange with the rank as its own only peer "
+                         "(protocol cost on one device; not the headline configuration)")
     ap.add_argument("--sweep", default=None, metavar="N1,N2,..",
                     help="run each N in a fresh spawned rank group; print per-N lines and a scaling summary")
     ap.add_argument("--no-fp32", action="store_true",
@@ -99,7 +102,7 @@ def run_rank(a) -> dict | None:
         persistent = None if a.engine == "auto" else a.engine == "persistent"
         trainer = FusedDDPTrainer(model, data, labels, batch_max=a.batch, lr=1e-2, dtype=dtype, rows=a.rows,
                                   max_indices=(a.warmup + a.steps) * a.batch, persistent=persistent,
-                                  comm=a.allreduce)
+                                  comm=a.allreduce, loopback=a.loopback)
         eng = trainer.engine
         eng.set_indices(order)
         eng.set_cursor(0)
@@ -148,7 +151,8 @@ def run_rank(a) -> dict | None:
         "allreduce": main_run["comm"],
         "per_rank_ms_per_step": [round(1e3 * p[0] / a.steps, 5) for p in per_rank],
         # exposed gradient-exchange wait per step, mean over the gradient segments (xGMI path only)
-        "allreduce_us_per_step": ([round(p[1], 2) for p in per_rank] if main_run["comm"] == "xgmi" else None),
+        "allreduce_us_per_step": ([round(p[1], 2) for p in per_rank] if main_run["comm"].startswith("xgmi")
+                                  else None),
         "data": "synthetic (CIFAR-10-shaped uint8 3x32x32, 50000 samples, random labels; random-init weights)",
         "config": {"model": "NetResDeep(n_chans1=32, n_blocks=10)", "global_batch": a.batch * world,
                    "per_rank_batch": a.batch, "seq_len": None, "image": "3x32x32",
@@ -233,6 +237,9 @@ def sweep(ns: list, argv: list) -> int:
 def main() -> int:
     argv = sys.argv[1:]
     a = _args(argv)
+    if a.loopback and (a.gpus != 1 or a.allreduce != "xgmi"):
+        print("bench.py: --loopback needs --gpus 1 --allreduce xgmi", file=sys.stderr)
+        return 2
     if a.sweep:
         rest, skip = [], False
         for x in argv:  # drop both "--sweep N1,N2" and "--sweep=N1,N2"

@@ -113,8 +113,10 @@ def compare_one_step(dtype: str, rows: int, B: int, graph: bool, seed: int = 0, 
     return out
 
 
-def trajectory(dtype: str, rows: int, B: int, steps: int, seed: int = 1, persistent: bool = False) -> dict:
-    """Multi-step loss trajectory + final params vs the oracle (graph mode)."""
+def trajectory(dtype: str, rows: int, B: int, steps: int, seed: int = 1, persistent: bool = False,
+               seed_epoch=None) -> dict:
+    """Multi-step loss trajectory + final params vs the oracle (graph mode).  seed_epoch: start the sliced engine's
+    device epoch there (e.g. EPOCH_WRAP - 3: the steps cross the wrap); the result then also says where it ended."""
     torch.manual_seed(seed)
     dev = torch.device("cuda", 0)
     ndata = B * steps
@@ -126,6 +128,8 @@ def trajectory(dtype: str, rows: int, B: int, steps: int, seed: int = 1, persist
     eng = NetResDeepEngine(model, data.to(dev), labels.to(dev), EngineConfig(
         batch_max=B, lr=1e-2, dtype=dtype, rows=rows, persistent=persistent))
     idx = torch.arange(ndata)
+    if seed_epoch is not None:
+        eng.set_epoch(int(seed_epoch))
     eng.set_indices(idx.numpy())
     eng.set_cursor(0)
     eng.read_loss(reset=True)
@@ -142,9 +146,10 @@ def trajectory(dtype: str, rows: int, B: int, steps: int, seed: int = 1, persist
     perr = max(rel(sd[k], rsd[k]) for k in keys)
     a = torch.cat([sd[k].detach().double().cpu().reshape(-1) for k in keys])
     b = torch.cat([rsd[k].detach().double().reshape(-1) for k in keys])
+    epoch_end = eng.epoch() if persistent else None
     eng.close()
     return {"losses_engine": losses_e, "losses_ref": losses_r, "max_param_rel_err": perr,
-            "param_rel_l2": ((a - b).norm() / b.norm()).item()}
+            "param_rel_l2": ((a - b).norm() / b.norm()).item(), "params": a, "epoch_end": epoch_end}
 
 
 def main():

@@ -44,6 +44,10 @@ def _args(argv=None):
                     help="1: each gradient bucket's SGD update runs right behind its all-reduce during the backward "
                          "(FlatSGD overlap=True; measured 4.6 %% slower on 1 GPU, where there is no all-reduce to hide "
                          "behind); 0: one SGD step after the backward")
+    ap.add_argument("--loopback", action="store_true",
+                    help="ops path, --gpus 1: every gradient bucket still runs the xGMI all-reduce kernel on the comm "
+                         "stream beside the backward, with the rank as its own only peer (the comm kernels' CU "
+                         "pressure measured on one device); reports allreduce_us_per_step")
     ap.add_argument("--infer", action="store_true",
                     help="inference (serving) throughput: eval-mode forward under no_grad, BN with the running "
                          "statistics (ops path: k_bn_eval_stats + k_bn_apply), no backward / optimizer")
@@ -89,7 +93,7 @@ def run_rank(a) -> None:
         ddp = torch.nn.parallel.DistributedDataParallel(model, device_ids=[local])
         opt = torch.optim.SGD(model.parameters(), lr=0.1, momentum=0.9)
     else:
-        ddp = FlatBucketDDP(model, bucket_cap_mb=a.bucket_mb, first_bucket_mb=1.0)
+        ddp = FlatBucketDDP(model, bucket_cap_mb=a.bucket_mb, first_bucket_mb=1.0, loopback=a.loopback)
         opt = FlatSGD(ddp, lr=0.1, momentum=0.9, overlap=bool(a.overlap_sgd))
     g = torch.Generator(device=dev).manual_seed(1234 + rank)
     x = torch.randn(a.batch, 3, a.image, a.image, device=dev, generator=g)
@@ -134,11 +138,15 @@ def run_rank(a) -> None:
             g_.replay()
             return static_loss
     dist.barrier()
+    if hasattr(ddp, "timing") and not a.infer:
+        ddp.comm_time(reset=True)
+        ddp.timing = True  # comm-stream span per step (first bucket launched -> backward finished)
     t0 = time.perf_counter()
     for _ in range(a.steps):
         loss = run()
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
+    comm_us, comm_n = ddp.comm_time() if getattr(ddp, "timing", False) else (0.0, 0)
     t = torch.tensor([dt], device=dev, dtype=torch.float64)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     dt = float(t.item())
@@ -159,6 +167,7 @@ def run_rank(a) -> None:
                                      if a.path == "ops" else "stock PyTorch: torch DDP + MIOpen convs + torch.optim.SGD, bf16 autocast" +
                                      (", channels_last" if cl else ", NCHW")},
                           "comm": getattr(ddp, "comm", None),
+                          "allreduce_us_per_step": round(comm_us / comm_n, 1) if comm_n else None,
                           "xgmi_calibration": getattr(getattr(ddp, "xgmi", None), "calibration", None)}),
               flush=True)
         if a.result_file:
@@ -203,6 +212,9 @@ def main() -> int:
             return 2
         run_rank(a)
         return 0
+    if a.loopback and (a.gpus != 1 or a.path != "ops" or a.graph):
+        print("resnet50.py: --loopback needs --gpus 1 --path ops (no --graph)", file=sys.stderr)
+        return 2
     if a.gpus == 1:
         os.environ.setdefault("WORLD_SIZE", "1")
         run_rank(a)

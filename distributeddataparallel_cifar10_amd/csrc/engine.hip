@@ -74,6 +74,9 @@ struct DcaInit {
   int force_comm;       // comm_mode 0 at world_size 1: still run the RCCL all-reduce + averaging SGD (tests)
   int auto_engine;      // the persistent engine was chosen automatically: keep one workgroup of co-residency
                         // slack (else the caller asked for it explicitly and may use every CU)
+  int loopback;         // world_size 1, comm_mode 2: run the xGMI exchange path with this rank as its own single
+                        // peer (uncached region, slab write-through, flags, peer reads, averaging SGD), so the
+                        // protocol's per-step cost is measurable on one device (bench.py --loopback)
 };
 
 }  // extern "C"
@@ -104,14 +107,10 @@ struct Engine {
   bool persistent = false;  // the image-sliced persistent step kernel (netresdeep_pks.hip; default)
   pks::Args qa{};
   bool comm_on = false;  // the step ends with a gradient collective (world_size > 1, or force_comm)
-  int resident = 0;      // persistent engine: step workgroups allowed in one grid (occupancy x CUs, minus a margin)
-  int cu_slots = 0;      // persistent engine: step workgroups the device holds at once (occupancy x CUs)
+  int resident = 0;      // persistent engine: live step workgroups allowed in one grid (coresident_budget, 1 rank)
+  int per_cu = 0, ncu = 0;  // persistent engine: step workgroups per CU (occupancy) and CUs of the device
   int staged_b = 0;  // persistent engine: batch slots of the current staging parity that hold the next batch
   int last_b = 0;    // batch size of the last enqueued step (BN slots are re-zeroed when it changes)
-  int seg_ch = 128;  // gradient-segment layout (pks::seg_layout): trunk / conv1 chunk size (256 on a shared device)
-  int red_in_step = 0;  // DCA_PKS_RED_IN_STEP=1 (with fc_in_step, world size 1 or xGMI, not shared): the remaining
-                        // gradient segments and the bookkeeping run at the end of the step kernel (pks::red_worker):
-                        // one kernel per step.  Off by default: measured slower (docs/ARCHITECTURE.md)
   int fc_in_step = 1;  // the fc1 / fc-tail gradient segments run on the step kernel's fc workers (pks::N_FCW extra
                        // workgroups beside the backward); off: in the reduction kernel.  Off whenever the step and
                        // its fc workers would exceed the co-resident budget, and when xGMI peers share this device
@@ -177,7 +176,7 @@ static int alloc_workspace(Engine* e) {
       {"COMMT", 16}, {"PKW", PKW_N * 2},
       {"PKS_GRAN", 2 * (size_t)pks::LMAX * pks::GSTR * 8}, {"PKS_YH", 10 * (size_t)pks::LMAX * 2 * 512 * 4},
       {"PKS_BNX", 2 * (size_t)pks::LMAX * 64 * 4},
-      {"PKS_HDONE", (size_t)pks::LMAX * 8 + 2 * 8 * 64 * 4},  // + the in-step arrival counters (pks::sdone_cnt)
+      {"PKS_HDONE", (size_t)pks::LMAX * 8},
       {"C1", e->in.debug ? bmax * 32 * 1024 * 4 : 16},
   };
   size_t total = 0;
@@ -240,8 +239,6 @@ static int alloc_workspace(Engine* e) {
   qa.yh = (float*)e->regions["PKS_YH"];
   qa.c1 = (float*)e->regions["C1"];
   qa.debug = e->in.debug;
-  qa.gap = 0;  // exchange polling: s_sleep(1) units between passes (0 measured best; DCA_PKS_POLL_GAP)
-  if (const char* pp = getenv("DCA_PKS_POLL_GAP")) qa.gap = atoi(pp);
   return 0;
 }
 
@@ -252,13 +249,9 @@ static int set_lds_limits(Engine* e) {
   HIPCK(hipFuncSetAttribute((const void*)e->khead1, hipFuncAttributeMaxDynamicSharedMemorySize, (int)e->s_head1));
   HIPCK(hipFuncSetAttribute((const void*)e->khead2, hipFuncAttributeMaxDynamicSharedMemorySize, (int)e->s_head2));
   HIPCK(hipFuncSetAttribute((const void*)e->kbwd, hipFuncAttributeMaxDynamicSharedMemorySize, (int)dg));
-  HIPCK(hipFuncSetAttribute((const void*)pks::k_pks_step<0, false>, hipFuncAttributeMaxDynamicSharedMemorySize,
+  HIPCK(hipFuncSetAttribute((const void*)pks::k_pks_step<0>, hipFuncAttributeMaxDynamicSharedMemorySize,
                             pks::Plan<0>::TOTAL));
-  HIPCK(hipFuncSetAttribute((const void*)pks::k_pks_step<1, false>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                            pks::Plan<1>::TOTAL));
-  HIPCK(hipFuncSetAttribute((const void*)pks::k_pks_step<0, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                            pks::Plan<0>::TOTAL));
-  HIPCK(hipFuncSetAttribute((const void*)pks::k_pks_step<1, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+  HIPCK(hipFuncSetAttribute((const void*)pks::k_pks_step<1>, hipFuncAttributeMaxDynamicSharedMemorySize,
                             pks::Plan<1>::TOTAL));
 
   return 0;
@@ -286,18 +279,33 @@ static int enqueue_xgmi_sgd(Engine* e, const Ctx& cx) {
 // all-reduce in between.
 // grid of the sliced step: S workgroups per image, image slots rounded up to a multiple of 8 (see k_pks_step)
 static int pks_grid(int B) { return (B + 7) / 8 * 8 * pks::S; }
+// the step workgroups that stay resident and spin in its exchanges (the padding ids of pks_grid exit at once)
+static int pks_live(int B) { return B * pks::S; }
 
-// Ranks sharing one device (shared-GPU rehearsal): a step workgroup needs a whole CU (256 VGPRs), and every
-// workgroup of a peer's spinning step or reduction kernel may hold one.  Each of the n ranks therefore gets a budget
-// of cu_slots / n CUs: its step grid (+ fc workers) and its reduction grid stay within it, so a late rank always
-// finds room for its step however the others are spread over their steps and reductions.
-static int share_budget(const Engine* e) { return e->shared_device > 1 ? e->cu_slots / e->shared_device : e->cu_slots; }
+// Co-residency budget: how many spinning workgroups ONE rank may have resident at once -- one rule for a device of
+// its own and a device shared by n ranks (the shared-GPU rehearsal).  Every workgroup of a persistent grid must be
+// resident together; the occupancy answer can be one block per CU high near register edges (MI355X guide,
+// Residency), so a margin stays free: one block per CU when several fit, else one CU -- unless the caller asked
+// for the whole (dedicated) device explicitly.  Ranks sharing the device split what is left evenly: a rank's step
+// (+ fc workers) and its reduction grid stay within its share, so a late rank always finds room for its step
+// however the others are spread over their steps and reductions.  (Before round 5 the shared share was
+// slots / n with no margin; 8 ranks x batch 8 filled it exactly and a BN exchange timed out.)
+// Mirrored in Python: runtime/engine.py coresident_budget (CPU-tested).
+static int coresident_budget(int per_cu, int ncu, int n_share, bool full_device) {
+  const int slots = per_cu * ncu;
+  const int margin = per_cu > 1 ? ncu : (full_device && n_share <= 1 ? 0 : 1);
+  return (slots - margin) / std::max(n_share, 1);
+}
+static int share_budget(const Engine* e) {
+  return e->shared_device > 1 ? coresident_budget(e->per_cu, e->ncu, e->shared_device, false) : e->resident;
+}
+// gradient-segment layout (pks::seg_layout): trunk / conv1 chunks of 128 elements, 256 on a shared device (fewer
+// reduction workgroups: they must leave CUs for a peer's step)
+static int seg_ch(const Engine* e) { return e->shared_device > 1 ? 256 : 128; }
 
-// Whether the step at batch B runs the fc gradient segments on fc workers (the step grid + N_FCW fits the budget).
+// Whether the step at batch B runs the fc gradient segments on fc workers (the live step + N_FCW fits the budget).
 static bool fc_in_step_for(const Engine* e, int B) {
-  const int gs = pks_grid(B) + pks::N_FCW;
-  if (!e->fc_in_step || gs > e->resident) return false;
-  return e->shared_device <= 1 || gs <= share_budget(e);
+  return e->fc_in_step && pks_live(B) + pks::N_FCW <= share_budget(e);
 }
 // Reduction grid: one workgroup per segment + the bookkeeping one; shared device: capped at the rank's budget
 // (k_pks_reduce_ar then loops over the segments).
@@ -321,36 +329,19 @@ static int enqueue_step_persistent(Engine* e, int B, int part) {
     ra.deadline = e->ar_deadline;
     ra.mode = !multi ? 0 : (xgmi ? 2 : 1);
     ra.fc_in_step = fc_in_step_for(e, B) ? 1 : 0;
-    ra.seg_ch = e->shared_device > 1 ? 256 : e->seg_ch;
-    // in-step reduction: needs the fc workers (the BN tail / bookkeeping pool layout assumes them), the fused SGD
-    // or the xGMI exchange (RCCL and the host all-reduce follow a separate reduction kernel), and a device of our
-    // own (ranks sharing one keep the budgeted, looped reduction kernel)
-    const bool red = e->red_in_step && ra.fc_in_step && ra.mode != 1 && e->shared_device <= 1 && part == 0 &&
-                     ra.seg_ch == 128;
-    // extra reducers: enough that every reduction task (BN tail, trunk / conv1 chunks, bookkeeping) has its own
-    // workgroup beside the 65 fc workers, within the co-resident budget
-    int nrx = 0;
-    if (red) {
-      const int tasks = pks::seg_layout(ra.seg_ch).r_ts + 2;
-      nrx = std::max(0, std::min({tasks - pks::N_FCW, e->resident - pks_grid(B) - pks::N_FCW, pks::NRX_MAX}));
-      ra.fc_in_step |= nrx << 8;  // (pks::red_nrx)
-    }
-    if (e->shared_device > 1 && pks_grid(B) > share_budget(e)) {
-      g_err = "shared-GPU rehearsal: " + std::to_string(e->shared_device) + " ranks x " + std::to_string(pks_grid(B)) +
-              " step workgroups (batch " + std::to_string(B) + ") exceed the device's " + std::to_string(e->cu_slots) +
-              " CUs; use a smaller per-rank batch";
+    ra.seg_ch = seg_ch(e);
+    if (pks_live(B) > share_budget(e)) {  // (set_shared_device already refused batch_max; kept as the last guard)
+      g_err = "persistent engine: " + std::to_string(pks_live(B)) + " step workgroups (batch " + std::to_string(B) +
+              ") exceed the co-residency budget of " + std::to_string(share_budget(e)) + " per rank";
       return -1;
     }
-    const dim3 grid(pks_grid(B) + (ra.fc_in_step ? pks::N_FCW : 0) + nrx);
+    const dim3 grid(pks_grid(B) + (ra.fc_in_step ? pks::N_FCW : 0));
     if (e->bf)
-      hipLaunchKernelGGL((red ? pks::k_pks_step<0, true> : pks::k_pks_step<0, false>), grid, dim3(pks::NTH),
-                         pks::Plan<0>::TOTAL, e->st, cx, e->qa, ra);
+      hipLaunchKernelGGL(pks::k_pks_step<0>, grid, dim3(pks::NTH), pks::Plan<0>::TOTAL, e->st, cx, e->qa, ra);
     else
-      hipLaunchKernelGGL((red ? pks::k_pks_step<1, true> : pks::k_pks_step<1, false>), grid, dim3(pks::NTH),
-                         pks::Plan<1>::TOTAL, e->st, cx, e->qa, ra);
-    if (!red)
-      hipLaunchKernelGGL(pks::k_pks_reduce_ar, dim3(reduce_grid(e, pks::reduce_segments(ra.fc_in_step, ra.seg_ch) + 1)),
-                         dim3(256), pks::stage_floats(B) * 4, e->st, cx, e->qa, B * pks::S, ra);
+      hipLaunchKernelGGL(pks::k_pks_step<1>, grid, dim3(pks::NTH), pks::Plan<1>::TOTAL, e->st, cx, e->qa, ra);
+    hipLaunchKernelGGL(pks::k_pks_reduce_ar, dim3(reduce_grid(e, pks::reduce_segments(ra.fc_in_step, ra.seg_ch) + 1)),
+                       dim3(256), pks::stage_floats(B) * 4, e->st, cx, e->qa, B * pks::S, ra);
   }
   if (multi && !xgmi) {  // RCCL (comm_mode 0, captured) or the host (comm_mode 1, between parts 1 and 2)
     if (part == 0) NCCK(ncclAllReduce(cx.grads, cx.grads, FLAT_N, ncclFloat32, ncclSum, e->comm, e->st));
@@ -413,7 +404,7 @@ extern "C" {
 
 const char* dca_last_error() { return g_err.c_str(); }
 
-int dca_abi_version() { return 5; }  // bump with every DcaInit / signature change
+int dca_abi_version() { return 6; }  // bump with every DcaInit / signature change
 
 int dca_nccl_unique_id(char* out128) {
   ncclUniqueId id;
@@ -448,8 +439,13 @@ static int engine_init(Engine* e, const DcaInit* in, int n_indices) {
     return -1;
   }
   // comm_on: the step ends with a gradient collective + the averaging SGD kernel.  force_comm runs that path at
-  // world_size 1 (a 1-rank RCCL communicator) so the graph-captured collective is testable on one GPU.
-  e->comm_on = in->world_size > 1 || (in->force_comm && in->comm_mode == 0);
+  // world_size 1 (a 1-rank RCCL communicator) so the graph-captured collective is testable on one GPU; loopback
+  // does the same for the xGMI exchange (this rank as its only peer).
+  if (in->loopback && (in->world_size != 1 || in->comm_mode != 2)) {
+    g_err = "loopback needs world_size 1 and comm_mode 2 (xGMI)";
+    return -1;
+  }
+  e->comm_on = in->world_size > 1 || (in->force_comm && in->comm_mode == 0) || in->loopback;
   if (e->bf && e->R == 4) dca::bind_kernels<true, 4, 16>(e);
   else if (e->bf) dca::bind_kernels<true, 2, 16>(e);
   else if (e->R == 4) dca::bind_kernels<false, 4, 8>(e);
@@ -463,18 +459,19 @@ static int engine_init(Engine* e, const DcaInit* in, int n_indices) {
     HIPCK(hipGetDevice(&dev));
     HIPCK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
     if (e->bf)
-      HIPCK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)dca::pks::k_pks_step<0, false>, dca::pks::NTH,
+      HIPCK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)dca::pks::k_pks_step<0>, dca::pks::NTH,
                                                         dca::pks::Plan<0>::TOTAL));
     else
-      HIPCK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)dca::pks::k_pks_step<1, false>, dca::pks::NTH,
+      HIPCK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)dca::pks::k_pks_step<1>, dca::pks::NTH,
                                                         dca::pks::Plan<1>::TOTAL));
     // one step workgroup per CU (256 VGPRs): a grid of every CU would leave no slack for anything else on the
     // device (another stream's kernel, another process), so an automatically chosen engine keeps a margin of one
     // workgroup -- batch 64 (256 workgroups) then falls back to the multi-kernel engine with a warning; an
-    // explicit persistent=True may use every CU
-    const int resident = per_cu > 1 ? (per_cu - 1) * ncu : (in->auto_engine ? ncu - 1 : ncu);
-    const int need = dca::pks_grid(in->bmax);
-    e->cu_slots = per_cu * ncu;
+    // explicit persistent=True may use every CU (coresident_budget)
+    const int resident = dca::coresident_budget(per_cu, ncu, 1, !in->auto_engine);
+    const int need = dca::pks_live(in->bmax);
+    e->per_cu = per_cu;
+    e->ncu = ncu;
     if (resident < need) {
       g_err = "persistent engine: " + std::to_string(need) + " workgroups cannot all be resident (" +
               std::to_string(per_cu) + " per CU x " + std::to_string(ncu) + " CUs); use the multi-kernel engine";
@@ -482,11 +479,6 @@ static int engine_init(Engine* e, const DcaInit* in, int n_indices) {
     }
     e->resident = resident;
     if (const char* fo = getenv("DCA_PKS_FC_IN_STEP")) e->fc_in_step = fo[0] != '0';
-    if (const char* ro = getenv("DCA_PKS_RED_IN_STEP")) e->red_in_step = ro[0] != '0';
-    if (const char* sc = getenv("DCA_PKS_SEG_CH")) {
-      const int v = atoi(sc);
-      e->seg_ch = v == 64 || v == 256 ? v : 128;
-    }
   }
   HIPCK(hipStreamCreateWithFlags(&e->st, hipStreamNonBlocking));
   HIPCK(hipStreamCreateWithFlags(&e->cst, hipStreamNonBlocking));
@@ -519,7 +511,7 @@ static int engine_init(Engine* e, const DcaInit* in, int n_indices) {
   c.n_data = in->n_data;
   c.n_idx = std::max(n_indices, 1);
   e->peers.ticks = (unsigned long long*)e->regions["COMMT"];
-  if (in->world_size > 1 && in->comm_mode == 2) {
+  if ((in->world_size > 1 || in->loopback) && in->comm_mode == 2) {
     if (in->world_size > dca::xg::MAXR) {
       g_err = "xGMI all-reduce: world_size > 8 (one node) -- use RCCL";
       return -1;
@@ -535,6 +527,10 @@ static int engine_init(Engine* e, const DcaInit* in, int n_indices) {
     HIPCK(hipDeviceSynchronize());
     const char* dl = getenv("DCA_XGMI_TIMEOUT_S");
     if (dl) e->ar_deadline = (unsigned long long)(atof(dl) * 1e8);
+    if (in->loopback) {  // the rank is its own (only) peer: no IPC mapping
+      e->peers.base[0] = e->xregion;
+      e->peers_open = true;
+    }
   }
   if (e->comm_on && in->comm_mode == 0) {
     ncclUniqueId id;
@@ -566,7 +562,7 @@ static void engine_free(Engine* e) {
   for (auto& kv : e->graphs) (void)hipGraphExecDestroy(kv.second);
   if (e->comm) (void)ncclCommDestroy(e->comm);
   for (int q = 0; q < dca::xg::MAXR; ++q)
-    if (e->peers_open && q != e->in.rank && q < e->in.world_size && e->peers.base[q])
+    if (e->peers_open && !e->in.loopback && q != e->in.rank && q < e->in.world_size && e->peers.base[q])
       (void)hipIpcCloseMemHandle(e->peers.base[q]);
   if (e->xregion) (void)hipFree(e->xregion);
   if (e->wsp) (void)hipFree(e->wsp);
@@ -614,7 +610,6 @@ static int ensure_staged(Engine* e, int B) {
   // match again; zeroed slots (tag 0) never match (bn_tag)
   if (e->persistent && B != e->last_b) {
     HIPCK(hipMemsetAsync(e->qa.bnx, 0, 2 * (size_t)dca::pks::LMAX * 64 * 4, e->st));
-    HIPCK(hipMemsetAsync(e->qa.hdone + dca::pks::LMAX, 0, 2 * 8 * 64 * 4, e->st));  // in-step arrival counters
   }
   e->last_b = B;
   return 0;
@@ -637,6 +632,46 @@ int dca_engine_set_cursor(void* h, int v) {
   HIPCK(hipMemcpyAsync(e->base.cursor, &v, sizeof(int), hipMemcpyHostToDevice, e->st));
   if (prime_ids(e)) return -1;
   HIPCK(hipStreamSynchronize(e->st));
+  return 0;
+}
+
+// Seed the step epoch (and, xGMI, every exchange flag of this rank's region) -- the epoch-wrap test hook: e.g.
+// EPOCH_WRAP - 3 and 2^32 - 3, so the next steps cross both wraps (pks::EPOCH_WRAP for the device epoch: staging
+// parity, BN tags, granule tags; 2^32 for the per-segment / per-workgroup exchange flags).  Every tag holder whose
+// validity depends on the epoch (BN partial slots, halo / head granules, head-done granules) is zeroed, because an
+// arbitrary jump could make a stale slot's tag match (a zero tag never does); the next batch is re-staged into the
+// new epoch's parity.  xGMI: collective -- every rank seeds the same flag value while no rank is stepping (barrier
+// before and after), since peers write into this rank's flag area.  Synchronous.
+int dca_engine_set_epoch(void* h, int device_epoch, int flag_epoch) {
+  Engine* e = (Engine*)h;
+  if (!e->persistent) {
+    g_err = "set_epoch: the sliced (persistent) engine only";
+    return -1;
+  }
+  if (device_epoch < 0 || (unsigned)device_epoch >= dca::pks::EPOCH_WRAP) {
+    g_err = "set_epoch: device epoch outside [0, EPOCH_WRAP)";
+    return -1;
+  }
+  HIPCK(hipStreamSynchronize(e->st));
+  HIPCK(hipMemcpy(e->qa.epoch, &device_epoch, sizeof(int), hipMemcpyHostToDevice));
+  HIPCK(hipMemset(e->qa.gran, 0, 2 * (size_t)dca::pks::LMAX * dca::pks::GSTR * 8));
+  HIPCK(hipMemset(e->qa.bnx, 0, 2 * (size_t)dca::pks::LMAX * 64 * 4));
+  HIPCK(hipMemset(e->qa.hdone, 0, (size_t)dca::pks::LMAX * 8));
+  if (e->xregion) {
+    std::vector<int> f(dca::xg::FLAG_BYTES / 4, flag_epoch);
+    HIPCK(hipMemcpy(e->xregion, f.data(), dca::xg::FLAG_BYTES, hipMemcpyHostToDevice));                 // k_xgmi_ar_sgd
+    HIPCK(hipMemcpy(e->xregion + dca::xg::REGION_BYTES, f.data(), dca::xg::FLAG_BYTES, hipMemcpyHostToDevice));  // segments
+  }
+  if (prime_ids(e)) return -1;
+  HIPCK(hipStreamSynchronize(e->st));
+  return 0;
+}
+
+// The current device epoch (synchronous).
+int dca_engine_epoch(void* h, int* out) {
+  Engine* e = (Engine*)h;
+  HIPCK(hipStreamSynchronize(e->st));
+  HIPCK(hipMemcpy(out, e->qa.epoch, sizeof(int), hipMemcpyDeviceToHost));
   return 0;
 }
 
@@ -883,7 +918,7 @@ int dca_engine_ipc_selftest(void* h, const float* src, float* dst, float timeout
     ra.st_n = dca::FLAT_N;
     ra.mode = 3;
     ra.fc_in_step = 0;  // every segment in the reduction kernel
-    ra.seg_ch = e->shared_device > 1 ? 256 : e->seg_ch;
+    ra.seg_ch = dca::seg_ch(e);
     dca::Ctx cx = e->base;
     cx.B = 1;
     hipLaunchKernelGGL(dca::pks::k_pks_reduce_ar, dim3(dca::reduce_grid(e, dca::pks::seg_layout(ra.seg_ch).nseg)),
@@ -930,17 +965,17 @@ int dca_engine_ipc_selftest_fc(void* h, const float* src, float* dst, float time
   ra.st_n = dca::FLAT_N;
   ra.mode = 3;
   ra.fc_in_step = 1;
-  ra.seg_ch = e->shared_device > 1 ? 256 : e->seg_ch;
+  ra.seg_ch = dca::seg_ch(e);
   dca::Ctx cx = e->base;
   cx.B = 0;  // no step workgroups: the whole grid is fc workers
   // one workgroup per fc segment, or (ranks sharing the device) the rank's CU budget: every rank's workgroup f waits
   // for its peers' workgroup f, so all ranks' grids must be co-resident (a step-kernel workgroup takes a whole CU)
   const dim3 grid(std::min(dca::pks::N_FCW, dca::share_budget(e)));
   if (e->bf)
-    hipLaunchKernelGGL((dca::pks::k_pks_step<0, false>), grid, dim3(dca::pks::NTH), dca::pks::Plan<0>::TOTAL, e->st, cx, e->qa,
+    hipLaunchKernelGGL(dca::pks::k_pks_step<0>, grid, dim3(dca::pks::NTH), dca::pks::Plan<0>::TOTAL, e->st, cx, e->qa,
                        ra);
   else
-    hipLaunchKernelGGL((dca::pks::k_pks_step<1, false>), grid, dim3(dca::pks::NTH), dca::pks::Plan<1>::TOTAL, e->st, cx, e->qa,
+    hipLaunchKernelGGL(dca::pks::k_pks_step<1>, grid, dim3(dca::pks::NTH), dca::pks::Plan<1>::TOTAL, e->st, cx, e->qa,
                        ra);
   HIPCK(hipGetLastError());
   HIPCK(hipStreamSynchronize(e->st));
@@ -979,7 +1014,7 @@ int dca_engine_ipc_bench(void* h, const float* src, float* dst, int iters, float
       ra.st_n = dca::FLAT_N;
       ra.mode = 3;
       ra.fc_in_step = 0;
-      ra.seg_ch = e->shared_device > 1 ? 256 : e->seg_ch;
+      ra.seg_ch = dca::seg_ch(e);
       dca::Ctx cx = e->base;
       cx.B = 1;
       hipLaunchKernelGGL(dca::pks::k_pks_reduce_ar, dim3(dca::reduce_grid(e, dca::pks::seg_layout(ra.seg_ch).nseg)),
@@ -1026,6 +1061,16 @@ int dca_engine_sync(void* h) {
 // stepping.  Drops the captured graphs.
 int dca_engine_set_shared_device(void* h, int n) {
   Engine* e = (Engine*)h;
+  if (e->persistent && n > 1) {
+    const int budget = dca::coresident_budget(e->per_cu, e->ncu, n, false);
+    if (dca::pks_live(e->in.bmax) > budget) {
+      g_err = "shared device: " + std::to_string(n) + " ranks x " + std::to_string(dca::pks_live(e->in.bmax)) +
+              " step workgroups (batch_max " + std::to_string(e->in.bmax) + ") exceed the per-rank co-residency budget " +
+              "of " + std::to_string(budget) + " of the device's " + std::to_string(e->per_cu * e->ncu) +
+              " workgroup slots (one kept free); use batch_max <= " + std::to_string(budget / dca::pks::S);
+      return -1;
+    }
+  }
   HIPCK(hipStreamSynchronize(e->st));
   for (auto& kv : e->graphs) (void)hipGraphExecDestroy(kv.second);
   e->graphs.clear();

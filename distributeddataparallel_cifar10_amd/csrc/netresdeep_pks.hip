@@ -53,9 +53,7 @@ constexpr int cmax(int a, int b) { return a > b ? a : b; }
 struct Args {
   unsigned long long* gran;  // [2][LMAX][GSTR] granules (halo rows, head partials)
   unsigned* bnx;             // [2][LMAX][64] BatchNorm partials, 4-byte self-tagged values (see bn_tag)
-  unsigned long long* hdone; // [LMAX] head-done granules {tagof(epoch, RND_HDONE), 0} (fc workers' start signal),
-                             // then the in-step reduction's arrival counters (sdone_cnt; no field of their own: one
-                             // more kernel-argument pointer pushed the 256-VGPR step kernel into scratch spills)
+  unsigned long long* hdone; // [LMAX] head-done granules {tagof(epoch, RND_HDONE), 0} (fc workers' start signal)
   int* epoch;                // device scalar, advanced by the reduce kernel after every step
   unsigned* err;             // bit r: exchange round r timed out
   float* tslab;              // [LMAX][WSLAB_N] trunk wgrad per workgroup (fragment order, read by k_pks_reduce)
@@ -65,7 +63,6 @@ struct Args {
   float* yh;                 // [10][LMAX][2][512] halo rows of y received in the forward (for the backward)
   float* c1;                 // debug: [B][32][32][32] conv1 pre-activation (NCHW), for the flip-aware oracle
   int debug;                 // also store X / DY / G / C1 for the numerical diagnostics
-  int gap;                   // sweep: s_sleep(1) units before re-issuing a failed pass (env DCA_PKS_POLL_GAP)
 };
 
 // ---- LDS plan (bytes; every region 16-byte aligned) ---------------------------------------------------------
@@ -367,8 +364,7 @@ __device__ __forceinline__ void sweep_wait(const Args& pa, int round, int wv, in
 #pragma unroll
     for (int p = 0; p < 2; ++p)
       if (xh[p][1] == htag && xh[p][3] == htag) need &= ~(1u << (8 + p));
-    if (__all(need == 0)) break;
-    sleep_units(pa.gap);
+    if (__all(need == 0)) break;  // (re-issued at once: any sleep between passes measured slower)
     if (spins >= SPIN_LIMIT) {
       if (lane == 0) atomicOr(pa.err, 1u << (round & 31));
       break;
@@ -440,13 +436,6 @@ __device__ __forceinline__ void st2_wt(float* p, float a, float b) {
 }
 __device__ __forceinline__ void st1_wt(float* p, float v) {
   __hip_atomic_store((unsigned*)p, __float_as_uint(v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-// write-through only when a reader in the same launch needs it (wt: wave-uniform); a plain store otherwise (measured:
-// the write-through form of these few values cost ~0.5 us per step when nothing in the launch reads them)
-template <bool WT>
-__device__ __forceinline__ void st1_maybe_wt(float* p, float v) {
-  if constexpr (WT) st1_wt(p, v);
-  else *p = v;
 }
 __device__ __forceinline__ void st4r_wt(float* rowp, int h, int lane, const float (&v)[4]) {
   st4_wt(rowp + h * 256 + lane * 4, f32x4{v[0], v[1], v[2], v[3]});
@@ -606,7 +595,6 @@ constexpr int SEG_MAX = 1024;
 constexpr int NSEG_MAX = WSLAB_N / 64 + (SSLAB_N + 63) / 64 + R_FC1 + 2;  // 227: flag-array stride per rank
 constexpr int N_FCW = R_FC1 + 1;                   // fc workers of the step kernel
 constexpr int RND_HDONE = 30;                      // tag round of the head-done granules (fc workers' start)
-constexpr int RND_SDONE = 31;                      // tag round of the slab-done granules (in-step reduction)
 struct SegLayout {
   int ch, r_trunk, r_ts, fct, bnt, nseg, off_fc1, off_fct, off_bnt;
 };
@@ -626,7 +614,6 @@ static_assert(seg_layout(64).nseg == NSEG_MAX && seg_layout(128).nseg <= NSEG_MA
               "flag stride");
 static_assert(seg_layout(128).off_bnt + BNT_LEN >= FLAT_N && seg_layout(128).off_bnt + BNT_LEN <= (int)xg::SLAB_FLOATS,
               "the 128-element layout covers the flat buffer and fits one slab");
-constexpr int NRX_MAX = 256;                       // extra reducer workgroups of the step kernel, upper bound
 static_assert((size_t)NSEG_MAX * xg::MAXR * 4 <= xg::FLAG_BYTES, "one flag per segment and rank");
 static_assert(seg_layout(64).off_bnt + BNT_LEN >= FLAT_N && seg_layout(256).off_bnt + BNT_LEN >= FLAT_N &&
                   seg_layout(256).off_bnt + BNT_LEN <= (int)xg::SLAB_FLOATS,
@@ -646,13 +633,9 @@ struct RedAr {
   float* st_dst;
   int st_n;
   int mode;
-  int fc_in_step;             // nonzero: the fc1 / fc-tail segments run on the step kernel's fc workers; bits 8..:
-                              // the in-step reduction's extra reducer count (red_nrx; k_pks_step<P, true> only).  No
-                              // fields of their own: a larger kernel argument pushed the 256-VGPR step kernel into
-                              // scratch spills
+  int fc_in_step;             // nonzero: the fc1 / fc-tail segments run on the step kernel's fc workers
   int seg_ch;                 // segment layout (seg_layout): 64, 128 or 256
 };
-__device__ __forceinline__ int red_nrx(const RedAr& ra) { return ra.fc_in_step >> 8; }
 
 __device__ __forceinline__ char* rbase(const RedAr& ra, int q) { return ra.peers.base[q] + xg::REGION_BYTES; }
 __device__ __forceinline__ float* rslab(const RedAr& ra, int q, int par) {
@@ -661,15 +644,24 @@ __device__ __forceinline__ float* rslab(const RedAr& ra, int q, int par) {
 
 // one-shot exchange of segment b (segv[0 .. len), len % 4 == 0) with every peer; on return segv holds the sum
 // ep0: this segment's last epoch (own flag), loaded by the caller early so its latency hides under the reduction
-// (thread 0's value; broadcast here through *s_ep)
+// (thread 0's value; broadcast here through s_ep[0]).  Returns false (workgroup-uniform) when the sum must not be
+// used: the exchange word was already set on entry or a wait expired.
+// Failing together: once this rank's exchange word is set (a peer wait expired), later exchanges neither publish
+// nor wait -- the flag stops advancing, so every peer's next wait for this rank expires too and every rank reports
+// the error -- instead of publishing ahead, which let a slow peer pass its wait on a later epoch's slab and run
+// SGD on a sum mixing epochs without noticing.
 template <int NTH>
-__device__ void seg_exchange(const Ctx& cx, const RedAr& ra, int b, float* segv, int len, int off, int ep0, int* s_ep) {
+__device__ bool seg_exchange(const Ctx& cx, const RedAr& ra, int b, float* segv, int len, int off, int ep0, int* s_ep) {
   const int t = threadIdx.x, W = cx.ws, me = cx.rank;
   int* myflags = (int*)rbase(ra, me);
   const unsigned long long t_in = __builtin_amdgcn_s_memrealtime();
-  if (t == 0) *s_ep = xg::next_ep(ep0);
+  if (t == 0) {
+    s_ep[0] = xg::next_ep(ep0);
+    s_ep[1] = xg::failed(ra.err);
+  }
   __syncthreads();
-  const int ep = *s_ep, par = ep & 1;
+  const int ep = s_ep[0], par = ep & 1;
+  if (s_ep[1]) return false;
   constexpr int SYS = 17;  // sc0 | sc1: write-through store / cache-bypassing load
   const __amdgpu_buffer_rsrc_t mine =
       __builtin_amdgcn_make_buffer_rsrc(rslab(ra, me, par), (short)0, (int)(xg::SLAB_FLOATS * 4), 0x00020000);
@@ -679,20 +671,11 @@ __device__ void seg_exchange(const Ctx& cx, const RedAr& ra, int b, float* segv,
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this thread's slab stores are performed
   __syncthreads();                                    // ... and every thread's
   if (t < W) xg::flag_store((int*)rbase(ra, t) + me * NSEG_MAX + b, ep);
-  // fail fast: once any exchange of this rank timed out (a peer stopped stepping) the host is about to stop the run
-  // (dca_engine_run_checked); later exchanges do not wait the full deadline again
-  if (t < W && !(__hip_atomic_load(ra.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & 0x80000000u)) {
-    const int* f = myflags + t * NSEG_MAX + b;
-    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
-    while (xg::flag_before(xg::flag_load(f), ep)) {
-      __builtin_amdgcn_s_sleep(1);
-      if (__builtin_amdgcn_s_memrealtime() - t0 > ra.deadline) {
-        atomicOr(ra.err, 0x80000000u);
-        break;
-      }
-    }
-  }
+  if (t < W) xg::wait_flag(myflags + t * NSEG_MAX + b, ep, ra.deadline, ra.err);
   __syncthreads();
+  if (t == 0) s_ep[1] = xg::failed(ra.err);  // this wait (or any other of this rank) expired
+  __syncthreads();
+  if (s_ep[1]) return false;
   if (t == 0 && b < seg_layout(ra.seg_ch).r_ts && ra.peers.ticks != nullptr) {  // exposed exchange wait, summed over the segments the
     atomicAdd(ra.peers.ticks, __builtin_amdgcn_s_memrealtime() - t_in);  // reduction kernel exchanges (metrics)
     if (b == 0) atomicAdd(ra.peers.ticks + 1, 1ull);
@@ -705,6 +688,7 @@ __device__ void seg_exchange(const Ctx& cx, const RedAr& ra, int b, float* segv,
     });
   }
   __syncthreads();
+  return true;
 }
 
 // parameter index of element k of segment b: >= 0 a parameter; -1 none; -2 - k: CC4 running-stat slot k
@@ -741,9 +725,7 @@ __device__ __forceinline__ f32x4 ld4_sc1(const float* base, int bytes, int off_f
 
 // trunk / stem chunk b of CH outputs in slab fragment order, summed over the nslab workgroup slabs: thread (grp,
 // slot) sums float4 `slot` of slabs grp, grp + NG, ... (all in flight for batch 32), fixed order
-// SC1: the slabs may have been written inside this launch (in-step reduction): sc1 loads; after a kernel boundary
-// plain loads (measured 0.6 us per step faster in k_pks_reduce_ar)
-template <int NTH, int CH, bool SC1>
+template <int NTH, int CH>
 __device__ __forceinline__ void seg_chunk(const Ctx& cx, const Args& pa, const SegLayout& Ls, int b, int nslab,
                                           float* segv, f32x4* red) {
   constexpr int NS = CH / 4, NG = NTH / NS, NU = 128 / NG;
@@ -754,10 +736,6 @@ __device__ __forceinline__ void seg_chunk(const Ctx& cx, const Args& pa, const S
   const float* src = stem ? cx.SSLAB : pa.tslab;
   const int stride = stem ? SSLAB_N : WSLAB_N;
   const int ec = e0 < stride ? e0 : stride - 4;  // conv1's last 256-chunk is partial (1088 = 4.25 x 256)
-  // sc1 loads: the slabs were written through (sc1) by workgroups on any XCD, possibly inside this very launch
-  // (red_worker); this CU's L2 may still hold last step's lines of them
-  const __amdgpu_buffer_rsrc_t rs =
-      __builtin_amdgcn_make_buffer_rsrc((void*)src, (short)0, nslab * stride * 4, 0x00020000);
   f32x4 sacc = z4();
   for (int k0 = 0; k0 < nslab; k0 += 128) {
     f32x4 v[NU];
@@ -765,10 +743,7 @@ __device__ __forceinline__ void seg_chunk(const Ctx& cx, const Args& pa, const S
     for (int u = 0; u < NU; ++u) {
       const int k = k0 + grp + NG * u;
       const int kc = k < nslab ? k : nslab - 1;
-      if constexpr (SC1)
-        v[u] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, (kc * stride + ec) * 4, 0, 16));
-      else
-        v[u] = ld4(src + (size_t)kc * stride + ec);
+      v[u] = ld4(src + (size_t)kc * stride + ec);  // plain loads: the slabs were written before the kernel boundary
     }
 #pragma unroll
     for (int u = 0; u < NU; ++u)
@@ -786,7 +761,7 @@ __device__ __forceinline__ void seg_chunk(const Ctx& cx, const Args& pa, const S
 
 // Segment b on this workgroup (NTH threads): reduce / compute into segv, exchange (mode 2), SGD.  LDS: segv
 // [SEG_MAX], red [NTH] f32x4, stage [stage_floats(B)], *s_ep.
-template <int NTH, bool SC1 = false>
+template <int NTH>
 __device__ void seg_process(const Ctx& cx, const Args& pa, const RedAr& ra, int b, int nslab, float* segv,
                             f32x4* red, float* stage, int* s_ep, int sslot, int swg) {
   const int t = threadIdx.x, B = cx.B;
@@ -808,10 +783,8 @@ __device__ void seg_process(const Ctx& cx, const Args& pa, const RedAr& ra, int 
   if (mode == 3) {
     for (int k = t; k < len; k += NTH) segv[k] = off + k < ra.st_n ? ra.st_src[off + k] : 0.f;
   } else if (b < Ls.r_ts) {
-    if constexpr (SC1) seg_chunk<NTH, 128, true>(cx, pa, Ls, b, nslab, segv, red);  // in-step: 128-element layout
-    else if (Ls.ch == 64) seg_chunk<NTH, 64, false>(cx, pa, Ls, b, nslab, segv, red);
-    else if (Ls.ch == 128) seg_chunk<NTH, 128, false>(cx, pa, Ls, b, nslab, segv, red);
-    else seg_chunk<NTH, 256, false>(cx, pa, Ls, b, nslab, segv, red);
+    if (Ls.ch == 128) seg_chunk<NTH, 128>(cx, pa, Ls, b, nslab, segv, red);
+    else seg_chunk<NTH, 256>(cx, pa, Ls, b, nslab, segv, red);
   } else if (b < Ls.fct) {
     // fc1 block: dW1[j][64f + kk .. +3] = sum_b dh[b][j] p[b][64f + kk ..], rows j = 16 h .. 16 h + 15
     const int fb = b - Ls.r_ts, f = fb >> 1, j0 = 16 * (fb & 1);
@@ -878,19 +851,17 @@ __device__ void seg_process(const Ctx& cx, const Args& pa, const RedAr& ra, int 
     for (int idx = t; idx < BNT_LEN; idx += NTH) {
       float sv;
       if (idx < 64) {
-        sv = __hip_atomic_load(pa.bng + idx, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // (as rm / rv below)
+        sv = pa.bng[idx];
       } else {
         const int k = idx - 64;
-        // sc1: written through by logical workgroup 0, possibly inside this launch (in-step reduction)
-        sv = cx.rank == 0 ? __hip_atomic_load(k < 32 ? cx.rm + k : cx.rv + (k - 32), __ATOMIC_RELAXED,
-                                              __HIP_MEMORY_SCOPE_AGENT) : 0.f;
+        sv = cx.rank == 0 ? (k < 32 ? cx.rm[k] : cx.rv[k - 32]) : 0.f;
       }
       segv[idx] = sv;
     }
   }
   __syncthreads();
   DCA_STAMP(cx, sslot, swg, 1);
-  if (mode >= 2) seg_exchange<NTH>(cx, ra, b, segv, len, off, ep0, s_ep);
+  if (mode >= 2 && !seg_exchange<NTH>(cx, ra, b, segv, len, off, ep0, s_ep)) return;  // no SGD on a failed sum
   DCA_STAMP(cx, sslot, swg, 2);
 #pragma unroll
   for (int i = 0; i < KMAX; ++i) {
@@ -928,14 +899,12 @@ __device__ void seg_process(const Ctx& cx, const Args& pa, const RedAr& ra, int 
 __device__ __forceinline__ void pks_bookkeeping(const Ctx& cx, const Args& pa) {
   const int t = threadIdx.x, B = cx.B;
   if (t >= 64) return;
-  // B <= 64; sc1: written through by the slice-0 workgroups, possibly inside this launch (red_worker)
-  float l = t < B ? __uint_as_float(__hip_atomic_load((const unsigned*)cx.HLOSS + t, __ATOMIC_RELAXED,
-                                                      __HIP_MEMORY_SCOPE_AGENT)) : 0.f;
+  float l = t < B ? cx.HLOSS[t] : 0.f;  // B <= 64
   double acc = 0.0;
-  int cur = 0, stp = 0;
+  int cur = 0, stp = 0, ep = 0;
   long long nb = 0;
-  const int ep = *pa.epoch;  // every lane (the counter reset below needs its parity)
   if (t == 0) {  // issued together with the loss loads: one memory round trip, not five dependent ones
+    ep = *pa.epoch;
     acc = *cx.loss_acc;
     cur = *cx.cursor;
     stp = *cx.step_count;
@@ -950,9 +919,6 @@ __device__ __forceinline__ void pks_bookkeeping(const Ctx& cx, const Args& pa) {
     *cx.nbt = nb + NBLK;  // BatchNorm num_batches_tracked: +1 per application
     *pa.epoch = (int)(((unsigned)ep + 1u) % EPOCH_WRAP);
   }
-  if (t < 8)  // the next step's arrival counters (in-step reduction; see sdone_cnt): everyone has arrived at this one
-    __hip_atomic_store((unsigned*)(pa.hdone + LMAX) + ((((ep & 1) ^ 1) * 8 + t) * 64), 0u, __ATOMIC_RELAXED,
-                       __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // fc worker fb (0 .. R_FC1 - 1: fc1 block fb; R_FC1: fc tail) of the step kernel: waits until every main workgroup
@@ -983,87 +949,17 @@ __device__ void fc_segment(const Ctx& cx, const Args& pa, const RedAr& ra, int f
   float* segv = (float*)smem;
   f32x4* red = (f32x4*)(smem + SEG_MAX * 4);
   float* stage = (float*)(smem + SEG_MAX * 4 + NTH * 16);
-  int* s_ep = (int*)(smem + SEG_MAX * 4 + NTH * 16 + stage_floats(cx.B) * 4);
+  int* s_ep = (int*)(smem + SEG_MAX * 4 + NTH * 16 + stage_floats(cx.B) * 4);  // [2]
   const SegLayout Ls = seg_layout(ra.seg_ch);
   seg_process<NTH>(cx, pa, ra, fb < R_FC1 ? Ls.r_ts + fb : Ls.fct, G, segv, red, stage, s_ep, 9, fb);
-}
-
-// In-step gradient reduction (k_pks_step<P, true>; replaces k_pks_reduce_ar and the kernel boundary before it).  The
-// step workgroups only announce their trunk / conv1 slabs (write-through, then a slab-done granule: sdone_publish)
-// and exit as before; the reduction runs on the REDUCERS -- the fc workers once their fc segment is done (~30 us
-// before the step ends) and red_nrx(ra) extra workgroups of the same launch on the CUs the step leaves free.  A reducer
-// publishes its own granule (so every workgroup of the launch has read this step's epoch before the bookkeeping
-// advances it), waits for all of them, then runs task v = its reducer index (+ the reducer count, ...): v = 0 the BN
-// tail, 1 .. r_ts the trunk / conv1 chunks (sc1 slab loads), r_ts + 1 the bookkeeping (loss, cursor, counters,
-// epoch); each segment with its xGMI exchange (world size > 1) and SGD, exactly as in k_pks_reduce_ar.  The step
-// workgroups' code (and register allocation) is unchanged: they never run a segment.  The slab hand-off is the
-// guide's sc1-store / agent-granule form (no release fence: the slabs are write-through; the readers' loads are sc1).
-// Arrival counters: 2 epoch parities x SDN shards (one 256-B line each, so the arrivals' atomics spread over
-// channels instead of queueing on one word: one word takes ~88 atomics per us, MI355X guide "dequeue").  Member w adds 1
-// to shard w % SDN of this step's parity once its write-through stores are performed; the reducers poll the SDN
-// shards until they sum to the member count.  The bookkeeping (which runs only after every member arrived) zeroes
-// the other parity's shards for the next step; every reduction path runs the bookkeeping, so a step of either kind
-// leaves the counters of the following one at zero.
-constexpr int SDN = 8, SD_STRIDE = 64;
-__device__ __forceinline__ unsigned* sdone_base(const Args& pa) { return (unsigned*)(pa.hdone + LMAX); }
-__device__ __forceinline__ unsigned* sdone_cnt(const Args& pa, int par, int shard) {
-  return sdone_base(pa) + (par * SDN + shard) * SD_STRIDE;
-}
-__device__ __forceinline__ void sdone_publish(const Args& pa, int who, int epoch) {
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this thread's write-through stores are performed
-  __syncthreads();                                    // ... and every thread's of this workgroup
-  if (threadIdx.x == 0)
-    __hip_atomic_fetch_add(sdone_cnt(pa, epoch & 1, who % SDN), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-// r: reducer index (fc worker fb = r, extra e = N_FCW + e)
-__device__ void red_worker(const Ctx& cx, const Args& pa, const RedAr& ra, int epoch, int r, char* smem) {
-  const int t = threadIdx.x, lane = t & 63, G = cx.B * S;
-  const int nred = N_FCW + red_nrx(ra);
-  const unsigned all = (unsigned)(G + nred);
-  sdone_publish(pa, G + r, epoch);
-  const SegLayout Ls = seg_layout(ra.seg_ch);
-  const int nv = Ls.r_ts + 2;  // BN tail, r_ts chunks, bookkeeping
-  if (r >= nv) return;         // nothing to do (its arrival still counts)
-  DCA_STAMP(cx, 10, r, 0);
-  if (t < 64) {  // one wave polls the shards, sleeping between passes until the step workgroups are near the end
-    for (unsigned spins = 0;; ++spins) {
-      unsigned got = lane < SDN ? __hip_atomic_load(sdone_cnt(pa, epoch & 1, lane), __ATOMIC_RELAXED,
-                                                    __HIP_MEMORY_SCOPE_AGENT) : 0u;
-      for (int o = 4; o; o >>= 1) got += __shfl_xor(got, o);
-      got = __shfl(got, 0);
-      if (got >= all) break;
-      if (spins >= SPIN_LIMIT) {
-        if (lane == 0) atomicOr(pa.err, 1u << 29);
-        break;
-      }
-      if (got + (unsigned)G / 2 < all) sleep_units(8);  // far from the end
-    }
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  }
-  __syncthreads();
-  DCA_STAMP(cx, 10, r, 1);
-  float* segv = (float*)smem;
-  f32x4* red = (f32x4*)(smem + SEG_MAX * 4);
-  float* stage = (float*)(smem + SEG_MAX * 4 + NTH * 16);
-  int* s_ep = (int*)(smem + SEG_MAX * 4 + NTH * 16 + stage_floats(cx.B) * 4);
-  for (int v = r; v < nv; v += nred) {
-    if (v == nv - 1) {
-      pks_bookkeeping(cx, pa);
-      continue;
-    }
-    DCA_STAMP(cx, 8, v, 0);
-    seg_process<NTH, true>(cx, pa, ra, v == 0 ? Ls.bnt : v - 1, G, segv, red, stage, s_ep, 8, v);
-    __syncthreads();  // segv / red are reused by the next segment
-  }
 }
 
 constexpr int P_KSHIFT = 906;  // misc: [10][32] BN shifts (last step's batch means)
 constexpr int P_LABEL = 1240;  // misc: this image's label
 
 // ============================================================================================================
-// The step of one main workgroup (slice s of image n).  RIS: the launch runs the in-step reduction.
-template <int P, bool RIS>
+// The step of one main workgroup (slice s of image n).
+template <int P>
 __device__ __forceinline__ void step_main(const Ctx& cx, const Args& pa, const RedAr& ra, char* smem) {
   using PL = Plan<P>;
   const int t = threadIdx.x, wv = t >> 6, lane = t & 63, c = lane & 15, q = lane >> 4;
@@ -1317,9 +1213,8 @@ __device__ __forceinline__ void step_main(const Ctx& cx, const Args& pa, const R
         misc[480 + ch] = misc[480 + ch] * (1.f - mo) + unb * mo;
         cx.STATS[i * 32 + ch] = make_float2(mean, invstd);
         if (i == NBLK - 1) {
-          // write-through when the BN-tail reducer reads them in this launch (in-step reduction)
-          st1_maybe_wt<RIS>(cx.rm + ch, misc[448 + ch]);
-          st1_maybe_wt<RIS>(cx.rv + ch, misc[480 + ch]);
+          cx.rm[ch] = misc[448 + ch];
+          cx.rv[ch] = misc[480 + ch];
         }
       }
     }
@@ -1641,8 +1536,8 @@ __device__ __forceinline__ void step_main(const Ctx& cx, const Args& pa, const R
     DCA_STAMP(cx, 4 + (NBLK - 1 - i) / 8, L, (NBLK - 1 - i) % 8);
   }
   if (L == 0 && t < 32) {
-    st1_maybe_wt<RIS>(pa.bng + t, dgam);  // (as rm / rv)
-    st1_maybe_wt<RIS>(pa.bng + 32 + t, dbet);
+    pa.bng[t] = dgam;
+    pa.bng[32 + t] = dbet;
   }
 
   // ======================= stem backward: max-pool bwd (saved argmax) -> ReLU mask -> conv1 wgrad ============
@@ -1711,7 +1606,7 @@ __device__ __forceinline__ void step_main(const Ctx& cx, const Args& pa, const R
     const float dbv = wg_csum<true>(db, 0.f, cred);
     DCA_STAMP(cx, 5, L, 3);
     float* ss = cx.SSLAB + (size_t)L * SSLAB_N;
-    if (t < 32) st1_maybe_wt<RIS>(ss + 1024 + t, dbv);  // (as rm / rv)
+    if (t < 32) ss[1024 + t] = dbv;
     // D[co][k] = sum over this slice's conv pixels of ds[p][co] * im2col[p][k]; K step = one conv row (32 px).
     // Wave wv: tile wv & 3 (mt = co half, nt = k tile), conv rows 4 (wv >> 2) .. +3; k >= 27 columns are
     // discarded by the reduce
@@ -1758,33 +1653,23 @@ __device__ __forceinline__ void step_main(const Ctx& cx, const Args& pa, const R
     }
   }
   DCA_STAMP(cx, 5, L, 7);
-  if constexpr (RIS) sdone_publish(pa, L, epoch);  // the reducers of this launch take it from here
 }
 
-// RIS (compile time): the in-step reduction's code exists only in the RIS instantiations, so the
-// default kernel's register allocation is the one without it
-template <int P, bool RIS>
+template <int P>
 __global__ void __launch_bounds__(NTH) k_pks_step(Ctx cx, Args pa, RedAr ra) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int gmain = (cx.B + 7) / 8 * 8 * S;
   if ((int)blockIdx.x < gmain) {
-    step_main<P, RIS>(cx, pa, ra, smem);
+    step_main<P>(cx, pa, ra, smem);
     return;
   }
-  // past the main grid: the fc workers (only with ra.fc_in_step), then the extra reducers (RIS)
+  // past the main grid: the fc workers (only with ra.fc_in_step); one fc segment each in a training step (nfw ==
+  // N_FCW); the self-test on a shared device launches fewer workers (its per-rank CU budget), which then take the
+  // segments in turn
   const int fb = (int)blockIdx.x - gmain, nfw = min((int)gridDim.x - gmain, N_FCW);
-  if (fb < N_FCW) {
-    // one fc segment each in a training step (nfw == N_FCW); the self-test on a shared device launches fewer
-    // workers (its per-rank CU budget), which then take the segments in turn
-    for (int f = fb; f < N_FCW; f += nfw) {
-      if (f != fb) __syncthreads();
-      fc_segment<P>(cx, pa, ra, f, smem);
-    }
-  }
-  if constexpr (RIS) {
-    const int epoch = *pa.epoch;  // unchanged until every workgroup has arrived (red_worker)
-    __syncthreads();              // the fc segment's LDS is reused
-    red_worker(cx, pa, ra, epoch, fb, smem);
+  for (int f = fb; f < N_FCW; f += nfw) {
+    if (f != fb) __syncthreads();
+    fc_segment<P>(cx, pa, ra, f, smem);
   }
 }
 
@@ -1819,7 +1704,7 @@ __global__ void __launch_bounds__(256) k_pks_reduce_ar(Ctx cx, Args pa, int nsla
   __shared__ __attribute__((aligned(16))) float segv[SEG_MAX];
   __shared__ f32x4 red[256];
   extern __shared__ __attribute__((aligned(16))) float stage[];
-  __shared__ int s_ep;
+  __shared__ int s_ep[2];
   const int nred = reduce_segments(ra.fc_in_step, ra.seg_ch), b = blockIdx.x, nwg = gridDim.x;
   const SegLayout Ls = seg_layout(ra.seg_ch);
   if (nwg > nred) {
@@ -1829,12 +1714,12 @@ __global__ void __launch_bounds__(256) k_pks_reduce_ar(Ctx cx, Args pa, int nsla
     }
     const int seg = !ra.fc_in_step || b < Ls.r_ts ? b : Ls.bnt;
     DCA_STAMP(cx, 8, b, 0);
-    seg_process<256>(cx, pa, ra, seg, nslab, segv, red, stage, &s_ep, 8, b);
+    seg_process<256>(cx, pa, ra, seg, nslab, segv, red, stage, s_ep, 8, b);
     return;
   }
   for (int k = b; k < nred; k += nwg) {
     const int seg = !ra.fc_in_step || k < Ls.r_ts ? k : Ls.bnt;
-    seg_process<256>(cx, pa, ra, seg, nslab, segv, red, stage, &s_ep, 8, k);
+    seg_process<256>(cx, pa, ra, seg, nslab, segv, red, stage, s_ep, 8, k);
     __syncthreads();  // segv / red / stage are reused by the next segment
   }
   if (b == nwg - 1 && ra.mode != 3) pks_bookkeeping(cx, pa);

@@ -59,13 +59,30 @@ __device__ __forceinline__ void flag_store(int* p, int v) {
 // not reached epoch ep yet" as a wrap-aware serial-number comparison; next_ep is the wrapping increment.
 __device__ __forceinline__ bool flag_before(int f, int ep) { return (int)((unsigned)f - (unsigned)ep) < 0; }
 __device__ __forceinline__ int next_ep(int f) { return (int)((unsigned)f + 1u); }
+// The exchange word's bit 31: a peer-flag wait of this rank expired (set here, read and cleared by the host).
+__device__ __forceinline__ int failed(const unsigned* err) {
+  return (__hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & 0x80000000u) ? 1 : 0;
+}
+// Wait until flag *f has reached epoch ep; on expiry of `deadline` (s_memrealtime ticks) set bit 31 of *err.
+__device__ __forceinline__ void wait_flag(const int* f, int ep, unsigned long long deadline, unsigned* err) {
+  const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+  while (flag_before(flag_load(f), ep)) {
+    __builtin_amdgcn_s_sleep(1);
+    if (__builtin_amdgcn_s_memrealtime() - t0 > deadline) {
+      atomicOr(err, 0x80000000u);
+      break;
+    }
+  }
+}
 __device__ __forceinline__ float* slab(const Peers& P, int q, int parity) {
   return (float*)(P.base[q] + FLAG_BYTES) + (size_t)parity * SLAB_FLOATS;
 }
 
 // src: this rank's gradient (cx.grads); `sgd` 0 = sum into `sum_out` only (self-test), 1 = training step.
-// `deadline_ticks`: wait limit in s_memrealtime ticks (100 MHz); on expiry err bit 31 is set and the
-// workgroup goes on with whatever it read (the host raises on the flag at its next check).
+// `deadline_ticks`: wait limit in s_memrealtime ticks (100 MHz); on expiry err bit 31 is set and the workgroup
+// neither sums nor updates (the host raises on the word at its next check).  With the word already set on entry it
+// does not publish either: the flag stops advancing, so every peer's next wait for this rank expires as well and all
+// ranks fail together (seg_exchange in netresdeep_pks.hip: same rule).
 template <bool BF>
 __global__ void __launch_bounds__(AR_T) k_xgmi_ar_sgd(Ctx cx, Peers P, const float* src, float* sum_out,
                                                       unsigned* err, int sgd, unsigned long long deadline_ticks) {
@@ -73,12 +90,16 @@ __global__ void __launch_bounds__(AR_T) k_xgmi_ar_sgd(Ctx cx, Peers P, const flo
   const int v = b * AR_T + t;
   const bool live = v < AR_V4;
   int* myflags = (int*)P.base[me];
-  __shared__ int s_ep;
+  __shared__ int s_ep, s_fail;
   const unsigned long long t_in = __builtin_amdgcn_s_memrealtime();
-  if (t == 0) s_ep = next_ep(flag_load(myflags + me * AR_NB + b));
+  if (t == 0) {
+    s_ep = next_ep(flag_load(myflags + me * AR_NB + b));
+    s_fail = failed(err);
+  }
   const f32x4 g = live ? *(const f32x4*)(src + 4 * v) : f32x4{0.f, 0.f, 0.f, 0.f};
   __syncthreads();
   const int ep = s_ep, par = ep & 1;
+  if (s_fail) return;
   constexpr int SYS = 17;  // cache policy sc0 | sc1: system-coherent (write-through store / cache-bypassing load)
   const __amdgpu_buffer_rsrc_t mine =
       __builtin_amdgcn_make_buffer_rsrc(slab(P, me, par), (short)0, (int)(SLAB_FLOATS * 4), 0x00020000);
@@ -86,23 +107,15 @@ __global__ void __launch_bounds__(AR_T) k_xgmi_ar_sgd(Ctx cx, Peers P, const flo
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this thread's slab store is performed
   __syncthreads();                                    // ... and every thread's of this workgroup
   if (t < W) flag_store((int*)P.base[t] + me * AR_NB + b, ep);
-  if (t < W && !(__hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & 0x80000000u)) {  // fail fast
-    const int* f = myflags + t * AR_NB + b;
-    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
-    while (flag_before(flag_load(f), ep)) {
-      __builtin_amdgcn_s_sleep(1);
-      if (__builtin_amdgcn_s_memrealtime() - t0 > deadline_ticks) {
-        atomicOr(err, 0x80000000u);
-        break;
-      }
-    }
-  }
+  if (t < W) wait_flag(myflags + t * AR_NB + b, ep, deadline_ticks, err);
+  __syncthreads();
+  if (t == 0) s_fail = failed(err);
   __syncthreads();
   if (b == 0 && t == 0 && P.ticks != nullptr) {  // exposed all-reduce time of this rank (metrics)
     atomicAdd(P.ticks, __builtin_amdgcn_s_memrealtime() - t_in);
     atomicAdd(P.ticks + 1, 1ull);
   }
-  if (!live) return;
+  if (!live || s_fail) return;
   // exactly W loads in flight at once (one per peer link), cache-bypassing, summed in rank order (rank_sum.h)
   const f32x4 s = rank_sum(W, [&](int q) {
     const __amdgpu_buffer_rsrc_t rs =

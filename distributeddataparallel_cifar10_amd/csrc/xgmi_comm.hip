@@ -19,6 +19,10 @@
 //   [in slab parity 0][in slab parity 1][out slab parity 0][out slab parity 1]   (slab_bytes each)
 // Element i of a bucket always sits at element i of a slab.
 //
+// Failing together: a workgroup that finds the error word set on entry returns at once (no publish, no wait, dst
+// keeps the rank's own values); one whose wait expires does not sum.  The flag then stops advancing, so every
+// peer's next wait for this rank expires too and all ranks report the error -- publishing ahead instead would let a
+// slow peer pass its wait on a later call's slab and sum mixed calls without noticing.
 // Protocol of workgroup b (the communicator launches exactly `nb` workgroups for every call, so every workgroup
 // advances its epoch on every call and ep is uniform across the grid and across ranks):
 //   1. ep = in_flags[me][b] + 1, parity = ep & 1
@@ -29,8 +33,8 @@
 //      two-shot: read piece b of MY segment from all W in slabs, sum in rank order, scale, write it to dst and to
 //      my out slab[parity] (write-through); vmcnt(0) + barrier; store ep into out_flags[me][b] of every rank;
 //      wait until my out_flags[q][b] >= ep for all q; read piece b of segment q from rank q's out slab into dst.
-//   Waits are bounded by s_memrealtime: on expiry bit 0 of *err is set and the workgroup continues (no hang; the
-//   host raises when it reads the error word).
+//   Waits are bounded by s_memrealtime: on expiry bit 0 of *err is set and the workgroup stops (no hang; the host
+//   raises when it reads the error word).
 // Reuse safety (as csrc/xgmi_allreduce.hip): workgroup b writes a slab of parity p at call k only after it passed
 // a wait of call k-1, i.e. after every peer STARTED call k-1, i.e. (stream order) after every peer finished call
 // k-2 -- the last call that read parity p.  This holds whatever the bucket partition of each call is.
@@ -124,9 +128,13 @@ __device__ __forceinline__ f4 slab_get(__amdgpu_buffer_rsrc_t r, long long v) {
   return __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(r, (int)(16 * v), 0, SYS));
 }
 
+__device__ __forceinline__ bool err_set(const Args& a) {
+  return __hip_atomic_load(a.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u;
+}
 // Raise flag[me][b] = ep on every rank, then wait for flag[q][b] >= ep on all q (thread q polls rank q's flag in
-// MY region).  Called by the whole workgroup after its slab stores; returns after a workgroup barrier.
-__device__ __forceinline__ void exchange(const Args& a, bool out, int ep) {
+// MY region).  Called by the whole workgroup after its slab stores; returns after a workgroup barrier, false
+// (workgroup-uniform) when a wait of this rank expired: the slabs read next may hold other epochs.
+__device__ __forceinline__ bool exchange(const Args& a, bool out, int ep, int* s_fail) {
   const int t = threadIdx.x, b = blockIdx.x;
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this thread's write-through slab stores are performed
   __syncthreads();                                    // ... and every thread's of this workgroup
@@ -135,9 +143,7 @@ __device__ __forceinline__ void exchange(const Args& a, bool out, int ep) {
     __hip_atomic_store(f, ep, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     const int* mine = (out ? out_flags(a.base[a.me]) : in_flags(a.base[a.me])) + t * NB_MAX + b;
     const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
-    // fail fast: after a timed-out wait (error word set, not yet read by the host) later calls do not wait again
-    const bool failed = __hip_atomic_load(a.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u;
-    while (!failed && (int)((unsigned)__hip_atomic_load(mine, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) - (unsigned)ep) < 0) {
+    while ((int)((unsigned)__hip_atomic_load(mine, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) - (unsigned)ep) < 0) {
       __builtin_amdgcn_s_sleep(1);
       if (__builtin_amdgcn_s_memrealtime() - t0 > a.deadline) {
         atomicOr(a.err, 1u);
@@ -146,6 +152,9 @@ __device__ __forceinline__ void exchange(const Args& a, bool out, int ep) {
     }
   }
   __syncthreads();
+  if (t == 0) *s_fail = err_set(a);
+  __syncthreads();
+  return !*s_fail;
 }
 
 // Sum float4 v over all W ranks' slabs (rank order), exactly W loads in flight at once (one per peer link).
@@ -174,10 +183,14 @@ template <bool BF, bool TWO>
 __global__ void __launch_bounds__(T) k_allreduce(Args a) {
   const int t = threadIdx.x, b = blockIdx.x, W = a.W, me = a.me;
   const long long nv = (a.n + 3) / 4;
-  __shared__ int s_ep;
-  if (t == 0) s_ep = __hip_atomic_load(in_flags(a.base[me]) + me * NB_MAX + b, __ATOMIC_RELAXED,
-                                       __HIP_MEMORY_SCOPE_SYSTEM) + 1u;  // wraps mod 2^32 (wrap-aware wait below)
+  __shared__ int s_ep, s_fail;
+  if (t == 0) {
+    s_ep = __hip_atomic_load(in_flags(a.base[me]) + me * NB_MAX + b, __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_SYSTEM) + 1u;  // wraps mod 2^32 (wrap-aware wait below)
+    s_fail = err_set(a);
+  }
   __syncthreads();
+  if (s_fail) return;
   const int ep = s_ep, par = ep & 1;
   const long long wire = BF ? 2 : 4;
   const long long sb = (nv * 4) * wire;  // slab bytes in use
@@ -188,7 +201,7 @@ __global__ void __launch_bounds__(T) k_allreduce(Args a) {
   if (!TWO) {
     const long long piece = (nv + a.nb - 1) / a.nb, lo = b * piece, hi = lo + piece < nv ? lo + piece : nv;
     for (long long v = lo + t; v < hi; v += T) slab_put<BF>(rin[me], v, load_src(a.src, v, a.n));
-    exchange(a, false, ep);
+    if (!exchange(a, false, ep, &s_fail)) return;
     for (long long v = lo + t; v < hi; v += T) {
       f4 s = gather_sum<BF>(rin, W, v) * a.scale;
       store_dst(a.dst, v, a.n, BF ? round_bf16(s) : s);
@@ -207,7 +220,7 @@ __global__ void __launch_bounds__(T) k_allreduce(Args a) {
     range(q, lo, hi);
     for (long long v = lo + t; v < hi; v += T) slab_put<BF>(rin[me], v, load_src(a.src, v, a.n));
   }
-  exchange(a, false, ep);
+  if (!exchange(a, false, ep, &s_fail)) return;
   const __amdgpu_buffer_rsrc_t rmine = rsrc(out_slab(a, me, par), sb);
   {
     long long lo, hi;
@@ -219,7 +232,7 @@ __global__ void __launch_bounds__(T) k_allreduce(Args a) {
       store_dst(a.dst, v, a.n, s);
     }
   }
-  exchange(a, true, ep);
+  if (!exchange(a, true, ep, &s_fail)) return;
   // all-gather: piece b of every other segment from its owner, W-1 loads in flight per thread
   __amdgpu_buffer_rsrc_t rout[MAXR];
   long long lo[MAXR], hi[MAXR], len = 0;

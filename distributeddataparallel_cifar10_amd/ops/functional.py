@@ -914,6 +914,7 @@ def conv_bn_act(x, conv: torch.nn.Conv2d, bn: torch.nn.BatchNorm2d, r=None, relu
         res_mode = 2 if r is not None else 0
     if conv.bias is not None:
         raise ValueError("conv_bn_act: conv without bias")
+    _check_join(bn, relu, res_mode)
     if not bn.training:  # inference: running statistics, no autograd
         _check_inference(conv.weight)
         with torch.no_grad():
@@ -1027,11 +1028,20 @@ def _bn_eval(x, r, bn: torch.nn.BatchNorm2d, relu, res_mode):
     return out
 
 
+def _check_join(bn, relu, res_mode):
+    """Training: act(bn + r) (res_mode 2) exists only WITH the ReLU -- its backward kernels recover the residual
+    gradient through the ReLU mask -- so the combination is refused here, before a forward whose backward would
+    fail (eval-mode inference supports it)."""
+    if res_mode == 2 and not relu and bn.training and torch.is_grad_enabled():
+        raise ValueError("res_mode 2 (bn + r) without ReLU is not supported in training; use relu=True or res_mode 1")
+
+
 def batch_norm_act(x, bn: torch.nn.BatchNorm2d, r=None, relu=True, res_mode=0):
     """BatchNorm2d `bn` over NHWC x.  Training mode: batch statistics, running stats updated in place,
     num_batches_tracked += 1.  Eval mode: running statistics (inference, under no_grad)."""
     if res_mode and r is None:
         raise ValueError("batch_norm_act: residual mode needs r")
+    _check_join(bn, relu, res_mode)
     if not bn.training:  # inference: running statistics, no autograd
         _check_inference(bn.weight)
         with torch.no_grad():
@@ -1077,6 +1087,9 @@ def max_pool2d(x, k=2, s=None, p=0):
 class _AvgPool(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, out_bf16):
+        if x.dtype != torch.bfloat16 or x.dim() != 4:
+            raise ValueError("global_avg_pool: NHWC bf16 input")
+        x = x.contiguous()  # the kernel indexes x as dense NHWC
         n, h, w, c = x.shape
         y = torch.empty(n, c, dtype=torch.bfloat16 if out_bf16 else torch.float32, device=x.device)
         N.check(N.lib().dca_ops_avgpool_fwd(N.ptr(x), N.ptr(y), n, h * w, c, int(out_bf16), N.stream(x.device)),

@@ -12,7 +12,8 @@
     the gradient buffer (no separate broadcast collective).
 
 comm="auto" picks "xgmi" when every rank is on this node (LOCAL_WORLD_SIZE == WORLD_SIZE, or no launcher env)
-and RCCL otherwise.  The xGMI path is verified at construction by a collective self-test (an exact all-reduce
+and RCCL otherwise.  ``loopback=True`` (world size 1, comm="xgmi"): the xGMI exchange path runs with the rank as its
+own only peer, so its per-step protocol cost is measurable on one device (``bench.py --allreduce xgmi --loopback``).  The xGMI path is verified at construction by a collective self-test (an exact all-reduce
 of a known pattern); if mapping or the self-test fails on ANY rank, every rank falls back to RCCL together.
 
 The generic ``FlatBucketDDP`` (any nn.Module, autograd hooks) lives in ``parallel/flat_ddp.py``.
@@ -46,7 +47,7 @@ class FusedDDPTrainer:
 
     def __init__(self, model: nn.Module, data_u8: torch.Tensor, labels: torch.Tensor, batch_max: int = 32,
                  lr: float = 1e-2, dtype: str = "bf16", rows: int = 4, max_indices: Optional[int] = None,
-                 persistent: Optional[bool] = None, comm: str = "auto"):
+                 persistent: Optional[bool] = None, comm: str = "auto", loopback: bool = False):
         world = dist.get_world_size() if dist.is_available() and dist.is_initialized() else 1
         rank = dist.get_rank() if world > 1 else 0
         self.world_size, self.rank = world, rank
@@ -58,6 +59,16 @@ class FusedDDPTrainer:
         args = dict(batch_max=batch_max, lr=lr, dtype=dtype, rows=rows, world_size=world, rank=rank,
                     persistent=persistent)
         self.engine = None
+        if loopback:
+            if world != 1 or comm != "xgmi":
+                raise ValueError("loopback needs world size 1 and comm='xgmi'")
+            eng = NetResDeepEngine(model, data_u8, labels, EngineConfig(**args, comm="xgmi", loopback=True),
+                                   max_indices=max_indices)
+            if not eng.xgmi_selftest():
+                eng.close()
+                raise RuntimeError("xGMI loopback self-test failed")
+            self.engine, self.comm, self.module, self.n_share = eng, "xgmi-loopback", model, 1
+            return
         if world > 1:
             broadcast_module_state(model, 0)
         if world > 1 and comm == "xgmi":

@@ -56,10 +56,12 @@ def _dist_on(group=None) -> bool:
 class FlatBucketDDP(nn.Module):
     def __init__(self, module: nn.Module, bucket_cap_mb: float = 4.0, first_bucket_mb: Optional[float] = 1.0,
                  broadcast_buffers: bool = True, process_group=None, device_ids=None, output_device=None,
-                 comm: str = "auto", wire: str = "fp32", algo: str = "auto"):
+                 comm: str = "auto", wire: str = "fp32", algo: str = "auto", loopback: bool = False):
         """``comm``: "auto" (xGMI for CUDA models when every rank is on this node, else the process group),
         "xgmi", or "process_group".  ``wire`` ("fp32" | "bf16") and ``algo`` ("auto" | "oneshot" | "twoshot")
-        apply to the xGMI path."""
+        apply to the xGMI path.  ``loopback`` (one rank, CUDA): every bucket still goes through the xGMI
+        communicator on the comm stream -- the rank is its own only peer -- so the per-bucket kernel's cost beside
+        the backward is measurable on one device (``bench/resnet50.py --loopback``)."""
         super().__init__()
         if comm not in ("auto", "xgmi", "process_group"):
             raise ValueError("comm must be 'auto', 'xgmi' or 'process_group'")
@@ -122,7 +124,17 @@ class FlatBucketDDP(nn.Module):
         self._sync_module_states()  # CC3
         self.comm, self.xgmi, self._comm_stream = "process_group" if self.world_size > 1 else "none", None, None
         self._wire, self._algo = wire, algo
-        if self.world_size > 1 and dev.type == "cuda" and dtype == torch.float32 and comm != "process_group":
+        if loopback:
+            if self.world_size != 1 or dev.type != "cuda" or dtype != torch.float32:
+                raise ValueError("loopback: one rank, fp32 parameters on a GPU")
+            from .xgmi import XgmiComm
+            self.xgmi = XgmiComm.create(max(e - s for s, e, _ in self.buckets), group=process_group, device=dev,
+                                        wire=wire)
+            if self.xgmi is None:
+                raise RuntimeError("xGMI loopback communicator unavailable")
+            self.comm = "xgmi-loopback"
+            self._comm_stream = torch.cuda.Stream(dev)
+        elif self.world_size > 1 and dev.type == "cuda" and dtype == torch.float32 and comm != "process_group":
             local = int(os.environ.get("LOCAL_WORLD_SIZE", str(self.world_size)))
             if comm == "xgmi" or (local == self.world_size and self.world_size <= 8):
                 from .xgmi import XgmiComm
@@ -204,7 +216,7 @@ class FlatBucketDDP(nn.Module):
 
     def _make_ready(self, p):
         def ready():
-            if self.world_size == 1 and self._fused_opt is None:
+            if self.world_size == 1 and self._fused_opt is None and self.xgmi is None:
                 return
             # idempotent per step: a kernel-written (sink) gradient reports readiness itself, and autograd may
             # still run the parameter's AccumulateGrad with an undefined gradient, firing the hook as well
@@ -223,13 +235,13 @@ class FlatBucketDDP(nn.Module):
     def _launch(self, bi: int) -> None:
         s, e, _ = self.buckets[bi]
         seg = self.flat_grad[s:e]
-        if self.timing and seg.is_cuda and self.world_size > 1 and not self.bucket_fire_order:
+        if self.timing and seg.is_cuda and (self.world_size > 1 or self.xgmi is not None) and not self.bucket_fire_order:
             ev = torch.cuda.Event(enable_timing=True)  # first bucket of the step: comm span starts
             cs = self._side_stream()
             cs.wait_stream(torch.cuda.current_stream(seg.device))
             ev.record(cs)
             self._comm_events.append([ev, None])
-        if self.world_size == 1:  # nothing to reduce: only the fused optimizer update (side stream on a GPU)
+        if self.world_size == 1 and self.xgmi is None:  # nothing to reduce: only the fused update (side stream on a GPU)
             if seg.is_cuda:
                 cs = self._side_stream()
                 cs.wait_stream(torch.cuda.current_stream(seg.device))

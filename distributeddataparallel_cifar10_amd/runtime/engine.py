@@ -69,6 +69,7 @@ class _DcaInit(ctypes.Structure):
         ("comm_mode", ctypes.c_int),
         ("force_comm", ctypes.c_int),
         ("auto_engine", ctypes.c_int),
+        ("loopback", ctypes.c_int),
     ]
 
 
@@ -107,6 +108,25 @@ def nccl_unique_id() -> bytes:
     return buf.raw
 
 
+# The sliced engine's step epoch wraps here (csrc/netresdeep_pks.hip EPOCH_WRAP = 6 * 2^23).
+EPOCH_WRAP = 6 << 23
+S_SLICES = 4  # workgroups per image of the sliced step (csrc/netresdeep_pks.hip pks::S)
+
+
+def coresident_budget(per_cu: int, ncu: int, n_share: int = 1, full_device: bool = False) -> int:
+    """Spinning workgroups ONE rank may hold resident at once (csrc/engine.hip coresident_budget, same rule): the
+    device's slots minus a margin -- one block per CU when several fit, else one CU (none only when a dedicated
+    device was asked for explicitly) -- split evenly over the ranks sharing the device."""
+    slots = per_cu * ncu
+    margin = ncu if per_cu > 1 else (0 if full_device and n_share <= 1 else 1)
+    return (slots - margin) // max(n_share, 1)
+
+
+def max_sliced_batch(per_cu: int, ncu: int, n_share: int = 1, full_device: bool = False) -> int:
+    """Largest per-rank batch whose sliced step (S_SLICES live workgroups per image) fits the budget."""
+    return min(64, coresident_budget(per_cu, ncu, n_share, full_device) // S_SLICES)
+
+
 @dataclass
 class EngineConfig:
     batch_max: int = 32
@@ -126,6 +146,9 @@ class EngineConfig:
     bn_eps: float = 1e-5
     force_comm: bool = False     # comm="rccl" at world_size 1: still run the graph-captured RCCL all-reduce and the
                                  # averaging SGD kernel (a 1-rank communicator) -- exercises that path on one GPU
+    loopback: bool = False       # comm="xgmi" at world_size 1: the xGMI exchange with this rank as its own only peer
+                                 # (uncached region, write-through slabs, flags, peer reads, averaging SGD): the
+                                 # protocol's per-step cost measured on one device (bench.py --loopback)
 
 
 class NetResDeepEngine:
@@ -175,6 +198,7 @@ class NetResDeepEngine:
             # the automatic choice keeps one CU of co-residency slack (batch 64 -> multi-kernel engine);
             # DCA_PKS_ALLOW_FULL_DEVICE=1 lets it use all 256 CUs (nothing else may then run on the GPU)
             auto_engine=1 if auto_engine and os.environ.get("DCA_PKS_ALLOW_FULL_DEVICE") != "1" else 0,
+            loopback=1 if cfg.loopback else 0,
         )
         self._init = init
         self.max_indices = int(max_indices or self.data.shape[0])
@@ -204,6 +228,20 @@ class NetResDeepEngine:
         (a rank's spinning kernels must always leave CUs for a peer's step).  Every rank must make the same
         call before stepping."""
         native.check(self.lib.dca_engine_set_shared_device(self.h, int(n)), "dca_engine_set_shared_device")
+
+    def set_epoch(self, device_epoch: int, flag_epoch: int = 0) -> None:
+        """Sliced engine: seed the step epoch and (xGMI) every exchange flag of this rank's region -- the epoch-wrap
+        test hook (``EPOCH_WRAP - 3`` / ``2**32 - 3`` cross both wraps within a few steps).  xGMI: collective, every
+        rank seeds the same values with no rank stepping (barrier before and after)."""
+        flag = int(flag_epoch) & 0xFFFFFFFF
+        flag = flag - (1 << 32) if flag >= (1 << 31) else flag  # the C int of the same bits
+        native.check(self.lib.dca_engine_set_epoch(self.h, int(device_epoch), flag), "dca_engine_set_epoch")
+
+    def epoch(self) -> int:
+        """The device step epoch (synchronous)."""
+        out = ctypes.c_int()
+        native.check(self.lib.dca_engine_epoch(self.h, ctypes.byref(out)), "dca_engine_epoch")
+        return int(out.value)
 
     def fc_in_step(self, batch: int) -> bool:
         """Whether a step at this batch size runs the fc gradient segments on the step kernel's fc workers."""
@@ -342,10 +380,12 @@ class NetResDeepEngine:
         return loss.value, steps.value
 
     def run_checked(self, batch: int, steps: int) -> int:
-        """`steps` graph-replayed steps with the device error words checked after every 16-step chunk (pipelined:
+        """`steps` graph-replayed steps with the device error words checked after every 8-step chunk (pipelined:
         the GPU never waits for the check).  Synchronous.  Raises (``check_errors``) as soon as an exchange timed
-        out -- a rank that stopped stepping is noticed within two chunks, not at the epoch end.  Returns the steps
-        run."""
+        out -- a rank that stopped stepping is noticed within two chunks (< 16 steps), not at the epoch end.  Returns
+        the steps run.  Only where every collective of the step is the engine's own (world size 1 or xGMI): a
+        rank stopping early cannot leave its peers inside a graph-captured RCCL all-reduce, which has no deadline
+        (``run_epoch`` uses plain replays there)."""
         done = ctypes.c_int()
         rc = self.lib.dca_engine_run_checked(self.h, int(batch), int(steps), ctypes.byref(done))
         if rc < 0:
@@ -356,8 +396,10 @@ class NetResDeepEngine:
         return int(done.value)
 
     def run_epoch(self, indices, batch: int, graph: bool = True) -> tuple[float, int]:
-        """One pass over `indices` in batches of `batch` (ragged last batch kept, drop_last=False).  With graphs
-        the error words are checked after every chunk (``run_checked``)."""
+        """One pass over `indices` in batches of `batch` (ragged last batch kept, drop_last=False).  With graphs at
+        world size 1 or over xGMI the error words are checked after every chunk (``run_checked``); with RCCL every
+        rank replays the whole epoch and the words are checked at its end (``read_loss``), so no rank stops
+        stepping while its peers wait in a captured all-reduce."""
         n = len(indices)
         self.set_indices(indices)
         self.set_cursor(0)
@@ -366,7 +408,7 @@ class NetResDeepEngine:
         for b, k in ((batch, full), (rem, 1 if rem else 0)):
             if not k:
                 continue
-            if graph and not (self.cfg.world_size > 1 and self.cfg.comm == "external"):
+            if graph and (self.cfg.world_size == 1 or self.cfg.comm == "xgmi"):
                 self.run_checked(b, k)
             else:
                 self.run(b, k, graph)

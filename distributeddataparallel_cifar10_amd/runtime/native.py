@@ -16,7 +16,7 @@ import torch  # noqa: F401  (must be imported before the native library, see mod
 
 from .. import build as _build
 
-ABI_VERSION = 5  # csrc/engine.hip dca_abi_version(): DcaInit layout / C signatures
+ABI_VERSION = 6  # csrc/engine.hip dca_abi_version(): DcaInit layout / C signatures
 _lock = threading.Lock()
 _lib = None
 
@@ -56,6 +56,8 @@ def _declare(lib):
     lib.dca_engine_precapture.argtypes = [c_void_p, c_int]
     lib.dca_engine_kind.argtypes = [c_void_p]
     lib.dca_engine_set_shared_device.argtypes = [c_void_p, c_int]
+    lib.dca_engine_set_epoch.argtypes = [c_void_p, c_int, c_int]
+    lib.dca_engine_epoch.argtypes = [c_void_p, ctypes.POINTER(c_int)]
     lib.dca_engine_fc_in_step.argtypes = [c_void_p, c_int]
     lib.dca_engine_comm_time.argtypes = [c_void_p, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_longlong),
                                          c_int]

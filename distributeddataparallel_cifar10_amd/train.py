@@ -41,6 +41,7 @@ class TrainConfig:
     batch_size: int = 32             # reference main.py:61 (main_no_ddp.py:31 hard-codes 64)
     data_path: str = "data/CIFAR-10/"
     synthetic: int = 0               # >0: use N synthetic CIFAR-shaped samples instead of the dataset
+    synthetic_learnable: bool = False  # synthetic labels a function of the image (class colour + stripes + noise)
     engine: str = "auto"             # auto | fused | torch
     dtype: str = "fp32"              # compute precision: fp32 = the reference's numerics (default), bf16 = MFMA bf16
     max_steps: Optional[int] = None  # per-epoch step cap (smoke tests / benchmarking)
@@ -71,6 +72,9 @@ def add_cli_args(ap: argparse.ArgumentParser, batch_default: int = 32) -> argpar
     ap.add_argument("--data-root", default=None)
     ap.add_argument("--synthetic", type=int, nargs="?", const=50000, default=0,
                     help="train on N synthetic CIFAR-shaped samples (default 50000)")
+    ap.add_argument("--synthetic-learnable", action="store_true",
+                    help="synthetic data whose label is a function of the image (class colour + stripe pattern + "
+                         "noise), so the loss falls; implies --synthetic 50000 unless given")
     ap.add_argument("--engine", default="auto", choices=["auto", "fused", "ops", "torch"],
                     help="fused: NetResDeep native engine; ops: the framework's HIP layer kernels (any supported "
                          "model) + FlatBucketDDP; torch: stock PyTorch ops + FlatBucketDDP")
@@ -101,8 +105,10 @@ def add_cli_args(ap: argparse.ArgumentParser, batch_default: int = 32) -> argpar
 
 
 def config_from_args(a: argparse.Namespace, data_path_default: str) -> TrainConfig:
+    learnable = bool(getattr(a, "synthetic_learnable", False))
     return TrainConfig(epochs=a.epochs, lr=a.lr, batch_size=a.batch_size, data_path=a.data_root or data_path_default,
-                       synthetic=a.synthetic or 0, engine=a.engine, dtype=a.dtype, max_steps=a.max_steps,
+                       synthetic=a.synthetic or (50000 if learnable else 0), synthetic_learnable=learnable,
+                       engine=a.engine, dtype=a.dtype, max_steps=a.max_steps,
                        checkpoint=not a.no_checkpoint, checkpoint_path=a.checkpoint_path, resume=a.resume,
                        metrics_json=a.metrics_json, seed=a.seed, set_epoch=a.set_epoch, fail_at_step=a.fail_at_step,
                        backend=a.backend, port=a.port, timeout_s=a.timeout, model=a.model, bucket_mb=a.bucket_mb,
@@ -111,7 +117,7 @@ def config_from_args(a: argparse.Namespace, data_path_default: str) -> TrainConf
 
 def load_dataset(cfg: TrainConfig):
     if cfg.synthetic:
-        return synthetic_cifar(cfg.synthetic, seed=cfg.seed)
+        return synthetic_cifar(cfg.synthetic, seed=cfg.seed, learnable=cfg.synthetic_learnable)
     return load_cifar10(cfg.data_path, train=True)
 
 

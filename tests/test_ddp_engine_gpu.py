@@ -130,8 +130,8 @@ def _xgmi_worker(rank, ws, port, dtype, persistent, q, comm="xgmi", own_device=F
         broadcast_module_state(model, 0)
         ref0 = copy.deepcopy(model)
         model = model.to(dev)
-        tr = FusedDDPTrainer(model, data.to(dev), labels.to(dev), batch_max=32, dtype=dtype, persistent=persistent,
-                             comm=comm, max_indices=len(order[rank]))
+        tr = FusedDDPTrainer(model, data.to(dev), labels.to(dev), batch_max=batch, dtype=dtype,
+                             persistent=persistent, comm=comm, max_indices=len(order[rank]))
         assert tr.comm == comm, f"asked for {comm}, got {tr.comm} (the xGMI path did not come up?)"
         eng = tr.engine
         if fc_workers is not None:
@@ -147,36 +147,7 @@ def _xgmi_worker(rank, ws, port, dtype, persistent, q, comm="xgmi", own_device=F
             print(f"[rank {rank}/{ws}] step {s} done", file=sys.stderr, flush=True)
         loss, steps = eng.read_loss()
         assert steps == STEPS
-        # single-process simulation of reference DDP over `ws` ranks
-        models = [copy.deepcopy(ref0) for _ in range(ws)]
-        for s in range(STEPS):
-            snap = {k: v.clone() for k, v in models[0].named_buffers()}
-            grads = []
-            for r in range(ws):
-                with torch.no_grad():
-                    for k, v in models[r].named_buffers():
-                        v.copy_(snap[k])
-                sel = order[r][s * batch:(s + 1) * batch]
-                out = reference_step(models[r], data[sel], labels[sel], lr=1e-2, apply_sgd=False,
-                                     bf16_operands=dtype == "bf16", fc1_bf16=persistent and dtype == "bf16")
-                grads.append(out["grads"])
-            with torch.no_grad():
-                for r in range(ws):
-                    for n, p in models[r].named_parameters():
-                        p -= 1e-2 * sum(g[n] for g in grads) / ws
-        sim = models[rank]
-        tol = 1e-3 if dtype == "fp32" else 3e-2
-        sd, rsd = model.state_dict(), sim.state_dict()
-        for k in ("fc1.weight", "fc2.bias", "resblocks.0.conv.weight", "resblocks.0.batch_norm.weight",
-                  "conv1.weight", "resblocks.0.batch_norm.running_mean", "resblocks.0.batch_norm.running_var"):
-            a, b = sd[k].detach().double().cpu(), rsd[k].detach().double()
-            err = ((a - b).norm() / b.norm()).item()
-            assert err < tol, (k, err)
-        # bitwise-identical parameters on every rank (fixed rank-order summation)
-        flat = torch.cat([p.detach().reshape(-1).cpu() for p in model.parameters()])
-        other = flat.clone()
-        dist.broadcast(other, 0)
-        assert torch.equal(flat, other)
+        _check_vs_simulation(model, ref0, data, labels, order, rank, ws, STEPS, batch, dtype, persistent)
         tr.close()
         q.put((rank, None))
     except Exception:
@@ -184,6 +155,103 @@ def _xgmi_worker(rank, ws, port, dtype, persistent, q, comm="xgmi", own_device=F
     finally:
         if dist.is_initialized():
             dist.destroy_process_group()
+
+
+def _simulate_ddp(ref0, data, labels, order, ws, steps, batch, dtype, persistent):
+    """Single-process simulation of reference DDP over `ws` ranks (CC4 rank-0 buffers, CC5 averaged gradients)."""
+    from distributeddataparallel_cifar10_amd.utils.oracle import reference_step
+    models = [copy.deepcopy(ref0) for _ in range(ws)]
+    for s in range(steps):
+        snap = {k: v.clone() for k, v in models[0].named_buffers()}
+        grads = []
+        for r in range(ws):
+            with torch.no_grad():
+                for k, v in models[r].named_buffers():
+                    v.copy_(snap[k])
+            sel = order[r][s * batch:(s + 1) * batch]
+            out = reference_step(models[r], data[sel], labels[sel], lr=1e-2, apply_sgd=False,
+                                 bf16_operands=dtype == "bf16", fc1_bf16=persistent and dtype == "bf16")
+            grads.append(out["grads"])
+        with torch.no_grad():
+            for r in range(ws):
+                for n, p in models[r].named_parameters():
+                    p -= 1e-2 * sum(g[n] for g in grads) / ws
+    return models
+
+
+def _check_vs_simulation(model, ref0, data, labels, order, rank, ws, steps, batch, dtype, persistent):
+    """This rank's state tracks the DDP simulation; parameters are bitwise identical on every rank."""
+    sim = _simulate_ddp(ref0, data, labels, order, ws, steps, batch, dtype, persistent)[rank]
+    tol = 1e-3 if dtype == "fp32" else 3e-2
+    sd, rsd = model.state_dict(), sim.state_dict()
+    for k in ("fc1.weight", "fc2.bias", "resblocks.0.conv.weight", "resblocks.0.batch_norm.weight",
+              "conv1.weight", "resblocks.0.batch_norm.running_mean", "resblocks.0.batch_norm.running_var"):
+        a, b = sd[k].detach().double().cpu(), rsd[k].detach().double()
+        err = ((a - b).norm() / b.norm()).item()
+        assert err < tol, (k, err)
+    # bitwise-identical parameters on every rank (fixed rank-order summation)
+    flat = torch.cat([p.detach().reshape(-1).cpu() for p in model.parameters()])
+    other = flat.clone()
+    dist.broadcast(other, 0)
+    assert torch.equal(flat, other)
+
+
+def _wrap_worker(rank, ws, port, dtype, q):
+    """Two runs from the same state over the same batches, the second with the device epoch seeded to EPOCH_WRAP - 3
+    and every xGMI exchange flag to 2^32 - 3, so its 8 steps cross both wraps: bitwise the first run's parameters,
+    and on the DDP simulation's trajectory."""
+    try:
+        os.environ["MASTER_ADDR"] = "127.0.0.1"
+        os.environ["MASTER_PORT"] = str(port)
+        os.environ["DCA_XGMI_TIMEOUT_S"] = "30"
+        dist.init_process_group("gloo", rank=rank, world_size=ws)
+        from distributeddataparallel_cifar10_amd.data.sampler import distributed_indices
+        from distributeddataparallel_cifar10_amd.data.synthetic import synthetic_cifar
+        from distributeddataparallel_cifar10_amd.models.netresdeep import NetResDeep
+        from distributeddataparallel_cifar10_amd.parallel.ddp import FusedDDPTrainer, broadcast_module_state
+        from distributeddataparallel_cifar10_amd.runtime.engine import EPOCH_WRAP
+        dev = torch.device("cuda", 0)
+        torch.cuda.set_device(dev)
+        batch, steps = 8, 8
+        data, labels = synthetic_cifar(NDATA, seed=7)
+        order = [distributed_indices(NDATA, ws, r) for r in range(ws)]
+        torch.manual_seed(200 + rank)
+        ref0 = NetResDeep()
+        broadcast_module_state(ref0, 0)
+        finals = []
+        for seeded in (False, True):
+            model = copy.deepcopy(ref0).to(dev)
+            tr = FusedDDPTrainer(model, data.to(dev), labels.to(dev), batch_max=batch, dtype=dtype, comm="xgmi",
+                                 max_indices=len(order[rank]))
+            assert tr.comm == "xgmi"
+            eng = tr.engine
+            if seeded:
+                dist.barrier()  # no rank steps while the flags are seeded (peers write into each other's flags)
+                eng.set_epoch(EPOCH_WRAP - 3, 2 ** 32 - 3)
+                dist.barrier()
+            eng.set_indices(order[rank])
+            eng.set_cursor(0)
+            eng.read_loss(reset=True)
+            eng.run(batch, steps)
+            _, n = eng.read_loss()  # raises on any exchange timeout
+            assert n == steps
+            if seeded:
+                assert eng.epoch() == 5, eng.epoch()
+                _check_vs_simulation(model, ref0, data, labels, order, rank, ws, steps, batch, dtype, True)
+            finals.append(torch.cat([p.detach().reshape(-1).cpu() for p in model.parameters()]))
+            tr.close()
+        assert torch.equal(finals[0], finals[1])
+        q.put((rank, None))
+    except Exception:
+        q.put((rank, traceback.format_exc()))
+    finally:
+        if dist.is_initialized():
+            dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("dtype", ["bf16", "fp32"])
+def test_xgmi_epoch_wrap_two_ranks_one_gpu(gpu, port, dtype):
+    spawn_ranks(_wrap_worker, 2, lambda r: (r, 2, port, dtype))
 
 
 @pytest.mark.parametrize("ws,dtype,persistent,batch", [(2, "bf16", True, B), (4, "bf16", True, B),
@@ -297,3 +365,54 @@ def _stall_worker(rank, ws, port, q):
 
 def test_peer_stall_raises_within_16_steps(gpu, port):
     spawn_ranks(_stall_worker, 2, lambda r: (r, 2, port))
+
+
+def _slow_peer_worker(rank, ws, port, q):
+    """Rank 1 pauses 3 s (> the 1 s exchange deadline) after 3 steps, then keeps stepping.  Rank 0's wait expires; from
+    then on rank 0 neither publishes nor waits, so rank 1's next exchanges expire too: BOTH ranks must report the
+    error (before round 5 rank 0 kept publishing ahead and the slow rank passed its waits on later epochs' slabs,
+    silently summing mixed epochs)."""
+    try:
+        import time
+        os.environ["MASTER_ADDR"] = "127.0.0.1"
+        os.environ["MASTER_PORT"] = str(port)
+        os.environ["DCA_XGMI_TIMEOUT_S"] = "1"
+        dist.init_process_group("gloo", rank=rank, world_size=ws)
+        from distributeddataparallel_cifar10_amd.data.synthetic import synthetic_cifar
+        from distributeddataparallel_cifar10_amd.models.netresdeep import NetResDeep
+        from distributeddataparallel_cifar10_amd.parallel.ddp import FusedDDPTrainer
+        dev = torch.device("cuda", 0)
+        data, labels = synthetic_cifar(NDATA, seed=5)
+        torch.manual_seed(0)
+        tr = FusedDDPTrainer(NetResDeep().to(dev), data.to(dev), labels.to(dev), batch_max=8, dtype="bf16",
+                             comm="xgmi", max_indices=NDATA)
+        assert tr.comm == "xgmi"
+        eng = tr.engine
+        batch, good = 8, 3
+        eng.set_indices(list(range(NDATA)))
+        eng.set_cursor(0)
+        eng.read_loss(reset=True)
+        raised = False
+        try:
+            if rank == 1:
+                eng.run(batch, good)
+                eng.sync()
+                time.sleep(3.0)
+                eng.run_checked(batch, NDATA // batch - good)
+            else:
+                eng.run_checked(batch, NDATA // batch)
+        except RuntimeError as ex:
+            raised = "xGMI" in str(ex)
+        assert raised, f"rank {rank} did not report the expired exchange"
+        dist.barrier()
+        tr.close()
+        q.put((rank, None))
+    except Exception:
+        q.put((rank, traceback.format_exc()))
+    finally:
+        if dist.is_initialized():
+            dist.destroy_process_group()
+
+
+def test_slow_peer_every_rank_reports(gpu, port):
+    spawn_ranks(_slow_peer_worker, 2, lambda r: (r, 2, port))

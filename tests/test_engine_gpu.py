@@ -84,6 +84,86 @@ def test_trajectory_matches_oracle(gpu, dtype, persistent, tol):
         assert abs(le - lr) < 5 * tol * max(1.0, abs(lr)), (le, lr)
 
 
+@pytest.mark.parametrize("dtype,tol", [("fp32", 1e-4), ("bf16", 3e-2)])
+def test_trajectory_across_epoch_wrap(gpu, dtype, tol):
+    """The device epoch seeded to EPOCH_WRAP - 3: the 8 steps cross the wrap (staging parity, BN partial tags,
+    granule tags all continue across it) -- still on the fp32 oracle's trajectory, and bitwise the run from epoch 0
+    (same state, same batches: the epoch only names the exchange rounds)."""
+    from engine_diag import trajectory
+    from distributeddataparallel_cifar10_amd.runtime.engine import EPOCH_WRAP
+    plain = trajectory(dtype, 4, 32, 8, persistent=True)
+    wrap = trajectory(dtype, 4, 32, 8, persistent=True, seed_epoch=EPOCH_WRAP - 3)
+    assert plain["epoch_end"] == 8 and wrap["epoch_end"] == 5, (plain["epoch_end"], wrap["epoch_end"])
+    assert wrap["param_rel_l2"] < tol and wrap["max_param_rel_err"] < 20 * tol, wrap
+    assert torch.equal(plain["params"], wrap["params"])
+    assert plain["losses_engine"] == wrap["losses_engine"]
+
+
+def test_shared_device_budget_refuses_exact_fill(gpu):
+    """One co-residency rule (csrc/engine.hip coresident_budget, mirrored by runtime/engine.py): 8 ranks sharing the
+    device at batch_max 8 (8 x 32 live step workgroups = every CU) are refused when the sharing is declared --
+    before any step could spin in a BN exchange that cannot complete -- while batch_max 4 is accepted."""
+    from distributeddataparallel_cifar10_amd.data.synthetic import synthetic_cifar
+    from distributeddataparallel_cifar10_amd.models.netresdeep import NetResDeep
+    from distributeddataparallel_cifar10_amd.runtime.engine import (EngineConfig, NetResDeepEngine,
+                                                                    max_sliced_batch)
+    props = torch.cuda.get_device_properties(gpu)
+    assert max_sliced_batch(1, props.multi_processor_count, 8) == (props.multi_processor_count - 1) // 8 // 4
+    data, labels = synthetic_cifar(64)
+    for bmax, ok in ((8, False), (4, True)):
+        eng = NetResDeepEngine(NetResDeep().to(gpu), data.to(gpu), labels.to(gpu), EngineConfig(batch_max=bmax))
+        try:
+            if ok:
+                eng.set_shared_device(8)
+            else:
+                with pytest.raises(RuntimeError, match="co-residency budget"):
+                    eng.set_shared_device(8)
+        finally:
+            eng.close()
+
+
+@pytest.mark.parametrize("dtype,tol", [("fp32", 2e-3), ("bf16", 3e-2)])
+def test_learnable_epochs_track_pytorch(gpu, dtype, tol):
+    """Three short epochs of learnable synthetic data (label = f(image)) on the sliced engine's ``run_epoch`` -- 20
+    full batches + a ragged batch of 16, the reference's epoch mean over len(loader) (main.py:43-44), 10 BN EMAs per
+    step, the same order every epoch (no set_epoch) -- against stock PyTorch fp32 (CPU) step by step: every epoch's
+    mean loss within `tol` (relative), the final parameters close, and the loss falling (the model learns)."""
+    import copy
+    from distributeddataparallel_cifar10_amd.data.synthetic import synthetic_cifar
+    from distributeddataparallel_cifar10_amd.models.netresdeep import NetResDeep
+    from distributeddataparallel_cifar10_amd.runtime.engine import EngineConfig, NetResDeepEngine
+    from distributeddataparallel_cifar10_amd.utils.oracle import reference_step
+    B, n = 32, 32 * 20 + 16
+    data, labels = synthetic_cifar(n, seed=3, learnable=True)
+    torch.manual_seed(5)
+    model = NetResDeep()
+    ref = copy.deepcopy(model)
+    model = model.to(gpu)
+    eng = NetResDeepEngine(model, data.to(gpu), labels.to(gpu), EngineConfig(batch_max=B, dtype=dtype))
+    assert eng.kind_name == "sliced"
+    nb = (n + B - 1) // B
+    eng_means, ref_means = [], []
+    for _ in range(3):
+        loss_sum, steps = eng.run_epoch(list(range(n)), B)
+        assert steps == nb
+        eng_means.append(loss_sum / nb)
+        tot = 0.0
+        for k in range(nb):
+            sel = slice(k * B, min((k + 1) * B, n))
+            tot += reference_step(ref, data[sel], labels[sel], lr=1e-2, bf16_operands=dtype == "bf16",
+                                  fc1_bf16=dtype == "bf16")["loss"]
+        ref_means.append(tot / nb)
+    eng.close()
+    for e, r in zip(eng_means, ref_means):
+        assert abs(e - r) <= tol * abs(r), (eng_means, ref_means)
+    assert eng_means[2] < 0.8 * eng_means[0] < 0.8 * 2.31, eng_means
+    sd, rsd = model.state_dict(), ref.state_dict()
+    a = torch.cat([sd[k].detach().double().cpu().reshape(-1) for k in rsd if rsd[k].dtype != torch.int64])
+    b = torch.cat([rsd[k].detach().double().reshape(-1) for k in rsd if rsd[k].dtype != torch.int64])
+    assert ((a - b).norm() / b.norm()).item() < 10 * tol
+    assert int(sd["resblocks.0.batch_norm.num_batches_tracked"]) == 10 * 3 * nb
+
+
 def test_graft_smoke(gpu):
     import __graft_entry__
     __graft_entry__.smoke()
