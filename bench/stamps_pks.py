@@ -80,9 +80,10 @@ def main():
     # fc workers of the step kernel (slot 9, fc1 block 0..63, 64 = fc tail): 0 start, 1 head seen + computed, ...
     red = raw.reshape(32, 256, 8, 2)[8]
     step_end = rte.max()
-    groups = {"trunk": range(0, 144), "stem": range(144, 161), "bn_tail": range(161, 162)}
-    r0 = red[:162, 0, 1].astype(np.int64)
-    r3 = red[:162, 3, 1].astype(np.int64)
+    # seg_layout(128) with the fc segments on the fc workers: 72 trunk chunks, 9 conv1 chunks, the BN tail
+    groups = {"trunk": range(0, 72), "stem": range(72, 81), "bn_tail": range(81, 82)}
+    r0 = red[:82, 0, 1].astype(np.int64)
+    r3 = red[:82, 3, 1].astype(np.int64)
     if (r0 != 0).all():
         print(json.dumps({"reduce_gap_after_step_us": round(float(r0.min() - step_end) / 100.0, 2),
                           "reduce_span_us": round(float(r3.max() - r0.min()) / 100.0, 2),
@@ -94,22 +95,6 @@ def main():
                               "sgd_us": round(float(seg[2]), 2),
                               "end_after_first_start_us": round(float(x[:, 3, 1].max() - r0.min()) / 100.0, 2)}),
                   flush=True)
-    # in-step reduction (red_worker; slot 10, reducer r = fc worker / extra: 0 entry, 1 every slab-done granule
-    # seen; slot 8, task v: 0 BN tail, 1 .. r_ts trunk / conv1 chunks -- 0 start, 1 summed, 2 exchanged, 3 end)
-    pw = raw.reshape(32, 256, 8, 2)[10].astype(np.int64)
-    nred = int((pw[:, 1, 1] != 0).sum())
-    if nred:
-        seen = pw[:nred, 1, 1]
-        tasks = red[:nred - 1].astype(np.int64)  # the last task index is the bookkeeping (no stamps)
-        tasks = tasks[tasks[:, 3, 1] != 0]
-        print(json.dumps({"red_in_step": True, "reducers": nred,
-                          "last_main_end_to_first_seen_us": round(float(seen.min() - step_end) / 100.0, 2),
-                          "last_main_end_to_last_seen_us": round(float(seen.max() - step_end) / 100.0, 2),
-                          "sum_us": round(float(np.median(tasks[:, 1, 1] - tasks[:, 0, 1])) / 100.0, 2),
-                          "exchange_us": round(float(np.median(tasks[:, 2, 1] - tasks[:, 1, 1])) / 100.0, 2),
-                          "sgd_us": round(float(np.median(tasks[:, 3, 1] - tasks[:, 2, 1])) / 100.0, 2),
-                          "last_task_end_after_last_main_end_us": round(float(tasks[:, 3, 1].max() - step_end) / 100.0, 2)}),
-              flush=True)
     fcw = raw.reshape(32, 256, 8, 2)[9][:65].astype(np.int64)
     if (fcw[:, 3, 1] != 0).all():
         print(json.dumps({"fc_workers": 65, "compute_us": round(float(np.median(fcw[:, 1, 1] - fcw[:, 0, 1])) / 100.0, 2),

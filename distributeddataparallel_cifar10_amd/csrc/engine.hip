@@ -114,6 +114,7 @@ struct Engine {
   int fc_in_step = 1;  // the fc1 / fc-tail gradient segments run on the step kernel's fc workers (pks::N_FCW extra
                        // workgroups beside the backward); off: in the reduction kernel.  Off whenever the step and
                        // its fc workers would exceed the co-resident budget, and when xGMI peers share this device
+  int prologue = 1;  // chunks apply each step's gradient segments in the next step's launch (prologue_ok)
   int shared_device = 0;  // set by the host: number of xGMI ranks on this device (shared-GPU rehearsal; 0/1: not
                           // shared): the coarse 107-segment layout, and fc workers only when every co-scheduled
                           // grid fits (fc_in_step_for), so a spinning kernel always leaves CUs for a peer's step
@@ -176,7 +177,7 @@ static int alloc_workspace(Engine* e) {
       {"COMMT", 16}, {"PKW", PKW_N * 2},
       {"PKS_GRAN", 2 * (size_t)pks::LMAX * pks::GSTR * 8}, {"PKS_YH", 10 * (size_t)pks::LMAX * 2 * 512 * 4},
       {"PKS_BNX", 2 * (size_t)pks::LMAX * 64 * 4},
-      {"PKS_HDONE", (size_t)pks::LMAX * 8},
+      {"PKS_HDONE", (size_t)pks::LMAX * 8 + 256 * 8},  // head-done | prologue ready granules
       {"C1", e->in.debug ? bmax * 32 * 1024 * 4 : 16},
   };
   size_t total = 0;
@@ -313,34 +314,67 @@ static int reduce_grid(const Engine* e, int nred_plus) {
   return e->shared_device > 1 ? std::min(nred_plus, share_budget(e)) : nred_plus;
 }
 
-static int enqueue_step_persistent(Engine* e, int B, int part) {
+// Whether a chunk of steps at batch B may apply each step's gradient segments in the NEXT step's launch (the
+// prologue reduction, netresdeep_pks.hip): the SGD must be fused into the segments (world size 1 or xGMI; RCCL and
+// the host all-reduce sit between reduction and SGD), the fc workers run in the step (the prologue leaves the fc
+// segments to them), and the reducers fit beside the live step within the co-residency budget.
+// DCA_PKS_PROLOGUE=0 turns it off (one reduction kernel after every step, the round-4 schedule).
+static bool prologue_ok(const Engine* e, int B) {
+  if (!e->persistent || !e->prologue) return false;
+  if (e->comm_on && e->in.comm_mode != 2) return false;
+  if (!fc_in_step_for(e, B)) return false;
+  return pks_live(B) + std::max(pks::N_FCW, pks::prologue_segments(seg_ch(e))) <= share_budget(e);
+}
+
+// The sliced step kernel: step s of its chunk; prev: the previous step's segments are applied in its prologue.
+static int enqueue_pks_step(Engine* e, int B, int s, bool prev) {
   Ctx cx = e->base;
   cx.B = B;
-  const bool multi = e->comm_on;
-  const bool xgmi = multi && e->in.comm_mode == 2;
+  const bool multi = e->comm_on, xgmi = multi && e->in.comm_mode == 2;
   if (xgmi && !e->peers_open) {
     g_err = "xGMI all-reduce: peers not mapped (call dca_engine_ipc_open first)";
     return -1;
   }
+  if (pks_live(B) > share_budget(e)) {  // (set_shared_device already refused batch_max; kept as the last guard)
+    g_err = "persistent engine: " + std::to_string(pks_live(B)) + " step workgroups (batch " + std::to_string(B) +
+            ") exceed the co-residency budget of " + std::to_string(share_budget(e)) + " per rank";
+    return -1;
+  }
+  pks::RedAr ra{};
+  ra.peers = e->peers;
+  ra.err = e->qa.err + 1;
+  ra.deadline = e->ar_deadline;
+  ra.mode = !multi ? 0 : (xgmi ? 2 : 1);
+  const bool fc = fc_in_step_for(e, B);
+  ra.fc_in_step = pks::ra_flags(fc, prev, s, 0);
+  ra.seg_ch = seg_ch(e);
+  const int extra = fc ? std::max(pks::N_FCW, prev ? pks::prologue_segments(ra.seg_ch) : 0) : 0;
+  const dim3 grid(pks_grid(B) + extra);
+  if (e->bf)
+    hipLaunchKernelGGL(pks::k_pks_step<0>, grid, dim3(pks::NTH), pks::Plan<0>::TOTAL, e->st, cx, e->qa, ra);
+  else
+    hipLaunchKernelGGL(pks::k_pks_step<1>, grid, dim3(pks::NTH), pks::Plan<1>::TOTAL, e->st, cx, e->qa, ra);
+  HIPCK(hipGetLastError());
+  return 0;
+}
+
+// The reduction kernel closing a chunk of `chunk` steps (the last step's segments + its bookkeeping, epoch and
+// cursor advanced by the chunk); then, RCCL / host all-reduce (mode 1), the collective and the averaging SGD.
+// part: 0 whole; 1 up to the all-reduce; 2 the SGD after it (comm_mode 1, the host runs the all-reduce between).
+static int enqueue_pks_reduce(Engine* e, int B, int chunk, int part) {
+  Ctx cx = e->base;
+  cx.B = B;
+  const bool multi = e->comm_on, xgmi = multi && e->in.comm_mode == 2;
   if (part != 2) {
     pks::RedAr ra{};
     ra.peers = e->peers;
     ra.err = e->qa.err + 1;
     ra.deadline = e->ar_deadline;
     ra.mode = !multi ? 0 : (xgmi ? 2 : 1);
-    ra.fc_in_step = fc_in_step_for(e, B) ? 1 : 0;
+    const bool fc = fc_in_step_for(e, B);
+    ra.fc_in_step = pks::ra_flags(fc, false, 0, chunk);
     ra.seg_ch = seg_ch(e);
-    if (pks_live(B) > share_budget(e)) {  // (set_shared_device already refused batch_max; kept as the last guard)
-      g_err = "persistent engine: " + std::to_string(pks_live(B)) + " step workgroups (batch " + std::to_string(B) +
-              ") exceed the co-residency budget of " + std::to_string(share_budget(e)) + " per rank";
-      return -1;
-    }
-    const dim3 grid(pks_grid(B) + (ra.fc_in_step ? pks::N_FCW : 0));
-    if (e->bf)
-      hipLaunchKernelGGL(pks::k_pks_step<0>, grid, dim3(pks::NTH), pks::Plan<0>::TOTAL, e->st, cx, e->qa, ra);
-    else
-      hipLaunchKernelGGL(pks::k_pks_step<1>, grid, dim3(pks::NTH), pks::Plan<1>::TOTAL, e->st, cx, e->qa, ra);
-    hipLaunchKernelGGL(pks::k_pks_reduce_ar, dim3(reduce_grid(e, pks::reduce_segments(ra.fc_in_step, ra.seg_ch) + 1)),
+    hipLaunchKernelGGL(pks::k_pks_reduce_ar, dim3(reduce_grid(e, pks::reduce_segments(fc, ra.seg_ch) + 1)),
                        dim3(256), pks::stage_floats(B) * 4, e->st, cx, e->qa, B * pks::S, ra);
   }
   if (multi && !xgmi) {  // RCCL (comm_mode 0, captured) or the host (comm_mode 1, between parts 1 and 2)
@@ -351,8 +385,28 @@ static int enqueue_step_persistent(Engine* e, int B, int part) {
   return 0;
 }
 
+// One step followed by its own reduction (a chunk of 1): eager runs, the host all-reduce, RCCL.
+static int enqueue_step_persistent(Engine* e, int B, int part) {
+  if (part != 2 && enqueue_pks_step(e, B, 0, false)) return -1;
+  return enqueue_pks_reduce(e, B, 1, part);
+}
+
 // Enqueue one full training step for batch B on e->st (and e->cst for the collectives).
-static int enqueue_step(Engine* e, int B, int part = 0) {
+static int enqueue_step(Engine* e, int B, int part = 0);
+// Enqueue `chunk` consecutive steps: with the prologue reduction `chunk` step kernels and one reduction kernel (one
+// kernel boundary per step), else step + reduction each.
+static int enqueue_chunk(Engine* e, int B, int chunk) {
+  if (!prologue_ok(e, B)) {
+    for (int s = 0; s < chunk; ++s)
+      if (enqueue_step(e, B)) return -1;
+    return 0;
+  }
+  for (int s = 0; s < chunk; ++s)
+    if (enqueue_pks_step(e, B, s, s > 0)) return -1;
+  return enqueue_pks_reduce(e, B, chunk, 0);
+}
+
+static int enqueue_step(Engine* e, int B, int part) {
   if (e->persistent) return enqueue_step_persistent(e, B, part);
   Ctx cx = e->base;
   cx.B = B;
@@ -479,6 +533,7 @@ static int engine_init(Engine* e, const DcaInit* in, int n_indices) {
     }
     e->resident = resident;
     if (const char* fo = getenv("DCA_PKS_FC_IN_STEP")) e->fc_in_step = fo[0] != '0';
+    if (const char* po = getenv("DCA_PKS_PROLOGUE")) e->prologue = po[0] != '0';
   }
   HIPCK(hipStreamCreateWithFlags(&e->st, hipStreamNonBlocking));
   HIPCK(hipStreamCreateWithFlags(&e->cst, hipStreamNonBlocking));
@@ -656,7 +711,7 @@ int dca_engine_set_epoch(void* h, int device_epoch, int flag_epoch) {
   HIPCK(hipMemcpy(e->qa.epoch, &device_epoch, sizeof(int), hipMemcpyHostToDevice));
   HIPCK(hipMemset(e->qa.gran, 0, 2 * (size_t)dca::pks::LMAX * dca::pks::GSTR * 8));
   HIPCK(hipMemset(e->qa.bnx, 0, 2 * (size_t)dca::pks::LMAX * 64 * 4));
-  HIPCK(hipMemset(e->qa.hdone, 0, (size_t)dca::pks::LMAX * 8));
+  HIPCK(hipMemset(e->qa.hdone, 0, (size_t)dca::pks::LMAX * 8 + 256 * 8));
   if (e->xregion) {
     std::vector<int> f(dca::xg::FLAG_BYTES / 4, flag_epoch);
     HIPCK(hipMemcpy(e->xregion, f.data(), dca::xg::FLAG_BYTES, hipMemcpyHostToDevice));                 // k_xgmi_ar_sgd
@@ -712,8 +767,7 @@ static hipGraphExec_t capture_graph(Engine* e, int B, int chunk) {
     g_err = std::string("hipStreamBeginCapture: ") + hipGetErrorString(ec);
     return nullptr;
   }
-  int rc = 0;
-  for (int s = 0; s < chunk && !rc; ++s) rc = dca::enqueue_step(e, B);
+  const int rc = dca::enqueue_chunk(e, B, chunk);
   ec = hipStreamEndCapture(e->st, &g);
   if (rc) {
     if (ec == hipSuccess) (void)hipGraphDestroy(g);

@@ -526,7 +526,8 @@ __device__ __forceinline__ void xr_row(char* XR, int xrow, int q, int ch, const 
 // weight staging: the NP planes (hi, lo) of one conv weight, stored in global memory in the LDS record layout
 // (common.h PKW_*), copied into WT by LDS-DMA -- no registers, no scratch; the issuing waves' vmcnt covers it.
 // 1 KB per wave instruction, chunks dealt round-robin to the waves; P = 0's 22.5 KB end in a half chunk.
-template <int P>
+// AUX: cache policy of the DMA loads (16 = sc1: the records were written in this launch by the prologue reduction)
+template <int P, int AUX = 0>
 __device__ __forceinline__ void wt_dma(char* wt, const unsigned short* src, int wv, int lane) {
   constexpr int BYTES = (P + 1) * PKW_PLANE * 2, NCH = (BYTES + 1023) / 1024;
   static_assert(BYTES == (P + 1) * Plan<P>::WT_PL, "record layout of pkw matches the LDS weight planes");
@@ -535,7 +536,7 @@ __device__ __forceinline__ void wt_dma(char* wt, const unsigned short* src, int 
     const int ck = wv + NW * m;
     if (ck < NCH && ck * 1024 + lane * 16 < BYTES)
       __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)((const char*)src + ck * 1024 + lane * 16),
-                                       (__attribute__((address_space(3))) void*)(wt + ck * 1024), 16, 0, 0);
+                                       (__attribute__((address_space(3))) void*)(wt + ck * 1024), 16, 0, AUX);
   }
 }
 
@@ -633,10 +634,26 @@ struct RedAr {
   float* st_dst;
   int st_n;
   int mode;
-  int fc_in_step;             // nonzero: the fc1 / fc-tail segments run on the step kernel's fc workers
+  int fc_in_step;             // flags (ra_fc / ra_prev / ra_s / ra_chunk): bit 0 the fc1 / fc-tail segments run on
+                              // the step kernel's fc workers; bit 1 (step kernel) the prologue reduction of the
+                              // previous step runs in this launch; bits 8..15 the step's index s in its chunk;
+                              // bits 16..23 (reduction kernel) the chunk length C it closes.  One int: a larger
+                              // kernel argument once pushed the 256-VGPR step kernel into scratch spills
   int seg_ch;                 // segment layout (seg_layout): 64, 128 or 256
 };
 
+__host__ __device__ __forceinline__ int ra_fc(const RedAr& ra) { return ra.fc_in_step & 1; }
+__host__ __device__ __forceinline__ int ra_prev(const RedAr& ra) { return (ra.fc_in_step >> 1) & 1; }
+__host__ __device__ __forceinline__ int ra_s(const RedAr& ra) { return (ra.fc_in_step >> 8) & 255; }
+__host__ __device__ __forceinline__ int ra_chunk(const RedAr& ra) { return (ra.fc_in_step >> 16) & 255; }
+__host__ __device__ __forceinline__ int ra_flags(int fc, int prev, int s, int chunk) {
+  return (fc ? 1 : 0) | (prev ? 2 : 0) | (s << 8) | (chunk << 16);
+}
+// The step's epoch and batch position: a chunk of C steps shares one device epoch / cursor base, advanced by C
+// (and C x B) by the reduction kernel that closes the chunk; step s of the chunk runs at base + s.
+__device__ __forceinline__ int step_epoch(const Args& pa, const RedAr& ra) {
+  return (int)(((unsigned)*pa.epoch + (unsigned)ra_s(ra)) % EPOCH_WRAP);
+}
 __device__ __forceinline__ char* rbase(const RedAr& ra, int q) { return ra.peers.base[q] + xg::REGION_BYTES; }
 __device__ __forceinline__ float* rslab(const RedAr& ra, int q, int par) {
   return (float*)(rbase(ra, q) + xg::FLAG_BYTES) + (size_t)par * xg::SLAB_FLOATS;
@@ -759,9 +776,33 @@ __device__ __forceinline__ void seg_chunk(const Ctx& cx, const Args& pa, const S
   }
 }
 
+// Write-through stores of the SGD results when the readers run in the SAME launch (the prologue reduction: the
+// step workgroups read the new weights after the ready granules, with sc1 loads): the fp32 parameter, the CC4 base,
+// and the sliced engine's bf16 hi / lo weight records (csrc/netresdeep_kernels.hip derive_param, pkw part: the only
+// derived copies of the trunk / conv1 parameters the sliced engine has).
+__device__ __forceinline__ void st2b_wt(unsigned short* p, unsigned short v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void derive_pkw_wt(const Ctx& cx, int e, float w) {
+  const unsigned short hi = bfbits(w), lo = bfbits(w - __uint_as_float((unsigned)hi << 16));
+  if (e >= OFF_CONVW && e < OFF_CONVW + 9216) {
+    const int r = e - OFF_CONVW, co = r / 288, ci = (r / 9) % 32, tap = r % 9;
+    const int fo = pkw_elem(tap * 32 + co, ci), dofs = PKW_DGRAD + pkw_elem((8 - tap) * 32 + ci, co);
+    st2b_wt(cx.pkw + fo, hi);
+    st2b_wt(cx.pkw + PKW_PLANE + fo, lo);
+    st2b_wt(cx.pkw + dofs, hi);
+    st2b_wt(cx.pkw + PKW_PLANE + dofs, lo);
+  } else if (e >= OFF_C1W && e < OFF_C1W + 864) {
+    const int r = e - OFF_C1W, slot = swf_slot(r / 27, r % 27);
+    st2b_wt(cx.pkw + PKW_STEM + slot, hi);
+    st2b_wt(cx.pkw + PKW_STEM + 1536 + slot, lo);
+  }
+}
+
 // Segment b on this workgroup (NTH threads): reduce / compute into segv, exchange (mode 2), SGD.  LDS: segv
-// [SEG_MAX], red [NTH] f32x4, stage [stage_floats(B)], *s_ep.
-template <int NTH>
+// [SEG_MAX], red [NTH] f32x4, stage [stage_floats(B)], s_ep[2].  WT: the SGD results are read inside this launch
+// (prologue reduction; trunk / conv1 / BN-tail segments only).
+template <int NTH, bool WT = false>
 __device__ void seg_process(const Ctx& cx, const Args& pa, const RedAr& ra, int b, int nslab, float* segv,
                             f32x4* red, float* stage, int* s_ep, int sslot, int swg) {
   const int t = threadIdx.x, B = cx.B;
@@ -884,19 +925,29 @@ __device__ void seg_process(const Ctx& cx, const Args& pa, const RedAr& ra, int 
         wv = oldp;
         wv -= cx.lr * g * cx.inv_ws;  // same rounding as k_apply_sgd / k_xgmi_ar_sgd
       }
-      cx.params[pidx] = wv;
-      derive_param<true>(cx, pidx, wv);
+      if constexpr (WT) {
+        st1_wt(cx.params + pidx, wv);
+        derive_pkw_wt(cx, pidx, wv);
+      } else {
+        cx.params[pidx] = wv;
+        derive_param<true>(cx, pidx, wv);
+      }
     } else if (pidx <= -2) {  // CC4: rank 0's running stats become every rank's base (rides the all-reduce)
       const int kk = -2 - pidx;
       if (mode == 1) cx.grads[OFF_RS + kk] = g;
-      else if (mode == 2) cx.rs_base[kk] = g;
+      else if (mode == 2) {
+        if constexpr (WT) st1_wt(cx.rs_base + kk, g);
+        else cx.rs_base[kk] = g;
+      }
     }
   }
   DCA_STAMP(cx, sslot, swg, 3);
 }
 
-// batch-mean loss, cursor, step / BN-batch counters, epoch: independent of every segment, so it runs beside them
-__device__ __forceinline__ void pks_bookkeeping(const Ctx& cx, const Args& pa) {
+// The finished step's batch-mean loss, step / BN-batch counters: independent of every segment, so it runs beside
+// them.  chunk > 0 (the reduction kernel closing a chunk of `chunk` steps): also the epoch / cursor base, advanced by
+// the chunk; 0 (a prologue reduction inside the chunk): they stay (the chunk's steps run at base + s).
+__device__ __forceinline__ void pks_bookkeeping(const Ctx& cx, const Args& pa, int chunk) {
   const int t = threadIdx.x, B = cx.B;
   if (t >= 64) return;
   float l = t < B ? cx.HLOSS[t] : 0.f;  // B <= 64
@@ -914,10 +965,12 @@ __device__ __forceinline__ void pks_bookkeeping(const Ctx& cx, const Args& pa) {
   for (int m = 1; m < 64; m <<= 1) l += __shfl_xor(l, m);  // fixed tree: identical every step
   if (t == 0) {
     *cx.loss_acc = acc + (double)(l / (float)B);
-    *cx.cursor = cur + B;
     *cx.step_count = stp + 1;
     *cx.nbt = nb + NBLK;  // BatchNorm num_batches_tracked: +1 per application
-    *pa.epoch = (int)(((unsigned)ep + 1u) % EPOCH_WRAP);
+    if (chunk > 0) {
+      *cx.cursor = cur + chunk * B;
+      *pa.epoch = (int)(((unsigned)ep + (unsigned)chunk) % EPOCH_WRAP);
+    }
   }
 }
 
@@ -927,7 +980,7 @@ __device__ __forceinline__ void pks_bookkeeping(const Ctx& cx, const Args& pa) {
 template <int P>
 __device__ void fc_segment(const Ctx& cx, const Args& pa, const RedAr& ra, int fb, char* smem) {
   const int t = threadIdx.x, lane = t & 63, G = cx.B * S;
-  const int epoch = *pa.epoch;
+  const int epoch = step_epoch(pa, ra);
   DCA_STAMP(cx, 9, fb, 0);
   if (t < 64) {  // ONE wave polls (sleeping between passes): the CU's other work is the step's, on other CUs
     const unsigned tag = tagof(epoch, RND_HDONE);
@@ -952,6 +1005,60 @@ __device__ void fc_segment(const Ctx& cx, const Args& pa, const RedAr& ra, int f
   int* s_ep = (int*)(smem + SEG_MAX * 4 + NTH * 16 + stage_floats(cx.B) * 4);  // [2]
   const SegLayout Ls = seg_layout(ra.seg_ch);
   seg_process<NTH>(cx, pa, ra, fb < R_FC1 ? Ls.r_ts + fb : Ls.fct, G, segv, red, stage, s_ep, 9, fb);
+}
+
+// ============================================================================================================
+// Prologue reduction (k_pks_step with ra_prev): the gradient segments of the PREVIOUS step -- its trunk / conv1 chunks
+// and the BN tail, i.e. what k_pks_reduce_ar would do after it -- run at the start of this launch on the reducer
+// workgroups (the fc workers first, then extras), while the step workgroups stage their input images.  Each segment
+// is reduced, exchanged (xGMI), applied (SGD, write-through: the readers are in this launch) and announced by a
+// ready granule {tagof(epoch, RND_RDONE)}; the step workgroups wait for all of them before they load the weights
+// and step constants (sc1 loads).  A chunk of C steps is then C step launches and ONE reduction kernel (the last
+// step's segments, closing the chunk): one kernel boundary per step instead of two (MI355X guide "boundary",
+// ~1.8 us each), and the reduction's own latency overlaps the stem's input staging.  The previous step's slabs,
+// BN-affine gradient and losses are read here before any step workgroup of this launch can write them again (they
+// write only after the ready wait).  Not used with RCCL / host all-reduce (mode 1: the collective must sit between
+// the reduction and the SGD) nor when the reducers do not fit beside the step (engine.hip prologue_ok).
+// ============================================================================================================
+constexpr int RND_RDONE = 29;  // tag round of the ready granules
+__host__ __device__ inline int prologue_segments(int seg_ch) { return seg_layout(seg_ch).r_ts + 1; }
+__device__ __forceinline__ unsigned long long* rdone(const Args& pa) { return pa.hdone + LMAX; }
+
+template <int P>
+__device__ void prologue_reduce(const Ctx& cx, const Args& pa, const RedAr& ra, int r, char* smem) {
+  const SegLayout Ls = seg_layout(ra.seg_ch);
+  const int nred = prologue_segments(ra.seg_ch);
+  if (r >= nred) return;
+  const int epoch = step_epoch(pa, ra);
+  float* segv = (float*)smem;
+  f32x4* red = (f32x4*)(smem + SEG_MAX * 4);
+  float* stage = (float*)(smem + SEG_MAX * 4 + NTH * 16);
+  int* s_ep = (int*)(smem + SEG_MAX * 4 + NTH * 16 + stage_floats(cx.B) * 4);  // [2]
+  DCA_STAMP(cx, 8, r, 0);
+  seg_process<NTH, true>(cx, pa, ra, r < Ls.r_ts ? r : Ls.bnt, cx.B * S, segv, red, stage, s_ep, 8, r);
+  if (r == nred - 1) pks_bookkeeping(cx, pa, 0);  // the previous step's loss and counters
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this thread's write-through stores are performed
+  __syncthreads();                                    // ... and every thread's of this workgroup
+  if (threadIdx.x == 0) gput(rdone(pa) + r, tagof(epoch, RND_RDONE), 0.f);
+}
+// Step workgroups: wait (one wave, bounded) until every reducer of this launch has announced its segment.
+__device__ __forceinline__ void wait_ready(const Args& pa, const RedAr& ra, int epoch) {
+  const int t = threadIdx.x, lane = t & 63;
+  if (t < 64) {
+    const int nred = prologue_segments(ra.seg_ch);
+    const unsigned tag = tagof(epoch, RND_RDONE);
+    for (unsigned spins = 0;; ++spins) {
+      bool ok = true;
+      for (int k = lane; k < nred; k += 64)
+        ok &= (unsigned)(__hip_atomic_load(rdone(pa) + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >> 32) == tag;
+      if (__all(ok)) break;
+      if (spins >= SPIN_LIMIT) {
+        if (lane == 0) atomicOr(pa.err, 1u << 28);
+        break;
+      }
+    }
+  }
+  __syncthreads();
 }
 
 constexpr int P_KSHIFT = 906;  // misc: [10][32] BN shifts (last step's batch means)
@@ -981,10 +1088,11 @@ __device__ __forceinline__ void step_main(const Ctx& cx, const Args& pa, const R
   char* U = smem + PL::O_U;
   char* WT = U + PL::U_WT;
   char* XR = U + PL::U_XR;
-  const int epoch = *pa.epoch;
+  const int epoch = step_epoch(pa, ra);
   const int par = epoch & 1;
+  const bool prev = ra_prev(ra);  // the previous step's gradient segments are applied in this launch (prologue)
   const uint8_t* my_img = pa.simg + (size_t)(par * 64 + n) * 3072;
-  const int next_id = sample_id(cx, B + n);
+  const int next_id = sample_id(cx, (ra_s(ra) + 1) * B + n);
   const float Ntot = (float)B * 256.f;
   const unsigned short* pkw = (const unsigned short*)cx.pkw;
   const size_t img8 = (size_t)n * 8192 + (size_t)row * 512;  // this row inside an image of a block's tensor
@@ -1007,6 +1115,16 @@ __device__ __forceinline__ void step_main(const Ctx& cx, const Args& pa, const R
     // [544,864), b2 [864,874), conv1 bias [874,906), BN shifts [906,1226)
     constexpr int NKC = 842, KCM = (NKC + NTH - 1) / NTH;
     float kc[KCM];
+    int lab = pa.slab[par * 64 + n];
+    // input words: thread t < 112 -> xin4 row j = t >> 3 (image row 8s-3+j), 4 columns 4 (t & 7) .., 3 channels
+    const int jr = (t >> 3) < 14 ? (t >> 3) : 13, yimg = 8 * s - 3 + jr, xq = t & 7;
+    const bool ivalid = t < 112 && yimg >= 0 && yimg < 32;
+    const unsigned* imw = (const unsigned*)my_img;
+    const int yc = yimg < 0 ? 0 : (yimg > 31 ? 31 : yimg);
+    unsigned iw0 = imw[yc * 8 + xq], iw1 = imw[256 + yc * 8 + xq], iw2 = imw[512 + yc * 8 + xq];
+    // prologue reduction: the weights / constants below are the reducers' (this launch): wait for their ready
+    // granules (the image loads above stay in flight), then read them with sc1 loads
+    if (prev) wait_ready(pa, ra, epoch);
 #pragma unroll
     for (int m = 0; m < KCM; ++m) {
       const int k = min(t + NTH * m, NKC - 1);
@@ -1020,23 +1138,22 @@ __device__ __forceinline__ void step_main(const Ctx& cx, const Args& pa, const R
                        : k < 490 ? cx.params + OFF_FC2B + (k - 480)
                        : k < 522 ? cx.params + OFF_C1B + (k - 490)
                                  : (const float*)cx.STATS + 2 * (k - 522);
-      kc[m] = *src;
+      kc[m] = prev ? __hip_atomic_load(src, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : *src;
     }
-    int lab = pa.slab[par * 64 + n];
-    // input words: thread t < 112 -> xin4 row j = t >> 3 (image row 8s-3+j), 4 columns 4 (t & 7) .., 3 channels
-    const int jr = (t >> 3) < 14 ? (t >> 3) : 13, yimg = 8 * s - 3 + jr, xq = t & 7;
-    const bool ivalid = t < 112 && yimg >= 0 && yimg < 32;
-    const unsigned* imw = (const unsigned*)my_img;
-    const int yc = yimg < 0 ? 0 : (yimg > 31 ? 31 : yimg);
-    unsigned iw0 = imw[yc * 8 + xq], iw1 = imw[256 + yc * 8 + xq], iw2 = imw[512 + yc * 8 + xq];
-    wt_dma<P>(WT, pkw, wv, lane);  // forward trunk weights, records [tap][co] x ci (hi, lo)
+    // forward trunk weights, records [tap][co] x ci (hi, lo)
+    if (prev) wt_dma<P, 16>(WT, pkw, wv, lane);
+    else wt_dma<P>(WT, pkw, wv, lane);
     uint2 bwr[P + 1][2][3];        // conv1 B fragments: lane (co = 16h + c, k-group q) of MFMA m
 #pragma unroll
     for (int p = 0; p <= P; ++p)
 #pragma unroll
       for (int h = 0; h < 2; ++h)
 #pragma unroll
-        for (int m = 0; m < 3; ++m) bwr[p][h][m] = ((const uint2*)(pkw + PKW_STEM + p * 1536))[(h * 3 + m) * 64 + lane];
+        for (int m = 0; m < 3; ++m) {
+          const unsigned long long* bp = (const unsigned long long*)(pkw + PKW_STEM + p * 1536) + (h * 3 + m) * 64 + lane;
+          const unsigned long long bv = prev ? __hip_atomic_load(bp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : *bp;
+          bwr[p][h][m] = uint2{(unsigned)bv, (unsigned)(bv >> 32)};
+        }
 #pragma unroll
     for (int m = 0; m < KCM; ++m) pin(kc[m]);
     pin(lab);
@@ -1193,7 +1310,10 @@ __device__ __forceinline__ void step_main(const Ctx& cx, const Args& pa, const R
     // AFTER an exchange: vmcnt is in order, so loads in flight when a sweep starts hold up its first pass (register
     // loads before the exchange + an LDS store a block later cost ~1.4 us in each of the two blocks, stamps)
     if (i == NBLK - 4) w1_dma<P>(cx, U + PL::U_W1, s, wv, lane);
-    if (i == NBLK - 1) wt_dma<P>(WT, pkw + PKW_DGRAD, wv, lane);  // dgrad weights, records [8 - tap][ci] x co
+    if (i == NBLK - 1) {  // dgrad weights, records [8 - tap][ci] x co (sc1: the prologue reduction wrote them)
+      if (prev) wt_dma<P, 16>(WT, pkw + PKW_DGRAD, wv, lane);
+      else wt_dma<P>(WT, pkw + PKW_DGRAD, wv, lane);
+    }
     lds_barrier();
     if (i == DCA_DETAIL_FWD) DCA_STAMP(cx, 6, L, 3);
     if (halo) st4r_wt(pa.yh + ((size_t)(i * LMAX + L) * 2 + hwhich) * 512, hh, lane, yo);
@@ -1488,7 +1608,7 @@ __device__ __forceinline__ void step_main(const Ctx& cx, const Args& pa, const R
     lds_barrier();
     // head outputs done: every wave's head stores (write-through) were retired by its sweep's waits (vmcnt counts
     // stores and loads in order) before this barrier -> one granule releases the fc workers
-    if (i == NBLK - 1 && ra.fc_in_step && t == 0) gput(pa.hdone + L, tagof(epoch, RND_HDONE), 0.f);
+    if (i == NBLK - 1 && ra_fc(ra) && t == 0) gput(pa.hdone + L, tagof(epoch, RND_HDONE), 0.f);
     if (i == DCA_DETAIL_BWD) DCA_STAMP(cx, 7, L, 5);
     if (L == 0 && t < 32) {  // BN affine gradients: dbeta = sum dz, dgamma = sum dz * xhat
       dbet += slot_total(cred, t);
@@ -1663,10 +1783,16 @@ __global__ void __launch_bounds__(NTH) k_pks_step(Ctx cx, Args pa, RedAr ra) {
     step_main<P>(cx, pa, ra, smem);
     return;
   }
-  // past the main grid: the fc workers (only with ra.fc_in_step); one fc segment each in a training step (nfw ==
-  // N_FCW); the self-test on a shared device launches fewer workers (its per-rank CU budget), which then take the
-  // segments in turn
-  const int fb = (int)blockIdx.x - gmain, nfw = min((int)gridDim.x - gmain, N_FCW);
+  // past the main grid: the reducers of the prologue reduction (ra_prev; the previous step's segments), then the fc
+  // workers (ra_fc); one fc segment each in a training step (nfw == N_FCW); the self-test on a shared device launches
+  // fewer workers (its per-rank CU budget), which then take the segments in turn
+  const int fb = (int)blockIdx.x - gmain;
+  if (ra_prev(ra)) {
+    prologue_reduce<P>(cx, pa, ra, fb, smem);
+    __syncthreads();  // its LDS is reused by the fc segment
+  }
+  if (!ra_fc(ra)) return;
+  const int nfw = min((int)gridDim.x - gmain, N_FCW);
   for (int f = fb; f < N_FCW; f += nfw) {
     if (f != fb) __syncthreads();
     fc_segment<P>(cx, pa, ra, f, smem);
@@ -1677,7 +1803,7 @@ __global__ void __launch_bounds__(NTH) k_pks_step(Ctx cx, Args pa, RedAr ra) {
 // The first batch after the host moved the cursor or replaced the index list (grid 64 x 256): image and label of
 // batch position b into the current staging parity (every later batch is staged by the step before it).
 __global__ void __launch_bounds__(256) k_pks_prime(Ctx cx, Args pa) {
-  const int t = threadIdx.x, b = blockIdx.x, par = *pa.epoch & 1, id = sample_id(cx, b);
+  const int t = threadIdx.x, b = blockIdx.x, par = *pa.epoch & 1, id = sample_id(cx, b);  // (a chunk's first step)
   if (t < 192)
     ((uint4*)(pa.simg + (size_t)(par * 64 + b) * 3072))[t] = ((const uint4*)(cx.data + (size_t)id * 3072))[t];
   if (t == 192) pa.slab[par * 64 + b] = cx.labels[id];
@@ -1705,24 +1831,24 @@ __global__ void __launch_bounds__(256) k_pks_reduce_ar(Ctx cx, Args pa, int nsla
   __shared__ f32x4 red[256];
   extern __shared__ __attribute__((aligned(16))) float stage[];
   __shared__ int s_ep[2];
-  const int nred = reduce_segments(ra.fc_in_step, ra.seg_ch), b = blockIdx.x, nwg = gridDim.x;
+  const int nred = reduce_segments(ra_fc(ra), ra.seg_ch), b = blockIdx.x, nwg = gridDim.x;
   const SegLayout Ls = seg_layout(ra.seg_ch);
   if (nwg > nred) {
     if (b >= nred) {
-      if (ra.mode != 3) pks_bookkeeping(cx, pa);
+      if (ra.mode != 3) pks_bookkeeping(cx, pa, ra_chunk(ra));
       return;
     }
-    const int seg = !ra.fc_in_step || b < Ls.r_ts ? b : Ls.bnt;
+    const int seg = !ra_fc(ra) || b < Ls.r_ts ? b : Ls.bnt;
     DCA_STAMP(cx, 8, b, 0);
     seg_process<256>(cx, pa, ra, seg, nslab, segv, red, stage, s_ep, 8, b);
     return;
   }
   for (int k = b; k < nred; k += nwg) {
-    const int seg = !ra.fc_in_step || k < Ls.r_ts ? k : Ls.bnt;
+    const int seg = !ra_fc(ra) || k < Ls.r_ts ? k : Ls.bnt;
     seg_process<256>(cx, pa, ra, seg, nslab, segv, red, stage, s_ep, 8, k);
     __syncthreads();  // segv / red / stage are reused by the next segment
   }
-  if (b == nwg - 1 && ra.mode != 3) pks_bookkeeping(cx, pa);
+  if (b == nwg - 1 && ra.mode != 3) pks_bookkeeping(cx, pa, ra_chunk(ra));
 }
 
 }  // namespace pks

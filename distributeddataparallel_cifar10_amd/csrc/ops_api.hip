@@ -214,7 +214,7 @@ using namespace dca::ops;
 extern "C" {
 
 const char* dca_ops_last_error() { return g_err.c_str(); }
-int dca_ops_abi_version() { return 9; }
+int dca_ops_abi_version() { return 10; }
 
 // Must match ops/_native.py::GemmArgs.
 int dca_ops_gemm(const GemmArgs* a, void* stream) {
@@ -244,11 +244,7 @@ int dca_ops_gemm(const GemmArgs* a, void* stream) {
     REQUIRE(g.conv != 2 || (g.K == pix && g.N == kc && !g.tb), "gemm: conv B shape mismatch");
   }
   REQUIRE(!g.col_stats || (g.stats_shift && g.splits <= 1), "gemm: column stats need a shift and no split-K");
-  REQUIRE(!g.bnb_part || (g.bnb_x && g.bnb_stats && g.bnb_gamma && g.bnb_beta && !g.col_stats && g.splits <= 1 &&
-                          g.out_bf16 && g.N % 8 == 0 && g.ldc % 8 == 0 && g.wperm_T <= 0 && !g.fp8),
-          "gemm: fused BN-backward statistics need a bf16 output with N % 8 == 0 and no split-K");
-  REQUIRE(!g.bnb_part || (g.beta == 0.f && !g.bias && !g.relu), "gemm: fused BN-backward statistics: plain output");
-  REQUIRE(!g.beta_mask || (g.beta_src && g.beta_src != g.C && g.beta != 0.f && g.out_bf16 && !g.ta && !g.bnb_part &&
+  REQUIRE(!g.beta_mask || (g.beta_src && g.beta_src != g.C && g.beta != 0.f && g.out_bf16 && !g.ta &&
                            g.splits <= 1 && g.wperm_T <= 0 && g.orow_S <= 0 && g.N % 8 == 0 && g.ldc % 8 == 0 &&
                            ((uintptr_t)g.beta_src & 15) == 0),
           "gemm: a masked accumulation source needs a separate 16-B aligned bf16 source, beta != 0 and a plain "
@@ -264,10 +260,6 @@ int dca_ops_gemm(const GemmArgs* a, void* stream) {
     OPCK(hipFuncSetAttribute((const void*)k_gemm<true, 128>, hipFuncAttributeMaxDynamicSharedMemorySize,
                              GemmTile<128>::LDS));
     OPCK(hipFuncSetAttribute((const void*)k_gemm<false, 64>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                             GemmTile<64>::LDS));
-    OPCK(hipFuncSetAttribute((const void*)k_gemm<false, 128, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                             GemmTile<128>::LDS));
-    OPCK(hipFuncSetAttribute((const void*)k_gemm<false, 64, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
                              GemmTile<64>::LDS));
     OPCK(hipFuncSetAttribute((const void*)k_gemm<true, 64>, hipFuncAttributeMaxDynamicSharedMemorySize,
                              GemmTile<64>::LDS));
@@ -288,10 +280,7 @@ int dca_ops_gemm(const GemmArgs* a, void* stream) {
 #undef WPP_ATTR
 #define GLDS_ATTR(F8, BNV, NWV)                                                                          \
   OPCK(hipFuncSetAttribute((const void*)k_gemm_glds<F8, BNV, NWV>, hipFuncAttributeMaxDynamicSharedMemorySize, \
-                           4 * GemmTile<BNV>::BUF));                                                          \
-  if (!F8)                                                                                                   \
-    OPCK(hipFuncSetAttribute((const void*)k_gemm_glds<false, BNV, NWV, true>,                               \
-                             hipFuncAttributeMaxDynamicSharedMemorySize, 4 * GemmTile<BNV>::BUF))
+                           4 * GemmTile<BNV>::BUF))
       GLDS_ATTR(false, 128, 4);
       GLDS_ATTR(true, 128, 4);
       GLDS_ATTR(false, 64, 4);
@@ -415,7 +404,7 @@ int dca_ops_gemm(const GemmArgs* a, void* stream) {
                                                (g.beta == 0.f || g.K <= 128 || (g.beta_mask && g.K <= 256)))));
     const bool st_ok = sk != 0 && shape_ok && !g.fp8 && !g.tb && g.splits == 1 && g.wperm_T <= 0 && g.orow_S <= 0 &&
                        !(conv && g.beta_mask) &&
-                       !g.bnb_part && !g.relu && g.out_bf16 && g.N % 64 == 0 && g.N <= 2048 && g.K % 64 == 0 &&
+                       !g.relu && g.out_bf16 && g.N % 64 == 0 && g.N <= 2048 && g.K % 64 == 0 &&
                        g.K > 0 && g.M > 0 && g.ldb % 8 == 0 && g.ldc % 8 == 0 && g.ldb >= g.K && g.ldc >= g.N &&
                        ((uintptr_t)g.A & 15) == 0 && ((uintptr_t)g.B & 15) == 0 && ((uintptr_t)g.C & 15) == 0 &&
                        ab < (1LL << 31) && bb < (1LL << 31) && cbytes < (1LL << 31) &&
@@ -466,7 +455,7 @@ int dca_ops_gemm(const GemmArgs* a, void* stream) {
     // 16 MFMAs per barrier interval do not cover the other group's fragment loads; DCA_OPS_PP=1 only)
     const bool pp_shape = ppk == 1 || (ppk == 2 && ppbn == 256 && g.N % 256 == 0 && pp_tiles >= 160 && g.K >= 1024);
     const bool pp = pp_shape && !g.fp8 && !g.ta && !g.tb && g.splits == 1 && g.wperm_T <= 0 && g.orow_S <= 0 &&
-                    !g.bnb_part && g.M >= 256 && g.N >= 128 && g.K >= 256 && ab < (1LL << 31) && bb < (1LL << 31) &&
+                    g.M >= 256 && g.N >= 128 && g.K >= 256 && ab < (1LL << 31) && bb < (1LL << 31) &&
                     (long)g.ldb * 2 % 16 == 0 && ((uintptr_t)g.A & 15) == 0 && ((uintptr_t)g.B & 15) == 0 &&
                     (g.conv == 1 ? (g.cC % 64 == 0 && g.cKH * g.cKW <= 32 && g.M < (1 << 24))
                                  : (g.conv == 0 && (long)g.lda * 2 % 16 == 0 && (long)g.K * 2 % 16 == 0));
@@ -510,9 +499,6 @@ int dca_ops_gemm(const GemmArgs* a, void* stream) {
       if (g.fp8) {
         if (w8) hipLaunchKernelGGL((k_gemm_glds<true, 64, 8>), grid, blk, l64, st, g);
         else hipLaunchKernelGGL((k_gemm_glds<true, 64, 4>), grid, blk, l64, st, g);
-      } else if (g.bnb_part) {
-        if (w8) hipLaunchKernelGGL((k_gemm_glds<false, 64, 8, true>), grid, blk, l64, st, g);
-        else hipLaunchKernelGGL((k_gemm_glds<false, 64, 4, true>), grid, blk, l64, st, g);
       } else {
         if (w8) hipLaunchKernelGGL((k_gemm_glds<false, 64, 8>), grid, blk, l64, st, g);
         else hipLaunchKernelGGL((k_gemm_glds<false, 64, 4>), grid, blk, l64, st, g);
@@ -521,9 +507,6 @@ int dca_ops_gemm(const GemmArgs* a, void* stream) {
       if (g.fp8) {
         if (w8) hipLaunchKernelGGL((k_gemm_glds<true, 128, 8>), grid, blk, l128, st, g);
         else hipLaunchKernelGGL((k_gemm_glds<true, 128, 4>), grid, blk, l128, st, g);
-      } else if (g.bnb_part) {
-        if (w8) hipLaunchKernelGGL((k_gemm_glds<false, 128, 8, true>), grid, blk, l128, st, g);
-        else hipLaunchKernelGGL((k_gemm_glds<false, 128, 4, true>), grid, blk, l128, st, g);
       } else {
         if (w8) hipLaunchKernelGGL((k_gemm_glds<false, 128, 8>), grid, blk, l128, st, g);
         else hipLaunchKernelGGL((k_gemm_glds<false, 128, 4>), grid, blk, l128, st, g);
@@ -532,12 +515,10 @@ int dca_ops_gemm(const GemmArgs* a, void* stream) {
   } else if (narrow) {
     const int lds = g.single ? GemmTile<64>::LDS_SINGLE : GemmTile<64>::LDS;
     if (g.fp8) hipLaunchKernelGGL((k_gemm<true, 64>), grid, dim3(GT), lds, st, g);
-    else if (g.bnb_part) hipLaunchKernelGGL((k_gemm<false, 64, true>), grid, dim3(GT), lds, st, g);
     else hipLaunchKernelGGL((k_gemm<false, 64>), grid, dim3(GT), lds, st, g);
   } else {
     const int lds = g.single ? GemmTile<128>::LDS_SINGLE : GemmTile<128>::LDS;
     if (g.fp8) hipLaunchKernelGGL((k_gemm<true, 128>), grid, dim3(GT), lds, st, g);
-    else if (g.bnb_part) hipLaunchKernelGGL((k_gemm<false, 128, true>), grid, dim3(GT), lds, st, g);
     else hipLaunchKernelGGL((k_gemm<false, 128>), grid, dim3(GT), lds, st, g);
   }
   if (g.splits > 1 || g.wperm_T > 0)
@@ -663,29 +644,6 @@ int dca_ops_bn_bwd(const void* dy, const void* x, const void* r, const float* st
     bn_bwd_apply_launch<8>(mode, false, M, C, st, (const bf16_t*)dy, (const bf16_t*)x, (const bf16_t*)r,
                            (const float2*)stats, gamma, beta, (const float2*)sums, (bf16_t*)dx, (bf16_t*)dr, M, C,
                            (const uint8_t*)mask);
-  OPCK(hipGetLastError());
-  return 0;
-}
-
-// The same backward when the statistics pass already ran in the producer of dy (the dgrad GEMM epilogue,
-// GemmArgs::bnb_part): nparts partial rows [nparts][C] of (sum dz, sum dz * xhat) -> finalize -> apply.
-int dca_ops_bn_bwd_parts(const void* dy, const void* x, const float* stats, const float* gamma, const float* beta,
-                         const float* part, int nparts, float* sums, float* dgamma, float* dbeta, void* dx, long M,
-                         int C, int accumulate, void* stream) {
-  REQUIRE(C % 8 == 0 && nparts > 0, "bn: C must be a multiple of 8");
-  hipStream_t st = (hipStream_t)stream;
-#define FIN(CW) hipLaunchKernelGGL((k_bn_bwd_finalize<CW, BN_FIN_NTH(CW)>), dim3((C + CW - 1) / CW), dim3(BN_FIN_NTH(CW)), 0, st, \
-                                   (const float2*)part, nparts, C, dgamma, dbeta, (float2*)sums, accumulate)
-  BN_FIN_DISPATCH(C, FIN);
-#undef FIN
-  if (C % 128 == 0)
-    bn_bwd_apply_launch<16>(BWD_RELU, bn_bwd_apply_fine(M, C), M, C, st, (const bf16_t*)dy, (const bf16_t*)x,
-                            (const bf16_t*)nullptr, (const float2*)stats, gamma, beta, (const float2*)sums,
-                            (bf16_t*)dx, (bf16_t*)nullptr, M, C, (const uint8_t*)nullptr);
-  else
-    bn_bwd_apply_launch<8>(BWD_RELU, false, M, C, st, (const bf16_t*)dy, (const bf16_t*)x, (const bf16_t*)nullptr,
-                           (const float2*)stats, gamma, beta, (const float2*)sums, (bf16_t*)dx, (bf16_t*)nullptr, M,
-                           C, (const uint8_t*)nullptr);
   OPCK(hipGetLastError());
   return 0;
 }

@@ -73,15 +73,6 @@ struct GemmArgs {
   // (n * orow_H + orow_S * i + orow_ph) * orow_W + orow_S * j + orow_pw of C -- the sub-pixel (parity class)
   // input gradients of a strided convolution written straight into dX
   int orow_S, orow_ph, orow_pw, orow_H, orow_W, orow_Ho, orow_Wo;
-  // fused BatchNorm-backward statistics (splits == 1, bf16 output, alpha only): the output is dL/d(out) of a
-  // BN + ReLU layer whose input x = bnb_x (same layout as C); per tile and column the partial sums of
-  // dz = out * [relu mask] and dz * xhat go to bnb_part[tile_m][N] -- that layer's backward statistics pass,
-  // done by the producer of dL/d(out) (ops BnLink)
-  const void* bnb_x;
-  const float* bnb_stats;  // [N] (mean, invstd)
-  const float* bnb_gamma;
-  const float* bnb_beta;
-  float2* bnb_part;
   // masked accumulation source (beta != 0, bf16 output): C = alpha A B + beta * (beta_src * mask) instead of
   // beta * C_old -- the residual gradient dout * [ReLU(bn3 + r) > 0] of a bottleneck, read from dout and the bn3
   // forward's bit mask (bit j of byte e / 8: element e of beta_src's [M][ldc] layout) so bn3's backward never writes
@@ -325,9 +316,7 @@ struct WaveGrid {  // NW waves as 2 (rows of 64) x NW/2 (column slices) over the
   static_assert(NF >= 1, "bad wave grid");
 };
 
-// BNB: the fused BN-backward statistics variant, kernels of their own (its registers must not raise the other
-// GEMMs' allocation); one column per thread, a pass over the staged fp32 tile after the output write
-template <int BN_, int NW = 4, bool BNB = false>
+template <int BN_, int NW = 4>
 __device__ __forceinline__ void gemm_epilogue(const GemmArgs& g, f32x4 (&acc)[4][WaveGrid<BN_, NW>::NF], char* smem,
                                               int m0, int n0, int tm, int ksplit) {
   using T = WaveGrid<BN_, NW>;
@@ -366,33 +355,8 @@ __device__ __forceinline__ void gemm_epilogue(const GemmArgs& g, f32x4 (&acc)[4]
     s1[e] = s2[e] = 0.f;
   }
   const bool full8 = col0 + 8 <= g.N && (g.ldc & 7) == 0;
-  constexpr int BRL = T::NT / BN_;  // BNB: row lanes of the one-column-per-thread statistics pass
-  const int bc = threadIdx.x % BN_, brl = threadIdx.x / BN_, bcol = n0 + bc;
-  float bmu = 0.f, bis = 0.f, bga = 0.f, bbe = 0.f, bs1 = 0.f, bs2 = 0.f;
-  if constexpr (BNB) {
-    if (bcol < g.N) {
-      bmu = g.bnb_stats[2 * bcol];
-      bis = g.bnb_stats[2 * bcol + 1];
-      bga = g.bnb_gamma[bcol];
-      bbe = g.bnb_beta[bcol];
-    }
-  }
-  constexpr int BRPT = BNB ? (GBM / 2) / BRL : 1;  // BNB rows per thread and half
-  unsigned short byv[BRPT];
 #pragma unroll 1
   for (int half = 0; half < 2; ++half) {
-    if constexpr (BNB) {  // this half's x values of the statistics pass, all in flight before the output write
-#pragma unroll
-      for (int k = 0; k < BRPT; ++k) {
-        const int row = min(m0 + half * 64 + brl + k * BRL, g.M - 1);
-        size_t orow = (size_t)row;
-        if (g.orow_S > 0) {
-          const int j = row % g.orow_Wo, t2 = row / g.orow_Wo, i = t2 % g.orow_Ho, n = t2 / g.orow_Ho;
-          orow = ((size_t)n * g.orow_H + g.orow_S * i + g.orow_ph) * g.orow_W + g.orow_S * j + g.orow_pw;
-        }
-        byv[k] = ((const unsigned short*)g.bnb_x)[orow * g.ldc + min(bcol, g.N - 1)];
-      }
-    }
     if (wr == half) {
 #pragma unroll
       for (int m = 0; m < 4; ++m)
@@ -476,36 +440,7 @@ __device__ __forceinline__ void gemm_epilogue(const GemmArgs& g, f32x4 (&acc)[4]
         }
       }
     }
-    if constexpr (BNB) {  // dz = (value as stored) * [relu(bn(x)) > 0], xhat from x at the same output position
-      if (bcol < g.N) {
-#pragma unroll
-        for (int k = 0; k < BRPT; ++k) {
-          const int r = brl + k * BRL;
-          if (m0 + half * 64 + r < g.M) {
-            const float d = bf2f(f2bf_rne(ct[cidx(r, bc)] * alpha));
-            const float xh = (bf2f(byv[k]) - bmu) * bis;
-            const float dz = xh * bga + bbe > 0.f ? d : 0.f;
-            bs1 += dz;
-            bs2 += dz * xh;
-          }
-        }
-      }
-    }
     __syncthreads();
-  }
-  if constexpr (BNB) {  // combine the row lanes of each column (fixed order)
-    float2* red = (float2*)smem;  // [BRL][BN_]
-    red[brl * BN_ + bc] = float2{bs1, bs2};
-    __syncthreads();
-    if (threadIdx.x < BN_ && bcol < g.N) {
-      float2 t = red[bc];
-      for (int k = 1; k < BRL; ++k) {
-        t.x += red[k * BN_ + bc].x;
-        t.y += red[k * BN_ + bc].y;
-      }
-      g.bnb_part[(size_t)tm * g.N + bcol] = t;
-    }
-    return;
   }
   if (g.col_stats) {  // combine the row lanes of each column group (fixed order), one float2 per column
     float2* red = (float2*)smem;  // [RL row lanes][BN_ cols]
@@ -524,7 +459,7 @@ __device__ __forceinline__ void gemm_epilogue(const GemmArgs& g, f32x4 (&acc)[4]
   }
 }
 
-template <bool FP8, int BN_, bool BNB = false>
+template <bool FP8, int BN_>
 __global__ void __launch_bounds__(GT) k_gemm(GemmArgs g) {
   using T = GemmTile<BN_>;
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -636,7 +571,7 @@ __global__ void __launch_bounds__(GT) k_gemm(GemmArgs g) {
     __syncthreads();
   }
 
-  gemm_epilogue<BN_, 4, BNB>(g, acc, smem, m0, n0, tm, ksplit);
+  gemm_epilogue<BN_, 4>(g, acc, smem, m0, n0, tm, ksplit);
 }
 
 
@@ -666,7 +601,7 @@ __device__ __forceinline__ void wait_vmcnt() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
 
-template <bool FP8, int BN_, int NW, bool BNB = false>
+template <bool FP8, int BN_, int NW>
 __global__ void __launch_bounds__(NW * 64) k_gemm_glds(GemmArgs g) {
   using T = GemmTile<BN_>;
   using Wg = WaveGrid<BN_, NW>;
@@ -918,7 +853,7 @@ __global__ void __launch_bounds__(NW * 64) k_gemm_glds(GemmArgs g) {
     __builtin_amdgcn_s_barrier();  // every wave is done reading buf before it is refilled
     asm volatile("" ::: "memory");
   }
-  gemm_epilogue<BN_, NW, BNB>(g, acc, smem, m0, n0, tm, ksplit);
+  gemm_epilogue<BN_, NW>(g, acc, smem, m0, n0, tm, ksplit);
 }
 
 // ---------------------------------------------------------------------------------------------------------

@@ -13,7 +13,7 @@ import torch
 
 from .. import build as _build
 
-ABI_VERSION = 9
+ABI_VERSION = 10
 _lock = threading.Lock()
 _lib = None
 
@@ -32,8 +32,7 @@ class GemmArgs(ctypes.Structure):
         ("stats_shift", c_void_p), ("amax_a", c_void_p), ("amax_b", c_void_p),
         ("wperm_C", c_int), ("wperm_Cpad", c_int), ("wperm_T", c_int), ("single", c_int),
         ("stages", c_int), ("orow_S", c_int), ("orow_ph", c_int), ("orow_pw", c_int), ("orow_H", c_int),
-        ("orow_W", c_int), ("orow_Ho", c_int), ("orow_Wo", c_int), ("bnb_x", c_void_p), ("bnb_stats", c_void_p),
-        ("bnb_gamma", c_void_p), ("bnb_beta", c_void_p), ("bnb_part", c_void_p),
+        ("orow_W", c_int), ("orow_Ho", c_int), ("orow_Wo", c_int),
         ("beta_src", c_void_p), ("beta_mask", c_void_p),
     ]
 
@@ -74,8 +73,6 @@ def _declare(lib):
     lib.dca_ops_bn_bwd.argtypes = [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                                    c_void_p, c_void_p, c_void_p, c_void_p, c_long, c_int, c_int, c_int, c_int,
                                    c_void_p, c_void_p]
-    lib.dca_ops_bn_bwd_parts.argtypes = [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_void_p,
-                                         c_void_p, c_void_p, c_void_p, c_long, c_int, c_int, c_void_p]
     lib.dca_ops_maxpool_fwd.argtypes = [c_void_p, c_void_p, c_void_p, P(PoolGeom), c_void_p]
     lib.dca_ops_maxpool_bwd.argtypes = [c_void_p, c_void_p, c_void_p, P(PoolGeom), c_void_p]
     lib.dca_ops_avgpool_fwd.argtypes = [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p]

@@ -19,10 +19,6 @@ import torch
 from . import _native as N
 
 
-# BnLink fusion (BN-backward statistics in the consumer's dgrad GEMM epilogue): off by default -- measured slower
-# at ResNet-50 batch 256 (8,417 vs 8,755 img/s: the epilogue's extra x reads and registers cost the dgrad GEMMs
-# more than the ~0.84 ms of statistics passes it removes); DCA_OPS_BNB_FUSE=1 turns it on
-_BNB_FUSE = os.environ.get("DCA_OPS_BNB_FUSE", "0") == "1"
 _BWD_TRACE = None  # diagnostics: a list to record the order of the fused conv-BN backward calls
 
 
@@ -40,7 +36,7 @@ def gemm(a: torch.Tensor, b: torch.Tensor, *, ta: bool = False, tb: bool = False
          beta: float = 0.0, splits: int = 0, alpha_dev: Optional[torch.Tensor] = None, conv: int = 0,
          geom=None, col_stats: Optional[torch.Tensor] = None, stats_shift: Optional[torch.Tensor] = None,
          mnk=None, amax_a: Optional[torch.Tensor] = None, amax_b: Optional[torch.Tensor] = None,
-         wperm=None, orow=None, bnb=None, beta_src: Optional[torch.Tensor] = None,
+         wperm=None, orow=None, beta_src: Optional[torch.Tensor] = None,
          beta_mask: Optional[torch.Tensor] = None) -> torch.Tensor:
     """C[M,N] = alpha * A(m,k) B(n,k) (+bias) (+beta*out) (ReLU).
 
@@ -52,9 +48,7 @@ def gemm(a: torch.Tensor, b: torch.Tensor, *, ta: bool = False, tb: bool = False
     wperm = (C, Cpad, T): weight-gradient output written straight into torch's [M, C, KH, KW] fp32 layout
     (``out``), GEMM column n = tap * Cpad + c; padded channels dropped.
     orow = (S, ph, pw, H, W, Ho, Wo): row m = pixel (n, i, j) of an Ho x Wo grid goes to row
-    (n H + S i + ph) W + S j + pw of ``out`` ([N H W, N_gemm]): a strided conv's sub-pixel input gradient.
-    bnb = (x, stats, gamma, beta, part): the output is dL/d(out) of a BN + ReLU layer with input x; the epilogue
-    writes that layer's backward statistics partials (sum dz, sum dz xhat) per 128-row tile into ``part``."""
+    (n H + S i + ph) W + S j + pw of ``out`` ([N H W, N_gemm]): a strided conv's sub-pixel input gradient."""
     _dev_check(a, b, bias, out)
     fp8 = a.dtype == torch.uint8
     if fp8 != (b.dtype == torch.uint8) or (not fp8 and (a.dtype != torch.bfloat16 or b.dtype != torch.bfloat16)):
@@ -84,7 +78,7 @@ def gemm(a: torch.Tensor, b: torch.Tensor, *, ta: bool = False, tb: bool = False
     if bias is not None and (bias.dtype != torch.float32 or bias.numel() != Nn):
         raise ValueError("gemm: bias must be fp32 [N]")
     tiles = math.ceil(M / 128) * math.ceil(Nn / 128)
-    if col_stats is not None or orow is not None or bnb is not None:
+    if col_stats is not None or orow is not None:
         splits = 1
     if splits <= 0:
         splits = 1
@@ -113,10 +107,6 @@ def gemm(a: torch.Tensor, b: torch.Tensor, *, ta: bool = False, tb: bool = False
         for f in ("N", "H", "W", "C", "KH", "KW", "Ho", "Wo"):
             setattr(args, "c" + f, getattr(geom, f))
         args.cS, args.cP = geom.stride, geom.pad
-    if bnb is not None:
-        bx, bst, bga, bbe, bpart = bnb
-        args.bnb_x, args.bnb_stats, args.bnb_gamma, args.bnb_beta, args.bnb_part = (
-            bx.data_ptr(), bst.data_ptr(), bga.data_ptr(), bbe.data_ptr(), bpart.data_ptr())
     if beta_mask is not None:  # C = A B + beta * (beta_src * mask bits): beta_src has C's [M, ldc] layout
         if beta_src is None or beta_src.dtype != torch.bfloat16 or not beta_src.is_contiguous() \
                 or beta_src.numel() != M * Nn or beta_mask.numel() * 8 != M * Nn or out.stride(0) != Nn:
@@ -643,13 +633,11 @@ def _unmask(src: torch.Tensor, mask: torch.Tensor) -> torch.Tensor:
     return (src.reshape(-1) * bits.view(-1).to(src.dtype)).view_as(src).contiguous()
 
 
-def _conv_bwd(dy, st, need_x: bool, need_w: bool, sink=None, x_join: Optional[GradJoin] = None, bnb=None):
+def _conv_bwd(dy, st, need_x: bool, need_w: bool, sink=None, x_join: Optional[GradJoin] = None):
     """(dx, dw) of a conv from dY [N,Ho,Wo,Cout] (any dtype) and the forward state.  The weight gradient is
     written by the GEMM's reduce pass directly in torch's [Cout, Cin, KH, KW] layout -- into ``sink`` (a flat
     gradient view, accumulated; dw returned as None) when given.  ``x_join``: the input is shared with another
-    consumer; its gradient is accumulated into (or seeds) the join's buffer (dx None until the last producer).
-    ``bnb``: a BnLink whose BN + ReLU layer produced this conv's input: when dx comes out of a GEMM epilogue,
-    that epilogue also emits the layer's backward statistics (link.part / link.nparts set)."""
+    consumer; its gradient is accumulated into (or seeds) the join's buffer (dx None until the last producer)."""
     g, (co, ci, kh, kw) = st["geom"], st["wshape"]
     packed = st.get("packed")
     M = g.N * g.Ho * g.Wo
@@ -664,24 +652,13 @@ def _conv_bwd(dy, st, need_x: bool, need_w: bool, sink=None, x_join: Optional[Gr
             masked = None
         beta = 1.0 if acc is not None or masked is not None else 0.0
         dst2 = acc.view(g.N * g.H * g.W, g.C) if acc is not None else None
-        if acc is not None or masked is not None or bnb is None or not bnb.ready or g.C % 8:
-            bnb = None
-
-        def bnb_args(rows, off):  # this GEMM's slice of the link's partial rows
-            if bnb is None:
-                return None
-            if bnb.part is None:
-                bnb.part = torch.empty(bnb.rows_total, g.C, 2, dtype=torch.float32, device=dy.device)
-            return (bnb.x, bnb.stats, bnb.gamma, bnb.beta, bnb.part[off:off + (rows + 127) // 128])
         if cols is not None and cols.data_ptr() == st["x"].data_ptr():  # 1x1 / stride 1: dX = dY . W
-            if bnb is not None:
-                bnb.rows_total = (M + 127) // 128
             msrc, mbits = (masked[0].view(M, g.C), masked[1]) if masked is not None else (None, None)
             if packed is not None and packed["dgrad"] is not None:  # W^T [Cin, Cout] from the pack: plain NT
-                dx = gemm(dyb, packed["dgrad"], out_dtype=torch.bfloat16, out=dst2, beta=beta, bnb=bnb_args(M, 0),
+                dx = gemm(dyb, packed["dgrad"], out_dtype=torch.bfloat16, out=dst2, beta=beta,
                           beta_src=msrc, beta_mask=mbits)
             else:
-                dx = gemm(dyb, st["wm"], tb=True, out_dtype=torch.bfloat16, out=dst2, beta=beta, bnb=bnb_args(M, 0),
+                dx = gemm(dyb, st["wm"], tb=True, out_dtype=torch.bfloat16, out=dst2, beta=beta,
                           beta_src=msrc, beta_mask=mbits)
             dx = dx.view(g.N, g.H, g.W, g.C)
         elif g.stride == 1 and co % 8 == 0 and kh == kw and g.pad <= kh - 1 and g.C == ci:
@@ -692,11 +669,8 @@ def _conv_bwd(dy, st, need_x: bool, need_w: bool, sink=None, x_join: Optional[Gr
                 wd = packed["dgrad"]
             else:
                 wd = st.get("w_master").flip(2, 3).permute(1, 2, 3, 0).reshape(ci, -1).to(torch.bfloat16).contiguous()
-            if bnb is not None:
-                bnb.rows_total = (g.N * g.H * g.W + 127) // 128
             dx = gemm(dyb.view(g.N, g.Ho, g.Wo, co), wd, conv=1, geom=gd, mnk=(g.N * g.H * g.W, ci, gd.K),
-                      out_dtype=torch.bfloat16, out=dst2, beta=beta,
-                      bnb=bnb_args(g.N * g.H * g.W, 0)).view(g.N, g.H, g.W, g.C)
+                      out_dtype=torch.bfloat16, out=dst2, beta=beta).view(g.N, g.H, g.W, g.C)
         elif (packed is not None and g.stride == 2 and g.H % 2 == 0 and g.W % 2 == 0 and g.C == ci
               and (packed.get("classes") or (kh == 1 and g.pad == 0 and packed["dgrad"] is not None))):
             # sub-pixel decomposition: each parity class of input pixels is a stride-1 implicit conv over dY whose
@@ -708,22 +682,14 @@ def _conv_bwd(dy, st, need_x: bool, need_w: bool, sink=None, x_join: Optional[Gr
             else:
                 dx = acc
             dy4 = dyb.view(g.N, g.Ho, g.Wo, co)
-            if bnb is not None and len(classes) != 4:  # (a 1x1/2 class leaves pixels of dX untouched: zeros)
-                bnb = None
-            if bnb is not None:
-                bnb.rows_total = sum((g.N * ((g.H - ph + 1) // 2) * ((g.W - pw + 1) // 2) + 127) // 128
-                                     for ph, pw, *_ in classes)
-            off = 0
             for ph, pw, nkh, nkw, pad_c, wc, _ in classes:
                 ho_c, wo_c = (g.H - ph + 1) // 2, (g.W - pw + 1) // 2
                 gc = N.ConvGeom(N=g.N, H=g.Ho, W=g.Wo, C=co, KH=nkh, KW=nkw, stride=1, pad=pad_c, Ho=ho_c, Wo=wo_c,
                                 K=nkh * nkw * co, Kp=nkh * nkw * co)
                 rows = g.N * ho_c * wo_c
                 gemm(dy4, wc, conv=1, geom=gc, mnk=(rows, ci, gc.K), out=dx.view(-1, ci), beta=beta,
-                     orow=(2, ph, pw, g.H, g.W, ho_c, wo_c), bnb=bnb_args(rows, off))
-                off += (rows + 127) // 128
+                     orow=(2, ph, pw, g.H, g.W, ho_c, wo_c))
         else:
-            bnb = None  # dX comes out of col2im: no GEMM epilogue sees it
             wm = st["wm"]
             dcols = gemm(dyb, wm, tb=True, out_dtype=torch.bfloat16)  # [M, Kp] = dY . Wm
             kp = wm.shape[1]
@@ -732,8 +698,6 @@ def _conv_bwd(dy, st, need_x: bool, need_w: bool, sink=None, x_join: Optional[Gr
             dx = acc if acc is not None else torch.empty(g.N, g.H, g.W, g.C, dtype=torch.bfloat16, device=dy.device)
             N.check(N.lib().dca_ops_col2im(N.ptr(dcols), N.ptr(dx), gc, int(acc is not None), N.stream(dy.device)),
                     "col2im")
-        if bnb is not None:
-            bnb.nparts = bnb.rows_total
         if x_join is not None:
             dx = x_join.contribute(dx if acc is None else acc)  # (a masked source: dx is the fresh sum)
     if need_w:
@@ -771,34 +735,13 @@ class _Conv2d(torch.autograd.Function):
         return dx, dw, db, None, None, None, None
 
 
-class BnLink:
-    """A BN + ReLU layer (no residual) whose output feeds exactly one conv: the consumer's dgrad GEMM epilogue
-    computes the layer's backward statistics (sum dz, sum dz * xhat), so its backward skips k_bn_bwd_stats -- one
-    read pass of dL/d(out) and x fewer.  Set in the producer's forward, filled by the consumer's backward,
-    consumed (and cleared) by the producer's backward."""
-
-    def __init__(self):
-        self.ready = False
-        self.x = self.stats = self.gamma = self.beta = self.part = None
-        self.rows_total = self.nparts = 0
-
-    def publish(self, x, stats, gamma, beta):
-        self.x, self.stats, self.gamma, self.beta, self.ready = x, stats, gamma, beta, True
-        self.part, self.nparts = None, 0
-
-    def take(self):
-        part, nparts = (self.part, self.nparts) if self.nparts else (None, 0)
-        self.__init__()
-        return part, nparts
-
-
 class _ConvBNAct(torch.autograd.Function):
     """conv (no bias) -> BatchNorm (train) -> ReLU / residual, with the BN statistics computed in the conv
     GEMM's epilogue (no separate statistics pass over the conv output)."""
 
     @staticmethod
     def forward(ctx, x, w, r, gamma, beta, running_mean, running_var, stride, pad, eps, momentum, relu, res_mode, fp8,
-                fp8_state, emit, packed, sinks, x_join, r_join, link_out, link_in, res_in):
+                fp8_state, emit, packed, sinks, x_join, r_join, res_in):
         ctx.res_in = res_in
         if res_in is not None:  # the consumer may hand this output's gradient over res_in instead of autograd
             ctx.set_materialize_grads(False)
@@ -831,9 +774,6 @@ class _ConvBNAct(torch.autograd.Function):
         ctx.wshape = tuple(w.shape)
         ctx.sinks = sinks
         ctx.joins = (x_join, r_join)
-        ctx.links = (link_out if relu and res_mode == 0 else None, link_in)
-        if ctx.links[0] is not None:
-            ctx.links[0].publish(y, stats, gamma.detach(), beta.detach())
         ctx.save_for_backward(y, r if mask is None else None, gamma, beta, stats, mask)
         ctx.relu, ctx.res_mode = relu, res_mode
         return out
@@ -845,14 +785,12 @@ class _ConvBNAct(torch.autograd.Function):
         if dout is None:  # (res_in: grad materialisation is off) the consumer's bn3 left dout and its mask
             rl = ctx.res_in
             if rl is None or rl.dout is None:
-                ctx.st = ctx.sinks = ctx.joins = ctx.links = ctx.res_in = None
-                return (None,) * 23
+                ctx.st = ctx.sinks = ctx.joins = ctx.res_in = None
+                return (None,) * 21
             dout, in_mask, rl.dout, rl.mask = rl.dout, rl.mask, None, None
         if _BWD_TRACE is not None:
             _BWD_TRACE.append((tuple(y.shape), in_mask is not None))
         sw, sg, sb = ctx.sinks if ctx.sinks is not None else (None, None, None)
-        link_out, link_in = ctx.links
-        parts = link_out.take() if link_out is not None else (None, 0)
         x_join, r_join = ctx.joins
         res_link = isinstance(r_join, ResidualLink) and mask is not None and ctx.res_mode == 2
         defer = (not res_link and r_join is not None and mask is not None and r_join.defer_ok
@@ -860,7 +798,6 @@ class _ConvBNAct(torch.autograd.Function):
         dout = dout.to(torch.bfloat16).contiguous()
         dy_conv, dr, dgamma, dbeta = _bn_backward(dout, y, r, gamma, beta, stats, ctx.relu, ctx.res_mode,
                                                   dgamma_out=sg[0] if sg else None, dbeta_out=sb[0] if sb else None,
-                                                  parts=parts if parts[0] is not None else None,
                                                   mask=mask if in_mask is None else in_mask,
                                                   want_dr=not (defer or res_link))
         if sg:
@@ -875,8 +812,7 @@ class _ConvBNAct(torch.autograd.Function):
         s2d = (ctx.st.get("packed") or {}).get("s2d")
         dx, dw = _conv_bwd(dy_conv, ctx.st, ctx.needs_input_grad[0], ctx.needs_input_grad[1] or sw is not None,
                            sink=sw[0] if sw and s2d is None else None,
-                           x_join=x_join if ctx.needs_input_grad[0] else None,
-                           bnb=link_in if ctx.needs_input_grad[0] else None)
+                           x_join=x_join if ctx.needs_input_grad[0] else None)
         if s2d is not None and dw is not None:  # [Co, 16, 4, 4] of the 4x4 conv -> the stem's [Co, C, 7, 7]
             co = dw.shape[0]
             src = dw.reshape(co, -1).contiguous()
@@ -889,15 +825,14 @@ class _ConvBNAct(torch.autograd.Function):
                 dw = out
         if sw:
             sw[1]()
-        ctx.st = ctx.sinks = ctx.joins = ctx.links = ctx.res_in = None
+        ctx.st = ctx.sinks = ctx.joins = ctx.res_in = None
         return (dx, dw, dr, dgamma, dbeta, None, None, None, None, None, None, None, None, None, None, None, None, None,
-                None, None, None, None, None)
+                None, None, None)
 
 
 def conv_bn_act(x, conv: torch.nn.Conv2d, bn: torch.nn.BatchNorm2d, r=None, relu=True, fp8=False, res_mode=None,
                 fp8_state: Optional[Fp8Delayed] = None, emit: Optional[Fp8Delayed] = None, packed=None,
                 direct_grads: bool = False, x_join: Optional[GradJoin] = None, r_join: Optional[GradJoin] = None,
-                link_out: Optional[BnLink] = None, link_in: Optional[BnLink] = None,
                 res_in: Optional[ResidualLink] = None):
     """act(bn(conv(x))) for NHWC bf16 x, conv without bias (BN in eval mode: inference under no_grad, running
     statistics); with a residual r: res_mode 2 (default,
@@ -906,10 +841,8 @@ def conv_bn_act(x, conv: torch.nn.Conv2d, bn: torch.nn.BatchNorm2d, r=None, relu
     packed: the conv's WeightPack entry.  direct_grads: the conv weight and BN affine parameters are used once
     per step, so their gradients may be written straight into FlatBucketDDP's flat buffer (``grad_sink``).
     x_join / r_join: the input x / the residual r is also consumed elsewhere (GradJoin): its gradient is summed
-    inside the producing kernels instead of by an autograd add.
-    link_out / link_in (BnLink): this BN + ReLU layer's output feeds exactly one conv (link_out), or this conv's
-    input is such a layer's output (link_in): the backward statistics of that layer come out of this conv's dgrad
-    GEMM epilogue (``DCA_OPS_BNB_FUSE=1``; off by default, measured slower)."""
+    inside the producing kernels instead of by an autograd add.  (Measured and removed in round 5: the BN-backward
+    statistics in the consumer's dgrad GEMM epilogue, 8,417 vs 8,755 img/s at ResNet-50 batch 256.)"""
     if res_mode is None:
         res_mode = 2 if r is not None else 0
     if conv.bias is not None:
@@ -932,8 +865,6 @@ def conv_bn_act(x, conv: torch.nn.Conv2d, bn: torch.nn.BatchNorm2d, r=None, relu
     return _ConvBNAct.apply(x, conv.weight, r, bn.weight, bn.bias, bn.running_mean, bn.running_var, conv.stride[0],
                             conv.padding[0], bn.eps, momentum, relu, res_mode, fp8, fp8_state, emit, packed, sinks,
                             x_join if torch.is_grad_enabled() else None, r_join if torch.is_grad_enabled() else None,
-                            link_out if torch.is_grad_enabled() and _BNB_FUSE else None,
-                            link_in if torch.is_grad_enabled() and _BNB_FUSE else None,
                             res_in if torch.is_grad_enabled() else None)
 
 
@@ -969,7 +900,7 @@ class _BatchNormAct(torch.autograd.Function):
         return dx, dr, dgamma, dbeta, None, None, None, None, None, None
 
 
-def _bn_backward(dy, x, r, gamma, beta, stats, relu, res_mode, dgamma_out=None, dbeta_out=None, parts=None,
+def _bn_backward(dy, x, r, gamma, beta, stats, relu, res_mode, dgamma_out=None, dbeta_out=None,
                  mask=None, want_dr: bool = True):
     """(dx, dr, dgamma, dbeta) of the fused BN + ReLU + residual.  dgamma_out / dbeta_out: flat gradient views
     to accumulate into (then dgamma / dbeta are returned as None).  mask: the forward's ReLU bit mask (res_mode 2;
@@ -985,14 +916,6 @@ def _bn_backward(dy, x, r, gamma, beta, stats, relu, res_mode, dgamma_out=None, 
     dx = torch.empty_like(x)
     # without dr (mask given): the residual's consumer reads dy and the mask itself (GradJoin.defer_masked)
     dr = torch.empty_like(x) if res_mode == 2 and (want_dr or mask is None) else None
-    if parts is not None:  # statistics already summed per tile by the dgrad GEMM that produced dy (BnLink)
-        if not relu or res_mode != 0:
-            raise ValueError("bn backward: fused statistics are for BN + ReLU without a residual")
-        part_t, nparts = parts
-        N.check(N.lib().dca_ops_bn_bwd_parts(N.ptr(dy), N.ptr(x), N.ptr(stats), N.ptr(gamma), N.ptr(beta),
-                                             N.ptr(part_t), int(nparts), N.ptr(sums), N.ptr(dgamma), N.ptr(dbeta),
-                                             N.ptr(dx), M, C, int(direct), N.stream(x.device)), "bn_bwd_parts")
-        return (dx, None, None, None) if direct else (dx, None, dgamma, dbeta)
     N.check(N.lib().dca_ops_bn_bwd(N.ptr(dy), N.ptr(x), N.ptr(r), N.ptr(stats), N.ptr(gamma), N.ptr(beta),
                                    N.ptr(part), N.ptr(sums), N.ptr(dgamma), N.ptr(dbeta), N.ptr(dx), N.ptr(dr),
                                    M, C, int(relu), int(res_mode), int(direct), N.ptr(mask), N.stream(x.device)),

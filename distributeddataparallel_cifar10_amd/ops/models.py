@@ -133,13 +133,12 @@ class OpsModel(nn.Module):
             self._fp8 = {}
         return self._fp8.setdefault(id(conv), F.Fp8Delayed())
 
-    def _conv_bn(self, h, conv, bn, relu=True, r=None, consumer=None, x_join=None, r_join=None, link_out=None,
-                 link_in=None, res_in=None):
+    def _conv_bn(self, h, conv, bn, relu=True, r=None, consumer=None, x_join=None, r_join=None, res_in=None):
         # every ResNet conv / BN is applied once per step: gradients may go straight into the flat DDP buffer
         return F.conv_bn_act(h, conv, bn, r=r, relu=relu, fp8=self._fp8_ok(conv), fp8_state=self._state(conv),
                              emit=self._state(consumer) if consumer is not None else None,
                              packed=self._pack.get(conv), direct_grads=True, x_join=x_join, r_join=r_join,
-                             link_out=link_out, link_in=link_in, res_in=res_in)
+                             res_in=res_in)
 
     def stem(self, h, conv, bn):
         """7x7/2 conv -> BN + ReLU -> 3x3/2 max pool (torchvision ResNet stem).  ``h`` is what ``begin`` returned:
@@ -169,12 +168,9 @@ class OpsModel(nn.Module):
                 idt = h
             else:
                 idt = self._conv_bn(h, b.downsample[0], b.downsample[1], relu=False, x_join=join, res_in=rlink)
-            # bn1 -> conv2 and bn2 -> conv3 are single-consumer BN + ReLU layers: their backward statistics come
-            # out of conv2's / conv3's dgrad GEMM epilogue (BnLink)
-            l1, l2 = F.BnLink(), F.BnLink()
-            out = self._conv_bn(h, b.conv1, b.bn1, x_join=join, consumer=b.conv2, link_out=l1)
-            out = self._conv_bn(out, b.conv2, b.bn2, consumer=b.conv3, link_in=l1, link_out=l2)
-            h = self._conv_bn(out, b.conv3, b.bn3, relu=True, r=idt, consumer=nxt, link_in=l2,
+            out = self._conv_bn(h, b.conv1, b.bn1, x_join=join, consumer=b.conv2)
+            out = self._conv_bn(out, b.conv2, b.bn2, consumer=b.conv3)
+            h = self._conv_bn(out, b.conv3, b.bn3, relu=True, r=idt, consumer=nxt,
                               r_join=join if b.downsample is None else rlink)  # relu(bn3(conv3) + identity)
         return h
 

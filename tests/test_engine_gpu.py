@@ -164,6 +164,40 @@ def test_learnable_epochs_track_pytorch(gpu, dtype, tol):
     assert int(sd["resblocks.0.batch_norm.num_batches_tracked"]) == 10 * 3 * nb
 
 
+@pytest.mark.parametrize("dtype", ["bf16", "fp32"])
+def test_prologue_reduction_bitwise(gpu, dtype, monkeypatch):
+    """Graph chunks with the prologue reduction (each step's gradient segments applied at the start of the next step's
+    launch, one reduction kernel per chunk) train bitwise like one reduction kernel after every step
+    (DCA_PKS_PROLOGUE=0): 37 steps = chunks of 16 + 16 + 4 + 1, a ragged batch in between, then the epoch / cursor
+    bases and the loss accumulator agree too."""
+    import copy
+    from distributeddataparallel_cifar10_amd.data.synthetic import synthetic_cifar
+    from distributeddataparallel_cifar10_amd.models.netresdeep import NetResDeep
+    from distributeddataparallel_cifar10_amd.runtime.engine import EngineConfig, NetResDeepEngine
+    data, labels = synthetic_cifar(2048, seed=4, learnable=True)
+    torch.manual_seed(9)
+    m0 = NetResDeep()
+    out = []
+    for pro in ("1", "0"):
+        monkeypatch.setenv("DCA_PKS_PROLOGUE", pro)
+        m = copy.deepcopy(m0).to(gpu)
+        eng = NetResDeepEngine(m, data.to(gpu), labels.to(gpu), EngineConfig(batch_max=32, dtype=dtype))
+        eng.set_indices(list(range(2048)))
+        eng.set_cursor(0)
+        eng.read_loss(reset=True)
+        eng.run(32, 36)
+        eng.run(20, 1)
+        loss, steps = eng.read_loss()
+        out.append((loss, steps, eng.epoch(), torch.cat([p.detach().reshape(-1).cpu() for p in m.parameters()]),
+                    m.resblocks[0].batch_norm.running_var.detach().cpu().clone(),
+                    int(m.resblocks[0].batch_norm.num_batches_tracked)))
+        eng.close()
+    (l1, s1, e1, p1, v1, n1), (l0, s0, e0, p0, v0, n0) = out
+    assert s1 == s0 == 37 and e1 == e0 == 37 and n1 == n0 == 370
+    assert l1 == l0, (l1, l0)
+    assert torch.equal(p1, p0) and torch.equal(v1, v0)
+
+
 def test_graft_smoke(gpu):
     import __graft_entry__
     __graft_entry__.smoke()
