@@ -526,8 +526,7 @@ __device__ __forceinline__ void xr_row(char* XR, int xrow, int q, int ch, const 
 // weight staging: the NP planes (hi, lo) of one conv weight, stored in global memory in the LDS record layout
 // (common.h PKW_*), copied into WT by LDS-DMA -- no registers, no scratch; the issuing waves' vmcnt covers it.
 // 1 KB per wave instruction, chunks dealt round-robin to the waves; P = 0's 22.5 KB end in a half chunk.
-// AUX: cache policy of the DMA loads (16 = sc1: the records were written in this launch by the prologue reduction)
-template <int P, int AUX = 0>
+template <int P>
 __device__ __forceinline__ void wt_dma(char* wt, const unsigned short* src, int wv, int lane) {
   constexpr int BYTES = (P + 1) * PKW_PLANE * 2, NCH = (BYTES + 1023) / 1024;
   static_assert(BYTES == (P + 1) * Plan<P>::WT_PL, "record layout of pkw matches the LDS weight planes");
@@ -536,8 +535,41 @@ __device__ __forceinline__ void wt_dma(char* wt, const unsigned short* src, int 
     const int ck = wv + NW * m;
     if (ck < NCH && ck * 1024 + lane * 16 < BYTES)
       __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)((const char*)src + ck * 1024 + lane * 16),
-                                       (__attribute__((address_space(3))) void*)(wt + ck * 1024), 16, 0, AUX);
+                                       (__attribute__((address_space(3))) void*)(wt + ck * 1024), 16, 0, 0);
   }
+}
+// The same planes when the prologue reduction wrote them in this launch: sc1 16-B buffer loads into registers, then
+// LDS stores (the guide's validated consumer form; LDS-DMA is not one of them)
+template <int P>
+__device__ __forceinline__ void wt_copy_sc1(char* wt, const unsigned short* src) {
+  constexpr int BYTES = (P + 1) * PKW_PLANE * 2, N16 = BYTES / 16, R = (N16 + NTH - 1) / NTH;
+  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)src, (short)0, BYTES, 0x00020000);
+  v4u v[R];
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    const int idx = (int)threadIdx.x + NTH * r;
+    v[r] = __builtin_amdgcn_raw_buffer_load_b128(rs, (idx < N16 ? idx : 0) * 16, 0, 16);
+  }
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    const int idx = (int)threadIdx.x + NTH * r;
+    if (idx < N16) *(v4u*)(wt + idx * 16) = v[r];
+  }
+}
+// conv1 B fragment of MFMA m (taps 4m + q), channel half h for this lane, plane p, from the fp32 weights (sc1 dword
+// loads: written in this launch by the prologue reduction) -- the swf_slot record the next launches read from pkw
+template <int P>
+__device__ __forceinline__ uint2 stem_bfrag_sc1(const Ctx& cx, int p, int h, int m, int lane) {
+  const int co = 16 * h + (lane & 15), tap = 4 * m + (lane >> 4);
+  unsigned short u[3];
+#pragma unroll
+  for (int ci = 0; ci < 3; ++ci) {
+    const float x = tap < 9 ? __hip_atomic_load(cx.params + OFF_C1W + co * 27 + ci * 9 + tap, __ATOMIC_RELAXED,
+                                                 __HIP_MEMORY_SCOPE_AGENT) : 0.f;
+    const unsigned short hi = bfbits(x);
+    u[ci] = p == 0 ? hi : bf_lo(x, hi);
+  }
+  return uint2{(unsigned)u[0] | ((unsigned)u[1] << 16), (unsigned)u[2]};
 }
 
 // fc1 slice of slice s: 32 rows x 512 local features (u = ch*16 + pr*8 + pw <-> global ch*64 + (2s + pr)*8 + pw),
@@ -776,26 +808,47 @@ __device__ __forceinline__ void seg_chunk(const Ctx& cx, const Args& pa, const S
   }
 }
 
-// Write-through stores of the SGD results when the readers run in the SAME launch (the prologue reduction: the
-// step workgroups read the new weights after the ready granules, with sc1 loads): the fp32 parameter, the CC4 base,
-// and the sliced engine's bf16 hi / lo weight records (csrc/netresdeep_kernels.hip derive_param, pkw part: the only
-// derived copies of the trunk / conv1 parameters the sliced engine has).
-__device__ __forceinline__ void st2b_wt(unsigned short* p, unsigned short v) {
-  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ void derive_pkw_wt(const Ctx& cx, int e, float w) {
-  const unsigned short hi = bfbits(w), lo = bfbits(w - __uint_as_float((unsigned)hi << 16));
-  if (e >= OFF_CONVW && e < OFF_CONVW + 9216) {
-    const int r = e - OFF_CONVW, co = r / 288, ci = (r / 9) % 32, tap = r % 9;
-    const int fo = pkw_elem(tap * 32 + co, ci), dofs = PKW_DGRAD + pkw_elem((8 - tap) * 32 + ci, co);
-    st2b_wt(cx.pkw + fo, hi);
-    st2b_wt(cx.pkw + PKW_PLANE + fo, lo);
-    st2b_wt(cx.pkw + dofs, hi);
-    st2b_wt(cx.pkw + PKW_PLANE + dofs, lo);
-  } else if (e >= OFF_C1W && e < OFF_C1W + 864) {
-    const int r = e - OFF_C1W, slot = swf_slot(r / 27, r % 27);
-    st2b_wt(cx.pkw + PKW_STEM + slot, hi);
-    st2b_wt(cx.pkw + PKW_STEM + 1536 + slot, lo);
+// Write-through stores of the SGD results when the readers run in the SAME launch (the prologue reduction: the step
+// workgroups read the new weights after the ready granules).  Only the hand-off forms the MI355X guide validates
+// (Guideline 16 / "Valid forms", table row 1): every byte stored sc1 by a 4- or 16-B store and drained before the
+// ready granule, every consumer load an sc1 global / buffer load into registers.  So the fp32 parameters and the CC4
+// base are dword sc1 stores, and the trunk's bf16 hi / lo weight records are written as whole 16-B chunks: a
+// 128-element trunk chunk (slab fragment order) is 8 output x 16 input channels of one tap = 16 forward chunks
+// (record tap*32 + co, channels ci) and 16 dgrad chunks (record (8 - tap)*32 + ci, channels co) per plane.  (The
+// first version stored every bf16 element with a 2-byte store and let the step workgroups LDS-DMA the records:
+// the forms the guide has no measurement for, and the trajectory drifted.)  conv1's records are scattered 2-byte slots:
+// written plainly for the NEXT launches; the step workgroups of this launch derive their conv1 fragments from the
+// fp32 weights instead (stem_bfrag_sc1).
+template <int NTH>
+__device__ __forceinline__ void pkw_trunk_chunks_wt(const Ctx& cx, const float* wnew, int e_base, int len) {
+  for (int t = threadIdx.x; t < 64 * (len / 128); t += NTH) {
+    const int hf = t >> 6, j = t & 63, kind = j >> 4, idx = j & 15;
+    const int e0 = e_base + hf * 128, tt = e0 >> 8, h = (e0 >> 7) & 1, mt = tt & 1, nt = tt >> 1;
+    const int tap = nt >> 1, cih = nt & 1;
+    const float* w = wnew + hf * 128;
+    unsigned short v[8];
+    int dst;
+    if (kind < 2) {  // forward record tap*32 + co, channels 16 cih + 8 qq .. +7
+      const int col = idx >> 1, qq = idx & 1, co = 16 * mt + 8 * h + col;
+#pragma unroll
+      for (int j8 = 0; j8 < 8; ++j8) {
+        const float x = w[64 * (col >> 2) + 4 * (8 * qq + j8) + (col & 3)];
+        const unsigned short hi = bfbits(x);
+        v[j8] = kind == 0 ? hi : bf_lo(x, hi);
+      }
+      dst = (kind == 1 ? PKW_PLANE : 0) + pkw_elem(tap * 32 + co, 16 * cih + 8 * qq);
+    } else {  // dgrad record (8 - tap)*32 + ci, channels 16 mt + 8 h .. +7
+      const int cl = idx;
+#pragma unroll
+      for (int c8 = 0; c8 < 8; ++c8) {
+        const float x = w[64 * (c8 >> 2) + 4 * cl + (c8 & 3)];
+        const unsigned short hi = bfbits(x);
+        v[c8] = kind == 2 ? hi : bf_lo(x, hi);
+      }
+      dst = PKW_DGRAD + (kind == 3 ? PKW_PLANE : 0) + pkw_elem((8 - tap) * 32 + 16 * cih + cl, 16 * mt + 8 * h);
+    }
+    st4_wt(cx.pkw + dst, __builtin_bit_cast(f32x4, v4u{v[0] | ((unsigned)v[1] << 16), v[2] | ((unsigned)v[3] << 16),
+                                                       v[4] | ((unsigned)v[5] << 16), v[6] | ((unsigned)v[7] << 16)}));
   }
 }
 
@@ -927,7 +980,8 @@ __device__ void seg_process(const Ctx& cx, const Args& pa, const RedAr& ra, int 
       }
       if constexpr (WT) {
         st1_wt(cx.params + pidx, wv);
-        derive_pkw_wt(cx, pidx, wv);
+        if (b < Ls.r_trunk) segv[k] = wv;             // the records: whole 16-B chunks below
+        else derive_param<true>(cx, pidx, wv);        // conv1 records: for the next launches (plain stores)
       } else {
         cx.params[pidx] = wv;
         derive_param<true>(cx, pidx, wv);
@@ -939,6 +993,12 @@ __device__ void seg_process(const Ctx& cx, const Args& pa, const RedAr& ra, int 
         if constexpr (WT) st1_wt(cx.rs_base + kk, g);
         else cx.rs_base[kk] = g;
       }
+    }
+  }
+  if constexpr (WT) {
+    if (b < Ls.r_trunk && mode != 1 && mode != 3) {  // this chunk's weight records (segv = the new weights)
+      __syncthreads();
+      pkw_trunk_chunks_wt<NTH>(cx, segv, b * Ls.ch, len);
     }
   }
   DCA_STAMP(cx, sslot, swg, 3);
@@ -1141,7 +1201,7 @@ __device__ __forceinline__ void step_main(const Ctx& cx, const Args& pa, const R
       kc[m] = prev ? __hip_atomic_load(src, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : *src;
     }
     // forward trunk weights, records [tap][co] x ci (hi, lo)
-    if (prev) wt_dma<P, 16>(WT, pkw, wv, lane);
+    if (prev) wt_copy_sc1<P>(WT, pkw);
     else wt_dma<P>(WT, pkw, wv, lane);
     uint2 bwr[P + 1][2][3];        // conv1 B fragments: lane (co = 16h + c, k-group q) of MFMA m
 #pragma unroll
@@ -1149,11 +1209,9 @@ __device__ __forceinline__ void step_main(const Ctx& cx, const Args& pa, const R
 #pragma unroll
       for (int h = 0; h < 2; ++h)
 #pragma unroll
-        for (int m = 0; m < 3; ++m) {
-          const unsigned long long* bp = (const unsigned long long*)(pkw + PKW_STEM + p * 1536) + (h * 3 + m) * 64 + lane;
-          const unsigned long long bv = prev ? __hip_atomic_load(bp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : *bp;
-          bwr[p][h][m] = uint2{(unsigned)bv, (unsigned)(bv >> 32)};
-        }
+        for (int m = 0; m < 3; ++m)
+          bwr[p][h][m] = prev ? stem_bfrag_sc1<P>(cx, p, h, m, lane)
+                              : ((const uint2*)(pkw + PKW_STEM + p * 1536))[(h * 3 + m) * 64 + lane];
 #pragma unroll
     for (int m = 0; m < KCM; ++m) pin(kc[m]);
     pin(lab);
@@ -1310,8 +1368,8 @@ __device__ __forceinline__ void step_main(const Ctx& cx, const Args& pa, const R
     // AFTER an exchange: vmcnt is in order, so loads in flight when a sweep starts hold up its first pass (register
     // loads before the exchange + an LDS store a block later cost ~1.4 us in each of the two blocks, stamps)
     if (i == NBLK - 4) w1_dma<P>(cx, U + PL::U_W1, s, wv, lane);
-    if (i == NBLK - 1) {  // dgrad weights, records [8 - tap][ci] x co (sc1: the prologue reduction wrote them)
-      if (prev) wt_dma<P, 16>(WT, pkw + PKW_DGRAD, wv, lane);
+    if (i == NBLK - 1) {  // dgrad weights, records [8 - tap][ci] x co (sc1 loads: the prologue reduction wrote them)
+      if (prev) wt_copy_sc1<P>(WT, pkw + PKW_DGRAD);
       else wt_dma<P>(WT, pkw + PKW_DGRAD, wv, lane);
     }
     lds_barrier();

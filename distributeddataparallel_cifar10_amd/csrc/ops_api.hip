@@ -35,78 +35,26 @@ inline int grid_for(long work, int per_block = 256, int cap = 8192) {
   return (int)std::max(1L, std::min(b, (long)cap));
 }
 bool g_lds_set = false;
-// DCA_OPS_WGRAD=0 routes weight gradients through the general k_gemm (A/B comparisons)
-inline bool getenv_flag(const char* name) {
-  const char* e = getenv(name);
-  return !(e && e[0] == '0');
-}
-// 3x3/2 max-pool specialisations: unrolled forward, output-driven backward (DCA_OPS_POOL_K3S2=0: generic kernels)
-inline bool getenv_pool_k3s2() {
-  static const bool v = getenv_flag("DCA_OPS_POOL_K3S2");
-  return v;
-}
-inline bool getenv_glds_ok() {
-  static const bool v = getenv_flag("DCA_OPS_GLDS");
-  return v;
-}
+// Dispatch policy.  Every rule below was chosen by measurement (docs/ARCHITECTURE.md "GEMM dispatch"); the A/B
+// environment switches of rounds 1-4 are gone (round 5), except DCA_OPS_STREAM, kept as the diagnostic A/B of the
+// persistent short-K kernel that is still being tuned (0 never, 1 every eligible shape, unset: the shape rule).
+// 3x3/2 max-pool specialisations: unrolled forward, output-driven backward (324 -> 107 us backward at batch 256)
+constexpr bool POOL_K3S2 = true;
 // bf16 implicit-conv glds (C % 64 == 0): neutral at batch 64, +2..6 % per conv GEMM at batch 256
-// (DCA_OPS_GLDS_CONV=0 turns it off)
-inline bool getenv_glds_conv() {
-  static const bool v = getenv_flag("DCA_OPS_GLDS_CONV");
-  return v;
-}
+constexpr bool GLDS_CONV = true;
 // single-buffer weight-gradient kernel: the loop is latency-bound, so more resident workgroups per CU win
-// (batch-256 census: M = 64 weight gradients 845 -> 580 us, 835 -> 556 us; DCA_OPS_WGRAD_SINGLE=0 turns it off)
-inline bool getenv_wgrad_single() {
-  static const bool v = getenv_flag("DCA_OPS_WGRAD_SINGLE");
-  return v;
-}
-// glds single-buffer mode (32 KiB LDS: ~1.5x the resident workgroups) for short K.  Batch-256 census vs
-// double-buffered: K <= 576 0.78-0.91x time, K = 1152 0.93x, K = 1024-4608 0.97-1.23x.
-// DCA_OPS_GLDS_SINGLE = 0: never, 1: always, unset: K-tiles per split <= 9.
+// (batch-256 census: M = 64 weight gradients 845 -> 580 us, 835 -> 556 us)
+constexpr bool WGRAD_SINGLE = true;
+// glds single-buffer mode (32 KiB LDS: ~1.5x the resident workgroups) for short K: K-tiles per split <= 9.
+// Batch-256 census vs double-buffered: K <= 576 0.78-0.91x time, K = 1152 0.93x, K = 1024-4608 0.97-1.23x.
+constexpr int GLDS_SINGLE_NK = 9;
 // narrow (128 x 64) short-K GEMMs on the single-buffer glds kernel: 0.89-0.90x the register-staged time at
-// batch 256 (802816 x 64 x {64, 256}); DCA_OPS_GLDS_NARROW=0 turns it off
-inline bool getenv_glds_narrow() {
-  static const bool v = getenv_flag("DCA_OPS_GLDS_NARROW");
-  return v;
-}
-inline bool getenv_glds_conv_any() {  // experiment: glds (per-lane tap decode) for every implicit conv
-  static const bool v = [] {
-    const char* e = getenv("DCA_OPS_GLDS_CONV_ANY");
-    return e && e[0] == '1';
-  }();
-  return v;
-}
-inline int getenv_reg_single_nk() {  // register-staged kernel: single-buffer up to this many K-tiles per split
-  static const int v = [] {
-    const char* e = getenv("DCA_OPS_REG_SINGLE_NK");
-    return e ? atoi(e) : 4;
-  }();
-  return v;
-}
-inline int getenv_glds_waves() {  // 0: automatic; DCA_OPS_GLDS_WAVES = 4 or 8 forces it
-  static const int v = [] {
-    const char* e = getenv("DCA_OPS_GLDS_WAVES");
-    const int n = e ? atoi(e) : 0;
-    return n == 4 || n == 8 ? n : 0;
-  }();
-  return v;
-}
-inline int getenv_glds_stages() {
-  static const int v = [] {
-    const char* e = getenv("DCA_OPS_GLDS_STAGES");
-    const int n = e ? atoi(e) : 2;
-    return n < 2 ? 2 : (n > 4 ? 4 : n);
-  }();
-  return v;
-}
-inline int getenv_glds_single() {
-  static const int v = [] {
-    const char* e = getenv("DCA_OPS_GLDS_SINGLE");
-    return e ? (e[0] == '1' ? 1 : 0) : -1;
-  }();
-  return v;
-}
+// batch 256 (802816 x 64 x {64, 256})
+constexpr bool GLDS_NARROW = true;
+// register-staged kernel: single LDS buffer up to this many K-tiles per split
+constexpr int REG_SINGLE_NK = 4;
+// glds K pipeline: 2 LDS buffers (3-4 measured 1.4-1.6x slower on the long-K shapes: fewer resident waves)
+constexpr int GLDS_STAGES = 2;
 inline int getenv_stream() {  // persistent short-K GEMM (k_gemm_stream): DCA_OPS_STREAM = 0 never, 1 whenever
   static const int v = [] {    // eligible, 2 (default) by the shape rule at the launch site
     const char* e = getenv("DCA_OPS_STREAM");
@@ -114,36 +62,11 @@ inline int getenv_stream() {  // persistent short-K GEMM (k_gemm_stream): DCA_OP
   }();
   return v;
 }
-inline bool getenv_stream_conv() {  // implicit 3x3 convolutions (N = 64 / 128) on k_gemm_stream; DCA_OPS_STREAM_CONV=0 off
-  static const bool v = getenv_flag("DCA_OPS_STREAM_CONV");
-  return v;
-}
-inline int getenv_pp() {  // ping-pong 256 x 256 GEMM (k_gemm_pp): DCA_OPS_PP = 0 never, 1 whenever eligible,
-  static const int v = [] {  // 2 (default) by the shape rule at the launch site
-    const char* e = getenv("DCA_OPS_PP");
-    return e ? atoi(e) : 2;
-  }();
-  return v;
-}
-// weight gradients with M >= 256 on the ping-pong LDS-DMA kernel (k_wgrad_pp): DCA_OPS_WGRAD_PP=0 turns it off
-inline bool getenv_wgrad_pp() {
-  static const bool v = getenv_flag("DCA_OPS_WGRAD_PP");
-  return v;
-}
-inline bool getenv_wgrad_pp_all() {  // DCA_OPS_WGRAD_PP_ALL=1: also the forms the shape rule leaves on k_wgrad
-  static const bool v = [] {
-    const char* e = getenv("DCA_OPS_WGRAD_PP_ALL");
-    return e && e[0] == '1';
-  }();
-  return v;
-}
-inline bool getenv_wgrad_ok() {
-  static const int v = [] {
-    const char* e = getenv("DCA_OPS_WGRAD");
-    return (e && e[0] == '0') ? 0 : 1;
-  }();
-  return v != 0;
-}
+// implicit 3x3 convolutions (N = 128) on k_gemm_stream (129.5 -> 117.5 us at batch 256)
+constexpr bool STREAM_CONV = true;
+// weight gradients with M >= 256 (and the swapped 1x1 forms) on the ping-pong LDS-DMA kernel k_wgrad_pp
+// (0.71-0.92x the k_wgrad time on every routed shape); the 64-wide / swapped implicit forms stay on k_wgrad
+// (1.4-1.7x slower on k_wgrad_pp, profiles/wgrad_pp_r3.log)
 inline int nparts_rows(long M) { return (int)((M + dca::ops::BN_ROWS - 1) / dca::ops::BN_ROWS); }
 // BN kernels: 16 channel lanes (256 contiguous bytes per row and wave instruction) when C % 128 == 0, else 8
 // finalize threads per workgroup: 1024 when one workgroup reduces one channel's partial rows (C < 256)
@@ -153,17 +76,11 @@ inline int nparts_rows(long M) { return (int)((M + dca::ops::BN_ROWS - 1) / dca:
 // batch-256 shapes): tensors of >= 2^26 elements stream with non-temporal loads / stores (statistics 181.6 -> 145.5 us,
 // residual apply 251.6 -> 209.5 us at 802816 x 256); the 16-lane backward apply of >= 2^25 elements also takes 128
 // rows per workgroup (twice the workgroups: 104.5 -> 84.2 us at 50176 x 1024).  Smaller tensors keep the default
-// cache policy and 256 rows (they are re-read while still in the Infinity Cache).  DCA_OPS_BN_TUNE=0: the round-3
-// shape (256 rows, default policy) everywhere.
+// cache policy and 256 rows (they are re-read while still in the Infinity Cache).  Same box, whole step: 10,292 ->
+// 10,494 img/s (profiles/resnet50_bntune_ab_r4t.log).
 using namespace dca::ops;
-inline bool getenv_bn_tune() {
-  static const bool v = getenv_flag("DCA_OPS_BN_TUNE");
-  return v;
-}
-inline bool bn_nt(long M, int C) { return getenv_bn_tune() && C % 128 == 0 && (long)M * C >= (1L << 26); }
-inline bool bn_bwd_apply_fine(long M, int C) {
-  return getenv_bn_tune() && C % 128 == 0 && (long)M * C >= (1L << 25);
-}
+inline bool bn_nt(long M, int C) { return C % 128 == 0 && (long)M * C >= (1L << 26); }
+inline bool bn_bwd_apply_fine(long M, int C) { return C % 128 == 0 && (long)M * C >= (1L << 25); }
 inline int bn_bwd_mode(int relu, int res_mode, const void* mask) {
   if (mask) return BWD_MASK;
   if (relu) return res_mode == 2 ? BWD_RES : BWD_RELU;
@@ -274,9 +191,7 @@ int dca_ops_gemm(const GemmArgs* a, void* stream) {
   OPCK(hipFuncSetAttribute((const void*)k_wgrad_pp<PBN, SW>, hipFuncAttributeMaxDynamicSharedMemorySize, WpTile<PBN>::LDS))
       WPP_ATTR(256, false);
       WPP_ATTR(128, false);
-      WPP_ATTR(64, false);
       WPP_ATTR(128, true);
-      WPP_ATTR(64, true);
 #undef WPP_ATTR
 #define GLDS_ATTR(F8, BNV, NWV)                                                                          \
   OPCK(hipFuncSetAttribute((const void*)k_gemm_glds<F8, BNV, NWV>, hipFuncAttributeMaxDynamicSharedMemorySize, \
@@ -293,8 +208,6 @@ int dca_ops_gemm(const GemmArgs* a, void* stream) {
     }
     OPCK(hipFuncSetAttribute((const void*)k_gemm_pp<256>, hipFuncAttributeMaxDynamicSharedMemorySize,
                              PpTile<256>::LDS));
-    OPCK(hipFuncSetAttribute((const void*)k_gemm_pp<128>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                             PpTile<128>::LDS));
     OPCK(hipFuncSetAttribute((const void*)k_gemm_stream<2, 1, false>, hipFuncAttributeMaxDynamicSharedMemorySize,
                              2 * (2 * G_TILE_BYTES + 8192) + 2 * 2048 * 4));
     OPCK(hipFuncSetAttribute((const void*)k_gemm_stream<2, 1, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -321,7 +234,7 @@ int dca_ops_gemm(const GemmArgs* a, void* stream) {
   // weight gradients (both operands pixel-major, bf16, 16-B aligned channel rows): the transposed-read kernel,
   // always through the slab + reduce pass
   const bool wgrad = !g.fp8 && g.ta && (g.tb || g.conv == 2) && g.M % 8 == 0 && g.N % 8 == 0 && g.lda % 8 == 0 &&
-                     (g.conv == 2 || g.ldb % 8 == 0) && g.ws != nullptr && getenv_wgrad_ok();
+                     (g.conv == 2 || g.ldb % 8 == 0) && g.ws != nullptr;
   if (wgrad) {
     REQUIRE(g.conv != 2 || (long)g.cN * g.cHo * g.cWo < (1L << 24), "gemm: weight-gradient pixel count >= 2^24");
     // the ping-pong kernel: the larger of M (output channels) / N (input channels x taps) along its 256-row side
@@ -334,13 +247,10 @@ int dca_ops_gemm(const GemmArgs* a, void* stream) {
     const long long b_by = g.conv == 2 ? (long long)g.cN * g.cH * g.cW * g.cC * 2 : (long long)g.K * g.ldb * 2;
     const bool sw = g.M < 256;
     const int big = sw ? g.N : g.M, small = sw ? g.M : g.N;
-    const bool all = getenv_wgrad_pp_all();  // every form the kernel has (tests / measurements)
-    const bool pp_shape = all ? (big >= 256 && small >= 64 && !(sw && small > 128))
-                              : (sw ? (g.conv != 2 && small > 64 && small <= 128 && big >= 256)
-                                    : (big >= 256 && small >= 128));
-    if (getenv_wgrad_pp() && pp_shape && a_by < (1LL << 31) && b_by < (1LL << 31) && ((uintptr_t)g.A & 15) == 0 &&
+    const bool pp_shape = sw ? (g.conv != 2 && small > 64 && small <= 128 && big >= 256) : (big >= 256 && small >= 128);
+    if (pp_shape && a_by < (1LL << 31) && b_by < (1LL << 31) && ((uintptr_t)g.A & 15) == 0 &&
         ((uintptr_t)g.B & 15) == 0 && (g.conv != 2 || g.cC % 8 == 0)) {
-      const int pbn = small <= 64 ? 64 : (sw ? 128 : ((small % 256 == 0 || small > 1024) ? 256 : 128));
+      const int pbn = sw ? 128 : ((small % 256 == 0 || small > 1024) ? 256 : 128);
       const long tiles = (long)((big + WP_BM - 1) / WP_BM) * ((small + pbn - 1) / pbn);
       const long want = std::max<long>(1, (256 + tiles - 1) / tiles);
       if (want < g.splits) {  // fewer, longer splits (the slab was sized for g.splits: smaller is fine)
@@ -350,10 +260,7 @@ int dca_ops_gemm(const GemmArgs* a, void* stream) {
         g.splits = (g.K + kps - 1) / kps;
       }
       const dim3 grid((unsigned)(tiles * g.splits)), blk(WP_NT);
-      if (pbn == 64) {
-        if (sw) hipLaunchKernelGGL((k_wgrad_pp<64, true>), grid, blk, WpTile<64>::LDS, st, g);
-        else hipLaunchKernelGGL((k_wgrad_pp<64, false>), grid, blk, WpTile<64>::LDS, st, g);
-      } else if (sw) {
+      if (sw) {
         hipLaunchKernelGGL((k_wgrad_pp<128, true>), grid, blk, WpTile<128>::LDS, st, g);
       } else if (pbn == 256) {
         hipLaunchKernelGGL((k_wgrad_pp<256, false>), grid, blk, WpTile<256>::LDS, st, g);
@@ -369,7 +276,7 @@ int dca_ops_gemm(const GemmArgs* a, void* stream) {
     REQUIRE(items < (1L << 31), "gemm: too many work items");
     const dim3 grid((unsigned)items);
     // single LDS buffer: more resident workgroups per CU for these latency-bound loops
-    g.single = getenv_wgrad_single() ? 1 : 0;
+    g.single = WGRAD_SINGLE ? 1 : 0;
     const int sh = g.single ? 1 : 0;
     const int l00 = WgradTile<64, 64, 2>::LDS >> sh, l01 = WgradTile<64, 128, 1>::LDS >> sh;
     const int l10 = WgradTile<128, 64, 4>::LDS >> sh, l11 = WgradTile<128, 128, 2>::LDS >> sh;
@@ -387,7 +294,7 @@ int dca_ops_gemm(const GemmArgs* a, void* stream) {
   //   N = 64: 256 x 64 tiles (802816 x 64 x 256: 123.4 -> 109.1 us);
   //   implicit conv with C % 64 == 0, N = 128: M >= 16384 (ResNet-50's layer-2 3x3 convolutions and their input
   //     gradients: 129.5 -> 117.5 us at batch 256).  The N = 64 conv stays on the one-tile kernel unless forced
-  //     (DCA_OPS_STREAM=1): 174 us there, 218 us with 128 x 64 stream tiles, 283 us with 256 x 64
+  //     (DCA_OPS_STREAM=1, diagnostic): 174 us there, 218 us with 128 x 64 stream tiles, 283 us with 256 x 64
   {
     const int sk = getenv_stream();
     const bool conv = g.conv == 1;
@@ -397,7 +304,7 @@ int dca_ops_gemm(const GemmArgs* a, void* stream) {
     const int mw = g.N % 128 == 0 ? 1 : 2;  // 128 x 128 tiles, or 256 x 64 for N % 128 == 64
     const bool shape_ok = conv ? (g.cC % 64 == 0 && g.cKH * g.cKW <= 32 && (g.N == 64 || g.N == 128) && g.orow_S <= 0 &&
                                   g.M < (1 << 24) &&
-                                  (sk == 1 || (sk == 2 && getenv_stream_conv() && g.N == 128 && g.M >= 16384)))
+                                  (sk == 1 || (sk == 2 && STREAM_CONV && g.N == 128 && g.M >= 16384)))
                                : (g.conv == 0 && !g.ta && g.lda % 8 == 0 && g.lda >= g.K &&
                                   (g.N % 128 == 0 || g.N == 64) &&
                                   (sk == 1 || (g.K <= 512 && g.M >= 16384 &&
@@ -450,18 +357,16 @@ int dca_ops_gemm(const GemmArgs* a, void* stream) {
     // N % 256 != 0 (e.g. 128): the 256 x 128 tile
     const int ppbn = g.N % 256 == 0 ? 256 : 128;
     const long pp_tiles = (long)((g.M + PP_BM - 1) / PP_BM) * ((g.N + ppbn - 1) / ppbn);
-    const int ppk = getenv_pp();
-    // (the 256 x 128 tile measured slower than the 128 x 128 kernels on every ResNet-50 N = 128 shape, +12-18 %:
-    // 16 MFMAs per barrier interval do not cover the other group's fragment loads; DCA_OPS_PP=1 only)
-    const bool pp_shape = ppk == 1 || (ppk == 2 && ppbn == 256 && g.N % 256 == 0 && pp_tiles >= 160 && g.K >= 1024);
+    // (a 256 x 128 tile measured slower than the 128 x 128 kernels on every ResNet-50 N = 128 shape, +12-18 %:
+    // 16 MFMAs per barrier interval do not cover the other group's fragment loads; removed in round 5)
+    const bool pp_shape = ppbn == 256 && pp_tiles >= 160 && g.K >= 1024;
     const bool pp = pp_shape && !g.fp8 && !g.ta && !g.tb && g.splits == 1 && g.wperm_T <= 0 && g.orow_S <= 0 &&
                     g.M >= 256 && g.N >= 128 && g.K >= 256 && ab < (1LL << 31) && bb < (1LL << 31) &&
                     (long)g.ldb * 2 % 16 == 0 && ((uintptr_t)g.A & 15) == 0 && ((uintptr_t)g.B & 15) == 0 &&
                     (g.conv == 1 ? (g.cC % 64 == 0 && g.cKH * g.cKW <= 32 && g.M < (1 << 24))
                                  : (g.conv == 0 && (long)g.lda * 2 % 16 == 0 && (long)g.K * 2 % 16 == 0));
     if (pp) {
-      if (ppbn == 256) hipLaunchKernelGGL(k_gemm_pp<256>, dim3((unsigned)pp_tiles), dim3(PP_NT), PpTile<256>::LDS, st, g);
-      else hipLaunchKernelGGL(k_gemm_pp<128>, dim3((unsigned)pp_tiles), dim3(PP_NT), PpTile<128>::LDS, st, g);
+      hipLaunchKernelGGL(k_gemm_pp<256>, dim3((unsigned)pp_tiles), dim3(PP_NT), PpTile<256>::LDS, st, g);
       OPCK(hipGetLastError());
       return 0;
     }
@@ -471,26 +376,24 @@ int dca_ops_gemm(const GemmArgs* a, void* stream) {
   const int bn = narrow ? 64 : 128;
   const int tiles = ((g.M + GBM - 1) / GBM) * ((g.N + bn - 1) / bn);
   const dim3 grid(tiles, g.splits);
-  g.single = g.k_per_split <= getenv_reg_single_nk() * kt ? 1 : 0;  // short K: one buffer, 2x workgroups per CU
+  g.single = g.k_per_split <= REG_SINGLE_NK * kt ? 1 : 0;  // short K: one buffer, 2x workgroups per CU
   // K-contiguous operands with 16-B aligned rows: direct global -> LDS staging (k_gemm_glds)
   const int esz = g.fp8 ? 1 : 2;
   // (measured, bench/gemm_bench.py: +18..100 % on plain NT GEMMs; bf16 implicit convs only when C % 64 == 0 (one
   // tap per K-tile: a wave-uniform decode); fp8 implicit convs always (the register-staged fp8
   // kernel needs 219 VGPRs: one wave per SIMD); short-K narrow tiles stay on the single-buffer register kernel)
-  const bool glds = getenv_glds_ok() && !g.ta && !g.tb && !(narrow && g.single && !getenv_glds_narrow()) &&
-                    (g.conv == 1 ? (g.fp8 || (g.cC % 64 == 0 && getenv_glds_conv()) || getenv_glds_conv_any())
+  const bool glds = !g.ta && !g.tb && !(narrow && g.single && !GLDS_NARROW) &&
+                    (g.conv == 1 ? (g.fp8 || (g.cC % 64 == 0 && GLDS_CONV))
                                  : (g.conv == 0 && (long)g.lda * esz % 16 == 0 && (long)g.K * esz % 16 == 0)) &&
                     (long)g.ldb * esz % 16 == 0 && ((uintptr_t)g.A & 15) == 0 && ((uintptr_t)g.B & 15) == 0;
   if (glds) {
-    const int gs = getenv_glds_single();
-    g.single = gs >= 0 ? gs : (g.k_per_split <= 9 * kt ? 1 : 0);
-    g.stages = g.single ? 1 : getenv_glds_stages();
+    g.single = g.k_per_split <= GLDS_SINGLE_NK * kt ? 1 : 0;
+    g.stages = g.single ? 1 : GLDS_STAGES;
     const int l64b = g.single ? GemmTile<64>::LDS_SINGLE : g.stages * GemmTile<64>::BUF;
     const int l128b = g.single ? GemmTile<128>::LDS_SINGLE : g.stages * GemmTile<128>::BUF;
     // 8 waves (4 per SIMD at 2 workgroups per CU) for the double-buffered long-K loops: 0.92-0.95x time on the
     // batch-256 long-K convs; the single-buffer short-K launches keep 4 (8 measured 1.13-1.41x there)
-    const int gw = getenv_glds_waves();
-    const bool w8 = gw ? gw == 8 : !g.single;
+    const bool w8 = !g.single;
     const dim3 blk(w8 ? 512 : 256);
     // the epilogue's column-statistics combine uses (threads / (BN / 8)) x BN float2 of LDS
     const int red64 = (w8 ? 512 : 256) / 8 * 64 * 8, red128 = (w8 ? 512 : 256) / 16 * 128 * 8;
@@ -659,7 +562,7 @@ int dca_ops_maxpool_fwd(const void* x, void* y, void* arg, const PoolGeom* geom,
   const PoolGeom g = *geom;
   REQUIRE(g.K * g.K <= 255 && g.K > 0 && g.S > 0, "maxpool: bad window");
   if (g.K == 3 && g.S == 2 && g.P == 1 && g.H == 2 * g.Ho && g.W == 2 * g.Wo && g.C % 8 == 0 &&
-      getenv_pool_k3s2()) {
+      POOL_K3S2) {
     const dim3 grid(grid_for((long)g.N * g.Ho * g.Wo * g.C / 8));
     if (pool_idx32(g))
       hipLaunchKernelGGL(k_maxpool_fwd_k3s2<unsigned>, grid, dim3(256), 0, (hipStream_t)stream,
@@ -684,7 +587,7 @@ int dca_ops_maxpool_fwd(const void* x, void* y, void* arg, const PoolGeom* geom,
 int dca_ops_maxpool_bwd(const void* dy, const void* arg, void* dx, const PoolGeom* geom, void* stream) {
   const PoolGeom g = *geom;
   if (g.K == 3 && g.S == 2 && g.P == 1 && g.H == 2 * g.Ho && g.W == 2 * g.Wo && g.C % 8 == 0 &&
-      getenv_pool_k3s2()) {
+      POOL_K3S2) {
     const dim3 grid(grid_for((long)g.N * g.Ho * g.Wo * g.C / 8));
     if (pool_idx32(g))
       hipLaunchKernelGGL(k_maxpool_bwd_k3s2<unsigned>, grid, dim3(256), 0, (hipStream_t)stream,
