@@ -772,12 +772,16 @@ __device__ __forceinline__ f32x4 ld4_sc1(const float* base, int bytes, int off_f
   return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, 4 * off_floats, 0, 16));
 }
 
-// trunk / stem chunk b of CH outputs in slab fragment order, summed over the nslab workgroup slabs: thread (grp,
-// slot) sums float4 `slot` of slabs grp, grp + NG, ... (all in flight for batch 32), fixed order
+// trunk / stem chunk b of CH outputs in slab fragment order, summed over the nslab workgroup slabs in ONE order for
+// every block size (the 512-thread prologue reducers and the 256-thread reduction kernel give bitwise-equal sums):
+// VG = 2048 / CH virtual groups, group gv sums float4 `slot` of slabs gv, gv + VG, ... in slab order; the chunk
+// total is sum_g (acc(g) + acc(g + VG / 2)) over g < VG / 2, in g order.  A 512-thread workgroup runs one virtual
+// group per thread, a 256-thread one two (gv = grp, grp + VG / 2: it adds the pair before the LDS combine).
 template <int NTH, int CH>
 __device__ __forceinline__ void seg_chunk(const Ctx& cx, const Args& pa, const SegLayout& Ls, int b, int nslab,
                                           float* segv, f32x4* red) {
-  constexpr int NS = CH / 4, NG = NTH / NS, NU = 128 / NG;
+  constexpr int NS = CH / 4, VG = 2048 / CH, NG = NTH / NS, VPG = VG / NG, NU = 128 / VG, HG = VG / 2;
+  static_assert(NG * VPG == VG && (VPG == 1 || VPG == 2), "512- or 256-thread reducers");
   const int t = threadIdx.x;
   const bool stem = b >= Ls.r_trunk;
   const int chunk = stem ? b - Ls.r_trunk : b;
@@ -785,25 +789,38 @@ __device__ __forceinline__ void seg_chunk(const Ctx& cx, const Args& pa, const S
   const float* src = stem ? cx.SSLAB : pa.tslab;
   const int stride = stem ? SSLAB_N : WSLAB_N;
   const int ec = e0 < stride ? e0 : stride - 4;  // conv1's last 256-chunk is partial (1088 = 4.25 x 256)
-  f32x4 sacc = z4();
+  f32x4 sacc[VPG];
+#pragma unroll
+  for (int vp = 0; vp < VPG; ++vp) sacc[vp] = z4();
   for (int k0 = 0; k0 < nslab; k0 += 128) {
-    f32x4 v[NU];
 #pragma unroll
-    for (int u = 0; u < NU; ++u) {
-      const int k = k0 + grp + NG * u;
-      const int kc = k < nslab ? k : nslab - 1;
-      v[u] = ld4(src + (size_t)kc * stride + ec);  // plain loads: the slabs were written before the kernel boundary
+    for (int vp = 0; vp < VPG; ++vp) {
+      const int gv = grp + NG * vp;
+      f32x4 v[NU];
+#pragma unroll
+      for (int u = 0; u < NU; ++u) {
+        const int k = k0 + gv + VG * u;
+        const int kc = k < nslab ? k : nslab - 1;
+        v[u] = ld4(src + (size_t)kc * stride + ec);  // plain loads: the slabs were written before the kernel boundary
+      }
+#pragma unroll
+      for (int u = 0; u < NU; ++u)
+        if (k0 + gv + VG * u < nslab) sacc[vp] += v[u];
     }
-#pragma unroll
-    for (int u = 0; u < NU; ++u)
-      if (k0 + grp + NG * u < nslab) sacc += v[u];
   }
-  red[t] = sacc;
+  red[t] = VPG == 2 ? sacc[0] + sacc[VPG - 1] : sacc[0];  // (VPG = 2: groups grp and grp + HG)
   __syncthreads();
   if (t < NS) {
-    f32x4 tot = red[t];
+    f32x4 tot;
+    if constexpr (VPG == 2) {
+      tot = red[t];
 #pragma unroll
-    for (int g = 1; g < NG; ++g) tot += red[NS * g + t];
+      for (int g = 1; g < HG; ++g) tot += red[NS * g + t];
+    } else {
+      tot = red[t] + red[NS * HG + t];
+#pragma unroll
+      for (int g = 1; g < HG; ++g) tot += red[NS * g + t] + red[NS * (g + HG) + t];
+    }
     *(f32x4*)(segv + slot * 4) = e0 < stride ? tot : z4();
   }
 }

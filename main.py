@@ -5,7 +5,8 @@ Same entry point, function names and default behaviour as the reference:
 prints ``Using N GPUs`` (N>1), ``Epoch {e}, Training loss {x}`` at epoch 1 and every 10th epoch, and
 ``training time: {s:.3f} seconds``; rank 0 writes ``data/CIFAR-10/birds_vs_airplanes.pt`` at the same epochs.
 
-The step runs on the native MI355X engine (HIP/CDNA4 kernels, hipGraph replay, gradient all-reduce over RCCL);
+The step runs on the native MI355X engine (HIP/CDNA4 kernels, hipGraph replay; the gradient all-reduce is the
+in-kernel xGMI exchange by default, RCCL with ``--allreduce rccl``);
 ``--engine torch`` selects the generic stock-op path.  Every flag is optional (see --help); without flags the
 behaviour is the reference's.  With no GPU, nothing runs unless ``--backend gloo --world-size N`` asks for CPU
 ranks (reference: 0 GPUs -> mp.spawn(nprocs=0) silently does nothing).

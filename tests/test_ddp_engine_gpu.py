@@ -334,7 +334,7 @@ def _stall_worker(rank, ws, port, q):
         dev = torch.device("cuda", 0)
         data, labels = synthetic_cifar(NDATA, seed=5)
         torch.manual_seed(0)
-        tr = FusedDDPTrainer(NetResDeep().to(dev), data.to(dev), labels.to(dev), batch_max=32, dtype="bf16",
+        tr = FusedDDPTrainer(NetResDeep().to(dev), data.to(dev), labels.to(dev), batch_max=8, dtype="bf16",
                              comm="xgmi", max_indices=NDATA)
         assert tr.comm == "xgmi"
         eng = tr.engine
