@@ -167,7 +167,11 @@ def run_rank(a) -> None:
                                      if a.path == "ops" else "stock PyTorch: torch DDP + MIOpen convs + torch.optim.SGD, bf16 autocast" +
                                      (", channels_last" if cl else ", NCHW")},
                           "comm": getattr(ddp, "comm", None),
+                          # span of the gradient collectives on the comm stream per step (first bucket launched
+                          # to backward end: overlapped with the backward, not the exposed cost -- that is the
+                          # step-time difference against the run without --loopback)
                           "allreduce_us_per_step": round(comm_us / comm_n, 1) if comm_n else None,
+                          "allreduce_metric": "comm-stream span per step (overlapped)" if comm_n else None,
                           "xgmi_calibration": getattr(getattr(ddp, "xgmi", None), "calibration", None)}),
               flush=True)
         if a.result_file:

@@ -28,10 +28,10 @@ def main(path: str) -> None:
         gx, wx, lds, vg, sg, scr = meta[n]
         print(f"{n[:60]:60s} {len(v):6d} {sum(v) / 1e3:9.2f} {100 * sum(v) / grand:5.1f} {v[len(v) // 2]:10.2f} {v[len(v) // 10]:8.2f} {v[9 * len(v) // 10]:8.2f} "
               f"{gx:6d} {wx:5d} {lds:7d} {vg:5d} {sg:5d} {scr:7d}")
-    seq = [(n, s, e) for n, s, e, *_ in rows if "k_pk_step" in n or "k_pk_reduce" in n]
+    seq = [(n, s, e) for n, s, e, *_ in rows if "k_pks_step" in n or "k_pks_reduce" in n]
     if len(seq) > 20:
         gaps = [(b[1] - a[2]) / 1e3 for a, b in zip(seq, seq[1:])]
-        steps = [i for i, r in enumerate(seq) if "k_pk_step" in r[0]]
+        steps = [i for i, r in enumerate(seq) if "k_pks_step" in r[0]]
         per = [(seq[b][1] - seq[a][1]) / 1e3 for a, b in zip(steps, steps[1:])]
         print(f"\npersistent step: period median {statistics.median(per):.2f} us over {len(per)} steps; "
               f"dispatch gap median {statistics.median(gaps):.2f} us, max {max(gaps):.2f} us")

@@ -124,8 +124,7 @@ def main() -> int:
                               "gbps": round(2 * P * (c + co) / us / 1e3, 1), "rel_err": float(f"{e:.2e}")}),
                   flush=True)
     print(json.dumps({"total_us_per_step": round(tot_us, 1), "tflops": round(tot_fl / max(tot_us, 1e-9) / 1e6, 1),
-                      "worst_rel_err": float(f"{worst:.2e}"),
-                      "variant": os.environ.get("DCA_OPS_WGRAD_PP", "default")}), flush=True)
+                      "worst_rel_err": float(f"{worst:.2e}")}), flush=True)
     return 0 if worst < 2e-2 else 1
 
 

@@ -725,9 +725,12 @@ __device__ bool seg_exchange(const Ctx& cx, const RedAr& ra, int b, float* segv,
   if (t == 0) s_ep[1] = xg::failed(ra.err);  // this wait (or any other of this rank) expired
   __syncthreads();
   if (s_ep[1]) return false;
-  if (t == 0 && b < seg_layout(ra.seg_ch).r_ts && ra.peers.ticks != nullptr) {  // exposed exchange wait, summed over the segments the
-    atomicAdd(ra.peers.ticks, __builtin_amdgcn_s_memrealtime() - t_in);  // reduction kernel exchanges (metrics)
-    if (b == 0) atomicAdd(ra.peers.ticks + 1, 1ull);
+  // metrics: exchange wait of the trunk / conv1 segments (the reduction's, on the step's critical path; the fc
+  // segments exchange beside the backward) -- ticks and count per segment, so comm_time() gives the mean wait of
+  // one segment exchange, i.e. the exposed exchange time of a step (the segments exchange in parallel)
+  if (t == 0 && b < seg_layout(ra.seg_ch).r_ts && ra.peers.ticks != nullptr) {
+    atomicAdd(ra.peers.ticks, __builtin_amdgcn_s_memrealtime() - t_in);
+    atomicAdd(ra.peers.ticks + 1, 1ull);
   }
   for (int k = 4 * t; k < len; k += 4 * NTH) {  // exactly W loads in flight, one per peer link (rank_sum.h)
     *(f32x4*)(segv + k) = rank_sum(W, [&](int q) {

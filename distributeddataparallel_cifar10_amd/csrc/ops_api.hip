@@ -55,9 +55,8 @@ constexpr bool GLDS_NARROW = true;
 constexpr int REG_SINGLE_NK = 4;
 // glds K pipeline: 2 LDS buffers (3-4 measured 1.4-1.6x slower on the long-K shapes: fewer resident waves)
 constexpr int GLDS_STAGES = 2;
-inline int getenv_stream() {  // persistent short-K GEMMs: DCA_OPS_STREAM = 0 never, 1 k_gemm_stream whenever
-  static const int v = [] {    // eligible, 2 (default) by the shape rules at the launch site, 3 the default without
-                               // k_gemm_rows (A/B), 4 k_gemm_rows whenever eligible (tests: small M)
+inline int getenv_stream() {  // persistent short-K GEMM (k_gemm_stream): DCA_OPS_STREAM = 0 never, 1 whenever
+  static const int v = [] {    // eligible, 2 (default) by the shape rule at the launch site
     const char* e = getenv("DCA_OPS_STREAM");
     return e ? atoi(e) : 2;
   }();
@@ -296,55 +295,6 @@ int dca_ops_gemm(const GemmArgs* a, void* stream) {
   //   implicit conv with C % 64 == 0, N = 128: M >= 16384 (ResNet-50's layer-2 3x3 convolutions and their input
   //     gradients: 129.5 -> 117.5 us at batch 256).  The N = 64 conv stays on the one-tile kernel unless forced
   //     (DCA_OPS_STREAM=1, diagnostic): 174 us there, 218 us with 128 x 64 stream tiles, 283 us with 256 x 64
-  // resident-weight row kernel (k_gemm_rows) first: plain NT, K in {64, 128, 256}, no accumulation, M >= 16384
-  {
-    const int sk = getenv_stream();
-    const long long ab = ((long long)(g.M - 1) * g.lda + g.K) * 2, bb = ((long long)(g.N - 1) * g.ldb + g.K) * 2;
-    const bool rows_ok = (sk == 2 || sk == 4) && g.conv == 0 && !g.ta && !g.tb && !g.fp8 && g.splits == 1 &&
-                         g.wperm_T <= 0 && g.orow_S <= 0 && !g.relu && g.out_bf16 && g.beta == 0.f && !g.beta_mask &&
-                         (g.K == 64 || g.K == 128 || g.K == 256) && g.N % 64 == 0 && g.M >= (sk == 4 ? 1 : 16384) &&
-                         g.lda % 8 == 0 && g.lda >= g.K && g.ldb % 8 == 0 && g.ldb >= g.K && g.ldc % 8 == 0 &&
-                         g.ldc >= g.N && ((uintptr_t)g.A & 15) == 0 && ((uintptr_t)g.B & 15) == 0 &&
-                         ((uintptr_t)g.C & 15) == 0 && ab < (1LL << 31) && bb < (1LL << 31) &&
-                         (long long)g.M * g.ldc * 2 < (1LL << 31);
-    if (rows_ok) {
-      static int ncu = 0;
-      if (!ncu) {
-        int dev = 0;
-        OPCK(hipGetDevice(&dev));
-        OPCK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
-      }
-      const int nfr = g.K == 64 ? (g.N % 256 == 0 ? 16 : g.N % 128 == 0 ? 8 : 4) : (g.K == 128 && g.N % 128 == 0 ? 8 : 4);
-      const int ncb = g.N / (16 * nfr);
-      int nx = std::max(1, 2 * ncu / 8);  // two resident workgroups per CU, split evenly over the column blocks
-      nx = std::max(ncb, nx / ncb * ncb);
-      const dim3 gr((unsigned)(8 * nx)), bl(RW_NT);
-#define ROWS_LAUNCH(NFR, KS, D)                                                                              \
-  do {                                                                                                       \
-    constexpr int lds_ = RowsTile<NFR, KS>::LDS;                                                             \
-    static bool attr_set = false;                                                                            \
-    if (!attr_set) {                                                                                         \
-      OPCK(hipFuncSetAttribute((const void*)k_gemm_rows<NFR, KS, D>,                                         \
-                               hipFuncAttributeMaxDynamicSharedMemorySize, lds_));                           \
-      attr_set = true;                                                                                       \
-    }                                                                                                        \
-    hipLaunchKernelGGL((k_gemm_rows<NFR, KS, D>), gr, bl, lds_, st, g);                                    \
-  } while (0)
-      if (g.K == 64) {
-        if (nfr == 16) ROWS_LAUNCH(16, 1, 2);
-        else if (nfr == 8) ROWS_LAUNCH(8, 1, 3);
-        else ROWS_LAUNCH(4, 1, 3);
-      } else if (g.K == 128) {
-        if (nfr == 8) ROWS_LAUNCH(8, 2, 3);
-        else ROWS_LAUNCH(4, 2, 3);
-      } else {
-        ROWS_LAUNCH(4, 4, 2);
-      }
-#undef ROWS_LAUNCH
-      OPCK(hipGetLastError());
-      return 0;
-    }
-  }
   {
     const int sk = getenv_stream();
     const bool conv = g.conv == 1;
@@ -354,7 +304,7 @@ int dca_ops_gemm(const GemmArgs* a, void* stream) {
     const int mw = g.N % 128 == 0 ? 1 : 2;  // 128 x 128 tiles, or 256 x 64 for N % 128 == 64
     const bool shape_ok = conv ? (g.cC % 64 == 0 && g.cKH * g.cKW <= 32 && (g.N == 64 || g.N == 128) && g.orow_S <= 0 &&
                                   g.M < (1 << 24) &&
-                                  (sk == 1 || (sk >= 2 && STREAM_CONV && g.N == 128 && g.M >= 16384)))
+                                  (sk == 1 || (sk == 2 && STREAM_CONV && g.N == 128 && g.M >= 16384)))
                                : (g.conv == 0 && !g.ta && g.lda % 8 == 0 && g.lda >= g.K &&
                                   (g.N % 128 == 0 || g.N == 64) &&
                                   (sk == 1 || (g.K <= 512 && g.M >= 16384 &&

@@ -1327,6 +1327,14 @@ __global__ void __launch_bounds__(ST_NT, 2) k_gemm_stream(GemmArgs g) {
   };
   typedef float f2 __attribute__((ext_vector_type(2)));
   typedef __bf16 bf2 __attribute__((ext_vector_type(2)));
+  // output image (STG: 128 x 128 tiles, the output-heavy N % 128 == 0 calls; the 256 x 64 tiles of the read-heavy
+  // N = 64 calls store straight from the accumulators -- staging them spilled): TM rows of RB bytes = CPR 16-B
+  // chunks; chunk c of row r at c ^ img_sw(r), so the 16 rows of a fragment store and the 16 chunks of a read-out
+  // pass each hit 16 distinct 16-B bank groups
+  constexpr bool STG = NF == 2 && MW == 1;
+  constexpr int RB = 2 * TN, CPR = TN / 8;
+  static_assert(TM * CPR == 8 * ST_NT, "8 read-out passes");
+  auto img_sw = [](int r) { return CPR == 16 ? (r & 15) : ((r >> 1) & 7); };
   st_v4u old[8];  // beta != 0: this tile's C_old rows (lane (q, j): row 16 m + j, columns c0 .. c0 + 4 NF - 1)
   unsigned omk[8];  // masked source: the mask byte of those columns (c0 % 8 == 0 for NF = 2, 0 or 4 for NF = 1)
   auto load_old = [&](int tm, int tn) {
@@ -1353,7 +1361,7 @@ __global__ void __launch_bounds__(ST_NT, 2) k_gemm_stream(GemmArgs g) {
   };
   // epilogue of tile (tm, tn): lane (q, j) owns columns c0 .. c0 + 4 NF - 1 of rows tm*128 + 16 m + j.
   // more: the DMA of the next K-step was issued after the C_old loads.  FULL: no row past M.
-  auto epilogue = [&](int tm, int tn, bool more, auto full, auto acc_old) {
+  auto epilogue = [&](int tm, int tn, bool more, char* stg, auto full, auto acc_old) {
     constexpr bool FULL = decltype(full)::value, BETA = decltype(acc_old)::value;
     constexpr int NP = 2 * NF;  // column pairs per lane
     const int c0 = tn * TN + WN * wn + 4 * NF * q;
@@ -1392,9 +1400,27 @@ __global__ void __launch_bounds__(ST_NT, 2) k_gemm_stream(GemmArgs g) {
         s1[e] += d;
         sq[e] += d * d;
       }
-      const unsigned o = in ? ((unsigned)row * (unsigned)g.ldc + c0) * 2u : OOB;
-      if constexpr (NF == 2) __builtin_amdgcn_raw_buffer_store_b128(st_v4u{pk[0], pk[1], pk[2], pk[3]}, crs, o, 0, 2);
-      else __builtin_amdgcn_raw_buffer_store_b64(st_v2u{pk[0], pk[1]}, crs, o, 0, 2);  // (nt: streamed output)
+      if constexpr (STG) {  // into the LDS image of the tile: row rl (2 TN bytes), 16-B chunk 4 wn + q, swizzled
+        const int rl = GBM * wm + 16 * m + j;
+        *(st_v4u*)(stg + rl * RB + (((4 * wn + q) ^ img_sw(rl)) << 4)) = st_v4u{pk[0], pk[1], pk[2], pk[3]};
+      } else {
+        const unsigned o = in ? ((unsigned)row * (unsigned)g.ldc + c0) * 2u : OOB;
+        if constexpr (NF == 2) __builtin_amdgcn_raw_buffer_store_b128(st_v4u{pk[0], pk[1], pk[2], pk[3]}, crs, o, 0, 2);
+        else __builtin_amdgcn_raw_buffer_store_b64(st_v2u{pk[0], pk[1]}, crs, o, 0, 2);  // (nt: streamed output)
+      }
+    }
+    if constexpr (STG) {
+      // whole rows out of the LDS image: a wave instruction stores 4 rows x 256 or 8 rows x 128 contiguous bytes
+      // (16 rows x 64 B straight from the accumulators is the fragment-shaped form the MI355X guide measures at 2x
+      // TA_BUSY)
+      __syncthreads();
+#pragma unroll
+      for (int ps = 0; ps < 8; ++ps) {
+        const int idx = ST_NT * ps + (int)threadIdx.x, rl = idx / CPR, ch = idx % CPR, row = tm * TM + rl;
+        const st_v4u v = *(const st_v4u*)(stg + rl * RB + ((ch ^ img_sw(rl)) << 4));
+        const unsigned o = row < g.M ? ((unsigned)row * (unsigned)g.ldc + tn * TN + 8 * ch) * 2u : OOB;
+        __builtin_amdgcn_raw_buffer_store_b128(v, crs, o, 0, 2);  // (nt: streamed output)
+      }
     }
     float r1[2 * NP], r2[2 * NP];
 #pragma unroll
@@ -1411,6 +1437,7 @@ __global__ void __launch_bounds__(ST_NT, 2) k_gemm_stream(GemmArgs g) {
           st_v4u{__float_as_uint(r1[2 * p]), __float_as_uint(r2[2 * p]), __float_as_uint(r1[2 * p + 1]),
                  __float_as_uint(r2[2 * p + 1])},
           srs, so + 16u * p, 0, 0);
+    if constexpr (STG) __syncthreads();  // the image is read out before its buffer takes the next DMA
   };
 
   // the stream: step s = (tile k, K-step kt), s = k * nk + kt; the DMA of step s + 1 is in flight during step s.
@@ -1452,202 +1479,15 @@ __global__ void __launch_bounds__(ST_NT, 2) k_gemm_stream(GemmArgs g) {
       __builtin_amdgcn_s_barrier();  // every wave is done reading this buffer before it is refilled
       asm volatile("" ::: "memory");
     }
+    // (STG: the tile's last K-step buffer, free after the barrier above, holds the output image)
     const bool full = tm * TM + GBM * wm + GBM <= g.M, more = (k + 1) * nk < steps;
+    char* stg = smem + (((k + 1) * nk - 1) & 1) * BUF;
     if (bta) {
-      if (full) epilogue(tm, tn, more, std::true_type{}, std::true_type{});
-      else epilogue(tm, tn, more, std::false_type{}, std::true_type{});
+      if (full) epilogue(tm, tn, more, stg, std::true_type{}, std::true_type{});
+      else epilogue(tm, tn, more, stg, std::false_type{}, std::true_type{});
     } else {
-      if (full) epilogue(tm, tn, more, std::true_type{}, std::false_type{});
-      else epilogue(tm, tn, more, std::false_type{}, std::false_type{});
-    }
-  }
-}
-
-// ---------------------------------------------------------------------------------------------------------
-// k_gemm_rows: the short-K (K = 64 .. 256) plain NT GEMMs of the channels-last 1x1 convolutions with the weight
-// column block RESIDENT in LDS and the activations streamed straight into registers.  k_gemm_stream stages A and B
-// through LDS by DMA with one K-step in flight per workgroup (32 KB), so an output-heavy call like 802816 x 256 x 64
-// sits at ~3.1 TB/s: latency-bound, not bandwidth-bound.  Here
-//   * the workgroup's weight block (16 NFR columns x K, <= 64 KB) is loaded into LDS once, in the permuted row order
-//     of k_gemm_stream (lane (q, j) ends with 8 consecutive output columns per fragment pair: 16-B stores);
-//   * each of the 4 waves owns 32 rows of a 128-row block and loads its A fragments (16 B per lane and 32-wide K
-//     slice, the MFMA's src1 layout) with buffer loads into registers, D tiles ahead -- no LDS traffic or barrier
-//     for A; with 2 workgroups per CU that keeps 8 x D x 32 x 2K bytes of reads in flight per CU;
-//   * epilogue from registers as in k_gemm_stream (alpha, bias, bf16, nt stores); the BN column statistics of the
-//     128-row block are summed per wave (DPP) and over the 4 waves in LDS (fixed order: deterministic), one
-//     col_stats row per block (the layout k_bn_finalize reduces);
-//   * schedule: XCD x = blockIdx % 8 owns row blocks [x nb / 8, (x + 1) nb / 8); its workgroups are split over
-//     the N / (16 NFR) column blocks (launcher: grid / 8 a multiple), so the column blocks of a row block run on
-//     one XCD at about the same time and re-read A from its L2.
-// Requirements (launcher): bf16 NT, K = 64 KS, N % (16 NFR) == 0, bf16 output, no beta / ReLU / split / remap,
-// 16-B aligned rows, operand and output byte ranges < 2^31.
-// ---------------------------------------------------------------------------------------------------------
-constexpr int RW_NT = 256;
-template <int NFR, int KS>
-struct RowsTile {
-  static constexpr int NCB = 16 * NFR;                                   // columns per block
-  static constexpr int LDS = KS * NCB * 128 + 2 * NCB * 4 + 4 * NCB * 8;  // B | bias, shift | statistics
-};
-template <int NFR, int KS, int D>
-__global__ void __launch_bounds__(RW_NT, 2) k_gemm_rows(GemmArgs g) {
-  static_assert(NFR % 2 == 0 && D >= 2, "fragment pairs, >= 2 A tiles in flight");
-  constexpr int NCB = RowsTile<NFR, KS>::NCB;
-  constexpr int NKK = 2 * KS;  // 32-wide K slices
-  constexpr int NL = 2 * NKK;  // A loads per lane and tile (2 row fragments x NKK)
-  constexpr int NST = NFR;     // output stores per lane and tile (2 row fragments x NFR / 2 column chunks)
-  static_assert((D - 1) * NL + NST + 1 <= 63, "vmcnt range");
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  constexpr unsigned OOB = 0x80000000u;
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, j = lane & 15, q = lane >> 4;
-  const int ncb = g.N / NCB, nblk = (g.M + GBM - 1) / GBM;
-  char* lb = smem;
-  float* sbias = (float*)(smem + KS * NCB * 128);
-  float* sshift = sbias + NCB;
-  float* sst = sshift + NCB;  // [4 waves][NCB] x (sum, sumsq)
-  const int nxwg = gridDim.x >> 3, xcd = blockIdx.x & 7, loc = blockIdx.x >> 3;
-  const int cb = loc % ncb, per = nxwg / ncb, slot = loc / ncb;
-  const int b_beg = (int)((long long)xcd * nblk / 8), b_end = (int)((long long)(xcd + 1) * nblk / 8);
-  const int nmy = b_end - b_beg > slot ? (b_end - b_beg - slot + per - 1) / per : 0;
-  const int n0 = cb * NCB;
-  // weight block: LDS row 16 f + i of K-tile kt holds weight row n0 + 32 (f >> 1) + 8 (i >> 2) + 4 (f & 1) + (i & 3)
-  const unsigned short* Bp = (const unsigned short*)g.B;
-  for (int e = threadIdx.x; e < KS * NCB * 8; e += RW_NT) {
-    const int c = e & 7, r = (e >> 3) % NCB, kt = e / (8 * NCB), f = r >> 4, i = r & 15;
-    const int n = n0 + 32 * (f >> 1) + 8 * (i >> 2) + 4 * (f & 1) + (i & 3);
-    *(uint4*)(lb + kt * NCB * 128 + lds_off(r, c)) = *(const uint4*)(Bp + (size_t)n * g.ldb + kt * 64 + c * 8);
-  }
-  for (int c = threadIdx.x; c < NCB; c += RW_NT) {
-    sbias[c] = g.bias ? g.bias[n0 + c] : 0.f;
-    sshift[c] = g.col_stats ? g.stats_shift[n0 + c] : 0.f;
-  }
-  const float alpha = gemm_alpha(g);
-  __syncthreads();  // (also drains these loads: the vmcnt accounting below starts from zero)
-  const __amdgpu_buffer_rsrc_t ars = __builtin_amdgcn_make_buffer_rsrc(
-      (void*)g.A, (short)0, (int)(((long long)(g.M - 1) * g.lda + g.K) * 2), 0x00020000);
-  const __amdgpu_buffer_rsrc_t crs = __builtin_amdgcn_make_buffer_rsrc(
-      g.C, (short)0, (int)((long long)g.M * g.ldc * 2), 0x00020000);
-  const __amdgpu_buffer_rsrc_t srs = __builtin_amdgcn_make_buffer_rsrc(
-      (void*)g.col_stats, (short)0, g.col_stats ? (int)((long long)nblk * g.N * 8) : 0, 0x00020000);
-  const unsigned lda2 = (unsigned)g.lda * 2u;
-  const bool stats = g.col_stats != nullptr;
-
-  st_v4u abuf[D][NL];
-  // A fragments of tile i of this wave's list (past the end: out-of-range offsets, zeros, no memory traffic -- the
-  // load count per tile stays constant for the vmcnt accounting)
-  auto load_a = [&](st_v4u(&dst)[NL], int i) {
-    const int b = b_beg + slot + i * per;
-#pragma unroll
-    for (int m = 0; m < 2; ++m) {
-      const int row = b * GBM + 32 * w + 16 * m + j;
-      const unsigned base = (i < nmy && row < g.M) ? (unsigned)row * lda2 + 16u * q : OOB;
-#pragma unroll
-      for (int kk = 0; kk < NKK; ++kk) dst[m * NKK + kk] = __builtin_amdgcn_raw_buffer_load_b128(ars, base, 64 * kk, 0);
-    }
-  };
-  f32x4 acc[2][NFR];
-  auto compute = [&](const st_v4u(&a)[NL]) {
-#pragma unroll
-    for (int kk = 0; kk < NKK; ++kk) {
-      const char* lk = lb + (kk >> 1) * NCB * 128;
-#pragma unroll
-      for (int f = 0; f < NFR; ++f) {
-        const s16x8 wf = *(const s16x8*)(lk + lds_off(16 * f + j, 4 * (kk & 1) + q));
-#pragma unroll
-        for (int m = 0; m < 2; ++m)
-          acc[m][f] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
-              wf, __builtin_bit_cast(s16x8, a[m * NKK + kk]), kk == 0 ? f32x4{0.f, 0.f, 0.f, 0.f} : acc[m][f], 0, 0, 0);
-      }
-    }
-  };
-  auto rowsum16 = [](float x) {
-    x += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, x), 0x111, 0xf, 0xf, true));
-    x += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, x), 0x112, 0xf, 0xf, true));
-    x += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, x), 0x114, 0xf, 0xf, true));
-    x += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, x), 0x118, 0xf, 0xf, true));
-    return x;
-  };
-  typedef float f2 __attribute__((ext_vector_type(2)));
-  typedef __bf16 bf2 __attribute__((ext_vector_type(2)));
-  // epilogue of row block b: lane (q, j) owns columns 32 t + 8 q .. + 7 of rows 16 m + j of the wave's 32 rows
-  auto epilogue = [&](int b, auto full) {
-    constexpr bool FULL = decltype(full)::value;
-    const int rb = b * GBM + 32 * w;
-#pragma unroll
-    for (int t = 0; t < NFR / 2; ++t) {
-      const int c = 32 * t + 8 * q;
-      f2 b2[4], sh2[4], s1[4], sq[4];
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        b2[e] = *(const f2*)(sbias + c + 2 * e);
-        sh2[e] = *(const f2*)(sshift + c + 2 * e);
-        s1[e] = sq[e] = f2{0.f, 0.f};
-      }
-#pragma unroll
-      for (int m = 0; m < 2; ++m) {
-        const int row = rb + 16 * m + j;
-        const bool in = FULL || row < g.M;
-        unsigned pk[4];
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {  // columns c + 2e, c + 2e + 1 = fragment 2t + (e >> 1), elements 2 (e & 1) + {0, 1}
-          const f32x4& a = acc[m][2 * t + (e >> 1)];
-          const f2 x = f2{a[2 * (e & 1)], a[2 * (e & 1) + 1]} * alpha + b2[e];
-          pk[e] = __builtin_bit_cast(unsigned, __builtin_convertvector(x, bf2));
-          f2 d = f2{__uint_as_float(pk[e] << 16), __uint_as_float(pk[e] & 0xffff0000u)} - sh2[e];  // as stored
-          if (!FULL && !in) d = f2{0.f, 0.f};
-          s1[e] += d;
-          sq[e] += d * d;
-        }
-        const unsigned o = in ? ((unsigned)row * (unsigned)g.ldc + (unsigned)(n0 + c)) * 2u : OOB;
-        __builtin_amdgcn_raw_buffer_store_b128(st_v4u{pk[0], pk[1], pk[2], pk[3]}, crs, o, 0, 2);  // (nt: streamed)
-      }
-      if (stats) {
-        float r[16];
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          r[4 * e] = rowsum16(s1[e][0]);
-          r[4 * e + 1] = rowsum16(sq[e][0]);
-          r[4 * e + 2] = rowsum16(s1[e][1]);
-          r[4 * e + 3] = rowsum16(sq[e][1]);
-        }
-        if (j == 15) {
-          float4* dst = (float4*)(sst + 2 * (w * NCB + c));
-#pragma unroll
-          for (int e = 0; e < 4; ++e) dst[e] = float4{r[4 * e], r[4 * e + 1], r[4 * e + 2], r[4 * e + 3]};
-        }
-      }
-    }
-  };
-
-#pragma unroll
-  for (int d = 0; d < D - 1; ++d) load_a(abuf[d], d);
-  for (int i0 = 0; i0 < nmy; i0 += D) {
-#pragma unroll
-    for (int sl = 0; sl < D; ++sl) {
-      const int i = i0 + sl;
-      if (i >= nmy) break;  // (workgroup-uniform)
-      load_a(abuf[(sl + D - 1) % D], i + D - 1);
-      // outstanding, oldest first: tile i's loads, tiles i + 1 .. i + D - 2, the previous epilogue's stores (NST,
-      // + 1 statistics store on the first NCB threads), tile i + D - 1
-      if (i == 0) wait_vmcnt<(D - 1) * NL>();
-      else wait_vmcnt<(D - 1) * NL + NST>();
-      compute(abuf[sl]);
-      const int b = b_beg + slot + i * per;
-      if (b * GBM + GBM <= g.M) epilogue(b, std::true_type{});
-      else epilogue(b, std::false_type{});
-      if (stats) {  // the block's 4 wave partials, in wave order
-        __syncthreads();
-        for (int c = threadIdx.x; c < NCB; c += RW_NT) {
-          float s = 0.f, s2 = 0.f;
-#pragma unroll
-          for (int v = 0; v < 4; ++v) {
-            s += sst[2 * (v * NCB + c)];
-            s2 += sst[2 * (v * NCB + c) + 1];
-          }
-          __builtin_amdgcn_raw_buffer_store_b64(st_v2u{__float_as_uint(s), __float_as_uint(s2)}, srs,
-                                                ((unsigned)b * (unsigned)g.N + (unsigned)(n0 + c)) * 8u, 0, 0);
-        }
-        __syncthreads();
-      }
+      if (full) epilogue(tm, tn, more, stg, std::true_type{}, std::false_type{});
+      else epilogue(tm, tn, more, stg, std::false_type{}, std::false_type{});
     }
   }
 }

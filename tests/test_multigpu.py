@@ -57,9 +57,9 @@ def test_ddp_engine_cross_device(gpu, port, comm, dtype):
     spawn_ranks(_xgmi_worker, ws, lambda r: (r, ws, port, dtype, True), dict(comm=comm, own_device=True), shared=False)
 
 
-def _check_bench_line(out, n, allreduce=None):
+def _check_bench_line(out, n, allreduce=None, batch=32):
     assert out["n_gpus"] == n and out["value"] > 0 and out["loss_finite"], out
-    assert out["config"]["parallelism"] == f"dp{n}" and out["config"]["global_batch"] == 32 * n
+    assert out["config"]["parallelism"] == f"dp{n}" and out["config"]["global_batch"] == batch * n
     if allreduce is not None:
         assert out["allreduce"] == allreduce, out
     if n > 1 and out["allreduce"] == "xgmi":
@@ -129,14 +129,15 @@ def test_resnet50_bench_self_launch(gpu):
 # ---- shared-GPU rehearsals of the same commands (run on the 1-GPU tier) ----------------------------------------
 def test_bench_driver_command_shared_gpu(gpu):
     """``python bench.py --gpus 2`` with both ranks on GPU 0: self-launch, gloo rendezvous, the engine's xGMI
-    gradient exchange between the ranks, slowest-rank timing and the fp32 second timing."""
-    lines = _bench(["bench.py", "--gpus", "2", "--steps", "32", "--warmup", "8"], shared=True)
+    gradient exchange between the ranks, slowest-rank timing and the fp32 second timing.  Per-rank batch 16: two
+    batch-32 grids (2 x 128 step workgroups) would fill the device exactly, which the co-residency rule refuses."""
+    lines = _bench(["bench.py", "--gpus", "2", "--batch", "16", "--steps", "32", "--warmup", "8"], shared=True)
     assert len(lines) == 1, lines
-    _check_bench_line(lines[0], 2, "xgmi")
+    _check_bench_line(lines[0], 2, "xgmi", batch=16)
 
 
 def test_bench_sweep_shared_gpu(gpu):
-    lines = _bench(["bench.py", "--sweep=1,2", "--steps", "32", "--warmup", "8", "--no-fp32"], shared=True,
+    lines = _bench(["bench.py", "--sweep=1,2", "--batch", "16", "--steps", "32", "--warmup", "8", "--no-fp32"], shared=True,
                    timeout=600)
     per_n, summary = lines[:-1], lines[-1]
     assert [ln["n_gpus"] for ln in per_n] == [1, 2] and all(ln["loss_finite"] for ln in per_n)
