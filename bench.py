@@ -150,7 +150,8 @@ def run_rank(a) -> dict | None:
         "engine": main_run["engine"],
         "allreduce": main_run["comm"],
         "per_rank_ms_per_step": [round(1e3 * p[0] / a.steps, 5) for p in per_rank],
-        # exposed gradient-exchange wait per step, mean over the gradient segments (xGMI path only)
+        # exposed gradient-exchange wait per step: the mean wait of one trunk / conv1 segment exchange (they run in
+        # parallel on the reduction's critical path; xGMI path only)
         "allreduce_us_per_step": ([round(p[1], 2) for p in per_rank] if main_run["comm"].startswith("xgmi")
                                   else None),
         "data": "synthetic (CIFAR-10-shaped uint8 3x32x32, 50000 samples, random labels; random-init weights)",

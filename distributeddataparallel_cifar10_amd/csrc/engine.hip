@@ -114,7 +114,10 @@ struct Engine {
   int fc_in_step = 1;  // the fc1 / fc-tail gradient segments run on the step kernel's fc workers (pks::N_FCW extra
                        // workgroups beside the backward); off: in the reduction kernel.  Off whenever the step and
                        // its fc workers would exceed the co-resident budget, and when xGMI peers share this device
-  int prologue = 1;  // chunks apply each step's gradient segments in the next step's launch (prologue_ok)
+  // chunks apply each step's gradient segments in the next step's launch (prologue_ok).  Off by default: same box,
+  // 300 steps bf16, 84.3 / 84.7 us with it against 83.3 / 83.0 us without (profiles/prologue_ab_r5h.log); the
+  // reducers' latency lands on the stem's critical path.  DCA_PKS_PROLOGUE=1 turns it on (bitwise equal: tests).
+  int prologue = 0;
   int shared_device = 0;  // set by the host: number of xGMI ranks on this device (shared-GPU rehearsal; 0/1: not
                           // shared): the coarse 107-segment layout, and fc workers only when every co-scheduled
                           // grid fits (fc_in_step_for), so a spinning kernel always leaves CUs for a peer's step
