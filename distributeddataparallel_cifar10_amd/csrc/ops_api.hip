@@ -295,6 +295,40 @@ int dca_ops_gemm(const GemmArgs* a, void* stream) {
   //   implicit conv with C % 64 == 0, N = 128: M >= 16384 (ResNet-50's layer-2 3x3 convolutions and their input
   //     gradients: 129.5 -> 117.5 us at batch 256).  The N = 64 conv stays on the one-tile kernel unless forced
   //     (DCA_OPS_STREAM=1, diagnostic): 174 us there, 218 us with 128 x 64 stream tiles, 283 us with 256 x 64
+  // stride-1 implicit convs with 64 outputs on narrow input rows -> k_direct_conv: the space-to-depth ResNet stem
+  // (4 x 4 taps over 16 channels) and the 64-channel 3 x 3 / pad 1 convolutions (layer 1 forward and input gradient)
+  const bool dc_stem = g.cC == 16 && g.cKH == 4 && g.cKW == 4 && g.cP == 0;
+  const bool dc_3x3 = g.cC == 64 && g.cKH == 3 && g.cKW == 3 && g.cP == 1;
+  if (g.conv == 1 && (dc_stem || dc_3x3) && g.cS == 1 && g.N == 64 && !g.fp8 && !g.tb && g.splits == 1 && g.wperm_T <= 0 && g.orow_S <= 0 && g.out_bf16 && !g.relu &&
+      g.beta == 0.f && !g.beta_mask && g.ldb >= g.K && g.ldb % 8 == 0 && g.ldc >= 64 && g.ldc % 8 == 0 &&
+      ((uintptr_t)g.A & 15) == 0 && ((uintptr_t)g.B & 15) == 0 && ((uintptr_t)g.C & 15) == 0 &&
+      (long long)g.cN * g.cH * g.cW * g.cC * 2 < (1LL << 31) && (long long)g.M * g.ldc * 2 < (1LL << 31) &&
+      g.M < (1 << 24)) {
+    static int ncu_s = 0;
+    if (!ncu_s) {
+      int dev = 0;
+      OPCK(hipGetDevice(&dev));
+      OPCK(hipDeviceGetAttribute(&ncu_s, hipDeviceAttributeMultiprocessorCount, dev));
+    }
+    const long blocks = (g.M + GBM - 1) / GBM;
+    long grid = std::min<long>(2L * ncu_s, (blocks + 7) / 8 * 8);
+    grid = std::max<long>(8, grid / 8 * 8);
+    if (dc_stem) {
+      constexpr int lds = DirectConv<16, 4, 4>::LDS;
+      hipLaunchKernelGGL((k_direct_conv<16, 4, 4>), dim3((unsigned)grid), dim3(DC_NT), lds, st, g);
+    } else {
+      constexpr int lds = DirectConv<64, 3, 3>::LDS;
+      static bool attr = false;
+      if (!attr) {
+        OPCK(hipFuncSetAttribute((const void*)k_direct_conv<64, 3, 3>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                 lds));
+        attr = true;
+      }
+      hipLaunchKernelGGL((k_direct_conv<64, 3, 3>), dim3((unsigned)grid), dim3(DC_NT), lds, st, g);
+    }
+    OPCK(hipGetLastError());
+    return 0;
+  }
   {
     const int sk = getenv_stream();
     const bool conv = g.conv == 1;

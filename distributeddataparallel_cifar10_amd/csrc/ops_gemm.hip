@@ -1492,6 +1492,178 @@ __global__ void __launch_bounds__(ST_NT, 2) k_gemm_stream(GemmArgs g) {
   }
 }
 
+// ---------------------------------------------------------------------------------------------------------
+// k_direct_conv<C, KH, KW>: stride-1 implicit convolutions with 64 output channels whose input rows are too narrow
+// for the LDS-staged implicit-GEMM kernels to stream well:
+//   * <16, 4, 4>: the space-to-depth ResNet stem (ops/functional.py stem_s2d_index): 4 x 4 taps over the 16-channel
+//     s2d input, no padding.  The generic kernels stage A through LDS in 16-B chunks per tap and ran it at 402 us
+//     (1.3 TB/s) at batch 256;
+//   * <64, 3, 3>: the 64-channel 3 x 3 / pad 1 convolutions of ResNet-50's layer 1 and their input gradients
+//     (122-142 us each on the one-tile glds kernel at batch 256: 1.5 TB/s, 415 TF).
+// Design:
+//   * persistent workgroups walk 128-pixel M blocks (XCD-contiguous ranges); the 64 x K weight matrix stays in LDS
+//     (K = KH KW C: 32 KB for the stem), rows permuted as in k_gemm_stream so a lane ends with 16 consecutive
+//     output channels of one pixel;
+//   * each wave owns 32 pixels of a block as two 16-pixel fragments and loads their A operands straight from
+//     global memory into registers: K-slice s (32 k) of pixel j is 16 B = 8 channels per lane (k = 32 s + 8 q);
+//     an input pixel is read by KH KW taps of up to KH KW output pixels, so these loads hit L1 / L2 after the first;
+//     padding taps load zeros through an out-of-range offset.  The next fragment's loads are in flight during this
+//     fragment's MFMAs and epilogue (two register buffers);
+//   * epilogue from registers: alpha, bias, bf16, 32 B per pixel and lane (nt stores); the BN column statistics of
+//     the block are summed over both fragments in registers, over 16 pixels by DPP, over the 4 waves in LDS in wave
+//     order: one col_stats row per 128-row block (the layout k_bn_finalize reduces).
+// Requirements (launcher): conv == 1, stride 1, N = 64, K = KH KW C, bf16 out, no beta / ReLU / split / remap,
+// byte ranges < 2^31.
+// ---------------------------------------------------------------------------------------------------------
+constexpr int DC_NT = 256;
+template <int C, int KH, int KW>
+struct DirectConv {
+  static constexpr int K = KH * KW * C, NS = K / 32;                 // K, 32-wide K slices
+  static constexpr int LDS = K * 128 + 2 * 64 * 4 + 4 * 64 * 8;      // weights | bias, shift | statistics
+  static_assert(K % 64 == 0 && (C % 8) == 0 && (32 % C == 0 || C % 32 == 0), "slices of whole 8-channel chunks");
+};
+template <int C, int KH, int KW>
+__global__ void __launch_bounds__(DC_NT, 2) k_direct_conv(GemmArgs g) {
+  using T = DirectConv<C, KH, KW>;
+  constexpr int NS = T::NS;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  constexpr unsigned OOB = 0x80000000u;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, j = lane & 15, q = lane >> 4;
+  char* lw = smem;  // weights: K-tile kt (64 k) at kt * 8 KB, row r (128 B, XOR-swizzled chunks: lds_off)
+  float* sbias = (float*)(smem + T::K * 128);
+  float* sshift = sbias + 64;
+  float* sst = sshift + 64;  // [4 waves][64] x (sum, sumsq)
+  // weight row r = 16 f + i of the LDS image holds output channel 16 (i >> 2) + 4 f + (i & 3): lane (q, j) of
+  // fragment f then holds channels 16 q + 4 f .. + 3, i.e. channels 16 q .. 16 q + 15 over the 4 fragments
+  const unsigned short* Bp = (const unsigned short*)g.B;
+  for (int e = threadIdx.x; e < T::K / 64 * 64 * 8; e += DC_NT) {
+    const int c = e & 7, r = (e >> 3) & 63, kt = e >> 9, f = r >> 4, i = r & 15;
+    const int co = 16 * (i >> 2) + 4 * f + (i & 3);
+    *(uint4*)(lw + kt * 8192 + lds_off(r, c)) = *(const uint4*)(Bp + (size_t)co * g.ldb + kt * 64 + c * 8);
+  }
+  if (threadIdx.x < 64) {
+    sbias[threadIdx.x] = g.bias ? g.bias[threadIdx.x] : 0.f;
+    sshift[threadIdx.x] = g.col_stats ? g.stats_shift[threadIdx.x] : 0.f;
+  }
+  const float alpha = gemm_alpha(g);
+  __syncthreads();
+  const int nblk = (g.M + GBM - 1) / GBM, nxwg = gridDim.x >> 3, xcd = blockIdx.x & 7, loc = blockIdx.x >> 3;
+  const int b_beg = (int)((long long)xcd * nblk / 8), b_end = (int)((long long)(xcd + 1) * nblk / 8);
+  const int nmy = b_end - b_beg > loc ? (b_end - b_beg - loc + nxwg - 1) / nxwg : 0;
+  const __amdgpu_buffer_rsrc_t xrs = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)g.A, (short)0, (int)((long long)g.cN * g.cH * g.cW * C * 2), 0x00020000);
+  const __amdgpu_buffer_rsrc_t crs = __builtin_amdgcn_make_buffer_rsrc(
+      g.C, (short)0, (int)((long long)g.M * g.ldc * 2), 0x00020000);
+  const __amdgpu_buffer_rsrc_t srs = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)g.col_stats, (short)0, g.col_stats ? (int)((long long)nblk * 64 * 8) : 0, 0x00020000);
+  const bool stats = g.col_stats != nullptr;
+  const float inv_wo = 1.f / (float)g.cWo, inv_ho = 1.f / (float)g.cHo;
+  typedef unsigned v4u_ __attribute__((ext_vector_type(4)));
+  // K-slice s of this lane: 8 channels c0 = (32 s + 8 q) % C of tap t = (32 s + 8 q) / C = (kh, kw)
+  auto slice_tap = [&](int s) { return (32 * s + 8 * q) / C; };
+  auto slice_off = [&](int s) {  // byte offset of the slice's chunk relative to the pixel's (ih0, iw0) corner
+    const int t = slice_tap(s), c0 = (32 * s + 8 * q) % C;
+    return (((t / KW) * g.cW + (t % KW)) * C + c0) * 2;
+  };
+  // fragment (block i of this workgroup's list, half m): pixel 128 b + 32 w + 16 m + j
+  auto load_frag = [&](v4u_(&dst)[NS], int i, int m) {
+    const int b = b_beg + loc + i * nxwg;
+    const int p = b * GBM + 32 * w + 16 * m + j;
+    int base = 0;
+    unsigned valid = 0u;  // bit t: tap t inside the input
+    if (i < nmy && p < g.M) {
+      int ow, oh;
+      const int t2 = fdiv_rc(p, g.cWo, inv_wo, ow), n = fdiv_rc(t2, g.cHo, inv_ho, oh);
+      const int ih0 = oh - g.cP, iw0 = ow - g.cP;
+      base = ((n * g.cH + ih0) * g.cW + iw0) * C * 2;  // (negative for a padded corner: used only when valid)
+#pragma unroll
+      for (int t = 0; t < KH * KW; ++t) {
+        const int ih = ih0 + t / KW, iw = iw0 + t % KW;
+        valid |= (ih >= 0 && ih < g.cH && iw >= 0 && iw < g.cW) ? 1u << t : 0u;
+      }
+    }
+#pragma unroll
+    for (int s = 0; s < NS; ++s) {
+      const unsigned o = (valid >> slice_tap(s)) & 1u ? (unsigned)(base + slice_off(s)) : OOB;
+      dst[s] = __builtin_amdgcn_raw_buffer_load_b128(xrs, o, 0, 0);
+    }
+  };
+  auto rowsum16 = [](float x) {
+    x += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, x), 0x111, 0xf, 0xf, true));
+    x += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, x), 0x112, 0xf, 0xf, true));
+    x += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, x), 0x114, 0xf, 0xf, true));
+    x += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, x), 0x118, 0xf, 0xf, true));
+    return x;
+  };
+  typedef float f2 __attribute__((ext_vector_type(2)));
+  typedef __bf16 bf2 __attribute__((ext_vector_type(2)));
+  f2 s1[8], sq[8];  // this lane's statistics of channels 16 q + 2 e, + 1 over the block's fragments so far
+  // one fragment: MFMAs, output, statistics
+  auto frag = [&](const v4u_(&a)[NS], int b, int m) {
+    f32x4 acc[4];
+#pragma unroll
+    for (int s = 0; s < NS; ++s) {
+      const char* lk = lw + (s >> 1) * 8192;
+#pragma unroll
+      for (int f = 0; f < 4; ++f) {
+        const s16x8 wf = *(const s16x8*)(lk + lds_off(16 * f + j, 4 * (s & 1) + q));
+        acc[f] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf, __builtin_bit_cast(s16x8, a[s]),
+                                                         s == 0 ? f32x4{0.f, 0.f, 0.f, 0.f} : acc[f], 0, 0, 0);
+      }
+    }
+    const int p = b * GBM + 32 * w + 16 * m + j;
+    const bool in = p < g.M;
+    unsigned pk[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {  // channels 16 q + 2 e, + 1 = fragment e >> 1, elements 2 (e & 1) + {0, 1}
+      const int c = 16 * q + 2 * e;
+      const f32x4& v = acc[e >> 1];
+      const f2 x = f2{v[2 * (e & 1)], v[2 * (e & 1) + 1]} * alpha + f2{sbias[c], sbias[c + 1]};
+      pk[e] = __builtin_bit_cast(unsigned, __builtin_convertvector(x, bf2));
+      f2 d = f2{__uint_as_float(pk[e] << 16), __uint_as_float(pk[e] & 0xffff0000u)} - f2{sshift[c], sshift[c + 1]};
+      if (!in) d = f2{0.f, 0.f};
+      s1[e] += d;
+      sq[e] += d * d;
+    }
+    const unsigned o = in ? ((unsigned)p * (unsigned)g.ldc + 16u * q) * 2u : OOB;
+    __builtin_amdgcn_raw_buffer_store_b128(v4u_{pk[0], pk[1], pk[2], pk[3]}, crs, o, 0, 2);
+    __builtin_amdgcn_raw_buffer_store_b128(v4u_{pk[4], pk[5], pk[6], pk[7]}, crs, o + 16u, 0, 2);
+  };
+  auto block_stats = [&](int b) {  // the block's statistics row; resets the running sums
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const float a0 = rowsum16(s1[e][0]), a1 = rowsum16(s1[e][1]);
+      const float b0 = rowsum16(sq[e][0]), b1 = rowsum16(sq[e][1]);
+      if (j == 15) *(float4*)(sst + 2 * (w * 64 + 16 * q + 2 * e)) = float4{a0, b0, a1, b1};
+      s1[e] = sq[e] = f2{0.f, 0.f};
+    }
+    __syncthreads();
+    if (threadIdx.x < 64) {
+      float s = 0.f, s2 = 0.f;
+#pragma unroll
+      for (int v = 0; v < 4; ++v) {
+        s += sst[2 * (v * 64 + threadIdx.x)];
+        s2 += sst[2 * (v * 64 + threadIdx.x) + 1];
+      }
+      __builtin_amdgcn_raw_buffer_store_b64(st_v2u{__float_as_uint(s), __float_as_uint(s2)}, srs,
+                                            ((unsigned)b * 64u + threadIdx.x) * 8u, 0, 0);
+    }
+    __syncthreads();
+  };
+#pragma unroll
+  for (int e = 0; e < 8; ++e) s1[e] = sq[e] = f2{0.f, 0.f};
+  v4u_ a0[NS], a1[NS];
+  if (nmy > 0) load_frag(a0, 0, 0);
+  for (int i = 0; i < nmy; ++i) {
+    const int b = b_beg + loc + i * nxwg;
+    load_frag(a1, i, 1);      // this block's second fragment, in flight during the first one's work
+    frag(a0, b, 0);
+    load_frag(a0, i + 1, 0);  // the next block's first fragment (past the end: zeros, no traffic)
+    frag(a1, b, 1);
+    if (stats) block_stats(b);
+  }
+}
+
 // Split-K combine: C = alpha * sum_s ws[s] (+bias) (+beta*C) (ReLU).  256 threads = 64 consecutive elements x 4
 // split lanes (lane l sums slabs l, l+4, ...; the 4 partials are added in lane order: deterministic), so
 // thousands of slabs of a small weight gradient are read by many threads with 256-B row segments.

@@ -51,7 +51,7 @@ template <int BM, int BN, int WAVES_M>
 struct WgradTile {
   static constexpr int WAVES_N = 4 / WAVES_M;
   static constexpr int FM = BM / (16 * WAVES_M), FN = BN / (16 * WAVES_N);
-  static constexpr int BK = 64;
+  static constexpr int BK = 64;  // (128-pixel K-tiles measured slower on the 64-channel 3x3: profiles/wgrad_bk128_ab_r5o.log)
   static constexpr int SA = BM * 2 + 32, SB = BN * 2 + 32;  // LDS row strides: 8 banks mod 64
   static constexpr int A_BYTES = BK * SA, B_BYTES = BK * SB, BUF = A_BYTES + B_BYTES, LDS = 2 * BUF;
   static constexpr int CA = BM / 8, CB = BN / 8;             // 16-B chunks per row
@@ -170,7 +170,7 @@ __global__ void __launch_bounds__(256) k_wgrad(GemmArgs g) {
     const char* la = smem + buf * T::BUF;
     const char* lb = la + T::A_BYTES;
 #pragma unroll
-    for (int s = 0; s < 2; ++s) {
+    for (int s = 0; s < T::BK / 32; ++s) {
       const int r0 = s * 32 + 4 * grp + q;  // read 0 row; read 1 is r0 + 16
       s16x8 af[T::FM], bfr[T::FN];
 #pragma unroll

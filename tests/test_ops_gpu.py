@@ -775,3 +775,27 @@ def test_strided_conv_subpixel_input_grad(gpu, k, p):
     y2 = conv_bn_act(x2, conv, bn, relu=True, packed=e, x_join=join)
     y2.backward(dy)
     assert _rel(x2.grad.float(), seed.float() + x.grad.float()) < 2e-2
+
+
+@pytest.mark.parametrize("n,h,w", [(2, 9, 11), (4, 56, 56), (3, 17, 5)])
+def test_direct_conv_3x3_64(gpu, n, h, w):
+    """k_direct_conv<64, 3, 3> (the 64-channel 3x3 / pad 1 convolutions: bf16 output + fused BN column statistics)
+    against torch fp32 on the same bf16-rounded operands: padding on every border, M tails, the per-128-row
+    statistics."""
+    from distributeddataparallel_cifar10_amd import ops
+    from distributeddataparallel_cifar10_amd.ops import functional as F
+    g = torch.Generator(device=gpu).manual_seed(n * h + w)
+    x = torch.randn(n, h, w, 64, device=gpu, generator=g).to(torch.bfloat16)
+    wt = torch.randn(64, 64, 3, 3, device=gpu, generator=g) * 0.05
+    geo = F._geom(x, wt, 1, 1)
+    wm = F._weight_matrix(wt, geo.K)
+    M = geo.N * geo.Ho * geo.Wo
+    shift = torch.randn(64, device=gpu, generator=g) * 0.1
+    parts = torch.full(((M + 127) // 128, 64, 2), float("nan"), device=gpu)
+    y = ops.gemm(x, wm, conv=1, geom=geo, mnk=(M, 64, geo.K), out_dtype=torch.bfloat16, col_stats=parts,
+                 stats_shift=shift)
+    ref = TF.conv2d(x.float().permute(0, 3, 1, 2), wt.to(torch.bfloat16).float(), padding=1)
+    ref = ref.permute(0, 2, 3, 1).reshape(M, 64)
+    assert _rel(y, ref) < 5e-3
+    d = y.float() - shift
+    assert _rel(parts[..., 0].sum(0), d.sum(0)) < 1e-4 and _rel(parts[..., 1].sum(0), (d * d).sum(0)) < 1e-4

@@ -104,3 +104,33 @@ def test_stem_s2d_ops_model_stem(gpu):
     assert rel(out.float().permute(0, 3, 1, 2), zr) < 2e-2
     cos = TF.cosine_similarity(m.conv1.weight.grad.flatten().double(), wr.grad.flatten().double(), dim=0).item()
     assert cos > 0.99, cos
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n,h,w", [(3, 50, 46), (2, 224, 224), (5, 37, 64)])
+def test_stem_conv_kernel_bf16_stats(gpu, n, h, w):
+    """The dedicated s2d stem kernel (k_stem_conv: bf16 output with the fused BN column statistics, the form the
+    ops model's stem calls) against torch fp32 on the same bf16-rounded operands: output, and the per-128-row
+    partial sums / sums of squares of the stored values."""
+    from distributeddataparallel_cifar10_amd.ops import functional as F
+    torch.manual_seed(n + h)
+    conv = torch.nn.Conv2d(3, 64, 7, stride=2, padding=3, bias=False).to(gpu)
+    pack = F.WeightPack([conv], (), [conv])
+    pack.pack()
+    e = pack.get(conv)
+    x = torch.randn(n, 3, h, w, device=gpu)
+    xs = F.nchw_to_s2d16(x)
+    wg, st, pd = F._s2d_args(conv.weight, 2, 3, e)
+    g = F._geom(xs, wg, st, pd)
+    M = g.N * g.Ho * g.Wo
+    shift = torch.randn(64, device=gpu) * 0.1
+    parts = torch.full(((M + 127) // 128, 64, 2), float("nan"), device=gpu)
+    y = F.gemm(xs, e["fwd"], conv=1, geom=g, mnk=(M, 64, g.K), out_dtype=torch.bfloat16, col_stats=parts,
+               stats_shift=shift)
+    xr = x.to(torch.bfloat16).float()
+    wr = conv.weight.detach().to(torch.bfloat16).float()
+    ref = TF.conv2d(xr, wr, stride=2, padding=3).permute(0, 2, 3, 1).reshape(M, 64)
+    rel = lambda a, b: ((a.double() - b.double()).norm() / b.double().norm()).item()  # noqa: E731
+    assert rel(y.float(), ref) < 5e-3
+    d = y.float() - shift
+    assert rel(parts[..., 0].sum(0), d.sum(0)) < 1e-4 and rel(parts[..., 1].sum(0), (d * d).sum(0)) < 1e-4
