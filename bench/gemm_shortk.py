@@ -38,6 +38,9 @@ def main():
     ap.add_argument("--tag", default=os.environ.get("DCA_TAG", "default"))
     ap.add_argument("--shape", default=None, help="MxNxK: only this shape")
     ap.add_argument("--beta", action="store_true", help="accumulate into the output (C += A B^T), no statistics")
+    ap.add_argument("--library", action="store_true",
+                    help="also time the library path on the same operands: torch.matmul (hipBLASLt) / torch conv2d "
+                         "(MIOpen, channels-last), no statistics")
     ap.add_argument("--conv", default=None,
                     help="NxHxCxCO[xKxSxP]: an implicit convolution forward instead (default 3x3, stride 1, pad 1)")
     a = ap.parse_args()
@@ -58,6 +61,12 @@ def main():
         us = timeit(lambda: ops.gemm(x, wm, conv=1, geom=geo, mnk=(M, co, geo.K), out_dtype=bf, **kw))
         print(json.dumps({"tag": a.tag, "conv3x3": a.conv, "us": round(us, 1),
                           "tflops": round(2 * M * co * geo.K / us / 1e6, 1)}), flush=True)
+        if a.library:
+            xn = x.permute(0, 3, 1, 2)  # NCHW view of the NHWC tensor: channels-last for MIOpen
+            wn = wt.to(bf).contiguous(memory_format=torch.channels_last)
+            us = timeit(lambda: torch.nn.functional.conv2d(xn, wn, stride=st, padding=pd))
+            print(json.dumps({"tag": "library", "conv3x3": a.conv, "us": round(us, 1),
+                              "tflops": round(2 * M * co * geo.K / us / 1e6, 1)}), flush=True)
         return
     for M, N, K in shapes:
         x = torch.randn(M, K, device=dev).to(bf)
@@ -77,6 +86,10 @@ def main():
                           "tflops": round(2 * M * N * K / us / 1e6, 1),
                           "gbps": round(2 * (M * K + (2 if a.beta else 1) * M * N) / us / 1e3, 1), "floor_us_5tbs": round(floor_us, 1),
                           "rel_err": round(err, 5)}), flush=True)
+        if a.library:
+            us = timeit(lambda: torch.matmul(x, w.t()))
+            print(json.dumps({"tag": "library", "shape": f"{M}x{N}x{K}", "us": round(us, 1),
+                              "tflops": round(2 * M * N * K / us / 1e6, 1)}), flush=True)
         del x, w, y, ref
 
 
