@@ -253,9 +253,13 @@ static int set_lds_limits(Engine* e) {
   HIPCK(hipFuncSetAttribute((const void*)e->khead1, hipFuncAttributeMaxDynamicSharedMemorySize, (int)e->s_head1));
   HIPCK(hipFuncSetAttribute((const void*)e->khead2, hipFuncAttributeMaxDynamicSharedMemorySize, (int)e->s_head2));
   HIPCK(hipFuncSetAttribute((const void*)e->kbwd, hipFuncAttributeMaxDynamicSharedMemorySize, (int)dg));
-  HIPCK(hipFuncSetAttribute((const void*)pks::k_pks_step<0>, hipFuncAttributeMaxDynamicSharedMemorySize,
+  HIPCK(hipFuncSetAttribute((const void*)pks::k_pks_step<0, false>, hipFuncAttributeMaxDynamicSharedMemorySize,
                             pks::Plan<0>::TOTAL));
-  HIPCK(hipFuncSetAttribute((const void*)pks::k_pks_step<1>, hipFuncAttributeMaxDynamicSharedMemorySize,
+  HIPCK(hipFuncSetAttribute((const void*)pks::k_pks_step<1, false>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            pks::Plan<1>::TOTAL));
+  HIPCK(hipFuncSetAttribute((const void*)pks::k_pks_step<0, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            pks::Plan<0>::TOTAL));
+  HIPCK(hipFuncSetAttribute((const void*)pks::k_pks_step<1, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
                             pks::Plan<1>::TOTAL));
 
   return 0;
@@ -353,10 +357,16 @@ static int enqueue_pks_step(Engine* e, int B, int s, bool prev) {
   ra.seg_ch = seg_ch(e);
   const int extra = fc ? std::max(pks::N_FCW, prev ? pks::prologue_segments(ra.seg_ch) : 0) : 0;
   const dim3 grid(pks_grid(B) + extra);
-  if (e->bf)
-    hipLaunchKernelGGL(pks::k_pks_step<0>, grid, dim3(pks::NTH), pks::Plan<0>::TOTAL, e->st, cx, e->qa, ra);
+  // (the prologue form only where this launch applies the previous step's segments)
+  const dim3 blk(pks::NTH);
+  if (e->bf && prev)
+    hipLaunchKernelGGL((pks::k_pks_step<0, true>), grid, blk, pks::Plan<0>::TOTAL, e->st, cx, e->qa, ra);
+  else if (e->bf)
+    hipLaunchKernelGGL((pks::k_pks_step<0, false>), grid, blk, pks::Plan<0>::TOTAL, e->st, cx, e->qa, ra);
+  else if (prev)
+    hipLaunchKernelGGL((pks::k_pks_step<1, true>), grid, blk, pks::Plan<1>::TOTAL, e->st, cx, e->qa, ra);
   else
-    hipLaunchKernelGGL(pks::k_pks_step<1>, grid, dim3(pks::NTH), pks::Plan<1>::TOTAL, e->st, cx, e->qa, ra);
+    hipLaunchKernelGGL((pks::k_pks_step<1, false>), grid, blk, pks::Plan<1>::TOTAL, e->st, cx, e->qa, ra);
   HIPCK(hipGetLastError());
   return 0;
 }
@@ -516,10 +526,10 @@ static int engine_init(Engine* e, const DcaInit* in, int n_indices) {
     HIPCK(hipGetDevice(&dev));
     HIPCK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
     if (e->bf)
-      HIPCK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)dca::pks::k_pks_step<0>, dca::pks::NTH,
+      HIPCK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)dca::pks::k_pks_step<0, false>, dca::pks::NTH,
                                                         dca::pks::Plan<0>::TOTAL));
     else
-      HIPCK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)dca::pks::k_pks_step<1>, dca::pks::NTH,
+      HIPCK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)dca::pks::k_pks_step<1, false>, dca::pks::NTH,
                                                         dca::pks::Plan<1>::TOTAL));
     // one step workgroup per CU (256 VGPRs): a grid of every CU would leave no slack for anything else on the
     // device (another stream's kernel, another process), so an automatically chosen engine keeps a margin of one
@@ -1029,10 +1039,10 @@ int dca_engine_ipc_selftest_fc(void* h, const float* src, float* dst, float time
   // for its peers' workgroup f, so all ranks' grids must be co-resident (a step-kernel workgroup takes a whole CU)
   const dim3 grid(std::min(dca::pks::N_FCW, dca::share_budget(e)));
   if (e->bf)
-    hipLaunchKernelGGL(dca::pks::k_pks_step<0>, grid, dim3(dca::pks::NTH), dca::pks::Plan<0>::TOTAL, e->st, cx, e->qa,
+    hipLaunchKernelGGL((dca::pks::k_pks_step<0, false>), grid, dim3(dca::pks::NTH), dca::pks::Plan<0>::TOTAL, e->st, cx, e->qa,
                        ra);
   else
-    hipLaunchKernelGGL(dca::pks::k_pks_step<1>, grid, dim3(dca::pks::NTH), dca::pks::Plan<1>::TOTAL, e->st, cx, e->qa,
+    hipLaunchKernelGGL((dca::pks::k_pks_step<1, false>), grid, dim3(dca::pks::NTH), dca::pks::Plan<1>::TOTAL, e->st, cx, e->qa,
                        ra);
   HIPCK(hipGetLastError());
   HIPCK(hipStreamSynchronize(e->st));

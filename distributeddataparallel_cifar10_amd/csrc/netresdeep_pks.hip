@@ -1145,8 +1145,9 @@ constexpr int P_KSHIFT = 906;  // misc: [10][32] BN shifts (last step's batch me
 constexpr int P_LABEL = 1240;  // misc: this image's label
 
 // ============================================================================================================
-// The step of one main workgroup (slice s of image n).
-template <int P>
+// The step of one main workgroup (slice s of image n).  PRO: the prologue-reduction form (compiled separately, so
+// the default form carries none of its code: the shared form ran ~1 us per step slower, profiles/pks_split_r6.log).
+template <int P, bool PRO>
 __device__ __forceinline__ void step_main(const Ctx& cx, const Args& pa, const RedAr& ra, char* smem) {
   using PL = Plan<P>;
   const int t = threadIdx.x, wv = t >> 6, lane = t & 63, c = lane & 15, q = lane >> 4;
@@ -1170,7 +1171,7 @@ __device__ __forceinline__ void step_main(const Ctx& cx, const Args& pa, const R
   char* XR = U + PL::U_XR;
   const int epoch = step_epoch(pa, ra);
   const int par = epoch & 1;
-  const bool prev = ra_prev(ra);  // the previous step's gradient segments are applied in this launch (prologue)
+  const bool prev = PRO && ra_prev(ra);  // the previous step's gradient segments are applied in this launch
   const uint8_t* my_img = pa.simg + (size_t)(par * 64 + n) * 3072;
   const int next_id = sample_id(cx, (ra_s(ra) + 1) * B + n);
   const float Ntot = (float)B * 256.f;
@@ -1195,16 +1196,25 @@ __device__ __forceinline__ void step_main(const Ctx& cx, const Args& pa, const R
     // [544,864), b2 [864,874), conv1 bias [874,906), BN shifts [906,1226)
     constexpr int NKC = 842, KCM = (NKC + NTH - 1) / NTH;
     float kc[KCM];
-    int lab = pa.slab[par * 64 + n];
+    int lab = 0;
     // input words: thread t < 112 -> xin4 row j = t >> 3 (image row 8s-3+j), 4 columns 4 (t & 7) .., 3 channels
     const int jr = (t >> 3) < 14 ? (t >> 3) : 13, yimg = 8 * s - 3 + jr, xq = t & 7;
     const bool ivalid = t < 112 && yimg >= 0 && yimg < 32;
     const unsigned* imw = (const unsigned*)my_img;
     const int yc = yimg < 0 ? 0 : (yimg > 31 ? 31 : yimg);
-    unsigned iw0 = imw[yc * 8 + xq], iw1 = imw[256 + yc * 8 + xq], iw2 = imw[512 + yc * 8 + xq];
-    // prologue reduction: the weights / constants below are the reducers' (this launch): wait for their ready
-    // granules (the image loads above stay in flight), then read them with sc1 loads
-    if (prev) wait_ready(pa, ra, epoch);
+    unsigned iw0 = 0u, iw1 = 0u, iw2 = 0u;
+    auto image_loads = [&] {
+      lab = pa.slab[par * 64 + n];
+      iw0 = imw[yc * 8 + xq];
+      iw1 = imw[256 + yc * 8 + xq];
+      iw2 = imw[512 + yc * 8 + xq];
+    };
+    if constexpr (PRO) {
+      // prologue reduction: the weights / constants below are the reducers' (this launch): wait for their ready
+      // granules (the image loads stay in flight), then read them with sc1 loads
+      image_loads();
+      if (prev) wait_ready(pa, ra, epoch);
+    }
 #pragma unroll
     for (int m = 0; m < KCM; ++m) {
       const int k = min(t + NTH * m, NKC - 1);
@@ -1220,6 +1230,7 @@ __device__ __forceinline__ void step_main(const Ctx& cx, const Args& pa, const R
                                  : (const float*)cx.STATS + 2 * (k - 522);
       kc[m] = prev ? __hip_atomic_load(src, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : *src;
     }
+    if constexpr (!PRO) image_loads();  // (after the constants: the round-4 order)
     // forward trunk weights, records [tap][co] x ci (hi, lo)
     if (prev) wt_copy_sc1<P>(WT, pkw);
     else wt_dma<P>(WT, pkw, wv, lane);
@@ -1853,21 +1864,23 @@ __device__ __forceinline__ void step_main(const Ctx& cx, const Args& pa, const R
   DCA_STAMP(cx, 5, L, 7);
 }
 
-template <int P>
+template <int P, bool PRO>
 __global__ void __launch_bounds__(NTH) k_pks_step(Ctx cx, Args pa, RedAr ra) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int gmain = (cx.B + 7) / 8 * 8 * S;
   if ((int)blockIdx.x < gmain) {
-    step_main<P>(cx, pa, ra, smem);
+    step_main<P, PRO>(cx, pa, ra, smem);
     return;
   }
   // past the main grid: the reducers of the prologue reduction (ra_prev; the previous step's segments), then the fc
   // workers (ra_fc); one fc segment each in a training step (nfw == N_FCW); the self-test on a shared device launches
   // fewer workers (its per-rank CU budget), which then take the segments in turn
   const int fb = (int)blockIdx.x - gmain;
-  if (ra_prev(ra)) {
-    prologue_reduce<P>(cx, pa, ra, fb, smem);
-    __syncthreads();  // its LDS is reused by the fc segment
+  if constexpr (PRO) {
+    if (ra_prev(ra)) {
+      prologue_reduce<P>(cx, pa, ra, fb, smem);
+      __syncthreads();  // its LDS is reused by the fc segment
+    }
   }
   if (!ra_fc(ra)) return;
   const int nfw = min((int)gridDim.x - gmain, N_FCW);

@@ -866,7 +866,9 @@ __global__ void __launch_bounds__(NW * 64) k_gemm_glds(GemmArgs g) {
 // Interval I_j (between barriers j and j + 1): group 0 runs L(s) in I_2s and M(s) in I_2s+1, group 1 L(s) in
 // I_2s+1 and M(s) in I_2s+2 (step s = 2 kt + h).  Staging, two LDS buffers (tile kt in buffer kt & 1):
 //   * tile kt + 1 is issued in I_4kt (group 0 before L(2kt), group 1 in M(2kt - 1)); its buffer last held tile
-//     kt - 1, read for the last time in I_4kt-1 and retired there (lgkmcnt(0) before that barrier);
+//     kt - 1, read for the last time in I_4kt-1 and retired there (lgkmcnt(0) before that barrier).  Plain GEMMs:
+//     group 1 issues in I_4kt+1 instead, before L(2kt), so no LDS-DMA issue delays an MFMA phase (50176 x 256 x
+//     2304: 86 -> 73 us; the implicit conv keeps I_4kt -- its gather lands later: profiles/gemm_pp_issue_ab_r6.log);
 //   * every issuing thread waits vmcnt(0) before the barrier ending I_4kt+3 (group 0 after M(2kt + 1), group 1
 //     after L(2kt + 1)), so tile kt + 1 is complete and visible when group 0 reads it in I_4kt+4.
 // Operand addressing as k_gemm_glds' fast path (per-lane offsets computed once, incremental tap for the conv).
@@ -1018,17 +1020,21 @@ __global__ void __launch_bounds__(PP_NT) k_gemm_pp(GemmArgs g) {
     }
     bar();  // group 1 runs one barrier behind
   } else {
+    const bool cv = g.conv == 1;
     if (nk > 1) issue(1);  // I_0: group 1's part of tile 1 (group 0 issued its part before L(0))
     bar();                 // end of I_0
 #pragma unroll 1
     for (int st = 0; st < 2 * nk; ++st) {
       const int kt = st >> 1, h = st & 1;
+      // plain GEMM: I_4kt+1 (an L phase, not the MFMA phase): tile kt + 1 into buffer (kt + 1) & 1, last read in
+      // I_4kt-1; implicit conv: I_4kt+4, tile kt + 2 (a gather lands later: one more interval of slack)
+      if (!cv && h == 0 && kt >= 1 && kt + 1 < nk) issue(kt + 1);
       load_frags(kt, h);
       if (h == 1) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // my part of tile kt + 1 landed (I_4kt+3)
-      bar();                                      // end of L(st)
-      if (h == 1 && kt + 2 < nk) issue(kt + 2);  // I_4kt+4: tile kt + 2 into buffer kt & 1, retired in I_4kt+3
+      bar();  // end of L(st)
+      if (cv && h == 1 && kt + 2 < nk) issue(kt + 2);
       mfmas();
-      bar();                                      // end of M(st)
+      bar();  // end of M(st)
     }
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
