@@ -124,6 +124,30 @@ void bn_apply_launch(long M, int C, hipStream_t st, A... a) {
     hipLaunchKernelGGL((k_bn_apply<16>), dim3(C / 128, nparts_rows(M)), dim3(256), 0, st, a...);
   }
 }
+// BN partial-row reduction (MODE 0 forward statistics, MODE 1 backward sums): with ticket words (ceil(C / 64), zero)
+// the coalesced ticketed kernel (k_bn_fin_ticket; the partial rows are overwritten), else the per-channel one
+template <int MODE>
+void bn_fin_launch(float* part, int nparts, long M, int C, float* a0, float* a1, float* out, float eps, float momentum,
+                   int accumulate, unsigned* ticket, hipStream_t st) {
+  if (ticket) {
+    const int rpb = bn_fin_rpb(nparts);
+    const dim3 grid((unsigned)((C + 63) / 64), (unsigned)((nparts + rpb - 1) / rpb));
+    hipLaunchKernelGGL((k_bn_fin_ticket<MODE>), grid, dim3(256), 0, st, (float2*)part, nparts, rpb, (int)M, C, a0, a1,
+                       (float2*)out, eps, momentum, accumulate, ticket);
+    return;
+  }
+  if constexpr (MODE == 0) {
+#define FIN(CW) hipLaunchKernelGGL((k_bn_finalize<CW, BN_FIN_NTH(CW)>), dim3((C + CW - 1) / CW), dim3(BN_FIN_NTH(CW)), 0, \
+                                   st, (const float2*)part, nparts, (int)M, C, a0, a1, (float2*)out, eps, momentum)
+    BN_FIN_DISPATCH(C, FIN);
+#undef FIN
+  } else {
+#define FIN(CW) hipLaunchKernelGGL((k_bn_bwd_finalize<CW, BN_FIN_NTH(CW)>), dim3((C + CW - 1) / CW), dim3(BN_FIN_NTH(CW)), \
+                                   0, st, (const float2*)part, nparts, C, a0, a1, (float2*)out, accumulate)
+    BN_FIN_DISPATCH(C, FIN);
+#undef FIN
+  }
+}
 }  // namespace
 
 using namespace dca::ops;
@@ -131,7 +155,7 @@ using namespace dca::ops;
 extern "C" {
 
 const char* dca_ops_last_error() { return g_err.c_str(); }
-int dca_ops_abi_version() { return 10; }
+int dca_ops_abi_version() { return 11; }
 
 // Must match ops/_native.py::GemmArgs.
 int dca_ops_gemm(const GemmArgs* a, void* stream) {
@@ -488,17 +512,14 @@ int dca_ops_col2im(const void* dcols, void* dx, const ConvGeom* geom, int accumu
 // (mean, invstd) kept for the backward.  momentum 0: running stats untouched (but still the shift).
 int dca_ops_bn_fwd(const void* x, const void* r, void* out, float* part, float* stats, const float* gamma,
                    const float* beta, float* rm, float* rv, long M, int C, float eps, float momentum, int relu,
-                   int res_mode, void* stream) {
+                   int res_mode, unsigned* ticket, void* stream) {
   REQUIRE(C % 8 == 0, "bn: C must be a multiple of 8");
   REQUIRE(res_mode == 0 || r != nullptr, "bn: residual missing");
   hipStream_t st = (hipStream_t)stream;
   const int nparts = (int)((M + BN_ROWS - 1) / BN_ROWS);
   hipLaunchKernelGGL(k_bn_stats, dim3((C + 63) / 64, nparts), dim3(256), 0, st, (const bf16_t*)x, rm, (float2*)part,
                      (int)M, C);
-#define FIN(CW) hipLaunchKernelGGL((k_bn_finalize<CW, BN_FIN_NTH(CW)>), dim3((C + CW - 1) / CW), dim3(BN_FIN_NTH(CW)), 0, st, (const float2*)part, \
-                                   nparts, (int)M, C, rm, rv, (float2*)stats, eps, momentum)
-  BN_FIN_DISPATCH(C, FIN);
-#undef FIN
+  bn_fin_launch<0>(part, nparts, M, C, rm, rv, stats, eps, momentum, 0, ticket, st);
   bn_apply_launch(M, C, st, (const bf16_t*)x, (const bf16_t*)r,
                      (bf16_t*)out, (const float2*)stats, gamma, beta, M, C, relu, res_mode, (uint8_t*)nullptr,
                      (const float*)nullptr, (unsigned*)nullptr, (uint8_t*)nullptr);
@@ -511,20 +532,17 @@ int dca_ops_bn_fwd(const void* x, const void* r, void* out, float* part, float* 
 // q / amax_prev / amax_out (optional): also write an fp8 copy of the output with delayed scaling (k_bn_apply);
 // amax_out is zeroed here first.
 // mask (optional, res_mode 2 + ReLU): [M C / 8] bytes, the ReLU mask for dca_ops_bn_bwd.
-int dca_ops_bn_fwd_parts(const void* x, const void* r, void* out, const float* part, int nparts, float* stats,
+int dca_ops_bn_fwd_parts(const void* x, const void* r, void* out, float* part, int nparts, float* stats,
                          const float* gamma, const float* beta, float* rm, float* rv, long M, int C, float eps,
                          float momentum, int relu, int res_mode, void* q, const float* amax_prev, unsigned* amax_out,
-                         void* mask, void* stream) {
+                         void* mask, unsigned* ticket, void* stream) {
   REQUIRE(C % 8 == 0, "bn: C must be a multiple of 8");
   REQUIRE(res_mode == 0 || r != nullptr, "bn: residual missing");
   REQUIRE(!q || (amax_prev && amax_out), "bn: fp8 output needs amax_prev and amax_out");
   REQUIRE(!mask || (relu && res_mode == 2), "bn: the stored mask is for ReLU(bn + r)");
   hipStream_t st = (hipStream_t)stream;
   if (q) OPCK(hipMemsetAsync(amax_out, 0, sizeof(unsigned), st));
-#define FIN(CW) hipLaunchKernelGGL((k_bn_finalize<CW, BN_FIN_NTH(CW)>), dim3((C + CW - 1) / CW), dim3(BN_FIN_NTH(CW)), 0, st, (const float2*)part, \
-                                   nparts, (int)M, C, rm, rv, (float2*)stats, eps, momentum)
-  BN_FIN_DISPATCH(C, FIN);
-#undef FIN
+  bn_fin_launch<0>(part, nparts, M, C, rm, rv, stats, eps, momentum, 0, ticket, st);
   bn_apply_launch(M, C, st, (const bf16_t*)x, (const bf16_t*)r,
                      (bf16_t*)out, (const float2*)stats, gamma, beta, M, C, relu, res_mode, (uint8_t*)q, amax_prev,
                      amax_out, (uint8_t*)mask);
@@ -550,7 +568,8 @@ int dca_ops_bn_eval(const void* x, const void* r, void* out, float* stats, const
 // mask (optional): the forward's ReLU bit mask (dca_ops_bn_fwd_parts); r is then not read.
 int dca_ops_bn_bwd(const void* dy, const void* x, const void* r, const float* stats, const float* gamma,
                    const float* beta, float* part, float* sums, float* dgamma, float* dbeta, void* dx, void* dr,
-                   long M, int C, int relu, int res_mode, int accumulate, const void* mask, void* stream) {
+                   long M, int C, int relu, int res_mode, int accumulate, const void* mask, unsigned* ticket,
+                   void* stream) {
   REQUIRE(C % 8 == 0, "bn: C must be a multiple of 8");
   // dr (= dz) may be omitted with the mask: the residual's consumer then reads dy and the mask itself
   REQUIRE(res_mode != 2 || mask != nullptr || (r != nullptr && dr != nullptr), "bn bwd: residual tensors missing");
@@ -569,10 +588,7 @@ int dca_ops_bn_bwd(const void* dy, const void* x, const void* r, const float* st
     bn_stats_launch<8>(mode, false, dim3((C + 63) / 64, nparts), st, (const bf16_t*)dy, (const bf16_t*)x,
                        (const bf16_t*)r, (const float2*)stats, gamma, beta, (float2*)part, (int)M, C,
                        (const uint8_t*)mask);
-#define FIN(CW) hipLaunchKernelGGL((k_bn_bwd_finalize<CW, BN_FIN_NTH(CW)>), dim3((C + CW - 1) / CW), dim3(BN_FIN_NTH(CW)), 0, st, \
-                                   (const float2*)part, nparts, C, dgamma, dbeta, (float2*)sums, accumulate)
-  BN_FIN_DISPATCH(C, FIN);
-#undef FIN
+  bn_fin_launch<1>(part, nparts, M, C, dgamma, dbeta, sums, 0.f, 0.f, accumulate, ticket, st);
   if (C % 128 == 0)
     bn_bwd_apply_launch<16>(mode, bn_bwd_apply_fine(M, C), M, C, st, (const bf16_t*)dy, (const bf16_t*)x,
                             (const bf16_t*)r, (const float2*)stats, gamma, beta, (const float2*)sums, (bf16_t*)dx,

@@ -13,7 +13,7 @@ import torch
 
 from .. import build as _build
 
-ABI_VERSION = 10
+ABI_VERSION = 11
 _lock = threading.Lock()
 _lib = None
 
@@ -64,15 +64,15 @@ def _declare(lib):
     lib.dca_ops_im2col.argtypes = [c_void_p, c_void_p, P(ConvGeom), c_void_p]
     lib.dca_ops_col2im.argtypes = [c_void_p, c_void_p, P(ConvGeom), c_int, c_void_p]
     lib.dca_ops_bn_fwd.argtypes = [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
-                                   c_void_p, c_long, c_int, c_float, c_float, c_int, c_int, c_void_p]
+                                   c_void_p, c_long, c_int, c_float, c_float, c_int, c_int, c_void_p, c_void_p]
     lib.dca_ops_bn_fwd_parts.argtypes = [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_void_p,
                                          c_void_p, c_void_p, c_long, c_int, c_float, c_float, c_int, c_int, c_void_p,
-                                         c_void_p, c_void_p, c_void_p, c_void_p]
+                                         c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]
     lib.dca_ops_bn_eval.argtypes = [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                                     c_long, c_int, c_float, c_int, c_int, c_void_p]
     lib.dca_ops_bn_bwd.argtypes = [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                                    c_void_p, c_void_p, c_void_p, c_void_p, c_long, c_int, c_int, c_int, c_int,
-                                   c_void_p, c_void_p]
+                                   c_void_p, c_void_p, c_void_p]
     lib.dca_ops_maxpool_fwd.argtypes = [c_void_p, c_void_p, c_void_p, P(PoolGeom), c_void_p]
     lib.dca_ops_maxpool_bwd.argtypes = [c_void_p, c_void_p, c_void_p, P(PoolGeom), c_void_p]
     lib.dca_ops_avgpool_fwd.argtypes = [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p]

@@ -767,7 +767,8 @@ class _ConvBNAct(torch.autograd.Function):
                                              float(eps), float(momentum), int(relu), int(res_mode), N.ptr(q),
                                              N.ptr(emit.amax_prev) if q is not None else None,
                                              N.ptr(emit.amax_out) if q is not None else None, N.ptr(mask),
-                                             N.stream(x.device)), "bn_fwd_parts")
+                                             N.ptr(_ticket(x.device, (co + 63) // 64)), N.stream(x.device)),
+                "bn_fwd_parts")
         if q is not None:
             emit.q, emit.src_ptr = q, out.data_ptr()
         ctx.st = st
@@ -888,7 +889,8 @@ class _BatchNormAct(torch.autograd.Function):
         stats = torch.empty(C, 2, dtype=torch.float32, device=x.device)
         N.check(N.lib().dca_ops_bn_fwd(N.ptr(x), N.ptr(r), N.ptr(out), N.ptr(part), N.ptr(stats), N.ptr(gamma),
                                        N.ptr(beta), N.ptr(running_mean), N.ptr(running_var), M, C, float(eps),
-                                       float(momentum), int(relu), int(res_mode), N.stream(x.device)), "bn_fwd")
+                                       float(momentum), int(relu), int(res_mode), N.ptr(_ticket(x.device, (C + 63) // 64)),
+                                       N.stream(x.device)), "bn_fwd")
         ctx.save_for_backward(x, r, gamma, beta, stats)
         ctx.relu, ctx.res_mode = relu, res_mode
         return out
@@ -918,7 +920,8 @@ def _bn_backward(dy, x, r, gamma, beta, stats, relu, res_mode, dgamma_out=None, 
     dr = torch.empty_like(x) if res_mode == 2 and (want_dr or mask is None) else None
     N.check(N.lib().dca_ops_bn_bwd(N.ptr(dy), N.ptr(x), N.ptr(r), N.ptr(stats), N.ptr(gamma), N.ptr(beta),
                                    N.ptr(part), N.ptr(sums), N.ptr(dgamma), N.ptr(dbeta), N.ptr(dx), N.ptr(dr),
-                                   M, C, int(relu), int(res_mode), int(direct), N.ptr(mask), N.stream(x.device)),
+                                   M, C, int(relu), int(res_mode), int(direct), N.ptr(mask),
+                                   N.ptr(_ticket(x.device, (C + 63) // 64)), N.stream(x.device)),
             "bn_bwd")
     if res_mode == 1:
         dr = dy

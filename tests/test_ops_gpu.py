@@ -185,6 +185,38 @@ def test_batch_norm_act(gpu, res_mode, relu):
     assert int(bn.num_batches_tracked) == int(ref_bn.num_batches_tracked) == 1
 
 
+@pytest.mark.parametrize("n,h,c", [(8, 64, 64), (16, 96, 136), (32, 320, 8), (2, 48, 1024)])
+def test_batch_norm_partial_reduction_shapes(gpu, n, h, c):
+    """The ticketed partial-row reduction (k_bn_fin_ticket) of the BN statistics / backward sums on shapes with many
+    partial rows (up to 12,800: several rows per workgroup and up to 100 row sums per column block), a partial last
+    64-channel column block (C = 136, 8) and many column blocks (C = 1024): output, running statistics and
+    dgamma / dbeta against torch fp32; a second call reuses the ticket words the first one reset."""
+    from distributeddataparallel_cifar10_amd.ops import batch_norm_act
+    g = torch.Generator(device=gpu).manual_seed(n + h + c)
+    bn = torch.nn.BatchNorm2d(c).to(gpu)
+    with torch.no_grad():
+        bn.weight.uniform_(0.5, 1.5)
+        bn.bias.uniform_(-0.2, 0.2)
+    ref_bn = torch.nn.BatchNorm2d(c).to(gpu)
+    ref_bn.load_state_dict(bn.state_dict())
+    for it in range(2):
+        x = _bf(torch.randn(n, h, h, c, device=gpu, generator=g) * 2 + 0.5 + it).requires_grad_()
+        bn.zero_grad()
+        ref_bn.zero_grad()
+        y = batch_norm_act(x, bn, relu=True)
+        dy = _bf(torch.randn(y.shape, device=gpu, generator=g))
+        y.backward(dy)
+        xr = x.detach().float().permute(0, 3, 1, 2).requires_grad_()
+        z = torch.relu(ref_bn(xr))
+        z.backward(dy.float().permute(0, 3, 1, 2))
+        assert _rel(y.float().permute(0, 3, 1, 2), z) < 1e-2
+        assert _rel(x.grad.float().permute(0, 3, 1, 2), xr.grad) < 2e-2
+        assert _rel(bn.weight.grad, ref_bn.weight.grad) < 1e-3
+        assert _rel(bn.bias.grad, ref_bn.bias.grad) < 1e-3
+        assert _rel(bn.running_mean, ref_bn.running_mean) < 1e-5
+        assert _rel(bn.running_var, ref_bn.running_var) < 1e-5
+
+
 # (3, 2, 1, even h) with c % 8 == 0 takes the output-driven k_maxpool_bwd_k3s2 backward (h = 14: odd Ho edge)
 @pytest.mark.parametrize("k,s,p,h", [(2, 2, 0, 16), (3, 2, 1, 15), (2, 2, 0, 7), (3, 2, 1, 16), (3, 2, 1, 14)])
 @pytest.mark.parametrize("c", [24, 5])
