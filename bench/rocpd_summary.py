@@ -6,6 +6,7 @@ between consecutive dispatches of the persistent training step.
 from __future__ import annotations
 
 import collections
+import os
 import sqlite3
 import statistics
 import sys
@@ -38,4 +39,6 @@ def main(path: str) -> None:
 
 
 if __name__ == "__main__":
+    if len(sys.argv) != 2 or sys.argv[1].startswith("-") or not os.path.isfile(sys.argv[1]):
+        sys.exit(__doc__)  # (sqlite3.connect would create an empty database at a wrong path)
     main(sys.argv[1])
