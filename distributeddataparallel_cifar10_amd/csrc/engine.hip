@@ -471,7 +471,7 @@ extern "C" {
 
 const char* dca_last_error() { return g_err.c_str(); }
 
-int dca_abi_version() { return 6; }  // bump with every DcaInit / signature change
+int dca_abi_version() { return 7; }  // bump with every DcaInit / signature change
 
 int dca_nccl_unique_id(char* out128) {
   ncclUniqueId id;
@@ -547,6 +547,13 @@ static int engine_init(Engine* e, const DcaInit* in, int n_indices) {
     e->resident = resident;
     if (const char* fo = getenv("DCA_PKS_FC_IN_STEP")) e->fc_in_step = fo[0] != '0';
     if (const char* po = getenv("DCA_PKS_PROLOGUE")) e->prologue = po[0] != '0';
+    if (e->prologue) {  // the prologue form is a separate instantiation: it must be as resident as the default one
+      int per_cu_pro = 0;
+      HIPCK(hipOccupancyMaxActiveBlocksPerMultiprocessor(
+          &per_cu_pro, e->bf ? (const void*)dca::pks::k_pks_step<0, true> : (const void*)dca::pks::k_pks_step<1, true>,
+          dca::pks::NTH, e->bf ? dca::pks::Plan<0>::TOTAL : dca::pks::Plan<1>::TOTAL));
+      if (per_cu_pro < per_cu) e->prologue = 0;
+    }
   }
   HIPCK(hipStreamCreateWithFlags(&e->st, hipStreamNonBlocking));
   HIPCK(hipStreamCreateWithFlags(&e->cst, hipStreamNonBlocking));
@@ -1150,6 +1157,9 @@ int dca_engine_fc_in_step(void* h, int B) {
   Engine* e = (Engine*)h;
   return e->persistent && fc_in_step_for(e, B) ? 1 : 0;
 }
+
+// Whether graph chunks at batch B apply each step's gradient segments in the next step's launch (prologue_ok).
+int dca_engine_prologue(void* h, int B) { return dca::prologue_ok((Engine*)h, B) ? 1 : 0; }
 
 // Handle of the engine stream (so Python can order torch work against it).
 void* dca_engine_stream(void* h) { return ((Engine*)h)->st; }

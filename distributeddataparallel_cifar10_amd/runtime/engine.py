@@ -247,6 +247,11 @@ class NetResDeepEngine:
         """Whether a step at this batch size runs the fc gradient segments on the step kernel's fc workers."""
         return bool(self.lib.dca_engine_fc_in_step(self.h, int(batch)))
 
+    def prologue(self, batch: int) -> bool:
+        """Whether graph chunks at this batch size reduce each step's gradient segments in the next step's launch
+        (DCA_PKS_PROLOGUE=1, where the budget and the all-reduce allow it)."""
+        return bool(self.lib.dca_engine_prologue(self.h, int(batch)))
+
     # ---- state sync ---------------------------------------------------------------------------------------
     def derive(self):
         """Re-derive the kernel-layout weight copies after the fp32 params changed outside the engine."""

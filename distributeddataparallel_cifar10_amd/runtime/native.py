@@ -16,7 +16,7 @@ import torch  # noqa: F401  (must be imported before the native library, see mod
 
 from .. import build as _build
 
-ABI_VERSION = 6  # csrc/engine.hip dca_abi_version(): DcaInit layout / C signatures
+ABI_VERSION = 7  # csrc/engine.hip dca_abi_version(): DcaInit layout / C signatures
 _lock = threading.Lock()
 _lib = None
 
@@ -59,6 +59,7 @@ def _declare(lib):
     lib.dca_engine_set_epoch.argtypes = [c_void_p, c_int, c_int]
     lib.dca_engine_epoch.argtypes = [c_void_p, ctypes.POINTER(c_int)]
     lib.dca_engine_fc_in_step.argtypes = [c_void_p, c_int]
+    lib.dca_engine_prologue.argtypes = [c_void_p, c_int]
     lib.dca_engine_comm_time.argtypes = [c_void_p, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_longlong),
                                          c_int]
     return lib

@@ -186,6 +186,7 @@ def test_prologue_reduction_bitwise(gpu, dtype, monkeypatch):
         monkeypatch.setenv("DCA_PKS_PROLOGUE", pro)
         m = copy.deepcopy(m0).to(gpu)
         eng = NetResDeepEngine(m, data.to(gpu), labels.to(gpu), EngineConfig(batch_max=32, dtype=dtype))
+        assert eng.prologue(32) == (pro == "1")  # the prologue form really runs (as resident as the default form)
         eng.set_indices(list(range(2048)))
         eng.set_cursor(0)
         eng.read_loss(reset=True)
