@@ -875,11 +875,13 @@ __device__ __forceinline__ void pkw_trunk_chunks_wt(const Ctx& cx, const float* 
 // Segment b on this workgroup (NTH threads): reduce / compute into segv, exchange (mode 2), SGD.  LDS: segv
 // [SEG_MAX], red [NTH] f32x4, stage [stage_floats(B)], s_ep[2].  WT: the SGD results are read inside this launch
 // (prologue reduction; trunk / conv1 / BN-tail segments only).
-template <int NTH, bool WT = false>
+// LEAN: mode 0 with the fc segments on the step kernel's fc workers (world size 1): trunk / conv1 chunks and the BN
+// tail only, no exchange -- compiled without the other modes' code.
+template <int NTH, bool WT = false, bool LEAN = false>
 __device__ void seg_process(const Ctx& cx, const Args& pa, const RedAr& ra, int b, int nslab, float* segv,
                             f32x4* red, float* stage, int* s_ep, int sslot, int swg) {
   const int t = threadIdx.x, B = cx.B;
-  const int mode = ra.mode;
+  const int mode = LEAN ? 0 : ra.mode;
   const SegLayout Ls = seg_layout(ra.seg_ch);
   const int len = seg_len(Ls, b), off = seg_off(Ls, b);
   // this segment's exchange epoch (own flag), and this thread's SGD elements (k = t + NTH i): parameter indices
@@ -899,7 +901,7 @@ __device__ void seg_process(const Ctx& cx, const Args& pa, const RedAr& ra, int 
   } else if (b < Ls.r_ts) {
     if (Ls.ch == 128) seg_chunk<NTH, 128>(cx, pa, Ls, b, nslab, segv, red);
     else seg_chunk<NTH, 256>(cx, pa, Ls, b, nslab, segv, red);
-  } else if (b < Ls.fct) {
+  } else if (!LEAN && b < Ls.fct) {
     // fc1 block: dW1[j][64f + kk .. +3] = sum_b dh[b][j] p[b][64f + kk ..], rows j = 16 h .. 16 h + 15
     const int fb = b - Ls.r_ts, f = fb >> 1, j0 = 16 * (fb & 1);
     float* dh_s = stage;           // [B][32]
@@ -930,7 +932,7 @@ __device__ void seg_process(const Ctx& cx, const Args& pa, const RedAr& ra, int 
       for (int bb = 0; bb < B; ++bb) a0 += dh_s[bb * 32 + j0 + jl] * ld4(p_s + bb * 64 + kk);
       st4(segv + jl * 64 + kk, a0);
     }
-  } else if (b == Ls.fct) {
+  } else if (!LEAN && b == Ls.fct) {
     // fc tail: fc1 bias [0,32), fc2 weight [32,352), fc2 bias [352,362), pad
     float* hh_s = stage;            // [B][32]
     float* dl_s = stage + B * 32;   // [B][16]
@@ -1917,6 +1919,7 @@ __host__ __device__ inline int reduce_segments(int fc_in_step, int seg_ch) {
 // peers, and each rank visits its segments in the same order, so the looped form cannot deadlock among reductions;
 // its point is that a rank's spinning reduction never holds more CUs than its step kernel (a step workgroup needs a
 // whole CU: 256 VGPRs), so a late peer always finds room for its step.
+template <bool LEAN>
 __global__ void __launch_bounds__(256) k_pks_reduce_ar(Ctx cx, Args pa, int nslab, RedAr ra) {
   __shared__ __attribute__((aligned(16))) float segv[SEG_MAX];
   __shared__ f32x4 red[256];
@@ -1931,12 +1934,12 @@ __global__ void __launch_bounds__(256) k_pks_reduce_ar(Ctx cx, Args pa, int nsla
     }
     const int seg = !ra_fc(ra) || b < Ls.r_ts ? b : Ls.bnt;
     DCA_STAMP(cx, 8, b, 0);
-    seg_process<256>(cx, pa, ra, seg, nslab, segv, red, stage, s_ep, 8, b);
+    seg_process<256, false, LEAN>(cx, pa, ra, seg, nslab, segv, red, stage, s_ep, 8, b);
     return;
   }
   for (int k = b; k < nred; k += nwg) {
     const int seg = !ra_fc(ra) || k < Ls.r_ts ? k : Ls.bnt;
-    seg_process<256>(cx, pa, ra, seg, nslab, segv, red, stage, s_ep, 8, k);
+    seg_process<256, false, LEAN>(cx, pa, ra, seg, nslab, segv, red, stage, s_ep, 8, k);
     __syncthreads();  // segv / red / stage are reused by the next segment
   }
   if (b == nwg - 1 && ra.mode != 3) pks_bookkeeping(cx, pa, ra_chunk(ra));
