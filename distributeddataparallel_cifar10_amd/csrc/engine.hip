@@ -388,12 +388,15 @@ static int enqueue_pks_reduce(Engine* e, int B, int chunk, int part) {
     ra.fc_in_step = pks::ra_flags(fc, false, 0, chunk);
     ra.seg_ch = seg_ch(e);
     const dim3 rgrid(reduce_grid(e, pks::reduce_segments(fc, ra.seg_ch) + 1));
-    if (ra.mode == 0 && fc)  // (the lean form: no exchange, no fc segments)
-      hipLaunchKernelGGL(pks::k_pks_reduce_ar<true>, rgrid, dim3(256), pks::stage_floats(B) * 4, e->st, cx, e->qa,
-                         B * pks::S, ra);
+    // the lean forms (no fc segments, one exchange mode): world size 1, or the xGMI exchange on a device of its own
+    const int lean = !fc ? 0 : (ra.mode == 0 ? 1 : (ra.mode == 2 && e->shared_device <= 1 ? 2 : 0));
+    const size_t lds = pks::stage_floats(B) * 4;
+    if (lean == 1)
+      hipLaunchKernelGGL(pks::k_pks_reduce_ar<1>, rgrid, dim3(256), lds, e->st, cx, e->qa, B * pks::S, ra);
+    else if (lean == 2)
+      hipLaunchKernelGGL(pks::k_pks_reduce_ar<2>, rgrid, dim3(256), lds, e->st, cx, e->qa, B * pks::S, ra);
     else
-      hipLaunchKernelGGL(pks::k_pks_reduce_ar<false>, rgrid, dim3(256), pks::stage_floats(B) * 4, e->st, cx, e->qa,
-                         B * pks::S, ra);
+      hipLaunchKernelGGL(pks::k_pks_reduce_ar<0>, rgrid, dim3(256), lds, e->st, cx, e->qa, B * pks::S, ra);
   }
   if (multi && !xgmi) {  // RCCL (comm_mode 0, captured) or the host (comm_mode 1, between parts 1 and 2)
     if (part == 0) NCCK(ncclAllReduce(cx.grads, cx.grads, FLAT_N, ncclFloat32, ncclSum, e->comm, e->st));
@@ -1000,7 +1003,7 @@ int dca_engine_ipc_selftest(void* h, const float* src, float* dst, float timeout
     ra.seg_ch = dca::seg_ch(e);
     dca::Ctx cx = e->base;
     cx.B = 1;
-    hipLaunchKernelGGL(dca::pks::k_pks_reduce_ar<false>, dim3(dca::reduce_grid(e, dca::pks::seg_layout(ra.seg_ch).nseg)),
+    hipLaunchKernelGGL(dca::pks::k_pks_reduce_ar<0>, dim3(dca::reduce_grid(e, dca::pks::seg_layout(ra.seg_ch).nseg)),
                        dim3(256), dca::pks::stage_floats(1) * 4, e->st, cx, e->qa, 1, ra);
   } else {
     dca::xg::Peers P = e->peers;
@@ -1096,7 +1099,7 @@ int dca_engine_ipc_bench(void* h, const float* src, float* dst, int iters, float
       ra.seg_ch = dca::seg_ch(e);
       dca::Ctx cx = e->base;
       cx.B = 1;
-      hipLaunchKernelGGL(dca::pks::k_pks_reduce_ar<false>, dim3(dca::reduce_grid(e, dca::pks::seg_layout(ra.seg_ch).nseg)),
+      hipLaunchKernelGGL(dca::pks::k_pks_reduce_ar<0>, dim3(dca::reduce_grid(e, dca::pks::seg_layout(ra.seg_ch).nseg)),
                          dim3(256), dca::pks::stage_floats(1) * 4, e->st, cx, e->qa, 1, ra);
     } else if (e->bf) {
       hipLaunchKernelGGL(dca::xg::k_xgmi_ar_sgd<true>, dim3(dca::xg::AR_NB), dim3(dca::xg::AR_T), 0, e->st,

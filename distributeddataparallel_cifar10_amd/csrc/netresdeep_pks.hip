@@ -875,13 +875,14 @@ __device__ __forceinline__ void pkw_trunk_chunks_wt(const Ctx& cx, const float* 
 // Segment b on this workgroup (NTH threads): reduce / compute into segv, exchange (mode 2), SGD.  LDS: segv
 // [SEG_MAX], red [NTH] f32x4, stage [stage_floats(B)], s_ep[2].  WT: the SGD results are read inside this launch
 // (prologue reduction; trunk / conv1 / BN-tail segments only).
-// LEAN: mode 0 with the fc segments on the step kernel's fc workers (world size 1): trunk / conv1 chunks and the BN
-// tail only, no exchange -- compiled without the other modes' code.
-template <int NTH, bool WT = false, bool LEAN = false>
+// LEAN 1: mode 0 with the fc segments on the step kernel's fc workers (world size 1): trunk / conv1 chunks and the BN
+// tail only, no exchange; LEAN 2: the same segments in mode 2 (the xGMI exchange) -- each compiled without the other
+// modes' code.
+template <int NTH, bool WT = false, int LEAN = 0>
 __device__ void seg_process(const Ctx& cx, const Args& pa, const RedAr& ra, int b, int nslab, float* segv,
                             f32x4* red, float* stage, int* s_ep, int sslot, int swg) {
   const int t = threadIdx.x, B = cx.B;
-  const int mode = LEAN ? 0 : ra.mode;
+  const int mode = LEAN == 1 ? 0 : (LEAN == 2 ? 2 : ra.mode);
   const SegLayout Ls = seg_layout(ra.seg_ch);
   const int len = seg_len(Ls, b), off = seg_off(Ls, b);
   // this segment's exchange epoch (own flag), and this thread's SGD elements (k = t + NTH i): parameter indices
@@ -1919,7 +1920,7 @@ __host__ __device__ inline int reduce_segments(int fc_in_step, int seg_ch) {
 // peers, and each rank visits its segments in the same order, so the looped form cannot deadlock among reductions;
 // its point is that a rank's spinning reduction never holds more CUs than its step kernel (a step workgroup needs a
 // whole CU: 256 VGPRs), so a late peer always finds room for its step.
-template <bool LEAN>
+template <int LEAN>
 __global__ void __launch_bounds__(256) k_pks_reduce_ar(Ctx cx, Args pa, int nslab, RedAr ra) {
   __shared__ __attribute__((aligned(16))) float segv[SEG_MAX];
   __shared__ f32x4 red[256];

@@ -203,6 +203,39 @@ def test_prologue_reduction_bitwise(gpu, dtype, monkeypatch):
     assert torch.equal(p1, p0) and torch.equal(v1, v0)
 
 
+@pytest.mark.parametrize("dtype,tol", [("fp32", 1e-4), ("bf16", 2e-2)])
+def test_xgmi_loopback_matches_local(gpu, dtype, tol):
+    """The xGMI exchange path at world size 1 with the rank as its own peer (loopback: segment slabs written through
+    to the uncached region, flags, peer reads, the averaging SGD -- the reduction kernel's mode-2 form that a
+    dedicated multi-GPU node runs) trains like the local path: 3 steps from the same initial state, losses and the
+    parameter vector within tolerance (the SGD rounds differently: fma vs multiply-subtract), no exchange error."""
+    import copy
+    from distributeddataparallel_cifar10_amd.data.synthetic import synthetic_cifar
+    from distributeddataparallel_cifar10_amd.models.netresdeep import NetResDeep
+    from distributeddataparallel_cifar10_amd.runtime.engine import EngineConfig, NetResDeepEngine
+    data, labels = synthetic_cifar(512, seed=8, learnable=True)
+    torch.manual_seed(13)
+    m0 = NetResDeep()
+    out = []
+    for loop in (False, True):
+        m = copy.deepcopy(m0).to(gpu)
+        cfg = EngineConfig(batch_max=32, dtype=dtype, comm="xgmi" if loop else "rccl", loopback=loop)
+        eng = NetResDeepEngine(m, data.to(gpu), labels.to(gpu), cfg)
+        if loop:
+            assert eng.xgmi_selftest()
+        eng.set_indices(list(range(512)))
+        eng.set_cursor(0)
+        eng.read_loss(reset=True)
+        eng.run(32, 3)
+        loss, steps = eng.read_loss()
+        eng.check_errors()  # raises on a set exchange / wait error word
+        out.append((loss, steps, torch.cat([p.detach().reshape(-1).cpu() for p in m.parameters()])))
+        eng.close()
+    (l0, s0, p0), (l1, s1, p1) = out
+    assert s0 == s1 == 3 and abs(l0 - l1) <= tol * abs(l0), (l0, l1)
+    assert ((p1 - p0).norm() / p0.norm()).item() < tol
+
+
 def test_graft_smoke(gpu):
     import __graft_entry__
     __graft_entry__.smoke()
