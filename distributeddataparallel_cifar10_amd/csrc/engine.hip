@@ -388,8 +388,9 @@ static int enqueue_pks_reduce(Engine* e, int B, int chunk, int part) {
     ra.fc_in_step = pks::ra_flags(fc, false, 0, chunk);
     ra.seg_ch = seg_ch(e);
     const dim3 rgrid(reduce_grid(e, pks::reduce_segments(fc, ra.seg_ch) + 1));
-    // the lean forms (no fc segments, one exchange mode): world size 1, or the xGMI exchange on a device of its own
-    const int lean = !fc ? 0 : (ra.mode == 0 ? 1 : (ra.mode == 2 && e->shared_device <= 1 ? 2 : 0));
+    // the lean forms (no fc segments, one exchange mode): world size 1, or the xGMI exchange (also on a shared
+    // device, so the multi-rank rehearsals run the form a multi-GPU node runs)
+    const int lean = !fc ? 0 : (ra.mode == 0 ? 1 : (ra.mode == 2 ? 2 : 0));
     const size_t lds = pks::stage_floats(B) * 4;
     if (lean == 1)
       hipLaunchKernelGGL(pks::k_pks_reduce_ar<1>, rgrid, dim3(256), lds, e->st, cx, e->qa, B * pks::S, ra);
