@@ -30,6 +30,13 @@ import time
 
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 
+# Cross-process GPU memory sharing (the xGMI all-reduce maps each peer's gradient region with hipIpcOpenMemHandle;
+# RCCL's intra-node transport shares buffers the same way) must use the dmabuf IPC path: the hosts' kernel driver
+# supports only dmabuf, and with the legacy IPC mode hipIpcGetMemHandle fails with "invalid argument"
+# (profiles/ipc_mode_legacy_r7.log).  Set before any HIP call of this process and inherited by every spawned or
+# torchrun-started rank; an explicit setting in the caller's environment wins.  Same rule: main.py, ppe_main_ddp.py.
+os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+
 BASELINE_METRIC = "images/sec (whole node) CIFAR-10 ResNet at 1/2/4/8 MI355X; scaling efficiency"
 # Practical bar (BASELINE.md publishes no number): the reference training step as-is -- PyTorch-ROCm eager + stock
 # DDP + its host data pipeline -- on one MI355X, measured per precision (bench/reference_eager.py):

@@ -325,7 +325,9 @@ static int reduce_grid(const Engine* e, int nred_plus) {
 // prologue reduction, netresdeep_pks.hip): the SGD must be fused into the segments (world size 1 or xGMI; RCCL and
 // the host all-reduce sit between reduction and SGD), the fc workers run in the step (the prologue leaves the fc
 // segments to them), and the reducers fit beside the live step within the co-residency budget.
-// DCA_PKS_PROLOGUE=0 turns it off (one reduction kernel after every step, the round-4 schedule).
+// Off by default (one reduction kernel after every step); DCA_PKS_PROLOGUE=1 turns it on.  With the xGMI exchange the
+// step's ready wait is bounded by the exchange deadline (netresdeep_pks.hip wait_ready), and the form is covered by a
+// two-rank shared-device test (tests/test_ddp_engine_gpu.py::test_xgmi_prologue_two_ranks_one_gpu).
 static bool prologue_ok(const Engine* e, int B) {
   if (!e->persistent || !e->prologue) return false;
   if (e->comm_on && e->in.comm_mode != 2) return false;

@@ -1124,21 +1124,28 @@ __device__ void prologue_reduce(const Ctx& cx, const Args& pa, const RedAr& ra, 
   __syncthreads();                                    // ... and every thread's of this workgroup
   if (threadIdx.x == 0) gput(rdone(pa) + r, tagof(epoch, RND_RDONE), 0.f);
 }
-// Step workgroups: wait (one wave, bounded) until every reducer of this launch has announced its segment.
+// Step workgroups: wait (one wave, bounded) until every reducer of this launch has announced its segment.  At world
+// size 1 the reducers never wait on anything, so a spin count bounds it; with the xGMI exchange (mode 2) a reducer
+// may itself wait up to ra.deadline for a lagging peer, so this wait is bounded by the same s_memrealtime deadline
+// (a spin count would expire first and let the step read weights the reducers are still writing).
 __device__ __forceinline__ void wait_ready(const Args& pa, const RedAr& ra, int epoch) {
   const int t = threadIdx.x, lane = t & 63;
   if (t < 64) {
     const int nred = prologue_segments(ra.seg_ch);
     const unsigned tag = tagof(epoch, RND_RDONE);
+    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
     for (unsigned spins = 0;; ++spins) {
       bool ok = true;
       for (int k = lane; k < nred; k += 64)
         ok &= (unsigned)(__hip_atomic_load(rdone(pa) + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >> 32) == tag;
       if (__all(ok)) break;
-      if (spins >= SPIN_LIMIT) {
+      const bool expired = ra.mode == 2 ? (__builtin_amdgcn_s_memrealtime() - t0 > ra.deadline + (ra.deadline >> 3))
+                                        : spins >= SPIN_LIMIT;
+      if (expired) {
         if (lane == 0) atomicOr(pa.err, 1u << 28);
         break;
       }
+      if (ra.mode == 2) __builtin_amdgcn_s_sleep(1);
     }
   }
   __syncthreads();

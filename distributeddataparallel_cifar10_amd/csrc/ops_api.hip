@@ -323,7 +323,8 @@ int dca_ops_gemm(const GemmArgs* a, void* stream) {
   // (4 x 4 taps over 16 channels) and the 64-channel 3 x 3 / pad 1 convolutions (layer 1 forward and input gradient)
   const bool dc_stem = g.cC == 16 && g.cKH == 4 && g.cKW == 4 && g.cP == 0;
   const bool dc_3x3 = g.cC == 64 && g.cKH == 3 && g.cKW == 3 && g.cP == 1;
-  if (g.conv == 1 && (dc_stem || dc_3x3) && g.cS == 1 && g.N == 64 && !g.fp8 && !g.tb && g.splits == 1 && g.wperm_T <= 0 && g.orow_S <= 0 && g.out_bf16 && !g.relu &&
+  // (the kernel loops over the compile-time K = KH KW C: an mnk override or a padded K must not reach it)
+  if (g.conv == 1 && (dc_stem || dc_3x3) && g.K == g.cKH * g.cKW * g.cC && g.cS == 1 && g.N == 64 && !g.fp8 && !g.tb && g.splits == 1 && g.wperm_T <= 0 && g.orow_S <= 0 && g.out_bf16 && !g.relu &&
       g.beta == 0.f && !g.beta_mask && g.ldb >= g.K && g.ldb % 8 == 0 && g.ldc >= 64 && g.ldc % 8 == 0 &&
       ((uintptr_t)g.A & 15) == 0 && ((uintptr_t)g.B & 15) == 0 && ((uintptr_t)g.C & 15) == 0 &&
       (long long)g.cN * g.cH * g.cW * g.cC * 2 < (1LL << 31) && (long long)g.M * g.ldc * 2 < (1LL << 31) &&

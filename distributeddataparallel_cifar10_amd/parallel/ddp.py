@@ -47,7 +47,8 @@ class FusedDDPTrainer:
 
     def __init__(self, model: nn.Module, data_u8: torch.Tensor, labels: torch.Tensor, batch_max: int = 32,
                  lr: float = 1e-2, dtype: str = "bf16", rows: int = 4, max_indices: Optional[int] = None,
-                 persistent: Optional[bool] = None, comm: str = "auto", loopback: bool = False):
+                 persistent: Optional[bool] = None, comm: str = "auto", loopback: bool = False,
+                 full_device: bool = False):
         world = dist.get_world_size() if dist.is_available() and dist.is_initialized() else 1
         rank = dist.get_rank() if world > 1 else 0
         self.world_size, self.rank = world, rank
@@ -57,7 +58,7 @@ class FusedDDPTrainer:
             local = int(os.environ.get("LOCAL_WORLD_SIZE", str(world)))
             comm = "xgmi" if 1 < world <= 8 and local == world else "rccl"
         args = dict(batch_max=batch_max, lr=lr, dtype=dtype, rows=rows, world_size=world, rank=rank,
-                    persistent=persistent)
+                    persistent=persistent, full_device=full_device and world == 1)
         self.engine = None
         if loopback:
             if world != 1 or comm != "xgmi":

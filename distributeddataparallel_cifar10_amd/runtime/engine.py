@@ -149,6 +149,9 @@ class EngineConfig:
     loopback: bool = False       # comm="xgmi" at world_size 1: the xGMI exchange with this rank as its own only peer
                                  # (uncached region, write-through slabs, flags, peer reads, averaging SGD): the
                                  # protocol's per-step cost measured on one device (bench.py --loopback)
+    full_device: bool = False    # automatic engine choice on a device this process has to itself: the sliced step may
+                                 # hold every CU (no slack CU), so batch 64 fits; a batch or a device that still does
+                                 # not fit falls back to the multi-kernel engine (main_no_ddp.py)
 
 
 class NetResDeepEngine:
@@ -161,6 +164,7 @@ class NetResDeepEngine:
         if cfg.dtype not in ("bf16", "fp32"):
             raise ValueError("dtype must be 'bf16' or 'fp32'")
         auto_engine = cfg.persistent is None
+        full_device = cfg.full_device or os.environ.get("DCA_PKS_ALLOW_FULL_DEVICE") == "1"
         if auto_engine:
             cfg.persistent = True  # the image-sliced persistent kernel (bf16 and fp32)
         if getattr(model, "n_chans1", 32) != 32 or getattr(model, "n_blocks", 10) != 10:
@@ -195,9 +199,9 @@ class NetResDeepEngine:
             rank=int(cfg.rank), nccl_id=ctypes.cast(self._nccl_id, ctypes.c_char_p),
             persistent=1 if cfg.persistent else 0, debug=1 if cfg.debug else 0, pk_waves=int(cfg.pk_waves),
             comm_mode={"rccl": 0, "external": 1, "xgmi": 2}[cfg.comm], force_comm=1 if cfg.force_comm else 0,
-            # the automatic choice keeps one CU of co-residency slack (batch 64 -> multi-kernel engine);
-            # DCA_PKS_ALLOW_FULL_DEVICE=1 lets it use all 256 CUs (nothing else may then run on the GPU)
-            auto_engine=1 if auto_engine and os.environ.get("DCA_PKS_ALLOW_FULL_DEVICE") != "1" else 0,
+            # the automatic choice keeps one CU of co-residency slack (batch 64 -> multi-kernel engine) unless the
+            # caller owns the device (cfg.full_device, or DCA_PKS_ALLOW_FULL_DEVICE=1): then all 256 CUs
+            auto_engine=1 if auto_engine and not full_device else 0,
             loopback=1 if cfg.loopback else 0,
         )
         self._init = init

@@ -41,7 +41,8 @@ class TrainConfig:
     batch_size: int = 32             # reference main.py:61 (main_no_ddp.py:31 hard-codes 64)
     data_path: str = "data/CIFAR-10/"
     synthetic: int = 0               # >0: use N synthetic CIFAR-shaped samples instead of the dataset
-    synthetic_learnable: bool = False  # synthetic labels a function of the image (class colour + stripes + noise)
+    synthetic_learnable: bool = False  # synthetic "hard" learnable set (data/synthetic.py: blended class colour,
+                                       # random-phase class stripes under noise, 10 % label noise)
     engine: str = "auto"             # auto | fused | torch
     dtype: str = "fp32"              # compute precision: fp32 = the reference's numerics (default), bf16 = MFMA bf16
     max_steps: Optional[int] = None  # per-epoch step cap (smoke tests / benchmarking)
@@ -73,8 +74,9 @@ def add_cli_args(ap: argparse.ArgumentParser, batch_default: int = 32) -> argpar
     ap.add_argument("--synthetic", type=int, nargs="?", const=50000, default=0,
                     help="train on N synthetic CIFAR-shaped samples (default 50000)")
     ap.add_argument("--synthetic-learnable", action="store_true",
-                    help="synthetic data whose label is a function of the image (class colour + stripe pattern + "
-                         "noise), so the loss falls; implies --synthetic 50000 unless given")
+                    help="synthetic data whose label is a function of the image (blended class colour + random-phase "
+                         "class stripes under noise, 10%% label noise), so the loss has a learning curve; implies "
+                         "--synthetic 50000 unless given")
     ap.add_argument("--engine", default="auto", choices=["auto", "fused", "ops", "torch"],
                     help="fused: NetResDeep native engine; ops: the framework's HIP layer kernels (any supported "
                          "model) + FlatBucketDDP; torch: stock PyTorch ops + FlatBucketDDP")
@@ -117,7 +119,7 @@ def config_from_args(a: argparse.Namespace, data_path_default: str) -> TrainConf
 
 def load_dataset(cfg: TrainConfig):
     if cfg.synthetic:
-        return synthetic_cifar(cfg.synthetic, seed=cfg.seed, learnable=cfg.synthetic_learnable)
+        return synthetic_cifar(cfg.synthetic, seed=cfg.seed, learnable="hard" if cfg.synthetic_learnable else False)
     return load_cifar10(cfg.data_path, train=True)
 
 

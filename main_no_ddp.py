@@ -45,12 +45,13 @@ def training_loop(model, train_loader):
     kind = resolve_engine(_cfg, device, model) if isinstance(model, torch.nn.Module) else None
     if kind == "fused":
         n_idx = len(train_loader) * train_loader.batch_size
-        # one process on a dedicated GPU: the sliced persistent engine may take the whole device (batch 64 = 256
-        # step workgroups, one per CU; the automatic choice keeps one CU free and would fall back to the
-        # multi-kernel engine: 273.5 vs 97.9 us per step, profiles/bench_b64_r5f.log)
+        # one process on a dedicated GPU: the automatic engine choice may give the sliced persistent engine the
+        # whole device (batch 64 = 256 step workgroups, one per CU; with one CU kept free it would fall back to the
+        # multi-kernel engine: 273.5 vs 97.9 us per step, profiles/bench_b64_r5f.log).  A batch above 64, or a
+        # device with fewer CUs, still falls back to the multi-kernel engine with a warning.
         model = FusedDDPTrainer(model, train_loader.data, train_loader.labels, batch_max=train_loader.batch_size,
                                 lr=_cfg.lr, dtype=_cfg.dtype, max_indices=max(n_idx, train_loader.batch_size),
-                                persistent=True)
+                                full_device=True)
     elif kind == "ops":  # the ops-layer HIP kernels (flat parameters, packed weights, HIP SGD)
         from distributeddataparallel_cifar10_amd.ops.models import OpsModel
         from distributeddataparallel_cifar10_amd.parallel.flat_ddp import FlatBucketDDP

@@ -11,32 +11,26 @@ stuck rank cannot keep holding CUs that the next test's grids need.
 from __future__ import annotations
 
 import os
-import signal
 import time
 
 import torch.multiprocessing as mp
 
 
-_LAST_GROUP: list = []  # PIDs of the previous rank group (this test process spawned them)
+_LAST_GROUP: list = []  # mp.Process objects of the previous rank group (this test process spawned them)
 
 
 def _previous_group_gone(wait_s: float = 60.0) -> None:
     """No process of the previous rank group may still exist when the next one starts: its hardware queues and IPC
     mappings would overlap the new group's start-up (round 4's illegal-instruction abort hit two ranks' first stock
-    kernels while the previous 8-rank group was still being torn down -- docs/STATUS.md).  Waits, then kills (own
-    PIDs only)."""
+    kernels while the previous 8-rank group was still being torn down -- docs/STATUS.md).  Waits, then kills.  Works
+    on the Process objects, never on bare PIDs: once a process has been reaped its PID may belong to someone else,
+    and Process.is_alive() / kill() never signal a reaped child."""
     deadline = time.time() + wait_s
-    for pid in _LAST_GROUP:
-        while True:
-            try:
-                os.kill(pid, 0)
-            except OSError:
-                break  # gone
-            if time.time() > deadline:
-                os.kill(pid, signal.SIGKILL)
-                time.sleep(0.5)
-                break
-            time.sleep(0.1)
+    for p in _LAST_GROUP:
+        p.join(timeout=max(0.0, deadline - time.time()))
+        if p.is_alive():
+            p.kill()
+            p.join(timeout=30)
     _LAST_GROUP.clear()
 
 
@@ -53,7 +47,7 @@ def spawn_ranks(target, ws: int, args_for_rank, kwargs=None, shared: bool = True
         procs = [ctx.Process(target=target, args=(*args_for_rank(r), q), kwargs=kwargs or {}) for r in range(ws)]
         for p in procs:
             p.start()
-            _LAST_GROUP.append(p.pid)
+            _LAST_GROUP.append(p)
     finally:
         if saved is None:
             os.environ.pop("GPU_MAX_HW_QUEUES", None)

@@ -126,3 +126,20 @@ def test_resolve_engine_large_batch_falls_back():
     assert resolve_engine(TrainConfig(batch_size=128), torch.device("cpu"), m) == "torch"
     with pytest.raises(ValueError, match="batch-size"):
         resolve_engine(TrainConfig(batch_size=128, engine="fused"), cuda, m)
+
+
+def test_bench_sets_dmabuf_ipc_mode():
+    """bench.py (the driver's multi-GPU command) selects the dmabuf IPC mode itself, before any HIP call, so the
+    xGMI all-reduce's IPC mappings work from a launcher environment without HSA_ENABLE_IPC_MODE_LEGACY; an
+    explicit setting in the environment wins."""
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    code = "import os, bench; print(os.environ.get('HSA_ENABLE_IPC_MODE_LEGACY'))"
+    env = dict(os.environ)
+    env.pop("HSA_ENABLE_IPC_MODE_LEGACY", None)
+    r = subprocess.run([sys.executable, "-c", code], cwd=root, env=env, capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0 and r.stdout.strip() == "0", (r.stdout, r.stderr[-2000:])
+    env["HSA_ENABLE_IPC_MODE_LEGACY"] = "1"
+    r = subprocess.run([sys.executable, "-c", code], cwd=root, env=env, capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0 and r.stdout.strip() == "1", (r.stdout, r.stderr[-2000:])

@@ -104,16 +104,20 @@ def test_engine_ddp_two_ranks_one_gpu(gpu, port, dtype, persistent, kernel):
     spawn_ranks(_worker, WS, lambda r: (r, port, dtype, persistent))
 
 
-def _xgmi_worker(rank, ws, port, dtype, persistent, q, comm="xgmi", own_device=False, batch=B, fc_workers=None):
+def _xgmi_worker(rank, ws, port, dtype, persistent, q, comm="xgmi", own_device=False, batch=B, fc_workers=None,
+                 prologue=False):
     """One rank of the fused trainer with the one-shot xGMI all-reduce.  By default all ranks share GPU 0: the
     IPC-mapped slabs are then peers on the same device, which exercises the whole protocol -- epochs, parities,
     flags.  own_device=True (tests/test_multigpu.py): rank r on GPU r, so the slabs and flags cross xGMI, and
     comm="rccl" runs the graph-captured RCCL all-reduce instead.  fc_workers: assert whether the sliced step ran
-    the fc gradient segments (and their xGMI exchange) on its fc workers."""
+    the fc gradient segments (and their xGMI exchange) on its fc workers.  prologue: the prologue-reduction form
+    (DCA_PKS_PROLOGUE=1; each step's segment exchange runs in the next step's launch), all steps in one chunk."""
     try:
         os.environ["MASTER_ADDR"] = "127.0.0.1"
         os.environ["MASTER_PORT"] = str(port)
         os.environ["DCA_XGMI_TIMEOUT_S"] = "30"  # a protocol bug ends as an error flag, not a hang
+        if prologue:
+            os.environ["DCA_PKS_PROLOGUE"] = "1"
         dist.init_process_group("gloo", rank=rank, world_size=ws)
         from distributeddataparallel_cifar10_amd.data.sampler import distributed_indices
         from distributeddataparallel_cifar10_amd.data.synthetic import synthetic_cifar
@@ -140,14 +144,22 @@ def _xgmi_worker(rank, ws, port, dtype, persistent, q, comm="xgmi", own_device=F
         eng.set_cursor(0)
         eng.read_loss(reset=True)
         import time
-        for s in range(STEPS):  # uneven producer timing: ranks reach each step's all-reduce at different times
-            time.sleep(0.03 * ((rank + s) % ws))
-            eng.run(batch, 1)  # graph-captured step, the all-reduce inside the graph
+        nsteps = STEPS
+        if prologue:
+            assert eng.prologue(batch), "the prologue form did not engage"
+            nsteps = 6
+            time.sleep(0.05 * rank)  # uneven start; the steps' exchanges then pace each other
+            eng.run(batch, nsteps)  # one graph chunk: steps 2.. reduce the previous step in their prologue
             eng.sync()
-            print(f"[rank {rank}/{ws}] step {s} done", file=sys.stderr, flush=True)
+        else:
+            for s in range(STEPS):  # uneven producer timing: ranks reach each step's all-reduce at different times
+                time.sleep(0.03 * ((rank + s) % ws))
+                eng.run(batch, 1)  # graph-captured step, the all-reduce inside the graph
+                eng.sync()
+                print(f"[rank {rank}/{ws}] step {s} done", file=sys.stderr, flush=True)
         loss, steps = eng.read_loss()
-        assert steps == STEPS
-        _check_vs_simulation(model, ref0, data, labels, order, rank, ws, STEPS, batch, dtype, persistent)
+        assert steps == nsteps
+        _check_vs_simulation(model, ref0, data, labels, order, rank, ws, nsteps, batch, dtype, persistent)
         tr.close()
         q.put((rank, None))
     except Exception:
@@ -277,14 +289,25 @@ def test_xgmi_fc_workers_two_ranks_one_gpu(gpu, port, dtype):
     spawn_ranks(_xgmi_worker, 2, lambda r: (r, 2, port, dtype, True), dict(batch=8, fc_workers=True))
 
 
+@pytest.mark.parametrize("dtype", ["bf16", "fp32"])
+def test_xgmi_prologue_two_ranks_one_gpu(gpu, port, dtype):
+    """The prologue-reduction form with the xGMI exchange (2 ranks sharing the GPU, batch 8): each step's segment
+    exchange and SGD run at the start of the next step's launch, whose step workgroups wait for them under the
+    exchange deadline.  Must track the DDP simulation with bitwise-equal parameters on both ranks."""
+    spawn_ranks(_xgmi_worker, 2, lambda r: (r, 2, port, dtype, True), dict(batch=8, prologue=True))
+
+
 def test_bench_two_ranks_shared_gpu(gpu, port):
     """The driver's multi-GPU bench command (torch.distributed.run, one rank per GPU) rehearsed with 2 ranks on
-    this box's one GPU: JSON contract, whole-job value, the xGMI all-reduce actually in use."""
+    this box's one GPU: JSON contract, whole-job value, the xGMI all-reduce actually in use.  The launcher's
+    environment has no HSA_ENABLE_IPC_MODE_LEGACY: bench.py must select the dmabuf IPC mode itself (the xGMI
+    all-reduce maps the peers' regions through IPC handles)."""
     import json
     import subprocess
     import sys
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     env = dict(os.environ, DCA_BENCH_SHARE_GPU="1", DCA_XGMI_TIMEOUT_S="60")
+    env.pop("HSA_ENABLE_IPC_MODE_LEGACY", None)
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2", "--master-addr",
            "127.0.0.1", "--master-port", str(port), "bench.py", "--gpus", "2", "--batch", "16", "--steps", "48",
            "--warmup", "16"]  # (2 x batch 32 would fill the device exactly: refused by the co-residency rule)

@@ -280,6 +280,36 @@ def test_main_single_gpu(gpu, tmp_path):
     assert len(sd) == 66 and int(sd["resblocks.0.batch_norm.num_batches_tracked"]) == 200
 
 
+@pytest.mark.parametrize("batch", [64, 96])
+def test_main_no_ddp_batches(gpu, batch):
+    """main_no_ddp.py on its dedicated GPU: batch 64 (the reference's) runs on the sliced engine over the full
+    device through the automatic choice (no explicit persistent=True, so a device or batch that does not fit falls
+    back instead of raising); batch 96 (above the fused engine's 64) runs on the ops-layer kernels."""
+    r = _run(["main_no_ddp.py", "--synthetic", "2048", "--epochs", "1", "--max-steps", "12", "--batch-size",
+              str(batch)])
+    assert r.returncode == 0, r.stderr[-3000:]
+    assert "Epoch 1, Training loss" in r.stdout and "training time:" in r.stdout, r.stdout[-2000:]
+
+
+def test_full_device_engine_choice(gpu):
+    """FusedDDPTrainer(full_device=True) at batch 64: the automatic choice takes the sliced engine on all CUs."""
+    from distributeddataparallel_cifar10_amd.data.synthetic import synthetic_cifar
+    from distributeddataparallel_cifar10_amd.models.netresdeep import NetResDeep
+    from distributeddataparallel_cifar10_amd.parallel.ddp import FusedDDPTrainer
+    data, labels = synthetic_cifar(256, seed=2)
+    tr = FusedDDPTrainer(NetResDeep().to(gpu), data.to(gpu), labels.to(gpu), batch_max=64, full_device=True)
+    try:
+        assert tr.engine.kind_name == "sliced"
+        tr.engine.set_indices(list(range(256)))
+        tr.engine.set_cursor(0)
+        tr.engine.read_loss(reset=True)
+        tr.engine.run(64, 2)
+        loss, steps = tr.engine.read_loss()
+        assert steps == 2 and loss == loss
+    finally:
+        tr.close()
+
+
 def test_bench_contract(gpu):
     r = _run(["bench.py", "--steps", "20", "--warmup", "5"])
     assert r.returncode == 0, r.stderr[-3000:]
