@@ -241,7 +241,18 @@ def train_loop(model, train_loader: DeviceLoader, rank: int, cfg: Optional[Train
     if prof is not None:
         _export_profile(prof, cfg.profile, rank, train_loader.device)
     print(time_line(total), flush=True)
-    return {"losses": history, "seconds": total, "steps": global_step}
+    # end-of-run record (metrics JSON only): the BN step counter after the last epoch -- the last checkpoint is the
+    # epoch-90 one (reference main.py:43-45), so the file holds an earlier count
+    nbt = _num_batches_tracked(unwrap(model))
+    mlog.write(final=True, steps_total=global_step, seconds_total=total, num_batches_tracked=nbt)
+    return {"losses": history, "seconds": total, "steps": global_step, "num_batches_tracked": nbt}
+
+
+def _num_batches_tracked(module) -> Optional[int]:
+    for name, buf in module.named_buffers():
+        if name.endswith("num_batches_tracked"):
+            return int(buf.item())
+    return None
 
 
 _SEEDS = {}
