@@ -51,6 +51,7 @@ def main():
     ap.add_argument("--which", default="both", choices=["both", "ours", "lib"])
     ap.add_argument("--conv", default=None, help="NxHxCxCO: a 3x3 / pad-1 implicit convolution instead")
     ap.add_argument("--summarize", nargs="*", default=None)
+    ap.add_argument("--zeros", action="store_true", help="zero-filled operands (DVFS comparison only)")
     a = ap.parse_args()
     if a.summarize is not None:
         summarize(a.summarize)
@@ -76,11 +77,14 @@ def main():
         M, N, K = (int(v) for v in a.shape.split("x"))
         x = torch.randn(M, K, device=dev).to(bf)
         w = torch.randn(N, K, device=dev).to(bf)
+        if a.zeros:
+            x.zero_()
+            w.zero_()
         ours = lambda: ops.gemm(x, w, out_dtype=bf)  # noqa: E731
         lib = lambda: torch.matmul(x, w.t())  # noqa: E731
         y = ours().float()
         ref = x.float() @ w.float().t()
-        print(json.dumps({"rel_err": ((y - ref).norm() / ref.norm()).item()}), flush=True)
+        print(json.dumps({"rel_err": ((y - ref).norm() / ref.norm().clamp_min(1e-30)).item()}), flush=True)
         del y, ref
     fns = {"ours": ours, "lib": lib}
     for name in (["ours", "lib"] if a.which == "both" else [a.which]):

@@ -612,7 +612,7 @@ __global__ void __launch_bounds__(NW * 64) k_gemm_glds(GemmArgs g) {
   int tm, tn;
   tile_coords(tile, ntm, ntn, tm, tn);
   const int m0 = tm * GBM, n0 = tn * BN_;
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, wr = wave / Wg::WC, wc = wave % Wg::WC;
+  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), wr = wave / Wg::WC, wc = wave % Wg::WC;
   constexpr int ESZ = FP8 ? 1 : 2;
   constexpr int KT = GBK_BYTES / ESZ;
   constexpr int NAI = RA / 8, NBI = RB / 8;  // A / B wave instructions (8 rows each) per tile
@@ -856,6 +856,116 @@ __global__ void __launch_bounds__(NW * 64) k_gemm_glds(GemmArgs g) {
   gemm_epilogue<BN_, NW>(g, acc, smem, m0, n0, tm, ksplit);
 }
 
+// Epilogue of the 256-row tiles (k_gemm_pp): four 64-row quarters of the fp32 tile are staged in LDS by
+// stage(q) (64 x BN fp32, 16-column groups XOR-swizzled by (row >> 2) & 3 -- the kernels' cidx), then written back
+// row-contiguously, 16 B per lane, with alpha / bias / beta / ReLU and the optional BN column statistics (one
+// partial row per 128 output rows, the k_bn_finalize layout).  stage is called with a compile-time q (unrolled:
+// the accumulator indices must stay static).
+template <int NT, int BN = 256, class StageFn>
+__device__ __forceinline__ void store_quarters_256(const GemmArgs& g, char* smem, int m0, int n0, int tm, StageFn stage) {
+  float* ct = (float*)smem;
+  auto cidx = [](int r, int c) { return r * BN + (c ^ (((r >> 2) & 3) << 4)); };
+  const float alpha = gemm_alpha(g);
+  constexpr int CG = BN / 8, RL = NT / CG;  // column groups of 8, row lanes
+  const int cg = threadIdx.x % CG, col0 = n0 + cg * 8;
+  float bias8[8], shift8[8], s1[8], s2[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    const int col = min(col0 + e, g.N - 1);
+    bias8[e] = g.bias ? g.bias[col] : 0.f;
+    shift8[e] = g.col_stats ? g.stats_shift[col] : 0.f;
+    s1[e] = s2[e] = 0.f;
+  }
+  const bool full8 = col0 + 8 <= g.N && (g.ldc & 7) == 0;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    stage(q);
+    __syncthreads();
+    for (int r = 0; r < 64 / RL; ++r) {
+      const int lrow = threadIdx.x / CG + RL * r, row = m0 + q * 64 + lrow;
+      if (row >= g.M || col0 >= g.N) continue;
+      const f32x4 a0 = *(const f32x4*)(ct + cidx(lrow, cg * 8)), a1 = *(const f32x4*)(ct + cidx(lrow, cg * 8 + 4));
+      const float av[8] = {a0[0], a0[1], a0[2], a0[3], a1[0], a1[1], a1[2], a1[3]};
+      const size_t o = (size_t)row * g.ldc + col0;
+      float old[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+      if (g.beta != 0.f) {
+        if (full8 && g.out_bf16) {
+          const uint4 u = *(const uint4*)((const unsigned short*)g.C + o);
+          const unsigned w4[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+          for (int e = 0; e < 8; ++e) old[e] = __uint_as_float((w4[e >> 1] >> ((e & 1) * 16)) << 16);
+        } else {
+          for (int e = 0; e < 8 && col0 + e < g.N; ++e)
+            old[e] = g.out_bf16 ? bf2f(((const unsigned short*)g.C)[o + e]) : ((const float*)g.C)[o + e];
+        }
+      }
+      float v[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        float x = av[e] * alpha + bias8[e] + g.beta * old[e];
+        if (g.relu) x = x > 0.f ? x : 0.f;
+        v[e] = x;
+      }
+      if (g.out_bf16) {
+        unsigned short hb[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) hb[e] = f2bf_rne(v[e]);
+        if (g.col_stats) {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            const float d = bf2f(hb[e]) - shift8[e];
+            s1[e] += d;
+            s2[e] += d * d;
+          }
+        }
+        if (full8) {
+          *(uint4*)((unsigned short*)g.C + o) =
+              uint4{hb[0] | ((unsigned)hb[1] << 16), hb[2] | ((unsigned)hb[3] << 16), hb[4] | ((unsigned)hb[5] << 16),
+                    hb[6] | ((unsigned)hb[7] << 16)};
+        } else {
+          for (int e = 0; e < 8 && col0 + e < g.N; ++e) ((unsigned short*)g.C)[o + e] = hb[e];
+        }
+      } else {
+        if (g.col_stats) {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            const float d = v[e] - shift8[e];
+            s1[e] += d;
+            s2[e] += d * d;
+          }
+        }
+        if (full8) {
+          *(f32x4*)((float*)g.C + o) = f32x4{v[0], v[1], v[2], v[3]};
+          *(f32x4*)((float*)g.C + o + 4) = f32x4{v[4], v[5], v[6], v[7]};
+        } else {
+          for (int e = 0; e < 8 && col0 + e < g.N; ++e) ((float*)g.C)[o + e] = v[e];
+        }
+      }
+    }
+    __syncthreads();
+    if (g.col_stats && (q & 1)) {  // one partial row per 128 output rows (the k_bn_finalize layout)
+      float2* red = (float2*)smem;  // [RL][BN]
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        red[(threadIdx.x / CG) * BN + cg * 8 + e] = float2{s1[e], s2[e]};
+        s1[e] = s2[e] = 0.f;
+      }
+      __syncthreads();
+      for (int c = threadIdx.x; c < BN; c += NT) {
+        const int col = n0 + c;
+        float2 t = red[c];
+        for (int k = 1; k < RL; ++k) {
+          t.x += red[k * BN + c].x;
+          t.y += red[k * BN + c].y;
+        }
+        const int prow = 2 * tm + (q >> 1);
+        if (col < g.N && prow * 128 < g.M) g.col_stats[(size_t)prow * g.N + col] = t;
+      }
+      __syncthreads();
+    }
+  }
+}
+
 // ---------------------------------------------------------------------------------------------------------
 // k_gemm_pp: 256 x 256 output tile, 512 threads as two wave groups that ping-pong (bf16, K-contiguous operands or
 // the C % 64 implicit conv; no split-K / row remap).  Group r (waves 4r .. 4r+3) owns rows 128r .., wave (r, c)
@@ -893,7 +1003,9 @@ __global__ void __launch_bounds__(PP_NT) k_gemm_pp(GemmArgs g) {
   int tm, tn;
   tile_coords(tile, ntm, ntn, tm, tn);
   const int m0 = tm * PP_BM, n0 = tn * PP_BN;
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, wr = wave >> 2;
+  // (wave index made provably uniform: every LDS-DMA's M0 base is then plain SALU arithmetic instead of a VALU
+  // address + v_readfirstlane per instruction -- 4096^3 127 -> 123 us, profiles/gemm_pmc_r7.txt)
+  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), wr = wave >> 2;
   const int wi = (wave & 3) / TT::WNG, wj = (wave & 3) % TT::WNG;  // wave position inside its group
   const int wrow = wr * 128 + wi * (128 / TT::WMG), wcol = wj * 64;
   constexpr int ESZ = 2, KT = GBK_BYTES / ESZ;
@@ -1040,24 +1152,10 @@ __global__ void __launch_bounds__(PP_NT) k_gemm_pp(GemmArgs g) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
 
-  // epilogue: four 64-row quarters staged in LDS (fp32, 64 KiB), written row-contiguously, 16 B per lane, with
-  // alpha / bias / beta / ReLU and the optional BN column statistics (one partial row per 128 output rows)
+  // epilogue: four 64-row quarters staged in LDS (fp32, 64 KiB), written row-contiguously (store_quarters_256)
   float* ct = (float*)smem;
   auto cidx = [](int r, int c) { return r * PP_BN + (c ^ (((r >> 2) & 3) << 4)); };
-  const float alpha = gemm_alpha(g);
-  constexpr int CG = PP_BN / 8, RL = PP_NT / CG;  // 32 column groups, 16 row lanes
-  const int cg = threadIdx.x % CG, col0 = n0 + cg * 8;
-  float bias8[8], shift8[8], s1[8], s2[8];
-#pragma unroll
-  for (int e = 0; e < 8; ++e) {
-    const int col = min(col0 + e, g.N - 1);
-    bias8[e] = g.bias ? g.bias[col] : 0.f;
-    shift8[e] = g.col_stats ? g.stats_shift[col] : 0.f;
-    s1[e] = s2[e] = 0.f;
-  }
-  const bool full8 = col0 + 8 <= g.N && (g.ldc & 7) == 0;
-#pragma unroll  // (compile-time accumulator indices: a runtime index would put acc in scratch)
-  for (int q = 0; q < 4; ++q) {
+  store_quarters_256<PP_NT, PP_BN>(g, smem, m0, n0, tm, [&](int q) {
     // quarter q = rows 64 q ..: group q >> 1; BN = 256: its accumulators (q & 1) * 4 ..; BN = 128: wave wi = q & 1
     if (wr == (q >> 1) && (TT::WMG == 1 || wi == (q & 1))) {
 #pragma unroll
@@ -1069,90 +1167,7 @@ __global__ void __launch_bounds__(PP_NT) k_gemm_pp(GemmArgs g) {
             ct[cidx(m * 16 + (lane >> 4) * 4 + j, wcol + n * 16 + (lane & 15))] =
                 acc[TT::WMG == 1 ? (q & 1) * 4 + m : m][n][j];
     }
-    __syncthreads();
-    for (int r = 0; r < 64 / RL; ++r) {
-      const int lrow = threadIdx.x / CG + RL * r, row = m0 + q * 64 + lrow;
-      if (row >= g.M || col0 >= g.N) continue;
-      const f32x4 a0 = *(const f32x4*)(ct + cidx(lrow, cg * 8)), a1 = *(const f32x4*)(ct + cidx(lrow, cg * 8 + 4));
-      const float av[8] = {a0[0], a0[1], a0[2], a0[3], a1[0], a1[1], a1[2], a1[3]};
-      const size_t o = (size_t)row * g.ldc + col0;
-      float old[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-      if (g.beta != 0.f) {
-        if (full8 && g.out_bf16) {
-          const uint4 u = *(const uint4*)((const unsigned short*)g.C + o);
-          const unsigned w4[4] = {u.x, u.y, u.z, u.w};
-#pragma unroll
-          for (int e = 0; e < 8; ++e) old[e] = __uint_as_float((w4[e >> 1] >> ((e & 1) * 16)) << 16);
-        } else {
-          for (int e = 0; e < 8 && col0 + e < g.N; ++e)
-            old[e] = g.out_bf16 ? bf2f(((const unsigned short*)g.C)[o + e]) : ((const float*)g.C)[o + e];
-        }
-      }
-      float v[8];
-#pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        float x = av[e] * alpha + bias8[e] + g.beta * old[e];
-        if (g.relu) x = x > 0.f ? x : 0.f;
-        v[e] = x;
-      }
-      if (g.out_bf16) {
-        unsigned short hb[8];
-#pragma unroll
-        for (int e = 0; e < 8; ++e) hb[e] = f2bf_rne(v[e]);
-        if (g.col_stats) {
-#pragma unroll
-          for (int e = 0; e < 8; ++e) {
-            const float d = bf2f(hb[e]) - shift8[e];
-            s1[e] += d;
-            s2[e] += d * d;
-          }
-        }
-        if (full8) {
-          *(uint4*)((unsigned short*)g.C + o) =
-              uint4{hb[0] | ((unsigned)hb[1] << 16), hb[2] | ((unsigned)hb[3] << 16), hb[4] | ((unsigned)hb[5] << 16),
-                    hb[6] | ((unsigned)hb[7] << 16)};
-        } else {
-          for (int e = 0; e < 8 && col0 + e < g.N; ++e) ((unsigned short*)g.C)[o + e] = hb[e];
-        }
-      } else {
-        if (g.col_stats) {
-#pragma unroll
-          for (int e = 0; e < 8; ++e) {
-            const float d = v[e] - shift8[e];
-            s1[e] += d;
-            s2[e] += d * d;
-          }
-        }
-        if (full8) {
-          *(f32x4*)((float*)g.C + o) = f32x4{v[0], v[1], v[2], v[3]};
-          *(f32x4*)((float*)g.C + o + 4) = f32x4{v[4], v[5], v[6], v[7]};
-        } else {
-          for (int e = 0; e < 8 && col0 + e < g.N; ++e) ((float*)g.C)[o + e] = v[e];
-        }
-      }
-    }
-    __syncthreads();
-    if (g.col_stats && (q & 1)) {  // one partial row per 128 output rows (the k_bn_finalize layout)
-      float2* red = (float2*)smem;  // [RL][PP_BN]
-#pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        red[(threadIdx.x / CG) * PP_BN + cg * 8 + e] = float2{s1[e], s2[e]};
-        s1[e] = s2[e] = 0.f;
-      }
-      __syncthreads();
-      if (threadIdx.x < PP_BN) {
-        const int col = n0 + threadIdx.x;
-        float2 t = red[threadIdx.x];
-        for (int k = 1; k < RL; ++k) {
-          t.x += red[k * PP_BN + threadIdx.x].x;
-          t.y += red[k * PP_BN + threadIdx.x].y;
-        }
-        const int prow = 2 * tm + (q >> 1);
-        if (col < g.N && prow * 128 < g.M) g.col_stats[(size_t)prow * g.N + col] = t;
-      }
-      __syncthreads();
-    }
-  }
+  });
 }
 
 // ---------------------------------------------------------------------------------------------------------
@@ -1202,7 +1217,7 @@ __global__ void __launch_bounds__(ST_NT, 2) k_gemm_stream(GemmArgs g) {
   constexpr int NST = 8 + 2 * NF;           // stores per lane and epilogue: 8 output rows + the statistics
   extern __shared__ __attribute__((aligned(16))) char smem[];
   constexpr unsigned OOB = 0x80000000u;
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, j = lane & 15, q = lane >> 4;
+  const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), j = lane & 15, q = lane >> 4;
   const int wm = w / NWN, wn = w % NWN;
   const int ntm = (g.M + TM - 1) / TM, ntn = g.N / TN, T = ntm * ntn, nk = g.K / 64;
   const int nstat = (g.M + GBM - 1) / GBM;  // col_stats rows (128-row blocks)
@@ -1534,7 +1549,7 @@ __global__ void __launch_bounds__(DC_NT, 2) k_direct_conv(GemmArgs g) {
   constexpr int NS = T::NS;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   constexpr unsigned OOB = 0x80000000u;
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, j = lane & 15, q = lane >> 4;
+  const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), j = lane & 15, q = lane >> 4;
   char* lw = smem;  // weights: K-tile kt (64 k) at kt * 8 KB, row r (128 B, XOR-swizzled chunks: lds_off)
   float* sbias = (float*)(smem + T::K * 128);
   float* sshift = sbias + 64;

@@ -69,7 +69,7 @@ __global__ void __launch_bounds__(256) k_wgrad(GemmArgs g) {
   const int m0 = (tile / ntn) * BM, n0 = (tile % ntn) * BN;
   const int k_begin = ksplit * g.k_per_split, k_end = min(g.K, k_begin + g.k_per_split);
   const int nk = (k_end - k_begin + T::BK - 1) / T::BK;
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int wm = wave / T::WAVES_N, wn = wave % T::WAVES_N;
   const unsigned short* A = (const unsigned short*)g.A;
   const unsigned short* B = (const unsigned short*)g.B;
@@ -316,7 +316,7 @@ __global__ void __launch_bounds__(WP_NT) k_wgrad_pp(GemmArgs g) {
   const int r0t = (tile / ntn) * WP_BM, c0t = (tile % ntn) * PBN;
   const int k_begin = ksplit * g.k_per_split, k_end = min(g.K, k_begin + g.k_per_split);
   const int nk = (k_end - k_begin + WP_KT - 1) / WP_KT;
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, wr = wave >> 2;
+  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), wr = wave >> 2;
   const int wi = (wave & 3) / T::WNG, wj = (wave & 3) % T::WNG;
   const int wrow = wr * 128 + wi * (128 / T::WMG), wcol = wj * 64;  // this wave's sub-tile in the 256 x PBN tile
   const bool conv = g.conv == 2;  // B (the row side when SW) is the implicit im2col of an NHWC input

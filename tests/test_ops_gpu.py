@@ -66,6 +66,30 @@ def test_gemm_pingpong_matches_torch(gpu):
     assert _rel(y.view(64, 26, 26, 256).permute(0, 3, 1, 2), ref) < 2e-3
 
 
+def test_gemm_256_exact_integers(gpu):
+    """The 256 x 256 GEMM (k_gemm_pp, the production route of these shapes) on small-integer bf16 operands, where
+    fp32 accumulation is exact: plain NT with an M tail and padded rows, and an implicit 3x3 convolution with padding
+    taps -- bitwise against float64 references (catches any staging, swizzle, buffer or fragment-layout error
+    exactly)."""
+    from distributeddataparallel_cifar10_amd import ops
+    from distributeddataparallel_cifar10_amd.ops import functional as F
+    g = torch.Generator(device=gpu).manual_seed(5)
+    bf = torch.bfloat16
+    for M, N, K, lda in [(4096, 2560, 1024, 1024), (4000, 2560, 2048, 2056), (4096, 4096, 4096, 4096)]:
+        a = torch.randint(-3, 4, (M, lda), device=gpu, generator=g).to(bf)[:, :K]
+        b = torch.randint(-3, 4, (N, K), device=gpu, generator=g).to(bf)
+        ref = (a.double() @ b.double().t()).float()
+        out = ops.gemm(a, b, out_dtype=torch.float32)
+        assert torch.equal(out, ref), (M, N, K, (out - ref).abs().max().item())
+    x = torch.randint(-2, 3, (64, 26, 26, 128), device=gpu, generator=g).to(bf)  # 43264 x 256 x 1152: 169 tiles
+    w = torch.randint(-2, 3, (256, 128, 3, 3), device=gpu, generator=g).float()
+    geo = F._geom(x, w, 1, 1)
+    wm = F._weight_matrix(w, geo.K)
+    y = ops.gemm(x, wm, conv=1, geom=geo, mnk=(geo.N * geo.Ho * geo.Wo, 256, geo.K), out_dtype=torch.float32)
+    ref = torch.nn.functional.conv2d(x.double().permute(0, 3, 1, 2), w.double(), padding=1).float()
+    assert torch.equal(y.view(64, 26, 26, 256).permute(0, 3, 1, 2), ref)
+
+
 def test_gemm_stream_matches_torch(gpu):
     """The persistent short-K GEMM (DCA_OPS_STREAM=1, read once per process: run in a child) on plain NT shapes
     with M tails, 1-8 K-tiles, padded strides, bias, beta and the fused BN column statistics (the 128 x 128 tiles
