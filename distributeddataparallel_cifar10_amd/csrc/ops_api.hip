@@ -55,6 +55,13 @@ constexpr bool GLDS_NARROW = true;
 constexpr int REG_SINGLE_NK = 4;
 // glds K pipeline: 2 LDS buffers (3-4 measured 1.4-1.6x slower on the long-K shapes: fewer resident waves)
 constexpr int GLDS_STAGES = 2;
+inline int getenv_pp4() {  // A/B knob: DCA_OPS_PP4=0 keeps the two-buffer k_gemm_pp (and its K >= 1024 rule)
+  static const int v = [] {
+    const char* e = getenv("DCA_OPS_PP4");
+    return e ? atoi(e) : 1;
+  }();
+  return v;
+}
 inline int getenv_stream() {  // persistent short-K GEMM (k_gemm_stream): DCA_OPS_STREAM = 0 never, 1 whenever
   static const int v = [] {    // eligible, 2 (default) by the shape rule at the launch site
     const char* e = getenv("DCA_OPS_STREAM");
@@ -232,6 +239,8 @@ int dca_ops_gemm(const GemmArgs* a, void* stream) {
     }
     OPCK(hipFuncSetAttribute((const void*)k_gemm_pp<256>, hipFuncAttributeMaxDynamicSharedMemorySize,
                              PpTile<256>::LDS));
+    OPCK(hipFuncSetAttribute((const void*)k_gemm_pp4<false>, hipFuncAttributeMaxDynamicSharedMemorySize, PP4_LDS));
+    OPCK(hipFuncSetAttribute((const void*)k_gemm_pp4<true>, hipFuncAttributeMaxDynamicSharedMemorySize, PP4_LDS));
     OPCK(hipFuncSetAttribute((const void*)k_gemm_stream<2, 1, false>, hipFuncAttributeMaxDynamicSharedMemorySize,
                              2 * (2 * G_TILE_BYTES + 8192) + 2 * 2048 * 4));
     OPCK(hipFuncSetAttribute((const void*)k_gemm_stream<2, 1, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -284,6 +293,9 @@ int dca_ops_gemm(const GemmArgs* a, void* stream) {
         g.splits = (g.K + kps - 1) / kps;
       }
       const dim3 grid((unsigned)(tiles * g.splits)), blk(WP_NT);
+      // (the four-slot k32 ring schedule of k_gemm_pp4 measured 20-30 % slower here: each interval would carry
+      // 24 transposed fragment reads and 6 DMA pieces, longer than the other group's 32 MFMAs;
+      // profiles/gemm_ring_ab_r7.log)
       if (sw) {
         hipLaunchKernelGGL((k_wgrad_pp<128, true>), grid, blk, WpTile<128>::LDS, st, g);
       } else if (pbn == 256) {
@@ -418,12 +430,20 @@ int dca_ops_gemm(const GemmArgs* a, void* stream) {
     const long pp_tiles = (long)((g.M + PP_BM - 1) / PP_BM) * ((g.N + ppbn - 1) / ppbn);
     // (a 256 x 128 tile measured slower than the 128 x 128 kernels on every ResNet-50 N = 128 shape, +12-18 %:
     // 16 MFMAs per barrier interval do not cover the other group's fragment loads; removed in round 5)
-    const bool pp_shape = ppbn == 256 && pp_tiles >= 160 && g.K >= 1024;
+    // k_gemm_pp4 (the default) also takes 512 <= K < 1024 (12544 x 2048 x 512 53.3 -> 46.1 us, 12544 x 1024 x 512
+    // 34.8 -> 25.4; below 160 tiles it still loses to the 128 x 128 kernels: profiles/gemm_ring_ab_r7.log)
+    const bool pp_shape = ppbn == 256 && pp_tiles >= 160 && g.K >= (getenv_pp4() ? 512 : 1024);
     const bool pp = pp_shape && !g.fp8 && !g.ta && !g.tb && g.splits == 1 && g.wperm_T <= 0 && g.orow_S <= 0 &&
                     g.M >= 256 && g.N >= 128 && g.K >= 256 && ab < (1LL << 31) && bb < (1LL << 31) &&
                     (long)g.ldb * 2 % 16 == 0 && ((uintptr_t)g.A & 15) == 0 && ((uintptr_t)g.B & 15) == 0 &&
                     (g.conv == 1 ? (g.cC % 64 == 0 && g.cKH * g.cKW <= 32 && g.M < (1 << 24))
                                  : (g.conv == 0 && (long)g.lda * 2 % 16 == 0 && (long)g.K * 2 % 16 == 0));
+    if (pp && g.K % 64 == 0 && getenv_pp4()) {  // the four-slot k32 ring form (k_gemm_pp4)
+      if (g.conv == 1) hipLaunchKernelGGL(k_gemm_pp4<true>, dim3((unsigned)pp_tiles), dim3(PP_NT), PP4_LDS, st, g);
+      else hipLaunchKernelGGL(k_gemm_pp4<false>, dim3((unsigned)pp_tiles), dim3(PP_NT), PP4_LDS, st, g);
+      OPCK(hipGetLastError());
+      return 0;
+    }
     if (pp) {
       hipLaunchKernelGGL(k_gemm_pp<256>, dim3((unsigned)pp_tiles), dim3(PP_NT), PpTile<256>::LDS, st, g);
       OPCK(hipGetLastError());

@@ -1171,6 +1171,173 @@ __global__ void __launch_bounds__(PP_NT) k_gemm_pp(GemmArgs g) {
 }
 
 // ---------------------------------------------------------------------------------------------------------
+// k_gemm_pp4: k_gemm_pp's 256 x 256 tile and ping-pong wave groups on a ring of four k32 slots (32 KiB each: A
+// [256][64 B] | B [256][64 B]) instead of two 64-deep K-tile buffers.  The PMC comparison with hipBLASLt
+// (profiles/gemm_pmc_r7.txt) put k_gemm_pp's loss in the barrier intervals that carry a whole K-tile's LDS-DMA
+// issue (8 pieces per thread in one interval, longer than the other group's 32 MFMAs).  Here every interval of a
+// group issues 4 pieces (2 A + 2 B: 16 rows x 64 B each) of the step two ahead, into the slot its own group finished
+// reading two steps ago, so the issue cost is spread evenly and each DMA still has three to four barrier intervals
+// (~1,500-2,000 MFMA cycles) to land:
+//   group 0, step s: L = issue(s + 2), fragment reads of s | barrier | M = 32 MFMAs of s, vmcnt retires s + 1 |
+//   barrier;  group 1 runs one barrier behind and retires s + 1 at the end of its L interval (the barrier that ends
+//   it is the one before group 0 reads s + 1).
+// Slot (s + 2) & 3 last held step s - 2, read by group 1 in interval 2s - 3 and retired by its M interval 2s - 2.
+// Rows of 64 B with 16-B chunks XOR-swizzled by (row >> 1) & 3 (the fragment reads' lane groups conflict-free);
+// the swizzle is applied to each lane's source chunk (the DMA image is lane-linear).  K % 64 == 0 (launcher).
+// ---------------------------------------------------------------------------------------------------------
+__device__ __forceinline__ int pp4_off(int row, int chunk) { return row * 64 + ((chunk ^ ((row >> 1) & 3)) << 4); }
+constexpr int PP4_SLOT = 2 * PP_BM * 64;  // 32 KiB
+constexpr int PP4_LDS = 4 * PP4_SLOT;     // 128 KiB
+
+template <bool CONV>
+__global__ void __launch_bounds__(PP_NT) k_gemm_pp4(GemmArgs g) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int ntm = (g.M + PP_BM - 1) / PP_BM, ntn = (g.N + PP_BM - 1) / PP_BM;
+  const int tile = xcd_remap(blockIdx.x, ntm * ntn);
+  int tm, tn;
+  tile_coords(tile, ntm, ntn, tm, tn);
+  const int m0 = tm * PP_BM, n0 = tn * PP_BM;
+  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), wr = wave >> 2;
+  const int wrow = wr * 128, wcol = (wave & 3) * 64;
+  constexpr int ESZ = 2;
+  const int nsteps = g.K / 32;
+  constexpr unsigned OOB = 0x80000000u;
+  const long long a_bytes = CONV ? (long long)g.cN * g.cH * g.cW * g.cC * ESZ : ((long long)(g.M - 1) * g.lda + g.K) * ESZ;
+  const long long b_bytes = ((long long)(g.N - 1) * g.ldb + g.K) * ESZ;
+  const __amdgpu_buffer_rsrc_t ars = __builtin_amdgcn_make_buffer_rsrc((void*)g.A, (short)0, (int)a_bytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t brs = __builtin_amdgcn_make_buffer_rsrc((void*)g.B, (short)0, (int)b_bytes, 0x00020000);
+  // staging: wave w loads rows 32 w + 16 i + (lane >> 2), i = 0, 1, of A and of B; chunk position lane & 3
+  const int lq = lane >> 2, lc = lane & 3;
+  unsigned aoff[2], amask[2], boff[2];
+  int s_tap = 0, s_kh = 0, s_kw = 0, s_c0b = 0, s_tapoff = 0;
+  unsigned rep = 0u;
+  float inv_wo = 0.f, inv_ho = 0.f;
+  if constexpr (CONV) {
+    inv_wo = 1.f / (float)g.cWo;
+    inv_ho = 1.f / (float)g.cHo;
+    for (int kh = 0; kh < g.cKH; ++kh) rep |= 1u << (kh * g.cKW);
+  }
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int r = wave * 32 + i * 16 + lq, m = m0 + r, n = n0 + r;
+    const unsigned cb = (unsigned)(lc ^ ((r >> 1) & 3)) << 4;
+    if constexpr (CONV) {
+      int ow, oh;
+      const int t = fdiv_rc(m < g.M ? m : 0, g.cWo, inv_wo, ow), nn = fdiv_rc(t, g.cHo, inv_ho, oh);
+      const int ih0 = oh * g.cS - g.cP, iw0 = ow * g.cS - g.cP;
+      aoff[i] = (unsigned)((((long long)nn * g.cH + ih0) * g.cW + iw0) * g.cC * ESZ + cb);
+      amask[i] = m < g.M ? tap_mask(ih0, iw0, g.cH, g.cW, g.cKH, g.cKW, rep) : 0u;
+    } else {
+      amask[i] = 0u;
+      aoff[i] = m < g.M ? (unsigned)((long long)m * g.lda * ESZ) + cb : OOB;
+    }
+    boff[i] = n < g.N ? (unsigned)((long long)n * g.ldb * ESZ) + cb : OOB;
+  }
+  // this thread's 4 DMA pieces of step st into slot st & 3 (steps issued in increasing order: the conv tap state)
+  auto issue = [&](int st) {
+    char* la = smem + (st & 3) * PP4_SLOT;
+    char* lb = la + PP_BM * 64;
+    const unsigned kb0 = (unsigned)st * 64u;
+    if constexpr (CONV) {
+      const unsigned sadd = (unsigned)(s_tapoff + s_c0b), bit = 1u << s_tap;
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+        blds16(ars, la + (wave * 32 + i * 16) * 64, (amask[i] & bit) ? aoff[i] + sadd : OOB, 0u);
+      s_c0b += 64;
+      if (s_c0b == g.cC * ESZ) {
+        s_c0b = 0;
+        ++s_tap;
+        if (++s_kw == g.cKW) {
+          s_kw = 0;
+          ++s_kh;
+        }
+        s_tapoff = (s_kh * g.cW + s_kw) * g.cC * ESZ;
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < 2; ++i) blds16(ars, la + (wave * 32 + i * 16) * 64, aoff[i], kb0);
+    }
+#pragma unroll
+    for (int i = 0; i < 2; ++i) blds16(brs, lb + (wave * 32 + i * 16) * 64, boff[i], kb0);
+  };
+  auto bar = [] {
+    __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+  };
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int m = 0; m < 8; ++m)
+#pragma unroll
+    for (int n = 0; n < 4; ++n) acc[m][n] = f32x4{0.f, 0.f, 0.f, 0.f};
+  s16x8 af[8], bfr[4];
+  const int frow = lane & 15, fch = lane >> 4;
+  auto load_frags = [&](int st) {
+    const char* la = smem + (st & 3) * PP4_SLOT;
+    const char* lb = la + PP_BM * 64;
+#pragma unroll
+    for (int m = 0; m < 8; ++m) af[m] = *(const s16x8*)(la + pp4_off(wrow + m * 16 + frow, fch));
+#pragma unroll
+    for (int n = 0; n < 4; ++n) bfr[n] = *(const s16x8*)(lb + pp4_off(wcol + n * 16 + frow, fch));
+  };
+  auto mfmas = [&] {
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int m = 0; m < 8; ++m)
+#pragma unroll
+      for (int n = 0; n < 4; ++n) acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[m], bfr[n], acc[m][n], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+  };
+  // prologue: steps 0 and 1 complete and visible
+  issue(0);
+  if (nsteps > 1) issue(1);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  bar();
+  if (wr == 0) {
+#pragma unroll 1
+    for (int st = 0; st < nsteps; ++st) {
+      const bool more = st + 2 < nsteps;
+      if (more) issue(st + 2);
+      load_frags(st);
+      bar();  // end of L(st)
+      mfmas();
+      if (more) wait_vmcnt<4>();  // step st + 1 landed (this thread's part); st + 2 in flight
+      else wait_vmcnt<0>();
+      bar();  // end of M(st)
+    }
+    bar();  // group 1 runs one barrier behind
+  } else {
+    bar();  // end of interval 0
+#pragma unroll 1
+    for (int st = 0; st < nsteps; ++st) {
+      const bool more = st + 2 < nsteps;
+      if (more) issue(st + 2);
+      load_frags(st);
+      if (more) wait_vmcnt<4>();  // step st + 1 landed before the barrier group 0 reads it behind
+      else wait_vmcnt<0>();
+      bar();  // end of L(st)
+      mfmas();
+      bar();  // end of M(st)
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  float* ct = (float*)smem;
+  auto cidx = [](int r, int c) { return r * PP_BM + (c ^ (((r >> 2) & 3) << 4)); };
+  store_quarters_256<PP_NT, 256>(g, smem, m0, n0, tm, [&](int q) {
+    if (wr == (q >> 1)) {
+#pragma unroll
+      for (int m = 0; m < 4; ++m)
+#pragma unroll
+        for (int n = 0; n < 4; ++n)
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+            ct[cidx(m * 16 + (lane >> 4) * 4 + j, wcol + n * 16 + (lane & 15))] = acc[(q & 1) * 4 + m][n][j];
+    }
+  });
+}
+
+// ---------------------------------------------------------------------------------------------------------
 // k_gemm_stream: persistent kernel for the short-K, output-heavy GEMMs of channels-last 1x1 convolutions (ResNet-50
 // at batch 256: M = 5e4..8e5 pixels, N = 128..2048, K = 64..256).  Those calls move ~3x more bytes out than in and
 // have 1-4 K-tiles per 128 x 128 tile, so the one-tile-per-workgroup kernels serialise load -> MFMA -> LDS-staged

@@ -37,14 +37,15 @@ def test_gemm_bf16(gpu, M, N, K, ta, tb):
 
 
 def test_gemm_pingpong_matches_torch(gpu):
-    """The ping-pong 256 x 256 GEMM (k_gemm_pp) on shapes its production rule routes to it (N % 256 == 0, >= 160
-    output tiles, K >= 1024): plain NT with M / K tails, bf16 output + bias + ReLU, the fused BN column statistics,
-    and an implicit 3x3 convolution with C % 64 == 0 -- against torch fp32."""
+    """The ping-pong 256 x 256 GEMMs on shapes the production rule routes to them (N % 256 == 0, >= 160 output
+    tiles): k_gemm_pp4 (K % 64 == 0, K >= 512) and k_gemm_pp (K = 1040: K % 64 != 0, K >= 1024); plain NT with M / K
+    tails, bf16 output + bias + ReLU, the fused BN column statistics, and an implicit 3x3 convolution with C % 64 == 0
+    -- against torch fp32."""
     from distributeddataparallel_cifar10_amd import ops
     from distributeddataparallel_cifar10_amd.ops import functional as F
     g = torch.Generator(device=gpu).manual_seed(0)
     bf = torch.bfloat16
-    for M, N, K in [(4096, 2560, 1024), (4000, 2560, 1040)]:
+    for M, N, K in [(4096, 2560, 1024), (4000, 2560, 1040), (4000, 2560, 576)]:
         a = torch.randn(M, K, device=gpu, generator=g).to(bf)
         b = torch.randn(N, K, device=gpu, generator=g).to(bf)
         bias = torch.randn(N, device=gpu, generator=g)
@@ -67,7 +68,7 @@ def test_gemm_pingpong_matches_torch(gpu):
 
 
 def test_gemm_256_exact_integers(gpu):
-    """The 256 x 256 GEMM (k_gemm_pp, the production route of these shapes) on small-integer bf16 operands, where
+    """The 256 x 256 GEMM (k_gemm_pp4, the production route of these shapes) on small-integer bf16 operands, where
     fp32 accumulation is exact: plain NT with an M tail and padded rows, and an implicit 3x3 convolution with padding
     taps -- bitwise against float64 references (catches any staging, swizzle, buffer or fragment-layout error
     exactly)."""
