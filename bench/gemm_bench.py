@@ -60,7 +60,7 @@ def main():
         us = timeit(lambda: ops.gemm(x, wm, conv=1, geom=g, mnk=(M, co, g.K), out_dtype=bf))
         rec(f"conv3x3 fwd {n}x{h}x{h}x{c}->{co}", us, fl, 2 * (M * c + M * co))
         dy = torch.randn(M, co, device=dev).to(bf)
-        sp = F._wgrad_splits(co, g.K, M)
+        sp = F._wgrad_splits(co, g.K, M, True)
         us = timeit(lambda: ops.gemm(dy, x, ta=True, conv=2, geom=g, mnk=(co, g.K, M), splits=sp))
         rec(f"conv3x3 wgrad {n}x{h}x{h}x{c}->{co} splits {sp}", us, fl, 2 * (M * c + M * co))
         cols = torch.randn(M, g.K, device=dev).to(bf)

@@ -76,8 +76,8 @@ def main() -> int:
             dst = torch.empty(co, c, k, k, device=dev)
 
             def run():
-                F.gemm(dy, x, ta=True, conv=2, geom=g, mnk=(co, g.K, M), splits=F._wgrad_splits(co, g.K, M), out=dst,
-                       beta=0.0, wperm=(c, g.C, k * k))
+                F.gemm(dy, x, ta=True, conv=2, geom=g, mnk=(co, g.K, M), splits=F._wgrad_splits(co, g.K, M, True),
+                       out=dst, beta=0.0, wperm=(c, g.C, k * k))
             us = timeit(run, a.iters)
             run()
             # reference on a slice of the batch (full-batch fp32 conv weight-gradient is slow and large)
@@ -89,7 +89,7 @@ def main() -> int:
             Ms = nb * g.Ho * g.Wo
             gs = F._geom(x[:nb].contiguous(), wt, s, p)
             F.gemm(dy[:Ms].contiguous(), x[:nb].contiguous(), ta=True, conv=2, geom=gs, mnk=(co, gs.K, Ms),
-                   splits=F._wgrad_splits(co, gs.K, Ms), out=dst_s, beta=0.0, wperm=(c, gs.C, k * k))
+                   splits=F._wgrad_splits(co, gs.K, Ms, True), out=dst_s, beta=0.0, wperm=(c, gs.C, k * k))
             e = check(dst_s, ref)
             worst = max(worst, e)
             fl = 2.0 * M * co * k * k * c
