@@ -69,7 +69,9 @@ inline int getenv_stream() {  // persistent short-K GEMM (k_gemm_stream): DCA_OP
   }();
   return v;
 }
-// implicit 3x3 convolutions (N = 128) on k_gemm_stream (129.5 -> 117.5 us at batch 256)
+// implicit 3x3 convolutions (N = 128) on k_gemm_stream (129.5 -> 117.5 us at batch 256), and the strided 1x1
+// (downsample) ones with N % 128 == 0 and M >= 16384 (256x56x56x256 -> 512: 177 -> 126 us, 256x28x28x512 -> 1024:
+// 116 -> 101 us; 256x14x14x1024 -> 2048, M = 12544, stays on pp4: 82 vs 95 us; profiles/stream_downsample_ab_r8f.log)
 constexpr bool STREAM_CONV = true;
 // weight gradients with M >= 256 (and the swapped 1x1 forms) on the ping-pong LDS-DMA kernel k_wgrad_pp
 // (0.71-0.92x the k_wgrad time on every routed shape); the 64-wide / swapped implicit forms stay on k_wgrad
@@ -373,9 +375,12 @@ int dca_ops_gemm(const GemmArgs* a, void* stream) {
     const long long bb = ((long long)(g.N - 1) * g.ldb + g.K) * 2;
     const long long cbytes = (long long)g.M * g.ldc * 2;
     const int mw = g.N % 128 == 0 ? 1 : 2;  // 128 x 128 tiles, or 256 x 64 for N % 128 == 64
-    const bool shape_ok = conv ? (g.cC % 64 == 0 && g.cKH * g.cKW <= 32 && (g.N == 64 || g.N == 128) && g.orow_S <= 0 &&
+    const bool shape_ok = conv ? (g.cC % 64 == 0 && g.cKH * g.cKW <= 32 &&
+                                  (g.N == 64 || g.N == 128 || (g.cKH * g.cKW == 1 && g.N % 128 == 0)) &&
+                                  g.orow_S <= 0 &&
                                   g.M < (1 << 24) &&
-                                  (sk == 1 || (sk == 2 && STREAM_CONV && g.N == 128 && g.M >= 16384)))
+                                  (sk == 1 || (sk == 2 && STREAM_CONV && g.M >= 16384 &&
+                                               (g.N == 128 || (g.cKH * g.cKW == 1 && g.N % 128 == 0)))))
                                : (g.conv == 0 && !g.ta && g.lda % 8 == 0 && g.lda >= g.K &&
                                   (g.N % 128 == 0 || g.N == 64) &&
                                   (sk == 1 || (g.K <= 512 && g.M >= 16384 &&

@@ -798,6 +798,27 @@ def test_ops_resnet_counts_batches_once_per_forward(gpu):
     assert counts == {3}, counts
 
 
+def test_strided_1x1_conv_on_stream_kernel(gpu):
+    """A strided 1x1 (downsample) convolution with N % 128 == 0 and M >= 16384 -- the production route onto the
+    persistent stream kernel's implicit-conv form -- with the fused BN column statistics, vs torch fp32."""
+    from distributeddataparallel_cifar10_amd import ops
+    from distributeddataparallel_cifar10_amd.ops import functional as F
+    g = torch.Generator(device=gpu).manual_seed(21)
+    n, h, c, co = 24, 56, 128, 384  # M = 24 x 28 x 28 = 18816
+    x = _bf(torch.randn(n, h, h, c, device=gpu, generator=g))
+    w = torch.randn(co, c, 1, 1, device=gpu, generator=g) * 0.05
+    geo = F._geom(x, w, 2, 0)
+    M = n * geo.Ho * geo.Wo
+    parts = torch.zeros((M + 127) // 128, co, 2, device=gpu)
+    shift = torch.randn(co, device=gpu, generator=g) * 0.1
+    y = ops.gemm(x, F._weight_matrix(w, geo.K), conv=1, geom=geo, mnk=(M, co, geo.K), out_dtype=torch.bfloat16,
+                 col_stats=parts, stats_shift=shift)
+    ref = torch.nn.functional.conv2d(x.float().permute(0, 3, 1, 2), _bf(w).float(), stride=2)
+    assert _rel(y.float().view(n, geo.Ho, geo.Wo, co).permute(0, 3, 1, 2), ref) < 5e-3
+    d = y.float() - shift
+    assert _rel(parts[..., 0].sum(0), d.sum(0)) < 1e-4 and _rel(parts[..., 1].sum(0), (d * d).sum(0)) < 1e-4
+
+
 @pytest.mark.parametrize("k,p", [(3, 1), (1, 0)])
 def test_strided_conv_subpixel_input_grad(gpu, k, p):
     """Stride-2 conv input gradient by parity classes (implicit stride-1 convs over dY, GEMM epilogue rows
