@@ -164,7 +164,7 @@ using namespace dca::ops;
 extern "C" {
 
 const char* dca_ops_last_error() { return g_err.c_str(); }
-int dca_ops_abi_version() { return 11; }
+int dca_ops_abi_version() { return 12; }
 
 // Must match ops/_native.py::GemmArgs.
 int dca_ops_gemm(const GemmArgs* a, void* stream) {
@@ -681,6 +681,46 @@ int dca_ops_maxpool_bwd(const void* dy, const void* arg, void* dx, const PoolGeo
   else
     hipLaunchKernelGGL(k_maxpool_bwd<long>, grid, dim3(256), 0, (hipStream_t)stream,
                        (const bf16_t*)dy, (const uint8_t*)arg, (bf16_t*)dx, g);
+  OPCK(hipGetLastError());
+  return 0;
+}
+
+// The ResNet stem's BatchNorm + ReLU + 3x3/2/1 max pool as one pass over the conv output y [N][H][W][C] (H = 2 Ho,
+// W = 2 Wo, C % 64 == 0), the BN column partials coming from the conv GEMM's epilogue (col_stats): finalize + fused
+// apply-and-pool into out / arg [N][Ho][Wo][C] (k_bn_pool_fwd).  Same values as dca_ops_bn_fwd_parts followed by
+// dca_ops_maxpool_fwd, without the activation in between.
+inline bool bn_pool_ok(const PoolGeom& g) {
+  return g.K == 3 && g.S == 2 && g.P == 1 && g.H == 2 * g.Ho && g.W == 2 * g.Wo && g.C % 64 == 0 && pool_idx32(g);
+}
+int dca_ops_bn_pool_fwd_parts(const void* y, float* part, int nparts, float* stats, const float* gamma,
+                              const float* beta, float* rm, float* rv, float eps, float momentum, void* out, void* arg,
+                              const PoolGeom* geom, unsigned* ticket, void* stream) {
+  const PoolGeom g = *geom;
+  REQUIRE(bn_pool_ok(g), "bn_pool: 3x3/2/1 pool with H = 2 Ho, W = 2 Wo, C % 64 == 0, 32-bit offsets");
+  hipStream_t st = (hipStream_t)stream;
+  const long M = (long)g.N * g.H * g.W;
+  bn_fin_launch<0>(part, nparts, M, g.C, rm, rv, stats, eps, momentum, 0, ticket, st);
+  hipLaunchKernelGGL(k_bn_pool_fwd<unsigned>, dim3(grid_for((long)g.N * g.Ho * g.Wo * g.C / 8)), dim3(256), 0, st,
+                     (const bf16_t*)y, (bf16_t*)out, (uint8_t*)arg, g, (const float2*)stats, gamma, beta);
+  OPCK(hipGetLastError());
+  return 0;
+}
+// Its backward from the pooled gradient dp and the argmax bytes: dx = d(conv output); dgamma / dbeta written, or
+// accumulated (flat gradient sinks).  part: [ceil(N Ho Wo / BNP_OPB)][C] float2 scratch, sums: [C] float2.
+int dca_ops_bn_pool_bwd(const void* dp, const void* arg, const void* y, const float* stats, const float* gamma,
+                        const float* beta, float* part, float* sums, float* dgamma, float* dbeta, void* dx,
+                        int accumulate, const PoolGeom* geom, unsigned* ticket, void* stream) {
+  const PoolGeom g = *geom;
+  REQUIRE(bn_pool_ok(g), "bn_pool: 3x3/2/1 pool with H = 2 Ho, W = 2 Wo, C % 64 == 0, 32-bit offsets");
+  hipStream_t st = (hipStream_t)stream;
+  const long npo = (long)g.N * g.Ho * g.Wo;
+  const int nparts = (int)((npo + BNP_OPB - 1) / BNP_OPB);
+  hipLaunchKernelGGL(k_bn_pool_bwd_stats<unsigned>, dim3(g.C / 64, nparts), dim3(256), 0, st, (const bf16_t*)dp,
+                     (const uint8_t*)arg, (const bf16_t*)y, (const float2*)stats, gamma, beta, (float2*)part, g);
+  bn_fin_launch<1>(part, nparts, (long)g.N * g.H * g.W, g.C, dgamma, dbeta, sums, 0.f, 0.f, accumulate, ticket, st);
+  hipLaunchKernelGGL(k_bn_pool_bwd_apply<unsigned>, dim3(grid_for(npo * g.C / 8)), dim3(256), 0, st,
+                     (const bf16_t*)dp, (const uint8_t*)arg, (const bf16_t*)y, (const float2*)stats, gamma, beta,
+                     (const float2*)sums, (bf16_t*)dx, g);
   OPCK(hipGetLastError());
   return 0;
 }

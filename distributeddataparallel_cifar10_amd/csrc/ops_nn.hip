@@ -677,9 +677,16 @@ __global__ void __launch_bounds__(256) k_maxpool_fwd(const bf16_t* __restrict__ 
 // their 9 loads one after another (a memory latency each); here all 9 are unrolled and in flight together.  Only
 // the top row / left column of a window can fall into the padding (H = 2 Ho): those taps load the window centre
 // and are skipped in the compare, which runs in the same tap order (first max wins, NaN propagates).
-template <typename IT>
-__global__ void __launch_bounds__(256) k_maxpool_fwd_k3s2(const bf16_t* __restrict__ x, bf16_t* __restrict__ y,
-                                                          uint8_t* __restrict__ arg, PoolGeom g) {
+// BN = true (the ResNet stem, k_bn_pool_fwd): x is the conv output y and every tap is first taken through the
+// training BatchNorm + ReLU and rounded to bf16 exactly as k_bn_apply stores it, so pooled values and argmax bytes
+// equal those of k_bn_apply followed by the plain pool -- without writing and re-reading the N x H x W x C
+// activation (822 MB per ResNet-50 step at batch 256).
+__device__ __forceinline__ float rbf16(float f) { return bf2f(f2bf_rne(f)); }
+template <typename IT, bool BN>
+__device__ __forceinline__ void maxpool_k3s2_fwd(const bf16_t* __restrict__ x, bf16_t* __restrict__ y,
+                                                 uint8_t* __restrict__ arg, const PoolGeom& g,
+                                                 const float2* __restrict__ stats, const float* __restrict__ gamma,
+                                                 const float* __restrict__ beta) {
   const IT cgs = (IT)(g.C >> 3), Wo = (IT)g.Wo, Ho = (IT)g.Ho;
   const IT total = (IT)g.N * Ho * Wo * cgs;
   for (IT i = (IT)blockIdx.x * 256 + threadIdx.x; i < total; i += (IT)gridDim.x * 256) {
@@ -698,6 +705,15 @@ __global__ void __launch_bounds__(256) k_maxpool_fwd_k3s2(const bf16_t* __restri
         const IT o = ok ? ctr + (IT)(kh * rs) - rs + (IT)(kw * g.C) - (IT)g.C : ctr;
         u[kh * 3 + kw] = *(const uint4*)(x + o);
       }
+    float sc[8], sh[8];
+    if constexpr (BN) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {  // k_bn_apply's per-channel coefficients
+        const float2 st = stats[c + j];
+        sc[j] = st.y * gamma[c + j];
+        sh[j] = beta[c + j] - st.x * sc[j];
+      }
+    }
     float best[8];
     int bi[8];
 #pragma unroll
@@ -710,6 +726,14 @@ __global__ void __launch_bounds__(256) k_maxpool_fwd_k3s2(const bf16_t* __restri
       if (!((t >= 3 || top) && (t % 3 > 0 || left))) continue;
       float v[8];
       unpack8(u[t], v);
+      if constexpr (BN) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          float z = v[j] * sc[j] + sh[j];
+          z = z > 0.f ? z : 0.f;
+          v[j] = rbf16(z);
+        }
+      }
 #pragma unroll
       for (int j = 0; j < 8; ++j)
         if (v[j] > best[j] || (v[j] != v[j] && best[j] == best[j])) {
@@ -723,12 +747,68 @@ __global__ void __launch_bounds__(256) k_maxpool_fwd_k3s2(const bf16_t* __restri
                                (unsigned)bi[4] | ((unsigned)bi[5] << 8) | ((unsigned)bi[6] << 16) | ((unsigned)bi[7] << 24)};
   }
 }
+template <typename IT>
+__global__ void __launch_bounds__(256) k_maxpool_fwd_k3s2(const bf16_t* __restrict__ x, bf16_t* __restrict__ y,
+                                                          uint8_t* __restrict__ arg, PoolGeom g) {
+  maxpool_k3s2_fwd<IT, false>(x, y, arg, g, nullptr, nullptr, nullptr);
+}
+template <typename IT>
+__global__ void __launch_bounds__(256) k_bn_pool_fwd(const bf16_t* __restrict__ x, bf16_t* __restrict__ y,
+                                                     uint8_t* __restrict__ arg, PoolGeom g,
+                                                     const float2* __restrict__ stats, const float* __restrict__ gamma,
+                                                     const float* __restrict__ beta) {
+  maxpool_k3s2_fwd<IT, true>(x, y, arg, g, stats, gamma, beta);
+}
 
-// 3x3 / stride 2 / pad 1 with H = 2 Ho, W = 2 Wo, C % 8 == 0 (the ResNet stem pool): one thread per OUTPUT
-// pixel and 8 channels writes the 2x2 input block (2oh..2oh+1, 2ow..2ow+1).  Even input rows/cols are reached only
-// by the centre tap of their own output; odd ones also by the next output's first tap.  Every dy / argmax record
-// is loaded once per thread (4 loads -> 4 stores, instead of 2.25 loads per store in the input-driven kernel).
-// Sums are taken in ascending tap order, as in k_maxpool_bwd.
+// 3x3 / stride 2 / pad 1 backward with H = 2 Ho, W = 2 Wo, C % 8 == 0 (the ResNet stem pool): output pixel
+// (n, oh, ow) and 8 channels own the 2x2 input block (2oh..2oh+1, 2ow..2ow+1).  Even input rows/cols are reached
+// only by the centre tap of their own output; odd ones also by the next output's first tap.  Every dy / argmax
+// record is loaded once per thread (4 loads -> 4 blocks, instead of 2.25 loads per store in the input-driven
+// kernel).  Sums are taken in ascending tap order, as in k_maxpool_bwd.  e[k][j]: input pixel k = 2 a + b of the
+// block (row offset a, column offset b), channel c + j, in fp32 (the pool backward rounds them to bf16).
+template <typename IT>
+__device__ __forceinline__ void maxpool_k3s2_block_grad(const bf16_t* __restrict__ dy,
+                                                        const uint8_t* __restrict__ arg, const PoolGeom& g, IT p,
+                                                        int c, int oh, int ow, float (&e)[4][8]) {
+  const bool hr = oh + 1 < g.Ho, hc = ow + 1 < g.Wo;
+  // records (oh, ow), (oh, ow+1), (oh+1, ow), (oh+1, ow+1); missing neighbours read the own record with an
+  // impossible tap (255) so all loads are unconditional
+  const IT o00 = p * g.C + c;
+  const IT o01 = hc ? o00 + g.C : o00;
+  const IT o10 = hr ? o00 + (IT)g.Wo * g.C : o00;
+  const IT o11 = hr && hc ? o00 + ((IT)g.Wo + 1) * g.C : o00;
+  float d00[8], d01[8], d10[8], d11[8];
+  unpack8(*(const uint4*)(dy + o00), d00);
+  unpack8(*(const uint4*)(dy + o01), d01);
+  unpack8(*(const uint4*)(dy + o10), d10);
+  unpack8(*(const uint4*)(dy + o11), d11);
+  const uint2 a00 = *(const uint2*)(arg + o00), a01 = *(const uint2*)(arg + o01);
+  const uint2 a10 = *(const uint2*)(arg + o10), a11 = *(const uint2*)(arg + o11);
+  const unsigned m01 = hc ? 0u : 0xffu, m10 = hr ? 0u : 0xffu, m11 = hr && hc ? 0u : 0xffu;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int sh = (j & 3) * 8;
+    const unsigned t00 = ((j < 4 ? a00.x : a00.y) >> sh) & 0xffu;
+    const unsigned t01 = (((j < 4 ? a01.x : a01.y) >> sh) & 0xffu) | m01;
+    const unsigned t10 = (((j < 4 ? a10.x : a10.y) >> sh) & 0xffu) | m10;
+    const unsigned t11 = (((j < 4 ? a11.x : a11.y) >> sh) & 0xffu) | m11;
+    e[0][j] = t00 == 4u ? d00[j] : 0.f;
+    float s = 0.f;
+    s += t01 == 3u ? d01[j] : 0.f;
+    s += t00 == 5u ? d00[j] : 0.f;
+    e[1][j] = s;
+    s = 0.f;
+    s += t10 == 1u ? d10[j] : 0.f;
+    s += t00 == 7u ? d00[j] : 0.f;
+    e[2][j] = s;
+    s = 0.f;
+    s += t11 == 0u ? d11[j] : 0.f;
+    s += t10 == 2u ? d10[j] : 0.f;
+    s += t01 == 6u ? d01[j] : 0.f;
+    s += t00 == 8u ? d00[j] : 0.f;
+    e[3][j] = s;
+  }
+}
 template <typename IT>
 __global__ void __launch_bounds__(256) k_maxpool_bwd_k3s2(const bf16_t* __restrict__ dy,
                                                           const uint8_t* __restrict__ arg, bf16_t* __restrict__ dx,
@@ -739,51 +819,128 @@ __global__ void __launch_bounds__(256) k_maxpool_bwd_k3s2(const bf16_t* __restri
     const int c = (int)(i % cgs) * 8;
     const IT p = i / cgs, pr = p / Wo;
     const int ow = (int)(p - pr * Wo), oh = (int)(pr % Ho), n = (int)(pr / Ho);
-    const bool hr = oh + 1 < g.Ho, hc = ow + 1 < g.Wo;
-    // records (oh, ow), (oh, ow+1), (oh+1, ow), (oh+1, ow+1); missing neighbours read the own record with an
-    // impossible tap (255) so all loads are unconditional
-    const IT o00 = p * g.C + c;
-    const IT o01 = hc ? o00 + g.C : o00;
-    const IT o10 = hr ? o00 + (IT)g.Wo * g.C : o00;
-    const IT o11 = hr && hc ? o00 + ((IT)g.Wo + 1) * g.C : o00;
-    float d00[8], d01[8], d10[8], d11[8];
-    unpack8(*(const uint4*)(dy + o00), d00);
-    unpack8(*(const uint4*)(dy + o01), d01);
-    unpack8(*(const uint4*)(dy + o10), d10);
-    unpack8(*(const uint4*)(dy + o11), d11);
-    const uint2 a00 = *(const uint2*)(arg + o00), a01 = *(const uint2*)(arg + o01);
-    const uint2 a10 = *(const uint2*)(arg + o10), a11 = *(const uint2*)(arg + o11);
-    const unsigned m01 = hc ? 0u : 0xffu, m10 = hr ? 0u : 0xffu, m11 = hr && hc ? 0u : 0xffu;
-    float e00[8], e01[8], e10[8], e11[8];
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const int sh = (j & 3) * 8;
-      const unsigned t00 = ((j < 4 ? a00.x : a00.y) >> sh) & 0xffu;
-      const unsigned t01 = (((j < 4 ? a01.x : a01.y) >> sh) & 0xffu) | m01;
-      const unsigned t10 = (((j < 4 ? a10.x : a10.y) >> sh) & 0xffu) | m10;
-      const unsigned t11 = (((j < 4 ? a11.x : a11.y) >> sh) & 0xffu) | m11;
-      e00[j] = t00 == 4u ? d00[j] : 0.f;
-      float s = 0.f;
-      s += t01 == 3u ? d01[j] : 0.f;
-      s += t00 == 5u ? d00[j] : 0.f;
-      e01[j] = s;
-      s = 0.f;
-      s += t10 == 1u ? d10[j] : 0.f;
-      s += t00 == 7u ? d00[j] : 0.f;
-      e10[j] = s;
-      s = 0.f;
-      s += t11 == 0u ? d11[j] : 0.f;
-      s += t10 == 2u ? d10[j] : 0.f;
-      s += t01 == 6u ? d01[j] : 0.f;
-      s += t00 == 8u ? d00[j] : 0.f;
-      e11[j] = s;
-    }
+    float e[4][8];
+    maxpool_k3s2_block_grad<IT>(dy, arg, g, p, c, oh, ow, e);
     const IT x00 = (((IT)n * g.H + 2 * oh) * g.W + 2 * ow) * g.C + c;
     const IT xr = (IT)g.W * g.C;
-    *(uint4*)(dx + x00) = pack8(e00);
-    *(uint4*)(dx + x00 + g.C) = pack8(e01);
-    *(uint4*)(dx + x00 + xr) = pack8(e10);
-    *(uint4*)(dx + x00 + xr + g.C) = pack8(e11);
+    *(uint4*)(dx + x00) = pack8(e[0]);
+    *(uint4*)(dx + x00 + g.C) = pack8(e[1]);
+    *(uint4*)(dx + x00 + xr) = pack8(e[2]);
+    *(uint4*)(dx + x00 + xr + g.C) = pack8(e[3]);
+  }
+}
+
+// The stem's BN backward through the fused pool (k_bn_pool_fwd): dz of an input pixel is the pool backward's value
+// (maxpool_k3s2_block_grad, rounded to bf16 as k_maxpool_bwd_k3s2 stores it) times the ReLU mask recomputed from
+// y, as BWD_RELU does -- so neither dz nor the post-ReLU activation is ever written (the unfused backward wrote dz
+// and read it twice: 1.1 GB per ResNet-50 step at batch 256).
+// Statistics: grid (C / 64, ceil(Npo / 64)) over the Npo output pixels, 256 threads = 8 channel groups x 32 pixel
+// lanes x 2 output pixels; part[blockIdx.y][C] = (sum dz, sum dz * xhat) of the block's 256 input pixels.
+constexpr int BNP_OPB = 64;  // output pixels per statistics workgroup
+template <typename IT>
+__global__ void __launch_bounds__(256) k_bn_pool_bwd_stats(const bf16_t* __restrict__ dp, const uint8_t* __restrict__ arg,
+                                                           const bf16_t* __restrict__ x, const float2* __restrict__ stats,
+                                                           const float* __restrict__ gamma,
+                                                           const float* __restrict__ beta, float2* __restrict__ part,
+                                                           PoolGeom g) {
+  __shared__ float2 red[32][64];
+  const int cgl = threadIdx.x & 7, pl = threadIdx.x >> 3, c = blockIdx.x * 64 + cgl * 8;
+  const IT npo = (IT)g.N * g.Ho * g.Wo;
+  float s[8], q[8], mu[8], is[8], ga[8], be[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    s[j] = q[j] = 0.f;
+    mu[j] = stats[c + j].x;
+    is[j] = stats[c + j].y;
+    ga[j] = gamma[c + j];
+    be[j] = beta[c + j];
+  }
+#pragma unroll
+  for (int u = 0; u < BNP_OPB / 32; ++u) {
+    const IT p = (IT)blockIdx.y * BNP_OPB + pl + 32 * u;
+    if (p >= npo) break;
+    const IT pr = p / (IT)g.Wo;
+    const int ow = (int)(p - pr * (IT)g.Wo), oh = (int)(pr % (IT)g.Ho), n = (int)(pr / (IT)g.Ho);
+    const IT x00 = (((IT)n * g.H + 2 * oh) * g.W + 2 * ow) * g.C + c, xr = (IT)g.W * g.C;
+    const uint4 X[4] = {*(const uint4*)(x + x00), *(const uint4*)(x + x00 + g.C), *(const uint4*)(x + x00 + xr),
+                        *(const uint4*)(x + x00 + xr + g.C)};
+    float e[4][8];
+    maxpool_k3s2_block_grad<IT>(dp, arg, g, p, c, oh, ow, e);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      float xv[8];
+      unpack8(X[k], xv);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {  // k_bn_bwd_stats<.., BWD_RELU, ..>'s arithmetic on the stored dz
+        const float xh = (xv[j] - mu[j]) * is[j];
+        float d = rbf16(e[k][j]);
+        const float z = xh * ga[j] + be[j];
+        d = z > 0.f ? d : 0.f;
+        s[j] += d;
+        q[j] = __builtin_fmaf(d, xh, q[j]);
+      }
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < 8; ++j) red[pl][cgl * 8 + j] = float2{s[j], q[j]};
+  __syncthreads();
+  if (threadIdx.x < 64) {
+    float2 a = red[0][threadIdx.x];
+    for (int k = 1; k < 32; ++k) {
+      a.x += red[k][threadIdx.x].x;
+      a.y += red[k][threadIdx.x].y;
+    }
+    part[(long)blockIdx.y * g.C + blockIdx.x * 64 + threadIdx.x] = a;
+  }
+}
+// dx = gamma * invstd * (dz - mean(dz) - xhat * mean(dz * xhat)) over the 2x2 input block of every output pixel
+// (k_bn_bwd_apply's coefficients and FMAs); M = N H W input pixels.
+template <typename IT>
+__global__ void __launch_bounds__(256) k_bn_pool_bwd_apply(const bf16_t* __restrict__ dp, const uint8_t* __restrict__ arg,
+                                                           const bf16_t* __restrict__ x, const float2* __restrict__ stats,
+                                                           const float* __restrict__ gamma,
+                                                           const float* __restrict__ beta,
+                                                           const float2* __restrict__ sums, bf16_t* __restrict__ dx,
+                                                           PoolGeom g) {
+  const IT cgs = (IT)(g.C >> 3), Wo = (IT)g.Wo, Ho = (IT)g.Ho;
+  const IT total = (IT)g.N * Ho * Wo * cgs;
+  const float inv_m = 1.f / (float)((long)g.N * g.H * g.W);
+  for (IT i = (IT)blockIdx.x * 256 + threadIdx.x; i < total; i += (IT)gridDim.x * 256) {
+    const int c = (int)(i % cgs) * 8;
+    const IT p = i / cgs, pr = p / Wo;
+    const int ow = (int)(p - pr * Wo), oh = (int)(pr % Ho), n = (int)(pr / Ho);
+    const IT x00 = (((IT)n * g.H + 2 * oh) * g.W + 2 * ow) * g.C + c, xr = (IT)g.W * g.C;
+    const IT xo[4] = {x00, x00 + g.C, x00 + xr, x00 + xr + g.C};
+    uint4 X[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) X[k] = *(const uint4*)(x + xo[k]);
+    float e[4][8];
+    maxpool_k3s2_block_grad<IT>(dp, arg, g, p, c, oh, ow, e);
+    float mu[8], is[8], ga[8], be[8], ca[8], cb[8], cd[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float2 st = stats[c + j], sm = sums[c + j];
+      mu[j] = st.x;
+      is[j] = st.y;
+      ga[j] = gamma[c + j];
+      be[j] = beta[c + j];
+      ca[j] = ga[j] * is[j];
+      cb[j] = -ca[j] * is[j] * sm.y * inv_m;
+      cd[j] = -ca[j] * sm.x * inv_m - cb[j] * mu[j];
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      float xv[8], d[8];
+      unpack8(X[k], xv);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        float dz = rbf16(e[k][j]);
+        const float z = (xv[j] - mu[j]) * is[j] * ga[j] + be[j];
+        dz = z > 0.f ? dz : 0.f;
+        d[j] = __builtin_fmaf(ca[j], dz, __builtin_fmaf(cb[j], xv[j], cd[j]));
+      }
+      *(uint4*)(dx + xo[k]) = pack8(d);
+    }
   }
 }
 

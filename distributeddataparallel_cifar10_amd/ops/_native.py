@@ -13,7 +13,7 @@ import torch
 
 from .. import build as _build
 
-ABI_VERSION = 11
+ABI_VERSION = 12
 _lock = threading.Lock()
 _lib = None
 
@@ -75,6 +75,11 @@ def _declare(lib):
                                    c_void_p, c_void_p, c_void_p]
     lib.dca_ops_maxpool_fwd.argtypes = [c_void_p, c_void_p, c_void_p, P(PoolGeom), c_void_p]
     lib.dca_ops_maxpool_bwd.argtypes = [c_void_p, c_void_p, c_void_p, P(PoolGeom), c_void_p]
+    lib.dca_ops_bn_pool_fwd_parts.argtypes = [c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p,
+                                              c_void_p, c_float, c_float, c_void_p, c_void_p, P(PoolGeom), c_void_p,
+                                              c_void_p]
+    lib.dca_ops_bn_pool_bwd.argtypes = [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                                        c_void_p, c_void_p, c_void_p, c_void_p, c_int, P(PoolGeom), c_void_p, c_void_p]
     lib.dca_ops_avgpool_fwd.argtypes = [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p]
     lib.dca_ops_avgpool_bwd.argtypes = [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p]
     lib.dca_ops_cross_entropy.argtypes = [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_float, c_void_p,

@@ -747,7 +747,7 @@ class _ConvBNAct(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, w, r, gamma, beta, running_mean, running_var, stride, pad, eps, momentum, relu, res_mode, fp8,
-                fp8_state, emit, packed, sinks, x_join, r_join, res_in):
+                fp8_state, emit, packed, sinks, x_join, r_join, res_in, pool):
         ctx.res_in = res_in
         if res_in is not None:  # the consumer may hand this output's gradient over res_in instead of autograd
             ctx.set_materialize_grads(False)
@@ -760,9 +760,27 @@ class _ConvBNAct(torch.autograd.Function):
         y, st = _conv_fwd(x, wg, None, stride, pad, False, fp8, col_stats=part, shift=running_mean,
                           fp8_state=fp8_state, packed=packed)
         st["w_master"] = w.detach()
+        stats = torch.empty(co, 2, dtype=torch.float32, device=x.device)
+        ctx.st = st
+        ctx.wshape = tuple(w.shape)
+        ctx.sinks = sinks
+        ctx.joins = (x_join, r_join)
+        ctx.relu, ctx.res_mode = relu, res_mode
+        ctx.pool = None
+        if pool:  # ReLU(bn(y)) -> 3x3/2/1 max pool in one pass: the activation itself is never written
+            pg = _pool_geom(y, 3, 2, 1)
+            out = torch.empty(pg.N, pg.Ho, pg.Wo, co, dtype=torch.bfloat16, device=x.device)
+            arg = torch.empty(pg.N, pg.Ho, pg.Wo, co, dtype=torch.uint8, device=x.device)
+            N.check(N.lib().dca_ops_bn_pool_fwd_parts(N.ptr(y), N.ptr(part), nparts, N.ptr(stats), N.ptr(gamma),
+                                                      N.ptr(beta), N.ptr(running_mean), N.ptr(running_var),
+                                                      float(eps), float(momentum), N.ptr(out), N.ptr(arg), pg,
+                                                      N.ptr(_ticket(x.device, (co + 63) // 64)), N.stream(x.device)),
+                    "bn_pool_fwd_parts")
+            ctx.pool = pg
+            ctx.save_for_backward(y, None, gamma, beta, stats, arg)
+            return out
         r = r.contiguous() if r is not None else None
         out = torch.empty_like(y)
-        stats = torch.empty(co, 2, dtype=torch.float32, device=x.device)
         q = None
         if emit is not None and emit.ready:  # fp8 copy of the output for the next (fp8) GEMM, delayed scaling
             q = torch.empty(out.shape, dtype=torch.uint8, device=x.device)
@@ -777,12 +795,7 @@ class _ConvBNAct(torch.autograd.Function):
                 "bn_fwd_parts")
         if q is not None:
             emit.q, emit.src_ptr = q, out.data_ptr()
-        ctx.st = st
-        ctx.wshape = tuple(w.shape)
-        ctx.sinks = sinks
-        ctx.joins = (x_join, r_join)
         ctx.save_for_backward(y, r if mask is None else None, gamma, beta, stats, mask)
-        ctx.relu, ctx.res_mode = relu, res_mode
         return out
 
     @staticmethod
@@ -793,7 +806,7 @@ class _ConvBNAct(torch.autograd.Function):
             rl = ctx.res_in
             if rl is None or rl.dout is None:
                 ctx.st = ctx.sinks = ctx.joins = ctx.res_in = None
-                return (None,) * 21
+                return (None,) * 22
             dout, in_mask, rl.dout, rl.mask = rl.dout, rl.mask, None, None
         if _BWD_TRACE is not None:
             _BWD_TRACE.append((tuple(y.shape), in_mask is not None))
@@ -803,10 +816,17 @@ class _ConvBNAct(torch.autograd.Function):
         defer = (not res_link and r_join is not None and mask is not None and r_join.defer_ok
                  and ctx.res_mode == 2)
         dout = dout.to(torch.bfloat16).contiguous()
-        dy_conv, dr, dgamma, dbeta = _bn_backward(dout, y, r, gamma, beta, stats, ctx.relu, ctx.res_mode,
-                                                  dgamma_out=sg[0] if sg else None, dbeta_out=sb[0] if sb else None,
-                                                  mask=mask if in_mask is None else in_mask,
-                                                  want_dr=not (defer or res_link))
+        if ctx.pool is not None:  # dout is the pooled gradient; `mask` holds the pool's argmax bytes
+            dy_conv, dgamma, dbeta = _bn_pool_backward(dout, mask, y, gamma, beta, stats, ctx.pool,
+                                                       dgamma_out=sg[0] if sg else None,
+                                                       dbeta_out=sb[0] if sb else None)
+            dr = None
+        else:
+            dy_conv, dr, dgamma, dbeta = _bn_backward(dout, y, r, gamma, beta, stats, ctx.relu, ctx.res_mode,
+                                                      dgamma_out=sg[0] if sg else None,
+                                                      dbeta_out=sb[0] if sb else None,
+                                                      mask=mask if in_mask is None else in_mask,
+                                                      want_dr=not (defer or res_link))
         if sg:
             sg[1]()
             sb[1]()
@@ -834,13 +854,13 @@ class _ConvBNAct(torch.autograd.Function):
             sw[1]()
         ctx.st = ctx.sinks = ctx.joins = ctx.res_in = None
         return (dx, dw, dr, dgamma, dbeta, None, None, None, None, None, None, None, None, None, None, None, None, None,
-                None, None, None)
+                None, None, None, None)
 
 
 def conv_bn_act(x, conv: torch.nn.Conv2d, bn: torch.nn.BatchNorm2d, r=None, relu=True, fp8=False, res_mode=None,
                 fp8_state: Optional[Fp8Delayed] = None, emit: Optional[Fp8Delayed] = None, packed=None,
                 direct_grads: bool = False, x_join: Optional[GradJoin] = None, r_join: Optional[GradJoin] = None,
-                res_in: Optional[ResidualLink] = None):
+                res_in: Optional[ResidualLink] = None, pool: bool = False):
     """act(bn(conv(x))) for NHWC bf16 x, conv without bias (BN in eval mode: inference under no_grad, running
     statistics); with a residual r: res_mode 2 (default,
     ResNet: act(bn + r)) or 1 (NetResDeep: act(bn) + r).  fp8: forward GEMM in fp8 e4m3 (fp8_state: this conv's
@@ -848,7 +868,9 @@ def conv_bn_act(x, conv: torch.nn.Conv2d, bn: torch.nn.BatchNorm2d, r=None, relu
     packed: the conv's WeightPack entry.  direct_grads: the conv weight and BN affine parameters are used once
     per step, so their gradients may be written straight into FlatBucketDDP's flat buffer (``grad_sink``).
     x_join / r_join: the input x / the residual r is also consumed elsewhere (GradJoin): its gradient is summed
-    inside the producing kernels instead of by an autograd add.  (Measured and removed in round 5: the BN-backward
+    inside the producing kernels instead of by an autograd add.  pool: follow with the 3x3 / stride 2 / pad 1 max
+    pool (the ResNet stem) in the same pass when ``bn_pool_ok`` (training, ReLU, no residual; else a separate
+    pool): returns the pooled tensor, and neither the activation nor its gradient is ever materialised.  (Measured and removed in round 5: the BN-backward
     statistics in the consumer's dgrad GEMM epilogue, 8,417 vs 8,755 img/s at ResNet-50 batch 256.)"""
     if res_mode is None:
         res_mode = 2 if r is not None else 0
@@ -860,7 +882,8 @@ def conv_bn_act(x, conv: torch.nn.Conv2d, bn: torch.nn.BatchNorm2d, r=None, relu
         with torch.no_grad():
             wg, stride, pad = _s2d_args(conv.weight, conv.stride[0], conv.padding[0], packed)
             y, _ = _conv_fwd(x, wg, None, stride, pad, False, False, packed=packed)
-            return _bn_eval(y, r, bn, relu, res_mode)
+            out = _bn_eval(y, r, bn, relu, res_mode)
+            return max_pool2d(out, 3, 2, 1) if pool else out
     momentum = bn.momentum if bn.track_running_stats else 0.0
     if bn.track_running_stats and not getattr(bn, "_dca_counted", False):
         bn.num_batches_tracked.add_(1)  # (a model that batches these increments marks its BNs _dca_counted)
@@ -869,10 +892,13 @@ def conv_bn_act(x, conv: torch.nn.Conv2d, bn: torch.nn.BatchNorm2d, r=None, relu
         sw, sg, sb = grad_sink(conv.weight), grad_sink(bn.weight), grad_sink(bn.bias)
         if sw is not None and sg is not None and sb is not None:
             sinks = (sw, sg, sb)
-    return _ConvBNAct.apply(x, conv.weight, r, bn.weight, bn.bias, bn.running_mean, bn.running_var, conv.stride[0],
-                            conv.padding[0], bn.eps, momentum, relu, res_mode, fp8, fp8_state, emit, packed, sinks,
-                            x_join if torch.is_grad_enabled() else None, r_join if torch.is_grad_enabled() else None,
-                            res_in if torch.is_grad_enabled() else None)
+    fuse = pool and relu and r is None and res_mode == 0 and emit is None and BN_POOL_FUSED and \
+        bn_pool_ok(x, conv, packed)
+    out = _ConvBNAct.apply(x, conv.weight, r, bn.weight, bn.bias, bn.running_mean, bn.running_var, conv.stride[0],
+                           conv.padding[0], bn.eps, momentum, relu, res_mode, fp8, fp8_state, emit, packed, sinks,
+                           x_join if torch.is_grad_enabled() else None, r_join if torch.is_grad_enabled() else None,
+                           res_in if torch.is_grad_enabled() else None, fuse)
+    return max_pool2d(out, 3, 2, 1) if pool and not fuse else out
 
 
 def conv2d(x, w, b=None, stride=1, pad=0, relu=False, fp8=False):
@@ -934,6 +960,46 @@ def _bn_backward(dy, x, r, gamma, beta, stats, relu, res_mode, dgamma_out=None, 
     if direct:
         return dx, dr, None, None
     return dx, dr, dgamma, dbeta
+
+
+# The ResNet stem's BN + ReLU + max pool in one pass (k_bn_pool_fwd / k_bn_pool_bwd_*); False: BN apply and the
+# pool as two passes each way (A/B comparisons: DCA_OPS_STEM_POOL=0)
+BN_POOL_FUSED = os.environ.get("DCA_OPS_STEM_POOL", "1") != "0"
+
+
+def _pool_geom(x: torch.Tensor, k: int, s: int, p: int):
+    n, h, w, c = x.shape
+    return N.PoolGeom(N=n, H=h, W=w, C=c, K=k, S=s, P=p, Ho=(h + 2 * p - k) // s + 1, Wo=(w + 2 * p - k) // s + 1)
+
+
+def bn_pool_ok(x: torch.Tensor, conv: torch.nn.Conv2d, packed=None) -> bool:
+    """The conv's output can take the fused BN + ReLU + 3x3/2/1 max pool: even H and W (every input pixel in the
+    2x2 block of one output pixel), C % 64 == 0, 32-bit element offsets."""
+    if not x.is_cuda:
+        return False
+    wg, stride, pad = _s2d_args(conv.weight, conv.stride[0], conv.padding[0], packed)
+    g = _geom(x, wg, stride, pad)
+    co = conv.out_channels
+    return (g.Ho % 2 == 0 and g.Wo % 2 == 0 and co % 64 == 0 and
+            g.N * g.Ho * g.Wo * co + 8192 * 256 < 2 ** 31)
+
+
+def _bn_pool_backward(dp, arg, y, gamma, beta, stats, pg, dgamma_out=None, dbeta_out=None):
+    """(dy, dgamma, dbeta) of ReLU(BN(y)) -> max pool from the pooled gradient dp and the argmax bytes; dgamma_out /
+    dbeta_out: flat gradient views accumulated into (then dgamma / dbeta are None)."""
+    C = y.shape[-1]
+    npo = pg.N * pg.Ho * pg.Wo
+    part = torch.empty((npo + 63) // 64, C, 2, dtype=torch.float32, device=y.device)
+    sums = torch.empty(C, 2, dtype=torch.float32, device=y.device)
+    direct = dgamma_out is not None and dbeta_out is not None
+    dgamma = dgamma_out if direct else torch.empty(C, dtype=torch.float32, device=y.device)
+    dbeta = dbeta_out if direct else torch.empty_like(dgamma)
+    dy = torch.empty_like(y)
+    N.check(N.lib().dca_ops_bn_pool_bwd(N.ptr(dp), N.ptr(arg), N.ptr(y), N.ptr(stats), N.ptr(gamma), N.ptr(beta),
+                                        N.ptr(part), N.ptr(sums), N.ptr(dgamma), N.ptr(dbeta), N.ptr(dy), int(direct),
+                                        pg, N.ptr(_ticket(y.device, (C + 63) // 64)), N.stream(y.device)),
+            "bn_pool_bwd")
+    return dy, (None if direct else dgamma), (None if direct else dbeta)
 
 
 def _check_inference(p: torch.Tensor) -> None:

@@ -8,7 +8,7 @@ switches to channels-last bf16 once, and runs:
 * NetResDeep (reference ``model/resnet.py:15-37``): conv1 + bias + ReLU fused in the GEMM epilogue -> 2x2 max
   pool -> 10 x [3x3 conv (im2col + MFMA GEMM) -> BN + ReLU + skip fused (res_mode 1)] -> max pool -> fc1 + ReLU
   -> fc2 (fp32 logits).  fc1's columns are permuted from the reference's NCHW flatten order to NHWC.
-* ResNet-50/101: stem 7x7/2 conv -> BN + ReLU -> 3x3/2 max pool -> bottlenecks (1x1, 3x3, 1x1 convs, each BN
+* ResNet-50/101: stem 7x7/2 conv -> BN + ReLU + 3x3/2 max pool (one fused pass) -> bottlenecks (1x1, 3x3, 1x1 convs, each BN
   fused with its ReLU; the last one with the residual add before the ReLU, res_mode 2) -> global average pool
   -> fc.  The 7x7/2 stem runs as a 4x4 stride-1 conv over a space-to-depth copy of the input (K 256 instead of
   392).  The bf16 (and fp8) GEMM operands of all convolutions are rebuilt from the fp32 weights by one
@@ -133,20 +133,20 @@ class OpsModel(nn.Module):
             self._fp8 = {}
         return self._fp8.setdefault(id(conv), F.Fp8Delayed())
 
-    def _conv_bn(self, h, conv, bn, relu=True, r=None, consumer=None, x_join=None, r_join=None, res_in=None):
+    def _conv_bn(self, h, conv, bn, relu=True, r=None, consumer=None, x_join=None, r_join=None, res_in=None,
+                 pool=False):
         # every ResNet conv / BN is applied once per step: gradients may go straight into the flat DDP buffer
         return F.conv_bn_act(h, conv, bn, r=r, relu=relu, fp8=self._fp8_ok(conv), fp8_state=self._state(conv),
                              emit=self._state(consumer) if consumer is not None else None,
                              packed=self._pack.get(conv), direct_grads=True, x_join=x_join, r_join=r_join,
-                             res_in=res_in)
+                             res_in=res_in, pool=pool)
 
     def stem(self, h, conv, bn):
         """7x7/2 conv -> BN + ReLU -> 3x3/2 max pool (torchvision ResNet stem).  ``h`` is what ``begin`` returned:
         for the space-to-depth stem its [N, Ho + 3, Wo + 3, 16] operand (the conv then runs as 4x4 / 1)."""
         if self._s2d is not None and conv is not self._s2d:
             raise ValueError("OpsModel.stem: begin() prepared the space-to-depth input of this model's first conv")
-        h = self._conv_bn(h, conv, bn)
-        return F.max_pool2d(h, 3, 2, 1)
+        return self._conv_bn(h, conv, bn, pool=True)  # BN + ReLU + pool in one pass each way (F.bn_pool_ok)
 
     def blocks(self, h, blocks):
         """Bottleneck blocks in sequence over NHWC bf16 ``h``."""

@@ -798,6 +798,52 @@ def test_ops_resnet_counts_batches_once_per_forward(gpu):
     assert counts == {3}, counts
 
 
+@pytest.mark.parametrize("n,h,ci,co", [(6, 64, 64, 64), (3, 30, 64, 128)])
+def test_bn_pool_fused_matches_two_pass(gpu, n, h, ci, co):
+    """conv -> BN + ReLU + 3x3/2/1 max pool in one pass each way (the ResNet stem, k_bn_pool_*) against the
+    two-pass form (k_bn_apply + k_maxpool_fwd_k3s2, k_maxpool_bwd_k3s2 + the BN backward): forward output and argmax
+    bitwise, BN running statistics bitwise, gradients to the summation order of the BN backward sums; and both
+    against torch fp32."""
+    import copy
+    from distributeddataparallel_cifar10_amd.ops import conv_bn_act, max_pool2d
+    from distributeddataparallel_cifar10_amd.ops import functional as F
+    g = torch.Generator(device=gpu).manual_seed(n * h + co)
+    conv = torch.nn.Conv2d(ci, co, 3, padding=1, bias=False).to(gpu)
+    bn = torch.nn.BatchNorm2d(co).to(gpu)
+    with torch.no_grad():
+        bn.weight.uniform_(0.5, 1.5, generator=g)
+        bn.bias.uniform_(-0.5, 0.5, generator=g)
+    conv2, bn2 = copy.deepcopy(conv), copy.deepcopy(bn)
+    x = _bf(torch.randn(n, h, h, ci, device=gpu, generator=g))
+    x1, x2 = x.clone().requires_grad_(), x.clone().requires_grad_()
+    assert F.bn_pool_ok(x1, conv)
+    y1 = conv_bn_act(x1, conv, bn, relu=True, pool=True)
+    y2 = max_pool2d(conv_bn_act(x2, conv2, bn2, relu=True), 3, 2, 1)
+    assert y1.shape == (n, h // 2, h // 2, co) and torch.equal(y1, y2)
+    assert torch.equal(bn.running_mean, bn2.running_mean) and torch.equal(bn.running_var, bn2.running_var)
+    dp = _bf(torch.randn(y1.shape, device=gpu, generator=g))
+    y1.backward(dp)
+    y2.backward(dp)
+    assert _rel(bn.weight.grad, bn2.weight.grad) < 1e-5 and _rel(bn.bias.grad, bn2.bias.grad) < 1e-5
+    assert _rel(conv.weight.grad, conv2.weight.grad) < 1e-3
+    assert _rel(x1.grad.float(), x2.grad.float()) < 1e-2
+    # torch fp32 reference of the same module chain
+    rc, rb = copy.deepcopy(conv2), torch.nn.BatchNorm2d(co).to(gpu)
+    rb.load_state_dict({k: v for k, v in bn.state_dict().items() if k not in ("running_mean", "running_var")},
+                       strict=False)
+    rc.weight.grad = rb.weight.grad = None
+    xr = x.float().permute(0, 3, 1, 2).requires_grad_()
+    z = TF.max_pool2d(torch.relu(rb(torch.nn.functional.conv2d(xr, _bf(rc.weight).float(), padding=1))), 3, 2, 1)
+    z.backward(dp.float().permute(0, 3, 1, 2))
+    assert _rel(y1.float().permute(0, 3, 1, 2), z) < 2e-2
+    assert _rel(bn.weight.grad, rb.weight.grad) < 2e-2 and _rel(bn.bias.grad, rb.bias.grad) < 2e-2
+    # the input gradient runs through the BN backward's cancellation in bf16 (dz - mean - xhat * mean(dz xhat)):
+    # the fused form must be as close to fp32 as the two-pass form
+    e1 = _rel(x1.grad.float().permute(0, 3, 1, 2), xr.grad)
+    e2 = _rel(x2.grad.float().permute(0, 3, 1, 2), xr.grad)
+    assert e1 < 1.05 * e2 + 1e-3 and e1 < 0.15, (e1, e2)
+
+
 def test_strided_1x1_conv_on_stream_kernel(gpu):
     """A strided 1x1 (downsample) convolution with N % 128 == 0 and M >= 16384 -- the production route onto the
     persistent stream kernel's implicit-conv form -- with the fused BN column statistics, vs torch fp32."""
