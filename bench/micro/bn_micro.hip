@@ -292,7 +292,7 @@ static void run_shape(const Bufs& B, long M, int C, bool bn3) {
   cells.push_back({"apply", "prod", e * (bn3 ? 6 : 4) + (bn3 ? e / 8 : 0), [=] {
     hipLaunchKernelGGL((k_bn_apply<CL>), g, b, 0, 0, B.a, bn3 ? B.b : nullptr, B.c, B.stats, B.gamma, B.beta, M, C, 1,
                        bn3 ? 2 : 0, (uint8_t*)nullptr, (const float*)nullptr, (unsigned*)nullptr,
-                       bn3 ? B.mk : nullptr);
+                       bn3 ? B.mk : nullptr, BnRes{});
   }});
   add_variants<CL, 256, 4, false>(cells, B, M, C, bn3, "r256u4");
   add_variants<CL, 256, 4, true>(cells, B, M, C, bn3, "r256u4nt");

@@ -164,7 +164,7 @@ using namespace dca::ops;
 extern "C" {
 
 const char* dca_ops_last_error() { return g_err.c_str(); }
-int dca_ops_abi_version() { return 12; }
+int dca_ops_abi_version() { return 13; }
 
 // Must match ops/_native.py::GemmArgs.
 int dca_ops_gemm(const GemmArgs* a, void* stream) {
@@ -548,7 +548,7 @@ int dca_ops_bn_fwd(const void* x, const void* r, void* out, float* part, float* 
   bn_fin_launch<0>(part, nparts, M, C, rm, rv, stats, eps, momentum, 0, ticket, st);
   bn_apply_launch(M, C, st, (const bf16_t*)x, (const bf16_t*)r,
                      (bf16_t*)out, (const float2*)stats, gamma, beta, M, C, relu, res_mode, (uint8_t*)nullptr,
-                     (const float*)nullptr, (unsigned*)nullptr, (uint8_t*)nullptr);
+                     (const float*)nullptr, (unsigned*)nullptr, (uint8_t*)nullptr, BnRes{});
   OPCK(hipGetLastError());
   return 0;
 }
@@ -558,20 +558,26 @@ int dca_ops_bn_fwd(const void* x, const void* r, void* out, float* part, float* 
 // q / amax_prev / amax_out (optional): also write an fp8 copy of the output with delayed scaling (k_bn_apply);
 // amax_out is zeroed here first.
 // mask (optional, res_mode 2 + ReLU): [M C / 8] bytes, the ReLU mask for dca_ops_bn_bwd.
+// out == nullptr: statistics only (a BN whose consumer applies it on the fly, BnRes).  rstats / rgamma / rbeta
+// (optional, res_mode 2): r is the raw input of another training BN with these statistics, applied on the fly.
 int dca_ops_bn_fwd_parts(const void* x, const void* r, void* out, float* part, int nparts, float* stats,
                          const float* gamma, const float* beta, float* rm, float* rv, long M, int C, float eps,
                          float momentum, int relu, int res_mode, void* q, const float* amax_prev, unsigned* amax_out,
-                         void* mask, unsigned* ticket, void* stream) {
+                         void* mask, const float* rstats, const float* rgamma, const float* rbeta, unsigned* ticket,
+                         void* stream) {
   REQUIRE(C % 8 == 0, "bn: C must be a multiple of 8");
   REQUIRE(res_mode == 0 || r != nullptr, "bn: residual missing");
   REQUIRE(!q || (amax_prev && amax_out), "bn: fp8 output needs amax_prev and amax_out");
   REQUIRE(!mask || (relu && res_mode == 2), "bn: the stored mask is for ReLU(bn + r)");
   hipStream_t st = (hipStream_t)stream;
+  REQUIRE(!rstats || (res_mode == 2 && rgamma && rbeta), "bn: an on-the-fly residual BN needs res_mode 2");
+  REQUIRE(out || (!q && !mask), "bn: statistics only: no fp8 copy / mask");
   if (q) OPCK(hipMemsetAsync(amax_out, 0, sizeof(unsigned), st));
   bn_fin_launch<0>(part, nparts, M, C, rm, rv, stats, eps, momentum, 0, ticket, st);
-  bn_apply_launch(M, C, st, (const bf16_t*)x, (const bf16_t*)r,
-                     (bf16_t*)out, (const float2*)stats, gamma, beta, M, C, relu, res_mode, (uint8_t*)q, amax_prev,
-                     amax_out, (uint8_t*)mask);
+  if (out)
+    bn_apply_launch(M, C, st, (const bf16_t*)x, (const bf16_t*)r,
+                    (bf16_t*)out, (const float2*)stats, gamma, beta, M, C, relu, res_mode, (uint8_t*)q, amax_prev,
+                    amax_out, (uint8_t*)mask, BnRes{(const float2*)rstats, rgamma, rbeta});
   OPCK(hipGetLastError());
   return 0;
 }
@@ -586,7 +592,7 @@ int dca_ops_bn_eval(const void* x, const void* r, void* out, float* stats, const
   hipLaunchKernelGGL(k_bn_eval_stats, dim3((C + 255) / 256), dim3(256), 0, st, rm, rv, (float2*)stats, C, eps);
   bn_apply_launch(M, C, st, (const bf16_t*)x, (const bf16_t*)r,
                      (bf16_t*)out, (const float2*)stats, gamma, beta, M, C, relu, res_mode, (uint8_t*)nullptr,
-                     (const float*)nullptr, (unsigned*)nullptr, (uint8_t*)nullptr);
+                     (const float*)nullptr, (unsigned*)nullptr, (uint8_t*)nullptr, BnRes{});
   OPCK(hipGetLastError());
   return 0;
 }

@@ -262,6 +262,16 @@ __global__ void __launch_bounds__(256) k_bn_eval_stats(const float* __restrict__
   if (c < C) stats[c] = float2{running_mean[c], rsqrtf(running_var[c] + eps)};
 }
 
+// A residual that is itself a training BatchNorm output, applied on the fly (res_mode 2): r' = r * rsc + rsh per
+// channel from its own batch statistics, so the ResNet downsample branch's BN never writes its output (the branch
+// returns its conv output y and this pass reads that instead of the BN'd copy: one full pass over a 4x-width
+// tensor per downsample block saved).  stats == nullptr: r is used as it is.
+struct BnRes {
+  const float2* stats;
+  const float* gamma;
+  const float* beta;
+};
+
 // out = fused(x); vectorised by 8 channels (C % 8 == 0)
 // Optionally also emits an fp8 e4m3 copy of the output for an fp8 consumer GEMM, with DELAYED scaling: the scale
 // 448 / amax comes from the previous step's amax of this tensor (amax_prev), and this step's amax is recorded in
@@ -272,7 +282,7 @@ __global__ void __launch_bounds__(256) k_bn_apply(const bf16_t* __restrict__ x, 
                                                   const float* __restrict__ gamma, const float* __restrict__ beta,
                                                   long M, int C, int relu, int res_mode, uint8_t* __restrict__ q,
                                                   const float* __restrict__ amax_prev, unsigned* __restrict__ amax_out,
-                                                  uint8_t* __restrict__ mk) {
+                                                  uint8_t* __restrict__ mk, BnRes rb) {
   // grid (ceil(C/(8 CL)), ceil(M/ROWS)): CL channel groups of 8 x 256/CL row lanes, z = x * sc + sh per channel
   __shared__ float red[256];
   const int cgl = threadIdx.x % CL, rl = threadIdx.x / CL, c0 = blockIdx.x * (8 * CL) + cgl * 8;
@@ -280,12 +290,18 @@ __global__ void __launch_bounds__(256) k_bn_apply(const bf16_t* __restrict__ x, 
   float qs = 1.f, amax = 0.f;
   if (q) qs = *amax_prev > 0.f ? 448.f / *amax_prev : 1.f;
   if (c0 < C) {
-    float sc[8], sh[8];
+    float sc[8], sh[8], rsc[8], rsh[8];
+    const bool raff = rb.stats != nullptr;
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       const float2 st = stats[c0 + j];
       sc[j] = st.y * gamma[c0 + j];
       sh[j] = beta[c0 + j] - st.x * sc[j];
+      if (raff) {
+        const float2 rs = rb.stats[c0 + j];
+        rsc[j] = rs.y * rb.gamma[c0 + j];
+        rsh[j] = rb.beta[c0 + j] - rs.x * rsc[j];
+      }
     }
     const long rend = M < r0 + ROWS ? M : r0 + ROWS;
     for (long base = r0 + rl; base < rend; base += (256 / CL) * BN_U) {
@@ -304,6 +320,10 @@ __global__ void __launch_bounds__(256) k_bn_apply(const bf16_t* __restrict__ x, 
       float v[8], rv[8];
       unpack8(X[u], v);
       if (res_mode) unpack8(R[u], rv);
+      if (raff) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) rv[j] = rv[j] * rsc[j] + rsh[j];
+      }
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         float z = v[j] * sc[j] + sh[j];

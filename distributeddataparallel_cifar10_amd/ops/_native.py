@@ -13,7 +13,7 @@ import torch
 
 from .. import build as _build
 
-ABI_VERSION = 12
+ABI_VERSION = 13
 _lock = threading.Lock()
 _lib = None
 
@@ -67,7 +67,8 @@ def _declare(lib):
                                    c_void_p, c_long, c_int, c_float, c_float, c_int, c_int, c_void_p, c_void_p]
     lib.dca_ops_bn_fwd_parts.argtypes = [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_void_p,
                                          c_void_p, c_void_p, c_long, c_int, c_float, c_float, c_int, c_int, c_void_p,
-                                         c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]
+                                         c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                                         c_void_p]
     lib.dca_ops_bn_eval.argtypes = [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                                     c_long, c_int, c_float, c_int, c_int, c_void_p]
     lib.dca_ops_bn_bwd.argtypes = [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,

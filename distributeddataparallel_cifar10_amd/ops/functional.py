@@ -540,14 +540,23 @@ class GradJoin:
         return self.buf if self.left == 0 else None
 
 
+# The downsample branch's BN applied on the fly by bn3's apply pass (ResidualLink.lazy); False: the branch writes
+# its BN output and bn3 reads it (A/B comparisons: DCA_OPS_RES_BN=0)
+RES_BN_ON_THE_FLY = os.environ.get("DCA_OPS_RES_BN", "1") != "0"
+
+
 class ResidualLink:
     """ReLU(bn3 + r) of a downsample bottleneck -> the downsample branch that produced r.  bn3's backward leaves
     (dout, its forward ReLU bit mask) here and returns no gradient for r, so dL/dr = dout * mask is never written;
     the downsample BN's backward (called by autograd with no gradient: its forward disables grad materialisation)
-    reads dout and the mask instead (k_bn_bwd_* in BWD_MASK mode)."""
+    reads dout and the mask instead (k_bn_bwd_* in BWD_MASK mode).  Forward: the branch's BN only finalises its
+    statistics and hands (its conv output, statistics, gamma, beta) over ``lazy``; bn3's apply pass normalises the
+    residual on the fly, so the branch's BN output is never written."""
 
     def __init__(self):
         self.dout = self.mask = None
+        # forward: (conv output data_ptr, stats, gamma, beta) of the branch's BN, applied by bn3 on the fly
+        self.lazy = None
 
 
 class Fp8Delayed:
@@ -780,10 +789,17 @@ class _ConvBNAct(torch.autograd.Function):
             ctx.save_for_backward(y, None, gamma, beta, stats, arg)
             return out
         r = r.contiguous() if r is not None else None
-        out = torch.empty_like(y)
+        # the downsample branch of a bottleneck (its output is only bn3's residual, over a ResidualLink): statistics
+        # only, the conv output y is returned and bn3's apply normalises it on the fly (k_bn_apply BnRes)
+        lazy = (RES_BN_ON_THE_FLY and isinstance(res_in, ResidualLink) and not relu and res_mode == 0 and r is None
+                and emit is None)
+        # bn3 of that block: its residual r is such a raw conv output
+        rl = (r_join.lazy if isinstance(r_join, ResidualLink) and r_join.lazy is not None and r is not None and
+              r_join.lazy[0] == r.data_ptr() and res_mode == 2 else None)
+        out = None if lazy else torch.empty_like(y)
         q = None
         if emit is not None and emit.ready:  # fp8 copy of the output for the next (fp8) GEMM, delayed scaling
-            q = torch.empty(out.shape, dtype=torch.uint8, device=x.device)
+            q = torch.empty(y.shape, dtype=torch.uint8, device=x.device)
         # ReLU(bn + r): the forward stores the ReLU mask as bits, so the backward reads M*C/8 bytes instead of r
         mask = torch.empty(M * co // 8, dtype=torch.uint8, device=x.device) if relu and res_mode == 2 else None
         N.check(N.lib().dca_ops_bn_fwd_parts(N.ptr(y), N.ptr(r), N.ptr(out), N.ptr(part), nparts, N.ptr(stats),
@@ -791,11 +807,17 @@ class _ConvBNAct(torch.autograd.Function):
                                              float(eps), float(momentum), int(relu), int(res_mode), N.ptr(q),
                                              N.ptr(emit.amax_prev) if q is not None else None,
                                              N.ptr(emit.amax_out) if q is not None else None, N.ptr(mask),
+                                             *((N.ptr(t) for t in rl[1:]) if rl is not None else (None,) * 3),
                                              N.ptr(_ticket(x.device, (co + 63) // 64)), N.stream(x.device)),
                 "bn_fwd_parts")
         if q is not None:
             emit.q, emit.src_ptr = q, out.data_ptr()
+        if rl is not None:
+            r_join.lazy = None
         ctx.save_for_backward(y, r if mask is None else None, gamma, beta, stats, mask)
+        if lazy:
+            res_in.lazy = (y.data_ptr(), stats, gamma, beta)
+            return y
         return out
 
     @staticmethod
