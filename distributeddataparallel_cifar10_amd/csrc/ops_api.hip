@@ -4,6 +4,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <tuple>
 #include <cstring>
 #include <string>
 #include <cstdlib>
@@ -123,15 +124,23 @@ void bn_bwd_apply_launch(int mode, bool fine, long M, int C, hipStream_t st, A..
   }
 #undef BAP
 }
+template <bool RAFF, typename... A>
+void bn_apply_launch_t(long M, int C, hipStream_t st, A... a) {
+  if (C % 128 != 0) {
+    hipLaunchKernelGGL((k_bn_apply<8, BN_ROWS, false, RAFF>), dim3((C + 63) / 64, nparts_rows(M)), dim3(256), 0, st, a...);
+  } else if (bn_nt(M, C)) {
+    hipLaunchKernelGGL((k_bn_apply<16, 128, true, RAFF>), dim3(C / 128, (unsigned)((M + 127) / 128)), dim3(256), 0, st,
+                       a...);
+  } else {
+    hipLaunchKernelGGL((k_bn_apply<16, BN_ROWS, false, RAFF>), dim3(C / 128, nparts_rows(M)), dim3(256), 0, st, a...);
+  }
+}
+// (the residual's on-the-fly BN -- the last argument, BnRes -- selects its own instantiation)
 template <typename... A>
 void bn_apply_launch(long M, int C, hipStream_t st, A... a) {
-  if (C % 128 != 0) {
-    hipLaunchKernelGGL((k_bn_apply<8>), dim3((C + 63) / 64, nparts_rows(M)), dim3(256), 0, st, a...);
-  } else if (bn_nt(M, C)) {
-    hipLaunchKernelGGL((k_bn_apply<16, 128, true>), dim3(C / 128, (unsigned)((M + 127) / 128)), dim3(256), 0, st, a...);
-  } else {
-    hipLaunchKernelGGL((k_bn_apply<16>), dim3(C / 128, nparts_rows(M)), dim3(256), 0, st, a...);
-  }
+  const BnRes rb = std::get<sizeof...(A) - 1>(std::tuple<A...>(a...));
+  if (rb.stats) bn_apply_launch_t<true>(M, C, st, a...);
+  else bn_apply_launch_t<false>(M, C, st, a...);
 }
 // BN partial-row reduction (MODE 0 forward statistics, MODE 1 backward sums): with ticket words (ceil(C / 64), zero)
 // the coalesced ticketed kernel (k_bn_fin_ticket; the partial rows are overwritten), else the per-channel one

@@ -276,7 +276,7 @@ struct BnRes {
 // Optionally also emits an fp8 e4m3 copy of the output for an fp8 consumer GEMM, with DELAYED scaling: the scale
 // 448 / amax comes from the previous step's amax of this tensor (amax_prev), and this step's amax is recorded in
 // amax_out for the next step -- no extra pass over the activation, no host sync.
-template <int CL, int ROWS = BN_ROWS, bool NT = false>
+template <int CL, int ROWS = BN_ROWS, bool NT = false, bool RAFF = false>
 __global__ void __launch_bounds__(256) k_bn_apply(const bf16_t* __restrict__ x, const bf16_t* __restrict__ r,
                                                   bf16_t* __restrict__ out, const float2* __restrict__ stats,
                                                   const float* __restrict__ gamma, const float* __restrict__ beta,
@@ -291,13 +291,12 @@ __global__ void __launch_bounds__(256) k_bn_apply(const bf16_t* __restrict__ x, 
   if (q) qs = *amax_prev > 0.f ? 448.f / *amax_prev : 1.f;
   if (c0 < C) {
     float sc[8], sh[8], rsc[8], rsh[8];
-    const bool raff = rb.stats != nullptr;
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       const float2 st = stats[c0 + j];
       sc[j] = st.y * gamma[c0 + j];
       sh[j] = beta[c0 + j] - st.x * sc[j];
-      if (raff) {
+      if constexpr (RAFF) {  // (its own instantiation: the plain passes keep their registers and schedule)
         const float2 rs = rb.stats[c0 + j];
         rsc[j] = rs.y * rb.gamma[c0 + j];
         rsh[j] = rb.beta[c0 + j] - rs.x * rsc[j];
@@ -320,7 +319,7 @@ __global__ void __launch_bounds__(256) k_bn_apply(const bf16_t* __restrict__ x, 
       float v[8], rv[8];
       unpack8(X[u], v);
       if (res_mode) unpack8(R[u], rv);
-      if (raff) {
+      if constexpr (RAFF) {
 #pragma unroll
         for (int j = 0; j < 8; ++j) rv[j] = rv[j] * rsc[j] + rsh[j];
       }
