@@ -63,6 +63,13 @@ inline int getenv_pp4() {  // A/B knob: DCA_OPS_PP4=0 keeps the two-buffer k_gem
   }();
   return v;
 }
+inline int getenv_conv_rows() {  // A/B knob: DCA_OPS_CONV_ROWS=0 keeps the 64-channel 3x3 convs on k_direct_conv
+  static const int v = [] {
+    const char* e = getenv("DCA_OPS_CONV_ROWS");
+    return e ? atoi(e) : 1;
+  }();
+  return v;
+}
 inline int getenv_stream() {  // persistent short-K GEMM (k_gemm_stream): DCA_OPS_STREAM = 0 never, 1 whenever
   static const int v = [] {    // eligible, 2 (default) by the shape rule at the launch site
     const char* e = getenv("DCA_OPS_STREAM");
@@ -361,7 +368,17 @@ int dca_ops_gemm(const GemmArgs* a, void* stream) {
     const long blocks = (g.M + GBM - 1) / GBM;
     long grid = std::min<long>(2L * ncu_s, (blocks + 7) / 8 * 8);
     grid = std::max<long>(8, grid / 8 * 8);
-    if (dc_stem) {
+    if (dc_3x3 && g.cW <= 64 && getenv_conv_rows()) {  // row-ring form (k_conv3x3_rows): the layer-1 shapes
+      long cg = std::min<long>(3L * ncu_s, (long)g.cN * g.cH);
+      if (g.col_stats) cg = std::min<long>(cg, blocks);  // one statistics row per workgroup
+      const dim3 cgd((unsigned)cg), cb(CR_NT);
+      switch ((g.cW + 15) >> 4) {
+        case 1: hipLaunchKernelGGL(k_conv3x3_rows<1>, cgd, cb, CR_LDS, st, g); break;
+        case 2: hipLaunchKernelGGL(k_conv3x3_rows<2>, cgd, cb, CR_LDS, st, g); break;
+        case 3: hipLaunchKernelGGL(k_conv3x3_rows<3>, cgd, cb, CR_LDS, st, g); break;
+        default: hipLaunchKernelGGL(k_conv3x3_rows<4>, cgd, cb, CR_LDS, st, g); break;
+      }
+    } else if (dc_stem) {
       constexpr int lds = DirectConv<16, 4, 4>::LDS;
       hipLaunchKernelGGL((k_direct_conv<16, 4, 4>), dim3((unsigned)grid), dim3(DC_NT), lds, st, g);
     } else {

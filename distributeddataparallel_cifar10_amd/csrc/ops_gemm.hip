@@ -1852,6 +1852,163 @@ __global__ void __launch_bounds__(DC_NT, 2) k_direct_conv(GemmArgs g) {
   }
 }
 
+// ---------------------------------------------------------------------------------------------------------
+// k_conv3x3_rows: the 64-channel 3 x 3 / pad 1 / stride 1 convolutions on rows of at most 64 pixels (ResNet-50's
+// layer 1 at 56 x 56: forward and input gradient).  k_direct_conv<64, 3, 3> loads each output pixel's 576 k straight
+// from global memory into MFMA registers: every input pixel is fetched 9 times and each wave-load touches 64
+// separate 16-B pieces, so its vector L1 makes one access per lane (PMC: 63.5 M L1 accesses per call, ~0.85 per
+// cycle and CU over the kernel, MFMA busy 0.19; profiles/conv3x3_rows_r9.txt).  Here a workgroup walks consecutive
+// output rows (n, oh) and keeps their input rows in an LDS ring:
+//   * 4 row slots of 66 pixels x 128 B (pixel iw at slot position iw + 1; position 0 and those past W stay zero),
+//     16-B chunks XOR-swizzled by position & 7 (one ds_read_b128 lane group = 16 pixels of one chunk covers the 64
+//     banks once); each input row is fetched once per workgroup with coalesced 16-B loads, issued one output row
+//     ahead and written to its slot after that row's MFMAs (slot (r + 2) & 3 held row r - 2, no longer read);
+//   * wave w owns output channels 16 w .. 16 w + 15: its 16 x 576 weight fragment (18 K-slices) stays in 72 VGPRs
+//     for the kernel's life, and per slice it reads the row's 16-pixel A fragments from LDS (one ds_read_b128 per
+//     MFMA).  The taps of a padding row (oh = 0 / H - 1) are skipped, uniformly per row;
+//   * epilogue: alpha, bias, bf16 into a double-buffered LDS output image (64 pixels x 128 B), stored as whole
+//     128-B pixel rows after the row's barrier (one barrier per output row); the BN column statistics (sum, sumsq
+//     of out - shift) stay in registers over the workgroup's rows and are written once, row v of col_stats for
+//     workgroup v, with the rows from grid to nblk - 1 zeroed (k_bn_finalize sums every row).
+// Requirements (launcher): those of k_direct_conv<64, 3, 3>, W <= 64, grid <= nblk when col_stats.
+// ---------------------------------------------------------------------------------------------------------
+constexpr int CR_NT = 256, CR_SLOT = 66 * 128, CR_OUT = 64 * 128;
+constexpr int CR_LDS = 4 * CR_SLOT + 2 * CR_OUT;
+__device__ __forceinline__ int cr_off(int px, int chunk) { return px * 128 + ((chunk ^ (px & 7)) << 4); }
+
+template <int NF>  // 16-pixel fragments per row: ceil(W / 16)
+__global__ void __launch_bounds__(CR_NT, 3) k_conv3x3_rows(GemmArgs g) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  typedef unsigned v4u_ __attribute__((ext_vector_type(4)));
+  constexpr unsigned OOB = 0x80000000u;
+  const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), j = lane & 15, q = lane >> 4;
+  const int H = g.cH, W = g.cW, R = g.cN * g.cH;  // output rows (n, oh); stride 1 / pad 1: input rows alike
+  const int grid = gridDim.x;
+  // XCD-contiguous row ranges: the workgroups of one XCD take neighbouring ranges (shared boundary rows in its L2)
+  const int vid = (grid & 7) == 0 ? (int)(blockIdx.x & 7) * (grid >> 3) + (int)(blockIdx.x >> 3) : (int)blockIdx.x;
+  const int r_beg = (int)((long long)vid * R / grid), r_end = (int)((long long)(vid + 1) * R / grid);
+  for (int e = threadIdx.x; e < 4 * CR_SLOT / 16; e += CR_NT) *(v4u_*)(smem + e * 16) = v4u_{0u, 0u, 0u, 0u};
+  // weights: lane (q, j) of slice s holds channel 16 w + j, k = 32 s + 8 q .. + 7 (k = tap * 64 + c)
+  const unsigned short* Bp = (const unsigned short*)g.B;
+  s16x8 wf[18];
+#pragma unroll
+  for (int s = 0; s < 18; ++s) wf[s] = *(const s16x8*)(Bp + (size_t)(16 * w + j) * g.ldb + 32 * s + 8 * q);
+  const float alpha = gemm_alpha(g);
+  float bias[4], shift[4], s1[4], sq[4];
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    const int c = 16 * w + 4 * q + e;
+    bias[e] = g.bias ? g.bias[c] : 0.f;
+    shift[e] = g.col_stats ? g.stats_shift[c] : 0.f;
+    s1[e] = sq[e] = 0.f;
+  }
+  const __amdgpu_buffer_rsrc_t xrs =
+      __builtin_amdgcn_make_buffer_rsrc((void*)g.A, (short)0, (int)((long long)R * W * 128), 0x00020000);
+  const __amdgpu_buffer_rsrc_t crs =
+      __builtin_amdgcn_make_buffer_rsrc(g.C, (short)0, (int)((long long)g.M * g.ldc * 2), 0x00020000);
+  // input row gr: W * 8 pieces of 16 B (pixel e >> 3, chunk e & 7), two per thread
+  auto row_load = [&](v4u_(&st)[2], int gr) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int e = threadIdx.x + CR_NT * i;
+      const unsigned o = (gr >= 0 && gr < R && e < W * 8) ? (unsigned)gr * (unsigned)W * 128u + (unsigned)e * 16u : OOB;
+      st[i] = __builtin_amdgcn_raw_buffer_load_b128(xrs, o, 0, 0);
+    }
+  };
+  auto row_store = [&](const v4u_(&st)[2], int gr) {
+    if (gr < 0 || gr >= R) return;
+    char* sl = smem + (gr & 3) * CR_SLOT;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int e = threadIdx.x + CR_NT * i;
+      if (e < W * 8) *(v4u_*)(sl + cr_off((e >> 3) + 1, e & 7)) = st[i];
+    }
+  };
+  v4u_ st[2];
+  __syncthreads();  // ring zeroed before any row lands in it
+  for (int d = -1; d <= 1; ++d) {
+    row_load(st, r_beg + d);
+    row_store(st, r_beg + d);
+  }
+  __syncthreads();
+  for (int r = r_beg; r < r_end; ++r) {
+    const int oh = r % H;
+    const bool pre = r + 1 < r_end;  // the next output row needs input row r + 2
+    if (pre) row_load(st, r + 2);
+    f32x4 acc[NF];
+#pragma unroll
+    for (int f = 0; f < NF; ++f) acc[f] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int kh = 0; kh < 3; ++kh) {
+      if (oh - 1 + kh < 0 || oh - 1 + kh >= H) continue;
+      const char* sl = smem + ((r - 1 + kh) & 3) * CR_SLOT;
+#pragma unroll
+      for (int kw = 0; kw < 3; ++kw) {
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const int s = (kh * 3 + kw) * 2 + h;
+#pragma unroll
+          for (int f = 0; f < NF; ++f) {
+            const s16x8 a = *(const s16x8*)(sl + cr_off(16 * f + j + kw, 4 * h + q));
+            acc[f] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[s], a, acc[f], 0, 0, 0);
+          }
+        }
+      }
+    }
+    // lane (q, j) of fragment f: channels 16 w + 4 q + e of pixel 16 f + j
+    char* ob = smem + 4 * CR_SLOT + (r & 1) * CR_OUT;
+#pragma unroll
+    for (int f = 0; f < NF; ++f) {
+      {
+        const int px = 16 * f + j;
+        unsigned short hv[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          hv[e] = f2bf_rne(acc[f][e] * alpha + bias[e]);
+          const float d = px < W ? bf2f(hv[e]) - shift[e] : 0.f;
+          s1[e] += d;
+          sq[e] += d * d;
+        }
+        *(uint2*)(ob + cr_off(px, 2 * w + (q >> 1)) + (q & 1) * 8) =
+            uint2{hv[0] | ((unsigned)hv[1] << 16), hv[2] | ((unsigned)hv[3] << 16)};
+      }
+    }
+    if (pre) row_store(st, r + 2);
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int e = threadIdx.x + CR_NT * i;
+      if (e < W * 8) {
+        const int px = e >> 3, c = e & 7;
+        const v4u_ v = *(const v4u_*)(ob + cr_off(px, c));
+        __builtin_amdgcn_raw_buffer_store_b128(v, crs, ((unsigned)(r * W + px) * (unsigned)g.ldc + 8u * c) * 2u, 0, 2);
+      }
+    }
+  }
+  if (g.col_stats) {
+    auto rowsum16 = [](float x) {
+      x += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, x), 0x111, 0xf, 0xf, true));
+      x += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, x), 0x112, 0xf, 0xf, true));
+      x += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, x), 0x114, 0xf, 0xf, true));
+      x += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, x), 0x118, 0xf, 0xf, true));
+      return x;
+    };
+    const int nblk = (g.M + GBM - 1) / GBM;
+    const __amdgpu_buffer_rsrc_t srs =
+        __builtin_amdgcn_make_buffer_rsrc((void*)g.col_stats, (short)0, (int)((long long)nblk * 64 * 8), 0x00020000);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const float a = rowsum16(s1[e]), b = rowsum16(sq[e]);
+      if (j == 15)
+        __builtin_amdgcn_raw_buffer_store_b64(st_v2u{__float_as_uint(a), __float_as_uint(b)}, srs,
+                                              ((unsigned)vid * 64u + 16u * w + 4u * q + e) * 8u, 0, 0);
+    }
+    for (int row = grid + vid; row < nblk; row += grid)
+      if (threadIdx.x < 64)
+        __builtin_amdgcn_raw_buffer_store_b64(st_v2u{0u, 0u}, srs, ((unsigned)row * 64u + threadIdx.x) * 8u, 0, 0);
+  }
+}
+
 // Split-K combine: C = alpha * sum_s ws[s] (+bias) (+beta*C) (ReLU).  256 threads = 64 consecutive elements x 4
 // split lanes (lane l sums slabs l, l+4, ...; the 4 partials are added in lane order: deterministic), so
 // thousands of slabs of a small weight gradient are read by many threads with 256-B row segments.

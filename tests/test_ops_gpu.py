@@ -937,11 +937,12 @@ def test_strided_conv_subpixel_input_grad(gpu, k, p):
     assert _rel(x2.grad.float(), seed.float() + x.grad.float()) < 2e-2
 
 
-@pytest.mark.parametrize("n,h,w", [(2, 9, 11), (4, 56, 56), (3, 17, 5)])
+@pytest.mark.parametrize("n,h,w", [(2, 9, 11), (4, 56, 56), (3, 17, 5), (2, 7, 64), (1, 5, 40), (2, 3, 20), (1, 6, 70)])
 def test_direct_conv_3x3_64(gpu, n, h, w):
-    """k_direct_conv<64, 3, 3> (the 64-channel 3x3 / pad 1 convolutions: bf16 output + fused BN column statistics)
-    against torch fp32 on the same bf16-rounded operands: padding on every border, M tails, the per-128-row
-    statistics."""
+    """The 64-channel 3x3 / pad 1 convolutions (bf16 output + fused BN column statistics) against torch fp32 on the
+    same bf16-rounded operands: padding on every border, M tails, the statistics rows (all of them written: the
+    buffer starts as NaN).  W <= 64 runs the row-ring kernel k_conv3x3_rows<ceil(W / 16)> (one to four fragments),
+    W = 70 the per-pixel k_direct_conv<64, 3, 3>."""
     from distributeddataparallel_cifar10_amd import ops
     from distributeddataparallel_cifar10_amd.ops import functional as F
     g = torch.Generator(device=gpu).manual_seed(n * h + w)
