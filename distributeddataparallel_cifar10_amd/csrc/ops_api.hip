@@ -63,7 +63,8 @@ inline int getenv_pp4() {  // A/B knob: DCA_OPS_PP4=0 keeps the two-buffer k_gem
   }();
   return v;
 }
-inline int getenv_conv_rows() {  // A/B knob: DCA_OPS_CONV_ROWS=0 keeps the 64-channel 3x3 convs on k_direct_conv
+inline int getenv_conv_rows() {  // A/B knob: DCA_OPS_CONV_ROWS=0 keeps the layer-1 3x3 convs and the stem on
+                                 // k_direct_conv
   static const int v = [] {
     const char* e = getenv("DCA_OPS_CONV_ROWS");
     return e ? atoi(e) : 1;
@@ -377,6 +378,20 @@ int dca_ops_gemm(const GemmArgs* a, void* stream) {
         case 2: hipLaunchKernelGGL(k_conv3x3_rows<2>, cgd, cb, CR_LDS, st, g); break;
         case 3: hipLaunchKernelGGL(k_conv3x3_rows<3>, cgd, cb, CR_LDS, st, g); break;
         default: hipLaunchKernelGGL(k_conv3x3_rows<4>, cgd, cb, CR_LDS, st, g); break;
+      }
+    } else if (dc_stem && g.cW <= 128 && getenv_conv_rows()) {  // the stem's row-ring form (k_conv_s2d_rows)
+      long cg = std::min<long>(3L * ncu_s, (long)g.cN * g.cHo);
+      if (g.col_stats) cg = std::min<long>(cg, blocks);
+      const dim3 cgd((unsigned)cg), cb(CR_NT);
+      switch ((g.cWo + 15) >> 4) {
+        case 1: hipLaunchKernelGGL(k_conv_s2d_rows<1>, cgd, cb, CS_LDS, st, g); break;
+        case 2: hipLaunchKernelGGL(k_conv_s2d_rows<2>, cgd, cb, CS_LDS, st, g); break;
+        case 3: hipLaunchKernelGGL(k_conv_s2d_rows<3>, cgd, cb, CS_LDS, st, g); break;
+        case 4: hipLaunchKernelGGL(k_conv_s2d_rows<4>, cgd, cb, CS_LDS, st, g); break;
+        case 5: hipLaunchKernelGGL(k_conv_s2d_rows<5>, cgd, cb, CS_LDS, st, g); break;
+        case 6: hipLaunchKernelGGL(k_conv_s2d_rows<6>, cgd, cb, CS_LDS, st, g); break;
+        case 7: hipLaunchKernelGGL(k_conv_s2d_rows<7>, cgd, cb, CS_LDS, st, g); break;
+        default: hipLaunchKernelGGL(k_conv_s2d_rows<8>, cgd, cb, CS_LDS, st, g); break;
       }
     } else if (dc_stem) {
       constexpr int lds = DirectConv<16, 4, 4>::LDS;

@@ -1876,6 +1876,32 @@ constexpr int CR_NT = 256, CR_SLOT = 66 * 128, CR_OUT = 64 * 128;
 constexpr int CR_LDS = 4 * CR_SLOT + 2 * CR_OUT;
 __device__ __forceinline__ int cr_off(int px, int chunk) { return px * 128 + ((chunk ^ (px & 7)) << 4); }
 
+// The row kernels' BN column statistics: lane (q, j) of wave w holds the sums of channels 16 w + 4 q + e over its
+// pixels; summed over j by DPP, written as row vid of col_stats, and the rows from grid to nblk - 1 zeroed.
+__device__ __forceinline__ void rows_stats_out(const GemmArgs& g, const float (&s1)[4], const float (&sq)[4], int vid,
+                                               int grid, int w, int q, int j) {
+  auto rowsum16 = [](float x) {
+    x += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, x), 0x111, 0xf, 0xf, true));
+    x += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, x), 0x112, 0xf, 0xf, true));
+    x += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, x), 0x114, 0xf, 0xf, true));
+    x += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, x), 0x118, 0xf, 0xf, true));
+    return x;
+  };
+  const int nblk = (g.M + GBM - 1) / GBM;
+  const __amdgpu_buffer_rsrc_t srs =
+      __builtin_amdgcn_make_buffer_rsrc((void*)g.col_stats, (short)0, (int)((long long)nblk * 64 * 8), 0x00020000);
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    const float a = rowsum16(s1[e]), b = rowsum16(sq[e]);
+    if (j == 15)
+      __builtin_amdgcn_raw_buffer_store_b64(st_v2u{__float_as_uint(a), __float_as_uint(b)}, srs,
+                                            ((unsigned)vid * 64u + 16u * w + 4u * q + e) * 8u, 0, 0);
+  }
+  for (int row = grid + vid; row < nblk; row += grid)
+    if (threadIdx.x < 64)
+      __builtin_amdgcn_raw_buffer_store_b64(st_v2u{0u, 0u}, srs, ((unsigned)row * 64u + threadIdx.x) * 8u, 0, 0);
+}
+
 template <int NF>  // 16-pixel fragments per row: ceil(W / 16)
 __global__ void __launch_bounds__(CR_NT, 3) k_conv3x3_rows(GemmArgs g) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -1985,28 +2011,108 @@ __global__ void __launch_bounds__(CR_NT, 3) k_conv3x3_rows(GemmArgs g) {
       }
     }
   }
-  if (g.col_stats) {
-    auto rowsum16 = [](float x) {
-      x += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, x), 0x111, 0xf, 0xf, true));
-      x += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, x), 0x112, 0xf, 0xf, true));
-      x += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, x), 0x114, 0xf, 0xf, true));
-      x += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, x), 0x118, 0xf, 0xf, true));
-      return x;
-    };
-    const int nblk = (g.M + GBM - 1) / GBM;
-    const __amdgpu_buffer_rsrc_t srs =
-        __builtin_amdgcn_make_buffer_rsrc((void*)g.col_stats, (short)0, (int)((long long)nblk * 64 * 8), 0x00020000);
+  if (g.col_stats) rows_stats_out(g, s1, sq, vid, grid, w, q, j);
+}
+
+// k_conv_s2d_rows: the space-to-depth ResNet stem (ops/functional.py stem_s2d_index: 4 x 4 taps over a 16-channel
+// input, no padding, stride 1, 64 outputs) in the row-ring form of k_conv3x3_rows, replacing k_direct_conv<16, 4, 4>
+// (207 us at batch 256, the same one-access-per-lane vector-L1 pattern):
+//   * 5 row slots of up to 128 input pixels x 32 B (no swizzle needed: the 16 lanes of a ds_read_b128 group read 16
+//     pixels' alternating 16-B halves, 256 distinct bytes); output row (n, oh) reads input rows oh .. oh + 3 of image
+//     n, the next one's new row is fetched during its MFMAs; the first row of a workgroup or of an image loads all
+//     four (one extra barrier);
+//   * wave w: channels 16 w .. + 15, its 16 x 256 weight fragment (8 K-slices; slice s = taps 2 s, 2 s + 1 of kernel
+//     row s >> 1) in 32 VGPRs; NF = ceil(Wo / 16) A fragments per slice from LDS;
+//   * epilogue as k_conv3x3_rows (double-buffered LDS output image of up to 128 pixels, statistics per workgroup).
+// Requirements (launcher): Wi <= 128 (Wo <= 125), grid <= nblk when col_stats.
+constexpr int CS_SLOT = 128 * 32, CS_OUT = 128 * 128, CS_LDS = 5 * CS_SLOT + 2 * CS_OUT;
+template <int NF>
+__global__ void __launch_bounds__(CR_NT, 3) k_conv_s2d_rows(GemmArgs g) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  typedef unsigned v4u_ __attribute__((ext_vector_type(4)));
+  constexpr unsigned OOB = 0x80000000u;
+  const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), j = lane & 15, q = lane >> 4;
+  const int Hi = g.cH, Wi = g.cW, Ho = g.cHo, Wo = g.cWo, R = g.cN * Ho;
+  const int grid = gridDim.x;
+  const int vid = (grid & 7) == 0 ? (int)(blockIdx.x & 7) * (grid >> 3) + (int)(blockIdx.x >> 3) : (int)blockIdx.x;
+  const int r_beg = (int)((long long)vid * R / grid), r_end = (int)((long long)(vid + 1) * R / grid);
+  // slots past Wi are read by the tail fragments' taps (discarded pixels): keep them finite
+  for (int e = threadIdx.x; e < 5 * CS_SLOT / 16; e += CR_NT) *(v4u_*)(smem + e * 16) = v4u_{0u, 0u, 0u, 0u};
+  const unsigned short* Bp = (const unsigned short*)g.B;
+  s16x8 wf[8];
 #pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      const float a = rowsum16(s1[e]), b = rowsum16(sq[e]);
-      if (j == 15)
-        __builtin_amdgcn_raw_buffer_store_b64(st_v2u{__float_as_uint(a), __float_as_uint(b)}, srs,
-                                              ((unsigned)vid * 64u + 16u * w + 4u * q + e) * 8u, 0, 0);
-    }
-    for (int row = grid + vid; row < nblk; row += grid)
-      if (threadIdx.x < 64)
-        __builtin_amdgcn_raw_buffer_store_b64(st_v2u{0u, 0u}, srs, ((unsigned)row * 64u + threadIdx.x) * 8u, 0, 0);
+  for (int s = 0; s < 8; ++s) wf[s] = *(const s16x8*)(Bp + (size_t)(16 * w + j) * g.ldb + 32 * s + 8 * q);
+  const float alpha = gemm_alpha(g);
+  float bias[4], shift[4], s1[4], sq[4];
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    const int c = 16 * w + 4 * q + e;
+    bias[e] = g.bias ? g.bias[c] : 0.f;
+    shift[e] = g.col_stats ? g.stats_shift[c] : 0.f;
+    s1[e] = sq[e] = 0.f;
   }
+  const int RI = g.cN * Hi;  // input rows
+  const __amdgpu_buffer_rsrc_t xrs =
+      __builtin_amdgcn_make_buffer_rsrc((void*)g.A, (short)0, (int)((long long)RI * Wi * 32), 0x00020000);
+  const __amdgpu_buffer_rsrc_t crs =
+      __builtin_amdgcn_make_buffer_rsrc(g.C, (short)0, (int)((long long)g.M * g.ldc * 2), 0x00020000);
+  auto row_load = [&](int gi) {  // input row gi: Wi * 2 pieces of 16 B, one per thread
+    const unsigned o = (gi < RI && (int)threadIdx.x < Wi * 2) ? ((unsigned)gi * (unsigned)Wi * 32u + threadIdx.x * 16u) : OOB;
+    return __builtin_amdgcn_raw_buffer_load_b128(xrs, o, 0, 0);
+  };
+  auto row_store = [&](const v4u_& v, int gi) {
+    if (gi < RI && (int)threadIdx.x < Wi * 2) *(v4u_*)(smem + (gi % 5) * CS_SLOT + threadIdx.x * 16) = v;
+  };
+  __syncthreads();  // ring zeroed
+  for (int r = r_beg; r < r_end; ++r) {
+    const int n = r / Ho, oh = r - n * Ho, gi0 = n * Hi + oh;  // input rows gi0 .. gi0 + 3
+    if (r == r_beg || oh == 0) {  // a workgroup's or an image's first row: all four rows (the last barrier freed them)
+      v4u_ v[4];
+#pragma unroll
+      for (int d = 0; d < 4; ++d) v[d] = row_load(gi0 + d);
+#pragma unroll
+      for (int d = 0; d < 4; ++d) row_store(v[d], gi0 + d);
+      __syncthreads();
+    }
+    const bool pre = r + 1 < r_end && oh + 1 < Ho;  // the next row of this image needs input row gi0 + 4
+    v4u_ nx;
+    if (pre) nx = row_load(gi0 + 4);
+    f32x4 acc[NF];
+#pragma unroll
+    for (int f = 0; f < NF; ++f) acc[f] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int s = 0; s < 8; ++s) {  // kernel row s >> 1, column 2 (s & 1) + (q >> 1), channels 8 (q & 1) .. + 7
+      const char* sl = smem + ((gi0 + (s >> 1)) % 5) * CS_SLOT + (2 * (s & 1) + (q >> 1)) * 32 + (q & 1) * 16;
+#pragma unroll
+      for (int f = 0; f < NF; ++f) {
+        const s16x8 a = *(const s16x8*)(sl + (16 * f + j) * 32);
+        acc[f] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[s], a, acc[f], 0, 0, 0);
+      }
+    }
+    char* ob = smem + 5 * CS_SLOT + (r & 1) * CS_OUT;
+#pragma unroll
+    for (int f = 0; f < NF; ++f) {
+      const int px = 16 * f + j;
+      unsigned short hv[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        hv[e] = f2bf_rne(acc[f][e] * alpha + bias[e]);
+        const float d = px < Wo ? bf2f(hv[e]) - shift[e] : 0.f;
+        s1[e] += d;
+        sq[e] += d * d;
+      }
+      *(uint2*)(ob + cr_off(px, 2 * w + (q >> 1)) + (q & 1) * 8) =
+          uint2{hv[0] | ((unsigned)hv[1] << 16), hv[2] | ((unsigned)hv[3] << 16)};
+    }
+    if (pre) row_store(nx, gi0 + 4);  // slot of row gi0 - 1, last read by the previous output row
+    __syncthreads();
+    for (int e = threadIdx.x; e < Wo * 8; e += CR_NT) {
+      const int px = e >> 3, c = e & 7;
+      const v4u_ v = *(const v4u_*)(ob + cr_off(px, c));
+      __builtin_amdgcn_raw_buffer_store_b128(v, crs, ((unsigned)(r * Wo + px) * (unsigned)g.ldc + 8u * c) * 2u, 0, 2);
+    }
+  }
+  if (g.col_stats) rows_stats_out(g, s1, sq, vid, grid, w, q, j);
 }
 
 // Split-K combine: C = alpha * sum_s ws[s] (+bias) (+beta*C) (ReLU).  256 threads = 64 consecutive elements x 4

@@ -107,11 +107,12 @@ def test_stem_s2d_ops_model_stem(gpu):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("n,h,w", [(3, 50, 46), (2, 224, 224), (5, 37, 64)])
+@pytest.mark.parametrize("n,h,w", [(3, 50, 46), (2, 224, 224), (5, 37, 64), (1, 40, 250), (1, 30, 262)])
 def test_stem_conv_kernel_bf16_stats(gpu, n, h, w):
-    """The dedicated s2d stem kernel (k_stem_conv: bf16 output with the fused BN column statistics, the form the
-    ops model's stem calls) against torch fp32 on the same bf16-rounded operands: output, and the per-128-row
-    partial sums / sums of squares of the stored values."""
+    """The dedicated s2d stem kernels (bf16 output with the fused BN column statistics, the form the ops model's stem
+    calls: k_conv_s2d_rows up to 128 s2d pixels per row -- w = 250 is the 8-fragment edge -- and k_direct_conv<16, 4,
+    4> beyond, w = 262) against torch fp32 on the same bf16-rounded operands: output, and the statistics rows (all of
+    them written: the buffer starts as NaN)."""
     from distributeddataparallel_cifar10_amd.ops import functional as F
     torch.manual_seed(n + h)
     conv = torch.nn.Conv2d(3, 64, 7, stride=2, padding=3, bias=False).to(gpu)
