@@ -24,7 +24,7 @@ M = geo.N * geo.Ho * geo.Wo
 shift = torch.zeros(64, device=dev)
 parts = torch.zeros((M + 127) // 128, 64, 2, device=dev)
 dy = torch.randn(M, 64, device=dev).to(bf)
-sp = F._wgrad_splits(64, geo.K, M, True)
+sp = F._wgrad_splits(64, geo.K, M, True, row_w=56)
 fns = {
     "fwd": lambda: F.gemm(x, wm, conv=1, geom=geo, mnk=(M, 64, geo.K), out_dtype=bf, col_stats=parts, stats_shift=shift),
     "wgrad": lambda: F.gemm(dy, x, ta=True, conv=2, geom=geo, mnk=(64, geo.K, M), splits=sp),

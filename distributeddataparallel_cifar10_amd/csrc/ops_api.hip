@@ -71,6 +71,13 @@ inline int getenv_conv_rows() {  // A/B knob: DCA_OPS_CONV_ROWS=0 keeps the laye
   }();
   return v;
 }
+inline int getenv_wgrad_rows() {  // A/B knob: DCA_OPS_WGRAD_ROWS=0 keeps the 64-channel 3x3 weight gradient on k_wgrad
+  static const int v = [] {
+    const char* e = getenv("DCA_OPS_WGRAD_ROWS");
+    return e ? atoi(e) : 1;
+  }();
+  return v;
+}
 inline int getenv_stream() {  // persistent short-K GEMM (k_gemm_stream): DCA_OPS_STREAM = 0 never, 1 whenever
   static const int v = [] {    // eligible, 2 (default) by the shape rule at the launch site
     const char* e = getenv("DCA_OPS_STREAM");
@@ -289,6 +296,28 @@ int dca_ops_gemm(const GemmArgs* a, void* stream) {
                      (g.conv == 2 || g.ldb % 8 == 0) && g.ws != nullptr;
   if (wgrad) {
     REQUIRE(g.conv != 2 || (long)g.cN * g.cHo * g.cWo < (1L << 24), "gemm: weight-gradient pixel count >= 2^24");
+    // the 64-channel 3 x 3 / pad 1 weight gradient on rows <= 64 pixels: the row-ring kernel (k_wgrad3x3_rows), one
+    // split slab per workgroup
+    if (g.conv == 2 && g.cC == 64 && g.cKH == 3 && g.cKW == 3 && g.cP == 1 && g.cS == 1 && g.cW <= 64 &&
+        g.cHo == g.cH && g.cWo == g.cW && g.M == 64 && g.N == 576 && g.K == g.cN * g.cH * g.cW && g.lda % 8 == 0 &&
+        g.lda >= 64 && ((uintptr_t)g.A & 15) == 0 && ((uintptr_t)g.B & 15) == 0 &&
+        (long long)g.cN * g.cH * g.cW * g.lda * 2 < (1LL << 31) && (long long)g.cN * g.cH * g.cW * 128 < (1LL << 31) &&
+        getenv_conv_rows() && getenv_wgrad_rows()) {
+      static int ncu_w = 0;
+      if (!ncu_w) {
+        int dev = 0;
+        OPCK(hipGetDevice(&dev));
+        OPCK(hipDeviceGetAttribute(&ncu_w, hipDeviceAttributeMultiprocessorCount, dev));
+      }
+      const long cg = std::min<long>(std::min<long>(g.splits, 2L * ncu_w), (long)g.cN * g.cH);
+      g.splits = (int)cg;
+      const dim3 cgd((unsigned)cg), cb(CR_NT);
+      if (g.cW <= 32) hipLaunchKernelGGL(k_wgrad3x3_rows<1>, cgd, cb, WR_LDS, st, g);
+      else hipLaunchKernelGGL(k_wgrad3x3_rows<2>, cgd, cb, WR_LDS, st, g);
+      hipLaunchKernelGGL(k_gemm_splitk_reduce, dim3(grid_for((long)g.M * g.N, RED_EL, 4096)), dim3(256), 0, st, g);
+      OPCK(hipGetLastError());
+      return 0;
+    }
     // the ping-pong kernel: the larger of M (output channels) / N (input channels x taps) along its 256-row side
     // (SW: N), the smaller one as a 256 / 128 column tile; 32-bit operand offsets, 16-B aligned rows.  The split
     // count is cut to about one workgroup per CU (one fits per CU).  Shape rule from bench/wgrad_bench.py at batch

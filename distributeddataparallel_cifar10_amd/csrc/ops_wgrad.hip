@@ -432,5 +432,142 @@ __global__ void __launch_bounds__(WP_NT) k_wgrad_pp(GemmArgs g) {
     }
 }
 
+// ---------------------------------------------------------------------------------------------------------
+// k_wgrad3x3_rows: weight gradient of the 64-channel 3 x 3 / pad 1 / stride 1 convolutions on rows of at most 64
+// pixels (ResNet-50's layer 1), dW[co][tap * 64 + c] = sum_p dY[p][co] X[p + tap][c], in the row form of
+// k_conv3x3_rows (ops_gemm.hip): a workgroup walks consecutive output rows (n, oh) with the three input rows in an
+// LDS ring (4 slots of 66 pixels x 128 B, pixel iw at position iw + 1) and the dY row in a double buffer, each row
+// fetched once per workgroup with coalesced 16-B loads one row ahead.  k_wgrad re-gathers the implicit im2col per
+// K-tile (13 VALU per MFMA, MFMA busy 0.19: profiles/conv3x3_rows_r9.txt).
+//   * wave w owns input channels 16 w .. + 15 of all 9 taps and all 64 output channels: 9 x 4 accumulator tiles
+//     (144 registers) for the workgroup's whole row range;
+//   * per 32-pixel chunk: the 4 dY fragments (16 co x 32 pixels) and per valid tap one X fragment (32 pixels x 16
+//     channels, shifted by kw) are read with ds_read_b64_tr_b16 (two per fragment: pixels 8 q .. + 3 and + 4 .. + 7
+//     of lane group q), i.e. 26 transposed reads for 36 MFMAs; the 16-B chunks of a pixel row are XOR-swizzled by
+//     wr_sw(pixel) so the 8 pixel rows x 32 B of a 32-lane half hit 64 distinct banks for every shift;
+//   * padding rows are skipped per row; pixels past W are zero in the dY image;
+//   * the workgroup's partial 64 x 576 sums go to split slab vid of the fp32 workspace (k_gemm_splitk_reduce sums
+//     them in a fixed order: deterministic).
+// Requirements (launcher): bf16, C = Cout = 64, W <= 64, grid <= the slab's splits.
+// ---------------------------------------------------------------------------------------------------------
+__device__ __forceinline__ int wr_off(int px, int chunk) {
+  return px * 128 + ((chunk ^ ((((px >> 1) & 3) << 1) ^ (((px >> 3) & 1) << 2))) << 4);
+}
+constexpr int WR_LDS = 4 * CR_SLOT + 2 * CR_OUT;
+template <int NPC>  // 32-pixel chunks per row: ceil(W / 32)
+__global__ void __launch_bounds__(CR_NT, 2) k_wgrad3x3_rows(GemmArgs g) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  typedef unsigned v4u_ __attribute__((ext_vector_type(4)));
+  constexpr unsigned OOB = 0x80000000u;
+  const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), j = lane & 15, q = lane >> 4;
+  const int ra = j >> 2, rp = j & 3;  // transposed read: lane 4 ra + rp of its group addresses block row ra, cols 4 rp..
+  const int H = g.cH, W = g.cW, R = g.cN * g.cH;
+  const int grid = gridDim.x;
+  const int vid = (grid & 7) == 0 ? (int)(blockIdx.x & 7) * (grid >> 3) + (int)(blockIdx.x >> 3) : (int)blockIdx.x;
+  const int r_beg = (int)((long long)vid * R / grid), r_end = (int)((long long)(vid + 1) * R / grid);
+  char* dyb = smem + 4 * CR_SLOT;
+  for (int e = threadIdx.x; e < WR_LDS / 16; e += CR_NT) *(v4u_*)(smem + e * 16) = v4u_{0u, 0u, 0u, 0u};
+  const __amdgpu_buffer_rsrc_t xrs =
+      __builtin_amdgcn_make_buffer_rsrc((void*)g.B, (short)0, (int)((long long)R * W * 128), 0x00020000);
+  const __amdgpu_buffer_rsrc_t drs =
+      __builtin_amdgcn_make_buffer_rsrc((void*)g.A, (short)0, (int)((long long)R * W * g.lda * 2), 0x00020000);
+  auto x_load = [&](v4u_(&st)[2], int gr) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int e = threadIdx.x + CR_NT * i;
+      const unsigned o = (gr >= 0 && gr < R && e < W * 8) ? (unsigned)gr * (unsigned)W * 128u + (unsigned)e * 16u : OOB;
+      st[i] = __builtin_amdgcn_raw_buffer_load_b128(xrs, o, 0, 0);
+    }
+  };
+  auto x_store = [&](const v4u_(&st)[2], int gr) {
+    if (gr < 0 || gr >= R) return;
+    char* sl = smem + (gr & 3) * CR_SLOT;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int e = threadIdx.x + CR_NT * i;
+      if (e < W * 8) *(v4u_*)(sl + wr_off((e >> 3) + 1, e & 7)) = st[i];
+    }
+  };
+  auto d_load = [&](v4u_(&st)[2], int r) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int e = threadIdx.x + CR_NT * i;
+      const unsigned o = (r < R && e < W * 8)
+                             ? ((unsigned)(r * W + (e >> 3)) * (unsigned)g.lda + 8u * (unsigned)(e & 7)) * 2u : OOB;
+      st[i] = __builtin_amdgcn_raw_buffer_load_b128(drs, o, 0, 0);
+    }
+  };
+  auto d_store = [&](const v4u_(&st)[2], int r) {
+    char* db = dyb + (r & 1) * CR_OUT;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int e = threadIdx.x + CR_NT * i;
+      if (e < W * 8) *(v4u_*)(db + wr_off(e >> 3, e & 7)) = st[i];
+    }
+  };
+  // one 16 x 32 operand: pixels px .. px + 7 (as 8 q + 0..3, + 4..7) of the 16 channels from byte column 32 cb
+  auto frag = [&](const char* base, int px, int cb) {
+    const int ch = 2 * cb + (rp >> 1), within = 8 * (rp & 1);
+    const s16x4 lo = lds_tr16(base + wr_off(px + ra, ch) + within);
+    const s16x4 hi = lds_tr16(base + wr_off(px + 4 + ra, ch) + within);
+    return s16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+  };
+  f32x4 acc[9][4];
+#pragma unroll
+  for (int t = 0; t < 9; ++t)
+#pragma unroll
+    for (int m = 0; m < 4; ++m) acc[t][m] = f32x4{0.f, 0.f, 0.f, 0.f};
+  v4u_ xs[2], ds[2];
+  __syncthreads();  // zeroed before any row lands
+  for (int d = -1; d <= 1; ++d) {
+    x_load(xs, r_beg + d);
+    x_store(xs, r_beg + d);
+  }
+  d_load(ds, r_beg);
+  d_store(ds, r_beg);
+  __syncthreads();
+  for (int r = r_beg; r < r_end; ++r) {
+    const int oh = r % H;
+    const bool pre = r + 1 < r_end;
+    if (pre) {
+      x_load(xs, r + 2);
+      d_load(ds, r + 1);
+    }
+    const char* db = dyb + (r & 1) * CR_OUT;
+#pragma unroll
+    for (int pc = 0; pc < NPC; ++pc) {
+      const int px0 = 32 * pc + 8 * q;
+      s16x8 a[4];
+#pragma unroll
+      for (int m = 0; m < 4; ++m) a[m] = frag(db, px0, m);
+#pragma unroll
+      for (int kh = 0; kh < 3; ++kh) {
+        if (oh - 1 + kh < 0 || oh - 1 + kh >= H) continue;
+        const char* sl = smem + ((r - 1 + kh) & 3) * CR_SLOT;
+#pragma unroll
+        for (int kw = 0; kw < 3; ++kw) {
+          const s16x8 b = frag(sl, px0 + kw, w);
+#pragma unroll
+          for (int m = 0; m < 4; ++m)
+            acc[kh * 3 + kw][m] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[m], b, acc[kh * 3 + kw][m], 0, 0, 0);
+        }
+      }
+    }
+    if (pre) {
+      x_store(xs, r + 2);  // slot of row r - 2, last read by the previous output row
+      d_store(ds, r + 1);  // the other dY buffer, last read by the previous output row
+    }
+    __syncthreads();
+  }
+  // lane (q, j) of tile (t, m): output channel 16 m + 4 q + e, input channel 16 w + j of tap t
+  float* wsp = g.ws + (size_t)vid * 64 * 576;
+#pragma unroll
+  for (int t = 0; t < 9; ++t)
+#pragma unroll
+    for (int m = 0; m < 4; ++m)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) wsp[(16 * m + 4 * q + e) * 576 + t * 64 + 16 * w + j] = acc[t][m][e];
+}
+
 }  // namespace ops
 }  // namespace dca

@@ -21,6 +21,9 @@ from . import _native as N
 
 _BWD_TRACE = None  # diagnostics: a list to record the order of the fused conv-BN backward calls
 WGRAD_NARROW_HALF = True  # _wgrad_splits' halved target for the narrow forms (False: the round-6 rule, for A/Bs)
+# the row-ring weight gradient of the 64-channel 3x3 convs (csrc/ops_wgrad.hip k_wgrad3x3_rows) is on unless either
+# of its native knobs turns it off; it sets that form's split count (_wgrad_splits)
+WGRAD_ROWS = os.environ.get("DCA_OPS_WGRAD_ROWS", "1") != "0" and os.environ.get("DCA_OPS_CONV_ROWS", "1") != "0"
 
 
 def _dev_check(*ts):
@@ -142,13 +145,17 @@ def amax_value(amax_bits: torch.Tensor) -> torch.Tensor:
     return amax_bits.view(torch.float32)
 
 
-def _wgrad_splits(M: int, Nn: int, K: int, implicit: bool = False) -> int:
+def _wgrad_splits(M: int, Nn: int, K: int, implicit: bool = False, row_w: int = 0) -> int:
     """Split-K factor for a weight-gradient GEMM (K = pixels: long, M x N small): enough workgroups to fill the
     chip twice over (2 resident per CU x 256 CUs), >= 4 K-tiles per split, fp32 slab <= 64 MiB.  Half that target
     for the plain 64-wide forms (k_wgrad 64 x 128 / 128 x 64 / 64 x 64 tiles: 802816 x {64, 256} x {64, 256}
     53 -> 43, 116 -> 99, 115 -> 101 us) and the 128-channel implicit 3x3 ones (k_wgrad_pp: 144 -> 134, 120 ->
     116 us), where the partial slabs and their reduce cost more than the extra workgroups hide
-    (profiles/wgrad_split_sweep_r8c.log; the 64-channel implicit 3x3 wants the full target: 148 vs 200 us)."""
+    (profiles/wgrad_split_sweep_r8c.log; the 64-channel implicit 3x3 wants the full target: 148 vs 200 us).
+    The 64-channel implicit 3x3 on input rows of row_w <= 64 pixels runs k_wgrad3x3_rows, one split slab per
+    workgroup: 512 splits = two workgroups per CU (its launcher takes min(splits, 2 x CUs, rows))."""
+    if implicit and M == 64 and Nn == 576 and 0 < row_w <= 64 and WGRAD_ROWS:
+        return max(1, min(512, K // 256))
     tiles = math.ceil(M / 128) * math.ceil(Nn / 128)
     narrow = (min(M, Nn) <= 64) if not implicit else (min(M, Nn) == 128)
     s = math.ceil((512 if narrow and WGRAD_NARROW_HALF else 1024) / tiles)
@@ -723,8 +730,8 @@ def _conv_bwd(dy, st, need_x: bool, need_w: bool, sink=None, x_join: Optional[Gr
             kp = cols.shape[1]
             gemm(dyb, cols, ta=True, tb=True, splits=_wgrad_splits(co, kp, M), out=dst, beta=beta, wperm=perm)
         else:  # implicit: B(n = tap*C + c, k = pixel) gathered from x
-            gemm(dyb, st["x"], ta=True, conv=2, geom=g, mnk=(co, g.K, M), splits=_wgrad_splits(co, g.K, M, True),
-                 out=dst, beta=beta, wperm=perm)
+            gemm(dyb, st["x"], ta=True, conv=2, geom=g, mnk=(co, g.K, M),
+                 splits=_wgrad_splits(co, g.K, M, True, row_w=g.W), out=dst, beta=beta, wperm=perm)
         dw = None if sink is not None else dst
     return dx, dw
 

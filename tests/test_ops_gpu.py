@@ -717,6 +717,26 @@ def test_wgrad_pingpong_implicit_conv(gpu, n, h, c, co, k, s, p):
     assert _rel(out, ref) < 1e-5, _rel(out, ref)
 
 
+@pytest.mark.parametrize("n,h,w", [(2, 9, 11), (4, 56, 56), (3, 17, 5), (2, 7, 64), (2, 5, 40), (1, 6, 70)])
+def test_wgrad3x3_rows(gpu, n, h, w):
+    """The 64-channel 3x3 / pad 1 weight gradient as the model calls it (implicit split count): W <= 64 runs the
+    row-ring k_wgrad3x3_rows<ceil(W / 32)> (one and two 32-pixel chunks, pixels past W, padding rows, one split slab
+    per workgroup), W = 70 the k_wgrad fallback; against torch fp32 in torch's [Cout, Cin, 3, 3] layout."""
+    from distributeddataparallel_cifar10_amd.ops import functional as F
+    g = torch.Generator(device=gpu).manual_seed(n * h + w)
+    x = _bf(torch.randn(n, h, w, 64, device=gpu, generator=g))
+    wt = torch.empty(64, 64, 3, 3, device=gpu)
+    geo = F._geom(x, wt, 1, 1)
+    M = n * geo.Ho * geo.Wo
+    dy = _bf(torch.randn(M, 64, device=gpu, generator=g))
+    ref = torch.nn.grad.conv2d_weight(x.float().permute(0, 3, 1, 2), wt.shape,
+                                      dy.float().view(n, geo.Ho, geo.Wo, 64).permute(0, 3, 1, 2), stride=1, padding=1)
+    out = torch.full_like(wt, float("nan"))
+    F.gemm(dy, x, ta=True, conv=2, geom=geo, mnk=(64, geo.K, M), splits=F._wgrad_splits(64, geo.K, M, True, row_w=w),
+           out=out, wperm=(64, 64, 9))
+    assert _rel(out, ref) < 1e-5, _rel(out, ref)
+
+
 def test_wgrad_pingpong_forms(gpu):
     """Every weight-gradient form the dispatch routes to k_wgrad_pp -- 256 x 256 and 256 x 128 column tiles, the
     swapped plain form (64 < M <= 128), the implicit-im2col B operand -- and the k_wgrad fallbacks beside them
