@@ -318,6 +318,32 @@ int dca_ops_gemm(const GemmArgs* a, void* stream) {
       OPCK(hipGetLastError());
       return 0;
     }
+    // the space-to-depth stem's weight gradient (4 x 4 taps over 16 channels) on rows <= 128 input pixels:
+    // k_wgrad_s2d_rows, one split slab per workgroup
+    if (g.conv == 2 && g.cC == 16 && g.cKH == 4 && g.cKW == 4 && g.cP == 0 && g.cS == 1 && g.cW <= 128 &&
+        g.cHo == g.cH - 3 && g.cWo == g.cW - 3 && g.M == 64 && g.N == 256 && g.K == g.cN * g.cHo * g.cWo &&
+        g.lda % 8 == 0 && g.lda >= 64 && ((uintptr_t)g.A & 15) == 0 && ((uintptr_t)g.B & 15) == 0 &&
+        (long long)g.cN * g.cHo * g.cWo * g.lda * 2 < (1LL << 31) && (long long)g.cN * g.cH * g.cW * 32 < (1LL << 31) &&
+        getenv_conv_rows() && getenv_wgrad_rows()) {
+      static int ncu_s2 = 0;
+      if (!ncu_s2) {
+        int dev = 0;
+        OPCK(hipGetDevice(&dev));
+        OPCK(hipDeviceGetAttribute(&ncu_s2, hipDeviceAttributeMultiprocessorCount, dev));
+      }
+      const long cg = std::min<long>(std::min<long>(g.splits, 3L * ncu_s2), (long)g.cN * g.cHo);
+      g.splits = (int)cg;
+      const dim3 cgd((unsigned)cg), cb(CR_NT);
+      switch ((g.cWo + 31) >> 5) {
+        case 1: hipLaunchKernelGGL(k_wgrad_s2d_rows<1>, cgd, cb, WS_LDS, st, g); break;
+        case 2: hipLaunchKernelGGL(k_wgrad_s2d_rows<2>, cgd, cb, WS_LDS, st, g); break;
+        case 3: hipLaunchKernelGGL(k_wgrad_s2d_rows<3>, cgd, cb, WS_LDS, st, g); break;
+        default: hipLaunchKernelGGL(k_wgrad_s2d_rows<4>, cgd, cb, WS_LDS, st, g); break;
+      }
+      hipLaunchKernelGGL(k_gemm_splitk_reduce, dim3(grid_for((long)g.M * g.N, RED_EL, 4096)), dim3(256), 0, st, g);
+      OPCK(hipGetLastError());
+      return 0;
+    }
     // the ping-pong kernel: the larger of M (output channels) / N (input channels x taps) along its 256-row side
     // (SW: N), the smaller one as a 256 / 128 column tile; 32-bit operand offsets, 16-B aligned rows.  The split
     // count is cut to about one workgroup per CU (one fits per CU).  Shape rule from bench/wgrad_bench.py at batch

@@ -569,5 +569,119 @@ __global__ void __launch_bounds__(CR_NT, 2) k_wgrad3x3_rows(GemmArgs g) {
       for (int e = 0; e < 4; ++e) wsp[(16 * m + 4 * q + e) * 576 + t * 64 + 16 * w + j] = acc[t][m][e];
 }
 
+// ---------------------------------------------------------------------------------------------------------
+// k_wgrad_s2d_rows: weight gradient of the space-to-depth stem conv (4 x 4 taps over 16 channels, no padding, 64
+// outputs; ops/functional.py stem_s2d_index), dW[co][tap * 16 + c] = sum_p dY[p][co] X[p + tap][c], in the row form
+// of k_conv_s2d_rows (ops_gemm.hip; k_wgrad<64, 128, 1> ran it at 226 us at batch 256):
+//   * input rows in 5 LDS slots of 128 pixels x 32 B (the first row of a workgroup or an image loads all four, later
+//     ones one row ahead), the dY row in a double buffer of 128 pixels x 128 B;
+//   * wave w owns kernel row kh = w: 4 taps x 4 output-channel tiles (64 accumulators), reading only input row
+//     oh + w; a tap's X fragment (32 pixels x the 16 channels) and the 4 dY fragments come from ds_read_b64_tr_b16,
+//     two per fragment, with the K order of k_wgrad (element e < 4 of lane group q = pixel 4 q + e, e >= 4 = pixel
+//     16 + 4 q + e - 4), so a 32-lane half reads 8 consecutive pixels: 256 contiguous bytes of an X slot, and 8 dY
+//     rows whose 16-B chunks are XOR-swizzled by ((pixel >> 1) & 3) << 1 (conflict-free);
+//   * pixels past Wo are zero in the dY image; partial sums to split slab vid (k_gemm_splitk_reduce).
+// Requirements (launcher): C = 16, KH = KW = 4, pad 0, stride 1, Cout = 64, Wi <= 128, grid <= the slab's splits.
+// ---------------------------------------------------------------------------------------------------------
+__device__ __forceinline__ int ws2_off(int px, int chunk) { return px * 128 + ((chunk ^ (((px >> 1) & 3) << 1)) << 4); }
+constexpr int WS_SLOT = 128 * 32, WS_DY = 128 * 128, WS_LDS = 5 * WS_SLOT + 2 * WS_DY;
+template <int NPC>  // 32-pixel chunks per output row: ceil(Wo / 32)
+__global__ void __launch_bounds__(CR_NT, 3) k_wgrad_s2d_rows(GemmArgs g) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  typedef unsigned v4u_ __attribute__((ext_vector_type(4)));
+  constexpr unsigned OOB = 0x80000000u;
+  const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), j = lane & 15, q = lane >> 4;
+  const int ra = j >> 2, rp = j & 3;
+  const int Hi = g.cH, Wi = g.cW, Ho = g.cHo, Wo = g.cWo, R = g.cN * Ho, RI = g.cN * Hi;
+  const int grid = gridDim.x;
+  const int vid = (grid & 7) == 0 ? (int)(blockIdx.x & 7) * (grid >> 3) + (int)(blockIdx.x >> 3) : (int)blockIdx.x;
+  const int r_beg = (int)((long long)vid * R / grid), r_end = (int)((long long)(vid + 1) * R / grid);
+  char* dyb = smem + 5 * WS_SLOT;
+  for (int e = threadIdx.x; e < WS_LDS / 16; e += CR_NT) *(v4u_*)(smem + e * 16) = v4u_{0u, 0u, 0u, 0u};
+  const __amdgpu_buffer_rsrc_t xrs =
+      __builtin_amdgcn_make_buffer_rsrc((void*)g.B, (short)0, (int)((long long)RI * Wi * 32), 0x00020000);
+  const __amdgpu_buffer_rsrc_t drs =
+      __builtin_amdgcn_make_buffer_rsrc((void*)g.A, (short)0, (int)((long long)R * Wo * g.lda * 2), 0x00020000);
+  auto x_load = [&](int gi) {  // input row gi: Wi * 2 pieces of 16 B, one per thread
+    const unsigned o =
+        (gi < RI && (int)threadIdx.x < Wi * 2) ? ((unsigned)gi * (unsigned)Wi * 32u + threadIdx.x * 16u) : OOB;
+    return __builtin_amdgcn_raw_buffer_load_b128(xrs, o, 0, 0);
+  };
+  auto x_store = [&](const v4u_& v, int gi) {
+    if (gi < RI && (int)threadIdx.x < Wi * 2) *(v4u_*)(smem + (gi % 5) * WS_SLOT + threadIdx.x * 16) = v;
+  };
+  auto d_load = [&](v4u_(&st)[4], int r) {  // dY row r: Wo * 8 pieces, up to 4 per thread
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int e = threadIdx.x + CR_NT * i;
+      const unsigned o = (r < R && e < Wo * 8)
+                             ? ((unsigned)(r * Wo + (e >> 3)) * (unsigned)g.lda + 8u * (unsigned)(e & 7)) * 2u : OOB;
+      st[i] = __builtin_amdgcn_raw_buffer_load_b128(drs, o, 0, 0);
+    }
+  };
+  auto d_store = [&](const v4u_(&st)[4], int r) {
+    char* db = dyb + (r & 1) * WS_DY;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int e = threadIdx.x + CR_NT * i;
+      if (e < Wo * 8) *(v4u_*)(db + ws2_off(e >> 3, e & 7)) = st[i];
+    }
+  };
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int t = 0; t < 4; ++t)
+#pragma unroll
+    for (int m = 0; m < 4; ++m) acc[t][m] = f32x4{0.f, 0.f, 0.f, 0.f};
+  v4u_ ds[4], xn;
+  __syncthreads();  // zeroed before any row lands
+  d_load(ds, r_beg);
+  d_store(ds, r_beg);
+  for (int r = r_beg; r < r_end; ++r) {
+    const int n = r / Ho, oh = r - n * Ho, gi0 = n * Hi + oh;
+    if (r == r_beg || oh == 0) {  // a workgroup's or an image's first row: all four input rows
+      v4u_ v[4];
+#pragma unroll
+      for (int d = 0; d < 4; ++d) v[d] = x_load(gi0 + d);
+#pragma unroll
+      for (int d = 0; d < 4; ++d) x_store(v[d], gi0 + d);
+      __syncthreads();
+    }
+    const bool pre = r + 1 < r_end, prex = pre && oh + 1 < Ho;
+    if (pre) d_load(ds, r + 1);
+    if (prex) xn = x_load(gi0 + 4);
+    const char* db = dyb + (r & 1) * WS_DY;
+    const char* sl = smem + ((gi0 + w) % 5) * WS_SLOT;  // this wave's kernel row
+#pragma unroll 1
+    for (int pc = 0; pc < NPC; ++pc) {
+      const int p0 = 32 * pc + 4 * q + ra;
+      s16x8 a[4];
+#pragma unroll
+      for (int m = 0; m < 4; ++m) {
+        const int ch = 2 * m + (rp >> 1), within = 8 * (rp & 1);
+        const s16x4 lo = lds_tr16(db + ws2_off(p0, ch) + within), hi = lds_tr16(db + ws2_off(p0 + 16, ch) + within);
+        a[m] = s16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+      }
+#pragma unroll
+      for (int kw = 0; kw < 4; ++kw) {
+        const s16x4 lo = lds_tr16(sl + (p0 + kw) * 32 + 8 * rp), hi = lds_tr16(sl + (p0 + 16 + kw) * 32 + 8 * rp);
+        const s16x8 b = s16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+#pragma unroll
+        for (int m = 0; m < 4; ++m) acc[kw][m] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[m], b, acc[kw][m], 0, 0, 0);
+      }
+    }
+    if (prex) x_store(xn, gi0 + 4);  // slot of row gi0 - 1, last read by the previous output row
+    if (pre) d_store(ds, r + 1);     // the other dY buffer, last read by the previous output row
+    __syncthreads();
+  }
+  // lane (q, j) of tile (kw, m): output channel 16 m + 4 q + e, column (4 w + kw) * 16 + j
+  float* wsp = g.ws + (size_t)vid * 64 * 256;
+#pragma unroll
+  for (int kw = 0; kw < 4; ++kw)
+#pragma unroll
+    for (int m = 0; m < 4; ++m)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) wsp[(16 * m + 4 * q + e) * 256 + (4 * w + kw) * 16 + j] = acc[kw][m][e];
+}
+
 }  // namespace ops
 }  // namespace dca

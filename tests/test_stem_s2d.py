@@ -135,3 +135,32 @@ def test_stem_conv_kernel_bf16_stats(gpu, n, h, w):
     assert rel(y.float(), ref) < 5e-3
     d = y.float() - shift
     assert rel(parts[..., 0].sum(0), d.sum(0)) < 1e-4 and rel(parts[..., 1].sum(0), (d * d).sum(0)) < 1e-4
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n,h,w", [(3, 50, 46), (2, 224, 224), (1, 40, 250), (1, 30, 262)])
+def test_stem_wgrad_rows(gpu, n, h, w):
+    """The s2d stem's weight gradient as the ops model calls it (implicit split count): k_wgrad_s2d_rows up to 128
+    s2d pixels per row (one to four 32-pixel chunks, image boundaries inside a workgroup's rows; w = 250 is the
+    128-pixel edge) and the k_wgrad fallback beyond (w = 262), mapped back to [Co, 3, 7, 7], against torch fp32."""
+    from distributeddataparallel_cifar10_amd.ops import functional as F
+    torch.manual_seed(n * h + w)
+    conv = torch.nn.Conv2d(3, 64, 7, stride=2, padding=3, bias=False).to(gpu)
+    pack = F.WeightPack([conv], (), [conv])
+    pack.pack()
+    e = pack.get(conv)
+    x = torch.randn(n, 3, h, w, device=gpu)
+    xs = F.nchw_to_s2d16(x)
+    wg, st, pd = F._s2d_args(conv.weight, 2, 3, e)
+    g = F._geom(xs, wg, st, pd)
+    M = g.N * g.Ho * g.Wo
+    dy = torch.randn(M, 64, device=gpu).to(torch.bfloat16)
+    d4 = torch.full((64, 16, 4, 4), float("nan"), device=gpu)
+    F.gemm(dy, xs, ta=True, conv=2, geom=g, mnk=(64, g.K, M), splits=F._wgrad_splits(64, g.K, M, True, row_w=g.W),
+           out=d4, wperm=(16, 16, 16))
+    dw = d4.view(64, -1).index_select(1, e["s2d"]["back_idx"]).view(64, 3, 7, 7)
+    xr = x.to(torch.bfloat16).float()
+    gref = torch.nn.grad.conv2d_weight(xr, conv.weight.shape, dy.float().view(g.N, g.Ho, g.Wo, 64).permute(0, 3, 1, 2),
+                                       stride=2, padding=3)
+    rel = lambda a, b: ((a.double() - b.double()).norm() / b.double().norm()).item()  # noqa: E731
+    assert rel(dw, gref) < 1e-5, rel(dw, gref)
