@@ -407,6 +407,29 @@ int dca_ops_gemm(const GemmArgs* a, void* stream) {
   //     (DCA_OPS_STREAM=1, diagnostic): 174 us there, 218 us with 128 x 64 stream tiles, 283 us with 256 x 64
   // stride-1 implicit convs with 64 outputs on narrow input rows -> k_direct_conv: the space-to-depth ResNet stem
   // (4 x 4 taps over 16 channels) and the 64-channel 3 x 3 / pad 1 convolutions (layer 1 forward and input gradient)
+  // the 128-channel 3 x 3 / pad 1 convs on rows <= 32 pixels (ResNet-50's layer 2 at 28 x 28, forward and input
+  // gradient) -> the row-ring kernel k_conv3x3_rows<NF, 128> (one 8-wave workgroup per CU)
+  if (g.conv == 1 && g.cC == 128 && g.cKH == 3 && g.cKW == 3 && g.cP == 1 && g.cS == 1 && g.cW <= 32 &&
+      g.cHo == g.cH && g.cWo == g.cW && g.N == 128 && g.K == 1152 && !g.fp8 && !g.tb && g.splits == 1 &&
+      g.wperm_T <= 0 && g.orow_S <= 0 && g.out_bf16 && !g.relu && g.beta == 0.f && !g.beta_mask && g.ldb >= g.K &&
+      g.ldb % 8 == 0 && g.ldc >= 128 && g.ldc % 8 == 0 && ((uintptr_t)g.A & 15) == 0 && ((uintptr_t)g.B & 15) == 0 &&
+      ((uintptr_t)g.C & 15) == 0 && (long long)g.cN * g.cH * g.cW * 256 < (1LL << 31) &&
+      (long long)g.M * g.ldc * 2 < (1LL << 31) && g.M < (1 << 24) && getenv_conv_rows()) {
+    static int ncu_r = 0;
+    if (!ncu_r) {
+      int dev = 0;
+      OPCK(hipGetDevice(&dev));
+      OPCK(hipDeviceGetAttribute(&ncu_r, hipDeviceAttributeMultiprocessorCount, dev));
+    }
+    long cg = std::min<long>(ncu_r, (long)g.cN * g.cH);
+    if (g.col_stats) cg = std::min<long>(cg, (g.M + GBM - 1) / GBM);
+    constexpr int lds = RowConv<128>::LDS;
+    const dim3 cgd((unsigned)cg), cb(RowConv<128>::NT);
+    if (g.cW <= 16) hipLaunchKernelGGL((k_conv3x3_rows<1, 128>), cgd, cb, lds, st, g);
+    else hipLaunchKernelGGL((k_conv3x3_rows<2, 128>), cgd, cb, lds, st, g);
+    OPCK(hipGetLastError());
+    return 0;
+  }
   const bool dc_stem = g.cC == 16 && g.cKH == 4 && g.cKW == 4 && g.cP == 0;
   const bool dc_3x3 = g.cC == 64 && g.cKH == 3 && g.cKW == 3 && g.cP == 1;
   // (the kernel loops over the compile-time K = KH KW C: an mnk override or a padded K must not reach it)

@@ -1877,7 +1877,9 @@ constexpr int CR_LDS = 4 * CR_SLOT + 2 * CR_OUT;
 __device__ __forceinline__ int cr_off(int px, int chunk) { return px * 128 + ((chunk ^ (px & 7)) << 4); }
 
 // The row kernels' BN column statistics: lane (q, j) of wave w holds the sums of channels 16 w + 4 q + e over its
-// pixels; summed over j by DPP, written as row vid of col_stats, and the rows from grid to nblk - 1 zeroed.
+// pixels; summed over j by DPP, written as row vid of col_stats ([nblk][NC][2]), and the rows from grid to nblk - 1
+// zeroed.
+template <int NC = 64>
 __device__ __forceinline__ void rows_stats_out(const GemmArgs& g, const float (&s1)[4], const float (&sq)[4], int vid,
                                                int grid, int w, int q, int j) {
   auto rowsum16 = [](float x) {
@@ -1889,21 +1891,37 @@ __device__ __forceinline__ void rows_stats_out(const GemmArgs& g, const float (&
   };
   const int nblk = (g.M + GBM - 1) / GBM;
   const __amdgpu_buffer_rsrc_t srs =
-      __builtin_amdgcn_make_buffer_rsrc((void*)g.col_stats, (short)0, (int)((long long)nblk * 64 * 8), 0x00020000);
+      __builtin_amdgcn_make_buffer_rsrc((void*)g.col_stats, (short)0, (int)((long long)nblk * NC * 8), 0x00020000);
 #pragma unroll
   for (int e = 0; e < 4; ++e) {
     const float a = rowsum16(s1[e]), b = rowsum16(sq[e]);
     if (j == 15)
       __builtin_amdgcn_raw_buffer_store_b64(st_v2u{__float_as_uint(a), __float_as_uint(b)}, srs,
-                                            ((unsigned)vid * 64u + 16u * w + 4u * q + e) * 8u, 0, 0);
+                                            ((unsigned)vid * NC + 16u * w + 4u * q + e) * 8u, 0, 0);
   }
   for (int row = grid + vid; row < nblk; row += grid)
-    if (threadIdx.x < 64)
-      __builtin_amdgcn_raw_buffer_store_b64(st_v2u{0u, 0u}, srs, ((unsigned)row * 64u + threadIdx.x) * 8u, 0, 0);
+    if (threadIdx.x < NC)
+      __builtin_amdgcn_raw_buffer_store_b64(st_v2u{0u, 0u}, srs, ((unsigned)row * NC + threadIdx.x) * 8u, 0, 0);
 }
 
-template <int NF>  // 16-pixel fragments per row: ceil(W / 16)
-__global__ void __launch_bounds__(CR_NT, 3) k_conv3x3_rows(GemmArgs g) {
+// C = 64: 4 waves (3 workgroups per CU), rows <= 64 pixels; C = 128 (layer 2, 28 x 28): 8 waves of 16 output
+// channels each, 144 weight VGPRs per lane (one workgroup per CU), rows <= 32 pixels.  16-B chunks of a pixel row
+// XOR-swizzled by pixel & (C / 8 - 1): for C = 128 the two 16-lane halves of a ds_read_b128 group (chunks c, c + 1)
+// still cover the 64 banks once.
+template <int C>
+struct RowConv {
+  static constexpr int NT = 4 * C, CH = C / 8, PXB = 2 * C, NS = 9 * C / 32, HS = C / 32;
+  static constexpr int SPX = C == 64 ? 66 : 34, SLOT = SPX * PXB, OUT = (SPX - 2) * PXB, LDS = 4 * SLOT + 2 * OUT;
+  static constexpr int NL = ((SPX - 2) * CH + NT - 1) / NT;  // 16-B row pieces per thread
+};
+template <int C>
+__device__ __forceinline__ int crc_off(int px, int chunk) {
+  return px * (2 * C) + ((chunk ^ (px & (C / 8 - 1))) << 4);
+}
+template <int NF, int C = 64>  // NF: 16-pixel fragments per row, ceil(W / 16)
+__global__ void __launch_bounds__(4 * C, C == 64 ? 3 : 1) k_conv3x3_rows(GemmArgs g) {
+  using T = RowConv<C>;
+  constexpr int NT = T::NT, NS = T::NS, NL = T::NL;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   typedef unsigned v4u_ __attribute__((ext_vector_type(4)));
   constexpr unsigned OOB = 0x80000000u;
@@ -1913,12 +1931,12 @@ __global__ void __launch_bounds__(CR_NT, 3) k_conv3x3_rows(GemmArgs g) {
   // XCD-contiguous row ranges: the workgroups of one XCD take neighbouring ranges (shared boundary rows in its L2)
   const int vid = (grid & 7) == 0 ? (int)(blockIdx.x & 7) * (grid >> 3) + (int)(blockIdx.x >> 3) : (int)blockIdx.x;
   const int r_beg = (int)((long long)vid * R / grid), r_end = (int)((long long)(vid + 1) * R / grid);
-  for (int e = threadIdx.x; e < 4 * CR_SLOT / 16; e += CR_NT) *(v4u_*)(smem + e * 16) = v4u_{0u, 0u, 0u, 0u};
-  // weights: lane (q, j) of slice s holds channel 16 w + j, k = 32 s + 8 q .. + 7 (k = tap * 64 + c)
+  for (int e = threadIdx.x; e < 4 * T::SLOT / 16; e += NT) *(v4u_*)(smem + e * 16) = v4u_{0u, 0u, 0u, 0u};
+  // weights: lane (q, j) of slice s holds channel 16 w + j, k = 32 s + 8 q .. + 7 (k = tap * C + c)
   const unsigned short* Bp = (const unsigned short*)g.B;
-  s16x8 wf[18];
+  s16x8 wf[NS];
 #pragma unroll
-  for (int s = 0; s < 18; ++s) wf[s] = *(const s16x8*)(Bp + (size_t)(16 * w + j) * g.ldb + 32 * s + 8 * q);
+  for (int s = 0; s < NS; ++s) wf[s] = *(const s16x8*)(Bp + (size_t)(16 * w + j) * g.ldb + 32 * s + 8 * q);
   const float alpha = gemm_alpha(g);
   float bias[4], shift[4], s1[4], sq[4];
 #pragma unroll
@@ -1929,28 +1947,29 @@ __global__ void __launch_bounds__(CR_NT, 3) k_conv3x3_rows(GemmArgs g) {
     s1[e] = sq[e] = 0.f;
   }
   const __amdgpu_buffer_rsrc_t xrs =
-      __builtin_amdgcn_make_buffer_rsrc((void*)g.A, (short)0, (int)((long long)R * W * 128), 0x00020000);
+      __builtin_amdgcn_make_buffer_rsrc((void*)g.A, (short)0, (int)((long long)R * W * T::PXB), 0x00020000);
   const __amdgpu_buffer_rsrc_t crs =
       __builtin_amdgcn_make_buffer_rsrc(g.C, (short)0, (int)((long long)g.M * g.ldc * 2), 0x00020000);
-  // input row gr: W * 8 pieces of 16 B (pixel e >> 3, chunk e & 7), two per thread
-  auto row_load = [&](v4u_(&st)[2], int gr) {
+  // input row gr: W * CH pieces of 16 B (pixel e / CH, chunk e % CH), NL per thread
+  auto row_load = [&](v4u_(&st)[NL], int gr) {
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int e = threadIdx.x + CR_NT * i;
-      const unsigned o = (gr >= 0 && gr < R && e < W * 8) ? (unsigned)gr * (unsigned)W * 128u + (unsigned)e * 16u : OOB;
+    for (int i = 0; i < NL; ++i) {
+      const int e = threadIdx.x + NT * i;
+      const unsigned o =
+          (gr >= 0 && gr < R && e < W * T::CH) ? (unsigned)gr * (unsigned)W * T::PXB + (unsigned)e * 16u : OOB;
       st[i] = __builtin_amdgcn_raw_buffer_load_b128(xrs, o, 0, 0);
     }
   };
-  auto row_store = [&](const v4u_(&st)[2], int gr) {
+  auto row_store = [&](const v4u_(&st)[NL], int gr) {
     if (gr < 0 || gr >= R) return;
-    char* sl = smem + (gr & 3) * CR_SLOT;
+    char* sl = smem + (gr & 3) * T::SLOT;
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int e = threadIdx.x + CR_NT * i;
-      if (e < W * 8) *(v4u_*)(sl + cr_off((e >> 3) + 1, e & 7)) = st[i];
+    for (int i = 0; i < NL; ++i) {
+      const int e = threadIdx.x + NT * i;
+      if (e < W * T::CH) *(v4u_*)(sl + crc_off<C>(e / T::CH + 1, e % T::CH)) = st[i];
     }
   };
-  v4u_ st[2];
+  v4u_ st[NL];
   __syncthreads();  // ring zeroed before any row lands in it
   for (int d = -1; d <= 1; ++d) {
     row_load(st, r_beg + d);
@@ -1967,51 +1986,49 @@ __global__ void __launch_bounds__(CR_NT, 3) k_conv3x3_rows(GemmArgs g) {
 #pragma unroll
     for (int kh = 0; kh < 3; ++kh) {
       if (oh - 1 + kh < 0 || oh - 1 + kh >= H) continue;
-      const char* sl = smem + ((r - 1 + kh) & 3) * CR_SLOT;
+      const char* sl = smem + ((r - 1 + kh) & 3) * T::SLOT;
 #pragma unroll
       for (int kw = 0; kw < 3; ++kw) {
 #pragma unroll
-        for (int h = 0; h < 2; ++h) {
-          const int s = (kh * 3 + kw) * 2 + h;
+        for (int h = 0; h < T::HS; ++h) {
+          const int s = (kh * 3 + kw) * T::HS + h;
 #pragma unroll
           for (int f = 0; f < NF; ++f) {
-            const s16x8 a = *(const s16x8*)(sl + cr_off(16 * f + j + kw, 4 * h + q));
+            const s16x8 a = *(const s16x8*)(sl + crc_off<C>(16 * f + j + kw, 4 * h + q));
             acc[f] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[s], a, acc[f], 0, 0, 0);
           }
         }
       }
     }
     // lane (q, j) of fragment f: channels 16 w + 4 q + e of pixel 16 f + j
-    char* ob = smem + 4 * CR_SLOT + (r & 1) * CR_OUT;
+    char* ob = smem + 4 * T::SLOT + (r & 1) * T::OUT;
 #pragma unroll
     for (int f = 0; f < NF; ++f) {
-      {
-        const int px = 16 * f + j;
-        unsigned short hv[4];
+      const int px = 16 * f + j;
+      unsigned short hv[4];
 #pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          hv[e] = f2bf_rne(acc[f][e] * alpha + bias[e]);
-          const float d = px < W ? bf2f(hv[e]) - shift[e] : 0.f;
-          s1[e] += d;
-          sq[e] += d * d;
-        }
-        *(uint2*)(ob + cr_off(px, 2 * w + (q >> 1)) + (q & 1) * 8) =
-            uint2{hv[0] | ((unsigned)hv[1] << 16), hv[2] | ((unsigned)hv[3] << 16)};
+      for (int e = 0; e < 4; ++e) {
+        hv[e] = f2bf_rne(acc[f][e] * alpha + bias[e]);
+        const float d = px < W ? bf2f(hv[e]) - shift[e] : 0.f;
+        s1[e] += d;
+        sq[e] += d * d;
       }
+      *(uint2*)(ob + crc_off<C>(px, 2 * w + (q >> 1)) + (q & 1) * 8) =
+          uint2{hv[0] | ((unsigned)hv[1] << 16), hv[2] | ((unsigned)hv[3] << 16)};
     }
     if (pre) row_store(st, r + 2);
     __syncthreads();
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int e = threadIdx.x + CR_NT * i;
-      if (e < W * 8) {
-        const int px = e >> 3, c = e & 7;
-        const v4u_ v = *(const v4u_*)(ob + cr_off(px, c));
+    for (int i = 0; i < NL; ++i) {
+      const int e = threadIdx.x + NT * i;
+      if (e < W * T::CH) {
+        const int px = e / T::CH, c = e % T::CH;
+        const v4u_ v = *(const v4u_*)(ob + crc_off<C>(px, c));
         __builtin_amdgcn_raw_buffer_store_b128(v, crs, ((unsigned)(r * W + px) * (unsigned)g.ldc + 8u * c) * 2u, 0, 2);
       }
     }
   }
-  if (g.col_stats) rows_stats_out(g, s1, sq, vid, grid, w, q, j);
+  if (g.col_stats) rows_stats_out<C>(g, s1, sq, vid, grid, w, q, j);
 }
 
 // k_conv_s2d_rows: the space-to-depth ResNet stem (ops/functional.py stem_s2d_index: 4 x 4 taps over a 16-channel

@@ -957,26 +957,29 @@ def test_strided_conv_subpixel_input_grad(gpu, k, p):
     assert _rel(x2.grad.float(), seed.float() + x.grad.float()) < 2e-2
 
 
-@pytest.mark.parametrize("n,h,w", [(2, 9, 11), (4, 56, 56), (3, 17, 5), (2, 7, 64), (1, 5, 40), (2, 3, 20), (1, 6, 70)])
-def test_direct_conv_3x3_64(gpu, n, h, w):
-    """The 64-channel 3x3 / pad 1 convolutions (bf16 output + fused BN column statistics) against torch fp32 on the
-    same bf16-rounded operands: padding on every border, M tails, the statistics rows (all of them written: the
-    buffer starts as NaN).  W <= 64 runs the row-ring kernel k_conv3x3_rows<ceil(W / 16)> (one to four fragments),
-    W = 70 the per-pixel k_direct_conv<64, 3, 3>."""
+@pytest.mark.parametrize("n,h,w,c", [(2, 9, 11, 64), (4, 56, 56, 64), (3, 17, 5, 64), (2, 7, 64, 64), (1, 5, 40, 64),
+                                     (2, 3, 20, 64), (1, 6, 70, 64), (4, 28, 28, 128), (3, 9, 11, 128),
+                                     (2, 5, 16, 128), (1, 6, 40, 128)])
+def test_direct_conv_3x3_64(gpu, n, h, w, c):
+    """The 64- and 128-channel 3x3 / pad 1 convolutions (bf16 output + fused BN column statistics) against torch
+    fp32 on the same bf16-rounded operands: padding on every border, M tails, the statistics rows (all of them
+    written: the buffer starts as NaN).  64 channels: W <= 64 runs the row-ring kernel k_conv3x3_rows<ceil(W / 16)>
+    (one to four fragments), W = 70 the per-pixel k_direct_conv<64, 3, 3>; 128 channels: W <= 32 runs
+    k_conv3x3_rows<ceil(W / 16), 128> (ResNet-50's layer 2 at 28 x 28), W = 40 the stream GEMM."""
     from distributeddataparallel_cifar10_amd import ops
     from distributeddataparallel_cifar10_amd.ops import functional as F
-    g = torch.Generator(device=gpu).manual_seed(n * h + w)
-    x = torch.randn(n, h, w, 64, device=gpu, generator=g).to(torch.bfloat16)
-    wt = torch.randn(64, 64, 3, 3, device=gpu, generator=g) * 0.05
+    g = torch.Generator(device=gpu).manual_seed(n * h + w + c)
+    x = torch.randn(n, h, w, c, device=gpu, generator=g).to(torch.bfloat16)
+    wt = torch.randn(c, c, 3, 3, device=gpu, generator=g) * (0.05 if c == 64 else 0.035)
     geo = F._geom(x, wt, 1, 1)
     wm = F._weight_matrix(wt, geo.K)
     M = geo.N * geo.Ho * geo.Wo
-    shift = torch.randn(64, device=gpu, generator=g) * 0.1
-    parts = torch.full(((M + 127) // 128, 64, 2), float("nan"), device=gpu)
-    y = ops.gemm(x, wm, conv=1, geom=geo, mnk=(M, 64, geo.K), out_dtype=torch.bfloat16, col_stats=parts,
+    shift = torch.randn(c, device=gpu, generator=g) * 0.1
+    parts = torch.full(((M + 127) // 128, c, 2), float("nan"), device=gpu)
+    y = ops.gemm(x, wm, conv=1, geom=geo, mnk=(M, c, geo.K), out_dtype=torch.bfloat16, col_stats=parts,
                  stats_shift=shift)
     ref = TF.conv2d(x.float().permute(0, 3, 1, 2), wt.to(torch.bfloat16).float(), padding=1)
-    ref = ref.permute(0, 2, 3, 1).reshape(M, 64)
+    ref = ref.permute(0, 2, 3, 1).reshape(M, c)
     assert _rel(y, ref) < 5e-3
     d = y.float() - shift
     assert _rel(parts[..., 0].sum(0), d.sum(0)) < 1e-4 and _rel(parts[..., 1].sum(0), (d * d).sum(0)) < 1e-4
