@@ -318,6 +318,27 @@ int dca_ops_gemm(const GemmArgs* a, void* stream) {
       OPCK(hipGetLastError());
       return 0;
     }
+    // the 128-channel 3 x 3 / pad 1 weight gradient on rows <= 32 pixels (layer 2): k_wgrad3x3_rows<1, 128>,
+    // two workgroups (output-channel halves) per split slab, one workgroup per CU
+    if (g.conv == 2 && g.cC == 128 && g.cKH == 3 && g.cKW == 3 && g.cP == 1 && g.cS == 1 && g.cW <= 32 &&
+        g.cHo == g.cH && g.cWo == g.cW && g.M == 128 && g.N == 1152 && g.K == g.cN * g.cH * g.cW && g.lda % 8 == 0 &&
+        g.lda >= 128 && ((uintptr_t)g.A & 15) == 0 && ((uintptr_t)g.B & 15) == 0 &&
+        (long long)g.cN * g.cH * g.cW * g.lda * 2 < (1LL << 31) && (long long)g.cN * g.cH * g.cW * 256 < (1LL << 31) &&
+        getenv_conv_rows() && getenv_wgrad_rows()) {
+      static int ncu_w2 = 0;
+      if (!ncu_w2) {
+        int dev = 0;
+        OPCK(hipGetDevice(&dev));
+        OPCK(hipDeviceGetAttribute(&ncu_w2, hipDeviceAttributeMultiprocessorCount, dev));
+      }
+      const long cg = std::min<long>(std::min<long>(g.splits, ncu_w2 / 2), (long)g.cN * g.cH);
+      g.splits = (int)cg;
+      const dim3 cgd((unsigned)(2 * cg)), cb(WgradRows<128>::NT);
+      hipLaunchKernelGGL((k_wgrad3x3_rows<1, 128>), cgd, cb, WgradRows<128>::LDS, st, g);
+      hipLaunchKernelGGL(k_gemm_splitk_reduce, dim3(grid_for((long)g.M * g.N, RED_EL, 4096)), dim3(256), 0, st, g);
+      OPCK(hipGetLastError());
+      return 0;
+    }
     // the space-to-depth stem's weight gradient (4 x 4 taps over 16 channels) on rows <= 128 input pixels:
     // k_wgrad_s2d_rows, one split slab per workgroup
     if (g.conv == 2 && g.cC == 16 && g.cKH == 4 && g.cKW == 4 && g.cP == 0 && g.cS == 1 && g.cW <= 128 &&

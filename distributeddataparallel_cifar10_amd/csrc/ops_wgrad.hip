@@ -448,68 +448,94 @@ __global__ void __launch_bounds__(WP_NT) k_wgrad_pp(GemmArgs g) {
 //   * padding rows are skipped per row; pixels past W are zero in the dY image;
 //   * the workgroup's partial 64 x 576 sums go to split slab vid of the fp32 workspace (k_gemm_splitk_reduce sums
 //     them in a fixed order: deterministic).
-// Requirements (launcher): bf16, C = Cout = 64, W <= 64, grid <= the slab's splits.
+// Requirements (launcher): bf16, C = Cout = 64 (W <= 64) or 128 (W <= 32), grid <= the slab's splits (x 2 for 128).
 // ---------------------------------------------------------------------------------------------------------
 __device__ __forceinline__ int wr_off(int px, int chunk) {
   return px * 128 + ((chunk ^ ((((px >> 1) & 3) << 1) ^ (((px >> 3) & 1) << 2))) << 4);
 }
-constexpr int WR_LDS = 4 * CR_SLOT + 2 * CR_OUT;
-template <int NPC>  // 32-pixel chunks per row: ceil(W / 32)
-__global__ void __launch_bounds__(CR_NT, 2) k_wgrad3x3_rows(GemmArgs g) {
+// X pixel rows of C channels: C = 64 as wr_off; C = 128 (256-B rows, one bank window per pixel): chunk XOR 2 f(px)
+// with f = (px & 3) | ((px >> 3) & 1) << 2, injective on the 8 pixels {b .. b + 3, b + 8 .. b + 11} of a 32-lane half
+template <int C>
+__device__ __forceinline__ int wx_off(int px, int chunk) {
+  if constexpr (C == 64) return wr_off(px, chunk);
+  else return px * 256 + ((chunk ^ (((px & 3) | (((px >> 3) & 1) << 2)) << 1)) << 4);
+}
+// C = 64: 4 waves, rows <= 64 pixels; C = 128 (layer 2, 28 x 28): 8 waves (input channels 16 w .. + 15 each), rows
+// <= 32 pixels, and the 128 output channels split over two workgroups (half = blockIdx.x % 2: 64 each, 144
+// accumulators per lane), one workgroup per CU
+template <int C>
+struct WgradRows {
+  static constexpr int NT = 4 * C, HALVES = C / 64, SPX = C == 64 ? 66 : 34, XCH = C / 8;
+  static constexpr int SLOT = SPX * 2 * C, DY = (SPX - 2) * 128, LDS = 4 * SLOT + 2 * DY;
+  static constexpr int NLX = ((SPX - 2) * XCH + NT - 1) / NT, NLD = ((SPX - 2) * 8 + NT - 1) / NT;
+};
+constexpr int WR_LDS = WgradRows<64>::LDS;
+template <int NPC, int C = 64>  // NPC: 32-pixel chunks per row, ceil(W / 32)
+__global__ void __launch_bounds__(4 * C, C == 64 ? 2 : 1) k_wgrad3x3_rows(GemmArgs g) {
+  using T = WgradRows<C>;
+  constexpr int NT = T::NT, NLX = T::NLX, NLD = T::NLD;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   typedef unsigned v4u_ __attribute__((ext_vector_type(4)));
   constexpr unsigned OOB = 0x80000000u;
   const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), j = lane & 15, q = lane >> 4;
   const int ra = j >> 2, rp = j & 3;  // transposed read: lane 4 ra + rp of its group addresses block row ra, cols 4 rp..
   const int H = g.cH, W = g.cW, R = g.cN * g.cH;
-  const int grid = gridDim.x;
-  const int vid = (grid & 7) == 0 ? (int)(blockIdx.x & 7) * (grid >> 3) + (int)(blockIdx.x >> 3) : (int)blockIdx.x;
+  const int half = (int)blockIdx.x % T::HALVES, bid = (int)blockIdx.x / T::HALVES, grid = gridDim.x / T::HALVES;
+  const int vid = (grid & 7) == 0 ? (bid & 7) * (grid >> 3) + (bid >> 3) : bid;
   const int r_beg = (int)((long long)vid * R / grid), r_end = (int)((long long)(vid + 1) * R / grid);
-  char* dyb = smem + 4 * CR_SLOT;
-  for (int e = threadIdx.x; e < WR_LDS / 16; e += CR_NT) *(v4u_*)(smem + e * 16) = v4u_{0u, 0u, 0u, 0u};
+  char* dyb = smem + 4 * T::SLOT;
+  for (int e = threadIdx.x; e < T::LDS / 16; e += NT) *(v4u_*)(smem + e * 16) = v4u_{0u, 0u, 0u, 0u};
   const __amdgpu_buffer_rsrc_t xrs =
-      __builtin_amdgcn_make_buffer_rsrc((void*)g.B, (short)0, (int)((long long)R * W * 128), 0x00020000);
+      __builtin_amdgcn_make_buffer_rsrc((void*)g.B, (short)0, (int)((long long)R * W * 2 * C), 0x00020000);
   const __amdgpu_buffer_rsrc_t drs =
       __builtin_amdgcn_make_buffer_rsrc((void*)g.A, (short)0, (int)((long long)R * W * g.lda * 2), 0x00020000);
-  auto x_load = [&](v4u_(&st)[2], int gr) {
+  auto x_load = [&](v4u_(&st)[NLX], int gr) {
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int e = threadIdx.x + CR_NT * i;
-      const unsigned o = (gr >= 0 && gr < R && e < W * 8) ? (unsigned)gr * (unsigned)W * 128u + (unsigned)e * 16u : OOB;
+    for (int i = 0; i < NLX; ++i) {
+      const int e = threadIdx.x + NT * i;
+      const unsigned o =
+          (gr >= 0 && gr < R && e < W * T::XCH) ? (unsigned)gr * (unsigned)W * (2u * C) + (unsigned)e * 16u : OOB;
       st[i] = __builtin_amdgcn_raw_buffer_load_b128(xrs, o, 0, 0);
     }
   };
-  auto x_store = [&](const v4u_(&st)[2], int gr) {
+  auto x_store = [&](const v4u_(&st)[NLX], int gr) {
     if (gr < 0 || gr >= R) return;
-    char* sl = smem + (gr & 3) * CR_SLOT;
+    char* sl = smem + (gr & 3) * T::SLOT;
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int e = threadIdx.x + CR_NT * i;
-      if (e < W * 8) *(v4u_*)(sl + wr_off((e >> 3) + 1, e & 7)) = st[i];
+    for (int i = 0; i < NLX; ++i) {
+      const int e = threadIdx.x + NT * i;
+      if (e < W * T::XCH) *(v4u_*)(sl + wx_off<C>(e / T::XCH + 1, e % T::XCH)) = st[i];
     }
   };
-  auto d_load = [&](v4u_(&st)[2], int r) {
+  auto d_load = [&](v4u_(&st)[NLD], int r) {  // this workgroup's 64 output channels of dY row r
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int e = threadIdx.x + CR_NT * i;
-      const unsigned o = (r < R && e < W * 8)
-                             ? ((unsigned)(r * W + (e >> 3)) * (unsigned)g.lda + 8u * (unsigned)(e & 7)) * 2u : OOB;
+    for (int i = 0; i < NLD; ++i) {
+      const int e = threadIdx.x + NT * i;
+      const unsigned o = (r < R && e < W * 8) ? ((unsigned)(r * W + (e >> 3)) * (unsigned)g.lda + 64u * half +
+                                                 8u * (unsigned)(e & 7)) * 2u
+                                              : OOB;
       st[i] = __builtin_amdgcn_raw_buffer_load_b128(drs, o, 0, 0);
     }
   };
-  auto d_store = [&](const v4u_(&st)[2], int r) {
-    char* db = dyb + (r & 1) * CR_OUT;
+  auto d_store = [&](const v4u_(&st)[NLD], int r) {
+    char* db = dyb + (r & 1) * T::DY;
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int e = threadIdx.x + CR_NT * i;
+    for (int i = 0; i < NLD; ++i) {
+      const int e = threadIdx.x + NT * i;
       if (e < W * 8) *(v4u_*)(db + wr_off(e >> 3, e & 7)) = st[i];
     }
   };
   // one 16 x 32 operand: pixels px .. px + 7 (as 8 q + 0..3, + 4..7) of the 16 channels from byte column 32 cb
-  auto frag = [&](const char* base, int px, int cb) {
+  auto frag_d = [&](const char* base, int px, int cb) {
     const int ch = 2 * cb + (rp >> 1), within = 8 * (rp & 1);
     const s16x4 lo = lds_tr16(base + wr_off(px + ra, ch) + within);
     const s16x4 hi = lds_tr16(base + wr_off(px + 4 + ra, ch) + within);
+    return s16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+  };
+  auto frag_x = [&](const char* base, int px, int cb) {
+    const int ch = 2 * cb + (rp >> 1), within = 8 * (rp & 1);
+    const s16x4 lo = lds_tr16(base + wx_off<C>(px + ra, ch) + within);
+    const s16x4 hi = lds_tr16(base + wx_off<C>(px + 4 + ra, ch) + within);
     return s16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
   };
   f32x4 acc[9][4];
@@ -517,7 +543,7 @@ __global__ void __launch_bounds__(CR_NT, 2) k_wgrad3x3_rows(GemmArgs g) {
   for (int t = 0; t < 9; ++t)
 #pragma unroll
     for (int m = 0; m < 4; ++m) acc[t][m] = f32x4{0.f, 0.f, 0.f, 0.f};
-  v4u_ xs[2], ds[2];
+  v4u_ xs[NLX], ds[NLD];
   __syncthreads();  // zeroed before any row lands
   for (int d = -1; d <= 1; ++d) {
     x_load(xs, r_beg + d);
@@ -533,20 +559,20 @@ __global__ void __launch_bounds__(CR_NT, 2) k_wgrad3x3_rows(GemmArgs g) {
       x_load(xs, r + 2);
       d_load(ds, r + 1);
     }
-    const char* db = dyb + (r & 1) * CR_OUT;
+    const char* db = dyb + (r & 1) * T::DY;
 #pragma unroll
     for (int pc = 0; pc < NPC; ++pc) {
       const int px0 = 32 * pc + 8 * q;
       s16x8 a[4];
 #pragma unroll
-      for (int m = 0; m < 4; ++m) a[m] = frag(db, px0, m);
+      for (int m = 0; m < 4; ++m) a[m] = frag_d(db, px0, m);
 #pragma unroll
       for (int kh = 0; kh < 3; ++kh) {
         if (oh - 1 + kh < 0 || oh - 1 + kh >= H) continue;
-        const char* sl = smem + ((r - 1 + kh) & 3) * CR_SLOT;
+        const char* sl = smem + ((r - 1 + kh) & 3) * T::SLOT;
 #pragma unroll
         for (int kw = 0; kw < 3; ++kw) {
-          const s16x8 b = frag(sl, px0 + kw, w);
+          const s16x8 b = frag_x(sl, px0 + kw, w);
 #pragma unroll
           for (int m = 0; m < 4; ++m)
             acc[kh * 3 + kw][m] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[m], b, acc[kh * 3 + kw][m], 0, 0, 0);
@@ -559,14 +585,14 @@ __global__ void __launch_bounds__(CR_NT, 2) k_wgrad3x3_rows(GemmArgs g) {
     }
     __syncthreads();
   }
-  // lane (q, j) of tile (t, m): output channel 16 m + 4 q + e, input channel 16 w + j of tap t
-  float* wsp = g.ws + (size_t)vid * 64 * 576;
+  // lane (q, j) of tile (t, m): output channel 64 half + 16 m + 4 q + e, input channel 16 w + j of tap t
+  float* wsp = g.ws + (size_t)vid * C * 9 * C;
 #pragma unroll
   for (int t = 0; t < 9; ++t)
 #pragma unroll
     for (int m = 0; m < 4; ++m)
 #pragma unroll
-      for (int e = 0; e < 4; ++e) wsp[(16 * m + 4 * q + e) * 576 + t * 64 + 16 * w + j] = acc[t][m][e];
+      for (int e = 0; e < 4; ++e) wsp[(64 * half + 16 * m + 4 * q + e) * (9 * C) + t * C + 16 * w + j] = acc[t][m][e];
 }
 
 // ---------------------------------------------------------------------------------------------------------

@@ -153,9 +153,12 @@ def _wgrad_splits(M: int, Nn: int, K: int, implicit: bool = False, row_w: int = 
     116 us), where the partial slabs and their reduce cost more than the extra workgroups hide
     (profiles/wgrad_split_sweep_r8c.log; the 64-channel implicit 3x3 wants the full target: 148 vs 200 us).
     The 64-channel implicit 3x3 on input rows of row_w <= 64 pixels runs k_wgrad3x3_rows, one split slab per
-    workgroup: 512 splits = two workgroups per CU (its launcher takes min(splits, 2 x CUs, rows))."""
+    workgroup: 512 splits = two workgroups per CU (its launcher takes min(splits, 2 x CUs, rows)); the 128-channel
+    one on rows <= 32 pixels two workgroups per slab, one per CU: 128 splits."""
     if implicit and M == 64 and Nn == 576 and 0 < row_w <= 64 and WGRAD_ROWS:
         return max(1, min(512, K // 256))
+    if implicit and M == 128 and Nn == 1152 and 0 < row_w <= 32 and WGRAD_ROWS:  # layer 2: 2 workgroups per split
+        return max(1, min(128, K // 256))
     tiles = math.ceil(M / 128) * math.ceil(Nn / 128)
     narrow = (min(M, Nn) <= 64) if not implicit else (min(M, Nn) == 128)
     s = math.ceil((512 if narrow and WGRAD_NARROW_HALF else 1024) / tiles)

@@ -717,23 +717,26 @@ def test_wgrad_pingpong_implicit_conv(gpu, n, h, c, co, k, s, p):
     assert _rel(out, ref) < 1e-5, _rel(out, ref)
 
 
-@pytest.mark.parametrize("n,h,w", [(2, 9, 11), (4, 56, 56), (3, 17, 5), (2, 7, 64), (2, 5, 40), (1, 6, 70)])
-def test_wgrad3x3_rows(gpu, n, h, w):
-    """The 64-channel 3x3 / pad 1 weight gradient as the model calls it (implicit split count): W <= 64 runs the
-    row-ring k_wgrad3x3_rows<ceil(W / 32)> (one and two 32-pixel chunks, pixels past W, padding rows, one split slab
-    per workgroup), W = 70 the k_wgrad fallback; against torch fp32 in torch's [Cout, Cin, 3, 3] layout."""
+@pytest.mark.parametrize("n,h,w,c", [(2, 9, 11, 64), (4, 56, 56, 64), (3, 17, 5, 64), (2, 7, 64, 64), (2, 5, 40, 64),
+                                     (1, 6, 70, 64), (4, 28, 28, 128), (3, 9, 11, 128), (2, 5, 32, 128),
+                                     (1, 6, 40, 128)])
+def test_wgrad3x3_rows(gpu, n, h, w, c):
+    """The 64- / 128-channel 3x3 / pad 1 weight gradients as the model calls them (implicit split count): W <= 64 /
+    32 run the row-ring k_wgrad3x3_rows<ceil(W / 32), C> (one and two 32-pixel chunks, pixels past W, padding rows,
+    one split slab per workgroup -- per output-channel half for 128), W = 70 / 40 the k_wgrad / ping-pong fallbacks;
+    against torch fp32 in torch's [Cout, Cin, 3, 3] layout."""
     from distributeddataparallel_cifar10_amd.ops import functional as F
-    g = torch.Generator(device=gpu).manual_seed(n * h + w)
-    x = _bf(torch.randn(n, h, w, 64, device=gpu, generator=g))
-    wt = torch.empty(64, 64, 3, 3, device=gpu)
+    g = torch.Generator(device=gpu).manual_seed(n * h + w + c)
+    x = _bf(torch.randn(n, h, w, c, device=gpu, generator=g))
+    wt = torch.empty(c, c, 3, 3, device=gpu)
     geo = F._geom(x, wt, 1, 1)
     M = n * geo.Ho * geo.Wo
-    dy = _bf(torch.randn(M, 64, device=gpu, generator=g))
+    dy = _bf(torch.randn(M, c, device=gpu, generator=g))
     ref = torch.nn.grad.conv2d_weight(x.float().permute(0, 3, 1, 2), wt.shape,
-                                      dy.float().view(n, geo.Ho, geo.Wo, 64).permute(0, 3, 1, 2), stride=1, padding=1)
+                                      dy.float().view(n, geo.Ho, geo.Wo, c).permute(0, 3, 1, 2), stride=1, padding=1)
     out = torch.full_like(wt, float("nan"))
-    F.gemm(dy, x, ta=True, conv=2, geom=geo, mnk=(64, geo.K, M), splits=F._wgrad_splits(64, geo.K, M, True, row_w=w),
-           out=out, wperm=(64, 64, 9))
+    F.gemm(dy, x, ta=True, conv=2, geom=geo, mnk=(c, geo.K, M), splits=F._wgrad_splits(c, geo.K, M, True, row_w=w),
+           out=out, wperm=(c, c, 9))
     assert _rel(out, ref) < 1e-5, _rel(out, ref)
 
 
