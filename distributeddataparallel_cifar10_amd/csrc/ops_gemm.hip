@@ -1906,8 +1906,13 @@ __device__ __forceinline__ void rows_stats_out(const GemmArgs& g, const float (&
 
 // C = 64: 4 waves (3 workgroups per CU), rows <= 64 pixels; C = 128 (layer 2, 28 x 28): 8 waves of 16 output
 // channels each, 144 weight VGPRs per lane (one workgroup per CU), rows <= 32 pixels.  16-B chunks of a pixel row
-// XOR-swizzled by pixel & (C / 8 - 1): for C = 128 the two 16-lane halves of a ds_read_b128 group (chunks c, c + 1)
-// still cover the 64 banks once.
+// XOR-swizzled by pixel & (C / 8 - 1).  A ds_read_b128 lane group holds lanes j in {0-3, 12-15} of one lane quarter
+// q and j in {4-11} of its partner q ^ 1.  With 128-B rows (C = 64) that is conflict-free for every tap shift as
+// is; with 256-B rows (C = 128) no pixel swizzle is (PMC: 25 % of the LDS cycles were conflicts), so for C = 128
+// lane j takes pixel cr_pix(j) = j < 8 ? j ^ 4 : j -- one half of a group then reads pixels {0-3, 8-11} + s, the
+// other {4-7, 12-15} + s, sets closed under + 8 -- and quarter q of K-slice h reads chunk cr_chunk(h, q) = 8 (q & 1)
+// + 4 (q >> 1) + h, so the halves' chunks differ by 8: x ^ 8 = x + 8 (mod 16) keeps each half inside its own bank
+// positions for every tap shift (brute-force checked over all shifts).
 template <int C>
 struct RowConv {
   static constexpr int NT = 4 * C, CH = C / 8, PXB = 2 * C, NS = 9 * C / 32, HS = C / 32;
@@ -1918,6 +1923,10 @@ template <int C>
 __device__ __forceinline__ int crc_off(int px, int chunk) {
   return px * (2 * C) + ((chunk ^ (px & (C / 8 - 1))) << 4);
 }
+template <int C>
+__device__ __forceinline__ int cr_pix(int j) { return C == 64 ? j : (j < 8 ? j ^ 4 : j); }
+template <int C>
+__device__ __forceinline__ int cr_chunk(int h, int q) { return C == 64 ? 4 * h + q : 8 * (q & 1) + 4 * (q >> 1) + h; }
 template <int NF, int C = 64>  // NF: 16-pixel fragments per row, ceil(W / 16)
 __global__ void __launch_bounds__(4 * C, C == 64 ? 3 : 1) k_conv3x3_rows(GemmArgs g) {
   using T = RowConv<C>;
@@ -1932,11 +1941,13 @@ __global__ void __launch_bounds__(4 * C, C == 64 ? 3 : 1) k_conv3x3_rows(GemmArg
   const int vid = (grid & 7) == 0 ? (int)(blockIdx.x & 7) * (grid >> 3) + (int)(blockIdx.x >> 3) : (int)blockIdx.x;
   const int r_beg = (int)((long long)vid * R / grid), r_end = (int)((long long)(vid + 1) * R / grid);
   for (int e = threadIdx.x; e < 4 * T::SLOT / 16; e += NT) *(v4u_*)(smem + e * 16) = v4u_{0u, 0u, 0u, 0u};
-  // weights: lane (q, j) of slice s holds channel 16 w + j, k = 32 s + 8 q .. + 7 (k = tap * C + c)
+  // weights: lane (q, j) of slice s = (tap, h) holds channel 16 w + j, k = tap * C + 8 cr_chunk(h, q) .. + 7
   const unsigned short* Bp = (const unsigned short*)g.B;
+  const int pj = cr_pix<C>(j);  // this lane's pixel within a 16-pixel fragment
   s16x8 wf[NS];
 #pragma unroll
-  for (int s = 0; s < NS; ++s) wf[s] = *(const s16x8*)(Bp + (size_t)(16 * w + j) * g.ldb + 32 * s + 8 * q);
+  for (int s = 0; s < NS; ++s)
+    wf[s] = *(const s16x8*)(Bp + (size_t)(16 * w + j) * g.ldb + (s / T::HS) * C + 8 * cr_chunk<C>(s % T::HS, q));
   const float alpha = gemm_alpha(g);
   float bias[4], shift[4], s1[4], sq[4];
 #pragma unroll
@@ -1994,17 +2005,17 @@ __global__ void __launch_bounds__(4 * C, C == 64 ? 3 : 1) k_conv3x3_rows(GemmArg
           const int s = (kh * 3 + kw) * T::HS + h;
 #pragma unroll
           for (int f = 0; f < NF; ++f) {
-            const s16x8 a = *(const s16x8*)(sl + crc_off<C>(16 * f + j + kw, 4 * h + q));
+            const s16x8 a = *(const s16x8*)(sl + crc_off<C>(16 * f + pj + kw, cr_chunk<C>(h, q)));
             acc[f] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[s], a, acc[f], 0, 0, 0);
           }
         }
       }
     }
-    // lane (q, j) of fragment f: channels 16 w + 4 q + e of pixel 16 f + j
+    // lane (q, j) of fragment f: channels 16 w + 4 q + e of pixel 16 f + cr_pix(j)
     char* ob = smem + 4 * T::SLOT + (r & 1) * T::OUT;
 #pragma unroll
     for (int f = 0; f < NF; ++f) {
-      const int px = 16 * f + j;
+      const int px = 16 * f + pj;
       unsigned short hv[4];
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
