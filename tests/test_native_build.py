@@ -113,3 +113,88 @@ def test_ops_reject_cpu_tensors():
     from distributeddataparallel_cifar10_amd import ops
     with pytest.raises(ValueError):
         ops.gemm(torch.zeros(4, 8, dtype=torch.bfloat16), torch.zeros(4, 8, dtype=torch.bfloat16))
+
+
+def test_wgrad_split_rules_for_the_row_kernels(monkeypatch):
+    """ops/functional.py _wgrad_splits: the row-ring weight gradients (csrc/ops_wgrad.hip k_wgrad3x3_rows) get one
+    split slab per workgroup -- 512 for the 64-channel 3x3 on rows <= 64 pixels, 128 for the 128-channel one on rows
+    <= 32 -- and every other shape, or the knob off, keeps the k_wgrad rule."""
+    from distributeddataparallel_cifar10_amd.ops import functional as F
+    monkeypatch.setattr(F, "WGRAD_ROWS", True)
+    k1, k2 = 256 * 56 * 56, 256 * 28 * 28
+    assert F._wgrad_splits(64, 576, k1, True, row_w=56) == 512
+    assert F._wgrad_splits(64, 576, 1000, True, row_w=10) == 3  # K // 256
+    assert F._wgrad_splits(128, 1152, k2, True, row_w=28) == 128
+    old1, old2 = F._wgrad_splits(64, 576, k1, True), F._wgrad_splits(128, 1152, k2, True)
+    assert (old1, old2) == (205, 57)
+    assert F._wgrad_splits(64, 576, k1, True, row_w=70) == old1
+    assert F._wgrad_splits(128, 1152, k2, True, row_w=40) == old2
+    monkeypatch.setattr(F, "WGRAD_ROWS", False)
+    assert F._wgrad_splits(64, 576, k1, True, row_w=56) == old1
+
+
+def test_row_kernel_lds_maps_are_conflict_free():
+    """The LDS layouts of the row-ring kernels, mirrored here from csrc/ops_gemm.hip / ops_wgrad.hip (the test also
+    checks the C++ still spells them this way): every ds_read_b128 lane group (4 x 16 lanes, bank = byte / 4 mod 64)
+    of the forward kernels and every 32-lane half of the ds_read_b64_tr_b16 reads of the weight gradients touches each
+    bank at most once, for every tap / pixel shift."""
+    src = "".join(open(os.path.join(nbuild.CSRC, f)).read() for f in ("ops_gemm.hip", "ops_wgrad.hip"))
+    for spelled in ("return px * (2 * C) + ((chunk ^ (px & (C / 8 - 1))) << 4);",
+                    "return C == 64 ? j : (j < 8 ? j ^ 4 : j);",
+                    "return C == 64 ? 4 * h + q : 8 * (q & 1) + 4 * (q >> 1) + h;",
+                    "return px * 128 + ((chunk ^ ((((px >> 1) & 3) << 1) ^ (((px >> 3) & 1) << 2))) << 4);",
+                    "else return px * 256 + ((chunk ^ (((px & 3) | (((px >> 3) & 1) << 2)) << 1)) << 4);",
+                    "return px * 128 + ((chunk ^ (((px >> 1) & 3) << 1)) << 4);"):
+        assert spelled in src, spelled
+
+    def crc(C, px, c):
+        return px * 2 * C + ((c ^ (px & (C // 8 - 1))) << 4)
+
+    def pix(C, j):
+        return j if C == 64 else (j ^ 4 if j < 8 else j)
+
+    def chunk(C, h, q):
+        return 4 * h + q if C == 64 else 8 * (q & 1) + 4 * (q >> 1) + h
+
+    def wr(px, c):
+        return px * 128 + ((c ^ ((((px >> 1) & 3) << 1) ^ (((px >> 3) & 1) << 2))) << 4)
+
+    def wx128(px, c):
+        return px * 256 + ((c ^ (((px & 3) | (((px >> 3) & 1) << 2)) << 1)) << 4)
+
+    def ws2(px, c):
+        return px * 128 + ((c ^ (((px >> 1) & 3) << 1)) << 4)
+
+    def worst(addrs, width):
+        banks = {}
+        for a in addrs:
+            for b in range(width // 4):
+                k = (a // 4 + b) % 64
+                banks[k] = banks.get(k, 0) + 1
+        return max(banks.values())
+
+    g16 = [list(range(0, 4)) + list(range(12, 16)) + list(range(20, 28)),
+           list(range(4, 12)) + list(range(16, 20)) + list(range(28, 32))]
+    g16 += [[lane + 32 for lane in g] for g in g16]
+    for C in (64, 128):  # forward: A fragment reads, lane (q, j) = pixel pix(j) + shift, chunk(h, q)
+        for o in range(40):
+            for h in range(C // 32):
+                for g in g16:
+                    assert worst([crc(C, pix(C, lane & 15) + o, chunk(C, h, lane >> 4)) for lane in g], 16) == 1
+    # weight gradients: one 32-lane half = lane groups q, q + 1; lane 4 a + p of a group reads row a of its block
+    # (pixel base + 8 q + 4 r + a, k_wgrad3x3_rows; base + 4 q + 16 r + a, k_wgrad_s2d_rows), 8 B at column 4 p
+    for o in range(40):
+        for cb in range(8):
+            for r in range(2):
+                for C, off in ((64, wr), (128, wx128)):
+                    if C == 64 and cb >= 4:
+                        continue
+                    ad = [off(o + 8 * q + 4 * r + a, 2 * cb + (p >> 1)) + 8 * (p & 1)
+                          for q in (0, 1) for a in range(4) for p in range(4)]
+                    assert worst(ad, 8) == 1, (C, o, cb, r)
+                if cb < 4:
+                    ad = [ws2(o + 4 * q + 16 * r + a, 2 * cb + (p >> 1)) + 8 * (p & 1)
+                          for q in (0, 1) for a in range(4) for p in range(4)]
+                    assert worst(ad, 8) == 1, ("s2d dY", o, cb, r)
+                    ad = [(o + 4 * q + 16 * r + a) * 32 + 8 * p for q in (0, 1) for a in range(4) for p in range(4)]
+                    assert worst(ad, 8) == 1, ("s2d X", o, r)
