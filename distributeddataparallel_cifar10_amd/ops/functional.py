@@ -154,11 +154,15 @@ def _wgrad_splits(M: int, Nn: int, K: int, implicit: bool = False, row_w: int = 
     (profiles/wgrad_split_sweep_r8c.log; the 64-channel implicit 3x3 wants the full target: 148 vs 200 us).
     The 64-channel implicit 3x3 on input rows of row_w <= 64 pixels runs k_wgrad3x3_rows, one split slab per
     workgroup: 512 splits = two workgroups per CU (its launcher takes min(splits, 2 x CUs, rows)); the 128-channel
-    one on rows <= 32 pixels two workgroups per slab, one per CU: 128 splits."""
+    one on rows <= 32 pixels two workgroups per slab, one per CU: 128 splits; the s2d stem's (k_wgrad_s2d_rows)
+    three per CU: 768 (150 -> 143 us over 512; 128 / 96 / 64 and 512 / 384 / 256 for the 3x3 forms measured slower:
+    profiles/wgrad_rows_splits_r9q.log).  row_w: input row width of a KH > 1 implicit conv, else 0."""
     if implicit and M == 64 and Nn == 576 and 0 < row_w <= 64 and WGRAD_ROWS:
         return max(1, min(512, K // 256))
     if implicit and M == 128 and Nn == 1152 and 0 < row_w <= 32 and WGRAD_ROWS:  # layer 2: 2 workgroups per split
         return max(1, min(128, K // 256))
+    if implicit and M == 64 and Nn == 256 and 0 < row_w <= 128 and WGRAD_ROWS:  # s2d stem: 3 workgroups per CU
+        return max(1, min(768, K // 256))
     tiles = math.ceil(M / 128) * math.ceil(Nn / 128)
     narrow = (min(M, Nn) <= 64) if not implicit else (min(M, Nn) == 128)
     s = math.ceil((512 if narrow and WGRAD_NARROW_HALF else 1024) / tiles)
@@ -734,7 +738,8 @@ def _conv_bwd(dy, st, need_x: bool, need_w: bool, sink=None, x_join: Optional[Gr
             gemm(dyb, cols, ta=True, tb=True, splits=_wgrad_splits(co, kp, M), out=dst, beta=beta, wperm=perm)
         else:  # implicit: B(n = tap*C + c, k = pixel) gathered from x
             gemm(dyb, st["x"], ta=True, conv=2, geom=g, mnk=(co, g.K, M),
-                 splits=_wgrad_splits(co, g.K, M, True, row_w=g.W), out=dst, beta=beta, wperm=perm)
+                 splits=_wgrad_splits(co, g.K, M, True, row_w=g.W if g.KH > 1 else 0), out=dst, beta=beta,
+                 wperm=perm)
         dw = None if sink is not None else dst
     return dx, dw
 

@@ -116,15 +116,17 @@ def test_ops_reject_cpu_tensors():
 
 
 def test_wgrad_split_rules_for_the_row_kernels(monkeypatch):
-    """ops/functional.py _wgrad_splits: the row-ring weight gradients (csrc/ops_wgrad.hip k_wgrad3x3_rows) get one
-    split slab per workgroup -- 512 for the 64-channel 3x3 on rows <= 64 pixels, 128 for the 128-channel one on rows
-    <= 32 -- and every other shape, or the knob off, keeps the k_wgrad rule."""
+    """ops/functional.py _wgrad_splits: the row-ring weight gradients (csrc/ops_wgrad.hip) get one split slab per
+    workgroup -- 512 for the 64-channel 3x3 on rows <= 64 pixels, 128 for the 128-channel one on rows <= 32, 768 for
+    the s2d stem on rows <= 128 -- and every other shape, or the knob off, keeps the k_wgrad rule."""
     from distributeddataparallel_cifar10_amd.ops import functional as F
     monkeypatch.setattr(F, "WGRAD_ROWS", True)
     k1, k2 = 256 * 56 * 56, 256 * 28 * 28
     assert F._wgrad_splits(64, 576, k1, True, row_w=56) == 512
     assert F._wgrad_splits(64, 576, 1000, True, row_w=10) == 3  # K // 256
     assert F._wgrad_splits(128, 1152, k2, True, row_w=28) == 128
+    assert F._wgrad_splits(64, 256, 256 * 112 * 112, True, row_w=115) == 768  # the s2d stem
+    assert F._wgrad_splits(64, 256, 256 * 112 * 112, True, row_w=134) == F._wgrad_splits(64, 256, 256 * 112 * 112, True)
     old1, old2 = F._wgrad_splits(64, 576, k1, True), F._wgrad_splits(128, 1152, k2, True)
     assert (old1, old2) == (205, 57)
     assert F._wgrad_splits(64, 576, k1, True, row_w=70) == old1
